@@ -1,0 +1,244 @@
+// Fused multi-head self-attention forward (flash-style, non-causal) for the
+// YOLOS-family tenant model, bf16 in / bf16 out, fp32 softmax, head_dim 64.
+//
+// CDNA4 design (not a port of any CUDA kernel):
+//  * one workgroup = 4 waves = 128 query rows of one (batch, head); each wave
+//    owns 32 query rows and keeps them as the B operand of
+//    v_mfma_f32_32x32x16_bf16 for the whole kernel;
+//  * "swapped" QK^T: S^T = K . Q^T, so every lane holds 16 of the 32 key
+//    scores of ONE query row (column = lane & 31) -> the row max / row sum are
+//    lane-local except for a single lane^32 exchange;
+//  * the S^T accumulator is re-used in registers as the B operand of
+//    O^T = V^T . P^T (no LDS round trip for P);
+//  * V^T fragments come from a row-major, XOR-swizzled V tile through the
+//    gfx950 transposing LDS read ds_read_b64_tr_b16;
+//  * K is read with ds_read_b128 from an XOR-swizzled image (conflict-free
+//    for both 16-lane groups);
+//  * K/V tiles (64 keys) are double-buffered in LDS with register staging:
+//    the next tile's global loads are issued before the MFMA work of the
+//    current tile and written to LDS after it;
+//  * the workgroup -> (batch, head, q-block) map is XCD-aware so q-blocks of
+//    one head share an XCD's L2 (K/V of one head = 870 KB at S=3401).
+#include "common.h"
+
+namespace {
+
+constexpr int D = 64;
+constexpr int WAVES = 4;
+constexpr int QBLK = 32 * WAVES;  // query rows per workgroup
+constexpr int KVBLK = 64;         // keys per LDS tile
+constexpr int NT = 64 * WAVES;
+constexpr int TILE_BYTES = KVBLK * D * 2;      // 8 KiB
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;    // K + V
+
+// byte offset of 16-byte chunk `ch` (0..7) of row `row` in the K image
+__device__ __forceinline__ int k_off(int row, int ch) {
+  return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4);
+}
+// byte offset of chunk `ch` of row `row` in the V image (conflict-free for the
+// 4-row x 64-byte blocks that ds_read_b64_tr_b16 gathers per half-wave)
+__device__ __forceinline__ int v_off(int row, int ch) {
+  return row * 128 + ((ch ^ (((row >> 1) & 1) << 2)) << 4);
+}
+
+__global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
+    const unsigned short* __restrict__ q, const unsigned short* __restrict__ k,
+    const unsigned short* __restrict__ v, unsigned short* __restrict__ o,
+    int B, int H, int Sq, int Skv, int ld_in, long long bs_in, int ld_out,
+    long long bs_out, float c /* softmax scale * log2(e) */, int nqb) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int nwg = B * H * nqb;
+  const int w = nos::xcd_remap(blockIdx.x, nwg);
+  const int b = w / (H * nqb);
+  const int rem = w - b * (H * nqb);
+  const int h = rem / nqb;
+  const int qb = rem - h * nqb;
+
+  const int tid = threadIdx.x;
+  const int wid = tid >> 6;
+  const int lane = tid & 63;
+  const int r = lane & 31;
+  const int hh = lane >> 5;
+
+  const unsigned short* qb_ptr = q + b * bs_in + h * D;
+  const unsigned short* kb_ptr = k + b * bs_in + h * D;
+  const unsigned short* vb_ptr = v + b * bs_in + h * D;
+
+  // ---- Q fragments (B operand): lane holds Q[row r][d = 16ks + 8hh .. +7]
+  const int qrow = qb * QBLK + wid * 32 + r;
+  const int qrow_c = qrow < Sq ? qrow : Sq - 1;
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+    qf[ks] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + (long long)qrow_c * ld_in + ks * 16 + hh * 8);
+
+  // ---- staging helpers: each thread moves 2 K chunks + 2 V chunks per tile
+  uint4 kreg[2], vreg[2];
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int cid = tid + NT * i;
+      const int row = cid >> 3, ch = cid & 7;
+      int kv = t * KVBLK + row;
+      kv = kv < Skv ? kv : Skv - 1;
+      kreg[i] = *reinterpret_cast<const uint4*>(kb_ptr + (long long)kv * ld_in + ch * 8);
+      vreg[i] = *reinterpret_cast<const uint4*>(vb_ptr + (long long)kv * ld_in + ch * 8);
+    }
+  };
+  auto store_tile = [&](int stage) {
+    unsigned char* base = smem + stage * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int cid = tid + NT * i;
+      const int row = cid >> 3, ch = cid & 7;
+      *reinterpret_cast<uint4*>(base + k_off(row, ch)) = kreg[i];
+      *reinterpret_cast<uint4*>(base + TILE_BYTES + v_off(row, ch)) = vreg[i];
+    }
+  };
+
+  const int ntiles = (Skv + KVBLK - 1) / KVBLK;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  f32x16_t oacc[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+
+  // tr-read lane geometry
+  const int g16 = (lane >> 4) & 1;
+  const int tq = (lane & 15) >> 2;
+  const int tp = lane & 3;
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int stage = t & 1;
+    const bool has_next = (t + 1) < ntiles;
+    if (has_next) load_tile(t + 1);
+
+    const unsigned char* kl = smem + stage * STAGE_BYTES;
+    const unsigned char* vl = kl + TILE_BYTES;
+
+    // ---- S^T = K . Q^T  (two 32-key blocks)
+    f32x16_t sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(kl + k_off(kb * 32 + r, 2 * ks + hh));
+        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], sacc[kb], 0, 0, 0);
+      }
+    }
+
+    // ---- mask keys past the end (only the last tile)
+    if ((t + 1) * KVBLK > Skv) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kv = t * KVBLK + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (kv >= Skv) sacc[kb][i] = -INFINITY;
+        }
+    }
+
+    // ---- online softmax (per lane = per query row)
+    float mt = sacc[0][0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mt = fmaxf(mt, sacc[0][i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[1][i]);
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m, mt);
+    const float alpha = __builtin_amdgcn_exp2f((m - m_new) * c);
+    m = m_new;
+    const float mc = m_new * c;
+    float psum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][i], c, -mc));
+        sacc[kb][i] = p;
+        psum += p;
+      }
+    l = fmaf(l, alpha, psum);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+
+    // ---- P^T fragments (B operand of O^T = V^T . P^T), straight from registers
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[kb][s2][j] = (__bf16)sacc[kb][8 * s2 + j];
+
+    // ---- O^T += V^T . P^T ; V^T fragments via the transposing LDS read
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int ch = 4 * db + 2 * g16 + (tp >> 1);
+      const int o8 = 8 * (tp & 1);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int row0 = kb * 32 + s2 * 16 + 4 * hh + tq;
+          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              LDS_PTR(s16x4_t, vl + v_off(row0, ch) + o8));
+          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              LDS_PTR(s16x4_t, vl + v_off(row0 + 8, ch) + o8));
+          const s16x8_t a16 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              __builtin_bit_cast(bf16x8_t, a16), pf[kb][s2], oacc[db], 0, 0, 0);
+        }
+    }
+
+    if (has_next) {
+      // every wave finished reading the buffer we are about to fill at the
+      // barrier that ended iteration t-1
+      store_tile(stage ^ 1);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: normalise and store O[q][h*64 + d]
+  const float ltot = l + __shfl_xor(l, 32, 64);
+  const float inv = 1.f / ltot;
+  if (qrow < Sq) {
+    unsigned short* op = o + b * bs_out + (long long)qrow * ld_out + h * D;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = 32 * db + 8 * g + 4 * hh;
+        bf16x4_t ov;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ov[e] = (__bf16)(oacc[db][4 * g + e] * inv);
+        *reinterpret_cast<bf16x4_t*>(op + d) = ov;
+      }
+  }
+}
+
+}  // namespace
+
+// q/k/v: bf16 [B, S, *] rows with row stride ld_in (elements) and batch stride
+// bs_in; head h occupies columns [h*64, h*64+64) relative to each pointer.
+// o: bf16 [B, Sq, H*64 (+pad)] with row stride ld_out and batch stride bs_out.
+NOS_API int nos_attn_fwd_d64(const void* q, const void* k, const void* v, void* o, int B,
+                             int H, int Sq, int Skv, int ld_in, long long bs_in, int ld_out,
+                             long long bs_out, float scale, hipStream_t stream) {
+  if (B <= 0 || H <= 0 || Sq <= 0 || Skv <= 0) return (int)hipErrorInvalidValue;
+  if ((ld_in % 8) != 0 || (ld_out % 4) != 0) return (int)hipErrorInvalidValue;
+  const int nqb = (Sq + QBLK - 1) / QBLK;
+  const int nwg = B * H * nqb;
+  const float c = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(attn_fwd_d64_kernel, dim3(nwg), dim3(NT), 2 * STAGE_BYTES, stream,
+                     (const unsigned short*)q, (const unsigned short*)k,
+                     (const unsigned short*)v, (unsigned short*)o, B, H, Sq, Skv, ld_in, bs_in,
+                     ld_out, bs_out, c, nqb);
+  return (int)hipGetLastError();
+}

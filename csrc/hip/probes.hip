@@ -1,0 +1,175 @@
+// CDNA4 occupancy / bandwidth probe kernels of the gpuagent.
+//
+// The gpuagent runs these on a stream whose CU mask equals the slice it wants
+// to price, so the numbers it publishes (status-gpu-<i>-<slice>-tflops /
+// -gbps annotations) are what a tenant on that slice can actually get:
+//
+//   probe_placement   every workgroup records HW_REG_XCC_ID + HW_REG_HW_ID
+//                     (CU / SH / SE) -> verifies CU-mask enforcement and
+//                     tells which XCDs a slice spans;
+//   probe_hbm_stream  16-byte-per-lane streaming copy (4 loads in flight per
+//                     lane) -> achievable GB/s of the slice;
+//   probe_mfma_peak   back-to-back v_mfma_f32_32x32x16_bf16 on register
+//                     operands, 4 independent accumulators -> peak MFMA rate
+//                     of the slice's CUs at the clock the chip holds;
+//   probe_gemm        the LDS-tiled MFMA GEMM (gemm.hip) run persistently
+//                     with a grid sized to the slice -> realistic TFLOP/s.
+#include "common.h"
+
+NOS_API int nos_gemm_bf16(const void* A, int lda, const void* W, int ldw, const void* bias,
+                          const void* R, int ldr, void* C, int ldc, int M, int N, int K, int epi,
+                          int max_wg, hipStream_t stream);
+
+namespace {
+
+__global__ void probe_placement_kernel(uint4* __restrict__ out, int spin) {
+  unsigned xcc, hwid;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  // keep the workgroup resident for a while so the dispatcher spreads the
+  // grid over every CU the queue's mask allows
+  unsigned long long t = t0;
+  while ((int)(t - t0) < spin) t = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) out[blockIdx.x] = make_uint4(xcc, hwid, blockIdx.x, (unsigned)t0);
+}
+
+__global__ __launch_bounds__(256) void probe_hbm_copy_kernel(const uint4* __restrict__ src,
+                                                            uint4* __restrict__ dst, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void probe_mfma_peak_kernel(float* __restrict__ out, int iters,
+                                                              unsigned seed) {
+  const int lane = threadIdx.x & 63;
+  s16x8_t a16, b16;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    // random-ish normal bf16 values (random data: DVFS behaves as in real work)
+    unsigned x = (seed ^ (lane * 2654435761u) ^ (j * 40503u)) * 2246822519u;
+    a16[j] = (short)(0x3c00 | (x & 0x80ff));
+    b16[j] = (short)(0x3c00 | ((x >> 16) & 0x80ff));
+  }
+  const bf16x8_t a = __builtin_bit_cast(bf16x8_t, a16);
+  const bf16x8_t b = __builtin_bit_cast(bf16x8_t, b16);
+  f32x16_t c0 = {}, c1 = {}, c2 = {}, c3 = {};
+  for (int i = 0; i < iters; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c3, 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += c0[i] + c1[i] + c2[i] + c3[i];
+  if (s == 1234.5f) out[blockIdx.x] = s;  // keep the chain live, (almost) never store
+}
+
+struct EventTimer {
+  hipEvent_t a = nullptr, b = nullptr;
+  EventTimer() { (void)hipEventCreate(&a); (void)hipEventCreate(&b); }
+  ~EventTimer() { (void)hipEventDestroy(a); (void)hipEventDestroy(b); }
+};
+
+}  // namespace
+
+// out_dev: device buffer of nwg uint4 {xcc_id, hw_id, block, t0}
+NOS_API int nos_probe_placement(void* out_dev, int nwg, int spin_ticks, hipStream_t stream) {
+  if (nwg <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(probe_placement_kernel, dim3(nwg), dim3(64), 0, stream, (uint4*)out_dev,
+                     spin_ticks);
+  return (int)hipGetLastError();
+}
+
+NOS_API int nos_probe_hbm_copy(const void* src, void* dst, long long bytes, int nwg,
+                               hipStream_t stream) {
+  if (bytes <= 0 || (bytes % 16) || nwg <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(probe_hbm_copy_kernel, dim3(nwg), dim3(256), 0, stream, (const uint4*)src,
+                     (uint4*)dst, bytes / 16);
+  return (int)hipGetLastError();
+}
+
+// Self-contained HBM probe: allocates 2 x bytes, times `iters` copies on
+// `stream`, returns achieved GB/s (read + write bytes) in *gbps.
+NOS_API int nos_probe_hbm(hipStream_t stream, long long bytes, int iters, int nwg, double* gbps) {
+  void *src = nullptr, *dst = nullptr;
+  HIP_CHECK_RET(hipMalloc(&src, bytes));
+  HIP_CHECK_RET(hipMalloc(&dst, bytes));
+  (void)hipMemsetAsync(src, 1, bytes, stream);
+  int rc = nos_probe_hbm_copy(src, dst, bytes, nwg, stream);  // warm-up
+  EventTimer tm;
+  (void)hipEventRecord(tm.a, stream);
+  for (int i = 0; i < iters && rc == 0; ++i) rc = nos_probe_hbm_copy(src, dst, bytes, nwg, stream);
+  (void)hipEventRecord(tm.b, stream);
+  (void)hipEventSynchronize(tm.b);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, tm.a, tm.b);
+  *gbps = (ms > 0.f) ? (2.0 * (double)bytes * iters) / (ms * 1e-3) / 1e9 : 0.0;
+  (void)hipFree(src);
+  (void)hipFree(dst);
+  return rc;
+}
+
+// Peak MFMA probe: nwg workgroups of 4 waves, `iters` x 4 MFMAs per wave.
+NOS_API int nos_probe_mfma_peak(hipStream_t stream, int nwg, int iters, double* tflops) {
+  float* scratch = nullptr;
+  HIP_CHECK_RET(hipMalloc(&scratch, sizeof(float) * nwg));
+  hipLaunchKernelGGL(probe_mfma_peak_kernel, dim3(nwg), dim3(256), 0, stream, scratch, 64, 7u);
+  EventTimer tm;
+  (void)hipEventRecord(tm.a, stream);
+  hipLaunchKernelGGL(probe_mfma_peak_kernel, dim3(nwg), dim3(256), 0, stream, scratch, iters, 11u);
+  (void)hipEventRecord(tm.b, stream);
+  (void)hipEventSynchronize(tm.b);
+  int rc = (int)hipGetLastError();
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, tm.a, tm.b);
+  const double flop = (double)nwg * 4 /*waves*/ * iters * 4 /*chains*/ * (32.0 * 32 * 16 * 2);
+  *tflops = (ms > 0.f) ? flop / (ms * 1e-3) / 1e12 : 0.0;
+  (void)hipFree(scratch);
+  return rc;
+}
+
+// Asynchronous launch of the peak-MFMA kernel (concurrency experiments):
+// scratch must hold nwg floats.
+NOS_API int nos_probe_mfma_peak_launch(hipStream_t stream, int nwg, int iters, void* scratch) {
+  if (nwg <= 0 || iters <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(probe_mfma_peak_kernel, dim3(nwg), dim3(256), 0, stream, (float*)scratch, iters, 13u);
+  return (int)hipGetLastError();
+}
+
+// GEMM probe: M = N = K = n (multiple of 128), persistent grid of max_wg
+// workgroups; returns achieved TFLOP/s over `iters` launches.
+NOS_API int nos_probe_gemm(hipStream_t stream, int n, int iters, int max_wg, double* tflops) {
+  if (n <= 0 || (n % 128)) return (int)hipErrorInvalidValue;
+  const size_t bytes = (size_t)n * n * 2;
+  void *a = nullptr, *w = nullptr, *c = nullptr;
+  HIP_CHECK_RET(hipMalloc(&a, bytes));
+  HIP_CHECK_RET(hipMalloc(&w, bytes));
+  HIP_CHECK_RET(hipMalloc(&c, bytes));
+  // 0x3c3c = 0.0115 in bf16: non-trivial operands, no overflow
+  (void)hipMemsetAsync(a, 0x3c, bytes, stream);
+  (void)hipMemsetAsync(w, 0x3c, bytes, stream);
+  int rc = nos_gemm_bf16(a, n, w, n, nullptr, nullptr, 0, c, n, n, n, n, 0, max_wg, stream);
+  EventTimer tm;
+  (void)hipEventRecord(tm.a, stream);
+  for (int i = 0; i < iters && rc == 0; ++i)
+    rc = nos_gemm_bf16(a, n, w, n, nullptr, nullptr, 0, c, n, n, n, n, 0, max_wg, stream);
+  (void)hipEventRecord(tm.b, stream);
+  (void)hipEventSynchronize(tm.b);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, tm.a, tm.b);
+  *tflops = (ms > 0.f) ? 2.0 * n * (double)n * n * iters / (ms * 1e-3) / 1e12 : 0.0;
+  (void)hipFree(a);
+  (void)hipFree(w);
+  (void)hipFree(c);
+  return rc;
+}

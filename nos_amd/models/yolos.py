@@ -1,0 +1,330 @@
+"""YOLOS (ViT detector) tenant model -- the workload of the reference's GPU-sharing demo.
+
+The reference benchmarks GPU sharing with pods running ``hustvl/yolos-small``
+inference in a loop (``demos/gpu-sharing-comparison/client/main.py:14-25``,
+results ``demos/gpu-sharing-comparison/README.md:69-71``).  This module
+re-implements that architecture for MI355X:
+
+* every linear layer is one gfx950 MFMA GEMM with a fused epilogue
+  (bias, exact GELU, residual add) -- ``nos_gemm_bf16``;
+* Q, K and V are one fused projection whose output feeds the flash-style
+  attention kernel directly (no head transposes) -- ``nos_attn_fwd_d64``;
+* LayerNorm is one bandwidth-bound kernel per call -- ``nos_layernorm_bf16``;
+* the whole forward is captured into one HIP graph per tenant
+  (:class:`GraphedTenant`), replayed on the tenant's (CU-masked) stream.
+
+Weights are random-initialised (no network, no checkpoints); the architecture
+and shapes follow yolos-small: hidden 384, 12 layers, 6 heads, MLP 1536,
+16x16 patches, 100 detection tokens, position embeddings for 800x1333
+interpolated (bicubic) to the input resolution, 3-layer MLP heads for 92 class
+logits and 4 box coordinates.  ``backend="torch"`` runs the same weights
+through eager PyTorch ops (hipBLASLt GEMMs + SDPA): the baseline the HIP path
+is measured against, and the numerics reference.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+
+
+@dataclass(frozen=True)
+class YolosConfig:
+    hidden_size: int = 384
+    num_hidden_layers: int = 12
+    num_attention_heads: int = 6
+    intermediate_size: int = 1536
+    patch_size: int = 16
+    num_channels: int = 3
+    image_size: tuple[int, int] = (800, 1333)
+    num_detection_tokens: int = 100
+    num_labels: int = 91
+    layer_norm_eps: float = 1e-12
+    initializer_range: float = 0.02
+
+    @classmethod
+    def small(cls) -> "YolosConfig":
+        return cls()
+
+    @classmethod
+    def tiny(cls) -> "YolosConfig":
+        return cls(hidden_size=192, num_attention_heads=3, intermediate_size=768, image_size=(800, 1333))
+
+    @classmethod
+    def test(cls) -> "YolosConfig":
+        """Small config for CPU tests (head_dim stays 64)."""
+        return cls(hidden_size=128, num_hidden_layers=2, num_attention_heads=2, intermediate_size=256,
+                   image_size=(64, 96), num_detection_tokens=10, num_labels=9)
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden_size // self.num_attention_heads
+
+
+def demo_input_hw() -> tuple[int, int]:
+    """Input size of the reference demo: COCO val2017 #39769 (640x480) resized by
+    YolosImageProcessor to shortest edge 800 (longest <= 1333) -> 800 x 1066."""
+    h, w = 480, 640
+    s = 800 / min(h, w)
+    nh, nw = int(round(h * s)), int(w * s)
+    if max(nh, nw) > 1333:
+        s = 1333 / max(h, w)
+        nh, nw = int(h * s), int(w * s)
+    return nh, nw
+
+
+def flops_per_image(cfg: YolosConfig, hw: tuple[int, int]) -> float:
+    """Multiply-add FLOPs of one forward at input size hw (matmuls + attention)."""
+    gh, gw = hw[0] // cfg.patch_size, hw[1] // cfg.patch_size
+    S = 1 + gh * gw + cfg.num_detection_tokens
+    h, m = cfg.hidden_size, cfg.intermediate_size
+    per_layer = 2 * S * h * (3 * h) + 2 * S * h * h + 2 * 2 * S * h * m + 2 * 2 * S * S * h
+    patch = 2 * gh * gw * (cfg.num_channels * cfg.patch_size ** 2) * h
+    heads = 2 * cfg.num_detection_tokens * (4 * h * h + h * (cfg.num_labels + 1) + h * 4)
+    return float(cfg.num_hidden_layers * per_layer + patch + heads)
+
+
+class _Layer(nn.Module):
+    def __init__(self, cfg: YolosConfig):
+        super().__init__()
+        h, m = cfg.hidden_size, cfg.intermediate_size
+        self.ln1_w = nn.Parameter(torch.ones(h))
+        self.ln1_b = nn.Parameter(torch.zeros(h))
+        self.qkv_w = nn.Parameter(torch.empty(3 * h, h))  # rows: [q; k; v], each [H*D]
+        self.qkv_b = nn.Parameter(torch.zeros(3 * h))
+        self.proj_w = nn.Parameter(torch.empty(h, h))
+        self.proj_b = nn.Parameter(torch.zeros(h))
+        self.ln2_w = nn.Parameter(torch.ones(h))
+        self.ln2_b = nn.Parameter(torch.zeros(h))
+        self.fc1_w = nn.Parameter(torch.empty(m, h))
+        self.fc1_b = nn.Parameter(torch.zeros(m))
+        self.fc2_w = nn.Parameter(torch.empty(h, m))
+        self.fc2_b = nn.Parameter(torch.zeros(h))
+
+
+class YolosDetector(nn.Module):
+    """YOLOS object detector (inference)."""
+
+    def __init__(self, cfg: YolosConfig | None = None, backend: str = "native"):
+        super().__init__()
+        self.cfg = cfg = cfg or YolosConfig.small()
+        if cfg.head_dim != 64:
+            raise ValueError("nos_amd YOLOS kernels are built for head_dim 64")
+        self.backend = backend
+        h = cfg.hidden_size
+        pd = cfg.num_channels * cfg.patch_size ** 2
+        gh0, gw0 = cfg.image_size[0] // cfg.patch_size, cfg.image_size[1] // cfg.patch_size
+        self.patch_w = nn.Parameter(torch.empty(h, pd))  # conv 16x16/16 as a GEMM, K = 768
+        self.patch_b = nn.Parameter(torch.zeros(h))
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, h))
+        self.det_tokens = nn.Parameter(torch.zeros(1, cfg.num_detection_tokens, h))
+        self.pos_embed = nn.Parameter(torch.zeros(1, 1 + gh0 * gw0 + cfg.num_detection_tokens, h))
+        self.layers = nn.ModuleList(_Layer(cfg) for _ in range(cfg.num_hidden_layers))
+        self.ln_f_w = nn.Parameter(torch.ones(h))
+        self.ln_f_b = nn.Parameter(torch.zeros(h))
+        # 3-layer MLP heads (hidden -> hidden -> hidden -> out), ReLU between
+        self.cls_head = nn.ParameterList()
+        self.box_head = nn.ParameterList()
+        for head, out in ((self.cls_head, cfg.num_labels + 1), (self.box_head, 4)):
+            for n_in, n_out in ((h, h), (h, h), (h, out)):
+                head.append(nn.Parameter(torch.empty(n_out, n_in)))
+                head.append(nn.Parameter(torch.zeros(n_out)))
+        self._pos_cache: dict[tuple, torch.Tensor] = {}
+        self.reset_parameters()
+
+    # ------------------------------------------------------------------ init
+    @torch.no_grad()
+    def reset_parameters(self, seed: int = 0) -> None:
+        g = torch.Generator().manual_seed(seed)
+        std = self.cfg.initializer_range
+        for name, p in self.named_parameters():
+            if p.dim() >= 2 or name.endswith(("cls_token", "det_tokens", "pos_embed")):
+                p.copy_(torch.randn(p.shape, generator=g) * std)
+        self._pos_cache.clear()
+
+    # ----------------------------------------------------- position embedding
+    def interpolated_pos_embed(self, hw: tuple[int, int]) -> torch.Tensor:
+        """[1, S, h] position embeddings for input size hw (bicubic, as the
+        reference model's InterpolateInitialPositionEmbeddings). A pure function of
+        the weights and the input shape, cached per (shape, device, dtype)."""
+        key = (hw, self.pos_embed.device, self.pos_embed.dtype, self.pos_embed._version)
+        pe = self._pos_cache.get(key)
+        if pe is None:
+            cfg = self.cfg
+            nd = cfg.num_detection_tokens
+            p = self.pos_embed.detach().float()
+            cls_pe, det_pe, patch_pe = p[:, :1], p[:, -nd:], p[:, 1:-nd]
+            gh0, gw0 = cfg.image_size[0] // cfg.patch_size, cfg.image_size[1] // cfg.patch_size
+            patch_pe = patch_pe.transpose(1, 2).reshape(1, cfg.hidden_size, gh0, gw0)
+            gh, gw = hw[0] // cfg.patch_size, hw[1] // cfg.patch_size
+            patch_pe = F.interpolate(patch_pe, size=(gh, gw), mode="bicubic", align_corners=False)
+            patch_pe = patch_pe.flatten(2).transpose(1, 2)
+            pe = torch.cat([cls_pe, patch_pe, det_pe], dim=1).to(self.pos_embed.dtype).contiguous()
+            self._pos_cache = {key: pe}
+        return pe
+
+    # --------------------------------------------------------------- forward
+    def patchify(self, pixel_values: torch.Tensor) -> torch.Tensor:
+        """[B, C, H, W] -> [B, gh*gw, C*p*p] in the conv weight's (c, ky, kx) order."""
+        B, C, H, W = pixel_values.shape
+        p = self.cfg.patch_size
+        gh, gw = H // p, W // p
+        x = pixel_values[:, :, : gh * p, : gw * p]
+        x = x.reshape(B, C, gh, p, gw, p).permute(0, 2, 4, 1, 3, 5)
+        return x.reshape(B, gh * gw, C * p * p)
+
+    def forward(self, pixel_values: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        if self.backend == "torch" or not pixel_values.is_cuda:
+            return self._forward_torch(pixel_values)
+        return self._forward_native(pixel_values)
+
+    def _embed(self, pixel_values: torch.Tensor, lin) -> torch.Tensor:
+        B, _, H, W = pixel_values.shape
+        patches = self.patchify(pixel_values.to(self.patch_w.dtype)).contiguous()
+        x = lin(patches, self.patch_w, self.patch_b)
+        cls = self.cls_token.expand(B, -1, -1)
+        det = self.det_tokens.expand(B, -1, -1)
+        x = torch.cat([cls, x, det], dim=1)
+        return (x + self.interpolated_pos_embed((H, W))).contiguous()
+
+    def _heads(self, x: torch.Tensor, lin) -> tuple[torch.Tensor, torch.Tensor]:
+        outs = []
+        for head in (self.cls_head, self.box_head):
+            y = x
+            for i in range(3):
+                y = lin(y, head[2 * i], head[2 * i + 1], act="relu" if i < 2 else None)
+            outs.append(y)
+        return outs[0], outs[1].float().sigmoid()
+
+    def _forward_native(self, pixel_values: torch.Tensor):
+        cfg = self.cfg
+        nh = cfg.num_attention_heads
+
+        def lin(x, w, b, act=None, residual=None):
+            return ops.linear(x.contiguous(), w, b, act=act, residual=residual)
+
+        h = self._embed(pixel_values, lin)
+        eps = cfg.layer_norm_eps
+        for L in self.layers:
+            y, _ = ops.layernorm(h, L.ln1_w, L.ln1_b, eps)
+            qkv = ops.linear(y, L.qkv_w, L.qkv_b)
+            a = ops.attention_qkv(qkv, nh)
+            h = ops.linear(a, L.proj_w, L.proj_b, residual=h)
+            y, _ = ops.layernorm(h, L.ln2_w, L.ln2_b, eps)
+            m = ops.linear(y, L.fc1_w, L.fc1_b, act="gelu")
+            h = ops.linear(m, L.fc2_w, L.fc2_b, residual=h)
+        y, _ = ops.layernorm(h, self.ln_f_w, self.ln_f_b, eps)
+        det = y[:, -cfg.num_detection_tokens:, :].contiguous()
+        return self._heads(det, lin)
+
+    def _forward_torch(self, pixel_values: torch.Tensor):
+        cfg = self.cfg
+        nh, hd = cfg.num_attention_heads, cfg.head_dim
+
+        def lin(x, w, b, act=None, residual=None):
+            y = F.linear(x, w, b)
+            if act == "gelu":
+                y = F.gelu(y)
+            elif act == "relu":
+                y = F.relu(y)
+            return y if residual is None else y + residual
+
+        h = self._embed(pixel_values, lin)
+        B, S, hs = h.shape
+        eps = cfg.layer_norm_eps
+        for L in self.layers:
+            y = F.layer_norm(h, (hs,), L.ln1_w, L.ln1_b, eps)
+            qkv = F.linear(y, L.qkv_w, L.qkv_b).view(B, S, 3, nh, hd)
+            q, k, v = (t.transpose(1, 2) for t in qkv.unbind(2))
+            a = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, S, hs)
+            h = F.linear(a, L.proj_w, L.proj_b) + h
+            y = F.layer_norm(h, (hs,), L.ln2_w, L.ln2_b, eps)
+            h = F.linear(F.gelu(F.linear(y, L.fc1_w, L.fc1_b)), L.fc2_w, L.fc2_b) + h
+        y = F.layer_norm(h, (hs,), self.ln_f_w, self.ln_f_b, eps)
+        det = y[:, -cfg.num_detection_tokens:, :]
+        return self._heads(det, lin)
+
+    # ------------------------------------------------------ HF weight import
+    @torch.no_grad()
+    def load_hf_state_dict(self, sd: dict[str, torch.Tensor]) -> None:
+        """Import a transformers YolosForObjectDetection state dict (parity tests)."""
+        def g(k):
+            return sd[k].to(self.patch_w.dtype)
+
+        self.patch_w.copy_(g("vit.embeddings.patch_embeddings.projection.weight").reshape(self.patch_w.shape))
+        self.patch_b.copy_(g("vit.embeddings.patch_embeddings.projection.bias"))
+        self.cls_token.copy_(g("vit.embeddings.cls_token"))
+        self.det_tokens.copy_(g("vit.embeddings.detection_tokens"))
+        self.pos_embed.copy_(g("vit.embeddings.position_embeddings"))
+        for i, L in enumerate(self.layers):
+            p = f"vit.encoder.layer.{i}."
+            L.ln1_w.copy_(g(p + "layernorm_before.weight"))
+            L.ln1_b.copy_(g(p + "layernorm_before.bias"))
+            L.qkv_w.copy_(torch.cat([g(p + f"attention.attention.{n}.weight") for n in ("query", "key", "value")]))
+            L.qkv_b.copy_(torch.cat([g(p + f"attention.attention.{n}.bias") for n in ("query", "key", "value")]))
+            L.proj_w.copy_(g(p + "attention.output.dense.weight"))
+            L.proj_b.copy_(g(p + "attention.output.dense.bias"))
+            L.ln2_w.copy_(g(p + "layernorm_after.weight"))
+            L.ln2_b.copy_(g(p + "layernorm_after.bias"))
+            L.fc1_w.copy_(g(p + "intermediate.dense.weight"))
+            L.fc1_b.copy_(g(p + "intermediate.dense.bias"))
+            L.fc2_w.copy_(g(p + "output.dense.weight"))
+            L.fc2_b.copy_(g(p + "output.dense.bias"))
+        self.ln_f_w.copy_(g("vit.layernorm.weight"))
+        self.ln_f_b.copy_(g("vit.layernorm.bias"))
+        for head, name in ((self.cls_head, "class_labels_classifier"), (self.box_head, "bbox_predictor")):
+            for i in range(3):
+                head[2 * i].copy_(g(f"{name}.layers.{i}.weight"))
+                head[2 * i + 1].copy_(g(f"{name}.layers.{i}.bias"))
+        self._pos_cache.clear()
+
+
+@dataclass
+class GraphedTenant:
+    """One tenant "pod": a model instance + static input, captured into a HIP
+    graph on its own stream (the stream carries the tenant's CU mask)."""
+
+    model: YolosDetector
+    stream: torch.cuda.Stream
+    pixel_values: torch.Tensor
+    graph: torch.cuda.CUDAGraph | None = None
+    outputs: tuple = field(default_factory=tuple)
+
+    def capture(self, warmup: int = 2) -> None:
+        with torch.cuda.stream(self.stream):
+            for _ in range(warmup):
+                self.outputs = self.model(self.pixel_values)
+        self.stream.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=self.stream):
+            self.outputs = self.model(self.pixel_values)
+        self.stream.synchronize()
+
+    def launch(self) -> None:
+        with torch.cuda.stream(self.stream):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self.outputs = self.model(self.pixel_values)
+
+
+def make_demo_input(cfg: YolosConfig, batch: int = 1, device="cpu", dtype=torch.bfloat16,
+                    hw: tuple[int, int] | None = None, seed: int = 0) -> torch.Tensor:
+    """Synthetic normalised image batch of the demo's shape (no dataset access)."""
+    hw = hw or demo_input_hw()
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn((batch, cfg.num_channels, *hw), generator=g)
+    return x.to(device=device, dtype=dtype)
+
+
+def seq_len(cfg: YolosConfig, hw: tuple[int, int]) -> int:
+    return 1 + (hw[0] // cfg.patch_size) * (hw[1] // cfg.patch_size) + cfg.num_detection_tokens
+
+
+__all__ = ["YolosConfig", "YolosDetector", "GraphedTenant", "make_demo_input", "demo_input_hw",
+           "flops_per_image", "seq_len", "math"]

@@ -1,0 +1,165 @@
+"""Hot ops of the nos-amd tenant workloads and probes.
+
+Every op has two implementations:
+
+* the gfx950 HIP kernel in ``libnos_hip.so`` (used for every CUDA/ROCm
+  tensor -- there is no silent fallback on a GPU: a missing library raises);
+* a plain PyTorch fp32 reference (used for CPU tensors and by the numerics
+  tests, which compare the HIP kernel against it).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+EPI_BIAS, EPI_GELU, EPI_RESID, EPI_RELU = 1, 2, 4, 8
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+# ----------------------------------------------------------------- references
+def linear_ref(x, weight, bias=None, act=None, residual=None):
+    y = x.float() @ weight.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if act == "gelu":
+        y = F.gelu(y)
+    elif act == "relu":
+        y = F.relu(y)
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(x.dtype)
+
+
+def layernorm_ref(x, gamma, beta, eps=1e-12, residual=None):
+    s = x.float() if residual is None else (x.float() + residual.float())
+    if residual is not None:
+        s = s.to(x.dtype).float()
+    y = F.layer_norm(s, (s.shape[-1],), gamma.float(), beta.float(), eps)
+    return y.to(x.dtype), (s.to(x.dtype) if residual is not None else None)
+
+
+def attention_ref(q, k, v, scale=None):
+    """q,k,v: [B, S, H, D] -> [B, S, H, D] (fp32 math)."""
+    d = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(d)
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    p = torch.softmax((qf @ kf.transpose(-1, -2)) * scale, dim=-1)
+    return (p @ vf).transpose(1, 2).to(q.dtype)
+
+
+# ---------------------------------------------------------------- dispatchers
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
+           act: str | None = None, residual: torch.Tensor | None = None,
+           out: torch.Tensor | None = None, max_wg: int = 0) -> torch.Tensor:
+    """y = act(x @ weight^T + bias) + residual; x [..., K], weight [N, K]."""
+    if not x.is_cuda:
+        return linear_ref(x, weight, bias, act, residual)
+    K = x.shape[-1]
+    N = weight.shape[0]
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    if x2.stride(-1) != 1 or weight.stride(-1) != 1 or K % 64 or x.dtype != torch.bfloat16:
+        raise ValueError("native linear needs bf16, unit inner stride and K % 64 == 0")
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    epi = 0
+    if bias is not None:
+        epi |= EPI_BIAS
+    if act == "gelu":
+        epi |= EPI_GELU
+    elif act == "relu":
+        epi |= EPI_RELU
+    r2 = None
+    if residual is not None:
+        epi |= EPI_RESID
+        r2 = residual.reshape(-1, N)
+    o2 = out.reshape(-1, N)
+    rc = _lib.lib().nos_gemm_bf16(x2.data_ptr(), x2.stride(0), weight.data_ptr(), weight.stride(0),
+                                  _ptr(bias), _ptr(r2), r2.stride(0) if r2 is not None else 0,
+                                  o2.data_ptr(), o2.stride(0), M, N, K, epi, max_wg, _stream())
+    _lib.check(rc, "nos_gemm_bf16")
+    return out.reshape(*x.shape[:-1], N)
+
+
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12,
+              residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
+              sum_out: torch.Tensor | None = None):
+    """LayerNorm(x + residual). Returns (y, sum) where sum = x + residual (or None)."""
+    if not x.is_cuda:
+        return layernorm_ref(x, gamma, beta, eps, residual)
+    D = x.shape[-1]
+    x2 = x.reshape(-1, D)
+    rows = x2.shape[0]
+    if out is None:
+        out = torch.empty_like(x)
+    if residual is not None and sum_out is None:
+        sum_out = torch.empty_like(x)
+    rc = _lib.lib().nos_layernorm_bf16(x2.data_ptr(), _ptr(residual), out.data_ptr(), _ptr(sum_out),
+                                       gamma.data_ptr(), beta.data_ptr(), rows, D, x2.stride(0),
+                                       out.reshape(-1, D).stride(0), float(eps), _stream())
+    _lib.check(rc, "nos_layernorm_bf16")
+    return out, sum_out
+
+
+def attention_qkv(qkv: torch.Tensor, num_heads: int, out: torch.Tensor | None = None,
+                  scale: float | None = None) -> torch.Tensor:
+    """Self-attention on a fused projection qkv [B, S, 3*H*64] -> [B, S, H*64]."""
+    B, S, three_hd = qkv.shape
+    D = three_hd // (3 * num_heads)
+    if not qkv.is_cuda:
+        q, k, v = qkv.view(B, S, 3, num_heads, D).unbind(2)
+        return attention_ref(q, k, v, scale).reshape(B, S, num_heads * D)
+    if D != 64:
+        raise ValueError("native attention supports head_dim 64")
+    if qkv.stride(-1) != 1:
+        raise ValueError("qkv must have unit inner stride")
+    if out is None:
+        out = torch.empty((B, S, num_heads * D), dtype=qkv.dtype, device=qkv.device)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    hd = num_heads * D
+    base = qkv.data_ptr()
+    es = qkv.element_size()
+    rc = _lib.lib().nos_attn_fwd_d64(base, base + hd * es, base + 2 * hd * es, out.data_ptr(), B,
+                                     num_heads, S, S, qkv.stride(1), qkv.stride(0), out.stride(1),
+                                     out.stride(0), float(scale), _stream())
+    _lib.check(rc, "nos_attn_fwd_d64")
+    return out
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """q,k,v [B, S, H, 64] (rows contiguous per token) -> [B, Sq, H, 64]."""
+    if not q.is_cuda:
+        return attention_ref(q, k, v, scale)
+    B, Sq, H, D = q.shape
+    Skv = k.shape[1]
+    if D != 64:
+        raise ValueError("native attention supports head_dim 64")
+    for t in (q, k, v):
+        if t.stride(-1) != 1 or t.stride(-2) != D:
+            raise ValueError("q/k/v need contiguous heads")
+    if not (q.stride(1) == k.stride(1) == v.stride(1) and q.stride(0) == k.stride(0) == v.stride(0)):
+        raise ValueError("q/k/v must share row and batch strides")
+    if out is None:
+        out = torch.empty((B, Sq, H, D), dtype=q.dtype, device=q.device)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    rc = _lib.lib().nos_attn_fwd_d64(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B, H,
+                                     Sq, Skv, q.stride(1), q.stride(0), out.stride(1), out.stride(0),
+                                     float(scale), _stream())
+    _lib.check(rc, "nos_attn_fwd_d64")
+    return out
+
+
+__all__ = ["linear", "layernorm", "attention", "attention_qkv", "linear_ref", "layernorm_ref",
+           "attention_ref"]

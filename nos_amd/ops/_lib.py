@@ -1,0 +1,101 @@
+"""ctypes binding of ``libnos_hip.so`` (gfx950 kernels + CU-mask streams).
+
+The library is linked against PyTorch's own HIP runtime, so ``torch`` is
+imported first and raw device pointers / ``hipStream_t`` handles from torch
+are passed straight through.  On a machine with a GPU the library MUST load:
+:func:`lib` raises instead of silently falling back to eager PyTorch
+(``NOS_AMD_ALLOW_FALLBACK=1`` relaxes that for debugging only).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+_LIB_PATH = Path(__file__).resolve().parent.parent / "_native" / "libnos_hip.so"
+_lock = threading.Lock()
+_lib: ctypes.CDLL | None = None
+_err: str | None = None
+
+c_int, c_ll, c_float, c_void_p, c_double = (ctypes.c_int, ctypes.c_longlong, ctypes.c_float,
+                                            ctypes.c_void_p, ctypes.c_double)
+
+_SIGS = {
+    "nos_attn_fwd_d64": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                         c_ll, c_int, c_ll, c_float, c_void_p],
+    "nos_gemm_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                      c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nos_layernorm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                           c_int, c_int, c_float, c_void_p],
+    "nos_probe_placement": [c_void_p, c_int, c_int, c_void_p],
+    "nos_probe_hbm_copy": [c_void_p, c_void_p, c_ll, c_int, c_void_p],
+    "nos_probe_hbm": [c_void_p, c_ll, c_int, c_int, ctypes.POINTER(c_double)],
+    "nos_probe_mfma_peak": [c_void_p, c_int, c_int, ctypes.POINTER(c_double)],
+    "nos_probe_mfma_peak_launch": [c_void_p, c_int, c_int, c_void_p],
+    "nos_probe_gemm": [c_void_p, c_int, c_int, c_int, ctypes.POINTER(c_double)],
+    "nos_stream_create_cumask": [ctypes.POINTER(ctypes.c_uint), c_int, ctypes.POINTER(c_void_p)],
+    "nos_stream_get_cumask": [c_void_p, c_int, ctypes.POINTER(ctypes.c_uint)],
+    "nos_stream_destroy": [c_void_p],
+    "nos_stream_sync": [c_void_p],
+    "nos_device_info": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_ll), ctypes.POINTER(c_int),
+                        ctypes.c_char_p, c_int],
+    "nos_runtime_version": [ctypes.POINTER(c_int)],
+}
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def lib_path() -> Path:
+    return _LIB_PATH
+
+
+def _load() -> ctypes.CDLL:
+    import torch  # noqa: F401  -- binds the process's HIP runtime first
+
+    if not _LIB_PATH.exists():
+        raise NativeUnavailable(
+            f"{_LIB_PATH} missing: run `python -m nos_amd._native.build` (hipcc, gfx950)")
+    L = ctypes.CDLL(str(_LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+    for name, argtypes in _SIGS.items():
+        fn = getattr(L, name)
+        fn.argtypes = argtypes
+        fn.restype = c_int
+    return L
+
+
+def lib() -> ctypes.CDLL:
+    global _lib, _err
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            try:
+                _lib = _load()
+            except Exception as e:  # pragma: no cover - depends on build state
+                _err = str(e)
+                raise NativeUnavailable(_err) from e
+    return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:
+        return False
+
+
+def require_native_on_gpu() -> None:
+    """Raise if a GPU is present but the native library cannot be loaded."""
+    import torch
+
+    if torch.cuda.is_available() and not available() and os.environ.get("NOS_AMD_ALLOW_FALLBACK") != "1":
+        raise NativeUnavailable(f"GPU present but libnos_hip.so not loadable: {_err}")
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with hipError {rc}")

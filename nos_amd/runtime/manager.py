@@ -1,0 +1,331 @@
+"""Controller runtime: controllers, watches, manager, leader election, health.
+
+The controller-runtime pattern of the reference (``Reconcile(ctx, req)`` +
+``SetupWithManager``) on top of :mod:`nos_amd.sim.apiserver`:
+
+* a :class:`Controller` owns a de-duplicating work queue, a reconciler, its
+  watches (``for_kind`` = enqueue the object itself; ``watches`` = map
+  function) and predicates;
+* the :class:`Manager` registers one API watch per (controller, kind) and runs
+  the controllers either with worker threads (``start()``; ``max_concurrent``
+  workers per controller like ``MaxConcurrentReconciles``) or deterministically
+  (``run_until_idle()`` / ``run_for()``, which also advance a fake clock to the
+  next requeue) -- the latter replaces envtest's ``Eventually`` polling;
+* optional Lease-based leader election (``leaderElect: true`` in the
+  reference's component configs) and healthz/readyz checks.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+import traceback
+from dataclasses import dataclass, field
+from typing import Any, Callable, Protocol
+
+from ..kube import objects as ko
+from ..sim.apiserver import ADDED, DELETED, MODIFIED, AlreadyExists, ApiServer, Conflict, NotFound, WatchEvent
+from .predicates import Event, Predicate
+from .workqueue import WorkQueue
+
+log = logging.getLogger("nos_amd.runtime")
+
+
+@dataclass(frozen=True)
+class Request:
+    name: str
+    namespace: str = ""
+
+    def __str__(self) -> str:
+        return f"{self.namespace}/{self.name}" if self.namespace else self.name
+
+
+@dataclass
+class Result:
+    requeue: bool = False
+    requeue_after: float = 0.0
+
+
+class Reconciler(Protocol):
+    def reconcile(self, req: Request) -> Result | None: ...
+
+
+MapFunc = Callable[[dict], list[Request]]
+
+
+def request_for(obj: dict) -> Request:
+    return Request(ko.name(obj), ko.namespace(obj))
+
+
+@dataclass
+class _WatchSpec:
+    kind: str
+    mapper: MapFunc
+    predicates: list[Predicate] = field(default_factory=list)
+    namespace: str | None = None
+    label_selector: Any = None
+
+
+_EV_TYPE = {ADDED: "create", MODIFIED: "update", DELETED: "delete"}
+
+
+class Controller:
+    def __init__(self, name: str, reconciler: Reconciler, max_concurrent: int = 1):
+        self.name = name
+        self.reconciler = reconciler
+        self.max_concurrent = max_concurrent
+        self.watch_specs: list[_WatchSpec] = []
+        self.queue: WorkQueue | None = None
+        self.reconcile_count = 0
+        self.error_count = 0
+        self.last_error: str | None = None
+
+    def for_kind(self, kind: str, *predicates: Predicate, namespace: str | None = None,
+                 label_selector: Any = None) -> "Controller":
+        self.watch_specs.append(_WatchSpec(kind, lambda o: [request_for(o)], list(predicates), namespace,
+                                           label_selector))
+        return self
+
+    def watches(self, kind: str, mapper: MapFunc, *predicates: Predicate, namespace: str | None = None,
+                label_selector: Any = None) -> "Controller":
+        self.watch_specs.append(_WatchSpec(kind, mapper, list(predicates), namespace, label_selector))
+        return self
+
+    def _handle(self, spec: _WatchSpec, wev: WatchEvent) -> None:
+        ev = Event(_EV_TYPE[wev.type], wev.object, wev.old)
+        if not all(p(ev) for p in spec.predicates):
+            return
+        try:
+            reqs = spec.mapper(wev.object)
+        except Exception:  # a mapper must never kill the watch
+            log.exception("mapper failed in %s", self.name)
+            return
+        for r in reqs:
+            self.queue.add(r)
+
+    def process_one(self, item: Request) -> None:
+        try:
+            res = self.reconciler.reconcile(item) or Result()
+            self.reconcile_count += 1
+            if res.requeue_after > 0:
+                self.queue.forget(item)
+                self.queue.add_after(item, res.requeue_after)
+            elif res.requeue:
+                self.queue.add_rate_limited(item)
+            else:
+                self.queue.forget(item)
+        except Exception as e:
+            self.error_count += 1
+            self.last_error = f"{type(e).__name__}: {e}"
+            if not isinstance(e, (Conflict, NotFound)):
+                log.debug("reconcile %s %s failed: %s", self.name, item, traceback.format_exc())
+            self.queue.add_rate_limited(item)
+        finally:
+            self.queue.done(item)
+
+
+class LeaderElector:
+    """coordination.k8s.io/v1 Lease based leader election."""
+
+    def __init__(self, api: ApiServer, lease_name: str, namespace: str, identity: str,
+                 lease_duration: float = 15.0, clock=None):
+        self.api, self.name, self.ns, self.identity = api, lease_name, namespace, identity
+        self.duration = lease_duration
+        self.clock = clock or api.clock
+
+    def try_acquire_or_renew(self) -> bool:
+        now = self.clock.now()
+        lease = self.api.try_get("Lease", self.name, self.ns)
+        spec = {"holderIdentity": self.identity, "leaseDurationSeconds": int(self.duration),
+                "renewTime": ko.now_rfc3339(now)}
+        if lease is None:
+            try:
+                self.api.create({"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
+                                 "metadata": {"name": self.name, "namespace": self.ns},
+                                 "spec": {**spec, "acquireTime": ko.now_rfc3339(now)}})
+                return True
+            except AlreadyExists:
+                return False
+        s = lease.get("spec", {})
+        holder = s.get("holderIdentity")
+        expired = ko.parse_time(s.get("renewTime")) + float(s.get("leaseDurationSeconds", self.duration)) < now
+        if holder not in (None, "", self.identity) and not expired:
+            return False
+        if holder != self.identity:
+            spec["acquireTime"] = ko.now_rfc3339(now)
+            spec["leaseTransitions"] = int(s.get("leaseTransitions", 0)) + 1
+        lease["spec"] = {**s, **spec}
+        try:
+            self.api.update(lease)
+            return True
+        except Conflict:
+            return False
+
+    def release(self) -> None:
+        lease = self.api.try_get("Lease", self.name, self.ns)
+        if lease and lease.get("spec", {}).get("holderIdentity") == self.identity:
+            lease["spec"]["holderIdentity"] = ""
+            try:
+                self.api.update(lease)
+            except Conflict:
+                pass
+
+
+class Manager:
+    def __init__(self, api: ApiServer, name: str = "manager", clock=None, leader_election: bool = False,
+                 leader_election_id: str | None = None, leader_election_namespace: str = "nos-system",
+                 identity: str | None = None):
+        self.api = api
+        self.name = name
+        self.clock = clock or api.clock
+        self.controllers: list[Controller] = []
+        self.runnables: list[Any] = []
+        self._watches = []
+        self._threads: list[threading.Thread] = []
+        self._stop = threading.Event()
+        self.started = False
+        self.health_checks: dict[str, Callable[[], bool]] = {"ping": lambda: True}
+        self.ready_checks: dict[str, Callable[[], bool]] = {"ping": lambda: True}
+        self.elector = (LeaderElector(api, leader_election_id or f"{name}-leader", leader_election_namespace,
+                                      identity or f"{name}-{id(self):x}", clock=self.clock)
+                        if leader_election else None)
+        self.is_leader = not leader_election
+
+    def add(self, controller: Controller) -> Controller:
+        controller.queue = WorkQueue(self.clock)
+        self.controllers.append(controller)
+        if self.started:
+            self._bind(controller)
+        return controller
+
+    def add_runnable(self, r: Any) -> None:
+        """r has start(manager) and optionally stop()."""
+        self.runnables.append(r)
+
+    def _bind(self, c: Controller) -> None:
+        for spec in c.watch_specs:
+            w = self.api.watch(spec.kind, namespace=spec.namespace, label_selector=spec.label_selector,
+                               callback=lambda ev, c=c, spec=spec: c._handle(spec, ev))
+            self._watches.append(w)
+
+    # ------------------------------------------------------------ lifecycle
+    def _elect(self) -> bool:
+        if self.elector is None:
+            return True
+        self.is_leader = self.elector.try_acquire_or_renew()
+        return self.is_leader
+
+    def setup(self) -> None:
+        """Bind watches (initial lists enqueue every existing object)."""
+        if self.started:
+            return
+        self.started = True
+        for c in self.controllers:
+            self._bind(c)
+        for r in self.runnables:
+            if hasattr(r, "start"):
+                r.start(self)
+
+    def start(self) -> None:
+        """Threaded mode."""
+        if self.elector is not None:
+            while not self._stop.is_set() and not self._elect():
+                self._stop.wait(1.0)
+            t = threading.Thread(target=self._renew_loop, daemon=True, name=f"{self.name}-lease")
+            t.start()
+            self._threads.append(t)
+        self.setup()
+        for c in self.controllers:
+            for i in range(c.max_concurrent):
+                t = threading.Thread(target=self._worker, args=(c,), daemon=True, name=f"{c.name}-{i}")
+                t.start()
+                self._threads.append(t)
+
+    def _renew_loop(self) -> None:
+        while not self._stop.wait(max(0.5, self.elector.duration / 3)):
+            if not self._elect():
+                log.error("%s lost leadership", self.name)
+
+    def _worker(self, c: Controller) -> None:
+        while not self._stop.is_set():
+            item = c.queue.get(timeout=0.1)
+            if item is None:
+                continue
+            c.process_one(item)
+
+    def stop(self) -> None:
+        self._stop.set()
+        for c in self.controllers:
+            c.queue.shutdown()
+        for w in self._watches:
+            w.stop()
+        for r in self.runnables:
+            if hasattr(r, "stop"):
+                r.stop()
+        for t in self._threads:
+            t.join(timeout=2)
+        if self.elector is not None:
+            self.elector.release()
+
+    # ------------------------------------------------------------ deterministic mode
+    def step(self) -> int:
+        """Process every item ready now once; returns the number processed."""
+        if not self.started:
+            self.setup()
+        if not self.is_leader and not self._elect():
+            return 0
+        n = 0
+        for c in self.controllers:
+            while True:
+                item = c.queue.get_nowait()
+                if item is None:
+                    break
+                c.process_one(item)
+                n += 1
+                if n > 100000:
+                    raise RuntimeError("runaway reconcile loop")
+        return n
+
+    def next_wakeup(self) -> float | None:
+        ds = [d for c in self.controllers if (d := c.queue.next_delay()) is not None]
+        return min(ds) if ds else None
+
+    def run_until_idle(self, max_time: float = 0.0, max_steps: int = 10000) -> int:
+        """Run ready work; with a fake clock, advance time to due requeues up to `max_time` seconds."""
+        total = 0
+        start = self.clock.now()
+        for _ in range(max_steps):
+            n = self.step()
+            total += n
+            if n:
+                continue
+            d = self.next_wakeup()
+            if d is None or max_time <= 0:
+                break
+            if self.clock.now() + max(d, 0) - start > max_time:
+                break
+            if hasattr(self.clock, "advance"):
+                self.clock.advance(max(d, 0) + 1e-6)
+            else:
+                time.sleep(max(d, 0))
+        return total
+
+    def run_for(self, seconds: float, tick: float = 1.0) -> int:
+        """Advance a fake clock by `seconds` in `tick` increments, processing work."""
+        total = 0
+        end = self.clock.now() + seconds
+        while self.clock.now() < end:
+            total += self.run_until_idle()
+            if hasattr(self.clock, "advance"):
+                self.clock.advance(min(tick, end - self.clock.now()))
+            else:
+                time.sleep(min(tick, end - self.clock.now()))
+        total += self.run_until_idle()
+        return total
+
+    # ------------------------------------------------------------ health
+    def healthz(self) -> bool:
+        return all(f() for f in self.health_checks.values())
+
+    def readyz(self) -> bool:
+        return all(f() for f in self.ready_checks.values())
