@@ -2,50 +2,54 @@
 // YOLOS-family tenant model, bf16 in / bf16 out, fp32 softmax, head_dim 64.
 //
 // CDNA4 design (not a port of any CUDA kernel):
-//  * one workgroup = 4 waves = 128 query rows of one (batch, head); each wave
-//    owns 32 query rows and keeps them as the B operand of
-//    v_mfma_f32_32x32x16_bf16 for the whole kernel;
+//  * one workgroup = 8 waves = 128 query rows of one (batch, head), split in
+//    two wave groups that walk interleaved 64-key tiles of the same K/V
+//    stream (group 0: even tiles, group 1: odd tiles) -- two waves per SIMD
+//    from one workgroup, so one wave's MFMAs overlap the other's softmax,
+//    without shrinking the grid (one inference has only ~160 128-row blocks);
+//    the groups' partial (m, l, O) are merged through LDS at the end;
+//  * each wave owns 32 query rows, held for the whole kernel as the B
+//    operand of v_mfma_f32_32x32x16_bf16;
 //  * "swapped" QK^T: S^T = K . Q^T, so every lane holds 16 of the 32 key
-//    scores of ONE query row (column = lane & 31) -> the row max / row sum are
-//    lane-local except for a single lane^32 exchange;
+//    scores of ONE query row (column = lane & 31): row max / sum are
+//    lane-local plus one v_permlane32_swap;
 //  * the S^T accumulator is re-used in registers as the B operand of
 //    O^T = V^T . P^T (no LDS round trip for P);
 //  * V^T fragments come from a row-major, XOR-swizzled V tile through the
-//    gfx950 transposing LDS read ds_read_b64_tr_b16;
-//  * K is read with ds_read_b128 from an XOR-swizzled image (conflict-free
-//    for both 16-lane groups);
-//  * K/V tiles (64 keys) are double-buffered in LDS with register staging:
-//    the next tile's global loads are issued before the MFMA work of the
-//    current tile and written to LDS after it;
-//  * the workgroup -> (batch, head, q-block) map is XCD-aware so q-blocks of
-//    one head share an XCD's L2 (K/V of one head = 870 KB at S=3401).
+//    gfx950 transposing LDS read ds_read_b64_tr_b16; K is read with
+//    ds_read_b128 from an XOR-swizzled image (both conflict-free);
+//  * K/V tiles are double-buffered in LDS with register staging (next
+//    tiles' global loads are issued before the MFMA work, written after it);
+//  * XCD-aware workgroup -> (batch, head, q-block) map: q-blocks of one
+//    head share an XCD's L2 (K/V of one head = 870 KB at S = 3401).
 #include "common.h"
 
 namespace {
 
 constexpr int D = 64;
-constexpr int WAVES = 4;
-constexpr int QBLK = 32 * WAVES;  // query rows per workgroup
-constexpr int KVBLK = 64;         // keys per LDS tile
-constexpr int NT = 64 * WAVES;
-constexpr int TILE_BYTES = KVBLK * D * 2;      // 8 KiB
-constexpr int STAGE_BYTES = 2 * TILE_BYTES;    // K + V
+constexpr int QBLK = 128;          // query rows per workgroup (4 waves x 32)
+constexpr int KVBLK = 64;          // keys per tile (per wave group)
+constexpr int NT = 512;            // 8 waves
+constexpr int TILE_BYTES = KVBLK * D * 2;   // 8 KiB
+constexpr int PAIR_BYTES = 4 * TILE_BYTES;  // K0 V0 K1 V1 (one tile per group)
+constexpr int LDS_BYTES = 2 * PAIR_BYTES;   // double buffered: 64 KiB
 
-// byte offset of 16-byte chunk `ch` (0..7) of row `row` in the K image
 __device__ __forceinline__ int k_off(int row, int ch) {
   return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4);
 }
-// byte offset of chunk `ch` of row `row` in the V image (conflict-free for the
-// 4-row x 64-byte blocks that ds_read_b64_tr_b16 gathers per half-wave)
 __device__ __forceinline__ int v_off(int row, int ch) {
   return row * 128 + ((ch ^ (((row >> 1) & 1) << 2)) << 4);
 }
 
+__device__ __forceinline__ float xor32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 __global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
     const unsigned short* __restrict__ q, const unsigned short* __restrict__ k,
-    const unsigned short* __restrict__ v, unsigned short* __restrict__ o,
-    int B, int H, int Sq, int Skv, int ld_in, long long bs_in, int ld_out,
-    long long bs_out, float c /* softmax scale * log2(e) */, int nqb) {
+    const unsigned short* __restrict__ v, unsigned short* __restrict__ o, int B, int H, int Sq, int Skv,
+    int ld_in, long long bs_in, int ld_out, long long bs_out, float c /* scale * log2(e) */, int nqb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int nwg = B * H * nqb;
@@ -57,6 +61,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
 
   const int tid = threadIdx.x;
   const int wid = tid >> 6;
+  const int grp = wid >> 2;     // wave group: 0 even tiles, 1 odd tiles
+  const int wq = wid & 3;       // query slice of the wave
   const int lane = tid & 63;
   const int r = lane & 31;
   const int hh = lane >> 5;
@@ -66,40 +72,43 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
   const unsigned short* vb_ptr = v + b * bs_in + h * D;
 
   // ---- Q fragments (B operand): lane holds Q[row r][d = 16ks + 8hh .. +7]
-  const int qrow = qb * QBLK + wid * 32 + r;
+  const int qrow = qb * QBLK + wq * 32 + r;
   const int qrow_c = qrow < Sq ? qrow : Sq - 1;
   bf16x8_t qf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks)
     qf[ks] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + (long long)qrow_c * ld_in + ks * 16 + hh * 8);
 
-  // ---- staging helpers: each thread moves 2 K chunks + 2 V chunks per tile
+  // ---- staging: per iteration 2 tiles (128 keys); each thread moves 2 K + 2 V chunks
   uint4 kreg[2], vreg[2];
-  auto load_tile = [&](int t) {
+  auto load_pair = [&](int it) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int cid = tid + NT * i;
+      const int cid = tid + NT * i;         // 0..1023 = 128 rows x 8 chunks
       const int row = cid >> 3, ch = cid & 7;
-      int kv = t * KVBLK + row;
+      int kv = it * 2 * KVBLK + row;
       kv = kv < Skv ? kv : Skv - 1;
       kreg[i] = *reinterpret_cast<const uint4*>(kb_ptr + (long long)kv * ld_in + ch * 8);
       vreg[i] = *reinterpret_cast<const uint4*>(vb_ptr + (long long)kv * ld_in + ch * 8);
     }
   };
-  auto store_tile = [&](int stage) {
-    unsigned char* base = smem + stage * STAGE_BYTES;
+  auto store_pair = [&](int stage) {
+    unsigned char* base = smem + stage * PAIR_BYTES;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int cid = tid + NT * i;
       const int row = cid >> 3, ch = cid & 7;
-      *reinterpret_cast<uint4*>(base + k_off(row, ch)) = kreg[i];
-      *reinterpret_cast<uint4*>(base + TILE_BYTES + v_off(row, ch)) = vreg[i];
+      const int g = row >> 6, lr = row & 63;   // tile of group g
+      unsigned char* tb = base + g * 2 * TILE_BYTES;
+      *reinterpret_cast<uint4*>(tb + k_off(lr, ch)) = kreg[i];
+      *reinterpret_cast<uint4*>(tb + TILE_BYTES + v_off(lr, ch)) = vreg[i];
     }
   };
 
   const int ntiles = (Skv + KVBLK - 1) / KVBLK;
-  load_tile(0);
-  store_tile(0);
+  const int niters = (ntiles + 1) / 2;
+  load_pair(0);
+  store_pair(0);
   __syncthreads();
 
   f32x16_t oacc[2];
@@ -107,119 +116,131 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
   for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
   float m = -INFINITY, l = 0.f;
 
-  // tr-read lane geometry
   const int g16 = (lane >> 4) & 1;
   const int tq = (lane & 15) >> 2;
   const int tp = lane & 3;
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int stage = t & 1;
-    const bool has_next = (t + 1) < ntiles;
-    if (has_next) load_tile(t + 1);
+  for (int it = 0; it < niters; ++it) {
+    const int stage = it & 1;
+    const bool has_next = (it + 1) < niters;
+    if (has_next) load_pair(it + 1);
 
-    const unsigned char* kl = smem + stage * STAGE_BYTES;
-    const unsigned char* vl = kl + TILE_BYTES;
+    const int t = 2 * it + grp;  // this group's tile
+    if (t < ntiles) {
+      const unsigned char* kl = smem + stage * PAIR_BYTES + grp * 2 * TILE_BYTES;
+      const unsigned char* vl = kl + TILE_BYTES;
 
-    // ---- S^T = K . Q^T  (two 32-key blocks)
-    f32x16_t sacc[2];
+      f32x16_t sacc[2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+      for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
+        for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(kl + k_off(kb * 32 + r, 2 * ks + hh));
-        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], sacc[kb], 0, 0, 0);
+        for (int ks = 0; ks < 4; ++ks) {
+          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(kl + k_off(kb * 32 + r, 2 * ks + hh));
+          sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], sacc[kb], 0, 0, 0);
+        }
       }
-    }
-
-    // ---- mask keys past the end (only the last tile)
-    if ((t + 1) * KVBLK > Skv) {
+      if ((t + 1) * KVBLK > Skv) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int kv = t * KVBLK + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+            if (kv >= Skv) sacc[kb][i] = -INFINITY;
+          }
+      }
+      float mt = sacc[0][0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mt = fmaxf(mt, sacc[0][i]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[1][i]);
+      mt = xor32_max(mt);
+      const float m_new = fmaxf(m, mt);
+      const float alpha = __builtin_amdgcn_exp2f((m - m_new) * c);
+      m = m_new;
+      const float mc = m_new * c;
+      float psum = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int kv = t * KVBLK + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (kv >= Skv) sacc[kb][i] = -INFINITY;
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][i], c, -mc));
+          sacc[kb][i] = p;
+          psum += p;
         }
-    }
+      l = fmaf(l, alpha, psum);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
 
-    // ---- online softmax (per lane = per query row)
-    float mt = sacc[0][0];
-#pragma unroll
-    for (int i = 1; i < 16; ++i) mt = fmaxf(mt, sacc[0][i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[1][i]);
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float m_new = fmaxf(m, mt);
-    const float alpha = __builtin_amdgcn_exp2f((m - m_new) * c);
-    m = m_new;
-    const float mc = m_new * c;
-    float psum = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][i], c, -mc));
-        sacc[kb][i] = p;
-        psum += p;
-      }
-    l = fmaf(l, alpha, psum);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
-
-    // ---- P^T fragments (B operand of O^T = V^T . P^T), straight from registers
-    bf16x8_t pf[2][2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pf[kb][s2][j] = (__bf16)sacc[kb][8 * s2 + j];
-
-    // ---- O^T += V^T . P^T ; V^T fragments via the transposing LDS read
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      const int ch = 4 * db + 2 * g16 + (tp >> 1);
-      const int o8 = 8 * (tp & 1);
+      bf16x8_t pf[2][2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int row0 = kb * 32 + s2 * 16 + 4 * hh + tq;
-          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              LDS_PTR(s16x4_t, vl + v_off(row0, ch) + o8));
-          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              LDS_PTR(s16x4_t, vl + v_off(row0 + 8, ch) + o8));
-          const s16x8_t a16 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              __builtin_bit_cast(bf16x8_t, a16), pf[kb][s2], oacc[db], 0, 0, 0);
-        }
-    }
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pf[kb][s2][j] = (__bf16)sacc[kb][8 * s2 + j];
 
-    if (has_next) {
-      // every wave finished reading the buffer we are about to fill at the
-      // barrier that ended iteration t-1
-      store_tile(stage ^ 1);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const int ch = 4 * db + 2 * g16 + (tp >> 1);
+        const int o8 = 8 * (tp & 1);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int row0 = kb * 32 + s2 * 16 + 4 * hh + tq;
+            const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, vl + v_off(row0, ch) + o8));
+            const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, vl + v_off(row0 + 8, ch) + o8));
+            const s16x8_t a16 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a16), pf[kb][s2],
+                                                               oacc[db], 0, 0, 0);
+          }
+      }
     }
+    if (has_next) store_pair(stage ^ 1);
     __syncthreads();
   }
 
-  // ---- epilogue: normalise and store O[q][h*64 + d]
-  const float ltot = l + __shfl_xor(l, 32, 64);
-  const float inv = 1.f / ltot;
-  if (qrow < Sq) {
-    unsigned short* op = o + b * bs_out + (long long)qrow * ld_out + h * D;
+  // ---- merge the two groups' partial softmax states through LDS
+  // layout per group-1 wave: [32 O floats][m][l] per lane, 34 x 64 floats
+  float* xch = reinterpret_cast<float*>(smem) + wq * (34 * 64);
+  if (grp == 1) {
 #pragma unroll
-    for (int db = 0; db < 2; ++db)
+    for (int i = 0; i < 16; ++i) {
+      xch[i * 64 + lane] = oacc[0][i];
+      xch[(16 + i) * 64 + lane] = oacc[1][i];
+    }
+    xch[32 * 64 + lane] = m;
+    xch[33 * 64 + lane] = l;
+  }
+  __syncthreads();
+  if (grp == 0) {
+    const float m1 = xch[32 * 64 + lane];
+    const float l1 = xch[33 * 64 + lane];
+    const float mf = fmaxf(m, m1);
+    const float a0 = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m - mf) * c);
+    const float a1 = (m1 == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m1 - mf) * c);
+    float lt = l * a0 + l1 * a1;
+    lt += __shfl_xor(lt, 32, 64);
+    const float inv = 1.f / lt;
+    if (qrow < Sq) {
+      unsigned short* op = o + b * bs_out + (long long)qrow * ld_out + h * D;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = 32 * db + 8 * g + 4 * hh;
-        bf16x4_t ov;
+      for (int db = 0; db < 2; ++db)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ov[e] = (__bf16)(oacc[db][4 * g + e] * inv);
-        *reinterpret_cast<bf16x4_t*>(op + d) = ov;
-      }
+        for (int g = 0; g < 4; ++g) {
+          const int d = 32 * db + 8 * g + 4 * hh;
+          bf16x4_t ov;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int ri = 4 * g + e;
+            const float o1 = xch[(16 * db + ri) * 64 + lane];
+            ov[e] = (__bf16)((oacc[db][ri] * a0 + o1 * a1) * inv);
+          }
+          *reinterpret_cast<bf16x4_t*>(op + d) = ov;
+        }
+    }
   }
 }
 
@@ -228,17 +249,16 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
 // q/k/v: bf16 [B, S, *] rows with row stride ld_in (elements) and batch stride
 // bs_in; head h occupies columns [h*64, h*64+64) relative to each pointer.
 // o: bf16 [B, Sq, H*64 (+pad)] with row stride ld_out and batch stride bs_out.
-NOS_API int nos_attn_fwd_d64(const void* q, const void* k, const void* v, void* o, int B,
-                             int H, int Sq, int Skv, int ld_in, long long bs_in, int ld_out,
-                             long long bs_out, float scale, hipStream_t stream) {
+NOS_API int nos_attn_fwd_d64(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq,
+                             int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float scale,
+                             hipStream_t stream) {
   if (B <= 0 || H <= 0 || Sq <= 0 || Skv <= 0) return (int)hipErrorInvalidValue;
   if ((ld_in % 8) != 0 || (ld_out % 4) != 0) return (int)hipErrorInvalidValue;
   const int nqb = (Sq + QBLK - 1) / QBLK;
   const int nwg = B * H * nqb;
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_fwd_d64_kernel, dim3(nwg), dim3(NT), 2 * STAGE_BYTES, stream,
-                     (const unsigned short*)q, (const unsigned short*)k,
-                     (const unsigned short*)v, (unsigned short*)o, B, H, Sq, Skv, ld_in, bs_in,
-                     ld_out, bs_out, c, nqb);
+  hipLaunchKernelGGL(attn_fwd_d64_kernel, dim3(nwg), dim3(NT), LDS_BYTES, stream, (const unsigned short*)q,
+                     (const unsigned short*)k, (const unsigned short*)v, (unsigned short*)o, B, H, Sq, Skv, ld_in,
+                     bs_in, ld_out, bs_out, c, nqb);
   return (int)hipGetLastError();
 }

@@ -1,7 +1,10 @@
-// bf16 GEMM with fused epilogue for gfx950:  C[M,N] = act(A[M,K] . W[N,K]^T + bias) (+ R)
+// bf16 GEMM with fused prologue / epilogue for gfx950:
 //
-// This is the "linear layer" of the tenant models (W in nn.Linear [out, in]
-// layout) and the body of the gpuagent's MFMA probe (probe_mfma_bf16 runs it
+//   plain:   C[M,N] = act(A[M,K] . W[N,K]^T + bias) (+ R)
+//   LN-fused C[M,N] = act(LayerNorm(A)[M,K] . W[N,K]^T + bias)            (K == hidden)
+//
+// This is every linear layer of the tenant models (W in nn.Linear [out, in]
+// layout) and the body of the gpuagent's MFMA probe (probe_gemm runs it
 // persistently on a CU-masked stream to price a slice).
 //
 // CDNA4 design:
@@ -12,11 +15,20 @@
 //    instruction) into a lane-linear image; the XOR swizzle that makes the
 //    ds_read_b128 fragment reads conflict-free is applied to the per-lane
 //    SOURCE address (linear destination + inverse-swizzled source + swizzled
-//    read);
-//  * two LDS buffers (64 KiB): tile k+1 is in flight while tile k is consumed;
-//  * optional persistent mode (grid smaller than the tile count) with an
-//    XCD-aware tile order so neighbouring tiles share an XCD's L2;
-//  * epilogue fuses bias, exact-erf GELU and a residual add, bf16 out.
+//    read, cdna_hip_programming.md rule 21);
+//  * two LDS buffers: tile k+1 is in flight while tile k is consumed;
+//  * LayerNorm fusion without a normalised copy of A: with W' = W * gamma
+//    (per-k column scale, precomputed), c1[n] = sum_k W'[n,k],
+//    c2[n] = sum_k W[n,k] beta[k] + bias[n]:
+//        LN(x) . W^T + bias = rstd * (x . W'^T - mu * c1) + c2
+//    so the MFMA main loop runs on the raw residual stream; per-row mean /
+//    variance are accumulated from the A tiles already staged in LDS (the
+//    K loop covers the whole row because K == hidden);
+//  * epilogue through LDS: accumulators (+bias / LN correction / GELU) are
+//    written as fp32 to LDS, then every thread stores 16-byte bf16 chunks
+//    of whole rows (coalesced) and adds the residual with 16-byte loads;
+//  * optional persistent mode (grid smaller than the tile count) and an
+//    XCD-aware tile order so tiles sharing a W panel share an XCD's L2.
 #include "common.h"
 
 namespace {
@@ -26,6 +38,11 @@ constexpr int NT = 256;
 constexpr int TILE_A_BYTES = BM * BK * 2;  // 16 KiB
 constexpr int TILE_B_BYTES = BN * BK * 2;  // 16 KiB
 constexpr int STAGE_BYTES = TILE_A_BYTES + TILE_B_BYTES;
+constexpr int CT_LD = BN + 4;                        // fp32 C tile row stride (floats)
+constexpr int CT_BYTES = BM * CT_LD * 4;             // 67,584 B
+constexpr int MAIN_BYTES = (2 * STAGE_BYTES > CT_BYTES) ? 2 * STAGE_BYTES : CT_BYTES;
+constexpr int STATS_OFF = MAIN_BYTES;                // mu[128], rstd[128]
+constexpr int LDS_BYTES = MAIN_BYTES + 2 * BM * 4;
 
 enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
 
@@ -36,9 +53,8 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_ba
 }
 
 // Stage a [128 rows][64 k] bf16 tile: 16 wave-instructions, 4 per wave.
-__device__ __forceinline__ void stage_tile(const unsigned short* __restrict__ src, int ld,
-                                           int row0, int nrows, int k0,
-                                           unsigned char* tile, int wid, int lane) {
+__device__ __forceinline__ void stage_tile(const unsigned short* __restrict__ src, int ld, int row0,
+                                           int nrows, int k0, unsigned char* tile, int wid, int lane) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int R = (wid * 4 + i) * 8;
@@ -51,16 +67,31 @@ __device__ __forceinline__ void stage_tile(const unsigned short* __restrict__ sr
   }
 }
 
-__device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+// erf(x) for GELU: Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7, far below
+// bf16 output precision) -- one exp + one rcp instead of the libm erff.
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(-ax * ax * 1.4426950408889634f);
+  const float r = fmaf(-p * t, e, 1.f);
+  return copysignf(r, x);
 }
 
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
+
+template <bool LN>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
     const unsigned short* __restrict__ A, int lda, const unsigned short* __restrict__ W, int ldw,
-    const unsigned short* __restrict__ bias, const unsigned short* __restrict__ R, int ldr,
-    unsigned short* __restrict__ C, int ldc, int M, int N, int K, int epi, int tiles_m,
-    int tiles_n) {
+    const unsigned short* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
+    const unsigned short* __restrict__ R, int ldr, unsigned short* __restrict__ C, int ldc, int M, int N,
+    int K, int epi, float eps, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* s_mu = reinterpret_cast<float*>(smem + STATS_OFF);
+  float* s_rstd = s_mu + BM;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int r = lane & 31, hh = lane >> 5;
   const int wm = wid >> 1, wn = wid & 1;
@@ -68,7 +99,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
   const int nk = K / BK;
 
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    // XCD-aware order: consecutive tiles (same W panel) share an XCD
     const int tt = (gridDim.x >= ntiles) ? nos::xcd_remap(tile, ntiles) : tile;
     const int tn = tt / tiles_m;  // column-panel major: tiles of one W panel adjacent
     const int tm = tt - tn * tiles_m;
@@ -81,6 +111,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+    // LN statistics: thread owns half a row of every A tile (shifted sums)
+    const int srow = tid >> 1, shalf = tid & 1;
+    float sshift = 0.f, ssum = 0.f, ssq = 0.f;
 
     stage_tile(A, lda, m0, M, 0, smem, wid, lane);
     stage_tile(W, ldw, n0, N, 0, smem + TILE_A_BYTES, wid, lane);
@@ -95,6 +129,20 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
       }
       const unsigned char* ta = cur;
       const unsigned char* tb = cur + TILE_A_BYTES;
+      if constexpr (LN) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int lc = shalf * 4 + c;
+          const s16x8_t v = *reinterpret_cast<const s16x8_t*>(ta + srow * 128 + ((lc ^ swz(srow)) << 4));
+          if (kt == 0 && c == 0) sshift = nos::bf16_to_f32((unsigned short)v[0]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = nos::bf16_to_f32((unsigned short)v[e]) - sshift;
+            ssum += d;
+            ssq = fmaf(d, d, ssq);
+          }
+        }
+      }
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
         bf16x8_t af[2], bf[2];
@@ -117,26 +165,117 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
       __syncthreads();  // next tile landed; everyone done with `cur`
     }
 
-    // ---- fused epilogue
+    if constexpr (LN) {
+      // combine the two half-rows (both halves used the same shift: the
+      // shift of the lower half is broadcast first)
+      const float sh_lo = __shfl(sshift, lane & ~1, 64);
+      // re-base the upper half's sums onto the lower half's shift
+      const float dlt = sshift - sh_lo;
+      const float kh = (float)(K / 2);
+      float s2 = ssum + dlt * kh;
+      float q2 = ssq + 2.f * dlt * ssum + dlt * dlt * kh;
+      s2 += __shfl_xor(s2, 1, 64);
+      q2 += __shfl_xor(q2, 1, 64);
+      if (shalf == 0) {
+        const float mean_d = s2 / (float)K;
+        const float var = fmaxf(q2 / (float)K - mean_d * mean_d, 0.f);
+        s_mu[srow] = sh_lo + mean_d;
+        s_rstd[srow] = rsqrtf(var + eps);
+      }
+      __syncthreads();
+    }
+
+    // ---- epilogue stage 1: raw accumulators -> fp32 LDS tile
+    float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
-      const int n = n0 + wn * 64 + ni * 32 + r;
-      if (n >= N) continue;
-      const float bv = (epi & EPI_BIAS) ? nos::bf16_to_f32(bias[n]) : 0.f;
+      const int cl = wn * 64 + ni * 32 + r;
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int m = m0 + wm * 64 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (m >= M) continue;
-          float x = acc[mi][ni][i] + bv;
-          if (epi & EPI_GELU) x = gelu_erf(x);
-          if (epi & EPI_RELU) x = fmaxf(x, 0.f);
-          if (epi & EPI_RESID) x += nos::bf16_to_f32(R[(long long)m * ldr + n]);
-          C[(long long)m * ldc + n] = nos::f32_to_bf16(x);
+          const int rl = wm * 64 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          ct[rl * CT_LD + cl] = acc[mi][ni][i];
         }
     }
+    __syncthreads();
+
+    // ---- epilogue stage 2: per 8-column chunk of one row: bias / LN
+    // correction, activation, residual, coalesced 16-byte bf16 store
+#pragma unroll 2
+    for (int it = 0; it < (BM * BN / 8) / NT; ++it) {
+      const int c = tid + NT * it;
+      const int rl = c >> 4, ch = c & 15;
+      const int m = m0 + rl, n = n0 + ch * 8;
+      if (m >= M || n >= N) continue;
+      const float4 lo = *reinterpret_cast<const float4*>(ct + rl * CT_LD + ch * 8);
+      const float4 hi = *reinterpret_cast<const float4*>(ct + rl * CT_LD + ch * 8 + 4);
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      const bool full = (n + 8 <= N);
+      if (LN) {
+        const float mu = s_mu[rl], rs = s_rstd[rl];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int ne = full ? n + e : min(n + e, N - 1);
+          v[e] = fmaf(rs, v[e] - mu * c1[ne], c2[ne]);
+        }
+      } else if (epi & EPI_BIAS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += nos::bf16_to_f32(bias[full ? n + e : min(n + e, N - 1)]);
+      }
+      if (epi & EPI_GELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+      }
+      if (epi & EPI_RELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (full && ((ldc | ldr) & 7) == 0) {
+        if (epi & EPI_RESID) {
+          const s16x8_t rv = *reinterpret_cast<const s16x8_t*>(R + (long long)m * ldr + n);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += nos::bf16_to_f32((unsigned short)rv[e]);
+        }
+        s16x8_t o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (short)nos::f32_to_bf16(v[e]);
+        *reinterpret_cast<s16x8_t*>(C + (long long)m * ldc + n) = o;
+      } else {
+        for (int e = 0; e < 8 && n + e < N; ++e) {
+          float x = v[e];
+          if (epi & EPI_RESID) x += nos::bf16_to_f32(R[(long long)m * ldr + n + e]);
+          C[(long long)m * ldc + n + e] = nos::f32_to_bf16(x);
+        }
+      }
+    }
+    __syncthreads();  // LDS is restaged by the next persistent tile
   }
+}
+
+int launch(const void* A, int lda, const void* W, int ldw, const void* bias, const float* c1,
+           const float* c2, const void* R, int ldr, void* C, int ldc, int M, int N, int K, int epi,
+           float eps, int max_wg, bool ln, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0) return (int)hipErrorInvalidValue;
+  if ((lda % 8) || (ldw % 8)) return (int)hipErrorInvalidValue;
+  if (!ln && (epi & EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
+  if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
+  if ((epi & EPI_RESID) && !R) return (int)hipErrorInvalidValue;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  int nwg = tiles_m * tiles_n;
+  if (max_wg > 0 && nwg > max_wg) nwg = max_wg;
+  auto Ap = (const unsigned short*)A;
+  auto Wp = (const unsigned short*)W;
+  auto Bp = (const unsigned short*)bias;
+  auto Rp = (const unsigned short*)R;
+  auto Cp = (unsigned short*)C;
+  if (ln)
+    hipLaunchKernelGGL(gemm_bf16_kernel<true>, dim3(nwg), dim3(NT), LDS_BYTES, stream, Ap, lda, Wp, ldw, Bp, c1,
+                       c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+  else
+    hipLaunchKernelGGL(gemm_bf16_kernel<false>, dim3(nwg), dim3(NT), LDS_BYTES, stream, Ap, lda, Wp, ldw, Bp,
+                       c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -144,19 +283,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
 // C = act(A . W^T + bias) (+ R).  A [M,K] (row stride lda), W [N,K] (ldw),
 // R/C [M,N] (ldr/ldc), all bf16.  K must be a multiple of 64 and every row
 // start 16-byte aligned.  max_wg > 0 caps the grid (persistent mode).
-NOS_API int nos_gemm_bf16(const void* A, int lda, const void* W, int ldw, const void* bias,
-                          const void* R, int ldr, void* C, int ldc, int M, int N, int K, int epi,
-                          int max_wg, hipStream_t stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0) return (int)hipErrorInvalidValue;
-  if ((lda % 8) || (ldw % 8)) return (int)hipErrorInvalidValue;
-  if ((epi & EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
-  if ((epi & EPI_RESID) && !R) return (int)hipErrorInvalidValue;
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
-  int nwg = tiles_m * tiles_n;
-  if (max_wg > 0 && nwg > max_wg) nwg = max_wg;
-  hipLaunchKernelGGL(gemm_bf16_kernel, dim3(nwg), dim3(NT), 2 * STAGE_BYTES, stream,
-                     (const unsigned short*)A, lda, (const unsigned short*)W, ldw,
-                     (const unsigned short*)bias, (const unsigned short*)R, ldr,
-                     (unsigned short*)C, ldc, M, N, K, epi, tiles_m, tiles_n);
-  return (int)hipGetLastError();
+NOS_API int nos_gemm_bf16(const void* A, int lda, const void* W, int ldw, const void* bias, const void* R,
+                          int ldr, void* C, int ldc, int M, int N, int K, int epi, int max_wg,
+                          hipStream_t stream) {
+  return launch(A, lda, W, ldw, bias, nullptr, nullptr, R, ldr, C, ldc, M, N, K, epi, 0.f, max_wg, false,
+                stream);
+}
+
+// C = act(LayerNorm(A) . W^T + bias) with W' = W * gamma (bf16 [N,K]),
+// c1 = rowsum(W') and c2 = W . beta + bias (fp32 [N]) precomputed by the
+// caller; K is the LayerNorm width.
+NOS_API int nos_gemm_ln_bf16(const void* A, int lda, const void* Wg, int ldw, const float* c1,
+                             const float* c2, void* C, int ldc, int M, int N, int K, int epi, float eps,
+                             int max_wg, hipStream_t stream) {
+  return launch(A, lda, Wg, ldw, nullptr, c1, c2, nullptr, 0, C, ldc, M, N, K, epi & ~(EPI_BIAS | EPI_RESID),
+                eps, max_wg, true, stream);
 }

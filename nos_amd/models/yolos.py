@@ -201,26 +201,42 @@ class YolosDetector(nn.Module):
             outs.append(y)
         return outs[0], outs[1].float().sigmoid()
 
+    @torch.no_grad()
+    def folded_weights(self) -> list[dict[str, torch.Tensor]]:
+        """Per layer: LayerNorm folded into the following GEMM
+        (:func:`nos_amd.ops.fold_layernorm`); recomputed when a weight changes."""
+        key = tuple(p._version for p in self.parameters()) + (self.patch_w.device, self.patch_w.dtype)
+        if getattr(self, "_folded_key", None) != key:
+            out = []
+            for L in self.layers:
+                qw, qc1, qc2 = ops.fold_layernorm(L.qkv_w, L.qkv_b, L.ln1_w, L.ln1_b)
+                fw, fc1, fc2 = ops.fold_layernorm(L.fc1_w, L.fc1_b, L.ln2_w, L.ln2_b)
+                out.append({"qkv_w": qw, "qkv_c1": qc1, "qkv_c2": qc2, "fc1_w": fw, "fc1_c1": fc1, "fc1_c2": fc2})
+            self._folded = out
+            self._folded_key = key
+        return self._folded
+
     def _forward_native(self, pixel_values: torch.Tensor):
+        """5 kernels per encoder layer: [LN1+QKV GEMM] [attention]
+        [proj GEMM + residual] [LN2+fc1 GEMM + GELU] [fc2 GEMM + residual]."""
         cfg = self.cfg
         nh = cfg.num_attention_heads
+        eps = cfg.layer_norm_eps
 
         def lin(x, w, b, act=None, residual=None):
             return ops.linear(x.contiguous(), w, b, act=act, residual=residual)
 
+        folded = self.folded_weights()
         h = self._embed(pixel_values, lin)
-        eps = cfg.layer_norm_eps
-        for L in self.layers:
-            y, _ = ops.layernorm(h, L.ln1_w, L.ln1_b, eps)
-            qkv = ops.linear(y, L.qkv_w, L.qkv_b)
+        for L, fw in zip(self.layers, folded):
+            qkv = ops.linear_ln(h, fw["qkv_w"], fw["qkv_c1"], fw["qkv_c2"], eps=eps)
             a = ops.attention_qkv(qkv, nh)
             h = ops.linear(a, L.proj_w, L.proj_b, residual=h)
-            y, _ = ops.layernorm(h, L.ln2_w, L.ln2_b, eps)
-            m = ops.linear(y, L.fc1_w, L.fc1_b, act="gelu")
+            m = ops.linear_ln(h, fw["fc1_w"], fw["fc1_c1"], fw["fc1_c2"], act="gelu", eps=eps)
             h = ops.linear(m, L.fc2_w, L.fc2_b, residual=h)
-        y, _ = ops.layernorm(h, self.ln_f_w, self.ln_f_b, eps)
-        det = y[:, -cfg.num_detection_tokens:, :].contiguous()
-        return self._heads(det, lin)
+        det = h[:, -cfg.num_detection_tokens:, :].contiguous()
+        y, _ = ops.layernorm(det, self.ln_f_w, self.ln_f_b, eps)
+        return self._heads(y, lin)
 
     def _forward_torch(self, pixel_values: torch.Tensor):
         cfg = self.cfg

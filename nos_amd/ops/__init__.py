@@ -92,6 +92,57 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     return out.reshape(*x.shape[:-1], N)
 
 
+@torch.no_grad()
+def fold_layernorm(weight: torch.Tensor, bias: torch.Tensor | None, gamma: torch.Tensor, beta: torch.Tensor
+                   ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Fold LayerNorm(gamma, beta) into the following linear layer.
+
+    LN(x) @ W^T + b = rstd * (x @ (W*gamma)^T - mu * c1) + c2 with
+    c1 = rowsum(W*gamma) (from the bf16-rounded folded weight, so the identity
+    holds for the values the kernel multiplies) and c2 = W @ beta + b.
+    Returns (W*gamma in W's dtype, c1 fp32, c2 fp32)."""
+    wg = (weight.float() * gamma.float()[None, :]).to(weight.dtype).contiguous()
+    c1 = wg.float().sum(dim=1).contiguous()
+    c2 = weight.float() @ beta.float()
+    if bias is not None:
+        c2 = c2 + bias.float()
+    return wg, c1, c2.contiguous()
+
+
+def linear_ln_ref(x, wg, c1, c2, act=None, eps=1e-12):
+    xf = x.float()
+    mu = xf.mean(-1, keepdim=True)
+    var = xf.var(-1, unbiased=False, keepdim=True)
+    y = ((xf @ wg.float().t()) - mu * c1) * torch.rsqrt(var + eps) + c2
+    if act == "gelu":
+        y = F.gelu(y)
+    elif act == "relu":
+        y = F.relu(y)
+    return y.to(x.dtype)
+
+
+def linear_ln(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, act: str | None = None,
+              eps: float = 1e-12, out: torch.Tensor | None = None, max_wg: int = 0) -> torch.Tensor:
+    """act(LayerNorm(x) @ W^T + b) with LN folded by :func:`fold_layernorm`."""
+    if not x.is_cuda:
+        return linear_ln_ref(x, wg, c1, c2, act, eps)
+    K = x.shape[-1]
+    N = wg.shape[0]
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    if x2.stride(-1) != 1 or K % 64 or x.dtype != torch.bfloat16:
+        raise ValueError("native linear_ln needs bf16, unit inner stride and K % 64 == 0")
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    epi = EPI_GELU if act == "gelu" else (EPI_RELU if act == "relu" else 0)
+    o2 = out.reshape(-1, N)
+    rc = _lib.lib().nos_gemm_ln_bf16(x2.data_ptr(), x2.stride(0), wg.data_ptr(), wg.stride(0), c1.data_ptr(),
+                                     c2.data_ptr(), o2.data_ptr(), o2.stride(0), M, N, K, epi, float(eps), max_wg,
+                                     _stream())
+    _lib.check(rc, "nos_gemm_ln_bf16")
+    return out.reshape(*x.shape[:-1], N)
+
+
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12,
               residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
               sum_out: torch.Tensor | None = None):
@@ -161,5 +212,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["linear", "layernorm", "attention", "attention_qkv", "linear_ref", "layernorm_ref",
-           "attention_ref"]
+__all__ = ["linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+           "linear_ln_ref", "layernorm_ref", "attention_ref"]

@@ -26,6 +26,8 @@ _SIGS = {
                          c_ll, c_int, c_ll, c_float, c_void_p],
     "nos_gemm_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nos_gemm_ln_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                         c_int, c_int, c_float, c_int, c_void_p],
     "nos_layernorm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                            c_int, c_int, c_float, c_void_p],
     "nos_probe_placement": [c_void_p, c_int, c_int, c_void_p],

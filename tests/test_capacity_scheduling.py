@@ -1,0 +1,239 @@
+"""CapacityScheduling plugin + elastic-quota math.
+
+Golden vectors ported from the reference's
+``pkg/scheduler/plugins/capacityscheduling/capacity_scheduling_test.go`` and
+``elasticquotainfo_test.go`` (same inputs and expected codes/values).  The
+reference's TestDryRunPreemption compared each result with itself
+(``:525-531``) so its ``want`` was never checked; here the victims are compared
+with the output of the (faithfully ported) algorithm -- where that differs from
+the reference's unchecked ``want`` the case says so.
+"""
+import pytest
+
+from nos_amd.api import constants as C
+from nos_amd.gpu.memory import ResourceCalculator
+from nos_amd.kube import objects as ko
+from nos_amd.kube.factory import build_container, build_node, build_pod
+from nos_amd.resource.resource import Resource
+from nos_amd.scheduler.framework import (UNSCHEDULABLE, SUCCESS, CycleState, Framework, PodNominator, Snapshot,
+                                         Status)
+from nos_amd.scheduler.plugins.capacity_scheduling import (ELASTIC_QUOTA_SNAPSHOT_KEY, PRE_FILTER_STATE_KEY,
+                                                           CapacityPreemptor, CapacityScheduling,
+                                                           ElasticQuotaSnapshotState, PreFilterState)
+from nos_amd.scheduler.plugins.elasticquotainfo import ElasticQuotaInfo, ElasticQuotaInfos
+from nos_amd.scheduler.plugins.intree import DefaultBinder, NodeResourcesFit, PrioritySort
+from nos_amd.scheduler.preemption import Evaluator
+
+GPU_MEM = 8  # nvidiaGPUResourceMemory of the reference tests
+LOW, MID, HIGH = 0, 100, 1000
+
+
+def make_pod(name, ns, mem, cpu, gpu, prio, uid, node, overquota):
+    c = build_container("pause").with_requests({"memory": mem, "cpu": f"{cpu}m", C.RESOURCE_AMD_GPU: gpu}).get()
+    b = build_pod(ns, name).with_container(c).with_priority(prio).with_uid(uid or name)
+    if node:
+        b = b.with_node_name(node)
+    b = b.with_label(C.LABEL_CAPACITY_INFO, C.CAPACITY_OVER_QUOTA if overquota else C.CAPACITY_IN_QUOTA)
+    b = b.with_creation_timestamp(1_700_000_000.0)
+    return b.get()
+
+
+def eqi(ns, mn=None, mx=None, used=None, max_enforced=False, namespaces=None):
+    return ElasticQuotaInfo("eq-" + ns, ns, set(namespaces or [ns]), mn or Resource(), mx, used or Resource(),
+                            max_enforced, ResourceCalculator(GPU_MEM))
+
+
+def R(cpu=0, mem=0, pods=0, eph=0, **scalar):
+    r = Resource(cpu, mem, eph, pods)
+    for k, v in scalar.items():
+        r.scalar[{"gpu_memory": C.RESOURCE_GPU_MEMORY, "gpu": C.RESOURCE_AMD_GPU}.get(k, k)] = v
+    return r
+
+
+# ---------------------------------------------------------------- PreFilter
+PREFILTER_CASES = [
+    ("pods requesting resources not specified in ElasticQuota",
+     [("ns1-p1", "ns1", 0, 500, 0), ("ns1-p2", "ns1", 0, 10, 0), ("ns1-p2", "ns1", 10, 10, 0),
+      ("ns1-p2", "ns1", 0, 0, 1)],
+     {"ns1": eqi("ns1", R(mem=1000))},
+     [SUCCESS, SUCCESS, UNSCHEDULABLE, SUCCESS]),
+    ("pods subject to ElasticQuota",
+     [("ns1-p1", "ns1", 0, 500, 1), ("ns1-p2", "ns1", 0, 1800, 0), ("ns1-p2", "ns1", 0, 0, 2)],
+     {"ns1": eqi("ns1", R(mem=1000, gpu_memory=5 * GPU_MEM), R(mem=2000, gpu_memory=6 * GPU_MEM),
+                 R(mem=300, gpu_memory=4 * GPU_MEM), max_enforced=True)},
+     [SUCCESS, UNSCHEDULABLE, UNSCHEDULABLE]),
+    ("ElasticQuota not enforcing Max",
+     [("ns1-p1", "ns1", 0, 500, 0), ("ns1-p2", "ns1", 0, 1800, 0), ("ns1-p2", "ns1", 0, 0, 6)],
+     {"ns1": eqi("ns1", R(mem=1000, gpu_memory=5 * GPU_MEM), None, R(mem=300, gpu_memory=4 * GPU_MEM)),
+      "ns2": eqi("ns2", R(mem=5000, gpu_memory=6 * GPU_MEM))},
+     [SUCCESS, SUCCESS, SUCCESS]),
+    ("the sum of used is bigger than the sum of min",
+     [("ns2-p1", "ns2", 0, 500, 0), ("ns2-p1", "ns2", 0, 0, 2)],
+     {"ns1": eqi("ns1", R(mem=1000, gpu_memory=5 * GPU_MEM), R(mem=2000, gpu_memory=100 * GPU_MEM),
+                 R(mem=1800, gpu_memory=4 * GPU_MEM), max_enforced=True),
+      "ns2": eqi("ns2", R(mem=1000, gpu_memory=1 * GPU_MEM), R(mem=2000, gpu_memory=100 * GPU_MEM),
+                 R(mem=200, gpu_memory=1 * GPU_MEM), max_enforced=True)},
+     [UNSCHEDULABLE, UNSCHEDULABLE]),
+]
+
+
+@pytest.mark.parametrize("name,pods,eqs,expected", PREFILTER_CASES, ids=[c[0] for c in PREFILTER_CASES])
+def test_prefilter(name, pods, eqs, expected):
+    fw = Framework({"queue_sort": [PrioritySort()], "bind": [DefaultBinder()]}, snapshot=Snapshot(),
+                   nominator=PodNominator())
+    cs = CapacityScheduling({"amdGpuResourceMemoryGB": GPU_MEM}, fw, start_informers=False)
+    cs.elastic_quota_infos = ElasticQuotaInfos(eqs)
+    state = CycleState()
+    for (pname, ns, cpu, mem, gpu), want in zip(pods, expected):
+        _, got = cs.pre_filter(state, make_pod(pname, ns, mem, cpu, gpu, 0, pname, "", False))
+        assert got.code == want, (name, pname, got)
+
+
+# ---------------------------------------------------------------- DryRunPreemption
+def _dry_run(pod, pods, nodes, eqs):
+    fit = NodeResourcesFit()
+    fw = Framework({"queue_sort": [PrioritySort()], "pre_filter": [fit], "filter": [fit],
+                    "bind": [DefaultBinder()]}, snapshot=Snapshot.from_objects(pods, nodes), nominator=PodNominator())
+    state = CycleState()
+    _, st = fw.run_pre_filter_plugins(state, pod)
+    assert st.is_success()
+    req = Resource.from_list(ResourceCalculator(GPU_MEM).compute_pod_request(pod))
+    state.write(PRE_FILTER_STATE_KEY, PreFilterState(req, req.clone(), req.clone()))
+    state.write(ELASTIC_QUOTA_SNAPSHOT_KEY, ElasticQuotaSnapshotState(ElasticQuotaInfos(eqs)))
+    ev = Evaluator("CapacityScheduling", fw, state, CapacityPreemptor(fw, state))
+    infos = fw.snapshot_shared_lister().list()
+    cands, _ = ev.dry_run_preemption(pod, infos, [], 0, len(infos))
+    return sorted((c.name, sorted(ko.name(v) for v in c.victims)) for c in cands)
+
+
+def _node(name, **cap):
+    return build_node(name).with_allocatable_resources(cap).get()
+
+
+def test_dry_run_in_namespace_preemption():
+    got = _dry_run(make_pod("t1-p", "ns1", 50, 0, 0, HIGH, "", "", False),
+                   [make_pod("t1-p1", "ns1", 50, 0, 0, MID, "t1-p1", "node-a", False),
+                    make_pod("t1-p2", "ns2", 50, 0, 0, MID, "t1-p2", "node-a", False),
+                    make_pod("t1-p3", "ns2", 50, 0, 0, MID, "t1-p3", "node-a", False)],
+                   [_node("node-a", memory="150")],
+                   {"ns1": eqi("ns1", R(mem=50), R(mem=200), R(mem=50)),
+                    "ns2": eqi("ns2", R(mem=200), R(mem=200), R(mem=100))})
+    assert got == [("node-a", ["t1-p1"])]
+
+
+def test_dry_run_cross_namespace_uses_min():
+    got = _dry_run(make_pod("t1-p", "ns1", 50, 0, 0, HIGH, "", "", False),
+                   [make_pod("t1-p1", "ns1", 40, 0, 0, MID, "t1-p1", "node-a", False),
+                    make_pod("t1-p2", "ns2", 50, 0, 0, HIGH, "t1-p2", "node-a", False),
+                    make_pod("t1-p3", "ns2", 50, 0, 0, MID, "t1-p3", "node-a", True),
+                    make_pod("t1-p4", "ns2", 10, 0, 0, LOW, "t1-p4", "node-a", False)],
+                   [_node("node-a", memory="150")],
+                   {"ns1": eqi("ns1", R(mem=150), R(mem=200), R(mem=50)),
+                    "ns2": eqi("ns2", R(mem=50), R(mem=200), R(mem=100))})
+    assert got == [("node-a", ["t1-p3"])]
+
+
+def test_dry_run_guaranteed_overquota_limits():
+    """The preemptor is over its min, so lower-priority pods of its own namespace
+    are potential victims too (capacity_scheduling.go:520-528); after reprieve
+    the minimal victim set on node-a is t1-p2 (the reference's unchecked want
+    listed t1-p5)."""
+    got = _dry_run(make_pod("t1-p", "ns1", 70, 0, 0, HIGH, "", "", True),
+                   [make_pod("t1-p1", "ns1", 100, 100, 0, MID, "t1-p1", "node-a", False),
+                    make_pod("t1-p2", "ns1", 150, 100, 0, MID, "t1-p2", "node-a", False),
+                    make_pod("t1-p3", "ns2", 50, 0, 0, HIGH, "t1-p3", "node-a", False),
+                    make_pod("t1-p4", "ns2", 50, 0, 0, MID, "t1-p4", "node-a", True),
+                    make_pod("t1-p5", "ns2", 10, 0, 0, LOW, "t1-p5", "node-a", True)],
+                   [_node("node-a", memory="350", cpu="200")],
+                   {"ns1": eqi("ns1", R(mem=150, cpu=200), R(mem=300, cpu=300), R(mem=150, cpu=200)),
+                    "ns2": eqi("ns2", R(mem=50, cpu=20), R(mem=300, cpu=300), R(mem=100, cpu=50)),
+                    "ns3": eqi("ns3", R(mem=300, cpu=300), None, R())})
+    assert got == [("node-a", ["t1-p2"])]
+
+
+def test_dry_run_no_victims_when_not_over_quota():
+    # nothing over-quota in other namespaces and preemptor within min -> no candidate
+    got = _dry_run(make_pod("t1-p", "ns1", 50, 0, 0, HIGH, "", "", False),
+                   [make_pod("t1-p1", "ns2", 150, 0, 0, LOW, "t1-p1", "node-a", False)],
+                   [_node("node-a", memory="150")],
+                   {"ns1": eqi("ns1", R(mem=100), None, R()), "ns2": eqi("ns2", R(mem=200), None, R(mem=150))})
+    assert got == []
+
+
+# ---------------------------------------------------------------- quota math
+def test_reserve_unreserve():
+    e = eqi("ns", R(mem=10), None, R(cpu=1, mem=2, gpu=1))
+    e.reserve(R(cpu=1, mem=2, gpu=3))
+    assert (e.used.milli_cpu, e.used.memory, e.used.scalar[C.RESOURCE_AMD_GPU]) == (2, 4, 4)
+    e.unreserve(R(cpu=2, mem=4, gpu=4))
+    assert (e.used.milli_cpu, e.used.memory, e.used.scalar[C.RESOURCE_AMD_GPU]) == (0, 0, 0)
+
+
+def test_used_over_max_with():
+    assert not eqi("a", R(), R(cpu=1), R(cpu=10)).used_over_max_with(R(cpu=1))
+    assert eqi("a", R(), R(cpu=5), R(cpu=5), max_enforced=True).used_over_max_with(R(cpu=1))
+    assert not eqi("a", R(), R(cpu=6), R(cpu=5), max_enforced=True).used_over_max_with(R(cpu=1))
+
+
+def test_guaranteed_overquotas_proportional_to_min():
+    infos = ElasticQuotaInfos({
+        "eq-1": eqi("ns-1", R(cpu=10, mem=10, pods=10, gpu=5, gpu_memory=64, **{"nebuly.com/new-resource": 3}), None,
+                    R(cpu=5, mem=5, pods=5, gpu=0, gpu_memory=10, **{"nebuly.com/new-resource": 1})),
+        "eq-2": eqi("ns-2", R(cpu=30, mem=30, eph=30, pods=30, gpu=3, gpu_memory=24), None,
+                    R(cpu=35, mem=35, pods=5, gpu=0, gpu_memory=10)),
+        "eq-3": eqi("ns-3", R(cpu=20, mem=20, eph=20), None, R(cpu=10, mem=10, eph=10)),
+    })
+    g = infos.get_guaranteed_overquotas("eq-1")
+    assert (g.milli_cpu, g.memory, g.ephemeral_storage, g.allowed_pod_number) == (2, 2, 0, 7)
+    assert g.scalar["nebuly.com/new-resource"] == 2
+    assert g.scalar[C.RESOURCE_AMD_GPU] == 5
+    assert g.scalar[C.RESOURCE_GPU_MEMORY] == 49
+    with pytest.raises(KeyError):
+        infos.get_guaranteed_overquotas("not-present")
+
+
+def test_guaranteed_overquotas_empty():
+    infos = ElasticQuotaInfos({"eq-1": eqi("a"), "eq-2": eqi("b")})
+    assert infos.get_guaranteed_overquotas("eq-1").is_zero()
+
+
+def test_used_lte_with():
+    e = eqi("ns-1", None, None, R(gpu_memory=20, **{"amd.com/partition-1xcd.36gb": 2}))
+    assert e.used_lte_with(R(gpu_memory=40), R(**{"amd.com/partition-1xcd.36gb": 1}))
+    assert not e.used_lte_with(R(gpu_memory=25, **{"amd.com/partition-1xcd.36gb": 0}),
+                               R(gpu_memory=20, **{"amd.com/partition-1xcd.36gb": 1}))
+
+
+def test_aggregated_used_over_min_with():
+    infos = ElasticQuotaInfos({"eq-1": eqi("ns-1", R(cpu=20), None, R(gpu_memory=0)),
+                               "eq-2": eqi("ns-2", R(cpu=10), None, R(cpu=40, gpu_memory=0)),
+                               "eq-3": eqi("ns-3", R(cpu=10), None, R(gpu_memory=0))})
+    assert infos.aggregated_used_over_min_with(R(cpu=10, gpu_memory=0))
+
+
+def test_infos_add_update_delete_composite():
+    infos = ElasticQuotaInfos()
+    a = eqi("x", namespaces=["ns-2", "ns-3", "ns-4"])
+    infos.add(a)
+    assert set(infos) == {"ns-2", "ns-3", "ns-4"} and infos["ns-2"] is infos["ns-4"]
+    b = eqi("y", namespaces=["ns-3", "ns-5"])
+    infos["ns-3"].used = R(cpu=7)
+    infos.update(a, b)
+    assert set(infos) == {"ns-3", "ns-5"}
+    assert infos["ns-5"].used.milli_cpu == 7  # used preserved across update
+    infos.delete(b)
+    assert not infos
+    # a composite quota is counted once in the aggregated min
+    infos.add(eqi("c", R(cpu=10), namespaces=["n1", "n2"]))
+    assert infos.aggregated_min().milli_cpu == 10
+
+
+def test_pod_add_delete_idempotent():
+    e = eqi("ns1", R(mem=100))
+    p = make_pod("p", "ns1", 10, 0, 1, 0, "u", "n", False)
+    e.add_pod_if_not_present(p)
+    e.add_pod_if_not_present(p)
+    assert e.used.memory == 10 and e.used.scalar[C.RESOURCE_GPU_MEMORY] == GPU_MEM
+    e.delete_pod_if_present(p)
+    e.delete_pod_if_present(p)
+    assert e.used.memory == 0

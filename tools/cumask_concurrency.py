@@ -19,7 +19,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
 TOTAL_WG = 512      # 2 per CU of the whole GPU
-ITERS = 4000
+ITERS = 200000
 
 
 def inproc(n: int, masked: bool) -> dict:

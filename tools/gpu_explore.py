@@ -36,7 +36,18 @@ def check_numerics(res: dict) -> None:
         ref = ops.linear_ref(x.cpu(), w.cpu(), b.cpu(), act=act, residual=r.cpu()).float()
         err = (y.float().cpu() - ref).abs().max().item()
         out[f"gemm_{M}x{N}x{K}_{act}"] = err
-    for (B, S, H) in [(1, 3401, 6), (2, 200, 2), (1, 64, 1), (1, 1000, 3)]:
+    for (M, N, K, act) in [(3401, 1152, 384, None), (3401, 1536, 384, "gelu"), (77, 100, 128, None)]:
+        x = torch.randn(M, K, device=dev, dtype=torch.bfloat16) * 2 + 0.5
+        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.05
+        b = torch.randn(N, device=dev, dtype=torch.bfloat16)
+        g = torch.randn(K, device=dev, dtype=torch.bfloat16)
+        be = torch.randn(K, device=dev, dtype=torch.bfloat16)
+        wg, c1, c2 = ops.fold_layernorm(w, b, g, be)
+        y = ops.linear_ln(x, wg, c1, c2, act=act)
+        ln = torch.nn.functional.layer_norm(x.float().cpu(), (K,), g.float().cpu(), be.float().cpu(), 1e-12)
+        ref = ops.linear_ref(ln.bfloat16(), w.cpu(), b.cpu(), act=act).float()
+        out[f"gemm_ln_{M}x{N}x{K}_{act}"] = (y.float().cpu() - ref).abs().max().item()
+    for (B, S, H) in [(1, 3401, 6), (2, 200, 2), (1, 64, 1), (1, 1000, 3), (1, 65, 2)]:
         qkv = torch.randn(B, S, 3 * H * 64, device=dev, dtype=torch.bfloat16)
         o = ops.attention_qkv(qkv, H)
         ref = ops.attention_qkv(qkv.cpu().float(), H)
