@@ -18,8 +18,14 @@
 //  * V^T fragments come from a row-major, XOR-swizzled V tile through the
 //    gfx950 transposing LDS read ds_read_b64_tr_b16; K is read with
 //    ds_read_b128 from an XOR-swizzled image (both conflict-free);
-//  * K/V tiles are double-buffered in LDS with register staging (next
-//    tiles' global loads are issued before the MFMA work, written after it);
+//  * K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
+//    instruction) into a 2-deep ring: no staging registers, no ds_write;
+//    the swizzle is applied to the per-lane SOURCE address (linear LDS
+//    destination, cdna_hip_programming.md rule 21);
+//  * every LDS address is a per-lane base register + an immediate: the
+//    swizzle terms that vary per lane are hoisted out of the key loop;
+//  * deferred rescale (T13): O and l are only rescaled when some row's
+//    running max grows by more than 8 (log2 units); P is bounded by 2^8;
 //  * XCD-aware workgroup -> (batch, head, q-block) map: q-blocks of one
 //    head share an XCD's L2 (K/V of one head = 870 KB at S = 3401).
 #include "common.h"
@@ -32,21 +38,22 @@ constexpr int KVBLK = 64;          // keys per tile (per wave group)
 constexpr int NT = 512;            // 8 waves
 constexpr int TILE_BYTES = KVBLK * D * 2;   // 8 KiB
 constexpr int PAIR_BYTES = 4 * TILE_BYTES;  // K0 V0 K1 V1 (one tile per group)
-constexpr int LDS_BYTES = 2 * PAIR_BYTES;   // double buffered: 64 KiB
+constexpr int LDS_BYTES = 2 * PAIR_BYTES;   // 2-deep ring: 64 KiB
+constexpr float RESCALE_THR = 8.f;          // log2 units
 
-__device__ __forceinline__ int k_off(int row, int ch) {
-  return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4);
-}
-__device__ __forceinline__ int v_off(int row, int ch) {
-  return row * 128 + ((ch ^ (((row >> 1) & 1) << 2)) << 4);
-}
+__device__ __forceinline__ int kswz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int vswz(int row) { return ((row >> 1) & 1) << 2; }
 
 __device__ __forceinline__ float xor32_max(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-__global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
+__device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__global__ __launch_bounds__(NT, 4) void attn_fwd_d64_kernel(
     const unsigned short* __restrict__ q, const unsigned short* __restrict__ k,
     const unsigned short* __restrict__ v, unsigned short* __restrict__ o, int B, int H, int Sq, int Skv,
     int ld_in, long long bs_in, int ld_out, long long bs_out, float c /* scale * log2(e) */, int nqb) {
@@ -60,7 +67,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
   const int qb = rem - h * nqb;
 
   const int tid = threadIdx.x;
-  const int wid = tid >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> SGPR branches
   const int grp = wid >> 2;     // wave group: 0 even tiles, 1 odd tiles
   const int wq = wid & 3;       // query slice of the wave
   const int lane = tid & 63;
@@ -79,55 +86,59 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
   for (int ks = 0; ks < 4; ++ks)
     qf[ks] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + (long long)qrow_c * ld_in + ks * 16 + hh * 8);
 
-  // ---- staging: per iteration 2 tiles (128 keys); each thread moves 2 K + 2 V chunks
-  uint4 kreg[2], vreg[2];
-  auto load_pair = [&](int it) {
+  // ---- LDS-DMA staging: per iteration 2 tiles x (K + V) = 32 x 1 KiB pieces,
+  // 4 per wave.  Piece p (0..31): tensor p>>4 (K/V), tile-row block (p&15)*8.
+  // Lane L writes row R + L/8, physical chunk L%8 = logical chunk ^ swizzle.
+  auto stage = [&](int it, int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int cid = tid + NT * i;         // 0..1023 = 128 rows x 8 chunks
-      const int row = cid >> 3, ch = cid & 7;
+    for (int i = 0; i < 4; ++i) {
+      const int p = wid * 4 + i;
+      const int is_v = p >> 4;
+      const int R = (p & 15) * 8;          // 0..120 across the two tiles
+      const int row = R + (lane >> 3);     // 0..127
+      const int g = row >> 6, lr = row & 63;
+      const int pc = lane & 7;
+      const int lc = pc ^ (is_v ? vswz(lr) : kswz(lr));
       int kv = it * 2 * KVBLK + row;
       kv = kv < Skv ? kv : Skv - 1;
-      kreg[i] = *reinterpret_cast<const uint4*>(kb_ptr + (long long)kv * ld_in + ch * 8);
-      vreg[i] = *reinterpret_cast<const uint4*>(vb_ptr + (long long)kv * ld_in + ch * 8);
-    }
-  };
-  auto store_pair = [&](int stage) {
-    unsigned char* base = smem + stage * PAIR_BYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int cid = tid + NT * i;
-      const int row = cid >> 3, ch = cid & 7;
-      const int g = row >> 6, lr = row & 63;   // tile of group g
-      unsigned char* tb = base + g * 2 * TILE_BYTES;
-      *reinterpret_cast<uint4*>(tb + k_off(lr, ch)) = kreg[i];
-      *reinterpret_cast<uint4*>(tb + TILE_BYTES + v_off(lr, ch)) = vreg[i];
+      const unsigned short* src = (is_v ? vb_ptr : kb_ptr) + (long long)kv * ld_in + lc * 8;
+      unsigned char* dst = smem + buf * PAIR_BYTES + g * 2 * TILE_BYTES + is_v * TILE_BYTES + (R & 63) * 128;
+      glds16(src, dst);
     }
   };
 
   const int ntiles = (Skv + KVBLK - 1) / KVBLK;
   const int niters = (ntiles + 1) / 2;
-  load_pair(0);
-  store_pair(0);
-  __syncthreads();
+  stage(0, 0);
+
+  // hoisted per-lane LDS offsets (relative to the group's K / V tile)
+  int koff[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) koff[ks] = r * 128 + (((2 * ks + hh) ^ kswz(r)) << 4);
+  const int g16 = (lane >> 4) & 1;
+  const int tq = (lane & 15) >> 2;
+  const int tp = lane & 3;
+  const int vlb = (tq >> 1) & 1;  // (row >> 1) & 1 of every row this lane's tr-reads touch
+  int voff[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+    voff[db] = (4 * hh + tq) * 128 + (((4 * (db ^ vlb)) + 2 * g16 + (tp >> 1)) << 4) + 8 * (tp & 1);
 
   f32x16_t oacc[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
   float m = -INFINITY, l = 0.f;
+  const float thr = RESCALE_THR / c;  // in raw score units
 
-  const int g16 = (lane >> 4) & 1;
-  const int tq = (lane & 15) >> 2;
-  const int tp = lane & 3;
+  __syncthreads();  // drains stage 0 (vmcnt(0)) and publishes it
 
   for (int it = 0; it < niters; ++it) {
-    const int stage = it & 1;
-    const bool has_next = (it + 1) < niters;
-    if (has_next) load_pair(it + 1);
+    const int buf = it & 1;
+    if (it + 1 < niters) stage(it + 1, buf ^ 1);  // buffer freed by the barrier that ended it-1
 
     const int t = 2 * it + grp;  // this group's tile
     if (t < ntiles) {
-      const unsigned char* kl = smem + stage * PAIR_BYTES + grp * 2 * TILE_BYTES;
+      const unsigned char* kl = smem + buf * PAIR_BYTES + grp * 2 * TILE_BYTES;
       const unsigned char* vl = kl + TILE_BYTES;
 
       f32x16_t sacc[2];
@@ -137,7 +148,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
         for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(kl + k_off(kb * 32 + r, 2 * ks + hh));
+          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(kl + koff[ks] + kb * 32 * 128);
           sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], sacc[kb], 0, 0, 0);
         }
       }
@@ -156,10 +167,16 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
 #pragma unroll
       for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[1][i]);
       mt = xor32_max(mt);
-      const float m_new = fmaxf(m, mt);
-      const float alpha = __builtin_amdgcn_exp2f((m - m_new) * c);
-      m = m_new;
-      const float mc = m_new * c;
+      // deferred rescale: only when some row's max grew by more than thr
+      if (!__all(mt - m <= thr)) {
+        const float m_new = fmaxf(m, mt);
+        const float alpha = __builtin_amdgcn_exp2f((m - m_new) * c);
+        m = m_new;
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+      }
+      const float mc = m * c;
       float psum = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
@@ -169,9 +186,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
           sacc[kb][i] = p;
           psum += p;
         }
-      l = fmaf(l, alpha, psum);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { oacc[0][i] *= alpha; oacc[1][i] *= alpha; }
+      l += psum;
 
       bf16x8_t pf[2][2];
 #pragma unroll
@@ -183,23 +198,20 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_d64_kernel(
 
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
-        const int ch = 4 * db + 2 * g16 + (tp >> 1);
-        const int o8 = 8 * (tp & 1);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
-            const int row0 = kb * 32 + s2 * 16 + 4 * hh + tq;
-            const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, vl + v_off(row0, ch) + o8));
-            const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, vl + v_off(row0 + 8, ch) + o8));
+            const unsigned char* base = vl + voff[db] + (kb * 32 + s2 * 16) * 128;
+            const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base));
+            const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + 8 * 128));
             const s16x8_t a16 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a16), pf[kb][s2],
                                                                oacc[db], 0, 0, 0);
           }
       }
     }
-    if (has_next) store_pair(stage ^ 1);
-    __syncthreads();
+    __syncthreads();  // next stage landed (vmcnt(0)); everyone done with `buf`
   }
 
   // ---- merge the two groups' partial softmax states through LDS

@@ -41,8 +41,8 @@ constexpr int STAGE_BYTES = TILE_A_BYTES + TILE_B_BYTES;
 constexpr int CT_LD = BN + 4;                        // fp32 C tile row stride (floats)
 constexpr int CT_BYTES = BM * CT_LD * 4;             // 67,584 B
 constexpr int MAIN_BYTES = (2 * STAGE_BYTES > CT_BYTES) ? 2 * STAGE_BYTES : CT_BYTES;
-constexpr int STATS_OFF = MAIN_BYTES;                // mu[128], rstd[128]
-constexpr int LDS_BYTES = MAIN_BYTES + 2 * BM * 4;
+constexpr int STATS_OFF = MAIN_BYTES;                // mu[128], rstd[128], p1[128], p2[128]
+constexpr int LDS_BYTES = MAIN_BYTES + 4 * BM * 4;
 
 enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
 
@@ -92,6 +92,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* s_mu = reinterpret_cast<float*>(smem + STATS_OFF);
   float* s_rstd = s_mu + BM;
+  float* s_p1 = s_rstd + BM;
+  float* s_p2 = s_p1 + BN;
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int r = lane & 31, hh = lane >> 5;
   const int wm = wid >> 1, wn = wid & 1;
@@ -198,6 +200,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
           ct[rl * CT_LD + cl] = acc[mi][ni][i];
         }
     }
+    // per-column epilogue parameters, loaded once per tile: (c1, c2) for the
+    // LN-fused form, (0, bias) otherwise
+    if (tid < BN) {
+      const int n = min(n0 + tid, N - 1);
+      s_p1[tid] = LN ? c1[n] : 0.f;
+      s_p2[tid] = LN ? c2[n] : ((epi & EPI_BIAS) ? nos::bf16_to_f32(bias[n]) : 0.f);
+    }
     __syncthreads();
 
     // ---- epilogue stage 2: per 8-column chunk of one row: bias / LN
@@ -212,16 +221,21 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
       const float4 hi = *reinterpret_cast<const float4*>(ct + rl * CT_LD + ch * 8 + 4);
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       const bool full = (n + 8 <= N);
-      if (LN) {
-        const float mu = s_mu[rl], rs = s_rstd[rl];
+      {
+        const float4 p1a = *reinterpret_cast<const float4*>(s_p1 + ch * 8);
+        const float4 p1b = *reinterpret_cast<const float4*>(s_p1 + ch * 8 + 4);
+        const float4 p2a = *reinterpret_cast<const float4*>(s_p2 + ch * 8);
+        const float4 p2b = *reinterpret_cast<const float4*>(s_p2 + ch * 8 + 4);
+        const float p1[8] = {p1a.x, p1a.y, p1a.z, p1a.w, p1b.x, p1b.y, p1b.z, p1b.w};
+        const float p2[8] = {p2a.x, p2a.y, p2a.z, p2a.w, p2b.x, p2b.y, p2b.z, p2b.w};
+        if (LN) {
+          const float mu = s_mu[rl], rs = s_rstd[rl];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int ne = full ? n + e : min(n + e, N - 1);
-          v[e] = fmaf(rs, v[e] - mu * c1[ne], c2[ne]);
+          for (int e = 0; e < 8; ++e) v[e] = fmaf(rs, v[e] - mu * p1[e], p2[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += p2[e];
         }
-      } else if (epi & EPI_BIAS) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += nos::bf16_to_f32(bias[full ? n + e : min(n + e, N - 1)]);
       }
       if (epi & EPI_GELU) {
 #pragma unroll

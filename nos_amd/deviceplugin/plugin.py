@@ -1,0 +1,241 @@
+"""nos-amd device plugin: the devices the kubelet hands to pods.
+
+Replaces the NVIDIA device plugin + MPS daemon the reference depends on
+(SURVEY.md 2.8).  It advertises three kinds of extended resources:
+
+* ``amd.com/gpu`` -- whole GPUs (nodes without a partitioning label, or
+  ``exposePartitionsAsGpu`` in static CPX mode: every logical partition is an
+  ``amd.com/gpu``, BASELINE config 2);
+* ``amd.com/partition-<n>xcd.<gb>gb`` -- the logical GPUs of the current
+  compute/memory partition mode (amdpart nodes), read from amd-smi;
+* ``amd.com/gpu-<gb>gb`` -- CU-mask slices (cumask nodes), replicas of each
+  GPU as listed by the gpupartitioner's plugin ConfigMap entry.
+
+``allocate`` returns what a real ``ContainerAllocateResponse`` carries:
+``HIP_VISIBLE_DEVICES`` (the physical / logical GPU), ``ROC_GLOBAL_CU_MASK``
+for slices (XCD-symmetric, see :mod:`nos_amd.gpu.topology`),
+``NOS_AMD_MEMORY_LIMIT_GB`` (cooperative memory cap; AMD has no MPS-style hard
+limit, SURVEY.md 7.4 hard part 3) and the ``/dev/kfd`` + ``/dev/dri/renderD*``
+device nodes.  CU masks of allocated replicas never move: when the slice
+table changes, new replicas are laid out in the CU slots left free.
+
+The configuration is re-read on change (no plugin restart, unlike the
+reference's NVIDIA plugin).  :mod:`nos_amd.deviceplugin.grpc_server` exposes
+this object over the kubelet device-plugin v1beta1 gRPC API.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+from dataclasses import dataclass, field
+
+import yaml
+
+from ..api import constants as C
+from ..gpu.amdsmi import PARTITIONS_PER_MODE, AmdSmi, GpuInfo
+from ..gpu.topology import MI355X_CUS_PER_XCD, MI355X_XCDS, CUSlice, logical_cu
+from ..ops.streams import mask_hex
+
+log = logging.getLogger("nos_amd.deviceplugin")
+
+
+@dataclass
+class Device:
+    id: str
+    resource: str
+    gpu_index: int
+    healthy: bool = True
+    partition: int = 0          # logical partition index (amdpart)
+    profile: str = ""           # partition / slice profile
+    memory_gb: int = 0
+
+
+@dataclass
+class ContainerAllocation:
+    envs: dict[str, str] = field(default_factory=dict)
+    devices: list[str] = field(default_factory=list)
+    device_ids: list[str] = field(default_factory=list)
+
+
+class NosAmdDevicePlugin:
+    def __init__(self, node_name: str, smi: AmdSmi, mode: str | None = None, expose_partitions_as_gpu: bool = False,
+                 cu_policy: str = "even"):
+        self.node_name = node_name
+        self.smi = smi
+        self.mode = mode              # None | "partition" | "cumask"
+        self.expose_partitions_as_gpu = expose_partitions_as_gpu
+        self.cu_policy = cu_policy
+        self._lock = threading.RLock()
+        self.config: dict | None = None
+        self.config_key: str | None = None
+        self.devices: dict[str, Device] = {}
+        self.allocated: dict[str, str] = {}      # device id -> owner (pod uid / container)
+        self.cu_slots: dict[str, CUSlice] = {}   # slice device id -> CU slot
+        self.listeners: list = []
+        self.generation = 0
+        self.refresh()
+
+    # ------------------------------------------------------------ inventory
+    def _gpus(self) -> list[GpuInfo]:
+        return self.smi.gpus()
+
+    def set_config(self, key: str | None, cfg_yaml: str | dict | None) -> None:
+        with self._lock:
+            self.config_key = key
+            self.config = yaml.safe_load(cfg_yaml) if isinstance(cfg_yaml, str) else cfg_yaml
+            if self.config and self.config.get("cuPolicy"):
+                self.cu_policy = self.config["cuPolicy"]
+        self.refresh()
+
+    def refresh(self) -> None:
+        """Recompute the advertised devices (after a mode switch or config change)."""
+        with self._lock:
+            devs: dict[str, Device] = {}
+            gpus = self._gpus()
+            if self.mode == C.PARTITIONING_CUMASK:
+                table = {g["index"]: g for g in (self.config or {}).get("gpus", [])}
+                for gi in gpus:
+                    for s in table.get(gi.index, {}).get("slices", []):
+                        prof = s["profile"]
+                        for r in range(int(s.get("replicas", 0))):
+                            did = f"{gi.uuid}::{prof}::{r}"
+                            devs[did] = Device(did, C.AMD_SLICE_RESOURCE_PREFIX + prof, gi.index, profile=prof,
+                                               memory_gb=int(s.get("memoryGB", prof[:-2])))
+            elif self.mode == C.PARTITIONING_AMDPART:
+                for gi in gpus:
+                    nparts = PARTITIONS_PER_MODE.get(gi.compute_mode, 1)
+                    xcds = max(1, (gi.num_xcds or MI355X_XCDS) // nparts)
+                    gb = gi.memory_gb // nparts
+                    prof = f"{xcds}xcd.{gb}gb"
+                    res = C.RESOURCE_AMD_GPU if self.expose_partitions_as_gpu else C.AMD_PARTITION_RESOURCE_PREFIX + prof
+                    for k in range(nparts):
+                        did = f"{gi.uuid}::p{k}"
+                        devs[did] = Device(did, res, gi.index, partition=k, profile=prof, memory_gb=gb)
+            else:
+                for gi in gpus:
+                    devs[gi.uuid] = Device(gi.uuid, C.RESOURCE_AMD_GPU, gi.index, profile="", memory_gb=gi.memory_gb)
+            # devices that disappeared but are still allocated stay (unhealthy) until released
+            for did, owner in self.allocated.items():
+                if did not in devs and did in self.devices:
+                    d = self.devices[did]
+                    devs[did] = Device(d.id, d.resource, d.gpu_index, False, d.partition, d.profile, d.memory_gb)
+            self.devices = devs
+            self._layout_cu_slots()
+            self.generation += 1
+        for cb in list(self.listeners):
+            try:
+                cb(self)
+            except Exception:
+                log.exception("device plugin listener failed")
+
+    def _layout_cu_slots(self) -> None:
+        """Give every slice replica an XCD-symmetric CU slot; allocated
+        replicas keep theirs, new ones share the remaining slots evenly."""
+        slots: dict[str, CUSlice] = {}
+        by_gpu: dict[int, list[Device]] = {}
+        for d in self.devices.values():
+            if d.resource.startswith(C.AMD_SLICE_RESOURCE_PREFIX):
+                by_gpu.setdefault(d.gpu_index, []).append(d)
+        for gi, devs in by_gpu.items():
+            cus_per_xcd = MI355X_CUS_PER_XCD
+            keep = {d.id: self.cu_slots[d.id] for d in devs if d.id in self.allocated and d.id in self.cu_slots}
+            taken = set()
+            for s in keep.values():
+                taken.update(range(s.start, s.start + s.per_xcd))
+            free_slots = [i for i in range(cus_per_xcd) if i not in taken]
+            new = sorted((d for d in devs if d.id not in keep), key=lambda d: d.id)
+            slots.update(keep)
+            if not new:
+                continue
+            if self.cu_policy == "shared" or not free_slots:
+                for d in new:
+                    slots[d.id] = CUSlice(0, cus_per_xcd)
+                continue
+            if self.cu_policy == "proportional":
+                gpu_mem = max(1, sum(x.memory_gb for x in devs))
+                want = [max(1, cus_per_xcd * d.memory_gb // max(gpu_mem, 1)) for d in new]
+            else:
+                want = [max(1, len(free_slots) // len(new))] * len(new)
+                for i in range(len(free_slots) - sum(want)):
+                    if i < len(want):
+                        want[i] += 1
+            pos = 0
+            for d, w in zip(new, want):
+                if pos + w > len(free_slots):  # out of free CUs: overlap round-robin
+                    pos = 0
+                run = free_slots[pos:pos + w]
+                # contiguous runs are not required: build from the first slot of the run
+                slots[d.id] = CUSlice(run[0], len(run)) if run == list(range(run[0], run[0] + len(run))) \
+                    else CUSlice(run[0], 1)
+                pos += w
+        self.cu_slots = slots
+
+    # ------------------------------------------------------------ device-plugin API
+    def resources(self) -> dict[str, list[Device]]:
+        with self._lock:
+            out: dict[str, list[Device]] = {}
+            for d in self.devices.values():
+                out.setdefault(d.resource, []).append(d)
+            return out
+
+    def list_devices(self, resource: str) -> list[Device]:
+        return self.resources().get(resource, [])
+
+    def allocate(self, resource: str, device_ids: list[str], owner: str = "") -> ContainerAllocation:
+        with self._lock:
+            alloc = ContainerAllocation(device_ids=list(device_ids))
+            gpus = {g.index: g for g in self._gpus()}
+            visible: list[str] = []
+            mask_cus: set[int] = set()
+            mem = 0
+            for did in device_ids:
+                d = self.devices.get(did)
+                if d is None or d.resource != resource:
+                    raise KeyError(f"unknown device {did} for {resource}")
+                if not d.healthy:
+                    raise RuntimeError(f"device {did} is unhealthy")
+                gi = gpus.get(d.gpu_index)
+                hip = str(gi.hip_id if gi and gi.hip_id >= 0 else d.gpu_index)
+                if resource.startswith(C.AMD_PARTITION_RESOURCE_PREFIX) or \
+                        (self.mode == C.PARTITIONING_AMDPART and resource == C.RESOURCE_AMD_GPU):
+                    # logical devices are enumerated GPU-major by the driver
+                    nparts = PARTITIONS_PER_MODE.get(gi.compute_mode, 1) if gi else 1
+                    hip = str(int(hip) * nparts + d.partition)
+                if hip not in visible:
+                    visible.append(hip)
+                if resource.startswith(C.AMD_SLICE_RESOURCE_PREFIX):
+                    s = self.cu_slots.get(did)
+                    if s is not None:
+                        mask_cus.update(s.cus())
+                mem += d.memory_gb
+                self.allocated[did] = owner or "unknown"
+                render = (gi.drm_render if gi and gi.drm_render >= 0 else 128 + d.gpu_index)
+                dev = f"/dev/dri/renderD{render}"
+                if dev not in alloc.devices:
+                    alloc.devices.append(dev)
+            alloc.devices.insert(0, "/dev/kfd")
+            alloc.envs[C.ENV_VISIBLE_DEVICES] = ",".join(visible)
+            if mask_cus:
+                n_cus = MI355X_XCDS * MI355X_CUS_PER_XCD
+                alloc.envs[C.ENV_CU_MASK] = mask_hex(sorted(mask_cus), n_cus)
+            if mem:
+                alloc.envs[C.ENV_MEMORY_LIMIT_GB] = str(mem)
+            return alloc
+
+    def release(self, device_ids: list[str]) -> None:
+        with self._lock:
+            for did in device_ids:
+                self.allocated.pop(did, None)
+            stale = [did for did in device_ids if did in self.devices and not self.devices[did].healthy]
+            for did in stale:
+                self.devices.pop(did, None)
+
+    def cu_slice_of(self, device_id: str) -> CUSlice | None:
+        return self.cu_slots.get(device_id)
+
+    def cus_of(self, device_id: str) -> list[int]:
+        s = self.cu_slots.get(device_id)
+        return s.cus() if s else []
+
+
+__all__ = ["NosAmdDevicePlugin", "Device", "ContainerAllocation", "logical_cu"]

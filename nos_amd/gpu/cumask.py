@@ -1,0 +1,287 @@
+"""CU-mask slice model -- the MPS analogue (``pkg/gpu/slicing``).
+
+A slice is a memory share of one GPU (``<gb>gb`` profile, resource
+``amd.com/gpu-<gb>gb``) plus a set of compute units enforced with a
+per-container CU mask (``ROC_GLOBAL_CU_MASK``; see :mod:`nos_amd.gpu.topology`
+for why masks are XCD-symmetric).  The memory side follows the reference
+exactly (``slicing/gpu.go:67-220``): the sum of the slices' memory must fit the
+GPU, slices are created from spare memory smallest-first, free slices may be
+dropped to make room and re-created afterwards, used slices are never touched.
+The compute side adds one constraint the reference did not have: every
+slice needs at least one CU on every XCD, so a GPU holds at most
+``cus_per_xcd`` (32 on MI355X) slices.
+"""
+from __future__ import annotations
+
+import re
+from dataclasses import dataclass, field
+
+from ..api import constants as C
+from ..kube import objects as ko
+from ..kube import quantity as q
+from .core import GenericError, Geometry, get_count, get_memory_gb, get_model, parse_node_annotations
+from .topology import MI355X_CUS_PER_XCD, MI355X_XCDS
+
+MIN_SLICE_MEMORY_GB = 1
+REPLICA_SEPARATOR = "::"  # device ids of slices: <gpu-uuid>::<replica>
+_PROFILE_RE = re.compile(C.REGEX_AMD_SLICE_PROFILE)
+_RESOURCE_RE = re.compile(C.REGEX_AMD_SLICE_RESOURCE)
+
+
+@dataclass(frozen=True, order=True)
+class SliceProfile:
+    name: str
+
+    def __post_init__(self):
+        if not _PROFILE_RE.match(self.name):
+            raise ValueError(f"invalid slice profile {self.name!r} (expected <gb>gb)")
+
+    @classmethod
+    def of(cls, gb: int) -> "SliceProfile":
+        return cls(f"{gb}gb")
+
+    @property
+    def memory_gb(self) -> int:
+        return int(self.name[:-2])
+
+    def smaller_than(self, other) -> bool:
+        return isinstance(other, SliceProfile) and self.memory_gb < other.memory_gb
+
+    def resource_name(self) -> str:
+        return C.AMD_SLICE_RESOURCE_PREFIX + self.name
+
+    def __str__(self) -> str:
+        return self.name
+
+
+def is_slice_resource(name: str) -> bool:
+    return bool(_RESOURCE_RE.match(name))
+
+
+def profile_of_resource(name: str) -> SliceProfile:
+    m = _RESOURCE_RE.match(name)
+    if not m:
+        raise ValueError(f"{name!r} is not a CU-mask slice resource")
+    return SliceProfile(m.group(1))
+
+
+def requested_profiles(pod: dict) -> dict[SliceProfile, int]:
+    from ..resource.resource import compute_pod_request
+
+    out: dict[SliceProfile, int] = {}
+    for name, v in compute_pod_request(pod).items():
+        if is_slice_resource(name) and q.value(v) > 0:
+            p = profile_of_resource(name)
+            out[p] = out.get(p, 0) + q.value(v)
+    return out
+
+
+@dataclass
+class SliceGPU:
+    model: str
+    index: int
+    memory_gb: int
+    used: dict[SliceProfile, int] = field(default_factory=dict)
+    free: dict[SliceProfile, int] = field(default_factory=dict)
+    max_slices: int = MI355X_CUS_PER_XCD
+
+    def validate(self) -> None:
+        total = 0
+        for d in (self.used, self.free):
+            for p, n in d.items():
+                if p.memory_gb < MIN_SLICE_MEMORY_GB:
+                    raise GenericError(f"min allowed slice size is {MIN_SLICE_MEMORY_GB}GB, but profile {p} "
+                                       f"has {p.memory_gb}GB")
+                total += p.memory_gb * n
+        if total > self.memory_gb:
+            raise GenericError(f"total memory of profiles ({total}) exceeds GPU memory ({self.memory_gb})")
+        if self.num_slices() > self.max_slices:
+            raise GenericError(f"{self.num_slices()} slices exceed the {self.max_slices} XCD-symmetric CU masks")
+
+    @classmethod
+    def new(cls, model: str, index: int, memory_gb: int, used=None, free=None,
+            max_slices: int = MI355X_CUS_PER_XCD) -> "SliceGPU":
+        g = cls(model, index, memory_gb, dict(used or {}), dict(free or {}), max_slices)
+        g.validate()
+        return g
+
+    def clone(self) -> "SliceGPU":
+        return SliceGPU(self.model, self.index, self.memory_gb, dict(self.used), dict(self.free), self.max_slices)
+
+    def geometry(self) -> Geometry:
+        g = Geometry()
+        for d in (self.used, self.free):
+            for p, n in d.items():
+                if n:
+                    g[p] = g.get(p, 0) + n
+        return g
+
+    def num_slices(self) -> int:
+        return sum(self.used.values()) + sum(self.free.values())
+
+    def tot_slices_memory(self) -> int:
+        return sum(p.memory_gb * n for d in (self.used, self.free) for p, n in d.items())
+
+    def can_create_more_slices(self) -> bool:
+        return (self.memory_gb - self.tot_slices_memory() >= MIN_SLICE_MEMORY_GB
+                and self.num_slices() < self.max_slices)
+
+    def create_slices(self, size_gb: int, num: int = 1) -> None:
+        if self.memory_gb - self.tot_slices_memory() < size_gb * num:
+            raise GenericError(f"not enough spare memory to create {num} slices of size {size_gb}GB")
+        if self.num_slices() + num > self.max_slices:
+            raise GenericError(f"cannot create {num} more slices: at most {self.max_slices} per GPU")
+        p = SliceProfile.of(size_gb)
+        self.free[p] = self.free.get(p, 0) + num
+
+    def has_free_capacity(self) -> bool:
+        return any(n > 0 for n in self.free.values()) or self.can_create_more_slices()
+
+    def add_pod(self, pod: dict) -> None:
+        req = requested_profiles(pod)
+        for p, n in req.items():
+            if self.free.get(p, 0) < n:
+                raise GenericError(f"not enough free slices (pod requests {n} {p}, but GPU only has "
+                                   f"{self.free.get(p, 0)})")
+        for p, n in req.items():
+            self.free[p] -= n
+            if self.free[p] == 0:
+                del self.free[p]
+            self.used[p] = self.used.get(p, 0) + n
+
+    def missing_slices(self, required: dict) -> dict[SliceProfile, int]:
+        out = {}
+        for p, n in required.items():
+            if isinstance(p, SliceProfile):
+                diff = n - self.free.get(p, 0)
+                if diff > 0:
+                    out[p] = diff
+        return out
+
+    def update_geometry_for(self, required: dict) -> bool:
+        missing = self.missing_slices(required)
+        if not missing:
+            return False
+        updated = False
+        original_free = dict(self.free)
+        for p in sorted(missing, key=lambda x: x.memory_gb):
+            # 1. create missing slices from spare memory
+            if self.can_create_more_slices():
+                for _ in range(missing[p]):
+                    try:
+                        self.create_slices(p.memory_gb)
+                    except GenericError:
+                        break
+                    missing[p] -= 1
+                    updated = True
+            # 2. drop the original free slices to make room, create the rest
+            qty = missing[p]
+            for k in original_free:
+                self.free.pop(k, None)
+            for _ in range(qty):
+                if not self.can_create_more_slices():
+                    break
+                try:
+                    self.create_slices(p.memory_gb)
+                except GenericError:
+                    break
+                missing[p] -= 1
+                updated = True
+            # 3. re-create the original free slices as far as they still fit
+            for k, v in original_free.items():
+                try:
+                    self.create_slices(k.memory_gb, v)
+                except GenericError:
+                    pass
+        return updated
+
+
+class SliceNode:
+    """``slicing.Node`` analogue; implements core.PartitionableNode."""
+
+    def __init__(self, name: str, gpus: list[SliceGPU], node_info):
+        self.name = name
+        self.gpus = gpus
+        self.node_info = node_info
+
+    @classmethod
+    def from_node_info(cls, ni) -> "SliceNode":
+        node = ni.node()
+        if node is None:
+            raise GenericError("node is nil")
+        model = get_model(node)
+        count = get_count(node)
+        mem = get_memory_gb(node)
+        cus = int(ko.labels(node).get(C.LABEL_AMD_CUS, MI355X_XCDS * MI355X_CUS_PER_XCD))
+        xcds = int(ko.labels(node).get(C.LABEL_AMD_XCDS, MI355X_XCDS))
+        max_slices = max(1, cus // max(1, xcds))
+        status, _ = parse_node_annotations(node)
+        by_gpu: dict[int, tuple[dict, dict]] = {}
+        for a in status:
+            try:
+                p = SliceProfile(a.profile)
+            except ValueError:
+                continue
+            used, free = by_gpu.setdefault(a.index, ({}, {}))
+            (used if a.is_used() else free)[p] = a.quantity
+        gpus = [SliceGPU.new(model, i, mem, *by_gpu[i], max_slices=max_slices) for i in sorted(by_gpu)]
+        have = {g.index for g in gpus}
+        for i in range(count):
+            if i not in have:
+                gpus.append(SliceGPU(model, i, mem, max_slices=max_slices))
+        gpus.sort(key=lambda g: g.index)
+        return cls(ko.name(node), gpus, ni)
+
+    def geometry(self) -> dict:
+        res: dict = {}
+        for g in self.gpus:
+            for p, n in g.geometry().items():
+                res[p] = res.get(p, 0) + n
+        return res
+
+    def has_free_capacity(self) -> bool:
+        return any(g.has_free_capacity() for g in self.gpus)
+
+    def update_geometry_for(self, slices: dict) -> bool:
+        if not self.gpus or not slices:
+            return False
+        required = dict(slices)
+        updated = False
+        for g in self.gpus:
+            updated = g.update_geometry_for(required) or updated
+            for p, n in g.free.items():
+                if p in required:
+                    required[p] -= n
+                    if required[p] <= 0:
+                        del required[p]
+        self._recompute_allocatable()
+        return updated
+
+    def _recompute_allocatable(self) -> None:
+        sc = {k: v for k, v in self.node_info.allocatable.scalar.items() if not is_slice_resource(k)}
+        for p, n in self.geometry().items():
+            sc[p.resource_name()] = n
+        self.node_info.allocatable.scalar = sc
+
+    def add_pod(self, pod: dict) -> None:
+        for g in self.gpus:
+            try:
+                g.add_pod(pod)
+            except GenericError:
+                continue
+            self.node_info.add_pod(pod)
+            return
+        raise GenericError("not enough free slices")
+
+    def clone(self) -> "SliceNode":
+        return SliceNode(self.name, [g.clone() for g in self.gpus], self.node_info.clone())
+
+
+class SliceCalculator:
+    def get_requested_slices(self, pod: dict) -> dict:
+        return dict(requested_profiles(pod))
+
+
+class SliceFilter:
+    def extract_slices(self, resources: dict[str, int]) -> dict:
+        return {profile_of_resource(k): int(v) for k, v in resources.items() if is_slice_resource(k)}

@@ -1,0 +1,306 @@
+"""Partitioning core: snapshot / tracker / sorter / planner / actuator.
+
+Same algorithm as the reference's ``internal/partitioning/core``:
+
+* :class:`ClusterSnapshot` with single-level ``fork`` / ``commit`` /
+  ``revert`` (deep clone of the partitionable nodes), candidate nodes (free
+  capacity, by name), lacking slices of a pod (pod request minus cluster-wide
+  free, filtered to GPU slices) -- ``snapshot.go:29-190``.  Fixed gotcha: the
+  planner fetches each candidate node from the fork *after* forking, so
+  ``revert`` really undoes a geometry change (the reference mutated pre-fork
+  node objects);
+* :class:`SliceTracker` (``tracker.go:26-88``);
+* pod sorter: priority desc, then smaller requested slice first
+  (``util.go:34-71``);
+* :class:`Planner` (``planner.go:67-207``): greedy node-by-node, per node
+  update the geometry for the lacking slices, then try every pod through the
+  scheduler framework's PreFilter + Filter; commit if any pod was added;
+* :class:`Actuator` (``actuator.go:27-66``): no-op when the desired state
+  equals the current one or is empty, else ``Partitioner.apply_partitioning``
+  per node with a new plan id.
+"""
+from __future__ import annotations
+
+import logging
+import time
+from dataclasses import dataclass, field
+from typing import Protocol
+
+from ..kube import objects as ko
+from ..resource.resource import Resource, compute_pod_request
+from ..scheduler.framework import CycleState, Framework, NodeInfo
+from .state import NodePartitioning, PartitioningState
+
+log = logging.getLogger("nos_amd.partitioning")
+
+
+class PartitionableNode(Protocol):
+    name: str
+    node_info: NodeInfo
+
+    def geometry(self) -> dict: ...
+
+    def has_free_capacity(self) -> bool: ...
+
+    def update_geometry_for(self, slices: dict) -> bool: ...
+
+    def add_pod(self, pod: dict) -> None: ...
+
+    def clone(self) -> "PartitionableNode": ...
+
+
+class PartitionCalculator(Protocol):
+    def get_partitioning(self, node: PartitionableNode) -> NodePartitioning: ...
+
+
+class Partitioner(Protocol):
+    def apply_partitioning(self, node: dict, plan_id: str, partitioning: NodePartitioning) -> None: ...
+
+
+class SnapshotTaker(Protocol):
+    def take_snapshot(self, cluster_state) -> "ClusterSnapshot": ...
+
+
+class NodeInitializer(Protocol):
+    def init_node_partitioning(self, node: dict) -> None: ...
+
+
+def new_plan_id(clock=None) -> str:
+    t = clock.now() if clock is not None else time.time()
+    return str(int(t * 1000))
+
+
+@dataclass
+class PartitioningPlan:
+    desired_state: PartitioningState
+    id: str = ""
+
+    def __post_init__(self):
+        if not self.id:
+            self.id = new_plan_id()
+
+
+class ClusterSnapshot:
+    def __init__(self, nodes: dict[str, PartitionableNode], partition_calculator: PartitionCalculator,
+                 slice_calculator, slice_filter):
+        self._data: dict[str, PartitionableNode] = dict(nodes)
+        self._forked: dict[str, PartitionableNode] | None = None
+        self.partition_calculator = partition_calculator
+        self.slice_calculator = slice_calculator
+        self.slice_filter = slice_filter
+
+    def _d(self) -> dict[str, PartitionableNode]:
+        return self._forked if self._forked is not None else self._data
+
+    def fork(self) -> None:
+        if self._forked is not None:
+            raise RuntimeError("snapshot already forked")
+        self._forked = {k: v.clone() for k, v in self._data.items()}
+
+    def commit(self) -> None:
+        if self._forked is not None:
+            self._data = self._forked
+            self._forked = None
+
+    def revert(self) -> None:
+        self._forked = None
+
+    def clone(self) -> "ClusterSnapshot":
+        c = ClusterSnapshot({k: v.clone() for k, v in self._data.items()}, self.partition_calculator,
+                            self.slice_calculator, self.slice_filter)
+        if self._forked is not None:
+            c._forked = {k: v.clone() for k, v in self._forked.items()}
+        return c
+
+    def get_nodes(self) -> dict[str, PartitionableNode]:
+        return self._d()
+
+    def get_node(self, name: str) -> PartitionableNode | None:
+        return self._d().get(name)
+
+    def set_node(self, n: PartitionableNode) -> None:
+        self._d()[n.name] = n
+
+    def get_candidate_nodes(self) -> list[str]:
+        return sorted(n.name for n in self._d().values() if n.has_free_capacity())
+
+    def get_partitioning_state(self) -> PartitioningState:
+        return PartitioningState({name: self.partition_calculator.get_partitioning(n)
+                                  for name, n in self.get_nodes().items()})
+
+    def lacking_resources(self, pod: dict) -> Resource:
+        req = Resource.from_list(compute_pod_request(pod))
+        alloc, requested = Resource(), Resource()
+        for n in self.get_nodes().values():
+            alloc.iadd(n.node_info.allocatable)
+            requested.iadd(n.node_info.requested)
+        available = alloc.subtract_non_negative(requested)
+        diff = available - req
+        res = Resource(min(diff.milli_cpu, 0), min(diff.memory, 0), min(diff.ephemeral_storage, 0),
+                       min(diff.allowed_pod_number, 0))
+        res.scalar = {k: v for k, v in diff.scalar.items() if v < 0}
+        return res.abs()
+
+    def get_lacking_slices(self, pod: dict) -> dict:
+        return self.slice_filter.extract_slices(self.lacking_resources(pod).scalar)
+
+    def add_pod(self, node_name: str, pod: dict) -> None:
+        n = self._d().get(node_name)
+        if n is None:
+            raise KeyError(f"could not find node {node_name} in cluster snapshot")
+        n.add_pod(pod)
+
+
+class SliceTracker:
+    def __init__(self, snapshot: ClusterSnapshot, calculator, pods: list[dict]):
+        self.calculator = calculator
+        self.requested: dict = {}
+        self.lacking: dict = {}
+        self.lookup: dict[str, dict] = {}
+        for pod in pods:
+            k = ko.key(pod)
+            per = self.lookup.setdefault(k, {})
+            for s, n in snapshot.get_lacking_slices(pod).items():
+                self.lacking[s] = self.lacking.get(s, 0) + n
+                per[s] = per.get(s, 0) + n
+            for s, n in calculator.get_requested_slices(pod).items():
+                self.requested[s] = self.requested.get(s, 0) + n
+
+    def get_lacking_slices(self) -> dict:
+        return self.lacking
+
+    def get_requested_slices(self) -> dict:
+        return self.requested
+
+    def remove(self, pod: dict) -> None:
+        for s, n in self.calculator.get_requested_slices(pod).items():
+            self.requested[s] = self.requested.get(s, 0) - n
+            if self.requested[s] <= 0:
+                del self.requested[s]
+        per = self.lookup.get(ko.key(pod))
+        if per:
+            for s, n in list(per.items()):
+                self.lacking[s] = self.lacking.get(s, 0) - n
+                per[s] -= n
+                if per[s] <= 0:
+                    del per[s]
+                if self.lacking[s] <= 0:
+                    del self.lacking[s]
+
+
+def sort_pods(pods: list[dict], slice_calculator) -> list[dict]:
+    """Priority desc; equal priority: the pod requesting the smaller slice first."""
+    import functools
+
+    def cmp(a, b):
+        pa, pb = ko.pod_priority(a), ko.pod_priority(b)
+        if pa != pb:
+            return -1 if pa > pb else 1
+        ra, rb = slice_calculator.get_requested_slices(a), slice_calculator.get_requested_slices(b)
+        if not ra or not rb:
+            return 0
+        sa, sb = min(ra, key=str), min(rb, key=str)
+        if sa.smaller_than(sb):
+            return -1
+        if sb.smaller_than(sa):
+            return 1
+        return 0
+
+    return sorted(pods, key=functools.cmp_to_key(cmp))
+
+
+def is_node_initialized(node: dict) -> bool:
+    from ..gpu.core import get_count, parse_node_annotations
+
+    try:
+        count = get_count(node)
+    except Exception:
+        return False
+    _, spec = parse_node_annotations(node)
+    return count == len({a.index for a in spec})
+
+
+class Planner:
+    def __init__(self, partition_calculator: PartitionCalculator, slice_calculator, framework: Framework):
+        self.partition_calculator = partition_calculator
+        self.slice_calculator = slice_calculator
+        self.framework = framework
+        self.last_stats: dict = {}
+
+    def plan(self, snapshot: ClusterSnapshot, candidate_pods: list[dict]) -> PartitioningPlan:
+        t0 = time.perf_counter()
+        state = snapshot.get_partitioning_state()
+        tracker = SliceTracker(snapshot, self.slice_calculator, candidate_pods)
+        placed = 0
+        if not tracker.get_lacking_slices():
+            self.last_stats = {"placed": 0, "seconds": time.perf_counter() - t0, "lacking": 0}
+            return PartitioningPlan(state)
+        pods = sort_pods(candidate_pods, self.slice_calculator)
+        for name in snapshot.get_candidate_nodes():
+            if not tracker.get_lacking_slices():
+                break
+            snapshot.fork()
+            n = snapshot.get_node(name)  # the forked copy (fixes the pre-fork mutation gotcha)
+            if n.update_geometry_for(dict(tracker.get_lacking_slices())):
+                snapshot.set_node(n)
+            added = 0
+            remaining = []
+            for pod in pods:
+                if self._try_add_pod(pod, name, snapshot):
+                    state[name] = self.partition_calculator.get_partitioning(snapshot.get_node(name))
+                    tracker.remove(pod)
+                    added += 1
+                else:
+                    remaining.append(pod)
+            if added:
+                snapshot.commit()
+                pods = remaining
+                placed += added
+            else:
+                snapshot.revert()
+        self.last_stats = {"placed": placed, "seconds": time.perf_counter() - t0,
+                           "lacking": sum(tracker.get_lacking_slices().values())}
+        return PartitioningPlan(state)
+
+    def _try_add_pod(self, pod: dict, node_name: str, snapshot: ClusterSnapshot) -> bool:
+        if snapshot.get_lacking_slices(pod):
+            return False
+        n = snapshot.get_node(node_name)
+        if n is None:
+            return False
+        if not self.can_schedule_pod(pod, n.node_info):
+            return False
+        try:
+            snapshot.add_pod(node_name, pod)
+        except Exception:
+            return False
+        return True
+
+    def can_schedule_pod(self, pod: dict, node_info: NodeInfo) -> bool:
+        state = CycleState()
+        _, s = self.framework.run_pre_filter_plugins(state, pod)
+        if not s.is_success():
+            return False
+        return self.framework.run_filter_plugins(state, pod, node_info).is_success()
+
+
+class Actuator:
+    def __init__(self, api, partitioner: Partitioner):
+        self.api = api
+        self.partitioner = partitioner
+
+    def apply(self, snapshot: ClusterSnapshot, plan: PartitioningPlan) -> bool:
+        if snapshot.get_partitioning_state().equal(plan.desired_state):
+            log.info("current and desired partitioning states are equal, nothing to do")
+            return False
+        if plan.desired_state.is_empty():
+            log.info("desired partitioning state is empty, nothing to do")
+            return False
+        for node_name, np_ in plan.desired_state.items():
+            node = self.api.get("Node", node_name)
+            self.partitioner.apply_partitioning(node, plan.id, np_)
+        return True
+
+
+__all__ = ["ClusterSnapshot", "SliceTracker", "Planner", "Actuator", "PartitioningPlan", "sort_pods",
+           "is_node_initialized", "new_plan_id", "field"]

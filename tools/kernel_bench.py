@@ -1,0 +1,89 @@
+"""Per-kernel timing at the YOLOS-small shapes (one process, interleaved rounds).
+
+python tools/kernel_bench.py [--only attn,gemm] [--iters 50]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+import torch  # noqa: E402
+
+from nos_amd import ops  # noqa: E402
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="attn,gemm,torch")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    torch.manual_seed(0)
+    S, H, hid, mlp = 3401, 6, 384, 1536
+    B = a.batch
+    res = {}
+    if "attn" in a.only:
+        qkv = torch.randn(B, S, 3 * hid, device="cuda", dtype=torch.bfloat16)
+        out = torch.empty(B, S, hid, device="cuda", dtype=torch.bfloat16)
+        us = timeit(lambda: ops.attention_qkv(qkv, H, out=out), a.iters)
+        fl = B * 4 * S * S * hid
+        res["attn_us"] = us
+        res["attn_tflops"] = fl / us / 1e6
+    if "torch" in a.only:
+        qkv = torch.randn(B, S, 3, H, 64, device="cuda", dtype=torch.bfloat16)
+        q, k, v = (t.transpose(1, 2).contiguous() for t in qkv.unbind(2))
+        us = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v), a.iters)
+        res["sdpa_us"] = us
+        res["sdpa_tflops"] = B * 4 * S * S * hid / us / 1e6
+    if "gemm" in a.only:
+        M = B * S
+        x = torch.randn(M, hid, device="cuda", dtype=torch.bfloat16)
+        for name, (N, K, act, ln, resid) in {
+            "qkv_ln": (3 * hid, hid, None, True, False),
+            "fc1_ln_gelu": (mlp, hid, "gelu", True, False),
+            "proj_resid": (hid, hid, None, False, True),
+            "fc2_resid": (hid, mlp, None, False, True),
+            "qkv_plain": (3 * hid, hid, None, False, False),
+        }.items():
+            xa = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+            w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+            b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
+            r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+            outg = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            if ln:
+                g = torch.randn(K, device="cuda", dtype=torch.bfloat16)
+                be = torch.randn(K, device="cuda", dtype=torch.bfloat16)
+                wg, c1, c2 = ops.fold_layernorm(w, b, g, be)
+                fn = lambda: ops.linear_ln(xa, wg, c1, c2, act=act, out=outg)  # noqa: E731
+            else:
+                fn = lambda: ops.linear(xa, w, b, act=act, residual=r if resid else None, out=outg)  # noqa: E731
+            us = timeit(fn, a.iters)
+            res[f"{name}_us"] = us
+            res[f"{name}_tflops"] = 2 * M * N * K / us / 1e6
+            tus = timeit(lambda: torch.nn.functional.linear(xa, w, b), a.iters)
+            res[f"{name}_torch_us"] = tus
+    print(json.dumps(res), flush=True)
+    if a.out:
+        Path(a.out).write_text(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
