@@ -1,0 +1,239 @@
+"""Partition agent: realises ``amdpart`` plans on one node (the reference's
+``migagent``, ``internal/controllers/migagent``).
+
+AMD compute partitions are a per-GPU MODE (SPX/DPX/QPX/CPX x NPS1/NPS2),
+not a set of independently created instances like MIG, so the diff planner
+is much simpler than ``migagent/plan/plan.go``: per GPU, either the current
+mode already yields the spec'd partitions, or the GPU must switch mode -- and
+it may switch only when none of its partitions is in use (kubelet
+PodResources) and amd-smi lists no process on it (the drain check of
+SURVEY.md 5.3).  After a switch the device plugin re-enumerates (the
+reference deletes the device-plugin pod and waits for it, ``pkg/gpu/client.go:51-135``;
+our plugin is reconfigured in place) and the reporter publishes the new
+status.
+
+* :class:`PartitionReporter` -- ``reporter.go:54-109``: status annotations
+  ``status-gpu-<i>-<profile>-<free|used>`` + ``status-mode-gpu-<i>`` +
+  ``status-partitioning-plan`` (the last plan id the actuator parsed);
+* :class:`PartitionActuator` -- ``actuator.go:71-201``: waits for a report
+  since its last apply, parses spec vs status, plans, applies.
+"""
+from __future__ import annotations
+
+import logging
+import time
+from dataclasses import dataclass, field
+
+from ..api import constants as C
+from ..gpu import amdpart as ap
+from ..gpu.amdsmi import PARTITIONS_PER_MODE
+from ..gpu.core import (devices_as_status_annotations, parse_node_annotations, spec_matches_status,
+                        status_equal)
+from ..kube import objects as ko
+from ..observability import metrics, tracing
+from ..runtime.manager import Controller, Request, Result
+from ..runtime.predicates import AnnotationsChanged, ExcludeDelete, MatchingName, NodeResourcesChanged, or_
+from .devices import NodeDeviceClient
+from .shared import SharedState
+
+log = logging.getLogger("nos_amd.agents.partagent")
+
+MODE_BY_PARTS = {v: k for k, v in PARTITIONS_PER_MODE.items()}
+
+
+def partition_profile_name(resource: str) -> str:
+    return ap.profile_of_resource(resource).name
+
+
+# ====================================================================== plan
+@dataclass(frozen=True)
+class ModeChange:
+    gpu_index: int
+    compute: str
+    memory: str
+    from_compute: str
+    from_memory: str
+
+
+@dataclass
+class PartitionPlan:
+    changes: list[ModeChange] = field(default_factory=list)
+    blocked: dict[int, str] = field(default_factory=dict)   # gpu -> reason
+
+    def is_empty(self) -> bool:
+        return not self.changes
+
+    def __eq__(self, other) -> bool:
+        return isinstance(other, PartitionPlan) and self.changes == other.changes
+
+
+def desired_modes(node: dict, gpus, memory_preference: str = "NPS1") -> dict[int, tuple[str, str]]:
+    """Per GPU, the (compute, memory) mode the spec annotations ask for.
+    ``spec-mode-gpu-<i>`` wins; otherwise it is derived from the single spec
+    profile (``<x>xcd.<gb>gb`` -> total_xcds / x partitions)."""
+    ann = ko.annotations(node)
+    _, spec = parse_node_annotations(node)
+    by_gpu: dict[int, list] = {}
+    for s in spec:
+        if s.quantity:
+            by_gpu.setdefault(s.index, []).append(s)
+    info = {g.index: g for g in gpus}
+    out: dict[int, tuple[str, str]] = {}
+    for i, g in info.items():
+        mode = ann.get(C.ANNOTATION_SPEC_MODE_FORMAT.format(index=i))
+        if mode and "/" in mode:
+            c, m = mode.split("/", 1)
+            out[i] = (c, m)
+            continue
+        specs = by_gpu.get(i)
+        if not specs:
+            continue
+        prof = ap.profile(specs[0].profile)
+        parts = max(1, (g.num_xcds or 8) // max(1, prof.xcds))
+        c = MODE_BY_PARTS.get(parts)
+        if c is None:
+            continue
+        out[i] = (c, memory_preference if parts in (2, 8) else "NPS1")
+    return out
+
+
+def new_partition_plan(node: dict, gpus, used_gpus: set[int], busy_gpus: set[int],
+                       memory_preference: str = "NPS1") -> PartitionPlan:
+    plan = PartitionPlan()
+    want = desired_modes(node, gpus, memory_preference)
+    for g in sorted(gpus, key=lambda x: x.index):
+        if g.index not in want:
+            continue
+        c, m = want[g.index]
+        if (g.compute_mode, g.memory_mode) == (c, m):
+            continue
+        if g.index in used_gpus:
+            plan.blocked[g.index] = "partitions in use"
+            continue
+        if g.index in busy_gpus:
+            plan.blocked[g.index] = "processes running"
+            continue
+        plan.changes.append(ModeChange(g.index, c, m, g.compute_mode, g.memory_mode))
+    return plan
+
+
+# ====================================================================== reporter
+class PartitionReporter:
+    def __init__(self, api, node_name: str, smi, lister, shared: SharedState, refresh_s: float = 10.0):
+        self.api, self.node_name, self.smi = api, node_name, smi
+        self.devices = NodeDeviceClient(smi, lister)
+        self.shared = shared
+        self.refresh_s = refresh_s
+        self.reports = 0
+
+    def status_annotations(self):
+        devs = self.devices.get_devices(C.AMD_PARTITION_RESOURCE_PREFIX)
+        return devices_as_status_annotations(devs, partition_profile_name)
+
+    def reconcile(self, req: Request) -> Result:
+        with self.shared.lock:
+            node = self.api.try_get("Node", self.node_name)
+            if node is None:
+                return Result()
+            status = self.status_annotations()
+            cur_status, _ = parse_node_annotations(node)
+            ann = ko.annotations(node)
+            modes = {C.ANNOTATION_STATUS_MODE_FORMAT.format(index=g.index): f"{g.compute_mode}/{g.memory_mode}"
+                     for g in self.smi.gpus()}
+            plan = self.shared.last_parsed_plan_id
+            if (status_equal(status, cur_status) and ann.get(C.ANNOTATION_REPORTED_PARTITIONING_PLAN, "") == plan
+                    and all(ann.get(k) == v for k, v in modes.items())):
+                self.shared.on_report_done()
+                return Result(requeue_after=self.refresh_s)
+            patch: dict[str, str | None] = {k: None for k in ann if k.startswith(C.ANNOTATION_GPU_STATUS_PREFIX)}
+            patch.update({s.key(): s.value() for s in status})
+            patch.update(modes)
+            if plan:
+                patch[C.ANNOTATION_REPORTED_PARTITIONING_PLAN] = plan
+            self.api.patch("Node", self.node_name, {"metadata": {"annotations": patch}})
+            self.reports += 1
+            self.shared.on_report_done()
+            return Result(requeue_after=self.refresh_s)
+
+    def controller(self) -> Controller:
+        return Controller(f"partagent-reporter-{self.node_name}", self).for_kind(
+            "Node", ExcludeDelete(), MatchingName(self.node_name), NodeResourcesChanged())
+
+
+# ====================================================================== actuator
+class PartitionActuator:
+    """``MigActuator`` analogue.  ``device_plugins`` are refreshed after a mode
+    switch (the reference restarts the device-plugin pod)."""
+
+    def __init__(self, api, node_name: str, smi, lister, shared: SharedState, device_plugins=(),
+                 memory_preference: str = "NPS1"):
+        self.api, self.node_name, self.smi = api, node_name, smi
+        self.devices = NodeDeviceClient(smi, lister)
+        self.shared = shared
+        self.device_plugins = list(device_plugins)
+        self.memory_preference = memory_preference
+        self.last_applied_plan: PartitionPlan | None = None
+        self.last_applied_status = None
+        self.applies = 0
+
+    def reconcile(self, req: Request) -> Result:
+        if not self.shared.at_least_one_report_since_last_apply():
+            return Result(requeue_after=1.0)
+        with self.shared.lock:
+            node = self.api.try_get("Node", self.node_name)
+            if node is None:
+                return Result()
+            plan_id = ko.annotations(node).get(C.ANNOTATION_PARTITIONING_PLAN, "")
+            if plan_id:
+                self.shared.last_parsed_plan_id = plan_id
+            status, spec = parse_node_annotations(node)
+            if spec_matches_status(spec, status) and not self._mode_mismatch(node):
+                return Result()
+            gpus = self.smi.gpus()
+            used = self.devices.used_gpus(C.AMD_PARTITION_RESOURCE_PREFIX) | self.devices.used_gpus(
+                C.RESOURCE_AMD_GPU)
+            busy = {g.index for g in gpus if self.smi.processes(g.index)}
+            plan = new_partition_plan(node, gpus, used, busy, self.memory_preference)
+            for gi, why in plan.blocked.items():
+                log.info("node %s gpu %d cannot be repartitioned now: %s", self.node_name, gi, why)
+            if plan.is_empty():
+                if plan.blocked:
+                    return Result(requeue_after=10.0)
+                return Result()
+            if self.last_applied_plan == plan and status_equal(self.last_applied_status or [], status):
+                log.info("plan already applied and state unchanged, skipping")
+                return Result()
+            self.apply(plan, plan_id)
+            self.last_applied_plan = plan
+            self.last_applied_status = status
+            self.shared.on_apply_done()
+            return Result(requeue_after=1.0)
+
+    def _mode_mismatch(self, node: dict) -> bool:
+        want = desired_modes(node, self.smi.gpus(), self.memory_preference)
+        return any((g.compute_mode, g.memory_mode) != want[g.index] for g in self.smi.gpus() if g.index in want)
+
+    def apply(self, plan: PartitionPlan, plan_id: str = "") -> None:
+        with tracing.span("partagent.apply", node=self.node_name, plan_id=plan_id, changes=len(plan.changes)):
+            for ch in plan.changes:
+                t0 = time.perf_counter()
+                try:
+                    if ch.memory != ch.from_memory:
+                        self.smi.set_memory_partition(ch.gpu_index, ch.memory)
+                    if ch.compute != ch.from_compute:
+                        self.smi.set_compute_partition(ch.gpu_index, ch.compute)
+                except Exception as e:
+                    log.error("node %s gpu %d: switching to %s/%s failed: %s", self.node_name, ch.gpu_index,
+                              ch.compute, ch.memory, e)
+                    continue
+                metrics.REPARTITION_DURATION.labels(mode=f"{ch.compute}/{ch.memory}").observe(
+                    time.perf_counter() - t0)
+                log.info("node %s gpu %d: %s/%s -> %s/%s", self.node_name, ch.gpu_index, ch.from_compute,
+                         ch.from_memory, ch.compute, ch.memory)
+            self.applies += 1
+            for p in self.device_plugins:
+                p.refresh()
+
+    def controller(self) -> Controller:
+        return Controller(f"partagent-actuator-{self.node_name}", self).for_kind(
+            "Node", ExcludeDelete(), MatchingName(self.node_name), or_(AnnotationsChanged(), NodeResourcesChanged()))

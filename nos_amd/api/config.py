@@ -93,6 +93,10 @@ class GpuPartitionerConfig(ControllerManagerSpec):
     # new: repartition of a GPU-wide mode may take seconds; the plan handshake times out after this
     plan_report_timeout_seconds: float = Field(300.0, alias="planReportTimeoutSeconds")
     amd_gpu_resource_memory_gb: int = Field(C.DEFAULT_AMD_GPU_RESOURCE_MEMORY_GB, alias="amdGpuResourceMemoryGB")
+    # new: CU-mask slice placement over a node's GPUs ("pack" = reference first-fit, "spread")
+    slice_placement: str = Field("pack", alias="slicePlacement")
+    # new: CU-mask layout of a GPU's slices in the device plugin ("even" | "proportional" | "shared")
+    cu_policy: str = Field("even", alias="cuPolicy")
 
     @model_validator(mode="before")
     @classmethod
@@ -108,6 +112,10 @@ class GpuPartitionerConfig(ControllerManagerSpec):
             raise ValueError("batchWindowIdleSeconds must be greater than 0")
         if self.device_plugin_delay_seconds <= 0:
             raise ValueError("devicePluginDelaySeconds must be greater than 0")
+        if self.slice_placement not in ("pack", "spread"):
+            raise ValueError("slicePlacement must be 'pack' or 'spread'")
+        if self.cu_policy not in ("even", "proportional", "shared"):
+            raise ValueError("cuPolicy must be 'even', 'proportional' or 'shared'")
 
     def with_defaults(self) -> "GpuPartitionerConfig":
         """Default the device-plugin ConfigMap name/namespace when missing

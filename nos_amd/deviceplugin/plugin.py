@@ -181,6 +181,31 @@ class NosAmdDevicePlugin:
     def list_devices(self, resource: str) -> list[Device]:
         return self.resources().get(resource, [])
 
+    def preferred_allocation(self, resource: str, available: list[str], must_include: list[str], size: int) -> list[str]:
+        """``GetPreferredAllocation``: "spread" (config ``allocation``) picks
+        devices on the GPUs with the fewest allocated devices, "pack" fills
+        GPUs in index order."""
+        with self._lock:
+            out = list(must_include)[:size]
+            cand = [d for d in available if d not in out and d in self.devices]
+            policy = (self.config or {}).get("allocation", "pack")
+            load: dict[int, int] = {}
+            for did in self.allocated:
+                d = self.devices.get(did)
+                if d is not None:
+                    load[d.gpu_index] = load.get(d.gpu_index, 0) + 1
+            while len(out) < size and cand:
+                if policy == "spread":
+                    best = min(cand, key=lambda x: (load.get(self.devices[x].gpu_index, 0),
+                                                    self.devices[x].gpu_index, x))
+                else:
+                    best = min(cand, key=lambda x: (self.devices[x].gpu_index, x))
+                out.append(best)
+                cand.remove(best)
+                gi = self.devices[best].gpu_index
+                load[gi] = load.get(gi, 0) + 1
+            return out
+
     def allocate(self, resource: str, device_ids: list[str], owner: str = "") -> ContainerAllocation:
         with self._lock:
             alloc = ContainerAllocation(device_ids=list(device_ids))
@@ -198,9 +223,11 @@ class NosAmdDevicePlugin:
                 hip = str(gi.hip_id if gi and gi.hip_id >= 0 else d.gpu_index)
                 if resource.startswith(C.AMD_PARTITION_RESOURCE_PREFIX) or \
                         (self.mode == C.PARTITIONING_AMDPART and resource == C.RESOURCE_AMD_GPU):
-                    # logical devices are enumerated GPU-major by the driver
-                    nparts = PARTITIONS_PER_MODE.get(gi.compute_mode, 1) if gi else 1
-                    hip = str(int(hip) * nparts + d.partition)
+                    # logical devices are enumerated GPU-major by the driver: the
+                    # partitions of GPU g follow all partitions of GPUs before it
+                    base = sum(PARTITIONS_PER_MODE.get(g.compute_mode, 1) for g in gpus.values()
+                               if (g.hip_id if g.hip_id >= 0 else g.index) < int(hip))
+                    hip = str(base + d.partition)
                 if hip not in visible:
                     visible.append(hip)
                 if resource.startswith(C.AMD_SLICE_RESOURCE_PREFIX):

@@ -117,7 +117,8 @@ def mi355x_geometries(memory_gb: int = 288, xcds: int = 8) -> list[ModeGeometry]
     return out
 
 
-_DEFAULT_MODELS = ["AMD Instinct MI355X", "MI355X", "AMD Instinct MI350X", "MI350X"]
+_DEFAULT_MODELS = ["AMD Instinct MI355X", "AMD-Instinct-MI355X", "MI355X",
+                   "AMD Instinct MI350X", "AMD-Instinct-MI350X", "MI350X"]
 _known: dict[str, list[ModeGeometry]] = {m: mi355x_geometries() for m in _DEFAULT_MODELS}
 
 

@@ -199,10 +199,14 @@ class SliceGPU:
 class SliceNode:
     """``slicing.Node`` analogue; implements core.PartitionableNode."""
 
-    def __init__(self, name: str, gpus: list[SliceGPU], node_info):
+    def __init__(self, name: str, gpus: list[SliceGPU], node_info, placement: str = "pack"):
         self.name = name
         self.gpus = gpus
         self.node_info = node_info
+        # "pack": first-fit over GPUs (the reference, keeps whole GPUs free);
+        # "spread": new slices go to the GPU with the most spare memory, so
+        # tenants are balanced over the node's GPUs (throughput-first)
+        self.placement = placement
 
     @classmethod
     def from_node_info(cls, ni) -> "SliceNode":
@@ -246,6 +250,10 @@ class SliceNode:
         if not self.gpus or not slices:
             return False
         required = dict(slices)
+        if self.placement == "spread":
+            updated = self._spread(required)
+            self._recompute_allocatable()
+            return updated
         updated = False
         for g in self.gpus:
             updated = g.update_geometry_for(required) or updated
@@ -257,6 +265,21 @@ class SliceNode:
         self._recompute_allocatable()
         return updated
 
+    def _spread(self, required: dict) -> bool:
+        updated = False
+        for p in sorted((x for x in required if isinstance(x, SliceProfile)), key=lambda x: x.memory_gb):
+            need = required[p] - sum(g.free.get(p, 0) for g in self.gpus)
+            while need > 0:
+                cands = [g for g in self.gpus if g.memory_gb - g.tot_slices_memory() >= p.memory_gb
+                         and g.num_slices() < g.max_slices]
+                if not cands:
+                    break
+                g = max(cands, key=lambda g: (g.memory_gb - g.tot_slices_memory(), -g.num_slices(), -g.index))
+                g.create_slices(p.memory_gb)
+                need -= 1
+                updated = True
+        return updated
+
     def _recompute_allocatable(self) -> None:
         sc = {k: v for k, v in self.node_info.allocatable.scalar.items() if not is_slice_resource(k)}
         for p, n in self.geometry().items():
@@ -264,7 +287,10 @@ class SliceNode:
         self.node_info.allocatable.scalar = sc
 
     def add_pod(self, pod: dict) -> None:
-        for g in self.gpus:
+        order = self.gpus
+        if self.placement == "spread":  # mirror the device plugin's preferred allocation
+            order = sorted(self.gpus, key=lambda g: (sum(g.used.values()), g.index))
+        for g in order:
             try:
                 g.add_pod(pod)
             except GenericError:
@@ -274,7 +300,7 @@ class SliceNode:
         raise GenericError("not enough free slices")
 
     def clone(self) -> "SliceNode":
-        return SliceNode(self.name, [g.clone() for g in self.gpus], self.node_info.clone())
+        return SliceNode(self.name, [g.clone() for g in self.gpus], self.node_info.clone(), self.placement)
 
 
 class SliceCalculator:

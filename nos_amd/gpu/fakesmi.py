@@ -1,0 +1,112 @@
+"""Per-node, pure-Python GPU inventory with the :class:`~nos_amd.gpu.amdsmi.AmdSmi`
+interface, for multi-node simulations.
+
+The native ``libnos_amdsmi`` keeps ONE backend per process (like the real
+amd-smi library), so a simulator with many nodes in one process gives each
+node a :class:`FakeSmi` instead.  Semantics match the C++ fake backend
+(``csrc/amdsmi/nos_amdsmi.cpp``): a compute-partition switch is refused while
+the GPU has processes, the partition count follows the mode, and faults can
+be injected.
+"""
+from __future__ import annotations
+
+import threading
+
+from .amdsmi import PARTITIONS_PER_MODE, AmdSmiError, GpuInfo, ProcInfo
+
+_MEMORY_MODES = ("NPS1", "NPS2", "NPS4", "NPS8")
+
+
+class FakeSmi:
+    backend = "pyfake"
+
+    def __init__(self, gpus: int = 8, compute: str = "SPX", memory: str = "NPS1", cus: int = 256, xcds: int = 8,
+                 vram_mb: int = 294912, model: str = "AMD Instinct MI355X", node: str = "node"):
+        self._lock = threading.RLock()
+        self.node = node
+        self.model = model
+        self.cus, self.xcds, self.vram_mb = cus, xcds, vram_mb
+        self.compute = [compute] * gpus
+        self.memory = [memory] * gpus
+        self.procs: list[dict[int, ProcInfo]] = [dict() for _ in range(gpus)]
+        self.activity_gfx = [0] * gpus
+        self.activity_umc = [0] * gpus
+        self.faults: set[str] = set()
+        self.lost: set[int] = set()
+        self.switches = 0
+
+    # ------------------------------------------------------------ queries
+    def count(self) -> int:
+        return len(self.compute) - len(self.lost)
+
+    def gpu(self, i: int) -> GpuInfo:
+        with self._lock:
+            if i < 0 or i >= len(self.compute) or i in self.lost:
+                raise AmdSmiError(-2, f"gpu({i})")
+            return GpuInfo(index=i, num_cus=self.cus, num_xcds=self.xcds, compute_mode=self.compute[i],
+                           memory_mode=self.memory[i], num_partitions=PARTITIONS_PER_MODE[self.compute[i]],
+                           hip_id=i, drm_render=128 + i, vram_mb=self.vram_mb, bdf=f"0000:{0x11 + i:02x}:00.0",
+                           uuid=f"GPU-{self.node}-{i:04d}", market_name=self.model)
+
+    def gpus(self) -> list[GpuInfo]:
+        return [self.gpu(i) for i in range(len(self.compute)) if i not in self.lost]
+
+    def activity(self, i: int) -> dict[str, int]:
+        return {"gfx": self.activity_gfx[i], "umc": self.activity_umc[i], "mm": 0}
+
+    def processes(self, i: int, max_procs: int = 256) -> list[ProcInfo]:
+        with self._lock:
+            return list(self.procs[i].values())[:max_procs]
+
+    def link(self, i: int, j: int) -> dict:
+        if i == j:
+            return {"type": "internal", "hops": 0, "weight": 0}
+        return {"type": "xgmi", "hops": 1, "weight": 15}
+
+    # ------------------------------------------------------------ setters
+    def set_compute_partition(self, i: int, mode: str) -> None:
+        with self._lock:
+            if "fail_set_compute" in self.faults:
+                raise AmdSmiError(-3, f"set_compute_partition({i}, {mode})")
+            if mode not in PARTITIONS_PER_MODE:
+                raise AmdSmiError(-4, f"unsupported compute mode {mode}")
+            if self.procs[i]:
+                raise AmdSmiError(-5, f"gpu {i} busy")
+            if self.compute[i] != mode:
+                self.compute[i] = mode
+                self.switches += 1
+
+    def set_memory_partition(self, i: int, mode: str) -> None:
+        with self._lock:
+            if "fail_set_memory" in self.faults:
+                raise AmdSmiError(-3, f"set_memory_partition({i}, {mode})")
+            if mode not in _MEMORY_MODES:
+                raise AmdSmiError(-4, f"unsupported memory mode {mode}")
+            if self.procs[i]:
+                raise AmdSmiError(-5, f"gpu {i} busy")
+            self.memory[i] = mode
+
+    # ------------------------------------------------------------ fake controls
+    def inject(self, fault: str) -> None:
+        with self._lock:
+            if fault == "clear":
+                self.faults.clear()
+                self.lost.clear()
+            elif fault.startswith("lose_gpu="):
+                self.lost.add(int(fault.split("=", 1)[1]))
+            else:
+                self.faults.add(fault)
+
+    def fake_add_process(self, i: int, pid: int, vram: int = 1 << 30, cus: int = 0) -> None:
+        with self._lock:
+            self.procs[i][pid] = ProcInfo(pid, cus, vram, f"proc{pid}")
+
+    def fake_remove_process(self, i: int, pid: int) -> None:
+        with self._lock:
+            self.procs[i].pop(pid, None)
+
+    def fake_set_activity(self, i: int, gfx: int, umc: int = 0) -> None:
+        self.activity_gfx[i], self.activity_umc[i] = gfx, umc
+
+    def close(self) -> None:
+        pass

@@ -138,7 +138,8 @@ class DevicePluginConfigRef:
     namespace: str = C.DEFAULT_DEVICE_PLUGIN_CM_NAMESPACE
 
 
-def plugin_config(node_name: str, plan_id: str, partitioning: NodePartitioning, cu_policy: str = "even") -> dict:
+def plugin_config(node_name: str, plan_id: str, partitioning: NodePartitioning, cu_policy: str = "even",
+                  allocation: str = "pack") -> dict:
     """Device-plugin configuration for one node (the ``ToPluginConfig`` of
     ``mps/partitioner.go:123-157``, AMD shape)."""
     gpus = []
@@ -146,17 +147,19 @@ def plugin_config(node_name: str, plan_id: str, partitioning: NodePartitioning, 
         slices = [{"profile": cm.profile_of_resource(r).name, "memoryGB": cm.profile_of_resource(r).memory_gb,
                    "replicas": n} for r, n in g.resources]
         gpus.append({"index": g.gpu_index, "slices": slices})
-    return {"version": "v1", "node": node_name, "planId": plan_id, "cuPolicy": cu_policy, "gpus": gpus}
+    return {"version": "v1", "node": node_name, "planId": plan_id, "cuPolicy": cu_policy, "allocation": allocation,
+            "gpus": gpus}
 
 
 class CuMaskPartitioner:
     def __init__(self, api, cm_ref: DevicePluginConfigRef | None = None, delay_s: float = 5.0, clock=None,
-                 cu_policy: str = "even"):
+                 cu_policy: str = "even", allocation: str = "pack"):
         self.api = api
         self.cm_ref = cm_ref or DevicePluginConfigRef()
         self.delay_s = delay_s
         self.clock = clock or api.clock
         self.cu_policy = cu_policy
+        self.allocation = allocation
 
     def apply_partitioning(self, node: dict, plan_id: str, partitioning: NodePartitioning) -> None:
         name = ko.name(node)
@@ -171,7 +174,7 @@ class CuMaskPartitioner:
                                     "data": {}})
         data = {k: None for k in (cmap.get("data") or {}) if k.startswith(name + "-")}
         key = f"{name}-{plan_id}"
-        data[key] = yaml.safe_dump(plugin_config(name, plan_id, partitioning, self.cu_policy), sort_keys=False)
+        data[key] = yaml.safe_dump(plugin_config(name, plan_id, partitioning, self.cu_policy, self.allocation), sort_keys=False)
         self.api.patch("ConfigMap", ref.name, {"data": data}, ref.namespace)
         if self.delay_s > 0:
             self.clock.sleep(self.delay_s)  # ConfigMap propagation (kept for fidelity)
@@ -184,8 +187,9 @@ class CuMaskPartitioner:
 
 
 class CuMaskSnapshotTaker:
-    def __init__(self, partition_calculator=None):
+    def __init__(self, partition_calculator=None, placement: str = "pack"):
         self.pc = partition_calculator or CuMaskPartitionCalculator()
+        self.placement = placement
 
     def take_snapshot(self, cs: ClusterState) -> ClusterSnapshot:
         nodes = {}
@@ -194,7 +198,9 @@ class CuMaskSnapshotTaker:
             if n is None or not is_cumask_enabled(n):
                 continue
             try:
-                nodes[name] = cm.SliceNode.from_node_info(ni.clone())
+                sn = cm.SliceNode.from_node_info(ni.clone())
+                sn.placement = self.placement
+                nodes[name] = sn
             except Exception as e:
                 log.debug("skipping node %s: %s", name, e)
         return ClusterSnapshot(nodes, self.pc, cm.SliceCalculator(), cm.SliceFilter())
@@ -219,8 +225,8 @@ def amdpart_strategy(api, clock=None) -> Strategy:
 
 
 def cumask_strategy(api, cm_ref: DevicePluginConfigRef | None = None, delay_s: float = 5.0, clock=None,
-                    cu_policy: str = "even") -> Strategy:
+                    cu_policy: str = "even", placement: str = "pack") -> Strategy:
     pc = CuMaskPartitionCalculator()
-    return Strategy(C.PARTITIONING_CUMASK, CuMaskSnapshotTaker(pc), pc,
-                    CuMaskPartitioner(api, cm_ref, delay_s, clock, cu_policy), cm.SliceCalculator(),
+    return Strategy(C.PARTITIONING_CUMASK, CuMaskSnapshotTaker(pc, placement), pc,
+                    CuMaskPartitioner(api, cm_ref, delay_s, clock, cu_policy, placement), cm.SliceCalculator(),
                     cm.SliceFilter())

@@ -31,56 +31,93 @@ log = logging.getLogger("nos_amd.scheduler")
 
 
 class SchedulerCache:
+    """Node infos maintained incrementally from informer events (the
+    kube-scheduler cache); :meth:`snapshot` clones them per cycle without
+    recomputing pod requests."""
+
     def __init__(self):
         self._lock = threading.RLock()
         self.nodes: dict[str, dict] = {}
         self.pods: dict[str, dict] = {}      # key -> assigned pod
         self.assumed: dict[str, str] = {}    # key -> node
+        self._infos: dict[str, NodeInfo] = {}
+        self._pod_node: dict[str, str] = {}  # key -> node the pod is accounted on
+
+    def _info(self, node_name: str) -> NodeInfo:
+        ni = self._infos.get(node_name)
+        if ni is None:
+            ni = NodeInfo(self.nodes.get(node_name))
+            self._infos[node_name] = ni
+        return ni
+
+    def _unaccount(self, k: str) -> None:
+        nn = self._pod_node.pop(k, None)
+        old = self.pods.get(k)
+        if nn is not None and old is not None and nn in self._infos:
+            try:
+                self._infos[nn].remove_pod(old)
+            except KeyError:
+                pass
+
+    def _account(self, k: str, p: dict) -> None:
+        nn = ko.pod_node(p)
+        self.pods[k] = p
+        self._pod_node[k] = nn
+        self._info(nn).add_pod(p)
 
     def update_node(self, n: dict) -> None:
         with self._lock:
-            self.nodes[ko.name(n)] = n
+            name = ko.name(n)
+            self.nodes[name] = n
+            self._info(name).set_node(n)
 
     def delete_node(self, n: dict) -> None:
         with self._lock:
-            self.nodes.pop(ko.name(n), None)
+            name = ko.name(n)
+            self.nodes.pop(name, None)
+            ni = self._infos.get(name)
+            if ni is not None and not ni.pods:
+                del self._infos[name]
+            elif ni is not None:
+                ni._node = None
 
     def update_pod(self, p: dict) -> None:
         with self._lock:
             k = ko.key(p)
+            self._unaccount(k)
+            self.pods.pop(k, None)
+            self.assumed.pop(k, None)
             if ko.pod_node(p) and not ko.is_terminated(p):
-                self.pods[k] = p
-                self.assumed.pop(k, None)
-            else:
-                self.pods.pop(k, None)
+                self._account(k, p)
 
     def delete_pod(self, p: dict) -> None:
         with self._lock:
-            self.pods.pop(ko.key(p), None)
-            self.assumed.pop(ko.key(p), None)
+            k = ko.key(p)
+            self._unaccount(k)
+            self.pods.pop(k, None)
+            self.assumed.pop(k, None)
 
     def assume(self, p: dict, node: str) -> None:
         with self._lock:
+            k = ko.key(p)
             q = dict(p)
             q["spec"] = dict(p.get("spec") or {})
             q["spec"]["nodeName"] = node
-            self.pods[ko.key(p)] = q
-            self.assumed[ko.key(p)] = node
+            self._unaccount(k)
+            self._account(k, q)
+            self.assumed[k] = node
 
     def forget(self, p: dict) -> None:
         with self._lock:
-            if ko.key(p) in self.assumed:
-                self.assumed.pop(ko.key(p))
-                self.pods.pop(ko.key(p), None)
+            k = ko.key(p)
+            if k in self.assumed:
+                self.assumed.pop(k)
+                self._unaccount(k)
+                self.pods.pop(k, None)
 
     def snapshot(self) -> Snapshot:
         with self._lock:
-            infos = {name: NodeInfo(n) for name, n in self.nodes.items()}
-            for p in self.pods.values():
-                ni = infos.get(ko.pod_node(p))
-                if ni is not None:
-                    ni.add_pod(p)
-            return Snapshot(infos.values())
+            return Snapshot(ni.clone() for name, ni in self._infos.items() if name in self.nodes)
 
 
 class SchedulingQueue:

@@ -224,6 +224,7 @@ class ApiServer:
 
     def _emit(self, kind: str, etype: str, obj: dict, old: dict | None = None) -> None:
         drop = self.faults.get("drop_watch_event", 0.0)
+        shared: tuple | None = None  # one copy per event, shared read-only by all watchers (informer cache)
         for w in list(self._watches):
             if w.kind != kind or w.closed:
                 continue
@@ -231,7 +232,9 @@ class ApiServer:
                 continue
             if drop and self._rng.random() < drop:
                 continue
-            w.push(WatchEvent(etype, copy.deepcopy(obj), copy.deepcopy(old) if old else None))
+            if shared is None:
+                shared = (copy.deepcopy(obj), copy.deepcopy(old) if old else None)
+            w.push(WatchEvent(etype, shared[0], shared[1]))
 
     def _remove_watch(self, w: Watch) -> None:
         with self._lock:

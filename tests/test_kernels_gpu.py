@@ -1,0 +1,165 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references.
+
+Every case runs the native kernel (libnos_hip.so must be loaded: the ops fail
+loudly on a GPU box without it) and compares with the fp32 reference of the
+same op on the CPU.  Tolerances are bf16-output tolerances (outputs are
+rounded to bf16: 2^-8 relative).
+"""
+from __future__ import annotations
+
+import pytest
+import torch
+
+from nos_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(y: torch.Tensor, ref: torch.Tensor) -> float:
+    return ((y.float().cpu() - ref.float()).abs().max() / ref.float().abs().max().clamp_min(1e-6)).item()
+
+
+@pytest.fixture(autouse=True)
+def _native():
+    from nos_amd.ops import _lib
+
+    _lib.require_native_on_gpu()
+    torch.manual_seed(0)
+
+
+@pytest.mark.parametrize("M,N,K,act,resid", [
+    (3401, 1152, 384, None, False), (3401, 1536, 384, "gelu", False), (3401, 384, 1536, None, True),
+    (3401, 384, 384, None, True), (100, 4, 384, "relu", False), (257, 200, 128, None, False),
+    (1, 8, 64, None, False), (4096, 4096, 1024, None, False)])
+def test_linear(M, N, K, act, resid):
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(M, N, device=DEV, dtype=torch.bfloat16) if resid else None
+    y = ops.linear(x, w, b, act=act, residual=r)
+    ref = ops.linear_ref(x.cpu().float(), w.cpu().float(), b.cpu().float(), act=act,
+                         residual=r.cpu().float() if resid else None)
+    assert y.shape == (M, N) and y.dtype == torch.bfloat16
+    assert _rel(y, ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("M,N,K,act", [(3401, 1152, 384, None), (3401, 1536, 384, "gelu"), (77, 100, 128, None),
+                                       (1, 64, 64, None)])
+def test_linear_layernorm_fused(M, N, K, act):
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 2 + 0.5
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    g = torch.randn(K, device=DEV, dtype=torch.bfloat16)
+    be = torch.randn(K, device=DEV, dtype=torch.bfloat16)
+    wg, c1, c2 = ops.fold_layernorm(w, b, g, be)
+    y = ops.linear_ln(x, wg, c1, c2, act=act)
+    ln = torch.nn.functional.layer_norm(x.float().cpu(), (K,), g.float().cpu(), be.float().cpu(), 1e-12)
+    ref = ops.linear_ref(ln, w.cpu().float(), b.cpu().float(), act=act)
+    assert _rel(y, ref) < 2e-2
+
+
+@pytest.mark.parametrize("B,S,H", [(1, 3401, 6), (2, 200, 2), (1, 64, 1), (1, 1000, 3), (1, 65, 2), (1, 1, 1),
+                                   (3, 129, 4)])
+def test_attention(B, S, H):
+    qkv = torch.randn(B, S, 3 * H * 64, device=DEV, dtype=torch.bfloat16)
+    o = ops.attention_qkv(qkv, H)
+    ref = ops.attention_qkv(qkv.cpu().float(), H)
+    assert o.shape == (B, S, H * 64)
+    assert (o.float().cpu() - ref).abs().max().item() < 1e-2
+
+
+def test_attention_large_logits_rescale_path():
+    """Scores spanning many rescale thresholds (peaky rows) exercise the deferred-rescale branch."""
+    B, S, H = 1, 777, 2
+    qkv = torch.randn(B, S, 3 * H * 64, device=DEV, dtype=torch.bfloat16)
+    qkv[..., : H * 64] *= 6.0
+    # increasing key norms along the sequence -> the running max keeps growing
+    ramp = torch.linspace(0.2, 3.0, S, device=DEV).view(1, S, 1)
+    qkv[..., H * 64: 2 * H * 64] = (qkv[..., H * 64: 2 * H * 64].float() * ramp).bfloat16()
+    o = ops.attention_qkv(qkv, H)
+    ref = ops.attention_qkv(qkv.cpu().float(), H)
+    assert (o.float().cpu() - ref).abs().max().item() < 2e-2
+
+
+def test_attention_strided_views():
+    """q/k/v as column views of one packed [B, S, 3*hid] tensor (no copies) and a padded output."""
+    B, S, H = 2, 300, 3
+    hid = H * 64
+    qkv = torch.randn(B, S, 3 * hid, device=DEV, dtype=torch.bfloat16)
+    out = torch.zeros(B, S, hid + 64, device=DEV, dtype=torch.bfloat16)
+    q, k, v = (qkv[..., i * hid:(i + 1) * hid].unflatten(-1, (H, 64)) for i in range(3))
+    ops.attention(q, k, v, out=out[..., :hid].unflatten(-1, (H, 64)))
+    ref = ops.attention_ref(q.cpu().float(), k.cpu().float(), v.cpu().float())
+    assert (out[..., :hid].float().cpu() - ref.reshape(B, S, hid)).abs().max().item() < 1e-2
+    assert out[..., hid:].abs().max().item() == 0  # padding untouched
+
+
+def test_layernorm_with_residual_sum():
+    x = torch.randn(3401, 384, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(3401, 384, device=DEV, dtype=torch.bfloat16)
+    g = torch.randn(384, device=DEV, dtype=torch.bfloat16)
+    bb = torch.randn(384, device=DEV, dtype=torch.bfloat16)
+    y, s = ops.layernorm(x, g, bb, 1e-12, residual=r)
+    ref_s = x.cpu().float() + r.cpu().float()
+    ref_y = torch.nn.functional.layer_norm(ref_s, (384,), g.cpu().float(), bb.cpu().float(), 1e-12)
+    assert (s.float().cpu() - ref_s).abs().max().item() < 3e-2
+    assert (y.float().cpu() - ref_y).abs().max().item() < 5e-2
+
+
+def test_yolos_native_matches_torch_path():
+    from nos_amd.models.yolos import YolosConfig, YolosDetector, demo_input_hw, make_demo_input
+
+    cfg = YolosConfig.small()
+    m = YolosDetector(cfg)
+    m.reset_parameters(0)
+    m = m.to(DEV, torch.bfloat16).eval()
+    x = make_demo_input(cfg, device=DEV, hw=demo_input_hw(), seed=0)
+    with torch.no_grad():
+        lg, bx = m(x)
+        m.backend = "torch"
+        lr, br = m(x)
+    assert (lg.float() - lr.float()).abs().max().item() < 0.05 * max(1.0, lr.float().abs().max().item())
+    assert (bx.float() - br.float()).abs().max().item() < 2e-2
+
+
+def test_graphed_tenants_on_cumask_streams():
+    from nos_amd.gpu.topology import split_even
+    from nos_amd.models.tenants import InferenceTenants, TenantSpec
+    from nos_amd.models.yolos import YolosConfig, demo_input_hw
+    from nos_amd.ops.streams import device_info
+
+    n_cus = device_info(0)["num_cus"]
+    specs = [TenantSpec(f"p{i}", s.cus()) for i, s in enumerate(split_even(2))]
+    ts = InferenceTenants(specs, n_cus, YolosConfig.small(), demo_input_hw(), use_graphs=True)
+    ts.prepare()
+    dt = ts.run(2)
+    ts.close()
+    assert dt > 0
+
+
+def test_cumask_stream_roundtrip():
+    from nos_amd.ops.streams import CUMaskedStream
+
+    cus = list(range(0, 256, 2))
+    s = CUMaskedStream(cus, 256)
+    try:
+        assert s.get_mask() == cus
+        x = torch.randn(1024, 1024, device=DEV)
+        with torch.cuda.stream(s.torch):
+            y = x @ x
+        s.synchronize()
+        assert torch.isfinite(y).all()
+    finally:
+        s.close()
+
+
+def test_probes_report_sane_numbers():
+    from nos_amd.ops import probes
+
+    stream = torch.cuda.current_stream().cuda_stream
+    summary = probes.placement_summary(probes.placement(stream))
+    assert len(summary["xccs"]) == 8
+    assert probes.hbm_gbps(stream) > 1000
+    assert probes.mfma_peak_tflops(stream, 1024) > 500

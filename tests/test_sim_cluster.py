@@ -1,0 +1,153 @@
+"""End-to-end control-plane scenarios on the in-process cluster (the
+reference's envtest integration suites): pending fractional pods
+-> partitioner plan -> agent / device plugin -> kubelet -> Running."""
+from __future__ import annotations
+
+from collections import Counter
+
+import pytest
+
+from nos_amd.api import constants as C
+from nos_amd.api import v1alpha1
+from nos_amd.api.config import GpuPartitionerConfig
+from nos_amd.bench_support import control_plane_plan, cus_from_hex
+from nos_amd.gpu.fakesmi import FakeSmi
+from nos_amd.gpu.topology import xcd_of
+from nos_amd.kube import objects as ko
+from nos_amd.sim.cluster import SimCluster
+
+
+def _envs(node):
+    return [rc.envs for conts in node.kubelet.running_containers().values() for rc in conts]
+
+
+def test_cumask_pack_places_all_pods_first_fit():
+    cl = SimCluster()
+    nd = cl.add_node("n1", C.PARTITIONING_CUMASK, gpus=2)
+    cl.settle(30)
+    for i in range(30):
+        cl.submit_pod(f"p{i}", {"amd.com/gpu-10gb": 1})
+    cl.settle(600, until=lambda: not cl.pending_pods())
+    assert len(cl.running_pods()) == 30
+    ann = ko.annotations(cl.api.get("Node", "n1"))
+    # first fit: GPU 0 is filled (28 x 10 GB <= 288 GB, 28 <= 32 masks) before GPU 1
+    assert ann["nos.nebuly.com/spec-gpu-0-10gb"] == "28"
+    assert ann["nos.nebuly.com/spec-gpu-1-10gb"] == "2"
+    assert ann[C.ANNOTATION_REPORTED_PARTITIONING_PLAN] == ann[C.ANNOTATION_PARTITIONING_PLAN]
+    envs = _envs(nd)
+    assert Counter(e[C.ENV_VISIBLE_DEVICES] for e in envs) == {"0": 28, "1": 2}
+
+
+def test_cumask_spread_masks_are_xcd_symmetric_and_disjoint():
+    cfg = GpuPartitionerConfig(slicePlacement="spread")
+    cl = SimCluster(partitioner_config=cfg)
+    nd = cl.add_node("n1", C.PARTITIONING_CUMASK, gpus=4)
+    cl.settle(30)
+    for i in range(16):
+        cl.submit_pod(f"p{i}", {"amd.com/gpu-10gb": 1})
+    cl.settle(600, until=lambda: not cl.pending_pods())
+    envs = _envs(nd)
+    assert Counter(e[C.ENV_VISIBLE_DEVICES] for e in envs) == {str(g): 4 for g in range(4)}
+    for g in range(4):
+        masks = [cus_from_hex(e[C.ENV_CU_MASK]) for e in envs if e[C.ENV_VISIBLE_DEVICES] == str(g)]
+        seen: set[int] = set()
+        for m in masks:
+            per_xcd = Counter(xcd_of(c) for c in m)
+            assert len(per_xcd) == 8 and len(set(per_xcd.values())) == 1, per_xcd
+            assert not (seen & set(m))
+            seen |= set(m)
+        assert len(seen) == 256  # the 4 slices own the whole GPU
+
+
+def test_cumask_capacity_is_min_of_memory_and_masks():
+    cl = SimCluster()
+    cl.add_node("n1", C.PARTITIONING_CUMASK, gpus=1)
+    cl.settle(30)
+    for i in range(40):
+        cl.submit_pod(f"p{i}", {"amd.com/gpu-8gb": 1})
+    cl.settle(300)
+    # 288 GB / 8 GB = 36 by memory, but only 32 XCD-symmetric masks per GPU
+    assert len(cl.running_pods()) == 32
+
+
+def test_amdpart_switches_modes_and_exposes_logical_devices():
+    cl = SimCluster()
+    nd = cl.add_node("n1", C.PARTITIONING_AMDPART, gpus=2)
+    cl.settle(30)
+    node = cl.api.get("Node", "n1")
+    assert ko.node_allocatable(node)["amd.com/partition-8xcd.288gb"] == 2
+    for i in range(8):
+        cl.submit_pod(f"s{i}", {"amd.com/partition-1xcd.36gb": 1})
+    cl.submit_pod("big", {"amd.com/partition-4xcd.144gb": 1})
+    cl.settle(600, until=lambda: not cl.pending_pods())
+    assert len(cl.running_pods()) == 9
+    assert sorted(zip(nd.smi.compute, nd.smi.memory)) == [("CPX", "NPS1"), ("DPX", "NPS1")]
+    vis = sorted(int(e[C.ENV_VISIBLE_DEVICES]) for e in _envs(nd))
+    # CPX GPU 0 -> logical 0..7; DPX GPU 1 -> logical 8, 9
+    assert vis[:8] == list(range(8)) and vis[8] in (8, 9)
+    ann = ko.annotations(cl.api.get("Node", "n1"))
+    assert ann[C.ANNOTATION_REPORTED_PARTITIONING_PLAN] == ann[C.ANNOTATION_PARTITIONING_PLAN]
+
+
+def test_amdpart_never_repartitions_a_busy_gpu():
+    cl = SimCluster()
+    nd = cl.add_node("n1", C.PARTITIONING_AMDPART, gpus=1)
+    cl.settle(30)
+    cl.submit_pod("whole", {"amd.com/partition-8xcd.288gb": 1})
+    cl.settle(120, until=lambda: not cl.pending_pods())
+    assert len(cl.running_pods()) == 1
+    cl.submit_pod("small", {"amd.com/partition-1xcd.36gb": 1})
+    cl.settle(300)
+    assert nd.smi.compute == ["SPX"] and nd.smi.switches == 0
+    assert [ko.name(p) for p in cl.pending_pods()] == ["small"]
+    # the GPU drains -> the pending pod's plan can be realised
+    nd.kubelet.complete_pod("default", "whole")
+    cl.settle(600, until=lambda: not cl.pending_pods())
+    assert nd.smi.compute == ["CPX"]
+    assert [ko.name(p) for p in cl.running_pods()] == ["small"]
+
+
+def test_amdpart_blocked_by_foreign_process():
+    cl = SimCluster()
+    smi = FakeSmi(gpus=1, node="n1")
+    cl.add_node("n1", C.PARTITIONING_AMDPART, smi=smi)
+    cl.settle(30)
+    smi.fake_add_process(0, 4242)
+    cl.submit_pod("small", {"amd.com/partition-1xcd.36gb": 1})
+    cl.settle(200)
+    assert smi.compute == ["SPX"]
+    smi.fake_remove_process(0, 4242)
+    cl.settle(600, until=lambda: not cl.pending_pods())
+    assert smi.compute == ["CPX"] and len(cl.running_pods()) == 1
+
+
+def test_elastic_quota_labels_running_pods():
+    cl = SimCluster()
+    cl.add_node("n1", C.PARTITIONING_CUMASK, gpus=1)
+    # as in the reference, min/max always bound cpu and memory (elasticquotainfo.go:319-326),
+    # so quotas must state them; team-a can borrow team-b's unused min
+    for ns, mn in (("team-a", 20), ("team-b", 40)):
+        cl.api.create({"kind": "Namespace", "metadata": {"name": ns}})
+        cl.api.create(v1alpha1.build_eq(ns, "q")
+                      .with_min({"nos.nebuly.com/gpu-memory": mn, "cpu": "8", "memory": "64Gi"})
+                      .with_max({"nos.nebuly.com/gpu-memory": 100, "cpu": "64", "memory": "1Ti"}).get())
+    cl.settle(30)
+    for i in range(4):
+        cl.submit_pod(f"p{i}", {"amd.com/gpu-10gb": 1}, namespace="team-a")
+        cl.clock.advance(1)
+    cl.settle(600, until=lambda: not cl.pending_pods())
+    cl.settle(30)
+    labels = {ko.name(p): ko.labels(p).get(C.LABEL_CAPACITY_INFO) for p in cl.pods("team-a")}
+    assert labels == {"p0": "in-quota", "p1": "in-quota", "p2": "over-quota", "p3": "over-quota"}
+    eq = cl.api.get(v1alpha1.KIND_EQ, "q", "team-a")
+    assert eq["status"]["used"]["nos.nebuly.com/gpu-memory"] == "40"
+
+
+@pytest.mark.parametrize("n_gpus", [1, 2])
+def test_bench_control_plane_plan(n_gpus):
+    masks, info = control_plane_plan(n_gpus=n_gpus, pods_per_gpu=4, slice_gb=10, num_cus=256, local_gpu=0)
+    assert len(masks) == 4
+    assert info["placed_pods"] == 4 * n_gpus and info["pending_pods"] == 0
+    assert info["schedulable_fractional_pods_per_node"] == 28 * n_gpus
+    assert info["plan_reported"]
+    assert sorted(c for m in masks for c in m) == list(range(256))
