@@ -44,8 +44,11 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pods-per-gpu", type=int, default=8)
     ap.add_argument("--slice-gb", type=int, default=10, help="GPU memory per fractional pod (demo: 10)")
-    ap.add_argument("--mode", choices=["cumask", "shared", "exclusive"], default="cumask",
-                    help="cumask: XCD-symmetric CU-mask slices; shared: unmasked concurrent streams")
+    ap.add_argument("--mode", choices=["cumask", "shared", "exclusive"], default="shared",
+                    help="device-plugin CU policy of the 10 GB slices -- shared: memory-capped slices whose "
+                         "kernels run concurrently on all CUs (the MPS behaviour of the reference demo); "
+                         "cumask: each slice also gets exclusive XCD-symmetric CUs (compute isolation); "
+                         "exclusive: one pod per GPU")
     ap.add_argument("--collective", action="store_true", help="add a GEMM + RCCL all-reduce tenant per GPU")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-control-plane", action="store_true")
@@ -76,9 +79,8 @@ def plan(args, world: int, num_cus: int) -> tuple[list[list[int] | None], dict]:
         from nos_amd.bench_support import control_plane_plan
 
         masks, info = control_plane_plan(n_gpus=world, pods_per_gpu=args.pods_per_gpu, slice_gb=args.slice_gb,
-                                         num_cus=num_cus, local_gpu=int(os.environ.get("LOCAL_RANK", "0")))
-        if args.mode == "shared":
-            masks = [None] * len(masks)
+                                         num_cus=num_cus, local_gpu=int(os.environ.get("LOCAL_RANK", "0")),
+                                         cu_policy="shared" if args.mode == "shared" else "even")
         return masks, info
     if args.mode == "shared":
         return [None] * args.pods_per_gpu, info

@@ -24,10 +24,9 @@
 //    destination, cdna_hip_programming.md rule 21);
 //  * every LDS address is a per-lane base register + an immediate: the
 //    swizzle terms that vary per lane are hoisted out of the key loop;
-//  * Q is pre-scaled by scale*log2(e) and the S accumulator starts at -m
-//    ("row constant as the initial accumulator"), so p = exp2(S') costs one
-//    v_exp per score; with the deferred rescale (T13) O and l are only
-//    rescaled when some row's max grows by more than 8 (P <= 2^8);
+//  * deferred rescale (T13): O and l are only rescaled when some row's max
+//    grows by more than 8 (log2 units; P <= 2^8); the reference max starts
+//    at the group's first tile max, so no -inf sentinels are needed;
 //  * XCD-aware workgroup -> (batch, head, q-block) map: q-blocks of one
 //    head share an XCD's L2 (K/V of one head = 870 KB at S = 3401).
 #include "common.h"
@@ -83,14 +82,10 @@ __global__ __launch_bounds__(NT, 4) void attn_fwd_d64_kernel(
   // ---- Q fragments (B operand): lane holds Q[row r][d = 16ks + 8hh .. +7]
   const int qrow = qb * QBLK + wq * 32 + r;
   const int qrow_c = qrow < Sq ? qrow : Sq - 1;
-  // pre-scaled by c = scale*log2(e): S' = Q'K^T is already in log2 units
   bf16x8_t qf[4];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const bf16x8_t raw = *reinterpret_cast<const bf16x8_t*>(qb_ptr + (long long)qrow_c * ld_in + ks * 16 + hh * 8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qf[ks][j] = (__bf16)((float)raw[j] * c);
-  }
+  for (int ks = 0; ks < 4; ++ks)
+    qf[ks] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + (long long)qrow_c * ld_in + ks * 16 + hh * 8);
 
   // ---- LDS-DMA staging: per iteration 2 tiles x (K + V) = 32 x 1 KiB pieces,
   // 4 per wave.  Piece p (0..31): tensor p>>4 (K/V), tile-row block (p&15)*8.
@@ -133,10 +128,11 @@ __global__ __launch_bounds__(NT, 4) void attn_fwd_d64_kernel(
   f32x16_t oacc[2];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
-  // m: the row's reference max (log2 units).  The S' accumulator starts at -m
-  // (MFMA adds Q'K^T on top), so p = exp2(acc) needs no subtraction; m only
-  // moves on the group's first tile and when a row's max exceeds it by more
-  // than RESCALE_THR (then p <= 2^RESCALE_THR in between).
+  // m: the row's reference max in log2 units (scores x c); p = exp2(s*c - m)
+  // is one FMA + one v_exp per score.  m only moves on the group's first tile
+  // and when a row's max exceeds it by more than RESCALE_THR (then
+  // p <= 2^RESCALE_THR in between).  (Pre-scaling Q by c instead would add a
+  // bf16 rounding of Q*c: ~0.1 abs error on peaky rows.)
   float m = 0.f, l = 0.f;
 
   __syncthreads();  // drains stage 0 (vmcnt(0)) and publishes it
@@ -154,7 +150,7 @@ __global__ __launch_bounds__(NT, 4) void attn_fwd_d64_kernel(
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[kb][i] = -m;
+        for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(kl + koff[ks] + kb * 32 * 128);
@@ -175,10 +171,10 @@ __global__ __launch_bounds__(NT, 4) void attn_fwd_d64_kernel(
       for (int i = 1; i < 16; ++i) mt = fmaxf(mt, sacc[0][i]);
 #pragma unroll
       for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[1][i]);
-      mt = xor32_max(mt);  // = tile max - m
-      if (it == 0 || !__all(mt <= RESCALE_THR)) {
+      const float mrel = fmaf(xor32_max(mt), c, -m);  // tile max - m (log2 units)
+      if (it == 0 || !__all(mrel <= RESCALE_THR)) {
         // first tile: m := tile max; later: raise m where the max grew
-        const float delta = it == 0 ? mt : fmaxf(mt, 0.f);
+        const float delta = it == 0 ? mrel : fmaxf(mrel, 0.f);
         const float alpha = __builtin_amdgcn_exp2f(-delta);
         m += delta;
         l *= alpha;
@@ -186,8 +182,6 @@ __global__ __launch_bounds__(NT, 4) void attn_fwd_d64_kernel(
         for (int i = 0; i < 16; ++i) {
           oacc[0][i] *= alpha;
           oacc[1][i] *= alpha;
-          sacc[0][i] -= delta;
-          sacc[1][i] -= delta;
         }
       }
       float psum = 0.f;
@@ -195,7 +189,7 @@ __global__ __launch_bounds__(NT, 4) void attn_fwd_d64_kernel(
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(sacc[kb][i]);
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][i], c, -m));
           sacc[kb][i] = p;
           psum += p;
         }
@@ -243,10 +237,13 @@ __global__ __launch_bounds__(NT, 4) void attn_fwd_d64_kernel(
   if (grp == 0) {
     const float m1 = xch[32 * 64 + lane];
     const float l1 = xch[33 * 64 + lane];
-    // a group that saw no tile has l == 0 and must not set the reference max
-    const float mf = l1 == 0.f ? m : fmaxf(m, m1);
+    // group 1 saw no tile when the sequence has a single tile: it must not set
+    // the reference max (a per-lane l1 == 0 test would be wrong: each lane
+    // holds a partial sum over half of the keys)
+    const bool g1 = ntiles > 1;
+    const float mf = g1 ? fmaxf(m, m1) : m;
     const float a0 = __builtin_amdgcn_exp2f(m - mf);
-    const float a1 = l1 == 0.f ? 0.f : __builtin_amdgcn_exp2f(m1 - mf);
+    const float a1 = g1 ? __builtin_amdgcn_exp2f(m1 - mf) : 0.f;
     float lt = l * a0 + l1 * a1;
     lt += __shfl_xor(lt, 32, 64);
     const float inv = 1.f / lt;

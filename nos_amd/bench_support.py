@@ -74,15 +74,15 @@ def control_plane_plan(n_gpus: int, pods_per_gpu: int, slice_gb: int, num_cus: i
     sim_s = cl.settle(3600, until=lambda: not cl.pending_pods())
     wall = time.perf_counter() - t0
     node = cl.nodes["mi355x-0"]
-    masks: list[list[int]] = []
+    masks: list[list[int] | None] = []
     per_gpu: dict[str, int] = {}
     for _key, conts in sorted(node.kubelet.running_containers().items()):
         for rc in conts:
             env = rc.envs
             gpu = env.get(C.ENV_VISIBLE_DEVICES, "")
             per_gpu[gpu] = per_gpu.get(gpu, 0) + 1
-            if gpu == str(local_gpu) and C.ENV_CU_MASK in env:
-                masks.append(cus_from_hex(env[C.ENV_CU_MASK]))
+            if gpu == str(local_gpu):  # no mask env: the slice runs on every CU (cuPolicy shared)
+                masks.append(cus_from_hex(env[C.ENV_CU_MASK]) if C.ENV_CU_MASK in env else None)
     ann = ko.annotations(cl.api.get("Node", "mi355x-0"))
     info.update({"placed_pods": len(cl.running_pods()), "pending_pods": len(cl.pending_pods()),
                  "pods_per_gpu_placed": per_gpu, "time_to_running_sim_seconds": round(sim_s, 3),
@@ -90,5 +90,5 @@ def control_plane_plan(n_gpus: int, pods_per_gpu: int, slice_gb: int, num_cus: i
                  "plan_id": ann.get(C.ANNOTATION_PARTITIONING_PLAN),
                  "plan_reported": ann.get(C.ANNOTATION_REPORTED_PARTITIONING_PLAN) ==
                  ann.get(C.ANNOTATION_PARTITIONING_PLAN),
-                 "slice_resource": res, "cus_per_pod": len(masks[0]) if masks else 0})
+                 "slice_resource": res, "cus_per_pod": len(masks[0]) if masks and masks[0] else num_cus, "cu_policy": cu_policy})
     return masks, info

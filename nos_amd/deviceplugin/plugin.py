@@ -242,8 +242,8 @@ class NosAmdDevicePlugin:
                     alloc.devices.append(dev)
             alloc.devices.insert(0, "/dev/kfd")
             alloc.envs[C.ENV_VISIBLE_DEVICES] = ",".join(visible)
-            if mask_cus:
-                n_cus = MI355X_XCDS * MI355X_CUS_PER_XCD
+            n_cus = MI355X_XCDS * MI355X_CUS_PER_XCD
+            if mask_cus and len(mask_cus) < n_cus:  # a full mask would only cost a dedicated HW queue
                 alloc.envs[C.ENV_CU_MASK] = mask_hex(sorted(mask_cus), n_cus)
             if mem:
                 alloc.envs[C.ENV_MEMORY_LIMIT_GB] = str(mem)

@@ -65,6 +65,15 @@ class Forbidden(ApiError):
     code, reason = 403, "Forbidden"
 
 
+class Expired(ApiError):
+    """410 Gone: a watch asked for a resourceVersion older than the event history."""
+
+    code, reason = 410, "Expired"
+
+
+ERRORS_BY_REASON = {c.reason: c for c in (NotFound, AlreadyExists, Conflict, Invalid, Forbidden, Expired)}
+
+
 def is_not_found(e: BaseException) -> bool:
     return isinstance(e, NotFound)
 
@@ -173,6 +182,9 @@ class ApiServer:
         self._rng = random.Random(seed)
         self.faults: dict[str, float] = {}  # conflict_on_write, drop_watch_event
         self.request_counts: collections.Counter = collections.Counter()
+        # (rv, kind, event) for watches that resume from a resourceVersion
+        self._history: collections.deque = collections.deque(maxlen=50000)
+        self._history_floor = 0  # events with rv <= floor may have been dropped
         for t in CORE_TYPES:
             self.register_type(t)
         self.register_field_indexer("Pod", "status.phase", ko.pod_phase)
@@ -224,7 +236,11 @@ class ApiServer:
 
     def _emit(self, kind: str, etype: str, obj: dict, old: dict | None = None) -> None:
         drop = self.faults.get("drop_watch_event", 0.0)
-        shared: tuple | None = None  # one copy per event, shared read-only by all watchers (informer cache)
+        # one copy per event, shared read-only by the history and all watchers (informer cache)
+        ev = WatchEvent(etype, copy.deepcopy(obj), copy.deepcopy(old) if old else None)
+        if len(self._history) == self._history.maxlen:
+            self._history_floor = self._history[0][0]
+        self._history.append((int(ko.resource_version(obj) or self._last_rv), kind, ev))
         for w in list(self._watches):
             if w.kind != kind or w.closed:
                 continue
@@ -232,9 +248,7 @@ class ApiServer:
                 continue
             if drop and self._rng.random() < drop:
                 continue
-            if shared is None:
-                shared = (copy.deepcopy(obj), copy.deepcopy(old) if old else None)
-            w.push(WatchEvent(etype, shared[0], shared[1]))
+            w.push(ev)
 
     def _remove_watch(self, w: Watch) -> None:
         with self._lock:
@@ -388,7 +402,8 @@ class ApiServer:
                 for kk, store in self._store.items():
                     if self._types[kk].namespaced:
                         for ok_ in [x for x, o in store.items() if ko.namespace(o) == name]:
-                            obj = store.pop(ok_)
+                            obj = copy.deepcopy(store.pop(ok_))
+                            ko.meta(obj)["resourceVersion"] = self._next_rv()
                             self._emit(kk, DELETED, obj)
             return gone
 
@@ -411,16 +426,39 @@ class ApiServer:
     # ------------------------------------------------------------ watch
     def watch(self, kind: str, namespace: str | None = None, label_selector=None,
               field_selector: str | None = None, send_initial: bool = True,
-              callback: Callable[[WatchEvent], None] | None = None) -> Watch:
+              callback: Callable[[WatchEvent], None] | None = None,
+              resource_version: str | None = None) -> Watch:
+        """Open a watch.  With ``resource_version`` the stream resumes after
+        that version (events replayed from the history, 410 Expired if they
+        were dropped); otherwise ``send_initial`` synthesises ADDED events for
+        the current objects, atomically with the registration."""
         self.type_of(kind)
         w = Watch(kind, namespace, self._label_reqs(label_selector), sel.parse_field_selector(field_selector),
                   self, callback=callback)
         with self._lock:
-            if send_initial:
+            if resource_version not in (None, ""):  # "0" = from the very beginning (empty store)
+                rv = int(resource_version)
+                if rv < self._history_floor:
+                    raise Expired(f"too old resource version: {rv} ({self._history_floor})")
+                for erv, ekind, ev in list(self._history):
+                    if erv > rv and ekind == kind and (w.matches(ev.object) or
+                                                       (ev.old is not None and w.matches(ev.old))):
+                        w.push(ev)
+            elif send_initial:
                 for o in self.list(kind, namespace, label_selector, field_selector):
                     w.push(WatchEvent(ADDED, o))
             self._watches.append(w)
         return w
+
+    def current_resource_version(self) -> str:
+        with self._lock:
+            return str(self._last_rv)
+
+    def list_with_version(self, kind: str, namespace: str | None = None, label_selector=None,
+                          field_selector: str | None = None) -> tuple[list[dict], str]:
+        """List + the resourceVersion to resume a watch from (one atomic step)."""
+        with self._lock:
+            return self.list(kind, namespace, label_selector, field_selector), str(self._last_rv)
 
     # ------------------------------------------------------------ checkpoint
     def snapshot(self) -> str:

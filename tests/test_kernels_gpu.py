@@ -103,9 +103,11 @@ def test_layernorm_with_residual_sum():
     bb = torch.randn(384, device=DEV, dtype=torch.bfloat16)
     y, s = ops.layernorm(x, g, bb, 1e-12, residual=r)
     ref_s = x.cpu().float() + r.cpu().float()
-    ref_y = torch.nn.functional.layer_norm(ref_s, (384,), g.cpu().float(), bb.cpu().float(), 1e-12)
     assert (s.float().cpu() - ref_s).abs().max().item() < 3e-2
-    assert (y.float().cpu() - ref_y).abs().max().item() < 5e-2
+    # the residual stream is bf16 (as in the model): normalise the rounded sum
+    ref_y = torch.nn.functional.layer_norm(ref_s.bfloat16().float(), (384,), g.cpu().float(), bb.cpu().float(),
+                                           1e-12)
+    assert _rel(y, ref_y) < 1e-2
 
 
 def test_yolos_native_matches_torch_path():
