@@ -257,6 +257,16 @@ class NosAmdDevicePlugin:
             for did in stale:
                 self.devices.pop(did, None)
 
+    def sync_allocated(self, used_device_ids: set[str]) -> None:
+        """The device-plugin API has no Deallocate: a deployed plugin learns
+        which devices are still in use from kubelet PodResources."""
+        with self._lock:
+            for did in list(self.allocated):
+                if did not in used_device_ids:
+                    self.release([did])
+            for did in used_device_ids:
+                self.allocated.setdefault(did, "podresources")
+
     def cu_slice_of(self, device_id: str) -> CUSlice | None:
         return self.cu_slots.get(device_id)
 
