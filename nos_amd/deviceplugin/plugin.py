@@ -119,8 +119,12 @@ class NosAmdDevicePlugin:
                 if did not in devs and did in self.devices:
                     d = self.devices[did]
                     devs[did] = Device(d.id, d.resource, d.gpu_index, False, d.partition, d.profile, d.memory_gb)
+            changed = ({k: (d.resource, d.healthy) for k, d in devs.items()} !=
+                       {k: (d.resource, d.healthy) for k, d in self.devices.items()}) or self.generation == 0
             self.devices = devs
             self._layout_cu_slots()
+            if not changed:
+                return
             self.generation += 1
         for cb in list(self.listeners):
             try:
