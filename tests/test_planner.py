@@ -1,0 +1,144 @@
+"""Planner scenarios (the reference's ``internal/partitioning/core/planner_test.go``)
+for both AMD strategies, with a stub scheduler framework whose PreFilter /
+Filter verdicts are programmable, plus the actuator and plan-id rules."""
+from __future__ import annotations
+
+from nos_amd.api import constants as C
+from nos_amd.gpu import amdpart as ap
+from nos_amd.gpu import cumask as cm
+from nos_amd.kube import factory as kf
+from nos_amd.partitioning.core import ClusterSnapshot, Planner, sort_pods
+from nos_amd.partitioning.strategies import AmdPartPartitionCalculator, CuMaskPartitionCalculator
+from nos_amd.scheduler.framework import NodeInfo, Status
+
+M = "AMD-Instinct-MI355X"
+
+
+class StubFramework:
+    def __init__(self, pre=Status.ok(), flt=Status.ok()):
+        self.pre, self.flt = pre, flt
+
+    def run_pre_filter_plugins(self, state, pod):
+        return None, self.pre
+
+    def run_filter_plugins(self, state, pod, ni):
+        return self.flt
+
+
+def _pod(name: str, res: str, n: int = 1, prio: int | None = None) -> dict:
+    b = kf.build_pod("ns", name).with_container(kf.build_container().with_cpu_milli_request(100)
+                                                .with_scalar_resource_request(res, n).get())
+    if prio is not None:
+        b = b.with_priority(prio)
+    return b.get()
+
+
+def _node(name: str, kind: str, count: int = 1, ann: dict | None = None, alloc: dict | None = None) -> dict:
+    return kf.build_node(name).with_labels({"amd.com/gpu.product": M, "amd.com/gpu.count": str(count),
+                                            "amd.com/gpu.memory": "294912",
+                                            C.LABEL_GPU_PARTITIONING: kind}) \
+        .with_annotations(ann or {}).with_allocatable_resources({"cpu": "64", "memory": "512Gi", "pods": "110",
+                                                                 **(alloc or {})}).get()
+
+
+def _cumask_snapshot(nodes: list[dict], placement: str = "pack") -> ClusterSnapshot:
+    sn = {}
+    for n in nodes:
+        s = cm.SliceNode.from_node_info(NodeInfo(n))
+        s.placement = placement
+        sn[n["metadata"]["name"]] = s
+    return ClusterSnapshot(sn, CuMaskPartitionCalculator(), cm.SliceCalculator(), cm.SliceFilter())
+
+
+def _amd_snapshot(nodes: list[dict]) -> ClusterSnapshot:
+    sn = {n["metadata"]["name"]: ap.PartitionNode.from_node_info(NodeInfo(n)) for n in nodes}
+    return ClusterSnapshot(sn, AmdPartPartitionCalculator(), ap.PartitionSliceCalculator(), ap.PartitionSliceFilter())
+
+
+def _cumask_planner(fw=None) -> Planner:
+    return Planner(CuMaskPartitionCalculator(), cm.SliceCalculator(), fw or StubFramework())
+
+
+def _amd_planner(fw=None) -> Planner:
+    return Planner(AmdPartPartitionCalculator(), ap.PartitionSliceCalculator(), fw or StubFramework())
+
+
+def _res(plan, node: str) -> list[dict]:
+    return [g.resource_dict() for g in sorted(plan.desired_state[node].gpus, key=lambda g: g.gpu_index)]
+
+
+def test_empty_snapshot():
+    plan = _cumask_planner().plan(_cumask_snapshot([]), [_pod("p", "amd.com/gpu-10gb")])
+    assert plan.desired_state.is_empty()
+
+
+def test_pods_without_slices_leave_state_unchanged():
+    snap = _cumask_snapshot([_node("n1", "cumask", ann={"nos.nebuly.com/status-gpu-0-10gb-free": "1"})])
+    plan = _cumask_planner().plan(snap, [kf.build_pod("ns", "cpu-only").get()])
+    assert _res(plan, "n1") == [{"amd.com/gpu-10gb": 1}]
+
+
+def test_cumask_creates_slices_on_free_capacity():
+    snap = _cumask_snapshot([_node("n1", "cumask", count=2)])
+    pods = [_pod(f"p{i}", "amd.com/gpu-20gb") for i in range(3)] + [_pod("q", "amd.com/gpu-10gb")]
+    plan = _cumask_planner().plan(snap, pods)
+    assert _res(plan, "n1") == [{"amd.com/gpu-10gb": 1, "amd.com/gpu-20gb": 3}, {}]
+
+
+def test_cumask_groups_small_free_slices_into_larger():
+    # 288 GB GPU: 1 used 100gb + 18 free 10gb slices (full); a 150gb pod needs the free ones dropped
+    snap = _cumask_snapshot([_node("n1", "cumask", ann={"nos.nebuly.com/status-gpu-0-100gb-used": "1",
+                                                        "nos.nebuly.com/status-gpu-0-10gb-free": "18"})])
+    plan = _cumask_planner().plan(snap, [_pod("big", "amd.com/gpu-150gb")])
+    # the original free slices are re-created all-or-nothing per profile (slicing/gpu.go:213-216):
+    # 18 x 10 GB no longer fit next to 100 + 150 GB, so none come back
+    assert _res(plan, "n1") == [{"amd.com/gpu-100gb": 1, "amd.com/gpu-150gb": 1}]
+
+
+def test_prefilter_or_filter_failure_changes_nothing():
+    for fw in (StubFramework(pre=Status.new("Unschedulable", "quota")),
+               StubFramework(flt=Status.new("Unschedulable", "taint"))):
+        snap = _cumask_snapshot([_node("n1", "cumask")])
+        plan = _cumask_planner(fw).plan(snap, [_pod("p", "amd.com/gpu-10gb")])
+        assert _res(plan, "n1") == [{}]
+
+
+def test_spread_placement_balances_gpus():
+    snap = _cumask_snapshot([_node("n1", "cumask", count=4)], placement="spread")
+    plan = _cumask_planner().plan(snap, [_pod(f"p{i}", "amd.com/gpu-10gb") for i in range(8)])
+    assert _res(plan, "n1") == [{"amd.com/gpu-10gb": 2}] * 4
+
+
+def test_amdpart_switches_idle_gpu_to_cpx():
+    snap = _amd_snapshot([_node("n1", "partition", count=2,
+                                ann={"nos.nebuly.com/status-gpu-0-8xcd.288gb-used": "1",
+                                     "nos.nebuly.com/status-gpu-1-8xcd.288gb-free": "1"})])
+    plan = _amd_planner().plan(snap, [_pod(f"s{i}", "amd.com/partition-1xcd.36gb") for i in range(3)])
+    gpus = sorted(plan.desired_state["n1"].gpus, key=lambda g: g.gpu_index)
+    assert gpus[0].resource_dict() == {"amd.com/partition-8xcd.288gb": 1}  # in use: untouched
+    assert gpus[1].resource_dict() == {"amd.com/partition-1xcd.36gb": 8} and gpus[1].mode == "CPX/NPS1"
+
+
+def test_amdpart_prefers_geometry_providing_most_lacking():
+    snap = _amd_snapshot([_node("n1", "partition", count=1,
+                                ann={"nos.nebuly.com/status-gpu-0-8xcd.288gb-free": "1"})])
+    plan = _amd_planner().plan(snap, [_pod("a", "amd.com/partition-4xcd.144gb"),
+                                      _pod("b", "amd.com/partition-4xcd.144gb")])
+    g = plan.desired_state["n1"].gpus[0]
+    assert g.resource_dict() == {"amd.com/partition-4xcd.144gb": 2} and g.mode == "DPX/NPS1"
+
+
+def test_sort_pods_priority_then_smaller_slice_first():
+    pods = [_pod("big", "amd.com/gpu-40gb"), _pod("small", "amd.com/gpu-10gb"),
+            _pod("vip", "amd.com/gpu-80gb", prio=100)]
+    assert [p["metadata"]["name"] for p in sort_pods(pods, cm.SliceCalculator())] == ["vip", "small", "big"]
+
+
+def test_snapshot_fork_revert_is_isolated():
+    snap = _cumask_snapshot([_node("n1", "cumask")])
+    snap.fork()
+    n = snap.get_node("n1")
+    n.update_geometry_for({cm.SliceProfile("10gb"): 2})
+    snap.set_node(n)
+    snap.revert()
+    assert snap.get_node("n1").gpus[0].num_slices() == 0
