@@ -28,7 +28,8 @@
 //    written as fp32 to LDS, then every thread stores 16-byte bf16 chunks
 //    of whole rows (coalesced) and adds the residual with 16-byte loads;
 //  * optional persistent mode (grid smaller than the tile count) and an
-//    XCD-aware tile order so tiles sharing a W panel share an XCD's L2.
+//    XCD-aware tile order so tiles sharing the larger operand panel share an
+//    XCD's L2.
 #include "common.h"
 
 namespace {
@@ -102,8 +103,18 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
 
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int tt = (gridDim.x >= ntiles) ? nos::xcd_remap(tile, ntiles) : tile;
-    const int tn = tt / tiles_m;  // column-panel major: tiles of one W panel adjacent
-    const int tm = tt - tn * tiles_m;
+    // consecutive tt share an XCD (and its L2): order them so they share the
+    // LARGER operand's panel -- each XCD then streams a few panels of it plus
+    // the whole smaller one (3401x384 A, 1152x384 W: 1.2 MB per XCD instead
+    // of 2.9 MB with W-panel-major order)
+    int tm, tn;
+    if (tiles_m >= tiles_n) {
+      tm = tt / tiles_n;
+      tn = tt - tm * tiles_n;
+    } else {
+      tn = tt / tiles_m;
+      tm = tt - tn * tiles_m;
+    }
     const int m0 = tm * BM, n0 = tn * BN;
 
     f32x16_t acc[2][2];
