@@ -81,3 +81,20 @@ class NodeLabeler:
 
     def controller(self) -> Controller:
         return Controller(f"labeler-{self.node_name}", self).for_kind("Node", MatchingName(self.node_name))
+
+
+def publish_node_metrics(node_name: str, status, smi) -> None:
+    """Prometheus gauges of the north-star measurement: fractional devices per
+    (node, profile) and GPU busy % (amd-smi gfx activity)."""
+    from ..observability import metrics
+
+    per_profile: dict[str, int] = {}
+    for s in status:
+        per_profile[s.profile] = per_profile.get(s.profile, 0) + s.quantity
+    for prof, n in per_profile.items():
+        metrics.SCHEDULABLE_PODS_PER_NODE.labels(node_name, prof).set(n)
+    for g in smi.gpus():
+        try:
+            metrics.GPU_UTIL.labels(node_name, str(g.index)).set(smi.activity(g.index).get("gfx", 0))
+        except Exception:  # activity is best effort (not every backend reports it)
+            pass

@@ -22,10 +22,10 @@ from ..api import constants as C
 from ..gpu import cumask as cm
 from ..gpu.core import devices_as_status_annotations, parse_node_annotations, spec_matches_status, status_equal
 from ..kube import objects as ko
-from ..observability import metrics
+from ..observability import metrics, tracing
 from ..runtime.manager import Controller, Request, Result
 from ..runtime.predicates import AnnotationsChanged, ExcludeDelete, MatchingName, NodeResourcesChanged, or_
-from .devices import NodeDeviceClient
+from .devices import NodeDeviceClient, publish_node_metrics
 
 log = logging.getLogger("nos_amd.agents.gpuagent")
 
@@ -86,6 +86,7 @@ class CuMaskReporter:
             return Result()
         status = self.status_annotations()
         cur_status, spec = parse_node_annotations(node)
+        publish_node_metrics(self.node_name, status, self.smi)
         ann = ko.annotations(node)
         plan = ann.get(C.ANNOTATION_PARTITIONING_PLAN, "")
         reported = ann.get(C.ANNOTATION_REPORTED_PARTITIONING_PLAN, "")
@@ -101,6 +102,8 @@ class CuMaskReporter:
             patch[C.ANNOTATION_REPORTED_PARTITIONING_PLAN] = new_reported
         self.api.patch("Node", self.node_name, {"metadata": {"annotations": patch}})
         self.reports += 1
+        if new_reported != reported:
+            tracing.event("agent.plan_reported", node=self.node_name, plan_id=new_reported, kind="cumask")
         return Result(requeue_after=self.refresh_s)
 
     def controller(self) -> Controller:

@@ -33,7 +33,7 @@ from ..kube import objects as ko
 from ..observability import metrics, tracing
 from ..runtime.manager import Controller, Request, Result
 from ..runtime.predicates import AnnotationsChanged, ExcludeDelete, MatchingName, NodeResourcesChanged, or_
-from .devices import NodeDeviceClient
+from .devices import NodeDeviceClient, publish_node_metrics
 from .shared import SharedState
 
 log = logging.getLogger("nos_amd.agents.partagent")
@@ -137,6 +137,7 @@ class PartitionReporter:
                 return Result()
             status = self.status_annotations()
             cur_status, _ = parse_node_annotations(node)
+            publish_node_metrics(self.node_name, status, self.smi)
             ann = ko.annotations(node)
             modes = {C.ANNOTATION_STATUS_MODE_FORMAT.format(index=g.index): f"{g.compute_mode}/{g.memory_mode}"
                      for g in self.smi.gpus()}
@@ -152,6 +153,8 @@ class PartitionReporter:
                 patch[C.ANNOTATION_REPORTED_PARTITIONING_PLAN] = plan
             self.api.patch("Node", self.node_name, {"metadata": {"annotations": patch}})
             self.reports += 1
+            if plan and ann.get(C.ANNOTATION_REPORTED_PARTITIONING_PLAN, "") != plan:
+                tracing.event("agent.plan_reported", node=self.node_name, plan_id=plan, kind="partition")
             self.shared.on_report_done()
             return Result(requeue_after=self.refresh_s)
 
@@ -166,8 +169,10 @@ class PartitionActuator:
     switch (the reference restarts the device-plugin pod)."""
 
     def __init__(self, api, node_name: str, smi, lister, shared: SharedState, device_plugins=(),
-                 memory_preference: str = "NPS1"):
+                 memory_preference: str = "NPS1", switch_timeout_s: float = 120.0):
         self.api, self.node_name, self.smi = api, node_name, smi
+        self.switch_timeout_s = switch_timeout_s
+        self.failures = 0
         self.devices = NodeDeviceClient(smi, lister)
         self.shared = shared
         self.device_plugins = list(device_plugins)
@@ -203,10 +208,15 @@ class PartitionActuator:
             if self.last_applied_plan == plan and status_equal(self.last_applied_status or [], status):
                 log.info("plan already applied and state unchanged, skipping")
                 return Result()
+            failures = self.failures
             self.apply(plan, plan_id)
+            self.shared.on_apply_done()
+            if self.failures > failures:
+                # do not remember a plan that did not (fully) apply: retry it
+                self.last_applied_plan = None
+                return Result(requeue_after=10.0)
             self.last_applied_plan = plan
             self.last_applied_status = status
-            self.shared.on_apply_done()
             return Result(requeue_after=1.0)
 
     def _mode_mismatch(self, node: dict) -> bool:
@@ -218,21 +228,55 @@ class PartitionActuator:
             for ch in plan.changes:
                 t0 = time.perf_counter()
                 try:
-                    if ch.memory != ch.from_memory:
-                        self.smi.set_memory_partition(ch.gpu_index, ch.memory)
-                    if ch.compute != ch.from_compute:
-                        self.smi.set_compute_partition(ch.gpu_index, ch.compute)
+                    self._switch(ch.gpu_index, ch.compute, ch.memory, ch.from_compute, ch.from_memory)
+                    if not self._verify(ch.gpu_index, ch.compute, ch.memory):
+                        raise RuntimeError("mode did not take effect")
                 except Exception as e:
-                    log.error("node %s gpu %d: switching to %s/%s failed: %s", self.node_name, ch.gpu_index,
-                              ch.compute, ch.memory, e)
+                    log.error("node %s gpu %d: switching to %s/%s failed: %s -- rolling back to %s/%s",
+                              self.node_name, ch.gpu_index, ch.compute, ch.memory, e, ch.from_compute,
+                              ch.from_memory)
+                    self.failures += 1
+                    self._rollback(ch)
                     continue
-                metrics.REPARTITION_DURATION.labels(mode=f"{ch.compute}/{ch.memory}").observe(
-                    time.perf_counter() - t0)
+                dt = time.perf_counter() - t0
+                metrics.REPARTITION_DURATION.labels(mode=f"{ch.compute}/{ch.memory}").observe(dt)
+                if dt > self.switch_timeout_s:
+                    log.warning("node %s gpu %d: mode switch took %.1fs (> %.0fs)", self.node_name, ch.gpu_index,
+                                dt, self.switch_timeout_s)
                 log.info("node %s gpu %d: %s/%s -> %s/%s", self.node_name, ch.gpu_index, ch.from_compute,
                          ch.from_memory, ch.compute, ch.memory)
             self.applies += 1
             for p in self.device_plugins:
                 p.refresh()
+
+    def _switch(self, gpu: int, compute: str, memory: str, from_compute: str, from_memory: str) -> None:
+        if memory != from_memory:
+            self.smi.set_memory_partition(gpu, memory)
+        if compute != from_compute:
+            self.smi.set_compute_partition(gpu, compute)
+
+    def _verify(self, gpu: int, compute: str, memory: str, retries: int = 3, delay_s: float = 0.2) -> bool:
+        """Read the mode back: the driver may report the old mode for a moment
+        after a switch (fault ``stale_mode``) or lose the device."""
+        for i in range(retries):
+            try:
+                g = self.smi.gpu(gpu)
+            except Exception:
+                return False
+            if (g.compute_mode, g.memory_mode) == (compute, memory):
+                return True
+            if i + 1 < retries:
+                time.sleep(delay_s)
+        return False
+
+    def _rollback(self, ch: ModeChange) -> None:
+        """Best effort: put the GPU back in the mode it had, so its old
+        partitions (which the status still advertises) stay valid."""
+        try:
+            g = self.smi.gpu(ch.gpu_index)
+            self._switch(ch.gpu_index, ch.from_compute, ch.from_memory, g.compute_mode, g.memory_mode)
+        except Exception as e:
+            log.error("node %s gpu %d: rollback failed: %s", self.node_name, ch.gpu_index, e)
 
     def controller(self) -> Controller:
         return Controller(f"partagent-actuator-{self.node_name}", self).for_kind(

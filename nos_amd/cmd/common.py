@@ -118,4 +118,4 @@ def manager_for(api, name: str, cfg):
 
     le = cfg.leader_election
     return Manager(api, name, leader_election=le.leader_elect, leader_election_id=le.resource_name or name,
-                   leader_election_namespace=le.resource_namespace)
+                   leader_election_namespace=le.resource_namespace, resync_s=300.0)

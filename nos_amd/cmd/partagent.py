@@ -41,7 +41,8 @@ def build(api, node: str, cfg, smi, lister, device_plugins):
     mgr = common.manager_for(api, f"nos-partagent-{node}", cfg)
     mgr.add(NodeLabeler(api, node, smi).controller())
     mgr.add(PartitionReporter(api, node, smi, lister, shared, cfg.report_config_interval_seconds).controller())
-    mgr.add(PartitionActuator(api, node, smi, lister, shared, device_plugins, cfg.default_memory_mode).controller())
+    mgr.add(PartitionActuator(api, node, smi, lister, shared, device_plugins, cfg.default_memory_mode,
+                              cfg.mode_switch_timeout_seconds).controller())
     return mgr
 
 

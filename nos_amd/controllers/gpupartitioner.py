@@ -147,6 +147,7 @@ class PartitionerController:
         pending = [p for p in self.api.list("Pod", field_selector=f"{C.POD_PHASE_KEY}={ko.PENDING}")
                    if not ko.pod_node(p)]
         pods = [p for p in pending if extra_resources_could_help_scheduling(p) and self._requests_kind(p)]
+        metrics.PENDING_FRACTIONAL_PODS.set(len(pods))
         if not pods:
             return
         with tracing.span("partitioner.plan", kind=self.kind, pods=len(pods)) as sp:

@@ -73,8 +73,12 @@ class FakeSmi:
             if self.procs[i]:
                 raise AmdSmiError(-5, f"gpu {i} busy")
             if self.compute[i] != mode:
+                if "stale_mode" in self.faults:  # the switch silently does not take effect
+                    return
                 self.compute[i] = mode
                 self.switches += 1
+                if "lose_after_switch" in self.faults:
+                    self.lost.add(i)
 
     def set_memory_partition(self, i: int, mode: str) -> None:
         with self._lock:

@@ -71,3 +71,17 @@ def spans(name: str | None = None) -> list[dict]:
 def clear() -> None:
     with _lock:
         _ring.clear()
+
+
+def plan_report_latencies() -> dict[str, float]:
+    """Seconds from each ``partitioner.plan`` span (plan applied) to the first
+    ``agent.plan_reported`` event of that plan id -- the batch -> plan ->
+    apply -> report latency of SURVEY.md 5.1."""
+    with _lock:
+        recs = list(_ring)
+    planned = {r["plan_id"]: r["end"] for r in recs if r["name"] == "partitioner.plan" and r.get("plan_id")}
+    out: dict[str, float] = {}
+    for r in recs:
+        if r["name"] == "agent.plan_reported" and r.get("plan_id") in planned and r["plan_id"] not in out:
+            out[r["plan_id"]] = max(0.0, r["end"] - planned[r["plan_id"]])
+    return out

@@ -24,6 +24,7 @@ from dataclasses import dataclass, field
 from typing import Any, Callable, Protocol
 
 from ..kube import objects as ko
+from ..observability import metrics
 from ..sim.apiserver import ADDED, DELETED, MODIFIED, AlreadyExists, ApiServer, Conflict, NotFound, WatchEvent
 from .predicates import Event, Predicate
 from .workqueue import WorkQueue
@@ -110,11 +111,15 @@ class Controller:
             if res.requeue_after > 0:
                 self.queue.forget(item)
                 self.queue.add_after(item, res.requeue_after)
+                metrics.RECONCILES.labels(self.name, "requeue_after").inc()
             elif res.requeue:
                 self.queue.add_rate_limited(item)
+                metrics.RECONCILES.labels(self.name, "requeue").inc()
             else:
                 self.queue.forget(item)
+                metrics.RECONCILES.labels(self.name, "success").inc()
         except Exception as e:
+            metrics.RECONCILES.labels(self.name, "error").inc()
             self.error_count += 1
             self.last_error = f"{type(e).__name__}: {e}"
             if not isinstance(e, (Conflict, NotFound)):
@@ -174,8 +179,13 @@ class LeaderElector:
 class Manager:
     def __init__(self, api: ApiServer, name: str = "manager", clock=None, leader_election: bool = False,
                  leader_election_id: str | None = None, leader_election_namespace: str = "nos-system",
-                 identity: str | None = None):
+                 identity: str | None = None, resync_s: float | None = None):
         self.api = api
+        # informer resync: re-deliver every watched object periodically, so a
+        # lost watch event (fault injection, broken stream) cannot strand an
+        # object forever (controller-runtime SyncPeriod)
+        self.resync_s = resync_s
+        self._next_resync: float | None = None
         self.name = name
         self.clock = clock or api.clock
         self.controllers: list[Controller] = []
@@ -240,11 +250,20 @@ class Manager:
                 t = threading.Thread(target=self._worker, args=(c,), daemon=True, name=f"{c.name}-{i}")
                 t.start()
                 self._threads.append(t)
+        if self.resync_s:
+            t = threading.Thread(target=self._resync_loop, daemon=True, name=f"{self.name}-resync")
+            t.start()
+            self._threads.append(t)
 
     def _renew_loop(self) -> None:
         while not self._stop.wait(max(0.5, self.elector.duration / 3)):
             if not self._elect():
                 log.error("%s lost leadership", self.name)
+
+    def _resync_loop(self) -> None:
+        while not self._stop.wait(self.resync_s):
+            if self.is_leader:
+                self.resync()
 
     def _worker(self, c: Controller) -> None:
         while not self._stop.is_set():
@@ -268,12 +287,38 @@ class Manager:
             self.elector.release()
 
     # ------------------------------------------------------------ deterministic mode
+    def resync(self) -> int:
+        """Re-enqueue every object of every watch (as update events old == new)."""
+        n = 0
+        for c in self.controllers:
+            for spec in c.watch_specs:
+                try:
+                    objs = self.api.list(spec.kind, spec.namespace, spec.label_selector)
+                except Exception as e:  # an unreachable API server must not kill the loop
+                    log.debug("resync list %s failed: %s", spec.kind, e)
+                    continue
+                for o in objs:
+                    c._handle(spec, WatchEvent(MODIFIED, o, o))
+                    n += 1
+        return n
+
+    def _maybe_resync(self) -> None:
+        if self.resync_s is None:
+            return
+        now = self.clock.monotonic()
+        if self._next_resync is None:
+            self._next_resync = now + self.resync_s
+        elif now >= self._next_resync:
+            self._next_resync = now + self.resync_s
+            self.resync()
+
     def step(self) -> int:
         """Process every item ready now once; returns the number processed."""
         if not self.started:
             self.setup()
         if not self.is_leader and not self._elect():
             return 0
+        self._maybe_resync()
         n = 0
         for c in self.controllers:
             while True:
@@ -288,6 +333,8 @@ class Manager:
 
     def next_wakeup(self) -> float | None:
         ds = [d for c in self.controllers if (d := c.queue.next_delay()) is not None]
+        if self.resync_s is not None and self._next_resync is not None:
+            ds.append(max(0.0, self._next_resync - self.clock.monotonic()))
         return min(ds) if ds else None
 
     def run_until_idle(self, max_time: float = 0.0, max_steps: int = 10000) -> int:

@@ -327,6 +327,34 @@ class Scheduler:
             pass
         self.queue.add_unschedulable(pod)
 
+    def resync(self) -> int:
+        """Informer resync: reconcile the cache and the queue with a fresh
+        list (covers watch events that were lost)."""
+        try:
+            nodes = self.api.list("Node")
+            pods = self.api.list("Pod")
+        except Exception as e:
+            log.debug("scheduler resync failed: %s", e)
+            return 0
+        with self._lock:
+            for n in nodes:
+                self.cache.update_node(n)
+            for name in set(self.cache.nodes) - {ko.name(n) for n in nodes}:
+                self.cache.delete_node({"metadata": {"name": name}})
+            live = set()
+            queued = 0
+            for p in pods:
+                live.add(ko.key(p))
+                if ko.pod_node(p):
+                    if ko.key(p) not in self.cache.assumed:
+                        self.cache.update_pod(p)
+                elif self._responsible(p) and not ko.is_terminated(p):
+                    self.queue.update(p)
+                    queued += 1
+            for k in [k for k in self.cache.pods if k not in live]:
+                self.cache.delete_pod(self.cache.pods[k])
+            return queued
+
     def run_until_idle(self, max_cycles: int = 100000) -> int:
         n = 0
         while n < max_cycles and self.schedule_one():
@@ -334,7 +362,8 @@ class Scheduler:
         now = self.clock.monotonic()
         if now - self._last_flush >= self.flush_interval:
             self._last_flush = now
-            if self.queue.move_all_to_active():
+            self.resync()
+            if self.queue.move_all_to_active() or len(self.queue):
                 n += self.run_until_idle(max_cycles - n)
         return n
 
@@ -353,6 +382,7 @@ class Scheduler:
                     self._stop.wait(0.02)
                     if self.clock.monotonic() - self._last_flush >= self.flush_interval:
                         self._last_flush = self.clock.monotonic()
+                        self.resync()
                         self.queue.move_all_to_active()
 
         self._thread = threading.Thread(target=loop, daemon=True, name="scheduler")

@@ -58,7 +58,9 @@ class SimNode:
 
 class SimCluster:
     def __init__(self, clock=None, partitioner_config: GpuPartitionerConfig | None = None,
-                 memory_gb: int = C.DEFAULT_AMD_GPU_RESOURCE_MEMORY_GB, scheduler_config=None):
+                 memory_gb: int = C.DEFAULT_AMD_GPU_RESOURCE_MEMORY_GB, scheduler_config=None,
+                 resync_s: float | None = None):
+        self.resync_s = resync_s  # informer resync period (None: off, event-driven only)
         self.clock = clock or FakeClock()
         self.api = ApiServer(self.clock)
         v1alpha1.register_types(self.api)
@@ -69,13 +71,13 @@ class SimCluster:
             self.api.create(kf.build_namespace(ns).get())
 
         # ---- operator
-        self.operator = Manager(self.api, "nos-operator", self.clock)
+        self.operator = Manager(self.api, "nos-operator", self.clock, resync_s=resync_s)
         self.operator.add(ElasticQuotaReconciler(self.api, memory_gb).controller())
         self.operator.add(CompositeElasticQuotaReconciler(self.api, memory_gb).controller())
 
         # ---- gpupartitioner
         self.cluster_state = ClusterState()
-        self.partitioner = Manager(self.api, "nos-gpupartitioner", self.clock)
+        self.partitioner = Manager(self.api, "nos-gpupartitioner", self.clock, resync_s=resync_s)
         sched_cfg = scheduler_config or nos_scheduler_config(memory_gb)
         fw = build_framework(sched_cfg.profiles[0], api=self.api)
         amd = amdpart_strategy(self.api, self.clock)
@@ -109,7 +111,7 @@ class SimCluster:
         plugin = NosAmdDevicePlugin(name, smi, mode=kind, cu_policy=self.cu_policy)
         kubelet = Kubelet(self.api, name, [plugin], node_resources=node_resources, runtime=runtime, on_stop=on_stop)
         kubelet.sync_node_status()
-        mgr = Manager(self.api, f"node-{name}", self.clock)
+        mgr = Manager(self.api, f"node-{name}", self.clock, resync_s=self.resync_s)
         mgr.add(kubelet.controller())
         labeler = NodeLabeler(self.api, name, smi)
         mgr.add(labeler.controller())
@@ -182,7 +184,8 @@ class SimCluster:
                 break
             d = self.next_wakeup()
             flush = self.scheduler.flush_interval - (self.clock.monotonic() - self.scheduler._last_flush)
-            cands = [x for x in (d, flush if self.scheduler.queue.unschedulable_count() else None) if x is not None]
+            want_flush = self.scheduler.queue.unschedulable_count() or self.resync_s is not None
+            cands = [x for x in (d, flush if want_flush else None) if x is not None]
             if not cands:
                 break
             dt = max(min(cands), 0) + 1e-3

@@ -156,7 +156,12 @@ class Kubelet:
         if ko.deletion_timestamp(pod) or ko.is_terminated(pod):
             self._teardown(pod)
             return
-        if key in self.containers or phase == ko.RUNNING:
+        if phase == ko.RUNNING:
+            return
+        if key in self.containers:
+            # admitted and started, but the Running status write was lost
+            # (e.g. a 409): write it again -- the status is level-triggered
+            self._set_running(pod, self.containers[key])
             return
         ok, reason, conts = self.admit(pod)
         if not ok:
@@ -168,6 +173,9 @@ class Kubelet:
             return
         if self.runtime is not None:
             self.runtime(pod, conts)
+        self._set_running(pod, conts)
+
+    def _set_running(self, pod: dict, conts: list[RunningContainer]) -> None:
         now = ko.now_rfc3339(self.api.clock.now())
         status = {"phase": ko.RUNNING, "startTime": now, "hostIP": "127.0.0.1",
                   "conditions": [c for c in ko.pod_conditions(pod) if c.get("type") != "Ready"]

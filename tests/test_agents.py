@@ -133,3 +133,35 @@ def test_device_client_maps_uuids_and_labels():
     assert dc.used_gpus() == {1}
     lab = node_labels(smi)
     assert lab[C.LABEL_AMD_COUNT] == "2" and lab[C.LABEL_AMD_PRODUCT] == "AMD-Instinct-MI355X"
+
+
+def test_actuator_rolls_back_a_switch_that_does_not_take_effect():
+    api = _api_with_node({"nos.nebuly.com/spec-gpu-0-1xcd.36gb": "8"})
+    smi = FakeSmi(gpus=1, node="n1")
+    smi.inject("stale_mode")
+    act = PartitionActuator(api, "n1", smi, FakeLister(), SharedState())
+    act._verify = lambda *a, **k: PartitionActuator._verify(act, *a, retries=2, delay_s=0)
+    act.reconcile(Request("n1"))
+    assert act.failures == 1 and smi.compute == ["SPX"]
+    smi.inject("clear")
+
+
+def test_actuator_survives_device_lost_after_switch():
+    api = _api_with_node({"nos.nebuly.com/spec-gpu-0-1xcd.36gb": "8"})
+    smi = FakeSmi(gpus=1, node="n1")
+    smi.inject("lose_after_switch")
+    act = PartitionActuator(api, "n1", smi, FakeLister(), SharedState())
+    act._verify = lambda *a, **k: PartitionActuator._verify(act, *a, retries=1, delay_s=0)
+    act.reconcile(Request("n1"))
+    assert act.failures == 1 and smi.count() == 0  # reported as failed, no crash
+
+
+def test_plan_report_latency_from_spans():
+    from nos_amd.observability import tracing
+
+    tracing.clear()
+    with tracing.span("partitioner.plan", kind="cumask") as s:
+        s.set(plan_id="p9")
+    tracing.event("agent.plan_reported", plan_id="p9", node="n1")
+    lat = tracing.plan_report_latencies()
+    assert set(lat) == {"p9"} and lat["p9"] >= 0
