@@ -100,6 +100,10 @@ def main(argv=None) -> int:
     _lib.require_native_on_gpu()
     dinfo = device_info(local)
     masks, cp = plan(args, world, dinfo["num_cus"])
+    from nos_amd import ops
+
+    # one pod owning the GPU wants latency-shaped GEMM tiles, co-running pods throughput-shaped ones
+    ops.set_gemm_policy("latency" if len(masks) == 1 else "throughput")
     cfg = YolosConfig.small()
     hw = demo_input_hw()
     specs = [TenantSpec(f"pod-{rank}-{i}", m) for i, m in enumerate(masks)]

@@ -34,18 +34,35 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int BM = 128, BK = 64;
 constexpr int NT = 256;
 constexpr int TILE_A_BYTES = BM * BK * 2;  // 16 KiB
-constexpr int TILE_B_BYTES = BN * BK * 2;  // 16 KiB
-constexpr int STAGE_BYTES = TILE_A_BYTES + TILE_B_BYTES;
-constexpr int CT_LD = BN + 4;                        // fp32 C tile row stride (floats)
-constexpr int CT_BYTES = BM * CT_LD * 4;             // 67,584 B
-constexpr int MAIN_BYTES = (2 * STAGE_BYTES > CT_BYTES) ? 2 * STAGE_BYTES : CT_BYTES;
-constexpr int STATS_OFF = MAIN_BYTES;                // mu[128], rstd[128], p1[128], p2[128]
-constexpr int LDS_BYTES = MAIN_BYTES + 4 * BM * 4;
+
+// BN (128 or 64) is a template parameter: N = 384 projections have only 81
+// 128x128 tiles for 256 CUs, 162 with 128x64 tiles.
+template <int BN>
+struct Cfg {
+  static constexpr int TILE_B_BYTES = BN * BK * 2;
+  static constexpr int STAGE_BYTES = TILE_A_BYTES + TILE_B_BYTES;
+  static constexpr int CT_LD = BN + 4;                 // fp32 C tile row stride (floats)
+  static constexpr int CT_BYTES = BM * CT_LD * 4;      // 67,584 B (BN 128) / 34,816 B (BN 64)
+  static constexpr int MAIN_BYTES = (2 * STAGE_BYTES > CT_BYTES) ? 2 * STAGE_BYTES : CT_BYTES;
+  static constexpr int STATS_OFF = MAIN_BYTES;         // mu[BM], rstd[BM], p1[BN], p2[BN]
+  static constexpr int LDS_BYTES = MAIN_BYTES + (2 * BM + 2 * BN) * 4;
+  static constexpr int WN = BN / 2;                    // wave tile: 64 x WN (2x2 waves)
+  static constexpr int NB = WN / 32;                   // 32-column MFMA blocks per wave
+};
 
 enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
+// Tile policy (process-wide, nos_gemm_set_policy):
+//  * 0 = throughput (default): always 128x128 tiles -- fewest bytes per FLOP;
+//    what fractional pods sharing a GPU want (measured: 8 co-running YOLOS
+//    pods lose ~4 % aggregate throughput with narrow tiles);
+//  * 1 = latency: when a GEMM has fewer 128x128 tiles than NARROW_TILES, use
+//    128x64 tiles to occupy twice the CUs (single tenant: N = 384 projections
+//    -24 %, FC2 -23 % kernel time).
+constexpr int NARROW_TILES = 200;
+int g_tile_policy = 0;
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
@@ -53,12 +70,14 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_ba
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// Stage a [128 rows][64 k] bf16 tile: 16 wave-instructions, 4 per wave.
+// Stage a [ROWS][64 k] bf16 tile: ROWS/8 wave-instructions, ROWS/32 per wave.
+template <int ROWS>
 __device__ __forceinline__ void stage_tile(const unsigned short* __restrict__ src, int ld, int row0,
                                            int nrows, int k0, unsigned char* tile, int wid, int lane) {
+  constexpr int PER_WAVE = ROWS / 32;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int R = (wid * 4 + i) * 8;
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int R = (wid * PER_WAVE + i) * 8;
     const int row = R + (lane >> 3);
     const int pc = lane & 7;
     const int lc = pc ^ swz(row);
@@ -84,14 +103,17 @@ __device__ __forceinline__ float erf_fast(float x) {
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
 
-template <bool LN>
+template <bool LN, int BN>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
     const unsigned short* __restrict__ A, int lda, const unsigned short* __restrict__ W, int ldw,
     const unsigned short* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
     const unsigned short* __restrict__ R, int ldr, unsigned short* __restrict__ C, int ldc, int M, int N,
     int K, int epi, float eps, int tiles_m, int tiles_n) {
+  using CF = Cfg<BN>;
+  constexpr int TILE_B_BYTES = CF::TILE_B_BYTES, STAGE_BYTES = CF::STAGE_BYTES, CT_LD = CF::CT_LD;
+  constexpr int WN = CF::WN, NB = CF::NB;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* s_mu = reinterpret_cast<float*>(smem + STATS_OFF);
+  float* s_mu = reinterpret_cast<float*>(smem + CF::STATS_OFF);
   float* s_rstd = s_mu + BM;
   float* s_p1 = s_rstd + BM;
   float* s_p2 = s_p1 + BN;
@@ -117,11 +139,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
     }
     const int m0 = tm * BM, n0 = tn * BN;
 
-    f32x16_t acc[2][2];
+    f32x16_t acc[2][NB];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < NB; ++b)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
 
@@ -129,16 +151,16 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
     const int srow = tid >> 1, shalf = tid & 1;
     float sshift = 0.f, ssum = 0.f, ssq = 0.f;
 
-    stage_tile(A, lda, m0, M, 0, smem, wid, lane);
-    stage_tile(W, ldw, n0, N, 0, smem + TILE_A_BYTES, wid, lane);
+    stage_tile<BM>(A, lda, m0, M, 0, smem, wid, lane);
+    stage_tile<BN>(W, ldw, n0, N, 0, smem + TILE_A_BYTES, wid, lane);
     __syncthreads();  // drains the DMA (vmcnt(0)) and publishes the tile
 
     for (int kt = 0; kt < nk; ++kt) {
       unsigned char* cur = smem + (kt & 1) * STAGE_BYTES;
       if (kt + 1 < nk) {
         unsigned char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
-        stage_tile(A, lda, m0, M, (kt + 1) * BK, nxt, wid, lane);
-        stage_tile(W, ldw, n0, N, (kt + 1) * BK, nxt + TILE_A_BYTES, wid, lane);
+        stage_tile<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wid, lane);
+        stage_tile<BN>(W, ldw, n0, N, (kt + 1) * BK, nxt + TILE_A_BYTES, wid, lane);
       }
       const unsigned char* ta = cur;
       const unsigned char* tb = cur + TILE_A_BYTES;
@@ -158,21 +180,21 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
       }
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
-        bf16x8_t af[2], bf[2];
+        bf16x8_t af[2], bf[NB];
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi) {
           const int row = wm * 64 + mi * 32 + r;
           af[mi] = *reinterpret_cast<const bf16x8_t*>(ta + row * 128 + (((2 * ks + hh) ^ swz(row)) << 4));
         }
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          const int row = wn * 64 + ni * 32 + r;
+        for (int ni = 0; ni < NB; ++ni) {
+          const int row = wn * WN + ni * 32 + r;
           bf[ni] = *reinterpret_cast<const bf16x8_t*>(tb + row * 128 + (((2 * ks + hh) ^ swz(row)) << 4));
         }
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
+          for (int ni = 0; ni < NB; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
       }
       __syncthreads();  // next tile landed; everyone done with `cur`
@@ -201,8 +223,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
     // ---- epilogue stage 1: raw accumulators -> fp32 LDS tile
     float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      const int cl = wn * 64 + ni * 32 + r;
+    for (int ni = 0; ni < NB; ++ni) {
+      const int cl = wn * WN + ni * 32 + r;
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -224,8 +246,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
     // correction, activation, residual, coalesced 16-byte bf16 store
 #pragma unroll 2
     for (int it = 0; it < (BM * BN / 8) / NT; ++it) {
+      constexpr int CHUNKS = BN / 8;  // 16-byte chunks per tile row
       const int c = tid + NT * it;
-      const int rl = c >> 4, ch = c & 15;
+      const int rl = c / CHUNKS, ch = c % CHUNKS;
       const int m = m0 + rl, n = n0 + ch * 8;
       if (m >= M || n >= N) continue;
       const float4 lo = *reinterpret_cast<const float4*>(ct + rl * CT_LD + ch * 8);
@@ -286,7 +309,11 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
   if (!ln && (epi & EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
   if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
   if ((epi & EPI_RESID) && !R) return (int)hipErrorInvalidValue;
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  // fewer 128-wide tiles than CUs (e.g. N = 384 projections): halve the N tile
+  const bool narrow = g_tile_policy == 1 && tiles_m * ((N + 127) / 128) < NARROW_TILES;
+  const int bn = narrow ? 64 : 128;
+  const int tiles_n = (N + bn - 1) / bn;
   int nwg = tiles_m * tiles_n;
   if (max_wg > 0 && nwg > max_wg) nwg = max_wg;
   auto Ap = (const unsigned short*)A;
@@ -294,12 +321,15 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
   auto Bp = (const unsigned short*)bias;
   auto Rp = (const unsigned short*)R;
   auto Cp = (unsigned short*)C;
-  if (ln)
-    hipLaunchKernelGGL(gemm_bf16_kernel<true>, dim3(nwg), dim3(NT), LDS_BYTES, stream, Ap, lda, Wp, ldw, Bp, c1,
-                       c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
-  else
-    hipLaunchKernelGGL(gemm_bf16_kernel<false>, dim3(nwg), dim3(NT), LDS_BYTES, stream, Ap, lda, Wp, ldw, Bp,
-                       c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+#define NOS_GEMM_LAUNCH(LNV, BNV)                                                                              \
+  hipLaunchKernelGGL((gemm_bf16_kernel<LNV, BNV>), dim3(nwg), dim3(NT), Cfg<BNV>::LDS_BYTES, stream, Ap, lda, \
+                     Wp, ldw, Bp, c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n)
+  if (ln) {
+    if (narrow) NOS_GEMM_LAUNCH(true, 64); else NOS_GEMM_LAUNCH(true, 128);
+  } else {
+    if (narrow) NOS_GEMM_LAUNCH(false, 64); else NOS_GEMM_LAUNCH(false, 128);
+  }
+#undef NOS_GEMM_LAUNCH
   return (int)hipGetLastError();
 }
 
@@ -308,6 +338,12 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
 // C = act(A . W^T + bias) (+ R).  A [M,K] (row stride lda), W [N,K] (ldw),
 // R/C [M,N] (ldr/ldc), all bf16.  K must be a multiple of 64 and every row
 // start 16-byte aligned.  max_wg > 0 caps the grid (persistent mode).
+NOS_API int nos_gemm_set_policy(int policy) {
+  if (policy != 0 && policy != 1) return (int)hipErrorInvalidValue;
+  g_tile_policy = policy;
+  return 0;
+}
+
 NOS_API int nos_gemm_bf16(const void* A, int lda, const void* W, int ldw, const void* bias, const void* R,
                           int ldr, void* C, int ldc, int M, int N, int K, int epi, int max_wg,
                           hipStream_t stream) {

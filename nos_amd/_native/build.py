@@ -73,14 +73,20 @@ def hipcc() -> str:
     return found
 
 
-def build_hip(force: bool = False, jobs: int = 8, verbose: bool = False) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
-    hdr = [CSRC / "hip" / "common.h"]
+def build_hip(force: bool = False, jobs: int = 8, verbose: bool = False, src_dir: Path | None = None,
+              out: Path | None = None, build_dir: Path | None = None) -> Path:
+    """``src_dir``/``out``/``build_dir`` build an experimental variant of the
+    kernels (tools/build_variant.py) without touching the in-tree library."""
+    src_dir = Path(src_dir) if src_dir else CSRC / "hip"
+    out_lib = Path(out) if out else HIP_LIB
+    bdir = Path(build_dir) if build_dir else BUILD
+    bdir.mkdir(parents=True, exist_ok=True)
+    hdr = [src_dir / "common.h"]
     objs: list[Path] = []
     todo: list[tuple[Path, Path]] = []
     for s in HIP_SOURCES:
-        src = CSRC / "hip" / s
-        obj = BUILD / (s + ".o")
+        src = src_dir / s
+        obj = bdir / (s + ".o")
         objs.append(obj)
         if force or _stale(obj, [src, *hdr]):
             todo.append((src, obj))
@@ -88,21 +94,21 @@ def build_hip(force: bool = False, jobs: int = 8, verbose: bool = False) -> Path
     def compile_one(pair: tuple[Path, Path]) -> None:
         src, obj = pair
         _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
-              "-Wno-unused-result", "-I", str(CSRC / "hip"), "-c", str(src), "-o", str(obj)], verbose)
+              "-Wno-unused-result", "-I", str(src_dir), "-c", str(src), "-o", str(obj)], verbose)
 
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
             list(ex.map(compile_one, todo))
-    if force or todo or _stale(HIP_LIB, objs):
+    if force or todo or _stale(out_lib, objs):
         tl = _torch_lib_dir()
-        link = ["g++", "-shared", "-fPIC", "-o", str(HIP_LIB), *map(str, objs)]
+        link = ["g++", "-shared", "-fPIC", "-o", str(out_lib), *map(str, objs)]
         if tl is not None:
             # bind to torch's own HIP runtime (same process-wide context)
             link += [f"-L{tl}", "-l:libamdhip64.so", f"-Wl,-rpath,{tl}"]
         else:
             link += [f"-L{ROCM / 'lib'}", "-lamdhip64", f"-Wl,-rpath,{ROCM / 'lib'}"]
         _run(link, verbose)
-    return HIP_LIB
+    return out_lib
 
 
 def build_amdsmi(force: bool = False, verbose: bool = False, sanitize: str | None = None) -> Path:

@@ -93,6 +93,14 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
 
 
 @torch.no_grad()
+def set_gemm_policy(policy: str) -> None:
+    """``"throughput"`` (default: 128x128 tiles, best when pods share a GPU) or
+    ``"latency"`` (128x64 tiles for GEMMs with fewer tiles than CUs, best for
+    a single tenant owning the GPU)."""
+    code = {"throughput": 0, "latency": 1}[policy]
+    _lib.check(_lib.lib().nos_gemm_set_policy(code), "nos_gemm_set_policy")
+
+
 def fold_layernorm(weight: torch.Tensor, bias: torch.Tensor | None, gamma: torch.Tensor, beta: torch.Tensor
                    ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Fold LayerNorm(gamma, beta) into the following linear layer.
@@ -212,5 +220,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_gemm_policy", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

@@ -13,7 +13,9 @@ import os
 import threading
 from pathlib import Path
 
-_LIB_PATH = Path(__file__).resolve().parent.parent / "_native" / "libnos_hip.so"
+# NOS_AMD_HIP_LIB: load an experimental kernel variant (tools/build_variant.py) instead
+_LIB_PATH = Path(os.environ.get("NOS_AMD_HIP_LIB") or
+                 Path(__file__).resolve().parent.parent / "_native" / "libnos_hip.so")
 _lock = threading.Lock()
 _lib: ctypes.CDLL | None = None
 _err: str | None = None
@@ -26,6 +28,7 @@ _SIGS = {
                          c_ll, c_int, c_ll, c_float, c_void_p],
     "nos_gemm_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nos_gemm_set_policy": [c_int],
     "nos_gemm_ln_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_int, c_int, c_float, c_int, c_void_p],
     "nos_layernorm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,

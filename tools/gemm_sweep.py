@@ -16,17 +16,8 @@ import torch  # noqa: E402
 from nos_amd import ops  # noqa: E402
 
 
-def timeit(fn, iters=100):
-    for _ in range(5):
-        fn()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters * 1e3
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from kernel_bench import timeit  # noqa: E402  (HIP-graph timing: no host launch overhead)
 
 
 def main():

@@ -17,16 +17,28 @@ from nos_amd import ops  # noqa: E402
 
 
 def timeit(fn, iters):
-    for _ in range(3):
-        fn()
+    """GPU time per call: `iters` calls captured in one HIP graph and replayed,
+    so host launch overhead (~10 us per eager ctypes/torch call) is excluded
+    -- this is how the tenants run (graph replay per pod)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters * 1e3  # us
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    g.replay()
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / iters * 1e3  # us
 
 
 def main():
