@@ -92,7 +92,6 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     return out.reshape(*x.shape[:-1], N)
 
 
-@torch.no_grad()
 def set_gemm_policy(policy: str) -> None:
     """``"throughput"`` (default: 128x128 tiles, best when pods share a GPU) or
     ``"latency"`` (128x64 tiles for GEMMs with fewer tiles than CUs, best for
@@ -101,6 +100,7 @@ def set_gemm_policy(policy: str) -> None:
     _lib.check(_lib.lib().nos_gemm_set_policy(code), "nos_gemm_set_policy")
 
 
+@torch.no_grad()
 def fold_layernorm(weight: torch.Tensor, bias: torch.Tensor | None, gamma: torch.Tensor, beta: torch.Tensor
                    ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Fold LayerNorm(gamma, beta) into the following linear layer.
