@@ -38,6 +38,7 @@ class Batcher(Generic[T]):
         if self.running:
             raise RuntimeError("batcher already started")
         self.running = True
+        self._stop.clear()  # a stopped batcher can be started again
         self.reset()
         if threaded:
             def loop():
