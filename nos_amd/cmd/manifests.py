@@ -10,11 +10,22 @@ agent on ``gpu-partitioning=partition`` nodes, gpuagent and device plugin on
 PodResources socket and the device-plugin directory.  RBAC follows the
 controller-gen markers of the reference controllers.
 
-python -m nos_amd.cmd.manifests --out config      (check: --check)
+Deployment knobs come from a Helm-style values tree (``DEFAULT_VALUES``;
+the reference's ``helm-charts/nos/values.yaml`` keys with AMD names), so a
+user can render a customised install without Helm:
+
+    python -m nos_amd.cmd.manifests --out config                 (defaults; --check)
+    python -m nos_amd.cmd.manifests --values my.yaml --set gpuPartitioner.cuPolicy=shared --stdout
+    python -m nos_amd.cmd.manifests --dump-values > values.yaml
+
+Like the chart's ``templates/validation.yaml`` the ``default`` namespace is
+refused; ``shareTelemetry: true`` adds the metrics-exporter post-install Job
+(``templates/pod_metrics-exporter.yaml``), off by default.
 """
 from __future__ import annotations
 
 import argparse
+import copy
 import sys
 from pathlib import Path
 
@@ -24,6 +35,82 @@ from ..api import constants as C
 from ..api import v1alpha1
 
 NS = "nos-system"
+
+DEFAULT_VALUES: dict = {
+    "namespace": NS,
+    "amdGpuResourceMemoryGB": C.DEFAULT_AMD_GPU_RESOURCE_MEMORY_GB,
+    "leaderElection": True,
+    "logLevel": "info",
+    "shareTelemetry": False,
+    "telemetryEndpoint": "",
+    "image": {"repository": "ghcr.io/nos-amd/nos-amd", "tag": "0.1.0"},
+    "rocmImage": {"repository": "ghcr.io/nos-amd/nos-amd-rocm", "tag": "0.1.0"},
+    "operator": {"enabled": True, "webhook": {"enabled": True}},
+    "scheduler": {"enabled": True, "schedulerName": "nos-scheduler"},
+    "gpuPartitioner": {
+        "enabled": True,
+        "batchWindowTimeoutSeconds": 60,
+        "batchWindowIdleSeconds": 10,
+        "devicePluginDelaySeconds": 5,
+        "planReportTimeoutSeconds": 300,
+        "slicePlacement": "pack",
+        "cuPolicy": "even",
+        "knownPartitionGeometries": None,  # list override of the built-in MI355X table
+        "partitionAgent": {"enabled": True, "reportConfigIntervalSeconds": 10, "allowModeChanges": True,
+                           "defaultComputeMode": "SPX", "defaultMemoryMode": "NPS1"},
+        "gpuAgent": {"enabled": True, "reportConfigIntervalSeconds": 10, "probeEnabled": True},
+        "devicePlugin": {"enabled": True},
+    },
+}
+
+_V: dict = DEFAULT_VALUES  # values of the render in progress (set by render())
+
+
+def _ns() -> str:
+    return _V["namespace"]
+
+
+def _img(key: str) -> str:
+    return f"{_V[key]['repository']}:{_V[key]['tag']}"
+
+
+def merge_values(base: dict, override: dict) -> dict:
+    """Deep merge (Helm semantics: maps merge, everything else replaces)."""
+    out = copy.deepcopy(base)
+    for k, v in (override or {}).items():
+        if isinstance(v, dict) and isinstance(out.get(k), dict):
+            out[k] = merge_values(out[k], v)
+        else:
+            out[k] = copy.deepcopy(v)
+    return out
+
+
+def apply_set(values: dict, expr: str) -> dict:
+    """``--set a.b.c=value`` (value parsed as YAML: numbers, booleans, lists)."""
+    path, _, raw = expr.partition("=")
+    if not path or not _:
+        raise ValueError(f"--set expects key=value, got {expr!r}")
+    node: dict = {}
+    cur = node
+    keys = path.split(".")
+    for k in keys[:-1]:
+        cur = cur.setdefault(k, {})
+    cur[keys[-1]] = yaml.safe_load(raw) if raw != "" else ""
+    return merge_values(values, node)
+
+
+def validate_values(v: dict) -> None:
+    if v["namespace"] in ("", "default"):
+        raise ValueError("nos-amd must not be installed in the 'default' namespace")
+    gp = v["gpuPartitioner"]
+    if gp["batchWindowTimeoutSeconds"] <= 0 or gp["batchWindowIdleSeconds"] <= 0:
+        raise ValueError("gpuPartitioner batch windows must be > 0")
+    if gp["slicePlacement"] not in ("pack", "spread"):
+        raise ValueError("gpuPartitioner.slicePlacement must be pack|spread")
+    if gp["cuPolicy"] not in ("even", "proportional", "shared"):
+        raise ValueError("gpuPartitioner.cuPolicy must be even|proportional|shared")
+    if int(v["amdGpuResourceMemoryGB"]) <= 0:
+        raise ValueError("amdGpuResourceMemoryGB must be > 0")
 
 
 class _Dumper(yaml.SafeDumper):
@@ -38,12 +125,11 @@ def _dump(o) -> str:
     return yaml.dump(o, Dumper=_Dumper, sort_keys=False)
 
 
-IMAGE = "ghcr.io/nos-amd/nos-amd:0.1.0"
-IMAGE_ROCM = "ghcr.io/nos-amd/nos-amd-rocm:0.1.0"  # rocm/pytorch base for the GPU-side DaemonSets
+IMAGE, IMAGE_ROCM = "image", "rocmImage"  # value keys; rocm/pytorch base for the GPU-side DaemonSets
 
 
 def _sa(name: str) -> dict:
-    return {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": name, "namespace": NS}}
+    return {"apiVersion": "v1", "kind": "ServiceAccount", "metadata": {"name": name, "namespace": _ns()}}
 
 
 def _cluster_role(name: str, rules: list[dict]) -> list[dict]:
@@ -51,7 +137,7 @@ def _cluster_role(name: str, rules: list[dict]) -> list[dict]:
              "rules": rules},
             {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRoleBinding", "metadata": {"name": name},
              "roleRef": {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole", "name": name},
-             "subjects": [{"kind": "ServiceAccount", "name": name, "namespace": NS}]}]
+             "subjects": [{"kind": "ServiceAccount", "name": name, "namespace": _ns()}]}]
 
 
 def _rule(groups, resources, verbs) -> dict:
@@ -65,7 +151,7 @@ EVENTS = _rule([""], ["events"], ["create", "patch"])
 
 
 def _config_map(name: str, files: dict[str, str]) -> dict:
-    return {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": name, "namespace": NS}, "data": files}
+    return {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": name, "namespace": _ns()}, "data": files}
 
 
 def _probes() -> dict:
@@ -77,7 +163,8 @@ def _probes() -> dict:
 
 def _container(name: str, module: str, args: list[str], image: str = IMAGE, env: dict | None = None,
                mounts: list[dict] | None = None, privileged: bool = False, probes: bool = True) -> dict:
-    c = {"name": name, "image": image, "command": ["python", "-m", module], "args": args,
+    c = {"name": name, "image": _img(image), "command": ["python", "-m", module],
+         "args": args + ["--log-level", _V["logLevel"]],
          "resources": {"requests": {"cpu": "100m", "memory": "128Mi"}, "limits": {"memory": "1Gi"}},
          "volumeMounts": mounts or []}
     if env:
@@ -93,7 +180,7 @@ def _container(name: str, module: str, args: list[str], image: str = IMAGE, env:
 
 def _deployment(name: str, container: dict, volumes: list[dict]) -> dict:
     return {"apiVersion": "apps/v1", "kind": "Deployment",
-            "metadata": {"name": name, "namespace": NS, "labels": {"app": name}},
+            "metadata": {"name": name, "namespace": _ns(), "labels": {"app": name}},
             "spec": {"replicas": 1, "selector": {"matchLabels": {"app": name}},
                      "template": {"metadata": {"labels": {"app": name}},
                                   "spec": {"serviceAccountName": name, "containers": [container],
@@ -117,7 +204,7 @@ HOST_MOUNTS = [
 
 def _daemonset(name: str, container: dict, kind: str, volumes: list[dict]) -> dict:
     return {"apiVersion": "apps/v1", "kind": "DaemonSet",
-            "metadata": {"name": name, "namespace": NS, "labels": {"app": name}},
+            "metadata": {"name": name, "namespace": _ns(), "labels": {"app": name}},
             "spec": {"selector": {"matchLabels": {"app": name}},
                      "template": {"metadata": {"labels": {"app": name}},
                                   "spec": {"serviceAccountName": name, "containers": [container],
@@ -151,23 +238,24 @@ def operator() -> dict[str, list[dict]]:
     vol, mnt = _cfg_mount(name + "-config")
     certs = {"name": "cert", "secret": {"secretName": "nos-amd-webhook-server-cert"}}
     c = _container("manager", "nos_amd.cmd.operator",
-                   ["--config", "/etc/nos-amd/operator_config.yaml", "--webhook-port", "9443",
-                    "--webhook-cert-dir", "/tmp/k8s-webhook-server/serving-certs"],
+                   ["--config", "/etc/nos-amd/operator_config.yaml"] +
+                   (["--webhook-port", "9443", "--webhook-cert-dir", "/tmp/k8s-webhook-server/serving-certs"]
+                    if _V["operator"]["webhook"]["enabled"] else []),
                    mounts=[mnt, {"name": "cert", "mountPath": "/tmp/k8s-webhook-server/serving-certs",
                                  "readOnly": True}])
     c["ports"] = [{"containerPort": 9443, "name": "webhook-server"}]
     cfg = {"apiVersion": C.CONFIG_API_VERSION, "kind": "OperatorConfig",
            "health": {"healthProbeBindAddress": ":8081"}, "metrics": {"bindAddress": "127.0.0.1:8080"},
-           "leaderElection": {"leaderElect": True, "resourceName": "nos-amd-operator"},
-           "amdGpuResourceMemoryGB": C.DEFAULT_AMD_GPU_RESOURCE_MEMORY_GB}
-    svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "nos-amd-webhook-service", "namespace": NS},
+           "leaderElection": {"leaderElect": _V["leaderElection"], "resourceName": "nos-amd-operator"},
+           "amdGpuResourceMemoryGB": _V["amdGpuResourceMemoryGB"]}
+    svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "nos-amd-webhook-service", "namespace": _ns()},
            "spec": {"selector": {"app": name}, "ports": [{"port": 443, "targetPort": 9443}]}}
 
     def hook(kind: str, path: str, ops: list[str]) -> dict:
         plural = kind.lower() + "s"
         return {"name": f"v{kind.lower()}.kb.io", "admissionReviewVersions": ["v1"], "sideEffects": "None",
                 "failurePolicy": "Fail",
-                "clientConfig": {"service": {"name": "nos-amd-webhook-service", "namespace": NS, "path": path}},
+                "clientConfig": {"service": {"name": "nos-amd-webhook-service", "namespace": _ns(), "path": path}},
                 "rules": [{"apiGroups": [C.GROUP], "apiVersions": [C.VERSION], "operations": ops,
                            "resources": [plural]}]}
 
@@ -175,17 +263,19 @@ def operator() -> dict[str, list[dict]]:
 
     vwc = {"apiVersion": "admissionregistration.k8s.io/v1", "kind": "ValidatingWebhookConfiguration",
            "metadata": {"name": "nos-amd-validating-webhook-configuration",
-                        "annotations": {"cert-manager.io/inject-ca-from": f"{NS}/nos-amd-serving-cert"}},
+                        "annotations": {"cert-manager.io/inject-ca-from": f"{_ns()}/nos-amd-serving-cert"}},
            "webhooks": [hook("ElasticQuota", EQ_PATH, ["CREATE", "UPDATE"]),
                         hook("CompositeElasticQuota", CEQ_PATH, ["CREATE", "UPDATE"])]}
     rules = [_rule([C.GROUP], ["elasticquotas", "compositeelasticquotas"], RW),
              _rule([C.GROUP], ["elasticquotas/status", "compositeelasticquotas/status"], ["get", "update", "patch"]),
              _rule([""], ["pods"], ["get", "list", "watch", "patch", "update"]), LEASES, EVENTS]
-    return {"operator/manager.yaml": [_sa(name), _config_map(name + "-config",
-                                                             {"operator_config.yaml": yaml.safe_dump(cfg)}),
-                                      _deployment(name, c, [vol, certs])],
-            "operator/rbac.yaml": _cluster_role(name, rules),
-            "operator/webhook.yaml": [svc, vwc]}
+    out = {"operator/manager.yaml": [_sa(name), _config_map(name + "-config",
+                                                            {"operator_config.yaml": yaml.safe_dump(cfg)}),
+                                     _deployment(name, c, [vol, certs])],
+           "operator/rbac.yaml": _cluster_role(name, rules)}
+    if _V["operator"]["webhook"]["enabled"]:
+        out["operator/webhook.yaml"] = [svc, vwc]
+    return out
 
 
 def scheduler() -> dict[str, list[dict]]:
@@ -193,13 +283,13 @@ def scheduler() -> dict[str, list[dict]]:
     vol, mnt = _cfg_mount(name + "-config")
     sched_cfg = {"apiVersion": "kubescheduler.config.k8s.io/v1", "kind": "KubeSchedulerConfiguration",
                  "leaderElection": {"leaderElect": False},
-                 "profiles": [{"schedulerName": "nos-scheduler",
+                 "profiles": [{"schedulerName": _V["scheduler"]["schedulerName"],
                                "plugins": {"preFilter": {"enabled": [{"name": "CapacityScheduling"}]},
                                            "postFilter": {"enabled": [{"name": "CapacityScheduling"}],
                                                           "disabled": [{"name": "*"}]},
                                            "reserve": {"enabled": [{"name": "CapacityScheduling"}]}},
                                "pluginConfig": [{"name": "CapacityScheduling", "args": {
-                                   "amdGpuResourceMemoryGB": C.DEFAULT_AMD_GPU_RESOURCE_MEMORY_GB}}]}]}
+                                   "amdGpuResourceMemoryGB": _V["amdGpuResourceMemoryGB"]}}]}]}
     c = _container("scheduler", "nos_amd.cmd.scheduler", ["--config", "/etc/nos-amd/scheduler_config.yaml",
                                                           "--health-probe-bind-address", ":8081"], mounts=[mnt])
     rules = [_rule([""], ["pods"], RO + ["patch", "update", "delete"]), _rule([""], ["pods/binding"], ["create"]),
@@ -215,6 +305,8 @@ def scheduler() -> dict[str, list[dict]]:
 def known_geometries_yaml() -> str:
     from ..gpu.amdpart import mi355x_geometries
 
+    if _V["gpuPartitioner"].get("knownPartitionGeometries"):
+        return yaml.safe_dump(_V["gpuPartitioner"]["knownPartitionGeometries"], sort_keys=False)
     gs = [{"compute": g.compute, "memory": g.memory, "profiles": {str(p): n for p, n in g.geometry.items()}}
           for g in mi355x_geometries()]
     return yaml.safe_dump([{"models": ["AMD-Instinct-MI355X", "AMD Instinct MI355X", "MI355X"],
@@ -223,17 +315,20 @@ def known_geometries_yaml() -> str:
 
 def gpupartitioner() -> dict[str, list[dict]]:
     name = "nos-amd-gpupartitioner"
+    gp = _V["gpuPartitioner"]
     vol, mnt = _cfg_mount(name + "-config")
     cfg = {"apiVersion": C.CONFIG_API_VERSION, "kind": "GpuPartitionerConfig",
            "health": {"healthProbeBindAddress": ":8081"}, "metrics": {"bindAddress": "127.0.0.1:8080"},
-           "leaderElection": {"leaderElect": True, "resourceName": "nos-amd-gpupartitioner"},
+           "leaderElection": {"leaderElect": _V["leaderElection"], "resourceName": "nos-amd-gpupartitioner"},
            "schedulerConfigFile": "/etc/nos-amd/scheduler_config.yaml",
            "knownPartitionGeometriesFile": "/etc/nos-amd/known_partition_geometries.yaml",
-           "batchWindowTimeoutSeconds": 60, "batchWindowIdleSeconds": 10,
-           "devicePluginConfigMap": {"name": C.DEFAULT_DEVICE_PLUGIN_CM_NAME, "namespace": NS},
-           "devicePluginDelaySeconds": 5, "planReportTimeoutSeconds": 300,
-           "amdGpuResourceMemoryGB": C.DEFAULT_AMD_GPU_RESOURCE_MEMORY_GB,
-           "slicePlacement": "pack", "cuPolicy": "even"}
+           "batchWindowTimeoutSeconds": gp["batchWindowTimeoutSeconds"],
+           "batchWindowIdleSeconds": gp["batchWindowIdleSeconds"],
+           "devicePluginConfigMap": {"name": C.DEFAULT_DEVICE_PLUGIN_CM_NAME, "namespace": _ns()},
+           "devicePluginDelaySeconds": gp["devicePluginDelaySeconds"],
+           "planReportTimeoutSeconds": gp["planReportTimeoutSeconds"],
+           "amdGpuResourceMemoryGB": _V["amdGpuResourceMemoryGB"],
+           "slicePlacement": gp["slicePlacement"], "cuPolicy": gp["cuPolicy"]}
     sched = scheduler()["scheduler/deployment.yaml"][1]["data"]["scheduler_config.yaml"]
     c = _container("manager", "nos_amd.cmd.gpupartitioner", ["--config", "/etc/nos-amd/gpu_partitioner_config.yaml"],
                    mounts=[mnt])
@@ -241,7 +336,7 @@ def gpupartitioner() -> dict[str, list[dict]]:
              _rule([""], ["configmaps"], RW), _rule([C.GROUP], ["elasticquotas", "compositeelasticquotas"], RO),
              _rule(["policy"], ["poddisruptionbudgets"], RO), LEASES, EVENTS]
     cm = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": C.DEFAULT_DEVICE_PLUGIN_CM_NAME,
-                                                                  "namespace": NS}, "data": {}}
+                                                                  "namespace": _ns()}, "data": {}}
     return {"gpupartitioner/manager.yaml": [
         _sa(name), _config_map(name + "-config", {"gpu_partitioner_config.yaml": yaml.safe_dump(cfg),
                                                   "scheduler_config.yaml": sched,
@@ -252,37 +347,44 @@ def gpupartitioner() -> dict[str, list[dict]]:
 
 def node_agents() -> dict[str, list[dict]]:
     out: dict[str, list[dict]] = {}
+    gp = _V["gpuPartitioner"]
+    pa, ga = gp["partitionAgent"], gp["gpuAgent"]
     node_rules = [_rule([""], ["nodes"], RO + ["patch", "update"]), _rule([""], ["pods"], RO + ["delete"]),
                   _rule([""], ["configmaps"], RO), EVENTS]
     # partition agent (migagent analogue)
     name = "nos-amd-partagent"
     vol, mnt = _cfg_mount(name + "-config")
     cfg = {"apiVersion": C.CONFIG_API_VERSION, "kind": "PartitionAgentConfig",
-           "health": {"healthProbeBindAddress": ":8081"}, "reportConfigIntervalSeconds": 10,
-           "allowModeChanges": True, "defaultComputeMode": "SPX", "defaultMemoryMode": "NPS1"}
+           "health": {"healthProbeBindAddress": ":8081"},
+           "reportConfigIntervalSeconds": pa["reportConfigIntervalSeconds"],
+           "allowModeChanges": pa["allowModeChanges"], "defaultComputeMode": pa["defaultComputeMode"],
+           "defaultMemoryMode": pa["defaultMemoryMode"]}
     c = _container("partagent", "nos_amd.cmd.partagent", ["--config", "/etc/nos-amd/partition_agent_config.yaml"],
                    image=IMAGE_ROCM, env=NODE_ENV, mounts=HOST_MOUNTS + [mnt], privileged=True)
-    out["partagent/daemonset.yaml"] = [_sa(name), _config_map(name + "-config", {
-        "partition_agent_config.yaml": yaml.safe_dump(cfg)}),
-        _daemonset(name, c, C.PARTITIONING_AMDPART, HOST_VOLUMES + [vol])]
-    out["partagent/rbac.yaml"] = _cluster_role(name, node_rules)
+    if pa["enabled"]:
+        out["partagent/daemonset.yaml"] = [_sa(name), _config_map(name + "-config", {
+            "partition_agent_config.yaml": yaml.safe_dump(cfg)}),
+            _daemonset(name, c, C.PARTITIONING_AMDPART, HOST_VOLUMES + [vol])]
+        out["partagent/rbac.yaml"] = _cluster_role(name, node_rules)
     # gpuagent (CU-mask reporter + probes)
     name = "nos-amd-gpuagent"
     vol, mnt = _cfg_mount(name + "-config")
     cfg = {"apiVersion": C.CONFIG_API_VERSION, "kind": "GpuAgentConfig", "health": {"healthProbeBindAddress": ":8081"},
-           "reportConfigIntervalSeconds": 10, "probeEnabled": True}
+           "reportConfigIntervalSeconds": ga["reportConfigIntervalSeconds"], "probeEnabled": ga["probeEnabled"]}
     c = _container("gpuagent", "nos_amd.cmd.gpuagent", ["--config", "/etc/nos-amd/gpu_agent_config.yaml"],
                    image=IMAGE_ROCM, env=NODE_ENV, mounts=HOST_MOUNTS + [mnt], privileged=True)
-    out["gpuagent/daemonset.yaml"] = [_sa(name), _config_map(name + "-config", {
-        "gpu_agent_config.yaml": yaml.safe_dump(cfg)}), _daemonset(name, c, C.PARTITIONING_CUMASK, HOST_VOLUMES + [vol])]
-    out["gpuagent/rbac.yaml"] = _cluster_role(name, node_rules)
+    if ga["enabled"]:
+        out["gpuagent/daemonset.yaml"] = [_sa(name), _config_map(name + "-config", {
+            "gpu_agent_config.yaml": yaml.safe_dump(cfg)}),
+            _daemonset(name, c, C.PARTITIONING_CUMASK, HOST_VOLUMES + [vol])]
+        out["gpuagent/rbac.yaml"] = _cluster_role(name, node_rules)
     # device plugin (one DaemonSet per partitioning kind + plain GPU nodes could reuse it)
     name = "nos-amd-device-plugin"
     vol, mnt = _cfg_mount(name + "-config")
     cfg = {"apiVersion": C.CONFIG_API_VERSION, "kind": "DevicePluginConfig",
            "health": {"healthProbeBindAddress": ":8081"},
-           "configMap": {"name": C.DEFAULT_DEVICE_PLUGIN_CM_NAME, "namespace": NS},
-           "socketDir": C.DEVICE_PLUGIN_DIR, "cuPolicy": "even"}
+           "configMap": {"name": C.DEFAULT_DEVICE_PLUGIN_CM_NAME, "namespace": _ns()},
+           "socketDir": C.DEVICE_PLUGIN_DIR, "cuPolicy": gp["cuPolicy"]}
     c = _container("device-plugin", "nos_amd.cmd.deviceplugin", ["--config", "/etc/nos-amd/device_plugin_config.yaml"],
                    image=IMAGE_ROCM, env=NODE_ENV,
                    mounts=HOST_MOUNTS + [{"name": "device-plugins", "mountPath": C.DEVICE_PLUGIN_DIR}, mnt],
@@ -295,20 +397,63 @@ def node_agents() -> dict[str, list[dict]]:
         ds["spec"]["template"]["metadata"]["labels"]["nos.nebuly.com/kind"] = kind
         ds["spec"]["template"]["spec"]["serviceAccountName"] = name
         dss.append(ds)
-    out["deviceplugin/daemonset.yaml"] = [_sa(name), _config_map(name + "-config", {
-        "device_plugin_config.yaml": yaml.safe_dump(cfg)})] + dss
-    out["deviceplugin/rbac.yaml"] = _cluster_role(name, node_rules)
+    if gp["devicePlugin"]["enabled"]:
+        out["deviceplugin/daemonset.yaml"] = [_sa(name), _config_map(name + "-config", {
+            "device_plugin_config.yaml": yaml.safe_dump(cfg)})] + dss
+        out["deviceplugin/rbac.yaml"] = _cluster_role(name, node_rules)
     return out
 
 
-def render() -> dict[str, str]:
-    files: dict[str, list[dict]] = {"namespace.yaml": [{"apiVersion": "v1", "kind": "Namespace",
-                                                        "metadata": {"name": NS}}]}
-    for part in (crds(), operator(), scheduler(), gpupartitioner(), node_agents()):
-        files.update(part)
-    out = {k: "---\n".join(_dump(o) for o in v) for k, v in files.items()}
+def telemetry() -> dict[str, list[dict]]:
+    """Post-install metrics export (``templates/configmap_metrics.yaml`` +
+    ``pod_metrics-exporter.yaml``): component toggles + chart values, POSTed to
+    ``telemetryEndpoint`` (or only logged when it is empty)."""
+    name = "nos-amd-metrics-exporter"
+    gp = _V["gpuPartitioner"]
+    metrics = {"installationUUID": "", "components": {
+        "nosOperator": _V["operator"]["enabled"], "nosScheduler": _V["scheduler"]["enabled"],
+        "nosGpuPartitioner": gp["enabled"]}, "chartValues": _V}
+    vol, mnt = _cfg_mount(name + "-config")
+    args = ["--metrics-file", "/etc/nos-amd/metrics.yaml"]
+    if _V["telemetryEndpoint"]:
+        args += ["--metrics-endpoint", _V["telemetryEndpoint"]]
+    c = _container("exporter", "nos_amd.cmd.metricsexporter", args, mounts=[mnt], probes=False)
+    job = {"apiVersion": "batch/v1", "kind": "Job",
+           "metadata": {"name": name, "namespace": _ns(),
+                        "annotations": {"helm.sh/hook": "post-install", "helm.sh/hook-delete-policy": "hook-succeeded"}},
+           "spec": {"backoffLimit": 0, "template": {"spec": {"restartPolicy": "Never", "containers": [c],
+                                                             "volumes": [vol]}}}}
+    return {"telemetry/job.yaml": [_config_map(name + "-config", {"metrics.yaml": yaml.safe_dump(metrics)}), job]}
+
+
+def render(values: dict | None = None) -> dict[str, str]:
+    """Render every manifest file for ``values`` (merged over DEFAULT_VALUES)."""
+    global _V
+    v = merge_values(DEFAULT_VALUES, values or {})
+    validate_values(v)
+    prev, _V = _V, v
+    try:
+        files: dict[str, list[dict]] = {"namespace.yaml": [{"apiVersion": "v1", "kind": "Namespace",
+                                                            "metadata": {"name": _ns()}}]}
+        parts = [crds()]
+        if v["operator"]["enabled"]:
+            parts.append(operator())
+        if v["scheduler"]["enabled"]:
+            parts.append(scheduler())
+        if v["gpuPartitioner"]["enabled"]:
+            parts.append(gpupartitioner())
+        parts.append(node_agents())
+        if v["shareTelemetry"]:
+            parts.append(telemetry())
+        for part in parts:
+            files.update(part)
+    finally:
+        _V = prev
+    out = {k: "---\n".join(_dump(o) for o in docs) for k, docs in files.items()}
+    out["values.yaml"] = "# the values this tree was rendered with (--values / --set to customise)\n" + \
+        yaml.safe_dump(v, sort_keys=False)
     out["kustomization.yaml"] = yaml.safe_dump({"apiVersion": "kustomize.config.k8s.io/v1beta1",
-                                                "kind": "Kustomization", "namespace": NS,
+                                                "kind": "Kustomization", "namespace": v["namespace"],
                                                 "resources": sorted(k for k in files if not k.startswith("samples/"))},
                                                sort_keys=False)
     return out
@@ -318,10 +463,27 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--out", default="config")
     ap.add_argument("--check", action="store_true", help="fail if the files on disk are stale")
+    ap.add_argument("--values", action="append", default=[], help="values YAML file(s), merged in order")
+    ap.add_argument("--set", action="append", default=[], help="key.path=value override (YAML value)")
+    ap.add_argument("--stdout", action="store_true", help="print one multi-document stream (helm template)")
+    ap.add_argument("--dump-values", action="store_true", help="print the default values and exit")
     a = ap.parse_args(argv)
+    if a.dump_values:
+        sys.stdout.write(yaml.safe_dump(DEFAULT_VALUES, sort_keys=False))
+        return 0
+    values: dict = {}
+    for f in a.values:
+        values = merge_values(values, yaml.safe_load(Path(f).read_text()) or {})
+    for expr in a.set:
+        values = apply_set(values, expr)
+    rendered = render(values)
+    if a.stdout:
+        docs = [text for rel, text in sorted(rendered.items()) if rel not in ("kustomization.yaml", "values.yaml")]
+        sys.stdout.write("---\n".join(docs))
+        return 0
     root = Path(a.out)
     stale = []
-    for rel, text in render().items():
+    for rel, text in rendered.items():
         p = root / rel
         header = "# generated by `python -m nos_amd.cmd.manifests`; do not edit\n"
         if a.check:

@@ -44,8 +44,9 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--metrics-file", default="")
     ap.add_argument("--metrics-endpoint", default="")
+    ap.add_argument("--log-level", default="info")
     args = ap.parse_args(argv)
-    logging.basicConfig(level=logging.INFO)
+    logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO))
     try:
         doc = schema(yaml.safe_load(Path(args.metrics_file).read_text()) or {})
     except Exception as e:

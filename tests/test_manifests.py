@@ -20,7 +20,7 @@ def test_config_tree_is_fresh():
 
 
 def _objs():
-    for f in sorted((REPO / "config").rglob("*.yaml")):
+    for f in sorted(p for p in (REPO / "config").rglob("*.yaml") if p.name != "values.yaml"):
         yield from (o for o in yaml.safe_load_all(f.read_text()) if o)
 
 
@@ -57,3 +57,41 @@ def test_daemonsets_are_privileged_and_node_selected():
         assert c["securityContext"]["privileged"] is True
         assert any(m["mountPath"] == "/var/lib/kubelet/pod-resources" for m in c["volumeMounts"])
         assert c["env"][0]["name"] == "NODE_NAME"
+
+
+def test_values_overrides_render_and_validate(tmp_path):
+    """Helm-values equivalent: overrides reach the embedded configs, disabled
+    components disappear, the default namespace is refused, telemetry is opt-in."""
+    base = manifests.render()
+    assert "telemetry/job.yaml" not in base
+    v = manifests.apply_set({}, "gpuPartitioner.cuPolicy=shared")
+    v = manifests.apply_set(v, "gpuPartitioner.batchWindowIdleSeconds=3")
+    v = manifests.merge_values(v, {"namespace": "gpu-sharing", "amdGpuResourceMemoryGB": 144,
+                                   "shareTelemetry": True,
+                                   "gpuPartitioner": {"gpuAgent": {"enabled": False}}})
+    out = manifests.render(v)
+    assert "gpuagent/daemonset.yaml" not in out and "partagent/daemonset.yaml" in out
+    docs = [o for rel, text in out.items() if not rel.startswith("samples/") and rel != "values.yaml"
+            for o in yaml.safe_load_all(text) if o]
+    assert all(o["metadata"].get("namespace", "gpu-sharing") == "gpu-sharing" for o in docs
+               if o["kind"] not in ("ClusterRole", "ClusterRoleBinding", "CustomResourceDefinition",
+                                    "ValidatingWebhookConfiguration", "Namespace", "Kustomization"))
+    cms = {k: t for o in docs if o["kind"] == "ConfigMap" for k, t in (o.get("data") or {}).items()}
+    p = tmp_path / "gp.yaml"
+    p.write_text(cms["gpu_partitioner_config.yaml"])
+    gp = cfgmod.load(p)
+    assert gp.batch_window_idle_seconds == 3 and gp.amd_gpu_resource_memory_gb == 144
+    assert yaml.safe_load(cms["scheduler_config.yaml"])["profiles"][0]["pluginConfig"][0]["args"][
+        "amdGpuResourceMemoryGB"] == 144
+    assert yaml.safe_load(cms["metrics.yaml"])["components"]["nosGpuPartitioner"] is True
+    import pytest
+    with pytest.raises(ValueError):
+        manifests.render({"namespace": "default"})
+    with pytest.raises(ValueError):
+        manifests.render(manifests.apply_set({}, "gpuPartitioner.slicePlacement=diagonal"))
+    # --stdout renders one stream; --dump-values round-trips through --values
+    vals = tmp_path / "values.yaml"
+    vals.write_text(yaml.safe_dump(manifests.DEFAULT_VALUES))
+    assert manifests.main(["--values", str(vals), "--out", str(tmp_path / "cfg")]) == 0
+    assert (tmp_path / "cfg" / "gpupartitioner" / "manager.yaml").read_text() == \
+        (REPO / "config" / "gpupartitioner" / "manager.yaml").read_text()
