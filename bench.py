@@ -57,14 +57,21 @@ def parse_args(argv=None):
 
 
 def init_dist():
+    """One rank per GPU over RCCL (backend "nccl").  NOS_AMD_BENCH_BACKEND=gloo
+    rehearses the multi-rank path with several ranks sharing one GPU (RCCL
+    refuses two ranks on one device): device = LOCAL_RANK mod device count."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("NOS_AMD_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -156,7 +163,9 @@ def main(argv=None) -> int:
             sampler.__exit__(None, None, None)
 
     util = sampler.mean() if sampler else None
-    t = torch.tensor([elapsed, util if util is not None else -1.0], dtype=torch.float64, device="cuda")
+    on_gpu = os.environ.get("NOS_AMD_BENCH_BACKEND", "nccl") == "nccl"
+    t = torch.tensor([elapsed, util if util is not None else -1.0], dtype=torch.float64,
+                     device="cuda" if on_gpu else "cpu")
     if world > 1:
         mx = t.clone()
         dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
