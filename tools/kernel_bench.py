@@ -71,6 +71,7 @@ def main():
         for name, (N, K, act, ln, resid) in {
             "qkv_ln": (3 * hid, hid, None, True, False),
             "fc1_ln_gelu": (mlp, hid, "gelu", True, False),
+            "fc1_ln_noact": (mlp, hid, None, True, False),
             "proj_resid": (hid, hid, None, False, True),
             "fc2_resid": (hid, mlp, None, False, True),
             "qkv_plain": (3 * hid, hid, None, False, False),
