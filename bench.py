@@ -204,7 +204,7 @@ def main(argv=None) -> int:
         "pod_latency_ms": round(ms_per_step, 3),
         "gpu_util_pct": None if util is None else round(util, 1),
         "achieved_tflops": round(value * fl / 1e12, 1),
-        "schedulable_fractional_pods_per_node": cp.get("schedulable_pods_per_node"),
+        "schedulable_fractional_pods_per_node": cp.get("schedulable_fractional_pods_per_node"),
         "control_plane": cp,
         "baseline_img_per_s_per_gpu": BASELINE_IMG_PER_S_PER_GPU,
     }

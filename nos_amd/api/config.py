@@ -112,8 +112,8 @@ class GpuPartitionerConfig(ControllerManagerSpec):
             raise ValueError("batchWindowIdleSeconds must be greater than 0")
         if self.device_plugin_delay_seconds <= 0:
             raise ValueError("devicePluginDelaySeconds must be greater than 0")
-        if self.slice_placement not in ("pack", "spread"):
-            raise ValueError("slicePlacement must be 'pack' or 'spread'")
+        if self.slice_placement not in ("pack", "spread", "measured"):
+            raise ValueError("slicePlacement must be 'pack', 'spread' or 'measured'")
         if self.cu_policy not in ("even", "proportional", "shared"):
             raise ValueError("cuPolicy must be 'even', 'proportional' or 'shared'")
 

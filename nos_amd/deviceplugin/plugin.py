@@ -35,6 +35,7 @@ from ..api import constants as C
 from ..gpu.amdsmi import PARTITIONS_PER_MODE, AmdSmi, GpuInfo
 from ..gpu.topology import MI355X_CUS_PER_XCD, MI355X_XCDS, CUSlice, logical_cu
 from ..ops.streams import mask_hex
+from ..partitioning import scoring
 
 log = logging.getLogger("nos_amd.deviceplugin")
 
@@ -73,6 +74,7 @@ class NosAmdDevicePlugin:
         self.cu_slots: dict[str, CUSlice] = {}   # slice device id -> CU slot
         self.listeners: list = []
         self.generation = 0
+        self._links: dict[tuple[int, int], float] = {}
         self.refresh()
 
     # ------------------------------------------------------------ inventory
@@ -186,21 +188,47 @@ class NosAmdDevicePlugin:
         return self.resources().get(resource, [])
 
     def preferred_allocation(self, resource: str, available: list[str], must_include: list[str], size: int) -> list[str]:
-        """``GetPreferredAllocation``: "spread" (config ``allocation``) picks
-        devices on the GPUs with the fewest allocated devices, "pack" fills
-        GPUs in index order."""
+        """``GetPreferredAllocation`` (config ``allocation``):
+
+        * "pack" fills GPUs in index order; "spread" picks the GPU with the
+          fewest allocated devices; "measured" the GPU where the pod gets the
+          largest share of the probe-measured TFLOP/s (``gpuWeights`` written
+          by the partitioner, partitioning/scoring.py);
+        * a request for several devices (one container spanning GPUs, e.g. an
+          RCCL tenant) is placed xGMI-aware whatever the policy: one device
+          per GPU first, then GPUs whose links carry the fewest multi-device
+          tenants, then the lowest amd-smi link weight to the GPUs already
+          chosen (``scoring.choose_devices_xgmi``).
+        """
         with self._lock:
             out = list(must_include)[:size]
             cand = [d for d in available if d not in out and d in self.devices]
-            policy = (self.config or {}).get("allocation", "pack")
+            cfg = self.config or {}
+            policy = cfg.get("allocation", "pack")
+            weights = {int(k): float(v) for k, v in (cfg.get("gpuWeights") or {}).items()}
             load: dict[int, int] = {}
-            for did in self.allocated:
+            owners: dict[str, set[int]] = {}
+            for did, owner in self.allocated.items():
                 d = self.devices.get(did)
                 if d is not None:
                     load[d.gpu_index] = load.get(d.gpu_index, 0) + 1
+                    owners.setdefault(owner, set()).add(d.gpu_index)
+            if size > 1:
+                coll: dict[int, int] = {}
+                for gpus in owners.values():
+                    if len(gpus) > 1:
+                        for g in gpus:
+                            coll[g] = coll.get(g, 0) + 1
+                return scoring.choose_devices_xgmi(cand + out, size, out, lambda x: self.devices[x].gpu_index,
+                                                   self._link_weight, coll, load)
+            default_w = (sum(weights.values()) / len(weights)) if weights else 1.0
             while len(out) < size and cand:
                 if policy == "spread":
                     best = min(cand, key=lambda x: (load.get(self.devices[x].gpu_index, 0),
+                                                    self.devices[x].gpu_index, x))
+                elif policy == "measured":
+                    best = min(cand, key=lambda x: (-weights.get(self.devices[x].gpu_index, default_w) /
+                                                    (load.get(self.devices[x].gpu_index, 0) + 1),
                                                     self.devices[x].gpu_index, x))
                 else:
                     best = min(cand, key=lambda x: (self.devices[x].gpu_index, x))
@@ -209,6 +237,17 @@ class NosAmdDevicePlugin:
                 gi = self.devices[best].gpu_index
                 load[gi] = load.get(gi, 0) + 1
             return out
+
+    def _link_weight(self, i: int, j: int) -> float:
+        key = (min(i, j), max(i, j))
+        w = self._links.get(key)
+        if w is None:
+            try:
+                w = float(self.smi.link(i, j).get("weight", 0))
+            except Exception:  # topology unreadable: every pair equal
+                w = 0.0
+            self._links[key] = w
+        return w
 
     def allocate(self, resource: str, device_ids: list[str], owner: str = "") -> ContainerAllocation:
         with self._lock:

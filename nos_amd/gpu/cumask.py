@@ -21,6 +21,7 @@ from ..kube import objects as ko
 from ..kube import quantity as q
 from .core import GenericError, Geometry, get_count, get_memory_gb, get_model, parse_node_annotations
 from .topology import MI355X_CUS_PER_XCD, MI355X_XCDS
+from ..partitioning import scoring
 
 MIN_SLICE_MEMORY_GB = 1
 REPLICA_SEPARATOR = "::"  # device ids of slices: <gpu-uuid>::<replica>
@@ -205,8 +206,12 @@ class SliceNode:
         self.node_info = node_info
         # "pack": first-fit over GPUs (the reference, keeps whole GPUs free);
         # "spread": new slices go to the GPU with the most spare memory, so
-        # tenants are balanced over the node's GPUs (throughput-first)
+        # tenants are balanced over the node's GPUs (throughput-first);
+        # "measured": new slices go to the GPU where a pod gets the largest
+        # share of the probe-measured throughput (partitioning/scoring.py)
         self.placement = placement
+        self.capacity: dict[int, float] = {}   # measured TFLOP/s per GPU (probe annotations)
+        self.measured = False
 
     @classmethod
     def from_node_info(cls, ni) -> "SliceNode":
@@ -234,7 +239,26 @@ class SliceNode:
             if i not in have:
                 gpus.append(SliceGPU(model, i, mem, max_slices=max_slices))
         gpus.sort(key=lambda g: g.index)
-        return cls(ko.name(node), gpus, ni)
+        out = cls(ko.name(node), gpus, ni)
+        table = scoring.probe_table(ko.annotations(node))
+        counts = {g.index: {p.name: g.used.get(p, 0) + g.free.get(p, 0) for p in set(g.used) | set(g.free)}
+                  for g in gpus}
+        caps = scoring.gpu_capacities(table, counts)
+        out.measured = bool(caps)
+        out.capacity = scoring.fill_unmeasured(caps, [g.index for g in gpus])
+        return out
+
+    def _share(self, g: "SliceGPU") -> float:
+        return scoring.expected_share(self.capacity.get(g.index, 1.0), g.num_slices())
+
+    def score(self) -> float | None:
+        """Best expected per-pod share of measured throughput on a GPU with
+        room for one more slice; ``None`` unless placement is "measured" and
+        the node carries probe data (the planner then keeps name order)."""
+        if self.placement != "measured" or not self.measured:
+            return None
+        return scoring.node_score(self.capacity, {g.index: g.num_slices() for g in self.gpus},
+                                  lambda gi: any(g.index == gi and g.has_free_capacity() for g in self.gpus))
 
     def geometry(self) -> dict:
         res: dict = {}
@@ -250,7 +274,7 @@ class SliceNode:
         if not self.gpus or not slices:
             return False
         required = dict(slices)
-        if self.placement == "spread":
+        if self.placement in ("spread", "measured"):
             updated = self._spread(required)
             self._recompute_allocatable()
             return updated
@@ -274,7 +298,10 @@ class SliceNode:
                          and g.num_slices() < g.max_slices]
                 if not cands:
                     break
-                g = max(cands, key=lambda g: (g.memory_gb - g.tot_slices_memory(), -g.num_slices(), -g.index))
+                if self.placement == "measured":
+                    g = max(cands, key=lambda g: (self._share(g), g.memory_gb - g.tot_slices_memory(), -g.index))
+                else:
+                    g = max(cands, key=lambda g: (g.memory_gb - g.tot_slices_memory(), -g.num_slices(), -g.index))
                 g.create_slices(p.memory_gb)
                 need -= 1
                 updated = True
@@ -290,6 +317,9 @@ class SliceNode:
         order = self.gpus
         if self.placement == "spread":  # mirror the device plugin's preferred allocation
             order = sorted(self.gpus, key=lambda g: (sum(g.used.values()), g.index))
+        elif self.placement == "measured":
+            order = sorted(self.gpus, key=lambda g: (-self.capacity.get(g.index, 1.0) / (sum(g.used.values()) + 1),
+                                                     g.index))
         for g in order:
             try:
                 g.add_pod(pod)
@@ -300,7 +330,9 @@ class SliceNode:
         raise GenericError("not enough free slices")
 
     def clone(self) -> "SliceNode":
-        return SliceNode(self.name, [g.clone() for g in self.gpus], self.node_info.clone(), self.placement)
+        c = SliceNode(self.name, [g.clone() for g in self.gpus], self.node_info.clone(), self.placement)
+        c.capacity, c.measured = dict(self.capacity), self.measured
+        return c
 
 
 class SliceCalculator:

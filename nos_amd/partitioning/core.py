@@ -122,7 +122,14 @@ class ClusterSnapshot:
         self._d()[n.name] = n
 
     def get_candidate_nodes(self) -> list[str]:
-        return sorted(n.name for n in self._d().values() if n.has_free_capacity())
+        """Nodes with free capacity in name order (``snapshot.go:93-103``);
+        nodes that expose a measured-throughput ``score()`` (cumask placement
+        "measured", see partitioning/scoring.py) come first, best score first."""
+        def key(n):
+            sc = n.score() if hasattr(n, "score") else None
+            return (sc is None, -(sc or 0.0), n.name)
+
+        return [n.name for n in sorted((n for n in self._d().values() if n.has_free_capacity()), key=key)]
 
     def get_partitioning_state(self) -> PartitioningState:
         return PartitioningState({name: self.partition_calculator.get_partitioning(n)

@@ -34,6 +34,7 @@ from ..gpu.core import SpecAnnotation, is_amdpart_enabled, is_cumask_enabled
 from ..kube import objects as ko
 from ..scheduler.framework import NodeInfo
 from .core import ClusterSnapshot, new_plan_id
+from . import scoring
 from .state import ClusterState, GPUPartitioning, NodePartitioning
 
 log = logging.getLogger("nos_amd.partitioning.strategies")
@@ -139,16 +140,22 @@ class DevicePluginConfigRef:
 
 
 def plugin_config(node_name: str, plan_id: str, partitioning: NodePartitioning, cu_policy: str = "even",
-                  allocation: str = "pack") -> dict:
+                  allocation: str = "pack", gpu_weights: dict[int, float] | None = None) -> dict:
     """Device-plugin configuration for one node (the ``ToPluginConfig`` of
-    ``mps/partitioner.go:123-157``, AMD shape)."""
+    ``mps/partitioner.go:123-157``, AMD shape).  With ``allocation:
+    measured`` it also carries the probe-measured TFLOP/s per GPU
+    (``gpuWeights``) that the plugin's GetPreferredAllocation divides among
+    the pods of each GPU."""
     gpus = []
     for g in sorted(partitioning.gpus, key=lambda x: x.gpu_index):
         slices = [{"profile": cm.profile_of_resource(r).name, "memoryGB": cm.profile_of_resource(r).memory_gb,
                    "replicas": n} for r, n in g.resources]
         gpus.append({"index": g.gpu_index, "slices": slices})
-    return {"version": "v1", "node": node_name, "planId": plan_id, "cuPolicy": cu_policy, "allocation": allocation,
-            "gpus": gpus}
+    out = {"version": "v1", "node": node_name, "planId": plan_id, "cuPolicy": cu_policy, "allocation": allocation,
+           "gpus": gpus}
+    if gpu_weights:
+        out["gpuWeights"] = {int(k): round(float(v), 3) for k, v in sorted(gpu_weights.items())}
+    return out
 
 
 class CuMaskPartitioner:
@@ -174,7 +181,13 @@ class CuMaskPartitioner:
                                     "data": {}})
         data = {k: None for k in (cmap.get("data") or {}) if k.startswith(name + "-")}
         key = f"{name}-{plan_id}"
-        data[key] = yaml.safe_dump(plugin_config(name, plan_id, partitioning, self.cu_policy, self.allocation), sort_keys=False)
+        weights = None
+        if self.allocation == "measured":
+            counts = {g.gpu_index: {cm.profile_of_resource(r).name: n for r, n in g.resources}
+                      for g in partitioning.gpus}
+            weights = scoring.gpu_capacities(scoring.probe_table(ko.annotations(node)), counts) or None
+        data[key] = yaml.safe_dump(plugin_config(name, plan_id, partitioning, self.cu_policy, self.allocation,
+                                                 weights), sort_keys=False)
         self.api.patch("ConfigMap", ref.name, {"data": data}, ref.namespace)
         if self.delay_s > 0:
             self.clock.sleep(self.delay_s)  # ConfigMap propagation (kept for fidelity)
