@@ -52,6 +52,8 @@ def parse_args(argv=None):
     ap.add_argument("--collective", action="store_true", help="add a GEMM + RCCL all-reduce tenant per GPU")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-control-plane", action="store_true")
+    ap.add_argument("--gemm-impl", choices=["register", "ring", "lds"], default="register",
+                    help="GEMM epilogue implementation (A/B switch; register is the default)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -111,6 +113,7 @@ def main(argv=None) -> int:
 
     # one pod owning the GPU wants latency-shaped GEMM tiles, co-running pods throughput-shaped ones
     ops.set_gemm_policy("latency" if len(masks) == 1 else "throughput")
+    ops.set_gemm_impl(args.gemm_impl)
     cfg = YolosConfig.small()
     hw = demo_input_hw()
     specs = [TenantSpec(f"pod-{rank}-{i}", m) for i, m in enumerate(masks)]

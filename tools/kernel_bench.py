@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--out", default="")
+    ap.add_argument("--impls", default="register", help="comma list of GEMM epilogue impls to A/B (register,lds)")
+    ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds per impl (median reported)")
     a = ap.parse_args()
     torch.manual_seed(0)
     S, H, hid, mlp = 3401, 6, 384, 1536
@@ -88,9 +90,18 @@ def main():
                 fn = lambda: ops.linear_ln(xa, wg, c1, c2, act=act, out=outg)  # noqa: E731
             else:
                 fn = lambda: ops.linear(xa, w, b, act=act, residual=r if resid else None, out=outg)  # noqa: E731
-            us = timeit(fn, a.iters)
-            res[f"{name}_us"] = us
-            res[f"{name}_tflops"] = 2 * M * N * K / us / 1e6
+            impls = a.impls.split(",")
+            times = {im: [] for im in impls}
+            for _ in range(a.rounds):
+                for im in impls:
+                    ops.set_gemm_impl(im)
+                    times[im].append(timeit(fn, a.iters))
+            ops.set_gemm_impl("register")
+            for im in impls:
+                t = sorted(times[im])[len(times[im]) // 2]
+                sfx = "" if im == impls[0] else f"_{im}"
+                res[f"{name}{sfx}_us"] = t
+                res[f"{name}{sfx}_tflops"] = 2 * M * N * K / t / 1e6
             tus = timeit(lambda: torch.nn.functional.linear(xa, w, b), a.iters)
             res[f"{name}_torch_us"] = tus
     print(json.dumps(res), flush=True)
