@@ -52,7 +52,7 @@ def parse_args(argv=None):
     ap.add_argument("--collective", action="store_true", help="add a GEMM + RCCL all-reduce tenant per GPU")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-control-plane", action="store_true")
-    ap.add_argument("--gemm-impl", choices=["register", "ring", "lds"], default="register",
+    ap.add_argument("--gemm-impl", choices=["register", "lds"], default="register",
                     help="GEMM epilogue implementation (A/B switch; register is the default)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)

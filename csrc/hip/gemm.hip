@@ -309,20 +309,20 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
 // per lane, so bias / LayerNorm correction / activation / residual run on
 // registers and the tile leaves as 16-byte row stores -- no fp32 LDS tile
 // (67 KiB less LDS per workgroup, no LDS write + read pass, one barrier fewer).
-// Register epilogue shared by the rk and ring kernels.  acc holds C^T blocks
+// Register epilogue of the rk kernel.  acc holds C^T blocks
 // (MFMA operands swapped): lane (r, hh) owns row r, columns 8j + 4hh + {0..3}
 // of each 32x32 block; a v_permlane32_swap per register pair gives each lane
 // 8 consecutive columns of its row, stored as one 16-byte chunk.
-template <bool LN, int BN>
-__device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[2][Cfg<BN>::NB], const float* s_mu,
+template <bool LN, int BN, int MI = 2>
+__device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[MI][Cfg<BN>::NB], const float* s_mu,
                                               const float* s_rstd, const float* s_p1, const float* s_p2,
                                               const unsigned short* __restrict__ R, int ldr,
                                               unsigned short* __restrict__ C, int ldc, int M, int N, int m0,
                                               int n0, int epi, bool vec_ok, int wm, int wn, int r, int hh) {
   constexpr int WN = Cfg<BN>::WN, NB = Cfg<BN>::NB;
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      const int rl = wm * 64 + mi * 32 + r;
+    for (int mi = 0; mi < MI; ++mi) {
+      const int rl = wm * (32 * MI) + mi * 32 + r;
       const int m = m0 + rl;
       float mu = 0.f, rs = 1.f;
       if constexpr (LN) {
@@ -513,180 +513,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------
-// Ring variant (impl 2): BK = 32, a 4-slot LDS ring with three K-steps in
-// flight.  The LDS-DMA of step k+3 is issued right after the barrier of step
-// k and retired by a COUNTED `s_waitcnt vmcnt` (never 0 inside the loop) plus
-// a raw s_barrier, so the loads span barriers instead of being drained every
-// K-step by __syncthreads (cdna_hip_programming.md §5 "Pipelining across
-// barriers").  64 KiB of ring + 2 KiB of parameters: still two workgroups per
-// CU, so co-running tenants' kernels keep sharing a CU.  Register epilogue.
-constexpr int RBK = 32;                 // ring K-step
-constexpr int RSLOTS = 4;               // ring slots
-constexpr int RAHEAD = 3;               // K-steps in flight
-
-__device__ __forceinline__ int rswz(int row) { return (row >> 2) & 3; }
-
-// Stage a [ROWS][32 k] bf16 tile (64-B rows, 16 rows per wave-instruction).
-// LDS image is lane-linear; the 16-B chunk c of row r sits at physical chunk
-// c ^ rswz(r) (inverse swizzle applied to the source address): conflict-free
-// ds_read_b128 for the 32-row fragment reads.
-template <int ROWS>
-__device__ __forceinline__ void stage_tile32(const unsigned short* __restrict__ src, int ld, int row0, int nrows,
-                                             int k0, unsigned char* tile, int wid, int lane) {
-  constexpr int PER_WAVE = ROWS / 64;
-#pragma unroll
-  for (int i = 0; i < PER_WAVE; ++i) {
-    const int R0 = (wid * PER_WAVE + i) * 16;
-    const int row = R0 + (lane >> 2);
-    const int lc = (lane & 3) ^ rswz(row);
-    int grow = row0 + row;
-    grow = grow < nrows ? grow : nrows - 1;
-    glds16(src + (long long)grow * ld + k0 + lc * 8, tile + R0 * 64);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <bool LN, int BN>
-__global__ __launch_bounds__(NT, 2) void gemm_bf16_ring_kernel(
-    const unsigned short* __restrict__ A, int lda, const unsigned short* __restrict__ W, int ldw,
-    const unsigned short* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
-    const unsigned short* __restrict__ R, int ldr, unsigned short* __restrict__ C, int ldc, int M, int N,
-    int K, int epi, float eps, int tiles_m, int tiles_n) {
-  constexpr int WN = Cfg<BN>::WN, NB = Cfg<BN>::NB;
-  constexpr int TA = BM * RBK * 2, TB = BN * RBK * 2, SLOT = TA + TB;
-  constexpr int G = BM / 64 + BN / 64;  // LDS-DMA instructions per wave per K-step
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* s_mu = reinterpret_cast<float*>(smem + RSLOTS * SLOT);
-  float* s_rstd = s_mu + BM;
-  float* s_p1 = s_rstd + BM;
-  float* s_p2 = s_p1 + BN;
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int r = lane & 31, hh = lane >> 5;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int ntiles = tiles_m * tiles_n;
-  const int nk = K / RBK;
-  const bool vec_ok = ((ldc | ldr) & 7) == 0;
-
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int tt = (gridDim.x >= ntiles) ? nos::xcd_remap(tile, ntiles) : tile;
-    int tm, tn;
-    if (tiles_m >= tiles_n) {
-      tm = tt / tiles_n;
-      tn = tt - tm * tiles_n;
-    } else {
-      tn = tt / tiles_m;
-      tm = tt - tn * tiles_m;
-    }
-    const int m0 = tm * BM, n0 = tn * BN;
-
-    f32x16_t acc[2][NB];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
-
-    const int srow = tid >> 1, shalf = tid & 1;
-    float sshift = 0.f, ssum = 0.f, ssq = 0.f;
-
-    // parameters first: their loads are waited for before the ring DMA is issued
-    if (tid < BN) {
-      const int n = min(n0 + tid, N - 1);
-      s_p1[tid] = LN ? c1[n] : 0.f;
-      s_p2[tid] = LN ? c2[n] : ((epi & EPI_BIAS) ? nos::bf16_to_f32(bias[n]) : 0.f);
-    }
-    int iss = 0;
-#pragma unroll
-    for (int p = 0; p < RAHEAD; ++p) {
-      if (iss < nk) {
-        unsigned char* sl = smem + (iss % RSLOTS) * SLOT;
-        stage_tile32<BM>(A, lda, m0, M, iss * RBK, sl, wid, lane);
-        stage_tile32<BN>(W, ldw, n0, N, iss * RBK, sl + TA, wid, lane);
-        ++iss;
-      }
-    }
-
-    for (int kt = 0; kt < nk; ++kt) {
-      // retire step kt: the steps issued after it may stay in flight
-      const int after = iss - kt - 1;
-      if (after >= 2) wait_vmcnt<2 * G>();
-      else if (after == 1) wait_vmcnt<G>();
-      else wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();  // every wave's DMA of step kt landed; step kt-1's slot is free
-      if (iss < nk) {
-        unsigned char* sl = smem + (iss % RSLOTS) * SLOT;
-        stage_tile32<BM>(A, lda, m0, M, iss * RBK, sl, wid, lane);
-        stage_tile32<BN>(W, ldw, n0, N, iss * RBK, sl + TA, wid, lane);
-        ++iss;
-      }
-      const unsigned char* ta = smem + (kt % RSLOTS) * SLOT;
-      const unsigned char* tb = ta + TA;
-      if constexpr (LN) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const int lc = shalf * 2 + c;
-          const s16x8_t v = *reinterpret_cast<const s16x8_t*>(ta + srow * 64 + ((lc ^ rswz(srow)) << 4));
-          if (kt == 0 && c == 0) sshift = nos::bf16_to_f32((unsigned short)v[0]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float d = nos::bf16_to_f32((unsigned short)v[e]) - sshift;
-            ssum += d;
-            ssq = fmaf(d, d, ssq);
-          }
-        }
-      }
-#pragma unroll
-      for (int ks = 0; ks < RBK / 16; ++ks) {
-        bf16x8_t af[2], bf[NB];
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-          const int row = wm * 64 + mi * 32 + r;
-          af[mi] = *reinterpret_cast<const bf16x8_t*>(ta + row * 64 + (((2 * ks + hh) ^ rswz(row)) << 4));
-        }
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni) {
-          const int row = wn * WN + ni * 32 + r;
-          bf[ni] = *reinterpret_cast<const bf16x8_t*>(tb + row * 64 + (((2 * ks + hh) ^ rswz(row)) << 4));
-        }
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < NB; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[ni], af[mi], acc[mi][ni], 0, 0, 0);
-      }
-    }
-
-    if constexpr (LN) {
-      const float sh_lo = __shfl(sshift, lane & ~1, 64);
-      const float dlt = sshift - sh_lo;
-      const float kh = (float)(K / 2);
-      float s2 = ssum + dlt * kh;
-      float q2 = ssq + 2.f * dlt * ssum + dlt * dlt * kh;
-      s2 += __shfl_xor(s2, 1, 64);
-      q2 += __shfl_xor(q2, 1, 64);
-      if (shalf == 0) {
-        const float mean_d = s2 / (float)K;
-        const float var = fmaxf(q2 / (float)K - mean_d * mean_d, 0.f);
-        s_mu[srow] = sh_lo + mean_d;
-        s_rstd[srow] = rsqrtf(var + eps);
-      }
-    }
-    __syncthreads();  // stats / params visible (no DMA in flight any more)
-    epilogue_rows<LN, BN>(acc, s_mu, s_rstd, s_p1, s_p2, R, ldr, C, ldc, M, N, m0, n0, epi, vec_ok, wm, wn, r,
-                          hh);
-    __syncthreads();  // ring slots and stats are rewritten by the next persistent tile
-  }
-}
-
-template <int BNV>
-constexpr int ring_lds_bytes() { return RSLOTS * (BM + BNV) * RBK * 2 + (2 * BM + 2 * BNV) * 4; }
-
 int g_epi_impl = 1;  // 0 = fp32 LDS-tile epilogue, 1 = register epilogue (nos_gemm_set_impl)
 
 template <int BNV>
@@ -695,7 +521,7 @@ constexpr int rk_lds_bytes() { return 2 * Cfg<BNV>::STAGE_BYTES + (2 * BM + 2 * 
 int launch(const void* A, int lda, const void* W, int ldw, const void* bias, const float* c1,
            const float* c2, const void* R, int ldr, void* C, int ldc, int M, int N, int K, int epi,
            float eps, int max_wg, bool ln, hipStream_t stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || (K % (g_epi_impl == 2 ? RBK : BK)) != 0) return (int)hipErrorInvalidValue;
+  if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0) return (int)hipErrorInvalidValue;
   if ((lda % 8) || (ldw % 8)) return (int)hipErrorInvalidValue;
   if (!ln && (epi & EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
   if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
@@ -714,10 +540,7 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
   auto Cp = (unsigned short*)C;
 #define NOS_GEMM_LAUNCH(LNV, BNV)                                                                              \
   do {                                                                                                          \
-    if (g_epi_impl == 2)                                                                                        \
-      hipLaunchKernelGGL((gemm_bf16_ring_kernel<LNV, BNV>), dim3(nwg), dim3(NT), ring_lds_bytes<BNV>(), stream,  \
-                         Ap, lda, Wp, ldw, Bp, c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n);  \
-    else if (g_epi_impl == 1)                                                                                   \
+    if (g_epi_impl == 1)                                                                                   \
       hipLaunchKernelGGL((gemm_bf16_rk_kernel<LNV, BNV>), dim3(nwg), dim3(NT), rk_lds_bytes<BNV>(), stream, Ap, \
                          lda, Wp, ldw, Bp, c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n);      \
     else                                                                                                        \
@@ -745,9 +568,9 @@ NOS_API int nos_gemm_set_policy(int policy) {
 }
 
 // Implementation (A/B switch): 0 = fp32 LDS-tile epilogue, 1 = register
-// epilogue, 2 = 4-slot BK-32 ring with counted vmcnt + register epilogue.
+// epilogue (default).
 NOS_API int nos_gemm_set_impl(int impl) {
-  if (impl < 0 || impl > 2) return (int)hipErrorInvalidValue;
+  if (impl != 0 && impl != 1) return (int)hipErrorInvalidValue;
   g_epi_impl = impl;
   return 0;
 }

@@ -102,10 +102,9 @@ def set_gemm_policy(policy: str) -> None:
 
 def set_gemm_impl(impl: str) -> None:
     """GEMM epilogue implementation: ``"register"`` (default: accumulators
-    transposed in registers, 16-byte row stores), ``"ring"`` (same epilogue,
-    BK-32 4-slot LDS ring with three K-steps in flight) or ``"lds"`` (fp32 LDS
-    tile; kept for A/B measurements)."""
-    code = {"lds": 0, "register": 1, "ring": 2}[impl]
+    transposed in registers, 16-byte row stores) or ``"lds"`` (fp32 LDS tile;
+    kept for A/B measurements)."""
+    code = {"lds": 0, "register": 1}[impl]
     _lib.check(_lib.lib().nos_gemm_set_impl(code), "nos_gemm_set_impl")
 
 
