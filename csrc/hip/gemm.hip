@@ -313,13 +313,33 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
 // (MFMA operands swapped): lane (r, hh) owns row r, columns 8j + 4hh + {0..3}
 // of each 32x32 block; a v_permlane32_swap per register pair gives each lane
 // 8 consecutive columns of its row, stored as one 16-byte chunk.
-template <bool LN, int BN, int MI = 2>
+template <bool LN, int BN, bool RESID, int MI = 2>
 __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[MI][Cfg<BN>::NB], const float* s_mu,
                                               const float* s_rstd, const float* s_p1, const float* s_p2,
                                               const unsigned short* __restrict__ R, int ldr,
                                               unsigned short* __restrict__ C, int ldc, int M, int N, int m0,
                                               int n0, int epi, bool vec_ok, int wm, int wn, int r, int hh) {
   constexpr int WN = Cfg<BN>::WN, NB = Cfg<BN>::NB;
+  // residual rows: all 16-byte loads issued up front (clamped addresses, no
+  // per-element branches) so their latencies overlap instead of one round
+  // trip per chunk
+  s16x8_t rpre[MI][NB][2];
+  if constexpr (RESID) {
+    if (vec_ok && N >= 8) {
+      const int nmax = ((N - 8) >> 3) << 3;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const int m = min(m0 + wm * (32 * MI) + mi * 32 + r, M - 1);
+#pragma unroll
+        for (int ni = 0; ni < NB; ++ni)
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) {
+            const int n = min(n0 + wn * WN + ni * 32 + 16 * pr + 8 * hh, nmax);
+            rpre[mi][ni][pr] = *reinterpret_cast<const s16x8_t*>(R + (long long)m * ldr + n);
+          }
+      }
+    }
+  }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
       const int rl = wm * (32 * MI) + mi * 32 + r;
@@ -369,8 +389,8 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[MI][Cfg<BN>:
           }
           if (m >= M || n >= N) continue;
           if (n + 8 <= N && vec_ok) {
-            if (epi & EPI_RESID) {
-              const s16x8_t rv = *reinterpret_cast<const s16x8_t*>(R + (long long)m * ldr + n);
+            if constexpr (RESID) {
+              const s16x8_t rv = rpre[mi][ni][pr];
 #pragma unroll
               for (int e = 0; e < 8; ++e) v[e] += nos::bf16_to_f32((unsigned short)rv[e]);
             }
@@ -381,7 +401,7 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[MI][Cfg<BN>:
           } else {
             for (int e = 0; e < 8 && n + e < N; ++e) {
               float x = v[e];
-              if (epi & EPI_RESID) x += nos::bf16_to_f32(R[(long long)m * ldr + n + e]);
+              if (RESID) x += nos::bf16_to_f32(R[(long long)m * ldr + n + e]);
               C[(long long)m * ldc + n + e] = nos::f32_to_bf16(x);
             }
           }
@@ -390,7 +410,7 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[MI][Cfg<BN>:
     }
 }
 
-template <bool LN, int BN>
+template <bool LN, int BN, bool RESID>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
     const unsigned short* __restrict__ A, int lda, const unsigned short* __restrict__ W, int ldw,
     const unsigned short* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
@@ -507,9 +527,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
       __syncthreads();
     }
 
-    epilogue_rows<LN, BN>(acc, s_mu, s_rstd, s_p1, s_p2, R, ldr, C, ldc, M, N, m0, n0, epi, vec_ok, wm, wn, r,
-                          hh);
-    __syncthreads();  // LDS (stages, stats, params) is rewritten by the next persistent tile
+    epilogue_rows<LN, BN, RESID>(acc, s_mu, s_rstd, s_p1, s_p2, R, ldr, C, ldc, M, N, m0, n0, epi, vec_ok, wm,
+                                 wn, r, hh);
+    // LDS (stages, stats, params) is rewritten by the next persistent tile; a
+    // workgroup's last tile ends without a barrier (it would drain the stores)
+    if (tile + (int)gridDim.x < ntiles) __syncthreads();
   }
 }
 
@@ -538,20 +560,26 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
   auto Bp = (const unsigned short*)bias;
   auto Rp = (const unsigned short*)R;
   auto Cp = (unsigned short*)C;
-#define NOS_GEMM_LAUNCH(LNV, BNV)                                                                              \
-  do {                                                                                                          \
-    if (g_epi_impl == 1)                                                                                   \
-      hipLaunchKernelGGL((gemm_bf16_rk_kernel<LNV, BNV>), dim3(nwg), dim3(NT), rk_lds_bytes<BNV>(), stream, Ap, \
-                         lda, Wp, ldw, Bp, c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n);      \
-    else                                                                                                        \
-      hipLaunchKernelGGL((gemm_bf16_kernel<LNV, BNV>), dim3(nwg), dim3(NT), Cfg<BNV>::LDS_BYTES, stream, Ap,    \
-                         lda, Wp, ldw, Bp, c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n);      \
+#define NOS_GEMM_ARGS                                                                                     \
+  Ap, lda, Wp, ldw, Bp, c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n
+#define NOS_GEMM_LAUNCH(LNV, BNV, RV)                                                                      \
+  do {                                                                                                      \
+    if (g_epi_impl == 1)                                                                                    \
+      hipLaunchKernelGGL((gemm_bf16_rk_kernel<LNV, BNV, RV>), dim3(nwg), dim3(NT), rk_lds_bytes<BNV>(),     \
+                         stream, NOS_GEMM_ARGS);                                                            \
+    else                                                                                                    \
+      hipLaunchKernelGGL((gemm_bf16_kernel<LNV, BNV>), dim3(nwg), dim3(NT), Cfg<BNV>::LDS_BYTES, stream,    \
+                         NOS_GEMM_ARGS);                                                                    \
   } while (0)
+  const bool resid = (epi & EPI_RESID) != 0;
   if (ln) {
-    if (narrow) NOS_GEMM_LAUNCH(true, 64); else NOS_GEMM_LAUNCH(true, 128);
+    if (narrow) NOS_GEMM_LAUNCH(true, 64, false); else NOS_GEMM_LAUNCH(true, 128, false);
+  } else if (resid) {
+    if (narrow) NOS_GEMM_LAUNCH(false, 64, true); else NOS_GEMM_LAUNCH(false, 128, true);
   } else {
-    if (narrow) NOS_GEMM_LAUNCH(false, 64); else NOS_GEMM_LAUNCH(false, 128);
+    if (narrow) NOS_GEMM_LAUNCH(false, 64, false); else NOS_GEMM_LAUNCH(false, 128, false);
   }
+#undef NOS_GEMM_ARGS
 #undef NOS_GEMM_LAUNCH
   return (int)hipGetLastError();
 }
