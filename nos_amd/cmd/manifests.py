@@ -105,8 +105,8 @@ def validate_values(v: dict) -> None:
     gp = v["gpuPartitioner"]
     if gp["batchWindowTimeoutSeconds"] <= 0 or gp["batchWindowIdleSeconds"] <= 0:
         raise ValueError("gpuPartitioner batch windows must be > 0")
-    if gp["slicePlacement"] not in ("pack", "spread"):
-        raise ValueError("gpuPartitioner.slicePlacement must be pack|spread")
+    if gp["slicePlacement"] not in ("pack", "spread", "measured"):
+        raise ValueError("gpuPartitioner.slicePlacement must be pack|spread|measured")
     if gp["cuPolicy"] not in ("even", "proportional", "shared"):
         raise ValueError("gpuPartitioner.cuPolicy must be even|proportional|shared")
     if int(v["amdGpuResourceMemoryGB"]) <= 0:
