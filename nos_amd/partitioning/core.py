@@ -21,13 +21,15 @@ Same algorithm as the reference's ``internal/partitioning/core``:
 """
 from __future__ import annotations
 
+import collections
+import heapq
 import logging
 import time
 from dataclasses import dataclass, field
 from typing import Protocol
 
 from ..kube import objects as ko
-from ..resource.resource import Resource, compute_pod_request
+from ..resource.resource import Resource, compute_pod_request, request_memo
 from ..scheduler.framework import CycleState, Framework, NodeInfo
 from .state import NodePartitioning, PartitioningState
 
@@ -85,6 +87,14 @@ class ClusterSnapshot:
                  slice_calculator, slice_filter):
         self._data: dict[str, PartitionableNode] = dict(nodes)
         self._forked: dict[str, PartitionableNode] | None = None
+        self._cow: set[str] = set()
+        # cluster-wide (allocatable, requested) of _data / _forked, kept up to
+        # date by add_pod and dropped by set_node: lacking_resources() is
+        # called per pod per candidate node, and re-summing every node there
+        # made planning O(nodes^2 x pods) (the reference's getLackingResources
+        # re-sums too, snapshot.go:132-165)
+        self._agg_data: tuple[Resource, Resource] | None = None
+        self._agg_fork: tuple[Resource, Resource] | None = None
         self.partition_calculator = partition_calculator
         self.slice_calculator = slice_calculator
         self.slice_filter = slice_filter
@@ -95,31 +105,73 @@ class ClusterSnapshot:
     def fork(self) -> None:
         if self._forked is not None:
             raise RuntimeError("snapshot already forked")
-        self._forked = {k: v.clone() for k, v in self._data.items()}
+        # copy-on-write: nodes are cloned when first touched inside the fork
+        # (get_node / add_pod); a deep copy of every node per candidate node
+        # made planning O(nodes^2)
+        self._forked = dict(self._data)
+        self._cow: set[str] = set()
+        self._agg_fork = None if self._agg_data is None else (self._agg_data[0].clone(), self._agg_data[1].clone())
 
     def commit(self) -> None:
         if self._forked is not None:
             self._data = self._forked
             self._forked = None
+            self._agg_data, self._agg_fork = self._agg_fork, None
 
     def revert(self) -> None:
         self._forked = None
+        self._agg_fork = None
+
+    def _aggregates(self) -> tuple[Resource, Resource]:
+        agg = self._agg_fork if self._forked is not None else self._agg_data
+        if agg is None:
+            alloc, requested = Resource(), Resource()
+            for n in self.get_nodes().values():
+                alloc.iadd(n.node_info.allocatable)
+                requested.iadd(n.node_info.requested)
+            agg = (alloc, requested)
+            if self._forked is not None:
+                self._agg_fork = agg
+            else:
+                self._agg_data = agg
+        return agg
+
+    def _invalidate(self) -> None:
+        if self._forked is not None:
+            self._agg_fork = None
+        else:
+            self._agg_data = None
 
     def clone(self) -> "ClusterSnapshot":
         c = ClusterSnapshot({k: v.clone() for k, v in self._data.items()}, self.partition_calculator,
                             self.slice_calculator, self.slice_filter)
         if self._forked is not None:
             c._forked = {k: v.clone() for k, v in self._forked.items()}
+            c._cow = set(c._forked)
         return c
 
     def get_nodes(self) -> dict[str, PartitionableNode]:
+        """Read-only view (mutate nodes through get_node / add_pod / set_node)."""
         return self._d()
 
+    def _writable(self, name: str) -> PartitionableNode | None:
+        d = self._d()
+        n = d.get(name)
+        if n is not None and self._forked is not None and name not in self._cow:
+            n = n.clone()
+            d[name] = n
+            self._cow.add(name)
+        return n
+
     def get_node(self, name: str) -> PartitionableNode | None:
-        return self._d().get(name)
+        """The node; inside a fork, the fork's own copy (safe to mutate)."""
+        return self._writable(name)
 
     def set_node(self, n: PartitionableNode) -> None:
         self._d()[n.name] = n
+        if self._forked is not None:
+            self._cow.add(n.name)
+        self._invalidate()
 
     def get_candidate_nodes(self) -> list[str]:
         """Nodes with free capacity in name order (``snapshot.go:93-103``);
@@ -137,10 +189,7 @@ class ClusterSnapshot:
 
     def lacking_resources(self, pod: dict) -> Resource:
         req = Resource.from_list(compute_pod_request(pod))
-        alloc, requested = Resource(), Resource()
-        for n in self.get_nodes().values():
-            alloc.iadd(n.node_info.allocatable)
-            requested.iadd(n.node_info.requested)
+        alloc, requested = self._aggregates()
         available = alloc.subtract_non_negative(requested)
         diff = available - req
         res = Resource(min(diff.milli_cpu, 0), min(diff.memory, 0), min(diff.ephemeral_storage, 0),
@@ -152,10 +201,18 @@ class ClusterSnapshot:
         return self.slice_filter.extract_slices(self.lacking_resources(pod).scalar)
 
     def add_pod(self, node_name: str, pod: dict) -> None:
-        n = self._d().get(node_name)
+        n = self._writable(node_name)
         if n is None:
             raise KeyError(f"could not find node {node_name} in cluster snapshot")
+        before = n.node_info.requested.clone()
+        alloc_before = n.node_info.allocatable.clone()
         n.add_pod(pod)
+        agg = self._agg_fork if self._forked is not None else self._agg_data
+        if agg is not None:
+            agg[1].isub(before)
+            agg[1].iadd(n.node_info.requested)
+            agg[0].isub(alloc_before)
+            agg[0].iadd(n.node_info.allocatable)
 
 
 class SliceTracker:
@@ -196,14 +253,17 @@ class SliceTracker:
 
 
 def sort_pods(pods: list[dict], slice_calculator) -> list[dict]:
-    """Priority desc; equal priority: the pod requesting the smaller slice first."""
+    """Priority desc; equal priority: the pod requesting the smaller slice
+    first (``util.go:34-71``).  Requested slices are computed once per pod."""
     import functools
 
+    keyed = [(ko.pod_priority(p), slice_calculator.get_requested_slices(p), p) for p in pods]
+
     def cmp(a, b):
-        pa, pb = ko.pod_priority(a), ko.pod_priority(b)
+        pa, pb = a[0], b[0]
         if pa != pb:
             return -1 if pa > pb else 1
-        ra, rb = slice_calculator.get_requested_slices(a), slice_calculator.get_requested_slices(b)
+        ra, rb = a[1], b[1]
         if not ra or not rb:
             return 0
         sa, sb = min(ra, key=str), min(rb, key=str)
@@ -213,7 +273,7 @@ def sort_pods(pods: list[dict], slice_calculator) -> list[dict]:
             return 1
         return 0
 
-    return sorted(pods, key=functools.cmp_to_key(cmp))
+    return [k[2] for k in sorted(keyed, key=functools.cmp_to_key(cmp))]
 
 
 def is_node_initialized(node: dict) -> bool:
@@ -235,6 +295,10 @@ class Planner:
         self.last_stats: dict = {}
 
     def plan(self, snapshot: ClusterSnapshot, candidate_pods: list[dict]) -> PartitioningPlan:
+        with request_memo():
+            return self._plan(snapshot, candidate_pods)
+
+    def _plan(self, snapshot: ClusterSnapshot, candidate_pods: list[dict]) -> PartitioningPlan:
         t0 = time.perf_counter()
         state = snapshot.get_partitioning_state()
         tracker = SliceTracker(snapshot, self.slice_calculator, candidate_pods)
@@ -243,26 +307,51 @@ class Planner:
             self.last_stats = {"placed": 0, "seconds": time.perf_counter() - t0, "lacking": 0}
             return PartitioningPlan(state)
         pods = sort_pods(candidate_pods, self.slice_calculator)
+        # pods grouped by (namespace, request) signature, each group an index
+        # queue in sort order.  Within one node's pass capacity only shrinks
+        # (the geometry is updated once, before the pass), so once a pod of a
+        # group fails on the node every later pod of that group would too:
+        # the pass walks the groups' heads in sort order (a heap) and drops a
+        # group at its first failure -- O((placed + groups) log groups) per
+        # node instead of re-simulating every pending pod on every node.
+        groups: dict[tuple, collections.deque] = {}
+        for i, pod in enumerate(pods):
+            sig = (ko.namespace(pod), frozenset(compute_pod_request(pod).items()))
+            groups.setdefault(sig, collections.deque()).append(i)
         for name in snapshot.get_candidate_nodes():
-            if not tracker.get_lacking_slices():
+            if not tracker.get_lacking_slices() or not groups:
                 break
             snapshot.fork()
             n = snapshot.get_node(name)  # the forked copy (fixes the pre-fork mutation gotcha)
             if n.update_geometry_for(dict(tracker.get_lacking_slices())):
                 snapshot.set_node(n)
-            added = 0
-            remaining = []
-            for pod in pods:
-                if self._try_add_pod(pod, name, snapshot):
-                    state[name] = self.partition_calculator.get_partitioning(snapshot.get_node(name))
-                    tracker.remove(pod)
-                    added += 1
-                else:
-                    remaining.append(pod)
+            added: list[tuple[tuple, int]] = []
+            heap = [(q[0], k) for k, q in enumerate(groups.values())]
+            keys = list(groups)
+            heapq.heapify(heap)
+            taken: dict[tuple, int] = {}
+            while heap:
+                i, k = heapq.heappop(heap)
+                sig = keys[k]
+                if not self._try_add_pod(pods[i], name, snapshot):
+                    continue  # the group is done on this node
+                state[name] = self.partition_calculator.get_partitioning(snapshot.get_node(name))
+                tracker.remove(pods[i])
+                added.append((sig, i))
+                t = taken.get(sig, 0) + 1
+                taken[sig] = t
+                q = groups[sig]
+                if t < len(q):
+                    heapq.heappush(heap, (q[t], k))
             if added:
                 snapshot.commit()
-                pods = remaining
-                placed += added
+                for sig, t in taken.items():
+                    q = groups[sig]
+                    for _ in range(t):
+                        q.popleft()
+                    if not q:
+                        del groups[sig]
+                placed += len(added)
             else:
                 snapshot.revert()
         self.last_stats = {"placed": placed, "seconds": time.perf_counter() - t0,

@@ -12,6 +12,9 @@ The reference computes the overhead sum and discards it
 """
 from __future__ import annotations
 
+import contextlib
+import threading
+
 from dataclasses import dataclass, field
 from fractions import Fraction
 from typing import Protocol
@@ -134,8 +137,38 @@ class Resource:
             (f",{sc}" if sc else "") + ")"
 
 
+_memo = threading.local()
+
+
+@contextlib.contextmanager
+def request_memo():
+    """Memoise :func:`compute_pod_request` per pod object for the duration of
+    the block (this thread only).  The planner evaluates the same pods
+    thousands of times per plan; their specs do not change inside a plan.
+    Keys are object ids, valid because the pods stay referenced by the caller
+    for the whole block."""
+    prev = getattr(_memo, "d", None)
+    _memo.d = {} if prev is None else prev
+    try:
+        yield
+    finally:
+        _memo.d = prev
+
+
 def compute_pod_request(pod: dict) -> dict[str, Fraction]:
     """max(sum(containers) + overhead, max(init containers)) as a ResourceList."""
+    memo = getattr(_memo, "d", None)
+    if memo is not None:
+        hit = memo.get(id(pod))
+        if hit is not None and hit[0] is pod:
+            return dict(hit[1])
+        out = _compute_pod_request(pod)
+        memo[id(pod)] = (pod, out)
+        return dict(out)
+    return _compute_pod_request(pod)
+
+
+def _compute_pod_request(pod: dict) -> dict[str, Fraction]:
     containers: dict[str, Fraction] = {}
     for c in ko.pod_containers(pod):
         containers = q.rl_add(containers, ko.container_requests(c))

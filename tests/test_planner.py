@@ -142,3 +142,52 @@ def test_snapshot_fork_revert_is_isolated():
     snap.set_node(n)
     snap.revert()
     assert snap.get_node("n1").gpus[0].num_slices() == 0
+
+
+def _fresh_lacking(snap: ClusterSnapshot, pod: dict):
+    """lacking_resources recomputed from scratch (no cached aggregates)."""
+    from nos_amd.resource.resource import Resource, compute_pod_request
+
+    req = Resource.from_list(compute_pod_request(pod))
+    alloc, requested = Resource(), Resource()
+    for n in snap.get_nodes().values():
+        alloc.iadd(n.node_info.allocatable)
+        requested.iadd(n.node_info.requested)
+    diff = alloc.subtract_non_negative(requested) - req
+    return {k: -v for k, v in diff.scalar.items() if v < 0}
+
+
+def test_snapshot_cached_aggregates_track_fork_add_commit_revert():
+    nodes = [_node(f"n{i}", C.PARTITIONING_CUMASK, 2, alloc={"amd.com/gpu-10gb": "2"},
+                   ann={"nos.nebuly.com/status-gpu-0-10gb-free": "2"}) for i in range(3)]
+    snap = _cumask_snapshot(nodes)
+    probe = _pod("probe", "amd.com/gpu-10gb", 5)
+    assert snap.lacking_resources(probe).scalar == _fresh_lacking(snap, probe)
+    snap.fork()
+    snap.add_pod("n0", _pod("a", "amd.com/gpu-10gb"))
+    assert snap.lacking_resources(probe).scalar == _fresh_lacking(snap, probe)
+    snap.revert()
+    assert snap.lacking_resources(probe).scalar == _fresh_lacking(snap, probe)
+    snap.fork()
+    n = snap.get_node("n1")
+    assert n.update_geometry_for({cm.SliceProfile("10gb"): 6})
+    snap.set_node(n)
+    snap.add_pod("n1", _pod("b", "amd.com/gpu-10gb"))
+    assert snap.lacking_resources(probe).scalar == _fresh_lacking(snap, probe)
+    snap.commit()
+    assert snap.lacking_resources(probe).scalar == _fresh_lacking(snap, probe)
+    snap.add_pod("n2", _pod("c", "amd.com/gpu-10gb"))
+    assert snap.lacking_resources(probe).scalar == _fresh_lacking(snap, probe)
+
+
+def test_planner_scales_linearly_enough():
+    """Guard for the O(nodes^2 x pods) regression the cached aggregates fixed
+    (tools/planner_bench.py, profiles/r01_planner_bench.json)."""
+    import time
+
+    import tools.planner_bench as pb
+
+    t0 = time.perf_counter()
+    r = pb.run_one(C.PARTITIONING_CUMASK, 100, 500)
+    assert r["placed"] == 500
+    assert time.perf_counter() - t0 < 20.0
