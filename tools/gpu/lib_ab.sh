@@ -4,8 +4,8 @@ set -o pipefail
 export TMPDIR=/tmp
 O=$GRAFT_REPO_ROOT/gpurun_out/$1; V=build/variants/$2/libnos_hip.so; W=${3:-gemm}
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
-rc=$?; tail -2 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+NOS_AMD_HIP_LIB=$V timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > $O/pytest_var.log 2>&1
+rc=$?; tail -2 $O/pytest_var.log; [ $rc -eq 0 ] || exit $rc
 for R in 1 2; do for B in 1 8; do
   NOS_AMD_HIP_LIB=$V timeout -k 10 120 python tools/kernel_bench.py --only $W --batch $B --iters 20 --rounds 2 --out $O/var_b${B}_r$R.json > /dev/null 2>> $O/err.log || exit 1
   timeout -k 10 120 python tools/kernel_bench.py --only $W --batch $B --iters 20 --rounds 2 --out $O/new_b${B}_r$R.json > /dev/null 2>> $O/err.log || exit 1
