@@ -455,22 +455,36 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
     const int srow = tid >> 1, shalf = tid & 1;
     float sshift = 0.f, ssum = 0.f, ssq = 0.f;
 
-    stage_tile<BM>(A, lda, m0, M, 0, smem, wid, lane);
-    stage_tile<BN>(W, ldw, n0, N, 0, smem + TILE_A_BYTES, wid, lane);
-    // per-column epilogue parameters: (c1, c2) for the LN-fused form, (0, bias) otherwise
+    // per-column epilogue parameters: (c1, c2) for the LN-fused form, (0,
+    // bias) otherwise -- loaded before any LDS-DMA is in flight, so waiting
+    // for them drains nothing
     if (tid < BN) {
       const int n = min(n0 + tid, N - 1);
       s_p1[tid] = LN ? c1[n] : 0.f;
       s_p2[tid] = LN ? c2[n] : ((epi & EPI_BIAS) ? nos::bf16_to_f32(bias[n]) : 0.f);
     }
-    __syncthreads();
+    // both stages of the first two K-steps are issued up front: step 1's
+    // loads overlap step 0's wait instead of starting after it
+    stage_tile<BM>(A, lda, m0, M, 0, smem, wid, lane);
+    stage_tile<BN>(W, ldw, n0, N, 0, smem + TILE_A_BYTES, wid, lane);
+    if (nk > 1) {
+      stage_tile<BM>(A, lda, m0, M, BK, smem + STAGE_BYTES, wid, lane);
+      stage_tile<BN>(W, ldw, n0, N, BK, smem + STAGE_BYTES + TILE_A_BYTES, wid, lane);
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(BM / 32 + BN / 32) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // step 0 landed for every wave; params visible
 
     for (int kt = 0; kt < nk; ++kt) {
       unsigned char* cur = smem + (kt & 1) * STAGE_BYTES;
-      if (kt + 1 < nk) {
-        unsigned char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
-        stage_tile<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wid, lane);
-        stage_tile<BN>(W, ldw, n0, N, (kt + 1) * BK, nxt + TILE_A_BYTES, wid, lane);
+      if (kt > 0) {
+        __syncthreads();  // step kt landed (vmcnt(0)); everyone done with step kt-1's buffer
+        if (kt + 1 < nk) {
+          unsigned char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
+          stage_tile<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wid, lane);
+          stage_tile<BN>(W, ldw, n0, N, (kt + 1) * BK, nxt + TILE_A_BYTES, wid, lane);
+        }
       }
       const unsigned char* ta = cur;
       const unsigned char* tb = cur + TILE_A_BYTES;
@@ -507,7 +521,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
           for (int ni = 0; ni < NB; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[ni], af[mi], acc[mi][ni], 0, 0, 0);
       }
-      __syncthreads();
     }
 
     if constexpr (LN) {
