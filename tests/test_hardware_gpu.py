@@ -1,0 +1,93 @@
+"""The real device path on an MI355X (weakness 3: "nothing
+exercises the real device path" in the reference).
+
+* libnos_amdsmi against the real amd-smi: read-only queries a partition agent
+  and the device plugin depend on (mode, XCDs/CUs, VRAM, activity, processes);
+* the device plugin on the real GPU: a CU-mask slice allocation's
+  ``ROC_GLOBAL_CU_MASK`` is handed to a child process (as the kubelet hands it
+  to a container) and the gfx950 placement probe, run inside that process,
+  must see exactly the slice's CUs on every XCD.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from nos_amd.api import constants as C
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _smi():
+    from nos_amd.gpu.amdsmi import AmdSmi
+
+    return AmdSmi.real()
+
+
+def _local_gpu(smi):
+    """The amd-smi GPU that is HIP device 0 of this process."""
+    gpus = smi.gpus()
+    for g in gpus:
+        if g.hip_id == 0:
+            return g
+    return gpus[0]
+
+
+def test_amdsmi_real_readonly_queries():
+    smi = _smi()
+    try:
+        assert smi.count() >= 1
+        g = _local_gpu(smi)
+        assert g.num_xcds == 8 and g.num_cus == 256, g
+        assert g.compute_mode in ("SPX", "DPX", "QPX", "CPX"), g
+        assert g.memory_mode.startswith("NPS"), g
+        assert 250 <= g.memory_gb <= 300, g   # 288 GB HBM3E
+        assert g.uuid and g.bdf, g
+        act = smi.activity(g.index)
+        assert 0 <= act["gfx"] <= 100 and 0 <= act["umc"] <= 100, act
+        torch.ones(1, device="cuda").sum().item()  # this process now holds a GPU context
+        procs = smi.processes(g.index)
+        assert isinstance(procs, list)
+    finally:
+        smi.close()
+
+
+def test_device_plugin_slice_mask_is_enforced_in_a_child_process():
+    from nos_amd.deviceplugin.plugin import NosAmdDevicePlugin
+
+    smi = _smi()
+    try:
+        g = _local_gpu(smi)
+        plugin = NosAmdDevicePlugin("node", smi, mode=C.PARTITIONING_CUMASK, cu_policy="even")
+        plugin.set_config("node-1", {"cuPolicy": "even", "allocation": "pack", "gpus": [
+            {"index": g.index, "slices": [{"profile": "10gb", "memoryGB": 10, "replicas": 4}]}]})
+        res = "amd.com/gpu-10gb"
+        devs = [d.id for d in plugin.list_devices(res)]
+        assert len(devs) == 4
+        pick = plugin.preferred_allocation(res, devs, [], 1)
+        alloc = plugin.allocate(res, pick, owner="pod-a")
+        mask = alloc.envs[C.ENV_CU_MASK]
+        assert alloc.envs[C.ENV_VISIBLE_DEVICES] == str(g.index)
+        expect = set(plugin.cus_of(pick[0]))
+        assert len(expect) == 64   # 4 slices of a 256-CU GPU, 8 CUs on each XCD
+    finally:
+        smi.close()
+    code = (
+        "import json, sys; sys.path.insert(0, %r)\n"
+        "from nos_amd.ops import probes\n"
+        "print(json.dumps(probes.placement_summary(probes.placement(nwg=4096))))\n" % REPO)
+    env = dict(os.environ)
+    env[C.ENV_CU_MASK] = mask   # what the kubelet puts in the container's environment
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    summary = json.loads(out.stdout.strip().splitlines()[-1])
+    assert summary["distinct_cus"] == 64, summary
+    assert summary["cus_per_xcc"] == {str(x): 8 for x in range(8)} or \
+        summary["cus_per_xcc"] == {x: 8 for x in range(8)}, summary
