@@ -60,8 +60,14 @@ class ContainerAllocation:
 
 class NosAmdDevicePlugin:
     def __init__(self, node_name: str, smi: AmdSmi, mode: str | None = None, expose_partitions_as_gpu: bool = False,
-                 cu_policy: str = "even"):
+                 cu_policy: str = "even", device_env: str = "host"):
+        if device_env not in ("host", "container"):
+            raise ValueError(f"device_env must be 'host' or 'container', not {device_env!r}")
         self.node_name = node_name
+        # "container": the runtime mounts only the allocated render nodes, so
+        # HIP inside the container numbers them 0..k-1 in host order;
+        # "host": tenants run on the host and see every GPU (simulator, bare metal)
+        self.device_env = device_env
         self.smi = smi
         self.mode = mode              # None | "partition" | "cumask"
         self.expose_partitions_as_gpu = expose_partitions_as_gpu
