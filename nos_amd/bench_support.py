@@ -64,8 +64,12 @@ def schedulable_pods(n_gpus: int, slice_gb: int, num_cus: int = 256, placement: 
 
 
 def control_plane_plan(n_gpus: int, pods_per_gpu: int, slice_gb: int, num_cus: int, local_gpu: int = 0,
-                       placement: str = "spread", cu_policy: str = "even") -> tuple[list[list[int]], dict]:
-    info = schedulable_pods(n_gpus, slice_gb, num_cus, placement)
+                       placement: str = "spread", cu_policy: str = "even", capacity_probe: bool = True
+                       ) -> tuple[list[list[int] | None], dict]:
+    """Masks of the pods placed on ``local_gpu`` (None = unmasked) and the
+    control-plane facts; ``info["envs"]`` holds each of those pods' full
+    device-plugin environment (what its container is started with)."""
+    info = schedulable_pods(n_gpus, slice_gb, num_cus, placement) if capacity_probe else {}
     cl = _cluster(n_gpus, num_cus, placement, cu_policy)
     res = f"{C.AMD_SLICE_RESOURCE_PREFIX}{slice_gb}gb"
     for i in range(n_gpus * pods_per_gpu):
@@ -75,6 +79,7 @@ def control_plane_plan(n_gpus: int, pods_per_gpu: int, slice_gb: int, num_cus: i
     wall = time.perf_counter() - t0
     node = cl.nodes["mi355x-0"]
     masks: list[list[int] | None] = []
+    envs: list[dict[str, str]] = []
     per_gpu: dict[str, int] = {}
     for _key, conts in sorted(node.kubelet.running_containers().items()):
         for rc in conts:
@@ -83,6 +88,7 @@ def control_plane_plan(n_gpus: int, pods_per_gpu: int, slice_gb: int, num_cus: i
             per_gpu[gpu] = per_gpu.get(gpu, 0) + 1
             if gpu == str(local_gpu):  # no mask env: the slice runs on every CU (cuPolicy shared)
                 masks.append(cus_from_hex(env[C.ENV_CU_MASK]) if C.ENV_CU_MASK in env else None)
+                envs.append({k: str(v) for k, v in env.items()})
     ann = ko.annotations(cl.api.get("Node", "mi355x-0"))
     info.update({"placed_pods": len(cl.running_pods()), "pending_pods": len(cl.pending_pods()),
                  "pods_per_gpu_placed": per_gpu, "time_to_running_sim_seconds": round(sim_s, 3),
@@ -90,5 +96,5 @@ def control_plane_plan(n_gpus: int, pods_per_gpu: int, slice_gb: int, num_cus: i
                  "plan_id": ann.get(C.ANNOTATION_PARTITIONING_PLAN),
                  "plan_reported": ann.get(C.ANNOTATION_REPORTED_PARTITIONING_PLAN) ==
                  ann.get(C.ANNOTATION_PARTITIONING_PLAN),
-                 "slice_resource": res, "cus_per_pod": len(masks[0]) if masks and masks[0] else num_cus, "cu_policy": cu_policy})
+                 "slice_resource": res, "cus_per_pod": len(masks[0]) if masks and masks[0] else num_cus, "cu_policy": cu_policy, "envs": envs})
     return masks, info

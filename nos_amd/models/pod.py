@@ -1,0 +1,185 @@
+"""One fractional-GPU tenant pod as its own process (the demo's client container).
+
+The reference's demo pod (``demos/gpu-sharing-comparison/client/main.py:14-25``)
+loads YOLOS-small in fp32 and runs inferences back to back forever; the
+"average inference time" of the published table is taken over the last
+2 minutes of that loop (``README.md:53-60``).  This is the MI355X pod:
+
+* it runs with exactly the environment the nos-amd device plugin allocated
+  (``HIP_VISIBLE_DEVICES``, ``ROC_GLOBAL_CU_MASK`` for CU-mask slices,
+  ``NOS_AMD_MEMORY_LIMIT_GB``, see ``deviceplugin/plugin.py:allocate``) -- the
+  parent does not touch the mask, HIP applies it to every queue of the pod;
+* the memory cap is enforced through the caching allocator
+  (:func:`nos_amd.utils.memlimit.apply_memory_limit`);
+* every inference is one HIP-graph replay of the whole forward followed by a
+  stream synchronize, and its completion time (CLOCK_MONOTONIC, comparable
+  across processes) is recorded, so the orchestrator
+  (:mod:`nos_amd.podbench`) can integrate exact fractional progress over any
+  wall-clock window.
+
+Precision: ``fp32`` (default, the reference's HF default precision) runs the
+PyTorch-ROCm path of :class:`YolosDetector` (hipBLASLt fp32 GEMMs, fp32 SDPA);
+``bf16`` runs the gfx950 kernels of ``libnos_hip.so``.
+
+Status protocol (``--status``: a float64 memory-mapped file, see
+:class:`StatusBoard`): row 0 = [stop flag, ...]; row 1+slot = [state, count,
+last completion time, pid].  On stop the pod writes all completion times to
+``<out>/pod-<slot>.json`` and exits 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+STATE_STARTING, STATE_READY, STATE_FAILED, STATE_DONE = 0.0, 1.0, 2.0, 3.0
+_COLS = 4
+
+
+class StatusBoard:
+    """Shared float64 table in a file (mmap), one writer per row."""
+
+    def __init__(self, path: str | os.PathLike, pods: int | None = None):
+        self.path = Path(path)
+        if pods is not None:
+            np.zeros((1 + pods, _COLS), dtype=np.float64).tofile(self.path)
+        self.arr = np.memmap(self.path, dtype=np.float64, mode="r+")
+        self.arr = self.arr.reshape(-1, _COLS)
+
+    @property
+    def pods(self) -> int:
+        return self.arr.shape[0] - 1
+
+    def stop(self) -> None:
+        self.arr[0, 0] = 1.0
+        self.arr.flush()
+
+    def stopped(self) -> bool:
+        return bool(self.arr[0, 0])
+
+    def row(self, slot: int) -> np.ndarray:
+        return self.arr[1 + slot]
+
+    def states(self) -> list[float]:
+        return [float(self.arr[1 + i, 0]) for i in range(self.pods)]
+
+    def counts(self) -> list[float]:
+        return [float(self.arr[1 + i, 1]) for i in range(self.pods)]
+
+
+def _build(dtype: str, seed: int, hw, device: str = "cuda"):
+    import torch
+
+    from .yolos import YolosConfig, YolosDetector, make_demo_input
+
+    cfg = YolosConfig.small() if device == "cuda" else YolosConfig.test()
+    if dtype == "fp32":
+        m = YolosDetector(cfg, backend="torch")
+        tdt = torch.float32
+    elif dtype == "bf16":
+        from ..ops import _lib
+
+        _lib.require_native_on_gpu()
+        m = YolosDetector(cfg, backend="native")
+        tdt = torch.bfloat16
+    else:
+        raise ValueError(f"dtype {dtype!r}")
+    m.reset_parameters(seed)
+    m = m.to(device, tdt).eval()
+    x = make_demo_input(cfg, device=device, dtype=tdt, hw=hw if device == "cuda" else cfg.image_size, seed=seed)
+    return m, x
+
+
+class _CpuTenant:
+    def __init__(self, model, x):
+        self.model, self.x = model, x
+
+    def launch(self) -> None:
+        self.model(self.x)
+
+    def synchronize(self) -> None:
+        pass
+
+
+def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool = True, seed: int = 0,
+            warmup: int = 3, device: str = "cuda") -> int:
+    """``device="cpu"`` runs the tiny test config on the CPU (protocol tests)."""
+    board = StatusBoard(status)
+    row = board.row(slot)
+    row[3] = os.getpid()
+    try:
+        import torch
+
+        from ..utils.memlimit import apply_memory_limit
+        from .yolos import GraphedTenant, demo_input_hw
+
+        gpu = device == "cuda"
+        frac = None
+        if gpu:
+            torch.cuda.set_device(0)  # the device plugin's HIP_VISIBLE_DEVICES leaves exactly the slice's GPU
+            frac = apply_memory_limit(0)
+            torch.backends.cuda.matmul.allow_tf32 = False  # true fp32 GEMMs (no reduced-precision shortcut)
+        m, x = _build(dtype, seed, demo_input_hw(), device)
+        if gpu:
+            s = torch.cuda.Stream()
+            t = GraphedTenant(m, s, x)
+        else:
+            s = t = _CpuTenant(m, x)
+        with torch.no_grad():
+            if graphs and gpu:
+                t.capture()
+            for _ in range(warmup):
+                t.launch()
+            s.synchronize()
+        props = torch.cuda.get_device_properties(0) if gpu else None
+        info = {"slot": slot, "pid": os.getpid(), "dtype": dtype, "graphs": graphs and gpu, "memory_fraction": frac,
+                "device": props.name if gpu else "cpu",
+                "multiprocessor_count": props.multi_processor_count if gpu else 0,
+                "cu_mask": os.environ.get("ROC_GLOBAL_CU_MASK"),
+                "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES"),
+                "memory_limit_gb": os.environ.get("NOS_AMD_MEMORY_LIMIT_GB"),
+                "max_allocated_gb": None}
+        row[0] = STATE_READY
+        times: list[float] = []
+        info["t_ready"] = time.monotonic()
+        with torch.no_grad():
+            while not board.stopped():
+                t.launch()
+                s.synchronize()
+                now = time.monotonic()
+                times.append(now)
+                row[1] = len(times)
+                row[2] = now
+        if gpu:
+            info["max_allocated_gb"] = round(torch.cuda.max_memory_allocated(0) / 2 ** 30, 3)
+        info["times"] = times
+        Path(out, f"pod-{slot}.json").write_text(json.dumps(info))
+        row[0] = STATE_DONE
+        return 0
+    except Exception as e:  # the orchestrator sees the failure in the board and in the file
+        Path(out, f"pod-{slot}.json").write_text(json.dumps({"slot": slot, "error": repr(e)}))
+        row[0] = STATE_FAILED
+        print(f"[pod {slot}] failed: {e!r}", file=sys.stderr, flush=True)
+        return 1
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="nos-amd fractional-GPU YOLOS pod")
+    ap.add_argument("--status", required=True)
+    ap.add_argument("--slot", type=int, required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
+    a = ap.parse_args(argv)
+    return run_pod(a.status, a.slot, a.out, a.dtype, not a.no_graphs, a.seed, device=a.device)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,71 @@
+"""Pod-process measurement protocol (nos_amd/podbench.py, nos_amd/models/pod.py).
+
+The pods run the tiny YOLOS test config on the CPU here; on a GPU box the same
+protocol runs the fp32 YOLOS-small pods of bench.py."""
+import time
+
+import pytest
+
+from nos_amd.podbench import PodFleet, PodLauncher, WindowStats, PodResult, progress
+
+
+def test_progress_interpolates_between_completions():
+    times = [1.0, 2.0, 4.0]
+    assert progress(times, 0.0, 0.0) == 0.0
+    assert progress(times, 0.5, 0.0) == pytest.approx(0.5)
+    assert progress(times, 1.0, 0.0) == pytest.approx(1.0)
+    assert progress(times, 3.0, 0.0) == pytest.approx(2.5)
+    assert progress(times, 9.0, 0.0) == 3.0
+    # the count inside a window is additive over sub-windows
+    a = progress(times, 3.0, 0.0) - progress(times, 0.7, 0.0)
+    b = progress(times, 1.9, 0.0) - progress(times, 0.7, 0.0)
+    c = progress(times, 3.0, 0.0) - progress(times, 1.9, 0.0)
+    assert a == pytest.approx(b + c)
+
+
+def test_window_latency_identity():
+    w = WindowStats(10.0, [PodResult(0, 50.0, 0.2, 0.3, True), PodResult(1, 25.0, 0.4, 0.5, True)])
+    # mean per-request latency: pods / latency == throughput exactly
+    assert w.throughput == pytest.approx(7.5)
+    assert len(w.pods) / w.mean_latency_s == pytest.approx(w.throughput)
+    assert w.concurrent == 2
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("use_launcher", [True, False])
+def test_cpu_pod_fleet_end_to_end(tmp_path, use_launcher):
+    launcher = PodLauncher() if use_launcher else None
+    envs = [{"NOS_AMD_MEMORY_LIMIT_GB": "10", "HIP_VISIBLE_DEVICES": "0"} for _ in range(3)]
+    fleet = PodFleet(envs, dtype="fp32", workdir=str(tmp_path), device="cpu", launcher=launcher,
+                     extra_env={"OMP_NUM_THREADS": "1"})
+    try:
+        fleet.start()
+        fleet.wait_ready(timeout_s=240)
+        time.sleep(0.3)
+        t0 = time.monotonic()
+        time.sleep(1.5)
+        t1 = time.monotonic()
+        time.sleep(0.3)
+        fleet.stop()
+        w = fleet.window(t0, t1)
+    finally:
+        fleet.close()
+        if launcher:
+            launcher.close()
+    assert len(w.pods) == 3
+    for p in w.pods:
+        assert p.completed > 1, p
+        assert p.info["memory_limit_gb"] == "10"
+        assert p.info["hip_visible_devices"] == "0"
+    assert w.concurrent == 3
+    assert len(w.pods) / w.mean_latency_s == pytest.approx(w.throughput)
+
+
+def test_failed_pod_is_reported(tmp_path):
+    fleet = PodFleet([{}], dtype="nope", workdir=str(tmp_path), device="cpu")
+    try:
+        fleet.start()
+        with pytest.raises(RuntimeError, match="pod 0 failed"):
+            fleet.wait_ready(timeout_s=120)
+    finally:
+        fleet.close()
