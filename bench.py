@@ -25,13 +25,16 @@ What one run does, per GPU (one rank per GPU, RCCL for the rank barrier):
    A pod counts as running concurrently when it completed inferences all
    through the window (no gap > 25 % of it).
 
-value = fractional pods observed running concurrently on the node (all GPUs);
-the slice size defaults to 20 GB so that this is also the node's schedulable
-capacity (288 GB / 20 GB = 14 per GPU; the pool runs at most 16 GPU processes
-per card, so 28 concurrent 10 GB pods cannot be started on it -- the 10 GB
-capacity is reported from the simulator).  vs_baseline = value / (8 x GPUs):
-8 is the reference's schedulable 10 GB fractional pods per A100-80GB (MPS,
-BASELINE.md).  gpu_util_pct is the mean amd-smi gfx activity over the window.
+value = fractional pods observed running concurrently on the node (all GPUs).
+On MI355X the bound is not memory but the amdgpu hardware scheduler: it runs
+at most 8 GPU processes per logical GPU at once (hws_max_conc_proc; more are
+time-sliced at a ~50 ms quantum, aggregate throughput falls:
+profiles/r02_pods_vs_throughput_hwqueues.json), so the control plane
+schedules at most 8 slices per SPX GPU (node label
+amd.com/gpu.max-concurrent-processes, nos_amd/gpu/kfd.py) and the default
+slice is 288 GB / 8 = 36 GB: schedulable == observed.  vs_baseline =
+value / (8 x GPUs): 8 is the reference's schedulable 10 GB fractional pods per
+A100-80GB (MPS).  gpu_util_pct is the mean amd-smi gfx activity over the window.
 aggregate_inf_per_s (fp32) is compared with 21.89 inf/s per GPU (the
 reference's best aggregate, 7 MPS pods on one A100).
 """
@@ -56,8 +59,8 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--step-s", type=float, default=0.6, help="wall seconds per timed step")
-    ap.add_argument("--pods-per-gpu", type=int, default=14)
-    ap.add_argument("--slice-gb", type=int, default=20, help="GPU memory per fractional pod")
+    ap.add_argument("--pods-per-gpu", type=int, default=8)
+    ap.add_argument("--slice-gb", type=int, default=36, help="GPU memory per fractional pod")
     ap.add_argument("--mode", choices=["shared", "cumask"], default="shared",
                     help="device-plugin CU policy -- shared: memory-capped slices whose kernels run on all CUs "
                          "(MPS behaviour of the reference demo); cumask: each slice gets exclusive XCD-symmetric CUs")

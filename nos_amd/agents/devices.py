@@ -13,6 +13,7 @@ import logging
 
 from ..api import constants as C
 from ..gpu.core import GpuDevice
+from ..gpu.kfd import max_concurrent_processes
 from ..kube import objects as ko
 from ..resource.client import Client
 from ..runtime.manager import Controller, Request, Result
@@ -59,7 +60,8 @@ def node_labels(smi) -> dict[str, str]:
     g0 = gpus[0]
     return {C.LABEL_AMD_PRODUCT: g0.market_name.replace(" ", "-"), C.LABEL_AMD_COUNT: str(len(gpus)),
             C.LABEL_AMD_MEMORY: str(g0.vram_mb), C.LABEL_AMD_XCDS: str(g0.num_xcds), C.LABEL_AMD_CUS: str(g0.num_cus),
-            C.LABEL_AMD_COMPUTE_MODE: g0.compute_mode, C.LABEL_AMD_MEMORY_MODE: g0.memory_mode}
+            C.LABEL_AMD_COMPUTE_MODE: g0.compute_mode, C.LABEL_AMD_MEMORY_MODE: g0.memory_mode,
+            C.LABEL_AMD_MAX_PROCS: str(max_concurrent_processes(smi))}
 
 
 class NodeLabeler:

@@ -64,6 +64,8 @@ LABEL_AMD_XCDS = "amd.com/gpu.xcds"
 LABEL_AMD_CUS = "amd.com/gpu.cus"
 LABEL_AMD_COMPUTE_MODE = "amd.com/gpu.compute-partition"
 LABEL_AMD_MEMORY_MODE = "amd.com/gpu.memory-partition"
+# processes the amdgpu HWS runs concurrently per logical GPU (hws_max_conc_proc, gpu/kfd.py)
+LABEL_AMD_MAX_PROCS = "amd.com/gpu.max-concurrent-processes"
 LABEL_DEVICE_PLUGIN_CONFIG = "nos.nebuly.com/device-plugin.config"
 
 # --------------------------------------------------------------- env

@@ -7,9 +7,11 @@ for why masks are XCD-symmetric).  The memory side follows the reference
 exactly (``slicing/gpu.go:67-220``): the sum of the slices' memory must fit the
 GPU, slices are created from spare memory smallest-first, free slices may be
 dropped to make room and re-created afterwards, used slices are never touched.
-The compute side adds one constraint the reference did not have: every
+The compute side adds two constraints the reference did not have: every
 slice needs at least one CU on every XCD, so a GPU holds at most
-``cus_per_xcd`` (32 on MI355X) slices.
+``cus_per_xcd`` (32 on MI355X) slices, and no more slices than the amdgpu
+hardware scheduler runs processes concurrently (node label
+``amd.com/gpu.max-concurrent-processes``, 8 by default; :mod:`nos_amd.gpu.kfd`).
 """
 from __future__ import annotations
 
@@ -224,6 +226,10 @@ class SliceNode:
         cus = int(ko.labels(node).get(C.LABEL_AMD_CUS, MI355X_XCDS * MI355X_CUS_PER_XCD))
         xcds = int(ko.labels(node).get(C.LABEL_AMD_XCDS, MI355X_XCDS))
         max_slices = max(1, cus // max(1, xcds))
+        # more slices than HWS process slots would be time-sliced, not shared (gpu/kfd.py)
+        procs = ko.labels(node).get(C.LABEL_AMD_MAX_PROCS)
+        if procs and int(procs) > 0:
+            max_slices = min(max_slices, int(procs))
         status, _ = parse_node_annotations(node)
         by_gpu: dict[int, tuple[dict, dict]] = {}
         for a in status:

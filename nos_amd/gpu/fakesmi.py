@@ -21,8 +21,10 @@ class FakeSmi:
     backend = "pyfake"
 
     def __init__(self, gpus: int = 8, compute: str = "SPX", memory: str = "NPS1", cus: int = 256, xcds: int = 8,
-                 vram_mb: int = 294912, model: str = "AMD Instinct MI355X", node: str = "node"):
+                 vram_mb: int = 294912, model: str = "AMD Instinct MI355X", node: str = "node",
+                 max_procs: int = 8):
         self._lock = threading.RLock()
+        self.max_concurrent_processes = max_procs  # KFD HWS concurrent processes per logical GPU
         self.node = node
         self.model = model
         self.cus, self.xcds, self.vram_mb = cus, xcds, vram_mb

@@ -17,9 +17,10 @@ loads YOLOS-small in fp32 and runs inferences back to back forever; the
   (:mod:`nos_amd.podbench`) can integrate exact fractional progress over any
   wall-clock window.
 
-Precision: ``fp32`` (default, the reference's HF default precision) runs the
-PyTorch-ROCm path of :class:`YolosDetector` (hipBLASLt fp32 GEMMs, fp32 SDPA);
-``bf16`` runs the gfx950 kernels of ``libnos_hip.so``.
+Precision: ``fp32`` (default, the reference's HF default precision) runs
+exact fp32: hipBLASLt fp32 GEMMs and the gfx950 fp32-MFMA flash attention of
+``libnos_hip.so`` (``csrc/hip/attention_f32.hip``); ``bf16`` runs the bf16
+gfx950 kernels (fused-epilogue GEMMs, bf16 flash attention, LayerNorm).
 
 Status protocol (``--status``: a float64 memory-mapped file, see
 :class:`StatusBoard`): row 0 = [stop flag, ...]; row 1+slot = [state, count,
@@ -78,8 +79,12 @@ def _build(dtype: str, seed: int, hw, device: str = "cuda"):
     from .yolos import YolosConfig, YolosDetector, make_demo_input
 
     cfg = YolosConfig.small() if device == "cuda" else YolosConfig.test()
-    if dtype == "fp32":
-        m = YolosDetector(cfg, backend="torch")
+    if dtype == "fp32":  # exact fp32: hipBLASLt fp32 GEMMs + the gfx950 fp32 MFMA attention
+        if device == "cuda":
+            from ..ops import _lib
+
+            _lib.require_native_on_gpu()
+        m = YolosDetector(cfg, backend="native" if device == "cuda" else "torch")
         tdt = torch.float32
     elif dtype == "bf16":
         from ..ops import _lib

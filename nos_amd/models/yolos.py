@@ -181,6 +181,8 @@ class YolosDetector(nn.Module):
     def forward(self, pixel_values: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
         if self.backend == "torch" or not pixel_values.is_cuda:
             return self._forward_torch(pixel_values)
+        if self.patch_w.dtype == torch.float32:
+            return self._forward_torch(pixel_values, native_attention=True)
         return self._forward_native(pixel_values)
 
     def _embed(self, pixel_values: torch.Tensor, lin) -> torch.Tensor:
@@ -238,7 +240,10 @@ class YolosDetector(nn.Module):
         y, _ = ops.layernorm(det, self.ln_f_w, self.ln_f_b, eps)
         return self._heads(y, lin)
 
-    def _forward_torch(self, pixel_values: torch.Tensor):
+    def _forward_torch(self, pixel_values: torch.Tensor, native_attention: bool = False):
+        """Eager PyTorch (numerics reference).  ``native_attention``: the exact-fp32
+        path of the fp32 pods -- hipBLASLt fp32 GEMMs, the gfx950 fp32 MFMA
+        flash attention (``nos_attn_fwd_f32_d64``) on the fused QKV output."""
         cfg = self.cfg
         nh, hd = cfg.num_attention_heads, cfg.head_dim
 
@@ -255,9 +260,12 @@ class YolosDetector(nn.Module):
         eps = cfg.layer_norm_eps
         for L in self.layers:
             y = F.layer_norm(h, (hs,), L.ln1_w, L.ln1_b, eps)
-            qkv = F.linear(y, L.qkv_w, L.qkv_b).view(B, S, 3, nh, hd)
-            q, k, v = (t.transpose(1, 2) for t in qkv.unbind(2))
-            a = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, S, hs)
+            qkv = F.linear(y, L.qkv_w, L.qkv_b)
+            if native_attention:
+                a = ops.attention_qkv(qkv, nh)
+            else:
+                q, k, v = (t.transpose(1, 2) for t in qkv.view(B, S, 3, nh, hd).unbind(2))
+                a = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, S, hs)
             h = F.linear(a, L.proj_w, L.proj_b) + h
             y = F.layer_norm(h, (hs,), L.ln2_w, L.ln2_b, eps)
             h = F.linear(F.gelu(F.linear(y, L.fc1_w, L.fc1_b)), L.fc2_w, L.fc2_b) + h

@@ -191,16 +191,21 @@ def attention_qkv(qkv: torch.Tensor, num_heads: int, out: torch.Tensor | None = 
         raise ValueError("native attention supports head_dim 64")
     if qkv.stride(-1) != 1:
         raise ValueError("qkv must have unit inner stride")
+    if qkv.dtype not in (torch.bfloat16, torch.float32):
+        raise ValueError("native attention takes bf16 or fp32")
     if out is None:
         out = torch.empty((B, S, num_heads * D), dtype=qkv.dtype, device=qkv.device)
+    if out.dtype != qkv.dtype or out.stride(-1) != 1 or out.shape != (B, S, num_heads * D):
+        raise ValueError("out must be [B, S, H*64] of qkv's dtype with unit inner stride")
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     hd = num_heads * D
     base = qkv.data_ptr()
     es = qkv.element_size()
-    rc = _lib.lib().nos_attn_fwd_d64(base, base + hd * es, base + 2 * hd * es, out.data_ptr(), B,
-                                     num_heads, S, S, qkv.stride(1), qkv.stride(0), out.stride(1),
-                                     out.stride(0), float(scale), _stream())
-    _lib.check(rc, "nos_attn_fwd_d64")
+    fn, name = ((_lib.lib().nos_attn_fwd_f32_d64, "nos_attn_fwd_f32_d64") if qkv.dtype == torch.float32
+                else (_lib.lib().nos_attn_fwd_d64, "nos_attn_fwd_d64"))
+    rc = fn(base, base + hd * es, base + 2 * hd * es, out.data_ptr(), B, num_heads, S, S, qkv.stride(1),
+            qkv.stride(0), out.stride(1), out.stride(0), float(scale), _stream())
+    _lib.check(rc, name)
     return out
 
 

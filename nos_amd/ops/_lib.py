@@ -26,6 +26,8 @@ c_int, c_ll, c_float, c_void_p, c_double = (ctypes.c_int, ctypes.c_longlong, cty
 _SIGS = {
     "nos_attn_fwd_d64": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                          c_ll, c_int, c_ll, c_float, c_void_p],
+    "nos_attn_fwd_f32_d64": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                             c_ll, c_int, c_ll, c_float, c_void_p],
     "nos_gemm_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nos_gemm_set_policy": [c_int],

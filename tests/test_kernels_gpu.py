@@ -106,6 +106,46 @@ def test_attention_strided_views():
     assert out[..., hid:].abs().max().item() == 0  # padding untouched
 
 
+@pytest.mark.parametrize("B,S,H", [(1, 3401, 6), (2, 77, 3), (1, 1, 1), (1, 33, 2), (3, 300, 2)])
+def test_attention_fp32_exact(B, S, H):
+    """fp32 MFMA attention against an fp64 reference: exact-f32 numerics."""
+    qkv = torch.randn(B, S, 3 * H * 64, device=DEV, dtype=torch.float32)
+    y = ops.attention_qkv(qkv, H)
+    q, k, v = qkv.cpu().double().view(B, S, 3, H, 64).unbind(2)
+    p = torch.softmax((q.transpose(1, 2) @ k.transpose(1, 2).transpose(-1, -2)) / 8.0, dim=-1)
+    ref = (p @ v.transpose(1, 2)).transpose(1, 2).reshape(B, S, H * 64)
+    assert y.dtype == torch.float32
+    err = (y.cpu().double() - ref).abs().max().item()
+    assert err < 2e-5 * max(1.0, ref.abs().max().item()), err
+
+
+def test_attention_fp32_strided_and_large_logits():
+    B, S, H = 2, 129, 6
+    base = torch.randn(B, S, 3 * H * 64 + 64, device=DEV) * 4.0  # padded rows: ld != 3*H*64, logits ~ +-100
+    qkv = base[:, :, : 3 * H * 64]
+    y = ops.attention_qkv(qkv, H)
+    ref = ops.attention_ref(*(t.cpu() for t in qkv.view(B, S, 3, H, 64).unbind(2))).reshape(B, S, H * 64)
+    assert torch.isfinite(y).all()
+    assert (y.cpu() - ref).abs().max().item() < 1e-4 * ref.abs().max().item()
+
+
+def test_yolos_fp32_native_attention_matches_torch():
+    from nos_amd.models.yolos import YolosConfig, YolosDetector, demo_input_hw, make_demo_input
+
+    cfg = YolosConfig.small()
+    m = YolosDetector(cfg, backend="native")
+    m.reset_parameters(1)
+    m = m.to(DEV, torch.float32).eval()
+    x = make_demo_input(cfg, device=DEV, dtype=torch.float32, hw=demo_input_hw(), seed=1)
+    with torch.no_grad():
+        torch.backends.cuda.matmul.allow_tf32 = False
+        logits, boxes = m(x)
+        m.backend = "torch"
+        rl, rb = m(x)
+    assert (logits - rl).abs().max().item() < 1e-3 * max(1.0, rl.abs().max().item())
+    assert (boxes - rb).abs().max().item() < 1e-4
+
+
 def test_layernorm_with_residual_sum():
     x = torch.randn(3401, 384, device=DEV, dtype=torch.bfloat16)
     r = torch.randn(3401, 384, device=DEV, dtype=torch.bfloat16)

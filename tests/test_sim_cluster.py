@@ -21,21 +21,26 @@ def _envs(node):
     return [rc.envs for conts in node.kubelet.running_containers().values() for rc in conts]
 
 
-def test_cumask_pack_places_all_pods_first_fit():
+@pytest.mark.parametrize("max_procs,pods,first", [(32, 30, 28), (8, 10, 8)])
+def test_cumask_pack_places_all_pods_first_fit(max_procs, pods, first):
+    from nos_amd.gpu.fakesmi import FakeSmi
+
     cl = SimCluster()
-    nd = cl.add_node("n1", C.PARTITIONING_CUMASK, gpus=2)
+    nd = cl.add_node("n1", C.PARTITIONING_CUMASK, smi=FakeSmi(gpus=2, node="n1", max_procs=max_procs))
     cl.settle(30)
-    for i in range(30):
+    for i in range(pods):
         cl.submit_pod(f"p{i}", {"amd.com/gpu-10gb": 1})
     cl.settle(600, until=lambda: not cl.pending_pods())
-    assert len(cl.running_pods()) == 30
+    assert len(cl.running_pods()) == pods
     ann = ko.annotations(cl.api.get("Node", "n1"))
-    # first fit: GPU 0 is filled (28 x 10 GB <= 288 GB, 28 <= 32 masks) before GPU 1
-    assert ann["nos.nebuly.com/spec-gpu-0-10gb"] == "28"
-    assert ann["nos.nebuly.com/spec-gpu-1-10gb"] == "2"
+    assert ko.labels(cl.api.get("Node", "n1"))[C.LABEL_AMD_MAX_PROCS] == str(max_procs)
+    # first fit: GPU 0 is filled before GPU 1 -- by memory (28 x 10 GB <= 288 GB, 28 <= 32 masks) or by the
+    # HWS concurrent-process limit (8: more would be time-sliced)
+    assert ann["nos.nebuly.com/spec-gpu-0-10gb"] == str(first)
+    assert ann["nos.nebuly.com/spec-gpu-1-10gb"] == str(pods - first)
     assert ann[C.ANNOTATION_REPORTED_PARTITIONING_PLAN] == ann[C.ANNOTATION_PARTITIONING_PLAN]
     envs = _envs(nd)
-    assert Counter(e[C.ENV_VISIBLE_DEVICES] for e in envs) == {"0": 28, "1": 2}
+    assert Counter(e[C.ENV_VISIBLE_DEVICES] for e in envs) == {"0": first, "1": pods - first}
 
 
 def test_cumask_spread_masks_are_xcd_symmetric_and_disjoint():
@@ -59,15 +64,18 @@ def test_cumask_spread_masks_are_xcd_symmetric_and_disjoint():
         assert len(seen) == 256  # the 4 slices own the whole GPU
 
 
-def test_cumask_capacity_is_min_of_memory_and_masks():
+@pytest.mark.parametrize("max_procs,expect", [(64, 32), (8, 8)])
+def test_cumask_capacity_is_min_of_memory_masks_and_processes(max_procs, expect):
+    from nos_amd.gpu.fakesmi import FakeSmi
+
     cl = SimCluster()
-    cl.add_node("n1", C.PARTITIONING_CUMASK, gpus=1)
+    cl.add_node("n1", C.PARTITIONING_CUMASK, smi=FakeSmi(gpus=1, node="n1", max_procs=max_procs))
     cl.settle(30)
     for i in range(40):
         cl.submit_pod(f"p{i}", {"amd.com/gpu-8gb": 1})
     cl.settle(300)
-    # 288 GB / 8 GB = 36 by memory, but only 32 XCD-symmetric masks per GPU
-    assert len(cl.running_pods()) == 32
+    # 288 GB / 8 GB = 36 by memory, 32 XCD-symmetric masks per GPU, and the HWS process limit
+    assert len(cl.running_pods()) == expect
 
 
 def test_amdpart_switches_modes_and_exposes_logical_devices():
@@ -148,6 +156,6 @@ def test_bench_control_plane_plan(n_gpus):
     masks, info = control_plane_plan(n_gpus=n_gpus, pods_per_gpu=4, slice_gb=10, num_cus=256, local_gpu=0)
     assert len(masks) == 4
     assert info["placed_pods"] == 4 * n_gpus and info["pending_pods"] == 0
-    assert info["schedulable_fractional_pods_per_node"] == 28 * n_gpus
+    assert info["schedulable_fractional_pods_per_node"] == 8 * n_gpus  # HWS process limit (gpu/kfd.py)
     assert info["plan_reported"]
     assert sorted(c for m in masks for c in m) == list(range(256))

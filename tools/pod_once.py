@@ -1,0 +1,46 @@
+"""One YOLOS-small pod in this process, for profiling (no subprocesses, so it
+can run under rocprofv3 directly).
+
+rocprofv3 --kernel-trace --stats -d gpurun_out/prof -- python tools/pod_once.py --dtype fp32 --iters 30
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--no-graphs", action="store_true")
+    a = ap.parse_args()
+    import torch
+
+    from nos_amd.models.pod import _build
+    from nos_amd.models.yolos import GraphedTenant, demo_input_hw
+
+    torch.backends.cuda.matmul.allow_tf32 = False
+    m, x = _build(a.dtype, 0, demo_input_hw())
+    s = torch.cuda.Stream()
+    t = GraphedTenant(m, s, x)
+    with torch.no_grad():
+        if not a.no_graphs:
+            t.capture()
+        for _ in range(3):
+            t.launch()
+        s.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.iters):
+            t.launch()
+        s.synchronize()
+    dt = (time.perf_counter() - t0) / a.iters
+    print(f"{a.dtype}: {dt * 1e3:.3f} ms/inference ({1 / dt:.1f} inf/s)")
+
+
+if __name__ == "__main__":
+    main()
