@@ -3,32 +3,38 @@
 // HF model (demos/gpu-sharing-comparison/client/main.py:19-20).
 //
 // gfx950 has an exact f32-input MFMA (v_mfma_f32_32x32x2_f32: fmaf-chain
-// numerics, 64 FLOP/clk/SIMD) but no xf32, so fp32 attention is MFMA-bound at
-// 1/16 of the bf16 rate; the design keeps the matrix pipe fed and everything
-// else off it:
+// numerics, 64 FLOP/clk/SIMD = 1/16 of bf16) but no xf32, so fp32 attention
+// is matrix-pipe bound; the design keeps that pipe fed and everything else
+// off it:
 //
-//  * one wave = 32 query rows of one (batch, head); waves are independent (no
-//    LDS, no barriers), four per workgroup; the grid is XCD-remapped so the
-//    q-blocks of one head share an XCD's L2 (K/V of one head = 1.7 MB fp32);
-//  * "swapped" QK^T: S^T = K . Q^T with the head dim split as d = 32*h + kk
-//    (h = lane >> 5, kk = MFMA step), so each lane loads 128 contiguous bytes
-//    of its K row and keeps its Q half-row (pre-scaled by scale*log2 e) in 32
-//    registers for the whole kernel;
-//  * S^T's accumulator has the query on the lane and 16 of the 32 keys in
-//    registers: row max / sum are lane-local plus one v_permlane32_swap, and
-//    O's per-query rescale is a per-lane scalar;
-//  * the accumulator registers ARE the B operand of O^T = V^T . P^T (register
-//    r of lane-half h is key (r&3) + 8(r>>2) + 4h, so V^T's A operand is
-//    gathered in that key order) -- no LDS round trip, no transpose;
-//  * the next key block's K and V are loaded into a second register set while
-//    the current one is multiplied (software-pipelined global loads).
+//  * one workgroup = W waves x 32 query rows of one (batch, head); K/V tiles
+//    of KVB keys are staged ONCE per workgroup into LDS by LDS-DMA
+//    (global_load_lds_dwordx4: no staging registers) into a 2-deep ring, one
+//    barrier per tile; the W waves share every byte (W x less L2 traffic than
+//    per-wave loads);
+//  * "swapped" QK^T: S^T = K . Q^T with the head dim split as d = 32h + kk
+//    (h = lane >> 5, kk = MFMA step): a lane's K operand is 128 contiguous
+//    bytes of its key row (8 x ds_read_b128 from an XOR-swizzled image,
+//    conflict-free) and its Q half-row (pre-scaled by scale*log2 e) stays in
+//    32 registers for the whole kernel;
+//  * S^T's accumulator has the query on the lane and 16 keys per 32-key tile
+//    in registers: row max / sum are lane-local plus one v_permlane32_swap,
+//    and O's per-query rescale is a per-lane scalar;
+//  * the accumulator registers ARE the B operand of O^T = V^T . P^T
+//    (register r of lane-half h is key (r&3) + 8(r>>2) + 4h), so V^T's A
+//    operand is gathered in that key order with ds_read_b32 from a V image
+//    whose 16-byte chunks are XOR-swizzled by key bit 2 (the two lane halves
+//    then hit disjoint banks) -- no LDS round trip for P, no transpose;
+//  * deferred rescale: the running max only moves when a row's tile max
+//    exceeds it by more than 8 (log2 units), so O and l are rescaled rarely;
+//  * XCD-aware workgroup order: the q-blocks of one head share an XCD's L2.
 #include "common.h"
 
 namespace {
 
 constexpr int D = 64;
-constexpr int WAVES = 4;
-constexpr int NT = 64 * WAVES;
+constexpr int ROW_BYTES = D * 4;      // 256 B = 16 chunks of 16 B
+constexpr float RESCALE_THR = 8.f;    // log2 units
 
 __device__ __forceinline__ float xor32_max(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -40,53 +46,45 @@ __device__ __forceinline__ float xor32_sum(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-struct KV {
-  float k[32];      // K[j0 + (lane&31)][32h + kk]
-  float v[2][16];   // V[j0 + key(r, h)][32t + (lane&31)]
-};
+__device__ __forceinline__ int kswz(int row) { return row & 15; }
+__device__ __forceinline__ int vswz(int row) { return ((row >> 2) & 1) << 3; }
 
-__device__ __forceinline__ void load_kv(KV& kv, const float* __restrict__ kbase, const float* __restrict__ vbase,
-                                        int j0, int Skv, int ld, int lane) {
-  const int h = lane >> 5, c = lane & 31;
-  const int jr = min(j0 + c, Skv - 1);
-  const float4* kp = reinterpret_cast<const float4*>(kbase + (long long)jr * ld + 32 * h);
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const float4 x = kp[u];
-    kv.k[4 * u + 0] = x.x;
-    kv.k[4 * u + 1] = x.y;
-    kv.k[4 * u + 2] = x.z;
-    kv.k[4 * u + 3] = x.w;
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int j = min(j0 + (r & 3) + 8 * (r >> 2) + 4 * h, Skv - 1);
-    const float* vp = vbase + (long long)j * ld + c;
-    kv.v[0][r] = vp[0];
-    kv.v[1][r] = vp[32];
-  }
+__device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-__global__ __launch_bounds__(NT, 2) void attn_fwd_f32_d64_kernel(
+template <int W, int KVB>
+__global__ __launch_bounds__(64 * W) void attn_fwd_f32_d64_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, float* __restrict__ o,
     int B, int H, int Sq, int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, int nqb) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int item = nos::xcd_remap(blockIdx.x, gridDim.x) * WAVES + wave;
-  if (item >= B * H * nqb) return;  // whole wave leaves; nothing below synchronises across waves
-  const int qb = item % nqb;
-  const int bh = item / nqb;
-  const int hh = bh % H, b = bh / H;
-  const int h = lane >> 5, col = lane & 31;
-  const int q0 = qb * 32;
+  constexpr int QBLK = 32 * W;
+  constexpr int TILE = KVB * ROW_BYTES;          // bytes of K (or V) per stage
+  constexpr int STAGE = 2 * TILE;
+  constexpr int PIECES = STAGE / 1024;           // 1 KiB per wave-wide LDS-DMA
+  constexpr int PER_WAVE = PIECES / W;
+  constexpr int NT32 = KVB / 32;                 // 32-key S^T tiles per stage
+  static_assert(PIECES % W == 0, "stage pieces must split evenly over the waves");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-  const long long boff = (long long)b * bs_in + hh * D;
-  const float* kbase = k + boff;
-  const float* vbase = v + boff;
+  const int nwg = B * H * nqb;
+  const int wg = nos::xcd_remap(blockIdx.x, nwg);
+  const int b = wg / (H * nqb);
+  const int rem = wg - b * (H * nqb);
+  const int hd = rem / nqb;
+  const int qb = rem - hd * nqb;
+
+  const int tid = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int h = lane >> 5, col = lane & 31;
+
+  const long long boff = (long long)b * bs_in + hd * D;
+  const float* kb_ptr = k + boff;
+  const float* vb_ptr = v + boff;
 
   float qf[32];
   {
-    const int qr = min(q0 + col, Sq - 1);
+    const int qr = min(qb * QBLK + wid * 32 + col, Sq - 1);
     const float4* qp = reinterpret_cast<const float4*>(q + boff + (long long)qr * ld_in + 32 * h);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -98,81 +96,150 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_f32_d64_kernel(
     }
   }
 
-  f32x16_t acc_o[2];
+  // piece p: tensor p / (PIECES/2) (K, V), 4 rows from (p % (PIECES/2)) * 4;
+  // lane L writes row R + L/16, physical chunk L%16 = logical chunk ^ swizzle
+  auto stage = [&](int it, int buf) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    acc_o[0][r] = 0.f;
-    acc_o[1][r] = 0.f;
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int p = wid * PER_WAVE + i;
+      const int is_v = p / (PIECES / 2);
+      const int R = (p % (PIECES / 2)) * 4;
+      const int row = R + (lane >> 4);
+      const int pc = lane & 15;
+      const int lc = pc ^ (is_v ? vswz(row) : kswz(row));
+      int kv = it * KVB + row;
+      kv = kv < Skv ? kv : Skv - 1;
+      const float* src = (is_v ? vb_ptr : kb_ptr) + (long long)kv * ld_in + lc * 4;
+      glds16(src, smem + buf * STAGE + is_v * TILE + R * ROW_BYTES);
+    }
+  };
+
+  const int ntiles = (Skv + KVB - 1) / KVB;
+  stage(0, 0);
+
+  int koff[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) koff[u] = col * ROW_BYTES + (((8 * h + u) ^ kswz(col)) << 4);
+  int voff[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) voff[dt] = 4 * h * ROW_BYTES + (((8 * dt + (col >> 2)) ^ (8 * h)) << 4) + (col & 3) * 4;
+
+  f32x16_t oacc[2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    oacc[0][i] = 0.f;
+    oacc[1][i] = 0.f;
   }
-  float m_run = -INFINITY;
-  float l_run = 0.f;  // this lane-half's partial row sum (halves merged at the end)
+  float m = 0.f, l = 0.f;  // reference max (log2 units), this lane-half's partial row sum
 
-  const int nkb = (Skv + 31) / 32;
-  KV cur, nxt;
-  load_kv(cur, kbase, vbase, 0, Skv, ld_in, lane);
-  for (int kb = 0; kb < nkb; ++kb) {
-    const int j0 = kb * 32;
-    if (kb + 1 < nkb) load_kv(nxt, kbase, vbase, j0 + 32, Skv, ld_in, lane);
+  __syncthreads();  // stage 0 landed (vmcnt(0)) and is visible
 
-    // S^T[j][i] (log2 units): lane holds query i = col, keys key(r, h)
-    f32x16_t s;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s[r] = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk) s = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.k[kk], qf[kk], s, 0, 0, 0);
+  for (int it = 0; it < ntiles; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < ntiles) stage(it + 1, buf ^ 1);  // that buffer was released by the barrier ending it-1
+    const unsigned char* kl = smem + buf * STAGE;
+    const unsigned char* vl = kl + TILE;
 
-    if (j0 + 32 > Skv) {  // tail block: keys past Skv never contribute
+    f32x16_t s[NT32];
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (j0 + (r & 3) + 8 * (r >> 2) + 4 * h >= Skv) s[r] = -INFINITY;
+    for (int t = 0; t < NT32; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[t][i] = 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float4 kx = *reinterpret_cast<const float4*>(kl + t * 32 * ROW_BYTES + koff[u]);
+        s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.x, qf[4 * u + 0], s[t], 0, 0, 0);
+        s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.y, qf[4 * u + 1], s[t], 0, 0, 0);
+        s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.z, qf[4 * u + 2], s[t], 0, 0, 0);
+        s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.w, qf[4 * u + 3], s[t], 0, 0, 0);
+      }
     }
-    float mb = s[0];
+    if ((it + 1) * KVB > Skv) {  // tail tile: keys past Skv never contribute
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mb = fmaxf(mb, s[r]);
-    mb = xor32_max(mb);
-    const float m_new = fmaxf(m_run, mb);
-    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);  // 0 on the first block
-    m_run = m_new;
-    float ls = 0.f;
+      for (int t = 0; t < NT32; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s[r] = __builtin_amdgcn_exp2f(s[r] - m_new);
-      ls += s[r];
+        for (int i = 0; i < 16; ++i)
+          if (it * KVB + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h >= Skv) s[t][i] = -INFINITY;
     }
-    l_run = l_run * alpha + ls;
+    float mt = s[0][0];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      acc_o[0][r] *= alpha;
-      acc_o[1][r] *= alpha;
-    }
-    // O^T[d][i] += V^T[d][j] P^T[j][i]; step r sums keys {key(r,0), key(r,1)}
+    for (int t = 0; t < NT32; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      acc_o[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.v[0][r], s[r], acc_o[0], 0, 0, 0);
-      acc_o[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.v[1][r], s[r], acc_o[1], 0, 0, 0);
+      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[t][i]);
+    const float mrel = xor32_max(mt) - m;
+    if (it == 0 || !__all(mrel <= RESCALE_THR)) {
+      const float delta = it == 0 ? mrel : fmaxf(mrel, 0.f);
+      const float alpha = __builtin_amdgcn_exp2f(-delta);
+      m += delta;
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        oacc[0][i] *= alpha;
+        oacc[1][i] *= alpha;
+      }
     }
-    if (kb + 1 < nkb) cur = nxt;
+    float ps = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT32; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        s[t][i] = __builtin_amdgcn_exp2f(s[t][i] - m);
+        ps += s[t][i];
+      }
+    l += ps;
+    // O^T[d][i] += V^T[d][j] P^T[j][i]; step (t, r) sums keys 32t + {key(r,0), key(r,1)}
+#pragma unroll
+    for (int t = 0; t < NT32; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int roff = (32 * t + (r & 3) + 8 * (r >> 2)) * ROW_BYTES;
+        const float v0 = *reinterpret_cast<const float*>(vl + roff + voff[0]);
+        const float v1 = *reinterpret_cast<const float*>(vl + roff + voff[1]);
+        oacc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0, s[t][r], oacc[0], 0, 0, 0);
+        oacc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, s[t][r], oacc[1], 0, 0, 0);
+      }
+    __syncthreads();  // next stage landed; every wave is done with this buffer
   }
 
-  const float inv = 1.f / xor32_sum(l_run);
-  const int qi = q0 + col;
+  const float inv = 1.f / xor32_sum(l);
+  const int qi = qb * QBLK + wid * 32 + col;
   if (qi < Sq) {
-    float* op = o + (long long)b * bs_out + (long long)qi * ld_out + hh * D;
+    float* op = o + (long long)b * bs_out + (long long)qi * ld_out + hd * D;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float4 y;
-        y.x = acc_o[t][4 * g + 0] * inv;
-        y.y = acc_o[t][4 * g + 1] * inv;
-        y.z = acc_o[t][4 * g + 2] * inv;
-        y.w = acc_o[t][4 * g + 3] * inv;
-        *reinterpret_cast<float4*>(op + 32 * t + 8 * g + 4 * h) = y;
+        y.x = oacc[dt][4 * g + 0] * inv;
+        y.y = oacc[dt][4 * g + 1] * inv;
+        y.z = oacc[dt][4 * g + 2] * inv;
+        y.w = oacc[dt][4 * g + 3] * inv;
+        *reinterpret_cast<float4*>(op + 32 * dt + 8 * g + 4 * h) = y;
       }
   }
 }
 
+template <int W, int KVB>
+int launch(const float* q, const float* k, const float* v, float* o, int B, int H, int Sq, int Skv, int ld_in,
+           long long bs_in, int ld_out, long long bs_out, float c, hipStream_t stream) {
+  const int nqb = (Sq + 32 * W - 1) / (32 * W);
+  const long long nwg = (long long)B * H * nqb;
+  if (nwg > (1LL << 30)) return (int)hipErrorInvalidValue;
+  const size_t lds = 2 * 2 * KVB * ROW_BYTES;
+  hipLaunchKernelGGL((attn_fwd_f32_d64_kernel<W, KVB>), dim3((unsigned)nwg), dim3(64 * W), lds, stream, q, k, v, o,
+                     B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
+  return (int)hipGetLastError();
+}
+
+int g_variant = 0;  // 0 auto, 1: 4 waves x 64-key tiles, 2: 2 waves x 32-key tiles
+
 }  // namespace
+
+NOS_API int nos_attn_f32_set_variant(int variant) {
+  if (variant < 0 || variant > 2) return (int)hipErrorInvalidValue;
+  g_variant = variant;
+  return 0;
+}
 
 // q/k/v: row r of batch b at base + b*bs_in + r*ld_in (+ head*64), fp32, 16-byte
 // aligned rows; o: [B, Sq, H*64] rows at b*bs_out + r*ld_out.
@@ -183,12 +250,11 @@ NOS_API int nos_attn_fwd_f32_d64(const float* q, const float* k, const float* v,
   if (ld_in < H * D || ld_out < H * D || (ld_in & 3) || (ld_out & 3) || (bs_in & 3) || (bs_out & 3))
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) return (int)hipErrorInvalidValue;
-  const int nqb = (Sq + 31) / 32;
-  const long long items = (long long)B * H * nqb;
-  if (items > (1LL << 30)) return (int)hipErrorInvalidValue;
-  const int grid = (int)((items + WAVES - 1) / WAVES);
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(attn_fwd_f32_d64_kernel, dim3(grid), dim3(NT), 0, stream, q, k, v, o, B, H, Sq, Skv, ld_in,
-                     bs_in, ld_out, bs_out, c, nqb);
-  return (int)hipGetLastError();
+  // auto = 4 waves x 64-key tiles: measured faster at every batch, even when
+  // one pod's 162 workgroups leave CUs idle (B=1: 260 vs 482 us; B=8: 1345 vs
+  // 1679 us, profiles/r02_attention_f32.json)
+  const int var = g_variant == 0 ? 1 : g_variant;
+  if (var == 1) return launch<4, 64>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
+  return launch<2, 32>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
 }

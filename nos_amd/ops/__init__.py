@@ -108,6 +108,14 @@ def set_gemm_impl(impl: str) -> None:
     _lib.check(_lib.lib().nos_gemm_set_impl(code), "nos_gemm_set_impl")
 
 
+def set_attention_f32_variant(variant: str) -> None:
+    """fp32 attention tiling: ``"auto"`` (default), ``"w4k64"`` (4 waves x 64-key
+    LDS tiles, best when the grid fills the chip) or ``"w2k32"`` (2 waves x
+    32-key tiles: twice the workgroups, for one small pod)."""
+    code = {"auto": 0, "w4k64": 1, "w2k32": 2}[variant]
+    _lib.check(_lib.lib().nos_attn_f32_set_variant(code), "nos_attn_f32_set_variant")
+
+
 @torch.no_grad()
 def fold_layernorm(weight: torch.Tensor, bias: torch.Tensor | None, gamma: torch.Tensor, beta: torch.Tensor
                    ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:

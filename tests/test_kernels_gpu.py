@@ -106,11 +106,16 @@ def test_attention_strided_views():
     assert out[..., hid:].abs().max().item() == 0  # padding untouched
 
 
-@pytest.mark.parametrize("B,S,H", [(1, 3401, 6), (2, 77, 3), (1, 1, 1), (1, 33, 2), (3, 300, 2)])
-def test_attention_fp32_exact(B, S, H):
+@pytest.mark.parametrize("variant", ["w4k64", "w2k32", "auto"])
+@pytest.mark.parametrize("B,S,H", [(1, 3401, 6), (2, 77, 3), (1, 1, 1), (1, 33, 2), (3, 300, 2), (1, 129, 1)])
+def test_attention_fp32_exact(B, S, H, variant):
     """fp32 MFMA attention against an fp64 reference: exact-f32 numerics."""
     qkv = torch.randn(B, S, 3 * H * 64, device=DEV, dtype=torch.float32)
-    y = ops.attention_qkv(qkv, H)
+    ops.set_attention_f32_variant(variant)
+    try:
+        y = ops.attention_qkv(qkv, H)
+    finally:
+        ops.set_attention_f32_variant("auto")
     q, k, v = qkv.cpu().double().view(B, S, 3, H, 64).unbind(2)
     p = torch.softmax((q.transpose(1, 2) @ k.transpose(1, 2).transpose(-1, -2)) / 8.0, dim=-1)
     ref = (p @ v.transpose(1, 2)).transpose(1, 2).reshape(B, S, H * 64)
