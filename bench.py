@@ -86,7 +86,7 @@ def plan(args, world: int, local: int, slice_gb: int, pods: int, mode: str) -> t
     from nos_amd.bench_support import control_plane_plan
 
     _, info = control_plane_plan(n_gpus=world, pods_per_gpu=pods, slice_gb=slice_gb, num_cus=256, local_gpu=local,
-                                 cu_policy="shared" if mode == "shared" else "even", capacity_probe=True)
+                                 cu_policy="shared" if mode == "shared" else "proportional", capacity_probe=True)
     return info.pop("envs"), info
 
 

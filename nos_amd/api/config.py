@@ -96,7 +96,7 @@ class GpuPartitionerConfig(ControllerManagerSpec):
     # new: CU-mask slice placement over a node's GPUs ("pack" = reference first-fit, "spread")
     slice_placement: str = Field("pack", alias="slicePlacement")
     # new: CU-mask layout of a GPU's slices in the device plugin ("even" | "proportional" | "shared")
-    cu_policy: str = Field("even", alias="cuPolicy")
+    cu_policy: str = Field("proportional", alias="cuPolicy")
 
     @model_validator(mode="before")
     @classmethod
@@ -165,7 +165,7 @@ class DevicePluginConfig(ControllerManagerSpec):
     # how CU masks are assigned to cumask slices: "even" (split the GPU's CUs
     # evenly among the slices of its geometry), "proportional" (to memory),
     # "shared" (no mask; MPS-without-limits semantics)
-    cu_policy: str = Field("even", alias="cuPolicy")
+    cu_policy: str = Field("proportional", alias="cuPolicy")
 
 
 class MetricsExporterConfig(_M):

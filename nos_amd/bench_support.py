@@ -64,7 +64,7 @@ def schedulable_pods(n_gpus: int, slice_gb: int, num_cus: int = 256, placement: 
 
 
 def control_plane_plan(n_gpus: int, pods_per_gpu: int, slice_gb: int, num_cus: int, local_gpu: int = 0,
-                       placement: str = "spread", cu_policy: str = "even", capacity_probe: bool = True
+                       placement: str = "spread", cu_policy: str = "proportional", capacity_probe: bool = True
                        ) -> tuple[list[list[int] | None], dict]:
     """Masks of the pods placed on ``local_gpu`` (None = unmasked) and the
     control-plane facts; ``info["envs"]`` holds each of those pods' full

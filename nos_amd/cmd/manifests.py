@@ -54,7 +54,7 @@ DEFAULT_VALUES: dict = {
         "devicePluginDelaySeconds": 5,
         "planReportTimeoutSeconds": 300,
         "slicePlacement": "pack",
-        "cuPolicy": "even",
+        "cuPolicy": "proportional",
         "knownPartitionGeometries": None,  # list override of the built-in MI355X table
         "partitionAgent": {"enabled": True, "reportConfigIntervalSeconds": 10, "allowModeChanges": True,
                            "defaultComputeMode": "SPX", "defaultMemoryMode": "NPS1"},

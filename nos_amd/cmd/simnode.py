@@ -22,7 +22,7 @@ def main(argv=None) -> int:
     ap.add_argument("--kind", choices=["cumask", "partition", "none"], default="cumask")
     ap.add_argument("--gpus", type=int, default=8)
     ap.add_argument("--podresources-socket", required=True)
-    ap.add_argument("--cu-policy", default="even")
+    ap.add_argument("--cu-policy", default="proportional")
     args = ap.parse_args(argv)
     common.setup_logging(args.log_level)
     from ..api import constants as C

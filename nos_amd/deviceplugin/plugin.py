@@ -33,7 +33,7 @@ import yaml
 
 from ..api import constants as C
 from ..gpu.amdsmi import PARTITIONS_PER_MODE, AmdSmi, GpuInfo
-from ..gpu.topology import MI355X_CUS_PER_XCD, MI355X_XCDS, CUSlice, logical_cu
+from ..gpu.topology import MI355X_CUS_PER_XCD, MI355X_MEMORY_GB, MI355X_XCDS, CUSlotSet, layout_slots, logical_cu
 from ..ops.streams import mask_hex
 from ..partitioning import scoring
 
@@ -60,7 +60,7 @@ class ContainerAllocation:
 
 class NosAmdDevicePlugin:
     def __init__(self, node_name: str, smi: AmdSmi, mode: str | None = None, expose_partitions_as_gpu: bool = False,
-                 cu_policy: str = "even", device_env: str = "host"):
+                 cu_policy: str = "proportional", device_env: str = "host"):
         if device_env not in ("host", "container"):
             raise ValueError(f"device_env must be 'host' or 'container', not {device_env!r}")
         self.node_name = node_name
@@ -77,7 +77,7 @@ class NosAmdDevicePlugin:
         self.config_key: str | None = None
         self.devices: dict[str, Device] = {}
         self.allocated: dict[str, str] = {}      # device id -> owner (pod uid / container)
-        self.cu_slots: dict[str, CUSlice] = {}   # slice device id -> CU slot
+        self.cu_slots: dict[str, CUSlotSet] = {}   # slice device id -> CU slots
         self.listeners: list = []
         self.generation = 0
         self._links: dict[tuple[int, int], float] = {}
@@ -127,10 +127,10 @@ class NosAmdDevicePlugin:
                 if did not in devs and did in self.devices:
                     d = self.devices[did]
                     devs[did] = Device(d.id, d.resource, d.gpu_index, False, d.partition, d.profile, d.memory_gb)
-            changed = ({k: (d.resource, d.healthy) for k, d in devs.items()} !=
-                       {k: (d.resource, d.healthy) for k, d in self.devices.items()}) or self.generation == 0
+            before = {k: (d.resource, d.healthy) for k, d in self.devices.items()}
             self.devices = devs
             self._layout_cu_slots()
+            changed = {k: (d.resource, d.healthy) for k, d in self.devices.items()} != before or self.generation == 0
             if not changed:
                 return
             self.generation += 1
@@ -141,45 +141,28 @@ class NosAmdDevicePlugin:
                 log.exception("device plugin listener failed")
 
     def _layout_cu_slots(self) -> None:
-        """Give every slice replica an XCD-symmetric CU slot; allocated
-        replicas keep theirs, new ones share the remaining slots evenly."""
-        slots: dict[str, CUSlice] = {}
+        """XCD-symmetric CU slots for every slice replica (:func:`layout_slots`):
+        allocated replicas keep theirs, the others get exactly their policy
+        share of the free slots, and a replica that cannot get it is advertised
+        unhealthy (never a smaller or overlapping mask)."""
+        slots: dict[str, CUSlotSet] = {}
         by_gpu: dict[int, list[Device]] = {}
         for d in self.devices.values():
             if d.resource.startswith(C.AMD_SLICE_RESOURCE_PREFIX):
                 by_gpu.setdefault(d.gpu_index, []).append(d)
+        mem = {g.index: g.memory_gb for g in self._gpus()}
         for gi, devs in by_gpu.items():
-            cus_per_xcd = MI355X_CUS_PER_XCD
-            keep = {d.id: self.cu_slots[d.id] for d in devs if d.id in self.allocated and d.id in self.cu_slots}
-            taken = set()
-            for s in keep.values():
-                taken.update(range(s.start, s.start + s.per_xcd))
-            free_slots = [i for i in range(cus_per_xcd) if i not in taken]
-            new = sorted((d for d in devs if d.id not in keep), key=lambda d: d.id)
-            slots.update(keep)
-            if not new:
-                continue
-            if self.cu_policy == "shared" or not free_slots:
-                for d in new:
-                    slots[d.id] = CUSlice(0, cus_per_xcd)
-                continue
-            if self.cu_policy == "proportional":
-                gpu_mem = max(1, sum(x.memory_gb for x in devs))
-                want = [max(1, cus_per_xcd * d.memory_gb // max(gpu_mem, 1)) for d in new]
-            else:
-                want = [max(1, len(free_slots) // len(new))] * len(new)
-                for i in range(len(free_slots) - sum(want)):
-                    if i < len(want):
-                        want[i] += 1
-            pos = 0
-            for d, w in zip(new, want):
-                if pos + w > len(free_slots):  # out of free CUs: overlap round-robin
-                    pos = 0
-                run = free_slots[pos:pos + w]
-                # contiguous runs are not required: build from the first slot of the run
-                slots[d.id] = CUSlice(run[0], len(run)) if run == list(range(run[0], run[0] + len(run))) \
-                    else CUSlice(run[0], 1)
-                pos += w
+            keep = {d.id: self.cu_slots[d.id].slots for d in devs if d.id in self.allocated and d.id in self.cu_slots}
+            live = [d for d in devs if d.healthy or d.id in keep]
+            got, bad = layout_slots([(d.id, d.memory_gb) for d in live], keep, self.cu_policy,
+                                    mem.get(gi, MI355X_MEMORY_GB), MI355X_CUS_PER_XCD)
+            for did, sl in got.items():
+                slots[did] = CUSlotSet(sl, MI355X_XCDS)
+            for did in bad:
+                d = self.devices[did]
+                self.devices[did] = Device(d.id, d.resource, d.gpu_index, False, d.partition, d.profile, d.memory_gb)
+                log.warning("slice %s gets no CU slots (%s policy, %d allocated replicas hold the rest): unhealthy",
+                            did, self.cu_policy, len(keep))
         self.cu_slots = slots
 
     # ------------------------------------------------------------ device-plugin API
@@ -299,12 +282,15 @@ class NosAmdDevicePlugin:
             return alloc
 
     def release(self, device_ids: list[str]) -> None:
+        """Free devices; freed CU slots are laid out again at once (a replica
+        that was unhealthy for lack of slots may become healthy)."""
         with self._lock:
-            for did in device_ids:
-                self.allocated.pop(did, None)
+            released = [did for did in device_ids if self.allocated.pop(did, None) is not None]
             stale = [did for did in device_ids if did in self.devices and not self.devices[did].healthy]
             for did in stale:
                 self.devices.pop(did, None)
+        if released and self.mode == C.PARTITIONING_CUMASK:
+            self.refresh()
 
     def sync_allocated(self, used_device_ids: set[str]) -> None:
         """The device-plugin API has no Deallocate: a deployed plugin learns
@@ -316,7 +302,7 @@ class NosAmdDevicePlugin:
             for did in used_device_ids:
                 self.allocated.setdefault(did, "podresources")
 
-    def cu_slice_of(self, device_id: str) -> CUSlice | None:
+    def cu_slice_of(self, device_id: str) -> CUSlotSet | None:
         return self.cu_slots.get(device_id)
 
     def cus_of(self, device_id: str) -> list[int]:

@@ -78,3 +78,87 @@ def pack_slices(sizes_per_xcd: list[int], cus_per_xcd: int = MI355X_CUS_PER_XCD,
         out.append(CUSlice(s, k, num_xcds))
         s += k
     return out
+
+
+@dataclass(frozen=True)
+class CUSlotSet:
+    """An arbitrary set of local CU slots, the same on every XCD (XCD-symmetric,
+    not necessarily contiguous: slices keep their slots while neighbours come
+    and go, so free slots fragment)."""
+
+    slots: frozenset
+    num_xcds: int = MI355X_XCDS
+
+    @property
+    def per_xcd(self) -> int:
+        return len(self.slots)
+
+    @property
+    def num_cus(self) -> int:
+        return self.per_xcd * self.num_xcds
+
+    def cus(self) -> list[int]:
+        return sorted(logical_cu(x, j, self.num_xcds) for x in range(self.num_xcds) for j in self.slots)
+
+    def overlaps(self, other: "CUSlotSet") -> bool:
+        return bool(self.slots & other.slots)
+
+
+SLOT_POLICIES = ("shared", "proportional", "even")
+
+
+def slot_wants(replicas: list[tuple[str, int]], policy: str, gpu_memory_gb: int,
+               cus_per_xcd: int = MI355X_CUS_PER_XCD) -> dict[str, int]:
+    """CU slots per XCD each replica is entitled to.
+
+    * ``proportional``: its memory share of the GPU (a 36 GB slice of a 288 GB
+      MI355X gets 4 of 32 slots per XCD), at least 1 -- stable as slices come
+      and go, so the default for exclusive slices;
+    * ``even``: an equal split among the replicas that exist now (leftover
+      slots to the first ones) -- for static slice tables;
+    * ``shared``: every slot (no mask, the MPS-like behaviour)."""
+    if policy == "shared":
+        return {rid: cus_per_xcd for rid, _ in replicas}
+    if policy == "proportional":
+        return {rid: max(1, cus_per_xcd * mem // max(1, gpu_memory_gb)) for rid, mem in replicas}
+    if policy == "even":
+        if not replicas:
+            return {}
+        base, extra = divmod(cus_per_xcd, len(replicas))
+        return {rid: max(1, base + (1 if i < extra else 0)) for i, (rid, _) in enumerate(sorted(replicas))}
+    raise ValueError(f"unknown CU slot policy {policy!r} (one of {SLOT_POLICIES})")
+
+
+def layout_slots(replicas: list[tuple[str, int]], keep: dict[str, frozenset], policy: str, gpu_memory_gb: int,
+                 cus_per_xcd: int = MI355X_CUS_PER_XCD) -> tuple[dict[str, frozenset], set[str]]:
+    """Lay out the CU slots of one GPU's slice replicas.
+
+    ``replicas``: (id, memory GB) of every replica, ``keep``: the slots of
+    replicas that are allocated to running pods (they never move).  Every other
+    replica gets exactly its :func:`slot_wants` share out of the slots no kept
+    replica holds (lowest free slots first, in replica-id order); a replica for
+    which not enough free slots remain is returned as *unhealthy* instead of
+    being given a smaller or overlapping mask.  Returns (slots per replica id,
+    unhealthy ids)."""
+    full = frozenset(range(cus_per_xcd))
+    if policy == "shared":
+        return {rid: full for rid, _ in replicas}, set()
+    wants = slot_wants(replicas, policy, gpu_memory_gb, cus_per_xcd)
+    out: dict[str, frozenset] = {}
+    taken: set[int] = set()
+    for rid, _ in replicas:
+        if rid in keep:
+            out[rid] = frozenset(keep[rid])
+            taken |= keep[rid]
+    free = [s for s in range(cus_per_xcd) if s not in taken]
+    bad: set[str] = set()
+    for rid, _ in sorted(replicas):
+        if rid in out:
+            continue
+        w = wants[rid]
+        if w > len(free):
+            bad.add(rid)
+            continue
+        out[rid] = frozenset(free[:w])
+        free = free[w:]
+    return out, bad

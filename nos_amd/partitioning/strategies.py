@@ -139,7 +139,7 @@ class DevicePluginConfigRef:
     namespace: str = C.DEFAULT_DEVICE_PLUGIN_CM_NAMESPACE
 
 
-def plugin_config(node_name: str, plan_id: str, partitioning: NodePartitioning, cu_policy: str = "even",
+def plugin_config(node_name: str, plan_id: str, partitioning: NodePartitioning, cu_policy: str = "proportional",
                   allocation: str = "pack", gpu_weights: dict[int, float] | None = None) -> dict:
     """Device-plugin configuration for one node (the ``ToPluginConfig`` of
     ``mps/partitioner.go:123-157``, AMD shape).  With ``allocation:
@@ -160,7 +160,7 @@ def plugin_config(node_name: str, plan_id: str, partitioning: NodePartitioning, 
 
 class CuMaskPartitioner:
     def __init__(self, api, cm_ref: DevicePluginConfigRef | None = None, delay_s: float = 5.0, clock=None,
-                 cu_policy: str = "even", allocation: str = "pack"):
+                 cu_policy: str = "proportional", allocation: str = "pack"):
         self.api = api
         self.cm_ref = cm_ref or DevicePluginConfigRef()
         self.delay_s = delay_s
@@ -238,7 +238,7 @@ def amdpart_strategy(api, clock=None) -> Strategy:
 
 
 def cumask_strategy(api, cm_ref: DevicePluginConfigRef | None = None, delay_s: float = 5.0, clock=None,
-                    cu_policy: str = "even", placement: str = "pack") -> Strategy:
+                    cu_policy: str = "proportional", placement: str = "pack") -> Strategy:
     pc = CuMaskPartitionCalculator()
     return Strategy(C.PARTITIONING_CUMASK, CuMaskSnapshotTaker(pc, placement), pc,
                     CuMaskPartitioner(api, cm_ref, delay_s, clock, cu_policy, placement), cm.SliceCalculator(),

@@ -14,7 +14,7 @@ from nos_amd.sim.kubelet_grpc import DeviceManager
 
 
 def _slice_cfg(plan: str, slices: dict[int, int]) -> str:
-    return yaml.safe_dump({"version": "v1", "planId": plan, "cuPolicy": "even", "allocation": "spread",
+    return yaml.safe_dump({"version": "v1", "planId": plan, "cuPolicy": "proportional", "allocation": "spread",
                            "gpus": [{"index": g, "slices": [{"profile": "10gb", "memoryGB": 10, "replicas": n}]}
                                     for g, n in slices.items()]})
 

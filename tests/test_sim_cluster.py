@@ -48,8 +48,8 @@ def test_cumask_spread_masks_are_xcd_symmetric_and_disjoint():
     cl = SimCluster(partitioner_config=cfg)
     nd = cl.add_node("n1", C.PARTITIONING_CUMASK, gpus=4)
     cl.settle(30)
-    for i in range(16):
-        cl.submit_pod(f"p{i}", {"amd.com/gpu-10gb": 1})
+    for i in range(16):  # proportional CU policy: a 72 GB slice owns a quarter of every XCD
+        cl.submit_pod(f"p{i}", {"amd.com/gpu-72gb": 1})
     cl.settle(600, until=lambda: not cl.pending_pods())
     envs = _envs(nd)
     assert Counter(e[C.ENV_VISIBLE_DEVICES] for e in envs) == {str(g): 4 for g in range(4)}
@@ -153,9 +153,9 @@ def test_elastic_quota_labels_running_pods():
 
 @pytest.mark.parametrize("n_gpus", [1, 2])
 def test_bench_control_plane_plan(n_gpus):
-    masks, info = control_plane_plan(n_gpus=n_gpus, pods_per_gpu=4, slice_gb=10, num_cus=256, local_gpu=0)
+    masks, info = control_plane_plan(n_gpus=n_gpus, pods_per_gpu=4, slice_gb=72, num_cus=256, local_gpu=0)
     assert len(masks) == 4
     assert info["placed_pods"] == 4 * n_gpus and info["pending_pods"] == 0
-    assert info["schedulable_fractional_pods_per_node"] == 8 * n_gpus  # HWS process limit (gpu/kfd.py)
+    assert info["schedulable_fractional_pods_per_node"] == 4 * n_gpus  # 288 GB / 72 GB
     assert info["plan_reported"]
     assert sorted(c for m in masks for c in m) == list(range(256))
