@@ -16,10 +16,21 @@
 //     (the role of the reference's hand-written mocks/mig.Client,
 //     pkg/test/mocks/mig/mig_client.go:27-80).
 //
+// Physical GPUs vs logical partitions: in DPX/QPX/CPX amd-smi enumerates one
+// processor handle PER PARTITION.  The library groups those handles back into
+// physical GPUs (by amd-smi socket, i.e. the device's PCI bus/device; the
+// partitions of one socket ordered by their KFD partition id) -- the role of
+// the reference's GetMigDeviceGpuIndex / parent-GPU lookup
+// (pkg/gpu/nvml/client.go:59-146).  nos_smi_count()/gpu_info() report
+// physical GPUs (the unit of a mode switch and of the node's GPU count);
+// nos_smi_partition_count()/partition_info() report the logical devices of
+// one GPU with their own HIP id, render node, CUs, XCDs and memory.
+//
 // All entry points are serialised by one mutex (the reference's NVML client
 // does Init/Shutdown per call, client.go:46-57; we keep one session open).
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -63,6 +74,20 @@ struct nos_gpu_info {
   char bdf[32];
   char uuid[64];
   char market_name[128];
+};
+
+struct nos_part_info {
+  int gpu_index;       // physical GPU
+  int partition;       // index of the logical device within its GPU
+  int hip_id;          // HIP device ordinal of the logical device
+  int drm_render;      // /dev/dri/renderD<n>
+  int kfd_node;
+  int num_cus;
+  int num_xcds;
+  int memory_shared;   // 1: partitions share one memory pool (NPS1), vram_mb is a fair share
+  long long vram_mb;
+  char bdf[32];
+  char uuid[64];
 };
 
 struct nos_proc_info {
@@ -115,6 +140,8 @@ struct Backend {
   virtual int activity(int i, int* gfx, int* umc, int* mm) = 0;
   virtual int processes(int i, nos_proc_info* out, int max, int* n) = 0;
   virtual int link(int i, int j, int* type, long long* hops, long long* weight) = 0;
+  virtual int partition_count(int i) = 0;
+  virtual int partition_info(int i, int p, nos_part_info* out) = 0;
   virtual int inject(const char* /*fault*/) { return NOS_SMI_ERR_UNSUPPORTED; }
   virtual int add_process(int, unsigned, long long, unsigned) { return NOS_SMI_ERR_UNSUPPORTED; }
   virtual int remove_process(int, unsigned) { return NOS_SMI_ERR_UNSUPPORTED; }
@@ -180,8 +207,11 @@ struct FakeBackend : Backend {
     o->compute_mode = g.compute;
     o->memory_mode = g.memory;
     o->num_partitions = partitions_for_mode(g.compute);
-    o->hip_id = i;
-    o->drm_render = 128 + i;
+    int base = 0;  // a GPU's HIP id / render node are those of its first logical device
+    for (int j = 0; j < i; ++j)
+      if (!gpus[j].lost) base += partitions_for_mode(gpus[j].compute);
+    o->hip_id = base;
+    o->drm_render = 128 + base;
     o->vram_mb = g.vram_mb;
     std::snprintf(o->bdf, sizeof(o->bdf), "0000:%02x:00.0", 0x05 + 0x10 * i);
     std::snprintf(o->uuid, sizeof(o->uuid), "GPU-fake-mi355x-%04d", i);
@@ -241,6 +271,36 @@ struct FakeBackend : Backend {
       *hops = 1;
       *weight = 15;
     }
+    return NOS_SMI_OK;
+  }
+
+  // logical devices: GPU-major enumeration (the driver's order), partition p of
+  // GPU i gets HIP id / render node after every partition of GPUs 0..i-1
+  int partition_count(int i) override {
+    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    return partitions_for_mode(gpus[i].compute);
+  }
+
+  int partition_info(int i, int p, nos_part_info* o) override {
+    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    const FakeGpu& g = gpus[i];
+    const int n = partitions_for_mode(g.compute);
+    if (p < 0 || p >= n) return NOS_SMI_ERR_BAD_INDEX;
+    int base = 0;
+    for (int j = 0; j < i; ++j)
+      if (!gpus[j].lost) base += partitions_for_mode(gpus[j].compute);
+    std::memset(o, 0, sizeof(*o));
+    o->gpu_index = i;
+    o->partition = p;
+    o->hip_id = base + p;
+    o->drm_render = 128 + base + p;
+    o->kfd_node = 1 + base + p;
+    o->num_cus = g.cus / n;
+    o->num_xcds = g.xcds / n > 0 ? g.xcds / n : 1;
+    o->memory_shared = (g.memory == 1 && n > 1) ? 1 : 0;
+    o->vram_mb = g.vram_mb / n;
+    std::snprintf(o->bdf, sizeof(o->bdf), "0000:%02x:00.%d", 0x05 + 0x10 * i, p);
+    std::snprintf(o->uuid, sizeof(o->uuid), "GPU-fake-mi355x-%04d-p%d", i, p);
     return NOS_SMI_OK;
   }
 
@@ -311,6 +371,7 @@ struct SmiApi {
   NOS_SMI_FN(amdsmi_get_gpu_process_list);
   NOS_SMI_FN(amdsmi_topo_get_link_type);
   NOS_SMI_FN(amdsmi_topo_get_link_weight);
+  NOS_SMI_FN(amdsmi_get_gpu_kfd_info);
 #undef NOS_SMI_FN
 
   bool load() {
@@ -339,6 +400,7 @@ struct SmiApi {
     NOS_SMI_LOAD(amdsmi_get_gpu_process_list);
     NOS_SMI_LOAD(amdsmi_topo_get_link_type);
     NOS_SMI_LOAD(amdsmi_topo_get_link_weight);
+    NOS_SMI_LOAD(amdsmi_get_gpu_kfd_info);
 #undef NOS_SMI_LOAD
     return amdsmi_init && amdsmi_get_socket_handles && amdsmi_get_processor_handles;
   }
@@ -346,24 +408,50 @@ struct SmiApi {
 
 struct AmdSmiBackend : Backend {
   SmiApi api;
-  std::vector<amdsmi_processor_handle> handles;
+  // physical GPU -> its processor handles (one per logical partition, ordered
+  // by KFD partition id; SPX: exactly one)
+  std::vector<std::vector<amdsmi_processor_handle>> gpus;
   bool allow_set = false;
 
   int open(bool allow_set_) {
     allow_set = allow_set_;
     if (!api.load()) return NOS_SMI_ERR_BACKEND;
     if (api.amdsmi_init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
+    return enumerate();
+  }
+
+  uint32_t partition_id(amdsmi_processor_handle h) {
+    amdsmi_kfd_info_t kfd{};
+    if (api.amdsmi_get_gpu_kfd_info && api.amdsmi_get_gpu_kfd_info(h, &kfd) == AMDSMI_STATUS_SUCCESS &&
+        kfd.current_partition_id != 0xFFFFFFFFu)
+      return kfd.current_partition_id;
+    amdsmi_bdf_t bdf{};
+    if (api.amdsmi_get_gpu_device_bdf && api.amdsmi_get_gpu_device_bdf(h, &bdf) == AMDSMI_STATUS_SUCCESS)
+      return (uint32_t)bdf.function_number;
+    return 0;
+  }
+
+  // one amd-smi socket = one physical device (its PCI bus/device); a socket
+  // lists the processor handles of every partition the current mode exposes
+  int enumerate() {
+    gpus.clear();
     uint32_t ns = 0;
     if (api.amdsmi_get_socket_handles(&ns, nullptr) != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
     std::vector<amdsmi_socket_handle> sockets(ns);
-    if (ns && api.amdsmi_get_socket_handles(&ns, sockets.data()) != AMDSMI_STATUS_SUCCESS)
-      return NOS_SMI_ERR_BACKEND;
+    if (ns && api.amdsmi_get_socket_handles(&ns, sockets.data()) != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
     for (uint32_t s = 0; s < ns; ++s) {
       uint32_t np = 0;
-      if (api.amdsmi_get_processor_handles(sockets[s], &np, nullptr) != AMDSMI_STATUS_SUCCESS) continue;
+      if (api.amdsmi_get_processor_handles(sockets[s], &np, nullptr) != AMDSMI_STATUS_SUCCESS || np == 0) continue;
       std::vector<amdsmi_processor_handle> ph(np);
-      if (np && api.amdsmi_get_processor_handles(sockets[s], &np, ph.data()) == AMDSMI_STATUS_SUCCESS)
-        handles.insert(handles.end(), ph.begin(), ph.begin() + np);
+      if (api.amdsmi_get_processor_handles(sockets[s], &np, ph.data()) != AMDSMI_STATUS_SUCCESS) continue;
+      ph.resize(np);
+      std::vector<std::pair<uint32_t, amdsmi_processor_handle>> keyed;
+      for (auto h : ph) keyed.emplace_back(partition_id(h), h);
+      std::stable_sort(keyed.begin(), keyed.end(),
+                       [](const auto& x, const auto& y) { return x.first < y.first; });
+      std::vector<amdsmi_processor_handle> parts;
+      for (auto& kv : keyed) parts.push_back(kv.second);
+      gpus.push_back(parts);
     }
     return NOS_SMI_OK;
   }
@@ -373,25 +461,67 @@ struct AmdSmiBackend : Backend {
     if (api.h) dlclose(api.h);
   }
 
-  bool ok(int i) const { return i >= 0 && i < (int)handles.size(); }
+  bool ok(int i) const { return i >= 0 && i < (int)gpus.size() && !gpus[i].empty(); }
 
-  int count() override { return (int)handles.size(); }
+  int count() override { return (int)gpus.size(); }
+
+  long long vram_mb(amdsmi_processor_handle h) {
+    amdsmi_vram_info_t vram{};
+    if (api.amdsmi_get_gpu_vram_info && api.amdsmi_get_gpu_vram_info(h, &vram) == AMDSMI_STATUS_SUCCESS)
+      return (long long)vram.vram_size;
+    return 0;
+  }
+
+  int cus(amdsmi_processor_handle h) {
+    amdsmi_asic_info_t asic{};
+    if (api.amdsmi_get_gpu_asic_info && api.amdsmi_get_gpu_asic_info(h, &asic) == AMDSMI_STATUS_SUCCESS)
+      return asic.num_of_compute_units == 0xFFFFFFFFu ? 0 : (int)asic.num_of_compute_units;
+    return 0;
+  }
+
+  int xcds(amdsmi_processor_handle h) {
+    uint16_t x = 0;
+    if (api.amdsmi_get_gpu_xcd_counter && api.amdsmi_get_gpu_xcd_counter(h, &x) == AMDSMI_STATUS_SUCCESS) return x;
+    return 0;
+  }
+
+  int memory_mode(amdsmi_processor_handle h) {
+    char buf[64] = {0};
+    if (api.amdsmi_get_gpu_memory_partition &&
+        api.amdsmi_get_gpu_memory_partition(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS)
+      return parse_memory(buf);
+    return 0;
+  }
+
+  // total memory of the physical GPU: in NPS1 every partition sees the whole
+  // pool, in NPSn each sees its NUMA range
+  long long total_vram_mb(int i) {
+    const auto& parts = gpus[i];
+    long long mx = 0, sum = 0;
+    for (auto h : parts) {
+      const long long v = vram_mb(h);
+      mx = v > mx ? v : mx;
+      sum += v;
+    }
+    return (parts.size() > 1 && memory_mode(parts[0]) != 1) ? sum : mx;
+  }
 
   int info(int i, nos_gpu_info* o) override {
     if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
     std::memset(o, 0, sizeof(*o));
-    auto h = handles[i];
+    const auto& parts = gpus[i];
+    auto h = parts[0];
     o->index = i;
     o->hip_id = -1;
     o->drm_render = -1;
     amdsmi_asic_info_t asic{};
-    if (api.amdsmi_get_gpu_asic_info && api.amdsmi_get_gpu_asic_info(h, &asic) == AMDSMI_STATUS_SUCCESS) {
+    if (api.amdsmi_get_gpu_asic_info && api.amdsmi_get_gpu_asic_info(h, &asic) == AMDSMI_STATUS_SUCCESS)
       std::snprintf(o->market_name, sizeof(o->market_name), "%s", asic.market_name);
-      o->num_cus = asic.num_of_compute_units == 0xFFFFFFFFu ? 0 : (int)asic.num_of_compute_units;
+    for (auto ph : parts) {
+      o->num_cus += cus(ph);
+      o->num_xcds += xcds(ph);
     }
-    amdsmi_vram_info_t vram{};
-    if (api.amdsmi_get_gpu_vram_info && api.amdsmi_get_gpu_vram_info(h, &vram) == AMDSMI_STATUS_SUCCESS)
-      o->vram_mb = (long long)vram.vram_size;
+    o->vram_mb = total_vram_mb(i);
     amdsmi_bdf_t bdf{};
     if (api.amdsmi_get_gpu_device_bdf && api.amdsmi_get_gpu_device_bdf(h, &bdf) == AMDSMI_STATUS_SUCCESS)
       std::snprintf(o->bdf, sizeof(o->bdf), "%04llx:%02x:%02x.%x",
@@ -405,68 +535,111 @@ struct AmdSmiBackend : Backend {
       o->hip_id = (int)en.hip_id;
       o->drm_render = (int)en.drm_render;
     }
-    uint16_t xcd = 0;
-    if (api.amdsmi_get_gpu_xcd_counter && api.amdsmi_get_gpu_xcd_counter(h, &xcd) == AMDSMI_STATUS_SUCCESS)
-      o->num_xcds = xcd;
     char buf[64] = {0};
     if (api.amdsmi_get_gpu_compute_partition &&
         api.amdsmi_get_gpu_compute_partition(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS)
       o->compute_mode = parse_compute(buf);
-    std::memset(buf, 0, sizeof(buf));
-    if (api.amdsmi_get_gpu_memory_partition &&
-        api.amdsmi_get_gpu_memory_partition(h, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS)
-      o->memory_mode = parse_memory(buf);
-    o->num_partitions = partitions_for_mode(o->compute_mode);
+    o->memory_mode = memory_mode(h);
+    o->num_partitions = (int)parts.size() > 1 ? (int)parts.size() : partitions_for_mode(o->compute_mode);
     return NOS_SMI_OK;
   }
 
-  int set_compute(int i, int mode) override {
+  int partition_count(int i) override {
     if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
-    if (!allow_set || !api.amdsmi_set_gpu_compute_partition) return NOS_SMI_ERR_UNSUPPORTED;
-    int n = 0;
-    nos_proc_info tmp[1];
-    if (processes(i, tmp, 1, &n) == NOS_SMI_OK && n > 0) return NOS_SMI_ERR_BUSY;
-    auto st = api.amdsmi_set_gpu_compute_partition(handles[i], (amdsmi_compute_partition_type_t)mode);
-    return st == AMDSMI_STATUS_SUCCESS ? NOS_SMI_OK : NOS_SMI_ERR_BACKEND;
+    return (int)gpus[i].size();
   }
 
-  int set_memory(int i, int mode) override {
+  int partition_info(int i, int p, nos_part_info* o) override {
     if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
-    if (!allow_set || !api.amdsmi_set_gpu_memory_partition) return NOS_SMI_ERR_UNSUPPORTED;
+    const auto& parts = gpus[i];
+    if (p < 0 || p >= (int)parts.size()) return NOS_SMI_ERR_BAD_INDEX;
+    auto h = parts[p];
+    std::memset(o, 0, sizeof(*o));
+    o->gpu_index = i;
+    o->partition = p;
+    o->hip_id = -1;
+    o->drm_render = -1;
+    o->kfd_node = -1;
+    amdsmi_enumeration_info_t en{};
+    if (api.amdsmi_get_gpu_enumeration_info &&
+        api.amdsmi_get_gpu_enumeration_info(h, &en) == AMDSMI_STATUS_SUCCESS) {
+      o->hip_id = (int)en.hip_id;
+      o->drm_render = (int)en.drm_render;
+    }
+    amdsmi_kfd_info_t kfd{};
+    if (api.amdsmi_get_gpu_kfd_info && api.amdsmi_get_gpu_kfd_info(h, &kfd) == AMDSMI_STATUS_SUCCESS &&
+        kfd.node_id != 0xFFFFFFFFu)
+      o->kfd_node = (int)kfd.node_id;
+    o->num_cus = cus(h);
+    o->num_xcds = xcds(h);
+    const int n = (int)parts.size();
+    o->memory_shared = (n > 1 && memory_mode(h) == 1) ? 1 : 0;
+    o->vram_mb = o->memory_shared ? total_vram_mb(i) / n : vram_mb(h);
+    amdsmi_bdf_t bdf{};
+    if (api.amdsmi_get_gpu_device_bdf && api.amdsmi_get_gpu_device_bdf(h, &bdf) == AMDSMI_STATUS_SUCCESS)
+      std::snprintf(o->bdf, sizeof(o->bdf), "%04llx:%02x:%02x.%x",
+                    (unsigned long long)bdf.domain_number, (unsigned)bdf.bus_number,
+                    (unsigned)bdf.device_number, (unsigned)bdf.function_number);
+    unsigned ulen = sizeof(o->uuid);
+    if (api.amdsmi_get_gpu_device_uuid) api.amdsmi_get_gpu_device_uuid(h, &ulen, o->uuid);
+    return NOS_SMI_OK;
+  }
+
+  // a mode switch is GPU-wide: issued on the first partition's handle; the
+  // handle set changes with the mode, so the session re-enumerates
+  int set_mode(int i, bool compute, int mode) {
+    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (compute ? !api.amdsmi_set_gpu_compute_partition : !api.amdsmi_set_gpu_memory_partition)
+      return NOS_SMI_ERR_UNSUPPORTED;
+    if (!allow_set) return NOS_SMI_ERR_UNSUPPORTED;
     int n = 0;
     nos_proc_info tmp[1];
     if (processes(i, tmp, 1, &n) == NOS_SMI_OK && n > 0) return NOS_SMI_ERR_BUSY;
-    auto st = api.amdsmi_set_gpu_memory_partition(handles[i], (amdsmi_memory_partition_type_t)mode);
-    return st == AMDSMI_STATUS_SUCCESS ? NOS_SMI_OK : NOS_SMI_ERR_BACKEND;
+    auto h = gpus[i][0];
+    auto st = compute ? api.amdsmi_set_gpu_compute_partition(h, (amdsmi_compute_partition_type_t)mode)
+                      : api.amdsmi_set_gpu_memory_partition(h, (amdsmi_memory_partition_type_t)mode);
+    if (st != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
+    if (api.amdsmi_shut_down) api.amdsmi_shut_down();
+    if (api.amdsmi_init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
+    return enumerate();
   }
+
+  int set_compute(int i, int mode) override { return set_mode(i, true, mode); }
+
+  int set_memory(int i, int mode) override { return set_mode(i, false, mode); }
 
   int activity(int i, int* gfx, int* umc, int* mm) override {
     if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
     if (!api.amdsmi_get_gpu_activity) return NOS_SMI_ERR_UNSUPPORTED;
     amdsmi_engine_usage_t u{};
-    if (api.amdsmi_get_gpu_activity(handles[i], &u) != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
+    if (api.amdsmi_get_gpu_activity(gpus[i][0], &u) != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
     *gfx = (int)u.gfx_activity;
     *umc = (int)u.umc_activity;
     *mm = (int)u.mm_activity;
     return NOS_SMI_OK;
   }
 
+  // processes of every partition of the GPU (a repartition drains them all)
   int processes(int i, nos_proc_info* out, int max, int* n) override {
     if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
     if (!api.amdsmi_get_gpu_process_list) return NOS_SMI_ERR_UNSUPPORTED;
-    uint32_t cnt = 0;
-    std::vector<amdsmi_proc_info_t> buf(64);
-    cnt = (uint32_t)buf.size();
-    auto st = api.amdsmi_get_gpu_process_list(handles[i], &cnt, buf.data());
-    if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) return NOS_SMI_ERR_BACKEND;
-    int k = 0;
-    for (uint32_t p = 0; p < cnt && p < buf.size(); ++p) {
-      if (k < max) {
-        out[k].pid = buf[p].pid;
-        out[k].cu_occupancy = buf[p].cu_occupancy;
-        out[k].vram_bytes = (long long)buf[p].memory_usage.vram_mem;
-        std::snprintf(out[k].name, sizeof(out[k].name), "%s", buf[p].name);
+    std::map<unsigned, nos_proc_info> seen;
+    for (auto h : gpus[i]) {
+      std::vector<amdsmi_proc_info_t> buf(64);
+      uint32_t cnt = (uint32_t)buf.size();
+      auto st = api.amdsmi_get_gpu_process_list(h, &cnt, buf.data());
+      if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) return NOS_SMI_ERR_BACKEND;
+      for (uint32_t p = 0; p < cnt && p < buf.size(); ++p) {
+        nos_proc_info& q = seen[buf[p].pid];
+        q.pid = buf[p].pid;
+        q.cu_occupancy += buf[p].cu_occupancy;
+        q.vram_bytes += (long long)buf[p].memory_usage.vram_mem;
+        std::snprintf(q.name, sizeof(q.name), "%s", buf[p].name);
       }
+    }
+    int k = 0;
+    for (auto& kv : seen) {
+      if (k < max) out[k] = kv.second;
       ++k;
     }
     *n = k;
@@ -484,9 +657,9 @@ struct AmdSmiBackend : Backend {
     if (!api.amdsmi_topo_get_link_type) return NOS_SMI_ERR_UNSUPPORTED;
     uint64_t h = 0, w = 0;
     amdsmi_link_type_t t = AMDSMI_LINK_TYPE_UNKNOWN;
-    if (api.amdsmi_topo_get_link_type(handles[i], handles[j], &h, &t) != AMDSMI_STATUS_SUCCESS)
+    if (api.amdsmi_topo_get_link_type(gpus[i][0], gpus[j][0], &h, &t) != AMDSMI_STATUS_SUCCESS)
       return NOS_SMI_ERR_BACKEND;
-    if (api.amdsmi_topo_get_link_weight) api.amdsmi_topo_get_link_weight(handles[i], handles[j], &w);
+    if (api.amdsmi_topo_get_link_weight) api.amdsmi_topo_get_link_weight(gpus[i][0], gpus[j][0], &w);
     *type = (int)t;
     *hops = (long long)h;
     *weight = (long long)w;
@@ -566,6 +739,14 @@ NOS_API int nos_smi_link(int i, int j, int* type, long long* hops, long long* we
   NOS_SMI_GUARD();
   return g_backend->link(i, j, type, hops, weight);
 }
+NOS_API int nos_smi_partition_count(int i) {
+  NOS_SMI_GUARD();
+  return g_backend->partition_count(i);
+}
+NOS_API int nos_smi_partition_info(int i, int p, nos_part_info* out) {
+  NOS_SMI_GUARD();
+  return g_backend->partition_info(i, p, out);
+}
 NOS_API int nos_smi_fake_inject(const char* fault) {
   NOS_SMI_GUARD();
   return g_backend->inject(fault);
@@ -587,3 +768,4 @@ NOS_API int nos_smi_struct_sizes(int* gpu_info, int* proc_info) {
   *proc_info = (int)sizeof(nos_proc_info);
   return NOS_SMI_OK;
 }
+NOS_API int nos_smi_part_struct_size() { return (int)sizeof(nos_part_info); }

@@ -32,7 +32,8 @@ from dataclasses import dataclass, field
 import yaml
 
 from ..api import constants as C
-from ..gpu.amdsmi import PARTITIONS_PER_MODE, AmdSmi, GpuInfo
+from ..gpu.amdpart import partition_profile
+from ..gpu.amdsmi import AmdSmi, GpuInfo
 from ..gpu.topology import MI355X_CUS_PER_XCD, MI355X_MEMORY_GB, MI355X_XCDS, CUSlotSet, layout_slots, logical_cu
 from ..ops.streams import mask_hex
 from ..partitioning import scoring
@@ -49,6 +50,8 @@ class Device:
     partition: int = 0          # logical partition index (amdpart)
     profile: str = ""           # partition / slice profile
     memory_gb: int = 0
+    hip_id: int = -1            # logical device's HIP ordinal (amdpart; -1: the GPU's)
+    drm_render: int = -1
 
 
 @dataclass
@@ -110,15 +113,16 @@ class NosAmdDevicePlugin:
                             devs[did] = Device(did, C.AMD_SLICE_RESOURCE_PREFIX + prof, gi.index, profile=prof,
                                                memory_gb=int(s.get("memoryGB", prof[:-2])))
             elif self.mode == C.PARTITIONING_AMDPART:
+                # one device per logical partition amd-smi enumerates for the GPU, named
+                # from the GPU's reported memory / XCDs (same function as the planner)
                 for gi in gpus:
-                    nparts = PARTITIONS_PER_MODE.get(gi.compute_mode, 1)
-                    xcds = max(1, (gi.num_xcds or MI355X_XCDS) // nparts)
-                    gb = gi.memory_gb // nparts
-                    prof = f"{xcds}xcd.{gb}gb"
+                    parts = self.smi.partitions(gi.index)
+                    prof = str(partition_profile(gi.memory_gb, gi.num_xcds or MI355X_XCDS, len(parts)))
                     res = C.RESOURCE_AMD_GPU if self.expose_partitions_as_gpu else C.AMD_PARTITION_RESOURCE_PREFIX + prof
-                    for k in range(nparts):
-                        did = f"{gi.uuid}::p{k}"
-                        devs[did] = Device(did, res, gi.index, partition=k, profile=prof, memory_gb=gb)
+                    for pi in parts:
+                        did = f"{gi.uuid}::p{pi.partition}"
+                        devs[did] = Device(did, res, gi.index, partition=pi.partition, profile=prof,
+                                           memory_gb=pi.memory_gb, hip_id=pi.hip_id, drm_render=pi.drm_render)
             else:
                 for gi in gpus:
                     devs[gi.uuid] = Device(gi.uuid, C.RESOURCE_AMD_GPU, gi.index, profile="", memory_gb=gi.memory_gb)
@@ -126,7 +130,8 @@ class NosAmdDevicePlugin:
             for did, owner in self.allocated.items():
                 if did not in devs and did in self.devices:
                     d = self.devices[did]
-                    devs[did] = Device(d.id, d.resource, d.gpu_index, False, d.partition, d.profile, d.memory_gb)
+                    devs[did] = Device(d.id, d.resource, d.gpu_index, False, d.partition, d.profile, d.memory_gb,
+                                       d.hip_id, d.drm_render)
             before = {k: (d.resource, d.healthy) for k, d in self.devices.items()}
             self.devices = devs
             self._layout_cu_slots()
@@ -160,7 +165,8 @@ class NosAmdDevicePlugin:
                 slots[did] = CUSlotSet(sl, MI355X_XCDS)
             for did in bad:
                 d = self.devices[did]
-                self.devices[did] = Device(d.id, d.resource, d.gpu_index, False, d.partition, d.profile, d.memory_gb)
+                self.devices[did] = Device(d.id, d.resource, d.gpu_index, False, d.partition, d.profile, d.memory_gb,
+                                           d.hip_id, d.drm_render)
                 log.warning("slice %s gets no CU slots (%s policy, %d allocated replicas hold the rest): unhealthy",
                             did, self.cu_policy, len(keep))
         self.cu_slots = slots
@@ -252,14 +258,8 @@ class NosAmdDevicePlugin:
                 if not d.healthy:
                     raise RuntimeError(f"device {did} is unhealthy")
                 gi = gpus.get(d.gpu_index)
-                hip = str(gi.hip_id if gi and gi.hip_id >= 0 else d.gpu_index)
-                if resource.startswith(C.AMD_PARTITION_RESOURCE_PREFIX) or \
-                        (self.mode == C.PARTITIONING_AMDPART and resource == C.RESOURCE_AMD_GPU):
-                    # logical devices are enumerated GPU-major by the driver: the
-                    # partitions of GPU g follow all partitions of GPUs before it
-                    base = sum(PARTITIONS_PER_MODE.get(g.compute_mode, 1) for g in gpus.values()
-                               if (g.hip_id if g.hip_id >= 0 else g.index) < int(hip))
-                    hip = str(base + d.partition)
+                # logical partitions carry their own HIP id (amd-smi enumeration info)
+                hip = str(d.hip_id if d.hip_id >= 0 else (gi.hip_id if gi and gi.hip_id >= 0 else d.gpu_index))
                 if hip not in visible:
                     visible.append(hip)
                 if resource.startswith(C.AMD_SLICE_RESOURCE_PREFIX):
@@ -268,7 +268,8 @@ class NosAmdDevicePlugin:
                         mask_cus.update(s.cus())
                 mem += d.memory_gb
                 self.allocated[did] = owner or "unknown"
-                render = (gi.drm_render if gi and gi.drm_render >= 0 else 128 + d.gpu_index)
+                render = (d.drm_render if d.drm_render >= 0 else
+                          gi.drm_render if gi and gi.drm_render >= 0 else 128 + d.gpu_index)
                 dev = f"/dev/dri/renderD{render}"
                 if dev not in alloc.devices:
                     alloc.devices.append(dev)

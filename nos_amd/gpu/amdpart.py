@@ -108,10 +108,18 @@ class ModeGeometry:
         return f"{self.compute}/{self.memory}"
 
 
+def partition_profile(memory_gb: int, xcds: int, parts: int) -> PartitionProfile:
+    """The profile of one of ``parts`` logical devices of a GPU with
+    ``memory_gb`` / ``xcds`` (as amd-smi reports them).  The planner (from the
+    node labels) and the device plugin (from amd-smi) both name partitions
+    through this one function, so their profiles always agree."""
+    return PartitionProfile(f"{max(1, xcds // parts)}xcd.{memory_gb // parts}gb")
+
+
 def mi355x_geometries(memory_gb: int = 288, xcds: int = 8) -> list[ModeGeometry]:
     out = []
     for compute, parts in (("SPX", 1), ("DPX", 2), ("QPX", 4), ("CPX", 8)):
-        prof = PartitionProfile(f"{xcds // parts}xcd.{memory_gb // parts}gb")
+        prof = partition_profile(memory_gb, xcds, parts)
         for memory in ("NPS1", "NPS2") if parts in (2, 8) else ("NPS1",):
             out.append(ModeGeometry(compute, memory, Geometry({prof: parts})))
     return out
@@ -119,7 +127,9 @@ def mi355x_geometries(memory_gb: int = 288, xcds: int = 8) -> list[ModeGeometry]
 
 _DEFAULT_MODELS = ["AMD Instinct MI355X", "AMD-Instinct-MI355X", "MI355X",
                    "AMD Instinct MI350X", "AMD-Instinct-MI350X", "MI350X"]
-_known: dict[str, list[ModeGeometry]] = {m: mi355x_geometries() for m in _DEFAULT_MODELS}
+# explicitly configured tables (knownPartitionGeometriesFile) win; otherwise the
+# geometries of a known model are derived from the memory / XCDs amd-smi reports
+_known: dict[str, list[ModeGeometry]] = {}
 
 
 def set_known_geometries(table: dict[str, list[ModeGeometry]]) -> None:
@@ -128,8 +138,17 @@ def set_known_geometries(table: dict[str, list[ModeGeometry]]) -> None:
     _known.update(table)
 
 
-def get_allowed_geometries(model: str) -> list[ModeGeometry] | None:
-    return _known.get(model)
+def get_allowed_geometries(model: str, memory_mb: int | None = None, xcds: int | None = None
+                           ) -> list[ModeGeometry] | None:
+    """Configured table of ``model``, else (MI350-series models) the mode
+    geometries of the GPU's measured memory (``amd.com/gpu.memory``, MB) and
+    XCD count -- never a hard-coded 288 GB when the node reports its size."""
+    if model in _known:
+        return _known[model]
+    if model in _DEFAULT_MODELS:
+        gb = int(round(memory_mb / 1024)) if memory_mb else 288
+        return mi355x_geometries(gb, xcds or 8)
+    return None
 
 
 def validate_known(table: dict[str, list[ModeGeometry]]) -> None:
@@ -176,8 +195,9 @@ class PartitionGPU:
     memory_mode_preference: str = "NPS1"
 
     @classmethod
-    def new(cls, model: str, index: int, used=None, free=None) -> "PartitionGPU":
-        allowed = get_allowed_geometries(model)
+    def new(cls, model: str, index: int, used=None, free=None, memory_mb: int | None = None,
+            xcds: int | None = None) -> "PartitionGPU":
+        allowed = get_allowed_geometries(model, memory_mb, xcds)
         if allowed is None:
             raise GenericError(f"model {model!r} is not associated with any known GPU")
         return cls(model, index, allowed, dict(used or {}), dict(free or {}))
@@ -296,6 +316,9 @@ class PartitionNode:
             raise GenericError("node is nil")
         model = get_model(node)
         count = get_count(node)
+        labels = ko.labels(node)
+        mem = int(labels[C.LABEL_AMD_MEMORY]) if labels.get(C.LABEL_AMD_MEMORY, "").isdigit() else None
+        xcds = int(labels[C.LABEL_AMD_XCDS]) if labels.get(C.LABEL_AMD_XCDS, "").isdigit() else None
         status, _ = parse_node_annotations(node)
         by_gpu: dict[int, list] = {}
         for a in status:
@@ -309,11 +332,11 @@ class PartitionNode:
                 except ValueError:
                     continue
                 (used if a.is_used() else free)[p] = a.quantity
-            gpus.append(PartitionGPU.new(model, idx, used, free))
+            gpus.append(PartitionGPU.new(model, idx, used, free, mem, xcds))
         have = {g.index for g in gpus}
         for i in range(count):
             if i not in have:
-                gpus.append(PartitionGPU.new(model, i))
+                gpus.append(PartitionGPU.new(model, i, memory_mb=mem, xcds=xcds))
         gpus.sort(key=lambda g: g.index)
         return cls(ko.name(node), gpus, ni)
 

@@ -5,6 +5,8 @@ the MI355X replacement for the reference's NVML client
 (``pkg/gpu/nvml/interface.go:23-35``).  Two backends share one interface:
 
 * ``AmdSmi.real()``  -- amd-smi (read-only unless ``allow_set=True``);
+  indices are PHYSICAL GPUs; :meth:`AmdSmi.partitions` lists the logical
+  devices (one amd-smi processor handle each) of a GPU in DPX/QPX/CPX;
 * ``AmdSmi.fake(...)`` -- an in-memory MI355X node (C++), with programmable
   processes, activity and fault injection, for the simulator and tests.
 """
@@ -42,6 +44,13 @@ class _GpuInfo(ctypes.Structure):
                 ("market_name", ctypes.c_char * 128)]
 
 
+class _PartInfo(ctypes.Structure):
+    _fields_ = [("gpu_index", ctypes.c_int), ("partition", ctypes.c_int), ("hip_id", ctypes.c_int),
+                ("drm_render", ctypes.c_int), ("kfd_node", ctypes.c_int), ("num_cus", ctypes.c_int),
+                ("num_xcds", ctypes.c_int), ("memory_shared", ctypes.c_int), ("vram_mb", ctypes.c_longlong),
+                ("bdf", ctypes.c_char * 32), ("uuid", ctypes.c_char * 64)]
+
+
 class _ProcInfo(ctypes.Structure):
     _fields_ = [("pid", ctypes.c_uint), ("cu_occupancy", ctypes.c_uint), ("vram_bytes", ctypes.c_longlong),
                 ("name", ctypes.c_char * 64)]
@@ -61,6 +70,28 @@ class GpuInfo:
     bdf: str
     uuid: str
     market_name: str
+
+    @property
+    def memory_gb(self) -> int:
+        return int(round(self.vram_mb / 1024))
+
+
+@dataclass(frozen=True)
+class PartitionInfo:
+    """One logical device (compute partition) of a physical GPU.  In SPX a GPU
+    has exactly one, equal to the GPU itself."""
+
+    gpu_index: int
+    partition: int
+    hip_id: int
+    drm_render: int
+    kfd_node: int
+    num_cus: int
+    num_xcds: int
+    memory_shared: bool   # NPS1 with several partitions: vram_mb is a 1/n share of one pool
+    vram_mb: int
+    bdf: str
+    uuid: str
 
     @property
     def memory_gb(self) -> int:
@@ -99,10 +130,13 @@ def _L():
             L.nos_smi_fake_add_process.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_longlong, ctypes.c_uint]
             L.nos_smi_fake_remove_process.argtypes = [ctypes.c_int, ctypes.c_uint]
             L.nos_smi_fake_set_activity.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+            L.nos_smi_partition_count.argtypes = [ctypes.c_int]
+            L.nos_smi_partition_info.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_PartInfo)]
             L.nos_smi_struct_sizes.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
             a, b = ctypes.c_int(), ctypes.c_int()
             L.nos_smi_struct_sizes(ctypes.byref(a), ctypes.byref(b))
-            if a.value != ctypes.sizeof(_GpuInfo) or b.value != ctypes.sizeof(_ProcInfo):
+            if (a.value != ctypes.sizeof(_GpuInfo) or b.value != ctypes.sizeof(_ProcInfo)
+                    or L.nos_smi_part_struct_size() != ctypes.sizeof(_PartInfo)):
                 raise RuntimeError("libnos_amdsmi ABI mismatch")
             _lib = L
     return _lib
@@ -151,6 +185,22 @@ class AmdSmi:
 
     def gpus(self) -> list[GpuInfo]:
         return [self.gpu(i) for i in range(self.count())]
+
+    def partitions(self, i: int) -> list[PartitionInfo]:
+        """Logical devices of physical GPU ``i`` in enumeration order (amd-smi
+        lists one processor handle per partition; the library groups them)."""
+        n = _L().nos_smi_partition_count(i)
+        if n < 0:
+            raise AmdSmiError(n, f"partition_count({i})")
+        out = []
+        for p in range(n):
+            x = _PartInfo()
+            rc = _L().nos_smi_partition_info(i, p, ctypes.byref(x))
+            if rc != 0:
+                raise AmdSmiError(rc, f"partition_info({i}, {p})")
+            out.append(PartitionInfo(x.gpu_index, x.partition, x.hip_id, x.drm_render, x.kfd_node, x.num_cus,
+                                     x.num_xcds, bool(x.memory_shared), x.vram_mb, x.bdf.decode(), x.uuid.decode()))
+        return out
 
     def activity(self, i: int) -> dict[str, int]:
         a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import threading
 
-from .amdsmi import PARTITIONS_PER_MODE, AmdSmiError, GpuInfo, ProcInfo
+from .amdsmi import PARTITIONS_PER_MODE, AmdSmiError, GpuInfo, PartitionInfo, ProcInfo
 
 _MEMORY_MODES = ("NPS1", "NPS2", "NPS4", "NPS8")
 
@@ -45,13 +45,29 @@ class FakeSmi:
         with self._lock:
             if i < 0 or i >= len(self.compute) or i in self.lost:
                 raise AmdSmiError(-2, f"gpu({i})")
+            base = sum(PARTITIONS_PER_MODE[self.compute[j]] for j in range(i) if j not in self.lost)
             return GpuInfo(index=i, num_cus=self.cus, num_xcds=self.xcds, compute_mode=self.compute[i],
                            memory_mode=self.memory[i], num_partitions=PARTITIONS_PER_MODE[self.compute[i]],
-                           hip_id=i, drm_render=128 + i, vram_mb=self.vram_mb, bdf=f"0000:{0x11 + i:02x}:00.0",
+                           hip_id=base, drm_render=128 + base, vram_mb=self.vram_mb, bdf=f"0000:{0x11 + i:02x}:00.0",
                            uuid=f"GPU-{self.node}-{i:04d}", market_name=self.model)
 
     def gpus(self) -> list[GpuInfo]:
         return [self.gpu(i) for i in range(len(self.compute)) if i not in self.lost]
+
+    def partitions(self, i: int) -> list[PartitionInfo]:
+        """Logical devices of GPU ``i``, numbered GPU-major like the driver
+        enumerates them (same model as the C++ fake backend)."""
+        with self._lock:
+            if i < 0 or i >= len(self.compute) or i in self.lost:
+                raise AmdSmiError(-2, f"partitions({i})")
+            base = sum(PARTITIONS_PER_MODE[self.compute[j]] for j in range(i) if j not in self.lost)
+            n = PARTITIONS_PER_MODE[self.compute[i]]
+            shared = self.memory[i] == "NPS1" and n > 1
+            return [PartitionInfo(gpu_index=i, partition=p, hip_id=base + p, drm_render=128 + base + p,
+                                  kfd_node=1 + base + p, num_cus=self.cus // n, num_xcds=max(1, self.xcds // n),
+                                  memory_shared=shared, vram_mb=self.vram_mb // n,
+                                  bdf=f"0000:{0x11 + i:02x}:00.{p}", uuid=f"GPU-{self.node}-{i:04d}-p{p}")
+                    for p in range(n)]
 
     def activity(self, i: int) -> dict[str, int]:
         return {"gfx": self.activity_gfx[i], "umc": self.activity_umc[i], "mm": 0}

@@ -40,6 +40,29 @@ def _local_gpu(smi):
     return gpus[0]
 
 
+def test_amdsmi_real_partitions_map_to_physical_gpus():
+    """Physical GPUs vs logical devices: every amd-smi processor handle is a
+    partition of exactly one physical GPU, HIP ids are unique, and (SPX) each
+    GPU's single partition is the GPU itself with its whole memory/CUs."""
+    smi = _smi()
+    try:
+        gpus = smi.gpus()
+        hip_ids = []
+        for g in gpus:
+            parts = smi.partitions(g.index)
+            assert len(parts) == g.num_partitions, (g, parts)
+            assert sum(p.num_cus for p in parts) == g.num_cus, parts
+            assert all(p.gpu_index == g.index for p in parts)
+            if len(parts) == 1:
+                assert parts[0].hip_id == g.hip_id and parts[0].memory_gb == g.memory_gb, (g, parts[0])
+            hip_ids += [p.hip_id for p in parts]
+        assert len(set(hip_ids)) == len(hip_ids)
+        visible = torch.cuda.device_count()
+        assert set(range(visible)) <= set(hip_ids) or len(hip_ids) >= visible, (hip_ids, visible)
+    finally:
+        smi.close()
+
+
 def test_amdsmi_real_readonly_queries():
     smi = _smi()
     try:
