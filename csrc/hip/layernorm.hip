@@ -14,7 +14,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(
     const unsigned short* __restrict__ x, const unsigned short* __restrict__ res,
     unsigned short* __restrict__ y, unsigned short* __restrict__ sum_out,
     const unsigned short* __restrict__ gamma, const unsigned short* __restrict__ beta, int rows,
-    int D, int ldx, int ldy, float eps) {
+    int D, int ldx, int ldy, int ldr, int lds, float eps) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[i][e] = nos::bf16_to_f32((unsigned short)xv[e]);
       if (res) {
-        const s16x8_t rv = *reinterpret_cast<const s16x8_t*>(res + (long long)row * ldx + vi * 8);
+        const s16x8_t rv = *reinterpret_cast<const s16x8_t*>(res + (long long)row * ldr + vi * 8);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[i][e] += nos::bf16_to_f32((unsigned short)rv[e]);
       }
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(
           sv[e] = (short)bb;
           v[i][e] = nos::bf16_to_f32(bb);
         }
-        *reinterpret_cast<s16x8_t*>(sum_out + (long long)row * ldx + vi * 8) = sv;
+        *reinterpret_cast<s16x8_t*>(sum_out + (long long)row * lds + vi * 8) = sv;
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) s += v[i][e];
@@ -83,9 +83,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(
 
 NOS_API int nos_layernorm_bf16(const void* x, const void* res, void* y, void* sum_out,
                                const void* gamma, const void* beta, int rows, int D, int ldx,
-                               int ldy, float eps, hipStream_t stream) {
+                               int ldy, int ldr, int lds, float eps, hipStream_t stream) {
+  // every row stride is the tensor's own (x, y, residual, sum_out); 16-byte vectors
   if (rows <= 0 || D <= 0 || (D % 8) != 0 || D > 4096) return (int)hipErrorInvalidValue;
-  if ((ldx % 8) || (ldy % 8)) return (int)hipErrorInvalidValue;
+  if ((ldx % 8) || (ldy % 8) || (ldr % 8) || (lds % 8) || ldx < D || ldy < D) return (int)hipErrorInvalidValue;
+  if ((res && ldr < D) || (sum_out && lds < D)) return (int)hipErrorInvalidValue;
   const int nvec = D / 8;
   const dim3 grid((rows + 3) / 4), block(256);
   auto X = (const unsigned short*)x;
@@ -95,12 +97,12 @@ NOS_API int nos_layernorm_bf16(const void* x, const void* res, void* y, void* su
   auto G = (const unsigned short*)gamma;
   auto Bt = (const unsigned short*)beta;
   if (nvec <= 64)
-    hipLaunchKernelGGL(layernorm_kernel<1>, grid, block, 0, stream, X, Rs, Y, S, G, Bt, rows, D, ldx, ldy, eps);
+    hipLaunchKernelGGL(layernorm_kernel<1>, grid, block, 0, stream, X, Rs, Y, S, G, Bt, rows, D, ldx, ldy, ldr, lds, eps);
   else if (nvec <= 128)
-    hipLaunchKernelGGL(layernorm_kernel<2>, grid, block, 0, stream, X, Rs, Y, S, G, Bt, rows, D, ldx, ldy, eps);
+    hipLaunchKernelGGL(layernorm_kernel<2>, grid, block, 0, stream, X, Rs, Y, S, G, Bt, rows, D, ldx, ldy, ldr, lds, eps);
   else if (nvec <= 256)
-    hipLaunchKernelGGL(layernorm_kernel<4>, grid, block, 0, stream, X, Rs, Y, S, G, Bt, rows, D, ldx, ldy, eps);
+    hipLaunchKernelGGL(layernorm_kernel<4>, grid, block, 0, stream, X, Rs, Y, S, G, Bt, rows, D, ldx, ldy, ldr, lds, eps);
   else
-    hipLaunchKernelGGL(layernorm_kernel<8>, grid, block, 0, stream, X, Rs, Y, S, G, Bt, rows, D, ldx, ldy, eps);
+    hipLaunchKernelGGL(layernorm_kernel<8>, grid, block, 0, stream, X, Rs, Y, S, G, Bt, rows, D, ldx, ldy, ldr, lds, eps);
   return (int)hipGetLastError();
 }

@@ -84,7 +84,11 @@ def serve_metrics(addr: str) -> None:
     log.info("metrics on :%d", port)
 
 
-def run_until_signal(stop: Callable[[], None]) -> None:
+def run_until_signal(stop: Callable[[], None], lost: threading.Event | None = None) -> int:
+    """Run until SIGTERM/SIGINT (exit 0) or until ``lost`` fires -- the leader
+    lease was lost -- then stop and return 1 so the process exits non-zero
+    and its supervisor restarts it as a follower (controller-runtime's
+    behaviour; never re-exec in place)."""
     ev = threading.Event()
 
     def _h(signum, frame):
@@ -93,8 +97,13 @@ def run_until_signal(stop: Callable[[], None]) -> None:
 
     signal.signal(signal.SIGTERM, _h)
     signal.signal(signal.SIGINT, _h)
-    ev.wait()
+    while not ev.wait(0.5):
+        if lost is not None and lost.is_set():
+            log.error("leader election lost, exiting")
+            stop()
+            return 1
     stop()
+    return 0
 
 
 def load_config(path: str, kind: str):

@@ -49,8 +49,7 @@ def main(argv=None) -> int:
     common.serve_metrics(cfg.metrics.bind_address)
     mgr.start()
     log.info("gpuagent started on %s", node)
-    common.run_until_signal(mgr.stop)
-    return 0
+    return common.run_until_signal(mgr.stop, mgr.lost_leadership)
 
 
 if __name__ == "__main__":

@@ -53,8 +53,7 @@ def main(argv=None) -> int:
     mgr.start()
     log.info("gpupartitioner started (batch window %.0fs/%.0fs)", cfg.batch_window_timeout_seconds,
              cfg.batch_window_idle_seconds)
-    common.run_until_signal(mgr.stop)
-    return 0
+    return common.run_until_signal(mgr.stop, mgr.lost_leadership)
 
 
 if __name__ == "__main__":

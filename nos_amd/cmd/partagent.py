@@ -72,8 +72,7 @@ def main(argv=None) -> int:
     common.serve_metrics(cfg.metrics.bind_address)
     mgr.start()
     log.info("partition agent started on %s (%d GPUs)", node, len(smi.gpus()))
-    common.run_until_signal(mgr.stop)
-    return 0
+    return common.run_until_signal(mgr.stop, mgr.lost_leadership)
 
 
 if __name__ == "__main__":

@@ -174,15 +174,34 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
     if not x.is_cuda:
         return layernorm_ref(x, gamma, beta, eps, residual)
     D = x.shape[-1]
+    for name, t in (("x", x), ("gamma", gamma), ("beta", beta), ("residual", residual), ("out", out),
+                    ("sum_out", sum_out)):
+        if t is not None and t.dtype != torch.bfloat16:
+            raise ValueError(f"native layernorm takes bf16 tensors ({name} is {t.dtype})")
+    if gamma.numel() != D or beta.numel() != D or not (gamma.is_contiguous() and beta.is_contiguous()):
+        raise ValueError("gamma/beta must be contiguous [D]")
+
+    def rows2d(name, t):
+        t2 = t.reshape(-1, D)  # a view when the rows are evenly strided, else a copy (never written back)
+        if t2.stride(-1) != 1 or t2.shape[0] != x2.shape[0]:
+            raise ValueError(f"{name} must have unit inner stride and x's rows")
+        return t2
+
     x2 = x.reshape(-1, D)
+    if x2.stride(-1) != 1:
+        raise ValueError("x must have unit inner stride")
     rows = x2.shape[0]
     if out is None:
-        out = torch.empty_like(x)
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
     if residual is not None and sum_out is None:
-        sum_out = torch.empty_like(x)
-    rc = _lib.lib().nos_layernorm_bf16(x2.data_ptr(), _ptr(residual), out.data_ptr(), _ptr(sum_out),
-                                       gamma.data_ptr(), beta.data_ptr(), rows, D, x2.stride(0),
-                                       out.reshape(-1, D).stride(0), float(eps), _stream())
+        sum_out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    o2 = out.view(-1, D)
+    r2 = rows2d("residual", residual) if residual is not None else None
+    s2 = sum_out.view(-1, D) if sum_out is not None else None
+    rc = _lib.lib().nos_layernorm_bf16(x2.data_ptr(), _ptr(r2), o2.data_ptr(), _ptr(s2), gamma.data_ptr(),
+                                       beta.data_ptr(), rows, D, x2.stride(0), o2.stride(0),
+                                       r2.stride(0) if r2 is not None else D, s2.stride(0) if s2 is not None else D,
+                                       float(eps), _stream())
     _lib.check(rc, "nos_layernorm_bf16")
     return out, sum_out
 

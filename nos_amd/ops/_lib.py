@@ -36,7 +36,7 @@ _SIGS = {
     "nos_gemm_ln_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_int, c_int, c_float, c_int, c_void_p],
     "nos_layernorm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
-                           c_int, c_int, c_float, c_void_p],
+                           c_int, c_int, c_int, c_int, c_float, c_void_p],
     "nos_probe_placement": [c_void_p, c_int, c_int, c_void_p],
     "nos_probe_hbm_copy": [c_void_p, c_void_p, c_ll, c_int, c_void_p],
     "nos_probe_hbm": [c_void_p, c_ll, c_int, c_int, ctypes.POINTER(c_double)],

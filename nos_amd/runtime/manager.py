@@ -176,6 +176,103 @@ class LeaderElector:
                 pass
 
 
+class LeaseKeeper:
+    """Keeps a Lease the way client-go's leader elector does: renew every
+    ``retry_period``; when no renewal has succeeded for ``renew_deadline``
+    (renewals refused because another identity holds an unexpired lease, or
+    the API server unreachable), leadership is LOST: ``on_lost`` runs once
+    and the keeper stops.  controller-runtime then exits the process
+    (``leaderelection lost``); our binaries do the same via ``on_lost``, so a
+    process that lost the lease never acts as leader again (no split brain).
+
+    Deterministic use (fake clocks): call :meth:`tick` from the driving loop."""
+
+    def __init__(self, elector: LeaderElector, renew_deadline: float | None = None,
+                 retry_period: float | None = None, on_lost: Callable[[], None] | None = None):
+        self.elector = elector
+        self.clock = elector.clock
+        self.renew_deadline = renew_deadline if renew_deadline is not None else elector.duration * 2 / 3
+        self.retry_period = retry_period if retry_period is not None else max(0.2, elector.duration / 7.5)
+        self.on_lost = on_lost
+        self.leading = False
+        self.lost = threading.Event()
+        self._last_ok: float | None = None
+        self._last_try: float | None = None
+        self._stop = threading.Event()
+        self._thread: threading.Thread | None = None
+
+    def _try(self) -> bool:
+        try:
+            return self.elector.try_acquire_or_renew()
+        except Exception as e:  # API blip: counts as a failed renewal, never kills the keeper
+            log.warning("lease %s/%s renew error: %s", self.elector.ns, self.elector.name, e)
+            return False
+
+    def acquire(self, stop: threading.Event | None = None, poll_s: float | None = None) -> bool:
+        """Block until the lease is ours (False if ``stop`` fires first)."""
+        stop = stop or self._stop
+        while not stop.is_set():
+            if self._try():
+                self.leading = True
+                self._last_ok = self._last_try = self.clock.monotonic()
+                return True
+            stop.wait(poll_s if poll_s is not None else self.retry_period)
+        return False
+
+    def tick(self) -> bool:
+        """One renewal step when due; returns whether we still lead."""
+        if not self.leading or self.lost.is_set():
+            return False
+        now = self.clock.monotonic()
+        if self._last_try is not None and now - self._last_try < self.retry_period:
+            return True
+        self._last_try = now
+        if self._try():
+            self._last_ok = now
+            return True
+        if self._last_ok is None or now - self._last_ok >= self.renew_deadline or self._held_by_other():
+            self._lose()
+            return False
+        return True
+
+    def _held_by_other(self) -> bool:
+        try:
+            lease = self.elector.api.try_get("Lease", self.elector.name, self.elector.ns)
+        except Exception:
+            return False
+        holder = (lease or {}).get("spec", {}).get("holderIdentity")
+        return bool(holder) and holder != self.elector.identity
+
+    def _lose(self) -> None:
+        self.leading = False
+        if not self.lost.is_set():
+            self.lost.set()
+            log.error("leader election lost: lease %s/%s (identity %s)", self.elector.ns, self.elector.name,
+                      self.elector.identity)
+            if self.on_lost:
+                self.on_lost()
+
+    def start(self) -> None:
+        def loop():
+            while not self._stop.wait(self.retry_period / 2):
+                if not self.tick():
+                    return
+
+        self._thread = threading.Thread(target=loop, daemon=True, name=f"lease-{self.elector.name}")
+        self._thread.start()
+
+    def stop(self, release: bool = True) -> None:
+        self._stop.set()
+        if self._thread and self._thread is not threading.current_thread():
+            self._thread.join(timeout=2)
+        if release and self.leading:
+            self.leading = False
+            try:
+                self.elector.release()
+            except Exception:
+                pass
+
+
 class Manager:
     def __init__(self, api: ApiServer, name: str = "manager", clock=None, leader_election: bool = False,
                  leader_election_id: str | None = None, leader_election_namespace: str = "nos-system",
@@ -199,7 +296,12 @@ class Manager:
         self.elector = (LeaderElector(api, leader_election_id or f"{name}-leader", leader_election_namespace,
                                       identity or f"{name}-{id(self):x}", clock=self.clock)
                         if leader_election else None)
+        self.lease = LeaseKeeper(self.elector, on_lost=self._on_lease_lost) if self.elector else None
         self.is_leader = not leader_election
+        # set when the lease was lost: the workers have stopped and the binary must
+        # exit non-zero (cmd/common.py), like controller-runtime -- never re-acquire
+        self.lost_leadership = threading.Event()
+        self.health_checks["leader"] = lambda: not self.lost_leadership.is_set()
 
     def add(self, controller: Controller) -> Controller:
         controller.queue = WorkQueue(self.clock)
@@ -220,10 +322,25 @@ class Manager:
 
     # ------------------------------------------------------------ lifecycle
     def _elect(self) -> bool:
+        """Acquire (not yet leading) or renew when due (leading).  A manager that
+        lost its lease stays stopped."""
         if self.elector is None:
             return True
-        self.is_leader = self.elector.try_acquire_or_renew()
+        if self.lost_leadership.is_set():
+            return False
+        if not self.lease.leading:
+            if self.lease._try():
+                self.lease.leading = True
+                self.lease._last_ok = self.lease._last_try = self.clock.monotonic()
+        else:
+            self.lease.tick()
+        self.is_leader = self.lease.leading
         return self.is_leader
+
+    def _on_lease_lost(self) -> None:
+        self.is_leader = False
+        self.lost_leadership.set()
+        self._stop.set()  # workers, resync and renew loops end; watches are closed by stop()
 
     def setup(self) -> None:
         """Bind watches (initial lists enqueue every existing object)."""
@@ -237,13 +354,13 @@ class Manager:
                 r.start(self)
 
     def start(self) -> None:
-        """Threaded mode."""
+        """Threaded mode.  With leader election this blocks until the lease is
+        acquired; losing it later stops every worker (``lost_leadership``)."""
         if self.elector is not None:
-            while not self._stop.is_set() and not self._elect():
-                self._stop.wait(1.0)
-            t = threading.Thread(target=self._renew_loop, daemon=True, name=f"{self.name}-lease")
-            t.start()
-            self._threads.append(t)
+            if not self.lease.acquire(self._stop, poll_s=1.0):
+                return
+            self.is_leader = True
+            self.lease.start()
         self.setup()
         for c in self.controllers:
             for i in range(c.max_concurrent):
@@ -255,11 +372,6 @@ class Manager:
             t.start()
             self._threads.append(t)
 
-    def _renew_loop(self) -> None:
-        while not self._stop.wait(max(0.5, self.elector.duration / 3)):
-            if not self._elect():
-                log.error("%s lost leadership", self.name)
-
     def _resync_loop(self) -> None:
         while not self._stop.wait(self.resync_s):
             if self.is_leader:
@@ -270,6 +382,8 @@ class Manager:
             item = c.queue.get(timeout=0.1)
             if item is None:
                 continue
+            if not self.is_leader:  # lease lost between get() and here: leave the item unprocessed
+                return
             c.process_one(item)
 
     def stop(self) -> None:
@@ -282,9 +396,10 @@ class Manager:
             if hasattr(r, "stop"):
                 r.stop()
         for t in self._threads:
-            t.join(timeout=2)
-        if self.elector is not None:
-            self.elector.release()
+            if t is not threading.current_thread():
+                t.join(timeout=2)
+        if self.lease is not None:
+            self.lease.stop(release=not self.lost_leadership.is_set())
 
     # ------------------------------------------------------------ deterministic mode
     def resync(self) -> int:
@@ -316,7 +431,7 @@ class Manager:
         """Process every item ready now once; returns the number processed."""
         if not self.started:
             self.setup()
-        if not self.is_leader and not self._elect():
+        if not self._elect():
             return 0
         self._maybe_resync()
         n = 0

@@ -21,6 +21,7 @@ import heapq
 import itertools
 import logging
 import threading
+import time
 from typing import Any
 
 from ..kube import objects as ko
@@ -254,9 +255,25 @@ class Scheduler:
         return self.frameworks.get((pod.get("spec") or {}).get("schedulerName", "default-scheduler"))
 
     def schedule_one(self) -> bool:
+        """One scheduling cycle.  An exception inside the cycle (API error,
+        plugin bug) never loses the pod: it goes back to the queue with
+        backoff and the loop carries on."""
         pod = self.queue.pop()
         if pod is None:
             return False
+        try:
+            return self._schedule_pod(pod)
+        except Exception:
+            log.exception("scheduling cycle of %s failed; requeued with backoff", ko.key(pod))
+            self.stats["cycle_errors"] = self.stats.get("cycle_errors", 0) + 1
+            try:
+                self.cache.forget(pod)
+            except Exception:
+                pass
+            self.queue.add_unschedulable(pod)
+            return True
+
+    def _schedule_pod(self, pod: dict) -> bool:
         fw = self._framework_for(pod)
         if fw is None:
             return True
@@ -378,15 +395,29 @@ class Scheduler:
 
         def loop():
             while not self._stop.is_set():
-                if not self.schedule_one():
+                self.heartbeat = time.monotonic()
+                try:
+                    if self.schedule_one():
+                        continue
                     self._stop.wait(0.02)
                     if self.clock.monotonic() - self._last_flush >= self.flush_interval:
                         self._last_flush = self.clock.monotonic()
                         self.resync()
                         self.queue.move_all_to_active()
+                except Exception:  # resync against an unreachable API server etc.: back off, keep going
+                    log.exception("scheduler loop error")
+                    self.stats["loop_errors"] = self.stats.get("loop_errors", 0) + 1
+                    self._stop.wait(1.0)
 
+        self.heartbeat = time.monotonic()
         self._thread = threading.Thread(target=loop, daemon=True, name="scheduler")
         self._thread.start()
+
+    def healthy(self, max_stall_s: float = 30.0) -> bool:
+        """Liveness: the scheduling thread runs and completed a loop recently."""
+        t = self._thread
+        return bool(t and t.is_alive() and not self._stop.is_set()
+                    and time.monotonic() - getattr(self, "heartbeat", 0.0) < max_stall_s)
 
     def stop(self) -> None:
         self._stop.set()

@@ -151,6 +151,22 @@ def test_yolos_fp32_native_attention_matches_torch():
     assert (boxes - rb).abs().max().item() < 1e-4
 
 
+def test_layernorm_strided_x_and_residual():
+    """x and residual are row-strided views of wider buffers: the
+    kernel reads each with its own stride and writes a dense sum."""
+    rows, D = 300, 384
+    xb = torch.randn(rows, D + 64, device=DEV, dtype=torch.bfloat16)
+    rb = torch.randn(rows, D + 128, device=DEV, dtype=torch.bfloat16)
+    x, r = xb[:, :D], rb[:, 64:64 + D]
+    g = torch.randn(D, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(D, device=DEV, dtype=torch.bfloat16)
+    y, s = ops.layernorm(x, g, b, 1e-12, residual=r)
+    ry, rs = ops.layernorm_ref(x.cpu(), g.cpu(), b.cpu(), 1e-12, residual=r.cpu())
+    assert s.is_contiguous() and _rel(s, rs) < 1e-2 and _rel(y, ry) < 2e-2
+    with pytest.raises(ValueError):
+        ops.layernorm(x, g.float(), b, 1e-12)
+
+
 def test_layernorm_with_residual_sum():
     x = torch.randn(3401, 384, device=DEV, dtype=torch.bfloat16)
     r = torch.randn(3401, 384, device=DEV, dtype=torch.bfloat16)
