@@ -97,6 +97,10 @@ class GpuPartitionerConfig(ControllerManagerSpec):
     slice_placement: str = Field("pack", alias="slicePlacement")
     # new: CU-mask layout of a GPU's slices in the device plugin ("even" | "proportional" | "shared")
     cu_policy: str = Field("proportional", alias="cuPolicy")
+    # amdpart anti-starvation: whole (SPX) GPUs per node never split for fractional pods
+    reserve_whole_gpus: int = Field(0, alias="reserveWholeGpus")
+    # NPS mode the planner asks for when a geometry exists in several memory modes
+    preferred_memory_mode: str = Field("NPS1", alias="preferredMemoryMode")
 
     @model_validator(mode="before")
     @classmethod

@@ -118,7 +118,7 @@ class ElasticQuotaReconciler:
 
     def find_for_pod(self, pod: dict) -> list[Request]:
         eqs = self.api.list(v1alpha1.KIND_EQ, ko.namespace(pod))
-        return [Request(ko.name(eqs[0]), ko.namespace(eqs[0]))] if eqs else []
+        return [Request(ko.name(e), ko.namespace(e)) for e in eqs]
 
     def controller(self, name: str = C.ELASTIC_QUOTA_CONTROLLER) -> Controller:
         return (Controller(name, self).for_kind(v1alpha1.KIND_EQ)

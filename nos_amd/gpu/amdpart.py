@@ -304,10 +304,20 @@ class PartitionGPU:
 class PartitionNode:
     """``mig.Node`` analogue; implements core.PartitionableNode."""
 
-    def __init__(self, name: str, gpus: list[PartitionGPU], node_info):
+    def __init__(self, name: str, gpus: list[PartitionGPU], node_info, reserve_whole_gpus: int = 0):
         self.name = name
         self.gpus = gpus
         self.node_info = node_info
+        # anti-starvation packing policy (SURVEY.md 7.4.1): a mode switch is GPU-wide
+        # and needs an idle GPU, so fractional requests are steered onto GPUs that are
+        # already partitioned, and the last ``reserve_whole_gpus`` whole (SPX) GPUs of
+        # the node are never split for them -- whole-GPU pods cannot starve behind
+        # a stream of small ones
+        self.reserve_whole_gpus = reserve_whole_gpus
+
+    def set_memory_mode_preference(self, nps: str) -> None:
+        for g in self.gpus:
+            g.memory_mode_preference = nps
 
     @classmethod
     def from_node_info(cls, ni) -> "PartitionNode":
@@ -357,18 +367,48 @@ class PartitionNode:
                 return True
         return False
 
+    def _is_whole(self, g: PartitionGPU) -> bool:
+        geo = g.geometry()
+        return len(geo) == 1 and next(iter(geo.values())) == 1
+
+    def _order(self) -> list[PartitionGPU]:
+        """Free partitions first (no switch), then GPUs already split (a switch
+        between split modes), whole GPUs last."""
+        def key(g):
+            has_free = any(n > 0 for n in g.free.values())
+            return (0 if has_free else 1, 1 if self._is_whole(g) else 0, g.index)
+        return sorted(self.gpus, key=key)
+
     def update_geometry_for(self, slices: dict) -> bool:
         if not self.gpus or not slices:
             return False
         required = dict(slices)
-        updated = False
+        # already-free partitions count first: no GPU is switched for demand they cover
         for g in self.gpus:
-            updated = g.update_geometry_for(required) or updated
             for p, n in g.free.items():
-                if p in required:
+                if p in required and n > 0:
                     required[p] -= n
                     if required[p] <= 0:
                         del required[p]
+        updated = False
+        whole_idle = sum(1 for g in self.gpus if self._is_whole(g) and not any(g.used.values()))
+        for g in self._order():
+            if not required:
+                break
+            whole = self._is_whole(g)
+            if whole and not any(g.used.values()) and whole_idle <= self.reserve_whole_gpus:
+                continue  # keep the reserve of whole GPUs
+            before = dict(g.free)
+            if g.update_geometry_for(required):
+                updated = True
+                if whole and not self._is_whole(g):
+                    whole_idle -= 1
+                for p, n in g.free.items():
+                    gained = n - before.get(p, 0)
+                    if p in required and gained > 0:
+                        required[p] -= gained
+                        if required[p] <= 0:
+                            del required[p]
         self._recompute_allocatable()
         return updated
 
@@ -389,7 +429,8 @@ class PartitionNode:
         raise GenericError("not enough free partitions")
 
     def clone(self) -> "PartitionNode":
-        return PartitionNode(self.name, [g.clone() for g in self.gpus], self.node_info.clone())
+        return PartitionNode(self.name, [g.clone() for g in self.gpus], self.node_info.clone(),
+                             self.reserve_whole_gpus)
 
 
 class PartitionSliceCalculator:

@@ -82,8 +82,10 @@ class AmdPartPartitioner:
 
 
 class AmdPartSnapshotTaker:
-    def __init__(self, partition_calculator=None):
+    def __init__(self, partition_calculator=None, reserve_whole_gpus: int = 0, memory_mode: str = "NPS1"):
         self.pc = partition_calculator or AmdPartPartitionCalculator()
+        self.reserve_whole_gpus = reserve_whole_gpus
+        self.memory_mode = memory_mode
 
     def take_snapshot(self, cs: ClusterState) -> ClusterSnapshot:
         nodes = {}
@@ -92,7 +94,10 @@ class AmdPartSnapshotTaker:
             if n is None or not is_amdpart_enabled(n):
                 continue
             try:
-                nodes[name] = ap.PartitionNode.from_node_info(ni.clone())
+                pn = ap.PartitionNode.from_node_info(ni.clone())
+                pn.reserve_whole_gpus = self.reserve_whole_gpus
+                pn.set_memory_mode_preference(self.memory_mode)
+                nodes[name] = pn
             except Exception as e:  # node not yet labelled by its agent
                 log.debug("skipping node %s: %s", name, e)
         return ClusterSnapshot(nodes, self.pc, ap.PartitionSliceCalculator(), ap.PartitionSliceFilter())
@@ -230,10 +235,11 @@ class Strategy:
     initializer: object | None = None
 
 
-def amdpart_strategy(api, clock=None) -> Strategy:
+def amdpart_strategy(api, clock=None, reserve_whole_gpus: int = 0, memory_mode: str = "NPS1") -> Strategy:
     pc = AmdPartPartitionCalculator()
     part = AmdPartPartitioner(api)
-    return Strategy(C.PARTITIONING_AMDPART, AmdPartSnapshotTaker(pc), pc, part, ap.PartitionSliceCalculator(),
+    return Strategy(C.PARTITIONING_AMDPART, AmdPartSnapshotTaker(pc, reserve_whole_gpus, memory_mode), pc, part,
+                    ap.PartitionSliceCalculator(),
                     ap.PartitionSliceFilter(), AmdPartNodeInitializer(api, part, pc, clock))
 
 

@@ -80,7 +80,7 @@ class SimCluster:
         self.partitioner = Manager(self.api, "nos-gpupartitioner", self.clock, resync_s=resync_s)
         sched_cfg = scheduler_config or nos_scheduler_config(memory_gb)
         fw = build_framework(sched_cfg.profiles[0], api=self.api)
-        amd = amdpart_strategy(self.api, self.clock)
+        amd = amdpart_strategy(self.api, self.clock, self.cfg.reserve_whole_gpus, self.cfg.preferred_memory_mode)
         cum = cumask_strategy(self.api, self.cm_ref, self.cfg.device_plugin_delay_seconds, self.clock,
                               self.cfg.cu_policy, self.cfg.slice_placement)
         self.partitioner.add(NodeController(self.api, self.cluster_state, amd.initializer).controller())

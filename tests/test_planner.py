@@ -191,3 +191,85 @@ def test_planner_scales_linearly_enough():
     r = pb.run_one(C.PARTITIONING_CUMASK, 100, 500)
     assert r["placed"] == 500
     assert time.perf_counter() - t0 < 20.0
+
+
+# ------------------------------------------- amdpart scenarios (planner_test.go:43-508 analogue)
+def _modes(plan, node):
+    return [g.mode for g in sorted(plan.desired_state[node].gpus, key=lambda g: g.gpu_index)]
+
+
+ONE = "amd.com/partition-1xcd.36gb"
+HALF = "amd.com/partition-4xcd.144gb"
+WHOLE = "amd.com/partition-8xcd.288gb"
+
+
+def test_amdpart_mixed_busy_idle_gpus_over_nodes():
+    """n1: GPU0 busy (SPX used), GPU1 idle SPX; n2: CPX GPU with 3 free 1xcd.
+    Five 1xcd pods: the free partitions of n2 are used first and only n1's IDLE
+    GPU is switched; the busy GPU is never touched."""
+    n1 = _node("n1", "partition", count=2, ann={"nos.nebuly.com/status-gpu-0-8xcd.288gb-used": "1",
+                                                "nos.nebuly.com/status-gpu-1-8xcd.288gb-free": "1"})
+    n2 = _node("n2", "partition", count=1, ann={"nos.nebuly.com/status-gpu-0-1xcd.36gb-used": "5",
+                                                "nos.nebuly.com/status-gpu-0-1xcd.36gb-free": "3"})
+    snap = _amd_snapshot([n1, n2])
+    plan = _amd_planner().plan(snap, [_pod(f"s{i}", ONE) for i in range(5)])
+    assert _res(plan, "n2") == [{ONE: 8}]
+    r1 = _res(plan, "n1")
+    assert r1[0] == {WHOLE: 1}
+    assert r1[1] == {ONE: 8}
+
+
+def test_amdpart_used_partitions_block_a_mode_switch():
+    n1 = _node("n1", "partition", count=2, ann={"nos.nebuly.com/status-gpu-0-1xcd.36gb-used": "2",
+                                                "nos.nebuly.com/status-gpu-0-1xcd.36gb-free": "6",
+                                                "nos.nebuly.com/status-gpu-1-8xcd.288gb-free": "1"})
+    plan = _amd_planner().plan(_amd_snapshot([n1]), [_pod("h", HALF)])
+    assert _res(plan, "n1") == [{ONE: 8}, {HALF: 2}]
+    assert _modes(plan, "n1")[1] == "DPX/NPS1"
+
+
+def test_amdpart_steers_to_already_split_gpu_before_whole_gpu():
+    """GPU0 idle SPX, GPU1 idle DPX: 1xcd demand re-splits GPU1 (already
+    fractional) and keeps GPU0 whole."""
+    n1 = _node("n1", "partition", count=2, ann={"nos.nebuly.com/status-gpu-0-8xcd.288gb-free": "1",
+                                                "nos.nebuly.com/status-gpu-1-4xcd.144gb-free": "2"})
+    plan = _amd_planner().plan(_amd_snapshot([n1]), [_pod(f"s{i}", ONE) for i in range(4)])
+    assert _res(plan, "n1") == [{WHOLE: 1}, {ONE: 8}]
+
+
+def test_amdpart_reserve_keeps_whole_gpus_for_whole_gpu_pods():
+    n1 = _node("n1", "partition", count=2, ann={"nos.nebuly.com/status-gpu-0-8xcd.288gb-free": "1",
+                                                "nos.nebuly.com/status-gpu-1-8xcd.288gb-free": "1"})
+    pods = [_pod(f"s{i}", ONE) for i in range(12)]
+    snap = _amd_snapshot([n1])
+    for n in snap.get_nodes().values():
+        n.reserve_whole_gpus = 1
+    plan = _amd_planner().plan(snap, pods)
+    assert sorted(map(str, _res(plan, "n1"))) == sorted(map(str, [{WHOLE: 1}, {ONE: 8}]))
+    # without the reserve both GPUs are split for the 12 small pods
+    plan = _amd_planner().plan(_amd_snapshot([n1]), pods)
+    assert _res(plan, "n1") == [{ONE: 8}, {ONE: 8}]
+
+
+def test_amdpart_memory_mode_preference():
+    n1 = _node("n1", "partition", count=1, ann={"nos.nebuly.com/status-gpu-0-8xcd.288gb-free": "1"})
+    for nps, want in (("NPS1", "CPX/NPS1"), ("NPS2", "CPX/NPS2")):
+        snap = _amd_snapshot([n1])
+        for n in snap.get_nodes().values():
+            n.set_memory_mode_preference(nps)
+        plan = _amd_planner().plan(snap, [_pod("s", ONE)])
+        assert _modes(plan, "n1") == [want]
+
+
+def test_amdpart_unsatisfiable_request_changes_nothing():
+    n1 = _node("n1", "partition", count=1, ann={"nos.nebuly.com/status-gpu-0-8xcd.288gb-used": "1"})
+    plan = _amd_planner().plan(_amd_snapshot([n1]), [_pod("s", ONE)])
+    assert _res(plan, "n1") == [{WHOLE: 1}]
+
+
+def test_amdpart_geometry_from_labels_in_planner():
+    """A node whose GPUs report 256 GB plans 1xcd.32gb partitions."""
+    n = _node("n1", "partition", count=1, ann={"nos.nebuly.com/status-gpu-0-8xcd.256gb-free": "1"})
+    n["metadata"]["labels"]["amd.com/gpu.memory"] = "262144"
+    plan = _amd_planner().plan(_amd_snapshot([n]), [_pod("s", "amd.com/partition-1xcd.32gb")])
+    assert _res(plan, "n1") == [{"amd.com/partition-1xcd.32gb": 8}]
