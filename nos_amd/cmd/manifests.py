@@ -46,6 +46,13 @@ DEFAULT_VALUES: dict = {
     "image": {"repository": "ghcr.io/nos-amd/nos-amd", "tag": "0.1.0"},
     "rocmImage": {"repository": "ghcr.io/nos-amd/nos-amd-rocm", "tag": "0.1.0"},
     "operator": {"enabled": True, "webhook": {"enabled": True}},
+    # webhook serving certificate: cert-manager Issuer + Certificate (config/operator/certificate.yaml);
+    # disabled -> provide the TLS secret "nos-amd-webhook-server-cert" yourself
+    "certManager": {"enabled": True},
+    # /metrics behind a kube-rbac-proxy sidecar (https :8443) + a Service per component,
+    # and Prometheus-operator ServiceMonitors for them
+    "metrics": {"authProxy": True, "serviceMonitor": True,
+                "authProxyImage": {"repository": "quay.io/brancz/kube-rbac-proxy", "tag": "v0.18.0"}},
     "scheduler": {"enabled": True, "schedulerName": "nos-scheduler"},
     "gpuPartitioner": {
         "enabled": True,
@@ -55,7 +62,9 @@ DEFAULT_VALUES: dict = {
         "planReportTimeoutSeconds": 300,
         "slicePlacement": "pack",
         "cuPolicy": "proportional",
-        "knownPartitionGeometries": None,  # list override of the built-in MI355X table
+        "reserveWholeGpus": 0,
+        "preferredMemoryMode": "NPS1",
+        "knownPartitionGeometries": None,  # list override; default: derived from each node's amd-smi memory/XCDs
         "partitionAgent": {"enabled": True, "reportConfigIntervalSeconds": 10, "allowModeChanges": True,
                            "defaultComputeMode": "SPX", "defaultMemoryMode": "NPS1"},
         "gpuAgent": {"enabled": True, "reportConfigIntervalSeconds": 10, "probeEnabled": True},
@@ -111,6 +120,8 @@ def validate_values(v: dict) -> None:
         raise ValueError("gpuPartitioner.cuPolicy must be even|proportional|shared")
     if int(v["amdGpuResourceMemoryGB"]) <= 0:
         raise ValueError("amdGpuResourceMemoryGB must be > 0")
+    if v["metrics"]["serviceMonitor"] and not v["metrics"]["authProxy"]:
+        raise ValueError("metrics.serviceMonitor scrapes the auth proxy: enable metrics.authProxy")
 
 
 class _Dumper(yaml.SafeDumper):
@@ -219,6 +230,73 @@ def _cfg_mount(name: str) -> tuple[dict, dict]:
     return ({"name": "config", "configMap": {"name": name}}, {"name": "config", "mountPath": "/etc/nos-amd"})
 
 
+WEBHOOK_SECRET = "nos-amd-webhook-server-cert"
+SERVING_CERT = "nos-amd-serving-cert"
+WEBHOOK_SERVICE = "nos-amd-webhook-service"
+METRICS_READER = "nos-amd-metrics-reader"
+
+
+def _with_metrics(name: str, workload: dict, upstream_port: int = 8080) -> list[dict]:
+    """Expose a component's /metrics (bound to 127.0.0.1:<upstream_port>)
+    through a kube-rbac-proxy sidecar on https :8443 (authn/z by token review,
+    the reference's operator_auth_proxy_patch.yaml), a Service, and a
+    ServiceMonitor (config/*/prometheus/monitor.yaml).  Returns the extra objects."""
+    m = _V["metrics"]
+    if not m["authProxy"]:
+        return []
+    img = m["authProxyImage"]
+    proxy = {"name": "kube-rbac-proxy", "image": f"{img['repository']}:{img['tag']}",
+             "args": ["--secure-listen-address=0.0.0.0:8443", f"--upstream=http://127.0.0.1:{upstream_port}/",
+                      "--logtostderr=true", "--v=0"],
+             "ports": [{"containerPort": 8443, "name": "https", "protocol": "TCP"}],
+             "resources": {"requests": {"cpu": "5m", "memory": "64Mi"}, "limits": {"memory": "128Mi"}},
+             "securityContext": {"allowPrivilegeEscalation": False, "capabilities": {"drop": ["ALL"]}}}
+    workload["spec"]["template"]["spec"]["containers"].append(proxy)
+    labels = dict(workload["spec"]["selector"]["matchLabels"])
+    svc = {"apiVersion": "v1", "kind": "Service",
+           "metadata": {"name": f"{name}-metrics", "namespace": _ns(), "labels": {"app": name, "metrics": "nos-amd"}},
+           "spec": {"selector": {"app": labels["app"]},
+                    "ports": [{"name": "https", "port": 8443, "targetPort": "https", "protocol": "TCP"}]}}
+    out = [svc]
+    if m["serviceMonitor"]:
+        out.append({"apiVersion": "monitoring.coreos.com/v1", "kind": "ServiceMonitor",
+                    "metadata": {"name": f"{name}-metrics-monitor", "namespace": _ns(), "labels": {"app": name}},
+                    "spec": {"selector": {"matchLabels": {"app": name, "metrics": "nos-amd"}},
+                             "endpoints": [{"path": "/metrics", "port": "https", "scheme": "https",
+                                            "bearerTokenFile": "/var/run/secrets/kubernetes.io/serviceaccount/token",
+                                            "tlsConfig": {"insecureSkipVerify": True}}]}})
+    return out
+
+
+def _auth_proxy_rules() -> list[dict]:
+    """What the kube-rbac-proxy sidecar needs to authenticate/authorise scrapers."""
+    return [_rule(["authentication.k8s.io"], ["tokenreviews"], ["create"]),
+            _rule(["authorization.k8s.io"], ["subjectaccessreviews"], ["create"])]
+
+
+def monitoring() -> dict[str, list[dict]]:
+    """ClusterRole a Prometheus service account is bound to for scraping."""
+    if not _V["metrics"]["authProxy"]:
+        return {}
+    return {"monitoring/metrics-reader.yaml": [
+        {"apiVersion": "rbac.authorization.k8s.io/v1", "kind": "ClusterRole", "metadata": {"name": METRICS_READER},
+         "rules": [{"nonResourceURLs": ["/metrics"], "verbs": ["get"]}]}]}
+
+
+def certificates() -> list[dict]:
+    """cert-manager self-signed Issuer + the webhook serving Certificate whose
+    secret the operator Deployment mounts and whose CA cert-manager injects into
+    the ValidatingWebhookConfiguration (config/operator/certmanager/certificate.yaml)."""
+    svc = f"{WEBHOOK_SERVICE}.{_ns()}.svc"
+    return [{"apiVersion": "cert-manager.io/v1", "kind": "Issuer",
+             "metadata": {"name": "nos-amd-selfsigned-issuer", "namespace": _ns()}, "spec": {"selfSigned": {}}},
+            {"apiVersion": "cert-manager.io/v1", "kind": "Certificate",
+             "metadata": {"name": SERVING_CERT, "namespace": _ns()},
+             "spec": {"dnsNames": [svc, svc + ".cluster.local"], "secretName": WEBHOOK_SECRET,
+                      "issuerRef": {"kind": "Issuer", "name": "nos-amd-selfsigned-issuer"},
+                      "privateKey": {"rotationPolicy": "Always"}}}]
+
+
 # ------------------------------------------------------------------ components
 def crds() -> dict[str, list[dict]]:
     samples = [v1alpha1.build_eq("team-a", "quota-a").with_min({"cpu": "2", "memory": "8Gi",
@@ -236,7 +314,7 @@ def crds() -> dict[str, list[dict]]:
 def operator() -> dict[str, list[dict]]:
     name = "nos-amd-operator"
     vol, mnt = _cfg_mount(name + "-config")
-    certs = {"name": "cert", "secret": {"secretName": "nos-amd-webhook-server-cert"}}
+    certs = {"name": "cert", "secret": {"secretName": WEBHOOK_SECRET}}
     c = _container("manager", "nos_amd.cmd.operator",
                    ["--config", "/etc/nos-amd/operator_config.yaml"] +
                    (["--webhook-port", "9443", "--webhook-cert-dir", "/tmp/k8s-webhook-server/serving-certs"]
@@ -248,14 +326,14 @@ def operator() -> dict[str, list[dict]]:
            "health": {"healthProbeBindAddress": ":8081"}, "metrics": {"bindAddress": "127.0.0.1:8080"},
            "leaderElection": {"leaderElect": _V["leaderElection"], "resourceName": "nos-amd-operator"},
            "amdGpuResourceMemoryGB": _V["amdGpuResourceMemoryGB"]}
-    svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "nos-amd-webhook-service", "namespace": _ns()},
+    svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": WEBHOOK_SERVICE, "namespace": _ns()},
            "spec": {"selector": {"app": name}, "ports": [{"port": 443, "targetPort": 9443}]}}
 
     def hook(kind: str, path: str, ops: list[str]) -> dict:
         plural = kind.lower() + "s"
         return {"name": f"v{kind.lower()}.kb.io", "admissionReviewVersions": ["v1"], "sideEffects": "None",
                 "failurePolicy": "Fail",
-                "clientConfig": {"service": {"name": "nos-amd-webhook-service", "namespace": _ns(), "path": path}},
+                "clientConfig": {"service": {"name": WEBHOOK_SERVICE, "namespace": _ns(), "path": path}},
                 "rules": [{"apiGroups": [C.GROUP], "apiVersions": [C.VERSION], "operations": ops,
                            "resources": [plural]}]}
 
@@ -263,19 +341,22 @@ def operator() -> dict[str, list[dict]]:
 
     vwc = {"apiVersion": "admissionregistration.k8s.io/v1", "kind": "ValidatingWebhookConfiguration",
            "metadata": {"name": "nos-amd-validating-webhook-configuration",
-                        "annotations": {"cert-manager.io/inject-ca-from": f"{_ns()}/nos-amd-serving-cert"}},
+                        "annotations": {"cert-manager.io/inject-ca-from": f"{_ns()}/{SERVING_CERT}"}},
            "webhooks": [hook("ElasticQuota", EQ_PATH, ["CREATE", "UPDATE"]),
                         hook("CompositeElasticQuota", CEQ_PATH, ["CREATE", "UPDATE"])]}
     rules = [_rule([C.GROUP], ["elasticquotas", "compositeelasticquotas"], RW),
              _rule([C.GROUP], ["elasticquotas/status", "compositeelasticquotas/status"], ["get", "update", "patch"]),
-             _rule([""], ["pods"], ["get", "list", "watch", "patch", "update"]), LEASES, EVENTS]
+             _rule([""], ["pods"], ["get", "list", "watch", "patch", "update"]), LEASES, EVENTS] + _auth_proxy_rules()
+    dep = _deployment(name, c, [vol, certs])
     out = {"operator/manager.yaml": [_sa(name), _config_map(name + "-config",
-                                                            {"operator_config.yaml": yaml.safe_dump(cfg)}),
-                                     _deployment(name, c, [vol, certs])],
+                                                            {"operator_config.yaml": yaml.safe_dump(cfg)}), dep],
            "operator/rbac.yaml": _cluster_role(name, rules)}
+    out["operator/metrics.yaml"] = _with_metrics(name, dep)
     if _V["operator"]["webhook"]["enabled"]:
         out["operator/webhook.yaml"] = [svc, vwc]
-    return out
+        if _V["certManager"]["enabled"]:
+            out["operator/certificate.yaml"] = certificates()
+    return {k: v for k, v in out.items() if v}
 
 
 def scheduler() -> dict[str, list[dict]]:
@@ -321,7 +402,9 @@ def gpupartitioner() -> dict[str, list[dict]]:
            "health": {"healthProbeBindAddress": ":8081"}, "metrics": {"bindAddress": "127.0.0.1:8080"},
            "leaderElection": {"leaderElect": _V["leaderElection"], "resourceName": "nos-amd-gpupartitioner"},
            "schedulerConfigFile": "/etc/nos-amd/scheduler_config.yaml",
-           "knownPartitionGeometriesFile": "/etc/nos-amd/known_partition_geometries.yaml",
+           "knownPartitionGeometriesFile": ("/etc/nos-amd/known_partition_geometries.yaml"
+                                            if gp.get("knownPartitionGeometries") else ""),
+           "reserveWholeGpus": gp["reserveWholeGpus"], "preferredMemoryMode": gp["preferredMemoryMode"],
            "batchWindowTimeoutSeconds": gp["batchWindowTimeoutSeconds"],
            "batchWindowIdleSeconds": gp["batchWindowIdleSeconds"],
            "devicePluginConfigMap": {"name": C.DEFAULT_DEVICE_PLUGIN_CM_NAME, "namespace": _ns()},
@@ -334,15 +417,17 @@ def gpupartitioner() -> dict[str, list[dict]]:
                    mounts=[mnt])
     rules = [_rule([""], ["pods"], RO), _rule([""], ["nodes"], RO + ["patch", "update"]),
              _rule([""], ["configmaps"], RW), _rule([C.GROUP], ["elasticquotas", "compositeelasticquotas"], RO),
-             _rule(["policy"], ["poddisruptionbudgets"], RO), LEASES, EVENTS]
+             _rule(["policy"], ["poddisruptionbudgets"], RO), LEASES, EVENTS] + _auth_proxy_rules()
     cm = {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": C.DEFAULT_DEVICE_PLUGIN_CM_NAME,
                                                                   "namespace": _ns()}, "data": {}}
-    return {"gpupartitioner/manager.yaml": [
-        _sa(name), _config_map(name + "-config", {"gpu_partitioner_config.yaml": yaml.safe_dump(cfg),
-                                                  "scheduler_config.yaml": sched,
-                                                  "known_partition_geometries.yaml": known_geometries_yaml()}),
-        cm, _deployment(name, c, [vol])],
-        "gpupartitioner/rbac.yaml": _cluster_role(name, rules)}
+    dep = _deployment(name, c, [vol])
+    files = {"gpu_partitioner_config.yaml": yaml.safe_dump(cfg), "scheduler_config.yaml": sched}
+    if gp.get("knownPartitionGeometries"):  # else geometries follow each node's amd-smi memory/XCDs
+        files["known_partition_geometries.yaml"] = known_geometries_yaml()
+    out = {"gpupartitioner/manager.yaml": [_sa(name), _config_map(name + "-config", files), cm, dep],
+           "gpupartitioner/rbac.yaml": _cluster_role(name, rules),
+           "gpupartitioner/metrics.yaml": _with_metrics(name, dep)}
+    return {k: v for k, v in out.items() if v}
 
 
 def node_agents() -> dict[str, list[dict]]:
@@ -355,29 +440,34 @@ def node_agents() -> dict[str, list[dict]]:
     name = "nos-amd-partagent"
     vol, mnt = _cfg_mount(name + "-config")
     cfg = {"apiVersion": C.CONFIG_API_VERSION, "kind": "PartitionAgentConfig",
-           "health": {"healthProbeBindAddress": ":8081"},
+           "health": {"healthProbeBindAddress": ":8081"}, "metrics": {"bindAddress": "127.0.0.1:8080"},
            "reportConfigIntervalSeconds": pa["reportConfigIntervalSeconds"],
            "allowModeChanges": pa["allowModeChanges"], "defaultComputeMode": pa["defaultComputeMode"],
            "defaultMemoryMode": pa["defaultMemoryMode"]}
     c = _container("partagent", "nos_amd.cmd.partagent", ["--config", "/etc/nos-amd/partition_agent_config.yaml"],
                    image=IMAGE_ROCM, env=NODE_ENV, mounts=HOST_MOUNTS + [mnt], privileged=True)
     if pa["enabled"]:
+        ds = _daemonset(name, c, C.PARTITIONING_AMDPART, HOST_VOLUMES + [vol])
         out["partagent/daemonset.yaml"] = [_sa(name), _config_map(name + "-config", {
-            "partition_agent_config.yaml": yaml.safe_dump(cfg)}),
-            _daemonset(name, c, C.PARTITIONING_AMDPART, HOST_VOLUMES + [vol])]
-        out["partagent/rbac.yaml"] = _cluster_role(name, node_rules)
+            "partition_agent_config.yaml": yaml.safe_dump(cfg)}), ds]
+        out["partagent/rbac.yaml"] = _cluster_role(name, node_rules + _auth_proxy_rules())
+        if extra := _with_metrics(name, ds):
+            out["partagent/metrics.yaml"] = extra
     # gpuagent (CU-mask reporter + probes)
     name = "nos-amd-gpuagent"
     vol, mnt = _cfg_mount(name + "-config")
     cfg = {"apiVersion": C.CONFIG_API_VERSION, "kind": "GpuAgentConfig", "health": {"healthProbeBindAddress": ":8081"},
+           "metrics": {"bindAddress": "127.0.0.1:8080"},
            "reportConfigIntervalSeconds": ga["reportConfigIntervalSeconds"], "probeEnabled": ga["probeEnabled"]}
     c = _container("gpuagent", "nos_amd.cmd.gpuagent", ["--config", "/etc/nos-amd/gpu_agent_config.yaml"],
                    image=IMAGE_ROCM, env=NODE_ENV, mounts=HOST_MOUNTS + [mnt], privileged=True)
     if ga["enabled"]:
+        ds = _daemonset(name, c, C.PARTITIONING_CUMASK, HOST_VOLUMES + [vol])
         out["gpuagent/daemonset.yaml"] = [_sa(name), _config_map(name + "-config", {
-            "gpu_agent_config.yaml": yaml.safe_dump(cfg)}),
-            _daemonset(name, c, C.PARTITIONING_CUMASK, HOST_VOLUMES + [vol])]
-        out["gpuagent/rbac.yaml"] = _cluster_role(name, node_rules)
+            "gpu_agent_config.yaml": yaml.safe_dump(cfg)}), ds]
+        out["gpuagent/rbac.yaml"] = _cluster_role(name, node_rules + _auth_proxy_rules())
+        if extra := _with_metrics(name, ds):
+            out["gpuagent/metrics.yaml"] = extra
     # device plugin (one DaemonSet per partitioning kind + plain GPU nodes could reuse it)
     name = "nos-amd-device-plugin"
     vol, mnt = _cfg_mount(name + "-config")
@@ -443,6 +533,7 @@ def render(values: dict | None = None) -> dict[str, str]:
         if v["gpuPartitioner"]["enabled"]:
             parts.append(gpupartitioner())
         parts.append(node_agents())
+        parts.append(monitoring())
         if v["shareTelemetry"]:
             parts.append(telemetry())
         for part in parts:

@@ -44,7 +44,59 @@ def test_embedded_configs_load(tmp_path):
                 c = cfgmod.load(p)
                 kinds.add(c.kind)
     assert {"OperatorConfig", "GpuPartitionerConfig", "PartitionAgentConfig", "GpuAgentConfig",
-            "DevicePluginConfig", "KubeSchedulerConfiguration", "geometries"} <= kinds
+            "DevicePluginConfig", "KubeSchedulerConfiguration"} <= kinds
+    # no fixed geometry table by default: the planner derives geometries from each node's amd-smi memory
+    assert "geometries" not in kinds
+
+
+def test_known_geometries_override_is_rendered(tmp_path):
+    table = [{"models": ["MI355X"], "allowedGeometries": [{"compute": "CPX", "memory": "NPS1",
+                                                          "profiles": {"1xcd.36gb": 8}}]}]
+    out = manifests.render({"gpuPartitioner": {"knownPartitionGeometries": table}})
+    cms = {k: t for o in yaml.safe_load_all(out["gpupartitioner/manager.yaml"]) if o and o["kind"] == "ConfigMap"
+           for k, t in (o.get("data") or {}).items()}
+    p = tmp_path / "g.yaml"
+    p.write_text(cms["known_partition_geometries.yaml"])
+    assert len(amdpart.load_known_geometries(p)["MI355X"]) == 1
+    assert yaml.safe_load(cms["gpu_partitioner_config.yaml"])["knownPartitionGeometriesFile"]
+
+
+def test_every_referenced_secret_certificate_and_service_is_rendered():
+    """Nothing a workload, webhook or monitor points at is left for the user to create."""
+    objs = [o for o in _objs() if "metadata" in o]
+    by_kind: dict = {}
+    for o in objs:
+        by_kind.setdefault(o["kind"], {})[o["metadata"]["name"]] = o
+    certs = by_kind.get("Certificate", {})
+    secrets_made = {c["spec"]["secretName"] for c in certs.values()} | set(by_kind.get("Secret", {}))
+    pods = [w["spec"]["template"] for k in ("Deployment", "DaemonSet") for w in by_kind.get(k, {}).values()]
+    for t in pods:
+        for v in t["spec"].get("volumes", []):
+            if "secret" in v:
+                assert v["secret"]["secretName"] in secrets_made, v
+    for vwc in by_kind.get("ValidatingWebhookConfiguration", {}).values():
+        ns_name = vwc["metadata"]["annotations"]["cert-manager.io/inject-ca-from"]
+        assert ns_name.split("/")[1] in certs
+        for h in vwc["webhooks"]:
+            assert h["clientConfig"]["service"]["name"] in by_kind["Service"]
+    for c in certs.values():
+        assert c["spec"]["issuerRef"]["name"] in by_kind["Issuer"]
+        assert any(d.startswith("nos-amd-webhook-service.") for d in c["spec"]["dnsNames"])
+    # every Service selects some workload's pods; every ServiceMonitor selects a Service with its port
+    for svc in by_kind["Service"].values():
+        sel = svc["spec"]["selector"]
+        assert any(all(t["metadata"]["labels"].get(k) == v for k, v in sel.items()) for t in pods), svc
+    monitors = by_kind.get("ServiceMonitor", {})
+    assert {m.split("-metrics-monitor")[0] for m in monitors} >= {"nos-amd-operator", "nos-amd-gpupartitioner",
+                                                                  "nos-amd-partagent", "nos-amd-gpuagent"}
+    for m in monitors.values():
+        want = m["spec"]["selector"]["matchLabels"]
+        svcs = [s for s in by_kind["Service"].values()
+                if all(s["metadata"].get("labels", {}).get(k) == v for k, v in want.items())]
+        assert svcs and all(any(p["name"] == m["spec"]["endpoints"][0]["port"] for p in s["spec"]["ports"])
+                            for s in svcs)
+    # the auth proxy can review tokens, and Prometheus has a reader role to bind
+    assert "nos-amd-metrics-reader" in by_kind["ClusterRole"]
 
 
 def test_daemonsets_are_privileged_and_node_selected():
