@@ -72,7 +72,12 @@ def parse_args(argv=None):
                     help="window of an extra bf16 (gfx950 kernels) fleet run (0 = skip)")
     ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES per pod (0 = HIP default)")
     ap.add_argument("--collective", choices=["auto", "on", "off"], default="auto",
-                    help="bf16 GEMM + RCCL all-reduce tenant per GPU (auto: on when WORLD_SIZE > 1)")
+                    help="one of each GPU's pods is a DP trainer (bf16 GEMM + RCCL all-reduce over xGMI, in "
+                         "lockstep across ranks); auto: on when WORLD_SIZE > 1")
+    ap.add_argument("--coll-dim", type=int, default=4096)
+    ap.add_argument("--coll-bucket-mb", type=int, default=64)
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: rehearsal of the whole launch path without a GPU (tiny pods, gloo)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -93,17 +98,24 @@ def plan(args, world: int, local: int, slice_gb: int, pods: int, mode: str) -> t
 class Dist:
     """Rank-level barrier/reductions: RCCL when every rank owns a GPU."""
 
-    def __init__(self):
+    def __init__(self, device: str = "cuda"):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.backend = os.environ.get("NOS_AMD_BENCH_BACKEND", "nccl")
+        self.cuda = device == "cuda"
+        self.backend = os.environ.get("NOS_AMD_BENCH_BACKEND", "nccl" if self.cuda else "gloo")
         self.dist = None
+        self.device = self.local
 
     def init_gpu(self) -> None:
         import torch
         import torch.distributed as dist
 
+        if not self.cuda:
+            if self.world > 1:
+                dist.init_process_group("gloo")
+                self.dist = dist
+            return
         dev = self.local if self.backend == "nccl" else self.local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(dev)
         self.device = dev
@@ -117,17 +129,19 @@ class Dist:
     def barrier_sync(self) -> None:
         import torch
 
-        torch.cuda.synchronize()
+        if self.cuda:
+            torch.cuda.synchronize()
         if self.dist:
             self.dist.barrier()
-        torch.cuda.synchronize()
+        if self.cuda:
+            torch.cuda.synchronize()
 
     def reduce(self, vals: list[float], op: str) -> list[float]:
         if not self.dist:
             return list(vals)
         import torch
 
-        dev = "cuda" if self.backend == "nccl" else "cpu"
+        dev = "cuda" if (self.cuda and self.backend == "nccl") else "cpu"
         t = torch.tensor(vals, dtype=torch.float64, device=dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
         return t.tolist()
@@ -178,21 +192,24 @@ class UtilSampler:
             self._t.join(timeout=2)
 
 
-def fleet_window(d: Dist, fleet, warmup: int, steps: int, step_s: float, sampler: UtilSampler | None, coll=None):
-    """Warm-up then timed steps of ``step_s`` wall seconds with every pod running."""
+def fleet_window(d: Dist, fleet, warmup: int, steps: int, step_s: float, sampler: UtilSampler | None,
+                 coll=None, coll_times: list | None = None):
+    """Warm-up then timed steps of ``step_s`` wall seconds with every pod running.
+    With a trainer pod in this rank, the rank runs it (lockstep across ranks)
+    instead of sleeping; its iteration completion times go to ``coll_times``."""
     t_end = time.monotonic() + warmup * step_s
+    if coll:
+        coll.run_until(t_end)
     while time.monotonic() < t_end:
-        if coll:
-            coll.step()
         time.sleep(0.05)
-        fleet.check_alive()
+    fleet.check_alive()
     d.barrier_sync()
     t0 = time.monotonic()
     for k in range(steps):
         deadline = t0 + (k + 1) * step_s
+        if coll:
+            coll.run_until(deadline, coll_times)
         while True:
-            if coll:
-                coll.step()
             now = time.monotonic()
             if now >= deadline:
                 break
@@ -204,25 +221,35 @@ def fleet_window(d: Dist, fleet, warmup: int, steps: int, step_s: float, sampler
     return t0, t1, util
 
 
-def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, step_s, sampler, coll=None):
+def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, step_s, sampler, coll=None,
+              device="cuda"):
     from nos_amd.podbench import PodFleet
 
-    fleet = PodFleet(envs, dtype=dtype, graphs=graphs, extra_env=extra_env, launcher=launcher)
+    fleet = PodFleet(envs, dtype=dtype, graphs=graphs, extra_env=extra_env, launcher=launcher, device=device)
+    coll_times: list[float] = []
     try:
         fleet.start()
         ready_s = fleet.wait_ready(timeout_s=900, progress_cb=lambda n, t: log(d.rank, f"{dtype} pods ready {n}/{t}"))
         d.barrier_sync()
-        t0, t1, (util, n_util) = fleet_window(d, fleet, warmup, steps, step_s, sampler, coll)
+        t0, t1, (util, n_util) = fleet_window(d, fleet, warmup, steps, step_s, sampler, coll, coll_times)
         fleet.stop()
         w = fleet.window(t0, t1)
     finally:
         fleet.close()
-    return w, util, n_util, ready_s
+    tr = None
+    if coll:
+        inside = [t0] + [t for t in coll_times if t0 < t < t1] + [t1]
+        gap = max(b - a for a, b in zip(inside, inside[1:]))
+        n_it = len(inside) - 2
+        tr = {"iterations": n_it, "running": n_it > 0 and gap < 0.25 * (t1 - t0), "max_gap_s": round(gap, 3),
+              "gemm_tflops": round(n_it * coll.flops_per_step() / (t1 - t0) / 1e12, 2),
+              "allreduce_gb_per_s": round(n_it * coll.bucket_bytes() / (t1 - t0) / 1e9, 2)}
+    return w, util, n_util, ready_s, tr
 
 
 def main(argv=None) -> int:
     args = parse_args(argv)
-    d = Dist()
+    d = Dist(args.device)
     world, rank, local = d.world, d.rank, d.local
     if world != args.gpus:
         log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}")
@@ -234,41 +261,58 @@ def main(argv=None) -> int:
 
         cp10 = schedulable_pods(world, 10)
     extra_env = {"GPU_MAX_HW_QUEUES": str(args.hw_queues)} if args.hw_queues else {}
+    if args.device == "cpu":
+        extra_env["OMP_NUM_THREADS"] = "1"
     log(rank, f"control plane placed {cp.get('placed_pods')} pods; local envs {envs[:2]}...")
 
     from nos_amd.podbench import PodLauncher
 
     launcher = PodLauncher()  # started before this rank touches the GPU: pods never fork from a GPU process
     d.init_gpu()
-    sampler = UtilSampler(d.device)
+    sampler = UtilSampler(d.device) if d.cuda else None
     coll = None
     use_coll = args.collective == "on" or (args.collective == "auto" and world > 1)
-    if use_coll:
+    pod_envs = envs
+    if use_coll:  # pod slot 0 of every GPU is the DP trainer, run by this rank (it owns the RCCL group)
         from nos_amd.models.tenants import CollectiveTenant
 
-        coll = CollectiveTenant(dim=2048, bucket_mb=16, device=d.device)
+        trainer_env, pod_envs = envs[0], envs[1:]
+        if d.cuda and trainer_env.get("NOS_AMD_MEMORY_LIMIT_GB"):
+            import torch
+
+            torch.cuda.set_per_process_memory_fraction(
+                min(1.0, float(trainer_env["NOS_AMD_MEMORY_LIMIT_GB"]) * 2 ** 30 /
+                    torch.cuda.get_device_properties(d.device).total_memory), d.device)
+        coll = CollectiveTenant(dim=args.coll_dim if d.cuda else 128, bucket_mb=args.coll_bucket_mb if d.cuda else 1,
+                                device=d.device if d.cuda else "cpu")
 
     ref = None
     if args.ref_pod_s > 0:  # one pod owning the whole GPU (no slice env but the device)
         env1 = [{"HIP_VISIBLE_DEVICES": envs[0].get("HIP_VISIBLE_DEVICES", str(local))}]
-        w1, u1, _, _ = run_fleet(d, launcher, env1, args.dtype, not args.no_graphs, extra_env, 2, 1, args.ref_pod_s, sampler)
+        w1, u1, _, _, _ = run_fleet(d, launcher, env1, args.dtype, not args.no_graphs, extra_env, 2, 1,
+                                    args.ref_pod_s, sampler, device=args.device)
         ref = {"inf_per_s": round(w1.throughput, 3), "latency_s": w1.mean_latency_s, "gpu_util_pct": u1}
 
-    w, util, n_util, ready_s = run_fleet(d, launcher, envs, args.dtype, not args.no_graphs, extra_env, args.warmup,
-                                         args.steps, args.step_s, sampler, coll)
+    w, util, n_util, ready_s, tr = run_fleet(d, launcher, pod_envs, args.dtype, not args.no_graphs, extra_env,
+                                             args.warmup, args.steps, args.step_s, sampler, coll, device=args.device)
     bf = None
-    if args.extra_bf16_s > 0 and args.dtype != "bf16":
-        wb, ub, _, _ = run_fleet(d, launcher, envs, "bf16", not args.no_graphs, extra_env, 2, 1, args.extra_bf16_s, sampler)
+    if args.extra_bf16_s > 0 and args.dtype != "bf16" and d.cuda:
+        wb, ub, _, _, _ = run_fleet(d, launcher, pod_envs, "bf16", not args.no_graphs, extra_env, 2, 1,
+                                    args.extra_bf16_s, sampler, coll)
         bf = {"inf_per_s": round(wb.throughput, 2), "mean_latency_s": wb.mean_latency_s,
               "concurrent_pods": wb.concurrent, "gpu_util_pct": ub}
-    sampler.close()
+    if sampler:
+        sampler.close()
     launcher.close()
 
     # whole-job aggregates (window = slowest rank's)
     elapsed, = d.reduce([w.window_s], "max")
-    sums = d.reduce([w.completed, float(w.concurrent), util if util is not None else -1e9, float(len(envs)),
-                     ref["inf_per_s"] if ref else 0.0, bf["inf_per_s"] if bf else 0.0], "sum")
-    completed, concurrent, util_sum, pods_total, ref_sum, bf_sum = sums
+    running = w.concurrent + (1 if tr and tr["running"] else 0)
+    sums = d.reduce([w.completed, float(running), util if util is not None else -1e9, float(len(pod_envs)),
+                     ref["inf_per_s"] if ref else 0.0, bf["inf_per_s"] if bf else 0.0,
+                     tr["gemm_tflops"] if tr else 0.0, tr["allreduce_gb_per_s"] if tr else 0.0,
+                     float(len(envs))], "sum")
+    completed, concurrent, util_sum, pods_total, ref_sum, bf_sum, tr_tf, tr_gbs, placed = sums
     agg = completed / elapsed
     util_mean = util_sum / world if util_sum >= 0 else None
     lat = pods_total * elapsed / completed if completed > 0 else None
@@ -290,12 +334,13 @@ def main(argv=None) -> int:
         "dtype": args.dtype,
         "data": "synthetic (random-init YOLOS-small weights, random 800x1066 image per pod)",
         "config": {"model": "YOLOS-small (hustvl/yolos-small architecture) inference pods",
-                   "global_batch": int(pods_total), "seq_len": seq_len(cfg, hw),
+                   "global_batch": int(pods_total), "seq_len": seq_len(cfg, hw), "device": args.device,
                    "parallelism": f"{args.mode} fractional slices, {args.pods_per_gpu} pod processes/GPU, "
                                   f"{world} GPU(s)",
                    "pods_per_gpu": args.pods_per_gpu, "slice_gb": args.slice_gb, "mode": args.mode,
                    "pod_execution": "one process per pod with its device-plugin env", "graphs": not args.no_graphs,
-                   "collective_tenant": bool(coll), "step_s": args.step_s},
+                   "collective_tenant": bool(coll), "step_s": args.step_s,
+                   "pods_placed_per_node": int(placed)},
         "gpu_util_pct": None if util_mean is None else round(util_mean, 1),
         "gpu_util_samples": n_util,
         "schedulable_fractional_pods_per_node": value,
@@ -312,12 +357,16 @@ def main(argv=None) -> int:
         "baseline": {"pods_per_gpu": BASELINE_PODS_PER_GPU, "inf_per_s_per_gpu": BASELINE_INF_PER_S_PER_GPU,
                      "aggregate_vs_single_pod_mps": 1.93, "aggregate_vs_single_pod_mig": 1.79},
         "bf16_gfx950_kernels": None if bf is None else {**bf, "inf_per_s_node": round(bf_sum, 2)},
+        "trainer_pods": None if tr is None else {"per_node_gemm_tflops": round(tr_tf, 2),
+                                                 "per_node_allreduce_gb_per_s": round(tr_gbs, 2),
+                                                 "rank0": tr, "bucket_mb": args.coll_bucket_mb,
+                                                 "gemm_dim": args.coll_dim},
         "rank0_window": w.as_dict(),
         "rank0_ref_pod": ref,
         "pods_ready_s": round(ready_s, 1),
         "control_plane": cp,
     }
-    if sampler.err:
+    if sampler and sampler.err:
         result["gpu_util_error"] = sampler.err
     if rank == 0:
         line = json.dumps(result)

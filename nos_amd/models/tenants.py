@@ -81,25 +81,75 @@ class InferenceTenants:
 
 
 class CollectiveTenant:
-    """DP trainer tenant: y = x @ W (bf16 GEMMs) then all-reduce of a gradient
-    bucket on its own stream; one per rank/GPU."""
+    """DP trainer pod: y = x @ W (GEMMs) then an all-reduce of a gradient
+    bucket (RCCL over xGMI on GPUs, gloo on the CPU rehearsal path); one per
+    rank/GPU.  Ranks run in LOCKSTEP: every iteration also all-reduces a stop
+    flag, so all ranks leave a time-bounded loop after the same iteration and
+    never issue mismatched collectives."""
 
-    def __init__(self, dim: int = 8192, bucket_mb: int = 64, device: int | None = None, stream=None):
-        dev = torch.cuda.current_device() if device is None else device
-        self.x = torch.randn(dim, dim, device=f"cuda:{dev}", dtype=torch.bfloat16)
-        self.w = torch.randn(dim, dim, device=f"cuda:{dev}", dtype=torch.bfloat16)
-        self.grad = torch.randn(bucket_mb * (1 << 20) // 2, device=f"cuda:{dev}", dtype=torch.bfloat16)
-        self.stream = stream if stream is not None else torch.cuda.Stream(device=dev)
+    def __init__(self, dim: int = 8192, bucket_mb: int = 64, device: int | str | None = None, stream=None):
+        if device == "cpu":
+            self.dev, dt = torch.device("cpu"), torch.float32
+        else:
+            dev = torch.cuda.current_device() if device is None else device
+            self.dev, dt = torch.device("cuda", dev), torch.bfloat16
+        g = torch.Generator().manual_seed(0)
+        self.x = torch.randn(dim, dim, generator=g).to(self.dev, dt)
+        self.w = torch.randn(dim, dim, generator=g).to(self.dev, dt) * dim ** -0.5
+        n = max(1, bucket_mb * (1 << 20) // self.x.element_size())
+        self.grad = torch.zeros(n, device=self.dev, dtype=dt)
+        self.flag = torch.zeros(1, device=self.dev, dtype=torch.float32)
+        self.stream = stream if (stream is not None or self.dev.type == "cpu") else torch.cuda.Stream(device=self.dev)
         self.dim = dim
+        self.iters = 0
 
-    def step(self) -> None:
+    def _dist(self):
         import torch.distributed as dist
 
-        with torch.cuda.stream(self.stream):
+        return dist if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1 else None
+
+    def step(self) -> None:
+        ctx = torch.cuda.stream(self.stream) if self.stream is not None else _null()
+        with ctx:
             y = self.x @ self.w
-            self.grad[: y.numel() // 64].copy_(y.view(-1)[: y.numel() // 64])
-            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-                dist.all_reduce(self.grad)
+            k = min(self.grad.numel(), y.numel())
+            self.grad[:k].copy_(y.view(-1)[:k])
+            d = self._dist()
+            if d is not None:
+                d.all_reduce(self.grad)
+
+    def run_until(self, deadline: float, times: list[float] | None = None) -> int:
+        """Iterate (GEMM + bucket all-reduce + stop-flag all-reduce) until every
+        rank has passed ``deadline`` (time.monotonic()); completion times of the
+        iterations are appended to ``times``."""
+        import torch.distributed as dist
+
+        n = 0
+        while True:
+            self.step()
+            ctx = torch.cuda.stream(self.stream) if self.stream is not None else _null()
+            with ctx:
+                self.flag.fill_(1.0 if time.monotonic() >= deadline else 0.0)
+                if self._dist() is not None:
+                    dist.all_reduce(self.flag, op=dist.ReduceOp.MAX)
+                stop = self.flag.item() > 0  # synchronises this iteration
+            n += 1
+            self.iters += 1
+            if times is not None:
+                times.append(time.monotonic())
+            if stop:
+                return n
 
     def flops_per_step(self) -> float:
         return 2.0 * self.dim ** 3
+
+    def bucket_bytes(self) -> int:
+        return self.grad.numel() * self.grad.element_size()
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

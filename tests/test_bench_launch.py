@@ -1,0 +1,41 @@
+"""The exact multi-GPU launch path of bench.py (python -m torch.distributed.run
+... bench.py --gpus N), rehearsed on the CPU: gloo instead of RCCL, tiny
+YOLOS pods on the CPU.  Every rank places its pods through the control plane,
+starts them as processes, runs its lockstep DP trainer pod, and rank 0 prints
+ONE JSON line aggregated over ranks."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _run(n: int, port: int) -> list[dict]:
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", str(n), "--device", "cpu",
+           "--steps", "4", "--warmup", "1", "--step-s", "0.4", "--ref-pod-s", "0", "--pods-per-gpu", "3"]
+    env = {**os.environ, "OMP_NUM_THREADS": "1"}
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+
+
+@pytest.mark.timeout(900)
+def test_torchrun_two_ranks_aggregate_one_json_line():
+    lines = _run(2, 29611)
+    assert len(lines) == 1  # rank 0 only
+    d = lines[0]
+    base = json.loads((REPO / "BASELINE.json").read_text())
+    assert d["metric"] == base["metric"]
+    assert d["n_gpus"] == 2 and d["steps"] == 4 and d["warmup"] == 1
+    # 3 pods per GPU: 2 inference pods + the DP trainer pod, all observed running, on both ranks
+    assert d["value"] == 6 and d["config"]["pods_placed_per_node"] == 6
+    assert d["trainer_pods"]["rank0"]["running"] and d["trainer_pods"]["per_node_allreduce_gb_per_s"] > 0
+    assert d["ms_per_step"] == pytest.approx(400, rel=0.2)
+    assert d["aggregate_inf_per_s"] > 0 and d["scaling"] == "weak"
