@@ -243,7 +243,7 @@ def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, 
         n_it = len(inside) - 2
         tr = {"iterations": n_it, "running": n_it > 0 and gap < 0.25 * (t1 - t0), "max_gap_s": round(gap, 3),
               "gemm_tflops": round(n_it * coll.flops_per_step() / (t1 - t0) / 1e12, 2),
-              "allreduce_gb_per_s": round(n_it * coll.bucket_bytes() / (t1 - t0) / 1e9, 2)}
+              "allreduce_gb_per_s": round(n_it * coll.bucket_bytes() / (t1 - t0) / 1e9, 2) if coll._dist() else 0.0}
     return w, util, n_util, ready_s, tr
 
 

@@ -141,6 +141,7 @@ struct Backend {
   virtual int processes(int i, nos_proc_info* out, int max, int* n) = 0;
   virtual int link(int i, int j, int* type, long long* hops, long long* weight) = 0;
   virtual int partition_count(int i) = 0;
+  virtual int clock(int i, int* cur_mhz, int* max_mhz) = 0;
   virtual int partition_info(int i, int p, nos_part_info* out) = 0;
   virtual int inject(const char* /*fault*/) { return NOS_SMI_ERR_UNSUPPORTED; }
   virtual int add_process(int, unsigned, long long, unsigned) { return NOS_SMI_ERR_UNSUPPORTED; }
@@ -274,6 +275,13 @@ struct FakeBackend : Backend {
     return NOS_SMI_OK;
   }
 
+  int clock(int i, int* cur, int* mx) override {
+    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    *mx = 2400;
+    *cur = gpus[i].gfx > 0 ? 2400 : 500;  // busy GPUs run at the top clock, idle ones deep-sleep
+    return NOS_SMI_OK;
+  }
+
   // logical devices: GPU-major enumeration (the driver's order), partition p of
   // GPU i gets HIP id / render node after every partition of GPUs 0..i-1
   int partition_count(int i) override {
@@ -372,6 +380,7 @@ struct SmiApi {
   NOS_SMI_FN(amdsmi_topo_get_link_type);
   NOS_SMI_FN(amdsmi_topo_get_link_weight);
   NOS_SMI_FN(amdsmi_get_gpu_kfd_info);
+  NOS_SMI_FN(amdsmi_get_clock_info);
 #undef NOS_SMI_FN
 
   bool load() {
@@ -401,6 +410,7 @@ struct SmiApi {
     NOS_SMI_LOAD(amdsmi_topo_get_link_type);
     NOS_SMI_LOAD(amdsmi_topo_get_link_weight);
     NOS_SMI_LOAD(amdsmi_get_gpu_kfd_info);
+    NOS_SMI_LOAD(amdsmi_get_clock_info);
 #undef NOS_SMI_LOAD
     return amdsmi_init && amdsmi_get_socket_handles && amdsmi_get_processor_handles;
   }
@@ -547,6 +557,17 @@ struct AmdSmiBackend : Backend {
   int partition_count(int i) override {
     if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
     return (int)gpus[i].size();
+  }
+
+  int clock(int i, int* cur, int* mx) override {
+    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (!api.amdsmi_get_clock_info) return NOS_SMI_ERR_UNSUPPORTED;
+    amdsmi_clk_info_t c{};
+    if (api.amdsmi_get_clock_info(gpus[i][0], AMDSMI_CLK_TYPE_GFX, &c) != AMDSMI_STATUS_SUCCESS)
+      return NOS_SMI_ERR_BACKEND;
+    *cur = (int)c.clk;
+    *mx = (int)c.max_clk;
+    return NOS_SMI_OK;
   }
 
   int partition_info(int i, int p, nos_part_info* o) override {
@@ -738,6 +759,10 @@ NOS_API int nos_smi_processes(int i, nos_proc_info* out, int max, int* n) {
 NOS_API int nos_smi_link(int i, int j, int* type, long long* hops, long long* weight) {
   NOS_SMI_GUARD();
   return g_backend->link(i, j, type, hops, weight);
+}
+NOS_API int nos_smi_clock(int i, int* cur_mhz, int* max_mhz) {
+  NOS_SMI_GUARD();
+  return g_backend->clock(i, cur_mhz, max_mhz);
 }
 NOS_API int nos_smi_partition_count(int i) {
   NOS_SMI_GUARD();

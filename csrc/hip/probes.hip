@@ -48,6 +48,41 @@ __global__ __launch_bounds__(256) void probe_hbm_copy_kernel(const uint4* __rest
   for (; i < n; i += stride) dst[i] = src[i];
 }
 
+// Streaming probes with 8 x 16 B per lane in flight: copy with non-temporal
+// loads/stores (the stream never pollutes L2/MALL for co-tenants) and a
+// read-only reduction (the read side alone).
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void probe_hbm_copy_nt_kernel(const u32x4_t* __restrict__ src,
+                                                               u32x4_t* __restrict__ dst, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 7 * stride < n; i += 8 * stride) {
+    u32x4_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+  }
+  for (; i < n; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
+__global__ __launch_bounds__(256) void probe_hbm_read_kernel(const u32x4_t* __restrict__ src,
+                                                            u32x4_t* __restrict__ sink, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  u32x4_t acc = {0u, 0u, 0u, 0u};
+  for (; i + 7 * stride < n; i += 8 * stride) {
+    u32x4_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc ^= v[u];
+  }
+  for (; i < n; i += stride) acc ^= src[i];
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[threadIdx.x] = acc;  // keep the loads live
+}
+
 __global__ __launch_bounds__(256) void probe_mfma_peak_kernel(float* __restrict__ out, int iters,
                                                               unsigned seed) {
   const int lane = threadIdx.x & 63;
@@ -114,6 +149,41 @@ NOS_API int nos_probe_hbm(hipStream_t stream, long long bytes, int iters, int nw
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, tm.a, tm.b);
   *gbps = (ms > 0.f) ? (2.0 * (double)bytes * iters) / (ms * 1e-3) / 1e9 : 0.0;
+  (void)hipFree(src);
+  (void)hipFree(dst);
+  return rc;
+}
+
+// HBM probe variants (mode 0: plain copy, 1: non-temporal copy, 2: read-only).
+// GB/s counts every byte moved (copy: read + write).
+NOS_API int nos_probe_hbm_mode(hipStream_t stream, long long bytes, int iters, int nwg, int mode, double* gbps) {
+  if (bytes <= 0 || (bytes % 16) || nwg <= 0 || iters <= 0 || mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+  void *src = nullptr, *dst = nullptr;
+  HIP_CHECK_RET(hipMalloc(&src, bytes));
+  HIP_CHECK_RET(hipMalloc(&dst, mode == 2 ? 4096 : bytes));
+  (void)hipMemsetAsync(src, 1, bytes, stream);
+  const long long n = bytes / 16;
+  auto launch = [&]() {
+    if (mode == 0)
+      hipLaunchKernelGGL(probe_hbm_copy_kernel, dim3(nwg), dim3(256), 0, stream, (const uint4*)src, (uint4*)dst, n);
+    else if (mode == 1)
+      hipLaunchKernelGGL(probe_hbm_copy_nt_kernel, dim3(nwg), dim3(256), 0, stream, (const u32x4_t*)src,
+                         (u32x4_t*)dst, n);
+    else
+      hipLaunchKernelGGL(probe_hbm_read_kernel, dim3(nwg), dim3(256), 0, stream, (const u32x4_t*)src,
+                         (u32x4_t*)dst, n);
+  };
+  launch();  // warm-up
+  EventTimer tm;
+  (void)hipEventRecord(tm.a, stream);
+  for (int i = 0; i < iters; ++i) launch();
+  (void)hipEventRecord(tm.b, stream);
+  (void)hipEventSynchronize(tm.b);
+  int rc = (int)hipGetLastError();
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, tm.a, tm.b);
+  const double moved = (mode == 2 ? 1.0 : 2.0) * (double)bytes * iters;
+  *gbps = (ms > 0.f) ? moved / (ms * 1e-3) / 1e9 : 0.0;
   (void)hipFree(src);
   (void)hipFree(dst);
   return rc;

@@ -19,6 +19,7 @@ import logging
 from typing import Callable
 
 from ..api import constants as C
+from .probe import METRICS as PROBE_METRICS
 from ..gpu import cumask as cm
 from ..gpu.core import devices_as_status_annotations, parse_node_annotations, spec_matches_status, status_equal
 from ..kube import objects as ko
@@ -72,11 +73,14 @@ class CuMaskReporter:
                     log.warning("probe of gpu %d slice %s failed: %s", s.index, s.profile, e)
                     self._probed[k] = {}
             r = self._probed[k]
-            if "tflops" in r:
-                out[C.ANNOTATION_SLICE_TFLOPS_FORMAT.format(index=s.index, profile=s.profile)] = f"{r['tflops']:.1f}"
-                metrics.SLICE_TFLOPS.labels(self.node_name, str(s.index), s.profile).set(r["tflops"])
+            for m in PROBE_METRICS:
+                if m in r:
+                    key = f"{C.ANNOTATION_PROBE_PREFIX}-{s.index}-{s.profile}-{m}"
+                    out[key] = f"{r[m]:.1f}" if "tflops" in m else f"{r[m]:.0f}"
+            if "gemmtflops" in r or "tflops" in r:
+                metrics.SLICE_TFLOPS.labels(self.node_name, str(s.index), s.profile).set(
+                    r.get("gemmtflops", r.get("tflops")))
             if "gbps" in r:
-                out[C.ANNOTATION_SLICE_GBPS_FORMAT.format(index=s.index, profile=s.profile)] = f"{r['gbps']:.0f}"
                 metrics.SLICE_GBPS.labels(self.node_name, str(s.index), s.profile).set(r["gbps"])
         return out
 

@@ -131,6 +131,7 @@ def _L():
             L.nos_smi_fake_remove_process.argtypes = [ctypes.c_int, ctypes.c_uint]
             L.nos_smi_fake_set_activity.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
             L.nos_smi_partition_count.argtypes = [ctypes.c_int]
+            L.nos_smi_clock.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
             L.nos_smi_partition_info.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_PartInfo)]
             L.nos_smi_struct_sizes.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
             a, b = ctypes.c_int(), ctypes.c_int()
@@ -208,6 +209,14 @@ class AmdSmi:
         if rc != 0:
             raise AmdSmiError(rc, f"activity({i})")
         return {"gfx": a.value, "umc": b.value, "mm": c.value}
+
+    def clock(self, i: int) -> dict[str, int]:
+        """Current and maximum GFX clock (MHz) -- tells DVFS apart from a kernel limit."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        rc = _L().nos_smi_clock(i, ctypes.byref(a), ctypes.byref(b))
+        if rc != 0:
+            raise AmdSmiError(rc, f"clock({i})")
+        return {"sclk_mhz": a.value, "max_sclk_mhz": b.value}
 
     def processes(self, i: int, max_procs: int = 256) -> list[ProcInfo]:
         arr = (_ProcInfo * max_procs)()

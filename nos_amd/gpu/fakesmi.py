@@ -69,6 +69,9 @@ class FakeSmi:
                                   bdf=f"0000:{0x11 + i:02x}:00.{p}", uuid=f"GPU-{self.node}-{i:04d}-p{p}")
                     for p in range(n)]
 
+    def clock(self, i: int) -> dict[str, int]:
+        return {"sclk_mhz": 2400 if self.activity_gfx[i] > 0 else 500, "max_sclk_mhz": 2400}
+
     def activity(self, i: int) -> dict[str, int]:
         return {"gfx": self.activity_gfx[i], "umc": self.activity_umc[i], "mm": 0}
 

@@ -40,6 +40,7 @@ _SIGS = {
     "nos_probe_placement": [c_void_p, c_int, c_int, c_void_p],
     "nos_probe_hbm_copy": [c_void_p, c_void_p, c_ll, c_int, c_void_p],
     "nos_probe_hbm": [c_void_p, c_ll, c_int, c_int, ctypes.POINTER(c_double)],
+    "nos_probe_hbm_mode": [c_void_p, c_ll, c_int, c_int, c_int, ctypes.POINTER(c_double)],
     "nos_probe_mfma_peak": [c_void_p, c_int, c_int, ctypes.POINTER(c_double)],
     "nos_probe_mfma_peak_launch": [c_void_p, c_int, c_int, c_void_p],
     "nos_probe_gemm": [c_void_p, c_int, c_int, c_int, ctypes.POINTER(c_double)],

@@ -55,6 +55,16 @@ def hbm_gbps(stream: int, bytes_: int = 1 << 30, iters: int = 5, nwg: int = 2048
     return v.value
 
 
+HBM_MODES = {"copy": 0, "copy_nt": 1, "read": 2}
+
+
+def hbm_mode_gbps(stream: int, mode: str = "copy_nt", bytes_: int = 1 << 30, iters: int = 5, nwg: int = 2048) -> float:
+    v = ctypes.c_double()
+    _lib.check(_lib.lib().nos_probe_hbm_mode(stream, bytes_, iters, nwg, HBM_MODES[mode], ctypes.byref(v)),
+               "probe_hbm_mode")
+    return v.value
+
+
 def mfma_peak_tflops(stream: int, nwg: int, iters: int = 20000) -> float:
     v = ctypes.c_double()
     _lib.check(_lib.lib().nos_probe_mfma_peak(stream, nwg, iters, ctypes.byref(v)), "probe_mfma_peak")

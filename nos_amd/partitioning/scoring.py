@@ -36,7 +36,14 @@ from typing import Callable, Iterable
 
 from ..api import constants as C
 
-_PROBE_RE = re.compile(re.escape(C.ANNOTATION_PROBE_PREFIX) + r"-(\d+)-([^-]+)-(tflops|gbps)$")
+_PROBE_RE = re.compile(re.escape(C.ANNOTATION_PROBE_PREFIX) +
+                       r"-(\d+)-([^-]+)-(tflops|gbps|gemmtflops|sclkmhz|loadedgbps|loadedgemmtflops)$")
+
+
+def _rate(p: dict[str, float]) -> float:
+    """A slice's measured compute rate: the realistic GEMM probe when published,
+    else the MFMA peak (older agents)."""
+    return p.get("gemmtflops", p.get("tflops", 0.0))
 
 
 def probe_table(annotations: dict[str, str]) -> dict[int, dict[str, dict[str, float]]]:
@@ -66,9 +73,9 @@ def gpu_capacities(table: dict[int, dict[str, dict[str, float]]],
     caps: dict[int, float] = {}
     for gi, profs in table.items():
         counts = slice_counts.get(gi, {})
-        tot = sum(p.get("tflops", 0.0) * counts.get(name, 0) for name, p in profs.items())
+        tot = sum(_rate(p) * counts.get(name, 0) for name, p in profs.items())
         if tot <= 0:
-            tot = max((p.get("tflops", 0.0) for p in profs.values()), default=0.0)
+            tot = max((_rate(p) for p in profs.values()), default=0.0)
         if tot > 0:
             caps[gi] = tot
     return caps
