@@ -25,6 +25,4 @@ for B in (1,8):
 for tag in ("var","new"):
     print(tag, [json.load(open(f))["value"] for f in sorted(glob.glob(f"{O}/bench_{tag}_r*.json"))])
 PY
-if [ -f build/variants/stamps/libnos_hip.so ]; then
-  NOS_AMD_HIP_LIB=build/variants/stamps/libnos_hip.so timeout -k 10 120 python tools/gemm_stamps.py $O/stamps.json > $O/stamps.log 2>&1 || exit 1
-fi
+

@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--impls", default="register", help="comma list of GEMM epilogue impls to A/B (register,lds)")
     ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds per impl (median reported)")
+    ap.add_argument("--policies", default="throughput", help="comma list of GEMM tile policies to A/B "
+                    "(throughput, latency)")
     a = ap.parse_args()
     torch.manual_seed(0)
     S, H, hid, mlp = 3401, 6, 384, 1536
@@ -90,16 +92,18 @@ def main():
                 fn = lambda: ops.linear_ln(xa, wg, c1, c2, act=act, out=outg)  # noqa: E731
             else:
                 fn = lambda: ops.linear(xa, w, b, act=act, residual=r if resid else None, out=outg)  # noqa: E731
-            impls = a.impls.split(",")
+            impls = [(im, po) for im in a.impls.split(",") for po in a.policies.split(",")]
             times = {im: [] for im in impls}
             for _ in range(a.rounds):
-                for im in impls:
+                for im, po in impls:
                     ops.set_gemm_impl(im)
-                    times[im].append(timeit(fn, a.iters))
+                    ops.set_gemm_policy(po)
+                    times[(im, po)].append(timeit(fn, a.iters))
             ops.set_gemm_impl("register")
+            ops.set_gemm_policy("throughput")
             for im in impls:
                 t = sorted(times[im])[len(times[im]) // 2]
-                sfx = "" if im == impls[0] else f"_{im}"
+                sfx = "" if im == impls[0] else f"_{im[0]}_{im[1]}"
                 res[f"{name}{sfx}_us"] = t
                 res[f"{name}{sfx}_tflops"] = 2 * M * N * K / t / 1e6
             tus = timeit(lambda: torch.nn.functional.linear(xa, w, b), a.iters)
