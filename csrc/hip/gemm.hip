@@ -24,9 +24,9 @@
 //    so the MFMA main loop runs on the raw residual stream; per-row mean /
 //    variance are accumulated from the A tiles already staged in LDS (the
 //    K loop covers the whole row because K == hidden);
-//  * epilogue through LDS: accumulators (+bias / LN correction / GELU) are
-//    written as fp32 to LDS, then every thread stores 16-byte bf16 chunks
-//    of whole rows (coalesced) and adds the residual with 16-byte loads;
+//  * register epilogue: swapped MFMA operands + v_permlane32_swap give each
+//    lane 8 consecutive columns of one row; bias / LN correction / GELU /
+//    residual are applied in registers and stored as 16-byte row chunks;
 //  * optional persistent mode (grid smaller than the tile count) and an
 //    XCD-aware tile order so tiles sharing the larger operand panel share an
 //    XCD's L2.
@@ -44,11 +44,6 @@ template <int BN>
 struct Cfg {
   static constexpr int TILE_B_BYTES = BN * BK * 2;
   static constexpr int STAGE_BYTES = TILE_A_BYTES + TILE_B_BYTES;
-  static constexpr int CT_LD = BN + 4;                 // fp32 C tile row stride (floats)
-  static constexpr int CT_BYTES = BM * CT_LD * 4;      // 67,584 B (BN 128) / 34,816 B (BN 64)
-  static constexpr int MAIN_BYTES = (2 * STAGE_BYTES > CT_BYTES) ? 2 * STAGE_BYTES : CT_BYTES;
-  static constexpr int STATS_OFF = MAIN_BYTES;         // mu[BM], rstd[BM], p1[BN], p2[BN]
-  static constexpr int LDS_BYTES = MAIN_BYTES + (2 * BM + 2 * BN) * 4;
   static constexpr int WN = BN / 2;                    // wave tile: 64 x WN (2x2 waves)
   static constexpr int NB = WN / 32;                   // 32-column MFMA blocks per wave
 };
@@ -103,213 +98,14 @@ __device__ __forceinline__ float erf_fast(float x) {
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
 
-template <bool LN, int BN>
-__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(
-    const unsigned short* __restrict__ A, int lda, const unsigned short* __restrict__ W, int ldw,
-    const unsigned short* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
-    const unsigned short* __restrict__ R, int ldr, unsigned short* __restrict__ C, int ldc, int M, int N,
-    int K, int epi, float eps, int tiles_m, int tiles_n) {
-  using CF = Cfg<BN>;
-  constexpr int TILE_B_BYTES = CF::TILE_B_BYTES, STAGE_BYTES = CF::STAGE_BYTES, CT_LD = CF::CT_LD;
-  constexpr int WN = CF::WN, NB = CF::NB;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* s_mu = reinterpret_cast<float*>(smem + CF::STATS_OFF);
-  float* s_rstd = s_mu + BM;
-  float* s_p1 = s_rstd + BM;
-  float* s_p2 = s_p1 + BN;
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  const int r = lane & 31, hh = lane >> 5;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int ntiles = tiles_m * tiles_n;
-  const int nk = K / BK;
-
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int tt = (gridDim.x >= ntiles) ? nos::xcd_remap(tile, ntiles) : tile;
-    // consecutive tt share an XCD (and its L2): order them so they share the
-    // LARGER operand's panel -- each XCD then streams a few panels of it plus
-    // the whole smaller one (3401x384 A, 1152x384 W: 1.2 MB per XCD instead
-    // of 2.9 MB with W-panel-major order)
-    int tm, tn;
-    if (tiles_m >= tiles_n) {
-      tm = tt / tiles_n;
-      tn = tt - tm * tiles_n;
-    } else {
-      tn = tt / tiles_m;
-      tm = tt - tn * tiles_m;
-    }
-    const int m0 = tm * BM, n0 = tn * BN;
-
-    f32x16_t acc[2][NB];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
-
-    // LN statistics: thread owns half a row of every A tile (shifted sums)
-    const int srow = tid >> 1, shalf = tid & 1;
-    float sshift = 0.f, ssum = 0.f, ssq = 0.f;
-
-    stage_tile<BM>(A, lda, m0, M, 0, smem, wid, lane);
-    stage_tile<BN>(W, ldw, n0, N, 0, smem + TILE_A_BYTES, wid, lane);
-    __syncthreads();  // drains the DMA (vmcnt(0)) and publishes the tile
-
-    for (int kt = 0; kt < nk; ++kt) {
-      unsigned char* cur = smem + (kt & 1) * STAGE_BYTES;
-      if (kt + 1 < nk) {
-        unsigned char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
-        stage_tile<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wid, lane);
-        stage_tile<BN>(W, ldw, n0, N, (kt + 1) * BK, nxt + TILE_A_BYTES, wid, lane);
-      }
-      const unsigned char* ta = cur;
-      const unsigned char* tb = cur + TILE_A_BYTES;
-      if constexpr (LN) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int lc = shalf * 4 + c;
-          const s16x8_t v = *reinterpret_cast<const s16x8_t*>(ta + srow * 128 + ((lc ^ swz(srow)) << 4));
-          if (kt == 0 && c == 0) sshift = nos::bf16_to_f32((unsigned short)v[0]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float d = nos::bf16_to_f32((unsigned short)v[e]) - sshift;
-            ssum += d;
-            ssq = fmaf(d, d, ssq);
-          }
-        }
-      }
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        bf16x8_t af[2], bf[NB];
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-          const int row = wm * 64 + mi * 32 + r;
-          af[mi] = *reinterpret_cast<const bf16x8_t*>(ta + row * 128 + (((2 * ks + hh) ^ swz(row)) << 4));
-        }
-#pragma unroll
-        for (int ni = 0; ni < NB; ++ni) {
-          const int row = wn * WN + ni * 32 + r;
-          bf[ni] = *reinterpret_cast<const bf16x8_t*>(tb + row * 128 + (((2 * ks + hh) ^ swz(row)) << 4));
-        }
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < NB; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bf[ni], acc[mi][ni], 0, 0, 0);
-      }
-      __syncthreads();  // next tile landed; everyone done with `cur`
-    }
-
-    if constexpr (LN) {
-      // combine the two half-rows (both halves used the same shift: the
-      // shift of the lower half is broadcast first)
-      const float sh_lo = __shfl(sshift, lane & ~1, 64);
-      // re-base the upper half's sums onto the lower half's shift
-      const float dlt = sshift - sh_lo;
-      const float kh = (float)(K / 2);
-      float s2 = ssum + dlt * kh;
-      float q2 = ssq + 2.f * dlt * ssum + dlt * dlt * kh;
-      s2 += __shfl_xor(s2, 1, 64);
-      q2 += __shfl_xor(q2, 1, 64);
-      if (shalf == 0) {
-        const float mean_d = s2 / (float)K;
-        const float var = fmaxf(q2 / (float)K - mean_d * mean_d, 0.f);
-        s_mu[srow] = sh_lo + mean_d;
-        s_rstd[srow] = rsqrtf(var + eps);
-      }
-      __syncthreads();
-    }
-
-    // ---- epilogue stage 1: raw accumulators -> fp32 LDS tile
-    float* ct = reinterpret_cast<float*>(smem);
-#pragma unroll
-    for (int ni = 0; ni < NB; ++ni) {
-      const int cl = wn * WN + ni * 32 + r;
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int rl = wm * 64 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          ct[rl * CT_LD + cl] = acc[mi][ni][i];
-        }
-    }
-    // per-column epilogue parameters, loaded once per tile: (c1, c2) for the
-    // LN-fused form, (0, bias) otherwise
-    if (tid < BN) {
-      const int n = min(n0 + tid, N - 1);
-      s_p1[tid] = LN ? c1[n] : 0.f;
-      s_p2[tid] = LN ? c2[n] : ((epi & EPI_BIAS) ? nos::bf16_to_f32(bias[n]) : 0.f);
-    }
-    __syncthreads();
-
-    // ---- epilogue stage 2: per 8-column chunk of one row: bias / LN
-    // correction, activation, residual, coalesced 16-byte bf16 store
-#pragma unroll 2
-    for (int it = 0; it < (BM * BN / 8) / NT; ++it) {
-      constexpr int CHUNKS = BN / 8;  // 16-byte chunks per tile row
-      const int c = tid + NT * it;
-      const int rl = c / CHUNKS, ch = c % CHUNKS;
-      const int m = m0 + rl, n = n0 + ch * 8;
-      if (m >= M || n >= N) continue;
-      const float4 lo = *reinterpret_cast<const float4*>(ct + rl * CT_LD + ch * 8);
-      const float4 hi = *reinterpret_cast<const float4*>(ct + rl * CT_LD + ch * 8 + 4);
-      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      const bool full = (n + 8 <= N);
-      {
-        const float4 p1a = *reinterpret_cast<const float4*>(s_p1 + ch * 8);
-        const float4 p1b = *reinterpret_cast<const float4*>(s_p1 + ch * 8 + 4);
-        const float4 p2a = *reinterpret_cast<const float4*>(s_p2 + ch * 8);
-        const float4 p2b = *reinterpret_cast<const float4*>(s_p2 + ch * 8 + 4);
-        const float p1[8] = {p1a.x, p1a.y, p1a.z, p1a.w, p1b.x, p1b.y, p1b.z, p1b.w};
-        const float p2[8] = {p2a.x, p2a.y, p2a.z, p2a.w, p2b.x, p2b.y, p2b.z, p2b.w};
-        if (LN) {
-          const float mu = s_mu[rl], rs = s_rstd[rl];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaf(rs, v[e] - mu * p1[e], p2[e]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += p2[e];
-        }
-      }
-      if (epi & EPI_GELU) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
-      }
-      if (epi & EPI_RELU) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      if (full && ((ldc | ldr) & 7) == 0) {
-        if (epi & EPI_RESID) {
-          const s16x8_t rv = *reinterpret_cast<const s16x8_t*>(R + (long long)m * ldr + n);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += nos::bf16_to_f32((unsigned short)rv[e]);
-        }
-        s16x8_t o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (short)nos::f32_to_bf16(v[e]);
-        *reinterpret_cast<s16x8_t*>(C + (long long)m * ldc + n) = o;
-      } else {
-        for (int e = 0; e < 8 && n + e < N; ++e) {
-          float x = v[e];
-          if (epi & EPI_RESID) x += nos::bf16_to_f32(R[(long long)m * ldr + n + e]);
-          C[(long long)m * ldc + n + e] = nos::f32_to_bf16(x);
-        }
-      }
-    }
-    __syncthreads();  // LDS is restaged by the next persistent tile
-  }
-}
-
 // ---------------------------------------------------------------------------
-// Register-epilogue variant (impl 1).  Same main loop, but the MFMA operands
-// are swapped (D = W_frag . A_frag), so each 32x32 accumulator block holds
-// C^T: lane (r, hh) owns output ROW r and columns 8j + 4hh + {0..3}.  One
-// v_permlane32_swap per register pair turns that into 8 consecutive columns
-// per lane, so bias / LayerNorm correction / activation / residual run on
-// registers and the tile leaves as 16-byte row stores -- no fp32 LDS tile
-// (67 KiB less LDS per workgroup, no LDS write + read pass, one barrier fewer).
-// Register epilogue of the rk kernel.  acc holds C^T blocks
+// Register epilogue.  The MFMA operands are swapped (D = W_frag . A_frag), so
+// each 32x32 accumulator block holds C^T: lane (r, hh) owns output ROW r and
+// columns 8j + 4hh + {0..3}.  One v_permlane32_swap per register pair turns
+// that into 8 consecutive columns per lane, so bias / LayerNorm correction /
+// activation / residual run on registers and the tile leaves as 16-byte row
+// stores -- no fp32 LDS tile (the round-1 LDS-tile epilogue measured slower
+// and was removed).  acc holds C^T blocks
 // (MFMA operands swapped): lane (r, hh) owns row r, columns 8j + 4hh + {0..3}
 // of each 32x32 block; a v_permlane32_swap per register pair gives each lane
 // 8 consecutive columns of its row, stored as one 16-byte chunk.
@@ -548,8 +344,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
   }
 }
 
-int g_epi_impl = 1;  // 0 = fp32 LDS-tile epilogue, 1 = register epilogue (nos_gemm_set_impl)
-
 template <int BNV>
 constexpr int rk_lds_bytes() { return 2 * Cfg<BNV>::STAGE_BYTES + (2 * BM + 2 * BNV) * 4; }
 
@@ -576,14 +370,8 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
 #define NOS_GEMM_ARGS                                                                                     \
   Ap, lda, Wp, ldw, Bp, c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n
 #define NOS_GEMM_LAUNCH(LNV, BNV, RV)                                                                      \
-  do {                                                                                                      \
-    if (g_epi_impl == 1)                                                                                    \
-      hipLaunchKernelGGL((gemm_bf16_rk_kernel<LNV, BNV, RV>), dim3(nwg), dim3(NT), rk_lds_bytes<BNV>(),     \
-                         stream, NOS_GEMM_ARGS);                                                            \
-    else                                                                                                    \
-      hipLaunchKernelGGL((gemm_bf16_kernel<LNV, BNV>), dim3(nwg), dim3(NT), Cfg<BNV>::LDS_BYTES, stream,    \
-                         NOS_GEMM_ARGS);                                                                    \
-  } while (0)
+  hipLaunchKernelGGL((gemm_bf16_rk_kernel<LNV, BNV, RV>), dim3(nwg), dim3(NT), rk_lds_bytes<BNV>(), stream,  \
+                     NOS_GEMM_ARGS)
   const bool resid = (epi & EPI_RESID) != 0;
   if (ln) {
     if (narrow) NOS_GEMM_LAUNCH(true, 64, false); else NOS_GEMM_LAUNCH(true, 128, false);
@@ -605,14 +393,6 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
 NOS_API int nos_gemm_set_policy(int policy) {
   if (policy != 0 && policy != 1) return (int)hipErrorInvalidValue;
   g_tile_policy = policy;
-  return 0;
-}
-
-// Implementation (A/B switch): 0 = fp32 LDS-tile epilogue, 1 = register
-// epilogue (default).
-NOS_API int nos_gemm_set_impl(int impl) {
-  if (impl != 0 && impl != 1) return (int)hipErrorInvalidValue;
-  g_epi_impl = impl;
   return 0;
 }
 

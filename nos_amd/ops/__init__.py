@@ -100,14 +100,6 @@ def set_gemm_policy(policy: str) -> None:
     _lib.check(_lib.lib().nos_gemm_set_policy(code), "nos_gemm_set_policy")
 
 
-def set_gemm_impl(impl: str) -> None:
-    """GEMM epilogue implementation: ``"register"`` (default: accumulators
-    transposed in registers, 16-byte row stores) or ``"lds"`` (fp32 LDS tile;
-    kept for A/B measurements)."""
-    code = {"lds": 0, "register": 1}[impl]
-    _lib.check(_lib.lib().nos_gemm_set_impl(code), "nos_gemm_set_impl")
-
-
 def set_attention_f32_variant(variant: str) -> None:
     """fp32 attention tiling: ``"auto"`` (default), ``"w4k64"`` (4 waves x 64-key
     LDS tiles, best when the grid fills the chip) or ``"w2k32"`` (2 waves x

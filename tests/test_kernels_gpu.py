@@ -33,9 +33,8 @@ def _native():
     (3401, 1152, 384, None, False), (3401, 1536, 384, "gelu", False), (3401, 384, 1536, None, True),
     (3401, 384, 384, None, True), (100, 4, 384, "relu", False), (257, 200, 128, None, False),
     (1, 8, 64, None, False), (4096, 4096, 1024, None, False)])
-@pytest.mark.parametrize("impl,policy", [("register", "throughput"), ("lds", "throughput"), ("register", "latency")])
-def test_linear(M, N, K, act, resid, impl, policy):
-    ops.set_gemm_impl(impl)
+@pytest.mark.parametrize("policy", ["throughput", "latency"])
+def test_linear(M, N, K, act, resid, policy):
     ops.set_gemm_policy(policy)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
@@ -44,7 +43,6 @@ def test_linear(M, N, K, act, resid, impl, policy):
     y = ops.linear(x, w, b, act=act, residual=r)
     ref = ops.linear_ref(x.cpu().float(), w.cpu().float(), b.cpu().float(), act=act,
                          residual=r.cpu().float() if resid else None)
-    ops.set_gemm_impl("register")
     ops.set_gemm_policy("throughput")
     assert y.shape == (M, N) and y.dtype == torch.bfloat16
     assert _rel(y, ref) < 1.5e-2
@@ -52,9 +50,8 @@ def test_linear(M, N, K, act, resid, impl, policy):
 
 @pytest.mark.parametrize("M,N,K,act", [(3401, 1152, 384, None), (3401, 1536, 384, "gelu"), (77, 100, 128, None),
                                        (1, 64, 64, None), (300, 384, 384, None)])
-@pytest.mark.parametrize("impl,policy", [("register", "throughput"), ("lds", "throughput"), ("register", "latency")])
-def test_linear_layernorm_fused(M, N, K, act, impl, policy):
-    ops.set_gemm_impl(impl)
+@pytest.mark.parametrize("policy", ["throughput", "latency"])
+def test_linear_layernorm_fused(M, N, K, act, policy):
     ops.set_gemm_policy(policy)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 2 + 0.5
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
@@ -65,7 +62,6 @@ def test_linear_layernorm_fused(M, N, K, act, impl, policy):
     y = ops.linear_ln(x, wg, c1, c2, act=act)
     ln = torch.nn.functional.layer_norm(x.float().cpu(), (K,), g.float().cpu(), be.float().cpu(), 1e-12)
     ref = ops.linear_ref(ln, w.cpu().float(), b.cpu().float(), act=act)
-    ops.set_gemm_impl("register")
     ops.set_gemm_policy("throughput")
     assert _rel(y, ref) < 2e-2
 

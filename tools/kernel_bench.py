@@ -47,7 +47,6 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--out", default="")
-    ap.add_argument("--impls", default="register", help="comma list of GEMM epilogue impls to A/B (register,lds)")
     ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds per impl (median reported)")
     ap.add_argument("--policies", default="throughput", help="comma list of GEMM tile policies to A/B "
                     "(throughput, latency)")
@@ -92,14 +91,12 @@ def main():
                 fn = lambda: ops.linear_ln(xa, wg, c1, c2, act=act, out=outg)  # noqa: E731
             else:
                 fn = lambda: ops.linear(xa, w, b, act=act, residual=r if resid else None, out=outg)  # noqa: E731
-            impls = [(im, po) for im in a.impls.split(",") for po in a.policies.split(",")]
+            impls = [("register", po) for po in a.policies.split(",")]
             times = {im: [] for im in impls}
             for _ in range(a.rounds):
                 for im, po in impls:
-                    ops.set_gemm_impl(im)
                     ops.set_gemm_policy(po)
                     times[(im, po)].append(timeit(fn, a.iters))
-            ops.set_gemm_impl("register")
             ops.set_gemm_policy("throughput")
             for im in impls:
                 t = sorted(times[im])[len(times[im]) // 2]
