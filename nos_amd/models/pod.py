@@ -129,6 +129,10 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             torch.cuda.set_device(0)  # the device plugin's HIP_VISIBLE_DEVICES leaves exactly the slice's GPU
             frac = apply_memory_limit(0)
             torch.backends.cuda.matmul.allow_tf32 = False  # true fp32 GEMMs (no reduced-precision shortcut)
+        if gpu and os.environ.get("NOS_AMD_GEMM_F32_POLICY"):  # A/B of the fp32 GEMM tile policy
+            from ..ops import set_gemm_f32_policy
+
+            set_gemm_f32_policy(os.environ["NOS_AMD_GEMM_F32_POLICY"])
         m, x = _build(dtype, seed, demo_input_hw(), device)
         if gpu:
             s = torch.cuda.Stream()

@@ -181,8 +181,6 @@ class YolosDetector(nn.Module):
     def forward(self, pixel_values: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
         if self.backend == "torch" or not pixel_values.is_cuda:
             return self._forward_torch(pixel_values)
-        if self.patch_w.dtype == torch.float32:
-            return self._forward_torch(pixel_values, native_attention=True)
         return self._forward_native(pixel_values)
 
     def _embed(self, pixel_values: torch.Tensor, lin) -> torch.Tensor:
@@ -220,7 +218,9 @@ class YolosDetector(nn.Module):
 
     def _forward_native(self, pixel_values: torch.Tensor):
         """5 kernels per encoder layer: [LN1+QKV GEMM] [attention]
-        [proj GEMM + residual] [LN2+fc1 GEMM + GELU] [fc2 GEMM + residual]."""
+        [proj GEMM + residual] [LN2+fc1 GEMM + GELU] [fc2 GEMM + residual] --
+        the bf16 MFMA kernels for bf16 weights, the exact-fp32 MFMA kernels
+        (gemm_f32.hip, attention_f32.hip) for fp32 weights."""
         cfg = self.cfg
         nh = cfg.num_attention_heads
         eps = cfg.layer_norm_eps
@@ -237,7 +237,10 @@ class YolosDetector(nn.Module):
             m = ops.linear_ln(h, fw["fc1_w"], fw["fc1_c1"], fw["fc1_c2"], act="gelu", eps=eps)
             h = ops.linear(m, L.fc2_w, L.fc2_b, residual=h)
         det = h[:, -cfg.num_detection_tokens:, :].contiguous()
-        y, _ = ops.layernorm(det, self.ln_f_w, self.ln_f_b, eps)
+        if det.dtype == torch.float32:  # 100 rows: not worth a kernel of its own in fp32
+            y = F.layer_norm(det, (cfg.hidden_size,), self.ln_f_w, self.ln_f_b, eps)
+        else:
+            y, _ = ops.layernorm(det, self.ln_f_w, self.ln_f_b, eps)
         return self._heads(y, lin)
 
     def _forward_torch(self, pixel_values: torch.Tensor, native_attention: bool = False):

@@ -69,6 +69,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     N = weight.shape[0]
     x2 = x.reshape(-1, K)
     M = x2.shape[0]
+    if x.dtype == torch.float32:
+        return _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K)
     if x2.stride(-1) != 1 or weight.stride(-1) != 1 or K % 64 or x.dtype != torch.bfloat16:
         raise ValueError("native linear needs bf16, unit inner stride and K % 64 == 0")
     if out is None:
@@ -92,12 +94,51 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     return out.reshape(*x.shape[:-1], N)
 
 
+def _epi(bias, act, residual) -> int:
+    e = EPI_BIAS if bias is not None else 0
+    e |= EPI_GELU if act == "gelu" else (EPI_RELU if act == "relu" else 0)
+    return e | (EPI_RESID if residual is not None else 0)
+
+
+def _check_f32(**ts) -> None:
+    for name, t in ts.items():
+        if t is not None and (t.dtype != torch.float32 or t.stride(-1) != 1):
+            raise ValueError(f"native fp32 GEMM: {name} must be fp32 with unit inner stride")
+
+
+def _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K):
+    """Exact-fp32 MFMA GEMM (csrc/hip/gemm_f32.hip) with fused bias/act/residual."""
+    _check_f32(x=x2, weight=weight, bias=bias)
+    if K % 32:
+        raise ValueError("native fp32 linear needs K % 32 == 0")
+    if bias is not None and not bias.is_contiguous():
+        raise ValueError("bias must be contiguous")
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    r2 = residual.reshape(-1, N) if residual is not None else None
+    _check_f32(residual=r2)
+    o2 = out.reshape(-1, N)
+    rc = _lib.lib().nos_gemm_f32(x2.data_ptr(), x2.stride(0), weight.data_ptr(), weight.stride(0), _ptr(bias),
+                                 _ptr(r2), r2.stride(0) if r2 is not None else 0, o2.data_ptr(), o2.stride(0),
+                                 M, N, K, _epi(bias, act, residual), _stream())
+    _lib.check(rc, "nos_gemm_f32")
+    return out.reshape(*x.shape[:-1], N)
+
+
 def set_gemm_policy(policy: str) -> None:
     """``"throughput"`` (default: 128x128 tiles, best when pods share a GPU) or
     ``"latency"`` (128x64 tiles for GEMMs with fewer tiles than CUs, best for
     a single tenant owning the GPU)."""
     code = {"throughput": 0, "latency": 1}[policy]
     _lib.check(_lib.lib().nos_gemm_set_policy(code), "nos_gemm_set_policy")
+
+
+def set_gemm_f32_policy(policy: str) -> None:
+    """fp32 GEMM tiles: ``"latency"`` (default; fewest rounds of tiles over
+    the CUs) or ``"throughput"`` (most MFMA-efficient tile; other co-running
+    pods fill the CUs a small grid leaves idle)."""
+    _lib.check(_lib.lib().nos_gemm_f32_set_policy({"throughput": 0, "latency": 1}[policy]),
+               "nos_gemm_f32_set_policy")
 
 
 def set_attention_f32_variant(variant: str) -> None:
@@ -146,6 +187,18 @@ def linear_ln(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Ten
     N = wg.shape[0]
     x2 = x.reshape(-1, K)
     M = x2.shape[0]
+    if x.dtype == torch.float32:
+        _check_f32(x=x2, weight=wg, c1=c1, c2=c2)
+        if K % 32:
+            raise ValueError("native fp32 linear_ln needs K % 32 == 0")
+        if out is None:
+            out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+        o2 = out.reshape(-1, N)
+        rc = _lib.lib().nos_gemm_ln_f32(x2.data_ptr(), x2.stride(0), wg.data_ptr(), wg.stride(0), c1.data_ptr(),
+                                        c2.data_ptr(), o2.data_ptr(), o2.stride(0), M, N, K, _epi(None, act, None),
+                                        float(eps), _stream())
+        _lib.check(rc, "nos_gemm_ln_f32")
+        return out.reshape(*x.shape[:-1], N)
     if x2.stride(-1) != 1 or K % 64 or x.dtype != torch.bfloat16:
         raise ValueError("native linear_ln needs bf16, unit inner stride and K % 64 == 0")
     if out is None:

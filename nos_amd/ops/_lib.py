@@ -30,7 +30,12 @@ _SIGS = {
                              c_ll, c_int, c_ll, c_float, c_void_p],
     "nos_gemm_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nos_gemm_f32": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
+                     c_int, c_int, c_void_p],
+    "nos_gemm_ln_f32": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                        c_int, c_float, c_void_p],
     "nos_gemm_set_policy": [c_int],
+    "nos_gemm_f32_set_policy": [c_int],
     "nos_attn_f32_set_variant": [c_int],
     "nos_gemm_ln_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_int, c_int, c_float, c_int, c_void_p],

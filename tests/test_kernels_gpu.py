@@ -130,6 +130,53 @@ def test_attention_fp32_strided_and_large_logits():
     assert (y.cpu() - ref).abs().max().item() < 1e-4 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("M,N,K,act,resid", [
+    (3401, 1152, 384, None, False), (3401, 1536, 384, "gelu", False), (3401, 384, 1536, None, True),
+    (3401, 384, 384, None, True), (100, 92, 384, "relu", False), (100, 4, 384, None, False), (257, 200, 96, None, True),
+    (8 * 3401, 384, 1536, None, True), (1, 8, 32, None, False), (3401, 100, 384, None, False)])
+@pytest.mark.parametrize("policy", ["throughput", "latency"])
+def test_linear_fp32_exact(M, N, K, act, resid, policy):
+    """fp32 MFMA GEMM against an fp64 reference (exact-f32 tolerance), every tile shape."""
+    x = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) * 0.05
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(M, N, device=DEV) if resid else None
+    ops.set_gemm_f32_policy(policy)
+    try:
+        y = ops.linear(x, w, b, act=act, residual=r)
+    finally:
+        ops.set_gemm_f32_policy("latency")
+    ref = x.cpu().double() @ w.cpu().double().t() + b.cpu().double()
+    if act == "gelu":
+        ref = torch.nn.functional.gelu(ref)
+    elif act == "relu":
+        ref = ref.clamp_min(0)
+    if resid:
+        ref = ref + r.cpu().double()
+    assert y.dtype == torch.float32 and y.shape == (M, N)
+    err = (y.cpu().double() - ref).abs().max().item()
+    assert err < 2e-5 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("M,N,K,act", [(3401, 1152, 384, None), (3401, 1536, 384, "gelu"), (77, 100, 384, None),
+                                       (1, 64, 64, None), (300, 384, 384, None)])
+def test_linear_layernorm_fused_fp32(M, N, K, act):
+    x = torch.randn(M, K, device=DEV) * 2 + 0.5
+    w = torch.randn(N, K, device=DEV) * 0.05
+    b = torch.randn(N, device=DEV)
+    g = torch.randn(K, device=DEV)
+    be = torch.randn(K, device=DEV)
+    wg, c1, c2 = ops.fold_layernorm(w, b, g, be)
+    y = ops.linear_ln(x, wg, c1, c2, act=act, eps=1e-12)
+    xd = x.cpu().double()
+    ln = torch.nn.functional.layer_norm(xd, (K,), g.cpu().double(), be.cpu().double(), 1e-12)
+    ref = ln @ w.cpu().double().t() + b.cpu().double()
+    if act == "gelu":
+        ref = torch.nn.functional.gelu(ref)
+    err = (y.cpu().double() - ref).abs().max().item()
+    assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
+
+
 def test_yolos_fp32_native_attention_matches_torch():
     from nos_amd.models.yolos import YolosConfig, YolosDetector, demo_input_hw, make_demo_input
 

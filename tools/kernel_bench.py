@@ -48,7 +48,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--out", default="")
     ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds per impl (median reported)")
-    ap.add_argument("--policies", default="throughput", help="comma list of GEMM tile policies to A/B "
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="GEMM dtype")
+    ap.add_argument("--policies", default="latency", help="comma list of GEMM tile policies to A/B "
                     "(throughput, latency)")
     a = ap.parse_args()
     torch.manual_seed(0)
@@ -70,7 +71,8 @@ def main():
         res["sdpa_tflops"] = B * 4 * S * S * hid / us / 1e6
     if "gemm" in a.only:
         M = B * S
-        x = torch.randn(M, hid, device="cuda", dtype=torch.bfloat16)
+        gdt = torch.float32 if a.dtype == "fp32" else torch.bfloat16
+        torch.backends.cuda.matmul.allow_tf32 = False
         for name, (N, K, act, ln, resid) in {
             "qkv_ln": (3 * hid, hid, None, True, False),
             "fc1_ln_gelu": (mlp, hid, "gelu", True, False),
@@ -79,14 +81,14 @@ def main():
             "fc2_resid": (hid, mlp, None, False, True),
             "qkv_plain": (3 * hid, hid, None, False, False),
         }.items():
-            xa = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
-            w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
-            b = torch.randn(N, device="cuda", dtype=torch.bfloat16)
-            r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
-            outg = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            xa = torch.randn(M, K, device="cuda", dtype=gdt)
+            w = torch.randn(N, K, device="cuda", dtype=gdt) * 0.05
+            b = torch.randn(N, device="cuda", dtype=gdt)
+            r = torch.randn(M, N, device="cuda", dtype=gdt)
+            outg = torch.empty(M, N, device="cuda", dtype=gdt)
             if ln:
-                g = torch.randn(K, device="cuda", dtype=torch.bfloat16)
-                be = torch.randn(K, device="cuda", dtype=torch.bfloat16)
+                g = torch.randn(K, device="cuda", dtype=gdt)
+                be = torch.randn(K, device="cuda", dtype=gdt)
                 wg, c1, c2 = ops.fold_layernorm(w, b, g, be)
                 fn = lambda: ops.linear_ln(xa, wg, c1, c2, act=act, out=outg)  # noqa: E731
             else:
@@ -95,9 +97,13 @@ def main():
             times = {im: [] for im in impls}
             for _ in range(a.rounds):
                 for im, po in impls:
-                    ops.set_gemm_policy(po)
+                    if a.dtype == "fp32":
+                        ops.set_gemm_f32_policy(po)
+                    else:
+                        ops.set_gemm_policy(po)
                     times[(im, po)].append(timeit(fn, a.iters))
             ops.set_gemm_policy("throughput")
+            ops.set_gemm_f32_policy("latency")
             for im in impls:
                 t = sorted(times[im])[len(times[im]) // 2]
                 sfx = "" if im == impls[0] else f"_{im[0]}_{im[1]}"

@@ -26,9 +26,10 @@ def main() -> None:
     ap.add_argument("--modes", default="shared,cumask")
     ap.add_argument("--window", type=float, default=10.0)
     ap.add_argument("--warmup", type=float, default=2.0)
-    ap.add_argument("--slice-gb", type=int, default=20)
+    ap.add_argument("--slice-gb", type=int, default=36)
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("--hw-queues", default="0", help="comma list of GPU_MAX_HW_QUEUES values (0 = default)")
+    ap.add_argument("--pod-env", action="append", default=[], help="extra KEY=VALUE for every pod (repeatable)")
     ap.add_argument("--out", default="gpurun_out/sharing_table.json")
     a = ap.parse_args()
 
@@ -47,14 +48,15 @@ def main() -> None:
     rows = []
     for hq in map(int, a.hw_queues.split(",")):
         extra = {"GPU_MAX_HW_QUEUES": str(hq)} if hq else {}
+        extra.update(kv.split("=", 1) for kv in a.pod_env)
         for mode in a.modes.split(","):
             for n in map(int, a.pods.split(",")):
                 envs, info = plans[(mode, n)]
                 t = time.monotonic()
-                w, util, n_util, ready = bench.run_fleet(d, launcher, envs, a.dtype, True, extra, 1, 1, a.window,
+                w, util, n_util, ready, _ = bench.run_fleet(d, launcher, envs, a.dtype, True, extra, 1, 1, a.window,
                                                          sampler, None)
                 w0 = bench.time.monotonic()
-                row = {"mode": mode, "hw_queues": hq, "dtype": a.dtype, **w.as_dict(), "gpu_util_pct": util,
+                row = {"mode": mode, "hw_queues": hq, "pod_env": a.pod_env, "dtype": a.dtype, **w.as_dict(), "gpu_util_pct": util,
                        "util_samples": n_util, "pods_ready_s": round(ready, 1),
                        "cus_per_pod": [p.info.get("cu_mask") for p in w.pods][:2],
                        "wall_s": round(w0 - t, 1)}
