@@ -4,10 +4,11 @@ loop per pod, exposing the Prometheus summary ``inference_time_seconds`` on
 :8000 so the per-pod latency of the three sharing modes can be compared with
 the same query as the reference demo.
 
-MI355X-native: bf16 weights of the hustvl/yolos-small architecture (random
-init -- no checkpoint download; pass --hf-checkpoint to load real weights with
-safetensors), the 800x1066 demo input size, the gfx950 kernels replayed as a
-HIP graph, and the slice's memory cap from the device plugin applied.
+MI355X-native: the hustvl/yolos-small architecture (random init -- no
+checkpoint download; pass --hf-checkpoint to load real weights with
+safetensors) in fp32 like the reference (``--dtype bf16`` for the bf16
+kernels), the 800x1066 demo input size, the gfx950 kernels replayed as a HIP
+graph, and the slice's memory cap from the device plugin applied.
 """
 from __future__ import annotations
 
@@ -24,6 +25,7 @@ def main(argv=None) -> int:
     ap.add_argument("--port", type=int, default=8000)
     ap.add_argument("--iterations", type=int, default=0, help="0 = run forever")
     ap.add_argument("--hf-checkpoint", default="", help="safetensors file of hustvl/yolos-small")
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
     a = ap.parse_args(argv)
     import torch
     from prometheus_client import Summary, start_http_server
@@ -42,8 +44,9 @@ def main(argv=None) -> int:
         model.load_hf_state_dict(load_file(a.hf_checkpoint))
     else:
         model.reset_parameters(0)
-    model = model.to("cuda", torch.bfloat16).eval()
-    x = make_demo_input(cfg, device="cuda", hw=demo_input_hw())
+    dt = torch.float32 if a.dtype == "fp32" else torch.bfloat16
+    model = model.to("cuda", dt).eval()
+    x = make_demo_input(cfg, device="cuda", dtype=dt, hw=demo_input_hw())
     stream = torch.cuda.Stream()
     tenant = GraphedTenant(model, stream, x)
     with torch.no_grad():
