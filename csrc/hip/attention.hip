@@ -184,24 +184,26 @@ __global__ __launch_bounds__(NT, 4) void attn_fwd_d64_kernel(
           oacc[1][i] *= alpha;
         }
       }
-      float psum = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kb][i], c, -m));
-          sacc[kb][i] = p;
-          psum += p;
-        }
-      l += psum;
-
+      // p = exp2(s*c - m): the scale-and-shift, the row-sum and the bf16
+      // conversion run as packed 2-wide ops (v_pk_fma_f32, v_pk_add_f32,
+      // v_cvt_pk_bf16_f32) -- only the exponentials stay one per score
+      const f32x2_t c2 = {c, c}, nm2 = {-m, -m};
+      f32x2_t ps2 = {0.f, 0.f};
       bf16x8_t pf[2][2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) pf[kb][s2][j] = (__bf16)sacc[kb][8 * s2 + j];
+        for (int j2 = 0; j2 < 8; ++j2) {
+          const f32x2_t sv = {sacc[kb][2 * j2], sacc[kb][2 * j2 + 1]};
+          f32x2_t x = sv * c2 + nm2;
+          x.x = __builtin_amdgcn_exp2f(x.x);
+          x.y = __builtin_amdgcn_exp2f(x.y);
+          ps2 += x;
+          const bf16x2_t pb = __builtin_convertvector(x, bf16x2_t);
+          pf[kb][j2 >> 2][2 * (j2 & 3)] = pb.x;
+          pf[kb][j2 >> 2][2 * (j2 & 3) + 1] = pb.y;
+        }
+      l += ps2.x + ps2.y;
 
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
