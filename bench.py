@@ -157,6 +157,7 @@ class UtilSampler:
 
     def __init__(self, hip_id: int, period_s: float = 0.02):
         self.samples: list[tuple[float, int]] = []
+        self.clocks: list[tuple[float, int]] = []
         self.err = None
         self._stop = threading.Event()
         self.period = period_s
@@ -174,17 +175,25 @@ class UtilSampler:
 
     def _run(self) -> None:
         nxt = time.monotonic()
+        k = 0
         while not self._stop.is_set():
             try:
                 self.samples.append((time.monotonic(), self.smi.activity(self.index)["gfx"]))
+                if k % 5 == 0:  # GFX clock at 10 Hz: tells DVFS apart from contention
+                    self.clocks.append((time.monotonic(), self.smi.clock(self.index)["sclk_mhz"]))
             except Exception as e:
                 self.err = repr(e)
+            k += 1
             nxt += self.period
             self._stop.wait(max(0.0, nxt - time.monotonic()))
 
     def mean(self, t0: float, t1: float) -> tuple[float | None, int]:
         v = [u for t, u in self.samples if t0 <= t <= t1]
         return (sum(v) / len(v) if v else None), len(v)
+
+    def mean_sclk(self, t0: float, t1: float) -> float | None:
+        v = [u for t, u in self.clocks if t0 <= t <= t1]
+        return round(sum(v) / len(v)) if v else None
 
     def close(self) -> None:
         self._stop.set()
@@ -218,6 +227,8 @@ def fleet_window(d: Dist, fleet, warmup: int, steps: int, step_s: float, sampler
     d.barrier_sync()
     t1 = time.monotonic()
     util = sampler.mean(t0, t1) if sampler else (None, 0)
+    if sampler:
+        fleet.sclk_mhz = sampler.mean_sclk(t0, t1)
     return t0, t1, util
 
 
@@ -234,6 +245,7 @@ def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, 
         t0, t1, (util, n_util) = fleet_window(d, fleet, warmup, steps, step_s, sampler, coll, coll_times)
         fleet.stop()
         w = fleet.window(t0, t1)
+        w.sclk_mhz = getattr(fleet, "sclk_mhz", None)
     finally:
         fleet.close()
     tr = None
@@ -343,6 +355,7 @@ def main(argv=None) -> int:
                    "pods_placed_per_node": int(placed)},
         "gpu_util_pct": None if util_mean is None else round(util_mean, 1),
         "gpu_util_samples": n_util,
+        "rank0_sclk_mhz": w.sclk_mhz,
         "schedulable_fractional_pods_per_node": value,
         "schedulable_fractional_pods_per_node_sim": cp.get("schedulable_fractional_pods_per_node"),
         "schedulable_10gb_pods_per_node_sim": cp10.get("schedulable_fractional_pods_per_node",

@@ -64,6 +64,7 @@ class PodResult:
 class WindowStats:
     window_s: float
     pods: list[PodResult]
+    sclk_mhz: float | None = None  # mean GFX clock over the window (amd-smi), when sampled
 
     @property
     def completed(self) -> float:
@@ -89,7 +90,7 @@ class WindowStats:
                 "mean_latency_s": None if self.mean_latency_s is None else round(self.mean_latency_s, 5),
                 "pod_latency_min_s": round(min(lat), 5) if lat else None,
                 "pod_latency_max_s": round(max(lat), 5) if lat else None,
-                "concurrent_pods": self.concurrent}
+                "concurrent_pods": self.concurrent, "sclk_mhz": self.sclk_mhz}
 
 
 class _RemoteProc:
