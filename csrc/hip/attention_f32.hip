@@ -53,15 +53,20 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_ba
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-template <int W, int KVB>
-__global__ __launch_bounds__(64 * W) void attn_fwd_f32_d64_kernel(
+// G = 2: two groups of W waves walk interleaved key tiles of the same
+// (batch, head, q-block) and merge (m, l, O) through LDS at the end -- two
+// waves per SIMD from ONE workgroup, so a single pod (162 q-blocks for 256
+// CUs) still overlaps one wave's softmax with the other's MFMAs.
+template <int W, int KVB, int G>
+__global__ __launch_bounds__(64 * W * G) void attn_fwd_f32_d64_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, float* __restrict__ o,
     int B, int H, int Sq, int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, int nqb) {
   constexpr int QBLK = 32 * W;
   constexpr int TILE = KVB * ROW_BYTES;          // bytes of K (or V) per stage
   constexpr int STAGE = 2 * TILE;
-  constexpr int PIECES = STAGE / 1024;           // 1 KiB per wave-wide LDS-DMA
+  constexpr int PIECES = STAGE / 1024;           // 1 KiB per wave-wide LDS-DMA, per group
   constexpr int PER_WAVE = PIECES / W;
+  constexpr int RING = G * STAGE;                // one stage of every group
   constexpr int NT32 = KVB / 32;                 // 32-key S^T tiles per stage
   static_assert(PIECES % W == 0, "stage pieces must split evenly over the waves");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -74,7 +79,9 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_f32_d64_kernel(
   const int qb = rem - hd * nqb;
 
   const int tid = threadIdx.x;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wall = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wall / W;                      // wave group (key tiles grp, grp + G, ...)
+  const int wid = wall - grp * W;                // wave within the group: its 32 query rows
   const int lane = tid & 63;
   const int h = lane >> 5, col = lane & 31;
 
@@ -98,6 +105,7 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_f32_d64_kernel(
 
   // piece p: tensor p / (PIECES/2) (K, V), 4 rows from (p % (PIECES/2)) * 4;
   // lane L writes row R + L/16, physical chunk L%16 = logical chunk ^ swizzle
+  // every group stages its own tile (G * it + grp) into its slot of the ring
   auto stage = [&](int it, int buf) {
 #pragma unroll
     for (int i = 0; i < PER_WAVE; ++i) {
@@ -107,14 +115,15 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_f32_d64_kernel(
       const int row = R + (lane >> 4);
       const int pc = lane & 15;
       const int lc = pc ^ (is_v ? vswz(row) : kswz(row));
-      int kv = it * KVB + row;
+      int kv = (G * it + grp) * KVB + row;
       kv = kv < Skv ? kv : Skv - 1;
       const float* src = (is_v ? vb_ptr : kb_ptr) + (long long)kv * ld_in + lc * 4;
-      glds16(src, smem + buf * STAGE + is_v * TILE + R * ROW_BYTES);
+      glds16(src, smem + buf * RING + grp * STAGE + is_v * TILE + R * ROW_BYTES);
     }
   };
 
   const int ntiles = (Skv + KVB - 1) / KVB;
+  const int niters = (ntiles + G - 1) / G;
   stage(0, 0);
 
   int koff[8];
@@ -134,71 +143,102 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_f32_d64_kernel(
 
   __syncthreads();  // stage 0 landed (vmcnt(0)) and is visible
 
-  for (int it = 0; it < ntiles; ++it) {
+  for (int it = 0; it < niters; ++it) {
     const int buf = it & 1;
-    if (it + 1 < ntiles) stage(it + 1, buf ^ 1);  // that buffer was released by the barrier ending it-1
-    const unsigned char* kl = smem + buf * STAGE;
-    const unsigned char* vl = kl + TILE;
+    if (it + 1 < niters) stage(it + 1, buf ^ 1);  // that buffer was released by the barrier ending it-1
+    const int tile = G * it + grp;                 // this group's key tile
+    if (tile < ntiles) {
+      const unsigned char* kl = smem + buf * RING + grp * STAGE;
+      const unsigned char* vl = kl + TILE;
 
-    f32x16_t s[NT32];
+      f32x16_t s[NT32];
 #pragma unroll
-    for (int t = 0; t < NT32; ++t) {
+      for (int t = 0; t < NT32; ++t) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s[t][i] = 0.f;
+        for (int i = 0; i < 16; ++i) s[t][i] = 0.f;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float4 kx = *reinterpret_cast<const float4*>(kl + t * 32 * ROW_BYTES + koff[u]);
-        s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.x, qf[4 * u + 0], s[t], 0, 0, 0);
-        s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.y, qf[4 * u + 1], s[t], 0, 0, 0);
-        s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.z, qf[4 * u + 2], s[t], 0, 0, 0);
-        s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.w, qf[4 * u + 3], s[t], 0, 0, 0);
+        for (int u = 0; u < 8; ++u) {
+          const float4 kx = *reinterpret_cast<const float4*>(kl + t * 32 * ROW_BYTES + koff[u]);
+          s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.x, qf[4 * u + 0], s[t], 0, 0, 0);
+          s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.y, qf[4 * u + 1], s[t], 0, 0, 0);
+          s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.z, qf[4 * u + 2], s[t], 0, 0, 0);
+          s[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kx.w, qf[4 * u + 3], s[t], 0, 0, 0);
+        }
       }
-    }
-    if ((it + 1) * KVB > Skv) {  // tail tile: keys past Skv never contribute
+      if ((tile + 1) * KVB > Skv) {  // tail tile: keys past Skv never contribute
+#pragma unroll
+        for (int t = 0; t < NT32; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (tile * KVB + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h >= Skv) s[t][i] = -INFINITY;
+      }
+      float mt = s[0][0];
 #pragma unroll
       for (int t = 0; t < NT32; ++t)
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (it * KVB + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h >= Skv) s[t][i] = -INFINITY;
+        for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[t][i]);
+      const float mrel = xor32_max(mt) - m;
+      if (it == 0 || !__all(mrel <= RESCALE_THR)) {  // the group's first tile sets the reference max
+        const float delta = it == 0 ? mrel : fmaxf(mrel, 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        m += delta;
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          oacc[0][i] *= alpha;
+          oacc[1][i] *= alpha;
+        }
+      }
+      float ps = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT32; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          s[t][i] = __builtin_amdgcn_exp2f(s[t][i] - m);
+          ps += s[t][i];
+        }
+      l += ps;
+      // O^T[d][i] += V^T[d][j] P^T[j][i]; step (t, r) sums keys 32t + {key(r,0), key(r,1)}
+#pragma unroll
+      for (int t = 0; t < NT32; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int roff = (32 * t + (r & 3) + 8 * (r >> 2)) * ROW_BYTES;
+          const float v0 = *reinterpret_cast<const float*>(vl + roff + voff[0]);
+          const float v1 = *reinterpret_cast<const float*>(vl + roff + voff[1]);
+          oacc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0, s[t][r], oacc[0], 0, 0, 0);
+          oacc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, s[t][r], oacc[1], 0, 0, 0);
+        }
     }
-    float mt = s[0][0];
-#pragma unroll
-    for (int t = 0; t < NT32; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[t][i]);
-    const float mrel = xor32_max(mt) - m;
-    if (it == 0 || !__all(mrel <= RESCALE_THR)) {
-      const float delta = it == 0 ? mrel : fmaxf(mrel, 0.f);
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-      m += delta;
-      l *= alpha;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        oacc[0][i] *= alpha;
-        oacc[1][i] *= alpha;
-      }
-    }
-    float ps = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT32; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        s[t][i] = __builtin_amdgcn_exp2f(s[t][i] - m);
-        ps += s[t][i];
-      }
-    l += ps;
-    // O^T[d][i] += V^T[d][j] P^T[j][i]; step (t, r) sums keys 32t + {key(r,0), key(r,1)}
-#pragma unroll
-    for (int t = 0; t < NT32; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int roff = (32 * t + (r & 3) + 8 * (r >> 2)) * ROW_BYTES;
-        const float v0 = *reinterpret_cast<const float*>(vl + roff + voff[0]);
-        const float v1 = *reinterpret_cast<const float*>(vl + roff + voff[1]);
-        oacc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0, s[t][r], oacc[0], 0, 0, 0);
-        oacc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, s[t][r], oacc[1], 0, 0, 0);
-      }
     __syncthreads();  // next stage landed; every wave is done with this buffer
+  }
+
+  float a0 = 1.f;
+  if constexpr (G == 2) {
+    // merge: group 1 hands (O, m, l) of every lane to group 0 through LDS (the ring is free now)
+    float* xch = reinterpret_cast<float*>(smem) + wid * (34 * 64);
+    if (grp == 1) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        xch[i * 64 + lane] = oacc[0][i];
+        xch[(16 + i) * 64 + lane] = oacc[1][i];
+      }
+      xch[32 * 64 + lane] = m;
+      xch[33 * 64 + lane] = l;
+    }
+    __syncthreads();
+    if (grp == 1) return;
+    const bool g1 = ntiles > 1;  // group 1 saw no tile when the sequence has one: its m means nothing
+    const float m1 = xch[32 * 64 + lane], l1 = xch[33 * 64 + lane];
+    const float mf = g1 ? fmaxf(m, m1) : m;
+    a0 = __builtin_amdgcn_exp2f(m - mf);
+    const float a1 = g1 ? __builtin_amdgcn_exp2f(m1 - mf) : 0.f;
+    l = l * a0 + l1 * a1;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      oacc[0][i] = oacc[0][i] * a0 + xch[i * 64 + lane] * a1;
+      oacc[1][i] = oacc[1][i] * a0 + xch[(16 + i) * 64 + lane] * a1;
+    }
   }
 
   const float inv = 1.f / xor32_sum(l);
@@ -219,19 +259,19 @@ __global__ __launch_bounds__(64 * W) void attn_fwd_f32_d64_kernel(
   }
 }
 
-template <int W, int KVB>
+template <int W, int KVB, int G>
 int launch(const float* q, const float* k, const float* v, float* o, int B, int H, int Sq, int Skv, int ld_in,
            long long bs_in, int ld_out, long long bs_out, float c, hipStream_t stream) {
   const int nqb = (Sq + 32 * W - 1) / (32 * W);
   const long long nwg = (long long)B * H * nqb;
   if (nwg > (1LL << 30)) return (int)hipErrorInvalidValue;
-  const size_t lds = 2 * 2 * KVB * ROW_BYTES;
-  hipLaunchKernelGGL((attn_fwd_f32_d64_kernel<W, KVB>), dim3((unsigned)nwg), dim3(64 * W), lds, stream, q, k, v, o,
-                     B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
+  const size_t lds = (size_t)G * 2 * 2 * KVB * ROW_BYTES;
+  hipLaunchKernelGGL((attn_fwd_f32_d64_kernel<W, KVB, G>), dim3((unsigned)nwg), dim3(64 * W * G), lds, stream, q,
+                     k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
   return (int)hipGetLastError();
 }
 
-int g_variant = 0;  // 0 auto, 1: 4 waves x 64-key tiles, 2: 2 waves x 32-key tiles
+int g_variant = 0;  // 0 auto, 1: 4 waves x 64-key tiles, 2: the same with 2 wave groups (split keys)
 
 }  // namespace
 
@@ -251,10 +291,11 @@ NOS_API int nos_attn_fwd_f32_d64(const float* q, const float* k, const float* v,
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) return (int)hipErrorInvalidValue;
   const float c = scale * 1.4426950408889634f;
-  // auto = 4 waves x 64-key tiles: measured faster at every batch, even when
-  // one pod's 162 workgroups leave CUs idle (B=1: 260 vs 482 us; B=8: 1345 vs
-  // 1679 us, profiles/r02_attention_f32.json)
-  const int var = g_variant == 0 ? 1 : g_variant;
-  if (var == 1) return launch<4, 64>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
-  return launch<2, 32>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
+  // auto: 2 wave groups when the grid leaves CUs without a workgroup (one pod
+  // at B=1: 162 workgroups, 237 vs 267 us), else 1 (B=8: 1357 vs 1399 us;
+  // profiles/r02_attention_f32.json)
+  const long long nwg = (long long)B * H * ((Sq + 127) / 128);
+  const int var = g_variant != 0 ? g_variant : nwg <= 256 ? 2 : 1;
+  if (var == 1) return launch<4, 64, 1>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
+  return launch<4, 64, 2>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
 }

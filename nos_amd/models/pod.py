@@ -133,6 +133,17 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             from ..ops import set_gemm_f32_policy
 
             set_gemm_f32_policy(os.environ["NOS_AMD_GEMM_F32_POLICY"])
+        if gpu and os.environ.get("NOS_AMD_ATTN_F32_VARIANT"):  # A/B of the fp32 attention tiling
+            from ..ops import set_attention_f32_variant
+
+            set_attention_f32_variant(os.environ["NOS_AMD_ATTN_F32_VARIANT"])
+        elif gpu and frac is not None and frac < 0.99:
+            # a fractional slice shares the CUs with other pods: one wave group per
+            # workgroup (the 2-group tiling only pays when this pod alone leaves CUs
+            # idle; 8 pods x 36 GB: 311 vs 302 inf/s, profiles/r02_attention_f32.json)
+            from ..ops import set_attention_f32_variant
+
+            set_attention_f32_variant("w4k64")
         m, x = _build(dtype, seed, demo_input_hw(), device)
         if gpu:
             s = torch.cuda.Stream()

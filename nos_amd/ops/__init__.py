@@ -143,9 +143,10 @@ def set_gemm_f32_policy(policy: str) -> None:
 
 def set_attention_f32_variant(variant: str) -> None:
     """fp32 attention tiling: ``"auto"`` (default), ``"w4k64"`` (4 waves x 64-key
-    LDS tiles, best when the grid fills the chip) or ``"w2k32"`` (2 waves x
-    32-key tiles: twice the workgroups, for one small pod)."""
-    code = {"auto": 0, "w4k64": 1, "w2k32": 2}[variant]
+    LDS tiles) or ``"w4k64g2"`` (two such wave groups per workgroup on
+    interleaved key tiles, merged at the end: 2 waves per SIMD from one
+    workgroup)."""
+    code = {"auto": 0, "w4k64": 1, "w4k64g2": 2}[variant]
     _lib.check(_lib.lib().nos_attn_f32_set_variant(code), "nos_attn_f32_set_variant")
 
 
