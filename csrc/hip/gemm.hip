@@ -55,9 +55,26 @@ enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
 //    pods lose ~4 % aggregate throughput with narrow tiles);
 //  * 1 = latency: when a GEMM has fewer 128x128 tiles than NARROW_TILES, use
 //    128x64 tiles to occupy twice the CUs (single tenant: N = 384 projections
-//    -24 %, FC2 -23 % kernel time).
+//    -24 %, FC2 -23 % kernel time);
+//  * 2 = narrow: always 128x64 (A/B only).
 constexpr int NARROW_TILES = 200;
 int g_tile_policy = 0;
+// persistent grid: 0 = one workgroup per tile, n > 0 = at most n workgroups
+// per CU, each running several tiles with the next tile's loads in flight
+// during the current epilogue (nos_gemm_set_persistent)
+int g_persist = 0;
+
+int num_cus() {
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
@@ -97,6 +114,26 @@ __device__ __forceinline__ float erf_fast(float x) {
 }
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
+
+// the same GELU on a register pair: the polynomial runs as packed-f32 FMAs
+// (v_pk_fma_f32 / v_pk_mul_f32, two columns per VALU op); rcp and exp stay
+// per element on the transcendental unit
+__device__ __forceinline__ f32x2_t gelu_erf2(f32x2_t x) {
+  const f32x2_t z = x * 0.70710678118654752f;
+  const f32x2_t az = {fabsf(z[0]), fabsf(z[1])};
+  const f32x2_t d = az * 0.3275911f + 1.f;
+  const f32x2_t t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f32x2_t p = t * 1.061405429f - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  const f32x2_t q = az * az * -1.4426950408889634f;
+  const f32x2_t e = {__builtin_amdgcn_exp2f(q[0]), __builtin_amdgcn_exp2f(q[1])};
+  const f32x2_t r = 1.f - p * t * e;  // erf(|z|)
+  const f32x2_t er = {copysignf(r[0], z[0]), copysignf(r[1], z[1])};
+  const f32x2_t hx = x * 0.5f;
+  return hx * er + hx;
+}
 
 // ---------------------------------------------------------------------------
 // Register epilogue.  The MFMA operands are swapped (D = W_frag . A_frag), so
@@ -168,16 +205,18 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[MI][Cfg<BN>:
           const float4 p2b = *reinterpret_cast<const float4*>(s_p2 + cl + 4);
           const float p1[8] = {p1a.x, p1a.y, p1a.z, p1a.w, p1b.x, p1b.y, p1b.z, p1b.w};
           const float p2[8] = {p2a.x, p2a.y, p2a.z, p2a.w, p2b.x, p2b.y, p2b.z, p2b.w};
-          if (LN) {
+          // LN correction / bias and activation on column pairs (packed f32)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaf(rs, v[e] - mu * p1[e], p2[e]);
-          } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += p2[e];
-          }
-          if (epi & EPI_GELU) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+          for (int e = 0; e < 8; e += 2) {
+            f32x2_t w = {v[e], v[e + 1]};
+            const f32x2_t q1 = {p1[e], p1[e + 1]}, q2 = {p2[e], p2[e + 1]};
+            if (LN)
+              w = (w - q1 * mu) * rs + q2;
+            else
+              w = w + q2;
+            if (epi & EPI_GELU) w = gelu_erf2(w);
+            v[e] = w[0];
+            v[e + 1] = w[1];
           }
           if (epi & EPI_RELU) {
 #pragma unroll
@@ -216,11 +255,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
   constexpr int STAGE_BYTES = CF::STAGE_BYTES;
   constexpr int WN = CF::WN, NB = CF::NB;
   constexpr int STATS_OFF = 2 * STAGE_BYTES;
+  constexpr int LOADS_PER_STAGE = BM / 32 + BN / 32;  // global_load_lds per wave per stage
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* s_mu = reinterpret_cast<float*>(smem + STATS_OFF);
   float* s_rstd = s_mu + BM;
-  float* s_p1 = s_rstd + BM;
-  float* s_p2 = s_p1 + BN;
+  float* s_par = s_rstd + BM;  // [2 tile parities][p1 BN | p2 BN]
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int r = lane & 31, hh = lane >> 5;
   const int wm = wid >> 1, wn = wid & 1;
@@ -228,18 +267,64 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
   const int nk = K / BK;
   const bool vec_ok = ((ldc | ldr) & 7) == 0;
 
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int tt = (gridDim.x >= ntiles) ? nos::xcd_remap(tile, ntiles) : tile;
+  // Tile order.  The dispatcher deals workgroup b to XCD b % 8; every XCD
+  // owns one contiguous chunk of the tile range (tiles sharing an A row panel
+  // share its L2) and its workgroups walk that chunk with a stride of the
+  // XCD's workgroup count.  With one workgroup per tile this is xcd_remap;
+  // with a smaller (persistent) grid each workgroup runs several tiles and
+  // issues the next tile's first two K-steps before the current epilogue, so
+  // their latency hides under the epilogue's math and stores.
+  const int G = gridDim.x, xcd = blockIdx.x % 8, j = blockIdx.x / 8;
+  const int wgs_x = G / 8 + (xcd < G % 8 ? 1 : 0);
+  const int t_lo = xcd * (ntiles / 8) + min(xcd, ntiles % 8);
+  const int t_cnt = ntiles / 8 + (xcd < ntiles % 8 ? 1 : 0);
+  if (j >= t_cnt) return;
+
+  auto coords = [&](int t, int& m0, int& n0) {
     int tm, tn;
     if (tiles_m >= tiles_n) {
-      tm = tt / tiles_n;
-      tn = tt - tm * tiles_n;
+      tm = t / tiles_n;
+      tn = t - tm * tiles_n;
     } else {
-      tn = tt / tiles_m;
-      tm = tt - tn * tiles_m;
+      tn = t / tiles_m;
+      tm = t - tn * tiles_m;
     }
-    const int m0 = tm * BM, n0 = tn * BN;
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+  // per-column epilogue parameters: (c1, c2) for the LN-fused form, (0, bias)
+  // otherwise; double-buffered by tile parity (a slower wave may still be in
+  // the previous tile's epilogue)
+  auto params = [&](int n0, int par) {
+    if (tid < BN) {
+      const int n = min(n0 + tid, N - 1);
+      s_par[par * 2 * BN + tid] = LN ? c1[n] : 0.f;
+      s_par[par * 2 * BN + BN + tid] = LN ? c2[n] : ((epi & EPI_BIAS) ? nos::bf16_to_f32(bias[n]) : 0.f);
+    }
+  };
+  // the first two K-steps of a tile into the two ring buffers
+  auto prologue = [&](int m0, int n0) {
+    stage_tile<BM>(A, lda, m0, M, 0, smem, wid, lane);
+    stage_tile<BN>(W, ldw, n0, N, 0, smem + TILE_A_BYTES, wid, lane);
+    if (nk > 1) {
+      stage_tile<BM>(A, lda, m0, M, BK, smem + STAGE_BYTES, wid, lane);
+      stage_tile<BN>(W, ldw, n0, N, BK, smem + STAGE_BYTES + TILE_A_BYTES, wid, lane);
+    }
+  };
 
+  int tile = t_lo + j, m0, n0, par = 0;
+  coords(tile, m0, n0);
+  // params are loaded before any LDS-DMA is in flight, so waiting for them
+  // drains nothing; step 1's loads overlap step 0's wait
+  params(n0, 0);
+  prologue(m0, n0);
+  if (nk > 1)
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(LOADS_PER_STAGE) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // step 0 landed for every wave; params visible
+
+  for (int it = 1;; ++it) {
     f32x16_t acc[2][NB];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -250,27 +335,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
 
     const int srow = tid >> 1, shalf = tid & 1;
     float sshift = 0.f, ssum = 0.f, ssq = 0.f;
-
-    // per-column epilogue parameters: (c1, c2) for the LN-fused form, (0,
-    // bias) otherwise -- loaded before any LDS-DMA is in flight, so waiting
-    // for them drains nothing
-    if (tid < BN) {
-      const int n = min(n0 + tid, N - 1);
-      s_p1[tid] = LN ? c1[n] : 0.f;
-      s_p2[tid] = LN ? c2[n] : ((epi & EPI_BIAS) ? nos::bf16_to_f32(bias[n]) : 0.f);
-    }
-    // both stages of the first two K-steps are issued up front: step 1's
-    // loads overlap step 0's wait instead of starting after it
-    stage_tile<BM>(A, lda, m0, M, 0, smem, wid, lane);
-    stage_tile<BN>(W, ldw, n0, N, 0, smem + TILE_A_BYTES, wid, lane);
-    if (nk > 1) {
-      stage_tile<BM>(A, lda, m0, M, BK, smem + STAGE_BYTES, wid, lane);
-      stage_tile<BN>(W, ldw, n0, N, BK, smem + STAGE_BYTES + TILE_A_BYTES, wid, lane);
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(BM / 32 + BN / 32) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // step 0 landed for every wave; params visible
 
     for (int kt = 0; kt < nk; ++kt) {
       unsigned char* cur = smem + (kt & 1) * STAGE_BYTES;
@@ -319,6 +383,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
       }
     }
 
+    const int k_next = j + it * wgs_x;
+    const bool more = k_next < t_cnt;
+    int m1 = 0, n1 = 0;
+    if (more) {
+      coords(t_lo + k_next, m1, n1);
+      __syncthreads();  // every wave is done reading the ring: the next tile may overwrite it
+      prologue(m1, n1);
+    }
+
     if constexpr (LN) {
       const float sh_lo = __shfl(sshift, lane & ~1, 64);
       const float dlt = sshift - sh_lo;
@@ -336,16 +409,25 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
       __syncthreads();
     }
 
-    epilogue_rows<LN, BN, RESID>(acc, s_mu, s_rstd, s_p1, s_p2, R, ldr, C, ldc, M, N, m0, n0, epi, vec_ok, wm,
-                                 wn, r, hh);
-    // LDS (stages, stats, params) is rewritten by the next persistent tile; a
-    // workgroup's last tile ends without a barrier (it would drain the stores)
-    if (tile + (int)gridDim.x < ntiles) __syncthreads();
+    const float* s_p1 = s_par + par * 2 * BN;
+    epilogue_rows<LN, BN, RESID>(acc, s_mu, s_rstd, s_p1, s_p1 + BN, R, ldr, C, ldc, M, N, m0, n0, epi, vec_ok,
+                                 wm, wn, r, hh);
+    // a workgroup's last tile ends without a barrier (it would drain the stores)
+    if (!more) break;
+    par ^= 1;
+    params(n1, par);
+    m0 = m1;
+    n0 = n1;
+    // the next tile's steps 0/1 were issued before the epilogue; its stores and
+    // residual loads share vmcnt, so wait for everything (step 0 has long landed)
+    // and make the parameters (and, for LN, the consumed s_mu) safe to reuse
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 }
 
 template <int BNV>
-constexpr int rk_lds_bytes() { return 2 * Cfg<BNV>::STAGE_BYTES + (2 * BM + 2 * BNV) * 4; }
+constexpr int rk_lds_bytes() { return 2 * Cfg<BNV>::STAGE_BYTES + (2 * BM + 4 * BNV) * 4; }
 
 int launch(const void* A, int lda, const void* W, int ldw, const void* bias, const float* c1,
            const float* c2, const void* R, int ldr, void* C, int ldc, int M, int N, int K, int epi,
@@ -357,10 +439,11 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
   if ((epi & EPI_RESID) && !R) return (int)hipErrorInvalidValue;
   const int tiles_m = (M + BM - 1) / BM;
   // fewer 128-wide tiles than CUs (e.g. N = 384 projections): halve the N tile
-  const bool narrow = g_tile_policy == 1 && tiles_m * ((N + 127) / 128) < NARROW_TILES;
+  const bool narrow = g_tile_policy == 2 || (g_tile_policy == 1 && tiles_m * ((N + 127) / 128) < NARROW_TILES);
   const int bn = narrow ? 64 : 128;
   const int tiles_n = (N + bn - 1) / bn;
   int nwg = tiles_m * tiles_n;
+  if (max_wg <= 0 && g_persist > 0) max_wg = g_persist * num_cus();
   if (max_wg > 0 && nwg > max_wg) nwg = max_wg;
   auto Ap = (const unsigned short*)A;
   auto Wp = (const unsigned short*)W;
@@ -391,8 +474,14 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
 // R/C [M,N] (ldr/ldc), all bf16.  K must be a multiple of 64 and every row
 // start 16-byte aligned.  max_wg > 0 caps the grid (persistent mode).
 NOS_API int nos_gemm_set_policy(int policy) {
-  if (policy != 0 && policy != 1) return (int)hipErrorInvalidValue;
+  if (policy < 0 || policy > 2) return (int)hipErrorInvalidValue;
   g_tile_policy = policy;
+  return 0;
+}
+
+NOS_API int nos_gemm_set_persistent(int wgs_per_cu) {
+  if (wgs_per_cu < 0 || wgs_per_cu > 8) return (int)hipErrorInvalidValue;
+  g_persist = wgs_per_cu;
   return 0;
 }
 

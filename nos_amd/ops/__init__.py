@@ -129,8 +129,15 @@ def set_gemm_policy(policy: str) -> None:
     """``"throughput"`` (default: 128x128 tiles, best when pods share a GPU) or
     ``"latency"`` (128x64 tiles for GEMMs with fewer tiles than CUs, best for
     a single tenant owning the GPU)."""
-    code = {"throughput": 0, "latency": 1}[policy]
+    code = {"throughput": 0, "latency": 1, "narrow": 2}[policy]
     _lib.check(_lib.lib().nos_gemm_set_policy(code), "nos_gemm_set_policy")
+
+
+def set_gemm_persistent(wgs_per_cu: int) -> None:
+    """bf16 GEMM grid: 0 = one workgroup per tile; n > 0 = at most n
+    workgroups per CU, each walking several tiles of its XCD's chunk and
+    loading the next tile while it runs the current epilogue."""
+    _lib.check(_lib.lib().nos_gemm_set_persistent(int(wgs_per_cu)), "nos_gemm_set_persistent")
 
 
 def set_gemm_f32_policy(policy: str) -> None:
@@ -306,5 +313,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_gemm_policy", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

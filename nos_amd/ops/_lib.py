@@ -35,6 +35,7 @@ _SIGS = {
     "nos_gemm_ln_f32": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                         c_int, c_float, c_void_p],
     "nos_gemm_set_policy": [c_int],
+    "nos_gemm_set_persistent": [c_int],
     "nos_gemm_f32_set_policy": [c_int],
     "nos_attn_f32_set_variant": [c_int],
     "nos_gemm_ln_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,

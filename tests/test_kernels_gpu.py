@@ -66,6 +66,37 @@ def test_linear_layernorm_fused(M, N, K, act, policy):
     assert _rel(y, ref) < 2e-2
 
 
+@pytest.mark.parametrize("M,N,K,act,resid,ln", [
+    (3401, 1152, 384, None, False, True), (3401, 1536, 384, "gelu", False, True), (3401, 384, 1536, None, True, False),
+    (257, 200, 128, "relu", False, False), (1000, 384, 64, None, True, False), (77, 100, 128, None, False, True)])
+@pytest.mark.parametrize("persist", [1, 2, 13])
+def test_linear_persistent_grid(M, N, K, act, resid, ln, persist):
+    """Persistent bf16 GEMM grid: every workgroup walks several tiles of its
+    XCD's chunk with the next tile's loads in flight during the epilogue.
+    persist = 13 is an explicit grid of 13 workgroups (uneven over the XCDs)."""
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 2 + 0.5
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * 0.05
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(M, N, device=DEV, dtype=torch.bfloat16) if resid else None
+    max_wg = persist if persist > 8 else 0
+    if persist <= 8:
+        ops.set_gemm_persistent(persist)
+    try:
+        if ln:
+            g = torch.randn(K, device=DEV, dtype=torch.bfloat16)
+            be = torch.randn(K, device=DEV, dtype=torch.bfloat16)
+            wg, c1, c2 = ops.fold_layernorm(w, b, g, be)
+            y = ops.linear_ln(x, wg, c1, c2, act=act, max_wg=max_wg)
+            xin = torch.nn.functional.layer_norm(x.float().cpu(), (K,), g.float().cpu(), be.float().cpu(), 1e-12)
+        else:
+            y = ops.linear(x, w, b, act=act, residual=r, max_wg=max_wg)
+            xin = x.cpu().float()
+    finally:
+        ops.set_gemm_persistent(0)
+    ref = ops.linear_ref(xin, w.cpu().float(), b.cpu().float(), act=act, residual=r.cpu().float() if resid else None)
+    assert _rel(y, ref) < 2e-2
+
+
 @pytest.mark.parametrize("B,S,H", [(1, 3401, 6), (2, 200, 2), (1, 64, 1), (1, 1000, 3), (1, 65, 2), (1, 1, 1),
                                    (3, 129, 4)])
 def test_attention(B, S, H):

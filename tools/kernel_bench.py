@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds per impl (median reported)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"], help="GEMM dtype")
+    ap.add_argument("--square", type=int, default=0, help="time one n x n x n GEMM instead of the YOLOS shapes")
+    ap.add_argument("--persist", default="0", help="comma list of bf16 GEMM persistent grids (workgroups/CU, 0 = off)")
     ap.add_argument("--policies", default="latency", help="comma list of GEMM tile policies to A/B "
                     "(throughput, latency)")
     a = ap.parse_args()
@@ -73,14 +75,18 @@ def main():
         M = B * S
         gdt = torch.float32 if a.dtype == "fp32" else torch.bfloat16
         torch.backends.cuda.matmul.allow_tf32 = False
-        for name, (N, K, act, ln, resid) in {
+        shapes = {
             "qkv_ln": (3 * hid, hid, None, True, False),
             "fc1_ln_gelu": (mlp, hid, "gelu", True, False),
             "fc1_ln_noact": (mlp, hid, None, True, False),
             "proj_resid": (hid, hid, None, False, True),
             "fc2_resid": (hid, mlp, None, False, True),
             "qkv_plain": (3 * hid, hid, None, False, False),
-        }.items():
+        }
+        if a.square:
+            shapes = {f"square{a.square}": (a.square, a.square, None, False, False)}
+        for name, (N, K, act, ln, resid) in shapes.items():
+            M = a.square or B * S
             xa = torch.randn(M, K, device="cuda", dtype=gdt)
             w = torch.randn(N, K, device="cuda", dtype=gdt) * 0.05
             b = torch.randn(N, device="cuda", dtype=gdt)
@@ -93,20 +99,22 @@ def main():
                 fn = lambda: ops.linear_ln(xa, wg, c1, c2, act=act, out=outg)  # noqa: E731
             else:
                 fn = lambda: ops.linear(xa, w, b, act=act, residual=r if resid else None, out=outg)  # noqa: E731
-            impls = [("register", po) for po in a.policies.split(",")]
+            impls = [(int(pe), po) for pe in a.persist.split(",") for po in a.policies.split(",")]
             times = {im: [] for im in impls}
             for _ in range(a.rounds):
-                for im, po in impls:
+                for pe, po in impls:
                     if a.dtype == "fp32":
                         ops.set_gemm_f32_policy(po)
                     else:
                         ops.set_gemm_policy(po)
-                    times[(im, po)].append(timeit(fn, a.iters))
+                        ops.set_gemm_persistent(pe)
+                    times[(pe, po)].append(timeit(fn, a.iters))
             ops.set_gemm_policy("throughput")
+            ops.set_gemm_persistent(0)
             ops.set_gemm_f32_policy("latency")
             for im in impls:
                 t = sorted(times[im])[len(times[im]) // 2]
-                sfx = "" if im == impls[0] else f"_{im[0]}_{im[1]}"
+                sfx = "" if im == impls[0] else f"_p{im[0]}_{im[1]}"
                 res[f"{name}{sfx}_us"] = t
                 res[f"{name}{sfx}_tflops"] = 2 * M * N * K / t / 1e6
             tus = timeit(lambda: torch.nn.functional.linear(xa, w, b), a.iters)
