@@ -9,14 +9,17 @@
 //
 // CDNA4 design:
 //  * 256-thread workgroup (4 waves as 2x2), output tile 128x128, each wave
-//    64x64 = 2x2 blocks of v_mfma_f32_32x32x16_bf16, BK = 64;
+//    64x64 = 2x2 blocks of v_mfma_f32_32x32x16_bf16, BK = 64; 128x64 for
+//    small-N GEMMs, 256x256 / 8 waves (128x64 wave tiles) for long-K GEMMs
+//    that fill the chip (the Cfg template below);
 //  * both operands are K-contiguous, so both are staged the same way: direct
 //    global->LDS DMA (global_load_lds_dwordx4, 1 KiB = 8 rows per wave
 //    instruction) into a lane-linear image; the XOR swizzle that makes the
 //    ds_read_b128 fragment reads conflict-free is applied to the per-lane
 //    SOURCE address (linear destination + inverse-swizzled source + swizzled
 //    read, cdna_hip_programming.md rule 21);
-//  * two LDS buffers: tile k+1 is in flight while tile k is consumed;
+//  * two LDS buffers: tile k+1 is in flight while tile k is consumed (a
+//    4-deep ring of BK = 32 slices measured slower: twice the barriers);
 //  * LayerNorm fusion without a normalised copy of A: with W' = W * gamma
 //    (per-k column scale, precomputed), c1[n] = sum_k W'[n,k],
 //    c2[n] = sum_k W[n,k] beta[k] + bias[n]:
@@ -26,7 +29,8 @@
 //    K loop covers the whole row because K == hidden);
 //  * register epilogue: swapped MFMA operands + v_permlane32_swap give each
 //    lane 8 consecutive columns of one row; bias / LN correction / GELU /
-//    residual are applied in registers and stored as 16-byte row chunks;
+//    residual are applied in registers (packed-f32 pairs) and stored as
+//    16-byte row chunks;
 //  * optional persistent mode (grid smaller than the tile count) and an
 //    XCD-aware tile order so tiles sharing the larger operand panel share an
 //    XCD's L2.
@@ -34,19 +38,43 @@
 
 namespace {
 
-constexpr int BM = 128, BK = 64;
-constexpr int NT = 256;
-constexpr int TILE_A_BYTES = BM * BK * 2;  // 16 KiB
-
-// BN (128 or 64) is a template parameter: N = 384 projections have only 81
-// 128x128 tiles for 256 CUs, 162 with 128x64 tiles.
-template <int BN>
-struct Cfg {
-  static constexpr int TILE_B_BYTES = BN * BK * 2;
-  static constexpr int STAGE_BYTES = TILE_A_BYTES + TILE_B_BYTES;
-  static constexpr int WN = BN / 2;                    // wave tile: 64 x WN (2x2 waves)
-  static constexpr int NB = WN / 32;                   // 32-column MFMA blocks per wave
+// LDS image of a [rows][BK] bf16 K-slice: RB-byte rows of CPR 16-byte chunks,
+// RPI rows per 1 KiB wave-instruction.  Chunk c of row r sits at chunk
+// c ^ swz(r): the 16 lanes of every ds_read_b128 lane group (rows r..r+31 of
+// one chunk) then hit 16 distinct 4-bank groups.
+template <int BK>
+struct Lay {
+  static constexpr int RB = 2 * BK, CPR = BK / 8, RPI = 64 / CPR;
+  static constexpr int SH = RB == 128 ? 1 : 2;  // rows per 256-byte bank wrap: 2 or 4
+  __device__ static __forceinline__ int swz(int row) { return (row >> SH) & (CPR - 1); }
 };
+
+// Workgroup tile BM x BN over WGM x WGN waves (wave tile WM x WN, MI x NB
+// blocks of 32x32), K-slices of BK in an S-deep LDS-DMA ring.  128x128 / 4
+// waves is the base; 128x64 doubles the tile count for small N; 256x256 / 8
+// waves (128x64 wave tiles) halves the L2->LDS bytes per FLOP of the base
+// tile (a 128x128 tile at the MFMA peak would need the whole L2 bandwidth)
+// and reads 0.75 instead of 1 LDS fragment per MFMA.
+template <int BM_, int BN_, int WGM_, int WGN_, int BK_ = 64, int S_ = 2>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, BK = BK_, S = S_;
+  using L = Lay<BK>;
+  static constexpr int NW = WGM * WGN, NT = 64 * NW;
+  static constexpr int WM = BM / WGM, WN = BN / WGN;
+  static constexpr int MI = WM / 32, NB = WN / 32;
+  static constexpr int TILE_A_BYTES = BM * L::RB;
+  static constexpr int TILE_B_BYTES = BN * L::RB;
+  static constexpr int STAGE_BYTES = TILE_A_BYTES + TILE_B_BYTES;
+  static constexpr int LOADS_PER_STAGE = (BM + BN) / (L::RPI * NW);  // global_load_lds per wave per stage
+  static constexpr int MINB = NT >= 512 ? 1 : 2;
+  static constexpr int LDS = S * STAGE_BYTES + (2 * BM + 4 * BN) * 4;
+  static_assert(NT == 2 * BM, "LayerNorm row statistics: two threads per row");
+  static_assert(BM % (L::RPI * NW) == 0 && BN % (L::RPI * NW) == 0, "staging: whole wave-instructions per wave");
+  static_assert(S >= 2 && S <= 4 && (S - 1) * LOADS_PER_STAGE < 64, "ring depth / vmcnt range");
+};
+using CfgBase = Cfg<128, 128, 2, 2>;
+using CfgNarrow = Cfg<128, 64, 2, 2>;
+using CfgBig = Cfg<256, 256, 2, 4>;
 
 enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
 // Tile policy (process-wide, nos_gemm_set_policy):
@@ -56,8 +84,11 @@ enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
 //  * 1 = latency: when a GEMM has fewer 128x128 tiles than NARROW_TILES, use
 //    128x64 tiles to occupy twice the CUs (single tenant: N = 384 projections
 //    -24 %, FC2 -23 % kernel time);
-//  * 2 = narrow: always 128x64 (A/B only).
+//  * 2 = narrow: always 128x64 (A/B only);
+//  * 3 = big: 256x256 tiles, 8 waves, whenever the GEMM has >= BIG_TILES of them
+//    (A/B; policies 0 and 1 pick them for long-K GEMMs that fill the chip).
 constexpr int NARROW_TILES = 200;
+constexpr int BIG_TILES = 1;
 int g_tile_policy = 0;
 // persistent grid: 0 = one workgroup per tile, n > 0 = at most n workgroups
 // per CU, each running several tiles with the next tile's loads in flight
@@ -76,27 +107,39 @@ int num_cus() {
   return cached[dev];
 }
 
-__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
-
 __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// Stage a [ROWS][64 k] bf16 tile: ROWS/8 wave-instructions, ROWS/32 per wave.
-template <int ROWS>
+// Stage a [ROWS][BK] bf16 K-slice: ROWS/RPI wave-instructions, spread over NW waves.
+template <int ROWS, int NW, int BK>
 __device__ __forceinline__ void stage_tile(const unsigned short* __restrict__ src, int ld, int row0,
                                            int nrows, int k0, unsigned char* tile, int wid, int lane) {
-  constexpr int PER_WAVE = ROWS / 32;
+  using L = Lay<BK>;
+  constexpr int PER_WAVE = ROWS / (L::RPI * NW);
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
-    const int R = (wid * PER_WAVE + i) * 8;
-    const int row = R + (lane >> 3);
-    const int pc = lane & 7;
-    const int lc = pc ^ swz(row);
+    const int R = (wid * PER_WAVE + i) * L::RPI;
+    const int row = R + lane / L::CPR;
+    const int pc = lane % L::CPR;
+    const int lc = pc ^ L::swz(row);
     int grow = row0 + row;
     grow = grow < nrows ? grow : nrows - 1;
-    glds16(src + (long long)grow * ld + k0 + lc * 8, tile + R * 128);
+    glds16(src + (long long)grow * ld + k0 + lc * 8, tile + R * L::RB);
   }
+}
+
+// s_waitcnt vmcnt(n * LPS) for a runtime n in [0, 3]: the immediate must be a constant
+template <int LPS>
+__device__ __forceinline__ void wait_stages(int n) {
+  if (n <= 0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (n == 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+  else if (n == 2)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPS) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LPS) : "memory");
 }
 
 // erf(x) for GELU: Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7, far below
@@ -146,13 +189,13 @@ __device__ __forceinline__ f32x2_t gelu_erf2(f32x2_t x) {
 // (MFMA operands swapped): lane (r, hh) owns row r, columns 8j + 4hh + {0..3}
 // of each 32x32 block; a v_permlane32_swap per register pair gives each lane
 // 8 consecutive columns of its row, stored as one 16-byte chunk.
-template <bool LN, int BN, bool RESID, int MI = 2>
-__device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[MI][Cfg<BN>::NB], const float* s_mu,
+template <bool LN, class CF, bool RESID>
+__device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[CF::MI][CF::NB], const float* s_mu,
                                               const float* s_rstd, const float* s_p1, const float* s_p2,
                                               const unsigned short* __restrict__ R, int ldr,
                                               unsigned short* __restrict__ C, int ldc, int M, int N, int m0,
                                               int n0, int epi, bool vec_ok, int wm, int wn, int r, int hh) {
-  constexpr int WN = Cfg<BN>::WN, NB = Cfg<BN>::NB;
+  constexpr int WN = CF::WN, NB = CF::NB, MI = CF::MI, WM = CF::WM;
   // residual rows: all 16-byte loads issued up front (clamped addresses, no
   // per-element branches) so their latencies overlap instead of one round
   // trip per chunk
@@ -162,7 +205,7 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[MI][Cfg<BN>:
       const int nmax = ((N - 8) >> 3) << 3;
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) {
-        const int m = min(m0 + wm * (32 * MI) + mi * 32 + r, M - 1);
+        const int m = min(m0 + wm * WM + mi * 32 + r, M - 1);
 #pragma unroll
         for (int ni = 0; ni < NB; ++ni)
 #pragma unroll
@@ -175,7 +218,7 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[MI][Cfg<BN>:
   }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
-      const int rl = wm * (32 * MI) + mi * 32 + r;
+      const int rl = wm * WM + mi * 32 + r;
       const int m = m0 + rl;
       float mu = 0.f, rs = 1.f;
       if constexpr (LN) {
@@ -245,24 +288,25 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[MI][Cfg<BN>:
     }
 }
 
-template <bool LN, int BN, bool RESID>
-__global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
+template <bool LN, class CF, bool RESID>
+__global__ __launch_bounds__(CF::NT, CF::MINB) void gemm_bf16_rk_kernel(
     const unsigned short* __restrict__ A, int lda, const unsigned short* __restrict__ W, int ldw,
     const unsigned short* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
     const unsigned short* __restrict__ R, int ldr, unsigned short* __restrict__ C, int ldc, int M, int N,
     int K, int epi, float eps, int tiles_m, int tiles_n) {
-  using CF = Cfg<BN>;
-  constexpr int STAGE_BYTES = CF::STAGE_BYTES;
-  constexpr int WN = CF::WN, NB = CF::NB;
-  constexpr int STATS_OFF = 2 * STAGE_BYTES;
-  constexpr int LOADS_PER_STAGE = BM / 32 + BN / 32;  // global_load_lds per wave per stage
+  using L = typename CF::L;
+  constexpr int BM = CF::BM, BN = CF::BN, NW = CF::NW, WGN = CF::WGN, BK = CF::BK, S = CF::S;
+  constexpr int STAGE_BYTES = CF::STAGE_BYTES, TILE_A_BYTES = CF::TILE_A_BYTES;
+  constexpr int WM = CF::WM, WN = CF::WN, MI = CF::MI, NB = CF::NB;
+  constexpr int STATS_OFF = S * STAGE_BYTES;
+  constexpr int LPS = CF::LOADS_PER_STAGE;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* s_mu = reinterpret_cast<float*>(smem + STATS_OFF);
   float* s_rstd = s_mu + BM;
   float* s_par = s_rstd + BM;  // [2 tile parities][p1 BN | p2 BN]
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int r = lane & 31, hh = lane >> 5;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WGN, wn = wid - wm * WGN;
   const int ntiles = tiles_m * tiles_n;
   const int nk = K / BK;
   const bool vec_ok = ((ldc | ldr) & 7) == 0;
@@ -272,7 +316,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
   // share its L2) and its workgroups walk that chunk with a stride of the
   // XCD's workgroup count.  With one workgroup per tile this is xcd_remap;
   // with a smaller (persistent) grid each workgroup runs several tiles and
-  // issues the next tile's first two K-steps before the current epilogue, so
+  // issues the next tile's first K-slices before the current epilogue, so
   // their latency hides under the epilogue's math and stores.
   const int G = gridDim.x, xcd = blockIdx.x % 8, j = blockIdx.x / 8;
   const int wgs_x = G / 8 + (xcd < G % 8 ? 1 : 0);
@@ -302,32 +346,29 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
       s_par[par * 2 * BN + BN + tid] = LN ? c2[n] : ((epi & EPI_BIAS) ? nos::bf16_to_f32(bias[n]) : 0.f);
     }
   };
-  // the first two K-steps of a tile into the two ring buffers
+  auto stage = [&](int m0, int n0, int kt) {
+    unsigned char* buf = smem + (kt % S) * STAGE_BYTES;
+    stage_tile<BM, NW, BK>(A, lda, m0, M, kt * BK, buf, wid, lane);
+    stage_tile<BN, NW, BK>(W, ldw, n0, N, kt * BK, buf + TILE_A_BYTES, wid, lane);
+  };
+  // the first S K-slices of a tile (the whole ring is free)
   auto prologue = [&](int m0, int n0) {
-    stage_tile<BM>(A, lda, m0, M, 0, smem, wid, lane);
-    stage_tile<BN>(W, ldw, n0, N, 0, smem + TILE_A_BYTES, wid, lane);
-    if (nk > 1) {
-      stage_tile<BM>(A, lda, m0, M, BK, smem + STAGE_BYTES, wid, lane);
-      stage_tile<BN>(W, ldw, n0, N, BK, smem + STAGE_BYTES + TILE_A_BYTES, wid, lane);
-    }
+#pragma unroll
+    for (int q = 0; q < S; ++q)
+      if (q < nk) stage(m0, n0, q);
   };
 
   int tile = t_lo + j, m0, n0, par = 0;
   coords(tile, m0, n0);
   // params are loaded before any LDS-DMA is in flight, so waiting for them
-  // drains nothing; step 1's loads overlap step 0's wait
+  // drains nothing
   params(n0, 0);
   prologue(m0, n0);
-  if (nk > 1)
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(LOADS_PER_STAGE) : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // step 0 landed for every wave; params visible
 
   for (int it = 1;; ++it) {
-    f32x16_t acc[2][NB];
+    f32x16_t acc[MI][NB];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < MI; ++a)
 #pragma unroll
       for (int b = 0; b < NB; ++b)
 #pragma unroll
@@ -337,22 +378,20 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
     float sshift = 0.f, ssum = 0.f, ssq = 0.f;
 
     for (int kt = 0; kt < nk; ++kt) {
-      unsigned char* cur = smem + (kt & 1) * STAGE_BYTES;
-      if (kt > 0) {
-        __syncthreads();  // step kt landed (vmcnt(0)); everyone done with step kt-1's buffer
-        if (kt + 1 < nk) {
-          unsigned char* nxt = smem + ((kt + 1) & 1) * STAGE_BYTES;
-          stage_tile<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wid, lane);
-          stage_tile<BN>(W, ldw, n0, N, (kt + 1) * BK, nxt + TILE_A_BYTES, wid, lane);
-        }
-      }
-      const unsigned char* ta = cur;
-      const unsigned char* tb = cur + TILE_A_BYTES;
+      // slice kt landed (the newer slices issued so far may stay in flight:
+      // S-1 of them after the prologue, S-2 later) and every wave is done
+      // with slice kt-1, whose buffer slice kt+S-1 reuses
+      wait_stages<LPS>(min(kt == 0 ? S - 1 : S - 2, nk - 1 - kt));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt > 0 && kt + S - 1 < nk) stage(m0, n0, kt + S - 1);
+      const unsigned char* ta = smem + (kt % S) * STAGE_BYTES;
+      const unsigned char* tb = ta + TILE_A_BYTES;
       if constexpr (LN) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int lc = shalf * 4 + c;
-          const s16x8_t v = *reinterpret_cast<const s16x8_t*>(ta + srow * 128 + ((lc ^ swz(srow)) << 4));
+        for (int c = 0; c < L::CPR / 2; ++c) {
+          const int lc = shalf * (L::CPR / 2) + c;
+          const s16x8_t v = *reinterpret_cast<const s16x8_t*>(ta + srow * L::RB + ((lc ^ L::swz(srow)) << 4));
           if (kt == 0 && c == 0) sshift = nos::bf16_to_f32((unsigned short)v[0]);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -364,19 +403,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
       }
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
-        bf16x8_t af[2], bf[NB];
+        bf16x8_t af[MI], bf[NB];
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-          const int row = wm * 64 + mi * 32 + r;
-          af[mi] = *reinterpret_cast<const bf16x8_t*>(ta + row * 128 + (((2 * ks + hh) ^ swz(row)) << 4));
+        for (int mi = 0; mi < MI; ++mi) {
+          const int row = wm * WM + mi * 32 + r;
+          af[mi] = *reinterpret_cast<const bf16x8_t*>(ta + row * L::RB + (((2 * ks + hh) ^ L::swz(row)) << 4));
         }
 #pragma unroll
         for (int ni = 0; ni < NB; ++ni) {
           const int row = wn * WN + ni * 32 + r;
-          bf[ni] = *reinterpret_cast<const bf16x8_t*>(tb + row * 128 + (((2 * ks + hh) ^ swz(row)) << 4));
+          bf[ni] = *reinterpret_cast<const bf16x8_t*>(tb + row * L::RB + (((2 * ks + hh) ^ L::swz(row)) << 4));
         }
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
+        for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
           for (int ni = 0; ni < NB; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[ni], af[mi], acc[mi][ni], 0, 0, 0);
@@ -393,6 +432,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
     }
 
     if constexpr (LN) {
+      // each thread saw half of its row's chunks: combine the two shifted sums
       const float sh_lo = __shfl(sshift, lane & ~1, 64);
       const float dlt = sshift - sh_lo;
       const float kh = (float)(K / 2);
@@ -410,7 +450,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
     }
 
     const float* s_p1 = s_par + par * 2 * BN;
-    epilogue_rows<LN, BN, RESID>(acc, s_mu, s_rstd, s_p1, s_p1 + BN, R, ldr, C, ldc, M, N, m0, n0, epi, vec_ok,
+    epilogue_rows<LN, CF, RESID>(acc, s_mu, s_rstd, s_p1, s_p1 + BN, R, ldr, C, ldc, M, N, m0, n0, epi, vec_ok,
                                  wm, wn, r, hh);
     // a workgroup's last tile ends without a barrier (it would drain the stores)
     if (!more) break;
@@ -418,30 +458,28 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_rk_kernel(
     params(n1, par);
     m0 = m1;
     n0 = n1;
-    // the next tile's steps 0/1 were issued before the epilogue; its stores and
-    // residual loads share vmcnt, so wait for everything (step 0 has long landed)
-    // and make the parameters (and, for LN, the consumed s_mu) safe to reuse
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    // the next tile's first slices were issued before the epilogue; its
+    // stores and residual loads share vmcnt, so drain everything here (the
+    // slices have long landed) -- the K loop's first barrier then publishes
+    // the parameters
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 }
 
-template <int BNV>
-constexpr int rk_lds_bytes() { return 2 * Cfg<BNV>::STAGE_BYTES + (2 * BM + 4 * BNV) * 4; }
+template <bool LNV, class CF, bool RV>
+void launch_cfg(int nwg, hipStream_t stream, const unsigned short* A, int lda, const unsigned short* W, int ldw,
+                const unsigned short* bias, const float* c1, const float* c2, const unsigned short* R, int ldr,
+                unsigned short* C, int ldc, int M, int N, int K, int epi, float eps, int tiles_m, int tiles_n) {
+  hipLaunchKernelGGL((gemm_bf16_rk_kernel<LNV, CF, RV>), dim3(nwg), dim3(CF::NT), CF::LDS, stream, A, lda, W, ldw,
+                     bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+}
 
-int launch(const void* A, int lda, const void* W, int ldw, const void* bias, const float* c1,
-           const float* c2, const void* R, int ldr, void* C, int ldc, int M, int N, int K, int epi,
-           float eps, int max_wg, bool ln, hipStream_t stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0) return (int)hipErrorInvalidValue;
-  if ((lda % 8) || (ldw % 8)) return (int)hipErrorInvalidValue;
-  if (!ln && (epi & EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
-  if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
-  if ((epi & EPI_RESID) && !R) return (int)hipErrorInvalidValue;
-  const int tiles_m = (M + BM - 1) / BM;
-  // fewer 128-wide tiles than CUs (e.g. N = 384 projections): halve the N tile
-  const bool narrow = g_tile_policy == 2 || (g_tile_policy == 1 && tiles_m * ((N + 127) / 128) < NARROW_TILES);
-  const int bn = narrow ? 64 : 128;
-  const int tiles_n = (N + bn - 1) / bn;
+template <class CF>
+int launch_tile(const void* A, int lda, const void* W, int ldw, const void* bias, const float* c1, const float* c2,
+                const void* R, int ldr, void* C, int ldc, int M, int N, int K, int epi, float eps, int max_wg,
+                bool ln, hipStream_t stream) {
+  const int tiles_m = (M + CF::BM - 1) / CF::BM;
+  const int tiles_n = (N + CF::BN - 1) / CF::BN;
   int nwg = tiles_m * tiles_n;
   if (max_wg <= 0 && g_persist > 0) max_wg = g_persist * num_cus();
   if (max_wg > 0 && nwg > max_wg) nwg = max_wg;
@@ -450,22 +488,40 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
   auto Bp = (const unsigned short*)bias;
   auto Rp = (const unsigned short*)R;
   auto Cp = (unsigned short*)C;
-#define NOS_GEMM_ARGS                                                                                     \
-  Ap, lda, Wp, ldw, Bp, c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps, tiles_m, tiles_n
-#define NOS_GEMM_LAUNCH(LNV, BNV, RV)                                                                      \
-  hipLaunchKernelGGL((gemm_bf16_rk_kernel<LNV, BNV, RV>), dim3(nwg), dim3(NT), rk_lds_bytes<BNV>(), stream,  \
-                     NOS_GEMM_ARGS)
-  const bool resid = (epi & EPI_RESID) != 0;
-  if (ln) {
-    if (narrow) NOS_GEMM_LAUNCH(true, 64, false); else NOS_GEMM_LAUNCH(true, 128, false);
-  } else if (resid) {
-    if (narrow) NOS_GEMM_LAUNCH(false, 64, true); else NOS_GEMM_LAUNCH(false, 128, true);
-  } else {
-    if (narrow) NOS_GEMM_LAUNCH(false, 64, false); else NOS_GEMM_LAUNCH(false, 128, false);
-  }
-#undef NOS_GEMM_ARGS
-#undef NOS_GEMM_LAUNCH
+  if (ln)
+    launch_cfg<true, CF, false>(nwg, stream, Ap, lda, Wp, ldw, Bp, c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps,
+                                tiles_m, tiles_n);
+  else if (epi & EPI_RESID)
+    launch_cfg<false, CF, true>(nwg, stream, Ap, lda, Wp, ldw, Bp, c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps,
+                                tiles_m, tiles_n);
+  else
+    launch_cfg<false, CF, false>(nwg, stream, Ap, lda, Wp, ldw, Bp, c1, c2, Rp, ldr, Cp, ldc, M, N, K, epi, eps,
+                                 tiles_m, tiles_n);
   return (int)hipGetLastError();
+}
+
+int launch(const void* A, int lda, const void* W, int ldw, const void* bias, const float* c1,
+           const float* c2, const void* R, int ldr, void* C, int ldc, int M, int N, int K, int epi,
+           float eps, int max_wg, bool ln, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || (K % 64) != 0) return (int)hipErrorInvalidValue;
+  if ((lda % 8) || (ldw % 8)) return (int)hipErrorInvalidValue;
+  if (!ln && (epi & EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
+  if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
+  if ((epi & EPI_RESID) && !R) return (int)hipErrorInvalidValue;
+  const int tiles_m = (M + 127) / 128;
+  // fewer 128-wide tiles than CUs (e.g. N = 384 projections): halve the N tile
+  const bool narrow = g_tile_policy == 2 || (g_tile_policy == 1 && tiles_m * ((N + 127) / 128) < NARROW_TILES);
+  // 256x256 tiles for long-K GEMMs that fill the chip with them and waste
+  // little of the last N tile (4096^3: 1080 vs 850 TF; the K = 384 / N = 384
+  // YOLOS projections stay on 128-wide tiles, measured faster there)
+  const int big_tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const bool big = g_tile_policy == 3 ? big_tiles >= BIG_TILES
+                 : g_tile_policy <= 1 && K >= 1024 && (N % 256 == 0 || N >= 2048) && big_tiles >= num_cus();
+#define NOS_GEMM_ARGS A, lda, W, ldw, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, max_wg, ln, stream
+  if (big) return launch_tile<CfgBig>(NOS_GEMM_ARGS);
+  if (narrow) return launch_tile<CfgNarrow>(NOS_GEMM_ARGS);
+  return launch_tile<CfgBase>(NOS_GEMM_ARGS);
+#undef NOS_GEMM_ARGS
 }
 
 }  // namespace
@@ -474,7 +530,7 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
 // R/C [M,N] (ldr/ldc), all bf16.  K must be a multiple of 64 and every row
 // start 16-byte aligned.  max_wg > 0 caps the grid (persistent mode).
 NOS_API int nos_gemm_set_policy(int policy) {
-  if (policy < 0 || policy > 2) return (int)hipErrorInvalidValue;
+  if (policy < 0 || policy > 3) return (int)hipErrorInvalidValue;
   g_tile_policy = policy;
   return 0;
 }

@@ -1,0 +1,47 @@
+"""A few GEMM launches per tile config for rocprofv3 PMC passes (tools/gpu/pmc_gemm.sh).
+
+Runs the 4096^3 GEMM and the batch-8 YOLOS fc2 (+residual) / fc1 (+LN +GELU)
+shapes with the base (128x128) and big (256x256) tile configs and torch
+(hipBLASLt); kernel names tell the configs apart (Cfg<BM,BN,...>, Cijk_*).
+"""
+from __future__ import annotations
+
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main() -> None:
+    import torch
+
+    from nos_amd import ops
+
+    torch.manual_seed(0)
+    dev = "cuda"
+    n = 4096
+    x = torch.randn(n, n, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(n, n, device=dev, dtype=torch.bfloat16) * 0.02
+    o = torch.empty(n, n, device=dev, dtype=torch.bfloat16)
+    for pol in ("throughput", "big"):
+        ops.set_gemm_policy(pol)
+        for _ in range(5):
+            ops.linear(x, w, out=o)
+    for _ in range(5):
+        torch.nn.functional.linear(x, w)
+    ops.set_gemm_policy("throughput")
+    M, hid, mlp = 8 * 3401, 384, 1536
+    h = torch.randn(M, mlp, device=dev, dtype=torch.bfloat16)
+    w2 = torch.randn(hid, mlp, device=dev, dtype=torch.bfloat16) * 0.02
+    b2 = torch.randn(hid, device=dev, dtype=torch.bfloat16)
+    r = torch.randn(M, hid, device=dev, dtype=torch.bfloat16)
+    o2 = torch.empty(M, hid, device=dev, dtype=torch.bfloat16)
+    for _ in range(5):
+        ops.linear(h, w2, b2, residual=r, out=o2)
+        torch.nn.functional.linear(h, w2, b2)
+    torch.cuda.synchronize()
+    print("ok")
+
+
+if __name__ == "__main__":
+    main()
