@@ -78,6 +78,11 @@ def parse_args(argv=None):
     ap.add_argument("--coll-bucket-mb", type=int, default=64)
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: rehearsal of the whole launch path without a GPU (tiny pods, gloo)")
+    ap.add_argument("--table", default="",
+                    help="also measure the reference demo's latency table: comma list of pod counts per GPU "
+                         "(e.g. 1,3,5,7), one aligned window per (mode, count); reported as latency_table")
+    ap.add_argument("--table-modes", default="shared,cumask")
+    ap.add_argument("--table-window-s", type=float, default=6.0)
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -276,6 +281,9 @@ def main(argv=None) -> int:
     if args.device == "cpu":
         extra_env["OMP_NUM_THREADS"] = "1"
     log(rank, f"control plane placed {cp.get('placed_pods')} pods; local envs {envs[:2]}...")
+    table_plans = [(mode, n, plan(args, world, local, args.slice_gb, n, mode)[0])
+                   for mode in args.table_modes.split(",") if args.table
+                   for n in map(int, args.table.split(","))]
 
     from nos_amd.podbench import PodLauncher
 
@@ -313,6 +321,15 @@ def main(argv=None) -> int:
                                     args.extra_bf16_s, sampler, coll)
         bf = {"inf_per_s": round(wb.throughput, 2), "mean_latency_s": wb.mean_latency_s,
               "concurrent_pods": wb.concurrent, "gpu_util_pct": ub}
+    table = []
+    for mode, n, tenvs in table_plans:  # the reference demo's latency-vs-pods rows (README.md:63-71)
+        wt, ut, _, _, _ = run_fleet(d, launcher, tenvs, args.dtype, not args.no_graphs, extra_env, 1, 1,
+                                    args.table_window_s, sampler, device=args.device)
+        table.append({"mode": mode, "pods": n, "concurrent": wt.concurrent, "inf_per_s": round(wt.throughput, 2),
+                      "mean_latency_s": wt.mean_latency_s, "gpu_util_pct": ut,
+                      "pods_over_latency": round(n / wt.mean_latency_s, 2) if wt.mean_latency_s else None,
+                      "cu_mask": (wt.pods[0].info.get("cu_mask") if wt.pods else None)})
+        log(rank, f"table {table[-1]}")
     if sampler:
         sampler.close()
     launcher.close()
@@ -375,6 +392,7 @@ def main(argv=None) -> int:
                                                  "rank0": tr, "bucket_mb": args.coll_bucket_mb,
                                                  "gemm_dim": args.coll_dim},
         "rank0_window": w.as_dict(),
+        "latency_table": table or None,
         "rank0_ref_pod": ref,
         "pods_ready_s": round(ready_s, 1),
         "control_plane": cp,

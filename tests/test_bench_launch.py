@@ -39,3 +39,20 @@ def test_torchrun_two_ranks_aggregate_one_json_line():
     assert d["trainer_pods"]["rank0"]["running"] and d["trainer_pods"]["per_node_allreduce_gb_per_s"] > 0
     assert d["ms_per_step"] == pytest.approx(400, rel=0.2)
     assert d["aggregate_inf_per_s"] > 0 and d["scaling"] == "weak"
+
+
+@pytest.mark.timeout(600)
+def test_latency_table_rows_are_self_consistent():
+    """bench.py --table: one aligned window per (mode, pods); pods / mean latency == throughput in every row."""
+    cmd = [sys.executable, "bench.py", "--device", "cpu", "--steps", "2", "--warmup", "1", "--step-s", "0.3",
+           "--ref-pod-s", "0", "--extra-bf16-s", "0", "--pods-per-gpu", "2", "--table", "1,3",
+           "--table-window-s", "0.8"]
+    r = subprocess.run(cmd, cwd=REPO, env={**os.environ, "OMP_NUM_THREADS": "1"}, capture_output=True, text=True,
+                       timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    rows = d["latency_table"]
+    assert [(t["mode"], t["pods"]) for t in rows] == [("shared", 1), ("shared", 3), ("cumask", 1), ("cumask", 3)]
+    for t in rows:
+        assert t["concurrent"] == t["pods"]
+        assert t["pods_over_latency"] == pytest.approx(t["inf_per_s"], rel=1e-3)
