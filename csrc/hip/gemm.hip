@@ -75,20 +75,16 @@ struct Cfg {
 using CfgBase = Cfg<128, 128, 2, 2>;
 using CfgNarrow = Cfg<128, 64, 2, 2>;
 using CfgBig = Cfg<256, 256, 2, 4>;
+using CfgWide = Cfg<256, 192, 4, 2>;  // N = 384 in two tiles, 256-row panels: one round on 256 CUs
 
 enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
-// Tile policy (process-wide, nos_gemm_set_policy):
-//  * 0 = throughput (default): always 128x128 tiles -- fewest bytes per FLOP;
-//    what fractional pods sharing a GPU want (measured: 8 co-running YOLOS
-//    pods lose ~4 % aggregate throughput with narrow tiles);
-//  * 1 = latency: when a GEMM has fewer 128x128 tiles than NARROW_TILES, use
-//    128x64 tiles to occupy twice the CUs (single tenant: N = 384 projections
-//    -24 %, FC2 -23 % kernel time);
-//  * 2 = narrow: always 128x64 (A/B only);
-//  * 3 = big: 256x256 tiles, 8 waves, whenever the GEMM has >= BIG_TILES of them
-//    (A/B; policies 0 and 1 pick them for long-K GEMMs that fill the chip).
-constexpr int NARROW_TILES = 200;
-constexpr int BIG_TILES = 1;
+// Tile policy (process-wide, nos_gemm_set_policy), see pick_tile():
+//  * 0 = throughput (default): least padded work over 128x128 / 256x192 /
+//    256x256 tiles -- what fractional pods sharing a GPU want (8 co-running
+//    YOLOS pods lose ~4 % aggregate throughput with 128x64 tiles);
+//  * 1 = latency: fewest rounds of tiles over the CUs, 128x64 included
+//    (single tenant: N = 384 projections at batch 1 -24 %, FC2 -23 %);
+//  * 2 / 3 / 4 = always 128x64 / 256x256 / 256x192 (A/B only).
 int g_tile_policy = 0;
 // persistent grid: 0 = one workgroup per tile, n > 0 = at most n workgroups
 // per CU, each running several tiles with the next tile's loads in flight
@@ -500,6 +496,44 @@ int launch_tile(const void* A, int lda, const void* W, int ldw, const void* bias
   return (int)hipGetLastError();
 }
 
+enum TileKind : int { T_BASE, T_NARROW, T_WIDE, T_BIG };
+
+// Tile choice by a cost model: (tiles or rounds of tiles) x tile area /
+// relative efficiency.  The efficiencies are measured per output element on
+// the batch-8 YOLOS shapes and 4096^3 (profiles/r02_gemm_bf16_tiles.json):
+// the 8-wave 256-row tiles read half the L2 bytes per FLOP and 0.75-0.83 LDS
+// fragments per MFMA; 128x64 reads 1.5.
+//  * latency policy: ceil(tiles / CUs) x area -- the rounds a single tenant waits;
+//  * throughput policy: tiles x area -- the work co-running pods share (and
+//    no 128x64, which costs them ~4 %);
+// the 512-thread tiles only when they occupy at least half the CUs (a few big
+// tiles would serialise one tenant on a handful of CUs).
+int pick_tile(int M, int N, int policy, int cus) {
+  if (policy == 2) return T_NARROW;
+  if (policy == 3) return T_BIG;
+  if (policy == 4) return T_WIDE;
+  struct Cand {
+    int kind, bm, bn;
+    double eff;
+  };
+  static constexpr Cand cands[] = {{T_BASE, 128, 128, 1.0}, {T_NARROW, 128, 64, 0.8}, {T_WIDE, 256, 192, 1.2},
+                                   {T_BIG, 256, 256, 1.25}};
+  int pick = T_BASE;
+  double best = 1e300;
+  for (const Cand& c : cands) {
+    if (policy == 0 && c.kind == T_NARROW) continue;
+    const long long tiles = (long long)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
+    if (c.bm == 256 && 2 * tiles < cus) continue;
+    const double per = (double)c.bm * c.bn / c.eff;
+    const double cost = policy == 1 ? (double)((tiles + cus - 1) / cus) * per : (double)tiles * per;
+    if (cost < best * 0.99) {  // ties keep the earlier (smaller) tile
+      best = cost;
+      pick = c.kind;
+    }
+  }
+  return pick;
+}
+
 int launch(const void* A, int lda, const void* W, int ldw, const void* bias, const float* c1,
            const float* c2, const void* R, int ldr, void* C, int ldc, int M, int N, int K, int epi,
            float eps, int max_wg, bool ln, hipStream_t stream) {
@@ -508,19 +542,13 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
   if (!ln && (epi & EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
   if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
   if ((epi & EPI_RESID) && !R) return (int)hipErrorInvalidValue;
-  const int tiles_m = (M + 127) / 128;
-  // fewer 128-wide tiles than CUs (e.g. N = 384 projections): halve the N tile
-  const bool narrow = g_tile_policy == 2 || (g_tile_policy == 1 && tiles_m * ((N + 127) / 128) < NARROW_TILES);
-  // 256x256 tiles for long-K GEMMs that fill the chip with them and waste
-  // little of the last N tile (4096^3: 1080 vs 850 TF; the K = 384 / N = 384
-  // YOLOS projections stay on 128-wide tiles, measured faster there)
-  const int big_tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  const bool big = g_tile_policy == 3 ? big_tiles >= BIG_TILES
-                 : g_tile_policy <= 1 && K >= 1024 && (N % 256 == 0 || N >= 2048) && big_tiles >= num_cus();
 #define NOS_GEMM_ARGS A, lda, W, ldw, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, max_wg, ln, stream
-  if (big) return launch_tile<CfgBig>(NOS_GEMM_ARGS);
-  if (narrow) return launch_tile<CfgNarrow>(NOS_GEMM_ARGS);
-  return launch_tile<CfgBase>(NOS_GEMM_ARGS);
+  switch (pick_tile(M, N, g_tile_policy, num_cus())) {
+    case T_NARROW: return launch_tile<CfgNarrow>(NOS_GEMM_ARGS);
+    case T_WIDE: return launch_tile<CfgWide>(NOS_GEMM_ARGS);
+    case T_BIG: return launch_tile<CfgBig>(NOS_GEMM_ARGS);
+    default: return launch_tile<CfgBase>(NOS_GEMM_ARGS);
+  }
 #undef NOS_GEMM_ARGS
 }
 
@@ -530,7 +558,7 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
 // R/C [M,N] (ldr/ldc), all bf16.  K must be a multiple of 64 and every row
 // start 16-byte aligned.  max_wg > 0 caps the grid (persistent mode).
 NOS_API int nos_gemm_set_policy(int policy) {
-  if (policy < 0 || policy > 3) return (int)hipErrorInvalidValue;
+  if (policy < 0 || policy > 4) return (int)hipErrorInvalidValue;
   g_tile_policy = policy;
   return 0;
 }

@@ -129,7 +129,7 @@ def set_gemm_policy(policy: str) -> None:
     """``"throughput"`` (default: 128x128 tiles, best when pods share a GPU) or
     ``"latency"`` (128x64 tiles for GEMMs with fewer tiles than CUs, best for
     a single tenant owning the GPU)."""
-    code = {"throughput": 0, "latency": 1, "narrow": 2, "big": 3}[policy]
+    code = {"throughput": 0, "latency": 1, "narrow": 2, "big": 3, "wide": 4}[policy]
     _lib.check(_lib.lib().nos_gemm_set_policy(code), "nos_gemm_set_policy")
 
 

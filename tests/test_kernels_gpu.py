@@ -33,7 +33,7 @@ def _native():
     (3401, 1152, 384, None, False), (3401, 1536, 384, "gelu", False), (3401, 384, 1536, None, True),
     (3401, 384, 384, None, True), (100, 4, 384, "relu", False), (257, 200, 128, None, False),
     (1, 8, 64, None, False), (4096, 4096, 1024, None, False)])
-@pytest.mark.parametrize("policy", ["throughput", "latency", "big"])
+@pytest.mark.parametrize("policy", ["throughput", "latency", "big", "wide"])
 def test_linear(M, N, K, act, resid, policy):
     ops.set_gemm_policy(policy)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
@@ -50,7 +50,7 @@ def test_linear(M, N, K, act, resid, policy):
 
 @pytest.mark.parametrize("M,N,K,act", [(3401, 1152, 384, None), (3401, 1536, 384, "gelu"), (77, 100, 128, None),
                                        (1, 64, 64, None), (300, 384, 384, None)])
-@pytest.mark.parametrize("policy", ["throughput", "latency", "big"])
+@pytest.mark.parametrize("policy", ["throughput", "latency", "big", "wide"])
 def test_linear_layernorm_fused(M, N, K, act, policy):
     ops.set_gemm_policy(policy)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 2 + 0.5
