@@ -260,6 +260,8 @@ def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, 
         n_it = len(inside) - 2
         tr = {"iterations": n_it, "running": n_it > 0 and gap < 0.25 * (t1 - t0), "max_gap_s": round(gap, 3),
               "gemm_tflops": round(n_it * coll.flops_per_step() / (t1 - t0) / 1e12, 2),
+              "buckets": len(coll.bucketer.buckets),
+              "buckets_launched_in_backward": coll.bucketer.launched_in_backward,
               "allreduce_gb_per_s": round(n_it * coll.bucket_bytes() / (t1 - t0) / 1e9, 2) if coll._dist() else 0.0}
     return w, util, n_util, ready_s, tr
 
@@ -390,7 +392,10 @@ def main(argv=None) -> int:
         "trainer_pods": None if tr is None else {"per_node_gemm_tflops": round(tr_tf, 2),
                                                  "per_node_allreduce_gb_per_s": round(tr_gbs, 2),
                                                  "rank0": tr, "bucket_mb": args.coll_bucket_mb,
-                                                 "gemm_dim": args.coll_dim},
+                                                 "gemm_dim": args.coll_dim,
+                                                 "step": "bf16 MLP (4 x dim^2 layers, batch dim) forward + backward, "
+                                                         "bucketed all-reduce launched from the gradient hooks "
+                                                         "(overlaps backward), SGD"},
         "rank0_window": w.as_dict(),
         "latency_table": table or None,
         "rank0_ref_pod": ref,

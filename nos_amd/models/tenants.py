@@ -4,9 +4,11 @@
   GPU, each with its own weights, input, HIP graph and (optionally) CU-masked
   stream: the MI355X version of the reference demo's 7-pod deployment
   (``demos/gpu-sharing-comparison/README.md:41-60``).
-* :class:`CollectiveTenant` -- a data-parallel "trainer" pod: bf16 GEMMs plus a
-  bucketed RCCL all-reduce of its gradient buffer over xGMI, so slices are
-  measured under real collective traffic.
+* :class:`CollectiveTenant` -- a data-parallel "trainer" pod: forward +
+  backward of a bf16 MLP with its gradients averaged in 64 MiB buckets by RCCL
+  over xGMI, each bucket's all-reduce launched from the gradient hooks while
+  backward still runs (``parallel.collectives.GradBucketer``), then an SGD
+  step -- so slices are measured under real collective traffic.
 """
 from __future__ import annotations
 
@@ -81,26 +83,38 @@ class InferenceTenants:
 
 
 class CollectiveTenant:
-    """DP trainer pod: y = x @ W (GEMMs) then an all-reduce of a gradient
-    bucket (RCCL over xGMI on GPUs, gloo on the CPU rehearsal path); one per
-    rank/GPU.  Ranks run in LOCKSTEP: every iteration also all-reduces a stop
-    flag, so all ranks leave a time-bounded loop after the same iteration and
-    never issue mismatched collectives."""
+    """DP trainer pod: per step, forward + backward of ``layers`` bf16
+    ``dim x dim`` linear layers on a ``batch x dim`` activation, bucketed
+    gradient all-reduce overlapped with backward (RCCL over xGMI on GPUs, gloo
+    on the CPU rehearsal path), SGD update; one per rank/GPU.  Ranks run in
+    LOCKSTEP: every iteration also all-reduces a stop flag, so all ranks leave
+    a time-bounded loop after the same iteration and never issue mismatched
+    collectives."""
 
-    def __init__(self, dim: int = 8192, bucket_mb: int = 64, device: int | str | None = None, stream=None):
+    def __init__(self, dim: int = 4096, bucket_mb: int = 64, device: int | str | None = None, stream=None,
+                 layers: int = 4, batch: int | None = None):
+        from ..parallel.collectives import GradBucketer
+
         if device == "cpu":
             self.dev, dt = torch.device("cpu"), torch.float32
         else:
             dev = torch.cuda.current_device() if device is None else device
             self.dev, dt = torch.device("cuda", dev), torch.bfloat16
         g = torch.Generator().manual_seed(0)
-        self.x = torch.randn(dim, dim, generator=g).to(self.dev, dt)
-        self.w = torch.randn(dim, dim, generator=g).to(self.dev, dt) * dim ** -0.5
-        n = max(1, bucket_mb * (1 << 20) // self.x.element_size())
-        self.grad = torch.zeros(n, device=self.dev, dtype=dt)
+        self.batch = batch or dim
+        self.x = torch.randn(self.batch, dim, generator=g).to(self.dev, dt)
+        self.model = torch.nn.Sequential(*[torch.nn.Linear(dim, dim, bias=False) for _ in range(layers)])
+        with torch.no_grad():
+            for m in self.model:
+                m.weight.copy_(torch.randn(dim, dim, generator=g) * dim ** -0.5)
+        self.model.to(self.dev, dt)
+        params = list(self.model.parameters())
+        self.bucketer = GradBucketer(params, bucket_bytes=max(1, bucket_mb) << 20, overlap=True).attach()
+        self.opt = torch.optim.SGD(params, lr=1e-3)
         self.flag = torch.zeros(1, device=self.dev, dtype=torch.float32)
         self.stream = stream if (stream is not None or self.dev.type == "cpu") else torch.cuda.Stream(device=self.dev)
         self.dim = dim
+        self.layers = layers
         self.iters = 0
 
     def _dist(self):
@@ -111,16 +125,16 @@ class CollectiveTenant:
     def step(self) -> None:
         ctx = torch.cuda.stream(self.stream) if self.stream is not None else _null()
         with ctx:
-            y = self.x @ self.w
-            k = min(self.grad.numel(), y.numel())
-            self.grad[:k].copy_(y.view(-1)[:k])
-            d = self._dist()
-            if d is not None:
-                d.all_reduce(self.grad)
+            y = self.model(self.x)
+            loss = y.float().square().mean()
+            loss.backward()  # bucket all-reduces start from the gradient hooks
+            self.bucketer.finish()
+            self.opt.step()
+            self.opt.zero_grad(set_to_none=False)
 
     def run_until(self, deadline: float, times: list[float] | None = None) -> int:
-        """Iterate (GEMM + bucket all-reduce + stop-flag all-reduce) until every
-        rank has passed ``deadline`` (time.monotonic()); completion times of the
+        """Iterate (train step + stop-flag all-reduce) until every rank has
+        passed ``deadline`` (time.monotonic()); completion times of the
         iterations are appended to ``times``."""
         import torch.distributed as dist
 
@@ -141,10 +155,10 @@ class CollectiveTenant:
                 return n
 
     def flops_per_step(self) -> float:
-        return 2.0 * self.dim ** 3
+        return 6.0 * self.batch * self.dim * self.dim * self.layers  # forward + backward (dX and dW)
 
     def bucket_bytes(self) -> int:
-        return self.grad.numel() * self.grad.element_size()
+        return sum(b.flat.numel() * b.flat.element_size() for b in self.bucketer.buckets)
 
 
 class _null:

@@ -5,10 +5,15 @@
 
 * :class:`GradBucketer` -- DP gradient synchronisation in fixed-size flat
   buckets (all-reduce, or reduce-scatter + all-gather for ZeRO-style
-  sharding), issued on a side stream so it overlaps the next bucket's
-  compute.  Bucket size defaults to 64 MiB: xGMI is point-to-point (7 links
-  x ~153 GB/s per MI355X), a ring all-reduce is per-link bound, and 64 MiB
-  amortises the ~20-30 us RCCL launch/latency to < 5 %.
+  sharding) on a side stream.  With :meth:`GradBucketer.attach` the buckets
+  are built in reverse parameter order (the order backward produces
+  gradients) and each bucket's all-reduce is launched from a
+  post-accumulate-grad hook the moment its last gradient lands, so the
+  collectives overlap the rest of backward; :meth:`GradBucketer.finish`
+  waits for them and writes the averaged gradients back.  Bucket size
+  defaults to 64 MiB: xGMI is point-to-point (7 links x ~153 GB/s per
+  MI355X), a ring all-reduce is per-link bound, and 64 MiB amortises the
+  ~20-30 us RCCL launch/latency to < 5 %.
 * :func:`busbw` -- NCCL-tests style bus bandwidth of an all-reduce.
 * :func:`init_from_env` -- RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* rendezvous
   (127.0.0.1), one rank per GPU.
@@ -58,17 +63,24 @@ class _Bucket:
 class GradBucketer:
     """Flatten gradients into buckets of ``bucket_bytes`` and average them
     across the process group (optionally sharded: reduce-scatter, then the
-    caller's optimizer updates its shard, then :meth:`all_gather`)."""
+    caller's optimizer updates its shard, then :meth:`all_gather`).
+
+    Two ways to drive it: :meth:`sync` after backward (all buckets at once),
+    or :meth:`attach` once and :meth:`finish` after every backward (buckets
+    launched from gradient hooks while backward still runs)."""
 
     def __init__(self, params: list[torch.Tensor], bucket_bytes: int = DEFAULT_BUCKET_BYTES, group=None,
-                 sharded: bool = False):
+                 sharded: bool = False, overlap: bool = False):
         self.group = group
         self.sharded = sharded
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.buckets: list[_Bucket] = []
+        # backward produces gradients roughly in reverse parameter order: build
+        # the buckets that way so the first buckets complete first
+        order = list(reversed(params)) if overlap else list(params)
         cur: list[torch.Tensor] = []
         size = 0
-        for p in params:
+        for p in order:
             nb = p.numel() * p.element_size()
             if cur and size + nb > bucket_bytes:
                 self.buckets.append(self._make(cur))
@@ -77,8 +89,13 @@ class GradBucketer:
             size += nb
         if cur:
             self.buckets.append(self._make(cur))
-        self.stream = torch.cuda.Stream() if (params and params[0].is_cuda) else None
+        self.stream = torch.cuda.Stream(device=params[0].device) if (params and params[0].is_cuda) else None
         self.last_seconds = 0.0
+        self._where = {id(p): i for i, b in enumerate(self.buckets) for p in b.params}
+        self._ready = [0] * len(self.buckets)
+        self._works: list = [None] * len(self.buckets)
+        self._hooks: list = []
+        self.launched_in_backward = 0  # bucket collectives started from a gradient hook (all steps)
 
     def _make(self, params: list[torch.Tensor]) -> _Bucket:
         n = sum(p.numel() for p in params)
@@ -102,6 +119,63 @@ class GradBucketer:
                 p.grad = torch.empty_like(p)
             p.grad.copy_(src[o:o + n].view_as(p))
 
+    # -- overlapped mode -------------------------------------------------
+    def attach(self) -> "GradBucketer":
+        """Launch each bucket's all-reduce from a post-accumulate-grad hook as
+        soon as all of its gradients exist (not sharded)."""
+        if self.sharded:
+            raise ValueError("overlapped bucketing is for all-reduce (sharded=False)")
+        for b in self.buckets:
+            for p in b.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        return self
+
+    def detach(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+    def _launch(self, i: int) -> None:
+        b = self.buckets[i]
+        if self.stream is not None:
+            # the gradients were produced on the backward stream of this thread
+            self.stream.wait_stream(torch.cuda.current_stream(b.flat.device))
+        ctx = torch.cuda.stream(self.stream) if self.stream is not None else _null()
+        with ctx:
+            self._pack(b)
+            self._works[i] = dist.all_reduce(b.flat, group=self.group, async_op=True) if self.world > 1 else None
+
+    def _on_grad(self, p: torch.Tensor) -> None:
+        i = self._where[id(p)]
+        self._ready[i] += 1
+        if self._ready[i] == len(self.buckets[i].params):
+            self._launch(i)
+            self.launched_in_backward += 1
+
+    def finish(self) -> None:
+        """Wait for this step's bucket collectives (launching any bucket whose
+        hooks did not all fire, e.g. unused parameters) and write the averaged
+        gradients back; the caller's stream then waits for them."""
+        t0 = time.perf_counter()
+        for i in range(len(self.buckets)):
+            if self._works[i] is None and self._ready[i] < len(self.buckets[i].params):
+                self._launch(i)
+        ctx = torch.cuda.stream(self.stream) if self.stream is not None else _null()
+        with ctx:
+            for i, b in enumerate(self.buckets):
+                w = self._works[i]
+                if w is not None:
+                    w.wait()  # on the side stream (NCCL) / blocking (gloo)
+                if self.world > 1:
+                    b.flat.div_(self.world)
+                self._unpack(b, b.flat)
+        if self.stream is not None:
+            torch.cuda.current_stream(self.buckets[0].flat.device).wait_stream(self.stream)
+        self._ready = [0] * len(self.buckets)
+        self._works = [None] * len(self.buckets)
+        self.last_seconds = time.perf_counter() - t0
+
+    # -- after-backward mode ---------------------------------------------
     def sync(self) -> list[torch.Tensor]:
         """Average all gradients; returns the local shards when ``sharded``."""
         t0 = time.perf_counter()

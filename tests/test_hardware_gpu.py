@@ -114,3 +114,24 @@ def test_device_plugin_slice_mask_is_enforced_in_a_child_process():
     assert summary["distinct_cus"] == 64, summary
     assert summary["cus_per_xcc"] == {str(x): 8 for x in range(8)} or \
         summary["cus_per_xcc"] == {x: 8 for x in range(8)}, summary
+
+
+def test_trainer_pod_step_on_gpu_overlaps_bucket_launches_with_backward():
+    """The DP trainer pod on the GPU (world 1): forward + backward with the
+    gradient hooks driving the bucketed collective path on a side stream, then
+    SGD; the loss falls and every bucket was started from inside backward."""
+    from nos_amd.models.tenants import CollectiveTenant
+
+    t = CollectiveTenant(dim=512, bucket_mb=1, device=0, layers=4, batch=256)
+    assert len(t.bucketer.buckets) >= 2
+    w0 = [m.weight.detach().clone() for m in t.model]
+    losses = []
+    for _ in range(3):
+        with torch.no_grad():
+            losses.append(t.model(t.x).float().square().mean().item())
+        t.step()
+    torch.cuda.synchronize()
+    assert t.bucketer.launched_in_backward == 3 * len(t.bucketer.buckets)
+    assert all(not torch.equal(a, m.weight) for a, m in zip(w0, t.model))
+    assert losses[-1] < losses[0]
+    assert t.flops_per_step() == 6.0 * 256 * 512 * 512 * 4

@@ -45,6 +45,52 @@ def _worker(rank: int, world: int, port: int, q) -> None:
         dist.destroy_process_group()
 
 
+def _overlap_worker(rank: int, world: int, port: int, q) -> None:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 32),
+                                    torch.nn.ReLU(), torch.nn.Linear(32, 4))
+        ref = [p.detach().clone().requires_grad_(True) for p in model.parameters()]
+        b = GradBucketer(list(model.parameters()), bucket_bytes=1500, overlap=True).attach()
+        ok = len(b.buckets) >= 3
+        torch.manual_seed(100 + rank)  # different data per rank
+        x = torch.randn(8, 16)
+        for step in range(2):  # twice: the hook bookkeeping resets between steps
+            model.zero_grad(set_to_none=False)
+            model(x).square().mean().backward()
+            launched = b.launched_in_backward
+            b.finish()
+            ok = ok and launched == (step + 1) * len(b.buckets)  # every bucket started inside backward
+        # reference: this rank's gradient (functional copy), all-reduced by hand
+        w1, b1, w2, b2, w3, b3 = ref
+        h = torch.relu(x @ w1.T + b1)
+        h = torch.relu(h @ w2.T + b2)
+        (h @ w3.T + b3).square().mean().backward()
+        for p, r in zip(model.parameters(), ref):
+            g = r.grad.clone()
+            dist.all_reduce(g)
+            ok = ok and torch.allclose(p.grad, g / world, atol=1e-6)
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_bucketer_matches_allreduced_gradients():
+    """Buckets launched from gradient hooks during backward average exactly like a plain all-reduce."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+    assert res == {0: True, 1: True}
+
+
 def test_grad_bucketer_two_ranks():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
