@@ -78,11 +78,12 @@ def parse_args(argv=None):
     ap.add_argument("--coll-bucket-mb", type=int, default=64)
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: rehearsal of the whole launch path without a GPU (tiny pods, gloo)")
-    ap.add_argument("--table", default="",
+    ap.add_argument("--table", default="auto",
                     help="also measure the reference demo's latency table: comma list of pod counts per GPU "
-                         "(e.g. 1,3,5,7), one aligned window per (mode, count); reported as latency_table")
+                         "(e.g. 1,3,5,7), one aligned window per (mode, count), reported as latency_table; "
+                         "auto = 1,3,5,7 on single-GPU runs, none on multi-GPU runs; '' = none")
     ap.add_argument("--table-modes", default="shared,cumask")
-    ap.add_argument("--table-window-s", type=float, default=6.0)
+    ap.add_argument("--table-window-s", type=float, default=5.0)
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -283,6 +284,8 @@ def main(argv=None) -> int:
     if args.device == "cpu":
         extra_env["OMP_NUM_THREADS"] = "1"
     log(rank, f"control plane placed {cp.get('placed_pods')} pods; local envs {envs[:2]}...")
+    if args.table == "auto":
+        args.table = "1,3,5,7" if world == 1 and args.device == "cuda" else ""
     table_plans = [(mode, n, plan(args, world, local, args.slice_gb, n, mode)[0])
                    for mode in args.table_modes.split(",") if args.table
                    for n in map(int, args.table.split(","))]
