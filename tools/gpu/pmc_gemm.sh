@@ -3,7 +3,7 @@
 # usage (on the GPU box, from the repo root): bash tools/gpu/pmc_gemm.sh
 set -o pipefail
 R=$PWD
-OUT=$R/gpurun_out/pmc_gemm
+OUT=$R/gpurun_out/${PMC_OUT:-pmc_gemm}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 i=0
