@@ -192,28 +192,27 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[CF::MI][CF::
                                               unsigned short* __restrict__ C, int ldc, int M, int N, int m0,
                                               int n0, int epi, bool vec_ok, int wm, int wn, int r, int hh) {
   constexpr int WN = CF::WN, NB = CF::NB, MI = CF::MI, WM = CF::WM;
-  // residual rows: all 16-byte loads issued up front (clamped addresses, no
-  // per-element branches) so their latencies overlap instead of one round
-  // trip per chunk
-  s16x8_t rpre[MI][NB][2];
-  if constexpr (RESID) {
-    if (vec_ok && N >= 8) {
-      const int nmax = ((N - 8) >> 3) << 3;
+  // residual rows: the 16-byte loads of row group mi+1 are issued before
+  // group mi is finished (clamped addresses, no per-element branches), so
+  // their latency overlaps the epilogue math; two groups live at a time keep
+  // the 8-wave tiles (MI = 4) from spilling
+  const bool rvec = RESID && vec_ok && N >= 8;
+  const int nmax = N >= 8 ? ((N - 8) >> 3) << 3 : 0;
+  s16x8_t rpre[2][NB][2];
+  auto rload = [&](int mi) {
+    const int m = min(m0 + wm * WM + mi * 32 + r, M - 1);
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const int m = min(m0 + wm * WM + mi * 32 + r, M - 1);
+    for (int ni = 0; ni < NB; ++ni)
 #pragma unroll
-        for (int ni = 0; ni < NB; ++ni)
-#pragma unroll
-          for (int pr = 0; pr < 2; ++pr) {
-            const int n = min(n0 + wn * WN + ni * 32 + 16 * pr + 8 * hh, nmax);
-            rpre[mi][ni][pr] = *reinterpret_cast<const s16x8_t*>(R + (long long)m * ldr + n);
-          }
+      for (int pr = 0; pr < 2; ++pr) {
+        const int n = min(n0 + wn * WN + ni * 32 + 16 * pr + 8 * hh, nmax);
+        rpre[mi & 1][ni][pr] = *reinterpret_cast<const s16x8_t*>(R + (long long)m * ldr + n);
       }
-    }
-  }
+  };
+  if (rvec) rload(0);
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
+      if (rvec && mi + 1 < MI) rload(mi + 1);
       const int rl = wm * WM + mi * 32 + r;
       const int m = m0 + rl;
       float mu = 0.f, rs = 1.f;
@@ -238,17 +237,14 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[CF::MI][CF::
           // now: 8 consecutive columns cl .. cl+7 of row rl
           const int cl = wn * WN + ni * 32 + 16 * pr + 8 * hh;
           const int n = n0 + cl;
-          const float4 p1a = *reinterpret_cast<const float4*>(s_p1 + cl);
-          const float4 p1b = *reinterpret_cast<const float4*>(s_p1 + cl + 4);
-          const float4 p2a = *reinterpret_cast<const float4*>(s_p2 + cl);
-          const float4 p2b = *reinterpret_cast<const float4*>(s_p2 + cl + 4);
-          const float p1[8] = {p1a.x, p1a.y, p1a.z, p1a.w, p1b.x, p1b.y, p1b.z, p1b.w};
-          const float p2[8] = {p2a.x, p2a.y, p2a.z, p2a.w, p2b.x, p2b.y, p2b.z, p2b.w};
-          // LN correction / bias and activation on column pairs (packed f32)
+          // LN correction / bias and activation on column pairs (packed f32);
+          // the per-column parameters come from LDS a pair at a time (few live
+          // registers next to the 8-wave tiles' accumulators)
 #pragma unroll
           for (int e = 0; e < 8; e += 2) {
             f32x2_t w = {v[e], v[e + 1]};
-            const f32x2_t q1 = {p1[e], p1[e + 1]}, q2 = {p2[e], p2[e + 1]};
+            const f32x2_t q1 = *reinterpret_cast<const f32x2_t*>(s_p1 + cl + e);
+            const f32x2_t q2 = *reinterpret_cast<const f32x2_t*>(s_p2 + cl + e);
             if (LN)
               w = (w - q1 * mu) * rs + q2;
             else
@@ -264,7 +260,7 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[CF::MI][CF::
           if (m >= M || n >= N) continue;
           if (n + 8 <= N && vec_ok) {
             if constexpr (RESID) {
-              const s16x8_t rv = rpre[mi][ni][pr];
+              const s16x8_t rv = rpre[mi & 1][ni][pr];
 #pragma unroll
               for (int e = 0; e < 8; ++e) v[e] += nos::bf16_to_f32((unsigned short)rv[e]);
             }
@@ -384,7 +380,9 @@ __global__ __launch_bounds__(CF::NT, CF::MINB) void gemm_bf16_rk_kernel(
       const unsigned char* ta = smem + (kt % S) * STAGE_BYTES;
       const unsigned char* tb = ta + TILE_A_BYTES;
       if constexpr (LN) {
-#pragma unroll
+        // one 16-byte chunk live at a time: the 8-wave tiles hold 128
+        // accumulator registers and would spill with all chunks in flight
+#pragma unroll(CF::NW > 4 ? 1 : L::CPR / 2)
         for (int c = 0; c < L::CPR / 2; ++c) {
           const int lc = shalf * (L::CPR / 2) + c;
           const s16x8_t v = *reinterpret_cast<const s16x8_t*>(ta + srow * L::RB + ((lc ^ L::swz(srow)) << 4));
