@@ -135,3 +135,22 @@ def test_trainer_pod_step_on_gpu_overlaps_bucket_launches_with_backward():
     assert all(not torch.equal(a, m.weight) for a, m in zip(w0, t.model))
     assert losses[-1] < losses[0]
     assert t.flops_per_step() == 6.0 * 256 * 512 * 512 * 4
+
+
+def test_slice_prober_prices_slices_on_their_cu_slots():
+    """The gpuagent's slice probe on the real GPU: a 36 GB slice (4 CUs per XCD)
+    against the whole GPU, idle and (for the slice) under co-tenant load on the
+    complement CUs.  More CUs must price higher; the loaded numbers exist."""
+    from nos_amd.agents.probe import METRICS, SliceProber
+
+    smi = _smi()
+    prober = SliceProber(smi, iters=2000, loaded=True)
+    small = prober(0, "36gb")
+    whole = SliceProber(smi, iters=2000, loaded=False)(0, "288gb")
+    assert small["cus"] == 32 and whole["cus"] == 256
+    for k in ("tflops", "gemmtflops", "gbps"):
+        assert small[k] > 0 and whole[k] > 0, k
+    assert whole["gemmtflops"] > 3 * small["gemmtflops"]
+    assert whole["tflops"] > 3 * small["tflops"]
+    assert small["loadedgbps"] > 0 and small["loadedgemmtflops"] > 0
+    assert set(small) >= set(METRICS)
