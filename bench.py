@@ -245,8 +245,18 @@ def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, 
     fleet = PodFleet(envs, dtype=dtype, graphs=graphs, extra_env=extra_env, launcher=launcher, device=device)
     coll_times: list[float] = []
     try:
-        fleet.start()
-        ready_s = fleet.wait_ready(timeout_s=900, progress_cb=lambda n, t: log(d.rank, f"{dtype} pods ready {n}/{t}"))
+        err = None
+        try:
+            fleet.start()
+            ready_s = fleet.wait_ready(timeout_s=900,
+                                       progress_cb=lambda n, t: log(d.rank, f"{dtype} pods ready {n}/{t}"))
+        except Exception as e:  # every rank learns of it below instead of waiting at a barrier
+            err = e
+        failed, = d.reduce([1.0 if err else 0.0], "max")
+        if err:
+            raise err
+        if failed:
+            raise RuntimeError(f"pods of another rank failed to start ({dtype})")
         d.barrier_sync()
         t0, t1, (util, n_util) = fleet_window(d, fleet, warmup, steps, step_s, sampler, coll, coll_times)
         fleet.stop()
