@@ -126,9 +126,12 @@ def _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K):
 
 
 def set_gemm_policy(policy: str) -> None:
-    """``"throughput"`` (default: 128x128 tiles, best when pods share a GPU) or
-    ``"latency"`` (128x64 tiles for GEMMs with fewer tiles than CUs, best for
-    a single tenant owning the GPU)."""
+    """bf16 GEMM tile choice (``csrc/hip/gemm.hip:pick_tile``):
+    ``"throughput"`` (default: least padded work over 128x128 / 256x192 /
+    256x256 tiles, best when pods share a GPU) or ``"latency"`` (fewest rounds
+    of tiles over the CUs, 128x64 included, best for a single tenant);
+    ``"narrow"`` / ``"big"`` / ``"wide"`` force 128x64 / 256x256 / 256x192
+    (A/B measurements)."""
     code = {"throughput": 0, "latency": 1, "narrow": 2, "big": 3, "wide": 4}[policy]
     _lib.check(_lib.lib().nos_gemm_set_policy(code), "nos_gemm_set_policy")
 
