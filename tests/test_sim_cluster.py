@@ -159,3 +159,36 @@ def test_bench_control_plane_plan(n_gpus):
     assert info["schedulable_fractional_pods_per_node"] == 4 * n_gpus  # 288 GB / 72 GB
     assert info["plan_reported"]
     assert sorted(c for m in masks for c in m) == list(range(256))
+
+
+def test_baseline_config3_eight_gpus_dynamic_spx_cpx_repartitioning():
+    """BASELINE config 3: one 8 x MI355X node, mixed pending partition requests
+    drive SPX/DPX/QPX/CPX switches; when the small pods finish, whole-GPU
+    requests switch the drained GPUs back to SPX."""
+    cl = SimCluster()
+    nd = cl.add_node("n1", C.PARTITIONING_AMDPART, gpus=8)
+    cl.settle(30)
+    want = {"amd.com/partition-1xcd.36gb": 16, "amd.com/partition-4xcd.144gb": 3,
+            "amd.com/partition-2xcd.72gb": 2, "amd.com/partition-8xcd.288gb": 2}
+    n = 0
+    for res, k in want.items():
+        for _ in range(k):
+            cl.submit_pod(f"p{n}", {res: 1})
+            n += 1
+            cl.clock.advance(0.5)
+    cl.settle(1200, until=lambda: not cl.pending_pods())
+    assert len(cl.running_pods()) == n
+    modes = Counter(nd.smi.compute)
+    assert modes["CPX"] == 2 and modes["DPX"] == 2 and modes["QPX"] >= 1 and modes["SPX"] >= 2
+    ann = ko.annotations(cl.api.get("Node", "n1"))
+    assert ann[C.ANNOTATION_REPORTED_PARTITIONING_PLAN] == ann[C.ANNOTATION_PARTITIONING_PLAN]
+    # the CPX pods finish; whole-GPU demand takes the drained GPUs back to SPX
+    for i in range(16):
+        nd.kubelet.complete_pod("default", f"p{i}")
+    for j in range(3):
+        cl.submit_pod(f"w{j}", {"amd.com/partition-8xcd.288gb": 1})
+        cl.clock.advance(0.5)
+    cl.settle(1200, until=lambda: not cl.pending_pods())
+    assert {ko.name(p) for p in cl.running_pods()} >= {"w0", "w1", "w2"}
+    assert Counter(nd.smi.compute)["CPX"] == 0
+    assert Counter(nd.smi.compute)["SPX"] >= 5
