@@ -35,6 +35,7 @@
 //    XCD-aware tile order so tiles sharing the larger operand panel share an
 //    XCD's L2.
 #include "common.h"
+#include "gemm_tiles.h"
 
 namespace {
 
@@ -382,7 +383,8 @@ __global__ __launch_bounds__(CF::NT, CF::MINB) void gemm_bf16_rk_kernel(
       if constexpr (LN) {
         // one 16-byte chunk live at a time: the 8-wave tiles hold 128
         // accumulator registers and would spill with all chunks in flight
-#pragma unroll(CF::NW > 4 ? 1 : L::CPR / 2)
+        constexpr int LN_UNROLL = CF::NW > 4 ? 1 : L::CPR / 2;
+#pragma unroll LN_UNROLL
         for (int c = 0; c < L::CPR / 2; ++c) {
           const int lc = shalf * (L::CPR / 2) + c;
           const s16x8_t v = *reinterpret_cast<const s16x8_t*>(ta + srow * L::RB + ((lc ^ L::swz(srow)) << 4));
@@ -494,44 +496,6 @@ int launch_tile(const void* A, int lda, const void* W, int ldw, const void* bias
   return (int)hipGetLastError();
 }
 
-enum TileKind : int { T_BASE, T_NARROW, T_WIDE, T_BIG };
-
-// Tile choice by a cost model: (tiles or rounds of tiles) x tile area /
-// relative efficiency.  The efficiencies are measured per output element on
-// the batch-8 YOLOS shapes and 4096^3 (profiles/r02_gemm_bf16_tiles.json):
-// the 8-wave 256-row tiles read half the L2 bytes per FLOP and 0.75-0.83 LDS
-// fragments per MFMA; 128x64 reads 1.5.
-//  * latency policy: ceil(tiles / CUs) x area -- the rounds a single tenant waits;
-//  * throughput policy: tiles x area -- the work co-running pods share (and
-//    no 128x64, which costs them ~4 %);
-// the 512-thread tiles only when they occupy at least half the CUs (a few big
-// tiles would serialise one tenant on a handful of CUs).
-int pick_tile(int M, int N, int policy, int cus) {
-  if (policy == 2) return T_NARROW;
-  if (policy == 3) return T_BIG;
-  if (policy == 4) return T_WIDE;
-  struct Cand {
-    int kind, bm, bn;
-    double eff;
-  };
-  static constexpr Cand cands[] = {{T_BASE, 128, 128, 1.0}, {T_NARROW, 128, 64, 0.8}, {T_WIDE, 256, 192, 1.2},
-                                   {T_BIG, 256, 256, 1.25}};
-  int pick = T_BASE;
-  double best = 1e300;
-  for (const Cand& c : cands) {
-    if (policy == 0 && c.kind == T_NARROW) continue;
-    const long long tiles = (long long)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
-    if (c.bm == 256 && 2 * tiles < cus) continue;
-    const double per = (double)c.bm * c.bn / c.eff;
-    const double cost = policy == 1 ? (double)((tiles + cus - 1) / cus) * per : (double)tiles * per;
-    if (cost < best * 0.99) {  // ties keep the earlier (smaller) tile
-      best = cost;
-      pick = c.kind;
-    }
-  }
-  return pick;
-}
-
 int launch(const void* A, int lda, const void* W, int ldw, const void* bias, const float* c1,
            const float* c2, const void* R, int ldr, void* C, int ldc, int M, int N, int K, int epi,
            float eps, int max_wg, bool ln, hipStream_t stream) {
@@ -541,6 +505,7 @@ int launch(const void* A, int lda, const void* W, int ldw, const void* bias, con
   if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
   if ((epi & EPI_RESID) && !R) return (int)hipErrorInvalidValue;
 #define NOS_GEMM_ARGS A, lda, W, ldw, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, max_wg, ln, stream
+  using namespace nos_gemm;
   switch (pick_tile(M, N, g_tile_policy, num_cus())) {
     case T_NARROW: return launch_tile<CfgNarrow>(NOS_GEMM_ARGS);
     case T_WIDE: return launch_tile<CfgWide>(NOS_GEMM_ARGS);
