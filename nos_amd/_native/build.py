@@ -81,7 +81,7 @@ def build_hip(force: bool = False, jobs: int = 8, verbose: bool = False, src_dir
     out_lib = Path(out) if out else HIP_LIB
     bdir = Path(build_dir) if build_dir else BUILD
     bdir.mkdir(parents=True, exist_ok=True)
-    hdr = [src_dir / "common.h"]
+    hdr = sorted(src_dir.glob("*.h"))  # every kernel source may include any of them
     objs: list[Path] = []
     todo: list[tuple[Path, Path]] = []
     for s in HIP_SOURCES:
