@@ -215,8 +215,13 @@ def fleet_window(d: Dist, fleet, warmup: int, steps: int, step_s: float, sampler
     t_end = time.monotonic() + warmup * step_s
     if coll:
         coll.run_until(t_end)
+    last_log = time.monotonic()
     while time.monotonic() < t_end:
         time.sleep(0.05)
+        if time.monotonic() - last_log > 30:  # long reference-style warm-ups: show progress
+            last_log = time.monotonic()
+            log(d.rank, f"warm-up: {t_end - last_log:.0f} s left")
+            fleet.check_alive()
     fleet.check_alive()
     d.barrier_sync()
     t0 = time.monotonic()
@@ -230,6 +235,9 @@ def fleet_window(d: Dist, fleet, warmup: int, steps: int, step_s: float, sampler
                 break
             time.sleep(min(0.05, deadline - now))
         fleet.check_alive()
+        if time.monotonic() - last_log > 30:
+            last_log = time.monotonic()
+            log(d.rank, f"window: step {k + 1}/{steps}")
     d.barrier_sync()
     t1 = time.monotonic()
     util = sampler.mean(t0, t1) if sampler else (None, 0)
