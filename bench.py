@@ -98,7 +98,16 @@ def plan(args, world: int, local: int, slice_gb: int, pods: int, mode: str) -> t
 
     _, info = control_plane_plan(n_gpus=world, pods_per_gpu=pods, slice_gb=slice_gb, num_cus=256, local_gpu=local,
                                  cu_policy="shared" if mode == "shared" else "proportional", capacity_probe=True)
-    return info.pop("envs"), info
+    envs = info.pop("envs")
+    if os.environ.get("NOS_AMD_BENCH_FOLD_GPUS") == "1":
+        # rehearsal of the multi-rank path on fewer GPUs than ranks (gloo between
+        # the ranks, which RCCL cannot do on a shared GPU): rank r's pods go to
+        # GPU r % visible GPUs, as the rank itself does (Dist.init_gpu)
+        import torch
+
+        gpu = str(local % max(1, torch.cuda.device_count()))  # counts devices without initialising HIP
+        envs = [{**e, "HIP_VISIBLE_DEVICES": gpu} for e in envs]
+    return envs, info
 
 
 class Dist:
