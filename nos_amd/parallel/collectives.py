@@ -21,6 +21,7 @@
 from __future__ import annotations
 
 import os
+import threading
 import time
 from dataclasses import dataclass, field
 
@@ -95,6 +96,7 @@ class GradBucketer:
         self._ready = [0] * len(self.buckets)
         self._works: list = [None] * len(self.buckets)
         self._hooks: list = []
+        self._lock = threading.Lock()  # hooks of different devices run on different autograd threads
         self.launched_in_backward = 0  # bucket collectives started from a gradient hook (all steps)
 
     def _make(self, params: list[torch.Tensor]) -> _Bucket:
@@ -147,10 +149,13 @@ class GradBucketer:
 
     def _on_grad(self, p: torch.Tensor) -> None:
         i = self._where[id(p)]
-        self._ready[i] += 1
-        if self._ready[i] == len(self.buckets[i].params):
+        with self._lock:
+            self._ready[i] += 1
+            full = self._ready[i] == len(self.buckets[i].params)
+            if full:
+                self.launched_in_backward += 1
+        if full:
             self._launch(i)
-            self.launched_in_backward += 1
 
     def finish(self) -> None:
         """Wait for this step's bucket collectives (launching any bucket whose
