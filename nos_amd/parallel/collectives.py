@@ -124,7 +124,10 @@ class GradBucketer:
     # -- overlapped mode -------------------------------------------------
     def attach(self) -> "GradBucketer":
         """Launch each bucket's all-reduce from a post-accumulate-grad hook as
-        soon as all of its gradients exist (not sharded)."""
+        soon as all of its gradients exist (not sharded).  Collectives start in
+        the order the buckets complete; with one device per rank (data
+        parallelism) backward runs the same graph on one autograd thread in
+        every rank, so that order is the same everywhere, as collectives need."""
         if self.sharded:
             raise ValueError("overlapped bucketing is for all-reduce (sharded=False)")
         for b in self.buckets:
