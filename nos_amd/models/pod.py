@@ -129,21 +129,20 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             torch.cuda.set_device(0)  # the device plugin's HIP_VISIBLE_DEVICES leaves exactly the slice's GPU
             frac = apply_memory_limit(0)
             torch.backends.cuda.matmul.allow_tf32 = False  # true fp32 GEMMs (no reduced-precision shortcut)
-        if gpu and os.environ.get("NOS_AMD_GEMM_F32_POLICY"):  # A/B of the fp32 GEMM tile policy
-            from ..ops import set_gemm_f32_policy
+            from ..ops import set_attention_f32_variant, set_gemm_f32_policy, set_gemm_policy
 
-            set_gemm_f32_policy(os.environ["NOS_AMD_GEMM_F32_POLICY"])
-        if gpu and os.environ.get("NOS_AMD_ATTN_F32_VARIANT"):  # A/B of the fp32 attention tiling
-            from ..ops import set_attention_f32_variant
-
-            set_attention_f32_variant(os.environ["NOS_AMD_ATTN_F32_VARIANT"])
-        elif gpu and frac is not None and frac < 0.99:
-            # a fractional slice shares the CUs with other pods: one wave group per
-            # workgroup (the 2-group tiling only pays when this pod alone leaves CUs
-            # idle; 8 pods x 36 GB: 311 vs 302 inf/s, profiles/r02_attention_f32.json)
-            from ..ops import set_attention_f32_variant
-
-            set_attention_f32_variant("w4k64")
+            whole = frac is None or frac >= 0.99
+            # kernel configs follow the slice.  A pod owning the whole GPU wants the
+            # fewest rounds of tiles (bf16 GEMM latency policy: fc2 19.7 -> 14.2 us
+            # at batch 1) and two attention wave groups when its grid leaves CUs
+            # idle (the kernel's auto rule).  A fractional slice shares the CUs
+            # with other pods: least-work tiles and one wave group (8 pods x 36 GB:
+            # 311 vs 302 inf/s, profiles/r02_attention_f32.json).  The env
+            # variables override for A/B runs.
+            set_gemm_policy(os.environ.get("NOS_AMD_GEMM_POLICY") or ("latency" if whole else "throughput"))
+            if os.environ.get("NOS_AMD_GEMM_F32_POLICY"):
+                set_gemm_f32_policy(os.environ["NOS_AMD_GEMM_F32_POLICY"])
+            set_attention_f32_variant(os.environ.get("NOS_AMD_ATTN_F32_VARIANT") or ("auto" if whole else "w4k64"))
         m, x = _build(dtype, seed, demo_input_hw(), device)
         if gpu:
             s = torch.cuda.Stream()
