@@ -37,6 +37,14 @@ value / (8 x GPUs): 8 is the reference's schedulable 10 GB fractional pods per
 A100-80GB (MPS).  gpu_util_pct is the mean amd-smi gfx activity over the window.
 aggregate_inf_per_s (fp32) is compared with 21.89 inf/s per GPU (the
 reference's best aggregate, 7 MPS pods on one A100).
+
+Also in the JSON: one whole-GPU pod's rate (``--ref-pod-s``), a bf16 fleet on
+the gfx950 kernels (``--extra-bf16-s``), the reference demo's latency table
+(1/3/5/7 pods, shared and CU-mask slices; default on single-GPU runs,
+``--table``), and with WORLD_SIZE > 1 a data-parallel trainer pod per GPU
+(slot 0, run by the rank: bf16 MLP forward + backward with bucketed RCCL
+all-reduces over xGMI launched from the gradient hooks, in lockstep across
+ranks), so slices are measured under collective traffic.
 """
 from __future__ import annotations
 
