@@ -79,6 +79,9 @@ def parse_args(argv=None):
     ap.add_argument("--extra-bf16-s", type=float, default=4.0,
                     help="window of an extra bf16 (gfx950 kernels) fleet run (0 = skip)")
     ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES per pod (0 = HIP default)")
+    ap.add_argument("--bursty", default="", metavar="ON_S:OFF_S",
+                    help="bursty tenants: every pod infers for ON_S seconds then idles OFF_S, out of phase "
+                         "with the others (utilisation under statistical multiplexing)")
     ap.add_argument("--collective", choices=["auto", "on", "off"], default="auto",
                     help="one of each GPU's pods is a DP trainer (bf16 GEMM + RCCL all-reduce over xGMI, in "
                          "lockstep across ranks); auto: on when WORLD_SIZE > 1")
@@ -318,6 +321,7 @@ def main(argv=None) -> int:
     extra_env = {"GPU_MAX_HW_QUEUES": str(args.hw_queues)} if args.hw_queues else {}
     if args.device == "cpu":
         extra_env["OMP_NUM_THREADS"] = "1"
+    fleet_env = {**extra_env, **({"NOS_AMD_POD_DUTY": args.bursty} if args.bursty else {})}
     log(rank, f"control plane placed {cp.get('placed_pods')} pods; local envs {envs[:2]}...")
     if args.table == "auto":
         args.table = "1,3,5,7" if world == 1 and args.device == "cuda" else ""
@@ -353,7 +357,7 @@ def main(argv=None) -> int:
                                     args.ref_pod_s, sampler, device=args.device)
         ref = {"inf_per_s": round(w1.throughput, 3), "latency_s": w1.mean_latency_s, "gpu_util_pct": u1}
 
-    w, util, n_util, ready_s, tr = run_fleet(d, launcher, pod_envs, args.dtype, not args.no_graphs, extra_env,
+    w, util, n_util, ready_s, tr = run_fleet(d, launcher, pod_envs, args.dtype, not args.no_graphs, fleet_env,
                                              args.warmup, args.steps, args.step_s, sampler, coll, device=args.device)
     bf = None
     if args.extra_bf16_s > 0 and args.dtype != "bf16" and d.cuda:
@@ -408,7 +412,7 @@ def main(argv=None) -> int:
                                   f"{world} GPU(s)",
                    "pods_per_gpu": args.pods_per_gpu, "slice_gb": args.slice_gb, "mode": args.mode,
                    "pod_execution": "one process per pod with its device-plugin env", "graphs": not args.no_graphs,
-                   "collective_tenant": bool(coll), "step_s": args.step_s,
+                   "collective_tenant": bool(coll), "step_s": args.step_s, "bursty": args.bursty or None,
                    "pods_placed_per_node": int(placed)},
         "gpu_util_pct": None if util_mean is None else round(util_mean, 1),
         "gpu_util_samples": n_util,

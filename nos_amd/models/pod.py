@@ -166,8 +166,16 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
         row[0] = STATE_READY
         times: list[float] = []
         info["t_ready"] = time.monotonic()
+        # bursty tenants (NOS_AMD_POD_DUTY="on_s:off_s"): infer for on_s, idle
+        # for off_s, with a per-pod phase so the pods do not burst in step
+        duty = os.environ.get("NOS_AMD_POD_DUTY")
+        on_s, off_s = (float(v) for v in duty.split(":")) if duty else (0.0, 0.0)
+        phase0 = time.monotonic() - (on_s + off_s) * ((slot * 0.618) % 1.0)
         with torch.no_grad():
             while not board.stopped():
+                if off_s > 0 and (time.monotonic() - phase0) % (on_s + off_s) >= on_s:
+                    time.sleep(0.005)
+                    continue
                 t.launch()
                 s.synchronize()
                 now = time.monotonic()

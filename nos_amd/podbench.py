@@ -294,7 +294,10 @@ class PodFleet:
             c = progress(times, t1, start) - progress(times, t0, start)
             inside = [t0] + [t for t in times if t0 < t < t1] + [t1]
             gap = max(b - a for a, b in zip(inside, inside[1:]))
-            running = times[0] <= t0 and times[-1] >= t1 and gap < 0.25 * w
+            # running through the window: warm before it, and never more than a
+            # quarter of it without a completion -- the gap list ends at t1, so a
+            # pod that stopped early fails it (a bursty pod idling at t1 does not)
+            running = times[0] <= t0 and gap < 0.25 * w
             info = {k: r.get(k) for k in ("pid", "multiprocessor_count", "cu_mask", "hip_visible_devices",
                                            "memory_limit_gb", "memory_fraction", "max_allocated_gb")}
             out.append(PodResult(i, c, (w / c) if c > 0 else None, gap, running, info))

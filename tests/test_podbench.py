@@ -69,3 +69,17 @@ def test_failed_pod_is_reported(tmp_path):
             fleet.wait_ready(timeout_s=120)
     finally:
         fleet.close()
+
+
+def test_running_criterion_allows_bursty_idle_at_the_window_end(tmp_path):
+    """A bursty pod may be idle when the window closes; one that stopped for
+    more than a quarter of the window is not counted as running."""
+    fleet = PodFleet([{}, {}, {}], workdir=str(tmp_path))
+    t0, t1 = 100.0, 112.0
+    steady = [99.0 + 0.1 * k for k in range(140)]                    # through t1
+    bursty = [t for t in steady if (t - 99.0) % 2.0 < 1.0]           # 1 s on / 1 s off, idle at t1
+    stopped = [t for t in steady if t < 106.0]                        # silent for the last 6 s
+    fleet.results = {0: {"times": steady}, 1: {"times": bursty}, 2: {"times": stopped}}
+    w = fleet.window(t0, t1)
+    assert [p.running for p in w.pods] == [True, True, False]
+    assert w.concurrent == 2
