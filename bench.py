@@ -426,6 +426,12 @@ def main(argv=None) -> int:
         "mean_latency_s": None if lat is None else round(lat, 5),
         "window_s": round(elapsed, 3),
         "achieved_tflops": round(agg * flops_per_image(cfg, hw) / 1e12, 2),
+        # the same as a share of the matrix pipes' peak at the measured clock
+        # (256 CUs x 4 SIMDs x 64 fp32 / 1024 bf16 FLOP per clock): amd-smi's
+        # gfx activity reads 100 % whenever any kernel runs, this does not
+        "matrix_pipe_util_pct": (round(100.0 * agg * flops_per_image(cfg, hw) /
+                                       (world * 256 * 4 * (64 if args.dtype == "fp32" else 1024) *
+                                        w.sclk_mhz * 1e6), 1) if d.cuda and w.sclk_mhz else None),
         "single_pod_inf_per_s": round(ref_sum, 3) if ref else None,
         "aggregate_vs_single_pod": round(agg / ref_sum, 3) if ref and ref_sum > 0 else None,
         "baseline": {"pods_per_gpu": BASELINE_PODS_PER_GPU, "inf_per_s_per_gpu": BASELINE_INF_PER_S_PER_GPU,
