@@ -305,6 +305,12 @@ def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, 
     return w, util, n_util, ready_s, tr
 
 
+def _hws_limit() -> int:
+    from nos_amd.gpu.kfd import hws_max_concurrent_processes
+
+    return hws_max_concurrent_processes()
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     d = Dist(args.device)
@@ -418,6 +424,9 @@ def main(argv=None) -> int:
         "gpu_util_samples": n_util,
         "rank0_sclk_mhz": w.sclk_mhz,
         "schedulable_fractional_pods_per_node": value,
+        # what bounds it on this node: the amdgpu hardware scheduler's concurrent
+        # processes per logical GPU (VMIDs), read from the driver
+        "hws_max_concurrent_processes_per_gpu": _hws_limit(),
         "schedulable_fractional_pods_per_node_sim": cp.get("schedulable_fractional_pods_per_node"),
         "schedulable_10gb_pods_per_node_sim": cp10.get("schedulable_fractional_pods_per_node",
                                                        cp.get("schedulable_fractional_pods_per_node")),
