@@ -56,3 +56,20 @@ def test_latency_table_rows_are_self_consistent():
     for t in rows:
         assert t["concurrent"] == t["pods"]
         assert t["pods_over_latency"] == pytest.approx(t["inf_per_s"], rel=1e-3)
+
+
+def test_fold_gpus_maps_every_rank_onto_the_visible_gpus(monkeypatch):
+    """NOS_AMD_BENCH_FOLD_GPUS=1 (multi-rank rehearsal on fewer GPUs): rank r's
+    pods get HIP_VISIBLE_DEVICES = r % visible GPUs; without it, the control
+    plane's own GPU index."""
+    import importlib
+    import types
+
+    sys.path.insert(0, str(REPO))
+    bench = importlib.import_module("bench")
+    args = types.SimpleNamespace()
+    envs, _ = bench.plan(args, 2, 1, 36, 2, "shared")
+    assert {e["HIP_VISIBLE_DEVICES"] for e in envs} == {"1"}
+    monkeypatch.setenv("NOS_AMD_BENCH_FOLD_GPUS", "1")
+    envs, _ = bench.plan(args, 2, 1, 36, 2, "shared")
+    assert {e["HIP_VISIBLE_DEVICES"] for e in envs} == {"0"}  # no GPU here: one visible device
