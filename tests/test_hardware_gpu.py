@@ -102,18 +102,24 @@ def test_device_plugin_slice_mask_is_enforced_in_a_child_process():
         assert len(expect) == 64   # 4 slices of a 256-CU GPU, 8 CUs on each XCD
     finally:
         smi.close()
+    # the mask is process-wide (HIP runtime): the default stream, a stream the
+    # tenant creates later and a high-priority one (as RCCL's internal streams
+    # are) must all stay on the slice's CUs
     code = (
-        "import json, sys; sys.path.insert(0, %r)\n"
+        "import json, sys, torch; sys.path.insert(0, %r)\n"
         "from nos_amd.ops import probes\n"
-        "print(json.dumps(probes.placement_summary(probes.placement(nwg=4096))))\n" % REPO)
+        "out = [probes.placement_summary(probes.placement(nwg=4096))]\n"
+        "for s in (torch.cuda.Stream(), torch.cuda.Stream(priority=-1)):\n"
+        "    out.append(probes.placement_summary(probes.placement(stream=s.cuda_stream, nwg=4096)))\n"
+        "print(json.dumps(out))\n" % REPO)
     env = dict(os.environ)
     env[C.ENV_CU_MASK] = mask   # what the kubelet puts in the container's environment
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr[-2000:]
-    summary = json.loads(out.stdout.strip().splitlines()[-1])
-    assert summary["distinct_cus"] == 64, summary
-    assert summary["cus_per_xcc"] == {str(x): 8 for x in range(8)} or \
-        summary["cus_per_xcc"] == {x: 8 for x in range(8)}, summary
+    for summary in json.loads(out.stdout.strip().splitlines()[-1]):
+        assert summary["distinct_cus"] == 64, summary
+        assert summary["cus_per_xcc"] == {str(x): 8 for x in range(8)} or \
+            summary["cus_per_xcc"] == {x: 8 for x in range(8)}, summary
 
 
 def test_trainer_pod_step_on_gpu_overlaps_bucket_launches_with_backward():
