@@ -90,7 +90,12 @@ class WindowStats:
                 "mean_latency_s": None if self.mean_latency_s is None else round(self.mean_latency_s, 5),
                 "pod_latency_min_s": round(min(lat), 5) if lat else None,
                 "pod_latency_max_s": round(max(lat), 5) if lat else None,
-                "concurrent_pods": self.concurrent, "sclk_mhz": self.sclk_mhz}
+                "concurrent_pods": self.concurrent, "sclk_mhz": self.sclk_mhz,
+                # memory isolation evidence: the most any pod allocated vs its slice
+                "pod_max_allocated_gb": max((p.info.get("max_allocated_gb") or 0.0 for p in self.pods if p.info),
+                                            default=None),
+                "pod_memory_limit_gb": next((p.info.get("memory_limit_gb") for p in self.pods
+                                             if p.info and p.info.get("memory_limit_gb")), None)}
 
 
 class _RemoteProc:
