@@ -110,3 +110,55 @@ def test_cumask_flow_across_processes(tmp_path):
                 p.kill()
         for log in logs:
             log.close()
+
+
+@pytest.mark.timeout(90)
+def test_partition_agent_binary_reports_over_the_wire(tmp_path):
+    """The partition agent as its own process (NODE_NAME, --fake-gpus, PodResources
+    over gRPC from a simulated node): it labels the node with the amd-smi GPU
+    facts and publishes the partition status annotations the gpupartitioner
+    plans from."""
+    port = _free_port()
+    url = f"http://127.0.0.1:{port}"
+    env = dict(os.environ, PYTHONPATH=str(REPO), NODE_NAME="node-p")
+    common = ["--api-server", url, "--health-probe-bind-address", "0", "--metrics-bind-address", "0"]
+    pa_cfg = tmp_path / "pa.yaml"
+    pa_cfg.write_text(yaml.safe_dump({"kind": "PartitionAgentConfig", "reportConfigIntervalSeconds": 1}))
+    sock = tmp_path / "kubelet.sock"
+    cmds = [
+        ["nos_amd.cmd.apiserver", "--port", str(port)],
+        ["nos_amd.cmd.simnode", "--name", "node-p", "--kind", "partition", "--gpus", "2",
+         "--podresources-socket", str(sock), *common],
+        ["nos_amd.cmd.partagent", "--config", str(pa_cfg), "--fake-gpus", "2", "--no-device-plugin-restart",
+         "--podresources-socket", str(sock), *common],
+    ]
+    procs: list[subprocess.Popen] = []
+    logs = []
+    try:
+        for i, c in enumerate(cmds):
+            log = open(tmp_path / f"p{i}.log", "w")
+            logs.append(log)
+            procs.append(subprocess.Popen([sys.executable, "-m", *c], env=env, stdout=log, stderr=subprocess.STDOUT))
+            if i == 0:
+                assert _wait(lambda: KubeClient(url).list("Namespace") is not None, 30, procs)
+            if i == 1:
+                assert _wait(sock.exists, 30, procs)
+        api = KubeClient(url)
+
+        def reported():
+            n = api.get("Node", "node-p")
+            ann = ko.annotations(n)
+            return (ko.labels(n).get(C.LABEL_AMD_COUNT) == "2"
+                    and any(k.startswith("nos.nebuly.com/status-gpu-0-") for k in ann)
+                    and any(k.startswith("nos.nebuly.com/status-gpu-1-") for k in ann))
+        assert _wait(reported, 40, procs), (tmp_path / "p2.log").read_text()[-3000:]
+    finally:
+        for p in reversed(procs):
+            p.terminate()
+        for p in reversed(procs):
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        for log in logs:
+            log.close()
