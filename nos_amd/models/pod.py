@@ -18,14 +18,18 @@ loads YOLOS-small in fp32 and runs inferences back to back forever; the
   wall-clock window.
 
 Precision: ``fp32`` (default, the reference's HF default precision) runs
-exact fp32: hipBLASLt fp32 GEMMs and the gfx950 fp32-MFMA flash attention of
-``libnos_hip.so`` (``csrc/hip/attention_f32.hip``); ``bf16`` runs the bf16
+exact fp32: the gfx950 fp32-MFMA GEMMs with fused epilogues
+(``csrc/hip/gemm_f32.hip``) and flash attention
+(``csrc/hip/attention_f32.hip``) of ``libnos_hip.so``; ``bf16`` runs the bf16
 gfx950 kernels (fused-epilogue GEMMs, bf16 flash attention, LayerNorm).
 
 Status protocol (``--status``: a float64 memory-mapped file, see
 :class:`StatusBoard`): row 0 = [stop flag, ...]; row 1+slot = [state, count,
 last completion time, pid].  On stop the pod writes all completion times to
-``<out>/pod-<slot>.json`` and exits 0.
+``<out>/pod-<slot>.json`` and exits 0.  A pod whose launcher is gone (the
+orchestrator was killed) exits too: the kernel sends it SIGTERM
+(``PR_SET_PDEATHSIG``) and the loop checks its parent, so no orphan keeps
+running kernels on the GPU.
 """
 from __future__ import annotations
 
@@ -35,6 +39,7 @@ import os
 import sys
 import time
 from pathlib import Path
+from typing import Callable
 
 import numpy as np
 
@@ -79,7 +84,7 @@ def _build(dtype: str, seed: int, hw, device: str = "cuda"):
     from .yolos import YolosConfig, YolosDetector, make_demo_input
 
     cfg = YolosConfig.small() if device == "cuda" else YolosConfig.test()
-    if dtype == "fp32":  # exact fp32: hipBLASLt fp32 GEMMs + the gfx950 fp32 MFMA attention
+    if dtype == "fp32":  # exact fp32: the gfx950 fp32-MFMA GEMMs and attention
         if device == "cuda":
             from ..ops import _lib
 
@@ -100,6 +105,20 @@ def _build(dtype: str, seed: int, hw, device: str = "cuda"):
     return m, x
 
 
+def _die_with_parent() -> Callable[[], bool]:
+    """SIGTERM this process when its parent exits (Linux prctl), and return a
+    check for the case the signal cannot cover (parent gone before prctl)."""
+    ppid0 = os.getppid()
+    try:
+        import ctypes
+        import signal
+
+        ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGTERM), 0, 0, 0)  # PR_SET_PDEATHSIG
+    except Exception:  # not Linux / no libc symbol: the getppid check below still works
+        pass
+    return lambda: os.getppid() != ppid0
+
+
 class _CpuTenant:
     def __init__(self, model, x):
         self.model, self.x = model, x
@@ -114,6 +133,7 @@ class _CpuTenant:
 def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool = True, seed: int = 0,
             warmup: int = 3, device: str = "cuda") -> int:
     """``device="cpu"`` runs the tiny test config on the CPU (protocol tests)."""
+    orphaned = _die_with_parent()
     board = StatusBoard(status)
     row = board.row(slot)
     row[3] = os.getpid()
@@ -173,6 +193,9 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
         phase0 = time.monotonic() - (on_s + off_s) * ((slot * 0.618) % 1.0)
         with torch.no_grad():
             while not board.stopped():
+                if orphaned():
+                    print(f"[pod {slot}] launcher gone: exiting", file=sys.stderr, flush=True)
+                    return 1
                 if off_s > 0 and (time.monotonic() - phase0) % (on_s + off_s) >= on_s:
                     time.sleep(0.005)
                     continue

@@ -192,6 +192,12 @@ def _launcher_main() -> int:
         except Exception as e:
             out = {"error": repr(e)}
         print(json.dumps(out), flush=True)
+    # stdin closed without "exit": the orchestrator died (killed at its time
+    # limit, crashed) -- take the pods down with it instead of leaving them on the GPU
+    for p in procs.values():
+        if p.poll() is None:
+            p.kill()
+            p.wait()
     return 0
 
 

@@ -2,6 +2,7 @@
 
 The pods run the tiny YOLOS test config on the CPU here; on a GPU box the same
 protocol runs the fp32 YOLOS-small pods of bench.py."""
+import os
 import time
 
 import pytest
@@ -83,3 +84,50 @@ def test_running_criterion_allows_bursty_idle_at_the_window_end(tmp_path):
     w = fleet.window(t0, t1)
     assert [p.running for p in w.pods] == [True, True, False]
     assert w.concurrent == 2
+
+
+def _alive(pid: int) -> bool:
+    """Running (not gone, not a zombie nobody reaped yet)."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+    except FileNotFoundError:
+        return False
+
+
+def _wait_gone(pids, timeout_s=30.0) -> list[int]:
+    deadline = time.monotonic() + timeout_s
+    while time.monotonic() < deadline:
+        left = [p for p in pids if _alive(p)]
+        if not left:
+            return []
+        time.sleep(0.1)
+    return [p for p in pids if _alive(p)]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("how", ["orchestrator_exits", "launcher_killed"])
+def test_pods_do_not_outlive_the_orchestrator(tmp_path, how):
+    """A bench killed at its time limit must not leave pods running kernels on
+    the GPU: the launcher kills its pods when its stdin closes, and a pod whose
+    launcher dies gets SIGTERM (PR_SET_PDEATHSIG) / sees its parent change."""
+    import signal
+
+    launcher = PodLauncher()
+    fleet = PodFleet([{}, {}], dtype="fp32", workdir=str(tmp_path), device="cpu", launcher=launcher,
+                     extra_env={"OMP_NUM_THREADS": "1"})
+    try:
+        fleet.start()
+        fleet.wait_ready(timeout_s=240)
+        pids = [int(fleet.board.row(i)[3]) for i in range(2)]
+        assert all(_alive(p) for p in pids)
+        if how == "orchestrator_exits":
+            launcher.p.stdin.close()  # what the orchestrator's death looks like to the launcher
+        else:
+            launcher.p.send_signal(signal.SIGKILL)
+        launcher.p.wait(timeout=30)
+        assert _wait_gone(pids) == []
+    finally:
+        for p in [int(fleet.board.row(i)[3]) for i in range(2)] if fleet.board is not None else []:
+            if p and _alive(p):
+                os.kill(p, signal.SIGKILL)
