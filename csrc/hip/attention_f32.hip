@@ -57,8 +57,8 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_ba
 // (batch, head, q-block) and merge (m, l, O) through LDS at the end -- two
 // waves per SIMD from ONE workgroup, so a single pod (162 q-blocks for 256
 // CUs) still overlaps one wave's softmax with the other's MFMAs.
-template <int W, int KVB, int G>
-__global__ __launch_bounds__(64 * W * G) void attn_fwd_f32_d64_kernel(
+template <int W, int KVB, int G, int OCC = 1>  // OCC: workgroups per CU the register budget must allow
+__global__ __launch_bounds__(64 * W * G, OCC) void attn_fwd_f32_d64_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, float* __restrict__ o,
     int B, int H, int Sq, int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, int nqb) {
   constexpr int QBLK = 32 * W;
@@ -259,24 +259,29 @@ __global__ __launch_bounds__(64 * W * G) void attn_fwd_f32_d64_kernel(
   }
 }
 
-template <int W, int KVB, int G>
+template <int W, int KVB, int G, int OCC = 1>
 int launch(const float* q, const float* k, const float* v, float* o, int B, int H, int Sq, int Skv, int ld_in,
            long long bs_in, int ld_out, long long bs_out, float c, hipStream_t stream) {
   const int nqb = (Sq + 32 * W - 1) / (32 * W);
   const long long nwg = (long long)B * H * nqb;
   if (nwg > (1LL << 30)) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)G * 2 * 2 * KVB * ROW_BYTES;
-  hipLaunchKernelGGL((attn_fwd_f32_d64_kernel<W, KVB, G>), dim3((unsigned)nwg), dim3(64 * W * G), lds, stream, q,
+  hipLaunchKernelGGL((attn_fwd_f32_d64_kernel<W, KVB, G, OCC>), dim3((unsigned)nwg), dim3(64 * W * G), lds, stream, q,
                      k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
   return (int)hipGetLastError();
 }
 
-int g_variant = 0;  // 0 auto, 1: 4 waves x 64-key tiles, 2: the same with 2 wave groups (split keys)
+// 0 auto, 1: 4 waves x 64-key tiles, 2: the same with 2 wave groups (split keys),
+// 3: 4 waves x 32-key tiles (half the LDS: more co-resident workgroups),
+// 4: 2 waves x 64-key tiles (64-query blocks), 5: 8 waves x 64-key tiles,
+// 6: variant 3 register-capped for 3 workgroups per CU (127 VGPRs, no
+//    AGPRs, no scratch: 4 waves per SIMD; the same cap on variant 1 spills)
+int g_variant = 0;
 
 }  // namespace
 
 NOS_API int nos_attn_f32_set_variant(int variant) {
-  if (variant < 0 || variant > 2) return (int)hipErrorInvalidValue;
+  if (variant < 0 || variant > 6) return (int)hipErrorInvalidValue;
   g_variant = variant;
   return 0;
 }
@@ -292,10 +297,15 @@ NOS_API int nos_attn_fwd_f32_d64(const float* q, const float* k, const float* v,
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) return (int)hipErrorInvalidValue;
   const float c = scale * 1.4426950408889634f;
   // auto: 2 wave groups when the grid leaves CUs without a workgroup (one pod
-  // at B=1: 162 workgroups, 237 vs 267 us), else 1 (B=8: 1357 vs 1399 us;
-  // profiles/r02_attention_f32.json)
+  // at B=1: 162 workgroups, 240 vs 269 us), else 32-key tiles at 4 waves per
+  // SIMD (B=8: 1298 vs 1357 us for 64-key tiles at 2;
+  // profiles/r02_attention_f32.json, r02_attention_f32_tilings.json)
   const long long nwg = (long long)B * H * ((Sq + 127) / 128);
-  const int var = g_variant != 0 ? g_variant : nwg <= 256 ? 2 : 1;
+  const int var = g_variant != 0 ? g_variant : nwg <= 256 ? 2 : 6;
   if (var == 1) return launch<4, 64, 1>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
+  if (var == 3) return launch<4, 32, 1>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
+  if (var == 4) return launch<2, 64, 1>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
+  if (var == 5) return launch<8, 64, 1>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
+  if (var == 6) return launch<4, 32, 1, 3>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
   return launch<4, 64, 2>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
 }

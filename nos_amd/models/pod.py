@@ -156,13 +156,15 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             # fewest rounds of tiles (bf16 GEMM latency policy: fc2 19.7 -> 14.2 us
             # at batch 1) and two attention wave groups when its grid leaves CUs
             # idle (the kernel's auto rule).  A fractional slice shares the CUs
-            # with other pods: least-work tiles and one wave group (8 pods x 36 GB:
-            # 311 vs 302 inf/s, profiles/r02_attention_f32.json).  The env
-            # variables override for A/B runs.
+            # with other pods: least-work tiles and one wave group on 32-key
+            # tiles, whose 32 KB of LDS leave room for other pods' workgroups on
+            # the CU (8 pods x 36 GB: 317 vs 310 inf/s for 64-key tiles, 302 for
+            # two groups; profiles/r02_attention_f32_tilings.json,
+            # r02_attention_f32.json).  The env variables override for A/B runs.
             set_gemm_policy(os.environ.get("NOS_AMD_GEMM_POLICY") or ("latency" if whole else "throughput"))
             if os.environ.get("NOS_AMD_GEMM_F32_POLICY"):
                 set_gemm_f32_policy(os.environ["NOS_AMD_GEMM_F32_POLICY"])
-            set_attention_f32_variant(os.environ.get("NOS_AMD_ATTN_F32_VARIANT") or ("auto" if whole else "w4k64"))
+            set_attention_f32_variant(os.environ.get("NOS_AMD_ATTN_F32_VARIANT") or ("auto" if whole else "w4k32"))
         m, x = _build(dtype, seed, demo_input_hw(), device)
         if gpu:
             s = torch.cuda.Stream()

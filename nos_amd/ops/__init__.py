@@ -155,8 +155,10 @@ def set_attention_f32_variant(variant: str) -> None:
     """fp32 attention tiling: ``"auto"`` (default), ``"w4k64"`` (4 waves x 64-key
     LDS tiles) or ``"w4k64g2"`` (two such wave groups per workgroup on
     interleaved key tiles, merged at the end: 2 waves per SIMD from one
-    workgroup)."""
-    code = {"auto": 0, "w4k64": 1, "w4k64g2": 2}[variant]
+    workgroup); A/B tilings: ``"w4k32"`` (32-key tiles, half the LDS),
+    ``"w2k64"`` (64-query blocks), ``"w8k64"`` (256-query blocks), ``"w4k32o4"`` (32-key tiles in 127
+    VGPRs: 4 waves per SIMD)."""
+    code = {"auto": 0, "w4k64": 1, "w4k64g2": 2, "w4k32": 3, "w2k64": 4, "w8k64": 5, "w4k32o4": 6}[variant]
     _lib.check(_lib.lib().nos_attn_f32_set_variant(code), "nos_attn_f32_set_variant")
 
 
