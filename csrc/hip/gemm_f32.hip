@@ -223,10 +223,13 @@ int launch_t(const float* A, int lda, const float* W, int ldw, const float* bias
 //    other pods fill the CUs a small grid leaves idle;
 //  * 1 = latency (default): the tile minimising
 //    rounds x per-tile time, with workgroups per CU {2, 3, 4} and relative
-//    per-FLOP efficiency {1.0, 0.9, 0.75} for 128x128 / 64x128 / 64x64.
+//    per-FLOP efficiency {1.0, 0.9, 0.75} for 128x128 / 64x128 / 64x64;
+//  * 2 = small: always 64x64 (33 KB of LDS, <= 64 VGPRs: the most room for
+//    co-running pods' workgroups on a CU).
 int g_policy = 1;
 
 int pick_tile(int M, int N) {
+  if (g_policy == 2) return 2;
   if (g_policy == 0) {
     if (M >= 128 && N >= 128) return 0;
     if (N >= 128) return 1;
@@ -275,7 +278,7 @@ int launch(const float* A, int lda, const float* W, int ldw, const float* bias, 
 }  // namespace
 
 NOS_API int nos_gemm_f32_set_policy(int policy) {
-  if (policy != 0 && policy != 1) return (int)hipErrorInvalidValue;
+  if (policy < 0 || policy > 2) return (int)hipErrorInvalidValue;
   g_policy = policy;
   return 0;
 }

@@ -162,8 +162,10 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             # two groups; profiles/r02_attention_f32_tilings.json,
             # r02_attention_f32.json).  The env variables override for A/B runs.
             set_gemm_policy(os.environ.get("NOS_AMD_GEMM_POLICY") or ("latency" if whole else "throughput"))
-            if os.environ.get("NOS_AMD_GEMM_F32_POLICY"):
-                set_gemm_f32_policy(os.environ["NOS_AMD_GEMM_F32_POLICY"])
+            # fp32 GEMMs: fewest rounds for a whole GPU; 64x64 tiles (33 KB LDS,
+            # <= 64 VGPRs) on a shared one (8 pods: 318.0 / 318.1 vs 317.3 / 314.2
+            # inf/s, profiles/r02_f32_gemm_policy_fleet_ab.json)
+            set_gemm_f32_policy(os.environ.get("NOS_AMD_GEMM_F32_POLICY") or ("latency" if whole else "small"))
             set_attention_f32_variant(os.environ.get("NOS_AMD_ATTN_F32_VARIANT") or ("auto" if whole else "w4k32"))
         m, x = _build(dtype, seed, demo_input_hw(), device)
         if gpu:

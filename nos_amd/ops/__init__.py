@@ -146,8 +146,9 @@ def set_gemm_persistent(wgs_per_cu: int) -> None:
 def set_gemm_f32_policy(policy: str) -> None:
     """fp32 GEMM tiles: ``"latency"`` (default; fewest rounds of tiles over
     the CUs) or ``"throughput"`` (most MFMA-efficient tile; other co-running
-    pods fill the CUs a small grid leaves idle)."""
-    _lib.check(_lib.lib().nos_gemm_f32_set_policy({"throughput": 0, "latency": 1}[policy]),
+    pods fill the CUs a small grid leaves idle) or ``"small"`` (always 64x64:
+    the least LDS and registers per workgroup)."""
+    _lib.check(_lib.lib().nos_gemm_f32_set_policy({"throughput": 0, "latency": 1, "small": 2}[policy]),
                "nos_gemm_f32_set_policy")
 
 

@@ -165,7 +165,7 @@ def test_attention_fp32_strided_and_large_logits():
     (3401, 1152, 384, None, False), (3401, 1536, 384, "gelu", False), (3401, 384, 1536, None, True),
     (3401, 384, 384, None, True), (100, 92, 384, "relu", False), (100, 4, 384, None, False), (257, 200, 96, None, True),
     (8 * 3401, 384, 1536, None, True), (1, 8, 32, None, False), (3401, 100, 384, None, False)])
-@pytest.mark.parametrize("policy", ["throughput", "latency"])
+@pytest.mark.parametrize("policy", ["throughput", "latency", "small"])
 def test_linear_fp32_exact(M, N, K, act, resid, policy):
     """fp32 MFMA GEMM against an fp64 reference (exact-f32 tolerance), every tile shape."""
     x = torch.randn(M, K, device=DEV)
