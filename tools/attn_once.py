@@ -15,10 +15,13 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=8)
     ap.add_argument("--dtypes", default="fp32,bf16")
+    ap.add_argument("--variant", default="auto", help="fp32 attention tiling (ops.set_attention_f32_variant)")
     a = ap.parse_args()
     import torch
 
     from nos_amd import ops
+
+    ops.set_attention_f32_variant(a.variant)
 
     for dt in a.dtypes.split(","):
         t = {"fp32": torch.float32, "bf16": torch.bfloat16}[dt]
