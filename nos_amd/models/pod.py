@@ -119,6 +119,27 @@ def _die_with_parent() -> Callable[[], bool]:
     return lambda: os.getppid() != ppid0
 
 
+def kernel_config(memory_fraction: float | None, env: dict | None = None) -> dict[str, str]:
+    """Kernel configs a pod picks from its slice (and ``NOS_AMD_*`` overrides
+    for A/B runs).
+
+    A pod owning the whole GPU wants the fewest rounds of tiles (bf16 GEMM
+    latency policy: fc2 19.7 -> 14.2 us at batch 1) and two attention wave
+    groups when its grid leaves CUs idle (the kernel's auto rule).  A
+    fractional slice shares the CUs with other pods, so per-workgroup
+    footprint wins over per-tile efficiency: bf16 least-work tiles, fp32
+    GEMMs on 64x64 tiles (33 KB LDS, <= 64 VGPRs; 8 pods: 318.0 / 318.1 vs
+    317.3 / 314.2 inf/s, profiles/r02_f32_gemm_policy_fleet_ab.json) and fp32
+    attention with one wave group on 32-key tiles, whose 32 KB LDS ring
+    leaves room for other pods' workgroups (317 vs 310 inf/s for 64-key
+    tiles, 302 for two groups; profiles/r02_attention_f32_tilings.json)."""
+    env = os.environ if env is None else env
+    whole = memory_fraction is None or memory_fraction >= 0.99
+    return {"gemm_bf16": env.get("NOS_AMD_GEMM_POLICY") or ("latency" if whole else "throughput"),
+            "gemm_f32": env.get("NOS_AMD_GEMM_F32_POLICY") or ("latency" if whole else "small"),
+            "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or ("auto" if whole else "w4k32")}
+
+
 class _CpuTenant:
     def __init__(self, model, x):
         self.model, self.x = model, x
@@ -151,22 +172,10 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             torch.backends.cuda.matmul.allow_tf32 = False  # true fp32 GEMMs (no reduced-precision shortcut)
             from ..ops import set_attention_f32_variant, set_gemm_f32_policy, set_gemm_policy
 
-            whole = frac is None or frac >= 0.99
-            # kernel configs follow the slice.  A pod owning the whole GPU wants the
-            # fewest rounds of tiles (bf16 GEMM latency policy: fc2 19.7 -> 14.2 us
-            # at batch 1) and two attention wave groups when its grid leaves CUs
-            # idle (the kernel's auto rule).  A fractional slice shares the CUs
-            # with other pods: least-work tiles and one wave group on 32-key
-            # tiles, whose 32 KB of LDS leave room for other pods' workgroups on
-            # the CU (8 pods x 36 GB: 317 vs 310 inf/s for 64-key tiles, 302 for
-            # two groups; profiles/r02_attention_f32_tilings.json,
-            # r02_attention_f32.json).  The env variables override for A/B runs.
-            set_gemm_policy(os.environ.get("NOS_AMD_GEMM_POLICY") or ("latency" if whole else "throughput"))
-            # fp32 GEMMs: fewest rounds for a whole GPU; 64x64 tiles (33 KB LDS,
-            # <= 64 VGPRs) on a shared one (8 pods: 318.0 / 318.1 vs 317.3 / 314.2
-            # inf/s, profiles/r02_f32_gemm_policy_fleet_ab.json)
-            set_gemm_f32_policy(os.environ.get("NOS_AMD_GEMM_F32_POLICY") or ("latency" if whole else "small"))
-            set_attention_f32_variant(os.environ.get("NOS_AMD_ATTN_F32_VARIANT") or ("auto" if whole else "w4k32"))
+            cfg = kernel_config(frac, os.environ)
+            set_gemm_policy(cfg["gemm_bf16"])
+            set_gemm_f32_policy(cfg["gemm_f32"])
+            set_attention_f32_variant(cfg["attention_f32"])
         m, x = _build(dtype, seed, demo_input_hw(), device)
         if gpu:
             s = torch.cuda.Stream()

@@ -131,3 +131,22 @@ def test_pods_do_not_outlive_the_orchestrator(tmp_path, how):
         for p in [int(fleet.board.row(i)[3]) for i in range(2)] if fleet.board is not None else []:
             if p and _alive(p):
                 os.kill(p, signal.SIGKILL)
+
+
+def test_pod_kernel_config_follows_the_slice():
+    from nos_amd.models.pod import kernel_config
+
+    whole = kernel_config(None, {})
+    assert whole == {"gemm_bf16": "latency", "gemm_f32": "latency", "attention_f32": "auto"}
+    assert kernel_config(1.0, {}) == whole
+    frac = kernel_config(36 / 288, {})
+    assert frac == {"gemm_bf16": "throughput", "gemm_f32": "small", "attention_f32": "w4k32"}
+    # A/B overrides win over the slice rule
+    assert kernel_config(0.125, {"NOS_AMD_ATTN_F32_VARIANT": "w4k64"})["attention_f32"] == "w4k64"
+    # every name is one the native library accepts
+    from nos_amd import ops
+    import inspect
+
+    src = inspect.getsource(ops.set_attention_f32_variant) + inspect.getsource(ops.set_gemm_f32_policy)
+    for v in (*whole.values(), *frac.values()):
+        assert f'"{v}"' in src or v in ("latency", "throughput")
