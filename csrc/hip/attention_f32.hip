@@ -275,13 +275,14 @@ int launch(const float* q, const float* k, const float* v, float* o, int B, int 
 // 3: 4 waves x 32-key tiles (half the LDS: more co-resident workgroups),
 // 4: 2 waves x 64-key tiles (64-query blocks), 5: 8 waves x 64-key tiles,
 // 6: variant 3 register-capped for 3 workgroups per CU (127 VGPRs, no
-//    AGPRs, no scratch: 4 waves per SIMD; the same cap on variant 1 spills)
+//    AGPRs, no scratch: 4 waves per SIMD; the same cap on variant 1 spills),
+// 7: two wave groups on 32-key tiles (64 KB LDS ring)
 int g_variant = 0;
 
 }  // namespace
 
 NOS_API int nos_attn_f32_set_variant(int variant) {
-  if (variant < 0 || variant > 6) return (int)hipErrorInvalidValue;
+  if (variant < 0 || variant > 7) return (int)hipErrorInvalidValue;
   g_variant = variant;
   return 0;
 }
@@ -307,5 +308,6 @@ NOS_API int nos_attn_fwd_f32_d64(const float* q, const float* k, const float* v,
   if (var == 4) return launch<2, 64, 1>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
   if (var == 5) return launch<8, 64, 1>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
   if (var == 6) return launch<4, 32, 1, 3>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
+  if (var == 7) return launch<4, 32, 2>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
   return launch<4, 64, 2>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
 }

@@ -158,8 +158,8 @@ def set_attention_f32_variant(variant: str) -> None:
     interleaved key tiles, merged at the end: 2 waves per SIMD from one
     workgroup); A/B tilings: ``"w4k32"`` (32-key tiles, half the LDS),
     ``"w2k64"`` (64-query blocks), ``"w8k64"`` (256-query blocks), ``"w4k32o4"`` (32-key tiles in 127
-    VGPRs: 4 waves per SIMD)."""
-    code = {"auto": 0, "w4k64": 1, "w4k64g2": 2, "w4k32": 3, "w2k64": 4, "w8k64": 5, "w4k32o4": 6}[variant]
+    VGPRs: 4 waves per SIMD), ``"w4k32g2"`` (two groups on 32-key tiles)."""
+    code = {"auto": 0, "w4k64": 1, "w4k64g2": 2, "w4k32": 3, "w2k64": 4, "w8k64": 5, "w4k32o4": 6, "w4k32g2": 7}[variant]
     _lib.check(_lib.lib().nos_attn_f32_set_variant(code), "nos_attn_f32_set_variant")
 
 

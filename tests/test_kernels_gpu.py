@@ -133,7 +133,7 @@ def test_attention_strided_views():
     assert out[..., hid:].abs().max().item() == 0  # padding untouched
 
 
-@pytest.mark.parametrize("variant", ["w4k64", "w4k64g2", "w4k32", "w4k32o4", "w2k64", "w8k64", "auto"])
+@pytest.mark.parametrize("variant", ["w4k64", "w4k64g2", "w4k32", "w4k32o4", "w4k32g2", "w2k64", "w8k64", "auto"])
 @pytest.mark.parametrize("B,S,H", [(1, 3401, 6), (2, 77, 3), (1, 1, 1), (1, 33, 2), (3, 300, 2), (1, 129, 1)])
 def test_attention_fp32_exact(B, S, H, variant):
     """fp32 MFMA attention against an fp64 reference: exact-f32 numerics."""
