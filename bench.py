@@ -116,7 +116,9 @@ def plan(args, world: int, local: int, slice_gb: int, pods: int, mode: str) -> t
         # GPU r % visible GPUs, as the rank itself does (Dist.init_gpu)
         import torch
 
-        gpu = str(local % max(1, torch.cuda.device_count()))  # counts devices without initialising HIP
+        # may initialise HIP (when amdsmi is unusable): main() starts the pod
+        # launcher before the first plan(), so no pod is forked from a GPU process
+        gpu = str(local % max(1, torch.cuda.device_count()))
         envs = [{**e, "HIP_VISIBLE_DEVICES": gpu} for e in envs]
     return envs, info
 
@@ -313,6 +315,11 @@ def _hws_limit() -> int:
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    from nos_amd.podbench import PodLauncher
+
+    # first of all: pods are forked by this launcher, which must never come
+    # from a process that has touched the GPU (plan() may count devices)
+    launcher = PodLauncher()
     d = Dist(args.device)
     world, rank, local = d.world, d.rank, d.local
     if world != args.gpus:
@@ -335,9 +342,6 @@ def main(argv=None) -> int:
                    for mode in args.table_modes.split(",") if args.table
                    for n in map(int, args.table.split(","))]
 
-    from nos_amd.podbench import PodLauncher
-
-    launcher = PodLauncher()  # started before this rank touches the GPU: pods never fork from a GPU process
     d.init_gpu()
     sampler = UtilSampler(d.device) if d.cuda else None
     coll = None

@@ -383,11 +383,18 @@ class PartitionNode:
         if not self.gpus or not slices:
             return False
         required = dict(slices)
-        # already-free partitions count first: no GPU is switched for demand they cover
+        # already-free partitions count first: no GPU is switched for demand they
+        # cover.  covered[gpu][p] remembers how much demand each GPU's free
+        # partitions absorbed, so that a later switch of that GPU (which destroys
+        # its free partitions: modes are GPU-wide) puts that demand back
+        # (mig/node.go:145-177 counts free devices after each GPU's update)
+        covered: dict[int, dict] = {}
         for g in self.gpus:
             for p, n in g.free.items():
                 if p in required and n > 0:
-                    required[p] -= n
+                    take = min(n, required[p])
+                    covered.setdefault(g.index, {})[p] = take
+                    required[p] -= take
                     if required[p] <= 0:
                         del required[p]
         updated = False
@@ -403,6 +410,11 @@ class PartitionNode:
                 updated = True
                 if whole and not self._is_whole(g):
                     whole_idle -= 1
+                # demand the destroyed free partitions covered is lacking again
+                for p, n in covered.pop(g.index, {}).items():
+                    lost = min(n, max(0, before.get(p, 0) - g.free.get(p, 0)))
+                    if lost > 0:
+                        required[p] = required.get(p, 0) + lost
                 for p, n in g.free.items():
                     gained = n - before.get(p, 0)
                     if p in required and gained > 0:

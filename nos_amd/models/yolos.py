@@ -244,9 +244,11 @@ class YolosDetector(nn.Module):
         return self._heads(y, lin)
 
     def _forward_torch(self, pixel_values: torch.Tensor, native_attention: bool = False):
-        """Eager PyTorch (numerics reference).  ``native_attention``: the exact-fp32
-        path of the fp32 pods -- hipBLASLt fp32 GEMMs, the gfx950 fp32 MFMA
-        flash attention (``nos_attn_fwd_f32_d64``) on the fused QKV output."""
+        """Eager PyTorch (numerics reference): torch GEMMs + SDPA.
+        ``native_attention`` swaps in the gfx950 fp32 MFMA flash attention
+        (``nos_attn_fwd_f32_d64``) on the fused QKV output, to test attention
+        alone; the fp32 pods themselves run :meth:`_forward_native` (the
+        exact-fp32 MFMA GEMMs of ``gemm_f32.hip`` + that attention)."""
         cfg = self.cfg
         nh, hd = cfg.num_attention_heads, cfg.head_dim
 

@@ -73,25 +73,13 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         return _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K)
     if x2.stride(-1) != 1 or weight.stride(-1) != 1 or K % 64 or x.dtype != torch.bfloat16:
         raise ValueError("native linear needs bf16, unit inner stride and K % 64 == 0")
-    if out is None:
-        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
-    epi = 0
-    if bias is not None:
-        epi |= EPI_BIAS
-    if act == "gelu":
-        epi |= EPI_GELU
-    elif act == "relu":
-        epi |= EPI_RELU
-    r2 = None
-    if residual is not None:
-        epi |= EPI_RESID
-        r2 = residual.reshape(-1, N)
-    o2 = out.reshape(-1, N)
+    o2, r2 = _gemm_io(x, weight, out, residual, M, N, K)
+    epi = _epi(bias, act, residual)
     rc = _lib.lib().nos_gemm_bf16(x2.data_ptr(), x2.stride(0), weight.data_ptr(), weight.stride(0),
                                   _ptr(bias), _ptr(r2), r2.stride(0) if r2 is not None else 0,
                                   o2.data_ptr(), o2.stride(0), M, N, K, epi, max_wg, _stream())
     _lib.check(rc, "nos_gemm_bf16")
-    return out.reshape(*x.shape[:-1], N)
+    return o2.view(*x.shape[:-1], N)
 
 
 def _epi(bias, act, residual) -> int:
@@ -106,6 +94,34 @@ def _check_f32(**ts) -> None:
             raise ValueError(f"native fp32 GEMM: {name} must be fp32 with unit inner stride")
 
 
+def _gemm_io(x: torch.Tensor, weight: torch.Tensor, out: torch.Tensor | None, residual: torch.Tensor | None,
+             M: int, N: int, K: int) -> tuple[torch.Tensor, torch.Tensor | None]:
+    """Shape/dtype checks every native GEMM does before launching: the kernels
+    write M x N elements of x's dtype through raw pointers, so a short, mistyped
+    or non-viewable ``out`` would corrupt GPU memory or silently lose the result.
+    Returns (out as a [M, N] view, residual as [M, N] or None)."""
+    if weight.dim() != 2 or weight.shape[1] != K:
+        raise ValueError(f"weight must be [N, {K}], got {tuple(weight.shape)}")
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    if out.dtype != x.dtype or out.device != x.device:
+        raise ValueError(f"out must be {x.dtype} on {x.device}, got {out.dtype} on {out.device}")
+    if out.shape[-1] != N or out.numel() != M * N:
+        raise ValueError(f"out must hold [{M}, {N}], got {tuple(out.shape)}")
+    try:
+        o2 = out.view(-1, N)
+    except RuntimeError as e:  # a reshape copy would be written and dropped
+        raise ValueError("out must be viewable as [M, N] (no copy)") from e
+    if o2.stride(-1) != 1:
+        raise ValueError("out must have unit inner stride")
+    r2 = None
+    if residual is not None:
+        if residual.shape[-1] != N or residual.numel() != M * N or residual.dtype != x.dtype:
+            raise ValueError(f"residual must be [{M}, {N}] of {x.dtype}, got {tuple(residual.shape)} {residual.dtype}")
+        r2 = residual.reshape(-1, N)
+    return o2, r2
+
+
 def _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K):
     """Exact-fp32 MFMA GEMM (csrc/hip/gemm_f32.hip) with fused bias/act/residual."""
     _check_f32(x=x2, weight=weight, bias=bias)
@@ -113,16 +129,13 @@ def _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K):
         raise ValueError("native fp32 linear needs K % 32 == 0")
     if bias is not None and not bias.is_contiguous():
         raise ValueError("bias must be contiguous")
-    if out is None:
-        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
-    r2 = residual.reshape(-1, N) if residual is not None else None
+    o2, r2 = _gemm_io(x, weight, out, residual, M, N, K)
     _check_f32(residual=r2)
-    o2 = out.reshape(-1, N)
     rc = _lib.lib().nos_gemm_f32(x2.data_ptr(), x2.stride(0), weight.data_ptr(), weight.stride(0), _ptr(bias),
                                  _ptr(r2), r2.stride(0) if r2 is not None else 0, o2.data_ptr(), o2.stride(0),
                                  M, N, K, _epi(bias, act, residual), _stream())
     _lib.check(rc, "nos_gemm_f32")
-    return out.reshape(*x.shape[:-1], N)
+    return o2.view(*x.shape[:-1], N)
 
 
 def set_gemm_policy(policy: str) -> None:
@@ -205,25 +218,21 @@ def linear_ln(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Ten
         _check_f32(x=x2, weight=wg, c1=c1, c2=c2)
         if K % 32:
             raise ValueError("native fp32 linear_ln needs K % 32 == 0")
-        if out is None:
-            out = torch.empty((M, N), dtype=x.dtype, device=x.device)
-        o2 = out.reshape(-1, N)
+        o2, _ = _gemm_io(x, wg, out, None, M, N, K)
         rc = _lib.lib().nos_gemm_ln_f32(x2.data_ptr(), x2.stride(0), wg.data_ptr(), wg.stride(0), c1.data_ptr(),
                                         c2.data_ptr(), o2.data_ptr(), o2.stride(0), M, N, K, _epi(None, act, None),
                                         float(eps), _stream())
         _lib.check(rc, "nos_gemm_ln_f32")
-        return out.reshape(*x.shape[:-1], N)
+        return o2.view(*x.shape[:-1], N)
     if x2.stride(-1) != 1 or K % 64 or x.dtype != torch.bfloat16:
         raise ValueError("native linear_ln needs bf16, unit inner stride and K % 64 == 0")
-    if out is None:
-        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    o2, _ = _gemm_io(x, wg, out, None, M, N, K)
     epi = EPI_GELU if act == "gelu" else (EPI_RELU if act == "relu" else 0)
-    o2 = out.reshape(-1, N)
     rc = _lib.lib().nos_gemm_ln_bf16(x2.data_ptr(), x2.stride(0), wg.data_ptr(), wg.stride(0), c1.data_ptr(),
                                      c2.data_ptr(), o2.data_ptr(), o2.stride(0), M, N, K, epi, float(eps), max_wg,
                                      _stream())
     _lib.check(rc, "nos_gemm_ln_bf16")
-    return out.reshape(*x.shape[:-1], N)
+    return o2.view(*x.shape[:-1], N)
 
 
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12,

@@ -20,6 +20,7 @@
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
 import time
@@ -95,6 +96,8 @@ class GradBucketer:
         self._where = {id(p): i for i, b in enumerate(self.buckets) for p in b.params}
         self._ready = [0] * len(self.buckets)
         self._works: list = [None] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
+        self._sync_enabled = True
         self._hooks: list = []
         self._lock = threading.Lock()  # hooks of different devices run on different autograd threads
         self.launched_in_backward = 0  # bucket collectives started from a gradient hook (all steps)
@@ -150,12 +153,32 @@ class GradBucketer:
             self._pack(b)
             self._works[i] = dist.all_reduce(b.flat, group=self.group, async_op=True) if self.world > 1 else None
 
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient accumulation (DDP's ``no_sync``): backward passes inside
+        this context only accumulate into ``p.grad``; the next backward outside
+        it launches the buckets with the accumulated gradients."""
+        prev, self._sync_enabled = self._sync_enabled, False
+        try:
+            yield
+        finally:
+            self._sync_enabled = prev
+
     def _on_grad(self, p: torch.Tensor) -> None:
+        if not self._sync_enabled:
+            return
         i = self._where[id(p)]
         with self._lock:
+            if self._launched[i]:
+                # a second backward before finish(): its gradients would be silently
+                # dropped (the bucket already holds the first micro-batch's)
+                raise RuntimeError(
+                    f"GradBucketer: bucket {i} was already launched in this step; call finish() after every "
+                    "backward, or run the earlier micro-batches of an accumulation under no_sync()")
             self._ready[i] += 1
             full = self._ready[i] == len(self.buckets[i].params)
             if full:
+                self._launched[i] = True
                 self.launched_in_backward += 1
         if full:
             self._launch(i)
@@ -166,7 +189,8 @@ class GradBucketer:
         gradients back; the caller's stream then waits for them."""
         t0 = time.perf_counter()
         for i in range(len(self.buckets)):
-            if self._works[i] is None and self._ready[i] < len(self.buckets[i].params):
+            if not self._launched[i]:
+                self._launched[i] = True
                 self._launch(i)
         ctx = torch.cuda.stream(self.stream) if self.stream is not None else _null()
         with ctx:
@@ -181,6 +205,7 @@ class GradBucketer:
             torch.cuda.current_stream(self.buckets[0].flat.device).wait_stream(self.stream)
         self._ready = [0] * len(self.buckets)
         self._works = [None] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
         self.last_seconds = time.perf_counter() - t0
 
     # -- after-backward mode ---------------------------------------------

@@ -261,11 +261,19 @@ class Scheduler:
         pod = self.queue.pop()
         if pod is None:
             return False
+        cycle: dict[str, Any] = {}
         try:
-            return self._schedule_pod(pod)
+            return self._schedule_pod(pod, cycle)
         except Exception:
             log.exception("scheduling cycle of %s failed; requeued with backoff", ko.key(pod))
             self.stats["cycle_errors"] = self.stats.get("cycle_errors", 0) + 1
+            reserved = cycle.get("reserved")
+            if reserved is not None:  # Reserve succeeded: give back what it took (e.g. quota "used")
+                fw, state, rpod, node = reserved
+                try:
+                    fw.run_reserve_plugins_unreserve(state, rpod, node)
+                except Exception:
+                    log.exception("unreserve of %s after a failed cycle failed", ko.key(pod))
             try:
                 self.cache.forget(pod)
             except Exception:
@@ -273,7 +281,8 @@ class Scheduler:
             self.queue.add_unschedulable(pod)
             return True
 
-    def _schedule_pod(self, pod: dict) -> bool:
+    def _schedule_pod(self, pod: dict, cycle: dict | None = None) -> bool:
+        cycle = {} if cycle is None else cycle
         fw = self._framework_for(pod)
         if fw is None:
             return True
@@ -309,15 +318,18 @@ class Scheduler:
             self.cache.forget(pod)
             self._unschedulable(fw, state, pod, s, {})
             return True
+        cycle["reserved"] = (fw, state, pod, node)
         s = fw.run_permit_plugins(state, pod, node)
         if s.is_success():
             s = fw.run_bind_plugins(state, pod, node)
         if not s.is_success():
+            cycle.pop("reserved", None)
             fw.run_reserve_plugins_unreserve(state, pod, node)
             self.cache.forget(pod)
             self.stats["errors"] += 1
             self.queue.add_unschedulable(pod)
             return True
+        cycle.pop("reserved", None)  # bound: the reservation is now the pod's real usage
         fw.run_post_bind_plugins(state, pod, node)
         self.nominator.delete_nominated_pod_if_exists(pod)
         self.stats["scheduled"] += 1

@@ -107,3 +107,34 @@ def test_grad_bucketer_two_ranks():
 def test_busbw_formula():
     assert busbw(1 << 30, 1.0, 8) == (1 << 30) * 2 * 7 / 8 / 1e9
     assert busbw(100, 1.0, 1) == 0.0
+
+
+def test_overlapped_bucketer_accumulation_contract():
+    """a second backward before finish() used to drop the later
+    micro-batches' gradients silently.  Now it raises, and no_sync() gives
+    DDP-style accumulation: the buckets carry the sum of every micro-batch."""
+    import pytest
+
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 2))
+    b = GradBucketer(list(model.parameters()), bucket_bytes=300, overlap=True).attach()
+    xs = [torch.randn(4, 8) for _ in range(3)]
+    model(xs[0]).sum().backward()
+    with pytest.raises(RuntimeError, match="already launched"):
+        model(xs[1]).sum().backward()
+    b.finish()
+    model.zero_grad(set_to_none=True)
+    with b.no_sync():
+        for x in xs[:2]:
+            model(x).sum().backward()
+    model(xs[2]).sum().backward()
+    launched = b.launched_in_backward
+    b.finish()
+    got = [p.grad.clone() for p in model.parameters()]
+    model.zero_grad(set_to_none=True)
+    b.detach()
+    for x in xs:
+        model(x).sum().backward()
+    assert launched >= len(b.buckets)
+    for g, p in zip(got, model.parameters()):
+        assert torch.allclose(g, p.grad, atol=1e-6)

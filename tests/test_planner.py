@@ -273,3 +273,20 @@ def test_amdpart_geometry_from_labels_in_planner():
     n["metadata"]["labels"]["amd.com/gpu.memory"] = "262144"
     plan = _amd_planner().plan(_amd_snapshot([n]), [_pod("s", "amd.com/partition-1xcd.32gb")])
     assert _res(plan, "n1") == [{"amd.com/partition-1xcd.32gb": 8}]
+
+
+def test_amdpart_switch_puts_back_demand_its_free_partitions_covered():
+    """GPU0 DPX with 2 free 4xcd partitions, GPU1 idle SPX; one
+    4xcd pod and one 1xcd pod pending.  Switching GPU0 to CPX for the 1xcd pod
+    destroys the free 4xcd partitions counted for the other pod, so that demand
+    is lacking again and GPU1 is split to DPX: both pods are placed
+    (mig/node.go:145-177 counts free devices after each GPU's update)."""
+    n1 = _node("n1", "partition", count=2, ann={"nos.nebuly.com/status-gpu-0-4xcd.144gb-free": "2",
+                                                "nos.nebuly.com/status-gpu-1-8xcd.288gb-free": "1"})
+    plan = _amd_planner().plan(_amd_snapshot([n1]), [_pod("h", HALF), _pod("s", ONE)])
+    res = _res(plan, "n1")
+    total = {}
+    for r in res:
+        for k, v in r.items():
+            total[k] = total.get(k, 0) + v
+    assert total.get(HALF, 0) >= 1 and total.get(ONE, 0) >= 1, res

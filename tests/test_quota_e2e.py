@@ -182,3 +182,33 @@ def test_baseline_config1_borrow_then_reclaim_by_preemption():
     la = _labels(cl, "team-a")
     assert len(la) == 4 and in_quota <= set(la)  # only over-quota pods were preempted
     assert cl.scheduler.stats["preemptions"] >= 1
+
+
+def test_cycle_exception_after_reserve_gives_the_quota_back():
+    """an exception escaping the cycle after Reserve (here: a
+    permit plugin bug) must run Unreserve, or CapacityScheduling keeps the pod
+    in its ElasticQuota "used" and admission drifts until a resync."""
+    cl = _cluster(lender_min=0)
+    _ns(cl, "team-a")
+    _eq(cl, "team-a", 20, 20)
+    cl.settle(30)
+    fw = next(iter(cl.scheduler.frameworks.values()))
+    calls = {"n": 0}
+    real_permit = fw.run_permit_plugins
+
+    def boom(state, pod, node):
+        calls["n"] += 1
+        if calls["n"] == 1:  # the pod goes away while its cycle fails: only Unreserve can give its quota back
+            cl.api.delete("Pod", ko.name(pod), ko.namespace(pod))
+            raise RuntimeError("permit plugin bug")
+        return real_permit(state, pod, node)
+
+    fw.run_permit_plugins = boom
+    cs = next(p for p in fw.plugins["reserve"] if p.name == "CapacityScheduling")
+    _submit(cl, "team-a", ["gone"])
+    assert calls["n"] == 1 and cl.scheduler.stats.get("cycle_errors") == 1
+    assert cs.elastic_quota_infos.get("team-a").used.scalar.get(GPU_MEM, 0) == 0
+    # two 10 GB pods fit the 20 GB max: nothing leaked from the failed cycle
+    _submit(cl, "team-a", ["p0", "p1"])
+    assert not cl.pending_pods()
+    assert cs.elastic_quota_infos.get("team-a").used.scalar.get(GPU_MEM, 0) == 20

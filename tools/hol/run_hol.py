@@ -1,0 +1,108 @@
+"""Sweep the dispatch head-of-line microbenchmark (holbench.hip) over pod
+counts, grid sizes and HW-queue settings, one process per pod with the
+device plugin's XCD-symmetric CU mask (or no mask).
+
+python tools/hol/run_hol.py --out gpurun_out/hol.json [--pods 1,3,4,5,8] [--grids 0,-4]
+
+Each row: per-pod slot efficiency (workgroup-seconds completed / slot-seconds
+the pod's mask owns).  The launcher never touches the GPU.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(REPO))
+BIN = REPO / "build" / "holbench"
+
+
+def build(force: bool = False) -> Path:
+    src = Path(__file__).with_name("holbench.hip")
+    if force or not BIN.exists() or BIN.stat().st_mtime < src.stat().st_mtime:
+        BIN.parent.mkdir(parents=True, exist_ok=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", str(src), "-o", str(BIN)],
+                       check=True)
+    return BIN
+
+
+def masks(n: int, per_xcd: int, mode: str) -> list[str | None]:
+    from nos_amd.gpu.topology import MI355X_CUS, logical_cu
+    from nos_amd.ops.streams import mask_hex
+
+    if mode == "none":
+        return [None] * n
+    out = []
+    for k in range(n):
+        slots = range(k * per_xcd, (k + 1) * per_xcd)
+        out.append(mask_hex([logical_cu(x, j) for x in range(8) for j in slots], MI355X_CUS))
+    return out
+
+
+def run_row(n: int, grid: int, hwq: int, mode: str, per_xcd: int, seconds: float, spin_us: float, lds: int,
+            depth: int, null_stream: int, timeout: float) -> dict:
+    start = time.monotonic_ns() + int(4e9)
+    procs = []
+    for k, m in enumerate(masks(n, per_xcd, mode)):
+        env = dict(os.environ)
+        env.pop("ROC_GLOBAL_CU_MASK", None)
+        if m:
+            env["ROC_GLOBAL_CU_MASK"] = m
+        if hwq:
+            env["GPU_MAX_HW_QUEUES"] = str(hwq)
+        cmd = [str(BIN), "--seconds", str(seconds), "--start-ns", str(start), "--grid", str(grid),
+               "--spin-us", str(spin_us), "--lds", str(lds), "--depth", str(depth), "--null-stream", str(null_stream),
+               "--tag", f"{mode}-n{n}-g{grid}-q{hwq}-p{k}"]
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    pods = []
+    for p in procs:
+        try:
+            out, err = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, err = p.communicate()
+        if p.returncode != 0:
+            pods.append({"error": err[-400:], "rc": p.returncode})
+            continue
+        pods.append(json.loads(out.strip().splitlines()[-1]))
+    effs = [q.get("slot_efficiency", 0.0) for q in pods]
+    return {"pods": n, "grid": grid, "hw_queues": hwq, "mask": mode, "per_xcd": per_xcd, "null_stream": null_stream,
+            "eff_min": round(min(effs), 3), "eff_max": round(max(effs), 3),
+            "eff_mean": round(sum(effs) / len(effs), 3), "per_pod": pods}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pods", default="1,3,4,5,8")
+    ap.add_argument("--grids", default="0,-4", help="0 = fit the mask's slots, -k = k x fit, k > 0 = absolute")
+    ap.add_argument("--hw-queues", default="0,1")
+    ap.add_argument("--masks", default="cumask")
+    ap.add_argument("--per-xcd", type=int, default=4)
+    ap.add_argument("--seconds", type=float, default=2.0)
+    ap.add_argument("--spin-us", type=float, default=50.0)
+    ap.add_argument("--lds", type=int, default=40960)
+    ap.add_argument("--depth", type=int, default=16)
+    ap.add_argument("--null-stream", type=int, default=0)
+    ap.add_argument("--out", default="gpurun_out/hol.json")
+    a = ap.parse_args()
+    build()
+    rows = []
+    for mode in a.masks.split(","):
+        for hwq in map(int, a.hw_queues.split(",")):
+            for grid in map(int, a.grids.split(",")):
+                for n in map(int, a.pods.split(",")):
+                    r = run_row(n, grid, hwq, mode, a.per_xcd, a.seconds, a.spin_us, a.lds, a.depth, a.null_stream,
+                                timeout=a.seconds + 60)
+                    print(json.dumps({k: v for k, v in r.items() if k != "per_pod"}), flush=True)
+                    rows.append(r)
+                    Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+                    Path(a.out).write_text(json.dumps(rows, indent=1))
+
+
+if __name__ == "__main__":
+    main()
