@@ -27,7 +27,19 @@
 // one GPU with their own HIP id, render node, CUs, XCDs and memory.
 //
 // All entry points are serialised by one mutex (the reference's NVML client
-// does Init/Shutdown per call, client.go:46-57; we keep one session open).
+// does Init/Shutdown per call, client.go:46-57; we keep one session open) --
+// except the slow part of a mode switch: nos_smi_set_*_partition validate and
+// mark the GPU "switching" under the mutex, call the driver WITHOUT it, then
+// re-enumerate under it again.  Queries about other GPUs keep answering while
+// a switch runs (or hangs); queries about the switching GPU return
+// NOS_SMI_ERR_SWITCHING instead of blocking.  The partition agent bounds the
+// switch with its own deadline (agents/partagent.py).
+//
+// The session enumerates handles at open time and after its own switches,
+// like amd-smi: a mode changed by ANOTHER process (another agent, amd-smi CLI)
+// is invisible until nos_smi_rescan() -- the device plugin calls it on every
+// poll.  The fake backend models that with a separate "hardware" state and
+// session view (fault "external_switch=<gpu>:<mode>").
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -56,6 +68,7 @@ enum NosSmiError : int {
   NOS_SMI_ERR_INJECTED = -6,    // fake backend fault injection
   NOS_SMI_ERR_INVALID = -7,
   NOS_SMI_ERR_TIMEOUT = -8,
+  NOS_SMI_ERR_SWITCHING = -9,   // a mode switch of this GPU is in progress
 };
 
 // compute modes: 1=SPX 2=DPX 3=TPX 4=QPX 5=CPX (amdsmi_compute_partition_type_t)
@@ -143,6 +156,16 @@ struct Backend {
   virtual int partition_count(int i) = 0;
   virtual int clock(int i, int* cur_mhz, int* max_mhz) = 0;
   virtual int partition_info(int i, int p, nos_part_info* out) = 0;
+  // re-read the device set (another process may have switched a mode)
+  virtual int rescan() = 0;
+  // mode switch in three steps: prepare (global lock held: validate, mark the
+  // GPU switching), run (no global lock: the slow driver call), finish (lock
+  // held: apply / re-enumerate, clear the mark)
+  virtual int switch_prepare(int i, bool compute, int mode) = 0;
+  virtual int switch_run(int i, bool compute, int mode) = 0;
+  virtual int switch_finish(int i, bool compute, int mode, int rc) = 0;
+  std::vector<char> switching;  // per GPU
+  bool is_switching(int i) const { return i >= 0 && i < (int)switching.size() && switching[i]; }
   virtual int inject(const char* /*fault*/) { return NOS_SMI_ERR_UNSUPPORTED; }
   virtual int add_process(int, unsigned, long long, unsigned) { return NOS_SMI_ERR_UNSUPPORTED; }
   virtual int remove_process(int, unsigned) { return NOS_SMI_ERR_UNSUPPORTED; }
@@ -160,7 +183,10 @@ struct FakeGpu {
 };
 
 struct FakeBackend : Backend {
+  // gpus: the hardware; view: what this session enumerated (compute / memory
+  // mode, lost) -- equal except after an external switch, until rescan()
   std::vector<FakeGpu> gpus;
+  std::vector<FakeGpu> view;
   std::string model = "AMD Instinct MI355X";
   bool fail_set_compute = false, fail_set_memory = false, stale_mode = false;
   bool lose_after_switch = false;
@@ -192,15 +218,30 @@ struct FakeBackend : Backend {
     if (proto.compute == 0) proto.compute = 1;
     if (proto.memory == 0) proto.memory = 1;
     gpus.assign(n, proto);
+    view = gpus;
+    switching.assign(n, 0);
+    pending_delay_ms.assign(n, 0);  // sized once: switch_run reads it without the lock
   }
 
-  bool ok(int i) const { return i >= 0 && i < (int)gpus.size() && !gpus[i].lost; }
+  bool ok(int i) const { return i >= 0 && i < (int)view.size() && !view[i].lost && !gpus[i].lost; }
+  // a query about GPU i: not lost, not in the middle of a mode switch
+  int check(int i) const {
+    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    return is_switching(i) ? NOS_SMI_ERR_SWITCHING : NOS_SMI_OK;
+  }
 
-  int count() override { return (int)gpus.size(); }
+  int count() override { return (int)view.size(); }
+
+  int rescan() override {
+    for (int i = 0; i < (int)gpus.size(); ++i)
+      if (is_switching(i)) return NOS_SMI_ERR_SWITCHING;
+    view = gpus;
+    return NOS_SMI_OK;
+  }
 
   int info(int i, nos_gpu_info* o) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
-    const FakeGpu& g = gpus[i];
+    if (int rc = check(i)) return rc;
+    const FakeGpu& g = view[i];
     std::memset(o, 0, sizeof(*o));
     o->index = i;
     o->num_cus = g.cus;
@@ -210,7 +251,7 @@ struct FakeBackend : Backend {
     o->num_partitions = partitions_for_mode(g.compute);
     int base = 0;  // a GPU's HIP id / render node are those of its first logical device
     for (int j = 0; j < i; ++j)
-      if (!gpus[j].lost) base += partitions_for_mode(gpus[j].compute);
+      if (!view[j].lost) base += partitions_for_mode(view[j].compute);
     o->hip_id = base;
     o->drm_render = 128 + base;
     o->vram_mb = g.vram_mb;
@@ -220,30 +261,50 @@ struct FakeBackend : Backend {
     return NOS_SMI_OK;
   }
 
-  int set_mode_common(int i, int* field, int mode, bool fail) {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
-    if (fail) return NOS_SMI_ERR_INJECTED;
+  std::vector<int> pending_delay_ms;
+
+  int switch_prepare(int i, bool compute, int mode) override {
+    if (compute ? (mode < 1 || mode > 5) : (mode != 1 && mode != 2 && mode != 4 && mode != 8))
+      return NOS_SMI_ERR_INVALID;
+    if (int rc = check(i)) return rc;
+    if (compute ? fail_set_compute : fail_set_memory) return NOS_SMI_ERR_INJECTED;
     if (!gpus[i].procs.empty()) return NOS_SMI_ERR_BUSY;
-    if (switch_delay_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(switch_delay_ms));
-    if (!stale_mode) *field = mode;
+    pending_delay_ms[i] = switch_delay_ms;
+    switching[i] = 1;
+    return NOS_SMI_OK;
+  }
+
+  // runs without the global lock: touches nothing shared but its own delay
+  int switch_run(int i, bool, int) override {
+    const int d = pending_delay_ms[i];
+    if (d > 0) std::this_thread::sleep_for(std::chrono::milliseconds(d));
+    return NOS_SMI_OK;
+  }
+
+  int switch_finish(int i, bool compute, int mode, int rc) override {
+    switching[i] = 0;
+    if (rc != NOS_SMI_OK) return rc;
+    if (!stale_mode) (compute ? gpus[i].compute : gpus[i].memory) = mode;
     if (lose_after_switch) gpus[i].lost = true;
+    // the session re-enumerates after its own switch (it then also sees any
+    // external change of the other GPUs); GPUs still switching keep their view
+    for (int j = 0; j < (int)gpus.size(); ++j)
+      if (!is_switching(j)) view[j] = gpus[j];
     return NOS_SMI_OK;
   }
 
   int set_compute(int i, int mode) override {
-    if (mode < 1 || mode > 5) return NOS_SMI_ERR_INVALID;
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
-    return set_mode_common(i, &gpus[i].compute, mode, fail_set_compute);
+    int rc = switch_prepare(i, true, mode);
+    return rc ? rc : switch_finish(i, true, mode, switch_run(i, true, mode));
   }
 
   int set_memory(int i, int mode) override {
-    if (mode != 1 && mode != 2 && mode != 4 && mode != 8) return NOS_SMI_ERR_INVALID;
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
-    return set_mode_common(i, &gpus[i].memory, mode, fail_set_memory);
+    int rc = switch_prepare(i, false, mode);
+    return rc ? rc : switch_finish(i, false, mode, switch_run(i, false, mode));
   }
 
   int activity(int i, int* gfx, int* umc, int* mm) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (int rc = check(i)) return rc;
     *gfx = gpus[i].gfx;
     *umc = gpus[i].umc;
     *mm = 0;
@@ -251,7 +312,7 @@ struct FakeBackend : Backend {
   }
 
   int processes(int i, nos_proc_info* out, int max, int* n) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (int rc = check(i)) return rc;
     int k = 0;
     for (auto& kv : gpus[i].procs) {
       if (k < max) out[k] = kv.second;
@@ -276,7 +337,7 @@ struct FakeBackend : Backend {
   }
 
   int clock(int i, int* cur, int* mx) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (int rc = check(i)) return rc;
     *mx = 2400;
     *cur = gpus[i].gfx > 0 ? 2400 : 500;  // busy GPUs run at the top clock, idle ones deep-sleep
     return NOS_SMI_OK;
@@ -285,18 +346,18 @@ struct FakeBackend : Backend {
   // logical devices: GPU-major enumeration (the driver's order), partition p of
   // GPU i gets HIP id / render node after every partition of GPUs 0..i-1
   int partition_count(int i) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
-    return partitions_for_mode(gpus[i].compute);
+    if (int rc = check(i)) return rc;
+    return partitions_for_mode(view[i].compute);
   }
 
   int partition_info(int i, int p, nos_part_info* o) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
-    const FakeGpu& g = gpus[i];
+    if (int rc = check(i)) return rc;
+    const FakeGpu& g = view[i];
     const int n = partitions_for_mode(g.compute);
     if (p < 0 || p >= n) return NOS_SMI_ERR_BAD_INDEX;
     int base = 0;
     for (int j = 0; j < i; ++j)
-      if (!gpus[j].lost) base += partitions_for_mode(gpus[j].compute);
+      if (!view[j].lost) base += partitions_for_mode(view[j].compute);
     std::memset(o, 0, sizeof(*o));
     o->gpu_index = i;
     o->partition = p;
@@ -321,11 +382,24 @@ struct FakeBackend : Backend {
     else if (f.rfind("switch_delay_ms=", 0) == 0) switch_delay_ms = std::stoi(f.substr(16));
     else if (f.rfind("lose_gpu=", 0) == 0) {
       int i = std::stoi(f.substr(9));
-      if (i >= 0 && i < (int)gpus.size()) gpus[i].lost = true;
+      if (i >= 0 && i < (int)gpus.size()) gpus[i].lost = view[i].lost = true;
+    } else if (f.rfind("external_switch=", 0) == 0) {
+      // "external_switch=<gpu>:<mode>": another process changed the GPU's compute
+      // (SPX..CPX) or memory (NPSn) mode; this session sees it after rescan()
+      const std::string arg = f.substr(16);
+      const size_t c = arg.find(':');
+      if (c == std::string::npos) return NOS_SMI_ERR_INVALID;
+      const int i = std::stoi(arg.substr(0, c));
+      const std::string m = arg.substr(c + 1);
+      if (i < 0 || i >= (int)gpus.size()) return NOS_SMI_ERR_BAD_INDEX;
+      if (int cm = parse_compute(m.c_str())) gpus[i].compute = cm;
+      else if (int mm = parse_memory(m.c_str())) gpus[i].memory = mm;
+      else return NOS_SMI_ERR_INVALID;
     } else if (f == "clear") {
       fail_set_compute = fail_set_memory = stale_mode = lose_after_switch = false;
       switch_delay_ms = 0;
       for (auto& g : gpus) g.lost = false;
+      for (auto& g : view) g.lost = false;
     } else {
       return NOS_SMI_ERR_INVALID;
     }
@@ -333,7 +407,7 @@ struct FakeBackend : Backend {
   }
 
   int add_process(int i, unsigned pid, long long vram, unsigned cus) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (i < 0 || i >= (int)gpus.size() || gpus[i].lost) return NOS_SMI_ERR_BAD_INDEX;
     nos_proc_info p{};
     p.pid = pid;
     p.vram_bytes = vram;
@@ -344,13 +418,13 @@ struct FakeBackend : Backend {
   }
 
   int remove_process(int i, unsigned pid) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (i < 0 || i >= (int)gpus.size() || gpus[i].lost) return NOS_SMI_ERR_BAD_INDEX;
     gpus[i].procs.erase(pid);
     return NOS_SMI_OK;
   }
 
   int set_activity(int i, int gfx, int umc) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (i < 0 || i >= (int)gpus.size() || gpus[i].lost) return NOS_SMI_ERR_BAD_INDEX;
     gpus[i].gfx = gfx;
     gpus[i].umc = umc;
     return NOS_SMI_OK;
@@ -421,7 +495,9 @@ struct AmdSmiBackend : Backend {
   // physical GPU -> its processor handles (one per logical partition, ordered
   // by KFD partition id; SPX: exactly one)
   std::vector<std::vector<amdsmi_processor_handle>> gpus;
+  std::vector<amdsmi_processor_handle> pending;  // per GPU: handle an in-flight switch was issued on
   bool allow_set = false;
+  bool need_rescan = false;  // a switch finished while another was in flight
 
   int open(bool allow_set_) {
     allow_set = allow_set_;
@@ -445,6 +521,7 @@ struct AmdSmiBackend : Backend {
   // lists the processor handles of every partition the current mode exposes
   int enumerate() {
     gpus.clear();
+    need_rescan = false;
     uint32_t ns = 0;
     if (api.amdsmi_get_socket_handles(&ns, nullptr) != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
     std::vector<amdsmi_socket_handle> sockets(ns);
@@ -463,7 +540,31 @@ struct AmdSmiBackend : Backend {
       for (auto& kv : keyed) parts.push_back(kv.second);
       gpus.push_back(parts);
     }
+    switching.assign(gpus.size(), 0);
+    pending.assign(gpus.size(), nullptr);
     return NOS_SMI_OK;
+  }
+
+  bool any_switching() const {
+    for (char c : switching)
+      if (c) return true;
+    return false;
+  }
+
+  // shut the session down and enumerate again: invalidates every handle, so
+  // never while a switch (holding a captured handle) is in flight
+  int reinit() {
+    if (any_switching()) return NOS_SMI_ERR_SWITCHING;
+    if (api.amdsmi_shut_down) api.amdsmi_shut_down();
+    if (api.amdsmi_init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
+    return enumerate();
+  }
+
+  int rescan() override { return reinit(); }
+
+  int check(int i) const {
+    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    return is_switching(i) ? NOS_SMI_ERR_SWITCHING : NOS_SMI_OK;
   }
 
   ~AmdSmiBackend() override {
@@ -517,7 +618,7 @@ struct AmdSmiBackend : Backend {
   }
 
   int info(int i, nos_gpu_info* o) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (int rc = check(i)) return rc;
     std::memset(o, 0, sizeof(*o));
     const auto& parts = gpus[i];
     auto h = parts[0];
@@ -555,12 +656,12 @@ struct AmdSmiBackend : Backend {
   }
 
   int partition_count(int i) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (int rc = check(i)) return rc;
     return (int)gpus[i].size();
   }
 
   int clock(int i, int* cur, int* mx) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (int rc = check(i)) return rc;
     if (!api.amdsmi_get_clock_info) return NOS_SMI_ERR_UNSUPPORTED;
     amdsmi_clk_info_t c{};
     if (api.amdsmi_get_clock_info(gpus[i][0], AMDSMI_CLK_TYPE_GFX, &c) != AMDSMI_STATUS_SUCCESS)
@@ -571,7 +672,7 @@ struct AmdSmiBackend : Backend {
   }
 
   int partition_info(int i, int p, nos_part_info* o) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (int rc = check(i)) return rc;
     const auto& parts = gpus[i];
     if (p < 0 || p >= (int)parts.size()) return NOS_SMI_ERR_BAD_INDEX;
     auto h = parts[p];
@@ -607,30 +708,50 @@ struct AmdSmiBackend : Backend {
   }
 
   // a mode switch is GPU-wide: issued on the first partition's handle; the
-  // handle set changes with the mode, so the session re-enumerates
-  int set_mode(int i, bool compute, int mode) {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+  // handle set changes with the mode, so the session re-enumerates afterwards
+  int switch_prepare(int i, bool compute, int mode) override {
+    if (int rc = check(i)) return rc;
     if (compute ? !api.amdsmi_set_gpu_compute_partition : !api.amdsmi_set_gpu_memory_partition)
       return NOS_SMI_ERR_UNSUPPORTED;
     if (!allow_set) return NOS_SMI_ERR_UNSUPPORTED;
     int n = 0;
     nos_proc_info tmp[1];
     if (processes(i, tmp, 1, &n) == NOS_SMI_OK && n > 0) return NOS_SMI_ERR_BUSY;
-    auto h = gpus[i][0];
-    auto st = compute ? api.amdsmi_set_gpu_compute_partition(h, (amdsmi_compute_partition_type_t)mode)
-                      : api.amdsmi_set_gpu_memory_partition(h, (amdsmi_memory_partition_type_t)mode);
-    if (st != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
-    if (api.amdsmi_shut_down) api.amdsmi_shut_down();
-    if (api.amdsmi_init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
-    return enumerate();
+    pending[i] = gpus[i][0];
+    switching[i] = 1;
+    return NOS_SMI_OK;
   }
 
-  int set_compute(int i, int mode) override { return set_mode(i, true, mode); }
+  int switch_run(int i, bool compute, int mode) override {
+    auto h = pending[i];
+    auto st = compute ? api.amdsmi_set_gpu_compute_partition(h, (amdsmi_compute_partition_type_t)mode)
+                      : api.amdsmi_set_gpu_memory_partition(h, (amdsmi_memory_partition_type_t)mode);
+    return st == AMDSMI_STATUS_SUCCESS ? NOS_SMI_OK : NOS_SMI_ERR_BACKEND;
+  }
 
-  int set_memory(int i, int mode) override { return set_mode(i, false, mode); }
+  int switch_finish(int i, bool, int, int rc) override {
+    switching[i] = 0;
+    pending[i] = nullptr;
+    if (any_switching()) {  // handles are still in use by another switch: re-enumerate when it ends
+      need_rescan = true;
+      return rc;
+    }
+    const int rs = reinit();
+    return rc != NOS_SMI_OK ? rc : rs;
+  }
+
+  int set_compute(int i, int mode) override {
+    int rc = switch_prepare(i, true, mode);
+    return rc ? rc : switch_finish(i, true, mode, switch_run(i, true, mode));
+  }
+
+  int set_memory(int i, int mode) override {
+    int rc = switch_prepare(i, false, mode);
+    return rc ? rc : switch_finish(i, false, mode, switch_run(i, false, mode));
+  }
 
   int activity(int i, int* gfx, int* umc, int* mm) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (int rc = check(i)) return rc;
     if (!api.amdsmi_get_gpu_activity) return NOS_SMI_ERR_UNSUPPORTED;
     amdsmi_engine_usage_t u{};
     if (api.amdsmi_get_gpu_activity(gpus[i][0], &u) != AMDSMI_STATUS_SUCCESS) return NOS_SMI_ERR_BACKEND;
@@ -642,7 +763,7 @@ struct AmdSmiBackend : Backend {
 
   // processes of every partition of the GPU (a repartition drains them all)
   int processes(int i, nos_proc_info* out, int max, int* n) override {
-    if (!ok(i)) return NOS_SMI_ERR_BAD_INDEX;
+    if (int rc = check(i)) return rc;
     if (!api.amdsmi_get_gpu_process_list) return NOS_SMI_ERR_UNSUPPORTED;
     std::map<unsigned, nos_proc_info> seen;
     for (auto h : gpus[i]) {
@@ -675,6 +796,7 @@ struct AmdSmiBackend : Backend {
       *weight = 0;
       return NOS_SMI_OK;
     }
+    if (is_switching(i) || is_switching(j)) return NOS_SMI_ERR_SWITCHING;
     if (!api.amdsmi_topo_get_link_type) return NOS_SMI_ERR_UNSUPPORTED;
     uint64_t h = 0, w = 0;
     amdsmi_link_type_t t = AMDSMI_LINK_TYPE_UNKNOWN;
@@ -689,15 +811,26 @@ struct AmdSmiBackend : Backend {
 };
 
 std::mutex g_mu;
-// Deliberately a raw pointer that is never destroyed by static destructors:
+// Deliberately a heap object that is never destroyed by static destructors:
 // amd-smi tears its own singletons down at exit, and shutting it down again from
 // our destructor afterwards segfaults (seen on MI355X, ROCm 7.2).  Explicit
-// nos_smi_close() releases the session.
-Backend* g_backend = nullptr;
+// nos_smi_close() releases the session (an in-flight mode switch keeps its
+// backend alive through its own reference until it returns).
+std::shared_ptr<Backend>& g_backend = *new std::shared_ptr<Backend>();
 
-void set_backend(Backend* b) {
-  delete g_backend;
-  g_backend = b;
+void set_backend(Backend* b) { g_backend.reset(b); }
+
+int do_switch(int i, bool compute, int mode) {
+  std::shared_ptr<Backend> b;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_backend) return NOS_SMI_ERR_NOT_OPEN;
+    b = g_backend;
+    if (int rc = b->switch_prepare(i, compute, mode)) return rc;
+  }
+  const int rc = b->switch_run(i, compute, mode);  // the slow part: no global lock
+  std::lock_guard<std::mutex> lk(g_mu);
+  return b->switch_finish(i, compute, mode, rc);
 }
 
 }  // namespace
@@ -740,13 +873,13 @@ NOS_API int nos_smi_gpu_info(int i, nos_gpu_info* out) {
   NOS_SMI_GUARD();
   return g_backend->info(i, out);
 }
-NOS_API int nos_smi_set_compute_partition(int i, int mode) {
+NOS_API int nos_smi_set_compute_partition(int i, int mode) { return do_switch(i, true, mode); }
+NOS_API int nos_smi_set_memory_partition(int i, int mode) { return do_switch(i, false, mode); }
+// re-enumerate (modes switched by another process become visible);
+// NOS_SMI_ERR_SWITCHING while one of this session's switches is in flight
+NOS_API int nos_smi_rescan() {
   NOS_SMI_GUARD();
-  return g_backend->set_compute(i, mode);
-}
-NOS_API int nos_smi_set_memory_partition(int i, int mode) {
-  NOS_SMI_GUARD();
-  return g_backend->set_memory(i, mode);
+  return g_backend->rescan();
 }
 NOS_API int nos_smi_activity(int i, int* gfx, int* umc, int* mm) {
   NOS_SMI_GUARD();

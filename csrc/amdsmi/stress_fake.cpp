@@ -40,6 +40,7 @@ int nos_smi_fake_add_process(int i, unsigned pid, long long vram, unsigned cus);
 int nos_smi_fake_remove_process(int i, unsigned pid);
 int nos_smi_fake_set_activity(int i, int gfx, int umc);
 int nos_smi_struct_sizes(int* gpu_info, int* proc_info);
+int nos_smi_rescan();
 }
 
 int main() {
@@ -82,6 +83,11 @@ int main() {
         } else {
           nos_smi_fake_inject(it % 2 ? "fail_set_compute" : "clear");
           nos_smi_set_memory_partition(g, it % 2 ? 2 : 1);
+          // another process switches a mode; this session re-enumerates (deferred
+          // while one of its own switches -- run outside the lock -- is in flight)
+          nos_smi_fake_inject(it % 3 ? "external_switch=3:CPX" : "external_switch=3:SPX");
+          if (it % 50 == 0) nos_smi_fake_inject("switch_delay_ms=1");
+          nos_smi_rescan();
         }
         ++ops;
       }

@@ -1,9 +1,10 @@
 """Device-plugin restart after a repartition (``pkg/gpu/client.go:51-135``).
 
 When the partition agent switches a GPU's compute/memory mode, the device
-plugin of that node must re-enumerate.  A deployed nos-amd device plugin
-notices mode changes itself (it re-reads amd-smi every poll), but a restart
-is the robust, reference-compatible path: delete the plugin pod on this node
+plugin of that node must re-enumerate.  The plugin's own amd-smi session
+only sees the new partitions after it re-enumerates (``nos_smi_rescan``,
+which the deployed plugin runs every ``rescanSeconds``); restarting it is the
+immediate, reference-compatible path: delete the plugin pod on this node
 (label ``app=nos-amd-device-plugin``) and wait until its replacement is
 Running (5 s poll, 1 min timeout).
 """

@@ -17,10 +17,21 @@ status.
   ``status-partitioning-plan`` (the last plan id the actuator parsed);
 * :class:`PartitionActuator` -- ``actuator.go:71-201``: waits for a report
   since its last apply, parses spec vs status, plans, applies.
+
+Every wait on the node's reconfiguration is bounded, as in the reference
+(device-plugin restart timeout ``pkg/gpu/client.go:86-135``, per-op errors
+``actuator.go:165-198``): a mode switch runs in a worker thread with a
+``switch_timeout_s`` deadline and the shared lock is never held across it, so
+the reporter keeps reporting (and the plan handshake keeps clearing) while a
+switch hangs.  A GPU past its deadline is marked failed
+(``status-error-gpu-<i>``) and not planned again until its switch returns;
+then it is verified, rolled back if the mode did not take effect, and the
+device plugins re-enumerate.
 """
 from __future__ import annotations
 
 import logging
+import threading
 import time
 from dataclasses import dataclass, field
 
@@ -98,11 +109,14 @@ def desired_modes(node: dict, gpus, memory_preference: str = "NPS1") -> dict[int
 
 
 def new_partition_plan(node: dict, gpus, used_gpus: set[int], busy_gpus: set[int],
-                       memory_preference: str = "NPS1") -> PartitionPlan:
+                       memory_preference: str = "NPS1", switching: set[int] = frozenset()) -> PartitionPlan:
     plan = PartitionPlan()
     want = desired_modes(node, gpus, memory_preference)
     for g in sorted(gpus, key=lambda x: x.index):
         if g.index not in want:
+            continue
+        if g.index in switching or getattr(g, "switching", False):
+            plan.blocked[g.index] = "mode switch in progress"
             continue
         c, m = want[g.index]
         if (g.compute_mode, g.memory_mode) == (c, m):
@@ -139,16 +153,23 @@ class PartitionReporter:
             cur_status, _ = parse_node_annotations(node)
             publish_node_metrics(self.node_name, status, self.smi)
             ann = ko.annotations(node)
-            modes = {C.ANNOTATION_STATUS_MODE_FORMAT.format(index=g.index): f"{g.compute_mode}/{g.memory_mode}"
+            modes = {C.ANNOTATION_STATUS_MODE_FORMAT.format(index=g.index):
+                     C.MODE_SWITCHING if g.switching else f"{g.compute_mode}/{g.memory_mode}"
                      for g in self.smi.gpus()}
+            errors = {C.ANNOTATION_STATUS_ERROR_FORMAT.format(index=i): why
+                      for i, why in self.shared.failures().items()}
+            stale_errors = [k for k in ann if k.startswith(C.ANNOTATION_STATUS_ERROR_PREFIX) and k not in errors]
             plan = self.shared.last_parsed_plan_id
             if (status_equal(status, cur_status) and ann.get(C.ANNOTATION_REPORTED_PARTITIONING_PLAN, "") == plan
-                    and all(ann.get(k) == v for k, v in modes.items())):
+                    and all(ann.get(k) == v for k, v in modes.items())
+                    and all(ann.get(k) == v for k, v in errors.items()) and not stale_errors):
                 self.shared.on_report_done()
                 return Result(requeue_after=self.refresh_s)
             patch: dict[str, str | None] = {k: None for k in ann if k.startswith(C.ANNOTATION_GPU_STATUS_PREFIX)}
             patch.update({s.key(): s.value() for s in status})
             patch.update(modes)
+            patch.update(errors)
+            patch.update({k: None for k in stale_errors})
             if plan:
                 patch[C.ANNOTATION_REPORTED_PARTITIONING_PLAN] = plan
             self.api.patch("Node", self.node_name, {"metadata": {"annotations": patch}})
@@ -166,13 +187,15 @@ class PartitionReporter:
 # ====================================================================== actuator
 class PartitionActuator:
     """``MigActuator`` analogue.  ``device_plugins`` are refreshed after a mode
-    switch (the reference restarts the device-plugin pod)."""
+    switch (the reference restarts the device-plugin pod).  Each switch runs in
+    a worker thread bounded by ``switch_timeout_s`` (see the module doc)."""
 
     def __init__(self, api, node_name: str, smi, lister, shared: SharedState, device_plugins=(),
                  memory_preference: str = "NPS1", switch_timeout_s: float = 120.0):
         self.api, self.node_name, self.smi = api, node_name, smi
         self.switch_timeout_s = switch_timeout_s
         self.failures = 0
+        self.timeouts = 0
         self.devices = NodeDeviceClient(smi, lister)
         self.shared = shared
         self.device_plugins = list(device_plugins)
@@ -180,11 +203,17 @@ class PartitionActuator:
         self.last_applied_plan: PartitionPlan | None = None
         self.last_applied_status = None
         self.applies = 0
+        self._ilock = threading.Lock()
+        self._inflight: dict[int, dict] = {}   # gpu -> switch still running past its deadline
+
+    def inflight(self) -> set[int]:
+        with self._ilock:
+            return set(self._inflight)
 
     def reconcile(self, req: Request) -> Result:
         if not self.shared.at_least_one_report_since_last_apply():
             return Result(requeue_after=1.0)
-        with self.shared.lock:
+        with self.shared.lock:  # planning only: the switches run after the lock is released
             node = self.api.try_get("Node", self.node_name)
             if node is None:
                 return Result()
@@ -195,10 +224,11 @@ class PartitionActuator:
             if spec_matches_status(spec, status) and not self._mode_mismatch(node):
                 return Result()
             gpus = self.smi.gpus()
+            inflight = self.inflight() | {g.index for g in gpus if g.switching}
             used = self.devices.used_gpus(C.AMD_PARTITION_RESOURCE_PREFIX) | self.devices.used_gpus(
                 C.RESOURCE_AMD_GPU)
-            busy = {g.index for g in gpus if self.smi.processes(g.index)}
-            plan = new_partition_plan(node, gpus, used, busy, self.memory_preference)
+            busy = {g.index for g in gpus if g.index not in inflight and self.smi.processes(g.index)}
+            plan = new_partition_plan(node, gpus, used, busy, self.memory_preference, inflight)
             for gi, why in plan.blocked.items():
                 log.info("node %s gpu %d cannot be repartitioned now: %s", self.node_name, gi, why)
             if plan.is_empty():
@@ -208,46 +238,109 @@ class PartitionActuator:
             if self.last_applied_plan == plan and status_equal(self.last_applied_status or [], status):
                 log.info("plan already applied and state unchanged, skipping")
                 return Result()
-            failures = self.failures
-            self.apply(plan, plan_id)
-            self.shared.on_apply_done()
-            if self.failures > failures:
-                # do not remember a plan that did not (fully) apply: retry it
-                self.last_applied_plan = None
-                return Result(requeue_after=10.0)
-            self.last_applied_plan = plan
-            self.last_applied_status = status
-            return Result(requeue_after=1.0)
+        failures = self.failures
+        self.apply(plan, plan_id)
+        self.shared.on_apply_done()
+        if self.failures > failures:
+            # do not remember a plan that did not (fully) apply: retry it
+            self.last_applied_plan = None
+            return Result(requeue_after=10.0)
+        self.last_applied_plan = plan
+        self.last_applied_status = status
+        return Result(requeue_after=1.0)
 
     def _mode_mismatch(self, node: dict) -> bool:
-        want = desired_modes(node, self.smi.gpus(), self.memory_preference)
-        return any((g.compute_mode, g.memory_mode) != want[g.index] for g in self.smi.gpus() if g.index in want)
+        gpus = self.smi.gpus()
+        want = desired_modes(node, gpus, self.memory_preference)
+        return any((g.compute_mode, g.memory_mode) != want[g.index] for g in gpus if g.index in want)
 
     def apply(self, plan: PartitionPlan, plan_id: str = "") -> None:
         with tracing.span("partagent.apply", node=self.node_name, plan_id=plan_id, changes=len(plan.changes)):
             for ch in plan.changes:
                 t0 = time.perf_counter()
-                try:
-                    self._switch(ch.gpu_index, ch.compute, ch.memory, ch.from_compute, ch.from_memory)
-                    if not self._verify(ch.gpu_index, ch.compute, ch.memory):
-                        raise RuntimeError("mode did not take effect")
-                except Exception as e:
-                    log.error("node %s gpu %d: switching to %s/%s failed: %s -- rolling back to %s/%s",
-                              self.node_name, ch.gpu_index, ch.compute, ch.memory, e, ch.from_compute,
-                              ch.from_memory)
+                outcome = self._bounded_switch(ch)
+                if outcome == "timeout":
                     self.failures += 1
-                    self._rollback(ch)
+                    self.timeouts += 1
+                    why = (f"switch to {ch.compute}/{ch.memory} still running after {self.switch_timeout_s:.1f}s "
+                           f"(deadline); GPU not planned until it returns")
+                    self.shared.mark_failed(ch.gpu_index, why)
+                    log.error("node %s gpu %d: %s", self.node_name, ch.gpu_index, why)
+                    tracing.event("partagent.switch_timeout", node=self.node_name, gpu=ch.gpu_index,
+                                  mode=f"{ch.compute}/{ch.memory}")
+                    continue
+                if not self._finish_switch(ch, outcome):
                     continue
                 dt = time.perf_counter() - t0
                 metrics.REPARTITION_DURATION.labels(mode=f"{ch.compute}/{ch.memory}").observe(dt)
-                if dt > self.switch_timeout_s:
-                    log.warning("node %s gpu %d: mode switch took %.1fs (> %.0fs)", self.node_name, ch.gpu_index,
-                                dt, self.switch_timeout_s)
-                log.info("node %s gpu %d: %s/%s -> %s/%s", self.node_name, ch.gpu_index, ch.from_compute,
-                         ch.from_memory, ch.compute, ch.memory)
+                log.info("node %s gpu %d: %s/%s -> %s/%s (%.2fs)", self.node_name, ch.gpu_index, ch.from_compute,
+                         ch.from_memory, ch.compute, ch.memory, dt)
             self.applies += 1
-            for p in self.device_plugins:
+            self._refresh_plugins()
+
+    def _refresh_plugins(self) -> None:
+        for p in self.device_plugins:
+            try:
                 p.refresh()
+            except Exception as e:  # a plugin that cannot re-enumerate now retries on its own poll
+                log.error("node %s: device plugin refresh failed: %s", self.node_name, e)
+
+    def _bounded_switch(self, ch: ModeChange):
+        """Run the switch + verification in a worker thread; wait at most
+        ``switch_timeout_s``.  Returns the worker's outcome dict, or "timeout"
+        (the worker keeps running and finishes the GPU itself: _late_done)."""
+        entry: dict = {"change": ch, "done": False, "late": False, "t0": time.monotonic()}
+
+        def work():
+            out: dict = {}
+            try:
+                self._switch(ch.gpu_index, ch.compute, ch.memory, ch.from_compute, ch.from_memory)
+                out["ok"] = self._verify(ch.gpu_index, ch.compute, ch.memory)
+            except Exception as e:  # reported by whoever finishes the switch
+                out["error"] = e
+            with self._ilock:
+                entry["done"] = True
+                entry["outcome"] = out
+                late = entry["late"]
+            if late:
+                self._late_done(ch, out, time.monotonic() - entry["t0"])
+
+        t = threading.Thread(target=work, daemon=True, name=f"partagent-switch-{self.node_name}-{ch.gpu_index}")
+        t.start()
+        t.join(self.switch_timeout_s)
+        with self._ilock:
+            if not entry["done"]:
+                entry["late"] = True
+                self._inflight[ch.gpu_index] = entry
+                return "timeout"
+            return entry["outcome"]
+
+    def _finish_switch(self, ch: ModeChange, outcome: dict) -> bool:
+        """Verification result of a switch that returned: True when the GPU is
+        in the new mode; otherwise roll back and mark the GPU failed."""
+        if outcome.get("ok"):
+            self.shared.clear_failed(ch.gpu_index)
+            return True
+        err = outcome.get("error") or RuntimeError("mode did not take effect")
+        log.error("node %s gpu %d: switching to %s/%s failed: %s -- rolling back to %s/%s", self.node_name,
+                  ch.gpu_index, ch.compute, ch.memory, err, ch.from_compute, ch.from_memory)
+        self.failures += 1
+        self.shared.mark_failed(ch.gpu_index, f"switch to {ch.compute}/{ch.memory} failed: {err}")
+        self._rollback(ch)
+        return False
+
+    def _late_done(self, ch: ModeChange, outcome: dict, took_s: float) -> None:
+        """A switch that ran past its deadline has returned (worker thread)."""
+        log.warning("node %s gpu %d: switch to %s/%s returned after %.1fs (deadline %.1fs)", self.node_name,
+                    ch.gpu_index, ch.compute, ch.memory, took_s, self.switch_timeout_s)
+        try:
+            if self._finish_switch(ch, outcome):
+                metrics.REPARTITION_DURATION.labels(mode=f"{ch.compute}/{ch.memory}").observe(took_s)
+            self._refresh_plugins()
+        finally:
+            with self._ilock:
+                self._inflight.pop(ch.gpu_index, None)
+            self.last_applied_plan = None  # plan again from the state the late switch left
 
     def _switch(self, gpu: int, compute: str, memory: str, from_compute: str, from_memory: str) -> None:
         if memory != from_memory:

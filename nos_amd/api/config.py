@@ -170,6 +170,12 @@ class DevicePluginConfig(ControllerManagerSpec):
     # evenly among the slices of its geometry), "proportional" (to memory),
     # "shared" (no mask; MPS-without-limits semantics)
     cu_policy: str = Field("proportional", alias="cuPolicy")
+    # HIP_VISIBLE_DEVICES of an allocation: "container" (0..k-1 over the render
+    # nodes mounted into the container) or "host" (host HIP ids, bare metal)
+    device_env: str = Field("container", alias="deviceEnv")
+    # seconds between amd-smi rescans (modes switched by the partition agent) and
+    # reads of the node's partitioning label
+    rescan_seconds: float = Field(5.0, alias="rescanSeconds")
 
 
 class MetricsExporterConfig(_M):

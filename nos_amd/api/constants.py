@@ -41,6 +41,11 @@ ANNOTATION_PROBE_PREFIX = "nos.nebuly.com/probe-gpu"
 # new: desired/current partition modes written by the amdpart strategy / agent
 ANNOTATION_SPEC_MODE_FORMAT = "nos.nebuly.com/spec-mode-gpu-{index}"
 ANNOTATION_STATUS_MODE_FORMAT = "nos.nebuly.com/status-mode-gpu-{index}"
+# set by the partition agent while a GPU's last mode switch failed or is still
+# running past its deadline (value: the reason); removed once the GPU is healthy
+ANNOTATION_STATUS_ERROR_FORMAT = "nos.nebuly.com/status-error-gpu-{index}"
+ANNOTATION_STATUS_ERROR_PREFIX = "nos.nebuly.com/status-error-gpu-"
+MODE_SWITCHING = "SWITCHING"
 
 # --------------------------------------------------------------- resources
 RESOURCE_GPU_MEMORY = "nos.nebuly.com/gpu-memory"  # v1alpha1/constants.go:24-27 (GB)

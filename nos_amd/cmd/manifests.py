@@ -474,7 +474,8 @@ def node_agents() -> dict[str, list[dict]]:
     cfg = {"apiVersion": C.CONFIG_API_VERSION, "kind": "DevicePluginConfig",
            "health": {"healthProbeBindAddress": ":8081"},
            "configMap": {"name": C.DEFAULT_DEVICE_PLUGIN_CM_NAME, "namespace": _ns()},
-           "socketDir": C.DEVICE_PLUGIN_DIR, "cuPolicy": gp["cuPolicy"]}
+           "socketDir": C.DEVICE_PLUGIN_DIR, "cuPolicy": gp["cuPolicy"], "deviceEnv": "container",
+           "rescanSeconds": 5}
     c = _container("device-plugin", "nos_amd.cmd.deviceplugin", ["--config", "/etc/nos-amd/device_plugin_config.yaml"],
                    image=IMAGE_ROCM, env=NODE_ENV,
                    mounts=HOST_MOUNTS + [{"name": "device-plugins", "mountPath": C.DEVICE_PLUGIN_DIR}, mnt],

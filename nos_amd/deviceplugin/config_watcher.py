@@ -27,9 +27,9 @@ class ConfigWatcher:
         self.cm_ref = cm_ref or DevicePluginConfigRef()
         self.loads = 0
 
-    def reconcile(self, req: Request) -> Result:
+    def reconcile(self, req: Request | None) -> Result:
         node = self.api.try_get("Node", self.node_name)
-        if node is None:
+        if node is None or self.plugin.mode != C.PARTITIONING_CUMASK:
             return Result()
         key = ko.labels(node).get(C.LABEL_DEVICE_PLUGIN_CONFIG)
         if not key:

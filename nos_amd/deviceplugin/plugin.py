@@ -12,15 +12,25 @@ Replaces the NVIDIA device plugin + MPS daemon the reference depends on
   GPU as listed by the gpupartitioner's plugin ConfigMap entry.
 
 ``allocate`` returns what a real ``ContainerAllocateResponse`` carries:
-``HIP_VISIBLE_DEVICES`` (the physical / logical GPU), ``ROC_GLOBAL_CU_MASK``
+``HIP_VISIBLE_DEVICES`` (``device_env="container"``, the DaemonSet default:
+0..k-1 over the allocated render nodes in host order, because the container
+runtime mounts only those nodes and HIP numbers what it sees from 0;
+``"host"``: host HIP ids, for tenants that see every GPU -- simulator, bare
+metal), ``ROC_GLOBAL_CU_MASK``
 for slices (XCD-symmetric, see :mod:`nos_amd.gpu.topology`),
 ``NOS_AMD_MEMORY_LIMIT_GB`` (cooperative memory cap; AMD has no MPS-style hard
 limit, SURVEY.md 7.4 hard part 3) and the ``/dev/kfd`` + ``/dev/dri/renderD*``
 device nodes.  CU masks of allocated replicas never move: when the slice
 table changes, new replicas are laid out in the CU slots left free.
 
-The configuration is re-read on change (no plugin restart, unlike the
-reference's NVIDIA plugin).  :mod:`nos_amd.deviceplugin.grpc_server` exposes
+The slice table is re-read on change (no plugin restart, unlike the
+reference's NVIDIA plugin).  Partition modes are a different matter: an
+amd-smi session only sees the devices it enumerated, so a mode switched by
+the partition agent (another process) becomes visible when :meth:`rescan`
+re-enumerates (``nos_smi_rescan``); the plugin binary calls it every poll,
+and it follows the node's partitioning label (:meth:`set_mode`).  The agent
+still restarts the plugin pod after a switch (``agents/dpclient.py``), the
+reference-compatible path.  :mod:`nos_amd.deviceplugin.grpc_server` exposes
 this object over the kubelet device-plugin v1beta1 gRPC API.
 """
 from __future__ import annotations
@@ -90,6 +100,31 @@ class NosAmdDevicePlugin:
     def _gpus(self) -> list[GpuInfo]:
         return self.smi.gpus()
 
+    def rescan(self) -> None:
+        """Re-enumerate amd-smi (modes another process switched become visible),
+        then recompute the devices.  A GPU whose switch is in flight keeps its
+        current devices until the next poll."""
+        rs = getattr(self.smi, "rescan", None)
+        if rs is not None:
+            try:
+                rs()
+            except Exception as e:  # e.g. a switch of this session in flight: retry next poll
+                log.info("amd-smi rescan deferred: %s", e)
+        self.refresh()
+
+    def set_mode(self, mode: str | None) -> bool:
+        """Follow the node's ``nos.nebuly.com/gpu-partitioning`` label (read
+        once at start-up before).  Returns True when the mode changed."""
+        with self._lock:
+            if mode == self.mode:
+                return False
+            log.info("node %s: partitioning mode %s -> %s", self.node_name, self.mode, mode)
+            self.mode = mode
+            if mode != C.PARTITIONING_CUMASK:
+                self.config, self.config_key = None, None
+        self.refresh()
+        return True
+
     def set_config(self, key: str | None, cfg_yaml: str | dict | None) -> None:
         with self._lock:
             self.config_key = key
@@ -116,6 +151,9 @@ class NosAmdDevicePlugin:
                 # one device per logical partition amd-smi enumerates for the GPU, named
                 # from the GPU's reported memory / XCDs (same function as the planner)
                 for gi in gpus:
+                    if getattr(gi, "switching", False):  # cannot be enumerated now: keep what it had
+                        devs.update({k: d for k, d in self.devices.items() if d.gpu_index == gi.index})
+                        continue
                     parts = self.smi.partitions(gi.index)
                     prof = str(partition_profile(gi.memory_gb, gi.num_xcds or MI355X_XCDS, len(parts)))
                     res = C.RESOURCE_AMD_GPU if self.expose_partitions_as_gpu else C.AMD_PARTITION_RESOURCE_PREFIX + prof
@@ -155,14 +193,16 @@ class NosAmdDevicePlugin:
         for d in self.devices.values():
             if d.resource.startswith(C.AMD_SLICE_RESOURCE_PREFIX):
                 by_gpu.setdefault(d.gpu_index, []).append(d)
-        mem = {g.index: g.memory_gb for g in self._gpus()}
+        info = {g.index: g for g in self._gpus()}
         for gi, devs in by_gpu.items():
+            g = info.get(gi)
+            xcds, per_xcd = _cu_geometry(g)
             keep = {d.id: self.cu_slots[d.id].slots for d in devs if d.id in self.allocated and d.id in self.cu_slots}
             live = [d for d in devs if d.healthy or d.id in keep]
             got, bad = layout_slots([(d.id, d.memory_gb) for d in live], keep, self.cu_policy,
-                                    mem.get(gi, MI355X_MEMORY_GB), MI355X_CUS_PER_XCD)
+                                    g.memory_gb if g else MI355X_MEMORY_GB, per_xcd)
             for did, sl in got.items():
-                slots[did] = CUSlotSet(sl, MI355X_XCDS)
+                slots[did] = CUSlotSet(sl, xcds)
             for did in bad:
                 d = self.devices[did]
                 self.devices[did] = Device(d.id, d.resource, d.gpu_index, False, d.partition, d.profile, d.memory_gb,
@@ -248,8 +288,9 @@ class NosAmdDevicePlugin:
         with self._lock:
             alloc = ContainerAllocation(device_ids=list(device_ids))
             gpus = {g.index: g for g in self._gpus()}
-            visible: list[str] = []
+            visible: list[tuple[int, str]] = []   # (render minor, host HIP id)
             mask_cus: set[int] = set()
+            n_cus = 0
             mem = 0
             for did in device_ids:
                 d = self.devices.get(did)
@@ -260,22 +301,28 @@ class NosAmdDevicePlugin:
                 gi = gpus.get(d.gpu_index)
                 # logical partitions carry their own HIP id (amd-smi enumeration info)
                 hip = str(d.hip_id if d.hip_id >= 0 else (gi.hip_id if gi and gi.hip_id >= 0 else d.gpu_index))
-                if hip not in visible:
-                    visible.append(hip)
+                render = (d.drm_render if d.drm_render >= 0 else
+                          gi.drm_render if gi and gi.drm_render >= 0 else 128 + d.gpu_index)
+                if all(h != hip for _, h in visible):
+                    visible.append((render, hip))
                 if resource.startswith(C.AMD_SLICE_RESOURCE_PREFIX):
                     s = self.cu_slots.get(did)
                     if s is not None:
                         mask_cus.update(s.cus())
+                    xcds, per_xcd = _cu_geometry(gi)
+                    n_cus = max(n_cus, xcds * per_xcd)
                 mem += d.memory_gb
                 self.allocated[did] = owner or "unknown"
-                render = (d.drm_render if d.drm_render >= 0 else
-                          gi.drm_render if gi and gi.drm_render >= 0 else 128 + d.gpu_index)
                 dev = f"/dev/dri/renderD{render}"
                 if dev not in alloc.devices:
                     alloc.devices.append(dev)
             alloc.devices.insert(0, "/dev/kfd")
-            alloc.envs[C.ENV_VISIBLE_DEVICES] = ",".join(visible)
-            n_cus = MI355X_XCDS * MI355X_CUS_PER_XCD
+            if self.device_env == "container":
+                # the runtime mounts only the allocated render nodes; HIP numbers
+                # them 0..k-1 in host (render minor) order
+                alloc.envs[C.ENV_VISIBLE_DEVICES] = ",".join(str(k) for k in range(len(visible)))
+            else:
+                alloc.envs[C.ENV_VISIBLE_DEVICES] = ",".join(h for _, h in visible)
             if mask_cus and len(mask_cus) < n_cus:  # a full mask would only cost a dedicated HW queue
                 alloc.envs[C.ENV_CU_MASK] = mask_hex(sorted(mask_cus), n_cus)
             if mem:
@@ -309,6 +356,13 @@ class NosAmdDevicePlugin:
     def cus_of(self, device_id: str) -> list[int]:
         s = self.cu_slots.get(device_id)
         return s.cus() if s else []
+
+
+def _cu_geometry(g: GpuInfo | None) -> tuple[int, int]:
+    """(XCDs, CUs per XCD) of a GPU as amd-smi reports it (MI355X when unknown)."""
+    if g is None or not g.num_xcds or not g.num_cus or g.num_cus % g.num_xcds:
+        return MI355X_XCDS, MI355X_CUS_PER_XCD
+    return g.num_xcds, g.num_cus // g.num_xcds
 
 
 __all__ = ["NosAmdDevicePlugin", "Device", "ContainerAllocation", "logical_cu"]

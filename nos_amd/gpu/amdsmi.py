@@ -13,6 +13,7 @@ the MI355X replacement for the reference's NVML client
 from __future__ import annotations
 
 import ctypes
+import dataclasses
 import threading
 from dataclasses import dataclass
 from pathlib import Path
@@ -27,7 +28,9 @@ PARTITIONS_PER_MODE = {"SPX": 1, "DPX": 2, "TPX": 3, "QPX": 4, "CPX": 8}
 LINK_TYPES = {0: "internal", 1: "pcie", 2: "xgmi", 3: "n/a", 4: "unknown"}
 
 ERRORS = {0: "ok", -1: "not open", -2: "bad index", -3: "backend error", -4: "unsupported",
-          -5: "busy (processes on GPU)", -6: "injected fault", -7: "invalid argument", -8: "timeout"}
+          -5: "busy (processes on GPU)", -6: "injected fault", -7: "invalid argument", -8: "timeout",
+          -9: "mode switch in progress"}
+ERR_SWITCHING = -9
 
 
 class AmdSmiError(RuntimeError):
@@ -70,6 +73,7 @@ class GpuInfo:
     bdf: str
     uuid: str
     market_name: str
+    switching: bool = False  # a mode switch is in flight: the fields are the last known state
 
     @property
     def memory_gb(self) -> int:
@@ -154,6 +158,7 @@ class AmdSmi:
         if rc != 0:
             raise AmdSmiError(rc, f"amdsmi open ({backend})")
         AmdSmi._active = self
+        self._last: dict[int, GpuInfo] = {}
 
     @classmethod
     def real(cls, allow_set: bool = False) -> "AmdSmi":
@@ -168,6 +173,15 @@ class AmdSmi:
     def close(self) -> None:
         _L().nos_smi_close()
 
+    def rescan(self) -> None:
+        """Re-enumerate the devices.  The session enumerates at open and after
+        its own mode switches; a mode another process switched (the partition
+        agent, the amd-smi CLI) is only visible after this call.  Raises with
+        ``rc == ERR_SWITCHING`` while one of this session's switches runs."""
+        rc = _L().nos_smi_rescan()
+        if rc != 0:
+            raise AmdSmiError(rc, "rescan")
+
     # ------------------------------------------------------------- queries
     def count(self) -> int:
         n = _L().nos_smi_count()
@@ -180,12 +194,24 @@ class AmdSmi:
         rc = _L().nos_smi_gpu_info(i, ctypes.byref(g))
         if rc != 0:
             raise AmdSmiError(rc, f"gpu_info({i})")
-        return GpuInfo(g.index, g.num_cus, g.num_xcds, COMPUTE_MODES.get(g.compute_mode, "UNKNOWN"),
+        info = GpuInfo(g.index, g.num_cus, g.num_xcds, COMPUTE_MODES.get(g.compute_mode, "UNKNOWN"),
                        MEMORY_MODES.get(g.memory_mode, "UNKNOWN"), g.num_partitions, g.hip_id, g.drm_render,
                        g.vram_mb, g.bdf.decode(), g.uuid.decode(), g.market_name.decode())
+        self._last[i] = info
+        return info
 
     def gpus(self) -> list[GpuInfo]:
-        return [self.gpu(i) for i in range(self.count())]
+        """Every GPU; one whose mode switch is in flight (in another thread) is
+        reported from its last known state with ``switching=True``."""
+        out = []
+        for i in range(self.count()):
+            try:
+                out.append(self.gpu(i))
+            except AmdSmiError as e:
+                if e.rc != ERR_SWITCHING or i not in self._last:
+                    raise
+                out.append(dataclasses.replace(self._last[i], switching=True))
+        return out
 
     def partitions(self, i: int) -> list[PartitionInfo]:
         """Logical devices of physical GPU ``i`` in enumeration order (amd-smi

@@ -7,12 +7,22 @@ node a :class:`FakeSmi` instead.  Semantics match the C++ fake backend
 (``csrc/amdsmi/nos_amdsmi.cpp``): a compute-partition switch is refused while
 the GPU has processes, the partition count follows the mode, and faults can
 be injected.
+
+Like a real amd-smi session it distinguishes the hardware from what the
+session enumerated: ``external_switch=<gpu>:<mode>`` changes the hardware
+only (another process switched the mode) and :meth:`rescan` makes it
+visible.  ``switch_delay_ms=<n>`` makes every switch take that long in real
+time WITHOUT holding the inventory lock; queries about a GPU whose switch is
+in flight raise ``AmdSmiError(ERR_SWITCHING)`` and :meth:`gpus` reports it
+from the last known state with ``switching=True`` (native library semantics).
 """
 from __future__ import annotations
 
+import dataclasses
 import threading
+import time
 
-from .amdsmi import PARTITIONS_PER_MODE, AmdSmiError, GpuInfo, PartitionInfo, ProcInfo
+from .amdsmi import ERR_SWITCHING, PARTITIONS_PER_MODE, AmdSmiError, GpuInfo, PartitionInfo, ProcInfo
 
 _MEMORY_MODES = ("NPS1", "NPS2", "NPS4", "NPS8")
 
@@ -28,8 +38,13 @@ class FakeSmi:
         self.node = node
         self.model = model
         self.cus, self.xcds, self.vram_mb = cus, xcds, vram_mb
-        self.compute = [compute] * gpus
+        self.compute = [compute] * gpus      # the session's view
         self.memory = [memory] * gpus
+        self.hw_compute = [compute] * gpus   # the hardware
+        self.hw_memory = [memory] * gpus
+        self.switching: set[int] = set()
+        self.switch_delay_s = 0.0
+        self._last: dict[int, GpuInfo] = {}
         self.procs: list[dict[int, ProcInfo]] = [dict() for _ in range(gpus)]
         self.activity_gfx = [0] * gpus
         self.activity_umc = [0] * gpus
@@ -41,25 +56,49 @@ class FakeSmi:
     def count(self) -> int:
         return len(self.compute) - len(self.lost)
 
+    def _check(self, i: int, what: str) -> None:
+        if i < 0 or i >= len(self.compute) or i in self.lost:
+            raise AmdSmiError(-2, f"{what}({i})")
+        if i in self.switching:
+            raise AmdSmiError(ERR_SWITCHING, f"{what}({i})")
+
     def gpu(self, i: int) -> GpuInfo:
         with self._lock:
-            if i < 0 or i >= len(self.compute) or i in self.lost:
-                raise AmdSmiError(-2, f"gpu({i})")
+            self._check(i, "gpu")
             base = sum(PARTITIONS_PER_MODE[self.compute[j]] for j in range(i) if j not in self.lost)
-            return GpuInfo(index=i, num_cus=self.cus, num_xcds=self.xcds, compute_mode=self.compute[i],
-                           memory_mode=self.memory[i], num_partitions=PARTITIONS_PER_MODE[self.compute[i]],
-                           hip_id=base, drm_render=128 + base, vram_mb=self.vram_mb, bdf=f"0000:{0x11 + i:02x}:00.0",
-                           uuid=f"GPU-{self.node}-{i:04d}", market_name=self.model)
+            g = GpuInfo(index=i, num_cus=self.cus, num_xcds=self.xcds, compute_mode=self.compute[i],
+                        memory_mode=self.memory[i], num_partitions=PARTITIONS_PER_MODE[self.compute[i]],
+                        hip_id=base, drm_render=128 + base, vram_mb=self.vram_mb, bdf=f"0000:{0x11 + i:02x}:00.0",
+                        uuid=f"GPU-{self.node}-{i:04d}", market_name=self.model)
+            self._last[i] = g
+            return g
 
     def gpus(self) -> list[GpuInfo]:
-        return [self.gpu(i) for i in range(len(self.compute)) if i not in self.lost]
+        """Every GPU; one whose mode switch is in flight is reported from its
+        last known state with ``switching=True`` (it cannot be queried now)."""
+        out = []
+        for i in range(len(self.compute)):
+            if i in self.lost:
+                continue
+            try:
+                out.append(self.gpu(i))
+            except AmdSmiError as e:
+                if e.rc != ERR_SWITCHING or i not in self._last:
+                    raise
+                out.append(dataclasses.replace(self._last[i], switching=True))
+        return out
+
+    def rescan(self) -> None:
+        with self._lock:
+            if self.switching:
+                raise AmdSmiError(ERR_SWITCHING, "rescan")
+            self.compute, self.memory = list(self.hw_compute), list(self.hw_memory)
 
     def partitions(self, i: int) -> list[PartitionInfo]:
         """Logical devices of GPU ``i``, numbered GPU-major like the driver
         enumerates them (same model as the C++ fake backend)."""
         with self._lock:
-            if i < 0 or i >= len(self.compute) or i in self.lost:
-                raise AmdSmiError(-2, f"partitions({i})")
+            self._check(i, "partitions")
             base = sum(PARTITIONS_PER_MODE[self.compute[j]] for j in range(i) if j not in self.lost)
             n = PARTITIONS_PER_MODE[self.compute[i]]
             shared = self.memory[i] == "NPS1" and n > 1
@@ -70,13 +109,16 @@ class FakeSmi:
                     for p in range(n)]
 
     def clock(self, i: int) -> dict[str, int]:
+        self._check(i, "clock")
         return {"sclk_mhz": 2400 if self.activity_gfx[i] > 0 else 500, "max_sclk_mhz": 2400}
 
     def activity(self, i: int) -> dict[str, int]:
+        self._check(i, "activity")
         return {"gfx": self.activity_gfx[i], "umc": self.activity_umc[i], "mm": 0}
 
     def processes(self, i: int, max_procs: int = 256) -> list[ProcInfo]:
         with self._lock:
+            self._check(i, "processes")
             return list(self.procs[i].values())[:max_procs]
 
     def link(self, i: int, j: int) -> dict:
@@ -85,31 +127,41 @@ class FakeSmi:
         return {"type": "xgmi", "hops": 1, "weight": 15}
 
     # ------------------------------------------------------------ setters
-    def set_compute_partition(self, i: int, mode: str) -> None:
+    def _switch(self, i: int, mode: str, compute: bool) -> None:
+        what = "set_compute_partition" if compute else "set_memory_partition"
         with self._lock:
-            if "fail_set_compute" in self.faults:
-                raise AmdSmiError(-3, f"set_compute_partition({i}, {mode})")
-            if mode not in PARTITIONS_PER_MODE:
-                raise AmdSmiError(-4, f"unsupported compute mode {mode}")
+            self._check(i, what)
+            if ("fail_set_compute" if compute else "fail_set_memory") in self.faults:
+                raise AmdSmiError(-3, f"{what}({i}, {mode})")
+            if mode not in (PARTITIONS_PER_MODE if compute else _MEMORY_MODES):
+                raise AmdSmiError(-4, f"unsupported {'compute' if compute else 'memory'} mode {mode}")
             if self.procs[i]:
                 raise AmdSmiError(-5, f"gpu {i} busy")
-            if self.compute[i] != mode:
-                if "stale_mode" in self.faults:  # the switch silently does not take effect
-                    return
-                self.compute[i] = mode
-                self.switches += 1
-                if "lose_after_switch" in self.faults:
-                    self.lost.add(i)
+            self.switching.add(i)
+            delay = self.switch_delay_s
+        try:
+            if delay > 0:  # the driver at work: the inventory lock is NOT held
+                time.sleep(delay)
+        finally:
+            with self._lock:
+                self.switching.discard(i)
+                hw = self.hw_compute if compute else self.hw_memory
+                if hw[i] != mode and "stale_mode" not in self.faults:  # stale: silently no effect
+                    hw[i] = mode
+                    if compute:
+                        self.switches += 1
+                    if "lose_after_switch" in self.faults:
+                        self.lost.add(i)
+                # the session re-enumerates after its own switch (GPUs still switching keep their view)
+                for j in range(len(self.compute)):
+                    if j not in self.switching:
+                        self.compute[j], self.memory[j] = self.hw_compute[j], self.hw_memory[j]
+
+    def set_compute_partition(self, i: int, mode: str) -> None:
+        self._switch(i, mode, True)
 
     def set_memory_partition(self, i: int, mode: str) -> None:
-        with self._lock:
-            if "fail_set_memory" in self.faults:
-                raise AmdSmiError(-3, f"set_memory_partition({i}, {mode})")
-            if mode not in _MEMORY_MODES:
-                raise AmdSmiError(-4, f"unsupported memory mode {mode}")
-            if self.procs[i]:
-                raise AmdSmiError(-5, f"gpu {i} busy")
-            self.memory[i] = mode
+        self._switch(i, mode, False)
 
     # ------------------------------------------------------------ fake controls
     def inject(self, fault: str) -> None:
@@ -117,8 +169,19 @@ class FakeSmi:
             if fault == "clear":
                 self.faults.clear()
                 self.lost.clear()
+                self.switch_delay_s = 0.0
             elif fault.startswith("lose_gpu="):
                 self.lost.add(int(fault.split("=", 1)[1]))
+            elif fault.startswith("switch_delay_ms="):
+                self.switch_delay_s = int(fault.split("=", 1)[1]) / 1000.0
+            elif fault.startswith("external_switch="):
+                gi, mode = fault.split("=", 1)[1].split(":", 1)
+                if mode in PARTITIONS_PER_MODE:
+                    self.hw_compute[int(gi)] = mode
+                elif mode in _MEMORY_MODES:
+                    self.hw_memory[int(gi)] = mode
+                else:
+                    raise AmdSmiError(-7, f"inject({fault})")
             else:
                 self.faults.add(fault)
 

@@ -63,6 +63,26 @@ def test_amdsmi_real_partitions_map_to_physical_gpus():
         smi.close()
 
 
+def test_amdsmi_real_rescan_keeps_the_handle_to_hip_id_mapping():
+    """nos_smi_rescan (the device plugin's poll) shuts the amd-smi session down
+    and enumerates again: the same physical GPUs, partitions and HIP ids /
+    render nodes must come back (no mode changed in between)."""
+    smi = _smi()
+    try:
+        def snapshot():
+            return [(g.index, g.uuid, g.bdf, g.hip_id, g.drm_render, g.compute_mode,
+                     tuple((p.partition, p.hip_id, p.drm_render) for p in smi.partitions(g.index)))
+                    for g in smi.gpus()]
+
+        before = snapshot()
+        smi.rescan()
+        after = snapshot()
+        assert before == after
+        assert all(not g.switching for g in smi.gpus())
+    finally:
+        smi.close()
+
+
 def test_amdsmi_real_readonly_queries():
     smi = _smi()
     try:

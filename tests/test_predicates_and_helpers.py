@@ -87,6 +87,8 @@ def test_device_plugin_restart_times_out_without_a_replacement():
 
 
 class _Plugin:
+    mode = C.PARTITIONING_CUMASK  # the watcher only loads slice tables on cumask nodes
+
     def __init__(self):
         self.config_key, self.config, self.loaded = None, None, []
 

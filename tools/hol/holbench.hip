@@ -11,9 +11,14 @@
 // serialise them (head-of-line blocking of a dispatch whose masked CUs are
 // full, or of a queue waiting on the previous kernel's barrier).
 //
-// holbench --seconds S --start-ns T --grid G --spin-us U --lds B --depth D
+// holbench --seconds S --start-ns T --grid G --spin-us U --lds B --depth D [--phases P]
 //   G = 0: one workgroup per resident slot of the mask ("fit"), G < 0:
-//   -G x fit ("oversubscribed").  Prints one JSON line.
+//   -G x fit ("oversubscribed").  --phases P > 0: "megakernel" mode -- each
+//   launch runs P spin phases separated by a grid-wide barrier (grid must be
+//   "fit": every workgroup resident), so a pod keeps at most `depth` packets in
+//   its queue for P phases of work.  The barrier gives up after 250 ms (flag
+//   in the output) so a non-resident grid can never hang the GPU.
+//   Prints one JSON line.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -43,6 +48,49 @@ __global__ __launch_bounds__(256) void spin_kernel(unsigned long long ticks, int
   if (lds[(threadIdx.x + 1) & 255] == 0x7fffffff) sink[blockIdx.x] = 1;  // keep LDS live, never taken
 }
 
+// grid-wide barrier over `nwg` co-resident workgroups (sense by generation);
+// every wave leaves after `limit` realtime ticks even if the grid never meets
+__device__ __forceinline__ bool grid_barrier(unsigned* count, unsigned* gen, unsigned nwg, int* abort_flag,
+                                             unsigned long long limit) {
+  __shared__ int ok;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ok = 1;
+    const unsigned g = __hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned arrived = __hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    if (arrived == nwg) {
+      __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+            __builtin_amdgcn_s_memrealtime() - t0 > limit) {
+          __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  }
+  __syncthreads();
+  return ok != 0;
+}
+
+__global__ __launch_bounds__(256) void phases_kernel(unsigned long long ticks, int phases, unsigned* bar,
+                                                     int* abort_flag, int* sink) {
+  extern __shared__ int lds[];
+  for (int p = 0; p < phases; ++p) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t = t0;
+    while (t - t0 < ticks) t = __builtin_amdgcn_s_memrealtime();
+    lds[threadIdx.x] = (int)t;
+    if (!grid_barrier(bar, bar + 1, gridDim.x, abort_flag, 25000000ull)) return;  // 250 ms
+  }
+  if (lds[(threadIdx.x + 1) & 255] == 0x7fffffff) sink[blockIdx.x] = 1;
+}
+
 static long long mono_ns() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -65,7 +113,7 @@ static int popcount_hex_mask(const char* s) {
 int main(int argc, char** argv) {
   double seconds = 3.0, spin_us = 50.0;
   long long start_ns = 0;
-  int grid = 0, lds = 40960, depth = 16, null_stream = 0;
+  int grid = 0, lds = 40960, depth = 16, null_stream = 0, phases = 0;
   const char* tag = "";
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string k = argv[i];
@@ -77,6 +125,7 @@ int main(int argc, char** argv) {
     else if (k == "--lds") lds = atoi(v);
     else if (k == "--depth") depth = atoi(v);
     else if (k == "--null-stream") null_stream = atoi(v);
+    else if (k == "--phases") phases = atoi(v);
     else if (k == "--tag") tag = v;
     else {
       fprintf(stderr, "unknown option %s\n", k.c_str());
@@ -98,13 +147,29 @@ int main(int argc, char** argv) {
   const int wg_per_cu = (160 * 1024) / lds < 8 ? (160 * 1024) / lds : 8;
   const int fit = cus * wg_per_cu;
   const int g = grid > 0 ? grid : grid == 0 ? fit : -grid * fit;
+  if (phases < 0 || phases > 4096 || (phases > 0 && g > fit)) {
+    fprintf(stderr, "--phases needs a grid that fits the mask's slots\n");
+    return 2;
+  }
   int* sink = nullptr;
   CK(hipMalloc(&sink, sizeof(int) * (size_t)g));
+  unsigned* bar = nullptr;
+  int* abort_flag = nullptr;
+  CK(hipMalloc(&bar, 2 * sizeof(unsigned)));
+  CK(hipMalloc(&abort_flag, sizeof(int)));
+  CK(hipMemset(bar, 0, 2 * sizeof(unsigned)));
+  CK(hipMemset(abort_flag, 0, sizeof(int)));
   hipStream_t st = nullptr;
   if (!null_stream) CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   // realtime counter: 100 MHz on MI300-class parts
   const unsigned long long ticks = (unsigned long long)(spin_us * 100.0);
-  hipLaunchKernelGGL(spin_kernel, dim3(g), dim3(256), lds, st, ticks, sink);  // warm-up
+  auto launch = [&]() {
+    if (phases > 0)  // the barrier's own LDS word: keep the per-CU total at (160 KB / lds) workgroups
+      hipLaunchKernelGGL(phases_kernel, dim3(g), dim3(256), lds - 1024, st, ticks, phases, bar, abort_flag, sink);
+    else
+      hipLaunchKernelGGL(spin_kernel, dim3(g), dim3(256), lds, st, ticks, sink);
+  };
+  launch();  // warm-up
   CK(hipGetLastError());
   CK(hipStreamSynchronize(st));
   while (start_ns && mono_ns() < start_ns) usleep(200);
@@ -114,9 +179,9 @@ int main(int argc, char** argv) {
   std::vector<double> batch_ms;
   while (mono_ns() < t_end) {
     const long long b0 = mono_ns();
-    for (int d = 0; d < depth; ++d) hipLaunchKernelGGL(spin_kernel, dim3(g), dim3(256), lds, st, ticks, sink);
+    for (int d = 0; d < depth; ++d) launch();
     CK(hipStreamSynchronize(st));
-    kernels += depth;
+    kernels += depth * (phases > 0 ? phases : 1);
     batch_ms.push_back((mono_ns() - b0) / 1e6);
   }
   const double el = (mono_ns() - t0) / 1e9;
@@ -125,14 +190,18 @@ int main(int argc, char** argv) {
   double mn = 1e30, mx = 0;
   for (double v : batch_ms) { mn = v < mn ? v : mn; mx = v > mx ? v : mx; }
   const double ideal_kernel_ms = spin_us * 1e-3 * ((g + fit - 1) / fit);
+  int aborted = 0;
+  CK(hipMemcpy(&aborted, abort_flag, sizeof(int), hipMemcpyDeviceToHost));
   printf("{\"tag\": \"%s\", \"pid\": %d, \"cus\": %d, \"mask\": \"%s\", \"wg_per_cu\": %d, \"fit\": %d, \"grid\": %d, "
          "\"spin_us\": %.1f, \"depth\": %d, \"null_stream\": %d, \"kernels\": %lld, \"elapsed_s\": %.4f, "
          "\"kernel_ms\": %.4f, \"ideal_kernel_ms\": %.4f, \"slot_efficiency\": %.4f, \"batch_ms_min\": %.3f, "
-         "\"batch_ms_max\": %.3f, \"t0_ns\": %lld}\n",
+         "\"batch_ms_max\": %.3f, \"t0_ns\": %lld, \"phases\": %d, \"barrier_aborted\": %d}\n",
          tag, (int)getpid(), cus, mask ? mask : "", wg_per_cu, fit, g, spin_us, depth, null_stream, kernels, el,
-         el * 1e3 / (double)kernels, ideal_kernel_ms, eff, mn, mx, t0);
+         el * 1e3 / (double)kernels, ideal_kernel_ms, eff, mn, mx, t0, phases, aborted);
   fflush(stdout);
   CK(hipFree(sink));
+  CK(hipFree(bar));
+  CK(hipFree(abort_flag));
   if (st) CK(hipStreamDestroy(st));
   return 0;
 }

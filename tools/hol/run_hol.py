@@ -45,7 +45,7 @@ def masks(n: int, per_xcd: int, mode: str) -> list[str | None]:
 
 
 def run_row(n: int, grid: int, hwq: int, mode: str, per_xcd: int, seconds: float, spin_us: float, lds: int,
-            depth: int, null_stream: int, timeout: float) -> dict:
+            depth: int, null_stream: int, timeout: float, phases: int = 0) -> dict:
     start = time.monotonic_ns() + int(4e9)
     procs = []
     for k, m in enumerate(masks(n, per_xcd, mode)):
@@ -57,7 +57,7 @@ def run_row(n: int, grid: int, hwq: int, mode: str, per_xcd: int, seconds: float
             env["GPU_MAX_HW_QUEUES"] = str(hwq)
         cmd = [str(BIN), "--seconds", str(seconds), "--start-ns", str(start), "--grid", str(grid),
                "--spin-us", str(spin_us), "--lds", str(lds), "--depth", str(depth), "--null-stream", str(null_stream),
-               "--tag", f"{mode}-n{n}-g{grid}-q{hwq}-p{k}"]
+               "--phases", str(phases), "--tag", f"{mode}-n{n}-g{grid}-q{hwq}-d{depth}-ph{phases}-p{k}"]
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     pods = []
     for p in procs:
@@ -72,6 +72,7 @@ def run_row(n: int, grid: int, hwq: int, mode: str, per_xcd: int, seconds: float
         pods.append(json.loads(out.strip().splitlines()[-1]))
     effs = [q.get("slot_efficiency", 0.0) for q in pods]
     return {"pods": n, "grid": grid, "hw_queues": hwq, "mask": mode, "per_xcd": per_xcd, "null_stream": null_stream,
+            "depth": depth, "phases": phases, "aborted": sum(q.get("barrier_aborted", 0) for q in pods),
             "eff_min": round(min(effs), 3), "eff_max": round(max(effs), 3),
             "eff_mean": round(sum(effs) / len(effs), 3), "per_pod": pods}
 
@@ -86,7 +87,8 @@ def main() -> None:
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--spin-us", type=float, default=50.0)
     ap.add_argument("--lds", type=int, default=40960)
-    ap.add_argument("--depth", type=int, default=16)
+    ap.add_argument("--depth", default="16", help="comma list: kernels queued per host synchronize")
+    ap.add_argument("--phases", default="0", help="comma list: 0 = one spin per launch, P = megakernel of P phases")
     ap.add_argument("--null-stream", type=int, default=0)
     ap.add_argument("--out", default="gpurun_out/hol.json")
     a = ap.parse_args()
@@ -95,9 +97,11 @@ def main() -> None:
     for mode in a.masks.split(","):
         for hwq in map(int, a.hw_queues.split(",")):
             for grid in map(int, a.grids.split(",")):
+              for depth in map(int, a.depth.split(",")):
+               for phases in map(int, a.phases.split(",")):
                 for n in map(int, a.pods.split(",")):
-                    r = run_row(n, grid, hwq, mode, a.per_xcd, a.seconds, a.spin_us, a.lds, a.depth, a.null_stream,
-                                timeout=a.seconds + 60)
+                    r = run_row(n, grid, hwq, mode, a.per_xcd, a.seconds, a.spin_us, a.lds, depth, a.null_stream,
+                                timeout=a.seconds + 60, phases=phases)
                     print(json.dumps({k: v for k, v in r.items() if k != "per_pod"}), flush=True)
                     rows.append(r)
                     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
