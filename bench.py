@@ -326,11 +326,15 @@ def main(argv=None) -> int:
         log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using {world}")
     # control plane first (CPU only): the GPU is initialised by the pods, then by this rank
     envs, cp = plan(args, world, local, args.slice_gb, args.pods_per_gpu, args.mode)
+    from nos_amd.api import constants as C
+    from nos_amd.bench_support import schedulable_pods
+
     cp10 = {}
     if args.slice_gb != 10:
-        from nos_amd.bench_support import schedulable_pods
-
         cp10 = schedulable_pods(world, 10)
+    # hybrid partitioning (modes + memory slices per partition): simulated only --
+    # the pool cannot switch compute/memory modes (needs root), parity unpinned
+    hyb10 = schedulable_pods(world, 10, kind=C.PARTITIONING_HYBRID)
     extra_env = {"GPU_MAX_HW_QUEUES": str(args.hw_queues)} if args.hw_queues else {}
     if args.device == "cpu":
         extra_env["OMP_NUM_THREADS"] = "1"
@@ -434,6 +438,11 @@ def main(argv=None) -> int:
         "schedulable_fractional_pods_per_node_sim": cp.get("schedulable_fractional_pods_per_node"),
         "schedulable_10gb_pods_per_node_sim": cp10.get("schedulable_fractional_pods_per_node",
                                                        cp.get("schedulable_fractional_pods_per_node")),
+        # the same 10 GB pods on a simulated HYBRID node of this many MI355X (the
+        # partitioner picks each GPU's compute/memory mode; 8 HWS process slots per
+        # partition): simulation, not hardware -- the pool cannot switch modes
+        "schedulable_10gb_pods_per_node_hybrid_sim": hyb10["schedulable_fractional_pods_per_node"],
+        "hybrid_sim_modes": hyb10.get("modes"),
         "aggregate_inf_per_s": round(agg, 3),
         "aggregate_inf_per_s_vs_baseline": round(agg / (BASELINE_INF_PER_S_PER_GPU * world), 2),
         "mean_latency_s": None if lat is None else round(lat, 5),

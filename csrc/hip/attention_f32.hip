@@ -57,7 +57,9 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_ba
 // (batch, head, q-block) and merge (m, l, O) through LDS at the end -- two
 // waves per SIMD from ONE workgroup, so a single pod (162 q-blocks for 256
 // CUs) still overlaps one wave's softmax with the other's MFMAs.
-template <int W, int KVB, int G, int OCC = 1>  // OCC: workgroups per CU the register budget must allow
+// OCC: workgroups per CU the register budget must allow; PERSIST: the
+// slice-sized-grid instantiation (a chunk of items per workgroup)
+template <int W, int KVB, int G, int OCC = 1, bool PERSIST = false>
 __global__ __launch_bounds__(64 * W * G, OCC) void attn_fwd_f32_d64_kernel(
     const float* __restrict__ q, const float* __restrict__ k, const float* __restrict__ v, float* __restrict__ o,
     int B, int H, int Sq, int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, int nqb) {
@@ -72,7 +74,18 @@ __global__ __launch_bounds__(64 * W * G, OCC) void attn_fwd_f32_d64_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int nwg = B * H * nqb;
-  const int wg = nos::xcd_remap(blockIdx.x, nwg);
+  // one (batch, head, q-block) per workgroup, or a chunk of them with a
+  // slice-sized grid (nos::xcd_chunk); the q-blocks of a head share an XCD
+  nos::XcdChunk chunk;
+  if constexpr (PERSIST) {
+    chunk = nos::xcd_chunk(blockIdx.x, gridDim.x, nwg);
+  } else {
+    chunk.first = nos::xcd_remap(blockIdx.x, nwg);
+    chunk.end = chunk.first + 1;
+    chunk.step = 1;
+  }
+  for (int wg = chunk.first; wg < chunk.end; wg += chunk.step) {
+  if (PERSIST && wg != chunk.first) __syncthreads();  // the previous item's ring / merge buffer is free
   const int b = wg / (H * nqb);
   const int rem = wg - b * (H * nqb);
   const int hd = rem / nqb;
@@ -227,7 +240,7 @@ __global__ __launch_bounds__(64 * W * G, OCC) void attn_fwd_f32_d64_kernel(
       xch[33 * 64 + lane] = l;
     }
     __syncthreads();
-    if (grp == 1) return;
+    if (grp == 1) continue;  // group 0 finishes the item; both meet at the next item's barrier
     const bool g1 = ntiles > 1;  // group 1 saw no tile when the sequence has one: its m means nothing
     const float m1 = xch[32 * 64 + lane], l1 = xch[33 * 64 + lane];
     const float mf = g1 ? fmaxf(m, m1) : m;
@@ -257,6 +270,7 @@ __global__ __launch_bounds__(64 * W * G, OCC) void attn_fwd_f32_d64_kernel(
         *reinterpret_cast<float4*>(op + 32 * dt + 8 * g + 4 * h) = y;
       }
   }
+  }  // items
 }
 
 template <int W, int KVB, int G, int OCC = 1>
@@ -266,8 +280,13 @@ int launch(const float* q, const float* k, const float* v, float* o, int B, int 
   const long long nwg = (long long)B * H * nqb;
   if (nwg > (1LL << 30)) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)G * 2 * 2 * KVB * ROW_BYTES;
-  hipLaunchKernelGGL((attn_fwd_f32_d64_kernel<W, KVB, G, OCC>), dim3((unsigned)nwg), dim3(64 * W * G), lds, stream, q,
-                     k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
+  const int grid = nos_grid_for((const void*)attn_fwd_f32_d64_kernel<W, KVB, G, OCC, true>, 64 * W * G, lds, nwg);
+  if (grid < nwg)
+    hipLaunchKernelGGL((attn_fwd_f32_d64_kernel<W, KVB, G, OCC, true>), dim3((unsigned)grid), dim3(64 * W * G), lds,
+                       stream, q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
+  else
+    hipLaunchKernelGGL((attn_fwd_f32_d64_kernel<W, KVB, G, OCC, false>), dim3((unsigned)nwg), dim3(64 * W * G), lds,
+                       stream, q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
   return (int)hipGetLastError();
 }
 

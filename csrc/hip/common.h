@@ -57,7 +57,32 @@ __device__ __forceinline__ int xcd_remap(int id, int nwg) {
   return base + idx;
 }
 
+// Persistent, XCD-aware work split (slice-sized grids).  The dispatcher deals
+// workgroup b to XCD b % 8; every XCD owns one contiguous chunk of the item
+// range (neighbouring items share its L2) and its workgroups walk the chunk
+// with a stride of the XCD's workgroup count.  With one workgroup per item
+// this is exactly xcd_remap; with a smaller grid each workgroup runs several
+// items.  Usage: for (int i = c.first; i < c.end; i += c.step) { ... }
+struct XcdChunk {
+  int first, end, step;
+};
+__device__ __forceinline__ XcdChunk xcd_chunk(int block, int grid, int n) {
+  const int nx = 8, xcd = block % nx, j = block / nx;
+  const int wgs_x = grid / nx + (xcd < grid % nx ? 1 : 0);
+  const int lo = xcd * (n / nx) + min(xcd, n % nx);
+  const int cnt = n / nx + (xcd < n % nx ? 1 : 0);
+  return XcdChunk{lo + j, lo + cnt, wgs_x > 0 ? wgs_x : 1};
+}
+
 }  // namespace nos
+
+// Grid cap for CU-slice tenants (runtime.hip): with a CU budget set
+// (nos_set_cu_budget, the pod's ROC_GLOBAL_CU_MASK popcount) a launch of
+// `items` workgroups is clamped to what the budgeted CUs hold at once
+// (occupancy x CUs, a multiple of 8), so the dispatch completes at launch and
+// never holds the command-processor pipe another pod's queue shares.
+// Returns `items` when no budget is set.
+int nos_grid_for(const void* kernel, int block_threads, size_t lds_bytes, long long items);
 
 #define HIP_CHECK_RET(expr)                       \
   do {                                            \

@@ -466,6 +466,8 @@ template <bool LNV, class CF, bool RV>
 void launch_cfg(int nwg, hipStream_t stream, const unsigned short* A, int lda, const unsigned short* W, int ldw,
                 const unsigned short* bias, const float* c1, const float* c2, const unsigned short* R, int ldr,
                 unsigned short* C, int ldc, int M, int N, int K, int epi, float eps, int tiles_m, int tiles_n) {
+  if (nwg == tiles_m * tiles_n)  // no explicit cap: a CU-slice tenant's budget (nos_set_cu_budget) applies
+    nwg = nos_grid_for((const void*)gemm_bf16_rk_kernel<LNV, CF, RV>, CF::NT, CF::LDS, nwg);
   hipLaunchKernelGGL((gemm_bf16_rk_kernel<LNV, CF, RV>), dim3(nwg), dim3(CF::NT), CF::LDS, stream, A, lda, W, ldw,
                      bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
 }

@@ -65,7 +65,10 @@ __device__ __forceinline__ float erf_fast(float x) {  // Abramowitz-Stegun 7.1.2
   return copysignf(r, x);
 }
 
-template <bool LN, int BM, int BN>
+// PERSIST: the slice-sized-grid instantiation (a chunk of tiles per
+// workgroup); the one-tile instantiation compiles the loop away and keeps the
+// register budget of a plain tile kernel
+template <bool LN, int BM, int BN, bool PERSIST>
 __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(
     const float* __restrict__ A, int lda, const float* __restrict__ W, int ldw, const float* __restrict__ bias,
     const float* __restrict__ c1, const float* __restrict__ c2, const float* __restrict__ R, int ldr,
@@ -80,10 +83,21 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(
   const int c = lane & 31, h = lane >> 5;
   const int wm = wid >> 1, wn = wid & 1;
   const int ntiles = tiles_m * tiles_n;
-  const int tt = nos::xcd_remap(blockIdx.x, ntiles);
-  const int tm = tt / tiles_n, tn = tt - tm * tiles_n;  // row-major: tiles of one A panel share an XCD
-  const int m0 = tm * BM, n0 = tn * BN;
   const int nk = K / BK;
+  // one tile per workgroup, or -- with a slice-sized grid -- a chunk of tiles
+  // per workgroup (nos::xcd_chunk); tiles of one A panel share an XCD's L2
+  nos::XcdChunk chunk;
+  if constexpr (PERSIST) {
+    chunk = nos::xcd_chunk(blockIdx.x, gridDim.x, ntiles);
+  } else {
+    chunk.first = nos::xcd_remap(blockIdx.x, ntiles);
+    chunk.end = chunk.first + 1;
+    chunk.step = 1;
+  }
+  for (int tt = chunk.first; tt < chunk.end; tt += chunk.step) {
+  if (PERSIST && tt != chunk.first) __syncthreads();  // the previous tile's ring and LN statistics are free
+  const int tm = tt / tiles_n, tn = tt - tm * tiles_n;  // row-major
+  const int m0 = tm * BM, n0 = tn * BN;
 
   f32x16_t acc[MI][NI];
 #pragma unroll
@@ -204,6 +218,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(
       }
     }
   }
+  }  // tiles
 }
 
 template <bool LN, int BM, int BN>
@@ -213,8 +228,13 @@ int launch_t(const float* A, int lda, const float* W, int ldw, const float* bias
   const long long ntiles = (long long)tiles_m * tiles_n;
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
   const size_t lds = 2 * (size_t)(BM + BN) * ROWB + 2 * BM * sizeof(float);
-  hipLaunchKernelGGL((gemm_f32_kernel<LN, BM, BN>), dim3((unsigned)ntiles), dim3(NT), lds, st, A, lda, W, ldw, bias,
-                     c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+  const int grid = nos_grid_for((const void*)gemm_f32_kernel<LN, BM, BN, true>, NT, lds, ntiles);
+  if (grid < ntiles)
+    hipLaunchKernelGGL((gemm_f32_kernel<LN, BM, BN, true>), dim3((unsigned)grid), dim3(NT), lds, st, A, lda, W, ldw,
+                       bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<LN, BM, BN, false>), dim3((unsigned)ntiles), dim3(NT), lds, st, A, lda, W,
+                       ldw, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
   return (int)hipGetLastError();
 }
 

@@ -10,6 +10,46 @@
 // probe_placement maps that numbering to XCDs).
 #include "common.h"
 
+#include <mutex>
+#include <unordered_map>
+
+namespace {
+int g_cu_budget = 0;  // 0: no budget (one workgroup per item)
+std::mutex g_occ_mu;
+std::unordered_map<unsigned long long, int> g_occ;  // (kernel, lds) -> resident workgroups per CU
+}  // namespace
+
+// CUs this process may use (a CU-mask slice's popcount); 0 switches the cap off.
+NOS_API int nos_set_cu_budget(int cus) {
+  if (cus < 0) return (int)hipErrorInvalidValue;
+  g_cu_budget = cus;
+  return 0;
+}
+
+NOS_API int nos_get_cu_budget() { return g_cu_budget; }
+
+int nos_grid_for(const void* kernel, int block_threads, size_t lds_bytes, long long items) {
+  if (g_cu_budget <= 0 || items <= 8) return (int)items;
+  const unsigned long long key = (unsigned long long)(uintptr_t)kernel ^ ((unsigned long long)lds_bytes << 48);
+  int occ = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    auto it = g_occ.find(key);
+    if (it != g_occ.end()) occ = it->second;
+  }
+  if (occ == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, block_threads, lds_bytes) != hipSuccess ||
+        occ <= 0)
+      occ = 1;
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    g_occ[key] = occ;
+  }
+  long long cap = (long long)occ * g_cu_budget;
+  cap -= cap % 8;
+  if (cap < 8) cap = 8;
+  return (int)(items < cap ? items : cap);
+}
+
 NOS_API int nos_stream_create_cumask(const unsigned* mask_words, int nwords, void** out_stream) {
   hipStream_t s = nullptr;
   hipError_t e;

@@ -23,8 +23,8 @@ CAPACITY_OVER_QUOTA = "over-quota"
 # PartitioningKind values (pkg/gpu/partitioning.go:87-91 had mig|mps|hybrid)
 PARTITIONING_AMDPART = "partition"  # compute/memory partition modes (MIG analogue)
 PARTITIONING_CUMASK = "cumask"      # CU-mask slices (MPS analogue)
-PARTITIONING_HYBRID = "hybrid"      # declared, not used (as in the reference)
-PARTITIONING_KINDS = (PARTITIONING_AMDPART, PARTITIONING_CUMASK)
+PARTITIONING_HYBRID = "hybrid"      # partition modes + memory slices per partition (gpu/hybrid.py)
+PARTITIONING_KINDS = (PARTITIONING_AMDPART, PARTITIONING_CUMASK, PARTITIONING_HYBRID)
 
 # --------------------------------------------------------------- annotations
 # v1alpha1/annotations.go:21-58 -- kept exactly

@@ -36,17 +36,23 @@ def cus_from_hex(mask: str) -> list[int]:
     return out
 
 
-def _cluster(n_gpus: int, num_cus: int, placement: str, cu_policy: str) -> SimCluster:
+def _cluster(n_gpus: int, num_cus: int, placement: str, cu_policy: str, kind: str = C.PARTITIONING_CUMASK
+             ) -> SimCluster:
     cfg = GpuPartitionerConfig(slicePlacement=placement, cuPolicy=cu_policy)
     cl = SimCluster(partitioner_config=cfg)
-    cl.add_node("mi355x-0", C.PARTITIONING_CUMASK, smi=FakeSmi(gpus=n_gpus, cus=num_cus, node="mi355x-0"))
+    cl.add_node("mi355x-0", kind, smi=FakeSmi(gpus=n_gpus, cus=num_cus, node="mi355x-0"))
     cl.settle(30)
     return cl
 
 
 def schedulable_pods(n_gpus: int, slice_gb: int, num_cus: int = 256, placement: str = "spread",
-                     per_gpu_attempt: int = 40) -> dict:
-    cl = _cluster(n_gpus, num_cus, placement, "even")
+                     per_gpu_attempt: int = 40, kind: str = C.PARTITIONING_CUMASK) -> dict:
+    """Submit ``per_gpu_attempt`` x GPUs slice pods to a fresh simulated node of
+    ``kind`` and count how many reach Running through the real scheduler,
+    partitioner, agents and device plugin (cumask: one logical GPU per MI355X,
+    8 HWS process slots; hybrid: the partitioner also picks each GPU's
+    compute/memory mode, 8 slots per partition)."""
+    cl = _cluster(n_gpus, num_cus, placement, "even", kind)
     total = n_gpus * per_gpu_attempt
     for i in range(total):
         cl.submit_pod(f"cap-{i}", {f"{C.AMD_SLICE_RESOURCE_PREFIX}{slice_gb}gb": 1})
@@ -58,9 +64,13 @@ def schedulable_pods(n_gpus: int, slice_gb: int, num_cus: int = 256, placement: 
         if running == last:
             break
         last = running
-    return {"schedulable_fractional_pods_per_node": len(cl.running_pods()),
-            "capacity_probe_sim_seconds": round(sim_s, 3), "capacity_probe_wall_seconds":
-                round(time.perf_counter() - t0, 3)}
+    out = {"schedulable_fractional_pods_per_node": len(cl.running_pods()),
+           "capacity_probe_sim_seconds": round(sim_s, 3), "capacity_probe_wall_seconds":
+               round(time.perf_counter() - t0, 3)}
+    if kind == C.PARTITIONING_HYBRID:
+        node = cl.nodes["mi355x-0"]
+        out["modes"] = [f"{c}/{m}" for c, m in zip(node.smi.compute, node.smi.memory)]
+    return out
 
 
 def control_plane_plan(n_gpus: int, pods_per_gpu: int, slice_gb: int, num_cus: int, local_gpu: int = 0,

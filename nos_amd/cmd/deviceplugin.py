@@ -23,7 +23,7 @@ def main(argv=None) -> int:
     from ..api import constants as C
     from ..deviceplugin.config_watcher import ConfigWatcher
     from ..deviceplugin.grpc_server import DevicePluginServers
-    from ..deviceplugin.plugin import NosAmdDevicePlugin
+    from ..deviceplugin.plugin import SLICE_MODES, NosAmdDevicePlugin
     from ..gpu.core import partitioning_kind
     from ..partitioning.strategies import DevicePluginConfigRef
     from .partagent import open_lister, open_smi
@@ -59,7 +59,7 @@ def main(argv=None) -> int:
         while not stop.wait(cfg.rescan_seconds):
             try:
                 n = api.try_get("Node", node)
-                if n is not None and plugin.set_mode(partitioning_kind(n)) and plugin.mode == C.PARTITIONING_CUMASK:
+                if n is not None and plugin.set_mode(partitioning_kind(n)) and plugin.mode in SLICE_MODES:
                     watcher.reconcile(None)
                 plugin.rescan()
             except Exception as e:

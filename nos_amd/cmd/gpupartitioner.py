@@ -1,6 +1,7 @@
 """nos-amd gpupartitioner (``cmd/gpupartitioner/gpupartitioner.go:72-268``):
 cluster state controllers + one partitioner controller per AMD strategy
-(``partition`` = compute/memory modes, ``cumask`` = CU-mask slices), planning
+(``partition`` = compute/memory modes, ``cumask`` = CU-mask slices,
+``hybrid`` = modes + memory slices per partition), planning
 with an embedded scheduler framework built from the scheduler config.
 
 python -m nos_amd.cmd.gpupartitioner --config gpu_partitioner_config.yaml
@@ -18,7 +19,7 @@ def build(api, cfg):
     from ..controllers.gpupartitioner import NodeController, PartitionerController, PodController
     from ..gpu import amdpart
     from ..partitioning.state import ClusterState
-    from ..partitioning.strategies import DevicePluginConfigRef, amdpart_strategy, cumask_strategy
+    from ..partitioning.strategies import DevicePluginConfigRef, amdpart_strategy, cumask_strategy, hybrid_strategy
     from ..scheduler.config import build_framework, load, nos_scheduler_config
 
     if cfg.known_partition_geometries_file:
@@ -32,10 +33,11 @@ def build(api, cfg):
     ref = DevicePluginConfigRef(cfg.device_plugin_config_map.name, cfg.device_plugin_config_map.namespace)
     amd = amdpart_strategy(api, None, cfg.reserve_whole_gpus, cfg.preferred_memory_mode)
     cum = cumask_strategy(api, ref, cfg.device_plugin_delay_seconds, None, cfg.cu_policy, cfg.slice_placement)
+    hyb = hybrid_strategy(api, ref, cfg.device_plugin_delay_seconds, None)
     mgr = common.manager_for(api, "nos-gpupartitioner", cfg)
     mgr.add(NodeController(api, cs, amd.initializer).controller())
     mgr.add(PodController(api, cs).controller())
-    for strat in (amd, cum):
+    for strat in (amd, cum, hyb):
         mgr.add(PartitionerController(api, cs, strat, fw, None, cfg.batch_window_timeout_seconds,
                                       cfg.batch_window_idle_seconds, cfg.plan_report_timeout_seconds).controller())
     return mgr

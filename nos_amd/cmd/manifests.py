@@ -213,7 +213,14 @@ HOST_MOUNTS = [
 ]
 
 
-def _daemonset(name: str, container: dict, kind: str, volumes: list[dict]) -> dict:
+def _daemonset(name: str, container: dict, kind: str | tuple[str, ...], volumes: list[dict]) -> dict:
+    if not isinstance(kind, str):  # several partitioning kinds: node affinity instead of a selector
+        ds = _daemonset(name, container, kind[0], volumes)
+        spec = ds["spec"]["template"]["spec"]
+        del spec["nodeSelector"]
+        spec["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
+            {"matchExpressions": [{"key": C.LABEL_GPU_PARTITIONING, "operator": "In", "values": list(kind)}]}]}}}
+        return ds
     return {"apiVersion": "apps/v1", "kind": "DaemonSet",
             "metadata": {"name": name, "namespace": _ns(), "labels": {"app": name}},
             "spec": {"selector": {"matchLabels": {"app": name}},
@@ -447,7 +454,8 @@ def node_agents() -> dict[str, list[dict]]:
     c = _container("partagent", "nos_amd.cmd.partagent", ["--config", "/etc/nos-amd/partition_agent_config.yaml"],
                    image=IMAGE_ROCM, env=NODE_ENV, mounts=HOST_MOUNTS + [mnt], privileged=True)
     if pa["enabled"]:
-        ds = _daemonset(name, c, C.PARTITIONING_AMDPART, HOST_VOLUMES + [vol])
+        # hybrid nodes run it too: it switches their modes, its hybrid reporter reports slices
+        ds = _daemonset(name, c, (C.PARTITIONING_AMDPART, C.PARTITIONING_HYBRID), HOST_VOLUMES + [vol])
         out["partagent/daemonset.yaml"] = [_sa(name), _config_map(name + "-config", {
             "partition_agent_config.yaml": yaml.safe_dump(cfg)}), ds]
         out["partagent/rbac.yaml"] = _cluster_role(name, node_rules + _auth_proxy_rules())
@@ -481,7 +489,7 @@ def node_agents() -> dict[str, list[dict]]:
                    mounts=HOST_MOUNTS + [{"name": "device-plugins", "mountPath": C.DEVICE_PLUGIN_DIR}, mnt],
                    privileged=True)
     dss = []
-    for kind in (C.PARTITIONING_CUMASK, C.PARTITIONING_AMDPART):
+    for kind in (C.PARTITIONING_CUMASK, C.PARTITIONING_AMDPART, C.PARTITIONING_HYBRID):
         ds = _daemonset(f"{name}-{kind}", c, kind, HOST_VOLUMES + [vol])
         ds["spec"]["template"]["metadata"]["labels"] = {"app": name}
         ds["spec"]["selector"]["matchLabels"] = {"app": name, "nos.nebuly.com/kind": kind}

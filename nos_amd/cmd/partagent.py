@@ -1,7 +1,7 @@
 """nos-amd partition agent (the reference's ``cmd/migagent/migagent.go:56-163``):
-per-node DaemonSet on ``nos.nebuly.com/gpu-partitioning=partition`` nodes.
-Reports the node's compute/memory partitions and applies the gpupartitioner's
-plans with amd-smi.
+per-node DaemonSet on ``nos.nebuly.com/gpu-partitioning=partition`` and
+``hybrid`` nodes.  Reports the node's compute/memory partitions (hybrid: the
+memory slices on them) and applies the gpupartitioner's plans with amd-smi.
 
 NODE_NAME=<node> python -m nos_amd.cmd.partagent --config partition_agent_config.yaml
 """
@@ -32,15 +32,18 @@ def open_lister(socket: str):
     return GrpcLister(socket)
 
 
-def build(api, node: str, cfg, smi, lister, device_plugins):
+def build(api, node: str, cfg, smi, lister, device_plugins, kind: str | None = None):
     from ..agents.devices import NodeLabeler
+    from ..agents.hybridagent import HybridReporter
     from ..agents.partagent import PartitionActuator, PartitionReporter
     from ..agents.shared import SharedState
+    from ..api import constants as C
 
     shared = SharedState()
     mgr = common.manager_for(api, f"nos-partagent-{node}", cfg)
     mgr.add(NodeLabeler(api, node, smi).controller())
-    mgr.add(PartitionReporter(api, node, smi, lister, shared, cfg.report_config_interval_seconds).controller())
+    reporter = HybridReporter if kind == C.PARTITIONING_HYBRID else PartitionReporter
+    mgr.add(reporter(api, node, smi, lister, shared, cfg.report_config_interval_seconds).controller())
     mgr.add(PartitionActuator(api, node, smi, lister, shared, device_plugins, cfg.default_memory_mode,
                               cfg.mode_switch_timeout_seconds).controller())
     return mgr
@@ -67,7 +70,9 @@ def main(argv=None) -> int:
         from ..agents.dpclient import DevicePluginClient
 
         dps.append(DevicePluginClient(api, node))
-    mgr = build(api, node, cfg, smi, lister, dps)
+    from ..gpu.core import partitioning_kind
+
+    mgr = build(api, node, cfg, smi, lister, dps, partitioning_kind(api.get("Node", node)))
     common.serve_health(cfg.health.health_probe_bind_address, mgr.healthz, mgr.readyz)
     common.serve_metrics(cfg.metrics.bind_address)
     mgr.start()

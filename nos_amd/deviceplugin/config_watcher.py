@@ -29,7 +29,7 @@ class ConfigWatcher:
 
     def reconcile(self, req: Request | None) -> Result:
         node = self.api.try_get("Node", self.node_name)
-        if node is None or self.plugin.mode != C.PARTITIONING_CUMASK:
+        if node is None or self.plugin.mode not in (C.PARTITIONING_CUMASK, C.PARTITIONING_HYBRID):
             return Result()
         key = ko.labels(node).get(C.LABEL_DEVICE_PLUGIN_CONFIG)
         if not key:

@@ -9,7 +9,10 @@ Replaces the NVIDIA device plugin + MPS daemon the reference depends on
 * ``amd.com/partition-<n>xcd.<gb>gb`` -- the logical GPUs of the current
   compute/memory partition mode (amdpart nodes), read from amd-smi;
 * ``amd.com/gpu-<gb>gb`` -- CU-mask slices (cumask nodes), replicas of each
-  GPU as listed by the gpupartitioner's plugin ConfigMap entry.
+  GPU as listed by the gpupartitioner's plugin ConfigMap entry; on hybrid
+  nodes the same memory slices placed on the GPU's logical partitions (first
+  fit decreasing over partition memory and HWS process slots, allocated
+  replicas never move; no CU mask inside a partition).
 
 ``allocate`` returns what a real ``ContainerAllocateResponse`` carries:
 ``HIP_VISIBLE_DEVICES`` (``device_env="container"``, the DaemonSet default:
@@ -44,6 +47,7 @@ import yaml
 from ..api import constants as C
 from ..gpu.amdpart import partition_profile
 from ..gpu.amdsmi import AmdSmi, GpuInfo
+from ..gpu.kfd import max_concurrent_processes
 from ..gpu.topology import MI355X_CUS_PER_XCD, MI355X_MEMORY_GB, MI355X_XCDS, CUSlotSet, layout_slots, logical_cu
 from ..ops.streams import mask_hex
 from ..partitioning import scoring
@@ -120,7 +124,7 @@ class NosAmdDevicePlugin:
                 return False
             log.info("node %s: partitioning mode %s -> %s", self.node_name, self.mode, mode)
             self.mode = mode
-            if mode != C.PARTITIONING_CUMASK:
+            if mode not in SLICE_MODES:
                 self.config, self.config_key = None, None
         self.refresh()
         return True
@@ -147,6 +151,8 @@ class NosAmdDevicePlugin:
                             did = f"{gi.uuid}::{prof}::{r}"
                             devs[did] = Device(did, C.AMD_SLICE_RESOURCE_PREFIX + prof, gi.index, profile=prof,
                                                memory_gb=int(s.get("memoryGB", prof[:-2])))
+            elif self.mode == C.PARTITIONING_HYBRID:
+                self._hybrid_devices(gpus, devs)
             elif self.mode == C.PARTITIONING_AMDPART:
                 # one device per logical partition amd-smi enumerates for the GPU, named
                 # from the GPU's reported memory / XCDs (same function as the planner)
@@ -183,12 +189,63 @@ class NosAmdDevicePlugin:
             except Exception:
                 log.exception("device plugin listener failed")
 
+    def _hybrid_devices(self, gpus: list[GpuInfo], devs: dict[str, "Device"]) -> None:
+        """Slice replicas of the table placed on each GPU's CURRENT logical
+        partitions: allocated replicas keep their partition, the others go
+        first-fit (largest first) where partition memory and the HWS process
+        slots allow; what does not fit (e.g. the table is laid out for CPX
+        while the agent has not switched the GPU yet) is advertised unhealthy
+        until a refresh after the switch."""
+        table = {g["index"]: g for g in (self.config or {}).get("gpus", [])}
+        per_part = max_concurrent_processes(self.smi)
+        for gi in gpus:
+            if getattr(gi, "switching", False):  # cannot be enumerated now: keep what it had
+                devs.update({k: d for k, d in self.devices.items() if d.gpu_index == gi.index})
+                continue
+            parts = self.smi.partitions(gi.index)
+            if not parts:
+                continue
+            entry = table.get(gi.index, {})
+            reps = [(f"{gi.uuid}::{s['profile']}::{r}", s["profile"], int(s.get("memoryGB", s["profile"][:-2])))
+                    for s in entry.get("slices", []) for r in range(int(s.get("replicas", 0)))]
+            # the table is laid out for entry["mode"]: until the partition agent has
+            # switched the GPU, only already-allocated replicas stay advertised --
+            # a pod bound to a slice of the OLD mode would block the switch forever
+            ready = entry.get("mode") in (None, "", f"{gi.compute_mode}/{gi.memory_mode}")
+            room = {p.partition: [p.memory_gb, per_part] for p in parts}
+            where: dict[str, int] = {}
+            for did, _, mem in reps:  # allocated replicas never move
+                old = self.devices.get(did)
+                if did in self.allocated and old is not None and old.partition in room:
+                    where[did] = old.partition
+                    room[old.partition][0] -= mem
+                    room[old.partition][1] -= 1
+            for did, _, mem in sorted(reps, key=lambda x: (-x[2], x[0])):
+                if did in where or not ready:
+                    continue
+                for p in parts:
+                    left = room[p.partition]
+                    if left[1] >= 1 and left[0] >= mem:
+                        where[did] = p.partition
+                        left[0] -= mem
+                        left[1] -= 1
+                        break
+            by_part = {p.partition: p for p in parts}
+            for did, prof, mem in reps:
+                pi = by_part.get(where.get(did, -1))
+                devs[did] = Device(did, C.AMD_SLICE_RESOURCE_PREFIX + prof, gi.index, healthy=pi is not None,
+                                   partition=pi.partition if pi else -1, profile=prof, memory_gb=mem,
+                                   hip_id=pi.hip_id if pi else -1, drm_render=pi.drm_render if pi else -1)
+
     def _layout_cu_slots(self) -> None:
         """XCD-symmetric CU slots for every slice replica (:func:`layout_slots`):
         allocated replicas keep theirs, the others get exactly their policy
         share of the free slots, and a replica that cannot get it is advertised
         unhealthy (never a smaller or overlapping mask)."""
         slots: dict[str, CUSlotSet] = {}
+        if self.mode != C.PARTITIONING_CUMASK:  # hybrid slices share their partition's CUs
+            self.cu_slots = slots
+            return
         by_gpu: dict[int, list[Device]] = {}
         for d in self.devices.values():
             if d.resource.startswith(C.AMD_SLICE_RESOURCE_PREFIX):
@@ -337,7 +394,7 @@ class NosAmdDevicePlugin:
             stale = [did for did in device_ids if did in self.devices and not self.devices[did].healthy]
             for did in stale:
                 self.devices.pop(did, None)
-        if released and self.mode == C.PARTITIONING_CUMASK:
+        if released and self.mode in SLICE_MODES:
             self.refresh()
 
     def sync_allocated(self, used_device_ids: set[str]) -> None:
@@ -356,6 +413,9 @@ class NosAmdDevicePlugin:
     def cus_of(self, device_id: str) -> list[int]:
         s = self.cu_slots.get(device_id)
         return s.cus() if s else []
+
+
+SLICE_MODES = (C.PARTITIONING_CUMASK, C.PARTITIONING_HYBRID)  # modes whose slice table comes from the ConfigMap
 
 
 def _cu_geometry(g: GpuInfo | None) -> tuple[int, int]:

@@ -140,6 +140,22 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None) -> dic
             "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or ("auto" if whole else "w4k32")}
 
 
+def slice_cu_budget(env: dict | None = None) -> int:
+    """CUs of the pod's CU-mask slice (popcount of ``ROC_GLOBAL_CU_MASK``), 0
+    for an unmasked pod.  ``NOS_AMD_CU_BUDGET`` overrides it (A/B runs: "0"
+    keeps one workgroup per tile on a masked slice)."""
+    env = os.environ if env is None else env
+    if env.get("NOS_AMD_CU_BUDGET") is not None:
+        return int(env["NOS_AMD_CU_BUDGET"])
+    m = env.get("ROC_GLOBAL_CU_MASK")
+    if not m:
+        return 0
+    try:
+        return bin(int(m, 16)).count("1")
+    except ValueError:
+        return 0
+
+
 class _CpuTenant:
     def __init__(self, model, x):
         self.model, self.x = model, x
@@ -170,12 +186,15 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             torch.cuda.set_device(0)  # the device plugin's HIP_VISIBLE_DEVICES leaves exactly the slice's GPU
             frac = apply_memory_limit(0)
             torch.backends.cuda.matmul.allow_tf32 = False  # true fp32 GEMMs (no reduced-precision shortcut)
-            from ..ops import set_attention_f32_variant, set_gemm_f32_policy, set_gemm_policy
+            from ..ops import set_attention_f32_variant, set_cu_budget, set_gemm_f32_policy, set_gemm_policy
 
             cfg = kernel_config(frac, os.environ)
             set_gemm_policy(cfg["gemm_bf16"])
             set_gemm_f32_policy(cfg["gemm_f32"])
             set_attention_f32_variant(cfg["attention_f32"])
+            budget = slice_cu_budget(os.environ)
+            if budget:  # CU-mask slice: slice-sized persistent grids (ops.set_cu_budget)
+                set_cu_budget(budget)
         m, x = _build(dtype, seed, demo_input_hw(), device)
         if gpu:
             s = torch.cuda.Stream()
@@ -193,6 +212,7 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
                 "device": props.name if gpu else "cpu",
                 "multiprocessor_count": props.multi_processor_count if gpu else 0,
                 "cu_mask": os.environ.get("ROC_GLOBAL_CU_MASK"),
+                "cu_budget": slice_cu_budget(os.environ) if gpu else 0,
                 "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES"),
                 "memory_limit_gb": os.environ.get("NOS_AMD_MEMORY_LIMIT_GB"),
                 "max_allocated_gb": None}

@@ -156,6 +156,20 @@ def set_gemm_persistent(wgs_per_cu: int) -> None:
     _lib.check(_lib.lib().nos_gemm_set_persistent(int(wgs_per_cu)), "nos_gemm_set_persistent")
 
 
+def set_cu_budget(cus: int) -> None:
+    """CUs this process may use (a CU-mask slice: the popcount of its
+    ``ROC_GLOBAL_CU_MASK``; 0 = no limit).  The fp32 GEMM / attention and the
+    bf16 GEMM then launch slice-sized persistent grids (resident workgroups x
+    budgeted CUs) instead of one workgroup per tile: every dispatch completes at
+    launch, so a pod never holds a command-processor pipe that another pod's
+    queue shares (profiles/r03_hol_*.json: 8 masked pods on 4 pipes per XCD)."""
+    _lib.check(_lib.lib().nos_set_cu_budget(int(cus)), "nos_set_cu_budget")
+
+
+def cu_budget() -> int:
+    return int(_lib.lib().nos_get_cu_budget())
+
+
 def set_gemm_f32_policy(policy: str) -> None:
     """fp32 GEMM tiles: ``"latency"`` (default; fewest rounds of tiles over
     the CUs) or ``"throughput"`` (most MFMA-efficient tile; other co-running
@@ -328,5 +342,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

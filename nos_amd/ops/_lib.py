@@ -56,6 +56,8 @@ _SIGS = {
     "nos_device_info": [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_ll), ctypes.POINTER(c_int),
                         ctypes.c_char_p, c_int],
     "nos_runtime_version": [ctypes.POINTER(c_int)],
+    "nos_set_cu_budget": [c_int],
+    "nos_get_cu_budget": [],
 }
 
 

@@ -16,6 +16,14 @@ handshake covers this path too (the gpuagent reports
 ``status-partitioning-plan``; the reference's MPS path had no handshake,
 SURVEY.md 3.2).
 
+``hybrid`` (the reference's declared-but-unused kind,
+``pkg/gpu/partitioning.go:87-91``): nodes labelled ``hybrid``; a plan picks a
+compute/memory mode per GPU AND memory slices (``amd.com/gpu-<N>gb``) that
+bin-pack into its partitions (:mod:`nos_amd.gpu.hybrid`).  It writes the
+cumask path's device-plugin ConfigMap entry (with each GPU's mode) plus the
+amdpart path's ``spec-mode-gpu-<i>`` annotations: the partition agent switches
+modes, the device plugin places the slices on the partitions.
+
 Each strategy provides the five pieces of the reference's factory: snapshot
 taker, partition calculator, partitioner, slice calculator, slice filter
 (+ the node initializer for amdpart).
@@ -30,7 +38,8 @@ import yaml
 from ..api import constants as C
 from ..gpu import amdpart as ap
 from ..gpu import cumask as cm
-from ..gpu.core import SpecAnnotation, is_amdpart_enabled, is_cumask_enabled
+from ..gpu import hybrid as hy
+from ..gpu.core import SpecAnnotation, is_amdpart_enabled, is_cumask_enabled, partitioning_kind
 from ..kube import objects as ko
 from ..scheduler.framework import NodeInfo
 from .core import ClusterSnapshot, new_plan_id
@@ -155,7 +164,10 @@ def plugin_config(node_name: str, plan_id: str, partitioning: NodePartitioning, 
     for g in sorted(partitioning.gpus, key=lambda x: x.gpu_index):
         slices = [{"profile": cm.profile_of_resource(r).name, "memoryGB": cm.profile_of_resource(r).memory_gb,
                    "replicas": n} for r, n in g.resources]
-        gpus.append({"index": g.gpu_index, "slices": slices})
+        entry = {"index": g.gpu_index, "slices": slices}
+        if g.mode:  # hybrid: the compute/memory mode the slices are laid out for
+            entry["mode"] = g.mode
+        gpus.append(entry)
     out = {"version": "v1", "node": node_name, "planId": plan_id, "cuPolicy": cu_policy, "allocation": allocation,
            "gpus": gpus}
     if gpu_weights:
@@ -198,10 +210,11 @@ class CuMaskPartitioner:
             self.clock.sleep(self.delay_s)  # ConfigMap propagation (kept for fidelity)
         specs = [SpecAnnotation(g.gpu_index, cm.profile_of_resource(r).name, n)
                  for g in partitioning.gpus for r, n in g.resources]
-        patch = _spec_patch(node, specs, plan_id)
+        modes = {C.ANNOTATION_SPEC_MODE_FORMAT.format(index=g.gpu_index): g.mode for g in partitioning.gpus if g.mode}
+        patch = _spec_patch(node, specs, plan_id, modes)
         patch["metadata"]["labels"] = {C.LABEL_DEVICE_PLUGIN_CONFIG: key}
         self.api.patch("Node", name, patch)
-        log.info("cumask plan %s applied to node %s", plan_id, name)
+        log.info("%s plan %s applied to node %s", "hybrid" if modes else "cumask", plan_id, name)
 
 
 class CuMaskSnapshotTaker:
@@ -222,6 +235,32 @@ class CuMaskSnapshotTaker:
             except Exception as e:
                 log.debug("skipping node %s: %s", name, e)
         return ClusterSnapshot(nodes, self.pc, cm.SliceCalculator(), cm.SliceFilter())
+
+
+# ====================================================================== hybrid
+class HybridPartitionCalculator:
+    def get_partitioning(self, node) -> NodePartitioning:
+        if not isinstance(node, hy.HybridNode):
+            return NodePartitioning([])
+        return NodePartitioning([GPUPartitioning.of(g.index, {p.resource_name(): n for p, n in g.geometry().items()},
+                                                    g.mode.id()) for g in node.gpus])
+
+
+class HybridSnapshotTaker:
+    def __init__(self, partition_calculator=None):
+        self.pc = partition_calculator or HybridPartitionCalculator()
+
+    def take_snapshot(self, cs: ClusterState) -> ClusterSnapshot:
+        nodes = {}
+        for name, ni in cs.get_nodes().items():
+            n = ni.node()
+            if n is None or partitioning_kind(n) != C.PARTITIONING_HYBRID:
+                continue
+            try:
+                nodes[name] = hy.HybridNode.from_node_info(ni.clone())
+            except Exception as e:  # node not yet labelled by its agent
+                log.debug("skipping node %s: %s", name, e)
+        return ClusterSnapshot(nodes, self.pc, hy.HybridSliceCalculator(), hy.HybridSliceFilter())
 
 
 @dataclass
@@ -249,3 +288,10 @@ def cumask_strategy(api, cm_ref: DevicePluginConfigRef | None = None, delay_s: f
     return Strategy(C.PARTITIONING_CUMASK, CuMaskSnapshotTaker(pc, placement), pc,
                     CuMaskPartitioner(api, cm_ref, delay_s, clock, cu_policy, placement), cm.SliceCalculator(),
                     cm.SliceFilter())
+
+
+def hybrid_strategy(api, cm_ref: DevicePluginConfigRef | None = None, delay_s: float = 5.0, clock=None) -> Strategy:
+    pc = HybridPartitionCalculator()
+    return Strategy(C.PARTITIONING_HYBRID, HybridSnapshotTaker(pc), pc,
+                    CuMaskPartitioner(api, cm_ref, delay_s, clock, "shared", "pack"), hy.HybridSliceCalculator(),
+                    hy.HybridSliceFilter())

@@ -21,6 +21,7 @@ from dataclasses import dataclass, field
 
 from ..agents.devices import NodeLabeler
 from ..agents.gpuagent import CuMaskReporter
+from ..agents.hybridagent import HybridReporter
 from ..agents.partagent import PartitionActuator, PartitionReporter
 from ..agents.shared import SharedState
 from ..api import constants as C
@@ -34,7 +35,7 @@ from ..gpu.fakesmi import FakeSmi
 from ..kube import factory as kf
 from ..kube import objects as ko
 from ..partitioning.state import ClusterState
-from ..partitioning.strategies import DevicePluginConfigRef, amdpart_strategy, cumask_strategy
+from ..partitioning.strategies import DevicePluginConfigRef, amdpart_strategy, cumask_strategy, hybrid_strategy
 from ..runtime.manager import Manager
 from ..scheduler.config import build_framework, nos_scheduler_config
 from ..scheduler.scheduler import Scheduler
@@ -83,10 +84,11 @@ class SimCluster:
         amd = amdpart_strategy(self.api, self.clock, self.cfg.reserve_whole_gpus, self.cfg.preferred_memory_mode)
         cum = cumask_strategy(self.api, self.cm_ref, self.cfg.device_plugin_delay_seconds, self.clock,
                               self.cfg.cu_policy, self.cfg.slice_placement)
+        hyb = hybrid_strategy(self.api, self.cm_ref, self.cfg.device_plugin_delay_seconds, self.clock)
         self.partitioner.add(NodeController(self.api, self.cluster_state, amd.initializer).controller())
         self.partitioner.add(PodController(self.api, self.cluster_state).controller())
         self.partitioner_controllers = {}
-        for strat in (amd, cum):
+        for strat in (amd, cum, hyb):
             pc = PartitionerController(self.api, self.cluster_state, strat, fw, self.clock,
                                        self.cfg.batch_window_timeout_seconds, self.cfg.batch_window_idle_seconds,
                                        self.cfg.plan_report_timeout_seconds)
@@ -122,6 +124,13 @@ class SimCluster:
             agents["actuator"] = PartitionActuator(self.api, name, smi, kubelet, shared, [plugin])
             mgr.add(agents["reporter"].controller())
             mgr.add(agents["actuator"].controller())
+        elif kind == C.PARTITIONING_HYBRID:  # partition agent (modes) + slice reporter + slice table watcher
+            shared = SharedState()
+            agents["config"] = ConfigWatcher(self.api, name, plugin, self.cm_ref)
+            agents["reporter"] = HybridReporter(self.api, name, smi, kubelet, shared)
+            agents["actuator"] = PartitionActuator(self.api, name, smi, kubelet, shared, [plugin])
+            for a in ("config", "reporter", "actuator"):
+                mgr.add(agents[a].controller())
         elif kind == C.PARTITIONING_CUMASK:
             agents["config"] = ConfigWatcher(self.api, name, plugin, self.cm_ref)
             agents["reporter"] = CuMaskReporter(self.api, name, smi, kubelet, probe=probe)

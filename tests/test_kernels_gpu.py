@@ -310,3 +310,44 @@ def test_probes_report_sane_numbers():
     assert len(summary["xccs"]) == 8
     assert probes.hbm_gbps(stream) > 1000
     assert probes.mfma_peak_tflops(stream, 1024) > 500
+
+
+@pytest.mark.parametrize("budget", [8, 32, 40])
+def test_slice_sized_persistent_grids_are_bit_identical(budget):
+    """With a CU budget (a CU-mask slice's popcount, ops.set_cu_budget) the fp32
+    GEMMs, the fp32 attention and the bf16 GEMM launch at most occupancy x
+    budget workgroups that each walk a chunk of tiles (nos::xcd_chunk): the
+    output must equal the one-workgroup-per-tile launch bit for bit (the tile
+    math is the same; only the tile -> workgroup mapping changes)."""
+    torch.manual_seed(budget)
+    x = torch.randn(3401, 384, device=DEV)
+    w = torch.randn(1152, 384, device=DEV) * 0.05
+    b = torch.randn(1152, device=DEV)
+    r = torch.randn(3401, 1152, device=DEV)
+    wg, c1, c2 = ops.fold_layernorm(w, b, torch.randn(384, device=DEV), torch.randn(384, device=DEV))
+    qkv = torch.randn(1, 3401, 3 * 6 * 64, device=DEV)
+    xb, wb, rb = x.bfloat16(), w.bfloat16(), r.bfloat16()
+
+    def run():
+        outs = []
+        for pol in ("small", "latency"):
+            ops.set_gemm_f32_policy(pol)
+            outs += [ops.linear(x, w, b, act="gelu", residual=r), ops.linear_ln(x, wg, c1, c2, act="gelu")]
+        ops.set_gemm_f32_policy("latency")
+        for var in ("w4k32", "w4k64g2", "w4k32o4"):
+            ops.set_attention_f32_variant(var)
+            outs.append(ops.attention_qkv(qkv, 6))
+        ops.set_attention_f32_variant("auto")
+        outs.append(ops.linear(xb, wb, None, residual=rb))
+        torch.cuda.synchronize()
+        return outs
+
+    assert ops.cu_budget() == 0
+    ref = run()
+    ops.set_cu_budget(budget)
+    try:
+        got = run()
+    finally:
+        ops.set_cu_budget(0)
+    for a, c in zip(ref, got):
+        assert torch.equal(a, c)

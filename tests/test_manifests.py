@@ -101,10 +101,17 @@ def test_every_referenced_secret_certificate_and_service_is_rendered():
 
 def test_daemonsets_are_privileged_and_node_selected():
     dss = [o for o in _objs() if o["kind"] == "DaemonSet"]
-    assert len(dss) == 4
+    assert len(dss) == 5  # partagent, gpuagent, device plugin x (cumask, partition, hybrid)
     for ds in dss:
         spec = ds["spec"]["template"]["spec"]
-        assert spec["nodeSelector"]["nos.nebuly.com/gpu-partitioning"] in ("partition", "cumask")
+        if "nodeSelector" in spec:
+            kinds = [spec["nodeSelector"]["nos.nebuly.com/gpu-partitioning"]]
+        else:  # the partition agent serves partition AND hybrid nodes
+            (expr,) = spec["affinity"]["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][
+                "nodeSelectorTerms"][0]["matchExpressions"]
+            assert expr["key"] == "nos.nebuly.com/gpu-partitioning" and expr["operator"] == "In"
+            kinds = expr["values"]
+        assert set(kinds) <= {"partition", "cumask", "hybrid"}
         c = spec["containers"][0]
         assert c["securityContext"]["privileged"] is True
         assert any(m["mountPath"] == "/var/lib/kubelet/pod-resources" for m in c["volumeMounts"])

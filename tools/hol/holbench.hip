@@ -19,6 +19,7 @@
 //   its queue for P phases of work.  The barrier gives up after 250 ms (flag
 //   in the output) so a non-resident grid can never hang the GPU.
 //   Prints one JSON line.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -38,12 +39,33 @@
     }                                                                          \
   } while (0)
 
-__global__ __launch_bounds__(256) void spin_kernel(unsigned long long ticks, int* sink) {
-  extern __shared__ int lds[];
+// the work of one workgroup: spin on the realtime counter (iters == 0) or a
+// fixed VALU chain (iters > 0: 8 independent FMA chains per lane, no memory
+// traffic) -- the ALU form does not poll a shared counter, so thousands of
+// co-running waves cannot slow each other down through it
+__device__ __forceinline__ int work(unsigned long long ticks, int iters) {
+  if (iters > 0) {
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = (float)(threadIdx.x + j);
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = fmaf(x[j], 0.999f, 0.5f);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += x[j];
+    return (int)s;
+  }
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   unsigned long long t = t0;
   while (t - t0 < ticks) t = __builtin_amdgcn_s_memrealtime();
-  lds[threadIdx.x] = (int)t;
+  return (int)t;
+}
+
+__global__ __launch_bounds__(256) void spin_kernel(unsigned long long ticks, int iters, int* sink) {
+  extern __shared__ int lds[];
+  lds[threadIdx.x] = work(ticks, iters);
   __syncthreads();
   if (lds[(threadIdx.x + 1) & 255] == 0x7fffffff) sink[blockIdx.x] = 1;  // keep LDS live, never taken
 }
@@ -78,14 +100,11 @@ __device__ __forceinline__ bool grid_barrier(unsigned* count, unsigned* gen, uns
   return ok != 0;
 }
 
-__global__ __launch_bounds__(256) void phases_kernel(unsigned long long ticks, int phases, unsigned* bar,
-                                                     int* abort_flag, int* sink) {
+__global__ __launch_bounds__(256) void phases_kernel(unsigned long long ticks, int iters, int phases,
+                                                     unsigned* bar, int* abort_flag, int* sink) {
   extern __shared__ int lds[];
   for (int p = 0; p < phases; ++p) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long t = t0;
-    while (t - t0 < ticks) t = __builtin_amdgcn_s_memrealtime();
-    lds[threadIdx.x] = (int)t;
+    lds[threadIdx.x] = work(ticks, iters);
     if (!grid_barrier(bar, bar + 1, gridDim.x, abort_flag, 25000000ull)) return;  // 250 ms
   }
   if (lds[(threadIdx.x + 1) & 255] == 0x7fffffff) sink[blockIdx.x] = 1;
@@ -113,7 +132,7 @@ static int popcount_hex_mask(const char* s) {
 int main(int argc, char** argv) {
   double seconds = 3.0, spin_us = 50.0;
   long long start_ns = 0;
-  int grid = 0, lds = 40960, depth = 16, null_stream = 0, phases = 0;
+  int grid = 0, lds = 40960, depth = 16, null_stream = 0, phases = 0, iters = 0, streams = 1, per_xcd = 4;
   const char* tag = "";
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string k = argv[i];
@@ -126,13 +145,17 @@ int main(int argc, char** argv) {
     else if (k == "--depth") depth = atoi(v);
     else if (k == "--null-stream") null_stream = atoi(v);
     else if (k == "--phases") phases = atoi(v);
+    else if (k == "--iters") iters = atoi(v);
+    else if (k == "--streams") streams = atoi(v);
+    else if (k == "--per-xcd") per_xcd = atoi(v);
     else if (k == "--tag") tag = v;
     else {
       fprintf(stderr, "unknown option %s\n", k.c_str());
       return 2;
     }
   }
-  if (lds < 1024 || lds > 65536 || depth < 1 || depth > 1024 || seconds <= 0 || seconds > 60) {
+  if (lds < 1024 || lds > 65536 || depth < 1 || depth > 1024 || seconds <= 0 || seconds > 60 || streams < 1 ||
+      streams > 16 || per_xcd < 1 || streams * per_xcd > 32) {
     fprintf(stderr, "bad arguments\n");
     return 2;
   }
@@ -159,15 +182,52 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&abort_flag, sizeof(int)));
   CK(hipMemset(bar, 0, 2 * sizeof(unsigned)));
   CK(hipMemset(abort_flag, 0, sizeof(int)));
+  if (streams > 1) {
+    // one process, `streams` streams each with its own XCD-symmetric CU mask
+    // (hipExtStreamCreateWithCUMask: per-queue masks, the in-process analogue of
+    // one pod per slice); kernels round-robin over the streams
+    const int fit1 = 8 * per_xcd * wg_per_cu;
+    std::vector<hipStream_t> ss(streams);
+    for (int k = 0; k < streams; ++k) {
+      uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int x = 0; x < 8; ++x)
+        for (int j = k * per_xcd; j < (k + 1) * per_xcd; ++j) {
+          const int bit = j * 8 + x;
+          m[bit / 32] |= 1u << (bit % 32);
+        }
+      CK(hipExtStreamCreateWithCUMask(&ss[k], 8, m));
+    }
+    const unsigned long long tk = (unsigned long long)(spin_us * 100.0);
+    for (int k = 0; k < streams; ++k)
+      hipLaunchKernelGGL(spin_kernel, dim3(fit1), dim3(256), lds, ss[k], tk, iters, sink);
+    CK(hipDeviceSynchronize());
+    while (start_ns && mono_ns() < start_ns) usleep(200);
+    const long long t0 = mono_ns(), t_end = t0 + (long long)(seconds * 1e9);
+    long long rounds = 0;
+    while (mono_ns() < t_end) {
+      for (int d = 0; d < depth; ++d)
+        for (int k = 0; k < streams; ++k)
+          hipLaunchKernelGGL(spin_kernel, dim3(fit1), dim3(256), lds, ss[k], tk, iters, sink);
+      CK(hipDeviceSynchronize());
+      rounds += depth;
+    }
+    const double el = (mono_ns() - t0) / 1e9;
+    printf("{\"tag\": \"%s\", \"streams\": %d, \"per_xcd\": %d, \"fit\": %d, \"iters\": %d, \"kernels_per_stream\": %lld, "
+           "\"elapsed_s\": %.4f, \"kernel_ms\": %.4f}\n", tag, streams, per_xcd, fit1, iters, rounds, el,
+           el * 1e3 / (double)rounds);
+    for (auto x : ss) CK(hipStreamDestroy(x));
+    return 0;
+  }
   hipStream_t st = nullptr;
   if (!null_stream) CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   // realtime counter: 100 MHz on MI300-class parts
   const unsigned long long ticks = (unsigned long long)(spin_us * 100.0);
   auto launch = [&]() {
     if (phases > 0)  // the barrier's own LDS word: keep the per-CU total at (160 KB / lds) workgroups
-      hipLaunchKernelGGL(phases_kernel, dim3(g), dim3(256), lds - 1024, st, ticks, phases, bar, abort_flag, sink);
+      hipLaunchKernelGGL(phases_kernel, dim3(g), dim3(256), lds - 1024, st, ticks, iters, phases, bar, abort_flag,
+                         sink);
     else
-      hipLaunchKernelGGL(spin_kernel, dim3(g), dim3(256), lds, st, ticks, sink);
+      hipLaunchKernelGGL(spin_kernel, dim3(g), dim3(256), lds, st, ticks, iters, sink);
   };
   launch();  // warm-up
   CK(hipGetLastError());
@@ -195,9 +255,9 @@ int main(int argc, char** argv) {
   printf("{\"tag\": \"%s\", \"pid\": %d, \"cus\": %d, \"mask\": \"%s\", \"wg_per_cu\": %d, \"fit\": %d, \"grid\": %d, "
          "\"spin_us\": %.1f, \"depth\": %d, \"null_stream\": %d, \"kernels\": %lld, \"elapsed_s\": %.4f, "
          "\"kernel_ms\": %.4f, \"ideal_kernel_ms\": %.4f, \"slot_efficiency\": %.4f, \"batch_ms_min\": %.3f, "
-         "\"batch_ms_max\": %.3f, \"t0_ns\": %lld, \"phases\": %d, \"barrier_aborted\": %d}\n",
+         "\"batch_ms_max\": %.3f, \"t0_ns\": %lld, \"phases\": %d, \"barrier_aborted\": %d, \"iters\": %d}\n",
          tag, (int)getpid(), cus, mask ? mask : "", wg_per_cu, fit, g, spin_us, depth, null_stream, kernels, el,
-         el * 1e3 / (double)kernels, ideal_kernel_ms, eff, mn, mx, t0, phases, aborted);
+         el * 1e3 / (double)kernels, ideal_kernel_ms, eff, mn, mx, t0, phases, aborted, iters);
   fflush(stdout);
   CK(hipFree(sink));
   CK(hipFree(bar));

@@ -31,7 +31,7 @@ def build(force: bool = False) -> Path:
     return BIN
 
 
-def masks(n: int, per_xcd: int, mode: str) -> list[str | None]:
+def masks(n: int, per_xcd: int, mode: str, starts: list[int] | None = None) -> list[str | None]:
     from nos_amd.gpu.topology import MI355X_CUS, logical_cu
     from nos_amd.ops.streams import mask_hex
 
@@ -39,16 +39,18 @@ def masks(n: int, per_xcd: int, mode: str) -> list[str | None]:
         return [None] * n
     out = []
     for k in range(n):
-        slots = range(k * per_xcd, (k + 1) * per_xcd)
+        s0 = starts[k] if starts else k * per_xcd
+        slots = range(s0, s0 + per_xcd)
         out.append(mask_hex([logical_cu(x, j) for x in range(8) for j in slots], MI355X_CUS))
     return out
 
 
 def run_row(n: int, grid: int, hwq: int, mode: str, per_xcd: int, seconds: float, spin_us: float, lds: int,
-            depth: int, null_stream: int, timeout: float, phases: int = 0) -> dict:
+            depth: int, null_stream: int, timeout: float, phases: int = 0, iters: int = 0,
+            starts: list[int] | None = None) -> dict:
     start = time.monotonic_ns() + int(4e9)
     procs = []
-    for k, m in enumerate(masks(n, per_xcd, mode)):
+    for k, m in enumerate(masks(n, per_xcd, mode, starts)):
         env = dict(os.environ)
         env.pop("ROC_GLOBAL_CU_MASK", None)
         if m:
@@ -57,7 +59,7 @@ def run_row(n: int, grid: int, hwq: int, mode: str, per_xcd: int, seconds: float
             env["GPU_MAX_HW_QUEUES"] = str(hwq)
         cmd = [str(BIN), "--seconds", str(seconds), "--start-ns", str(start), "--grid", str(grid),
                "--spin-us", str(spin_us), "--lds", str(lds), "--depth", str(depth), "--null-stream", str(null_stream),
-               "--phases", str(phases), "--tag", f"{mode}-n{n}-g{grid}-q{hwq}-d{depth}-ph{phases}-p{k}"]
+               "--phases", str(phases), "--iters", str(iters), "--tag", f"{mode}-n{n}-g{grid}-q{hwq}-d{depth}-ph{phases}-p{k}"]
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     pods = []
     for p in procs:
@@ -71,10 +73,12 @@ def run_row(n: int, grid: int, hwq: int, mode: str, per_xcd: int, seconds: float
             continue
         pods.append(json.loads(out.strip().splitlines()[-1]))
     effs = [q.get("slot_efficiency", 0.0) for q in pods]
+    kms = [q.get("kernel_ms", 0.0) for q in pods]
     return {"pods": n, "grid": grid, "hw_queues": hwq, "mask": mode, "per_xcd": per_xcd, "null_stream": null_stream,
             "depth": depth, "phases": phases, "aborted": sum(q.get("barrier_aborted", 0) for q in pods),
             "eff_min": round(min(effs), 3), "eff_max": round(max(effs), 3),
-            "eff_mean": round(sum(effs) / len(effs), 3), "per_pod": pods}
+            "eff_mean": round(sum(effs) / len(effs), 3), "iters": iters, "slot_starts": starts,
+            "kernel_ms_min": round(min(kms), 4), "kernel_ms_max": round(max(kms), 4), "per_pod": pods}
 
 
 def main() -> None:
@@ -90,6 +94,10 @@ def main() -> None:
     ap.add_argument("--depth", default="16", help="comma list: kernels queued per host synchronize")
     ap.add_argument("--phases", default="0", help="comma list: 0 = one spin per launch, P = megakernel of P phases")
     ap.add_argument("--null-stream", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=0, help="> 0: VALU work per workgroup instead of the realtime spin "
+                    "(compare kernel_ms with the 1-pod row)")
+    ap.add_argument("--slot-starts", default="", help="';'-separated lists of per-pod first slots, e.g. '0,16;0,4' "
+                    "(overrides --pods: one row per list)")
     ap.add_argument("--out", default="gpurun_out/hol.json")
     a = ap.parse_args()
     build()
@@ -99,9 +107,12 @@ def main() -> None:
             for grid in map(int, a.grids.split(",")):
               for depth in map(int, a.depth.split(",")):
                for phases in map(int, a.phases.split(",")):
-                for n in map(int, a.pods.split(",")):
+                layouts = ([[int(x) for x in lst.split(",")] for lst in a.slot_starts.split(";")] if a.slot_starts
+                           else [None] * len(a.pods.split(",")))
+                for n, starts in zip([len(x) for x in layouts] if a.slot_starts else map(int, a.pods.split(",")),
+                                     layouts):
                     r = run_row(n, grid, hwq, mode, a.per_xcd, a.seconds, a.spin_us, a.lds, depth, a.null_stream,
-                                timeout=a.seconds + 60, phases=phases)
+                                timeout=a.seconds + 60, phases=phases, iters=a.iters, starts=starts)
                     print(json.dumps({k: v for k, v in r.items() if k != "per_pod"}), flush=True)
                     rows.append(r)
                     Path(a.out).parent.mkdir(parents=True, exist_ok=True)
