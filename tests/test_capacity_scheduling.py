@@ -237,3 +237,71 @@ def test_pod_add_delete_idempotent():
     e.delete_pod_if_present(p)
     e.delete_pod_if_present(p)
     assert e.used.memory == 0
+
+
+# ---------------------------------------------------------------- PDB-aware preemption
+def _pdb(ns, name, app, allowed):
+    return {"kind": "PodDisruptionBudget", "metadata": {"name": name, "namespace": ns},
+            "spec": {"selector": {"matchLabels": {"app": app}}}, "status": {"disruptionsAllowed": allowed}}
+
+
+def _labelled(pod, app):
+    pod["metadata"]["labels"]["app"] = app
+    return pod
+
+
+def _dry_run_pdb(pod, pods, nodes, eqs, pdbs):
+    fit = NodeResourcesFit()
+    fw = Framework({"queue_sort": [PrioritySort()], "pre_filter": [fit], "filter": [fit],
+                    "bind": [DefaultBinder()]}, snapshot=Snapshot.from_objects(pods, nodes), nominator=PodNominator())
+    state = CycleState()
+    fw.run_pre_filter_plugins(state, pod)
+    req = Resource.from_list(ResourceCalculator(GPU_MEM).compute_pod_request(pod))
+    state.write(PRE_FILTER_STATE_KEY, PreFilterState(req, req.clone(), req.clone()))
+    state.write(ELASTIC_QUOTA_SNAPSHOT_KEY, ElasticQuotaSnapshotState(ElasticQuotaInfos(eqs)))
+    ev = Evaluator("CapacityScheduling", fw, state, CapacityPreemptor(fw, state))
+    infos = fw.snapshot_shared_lister().list()
+    cands, _ = ev.dry_run_preemption(pod, infos, pdbs, 0, len(infos))
+    return {c.name: (sorted(ko.name(v) for v in c.victims), c.num_pdb_violations) for c in cands}
+
+
+EQS_PDB = {"ns1": eqi("ns1", R(mem=100), R(mem=300), R(mem=50)),
+           "ns2": eqi("ns2", R(mem=50), R(mem=300), R(mem=100)),
+           "ns3": eqi("ns3", R(mem=300), None, R())}  # idle lender: the sum of mins leaves room
+
+
+def test_pdb_violating_victim_is_reprieved_first():
+    """Two over-quota victims of ns2 on node-a, one of them covered by a PDB
+    that allows no disruption.  Reprieve tries PDB-violating victims first
+    (capacity_scheduling.go:634-673, filterPodsWithPDBViolation :850-895): the
+    protected pod is kept although it is the less important one, the other is
+    evicted, and no violation is counted."""
+    pods = [make_pod("p1", "ns1", 50, 0, 0, MID, "p1", "node-a", False),
+            _labelled(make_pod("p3", "ns2", 50, 0, 0, MID, "p3", "node-a", True), "guarded"),
+            _labelled(make_pod("p4", "ns2", 50, 0, 0, MID + 50, "p4", "node-a", True), "free")]
+    pre = make_pod("pre", "ns1", 50, 0, 0, HIGH, "", "", False)
+    node = [_node("node-a", memory="150")]
+    # without a PDB the more important p4 is reprieved and p3 goes
+    assert _dry_run_pdb(pre, pods, node, EQS_PDB, []) == {"node-a": (["p3"], 0)}
+    got = _dry_run_pdb(pre, pods, node, EQS_PDB, [_pdb("ns2", "guard", "guarded", 0)])
+    assert got == {"node-a": (["p4"], 0)}
+    # a PDB that still allows one disruption does not protect it
+    assert _dry_run_pdb(pre, pods, node, EQS_PDB, [_pdb("ns2", "guard", "guarded", 1)]) == {"node-a": (["p3"], 0)}
+
+
+def test_pdb_violations_are_counted_and_steer_node_choice():
+    """When the protected pod must go anyway it is counted as a violation; the
+    evaluator then prefers the node whose victims violate no PDB
+    (pickOneNodeForPreemption: fewest violations first)."""
+    from nos_amd.scheduler.preemption import Candidate, pick_one_node_for_preemption
+
+    pods = [_labelled(make_pod("p3", "ns2", 50, 0, 0, MID, "p3", "node-a", True), "guarded"),
+            _labelled(make_pod("p4", "ns2", 50, 0, 0, MID, "p4", "node-a", True), "free"),
+            _labelled(make_pod("q1", "ns2", 50, 0, 0, MID, "q1", "node-b", True), "free"),
+            _labelled(make_pod("q2", "ns2", 50, 0, 0, MID, "q2", "node-b", True), "free")]
+    pre = make_pod("pre", "ns1", 100, 0, 0, HIGH, "", "", False)
+    nodes = [_node("node-a", memory="100"), _node("node-b", memory="100")]
+    got = _dry_run_pdb(pre, pods, nodes, EQS_PDB, [_pdb("ns2", "guard", "guarded", 0)])
+    assert got == {"node-a": (["p3", "p4"], 1), "node-b": (["q1", "q2"], 0)}
+    cands = {n: Candidate(n, [p for p in pods if ko.name(p) in v], k) for n, (v, k) in got.items()}
+    assert pick_one_node_for_preemption(cands) == "node-b"

@@ -138,3 +138,28 @@ def test_overlapped_bucketer_accumulation_contract():
     assert launched >= len(b.buckets)
     for g, p in zip(got, model.parameters()):
         assert torch.allclose(g, p.grad, atol=1e-6)
+
+
+def test_allreduce_sweep_tool_launches_under_torchrun(tmp_path):
+    """tools/allreduce_sweep.py through the same launcher the GPU sweep uses
+    (torch.distributed.run, 2 ranks, 127.0.0.1), gloo on the CPU: one row per
+    message size with NCCL-tests busbw, slowest rank's time."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parent.parent
+    out = tmp_path / "sweep.json"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+                        str(repo / "tools" / "allreduce_sweep.py"), "--device", "cpu", "--min-bytes", str(1 << 16),
+                        "--max-bytes", str(1 << 18), "--iters", "3", "--warmup", "1", "--out", str(out)],
+                       capture_output=True, text=True, timeout=180, cwd=str(repo),
+                       env={**__import__("os").environ, "OMP_NUM_THREADS": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(out.read_text())
+    assert d["world_size"] == 2 and d["backend"] == "gloo"
+    assert [x["bytes"] for x in d["rows"]] == [1 << 16, 1 << 17, 1 << 18]
+    for x in d["rows"]:
+        assert x["seconds"] > 0 and abs(x["busbw_gbps"] - x["algbw_gbps"] * 2 * 1 / 2) < 1e-9
