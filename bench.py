@@ -42,9 +42,11 @@ Also in the JSON: one whole-GPU pod's rate (``--ref-pod-s``), a bf16 fleet on
 the gfx950 kernels (``--extra-bf16-s``), the reference demo's latency table
 (1/3/5/7 pods, shared and CU-mask slices; default on single-GPU runs,
 ``--table``), and with WORLD_SIZE > 1 a data-parallel trainer pod per GPU
-(slot 0, run by the rank: bf16 MLP forward + backward with bucketed RCCL
-all-reduces over xGMI launched from the gradient hooks, in lockstep across
-ranks), so slices are measured under collective traffic.
+(slot 0: its own pod process with its device-plugin env, CU mask included,
+nos_amd/models/trainer_pod.py -- bf16 MLP forward + backward with bucketed
+RCCL all-reduces over xGMI launched from the gradient hooks, the trainer pods
+of all GPUs one job in lockstep), so slices are measured under collective
+traffic.
 """
 from __future__ import annotations
 
@@ -229,14 +231,9 @@ class UtilSampler:
             self._t.join(timeout=2)
 
 
-def fleet_window(d: Dist, fleet, warmup: int, steps: int, step_s: float, sampler: UtilSampler | None,
-                 coll=None, coll_times: list | None = None):
-    """Warm-up then timed steps of ``step_s`` wall seconds with every pod running.
-    With a trainer pod in this rank, the rank runs it (lockstep across ranks)
-    instead of sleeping; its iteration completion times go to ``coll_times``."""
+def fleet_window(d: Dist, fleet, warmup: int, steps: int, step_s: float, sampler: UtilSampler | None):
+    """Warm-up then timed steps of ``step_s`` wall seconds with every pod running."""
     t_end = time.monotonic() + warmup * step_s
-    if coll:
-        coll.run_until(t_end)
     last_log = time.monotonic()
     while time.monotonic() < t_end:
         time.sleep(0.05)
@@ -249,8 +246,6 @@ def fleet_window(d: Dist, fleet, warmup: int, steps: int, step_s: float, sampler
     t0 = time.monotonic()
     for k in range(steps):
         deadline = t0 + (k + 1) * step_s
-        if coll:
-            coll.run_until(deadline, coll_times)
         while True:
             now = time.monotonic()
             if now >= deadline:
@@ -268,12 +263,49 @@ def fleet_window(d: Dist, fleet, warmup: int, steps: int, step_s: float, sampler
     return t0, t1, util
 
 
-def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, step_s, sampler, coll=None,
-              device="cuda"):
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def with_trainer(d: Dist, envs: list[dict], args) -> list[dict]:
+    """Pod slot 0 of every GPU becomes the DP trainer pod: the same device-plugin
+    env plus the job's rendezvous (rank 0 picks a fresh port, every rank learns
+    it through the bench's own group).  Collective call: all ranks, same order."""
+    port = int(d.reduce([float(_free_port()) if d.rank == 0 else 0.0], "max")[0])
+    t = {**envs[0], "NOS_AMD_POD_KIND": "trainer", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+         "RANK": str(d.rank), "WORLD_SIZE": str(d.world), "LOCAL_RANK": "0",
+         "NOS_AMD_COLL_DIM": str(args.coll_dim), "NOS_AMD_COLL_BUCKET_MB": str(args.coll_bucket_mb)}
+    if not d.cuda or os.environ.get("NOS_AMD_BENCH_FOLD_GPUS") == "1":
+        t["NOS_AMD_TRAINER_BACKEND"] = "gloo"  # several ranks' trainers on one GPU: RCCL refuses that
+    return [t] + list(envs[1:])
+
+
+def trainer_stats(w) -> dict | None:
+    """This rank's trainer pod over the window: iterations, GEMM TFLOP/s,
+    gradient bytes all-reduced per second, and its one-bucket busbw probe."""
+    tps = w.trainer_pods
+    if not tps:
+        return None
+    p = tps[0]
+    i = p.info
+    n_it = p.completed
+    return {"iterations": round(n_it, 2), "running": p.running, "max_gap_s": round(p.max_gap_s, 3),
+            "gemm_tflops": round(n_it * (i.get("flops_per_step") or 0) / w.window_s / 1e12, 2),
+            "buckets": i.get("buckets"), "buckets_launched_in_backward": i.get("launched_in_backward"),
+            "allreduce_gb_per_s": round(n_it * (i.get("bucket_bytes") or 0) / w.window_s / 1e9, 2)
+            if (i.get("world_size") or 1) > 1 else 0.0,
+            "bucket_busbw_gbps": i.get("bucket_busbw_gbps"), "backend": i.get("backend"),
+            "cu_mask": i.get("cu_mask"), "pid": i.get("pid")}
+
+
+def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, step_s, sampler, device="cuda"):
     from nos_amd.podbench import PodFleet
 
     fleet = PodFleet(envs, dtype=dtype, graphs=graphs, extra_env=extra_env, launcher=launcher, device=device)
-    coll_times: list[float] = []
     try:
         err = None
         try:
@@ -288,23 +320,13 @@ def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, 
         if failed:
             raise RuntimeError(f"pods of another rank failed to start ({dtype})")
         d.barrier_sync()
-        t0, t1, (util, n_util) = fleet_window(d, fleet, warmup, steps, step_s, sampler, coll, coll_times)
+        t0, t1, (util, n_util) = fleet_window(d, fleet, warmup, steps, step_s, sampler)
         fleet.stop()
         w = fleet.window(t0, t1)
         w.sclk_mhz = getattr(fleet, "sclk_mhz", None)
     finally:
         fleet.close()
-    tr = None
-    if coll:
-        inside = [t0] + [t for t in coll_times if t0 < t < t1] + [t1]
-        gap = max(b - a for a, b in zip(inside, inside[1:]))
-        n_it = len(inside) - 2
-        tr = {"iterations": n_it, "running": n_it > 0 and gap < 0.25 * (t1 - t0), "max_gap_s": round(gap, 3),
-              "gemm_tflops": round(n_it * coll.flops_per_step() / (t1 - t0) / 1e12, 2),
-              "buckets": len(coll.bucketer.buckets),
-              "buckets_launched_in_backward": coll.bucketer.launched_in_backward,
-              "allreduce_gb_per_s": round(n_it * coll.bucket_bytes() / (t1 - t0) / 1e9, 2) if coll._dist() else 0.0}
-    return w, util, n_util, ready_s, tr
+    return w, util, n_util, ready_s, trainer_stats(w)
 
 
 def _hws_limit() -> int:
@@ -348,21 +370,10 @@ def main(argv=None) -> int:
 
     d.init_gpu()
     sampler = UtilSampler(d.device) if d.cuda else None
-    coll = None
     use_coll = args.collective == "on" or (args.collective == "auto" and world > 1)
+    # pod slot 0 of every GPU is the DP trainer pod (its own process; a fresh job per fleet)
+    fleet_envs = (lambda e: with_trainer(d, e, args)) if use_coll else (lambda e: e)
     pod_envs = envs
-    if use_coll:  # pod slot 0 of every GPU is the DP trainer, run by this rank (it owns the RCCL group)
-        from nos_amd.models.tenants import CollectiveTenant
-
-        trainer_env, pod_envs = envs[0], envs[1:]
-        if d.cuda and trainer_env.get("NOS_AMD_MEMORY_LIMIT_GB"):
-            import torch
-
-            torch.cuda.set_per_process_memory_fraction(
-                min(1.0, float(trainer_env["NOS_AMD_MEMORY_LIMIT_GB"]) * 2 ** 30 /
-                    torch.cuda.get_device_properties(d.device).total_memory), d.device)
-        coll = CollectiveTenant(dim=args.coll_dim if d.cuda else 128, bucket_mb=args.coll_bucket_mb if d.cuda else 1,
-                                device=d.device if d.cuda else "cpu")
 
     ref = None
     if args.ref_pod_s > 0:  # one pod owning the whole GPU (no slice env but the device)
@@ -371,12 +382,13 @@ def main(argv=None) -> int:
                                     args.ref_pod_s, sampler, device=args.device)
         ref = {"inf_per_s": round(w1.throughput, 3), "latency_s": w1.mean_latency_s, "gpu_util_pct": u1}
 
-    w, util, n_util, ready_s, tr = run_fleet(d, launcher, pod_envs, args.dtype, not args.no_graphs, fleet_env,
-                                             args.warmup, args.steps, args.step_s, sampler, coll, device=args.device)
+    w, util, n_util, ready_s, tr = run_fleet(d, launcher, fleet_envs(pod_envs), args.dtype, not args.no_graphs,
+                                             fleet_env, args.warmup, args.steps, args.step_s, sampler,
+                                             device=args.device)
     bf = None
     if args.extra_bf16_s > 0 and args.dtype != "bf16" and d.cuda:
-        wb, ub, _, _, _ = run_fleet(d, launcher, pod_envs, "bf16", not args.no_graphs, extra_env, 2, 1,
-                                    args.extra_bf16_s, sampler, coll)
+        wb, ub, _, _, _ = run_fleet(d, launcher, fleet_envs(pod_envs), "bf16", not args.no_graphs, extra_env, 2, 1,
+                                    args.extra_bf16_s, sampler)
         bf = {"inf_per_s": round(wb.throughput, 2), "mean_latency_s": wb.mean_latency_s,
               "concurrent_pods": wb.concurrent, "gpu_util_pct": ub}
     table = []
@@ -394,8 +406,8 @@ def main(argv=None) -> int:
 
     # whole-job aggregates (window = slowest rank's)
     elapsed, = d.reduce([w.window_s], "max")
-    running = w.concurrent + (1 if tr and tr["running"] else 0)
-    sums = d.reduce([w.completed, float(running), util if util is not None else -1e9, float(len(pod_envs)),
+    running = w.concurrent  # inference pods and the trainer pod alike
+    sums = d.reduce([w.completed, float(running), util if util is not None else -1e9, float(len(w.inference_pods)),
                      ref["inf_per_s"] if ref else 0.0, bf["inf_per_s"] if bf else 0.0,
                      tr["gemm_tflops"] if tr else 0.0, tr["allreduce_gb_per_s"] if tr else 0.0,
                      float(len(envs))], "sum")
@@ -426,7 +438,7 @@ def main(argv=None) -> int:
                                   f"{world} GPU(s)",
                    "pods_per_gpu": args.pods_per_gpu, "slice_gb": args.slice_gb, "mode": args.mode,
                    "pod_execution": "one process per pod with its device-plugin env", "graphs": not args.no_graphs,
-                   "collective_tenant": bool(coll), "step_s": args.step_s, "bursty": args.bursty or None,
+                   "collective_tenant": use_coll, "step_s": args.step_s, "bursty": args.bursty or None,
                    "pods_placed_per_node": int(placed)},
         "gpu_util_pct": None if util_mean is None else round(util_mean, 1),
         "gpu_util_samples": n_util,
@@ -465,7 +477,12 @@ def main(argv=None) -> int:
                                                  "gemm_dim": args.coll_dim,
                                                  "step": "bf16 MLP (4 x dim^2 layers, batch dim) forward + backward, "
                                                          "bucketed all-reduce launched from the gradient hooks "
-                                                         "(overlaps backward), SGD"},
+                                                         "(overlaps backward), SGD",
+                                                 "execution": "one pod process per GPU with its device-plugin env "
+                                                              "(models/trainer_pod.py), RCCL job across the GPUs",
+                                                 "allreduce_gb_per_s": "gradient bytes all-reduced per second "
+                                                                       "(payload); rank0.bucket_busbw_gbps = one "
+                                                                       "bucket's all-reduce, NCCL-tests busbw"},
         "rank0_window": w.as_dict(),
         "latency_table": table or None,
         "rank0_ref_pod": ref,

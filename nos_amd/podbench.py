@@ -68,7 +68,16 @@ class WindowStats:
 
     @property
     def completed(self) -> float:
-        return sum(p.completed for p in self.pods)
+        """Inferences (trainer pods' iterations are not inferences)."""
+        return sum(p.completed for p in self.inference_pods)
+
+    @property
+    def inference_pods(self) -> list["PodResult"]:
+        return [p for p in self.pods if p.info.get("kind") != "trainer"]
+
+    @property
+    def trainer_pods(self) -> list["PodResult"]:
+        return [p for p in self.pods if p.info.get("kind") == "trainer"]
 
     @property
     def throughput(self) -> float:
@@ -81,10 +90,10 @@ class WindowStats:
     @property
     def mean_latency_s(self) -> float | None:
         c = self.completed
-        return len(self.pods) * self.window_s / c if c > 0 else None
+        return len(self.inference_pods) * self.window_s / c if c > 0 else None
 
     def as_dict(self) -> dict:
-        lat = [p.latency_s for p in self.pods if p.latency_s]
+        lat = [p.latency_s for p in self.inference_pods if p.latency_s]
         return {"pods": len(self.pods), "window_s": round(self.window_s, 3),
                 "completed": round(self.completed, 2), "inf_per_s": round(self.throughput, 3),
                 "mean_latency_s": None if self.mean_latency_s is None else round(self.mean_latency_s, 5),
@@ -229,12 +238,17 @@ class PodFleet:
             # a pod sees only its own allocation: drop the launcher's rank/device variables
             for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
                       "ROC_GLOBAL_CU_MASK", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
-                      "NOS_AMD_MEMORY_LIMIT_GB", "TORCHELASTIC_RUN_ID", "GROUP_RANK", "ROLE_RANK"):
+                      "NOS_AMD_MEMORY_LIMIT_GB", "GROUP_RANK", "ROLE_RANK", "LOCAL_WORLD_SIZE", "GROUP_WORLD_SIZE",
+                      "ROLE_WORLD_SIZE", "ROLE_NAME"):
                 env.pop(k, None)
+            for k in [k for k in env if k.startswith("TORCHELASTIC_")]:
+                env.pop(k)  # e.g. TORCHELASTIC_USE_AGENT_STORE: a trainer pod's job must host its own store
             env.update(self.extra_env)
             env.update(penv)
             env["PYTHONPATH"] = str(REPO) + os.pathsep + env.get("PYTHONPATH", "")
-            cmd = [sys.executable, "-u", "-m", "nos_amd.models.pod", "--status", str(self.board.path),
+            # NOS_AMD_POD_KIND=trainer: the DP trainer tenant (models/trainer_pod.py) instead of a YOLOS pod
+            module = "nos_amd.models.trainer_pod" if env.get("NOS_AMD_POD_KIND") == "trainer" else "nos_amd.models.pod"
+            cmd = [sys.executable, "-u", "-m", module, "--status", str(self.board.path),
                    "--slot", str(i), "--out", str(self.dir), "--dtype", self.dtype, "--seed", str(self.seed0 + i),
                    "--device", self.device]
             if not self.graphs:
@@ -298,8 +312,9 @@ class PodFleet:
         for i in range(len(self.envs)):
             r = self.results.get(i, {})
             times = r.get("times") or []
+            kind = r.get("kind") or ("trainer" if self.envs[i].get("NOS_AMD_POD_KIND") == "trainer" else "inference")
             if not times:
-                out.append(PodResult(i, 0.0, None, w, False, {"error": r.get("error")}))
+                out.append(PodResult(i, 0.0, None, w, False, {"error": r.get("error"), "kind": kind}))
                 continue
             start = r.get("t_ready", times[0])
             c = progress(times, t1, start) - progress(times, t0, start)
@@ -310,7 +325,10 @@ class PodFleet:
             # pod that stopped early fails it (a bursty pod idling at t1 does not)
             running = times[0] <= t0 and gap < 0.25 * w
             info = {k: r.get(k) for k in ("pid", "multiprocessor_count", "cu_mask", "hip_visible_devices",
-                                           "memory_limit_gb", "memory_fraction", "max_allocated_gb")}
+                                           "memory_limit_gb", "memory_fraction", "max_allocated_gb", "cu_budget",
+                                           "kind", "world_size", "backend", "flops_per_step", "bucket_bytes",
+                                           "buckets", "bucket_busbw_gbps", "launched_in_backward")}
+            info["kind"] = kind
             out.append(PodResult(i, c, (w / c) if c > 0 else None, gap, running, info))
         return WindowStats(w, out)
 
