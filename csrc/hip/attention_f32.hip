@@ -321,7 +321,7 @@ NOS_API int nos_attn_fwd_f32_d64(const float* q, const float* k, const float* v,
   // SIMD (B=8: 1298 vs 1357 us for 64-key tiles at 2;
   // profiles/r02_attention_f32.json, r02_attention_f32_tilings.json)
   const long long nwg = (long long)B * H * ((Sq + 127) / 128);
-  const int var = g_variant != 0 ? g_variant : nwg <= 256 ? 2 : 6;
+  const int var = g_variant != 0 ? g_variant : nwg <= nos_effective_cus() ? 2 : 6;
   if (var == 1) return launch<4, 64, 1>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
   if (var == 3) return launch<4, 32, 1>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);
   if (var == 4) return launch<2, 64, 1>(q, k, v, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, stream);

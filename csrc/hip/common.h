@@ -84,6 +84,10 @@ __device__ __forceinline__ XcdChunk xcd_chunk(int block, int grid, int n) {
 // Returns `items` when no budget is set.
 int nos_grid_for(const void* kernel, int block_threads, size_t lds_bytes, long long items);
 
+// CUs the tile/variant cost models plan for: the CU budget when one is set
+// (a CU-mask slice), else the current device's CU count.
+int nos_effective_cus();
+
 #define HIP_CHECK_RET(expr)                       \
   do {                                            \
     hipError_t _e = (expr);                       \

@@ -92,17 +92,7 @@ int g_tile_policy = 0;
 // during the current epilogue (nos_gemm_set_persistent)
 int g_persist = 0;
 
-int num_cus() {
-  static int cached[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cached[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cached[dev] = n;
-  }
-  return cached[dev];
-}
+int num_cus() { return nos_effective_cus(); }  // a CU-slice tenant plans for its budget
 
 __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);

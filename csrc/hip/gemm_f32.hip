@@ -257,11 +257,12 @@ int pick_tile(int M, int N) {
   }
   const int bm[3] = {128, 64, 64}, bn[3] = {128, 128, 64}, per_cu[3] = {2, 3, 4};
   const double eff[3] = {1.0, 0.9, 0.75};
+  const long long cus = nos_effective_cus();  // a CU-mask slice plans for its own CUs
   int best = 2;
   double best_cost = 1e300;
   for (int c = 0; c < 3; ++c) {
     const long long tiles = (long long)((M + bm[c] - 1) / bm[c]) * ((N + bn[c] - 1) / bn[c]);
-    const long long slots = 256LL * per_cu[c];
+    const long long slots = cus * per_cu[c];
     const long long rounds = (tiles + slots - 1) / slots;
     const double cost = (double)rounds * bm[c] * bn[c] / eff[c];
     if (cost < best_cost - 1e-9) {

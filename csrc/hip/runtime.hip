@@ -28,6 +28,19 @@ NOS_API int nos_set_cu_budget(int cus) {
 
 NOS_API int nos_get_cu_budget() { return g_cu_budget; }
 
+int nos_effective_cus() {
+  if (g_cu_budget > 0) return g_cu_budget;
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 int nos_grid_for(const void* kernel, int block_threads, size_t lds_bytes, long long items) {
   if (g_cu_budget <= 0 || items <= 8) return (int)items;
   const unsigned long long key = (unsigned long long)(uintptr_t)kernel ^ ((unsigned long long)lds_bytes << 48);
