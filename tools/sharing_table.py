@@ -54,7 +54,7 @@ def main() -> None:
                 envs, info = plans[(mode, n)]
                 t = time.monotonic()
                 w, util, n_util, ready, _ = bench.run_fleet(d, launcher, envs, a.dtype, True, extra, 1, 1, a.window,
-                                                         sampler, None)
+                                                         sampler)
                 w0 = bench.time.monotonic()
                 row = {"mode": mode, "hw_queues": hq, "pod_env": a.pod_env, "dtype": a.dtype, **w.as_dict(), "gpu_util_pct": util,
                        "util_samples": n_util, "pods_ready_s": round(ready, 1),
