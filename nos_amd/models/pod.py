@@ -119,25 +119,32 @@ def _die_with_parent() -> Callable[[], bool]:
     return lambda: os.getppid() != ppid0
 
 
-def kernel_config(memory_fraction: float | None, env: dict | None = None) -> dict[str, str]:
+def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_budget: int = 0) -> dict[str, str]:
     """Kernel configs a pod picks from its slice (and ``NOS_AMD_*`` overrides
     for A/B runs).
 
     A pod owning the whole GPU wants the fewest rounds of tiles (bf16 GEMM
     latency policy: fc2 19.7 -> 14.2 us at batch 1) and two attention wave
     groups when its grid leaves CUs idle (the kernel's auto rule).  A
-    fractional slice shares the CUs with other pods, so per-workgroup
-    footprint wins over per-tile efficiency: bf16 least-work tiles, fp32
-    GEMMs on 64x64 tiles (33 KB LDS, <= 64 VGPRs; 8 pods: 318.0 / 318.1 vs
-    317.3 / 314.2 inf/s, profiles/r02_f32_gemm_policy_fleet_ab.json) and fp32
-    attention with one wave group on 32-key tiles, whose 32 KB LDS ring
-    leaves room for other pods' workgroups (317 vs 310 inf/s for 64-key
-    tiles, 302 for two groups; profiles/r02_attention_f32_tilings.json)."""
+    fractional slice that SHARES the CUs with other pods wants small
+    per-workgroup footprints: bf16 least-work tiles, fp32 GEMMs on 64x64
+    tiles (33 KB LDS, <= 64 VGPRs; 8 pods: 318.0 / 318.1 vs 317.3 / 314.2
+    inf/s, profiles/r02_f32_gemm_policy_fleet_ab.json) and fp32 attention with
+    one wave group on 32-key tiles (317 vs 310 inf/s for 64-key tiles,
+    profiles/r02_attention_f32_tilings.json).  A CU-mask slice (``cu_budget``
+    CUs of its own, persistent grids) plans for its own CUs: budget-aware
+    latency tiles and the auto attention rule, which picks the register-capped
+    32-key tiling (4 waves per SIMD) -- 7 exclusive 32-CU pods 217.6 -> 231.0
+    inf/s, solo 29.0 -> 27.2 ms (profiles/r03_cumask_kernel_configs.json)."""
     env = os.environ if env is None else env
     whole = memory_fraction is None or memory_fraction >= 0.99
+    if cu_budget and not whole:
+        gf, att = "latency", "auto"
+    else:
+        gf, att = ("latency", "auto") if whole else ("small", "w4k32")
     return {"gemm_bf16": env.get("NOS_AMD_GEMM_POLICY") or ("latency" if whole else "throughput"),
-            "gemm_f32": env.get("NOS_AMD_GEMM_F32_POLICY") or ("latency" if whole else "small"),
-            "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or ("auto" if whole else "w4k32")}
+            "gemm_f32": env.get("NOS_AMD_GEMM_F32_POLICY") or gf,
+            "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or att}
 
 
 def slice_cu_budget(env: dict | None = None) -> int:
@@ -188,11 +195,11 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             torch.backends.cuda.matmul.allow_tf32 = False  # true fp32 GEMMs (no reduced-precision shortcut)
             from ..ops import set_attention_f32_variant, set_cu_budget, set_gemm_f32_policy, set_gemm_policy
 
-            cfg = kernel_config(frac, os.environ)
+            budget = slice_cu_budget(os.environ)
+            cfg = kernel_config(frac, os.environ, budget)
             set_gemm_policy(cfg["gemm_bf16"])
             set_gemm_f32_policy(cfg["gemm_f32"])
             set_attention_f32_variant(cfg["attention_f32"])
-            budget = slice_cu_budget(os.environ)
             if budget:  # CU-mask slice: slice-sized persistent grids (ops.set_cu_budget)
                 set_cu_budget(budget)
         m, x = _build(dtype, seed, demo_input_hw(), device)
