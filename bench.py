@@ -302,6 +302,10 @@ def trainer_stats(w) -> dict | None:
             "cu_mask": i.get("cu_mask"), "pid": i.get("pid")}
 
 
+class FleetStartError(RuntimeError):
+    """Pods of some rank failed to start; raised on EVERY rank (the flag is reduced)."""
+
+
 def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, step_s, sampler, device="cuda"):
     from nos_amd.podbench import PodFleet
 
@@ -316,9 +320,9 @@ def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, 
             err = e
         failed, = d.reduce([1.0 if err else 0.0], "max")
         if err:
-            raise err
+            raise FleetStartError(f"{dtype} pods failed to start: {err!r}") from err
         if failed:
-            raise RuntimeError(f"pods of another rank failed to start ({dtype})")
+            raise FleetStartError(f"pods of another rank failed to start ({dtype})")
         d.barrier_sync()
         t0, t1, (util, n_util) = fleet_window(d, fleet, warmup, steps, step_s, sampler)
         fleet.stop()
@@ -382,9 +386,23 @@ def main(argv=None) -> int:
                                     args.ref_pod_s, sampler, device=args.device)
         ref = {"inf_per_s": round(w1.throughput, 3), "latency_s": w1.mean_latency_s, "gpu_util_pct": u1}
 
-    w, util, n_util, ready_s, tr = run_fleet(d, launcher, fleet_envs(pod_envs), args.dtype, not args.no_graphs,
-                                             fleet_env, args.warmup, args.steps, args.step_s, sampler,
-                                             device=args.device)
+    trainer_error = None
+    try:
+        w, util, n_util, ready_s, tr = run_fleet(d, launcher, fleet_envs(pod_envs), args.dtype, not args.no_graphs,
+                                                 fleet_env, args.warmup, args.steps, args.step_s, sampler,
+                                                 device=args.device)
+    except FleetStartError as e:
+        if not use_coll:
+            raise
+        # the trainer job could not form (e.g. RCCL refused the pods' transport):
+        # every rank saw the same flag, so every rank measures the inference fleet
+        # alone and the line says why there is no trainer row
+        trainer_error = str(e)[:400]
+        log(rank, f"trainer pods failed to start, measuring without them: {trainer_error}")
+        use_coll, fleet_envs = False, (lambda e: e)
+        w, util, n_util, ready_s, tr = run_fleet(d, launcher, pod_envs, args.dtype, not args.no_graphs,
+                                                 fleet_env, args.warmup, args.steps, args.step_s, sampler,
+                                                 device=args.device)
     bf = None
     if args.extra_bf16_s > 0 and args.dtype != "bf16" and d.cuda:
         wb, ub, _, _, _ = run_fleet(d, launcher, fleet_envs(pod_envs), "bf16", not args.no_graphs, extra_env, 2, 1,
@@ -471,6 +489,7 @@ def main(argv=None) -> int:
         "baseline": {"pods_per_gpu": BASELINE_PODS_PER_GPU, "inf_per_s_per_gpu": BASELINE_INF_PER_S_PER_GPU,
                      "aggregate_vs_single_pod_mps": 1.93, "aggregate_vs_single_pod_mig": 1.79},
         "bf16_gfx950_kernels": None if bf is None else {**bf, "inf_per_s_node": round(bf_sum, 2)},
+        "trainer_error": trainer_error,
         "trainer_pods": None if tr is None else {"per_node_gemm_tflops": round(tr_tf, 2),
                                                  "per_node_allreduce_gb_per_s": round(tr_gbs, 2),
                                                  "rank0": tr, "bucket_mb": args.coll_bucket_mb,

@@ -45,6 +45,8 @@ def run_trainer(status: str, slot: int, out: str, device: str = "cuda", dim: int
         from ..utils.memlimit import apply_memory_limit
         from .tenants import CollectiveTenant
 
+        if os.environ.get("NOS_AMD_TRAINER_FAULT") == "init":  # test hook: the job never forms
+            raise RuntimeError("injected trainer init fault")
         gpu = device == "cuda"
         world = int(os.environ.get("WORLD_SIZE", "1"))
         backend = os.environ.get("NOS_AMD_TRAINER_BACKEND") or ("nccl" if gpu else "gloo")

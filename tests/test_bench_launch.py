@@ -16,11 +16,11 @@ import pytest
 REPO = Path(__file__).resolve().parent.parent
 
 
-def _run(n: int, port: int) -> list[dict]:
+def _run(n: int, port: int, **env_extra) -> list[dict]:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", str(n), "--device", "cpu",
            "--steps", "4", "--warmup", "1", "--step-s", "0.4", "--ref-pod-s", "0", "--pods-per-gpu", "3"]
-    env = {**os.environ, "OMP_NUM_THREADS": "1"}
+    env = {**os.environ, "OMP_NUM_THREADS": "1", **env_extra}
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     return [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
@@ -39,6 +39,18 @@ def test_torchrun_two_ranks_aggregate_one_json_line():
     assert d["trainer_pods"]["rank0"]["running"] and d["trainer_pods"]["per_node_allreduce_gb_per_s"] > 0
     assert d["ms_per_step"] == pytest.approx(400, rel=0.2)
     assert d["aggregate_inf_per_s"] > 0 and d["scaling"] == "weak"
+
+
+@pytest.mark.timeout(900)
+def test_trainer_job_that_cannot_form_falls_back_on_every_rank():
+    """A trainer pod that fails before READY (here: an injected init fault) makes
+    EVERY rank re-run the window without trainer pods; the line records why."""
+    lines = _run(2, 29617, NOS_AMD_TRAINER_FAULT="init")
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["trainer_pods"] is None and "failed to start" in d["trainer_error"]
+    assert d["config"]["collective_tenant"] is False
+    assert d["value"] == 6 and d["aggregate_inf_per_s"] > 0  # 3 inference pods per rank
 
 
 @pytest.mark.timeout(600)
