@@ -295,7 +295,8 @@ int launch(const float* q, const float* k, const float* v, float* o, int B, int 
 // 4: 2 waves x 64-key tiles (64-query blocks), 5: 8 waves x 64-key tiles,
 // 6: variant 3 register-capped for 3 workgroups per CU (127 VGPRs, no
 //    AGPRs, no scratch: 4 waves per SIMD; the same cap on variant 1 spills),
-// 7: two wave groups on 32-key tiles (64 KB LDS ring)
+// 7: two wave groups on 32-key tiles (64 KB LDS ring),
+// (the bf16x6 split kernel, attention_f32x.hip, takes a workspace: its own entry)
 int g_variant = 0;
 
 }  // namespace

@@ -1,0 +1,319 @@
+// fp32 self-attention (head_dim 64, non-causal) on the bf16 matrix pipes:
+// every fp32 operand is split into three bf16 pieces x = x0 + x1 + x2
+// (x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1): 3 x 8 mantissa
+// bits hold all 24 of an fp32, so the split is exact), and every product
+// a.b is the sum of the six piece products whose order is <= 2^-16 |a.b|:
+//   a0b0 + a0b1 + a1b0 + a0b2 + a1b1 + a2b0.
+// A bf16 x bf16 product is exact in fp32 and v_mfma_f32_32x32x16_bf16
+// accumulates in fp32, so the only error beyond fp32 accumulation is the
+// dropped a1b2 + a2b1 + a2b2 (<= ~2^-23 |a.b|, the size of one fp32 rounding
+// of the product).  Six bf16 MFMAs (32 cycles each) replace eight
+// v_mfma_f32_32x32x2_f32 (64 cycles each) per 16-deep step: 2.7x less
+// matrix-pipe time than the exact-f32 MFMA (attention_f32.hip) at the same
+// accuracy (tests/test_kernels_gpu.py checks both against fp64).
+//
+// Design (CDNA4; the bf16 kernel's structure, attention.hip):
+//  * K and V are split ONCE per call by a streaming kernel into six bf16
+//    planes per token (K0 K1 K2 V0 V1 V2, every head's 64 dims contiguous)
+//    instead of once per workgroup that reads them (27 q-blocks per head);
+//  * one workgroup = 4 waves x 32 query rows of one (batch, head); 32-key
+//    tiles of the six planes (4 KiB each) arrive by LDS-DMA
+//    (global_load_lds_dwordx4, swizzle applied to the source address) into a
+//    2-deep ring: no staging registers, no VALU, one barrier per tile;
+//  * swapped QK^T (S^T = K . Q^T): Q's three pieces (pre-scaled by
+//    scale * log2 e) stay in registers as the B operand; K pieces are read
+//    with ds_read_b128 from XOR-swizzled images;
+//  * the S^T accumulator (query on the lane, 16 keys in registers) gives the
+//    row max / sum lane-locally plus one v_permlane32_swap; P = exp2(S - m)
+//    is split into three pieces in registers and used directly as the B
+//    operand of O^T = V^T . P^T, whose V^T pieces come from the transposing
+//    LDS read ds_read_b64_tr_b16 (no LDS round trip for P);
+//  * deferred rescale (P <= 2^8) and XCD-aware (batch, head, q-block) order
+//    as in attention_f32.hip; PERSIST: slice-sized grid (nos::xcd_chunk).
+#include "common.h"
+#include "split_bf16.h"
+
+namespace {
+
+constexpr int D = 64;
+constexpr int W = 4;                    // waves per workgroup
+constexpr int NT = 64 * W;
+constexpr int QBLK = 32 * W;            // query rows per workgroup
+constexpr int KVB = 32;                 // keys per tile
+constexpr int IMG = KVB * D * 2;        // one bf16 piece image: 4 KiB
+constexpr int STAGE = 6 * IMG;          // K0 K1 K2 V0 V1 V2
+constexpr int LDS_BYTES = 2 * STAGE;    // 48 KiB ring
+constexpr float RESCALE_THR = 8.f;      // log2 units
+
+__device__ __forceinline__ int kswz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int vswz(int row) { return ((row >> 1) & 1) << 2; }
+
+__device__ __forceinline__ float xor32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <bool PERSIST>
+__global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
+    const float* __restrict__ q, const unsigned short* __restrict__ kvs, float* __restrict__ o, int B, int H, int Sq,
+    int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, int nqb) {
+  const int ldh = H * D;  // elements per plane row
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int nwg = B * H * nqb;
+  nos::XcdChunk chunk;
+  if constexpr (PERSIST) {
+    chunk = nos::xcd_chunk(blockIdx.x, gridDim.x, nwg);
+  } else {
+    chunk.first = nos::xcd_remap(blockIdx.x, nwg);
+    chunk.end = chunk.first + 1;
+    chunk.step = 1;
+  }
+
+  const int tid = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int r = lane & 31;
+  const int hh = lane >> 5;
+
+  // hoisted per-lane LDS read offsets (relative to a piece image)
+  int koff[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) koff[ks] = r * 128 + (((2 * ks + hh) ^ kswz(r)) << 4);
+  const int g16 = (lane >> 4) & 1;
+  const int tq = (lane & 15) >> 2;
+  const int tp = lane & 3;
+  const int vlb = (tq >> 1) & 1;
+  int voff[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+    voff[db] = (4 * hh + tq) * 128 + (((4 * (db ^ vlb)) + 2 * g16 + (tp >> 1)) << 4) + 8 * (tp & 1);
+
+  const int ntiles = (Skv + KVB - 1) / KVB;
+  const int skvp = ntiles * KVB;
+  int soff[6];  // staging: per-lane element offset of instruction i within a tile
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int p = wid * 6 + i;
+    const int plane = p >> 2;
+    const int row = (p & 3) * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ (plane < 3 ? kswz(row) : vswz(row));
+    soff[i] = (row * 6 + plane) * ldh + lc * 8;
+  }
+
+  for (int w = chunk.first; w < chunk.end; w += chunk.step) {
+    if (PERSIST && w != chunk.first) __syncthreads();  // the previous item is done with the ring
+    const int b = w / (H * nqb);
+    const int rem = w - b * (H * nqb);
+    const int hd = rem / nqb;
+    const int qb = rem - hd * nqb;
+    const long long boff = (long long)b * bs_in + hd * D;
+
+    // ---- Q pieces (B operand): lane holds Q[row r][d = 16ks + 8hh .. +7] * c
+    const int qrow = qb * QBLK + wid * 32 + r;
+    bf16x8_t qf[4][3];
+    {
+      const float* qp = q + boff + (long long)min(qrow, Sq - 1) * ld_in + 8 * hh;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const float4 x0 = *reinterpret_cast<const float4*>(qp + 16 * ks);
+        const float4 x1 = *reinterpret_cast<const float4*>(qp + 16 * ks + 4);
+        const float x[8] = {x0.x * c, x0.y * c, x0.z * c, x0.w * c, x1.x * c, x1.y * c, x1.z * c, x1.w * c};
+        nos::split8(x, qf[ks][0], qf[ks][1], qf[ks][2]);
+      }
+    }
+
+    // ---- LDS-DMA staging: per tile 6 planes x 32 rows x 128 B = 24 wave
+    // instructions, 6 per wave.  Instruction p: plane p / 4, rows (p % 4) * 8
+    // + lane / 8, physical chunk lane % 8 = logical chunk ^ swizzle.
+    // The planes are padded to whole tiles with zeros: a tile's address is a
+    // wave-uniform base plus the hoisted per-lane offsets.
+    const unsigned short* pb = kvs + (long long)b * skvp * (6 * ldh) + hd * D;
+    auto stage = [&](int t, int buf) {
+      const unsigned short* tb = pb + (long long)t * (KVB * 6) * ldh;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int p = wid * 6 + i;
+        glds16(tb + soff[i], smem + buf * STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
+      }
+    };
+    stage(0, 0);
+
+    f32x16_t oacc[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      oacc[0][i] = 0.f;
+      oacc[1][i] = 0.f;
+    }
+    float m = 0.f, l = 0.f;  // reference max (log2 units), this lane-half's partial row sum
+
+    __syncthreads();  // tile 0 landed and is visible
+
+    for (int t = 0; t < ntiles; ++t) {
+      const int buf = t & 1;
+      const bool more = t + 1 < ntiles;
+      if (more) stage(t + 1, buf ^ 1);  // that buffer was released by the barrier ending t-1
+      const unsigned char* kl = smem + buf * STAGE;
+      const unsigned char* vl = kl + 3 * IMG;
+
+      f32x16_t s;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bf16x8_t a[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8_t*>(kl + p * IMG + koff[ks]);
+        s = nos::mma6(a, qf[ks], s);
+      }
+      if ((t + 1) * KVB > Skv) {  // tail tile: keys past Skv never contribute
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (t * KVB + (i & 3) + 8 * (i >> 2) + 4 * hh >= Skv) s[i] = -INFINITY;
+      }
+      float mt = s[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mt = fmaxf(mt, s[i]);
+      const float mrel = xor32_max(mt) - m;
+      if (t == 0 || !__all(mrel <= RESCALE_THR)) {  // the first tile sets the reference max
+        const float delta = t == 0 ? mrel : fmaxf(mrel, 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        m += delta;
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          oacc[0][i] *= alpha;
+          oacc[1][i] *= alpha;
+        }
+      }
+      // P = exp2(S - m), split into three pieces: pf[s2][piece] covers the
+      // 16 keys of registers 8*s2 .. 8*s2+7
+      bf16x8_t pf[2][3];
+      f32x2_t ps2 = {0.f, 0.f};
+      const f32x2_t nm2 = {-m, -m};
+#pragma unroll
+      for (int j2 = 0; j2 < 8; ++j2) {
+        f32x2_t x = f32x2_t{s[2 * j2], s[2 * j2 + 1]} + nm2;
+        x.x = __builtin_amdgcn_exp2f(x.x);
+        x.y = __builtin_amdgcn_exp2f(x.y);
+        ps2 += x;
+        bf16x2_t a, bb, cc;
+        nos::split2(x, a, bb, cc);
+        const int s2 = j2 >> 2, e = 2 * (j2 & 3);
+        pf[s2][0][e] = a.x; pf[s2][0][e + 1] = a.y;
+        pf[s2][1][e] = bb.x; pf[s2][1][e + 1] = bb.y;
+        pf[s2][2][e] = cc.x; pf[s2][2][e + 1] = cc.y;
+      }
+      l += ps2.x + ps2.y;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8_t a[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const unsigned char* base = vl + p * IMG + voff[db] + s2 * 16 * 128;
+            const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base));
+            const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + 8 * 128));
+            const s16x8_t a16 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            a[p] = __builtin_bit_cast(bf16x8_t, a16);
+          }
+          oacc[db] = nos::mma6(a, pf[s2], oacc[db]);
+        }
+      __syncthreads();  // next tile landed (vmcnt(0)); every wave is done with `buf`
+    }
+
+    const float inv = 1.f / xor32_sum(l);
+    if (qrow < Sq) {
+      float* op = o + (long long)b * bs_out + (long long)qrow * ld_out + hd * D;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float4 y;
+          y.x = oacc[db][4 * g + 0] * inv;
+          y.y = oacc[db][4 * g + 1] * inv;
+          y.z = oacc[db][4 * g + 2] * inv;
+          y.w = oacc[db][4 * g + 3] * inv;
+          *reinterpret_cast<float4*>(op + 32 * db + 8 * g + 4 * hh) = y;
+        }
+    }
+  }  // items
+}
+
+// K and V rows of the fused projection -> six bf16 planes per token:
+// kvs[b][s][plane][H*64], plane = 3 * (0 K, 1 V) + piece, s < Skvp (rows
+// past Skv are zeros).  One thread: 8 dims of one (token, tensor, head).
+__global__ __launch_bounds__(256) void split_kv_kernel(const float* __restrict__ k, const float* __restrict__ v,
+                                                       unsigned short* __restrict__ kvs, int S, int Sp, int H,
+                                                       int ld_in, long long bs_in, int n8) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  const int per_tok = 16 * H;                 // 8-dim chunks of K and V per token
+  const int tok = i / per_tok;
+  const int rem = i - tok * per_tok;
+  const int is_v = rem >= 8 * H;
+  const int ch = rem - is_v * 8 * H;          // chunk within the H*64 row
+  const int b = tok / Sp, s = tok - b * Sp;
+  bf16x8_t p[3];
+  if (s < S) {
+    const float* src = (is_v ? v : k) + b * bs_in + (long long)s * ld_in + ch * 8;
+    const float4 x0 = reinterpret_cast<const float4*>(src)[0];
+    const float4 x1 = reinterpret_cast<const float4*>(src)[1];
+    const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    nos::split8(x, p[0], p[1], p[2]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[0][j] = p[1][j] = p[2][j] = (__bf16)0.f;
+  }
+  unsigned short* dst = kvs + ((long long)tok * 6 + 3 * is_v) * (H * D) + ch * 8;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) *reinterpret_cast<bf16x8_t*>(dst + j * H * D) = p[j];
+}
+
+}  // namespace
+
+// Workspace bytes of nos_attn_fwd_f32x6_d64 (the split K/V planes).
+NOS_API long long nos_attn_f32x6_workspace(int B, int H, int Skv) {
+  const long long skvp = (Skv + KVB - 1) / KVB * KVB;
+  return (long long)B * skvp * 6 * H * D * 2;
+}
+
+// The exact-fp32 kernel's contract (attention_f32.hip: nos_attn_fwd_f32_d64)
+// plus a workspace of nos_attn_f32x6_workspace() bytes (16-byte aligned).
+NOS_API int nos_attn_fwd_f32x6_d64(const float* q, const float* k, const float* v, float* o, int B, int H, int Sq,
+                                   int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float scale,
+                                   void* ws, long long ws_bytes, hipStream_t stream) {
+  if (B <= 0 || H <= 0 || Sq <= 0 || Skv <= 0) return (int)hipErrorInvalidValue;
+  if (ld_in < H * D || ld_out < H * D || (ld_in & 3) || (ld_out & 3) || (bs_in & 3) || (bs_out & 3))
+    return (int)hipErrorInvalidValue;
+  if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o | (uintptr_t)ws) & 15) return (int)hipErrorInvalidValue;
+  if (ws == nullptr || ws_bytes < nos_attn_f32x6_workspace(B, H, Skv)) return (int)hipErrorInvalidValue;
+  const float c = scale * 1.4426950408889634f;
+  const int nqb = (Sq + QBLK - 1) / QBLK;
+  const long long nwg = (long long)B * H * nqb;
+  if (nwg > (1LL << 30)) return (int)hipErrorInvalidValue;
+  const int skvp = (Skv + KVB - 1) / KVB * KVB;
+  const long long n8 = (long long)B * skvp * 2 * H * 8;
+  if (n8 > INT_MAX || (long long)skvp * 6 * H * D > INT_MAX) return (int)hipErrorInvalidValue;
+  auto* kvs = static_cast<unsigned short*>(ws);
+  hipLaunchKernelGGL(split_kv_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, stream, k, v, kvs, Skv, skvp,
+                     H, ld_in, bs_in, (int)n8);
+  const int grid = nos_grid_for((const void*)attn_fwd_f32x6_d64_kernel<true>, NT, LDS_BYTES, nwg);
+  if (grid < nwg)
+    hipLaunchKernelGGL(attn_fwd_f32x6_d64_kernel<true>, dim3((unsigned)grid), dim3(NT), LDS_BYTES, stream, q, kvs,
+                       o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
+  else
+    hipLaunchKernelGGL(attn_fwd_f32x6_d64_kernel<false>, dim3((unsigned)nwg), dim3(NT), LDS_BYTES, stream, q, kvs,
+                       o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
+  return (int)hipGetLastError();
+}

@@ -298,6 +298,10 @@ int launch(const float* A, int lda, const float* W, int ldw, const float* bias, 
 
 }  // namespace
 
+// The tile the policy picks for an M x N output (0: 128x128, 1: 64x128,
+// 2: 64x64) -- shared with the bf16x6 split GEMM (gemm_f32x.hip).
+NOS_API int nos_gemm_f32_pick_tile(int M, int N) { return pick_tile(M, N); }
+
 NOS_API int nos_gemm_f32_set_policy(int policy) {
   if (policy < 0 || policy > 2) return (int)hipErrorInvalidValue;
   g_policy = policy;

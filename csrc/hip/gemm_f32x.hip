@@ -1,0 +1,274 @@
+// fp32 GEMM with fused LayerNorm / bias / GELU / ReLU / residual on the bf16
+// matrix pipes (bf16x6 split, split_bf16.h): the contract and epilogues of
+// the exact-f32 MFMA GEMM (gemm_f32.hip), 2.7x less matrix-pipe time per
+// FLOP at the same accuracy (tests/test_kernels_gpu.py checks both against
+// fp64).
+//
+//   plain:     C[M,N] = act(A[M,K] . W[N,K]^T + bias) (+ R)
+//   LN-fused:  C[M,N] = act(rstd * (A . W'^T - mu * c1) + c2)  (folded LayerNorm)
+//
+// Design:
+//  * W is a weight: it arrives PRE-SPLIT as three bf16 planes [3][N][K]
+//    (ops.split_f32_weight, once per weight); A (activations) is fp32;
+//  * 4 waves (2 x 2) per workgroup, tiles 128x128 / 64x128 / 64x64 chosen by
+//    the fp32 GEMM's tile policy (nos_gemm_f32_pick_tile), each wave (BM/2) x
+//    (BN/2) as 32x32 blocks, BK = 32 per stage = two 16-deep MFMA steps;
+//  * LDS-DMA (global_load_lds_dwordx4) into a 2-deep ring: the A tile as fp32
+//    rows of 128 B (chunks XOR-swizzled by row & 7), the three W planes as
+//    rows of 64 B (chunks swizzled by (row >> 2) & 3) -- both conflict-free
+//    for the fragment reads; one barrier per stage;
+//  * a wave splits its A fragments in registers (the K-contiguous 8 floats
+//    of a 16-deep step are exactly one bf16x8 operand) and issues six
+//    v_mfma_f32_32x32x16_bf16 per 32x32 block and step;
+//  * epilogue and LayerNorm statistics as in gemm_f32.hip.
+#include "common.h"
+#include "split_bf16.h"
+
+namespace {
+
+constexpr int BK = 32;              // k per stage
+constexpr int NT = 256;
+constexpr int AROW = BK * 4;        // fp32 A row per stage: 128 B
+constexpr int WROW = BK * 2;        // bf16 W plane row per stage: 64 B
+enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
+
+__device__ __forceinline__ int aswz(int row) { return row & 7; }
+__device__ __forceinline__ int wswz(int row) { return (row >> 2) & 3; }
+
+__device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ float erf_fast(float x) {  // Abramowitz-Stegun 7.1.26, |err| <= 1.5e-7
+  const float ax = fabsf(x);
+  const float t = 1.f / fmaf(0.3275911f, ax, 1.f);
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float r = fmaf(-p * t, expf(-ax * ax), 1.f);
+  return copysignf(r, x);
+}
+
+template <bool LN, int BM, int BN, bool PERSIST>
+__global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
+    const float* __restrict__ A, int lda, const unsigned short* __restrict__ Wp, int ldw, long long wplane,
+    const float* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
+    const float* __restrict__ R, int ldr, float* __restrict__ C, int ldc, int M, int N, int K, int epi, float eps,
+    int tiles_m, int tiles_n) {
+  constexpr int TA = BM * AROW, TWP = BN * WROW, STAGE = TA + 3 * TWP;
+  constexpr int MI = BM / 64, NI = BN / 64;  // 32x32 blocks per wave (waves are 2 x 2)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* s_mu = reinterpret_cast<float*>(smem + 2 * STAGE);
+  float* s_rstd = s_mu + BM;
+
+  const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int c = lane & 31, h = lane >> 5;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntiles = tiles_m * tiles_n;
+  const int nk = K / BK;
+  nos::XcdChunk chunk;
+  if constexpr (PERSIST) {
+    chunk = nos::xcd_chunk(blockIdx.x, gridDim.x, ntiles);
+  } else {
+    chunk.first = nos::xcd_remap(blockIdx.x, ntiles);
+    chunk.end = chunk.first + 1;
+    chunk.step = 1;
+  }
+  for (int tt = chunk.first; tt < chunk.end; tt += chunk.step) {
+  if (PERSIST && tt != chunk.first) __syncthreads();  // the previous tile's ring and LN statistics are free
+  const int tm = tt / tiles_n, tn = tt - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // A: BM rows x 128 B = BM/8 wave instructions; W: 3 planes x BN rows x 64 B
+  // = 3*BN/16 wave instructions; all spread over the 4 waves
+  auto stage = [&](int k0, unsigned char* dst) {
+#pragma unroll
+    for (int p = wid; p < BM / 8; p += 4) {
+      const int row = p * 8 + (lane >> 3);
+      int grow = m0 + row;
+      grow = grow < M ? grow : M - 1;
+      glds16(A + (long long)grow * lda + k0 + (((lane & 7) ^ aswz(row)) << 2), dst + p * 8 * AROW);
+    }
+#pragma unroll
+    for (int p = wid; p < 3 * BN / 16; p += 4) {
+      const int plane = p / (BN / 16), rb = (p % (BN / 16)) * 16;
+      const int row = rb + (lane >> 2);
+      int gn = n0 + row;
+      gn = gn < N ? gn : N - 1;
+      glds16(Wp + plane * wplane + (long long)gn * ldw + k0 + (((lane & 3) ^ wswz(row)) << 3),
+             dst + TA + plane * TWP + rb * WROW);
+    }
+  };
+
+  f32x16_t acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  constexpr int TPR = NT / BM;           // LN statistics: threads per row
+  constexpr int FPT = BK / TPR;          // floats per thread per stage
+  const int srow = tid / TPR, spart = tid % TPR;
+  float sshift = 0.f, ssum = 0.f, ssq = 0.f;
+
+  stage(0, smem);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned char* cur = smem + (kt & 1) * STAGE;
+    if (kt + 1 < nk) stage((kt + 1) * BK, smem + ((kt + 1) & 1) * STAGE);  // released by the barrier ending kt-1
+    const unsigned char* ta = cur;
+    const unsigned char* tw = cur + TA;
+    if constexpr (LN) {
+#pragma unroll
+      for (int q = 0; q < FPT / 4; ++q) {
+        const int lc = spart * (FPT / 4) + q;
+        const float4 v = *reinterpret_cast<const float4*>(ta + srow * AROW + ((lc ^ aswz(srow)) << 4));
+        if (kt == 0 && q == 0) sshift = v.x;
+        const float d0 = v.x - sshift, d1 = v.y - sshift, d2 = v.z - sshift, d3 = v.w - sshift;
+        ssum += (d0 + d1) + (d2 + d3);
+        ssq = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, ssq))));
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {  // 16-deep MFMA steps: lane holds k = 16s + 8h .. +7
+      bf16x8_t af[MI][3], wf[NI][3];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wm * (BM / 2) + i * 32 + c;
+        const float4 x0 = *reinterpret_cast<const float4*>(ta + row * AROW + (((4 * s + 2 * h) ^ aswz(row)) << 4));
+        const float4 x1 = *reinterpret_cast<const float4*>(ta + row * AROW + (((4 * s + 2 * h + 1) ^ aswz(row)) << 4));
+        const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        nos::split8(x, af[i][0], af[i][1], af[i][2]);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int row = wn * (BN / 2) + j * 32 + c;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          wf[j][p] = *reinterpret_cast<const bf16x8_t*>(tw + p * TWP + row * WROW + (((2 * s + h) ^ wswz(row)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = nos::mma6(af[i], wf[j], acc[i][j]);
+    }
+    __syncthreads();  // next stage landed (vmcnt(0)); every wave is done with this one
+  }
+
+  if constexpr (LN) {
+    const float kpart = (float)(K / TPR);
+    float mean = sshift + ssum / kpart, m2 = ssq - ssum * ssum / kpart, cnt = kpart;
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) {  // Chan's parallel combination of the shifted partial sums
+      const float om = __shfl_xor(mean, o, 64), om2 = __shfl_xor(m2, o, 64), oc = __shfl_xor(cnt, o, 64);
+      const float tot = cnt + oc, dl = om - mean;
+      mean = mean + dl * (oc / tot);
+      m2 = m2 + om2 + dl * dl * (cnt * oc / tot);
+      cnt = tot;
+    }
+    if (spart == 0) {
+      s_mu[srow] = mean;
+      s_rstd[srow] = rsqrtf(fmaxf(m2 / (float)K, 0.f) + eps);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: register i of lane (c, h) = row (i&3) + 8(i>>2) + 4h of the block, column c
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int n = n0 + wn * (BN / 2) + j * 32 + c;
+    const int nc = n < N ? n : N - 1;
+    const float p1 = LN ? c1[nc] : 0.f;
+    const float p2 = LN ? c2[nc] : ((epi & EPI_BIAS) ? bias[nc] : 0.f);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int m = m0 + rl;
+        float v = acc[i][j][r];
+        if constexpr (LN) v = fmaf(s_rstd[rl], v - s_mu[rl] * p1, p2);
+        else v += p2;
+        if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+        if (epi & EPI_RELU) v = fmaxf(v, 0.f);
+        if (m < M && n < N) {
+          if (epi & EPI_RESID) v += R[(long long)m * ldr + n];
+          C[(long long)m * ldc + n] = v;
+        }
+      }
+    }
+  }
+  }  // tiles
+}
+
+template <bool LN, int BM, int BN>
+int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
+             const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K,
+             int epi, float eps, hipStream_t st) {
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const long long ntiles = (long long)tiles_m * tiles_n;
+  if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
+  const size_t lds = 2 * (size_t)(BM * AROW + 3 * BN * WROW) + 2 * BM * sizeof(float);
+  const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true>, NT, lds, ntiles);
+  if (grid < ntiles)
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true>), dim3((unsigned)grid), dim3(NT), lds, st, A, lda, Wp,
+                       ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false>), dim3((unsigned)ntiles), dim3(NT), lds, st, A, lda,
+                       Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+NOS_API int nos_gemm_f32_pick_tile(int M, int N);
+
+namespace {
+
+int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
+           const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi,
+           float eps, bool ln, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0) return (int)hipErrorInvalidValue;
+  if ((lda % 4) || (ldw % 8) || (wplane % 8) || lda < K || ldw < K || ldc < N || wplane < (long long)N * ldw)
+    return (int)hipErrorInvalidValue;
+  if (((uintptr_t)A | (uintptr_t)Wp) & 15) return (int)hipErrorInvalidValue;
+  if (!ln && (epi & EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
+  if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
+  if ((epi & EPI_RESID) && (!R || ldr < N)) return (int)hipErrorInvalidValue;
+  const int cfg = nos_gemm_f32_pick_tile(M, N);
+#define NOS_F32X_LAUNCH(LNV, BMV, BNV) \
+  launch_t<LNV, BMV, BNV>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, st)
+  if (ln) {
+    if (cfg == 0) return NOS_F32X_LAUNCH(true, 128, 128);
+    if (cfg == 1) return NOS_F32X_LAUNCH(true, 64, 128);
+    return NOS_F32X_LAUNCH(true, 64, 64);
+  }
+  if (cfg == 0) return NOS_F32X_LAUNCH(false, 128, 128);
+  if (cfg == 1) return NOS_F32X_LAUNCH(false, 64, 128);
+  return NOS_F32X_LAUNCH(false, 64, 64);
+#undef NOS_F32X_LAUNCH
+}
+
+}  // namespace
+
+// C = act(A . W^T + bias) (+ R), fp32 A [M,K] (lda), W as three bf16 planes
+// Wp + p * wplane, each [N,K] (ldw); K % 32 == 0, rows 16-byte aligned.
+NOS_API int nos_gemm_f32x6(const float* A, int lda, const void* Wp, int ldw, long long wplane, const float* bias,
+                           const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi,
+                           hipStream_t stream) {
+  return launch(A, lda, static_cast<const unsigned short*>(Wp), ldw, wplane, bias, nullptr, nullptr, R, ldr, C, ldc,
+                M, N, K, epi, 0.f, false, stream);
+}
+
+// C = act(LayerNorm(A) . W^T + bias) in the folded form (ops.fold_layernorm),
+// W' = W * gamma as three bf16 planes; K is the LayerNorm width.
+NOS_API int nos_gemm_ln_f32x6(const float* A, int lda, const void* Wp, int ldw, long long wplane, const float* c1,
+                              const float* c2, float* C, int ldc, int M, int N, int K, int epi, float eps,
+                              hipStream_t stream) {
+  return launch(A, lda, static_cast<const unsigned short*>(Wp), ldw, wplane, nullptr, c1, c2, nullptr, 0, C, ldc, M,
+                N, K, epi & ~(EPI_BIAS | EPI_RESID), eps, true, stream);
+}

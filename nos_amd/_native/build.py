@@ -29,7 +29,7 @@ BUILD = REPO / "build" / "native"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("NOS_AMD_ARCH", "gfx950")
 
-HIP_SOURCES = ["attention.hip", "attention_f32.hip", "gemm_f32.hip", "gemm.hip", "layernorm.hip", "probes.hip", "runtime.hip"]
+HIP_SOURCES = ["attention.hip", "attention_f32.hip", "attention_f32x.hip", "gemm_f32.hip", "gemm_f32x.hip", "gemm.hip", "layernorm.hip", "probes.hip", "runtime.hip"]
 HIP_LIB = HERE / "libnos_hip.so"
 SMI_LIB = HERE / "libnos_amdsmi.so"
 

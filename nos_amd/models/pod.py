@@ -135,16 +135,25 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
     CUs of its own, persistent grids) plans for its own CUs: budget-aware
     latency tiles and the auto attention rule, which picks the register-capped
     32-key tiling (4 waves per SIMD) -- 7 exclusive 32-CU pods 217.6 -> 231.0
-    inf/s, solo 29.0 -> 27.2 ms (profiles/r03_cumask_kernel_configs.json)."""
+    inf/s, solo 29.0 -> 27.2 ms (profiles/r03_cumask_kernel_configs.json).
+
+    fp32 math: every pod runs the bf16x6 split kernels (fp32 operands as three
+    exact bf16 pieces, six piece products on the bf16 matrix pipes; error vs
+    fp64 <= the exact-f32 MFMA's, tests/test_kernels_gpu.py): attention
+    (attention_f32x.hip) for every slice kind -- 8-pod fleet 318 -> 407 inf/s
+    -- and the GEMMs (gemm_f32x.hip) -> 415 inf/s
+    (profiles/r03_f32x6_fleet_ab.json).  ``NOS_AMD_F32_MATH=exact`` /
+    ``NOS_AMD_ATTN_F32_VARIANT=<tiling>`` select the exact-f32 MFMA kernels."""
     env = os.environ if env is None else env
     whole = memory_fraction is None or memory_fraction >= 0.99
     if cu_budget and not whole:
-        gf, att = "latency", "auto"
+        gf = "latency"
     else:
-        gf, att = ("latency", "auto") if whole else ("small", "w4k32")
+        gf = "latency" if whole else "small"
     return {"gemm_bf16": env.get("NOS_AMD_GEMM_POLICY") or ("latency" if whole else "throughput"),
             "gemm_f32": env.get("NOS_AMD_GEMM_F32_POLICY") or gf,
-            "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or att}
+            "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or "x6",
+            "f32_math": env.get("NOS_AMD_F32_MATH") or "x6"}
 
 
 def slice_cu_budget(env: dict | None = None) -> int:
@@ -193,13 +202,15 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             torch.cuda.set_device(0)  # the device plugin's HIP_VISIBLE_DEVICES leaves exactly the slice's GPU
             frac = apply_memory_limit(0)
             torch.backends.cuda.matmul.allow_tf32 = False  # true fp32 GEMMs (no reduced-precision shortcut)
-            from ..ops import set_attention_f32_variant, set_cu_budget, set_gemm_f32_policy, set_gemm_policy
+            from ..ops import (set_attention_f32_variant, set_cu_budget, set_f32_math, set_gemm_f32_policy,
+                               set_gemm_policy)
 
             budget = slice_cu_budget(os.environ)
             cfg = kernel_config(frac, os.environ, budget)
             set_gemm_policy(cfg["gemm_bf16"])
             set_gemm_f32_policy(cfg["gemm_f32"])
             set_attention_f32_variant(cfg["attention_f32"])
+            set_f32_math(cfg["f32_math"])
             if budget:  # CU-mask slice: slice-sized persistent grids (ops.set_cu_budget)
                 set_cu_budget(budget)
         m, x = _build(dtype, seed, demo_input_hw(), device)
@@ -220,6 +231,7 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
                 "multiprocessor_count": props.multi_processor_count if gpu else 0,
                 "cu_mask": os.environ.get("ROC_GLOBAL_CU_MASK"),
                 "cu_budget": slice_cu_budget(os.environ) if gpu else 0,
+                "kernel_config": cfg if gpu else None,
                 "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES"),
                 "memory_limit_gb": os.environ.get("NOS_AMD_MEMORY_LIMIT_GB"),
                 "max_allocated_gb": None}

@@ -123,7 +123,9 @@ def _gemm_io(x: torch.Tensor, weight: torch.Tensor, out: torch.Tensor | None, re
 
 
 def _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K):
-    """Exact-fp32 MFMA GEMM (csrc/hip/gemm_f32.hip) with fused bias/act/residual."""
+    """fp32 GEMM with fused bias/act/residual: the exact-f32 MFMA kernel
+    (csrc/hip/gemm_f32.hip) or, under ``set_f32_math("x6")``, the bf16x6 split
+    kernel (gemm_f32x.hip) on the weight's cached bf16 planes."""
     _check_f32(x=x2, weight=weight, bias=bias)
     if K % 32:
         raise ValueError("native fp32 linear needs K % 32 == 0")
@@ -131,11 +133,70 @@ def _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K):
         raise ValueError("bias must be contiguous")
     o2, r2 = _gemm_io(x, weight, out, residual, M, N, K)
     _check_f32(residual=r2)
-    rc = _lib.lib().nos_gemm_f32(x2.data_ptr(), x2.stride(0), weight.data_ptr(), weight.stride(0), _ptr(bias),
-                                 _ptr(r2), r2.stride(0) if r2 is not None else 0, o2.data_ptr(), o2.stride(0),
-                                 M, N, K, _epi(bias, act, residual), _stream())
-    _lib.check(rc, "nos_gemm_f32")
+    ldr = r2.stride(0) if r2 is not None else 0
+    if _F32_MATH == "x6":
+        wp = split_f32_weight(weight)
+        rc = _lib.lib().nos_gemm_f32x6(x2.data_ptr(), x2.stride(0), wp.data_ptr(), wp.stride(1), wp.stride(0),
+                                       _ptr(bias), _ptr(r2), ldr, o2.data_ptr(), o2.stride(0), M, N, K,
+                                       _epi(bias, act, residual), _stream())
+        _lib.check(rc, "nos_gemm_f32x6")
+    else:
+        rc = _lib.lib().nos_gemm_f32(x2.data_ptr(), x2.stride(0), weight.data_ptr(), weight.stride(0), _ptr(bias),
+                                     _ptr(r2), ldr, o2.data_ptr(), o2.stride(0), M, N, K, _epi(bias, act, residual),
+                                     _stream())
+        _lib.check(rc, "nos_gemm_f32")
     return o2.view(*x.shape[:-1], N)
+
+
+_F32_MATH = "exact"
+_SPLIT_CACHE: dict[int, tuple] = {}
+
+
+def set_f32_math(mode: str) -> None:
+    """How fp32 GEMMs use the matrix pipes: ``"exact"`` -- the f32-input MFMA
+    (v_mfma_f32_32x32x2_f32, an fmaf chain, 1/16 of the bf16 rate) -- or
+    ``"x6"`` -- every operand split into three bf16 pieces (exact: 3 x 8
+    mantissa bits) and the six piece products of order >= 2^-16 summed by
+    bf16 MFMAs in fp32 (csrc/hip/split_bf16.h): the same accuracy against fp64
+    (tests/test_kernels_gpu.py) at 6/16 of the matrix-pipe time.  The fp32
+    attention has its own switch (``set_attention_f32_variant("x6")``)."""
+    global _F32_MATH
+    if mode not in ("exact", "x6"):
+        raise ValueError(f"f32 math must be 'exact' or 'x6', got {mode!r}")
+    _F32_MATH = mode
+
+
+def f32_math() -> str:
+    return _F32_MATH
+
+
+def split_bf16x3(t: torch.Tensor) -> torch.Tensor:
+    """fp32 tensor -> [3, *t.shape] bf16 pieces with t == p0 + p1 + p2 exactly."""
+    t = t.float()
+    p0 = t.to(torch.bfloat16)
+    r = t - p0.float()
+    p1 = r.to(torch.bfloat16)
+    p2 = (r - p1.float()).to(torch.bfloat16)
+    return torch.stack([p0, p1, p2]).contiguous()
+
+
+@torch.no_grad()
+def split_f32_weight(w: torch.Tensor) -> torch.Tensor:
+    """The bf16x3 planes [3, N, K] of an fp32 weight, cached per tensor and
+    version (a weight is split once; the first forward, before any graph
+    capture, fills the cache)."""
+    key = id(w)
+    hit = _SPLIT_CACHE.get(key)
+    if hit is not None:
+        ref, ver, ptr, planes = hit
+        if ref() is w and ver == w._version and ptr == w.data_ptr():
+            return planes
+    import weakref
+
+    planes = split_bf16x3(w)
+    _SPLIT_CACHE[key] = (weakref.ref(w, lambda _r, k=key: _SPLIT_CACHE.pop(k, None)), w._version, w.data_ptr(),
+                         planes)
+    return planes
 
 
 def set_gemm_policy(policy: str) -> None:
@@ -185,9 +246,21 @@ def set_attention_f32_variant(variant: str) -> None:
     interleaved key tiles, merged at the end: 2 waves per SIMD from one
     workgroup); A/B tilings: ``"w4k32"`` (32-key tiles, half the LDS),
     ``"w2k64"`` (64-query blocks), ``"w8k64"`` (256-query blocks), ``"w4k32o4"`` (32-key tiles in 127
-    VGPRs: 4 waves per SIMD), ``"w4k32g2"`` (two groups on 32-key tiles)."""
-    code = {"auto": 0, "w4k64": 1, "w4k64g2": 2, "w4k32": 3, "w2k64": 4, "w8k64": 5, "w4k32o4": 6, "w4k32g2": 7}[variant]
+    VGPRs: 4 waves per SIMD), ``"w4k32g2"`` (two groups on 32-key tiles); ``"x6"``: the bf16x6 split
+    kernel (attention_f32x.hip: fp32 operands as three bf16 pieces, six
+    exact piece products per product on the bf16 matrix pipes)."""
+    global _ATTN_F32_VARIANT
+    code = {"auto": 0, "w4k64": 1, "w4k64g2": 2, "w4k32": 3, "w2k64": 4, "w8k64": 5, "w4k32o4": 6, "w4k32g2": 7,
+            "x6": 0}[variant]
     _lib.check(_lib.lib().nos_attn_f32_set_variant(code), "nos_attn_f32_set_variant")
+    _ATTN_F32_VARIANT = variant
+
+
+_ATTN_F32_VARIANT = "auto"
+
+
+def attention_f32_variant() -> str:
+    return _ATTN_F32_VARIANT
 
 
 @torch.no_grad()
@@ -233,10 +306,17 @@ def linear_ln(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Ten
         if K % 32:
             raise ValueError("native fp32 linear_ln needs K % 32 == 0")
         o2, _ = _gemm_io(x, wg, out, None, M, N, K)
-        rc = _lib.lib().nos_gemm_ln_f32(x2.data_ptr(), x2.stride(0), wg.data_ptr(), wg.stride(0), c1.data_ptr(),
-                                        c2.data_ptr(), o2.data_ptr(), o2.stride(0), M, N, K, _epi(None, act, None),
-                                        float(eps), _stream())
-        _lib.check(rc, "nos_gemm_ln_f32")
+        if _F32_MATH == "x6":
+            wp = split_f32_weight(wg)
+            rc = _lib.lib().nos_gemm_ln_f32x6(x2.data_ptr(), x2.stride(0), wp.data_ptr(), wp.stride(1), wp.stride(0),
+                                              c1.data_ptr(), c2.data_ptr(), o2.data_ptr(), o2.stride(0), M, N, K,
+                                              _epi(None, act, None), float(eps), _stream())
+            _lib.check(rc, "nos_gemm_ln_f32x6")
+        else:
+            rc = _lib.lib().nos_gemm_ln_f32(x2.data_ptr(), x2.stride(0), wg.data_ptr(), wg.stride(0), c1.data_ptr(),
+                                            c2.data_ptr(), o2.data_ptr(), o2.stride(0), M, N, K,
+                                            _epi(None, act, None), float(eps), _stream())
+            _lib.check(rc, "nos_gemm_ln_f32")
         return o2.view(*x.shape[:-1], N)
     if x2.stride(-1) != 1 or K % 64 or x.dtype != torch.bfloat16:
         raise ValueError("native linear_ln needs bf16, unit inner stride and K % 64 == 0")
@@ -310,11 +390,18 @@ def attention_qkv(qkv: torch.Tensor, num_heads: int, out: torch.Tensor | None = 
     hd = num_heads * D
     base = qkv.data_ptr()
     es = qkv.element_size()
-    fn, name = ((_lib.lib().nos_attn_fwd_f32_d64, "nos_attn_fwd_f32_d64") if qkv.dtype == torch.float32
-                else (_lib.lib().nos_attn_fwd_d64, "nos_attn_fwd_d64"))
-    rc = fn(base, base + hd * es, base + 2 * hd * es, out.data_ptr(), B, num_heads, S, S, qkv.stride(1),
-            qkv.stride(0), out.stride(1), out.stride(0), float(scale), _stream())
-    _lib.check(rc, name)
+    L = _lib.lib()
+    args = (base, base + hd * es, base + 2 * hd * es, out.data_ptr(), B, num_heads, S, S, qkv.stride(1),
+            qkv.stride(0), out.stride(1), out.stride(0), float(scale))
+    if qkv.dtype == torch.float32 and _ATTN_F32_VARIANT == "x6":
+        # the split K/V planes: a stream-ordered allocation (graph-capture safe)
+        nbytes = int(L.nos_attn_f32x6_workspace(B, num_heads, S))
+        ws = torch.empty(nbytes // 2, dtype=torch.int16, device=qkv.device)
+        _lib.check(L.nos_attn_fwd_f32x6_d64(*args, ws.data_ptr(), nbytes, _stream()), "nos_attn_fwd_f32x6_d64")
+        return out
+    fn, name = ((L.nos_attn_fwd_f32_d64, "nos_attn_fwd_f32_d64") if qkv.dtype == torch.float32
+                else (L.nos_attn_fwd_d64, "nos_attn_fwd_d64"))
+    _lib.check(fn(*args, _stream()), name)
     return out
 
 
@@ -342,5 +429,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_f32_math", "f32_math", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

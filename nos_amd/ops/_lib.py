@@ -28,12 +28,20 @@ _SIGS = {
                          c_ll, c_int, c_ll, c_float, c_void_p],
     "nos_attn_fwd_f32_d64": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                              c_ll, c_int, c_ll, c_float, c_void_p],
+    "nos_attn_fwd_f32x6_d64": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                               c_ll, c_int, c_ll, c_float, c_void_p, c_ll, c_void_p],
+    "nos_attn_f32x6_workspace": [c_int, c_int, c_int],
     "nos_gemm_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nos_gemm_f32": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
                      c_int, c_int, c_void_p],
     "nos_gemm_ln_f32": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                         c_int, c_float, c_void_p],
+    "nos_gemm_f32x6": [c_void_p, c_int, c_void_p, c_int, c_ll, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int,
+                       c_int, c_int, c_int, c_void_p],
+    "nos_gemm_ln_f32x6": [c_void_p, c_int, c_void_p, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                          c_int, c_int, c_float, c_void_p],
+    "nos_gemm_f32_pick_tile": [c_int, c_int],
     "nos_gemm_set_policy": [c_int],
     "nos_gemm_set_persistent": [c_int],
     "nos_gemm_f32_set_policy": [c_int],
@@ -61,6 +69,9 @@ _SIGS = {
 }
 
 
+_RESTYPES = {"nos_attn_f32x6_workspace": c_ll}
+
+
 class NativeUnavailable(RuntimeError):
     pass
 
@@ -79,7 +90,7 @@ def _load() -> ctypes.CDLL:
     for name, argtypes in _SIGS.items():
         fn = getattr(L, name)
         fn.argtypes = argtypes
-        fn.restype = c_int
+        fn.restype = _RESTYPES.get(name, c_int)
     return L
 
 

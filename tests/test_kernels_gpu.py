@@ -133,7 +133,7 @@ def test_attention_strided_views():
     assert out[..., hid:].abs().max().item() == 0  # padding untouched
 
 
-@pytest.mark.parametrize("variant", ["w4k64", "w4k64g2", "w4k32", "w4k32o4", "w4k32g2", "w2k64", "w8k64", "auto"])
+@pytest.mark.parametrize("variant", ["w4k64", "w4k64g2", "w4k32", "w4k32o4", "w4k32g2", "w2k64", "w8k64", "x6", "auto"])
 @pytest.mark.parametrize("B,S,H", [(1, 3401, 6), (2, 77, 3), (1, 1, 1), (1, 33, 2), (3, 300, 2), (1, 129, 1)])
 def test_attention_fp32_exact(B, S, H, variant):
     """fp32 MFMA attention against an fp64 reference: exact-f32 numerics."""
@@ -151,6 +151,52 @@ def test_attention_fp32_exact(B, S, H, variant):
     assert err < 2e-5 * max(1.0, ref.abs().max().item()), err
 
 
+@pytest.mark.parametrize("scale_in", [1.0, 4.0])
+def test_attention_fp32_split_is_as_accurate_as_exact_f32(scale_in):
+    """The bf16x6 split kernel (three bf16 pieces per fp32 operand, six exact
+    piece products) against fp64, next to the exact-f32 MFMA kernel on the
+    same inputs: its error may not exceed the exact kernel's by more than 50 %
+    (mean and max), at YOLOS-small's shape, plain and with logits ~ +-100."""
+    torch.manual_seed(3)
+    B, S, H = 1, 3401, 6
+    qkv = torch.randn(B, S, 3 * H * 64, device=DEV) * scale_in
+    q, k, v = qkv.cpu().double().view(B, S, 3, H, 64).unbind(2)
+    p = torch.softmax((q.transpose(1, 2) @ k.transpose(1, 2).transpose(-1, -2)) / 8.0, dim=-1)
+    ref = (p @ v.transpose(1, 2)).transpose(1, 2).reshape(B, S, H * 64)
+    errs = {}
+    for variant in ("w4k32o4", "x6"):
+        ops.set_attention_f32_variant(variant)
+        try:
+            y = ops.attention_qkv(qkv, H)
+        finally:
+            ops.set_attention_f32_variant("auto")
+        e = (y.cpu().double() - ref).abs()
+        errs[variant] = (e.max().item(), e.mean().item())
+    print("attention fp32 error vs fp64 (max, mean):", errs)
+    assert errs["x6"][0] <= 1.5 * errs["w4k32o4"][0] + 1e-7, errs
+    assert errs["x6"][1] <= 1.5 * errs["w4k32o4"][1], errs
+
+
+@pytest.mark.parametrize("M,N,K", [(3401, 1152, 384), (3401, 384, 1536)])
+def test_linear_fp32_split_is_as_accurate_as_exact_f32(M, N, K):
+    """bf16x6 split GEMM vs the exact-f32 MFMA GEMM, both against fp64 on the
+    same inputs: max and mean error within 1.5x of the exact kernel's."""
+    torch.manual_seed(5)
+    x = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV) * 0.05
+    ref = x.cpu().double() @ w.cpu().double().t()
+    errs = {}
+    for m in ("exact", "x6"):
+        ops.set_f32_math(m)
+        try:
+            e = (ops.linear(x, w).cpu().double() - ref).abs()
+        finally:
+            ops.set_f32_math("exact")
+        errs[m] = (e.max().item(), e.mean().item())
+    print("linear fp32 error vs fp64 (max, mean):", errs)
+    assert errs["x6"][0] <= 1.5 * errs["exact"][0] and errs["x6"][1] <= 1.5 * errs["exact"][1], errs
+
+
 def test_attention_fp32_strided_and_large_logits():
     B, S, H = 2, 129, 6
     base = torch.randn(B, S, 3 * H * 64 + 64, device=DEV) * 4.0  # padded rows: ld != 3*H*64, logits ~ +-100
@@ -166,17 +212,21 @@ def test_attention_fp32_strided_and_large_logits():
     (3401, 384, 384, None, True), (100, 92, 384, "relu", False), (100, 4, 384, None, False), (257, 200, 96, None, True),
     (8 * 3401, 384, 1536, None, True), (1, 8, 32, None, False), (3401, 100, 384, None, False)])
 @pytest.mark.parametrize("policy", ["throughput", "latency", "small"])
-def test_linear_fp32_exact(M, N, K, act, resid, policy):
-    """fp32 MFMA GEMM against an fp64 reference (exact-f32 tolerance), every tile shape."""
+@pytest.mark.parametrize("math_", ["exact", "x6"])
+def test_linear_fp32_exact(M, N, K, act, resid, policy, math_):
+    """fp32 GEMM (exact-f32 MFMA, and the bf16x6 split) against an fp64
+    reference at the exact-f32 tolerance, every tile shape."""
     x = torch.randn(M, K, device=DEV)
     w = torch.randn(N, K, device=DEV) * 0.05
     b = torch.randn(N, device=DEV)
     r = torch.randn(M, N, device=DEV) if resid else None
     ops.set_gemm_f32_policy(policy)
+    ops.set_f32_math(math_)
     try:
         y = ops.linear(x, w, b, act=act, residual=r)
     finally:
         ops.set_gemm_f32_policy("latency")
+        ops.set_f32_math("exact")
     ref = x.cpu().double() @ w.cpu().double().t() + b.cpu().double()
     if act == "gelu":
         ref = torch.nn.functional.gelu(ref)
@@ -191,14 +241,19 @@ def test_linear_fp32_exact(M, N, K, act, resid, policy):
 
 @pytest.mark.parametrize("M,N,K,act", [(3401, 1152, 384, None), (3401, 1536, 384, "gelu"), (77, 100, 384, None),
                                        (1, 64, 64, None), (300, 384, 384, None)])
-def test_linear_layernorm_fused_fp32(M, N, K, act):
+@pytest.mark.parametrize("math_", ["exact", "x6"])
+def test_linear_layernorm_fused_fp32(M, N, K, act, math_):
     x = torch.randn(M, K, device=DEV) * 2 + 0.5
     w = torch.randn(N, K, device=DEV) * 0.05
     b = torch.randn(N, device=DEV)
     g = torch.randn(K, device=DEV)
     be = torch.randn(K, device=DEV)
     wg, c1, c2 = ops.fold_layernorm(w, b, g, be)
-    y = ops.linear_ln(x, wg, c1, c2, act=act, eps=1e-12)
+    ops.set_f32_math(math_)
+    try:
+        y = ops.linear_ln(x, wg, c1, c2, act=act, eps=1e-12)
+    finally:
+        ops.set_f32_math("exact")
     xd = x.cpu().double()
     ln = torch.nn.functional.layer_norm(xd, (K,), g.cpu().double(), be.cpu().double(), 1e-12)
     ref = ln @ w.cpu().double().t() + b.cpu().double()
@@ -330,11 +385,14 @@ def test_slice_sized_persistent_grids_are_bit_identical(budget):
 
     def run():
         outs = []
-        for pol in ("small", "latency"):
-            ops.set_gemm_f32_policy(pol)
-            outs += [ops.linear(x, w, b, act="gelu", residual=r), ops.linear_ln(x, wg, c1, c2, act="gelu")]
+        for m in ("exact", "x6"):
+            ops.set_f32_math(m)
+            for pol in ("small", "latency", "throughput"):
+                ops.set_gemm_f32_policy(pol)
+                outs += [ops.linear(x, w, b, act="gelu", residual=r), ops.linear_ln(x, wg, c1, c2, act="gelu")]
+        ops.set_f32_math("exact")
         ops.set_gemm_f32_policy("latency")
-        for var in ("w4k32", "w4k64g2", "w4k32o4"):
+        for var in ("w4k32", "w4k64g2", "w4k32o4", "x6"):
             ops.set_attention_f32_variant(var)
             outs.append(ops.attention_qkv(qkv, 6))
         ops.set_attention_f32_variant("auto")

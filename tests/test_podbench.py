@@ -137,20 +137,22 @@ def test_pod_kernel_config_follows_the_slice():
     from nos_amd.models.pod import kernel_config
 
     whole = kernel_config(None, {})
-    assert whole == {"gemm_bf16": "latency", "gemm_f32": "latency", "attention_f32": "auto"}
+    assert whole == {"gemm_bf16": "latency", "gemm_f32": "latency", "attention_f32": "x6", "f32_math": "x6"}
     assert kernel_config(1.0, {}) == whole
     frac = kernel_config(36 / 288, {})
-    assert frac == {"gemm_bf16": "throughput", "gemm_f32": "small", "attention_f32": "w4k32"}
-    # an exclusive CU-mask slice plans for its own CUs (budget-aware tiles, auto attention)
+    assert frac == {"gemm_bf16": "throughput", "gemm_f32": "small", "attention_f32": "x6", "f32_math": "x6"}
+    # an exclusive CU-mask slice plans for its own CUs (budget-aware tiles)
     assert kernel_config(36 / 288, {}, cu_budget=32) == {"gemm_bf16": "throughput", "gemm_f32": "latency",
-                                                         "attention_f32": "auto"}
+                                                         "attention_f32": "x6", "f32_math": "x6"}
     assert kernel_config(None, {}, cu_budget=32) == whole
-    # A/B overrides win over the slice rule
+    # A/B overrides win over the slice rule: the exact-f32 MFMA kernels stay selectable
     assert kernel_config(0.125, {"NOS_AMD_ATTN_F32_VARIANT": "w4k64"})["attention_f32"] == "w4k64"
+    assert kernel_config(0.125, {"NOS_AMD_F32_MATH": "exact"})["f32_math"] == "exact"
     # every name is one the native library accepts
     from nos_amd import ops
     import inspect
 
-    src = inspect.getsource(ops.set_attention_f32_variant) + inspect.getsource(ops.set_gemm_f32_policy)
+    src = (inspect.getsource(ops.set_attention_f32_variant) + inspect.getsource(ops.set_gemm_f32_policy)
+           + inspect.getsource(ops.set_f32_math))
     for v in (*whole.values(), *frac.values()):
         assert f'"{v}"' in src or v in ("latency", "throughput")

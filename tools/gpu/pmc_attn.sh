@@ -11,7 +11,8 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 i=0
 for CNT in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_MFMA" \
-           "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_WAVES"; do
+           "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_WAVES" \
+           "TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum SQ_WAIT_INST_ANY SQ_INSTS_VMEM GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $CNT --output-format csv -d $OUT/pass$i -o run -- python3 $R/tools/attn_once.py --B $B --variant $V --dtypes $DT > $OUT/pass$i.log 2>&1 || exit 1
 done

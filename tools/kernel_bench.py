@@ -53,7 +53,9 @@ def main():
     ap.add_argument("--persist", default="0", help="comma list of bf16 GEMM persistent grids (workgroups/CU, 0 = off)")
     ap.add_argument("--policies", default="latency", help="comma list of GEMM tile policies to A/B "
                     "(throughput, latency)")
+    ap.add_argument("--f32-math", default="exact", choices=["exact", "x6"], help="fp32 GEMM math (ops.set_f32_math)")
     a = ap.parse_args()
+    ops.set_f32_math(a.f32_math)
     torch.manual_seed(0)
     S, H, hid, mlp = 3401, 6, 384, 1536
     B = a.batch
