@@ -62,7 +62,7 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_ba
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-template <bool PERSIST>
+template <bool PERSIST, int SPREAD>
 __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
     const float* __restrict__ q, const unsigned short* __restrict__ kvs, float* __restrict__ o, int B, int H, int Sq,
     int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, int nqb) {
@@ -138,15 +138,12 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
     // The planes are padded to whole tiles with zeros: a tile's address is a
     // wave-uniform base plus the hoisted per-lane offsets.
     const unsigned short* pb = kvs + (long long)b * skvp * (6 * ldh) + hd * D;
-    auto stage = [&](int t, int buf) {
-      const unsigned short* tb = pb + (long long)t * (KVB * 6) * ldh;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const int p = wid * 6 + i;
-        glds16(tb + soff[i], smem + buf * STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
-      }
+    auto stage_piece = [&](int t, int buf, int i) {
+      const int p = wid * 6 + i;
+      glds16(pb + (long long)t * (KVB * 6) * ldh + soff[i], smem + buf * STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
     };
-    stage(0, 0);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) stage_piece(0, 0, i);
 
     f32x16_t oacc[2];
 #pragma unroll
@@ -161,7 +158,13 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
     for (int t = 0; t < ntiles; ++t) {
       const int buf = t & 1;
       const bool more = t + 1 < ntiles;
-      if (more) stage(t + 1, buf ^ 1);  // that buffer was released by the barrier ending t-1
+      // the next tile's 6 DMA pieces (into the buffer released by the barrier
+      // ending t-1): all up front (SPREAD 0), or spread between the QK^T (1)
+      // or the PV (2) MFMA groups so their issue cost overlaps this wave's MFMAs
+      if (SPREAD == 0 && more) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) stage_piece(t + 1, buf ^ 1, i);
+      }
       const unsigned char* kl = smem + buf * STAGE;
       const unsigned char* vl = kl + 3 * IMG;
 
@@ -174,6 +177,12 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
 #pragma unroll
         for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8_t*>(kl + p * IMG + koff[ks]);
         s = nos::mma6(a, qf[ks], s);
+        if (SPREAD == 1 && more) {
+          __builtin_amdgcn_sched_barrier(0);
+          stage_piece(t + 1, buf ^ 1, ks < 2 ? 2 * ks : ks + 2);
+          if (ks < 2) stage_piece(t + 1, buf ^ 1, 2 * ks + 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       if ((t + 1) * KVB > Skv) {  // tail tile: keys past Skv never contribute
 #pragma unroll
@@ -228,6 +237,13 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
             a[p] = __builtin_bit_cast(bf16x8_t, a16);
           }
           oacc[db] = nos::mma6(a, pf[s2], oacc[db]);
+          if (SPREAD == 2 && more) {
+            const int g = 2 * db + s2;
+            __builtin_amdgcn_sched_barrier(0);
+            stage_piece(t + 1, buf ^ 1, g < 2 ? 2 * g : g + 2);
+            if (g < 2) stage_piece(t + 1, buf ^ 1, 2 * g + 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
       __syncthreads();  // next tile landed (vmcnt(0)); every wave is done with `buf`
     }
@@ -280,7 +296,28 @@ __global__ __launch_bounds__(256) void split_kv_kernel(const float* __restrict__
   for (int j = 0; j < 3; ++j) *reinterpret_cast<bf16x8_t*>(dst + j * H * D) = p[j];
 }
 
+template <int SPREAD>
+int launch(const float* q, const unsigned short* kvs, float* o, int B, int H, int Sq, int Skv, int ld_in,
+           long long bs_in, int ld_out, long long bs_out, float c, int nqb, long long nwg, hipStream_t stream) {
+  const int grid = nos_grid_for((const void*)attn_fwd_f32x6_d64_kernel<true, SPREAD>, NT, LDS_BYTES, nwg);
+  if (grid < nwg)
+    hipLaunchKernelGGL((attn_fwd_f32x6_d64_kernel<true, SPREAD>), dim3((unsigned)grid), dim3(NT), LDS_BYTES, stream,
+                       q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
+  else
+    hipLaunchKernelGGL((attn_fwd_f32x6_d64_kernel<false, SPREAD>), dim3((unsigned)nwg), dim3(NT), LDS_BYTES, stream,
+                       q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
+  return (int)hipGetLastError();
+}
+
+int g_spread = 0;
+
 }  // namespace
+
+NOS_API int nos_attn_f32x6_set_spread(int spread) {
+  if (spread < 0 || spread > 2) return (int)hipErrorInvalidValue;
+  g_spread = spread;
+  return 0;
+}
 
 // Workspace bytes of nos_attn_fwd_f32x6_d64 (the split K/V planes).
 NOS_API long long nos_attn_f32x6_workspace(int B, int H, int Skv) {
@@ -308,12 +345,7 @@ NOS_API int nos_attn_fwd_f32x6_d64(const float* q, const float* k, const float* 
   auto* kvs = static_cast<unsigned short*>(ws);
   hipLaunchKernelGGL(split_kv_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, stream, k, v, kvs, Skv, skvp,
                      H, ld_in, bs_in, (int)n8);
-  const int grid = nos_grid_for((const void*)attn_fwd_f32x6_d64_kernel<true>, NT, LDS_BYTES, nwg);
-  if (grid < nwg)
-    hipLaunchKernelGGL(attn_fwd_f32x6_d64_kernel<true>, dim3((unsigned)grid), dim3(NT), LDS_BYTES, stream, q, kvs,
-                       o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
-  else
-    hipLaunchKernelGGL(attn_fwd_f32x6_d64_kernel<false>, dim3((unsigned)nwg), dim3(NT), LDS_BYTES, stream, q, kvs,
-                       o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
-  return (int)hipGetLastError();
+  if (g_spread == 1) return launch<1>(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb, nwg, stream);
+  if (g_spread == 2) return launch<2>(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb, nwg, stream);
+  return launch<0>(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb, nwg, stream);
 }

@@ -13,10 +13,11 @@
 //  * 4 waves (2 x 2) per workgroup, tiles 128x128 / 64x128 / 64x64 chosen by
 //    the fp32 GEMM's tile policy (nos_gemm_f32_pick_tile), each wave (BM/2) x
 //    (BN/2) as 32x32 blocks, BK = 32 per stage = two 16-deep MFMA steps;
-//  * LDS-DMA (global_load_lds_dwordx4) into a 2-deep ring: the A tile as fp32
-//    rows of 128 B (chunks XOR-swizzled by row & 7), the three W planes as
-//    rows of 64 B (chunks swizzled by (row >> 2) & 3) -- both conflict-free
-//    for the fragment reads; one barrier per stage;
+//  * LDS-DMA (global_load_lds_dwordx4) into an S-deep ring: the A tile as
+//    fp32 rows of 128 B (chunks XOR-swizzled by row & 7), the three W planes
+//    as rows of 64 B (chunks swizzled by (row >> 2) & 3) -- both conflict-free
+//    for the fragment reads; one raw s_barrier per stage behind a COUNTED
+//    vmcnt (S-2 later stages may stay in flight across it);
 //  * a wave splits its A fragments in registers (the K-contiguous 8 floats
 //    of a 16-deep step are exactly one bf16x8 operand) and issues six
 //    v_mfma_f32_32x32x16_bf16 per 32x32 block and step;
@@ -50,6 +51,30 @@ __device__ __forceinline__ float erf_fast(float x) {  // Abramowitz-Stegun 7.1.2
   return copysignf(r, x);
 }
 
+// s_waitcnt vmcnt(n * LPS) for a runtime n in [0, 3] (the immediate must be a constant)
+template <int LPS>
+__device__ __forceinline__ void wait_stages(int n) {
+  if (n <= 0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (n == 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+  else if (n == 2)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPS) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LPS) : "memory");
+}
+
+template <int BM, int BN>
+struct Ring {
+  // stages in the ring: 3 for 64x64 measured slower than 2 (LDS for 2 instead
+  // of 3 workgroups per CU outweighs the deeper prefetch: fc2 71.5 -> 68.8 TF
+  // at batch 1, qkv 104 -> 80 at batch 8)
+  static constexpr int S = 2;
+  static constexpr int LPS = BM / 32 + 3 * BN / 64;         // DMA instructions per wave per stage
+  static_assert((BM / 8) % 4 == 0 && (3 * BN / 16) % 4 == 0, "every wave issues the same DMA count");
+  static_assert(S >= 2 && S <= 4 && (S - 1) * LPS < 64, "ring depth / vmcnt range");
+};
+
 template <bool LN, int BM, int BN, bool PERSIST>
 __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
     const float* __restrict__ A, int lda, const unsigned short* __restrict__ Wp, int ldw, long long wplane,
@@ -58,8 +83,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
     int tiles_m, int tiles_n) {
   constexpr int TA = BM * AROW, TWP = BN * WROW, STAGE = TA + 3 * TWP;
   constexpr int MI = BM / 64, NI = BN / 64;  // 32x32 blocks per wave (waves are 2 x 2)
+  constexpr int S = Ring<BM, BN>::S, LPS = Ring<BM, BN>::LPS;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* s_mu = reinterpret_cast<float*>(smem + 2 * STAGE);
+  float* s_mu = reinterpret_cast<float*>(smem + S * STAGE);
   float* s_rstd = s_mu + BM;
 
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -114,12 +140,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
   const int srow = tid / TPR, spart = tid % TPR;
   float sshift = 0.f, ssum = 0.f, ssq = 0.f;
 
-  stage(0, smem);
-  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < S; ++q)
+    if (q < nk) stage(q * BK, smem + q * STAGE);
 
   for (int kt = 0; kt < nk; ++kt) {
-    const unsigned char* cur = smem + (kt & 1) * STAGE;
-    if (kt + 1 < nk) stage((kt + 1) * BK, smem + ((kt + 1) & 1) * STAGE);  // released by the barrier ending kt-1
+    // slice kt landed (the newer slices issued so far stay in flight: S-1 of
+    // them after the prologue, S-2 later) and every wave is done with slice
+    // kt-1, whose buffer slice kt+S-1 reuses
+    wait_stages<LPS>(min(kt == 0 ? S - 1 : S - 2, nk - 1 - kt));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt > 0 && kt + S - 1 < nk) stage((kt + S - 1) * BK, smem + ((kt + S - 1) % S) * STAGE);
+    const unsigned char* cur = smem + (kt % S) * STAGE;
     const unsigned char* ta = cur;
     const unsigned char* tw = cur + TA;
     if constexpr (LN) {
@@ -156,8 +189,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
 #pragma unroll
         for (int j = 0; j < NI; ++j) acc[i][j] = nos::mma6(af[i], wf[j], acc[i][j]);
     }
-    __syncthreads();  // next stage landed (vmcnt(0)); every wave is done with this one
   }
+  __syncthreads();  // every wave is done with the ring (the next tile's prologue, the LN statistics)
 
   if constexpr (LN) {
     const float kpart = (float)(K / TPR);
@@ -212,7 +245,7 @@ int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long lo
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const long long ntiles = (long long)tiles_m * tiles_n;
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
-  const size_t lds = 2 * (size_t)(BM * AROW + 3 * BN * WROW) + 2 * BM * sizeof(float);
+  const size_t lds = Ring<BM, BN>::S * (size_t)(BM * AROW + 3 * BN * WROW) + 2 * BM * sizeof(float);
   const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true>, NT, lds, ntiles);
   if (grid < ntiles)
     hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true>), dim3((unsigned)grid), dim3(NT), lds, st, A, lda, Wp,

@@ -251,12 +251,16 @@ def set_attention_f32_variant(variant: str) -> None:
     exact piece products per product on the bf16 matrix pipes)."""
     global _ATTN_F32_VARIANT
     code = {"auto": 0, "w4k64": 1, "w4k64g2": 2, "w4k32": 3, "w2k64": 4, "w8k64": 5, "w4k32o4": 6, "w4k32g2": 7,
-            "x6": 0}[variant]
+            "x6": 0, "x6s0": 0, "x6s1": 0, "x6s2": 0}[variant]
     _lib.check(_lib.lib().nos_attn_f32_set_variant(code), "nos_attn_f32_set_variant")
+    if variant.startswith("x6"):  # x6s<n>: where the x6 kernel issues the next tile's DMA (A/B)
+        _lib.check(_lib.lib().nos_attn_f32x6_set_spread(int(variant[3:] or _X6_SPREAD_DEFAULT)),
+                   "nos_attn_f32x6_set_spread")
     _ATTN_F32_VARIANT = variant
 
 
 _ATTN_F32_VARIANT = "auto"
+_X6_SPREAD_DEFAULT = 0
 
 
 def attention_f32_variant() -> str:
@@ -393,7 +397,7 @@ def attention_qkv(qkv: torch.Tensor, num_heads: int, out: torch.Tensor | None = 
     L = _lib.lib()
     args = (base, base + hd * es, base + 2 * hd * es, out.data_ptr(), B, num_heads, S, S, qkv.stride(1),
             qkv.stride(0), out.stride(1), out.stride(0), float(scale))
-    if qkv.dtype == torch.float32 and _ATTN_F32_VARIANT == "x6":
+    if qkv.dtype == torch.float32 and _ATTN_F32_VARIANT.startswith("x6"):
         # the split K/V planes: a stream-ordered allocation (graph-capture safe)
         nbytes = int(L.nos_attn_f32x6_workspace(B, num_heads, S))
         ws = torch.empty(nbytes // 2, dtype=torch.int16, device=qkv.device)

@@ -18,6 +18,7 @@ def main() -> None:
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--memory-fraction", type=float, default=None, help="as a fractional pod (kernel_config)")
     a = ap.parse_args()
     import torch
 
@@ -25,6 +26,17 @@ def main() -> None:
     from nos_amd.models.yolos import GraphedTenant, demo_input_hw
 
     torch.backends.cuda.matmul.allow_tf32 = False
+    import os
+
+    from nos_amd import ops
+    from nos_amd.models.pod import kernel_config
+
+    cfg = kernel_config(a.memory_fraction, os.environ)  # the pod's kernel choices (NOS_AMD_* overrides apply)
+    ops.set_gemm_policy(cfg["gemm_bf16"])
+    ops.set_gemm_f32_policy(cfg["gemm_f32"])
+    ops.set_attention_f32_variant(cfg["attention_f32"])
+    ops.set_f32_math(cfg["f32_math"])
+    print("kernel config", cfg, flush=True)
     m, x = _build(a.dtype, 0, demo_input_hw())
     s = torch.cuda.Stream()
     t = GraphedTenant(m, s, x)
