@@ -36,8 +36,16 @@ enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
 __device__ __forceinline__ int aswz(int row) { return row & 7; }
 __device__ __forceinline__ int wswz(int row) { return (row >> 2) & 3; }
 
+// LDS-DMA of 16 bytes per lane (lane L -> lds_wave_base + 16 L), issued as
+// inline asm: the compiler then does not know the instruction writes LDS and
+// inserts no vmcnt(0) before the next ds_read (hipcc assumes every ds_read may
+// alias an in-flight LDS-DMA, which drained the NEXT stage's loads before the
+// CURRENT stage's fragment reads -- a full L2/HBM round trip per K step).
+// The explicit counted waits (wait_stages) + barrier provide the ordering.
 __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
 }
 
 __device__ __forceinline__ float erf_fast(float x) {  // Abramowitz-Stegun 7.1.26, |err| <= 1.5e-7
@@ -64,18 +72,15 @@ __device__ __forceinline__ void wait_stages(int n) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LPS) : "memory");
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int S_ = 2>
 struct Ring {
-  // stages in the ring: 3 for 64x64 measured slower than 2 (LDS for 2 instead
-  // of 3 workgroups per CU outweighs the deeper prefetch: fc2 71.5 -> 68.8 TF
-  // at batch 1, qkv 104 -> 80 at batch 8)
-  static constexpr int S = 2;
+  static constexpr int S = S_;  // stages in the ring
   static constexpr int LPS = BM / 32 + 3 * BN / 64;         // DMA instructions per wave per stage
   static_assert((BM / 8) % 4 == 0 && (3 * BN / 16) % 4 == 0, "every wave issues the same DMA count");
   static_assert(S >= 2 && S <= 4 && (S - 1) * LPS < 64, "ring depth / vmcnt range");
 };
 
-template <bool LN, int BM, int BN, bool PERSIST>
+template <bool LN, int BM, int BN, bool PERSIST, int RS>
 __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
     const float* __restrict__ A, int lda, const unsigned short* __restrict__ Wp, int ldw, long long wplane,
     const float* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
@@ -83,7 +88,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
     int tiles_m, int tiles_n) {
   constexpr int TA = BM * AROW, TWP = BN * WROW, STAGE = TA + 3 * TWP;
   constexpr int MI = BM / 64, NI = BN / 64;  // 32x32 blocks per wave (waves are 2 x 2)
-  constexpr int S = Ring<BM, BN>::S, LPS = Ring<BM, BN>::LPS;
+  constexpr int S = Ring<BM, BN, RS>::S, LPS = Ring<BM, BN, RS>::LPS;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* s_mu = reinterpret_cast<float*>(smem + S * STAGE);
   float* s_rstd = s_mu + BM;
@@ -110,14 +115,16 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
   // = 3*BN/16 wave instructions; all spread over the 4 waves
   auto stage = [&](int k0, unsigned char* dst) {
 #pragma unroll
-    for (int p = wid; p < BM / 8; p += 4) {
+    for (int i = 0; i < BM / 32; ++i) {  // A pieces of this wave (unconditional: no branch per piece)
+      const int p = wid * (BM / 32) + i;
       const int row = p * 8 + (lane >> 3);
       int grow = m0 + row;
       grow = grow < M ? grow : M - 1;
       glds16(A + (long long)grow * lda + k0 + (((lane & 7) ^ aswz(row)) << 2), dst + p * 8 * AROW);
     }
 #pragma unroll
-    for (int p = wid; p < 3 * BN / 16; p += 4) {
+    for (int i = 0; i < 3 * BN / 64; ++i) {
+      const int p = wid * (3 * BN / 64) + i;
       const int plane = p / (BN / 16), rb = (p % (BN / 16)) * 16;
       const int row = rb + (lane >> 2);
       int gn = n0 + row;
@@ -151,8 +158,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
     wait_stages<LPS>(min(kt == 0 ? S - 1 : S - 2, nk - 1 - kt));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt > 0 && kt + S - 1 < nk) stage((kt + S - 1) * BK, smem + ((kt + S - 1) % S) * STAGE);
-    const unsigned char* cur = smem + (kt % S) * STAGE;
+    const int slot = S == 2 ? (kt & 1) : kt % S;
+    if (kt > 0 && kt + S - 1 < nk) stage((kt + S - 1) * BK, smem + (S == 2 ? slot ^ 1 : (kt + S - 1) % S) * STAGE);
+    const unsigned char* cur = smem + slot * STAGE;
     const unsigned char* ta = cur;
     const unsigned char* tw = cur + TA;
     if constexpr (LN) {
@@ -238,21 +246,21 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
   }  // tiles
 }
 
-template <bool LN, int BM, int BN>
+template <bool LN, int BM, int BN, int RS>
 int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
              const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K,
              int epi, float eps, hipStream_t st) {
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const long long ntiles = (long long)tiles_m * tiles_n;
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
-  const size_t lds = Ring<BM, BN>::S * (size_t)(BM * AROW + 3 * BN * WROW) + 2 * BM * sizeof(float);
-  const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true>, NT, lds, ntiles);
+  const size_t lds = RS * (size_t)(BM * AROW + 3 * BN * WROW) + 2 * BM * sizeof(float);
+  const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true, RS>, NT, lds, ntiles);
   if (grid < ntiles)
-    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true>), dim3((unsigned)grid), dim3(NT), lds, st, A, lda, Wp,
-                       ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
-  else
-    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false>), dim3((unsigned)ntiles), dim3(NT), lds, st, A, lda,
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true, RS>), dim3((unsigned)grid), dim3(NT), lds, st, A, lda,
                        Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false, RS>), dim3((unsigned)ntiles), dim3(NT), lds, st, A,
+                       lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
   return (int)hipGetLastError();
 }
 
@@ -261,6 +269,8 @@ int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long lo
 NOS_API int nos_gemm_f32_pick_tile(int M, int N);
 
 namespace {
+
+int g_ring = 2;  // LDS ring depth of the 64x64 / 64x128 tiles (nos_gemm_f32x6_set_ring)
 
 int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
            const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi,
@@ -273,20 +283,27 @@ int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long
   if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
   if ((epi & EPI_RESID) && (!R || ldr < N)) return (int)hipErrorInvalidValue;
   const int cfg = nos_gemm_f32_pick_tile(M, N);
-#define NOS_F32X_LAUNCH(LNV, BMV, BNV) \
-  launch_t<LNV, BMV, BNV>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, st)
+#define NOS_F32X_LAUNCH(LNV, BMV, BNV, RSV) \
+  launch_t<LNV, BMV, BNV, RSV>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, st)
+  const bool deep = g_ring == 3;
   if (ln) {
-    if (cfg == 0) return NOS_F32X_LAUNCH(true, 128, 128);
-    if (cfg == 1) return NOS_F32X_LAUNCH(true, 64, 128);
-    return NOS_F32X_LAUNCH(true, 64, 64);
+    if (cfg == 0) return NOS_F32X_LAUNCH(true, 128, 128, 2);
+    if (cfg == 1) return deep ? NOS_F32X_LAUNCH(true, 64, 128, 3) : NOS_F32X_LAUNCH(true, 64, 128, 2);
+    return deep ? NOS_F32X_LAUNCH(true, 64, 64, 3) : NOS_F32X_LAUNCH(true, 64, 64, 2);
   }
-  if (cfg == 0) return NOS_F32X_LAUNCH(false, 128, 128);
-  if (cfg == 1) return NOS_F32X_LAUNCH(false, 64, 128);
-  return NOS_F32X_LAUNCH(false, 64, 64);
+  if (cfg == 0) return NOS_F32X_LAUNCH(false, 128, 128, 2);
+  if (cfg == 1) return deep ? NOS_F32X_LAUNCH(false, 64, 128, 3) : NOS_F32X_LAUNCH(false, 64, 128, 2);
+  return deep ? NOS_F32X_LAUNCH(false, 64, 64, 3) : NOS_F32X_LAUNCH(false, 64, 64, 2);
 #undef NOS_F32X_LAUNCH
 }
 
 }  // namespace
+
+NOS_API int nos_gemm_f32x6_set_ring(int stages) {
+  if (stages != 2 && stages != 3) return (int)hipErrorInvalidValue;
+  g_ring = stages;
+  return 0;
+}
 
 // C = act(A . W^T + bias) (+ R), fp32 A [M,K] (lda), W as three bf16 planes
 // Wp + p * wplane, each [N,K] (ldw); K % 32 == 0, rows 16-byte aligned.
