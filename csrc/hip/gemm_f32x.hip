@@ -27,14 +27,19 @@
 
 namespace {
 
-constexpr int BK = 32;              // k per stage
 constexpr int NT = 256;
-constexpr int AROW = BK * 4;        // fp32 A row per stage: 128 B
-constexpr int WROW = BK * 2;        // bf16 W plane row per stage: 64 B
 enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
 
-__device__ __forceinline__ int aswz(int row) { return row & 7; }
-__device__ __forceinline__ int wswz(int row) { return (row >> 2) & 3; }
+// LDS images of one K stage of BK (32 or 64): the fp32 A rows (AROW bytes,
+// ACH 16-byte chunks) and the bf16 W plane rows (WROW bytes, WCH chunks),
+// chunks XOR-swizzled so 16 consecutive lanes reading the same logical chunk
+// of 16 consecutive rows hit 16 distinct 16-byte bank slots
+template <int BK_>
+struct Lay {
+  static constexpr int BK = BK_, AROW = BK * 4, WROW = BK * 2, ACH = AROW / 16, WCH = WROW / 16;
+  __device__ static int aswz(int row) { return BK == 32 ? (row & 7) : (row & 15); }
+  __device__ static int wswz(int row) { return BK == 32 ? ((row >> 2) & 3) : ((row >> 1) & 7); }
+};
 
 // LDS-DMA of 16 bytes per lane (lane L -> lds_wave_base + 16 L), issued as
 // inline asm: the compiler then does not know the instruction writes LDS and
@@ -72,25 +77,25 @@ __device__ __forceinline__ void wait_stages(int n) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LPS) : "memory");
 }
 
-template <int BM, int BN, int S_ = 2>
-struct Ring {
-  static constexpr int S = S_;  // stages in the ring
-  static constexpr int LPS = BM / 32 + 3 * BN / 64;         // DMA instructions per wave per stage
-  static_assert((BM / 8) % 4 == 0 && (3 * BN / 16) % 4 == 0, "every wave issues the same DMA count");
-  static_assert(S >= 2 && S <= 4 && (S - 1) * LPS < 64, "ring depth / vmcnt range");
-};
 
-template <bool LN, int BM, int BN, bool PERSIST, int RS>
+template <bool LN, int BM, int BN, bool PERSIST, int RS, int BK>
 __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
     const float* __restrict__ A, int lda, const unsigned short* __restrict__ Wp, int ldw, long long wplane,
     const float* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
     const float* __restrict__ R, int ldr, float* __restrict__ C, int ldc, int M, int N, int K, int epi, float eps,
     int tiles_m, int tiles_n) {
+  using L = Lay<BK>;
+  constexpr int AROW = L::AROW, WROW = L::WROW, ACH = L::ACH, WCH = L::WCH;
   constexpr int TA = BM * AROW, TWP = BN * WROW, STAGE = TA + 3 * TWP;
+  constexpr int APW = BM * AROW / 1024 / 4, WPW = 3 * BN * WROW / 1024 / 4;  // DMA pieces per wave
+  static_assert((BM * AROW / 1024) % 4 == 0 && (3 * BN * WROW / 1024) % 4 == 0, "equal DMA count per wave");
   constexpr int MI = BM / 64, NI = BN / 64;  // 32x32 blocks per wave (waves are 2 x 2)
-  constexpr int S = Ring<BM, BN, RS>::S, LPS = Ring<BM, BN, RS>::LPS;
+  constexpr int S = RS, LPS = APW + WPW;
+  static_assert(S >= 2 && S <= 4 && (S - 1) * LPS < 64, "ring depth / vmcnt range");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* s_mu = reinterpret_cast<float*>(smem + S * STAGE);
+  // the LayerNorm statistics overlay the ring: written after the K loop's
+  // last barrier, read in the epilogue, before the next tile's prologue
+  float* s_mu = reinterpret_cast<float*>(smem);
   float* s_rstd = s_mu + BM;
 
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -114,22 +119,23 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
   // A: BM rows x 128 B = BM/8 wave instructions; W: 3 planes x BN rows x 64 B
   // = 3*BN/16 wave instructions; all spread over the 4 waves
   auto stage = [&](int k0, unsigned char* dst) {
+    constexpr int ARPI = 1024 / AROW, WRPI = 1024 / WROW;  // rows per DMA instruction
 #pragma unroll
-    for (int i = 0; i < BM / 32; ++i) {  // A pieces of this wave (unconditional: no branch per piece)
-      const int p = wid * (BM / 32) + i;
-      const int row = p * 8 + (lane >> 3);
+    for (int i = 0; i < APW; ++i) {  // A pieces of this wave (unconditional: no branch per piece)
+      const int p = wid * APW + i;
+      const int row = p * ARPI + lane / ACH;
       int grow = m0 + row;
       grow = grow < M ? grow : M - 1;
-      glds16(A + (long long)grow * lda + k0 + (((lane & 7) ^ aswz(row)) << 2), dst + p * 8 * AROW);
+      glds16(A + (long long)grow * lda + k0 + (((lane % ACH) ^ L::aswz(row)) << 2), dst + p * 1024);
     }
 #pragma unroll
-    for (int i = 0; i < 3 * BN / 64; ++i) {
-      const int p = wid * (3 * BN / 64) + i;
-      const int plane = p / (BN / 16), rb = (p % (BN / 16)) * 16;
-      const int row = rb + (lane >> 2);
+    for (int i = 0; i < WPW; ++i) {
+      const int p = wid * WPW + i;
+      const int plane = p / (BN / WRPI), rb = (p % (BN / WRPI)) * WRPI;
+      const int row = rb + lane / WCH;
       int gn = n0 + row;
       gn = gn < N ? gn : N - 1;
-      glds16(Wp + plane * wplane + (long long)gn * ldw + k0 + (((lane & 3) ^ wswz(row)) << 3),
+      glds16(Wp + plane * wplane + (long long)gn * ldw + k0 + (((lane % WCH) ^ L::wswz(row)) << 3),
              dst + TA + plane * TWP + rb * WROW);
     }
   };
@@ -167,7 +173,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
 #pragma unroll
       for (int q = 0; q < FPT / 4; ++q) {
         const int lc = spart * (FPT / 4) + q;
-        const float4 v = *reinterpret_cast<const float4*>(ta + srow * AROW + ((lc ^ aswz(srow)) << 4));
+        const float4 v = *reinterpret_cast<const float4*>(ta + srow * AROW + ((lc ^ L::aswz(srow)) << 4));
         if (kt == 0 && q == 0) sshift = v.x;
         const float d0 = v.x - sshift, d1 = v.y - sshift, d2 = v.z - sshift, d3 = v.w - sshift;
         ssum += (d0 + d1) + (d2 + d3);
@@ -175,13 +181,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
       }
     }
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {  // 16-deep MFMA steps: lane holds k = 16s + 8h .. +7
+    for (int s = 0; s < BK / 16; ++s) {  // 16-deep MFMA steps: lane holds k = 16s + 8h .. +7
       bf16x8_t af[MI][3], wf[NI][3];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int row = wm * (BM / 2) + i * 32 + c;
-        const float4 x0 = *reinterpret_cast<const float4*>(ta + row * AROW + (((4 * s + 2 * h) ^ aswz(row)) << 4));
-        const float4 x1 = *reinterpret_cast<const float4*>(ta + row * AROW + (((4 * s + 2 * h + 1) ^ aswz(row)) << 4));
+        const float4 x0 = *reinterpret_cast<const float4*>(ta + row * AROW + (((4 * s + 2 * h) ^ L::aswz(row)) << 4));
+        const float4 x1 =
+            *reinterpret_cast<const float4*>(ta + row * AROW + (((4 * s + 2 * h + 1) ^ L::aswz(row)) << 4));
         const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
         nos::split8(x, af[i][0], af[i][1], af[i][2]);
       }
@@ -190,7 +197,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
         const int row = wn * (BN / 2) + j * 32 + c;
 #pragma unroll
         for (int p = 0; p < 3; ++p)
-          wf[j][p] = *reinterpret_cast<const bf16x8_t*>(tw + p * TWP + row * WROW + (((2 * s + h) ^ wswz(row)) << 4));
+          wf[j][p] =
+              *reinterpret_cast<const bf16x8_t*>(tw + p * TWP + row * WROW + (((2 * s + h) ^ L::wswz(row)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -246,20 +254,21 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
   }  // tiles
 }
 
-template <bool LN, int BM, int BN, int RS>
+template <bool LN, int BM, int BN, int RS, int BK>
 int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
              const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K,
              int epi, float eps, hipStream_t st) {
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const long long ntiles = (long long)tiles_m * tiles_n;
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
-  const size_t lds = RS * (size_t)(BM * AROW + 3 * BN * WROW) + 2 * BM * sizeof(float);
-  const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true, RS>, NT, lds, ntiles);
+  const size_t ring = RS * (size_t)(BM * Lay<BK>::AROW + 3 * BN * Lay<BK>::WROW);
+  const size_t lds = ring > 2 * BM * sizeof(float) ? ring : 2 * BM * sizeof(float);
+  const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true, RS, BK>, NT, lds, ntiles);
   if (grid < ntiles)
-    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true, RS>), dim3((unsigned)grid), dim3(NT), lds, st, A, lda,
-                       Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true, RS, BK>), dim3((unsigned)grid), dim3(NT), lds, st, A,
+                       lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
   else
-    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false, RS>), dim3((unsigned)ntiles), dim3(NT), lds, st, A,
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false, RS, BK>), dim3((unsigned)ntiles), dim3(NT), lds, st, A,
                        lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
   return (int)hipGetLastError();
 }
@@ -270,12 +279,14 @@ NOS_API int nos_gemm_f32_pick_tile(int M, int N);
 
 namespace {
 
-int g_ring = 2;  // LDS ring depth of the 64x64 / 64x128 tiles (nos_gemm_f32x6_set_ring)
+// K-stage config (nos_gemm_f32x6_set_stage): 0 = BK 32 in a 2-deep ring,
+// 1 = BK 32, 3-deep (64x64 / 64x128 tiles), 2 = BK 64, 2-deep (K % 64 == 0)
+int g_stage = 0;
 
 int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
            const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi,
            float eps, bool ln, hipStream_t st) {
-  if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0) return (int)hipErrorInvalidValue;
+  if (M <= 0 || N <= 0 || K <= 0 || (K % 32) != 0) return (int)hipErrorInvalidValue;
   if ((lda % 4) || (ldw % 8) || (wplane % 8) || lda < K || ldw < K || ldc < N || wplane < (long long)N * ldw)
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)A | (uintptr_t)Wp) & 15) return (int)hipErrorInvalidValue;
@@ -283,25 +294,32 @@ int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long
   if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
   if ((epi & EPI_RESID) && (!R || ldr < N)) return (int)hipErrorInvalidValue;
   const int cfg = nos_gemm_f32_pick_tile(M, N);
-#define NOS_F32X_LAUNCH(LNV, BMV, BNV, RSV) \
-  launch_t<LNV, BMV, BNV, RSV>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, st)
-  const bool deep = g_ring == 3;
+  const int stg = (g_stage == 2 && K % 64 != 0) ? 0 : g_stage;
+#define NOS_F32X_LAUNCH(LNV, BMV, BNV, RSV, BKV) \
+  launch_t<LNV, BMV, BNV, RSV, BKV>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, st)
+#define NOS_F32X_TILES(LNV)                                                                        \
+  if (cfg == 0) return NOS_F32X_LAUNCH(LNV, 128, 128, 2, 32);                                     \
+  if (cfg == 1) {                                                                                  \
+    if (stg == 1) return NOS_F32X_LAUNCH(LNV, 64, 128, 3, 32);                                    \
+    if (stg == 2) return NOS_F32X_LAUNCH(LNV, 64, 128, 2, 64);                                    \
+    return NOS_F32X_LAUNCH(LNV, 64, 128, 2, 32);                                                   \
+  }                                                                                                \
+  if (stg == 1) return NOS_F32X_LAUNCH(LNV, 64, 64, 3, 32);                                       \
+  if (stg == 2) return NOS_F32X_LAUNCH(LNV, 64, 64, 2, 64);                                       \
+  return NOS_F32X_LAUNCH(LNV, 64, 64, 2, 32);
   if (ln) {
-    if (cfg == 0) return NOS_F32X_LAUNCH(true, 128, 128, 2);
-    if (cfg == 1) return deep ? NOS_F32X_LAUNCH(true, 64, 128, 3) : NOS_F32X_LAUNCH(true, 64, 128, 2);
-    return deep ? NOS_F32X_LAUNCH(true, 64, 64, 3) : NOS_F32X_LAUNCH(true, 64, 64, 2);
+    NOS_F32X_TILES(true)
   }
-  if (cfg == 0) return NOS_F32X_LAUNCH(false, 128, 128, 2);
-  if (cfg == 1) return deep ? NOS_F32X_LAUNCH(false, 64, 128, 3) : NOS_F32X_LAUNCH(false, 64, 128, 2);
-  return deep ? NOS_F32X_LAUNCH(false, 64, 64, 3) : NOS_F32X_LAUNCH(false, 64, 64, 2);
+  NOS_F32X_TILES(false)
+#undef NOS_F32X_TILES
 #undef NOS_F32X_LAUNCH
 }
 
 }  // namespace
 
-NOS_API int nos_gemm_f32x6_set_ring(int stages) {
-  if (stages != 2 && stages != 3) return (int)hipErrorInvalidValue;
-  g_ring = stages;
+NOS_API int nos_gemm_f32x6_set_stage(int cfg) {
+  if (cfg < 0 || cfg > 2) return (int)hipErrorInvalidValue;
+  g_stage = cfg;
   return 0;
 }
 

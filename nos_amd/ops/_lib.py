@@ -43,7 +43,7 @@ _SIGS = {
     "nos_gemm_ln_f32x6": [c_void_p, c_int, c_void_p, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                           c_int, c_int, c_float, c_void_p],
     "nos_gemm_f32_pick_tile": [c_int, c_int],
-    "nos_gemm_f32x6_set_ring": [c_int],
+    "nos_gemm_f32x6_set_stage": [c_int],
     "nos_gemm_set_policy": [c_int],
     "nos_gemm_set_persistent": [c_int],
     "nos_gemm_f32_set_policy": [c_int],

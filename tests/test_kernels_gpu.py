@@ -197,6 +197,36 @@ def test_linear_fp32_split_is_as_accurate_as_exact_f32(M, N, K):
     assert errs["x6"][0] <= 1.5 * errs["exact"][0] and errs["x6"][1] <= 1.5 * errs["exact"][1], errs
 
 
+@pytest.mark.parametrize("stage", [1, 2])
+@pytest.mark.parametrize("M,N,K,ln", [(3401, 1152, 384, True), (3401, 384, 1536, False), (257, 200, 96, False),
+                                      (100, 92, 384, True)])
+def test_linear_fp32_split_stage_configs(stage, M, N, K, ln):
+    """The x6 GEMM's other K-stage configs (1: BK 32 in a 3-deep ring, 2: BK 64
+    -- K % 64 != 0 falls back to BK 32) against fp64 at the exact-f32 tolerance."""
+    from nos_amd.ops import _lib
+
+    x = torch.randn(M, K, device=DEV) * 2 + 0.5
+    w = torch.randn(N, K, device=DEV) * 0.05
+    b = torch.randn(N, device=DEV)
+    ops.set_f32_math("x6")
+    _lib.check(_lib.lib().nos_gemm_f32x6_set_stage(stage), "set_stage")
+    try:
+        if ln:
+            g, be = torch.randn(K, device=DEV), torch.randn(K, device=DEV)
+            wg, c1, c2 = ops.fold_layernorm(w, b, g, be)
+            y = ops.linear_ln(x, wg, c1, c2, act="gelu")
+            xd = torch.nn.functional.layer_norm(x.cpu().double(), (K,), g.cpu().double(), be.cpu().double(), 1e-12)
+            ref = torch.nn.functional.gelu(xd @ w.cpu().double().t() + b.cpu().double())
+        else:
+            y = ops.linear(x, w, b)
+            ref = x.cpu().double() @ w.cpu().double().t() + b.cpu().double()
+    finally:
+        _lib.check(_lib.lib().nos_gemm_f32x6_set_stage(0), "set_stage")
+        ops.set_f32_math("exact")
+    err = (y.cpu().double() - ref).abs().max().item()
+    assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
+
+
 def test_attention_fp32_strided_and_large_logits():
     B, S, H = 2, 129, 6
     base = torch.randn(B, S, 3 * H * 64 + 64, device=DEV) * 4.0  # padded rows: ld != 3*H*64, logits ~ +-100
