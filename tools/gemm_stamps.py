@@ -1,5 +1,5 @@
 """Per-phase cycle split of the x6 fp32 GEMM from an s_memtime-stamped build
-(an A/B variant built by tools/build_variant.py with a stamp patch, loaded via
+(python tools/build_variant.py stamps tools/patches/gemm_f32x_stamps.py, loaded via
 NOS_AMD_HIP_LIB; stamps go to a device array of their own, never to outputs).
 
 NOS_AMD_HIP_LIB=build/variants/stamps/libnos_hip.so python tools/gemm_stamps.py --batch 1
