@@ -290,3 +290,29 @@ def test_amdpart_switch_puts_back_demand_its_free_partitions_covered():
         for k, v in r.items():
             total[k] = total.get(k, 0) + v
     assert total.get(HALF, 0) >= 1 and total.get(ONE, 0) >= 1, res
+
+
+def test_slice_tracker_counts_lacking_and_requested_slices_and_forgets_removed_pods():
+    """The reference's ``tracker_test.go``: per-pod lacking slices are summed,
+    requested slices counted for every pod, and removing a pod gives back
+    exactly what it added (a removed pod's lacking entries disappear at 0)."""
+    from nos_amd.partitioning.core import SliceTracker
+
+    snap = _cumask_snapshot([_node("n1", "cumask", ann={"nos.nebuly.com/status-gpu-0-10gb-free": "1"},
+                                   alloc={"amd.com/gpu-10gb": "1"})])
+    fits = _pod("fits", "amd.com/gpu-10gb")
+    big = _pod("big", "amd.com/gpu-20gb", 2)
+    more = _pod("more", "amd.com/gpu-20gb", 1)
+    t = SliceTracker(snap, cm.SliceCalculator(), [fits, big, more])
+    req = {str(k): v for k, v in t.get_requested_slices().items()}
+    lack = {str(k): v for k, v in t.get_lacking_slices().items()}
+    assert req == {"10gb": 1, "20gb": 3}
+    assert lack == {"20gb": 3}  # the free 10gb slice covers "fits"
+    t.remove(big)
+    assert {str(k): v for k, v in t.get_lacking_slices().items()} == {"20gb": 1}
+    assert {str(k): v for k, v in t.get_requested_slices().items()} == {"10gb": 1, "20gb": 1}
+    t.remove(more)
+    t.remove(fits)
+    assert t.get_lacking_slices() == {} and t.get_requested_slices() == {}
+    t.remove(_pod("never-tracked", "amd.com/gpu-20gb"))  # unknown pods: requested may not go negative
+    assert t.get_lacking_slices() == {} and t.get_requested_slices() == {}
