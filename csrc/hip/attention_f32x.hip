@@ -62,14 +62,15 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_ba
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-template <bool PERSIST, int SPREAD>
+template <bool PERSIST>
 __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
     const float* __restrict__ q, const unsigned short* __restrict__ kvs, float* __restrict__ o, int B, int H, int Sq,
-    int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, int nqb) {
+    int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, int nqb, int nsplit,
+    float* __restrict__ part) {
   const int ldh = H * D;  // elements per plane row
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-  const int nwg = B * H * nqb;
+  const int nwg = B * H * nqb * nsplit;
   nos::XcdChunk chunk;
   if constexpr (PERSIST) {
     chunk = nos::xcd_chunk(blockIdx.x, gridDim.x, nwg);
@@ -112,11 +113,17 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
 
   for (int w = chunk.first; w < chunk.end; w += chunk.step) {
     if (PERSIST && w != chunk.first) __syncthreads();  // the previous item is done with the ring
-    const int b = w / (H * nqb);
-    const int rem = w - b * (H * nqb);
+    // item = (batch, head, q-block, key split), the splits of a q-block and
+    // the q-blocks of a head adjacent (one XCD's L2)
+    const int sp = w % nsplit;
+    const int wq = w / nsplit;
+    const int b = wq / (H * nqb);
+    const int rem = wq - b * (H * nqb);
     const int hd = rem / nqb;
     const int qb = rem - hd * nqb;
     const long long boff = (long long)b * bs_in + hd * D;
+    const int tps = (ntiles + nsplit - 1) / nsplit;  // key tiles per split (the host keeps every split non-empty)
+    const int t0 = sp * tps, t1 = min(ntiles, t0 + tps);
 
     // ---- Q pieces (B operand): lane holds Q[row r][d = 16ks + 8hh .. +7] * c
     const int qrow = qb * QBLK + wid * 32 + r;
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
       glds16(pb + (long long)t * (KVB * 6) * ldh + soff[i], smem + buf * STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
     };
 #pragma unroll
-    for (int i = 0; i < 6; ++i) stage_piece(0, 0, i);
+    for (int i = 0; i < 6; ++i) stage_piece(t0, 0, i);
 
     f32x16_t oacc[2];
 #pragma unroll
@@ -155,13 +162,13 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
 
     __syncthreads();  // tile 0 landed and is visible
 
-    for (int t = 0; t < ntiles; ++t) {
-      const int buf = t & 1;
-      const bool more = t + 1 < ntiles;
-      // the next tile's 6 DMA pieces (into the buffer released by the barrier
-      // ending t-1): all up front (SPREAD 0), or spread between the QK^T (1)
-      // or the PV (2) MFMA groups so their issue cost overlaps this wave's MFMAs
-      if (SPREAD == 0 && more) {
+    for (int t = t0; t < t1; ++t) {
+      const int buf = (t - t0) & 1;
+      const bool more = t + 1 < t1;
+      // the next tile's 6 DMA pieces, into the buffer released by the barrier
+      // ending t-1 (issuing them between the QK^T or the PV MFMA groups
+      // instead measured the same or slower: profiles/r03_f32x6_fleet_ab.json)
+      if (more) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) stage_piece(t + 1, buf ^ 1, i);
       }
@@ -177,12 +184,6 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
 #pragma unroll
         for (int p = 0; p < 3; ++p) a[p] = *reinterpret_cast<const bf16x8_t*>(kl + p * IMG + koff[ks]);
         s = nos::mma6(a, qf[ks], s);
-        if (SPREAD == 1 && more) {
-          __builtin_amdgcn_sched_barrier(0);
-          stage_piece(t + 1, buf ^ 1, ks < 2 ? 2 * ks : ks + 2);
-          if (ks < 2) stage_piece(t + 1, buf ^ 1, 2 * ks + 1);
-          __builtin_amdgcn_sched_barrier(0);
-        }
       }
       if ((t + 1) * KVB > Skv) {  // tail tile: keys past Skv never contribute
 #pragma unroll
@@ -193,8 +194,8 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
 #pragma unroll
       for (int i = 1; i < 16; ++i) mt = fmaxf(mt, s[i]);
       const float mrel = xor32_max(mt) - m;
-      if (t == 0 || !__all(mrel <= RESCALE_THR)) {  // the first tile sets the reference max
-        const float delta = t == 0 ? mrel : fmaxf(mrel, 0.f);
+      if (t == t0 || !__all(mrel <= RESCALE_THR)) {  // the first tile sets the reference max
+        const float delta = t == t0 ? mrel : fmaxf(mrel, 0.f);
         const float alpha = __builtin_amdgcn_exp2f(-delta);
         m += delta;
         l *= alpha;
@@ -237,18 +238,30 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
             a[p] = __builtin_bit_cast(bf16x8_t, a16);
           }
           oacc[db] = nos::mma6(a, pf[s2], oacc[db]);
-          if (SPREAD == 2 && more) {
-            const int g = 2 * db + s2;
-            __builtin_amdgcn_sched_barrier(0);
-            stage_piece(t + 1, buf ^ 1, g < 2 ? 2 * g : g + 2);
-            if (g < 2) stage_piece(t + 1, buf ^ 1, 2 * g + 1);
-            __builtin_amdgcn_sched_barrier(0);
-          }
         }
       __syncthreads();  // next tile landed (vmcnt(0)); every wave is done with `buf`
     }
 
-    const float inv = 1.f / xor32_sum(l);
+    const float lt = xor32_sum(l);
+    if (nsplit > 1) {  // unnormalised partial (O, m, l) of this key range: nos_attn_f32x6 merges them
+      if (qrow < Sq) {
+        const long long row = ((long long)sp * B + b) * Sq + qrow;
+        float* op = part + row * ldh + hd * D;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(op + 32 * db + 8 * g + 4 * hh) =
+                float4{oacc[db][4 * g + 0], oacc[db][4 * g + 1], oacc[db][4 * g + 2], oacc[db][4 * g + 3]};
+        if (hh == 0) {
+          float* ml = part + (long long)nsplit * B * Sq * ldh + (row * H + hd) * 2;
+          ml[0] = m;
+          ml[1] = lt;
+        }
+      }
+      continue;
+    }
+    const float inv = 1.f / lt;
     if (qrow < Sq) {
       float* op = o + (long long)b * bs_out + (long long)qrow * ld_out + hd * D;
 #pragma unroll
@@ -296,33 +309,88 @@ __global__ __launch_bounds__(256) void split_kv_kernel(const float* __restrict__
   for (int j = 0; j < 3; ++j) *reinterpret_cast<bf16x8_t*>(dst + j * H * D) = p[j];
 }
 
-template <int SPREAD>
 int launch(const float* q, const unsigned short* kvs, float* o, int B, int H, int Sq, int Skv, int ld_in,
-           long long bs_in, int ld_out, long long bs_out, float c, int nqb, long long nwg, hipStream_t stream) {
-  const int grid = nos_grid_for((const void*)attn_fwd_f32x6_d64_kernel<true, SPREAD>, NT, LDS_BYTES, nwg);
+           long long bs_in, int ld_out, long long bs_out, float c, int nqb, int nsplit, float* part,
+           hipStream_t stream) {
+  const long long nwg = (long long)B * H * nqb * nsplit;
+  const int grid = nos_grid_for((const void*)attn_fwd_f32x6_d64_kernel<true>, NT, LDS_BYTES, nwg);
   if (grid < nwg)
-    hipLaunchKernelGGL((attn_fwd_f32x6_d64_kernel<true, SPREAD>), dim3((unsigned)grid), dim3(NT), LDS_BYTES, stream,
-                       q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
+    hipLaunchKernelGGL((attn_fwd_f32x6_d64_kernel<true>), dim3((unsigned)grid), dim3(NT), LDS_BYTES, stream,
+                       q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb, nsplit, part);
   else
-    hipLaunchKernelGGL((attn_fwd_f32x6_d64_kernel<false, SPREAD>), dim3((unsigned)nwg), dim3(NT), LDS_BYTES, stream,
-                       q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
+    hipLaunchKernelGGL((attn_fwd_f32x6_d64_kernel<false>), dim3((unsigned)nwg), dim3(NT), LDS_BYTES, stream,
+                       q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb, nsplit, part);
   return (int)hipGetLastError();
 }
 
-int g_spread = 0;
+int g_kvsplit = 0;  // 0 = auto (nos_attn_f32x6_set_kvsplit)
+constexpr int MAX_SPLIT = 4;
+constexpr int WG_PER_CU = 3;  // the kernel's launch bound
+
+// Key splits: when one split per q-block leaves resident-workgroup slots of
+// the (budgeted) CUs empty -- one YOLOS image is 162 q-blocks for 768 slots --
+// split the keys so the grid fills them, at most MAX_SPLIT ways and never so
+// finely that a split has no tile.
+int pick_split(long long nwg1, int ntiles) {
+  int n = g_kvsplit;
+  if (n == 0) {
+    const long long slots = (long long)WG_PER_CU * nos_effective_cus();
+    n = nwg1 >= slots ? 1 : (int)(slots / nwg1);
+  }
+  n = n < 1 ? 1 : (n > MAX_SPLIT ? MAX_SPLIT : n);
+  while (n > 1 && (long long)(n - 1) * ((ntiles + n - 1) / n) >= ntiles) --n;  // the last split non-empty
+  return n;
+}
+
+// KV-split merge: per (batch, row, head) and 4 dims, O = sum_i O_i 2^(m_i - M) /
+// sum_i l_i 2^(m_i - M), M = max_i m_i (m in log2 units, O_i unnormalised)
+__global__ __launch_bounds__(256) void merge_splits_kernel(const float* __restrict__ part, float* __restrict__ o,
+                                                           int B, int H, int Sq, int nsplit, int ld_out,
+                                                           long long bs_out, long long n4) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int ldh = H * D;
+  const long long row = i / (ldh / 4);               // b * Sq + s
+  const int col = (int)(i - row * (ldh / 4)) * 4;    // hd * 64 + d
+  const int hd = col / D;
+  const long long per_split = (long long)B * Sq;
+  const float* ml = part + (long long)nsplit * per_split * ldh;
+  float mx = -INFINITY;
+  for (int sp = 0; sp < nsplit; ++sp) mx = fmaxf(mx, ml[((sp * per_split + row) * H + hd) * 2]);
+  float L = 0.f;
+  float4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int sp = 0; sp < nsplit; ++sp) {
+    const long long r = sp * per_split + row;
+    const float a = __builtin_amdgcn_exp2f(ml[(r * H + hd) * 2] - mx);
+    L = fmaf(ml[(r * H + hd) * 2 + 1], a, L);
+    const float4 v = *reinterpret_cast<const float4*>(part + r * ldh + col);
+    acc.x = fmaf(v.x, a, acc.x);
+    acc.y = fmaf(v.y, a, acc.y);
+    acc.z = fmaf(v.z, a, acc.z);
+    acc.w = fmaf(v.w, a, acc.w);
+  }
+  const float inv = 1.f / L;
+  const long long b = row / Sq, s = row - b * Sq;
+  *reinterpret_cast<float4*>(o + b * bs_out + s * ld_out + col) = float4{acc.x * inv, acc.y * inv, acc.z * inv,
+                                                                          acc.w * inv};
+}
 
 }  // namespace
 
-NOS_API int nos_attn_f32x6_set_spread(int spread) {
-  if (spread < 0 || spread > 2) return (int)hipErrorInvalidValue;
-  g_spread = spread;
+
+// Workspace bytes of nos_attn_fwd_f32x6_d64 (the split K/V planes).
+NOS_API int nos_attn_f32x6_set_kvsplit(int n) {
+  if (n < 0 || n > MAX_SPLIT) return (int)hipErrorInvalidValue;
+  g_kvsplit = n;
   return 0;
 }
 
-// Workspace bytes of nos_attn_fwd_f32x6_d64 (the split K/V planes).
-NOS_API long long nos_attn_f32x6_workspace(int B, int H, int Skv) {
+// Workspace bytes of nos_attn_fwd_f32x6_d64: the split K/V planes, then room
+// for MAX_SPLIT partial (O, m, l) per query row and head.
+NOS_API long long nos_attn_f32x6_workspace(int B, int H, int Sq, int Skv) {
   const long long skvp = (Skv + KVB - 1) / KVB * KVB;
-  return (long long)B * skvp * 6 * H * D * 2;
+  const long long planes = ((long long)B * skvp * 6 * H * D * 2 + 15) / 16 * 16;
+  return planes + (long long)MAX_SPLIT * B * Sq * H * (D + 2) * 4;
 }
 
 // The exact-fp32 kernel's contract (attention_f32.hip: nos_attn_fwd_f32_d64)
@@ -334,7 +402,7 @@ NOS_API int nos_attn_fwd_f32x6_d64(const float* q, const float* k, const float* 
   if (ld_in < H * D || ld_out < H * D || (ld_in & 3) || (ld_out & 3) || (bs_in & 3) || (bs_out & 3))
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o | (uintptr_t)ws) & 15) return (int)hipErrorInvalidValue;
-  if (ws == nullptr || ws_bytes < nos_attn_f32x6_workspace(B, H, Skv)) return (int)hipErrorInvalidValue;
+  if (ws == nullptr || ws_bytes < nos_attn_f32x6_workspace(B, H, Sq, Skv)) return (int)hipErrorInvalidValue;
   const float c = scale * 1.4426950408889634f;
   const int nqb = (Sq + QBLK - 1) / QBLK;
   const long long nwg = (long long)B * H * nqb;
@@ -345,7 +413,13 @@ NOS_API int nos_attn_fwd_f32x6_d64(const float* q, const float* k, const float* 
   auto* kvs = static_cast<unsigned short*>(ws);
   hipLaunchKernelGGL(split_kv_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, stream, k, v, kvs, Skv, skvp,
                      H, ld_in, bs_in, (int)n8);
-  if (g_spread == 1) return launch<1>(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb, nwg, stream);
-  if (g_spread == 2) return launch<2>(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb, nwg, stream);
-  return launch<0>(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb, nwg, stream);
+  const int nsplit = pick_split(nwg, skvp / KVB);
+  float* part = reinterpret_cast<float*>(static_cast<unsigned char*>(ws) +
+                                         ((long long)B * skvp * 6 * H * D * 2 + 15) / 16 * 16);
+  const int rc = launch(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb, nsplit, part, stream);
+  if (rc != 0 || nsplit == 1) return rc;
+  const long long n4 = (long long)B * Sq * H * (D / 4);
+  hipLaunchKernelGGL(merge_splits_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, part, o, B, H, Sq,
+                     nsplit, ld_out, bs_out, n4);
+  return (int)hipGetLastError();
 }

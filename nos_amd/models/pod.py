@@ -142,7 +142,10 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
     fp64 <= the exact-f32 MFMA's, tests/test_kernels_gpu.py): attention
     (attention_f32x.hip) for every slice kind -- 8-pod fleet 318 -> 407 inf/s
     -- and the GEMMs (gemm_f32x.hip) -> 415 inf/s
-    (profiles/r03_f32x6_fleet_ab.json).  ``NOS_AMD_F32_MATH=exact`` /
+    (profiles/r03_f32x6_fleet_ab.json).  A whole-GPU pod splits the keys
+    when its grid leaves CU slots empty (``x6``: batch-1 attention 164 -> 133
+    us); fractional pods never split (``x6n``: the co-tenants fill the slots,
+    8 pods 410 vs 399 inf/s with the split).  ``NOS_AMD_F32_MATH=exact`` /
     ``NOS_AMD_ATTN_F32_VARIANT=<tiling>`` select the exact-f32 MFMA kernels."""
     env = os.environ if env is None else env
     whole = memory_fraction is None or memory_fraction >= 0.99
@@ -152,7 +155,7 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
         gf = "latency" if whole else "small"
     return {"gemm_bf16": env.get("NOS_AMD_GEMM_POLICY") or ("latency" if whole else "throughput"),
             "gemm_f32": env.get("NOS_AMD_GEMM_F32_POLICY") or gf,
-            "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or "x6",
+            "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or ("x6" if whole else "x6n"),
             "f32_math": env.get("NOS_AMD_F32_MATH") or "x6"}
 
 

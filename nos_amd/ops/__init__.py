@@ -248,19 +248,22 @@ def set_attention_f32_variant(variant: str) -> None:
     ``"w2k64"`` (64-query blocks), ``"w8k64"`` (256-query blocks), ``"w4k32o4"`` (32-key tiles in 127
     VGPRs: 4 waves per SIMD), ``"w4k32g2"`` (two groups on 32-key tiles); ``"x6"``: the bf16x6 split
     kernel (attention_f32x.hip: fp32 operands as three bf16 pieces, six
-    exact piece products per product on the bf16 matrix pipes)."""
+    exact piece products per product on the bf16 matrix pipes; the keys are
+    split 1-4 ways when the grid would leave CU slots empty), ``"x6k<n>"``
+    with n key splits forced, ``"x6n"`` = ``"x6k1"`` (never split)."""
     global _ATTN_F32_VARIANT
-    code = {"auto": 0, "w4k64": 1, "w4k64g2": 2, "w4k32": 3, "w2k64": 4, "w8k64": 5, "w4k32o4": 6, "w4k32g2": 7,
-            "x6": 0, "x6s0": 0, "x6s1": 0, "x6s2": 0}[variant]
+    x6 = {"x6": 0, "x6n": 1, "x6k1": 1, "x6k2": 2, "x6k3": 3, "x6k4": 4}
+    code = {"auto": 0, "w4k64": 1, "w4k64g2": 2, "w4k32": 3, "w2k64": 4, "w8k64": 5, "w4k32o4": 6,
+            "w4k32g2": 7}.get(variant, 0)
+    if variant not in x6 and code == 0 and variant != "auto":
+        raise KeyError(variant)
     _lib.check(_lib.lib().nos_attn_f32_set_variant(code), "nos_attn_f32_set_variant")
-    if variant.startswith("x6"):  # x6s<n>: where the x6 kernel issues the next tile's DMA (A/B)
-        _lib.check(_lib.lib().nos_attn_f32x6_set_spread(int(variant[3:] or _X6_SPREAD_DEFAULT)),
-                   "nos_attn_f32x6_set_spread")
+    if variant in x6:  # x6k<n>: n key splits (x6: auto)
+        _lib.check(_lib.lib().nos_attn_f32x6_set_kvsplit(x6[variant]), "nos_attn_f32x6_set_kvsplit")
     _ATTN_F32_VARIANT = variant
 
 
 _ATTN_F32_VARIANT = "auto"
-_X6_SPREAD_DEFAULT = 0
 
 
 def attention_f32_variant() -> str:
@@ -399,7 +402,7 @@ def attention_qkv(qkv: torch.Tensor, num_heads: int, out: torch.Tensor | None = 
             qkv.stride(0), out.stride(1), out.stride(0), float(scale))
     if qkv.dtype == torch.float32 and _ATTN_F32_VARIANT.startswith("x6"):
         # the split K/V planes: a stream-ordered allocation (graph-capture safe)
-        nbytes = int(L.nos_attn_f32x6_workspace(B, num_heads, S))
+        nbytes = int(L.nos_attn_f32x6_workspace(B, num_heads, S, S))
         ws = torch.empty(nbytes // 2, dtype=torch.int16, device=qkv.device)
         _lib.check(L.nos_attn_fwd_f32x6_d64(*args, ws.data_ptr(), nbytes, _stream()), "nos_attn_fwd_f32x6_d64")
         return out

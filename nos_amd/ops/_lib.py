@@ -30,8 +30,8 @@ _SIGS = {
                              c_ll, c_int, c_ll, c_float, c_void_p],
     "nos_attn_fwd_f32x6_d64": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                c_ll, c_int, c_ll, c_float, c_void_p, c_ll, c_void_p],
-    "nos_attn_f32x6_workspace": [c_int, c_int, c_int],
-    "nos_attn_f32x6_set_spread": [c_int],
+    "nos_attn_f32x6_workspace": [c_int, c_int, c_int, c_int],
+    "nos_attn_f32x6_set_kvsplit": [c_int],
     "nos_gemm_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nos_gemm_f32": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,

@@ -133,7 +133,8 @@ def test_attention_strided_views():
     assert out[..., hid:].abs().max().item() == 0  # padding untouched
 
 
-@pytest.mark.parametrize("variant", ["w4k64", "w4k64g2", "w4k32", "w4k32o4", "w4k32g2", "w2k64", "w8k64", "x6", "auto"])
+@pytest.mark.parametrize("variant", ["w4k64", "w4k64g2", "w4k32", "w4k32o4", "w4k32g2", "w2k64", "w8k64", "x6", "x6n",
+                                     "x6k2", "x6k3", "x6k4", "auto"])
 @pytest.mark.parametrize("B,S,H", [(1, 3401, 6), (2, 77, 3), (1, 1, 1), (1, 33, 2), (3, 300, 2), (1, 129, 1)])
 def test_attention_fp32_exact(B, S, H, variant):
     """fp32 MFMA attention against an fp64 reference: exact-f32 numerics."""
@@ -422,7 +423,7 @@ def test_slice_sized_persistent_grids_are_bit_identical(budget):
                 outs += [ops.linear(x, w, b, act="gelu", residual=r), ops.linear_ln(x, wg, c1, c2, act="gelu")]
         ops.set_f32_math("exact")
         ops.set_gemm_f32_policy("latency")
-        for var in ("w4k32", "w4k64g2", "w4k32o4", "x6"):
+        for var in ("w4k32", "w4k64g2", "w4k32o4", "x6n", "x6k2"):
             ops.set_attention_f32_variant(var)
             outs.append(ops.attention_qkv(qkv, 6))
         ops.set_attention_f32_variant("auto")
