@@ -78,7 +78,7 @@ __device__ __forceinline__ void wait_stages(int n) {
 }
 
 
-template <bool LN, int BM, int BN, bool PERSIST, int RS, int BK>
+template <bool LN, int BM, int BN, bool PERSIST, int RS, int BK, int WGM = 2>
 __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
     const float* __restrict__ A, int lda, const unsigned short* __restrict__ Wp, int ldw, long long wplane,
     const float* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
@@ -89,7 +89,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
   constexpr int TA = BM * AROW, TWP = BN * WROW, STAGE = TA + 3 * TWP;
   constexpr int APW = BM * AROW / 1024 / 4, WPW = 3 * BN * WROW / 1024 / 4;  // DMA pieces per wave
   static_assert((BM * AROW / 1024) % 4 == 0 && (3 * BN * WROW / 1024) % 4 == 0, "equal DMA count per wave");
-  constexpr int MI = BM / 64, NI = BN / 64;  // 32x32 blocks per wave (waves are 2 x 2)
+  // waves WGM x WGN over the tile, each (BM/WGM) x (BN/WGN) as 32x32 blocks;
+  // 4 x 1 makes every wave split ONE A block for all its W blocks
+  constexpr int WGN = 4 / WGM, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
+  static_assert(MI >= 1 && NI >= 1 && WGM * WGN == 4, "wave layout");
   constexpr int S = RS, LPS = APW + WPW;
   static_assert(S >= 2 && S <= 4 && (S - 1) * LPS < 64, "ring depth / vmcnt range");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -100,7 +103,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
 
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int c = lane & 31, h = lane >> 5;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WGN, wn = wid % WGN;
   const int ntiles = tiles_m * tiles_n;
   const int nk = K / BK;
   nos::XcdChunk chunk;
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
       bf16x8_t af[MI][3], wf[NI][3];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const int row = wm * (BM / 2) + i * 32 + c;
+        const int row = wm * (BM / WGM) + i * 32 + c;
         const float4 x0 = *reinterpret_cast<const float4*>(ta + row * AROW + (((4 * s + 2 * h) ^ L::aswz(row)) << 4));
         const float4 x1 =
             *reinterpret_cast<const float4*>(ta + row * AROW + (((4 * s + 2 * h + 1) ^ L::aswz(row)) << 4));
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int row = wn * (BN / 2) + j * 32 + c;
+        const int row = wn * (BN / WGN) + j * 32 + c;
 #pragma unroll
         for (int p = 0; p < 3; ++p)
           wf[j][p] =
@@ -229,7 +232,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
   // epilogue: register i of lane (c, h) = row (i&3) + 8(i>>2) + 4h of the block, column c
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
-    const int n = n0 + wn * (BN / 2) + j * 32 + c;
+    const int n = n0 + wn * (BN / WGN) + j * 32 + c;
     const int nc = n < N ? n : N - 1;
     const float p1 = LN ? c1[nc] : 0.f;
     const float p2 = LN ? c2[nc] : ((epi & EPI_BIAS) ? bias[nc] : 0.f);
@@ -237,7 +240,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
     for (int i = 0; i < MI; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int rl = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int m = m0 + rl;
         float v = acc[i][j][r];
         if constexpr (LN) v = fmaf(s_rstd[rl], v - s_mu[rl] * p1, p2);
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
   }  // tiles
 }
 
-template <bool LN, int BM, int BN, int RS, int BK>
+template <bool LN, int BM, int BN, int RS, int BK, int WGM = 2>
 int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
              const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K,
              int epi, float eps, hipStream_t st) {
@@ -263,12 +266,12 @@ int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long lo
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
   const size_t ring = RS * (size_t)(BM * Lay<BK>::AROW + 3 * BN * Lay<BK>::WROW);
   const size_t lds = ring > 2 * BM * sizeof(float) ? ring : 2 * BM * sizeof(float);
-  const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true, RS, BK>, NT, lds, ntiles);
+  const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM>, NT, lds, ntiles);
   if (grid < ntiles)
-    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true, RS, BK>), dim3((unsigned)grid), dim3(NT), lds, st, A,
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM>), dim3((unsigned)grid), dim3(NT), lds, st, A,
                        lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
   else
-    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false, RS, BK>), dim3((unsigned)ntiles), dim3(NT), lds, st, A,
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false, RS, BK, WGM>), dim3((unsigned)ntiles), dim3(NT), lds, st, A,
                        lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
   return (int)hipGetLastError();
 }
@@ -282,6 +285,10 @@ namespace {
 // K-stage config (nos_gemm_f32x6_set_stage): 0 = BK 32 in a 2-deep ring,
 // 1 = BK 32, 3-deep (64x64 / 64x128 tiles), 2 = BK 64, 2-deep (K % 64 == 0)
 int g_stage = 0;
+// tile override (nos_gemm_f32x6_set_tile): -1 = the fp32 GEMM's tile policy,
+// 0 / 1 / 2 = 128x128 / 64x128 / 64x64 (2 x 2 waves), 3 = 128x64 (4 x 1 waves),
+// 4 = 128x64 where N >= 1024, the policy's tile elsewhere
+int g_tile = -1;
 
 int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
            const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi,
@@ -293,12 +300,16 @@ int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long
   if (!ln && (epi & EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
   if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
   if ((epi & EPI_RESID) && (!R || ldr < N)) return (int)hipErrorInvalidValue;
-  const int cfg = nos_gemm_f32_pick_tile(M, N);
+  int cfg = g_tile >= 0 && g_tile != 4 ? g_tile : nos_gemm_f32_pick_tile(M, N);
+  if (g_tile == 4 && N >= 1024) cfg = 3;  // 128x64 (4 x 1 waves) for the wide projections only
   const int stg = (g_stage == 2 && K % 64 != 0) ? 0 : g_stage;
 #define NOS_F32X_LAUNCH(LNV, BMV, BNV, RSV, BKV) \
   launch_t<LNV, BMV, BNV, RSV, BKV>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, st)
 #define NOS_F32X_TILES(LNV)                                                                        \
   if (cfg == 0) return NOS_F32X_LAUNCH(LNV, 128, 128, 2, 32);                                     \
+  if (cfg == 3)                                                                                    \
+    return launch_t<LNV, 128, 64, 2, 32, 4>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, \
+                                            eps, st);                                              \
   if (cfg == 1) {                                                                                  \
     if (stg == 1) return NOS_F32X_LAUNCH(LNV, 64, 128, 3, 32);                                    \
     if (stg == 2) return NOS_F32X_LAUNCH(LNV, 64, 128, 2, 64);                                    \
@@ -316,6 +327,12 @@ int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long
 }
 
 }  // namespace
+
+NOS_API int nos_gemm_f32x6_set_tile(int tile) {
+  if (tile < -1 || tile > 4) return (int)hipErrorInvalidValue;
+  g_tile = tile;
+  return 0;
+}
 
 NOS_API int nos_gemm_f32x6_set_stage(int cfg) {
   if (cfg < 0 || cfg > 2) return (int)hipErrorInvalidValue;

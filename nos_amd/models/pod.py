@@ -214,6 +214,10 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             set_gemm_f32_policy(cfg["gemm_f32"])
             set_attention_f32_variant(cfg["attention_f32"])
             set_f32_math(cfg["f32_math"])
+            if os.environ.get("NOS_AMD_X6_TILE"):  # A/B: x6 GEMM tile override (gemm_f32x.hip g_tile)
+                from ..ops import _lib
+
+                _lib.check(_lib.lib().nos_gemm_f32x6_set_tile(int(os.environ["NOS_AMD_X6_TILE"])), "set_tile")
             if budget:  # CU-mask slice: slice-sized persistent grids (ops.set_cu_budget)
                 set_cu_budget(budget)
         m, x = _build(dtype, seed, demo_input_hw(), device)

@@ -198,12 +198,13 @@ def test_linear_fp32_split_is_as_accurate_as_exact_f32(M, N, K):
     assert errs["x6"][0] <= 1.5 * errs["exact"][0] and errs["x6"][1] <= 1.5 * errs["exact"][1], errs
 
 
-@pytest.mark.parametrize("stage", [1, 2])
+@pytest.mark.parametrize("stage,tile", [(1, -1), (2, -1), (0, 3)])
 @pytest.mark.parametrize("M,N,K,ln", [(3401, 1152, 384, True), (3401, 384, 1536, False), (257, 200, 96, False),
                                       (100, 92, 384, True)])
-def test_linear_fp32_split_stage_configs(stage, M, N, K, ln):
+def test_linear_fp32_split_stage_configs(stage, tile, M, N, K, ln):
     """The x6 GEMM's other K-stage configs (1: BK 32 in a 3-deep ring, 2: BK 64
-    -- K % 64 != 0 falls back to BK 32) against fp64 at the exact-f32 tolerance."""
+    -- K % 64 != 0 falls back to BK 32) and the 128x64 4x1-wave tile against
+    fp64 at the exact-f32 tolerance."""
     from nos_amd.ops import _lib
 
     x = torch.randn(M, K, device=DEV) * 2 + 0.5
@@ -211,6 +212,7 @@ def test_linear_fp32_split_stage_configs(stage, M, N, K, ln):
     b = torch.randn(N, device=DEV)
     ops.set_f32_math("x6")
     _lib.check(_lib.lib().nos_gemm_f32x6_set_stage(stage), "set_stage")
+    _lib.check(_lib.lib().nos_gemm_f32x6_set_tile(tile), "set_tile")
     try:
         if ln:
             g, be = torch.randn(K, device=DEV), torch.randn(K, device=DEV)
@@ -223,6 +225,7 @@ def test_linear_fp32_split_stage_configs(stage, M, N, K, ln):
             ref = x.cpu().double() @ w.cpu().double().t() + b.cpu().double()
     finally:
         _lib.check(_lib.lib().nos_gemm_f32x6_set_stage(0), "set_stage")
+        _lib.check(_lib.lib().nos_gemm_f32x6_set_tile(-1), "set_tile")
         ops.set_f32_math("exact")
     err = (y.cpu().double() - ref).abs().max().item()
     assert err < 1e-4 * max(1.0, ref.abs().max().item()), err

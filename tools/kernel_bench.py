@@ -53,10 +53,13 @@ def main():
     ap.add_argument("--persist", default="0", help="comma list of bf16 GEMM persistent grids (workgroups/CU, 0 = off)")
     ap.add_argument("--policies", default="latency", help="comma list of GEMM tile policies to A/B "
                     "(throughput, latency)")
+    ap.add_argument("--x6-tile", type=int, default=-1, help="x6 GEMM tile override (3: 128x64 4x1 waves)")
     ap.add_argument("--stage", type=int, default=0, help="x6 GEMM K-stage config (1: BK32 3-deep, 2: BK64)")
     ap.add_argument("--f32-math", default="exact", choices=["exact", "x6"], help="fp32 GEMM math (ops.set_f32_math)")
     a = ap.parse_args()
     ops.set_f32_math(a.f32_math)
+    if a.x6_tile >= 0:
+        ops._lib.check(ops._lib.lib().nos_gemm_f32x6_set_tile(a.x6_tile), "nos_gemm_f32x6_set_tile")
     if a.stage:
         ops._lib.check(ops._lib.lib().nos_gemm_f32x6_set_stage(a.stage), "nos_gemm_f32x6_set_stage")
     torch.manual_seed(0)
