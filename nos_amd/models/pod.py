@@ -145,7 +145,8 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
     (profiles/r03_f32x6_fleet_ab.json).  A whole-GPU pod splits the keys
     when its grid leaves CU slots empty (``x6``: batch-1 attention 164 -> 133
     us); fractional pods never split (``x6n``: the co-tenants fill the slots,
-    8 pods 410 vs 399 inf/s with the split).  ``NOS_AMD_F32_MATH=exact`` /
+    8 pods 410 vs 399 inf/s with the split) and run the x6 GEMMs on 128x64
+    tiles with 4 x 1 waves (445 vs 425 inf/s).  ``NOS_AMD_F32_MATH=exact`` /
     ``NOS_AMD_ATTN_F32_VARIANT=<tiling>`` select the exact-f32 MFMA kernels."""
     env = os.environ if env is None else env
     whole = memory_fraction is None or memory_fraction >= 0.99
@@ -156,7 +157,8 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
     return {"gemm_bf16": env.get("NOS_AMD_GEMM_POLICY") or ("latency" if whole else "throughput"),
             "gemm_f32": env.get("NOS_AMD_GEMM_F32_POLICY") or gf,
             "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or ("x6" if whole else "x6n"),
-            "f32_math": env.get("NOS_AMD_F32_MATH") or "x6"}
+            "f32_math": env.get("NOS_AMD_F32_MATH") or "x6",
+            "gemm_f32x6_tile": env.get("NOS_AMD_X6_TILE") or ("policy" if whole else "128x64")}
 
 
 def slice_cu_budget(env: dict | None = None) -> int:
@@ -206,7 +208,7 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             frac = apply_memory_limit(0)
             torch.backends.cuda.matmul.allow_tf32 = False  # true fp32 GEMMs (no reduced-precision shortcut)
             from ..ops import (set_attention_f32_variant, set_cu_budget, set_f32_math, set_gemm_f32_policy,
-                               set_gemm_policy)
+                               set_gemm_f32x6_tile, set_gemm_policy)
 
             budget = slice_cu_budget(os.environ)
             cfg = kernel_config(frac, os.environ, budget)
@@ -214,10 +216,7 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             set_gemm_f32_policy(cfg["gemm_f32"])
             set_attention_f32_variant(cfg["attention_f32"])
             set_f32_math(cfg["f32_math"])
-            if os.environ.get("NOS_AMD_X6_TILE"):  # A/B: x6 GEMM tile override (gemm_f32x.hip g_tile)
-                from ..ops import _lib
-
-                _lib.check(_lib.lib().nos_gemm_f32x6_set_tile(int(os.environ["NOS_AMD_X6_TILE"])), "set_tile")
+            set_gemm_f32x6_tile(cfg["gemm_f32x6_tile"])
             if budget:  # CU-mask slice: slice-sized persistent grids (ops.set_cu_budget)
                 set_cu_budget(budget)
         m, x = _build(dtype, seed, demo_input_hw(), device)

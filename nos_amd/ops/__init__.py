@@ -170,6 +170,13 @@ def f32_math() -> str:
     return _F32_MATH
 
 
+def set_gemm_f32x6_tile(tile: str) -> None:
+    """x6 GEMM tile: ``"policy"`` (the fp32 GEMM policy's tile) or ``"128x64"``
+    (4 x 1 waves: each wave splits one A block for both of its W blocks --
+    8 fractional pods 445 vs 425 inf/s, profiles/r03_f32x6_fleet_ab.json)."""
+    _lib.check(_lib.lib().nos_gemm_f32x6_set_tile({"policy": -1, "128x64": 3}[tile]), "nos_gemm_f32x6_set_tile")
+
+
 def split_bf16x3(t: torch.Tensor) -> torch.Tensor:
     """fp32 tensor -> [3, *t.shape] bf16 pieces with t == p0 + p1 + p2 exactly."""
     t = t.float()
@@ -436,5 +443,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_f32_math", "f32_math", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_f32_math", "f32_math", "set_gemm_f32x6_tile", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

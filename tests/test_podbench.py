@@ -137,13 +137,16 @@ def test_pod_kernel_config_follows_the_slice():
     from nos_amd.models.pod import kernel_config
 
     whole = kernel_config(None, {})
-    assert whole == {"gemm_bf16": "latency", "gemm_f32": "latency", "attention_f32": "x6", "f32_math": "x6"}
+    assert whole == {"gemm_bf16": "latency", "gemm_f32": "latency", "attention_f32": "x6", "f32_math": "x6",
+                     "gemm_f32x6_tile": "policy"}
     assert kernel_config(1.0, {}) == whole
     frac = kernel_config(36 / 288, {})
-    assert frac == {"gemm_bf16": "throughput", "gemm_f32": "small", "attention_f32": "x6n", "f32_math": "x6"}
+    assert frac == {"gemm_bf16": "throughput", "gemm_f32": "small", "attention_f32": "x6n", "f32_math": "x6",
+                    "gemm_f32x6_tile": "128x64"}
     # an exclusive CU-mask slice plans for its own CUs (budget-aware tiles)
     assert kernel_config(36 / 288, {}, cu_budget=32) == {"gemm_bf16": "throughput", "gemm_f32": "latency",
-                                                         "attention_f32": "x6n", "f32_math": "x6"}
+                                                         "attention_f32": "x6n", "f32_math": "x6",
+                                                         "gemm_f32x6_tile": "128x64"}
     assert kernel_config(None, {}, cu_budget=32) == whole
     # A/B overrides win over the slice rule: the exact-f32 MFMA kernels stay selectable
     assert kernel_config(0.125, {"NOS_AMD_ATTN_F32_VARIANT": "w4k64"})["attention_f32"] == "w4k64"
@@ -153,6 +156,6 @@ def test_pod_kernel_config_follows_the_slice():
     import inspect
 
     src = (inspect.getsource(ops.set_attention_f32_variant) + inspect.getsource(ops.set_gemm_f32_policy)
-           + inspect.getsource(ops.set_f32_math))
+           + inspect.getsource(ops.set_f32_math) + inspect.getsource(ops.set_gemm_f32x6_tile))
     for v in (*whole.values(), *frac.values()):
         assert f'"{v}"' in src or v in ("latency", "throughput")
