@@ -278,7 +278,9 @@ def with_trainer(d: Dist, envs: list[dict], args) -> list[dict]:
     port = int(d.reduce([float(_free_port()) if d.rank == 0 else 0.0], "max")[0])
     t = {**envs[0], "NOS_AMD_POD_KIND": "trainer", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
          "RANK": str(d.rank), "WORLD_SIZE": str(d.world), "LOCAL_RANK": "0",
-         "NOS_AMD_COLL_DIM": str(args.coll_dim), "NOS_AMD_COLL_BUCKET_MB": str(args.coll_bucket_mb)}
+         "NOS_AMD_COLL_DIM": str(args.coll_dim), "NOS_AMD_COLL_BUCKET_MB": str(args.coll_bucket_mb),
+         # a job that cannot form fails within 2 minutes: every rank then measures without it
+         "NOS_AMD_TRAINER_TIMEOUT_S": os.environ.get("NOS_AMD_TRAINER_TIMEOUT_S", "120")}
     if not d.cuda or os.environ.get("NOS_AMD_BENCH_FOLD_GPUS") == "1":
         t["NOS_AMD_TRAINER_BACKEND"] = "gloo"  # several ranks' trainers on one GPU: RCCL refuses that
     return [t] + list(envs[1:])
