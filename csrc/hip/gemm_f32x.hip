@@ -287,7 +287,8 @@ namespace {
 int g_stage = 0;
 // tile override (nos_gemm_f32x6_set_tile): -1 = the fp32 GEMM's tile policy,
 // 0 / 1 / 2 = 128x128 / 64x128 / 64x64 (2 x 2 waves), 3 = 128x64 (4 x 1 waves),
-// 4 = 128x64 where N >= 1024, the policy's tile elsewhere
+// 4 = 128x64 where N >= 1024, the policy's tile elsewhere, 5 = 128x128 (4 x 1
+// waves), 6 = 128x128 where N >= 1024, 128x64 elsewhere (4 x 1 waves)
 int g_tile = -1;
 
 int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
@@ -300,8 +301,9 @@ int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long
   if (!ln && (epi & EPI_BIAS) && !bias) return (int)hipErrorInvalidValue;
   if (ln && (!c1 || !c2)) return (int)hipErrorInvalidValue;
   if ((epi & EPI_RESID) && (!R || ldr < N)) return (int)hipErrorInvalidValue;
-  int cfg = g_tile >= 0 && g_tile != 4 ? g_tile : nos_gemm_f32_pick_tile(M, N);
+  int cfg = g_tile >= 0 && g_tile != 4 && g_tile != 6 ? g_tile : nos_gemm_f32_pick_tile(M, N);
   if (g_tile == 4 && N >= 1024) cfg = 3;  // 128x64 (4 x 1 waves) for the wide projections only
+  if (g_tile == 6) cfg = N >= 1024 ? 5 : 3;  // 128x128 / 128x64, 4 x 1 waves
   const int stg = (g_stage == 2 && K % 64 != 0) ? 0 : g_stage;
 #define NOS_F32X_LAUNCH(LNV, BMV, BNV, RSV, BKV) \
   launch_t<LNV, BMV, BNV, RSV, BKV>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, st)
@@ -310,6 +312,9 @@ int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long
   if (cfg == 3)                                                                                    \
     return launch_t<LNV, 128, 64, 2, 32, 4>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, \
                                             eps, st);                                              \
+  if (cfg == 5)                                                                                    \
+    return launch_t<LNV, 128, 128, 2, 32, 4>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K,    \
+                                             epi, eps, st);                                        \
   if (cfg == 1) {                                                                                  \
     if (stg == 1) return NOS_F32X_LAUNCH(LNV, 64, 128, 3, 32);                                    \
     if (stg == 2) return NOS_F32X_LAUNCH(LNV, 64, 128, 2, 64);                                    \
@@ -329,7 +334,7 @@ int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long
 }  // namespace
 
 NOS_API int nos_gemm_f32x6_set_tile(int tile) {
-  if (tile < -1 || tile > 4) return (int)hipErrorInvalidValue;
+  if (tile < -1 || tile > 6) return (int)hipErrorInvalidValue;
   g_tile = tile;
   return 0;
 }

@@ -145,8 +145,8 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
     (profiles/r03_f32x6_fleet_ab.json).  A whole-GPU pod splits the keys
     when its grid leaves CU slots empty (``x6``: batch-1 attention 164 -> 133
     us); fractional pods never split (``x6n``: the co-tenants fill the slots,
-    8 pods 410 vs 399 inf/s with the split) and run the x6 GEMMs on 128x64
-    tiles with 4 x 1 waves (445 vs 425 inf/s).  ``NOS_AMD_F32_MATH=exact`` /
+    8 pods 410 vs 399 inf/s with the split) and run the x6 GEMMs on 128x128
+    tiles with 4 x 1 waves (466 vs 448 for 128x64 and 425 for 64x64 tiles).  ``NOS_AMD_F32_MATH=exact`` /
     ``NOS_AMD_ATTN_F32_VARIANT=<tiling>`` select the exact-f32 MFMA kernels."""
     env = os.environ if env is None else env
     whole = memory_fraction is None or memory_fraction >= 0.99
@@ -158,7 +158,7 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
             "gemm_f32": env.get("NOS_AMD_GEMM_F32_POLICY") or gf,
             "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or ("x6" if whole else "x6n"),
             "f32_math": env.get("NOS_AMD_F32_MATH") or "x6",
-            "gemm_f32x6_tile": env.get("NOS_AMD_X6_TILE") or ("policy" if whole else "128x64")}
+            "gemm_f32x6_tile": env.get("NOS_AMD_X6_TILE") or ("policy" if whole else "128x128")}
 
 
 def slice_cu_budget(env: dict | None = None) -> int:

@@ -171,10 +171,14 @@ def f32_math() -> str:
 
 
 def set_gemm_f32x6_tile(tile: str) -> None:
-    """x6 GEMM tile: ``"policy"`` (the fp32 GEMM policy's tile) or ``"128x64"``
-    (4 x 1 waves: each wave splits one A block for both of its W blocks --
-    8 fractional pods 445 vs 425 inf/s, profiles/r03_f32x6_fleet_ab.json)."""
-    _lib.check(_lib.lib().nos_gemm_f32x6_set_tile({"policy": -1, "128x64": 3}[tile]), "nos_gemm_f32x6_set_tile")
+    """x6 GEMM tile: ``"policy"`` (the fp32 GEMM policy's tile), ``"128x64"`` or
+    ``"128x128"`` (4 x 1 waves: each wave splits one A block for all of its W
+    blocks -- 8 fractional pods 425 (64x64) -> 448 (128x64) -> 466 (128x128)
+    inf/s, profiles/r03_f32x6_fleet_ab.json), ``"wide"`` (128x128 where
+    N >= 1024, else 128x64)."""
+    names = {"policy": -1, "128x64": 3, "128x128": 5, "wide": 6}  # wide: 128x128 if N >= 1024, else 128x64
+    code = names[tile] if tile in names else int(tile)  # numeric codes: gemm_f32x.hip g_tile (A/B)
+    _lib.check(_lib.lib().nos_gemm_f32x6_set_tile(code), "nos_gemm_f32x6_set_tile")
 
 
 def split_bf16x3(t: torch.Tensor) -> torch.Tensor:
