@@ -27,7 +27,6 @@
 
 namespace {
 
-constexpr int NT = 256;
 enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
 
 // LDS images of one K stage of BK (32 or 64): the fp32 A rows (AROW bytes,
@@ -78,21 +77,23 @@ __device__ __forceinline__ void wait_stages(int n) {
 }
 
 
-template <bool LN, int BM, int BN, bool PERSIST, int RS, int BK, int WGM = 2>
-__global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
+// WGM x WGN waves per workgroup (4 or 8); NT threads
+template <bool LN, int BM, int BN, bool PERSIST, int RS, int BK, int WGM = 2, int WGN = 2>
+__global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_f32x6_kernel(
     const float* __restrict__ A, int lda, const unsigned short* __restrict__ Wp, int ldw, long long wplane,
     const float* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
     const float* __restrict__ R, int ldr, float* __restrict__ C, int ldc, int M, int N, int K, int epi, float eps,
     int tiles_m, int tiles_n) {
+  // waves WGM x WGN over the tile, each (BM/WGM) x (BN/WGN) as 32x32 blocks;
+  // WGM x 1 makes every wave split ONE A block for all its W blocks
+  constexpr int NW = WGM * WGN, NT = 64 * NW, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
+  static_assert(MI >= 1 && NI >= 1 && (NW == 4 || NW == 8), "wave layout");
   using L = Lay<BK>;
   constexpr int AROW = L::AROW, WROW = L::WROW, ACH = L::ACH, WCH = L::WCH;
   constexpr int TA = BM * AROW, TWP = BN * WROW, STAGE = TA + 3 * TWP;
-  constexpr int APW = BM * AROW / 1024 / 4, WPW = 3 * BN * WROW / 1024 / 4;  // DMA pieces per wave
-  static_assert((BM * AROW / 1024) % 4 == 0 && (3 * BN * WROW / 1024) % 4 == 0, "equal DMA count per wave");
-  // waves WGM x WGN over the tile, each (BM/WGM) x (BN/WGN) as 32x32 blocks;
-  // 4 x 1 makes every wave split ONE A block for all its W blocks
-  constexpr int WGN = 4 / WGM, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
-  static_assert(MI >= 1 && NI >= 1 && WGM * WGN == 4, "wave layout");
+  constexpr int APW = BM * AROW / 1024 / NW, WPW = 3 * BN * WROW / 1024 / NW;  // DMA pieces per wave
+  static_assert((BM * AROW / 1024) % NW == 0 && (3 * BN * WROW / 1024) % NW == 0, "equal DMA count per wave");
+  static_assert(NT % BM == 0 && BK % (4 * (NT / BM)) == 0, "LayerNorm statistics: whole float4s per thread");
   constexpr int S = RS, LPS = APW + WPW;
   static_assert(S >= 2 && S <= 4 && (S - 1) * LPS < 64, "ring depth / vmcnt range");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32x6_kernel(
   }  // tiles
 }
 
-template <bool LN, int BM, int BN, int RS, int BK, int WGM = 2>
+template <bool LN, int BM, int BN, int RS, int BK, int WGM = 2, int WGN = 2>
 int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
              const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K,
              int epi, float eps, hipStream_t st) {
@@ -266,12 +267,13 @@ int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long lo
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
   const size_t ring = RS * (size_t)(BM * Lay<BK>::AROW + 3 * BN * Lay<BK>::WROW);
   const size_t lds = ring > 2 * BM * sizeof(float) ? ring : 2 * BM * sizeof(float);
-  const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM>, NT, lds, ntiles);
+  constexpr int NT = 64 * WGM * WGN;
+  const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM, WGN>, NT, lds, ntiles);
   if (grid < ntiles)
-    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM>), dim3((unsigned)grid), dim3(NT), lds, st, A,
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM, WGN>), dim3((unsigned)grid), dim3(NT), lds, st, A,
                        lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
   else
-    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false, RS, BK, WGM>), dim3((unsigned)ntiles), dim3(NT), lds, st, A,
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false, RS, BK, WGM, WGN>), dim3((unsigned)ntiles), dim3(NT), lds, st, A,
                        lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
   return (int)hipGetLastError();
 }
@@ -288,7 +290,8 @@ int g_stage = 0;
 // tile override (nos_gemm_f32x6_set_tile): -1 = the fp32 GEMM's tile policy,
 // 0 / 1 / 2 = 128x128 / 64x128 / 64x64 (2 x 2 waves), 3 = 128x64 (4 x 1 waves),
 // 4 = 128x64 where N >= 1024, the policy's tile elsewhere, 5 = 128x128 (4 x 1
-// waves), 6 = 128x128 where N >= 1024, 128x64 elsewhere (4 x 1 waves)
+// waves), 6 = 128x128 where N >= 1024, 128x64 elsewhere (4 x 1 waves),
+// 7 = 256x128 (8 x 1 waves)
 int g_tile = -1;
 
 int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
@@ -310,10 +313,13 @@ int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long
 #define NOS_F32X_TILES(LNV)                                                                        \
   if (cfg == 0) return NOS_F32X_LAUNCH(LNV, 128, 128, 2, 32);                                     \
   if (cfg == 3)                                                                                    \
-    return launch_t<LNV, 128, 64, 2, 32, 4>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, \
+    return launch_t<LNV, 128, 64, 2, 32, 4, 1>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, \
                                             eps, st);                                              \
+  if (cfg == 7)                                                                                    \
+    return launch_t<LNV, 256, 128, 2, 32, 8, 1>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K,  \
+                                                epi, eps, st);                                     \
   if (cfg == 5)                                                                                    \
-    return launch_t<LNV, 128, 128, 2, 32, 4>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K,    \
+    return launch_t<LNV, 128, 128, 2, 32, 4, 1>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K,    \
                                              epi, eps, st);                                        \
   if (cfg == 1) {                                                                                  \
     if (stg == 1) return NOS_F32X_LAUNCH(LNV, 64, 128, 3, 32);                                    \
@@ -334,7 +340,7 @@ int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long
 }  // namespace
 
 NOS_API int nos_gemm_f32x6_set_tile(int tile) {
-  if (tile < -1 || tile > 6) return (int)hipErrorInvalidValue;
+  if (tile < -1 || tile > 7) return (int)hipErrorInvalidValue;
   g_tile = tile;
   return 0;
 }

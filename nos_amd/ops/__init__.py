@@ -176,7 +176,7 @@ def set_gemm_f32x6_tile(tile: str) -> None:
     blocks -- 8 fractional pods 425 (64x64) -> 448 (128x64) -> 466 (128x128)
     inf/s, profiles/r03_f32x6_fleet_ab.json), ``"wide"`` (128x128 where
     N >= 1024, else 128x64)."""
-    names = {"policy": -1, "128x64": 3, "128x128": 5, "wide": 6}  # wide: 128x128 if N >= 1024, else 128x64
+    names = {"policy": -1, "128x64": 3, "128x128": 5, "wide": 6, "256x128": 7}  # wide: 128x128 if N >= 1024, else 128x64
     code = names[tile] if tile in names else int(tile)  # numeric codes: gemm_f32x.hip g_tile (A/B)
     _lib.check(_lib.lib().nos_gemm_f32x6_set_tile(code), "nos_gemm_f32x6_set_tile")
 

@@ -198,7 +198,7 @@ def test_linear_fp32_split_is_as_accurate_as_exact_f32(M, N, K):
     assert errs["x6"][0] <= 1.5 * errs["exact"][0] and errs["x6"][1] <= 1.5 * errs["exact"][1], errs
 
 
-@pytest.mark.parametrize("stage,tile", [(1, -1), (2, -1), (0, 3), (0, 5)])
+@pytest.mark.parametrize("stage,tile", [(1, -1), (2, -1), (0, 3), (0, 5), (0, 7)])
 @pytest.mark.parametrize("M,N,K,ln", [(3401, 1152, 384, True), (3401, 384, 1536, False), (257, 200, 96, False),
                                       (100, 92, 384, True)])
 def test_linear_fp32_split_stage_configs(stage, tile, M, N, K, ln):
