@@ -395,25 +395,32 @@ NOS_API long long nos_attn_f32x6_workspace(int B, int H, int Sq, int Skv) {
 
 // The exact-fp32 kernel's contract (attention_f32.hip: nos_attn_fwd_f32_d64)
 // plus a workspace of nos_attn_f32x6_workspace() bytes (16-byte aligned).
-NOS_API int nos_attn_fwd_f32x6_d64(const float* q, const float* k, const float* v, float* o, int B, int H, int Sq,
-                                   int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float scale,
-                                   void* ws, long long ws_bytes, hipStream_t stream) {
+namespace {
+
+// shared argument checks of the two entries; 0 = ok
+int check_args(const void* q, const void* o, const void* ws, long long ws_bytes, int B, int H, int Sq, int Skv,
+               int ld_in, long long bs_in, int ld_out, long long bs_out) {
   if (B <= 0 || H <= 0 || Sq <= 0 || Skv <= 0) return (int)hipErrorInvalidValue;
   if (ld_in < H * D || ld_out < H * D || (ld_in & 3) || (ld_out & 3) || (bs_in & 3) || (bs_out & 3))
     return (int)hipErrorInvalidValue;
-  if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o | (uintptr_t)ws) & 15) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)q | (uintptr_t)o | (uintptr_t)ws) & 15) return (int)hipErrorInvalidValue;
   if (ws == nullptr || ws_bytes < nos_attn_f32x6_workspace(B, H, Sq, Skv)) return (int)hipErrorInvalidValue;
+  const long long skvp = (Skv + KVB - 1) / KVB * KVB;
+  if ((long long)B * H * ((Sq + QBLK - 1) / QBLK) > (1LL << 28) || (long long)B * skvp * 2 * H * 8 > INT_MAX ||
+      skvp * 6 * H * D > INT_MAX)
+    return (int)hipErrorInvalidValue;
+  return 0;
+}
+
+// the attention proper, from the six planes at the start of ws
+int run_from_planes(const float* q, float* o, int B, int H, int Sq, int Skv, int ld_in, long long bs_in, int ld_out,
+                    long long bs_out, float scale, void* ws, hipStream_t stream) {
   const float c = scale * 1.4426950408889634f;
   const int nqb = (Sq + QBLK - 1) / QBLK;
   const long long nwg = (long long)B * H * nqb;
-  if (nwg > (1LL << 30)) return (int)hipErrorInvalidValue;
   const int skvp = (Skv + KVB - 1) / KVB * KVB;
-  const long long n8 = (long long)B * skvp * 2 * H * 8;
-  if (n8 > INT_MAX || (long long)skvp * 6 * H * D > INT_MAX) return (int)hipErrorInvalidValue;
-  auto* kvs = static_cast<unsigned short*>(ws);
-  hipLaunchKernelGGL(split_kv_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, stream, k, v, kvs, Skv, skvp,
-                     H, ld_in, bs_in, (int)n8);
   const int nsplit = pick_split(nwg, skvp / KVB);
+  auto* kvs = static_cast<unsigned short*>(ws);
   float* part = reinterpret_cast<float*>(static_cast<unsigned char*>(ws) +
                                          ((long long)B * skvp * 6 * H * D * 2 + 15) / 16 * 16);
   const int rc = launch(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb, nsplit, part, stream);
@@ -422,4 +429,37 @@ NOS_API int nos_attn_fwd_f32x6_d64(const float* q, const float* k, const float* 
   hipLaunchKernelGGL(merge_splits_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, part, o, B, H, Sq,
                      nsplit, ld_out, bs_out, n4);
   return (int)hipGetLastError();
+}
+
+}  // namespace
+
+NOS_API int nos_attn_fwd_f32x6_d64(const float* q, const float* k, const float* v, float* o, int B, int H, int Sq,
+                                   int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float scale,
+                                   void* ws, long long ws_bytes, hipStream_t stream) {
+  if (int rc = check_args(q, o, ws, ws_bytes, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out)) return rc;
+  if (((uintptr_t)k | (uintptr_t)v) & 15) return (int)hipErrorInvalidValue;
+  const int skvp = (Skv + KVB - 1) / KVB * KVB;
+  const long long n8 = (long long)B * skvp * 2 * H * 8;
+  hipLaunchKernelGGL(split_kv_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, stream, k, v,
+                     static_cast<unsigned short*>(ws), Skv, skvp, H, ld_in, bs_in, (int)n8);
+  return run_from_planes(q, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, scale, ws, stream);
+}
+
+// The same attention when the K/V planes are already at the start of ws
+// (written by the QKV projection's epilogue, nos_gemm_ln_f32x6_qkv): only the
+// padding rows of every batch are zeroed here.
+NOS_API int nos_attn_fwd_f32x6_presplit_d64(const float* q, float* o, int B, int H, int Sq, int Skv, int ld_in,
+                                            long long bs_in, int ld_out, long long bs_out, float scale, void* ws,
+                                            long long ws_bytes, hipStream_t stream) {
+  if (int rc = check_args(q, o, ws, ws_bytes, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out)) return rc;
+  const int skvp = (Skv + KVB - 1) / KVB * KVB;
+  if (skvp > Skv) {
+    const size_t row_bytes = (size_t)6 * H * D * 2;
+    for (int b = 0; b < B; ++b) {
+      unsigned char* pad = static_cast<unsigned char*>(ws) + ((size_t)b * skvp + Skv) * row_bytes;
+      const hipError_t e = hipMemsetAsync(pad, 0, (size_t)(skvp - Skv) * row_bytes, stream);
+      if (e != hipSuccess) return (int)e;
+    }
+  }
+  return run_from_planes(q, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, scale, ws, stream);
 }

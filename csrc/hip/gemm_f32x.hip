@@ -77,13 +77,27 @@ __device__ __forceinline__ void wait_stages(int n) {
 }
 
 
+// Optional second output of the fused-LN QKV projection: columns >= qcols (K
+// then V, hd = H * 64 each) are written as the six bf16 planes the bf16x6
+// attention reads (attention_f32x.hip: kvs[b][s][plane][hd], rows padded to
+// skvp per batch), exactly the split its streaming kernel would make, so the
+// fp32 K/V never go to memory; the Q columns go to C as usual.
+struct KvOut {
+  unsigned short* kvs = nullptr;
+  int qcols = 0, hd = 0, S = 0, skvp = 0;
+};
+
+__device__ __forceinline__ unsigned short bf16_bits(float x) {
+  return __builtin_bit_cast(unsigned short, (__bf16)x);
+}
+
 // WGM x WGN waves per workgroup (4 or 8); NT threads
 template <bool LN, int BM, int BN, bool PERSIST, int RS, int BK, int WGM = 2, int WGN = 2>
 __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_f32x6_kernel(
     const float* __restrict__ A, int lda, const unsigned short* __restrict__ Wp, int ldw, long long wplane,
     const float* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
     const float* __restrict__ R, int ldr, float* __restrict__ C, int ldc, int M, int N, int K, int epi, float eps,
-    int tiles_m, int tiles_n) {
+    int tiles_m, int tiles_n, KvOut kv) {
   // waves WGM x WGN over the tile, each (BM/WGM) x (BN/WGN) as 32x32 blocks;
   // WGM x 1 makes every wave split ONE A block for all its W blocks
   constexpr int NW = WGM * WGN, NT = 64 * NW, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
@@ -250,7 +264,21 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_f3
         if (epi & EPI_RELU) v = fmaxf(v, 0.f);
         if (m < M && n < N) {
           if (epi & EPI_RESID) v += R[(long long)m * ldr + n];
-          C[(long long)m * ldc + n] = v;
+          if (kv.kvs != nullptr && n >= kv.qcols) {
+            const int t = (n - kv.qcols) >= kv.hd;  // 0: K, 1: V
+            const int col = n - kv.qcols - t * kv.hd;
+            const int b = kv.S == M ? 0 : m / kv.S;
+            const long long row = (long long)b * kv.skvp + (m - b * kv.S);
+            unsigned short* dst = kv.kvs + (row * 6 + 3 * t) * kv.hd + col;
+            const __bf16 p0 = (__bf16)v;
+            const float r1 = v - (float)p0;
+            const __bf16 p1 = (__bf16)r1;
+            dst[0] = __builtin_bit_cast(unsigned short, p0);
+            dst[kv.hd] = __builtin_bit_cast(unsigned short, p1);
+            dst[2 * kv.hd] = bf16_bits(r1 - (float)p1);
+          } else {
+            C[(long long)m * ldc + n] = v;
+          }
         }
       }
     }
@@ -261,7 +289,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_f3
 template <bool LN, int BM, int BN, int RS, int BK, int WGM = 2, int WGN = 2>
 int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
              const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K,
-             int epi, float eps, hipStream_t st) {
+             int epi, float eps, hipStream_t st, KvOut kv) {
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const long long ntiles = (long long)tiles_m * tiles_n;
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
@@ -271,10 +299,10 @@ int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long lo
   const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM, WGN>, NT, lds, ntiles);
   if (grid < ntiles)
     hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM, WGN>), dim3((unsigned)grid), dim3(NT), lds, st, A,
-                       lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+                       lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n, kv);
   else
     hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false, RS, BK, WGM, WGN>), dim3((unsigned)ntiles), dim3(NT), lds, st, A,
-                       lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n);
+                       lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n, kv);
   return (int)hipGetLastError();
 }
 
@@ -296,7 +324,7 @@ int g_tile = -1;
 
 int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
            const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi,
-           float eps, bool ln, hipStream_t st) {
+           float eps, bool ln, hipStream_t st, KvOut kv = KvOut()) {
   if (M <= 0 || N <= 0 || K <= 0 || (K % 32) != 0) return (int)hipErrorInvalidValue;
   if ((lda % 4) || (ldw % 8) || (wplane % 8) || lda < K || ldw < K || ldc < N || wplane < (long long)N * ldw)
     return (int)hipErrorInvalidValue;
@@ -309,18 +337,18 @@ int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long
   if (g_tile == 6) cfg = N >= 1024 ? 5 : 3;  // 128x128 / 128x64, 4 x 1 waves
   const int stg = (g_stage == 2 && K % 64 != 0) ? 0 : g_stage;
 #define NOS_F32X_LAUNCH(LNV, BMV, BNV, RSV, BKV) \
-  launch_t<LNV, BMV, BNV, RSV, BKV>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, st)
+  launch_t<LNV, BMV, BNV, RSV, BKV>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, st, kv)
 #define NOS_F32X_TILES(LNV)                                                                        \
   if (cfg == 0) return NOS_F32X_LAUNCH(LNV, 128, 128, 2, 32);                                     \
   if (cfg == 3)                                                                                    \
     return launch_t<LNV, 128, 64, 2, 32, 4, 1>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, \
-                                            eps, st);                                              \
+                                            eps, st, kv);                                              \
   if (cfg == 7)                                                                                    \
     return launch_t<LNV, 256, 128, 2, 32, 8, 1>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K,  \
-                                                epi, eps, st);                                     \
+                                                epi, eps, st, kv);                                     \
   if (cfg == 5)                                                                                    \
     return launch_t<LNV, 128, 128, 2, 32, 4, 1>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K,    \
-                                             epi, eps, st);                                        \
+                                             epi, eps, st, kv);                                        \
   if (cfg == 1) {                                                                                  \
     if (stg == 1) return NOS_F32X_LAUNCH(LNV, 64, 128, 3, 32);                                    \
     if (stg == 2) return NOS_F32X_LAUNCH(LNV, 64, 128, 2, 64);                                    \
@@ -367,4 +395,24 @@ NOS_API int nos_gemm_ln_f32x6(const float* A, int lda, const void* Wp, int ldw, 
                               hipStream_t stream) {
   return launch(A, lda, static_cast<const unsigned short*>(Wp), ldw, wplane, nullptr, c1, c2, nullptr, 0, C, ldc, M,
                 N, K, epi & ~(EPI_BIAS | EPI_RESID), eps, true, stream);
+}
+
+// The fused-LN QKV projection whose K / V columns (N = 3 * hd) are written as
+// the bf16x6 attention's planes at kvs (nos_attn_f32x6_workspace layout,
+// S rows per batch padded to skvp); Q goes to C[:, :hd].  The attention then
+// runs from the planes (nos_attn_fwd_f32x6_presplit_d64): no fp32 K/V store,
+// no streaming split.
+NOS_API int nos_gemm_ln_f32x6_qkv(const float* A, int lda, const void* Wp, int ldw, long long wplane,
+                                  const float* c1, const float* c2, float* C, int ldc, int M, int N, int K, int epi,
+                                  float eps, void* kvs, int S, int skvp, hipStream_t stream) {
+  if (kvs == nullptr || N % 3 != 0 || S <= 0 || M % S != 0 || skvp < S || (((uintptr_t)kvs) & 15))
+    return (int)hipErrorInvalidValue;
+  KvOut kv;
+  kv.kvs = static_cast<unsigned short*>(kvs);
+  kv.hd = N / 3;
+  kv.qcols = kv.hd;
+  kv.S = S;
+  kv.skvp = skvp;
+  return launch(A, lda, static_cast<const unsigned short*>(Wp), ldw, wplane, nullptr, c1, c2, nullptr, 0, C, ldc, M,
+                N, K, epi & ~(EPI_BIAS | EPI_RESID), eps, true, stream, kv);
 }

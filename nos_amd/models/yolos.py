@@ -230,9 +230,17 @@ class YolosDetector(nn.Module):
 
         folded = self.folded_weights()
         h = self._embed(pixel_values, lin)
+        # fp32 under x6 math: the QKV projection writes K / V as the attention's
+        # bf16 planes directly (no fp32 K/V round trip, no split kernel)
+        presplit = (h.is_cuda and h.dtype == torch.float32 and ops.f32_math() == "x6"
+                    and ops.attention_f32_variant().startswith("x6"))
         for L, fw in zip(self.layers, folded):
-            qkv = ops.linear_ln(h, fw["qkv_w"], fw["qkv_c1"], fw["qkv_c2"], eps=eps)
-            a = ops.attention_qkv(qkv, nh)
+            if presplit:
+                qkv, ws = ops.linear_ln_qkv_x6(h, fw["qkv_w"], fw["qkv_c1"], fw["qkv_c2"], nh, eps=eps)
+                a = ops.attention_presplit(qkv, ws, nh)
+            else:
+                qkv = ops.linear_ln(h, fw["qkv_w"], fw["qkv_c1"], fw["qkv_c2"], eps=eps)
+                a = ops.attention_qkv(qkv, nh)
             h = ops.linear(a, L.proj_w, L.proj_b, residual=h)
             m = ops.linear_ln(h, fw["fc1_w"], fw["fc1_c1"], fw["fc1_c2"], act="gelu", eps=eps)
             h = ops.linear(m, L.fc2_w, L.fc2_b, residual=h)

@@ -423,6 +423,56 @@ def attention_qkv(qkv: torch.Tensor, num_heads: int, out: torch.Tensor | None = 
     return out
 
 
+def linear_ln_qkv_x6(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, num_heads: int,
+                     eps: float = 1e-12) -> tuple[torch.Tensor, torch.Tensor]:
+    """The fused-LayerNorm QKV projection of an fp32 pod under x6 math, with
+    its K / V columns written straight into the bf16x6 attention's plane
+    workspace (``nos_gemm_ln_f32x6_qkv``): returns (qkv [B, S, 3*H*64] whose
+    Q columns are valid, workspace) for :func:`attention_presplit`.  The
+    planes are exactly the split the attention's own streaming kernel makes:
+    the result equals ``attention_qkv(linear_ln(...))`` bit for bit."""
+    B, S, K = x.shape
+    N = wg.shape[0]
+    D = 64
+    if N != 3 * num_heads * D or x.dtype != torch.float32 or not x.is_cuda:
+        raise ValueError("linear_ln_qkv_x6: fp32 CUDA input and a [3*H*64, K] projection")
+    _check_f32(x=x, weight=wg, c1=c1, c2=c2)
+    if K % 32:
+        raise ValueError("linear_ln_qkv_x6 needs K % 32 == 0")
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    out = torch.empty((B, S, N), dtype=torch.float32, device=x.device)
+    L = _lib.lib()
+    nbytes = int(L.nos_attn_f32x6_workspace(B, num_heads, S, S))
+    ws = torch.empty(nbytes // 2, dtype=torch.int16, device=x.device)
+    skvp = (S + 31) // 32 * 32
+    wp = split_f32_weight(wg)
+    rc = L.nos_gemm_ln_f32x6_qkv(x2.data_ptr(), x2.stride(0), wp.data_ptr(), wp.stride(1), wp.stride(0),
+                                 c1.data_ptr(), c2.data_ptr(), out.data_ptr(), N, M, N, K, 0, float(eps),
+                                 ws.data_ptr(), S, skvp, _stream())
+    _lib.check(rc, "nos_gemm_ln_f32x6_qkv")
+    return out, ws
+
+
+def attention_presplit(qkv: torch.Tensor, ws: torch.Tensor, num_heads: int, scale: float | None = None,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+    """bf16x6 attention from the planes :func:`linear_ln_qkv_x6` wrote (the Q
+    columns of ``qkv`` are read)."""
+    B, S, three_hd = qkv.shape
+    hd = three_hd // 3
+    if out is None:
+        out = torch.empty((B, S, hd), dtype=torch.float32, device=qkv.device)
+    if out.dtype != torch.float32 or out.stride(-1) != 1 or out.shape != (B, S, hd):
+        raise ValueError("out must be [B, S, H*64] fp32 with unit inner stride")
+    scale = scale if scale is not None else 1.0 / math.sqrt(64)
+    rc = _lib.lib().nos_attn_fwd_f32x6_presplit_d64(qkv.data_ptr(), out.data_ptr(), B, num_heads, S, S,
+                                                    qkv.stride(1), qkv.stride(0), out.stride(1), out.stride(0),
+                                                    float(scale), ws.data_ptr(), ws.numel() * ws.element_size(),
+                                                    _stream())
+    _lib.check(rc, "nos_attn_fwd_f32x6_presplit_d64")
+    return out
+
+
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None,
               out: torch.Tensor | None = None) -> torch.Tensor:
     """q,k,v [B, S, H, 64] (rows contiguous per token) -> [B, Sq, H, 64]."""
@@ -447,5 +497,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_f32_math", "f32_math", "set_gemm_f32x6_tile", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_f32_math", "f32_math", "set_gemm_f32x6_tile", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

@@ -31,6 +31,10 @@ _SIGS = {
     "nos_attn_fwd_f32x6_d64": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                c_ll, c_int, c_ll, c_float, c_void_p, c_ll, c_void_p],
     "nos_attn_f32x6_workspace": [c_int, c_int, c_int, c_int],
+    "nos_attn_fwd_f32x6_presplit_d64": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_ll, c_int, c_ll,
+                                        c_float, c_void_p, c_ll, c_void_p],
+    "nos_gemm_ln_f32x6_qkv": [c_void_p, c_int, c_void_p, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                              c_int, c_int, c_int, c_float, c_void_p, c_int, c_int, c_void_p],
     "nos_attn_f32x6_set_kvsplit": [c_int],
     "nos_gemm_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],

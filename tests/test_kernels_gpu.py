@@ -443,3 +443,29 @@ def test_slice_sized_persistent_grids_are_bit_identical(budget):
         ops.set_cu_budget(0)
     for a, c in zip(ref, got):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("B,S,H", [(1, 3401, 6), (2, 77, 3), (3, 33, 2)])
+@pytest.mark.parametrize("variant", ["x6n", "x6"])
+def test_qkv_projection_writing_the_attention_planes_is_bit_identical(B, S, H, variant):
+    """LN-QKV GEMM whose epilogue writes K/V as the bf16x6 attention's planes
+    (no fp32 K/V, no split kernel) == the unfused LN GEMM + x6 attention, bit
+    for bit (the same pieces of the same fp32 values), padding rows between
+    batches included."""
+    torch.manual_seed(B * S)
+    K = 384
+    x = torch.randn(B, S, K, device=DEV) * 2 + 0.5
+    w = torch.randn(3 * H * 64, K, device=DEV) * 0.05
+    b = torch.randn(3 * H * 64, device=DEV)
+    wg, c1, c2 = ops.fold_layernorm(w, b, torch.randn(K, device=DEV), torch.randn(K, device=DEV))
+    ops.set_f32_math("x6")
+    ops.set_attention_f32_variant(variant)
+    try:
+        ref = ops.attention_qkv(ops.linear_ln(x, wg, c1, c2), H)
+        qkv, ws = ops.linear_ln_qkv_x6(x, wg, c1, c2, H)
+        got = ops.attention_presplit(qkv, ws, H)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_f32_math("exact")
+        ops.set_attention_f32_variant("auto")
+    assert torch.equal(got, ref)
