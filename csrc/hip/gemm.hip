@@ -189,7 +189,11 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[CF::MI][CF::
   // the 8-wave tiles (MI = 4) from spilling
   const bool rvec = RESID && vec_ok && N >= 8;
   const int nmax = N >= 8 ? ((N - 8) >> 3) << 3 : 0;
-  s16x8_t rpre[2][NB][2];
+  // prefetch depth: the 256x256 tile (8 waves, MI = 4) keeps ONE group of
+  // residual rows live (issued at the start of its own group) -- two spilled
+  // 4 VGPRs / 20 B of scratch there
+  constexpr int RPD = (CF::NW > 4 && MI >= 4) ? 1 : 2;
+  s16x8_t rpre[RPD][NB][2];
   auto rload = [&](int mi) {
     const int m = min(m0 + wm * WM + mi * 32 + r, M - 1);
 #pragma unroll
@@ -197,13 +201,14 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[CF::MI][CF::
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         const int n = min(n0 + wn * WN + ni * 32 + 16 * pr + 8 * hh, nmax);
-        rpre[mi & 1][ni][pr] = *reinterpret_cast<const s16x8_t*>(R + (long long)m * ldr + n);
+        rpre[mi % RPD][ni][pr] = *reinterpret_cast<const s16x8_t*>(R + (long long)m * ldr + n);
       }
   };
   if (rvec) rload(0);
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
-      if (rvec && mi + 1 < MI) rload(mi + 1);
+      if (RPD == 1 && rvec && mi > 0) rload(mi);
+      if (RPD == 2 && rvec && mi + 1 < MI) rload(mi + 1);
       const int rl = wm * WM + mi * 32 + r;
       const int m = m0 + rl;
       float mu = 0.f, rs = 1.f;
@@ -251,7 +256,7 @@ __device__ __forceinline__ void epilogue_rows(const f32x16_t (&acc)[CF::MI][CF::
           if (m >= M || n >= N) continue;
           if (n + 8 <= N && vec_ok) {
             if constexpr (RESID) {
-              const s16x8_t rv = rpre[mi & 1][ni][pr];
+              const s16x8_t rv = rpre[mi % RPD][ni][pr];
 #pragma unroll
               for (int e = 0; e < 8; ++e) v[e] += nos::bf16_to_f32((unsigned short)rv[e]);
             }
@@ -329,10 +334,14 @@ __global__ __launch_bounds__(CF::NT, CF::MINB) void gemm_bf16_rk_kernel(
       s_par[par * 2 * BN + BN + tid] = LN ? c2[n] : ((epi & EPI_BIAS) ? nos::bf16_to_f32(bias[n]) : 0.f);
     }
   };
+  // the staging lane index is re-derived per tile through an opaque copy:
+  // hoisted to kernel entry, the lane-constant staging offsets of the 8-wave
+  // LN tiles stayed live around the tile loop and spilled (10 VGPRs)
+  int lane_st = lane;
   auto stage = [&](int m0, int n0, int kt) {
     unsigned char* buf = smem + (kt % S) * STAGE_BYTES;
-    stage_tile<BM, NW, BK>(A, lda, m0, M, kt * BK, buf, wid, lane);
-    stage_tile<BN, NW, BK>(W, ldw, n0, N, kt * BK, buf + TILE_A_BYTES, wid, lane);
+    stage_tile<BM, NW, BK>(A, lda, m0, M, kt * BK, buf, wid, lane_st);
+    stage_tile<BN, NW, BK>(W, ldw, n0, N, kt * BK, buf + TILE_A_BYTES, wid, lane_st);
   };
   // the first S K-slices of a tile (the whole ring is free)
   auto prologue = [&](int m0, int n0) {
@@ -349,6 +358,7 @@ __global__ __launch_bounds__(CF::NT, CF::MINB) void gemm_bf16_rk_kernel(
   prologue(m0, n0);
 
   for (int it = 1;; ++it) {
+    asm volatile("" : "+v"(lane_st));
     f32x16_t acc[MI][NB];
 #pragma unroll
     for (int a = 0; a < MI; ++a)
