@@ -69,11 +69,16 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--step-s", type=float, default=0.6, help="wall seconds per timed step")
-    ap.add_argument("--pods-per-gpu", type=int, default=8)
-    ap.add_argument("--slice-gb", type=int, default=36, help="GPU memory per fractional pod")
-    ap.add_argument("--mode", choices=["shared", "cumask"], default="shared",
-                    help="device-plugin CU policy -- shared: memory-capped slices whose kernels run on all CUs "
-                         "(MPS behaviour of the reference demo); cumask: each slice gets exclusive XCD-symmetric CUs")
+    ap.add_argument("--pods-per-gpu", type=int, default=0,
+                    help="default: 28 in server mode (10 GB slices fill 288 GB), else 8 (the HWS process limit)")
+    ap.add_argument("--slice-gb", type=int, default=0, help="GPU memory per fractional pod (default 10 / 36)")
+    ap.add_argument("--mode", choices=["server", "shared", "cumask"], default="server",
+                    help="server: slices served by the GPU's pod server (nos_amd/podserver, the MPS analogue: "
+                         "pods are CPU-only client processes, their inferences run in one HIP context); "
+                         "shared: each pod its own GPU process, memory-capped, kernels on all CUs; "
+                         "cumask: each pod its own GPU process with exclusive XCD-symmetric CUs")
+    ap.add_argument("--server-lanes", type=int, default=8,
+                    help="pod server lanes (streams, one hardware queue each) the tenants' graphs run on")
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--ref-pod-s", type=float, default=4.0,
@@ -106,11 +111,16 @@ def log(rank: int, msg: str) -> None:
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+POD_SERVER_TENANTS = 48  # per GPU, MPS's client limit; memory bounds it first (28 x 10 GB)
+
+
 def plan(args, world: int, local: int, slice_gb: int, pods: int, mode: str) -> tuple[list[dict], dict]:
     from nos_amd.bench_support import control_plane_plan
 
     _, info = control_plane_plan(n_gpus=world, pods_per_gpu=pods, slice_gb=slice_gb, num_cus=256, local_gpu=local,
-                                 cu_policy="shared" if mode == "shared" else "proportional", capacity_probe=True)
+                                 cu_policy="proportional" if mode == "cumask" else "shared", capacity_probe=True,
+                                 pod_server_tenants=POD_SERVER_TENANTS if mode == "server" else 0,
+                                 pod_server_dir=getattr(args, "pod_server_dir", "/tmp/nos_ps"))
     envs = info.pop("envs")
     if os.environ.get("NOS_AMD_BENCH_FOLD_GPUS") == "1":
         # rehearsal of the multi-rank path on fewer GPUs than ranks (gloo between
@@ -274,9 +284,14 @@ def _free_port() -> int:
 def with_trainer(d: Dist, envs: list[dict], args) -> list[dict]:
     """Pod slot 0 of every GPU becomes the DP trainer pod: the same device-plugin
     env plus the job's rendezvous (rank 0 picks a fresh port, every rank learns
-    it through the bench's own group).  Collective call: all ranks, same order."""
+    it through the bench's own group).  Collective call: all ranks, same order.
+    On a pod-server slice the trainer is still its own GPU process (RCCL needs
+    its own context): it gets the GPU instead of the server socket."""
     port = int(d.reduce([float(_free_port()) if d.rank == 0 else 0.0], "max")[0])
-    t = {**envs[0], "NOS_AMD_POD_KIND": "trainer", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+    e0 = dict(envs[0])
+    if e0.pop("NOS_AMD_POD_SERVER", None) is not None:
+        e0["HIP_VISIBLE_DEVICES"] = args.gpu_env
+    t = {**e0, "NOS_AMD_POD_KIND": "trainer", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
          "RANK": str(d.rank), "WORLD_SIZE": str(d.world), "LOCAL_RANK": "0",
          "NOS_AMD_COLL_DIM": str(args.coll_dim), "NOS_AMD_COLL_BUCKET_MB": str(args.coll_bucket_mb),
          # a job that cannot form fails within 2 minutes: every rank then measures without it
@@ -335,6 +350,52 @@ def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, 
     return w, util, n_util, ready_s, trainer_stats(w)
 
 
+class PodServerProc:
+    """This rank's pod server (nos_amd/cmd/podserver.py), started by the clean
+    launcher like the pods, on the rank's GPU."""
+
+    def __init__(self, launcher, args, gpu_env: str, workdir: str):
+        import subprocess
+
+        from nos_amd.podbench import REPO
+
+        self.path = os.path.join(args.pod_server_dir, f"gpu-{args.local_gpu}.sock")
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                            "ROC_GLOBAL_CU_MASK", "CUDA_VISIBLE_DEVICES") and not k.startswith("TORCHELASTIC_")}
+        env.update({"HIP_VISIBLE_DEVICES": gpu_env, "PYTHONPATH": str(REPO) + os.pathsep + env.get("PYTHONPATH", "")})
+        cmd = [sys.executable, "-u", "-m", "nos_amd.cmd.podserver", "--gpu", str(args.local_gpu), "--socket",
+               self.path, "--lanes", str(args.server_lanes), "--max-tenants", str(POD_SERVER_TENANTS),
+               "--device", args.device]
+        self.log = os.path.join(workdir, "podserver.log")
+        self.proc = launcher.spawn(cmd, env, self.log, str(REPO))
+        self._timeout = subprocess.TimeoutExpired
+
+    def wait_ready(self, timeout_s: float = 300.0) -> float:
+        t0 = time.monotonic()
+        while not os.path.exists(self.path):
+            if self.proc.poll() is not None:
+                raise RuntimeError(f"pod server exited ({self.proc.poll()}): {open(self.log).read()[-2000:]}")
+            if time.monotonic() - t0 > timeout_s:
+                raise TimeoutError(f"pod server not ready after {timeout_s} s")
+            time.sleep(0.1)
+        return time.monotonic() - t0
+
+    def info(self) -> dict:
+        from nos_amd.podserver.client import PodClient
+
+        c = PodClient(self.path, connect_timeout_s=5)
+        try:
+            st = c.stats()
+        finally:
+            c.close()
+        return {"pid": st.get("pid"), **{k: st["server"].get(k) for k in ("lanes", "hw_queues", "device")}}
+
+    def close(self) -> None:
+        if self.proc.poll() is None:
+            self.proc.kill()
+
+
 def _hws_limit() -> int:
     from nos_amd.gpu.kfd import hws_max_concurrent_processes
 
@@ -343,6 +404,14 @@ def _hws_limit() -> int:
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    server_mode = args.mode == "server"
+    args.pods_per_gpu = args.pods_per_gpu or (28 if server_mode else 8)
+    args.slice_gb = args.slice_gb or (10 if server_mode else 36)
+    import tempfile
+
+    # short: a Unix socket path has at most 107 bytes
+    args.pod_server_dir = tempfile.mkdtemp(prefix="nos_ps_", dir="/tmp")
+    args.local_gpu = int(os.environ.get("LOCAL_RANK", "0"))
     from nos_amd.podbench import PodLauncher
 
     # first of all: pods are forked by this launcher, which must never come
@@ -370,9 +439,13 @@ def main(argv=None) -> int:
     log(rank, f"control plane placed {cp.get('placed_pods')} pods; local envs {envs[:2]}...")
     if args.table == "auto":
         args.table = "1,3,5,7" if world == 1 and args.device == "cuda" else ""
-    table_plans = [(mode, n, plan(args, world, local, args.slice_gb, n, mode)[0])
+    if server_mode and "server" not in args.table_modes.split(","):
+        args.table_modes = "server," + args.table_modes
+    # table rows: the main run's slice size for server rows, 36 GB process slices otherwise
+    table_plans = [(mode, n, plan(args, world, local, args.slice_gb if mode == "server" else 36, n, mode)[0])
                    for mode in args.table_modes.split(",") if args.table
                    for n in map(int, args.table.split(","))]
+    args.gpu_env = envs[0].get("HIP_VISIBLE_DEVICES", str(local))  # this rank's GPU (folded runs: shared)
 
     d.init_gpu()
     sampler = UtilSampler(d.device) if d.cuda else None
@@ -388,6 +461,10 @@ def main(argv=None) -> int:
                                     args.ref_pod_s, sampler, device=args.device)
         ref = {"inf_per_s": round(w1.throughput, 3), "latency_s": w1.mean_latency_s, "gpu_util_pct": u1}
 
+    server = None
+    if server_mode or any(m == "server" for m, _, _ in table_plans):
+        server = PodServerProc(launcher, args, args.gpu_env, args.pod_server_dir)
+        log(rank, f"pod server ready in {server.wait_ready():.1f} s on {server.path}")
     trainer_error = None
     try:
         w, util, n_util, ready_s, tr = run_fleet(d, launcher, fleet_envs(pod_envs), args.dtype, not args.no_graphs,
@@ -420,6 +497,13 @@ def main(argv=None) -> int:
                       "pods_over_latency": round(n / wt.mean_latency_s, 2) if wt.mean_latency_s else None,
                       "cu_mask": (wt.pods[0].info.get("cu_mask") if wt.pods else None)})
         log(rank, f"table {table[-1]}")
+    server_info = None
+    if server is not None:
+        try:
+            server_info = server.info()
+        except Exception as e:  # reported, not fatal: the pods' own records are the measurement
+            server_info = {"error": repr(e)}
+        server.close()
     if sampler:
         sampler.close()
     launcher.close()
@@ -461,7 +545,11 @@ def main(argv=None) -> int:
                    "parallelism": f"{args.mode} fractional slices, {args.pods_per_gpu} pod processes/GPU, "
                                   f"{world} GPU(s)",
                    "pods_per_gpu": args.pods_per_gpu, "slice_gb": args.slice_gb, "mode": args.mode,
-                   "pod_execution": "one process per pod with its device-plugin env", "graphs": not args.no_graphs,
+                   "pod_execution": ("one CPU-only client process per pod with its device-plugin env (pod-server "
+                                     "socket + slice), its inferences run as HIP-graph replays in the GPU's pod "
+                                     f"server process ({args.server_lanes} lanes; the MPS architecture)")
+                   if server_mode else "one GPU process per pod with its device-plugin env",
+                   "graphs": not args.no_graphs,
                    "collective_tenant": use_coll, "step_s": args.step_s, "bursty": args.bursty or None,
                    "pods_placed_per_node": int(placed)},
         "gpu_util_pct": None if util_mean is None else round(util_mean, 1),
@@ -471,6 +559,9 @@ def main(argv=None) -> int:
         # what bounds it on this node: the amdgpu hardware scheduler's concurrent
         # processes per logical GPU (VMIDs), read from the driver
         "hws_max_concurrent_processes_per_gpu": _hws_limit(),
+        # server mode: the GPU processes are the pod server (+ the trainer pod),
+        # so the HWS bound does not apply to the pods; memory does (28 x 10 GB)
+        "pod_server": None if not server_mode else {**(server_info or {}), "tenants_per_gpu_max": POD_SERVER_TENANTS},
         "schedulable_fractional_pods_per_node_sim": cp.get("schedulable_fractional_pods_per_node"),
         "schedulable_10gb_pods_per_node_sim": cp10.get("schedulable_fractional_pods_per_node",
                                                        cp.get("schedulable_fractional_pods_per_node")),
@@ -529,6 +620,9 @@ def main(argv=None) -> int:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     d.close()
+    import shutil
+
+    shutil.rmtree(args.pod_server_dir, ignore_errors=True)
     return 0
 
 

@@ -53,12 +53,13 @@ class NodeDeviceClient:
         return {d.gpu_index for d in self.get_used_devices(prefix)}
 
 
-def node_labels(smi) -> dict[str, str]:
+def node_labels(smi, pod_server_tenants: int = 0) -> dict[str, str]:
     gpus = smi.gpus()
     if not gpus:
         return {C.LABEL_AMD_COUNT: "0"}
     g0 = gpus[0]
-    return {C.LABEL_AMD_PRODUCT: g0.market_name.replace(" ", "-"), C.LABEL_AMD_COUNT: str(len(gpus)),
+    extra = {C.LABEL_POD_SERVER_TENANTS: str(pod_server_tenants)} if pod_server_tenants > 0 else {}
+    return {**extra, C.LABEL_AMD_PRODUCT: g0.market_name.replace(" ", "-"), C.LABEL_AMD_COUNT: str(len(gpus)),
             C.LABEL_AMD_MEMORY: str(g0.vram_mb), C.LABEL_AMD_XCDS: str(g0.num_xcds), C.LABEL_AMD_CUS: str(g0.num_cus),
             C.LABEL_AMD_COMPUTE_MODE: g0.compute_mode, C.LABEL_AMD_MEMORY_MODE: g0.memory_mode,
             C.LABEL_AMD_MAX_PROCS: str(max_concurrent_processes(smi))}
@@ -67,14 +68,15 @@ def node_labels(smi) -> dict[str, str]:
 class NodeLabeler:
     REFRESH_S = 60.0
 
-    def __init__(self, api, node_name: str, smi):
+    def __init__(self, api, node_name: str, smi, pod_server_tenants: int = 0):
         self.api, self.node_name, self.smi = api, node_name, smi
+        self.pod_server_tenants = pod_server_tenants  # > 0: the node runs the pod server (MPS analogue)
 
     def reconcile(self, req: Request) -> Result:
         node = self.api.try_get("Node", self.node_name)
         if node is None:
             return Result()
-        want = node_labels(self.smi)
+        want = node_labels(self.smi, self.pod_server_tenants)
         have = ko.labels(node)
         diff = {k: v for k, v in want.items() if have.get(k) != v}
         if diff:

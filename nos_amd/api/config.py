@@ -157,6 +157,10 @@ class GpuAgentConfig(ControllerManagerSpec):
     probe_enabled: bool = Field(True, alias="probeEnabled")
     probe_interval_seconds: float = Field(300.0, alias="probeIntervalSeconds")
     probe_gemm_size: int = Field(4096, alias="probeGemmSize")
+    # > 0: the node runs the pod server (nos_amd/podserver) with this many
+    # tenants per GPU; published as nos.nebuly.com/pod-server.tenants, it lifts
+    # the HWS process bound on cumask slices per GPU
+    pod_server_tenants: int = Field(0, alias="podServerTenants")
 
 
 class DevicePluginConfig(ControllerManagerSpec):
@@ -176,6 +180,11 @@ class DevicePluginConfig(ControllerManagerSpec):
     # seconds between amd-smi rescans (modes switched by the partition agent) and
     # reads of the node's partitioning label
     rescan_seconds: float = Field(5.0, alias="rescanSeconds")
+    # pod-server slices (nos_amd/podserver, the MPS analogue): slices of a cumask
+    # node are served by the node's pod server, one per GPU at
+    # <podServerSocketDir>/gpu-<index>.sock; pods get that socket (mounted) and
+    # their slice, never a device node.  "" = pods run as GPU processes.
+    pod_server_socket_dir: str = Field("", alias="podServerSocketDir")
 
 
 class MetricsExporterConfig(_M):

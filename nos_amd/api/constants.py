@@ -72,12 +72,19 @@ LABEL_AMD_MEMORY_MODE = "amd.com/gpu.memory-partition"
 # processes the amdgpu HWS runs concurrently per logical GPU (hws_max_conc_proc, gpu/kfd.py)
 LABEL_AMD_MAX_PROCS = "amd.com/gpu.max-concurrent-processes"
 LABEL_DEVICE_PLUGIN_CONFIG = "nos.nebuly.com/device-plugin.config"
+# tenants the node's pod server (nos_amd/podserver, MPS analogue) hosts per GPU:
+# present = slices are served by the pod server, and this replaces the HWS
+# process bound on slices per GPU (the server is ONE GPU process)
+LABEL_POD_SERVER_TENANTS = "nos.nebuly.com/pod-server.tenants"
 
 # --------------------------------------------------------------- env
 ENV_NODE_NAME = "NODE_NAME"
 ENV_CU_MASK = "ROC_GLOBAL_CU_MASK"
 ENV_VISIBLE_DEVICES = "HIP_VISIBLE_DEVICES"
 ENV_MEMORY_LIMIT_GB = "NOS_AMD_MEMORY_LIMIT_GB"
+ENV_POD_SERVER = "NOS_AMD_POD_SERVER"        # pod-server socket of the slice's GPU
+ENV_POD_CU_MASK = "NOS_AMD_POD_CU_MASK"      # CU mask the pod server applies to the tenant's stream
+DEFAULT_POD_SERVER_SOCKET_DIR = "/run/nos-amd/podserver"
 
 # --------------------------------------------------------------- defaults
 DEFAULT_AMD_GPU_RESOURCE_MEMORY_GB = 288   # one MI355X (HBM3E)

@@ -16,6 +16,7 @@ timed by the bench.  Two runs on a fresh cluster with one ``cumask`` node of
 """
 from __future__ import annotations
 
+import re
 import time
 
 from .api import constants as C
@@ -36,23 +37,26 @@ def cus_from_hex(mask: str) -> list[int]:
     return out
 
 
-def _cluster(n_gpus: int, num_cus: int, placement: str, cu_policy: str, kind: str = C.PARTITIONING_CUMASK
-             ) -> SimCluster:
+def _cluster(n_gpus: int, num_cus: int, placement: str, cu_policy: str, kind: str = C.PARTITIONING_CUMASK,
+             pod_server_tenants: int = 0, pod_server_dir: str = C.DEFAULT_POD_SERVER_SOCKET_DIR) -> SimCluster:
     cfg = GpuPartitionerConfig(slicePlacement=placement, cuPolicy=cu_policy)
     cl = SimCluster(partitioner_config=cfg)
-    cl.add_node("mi355x-0", kind, smi=FakeSmi(gpus=n_gpus, cus=num_cus, node="mi355x-0"))
+    cl.add_node("mi355x-0", kind, smi=FakeSmi(gpus=n_gpus, cus=num_cus, node="mi355x-0"),
+                pod_server_tenants=pod_server_tenants, pod_server_dir=pod_server_dir)
     cl.settle(30)
     return cl
 
 
 def schedulable_pods(n_gpus: int, slice_gb: int, num_cus: int = 256, placement: str = "spread",
-                     per_gpu_attempt: int = 40, kind: str = C.PARTITIONING_CUMASK) -> dict:
+                     per_gpu_attempt: int = 40, kind: str = C.PARTITIONING_CUMASK, pod_server_tenants: int = 0
+                     ) -> dict:
     """Submit ``per_gpu_attempt`` x GPUs slice pods to a fresh simulated node of
     ``kind`` and count how many reach Running through the real scheduler,
     partitioner, agents and device plugin (cumask: one logical GPU per MI355X,
-    8 HWS process slots; hybrid: the partitioner also picks each GPU's
-    compute/memory mode, 8 slots per partition)."""
-    cl = _cluster(n_gpus, num_cus, placement, "even", kind)
+    8 HWS process slots, or ``pod_server_tenants`` when the pod server hosts
+    the slices; hybrid: the partitioner also picks each GPU's compute/memory
+    mode, 8 slots per partition)."""
+    cl = _cluster(n_gpus, num_cus, placement, "even", kind, pod_server_tenants)
     total = n_gpus * per_gpu_attempt
     for i in range(total):
         cl.submit_pod(f"cap-{i}", {f"{C.AMD_SLICE_RESOURCE_PREFIX}{slice_gb}gb": 1})
@@ -73,14 +77,28 @@ def schedulable_pods(n_gpus: int, slice_gb: int, num_cus: int = 256, placement: 
     return out
 
 
+def _gpu_of(env: dict) -> str:
+    """Host GPU of an allocation: its HIP id, or the pod server's socket name."""
+    if env.get(C.ENV_VISIBLE_DEVICES):
+        return env[C.ENV_VISIBLE_DEVICES]
+    sock = env.get(C.ENV_POD_SERVER, "")
+    m = re.search(r"gpu-(\d+)\.sock$", sock.split(",")[0])
+    return m.group(1) if m else ""
+
+
 def control_plane_plan(n_gpus: int, pods_per_gpu: int, slice_gb: int, num_cus: int, local_gpu: int = 0,
-                       placement: str = "spread", cu_policy: str = "proportional", capacity_probe: bool = True
+                       placement: str = "spread", cu_policy: str = "proportional", capacity_probe: bool = True,
+                       pod_server_tenants: int = 0, pod_server_dir: str = C.DEFAULT_POD_SERVER_SOCKET_DIR
                        ) -> tuple[list[list[int] | None], dict]:
     """Masks of the pods placed on ``local_gpu`` (None = unmasked) and the
     control-plane facts; ``info["envs"]`` holds each of those pods' full
-    device-plugin environment (what its container is started with)."""
-    info = schedulable_pods(n_gpus, slice_gb, num_cus, placement) if capacity_probe else {}
-    cl = _cluster(n_gpus, num_cus, placement, cu_policy)
+    device-plugin environment (what its container is started with).
+    ``pod_server_tenants`` > 0: the node's slices are pod-server slices
+    (sockets under ``pod_server_dir``)."""
+    info = schedulable_pods(n_gpus, slice_gb, num_cus, placement, pod_server_tenants=pod_server_tenants) \
+        if capacity_probe else {}
+    cl = _cluster(n_gpus, num_cus, placement, cu_policy, pod_server_tenants=pod_server_tenants,
+                  pod_server_dir=pod_server_dir)
     res = f"{C.AMD_SLICE_RESOURCE_PREFIX}{slice_gb}gb"
     for i in range(n_gpus * pods_per_gpu):
         cl.submit_pod(f"yolos-{i}", {res: 1})
@@ -94,10 +112,11 @@ def control_plane_plan(n_gpus: int, pods_per_gpu: int, slice_gb: int, num_cus: i
     for _key, conts in sorted(node.kubelet.running_containers().items()):
         for rc in conts:
             env = rc.envs
-            gpu = env.get(C.ENV_VISIBLE_DEVICES, "")
+            gpu = _gpu_of(env)
             per_gpu[gpu] = per_gpu.get(gpu, 0) + 1
             if gpu == str(local_gpu):  # no mask env: the slice runs on every CU (cuPolicy shared)
-                masks.append(cus_from_hex(env[C.ENV_CU_MASK]) if C.ENV_CU_MASK in env else None)
+                mask = env.get(C.ENV_CU_MASK) or env.get(C.ENV_POD_CU_MASK)
+                masks.append(cus_from_hex(mask) if mask else None)
                 envs.append({k: str(v) for k, v in env.items()})
     ann = ko.annotations(cl.api.get("Node", "mi355x-0"))
     info.update({"placed_pods": len(cl.running_pods()), "pending_pods": len(cl.pending_pods()),

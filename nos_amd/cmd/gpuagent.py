@@ -19,7 +19,7 @@ def build(api, node: str, cfg, smi, lister, probe=None):
     from ..agents.gpuagent import CuMaskReporter
 
     mgr = common.manager_for(api, f"nos-gpuagent-{node}", cfg)
-    mgr.add(NodeLabeler(api, node, smi).controller())
+    mgr.add(NodeLabeler(api, node, smi, cfg.pod_server_tenants).controller())
     mgr.add(CuMaskReporter(api, node, smi, lister, cfg.report_config_interval_seconds, probe).controller())
     return mgr
 

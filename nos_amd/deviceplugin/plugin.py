@@ -73,14 +73,18 @@ class ContainerAllocation:
     envs: dict[str, str] = field(default_factory=dict)
     devices: list[str] = field(default_factory=list)
     device_ids: list[str] = field(default_factory=list)
+    mounts: list[str] = field(default_factory=list)   # host directories mounted at the same path
 
 
 class NosAmdDevicePlugin:
     def __init__(self, node_name: str, smi: AmdSmi, mode: str | None = None, expose_partitions_as_gpu: bool = False,
-                 cu_policy: str = "proportional", device_env: str = "host"):
+                 cu_policy: str = "proportional", device_env: str = "host", pod_server_dir: str = ""):
         if device_env not in ("host", "container"):
             raise ValueError(f"device_env must be 'host' or 'container', not {device_env!r}")
         self.node_name = node_name
+        # cumask slices served by the node's pod server (nos_amd/podserver): the
+        # pod gets the socket of its GPU's server, never a device node
+        self.pod_server_dir = pod_server_dir
         # "container": the runtime mounts only the allocated render nodes, so
         # HIP inside the container numbers them 0..k-1 in host order;
         # "host": tenants run on the host and see every GPU (simulator, bare metal)
@@ -342,6 +346,9 @@ class NosAmdDevicePlugin:
         return w
 
     def allocate(self, resource: str, device_ids: list[str], owner: str = "") -> ContainerAllocation:
+        if (self.pod_server_dir and self.mode == C.PARTITIONING_CUMASK
+                and resource.startswith(C.AMD_SLICE_RESOURCE_PREFIX)):
+            return self._allocate_pod_server(resource, device_ids, owner)
         with self._lock:
             alloc = ContainerAllocation(device_ids=list(device_ids))
             gpus = {g.index: g for g in self._gpus()}
@@ -382,6 +389,43 @@ class NosAmdDevicePlugin:
                 alloc.envs[C.ENV_VISIBLE_DEVICES] = ",".join(h for _, h in visible)
             if mask_cus and len(mask_cus) < n_cus:  # a full mask would only cost a dedicated HW queue
                 alloc.envs[C.ENV_CU_MASK] = mask_hex(sorted(mask_cus), n_cus)
+            if mem:
+                alloc.envs[C.ENV_MEMORY_LIMIT_GB] = str(mem)
+            return alloc
+
+    def _allocate_pod_server(self, resource: str, device_ids: list[str], owner: str) -> ContainerAllocation:
+        """A slice served by the GPU's pod server (the MPS-client analogue): the
+        server socket, the slice's memory and, unless the CU policy is
+        "shared", its CU mask for the server to apply to the tenant's stream.
+        No ``/dev/kfd`` and no render node: the pod must not open the GPU
+        (that would take an HWS process slot, which is what the server saves)."""
+        from ..cmd.podserver import socket_path
+
+        with self._lock:
+            alloc = ContainerAllocation(device_ids=list(device_ids), mounts=[self.pod_server_dir])
+            gpus = {g.index: g for g in self._gpus()}
+            socks: list[str] = []
+            mask_cus: set[int] = set()
+            n_cus = mem = 0
+            for did in device_ids:
+                d = self.devices.get(did)
+                if d is None or d.resource != resource:
+                    raise KeyError(f"unknown device {did} for {resource}")
+                if not d.healthy:
+                    raise RuntimeError(f"device {did} is unhealthy")
+                sp = str(socket_path(self.pod_server_dir, d.gpu_index))
+                if sp not in socks:
+                    socks.append(sp)
+                s = self.cu_slots.get(did)
+                if s is not None:
+                    mask_cus.update(s.cus())
+                xcds, per_xcd = _cu_geometry(gpus.get(d.gpu_index))
+                n_cus = max(n_cus, xcds * per_xcd)
+                mem += d.memory_gb
+                self.allocated[did] = owner or "unknown"
+            alloc.envs[C.ENV_POD_SERVER] = ",".join(socks)
+            if mask_cus and len(mask_cus) < n_cus:
+                alloc.envs[C.ENV_POD_CU_MASK] = mask_hex(sorted(mask_cus), n_cus)
             if mem:
                 alloc.envs[C.ENV_MEMORY_LIMIT_GB] = str(mem)
             return alloc

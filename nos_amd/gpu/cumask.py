@@ -12,6 +12,10 @@ slice needs at least one CU on every XCD, so a GPU holds at most
 ``cus_per_xcd`` (32 on MI355X) slices, and no more slices than the amdgpu
 hardware scheduler runs processes concurrently (node label
 ``amd.com/gpu.max-concurrent-processes``, 8 by default; :mod:`nos_amd.gpu.kfd`).
+On a node whose slices are served by the pod server (label
+``nos.nebuly.com/pod-server.tenants``, :mod:`nos_amd.podserver`) the bound is
+the server's tenant count instead: all tenants share one GPU process, and
+memory bounds the slices as in the reference.
 """
 from __future__ import annotations
 
@@ -230,6 +234,11 @@ class SliceNode:
         procs = ko.labels(node).get(C.LABEL_AMD_MAX_PROCS)
         if procs and int(procs) > 0:
             max_slices = min(max_slices, int(procs))
+        # ... unless the node's pod server hosts the slices: ONE GPU process per
+        # GPU whatever the tenant count (nos_amd/podserver, the MPS analogue)
+        tenants = ko.labels(node).get(C.LABEL_POD_SERVER_TENANTS, "")
+        if tenants.isdigit() and int(tenants) > 0:
+            max_slices = int(tenants)
         status, _ = parse_node_annotations(node)
         by_gpu: dict[int, tuple[dict, dict]] = {}
         for a in status:

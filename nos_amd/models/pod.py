@@ -177,6 +177,20 @@ def slice_cu_budget(env: dict | None = None) -> int:
         return 0
 
 
+class _ServerTenant:
+    """A pod on a pod-server slice: its inferences run in the GPU's pod server
+    (nos_amd/podserver); this process never opens the GPU."""
+
+    def __init__(self, client):
+        self.client = client
+
+    def launch(self) -> None:
+        self.client.infer()
+
+    def synchronize(self) -> None:  # infer() returns when the server's replay has finished
+        pass
+
+
 class _CpuTenant:
     def __init__(self, model, x):
         self.model, self.x = model, x
@@ -195,7 +209,28 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
     board = StatusBoard(status)
     row = board.row(slot)
     row[3] = os.getpid()
+    client = None
     try:
+        from ..api import constants as C
+
+        if os.environ.get(C.ENV_POD_SERVER):
+            # pod-server slice: register the model in the server, infer through it
+            from ..podserver.client import PodClient
+
+            client = PodClient.from_env()
+            rep = client.register(f"pod-{slot}", dtype=dtype, seed=seed)
+            s = t = _ServerTenant(client)
+            for _ in range(warmup):
+                t.launch()
+            srv = rep.get("server") or {}
+            info = {"slot": slot, "pid": os.getpid(), "dtype": dtype, "graphs": graphs, "memory_fraction": None,
+                    "device": srv.get("device"), "multiprocessor_count": srv.get("multiprocessor_count"),
+                    "cu_mask": os.environ.get(C.ENV_POD_CU_MASK), "cu_budget": 0,
+                    "kernel_config": srv.get("kernel_config"), "hip_visible_devices": None,
+                    "memory_limit_gb": os.environ.get(C.ENV_MEMORY_LIMIT_GB),
+                    "max_allocated_gb": rep.get("footprint_gb"), "pod_server": os.environ[C.ENV_POD_SERVER],
+                    "server_lanes": srv.get("lanes"), "server_tenant": rep.get("tenant")}
+            return _loop(board, row, slot, out, t, s, info, orphaned, gpu=False)
         import torch
 
         from ..utils.memlimit import apply_memory_limit
@@ -241,39 +276,50 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
                 "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES"),
                 "memory_limit_gb": os.environ.get("NOS_AMD_MEMORY_LIMIT_GB"),
                 "max_allocated_gb": None}
-        row[0] = STATE_READY
-        times: list[float] = []
-        info["t_ready"] = time.monotonic()
-        # bursty tenants (NOS_AMD_POD_DUTY="on_s:off_s"): infer for on_s, idle
-        # for off_s, with a per-pod phase so the pods do not burst in step
-        duty = os.environ.get("NOS_AMD_POD_DUTY")
-        on_s, off_s = (float(v) for v in duty.split(":")) if duty else (0.0, 0.0)
-        phase0 = time.monotonic() - (on_s + off_s) * ((slot * 0.618) % 1.0)
-        with torch.no_grad():
-            while not board.stopped():
-                if orphaned():
-                    print(f"[pod {slot}] launcher gone: exiting", file=sys.stderr, flush=True)
-                    return 1
-                if off_s > 0 and (time.monotonic() - phase0) % (on_s + off_s) >= on_s:
-                    time.sleep(0.005)
-                    continue
-                t.launch()
-                s.synchronize()
-                now = time.monotonic()
-                times.append(now)
-                row[1] = len(times)
-                row[2] = now
-        if gpu:
-            info["max_allocated_gb"] = round(torch.cuda.max_memory_allocated(0) / 2 ** 30, 3)
-        info["times"] = times
-        Path(out, f"pod-{slot}.json").write_text(json.dumps(info))
-        row[0] = STATE_DONE
-        return 0
+        torch.set_grad_enabled(False)  # inference only (eager CPU tenants; graphs were captured without grad)
+        return _loop(board, row, slot, out, t, s, info, orphaned, gpu)
     except Exception as e:  # the orchestrator sees the failure in the board and in the file
         Path(out, f"pod-{slot}.json").write_text(json.dumps({"slot": slot, "error": repr(e)}))
         row[0] = STATE_FAILED
         print(f"[pod {slot}] failed: {e!r}", file=sys.stderr, flush=True)
         return 1
+    finally:
+        if client is not None:
+            client.close()
+
+
+def _loop(board: StatusBoard, row, slot: int, out: str, t, s, info: dict, orphaned, gpu: bool) -> int:
+    """Back-to-back inferences until the board says stop; completion times to
+    ``<out>/pod-<slot>.json``."""
+    row[0] = STATE_READY
+    times: list[float] = []
+    info["t_ready"] = time.monotonic()
+    # bursty tenants (NOS_AMD_POD_DUTY="on_s:off_s"): infer for on_s, idle
+    # for off_s, with a per-pod phase so the pods do not burst in step
+    duty = os.environ.get("NOS_AMD_POD_DUTY")
+    on_s, off_s = (float(v) for v in duty.split(":")) if duty else (0.0, 0.0)
+    phase0 = time.monotonic() - (on_s + off_s) * ((slot * 0.618) % 1.0)
+    while not board.stopped():
+        if orphaned():
+            print(f"[pod {slot}] launcher gone: exiting", file=sys.stderr, flush=True)
+            return 1
+        if off_s > 0 and (time.monotonic() - phase0) % (on_s + off_s) >= on_s:
+            time.sleep(0.005)
+            continue
+        t.launch()
+        s.synchronize()
+        now = time.monotonic()
+        times.append(now)
+        row[1] = len(times)
+        row[2] = now
+    if gpu:
+        import torch
+
+        info["max_allocated_gb"] = round(torch.cuda.max_memory_allocated(0) / 2 ** 30, 3)
+    info["times"] = times
+    Path(out, f"pod-{slot}.json").write_text(json.dumps(info))
+    row[0] = STATE_DONE
+    return 0
 
 
 def main(argv=None) -> int:

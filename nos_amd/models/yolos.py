@@ -332,13 +332,15 @@ class GraphedTenant:
     graph: torch.cuda.CUDAGraph | None = None
     outputs: tuple = field(default_factory=tuple)
 
-    def capture(self, warmup: int = 2) -> None:
+    def capture(self, warmup: int = 2, capture_error_mode: str = "global") -> None:
+        """``capture_error_mode="thread_local"`` when other threads keep
+        launching while this one captures (the pod server's lanes)."""
         with torch.cuda.stream(self.stream):
             for _ in range(warmup):
                 self.outputs = self.model(self.pixel_values)
         self.stream.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=self.stream):
+        with torch.cuda.graph(self.graph, stream=self.stream, capture_error_mode=capture_error_mode):
             self.outputs = self.model(self.pixel_values)
         self.stream.synchronize()
 

@@ -1,0 +1,394 @@
+"""nos-amd pod server: the MI355X stand-in for the NVIDIA MPS control daemon.
+
+Why it exists.  The reference shares a GPU between up to 48 client pods through
+MPS (``pkg/gpu/slicing``; the nvidia-device-plugin starts the MPS daemon): the
+clients' kernels run in ONE server context.  AMD has no MPS.  Separate pod
+processes on one MI355X each take a KFD process slot of the amdgpu hardware
+scheduler, which runs at most 8 of them at once (``gpu/kfd.py``); a ninth is
+time-sliced at a ~50 ms quantum and aggregate throughput falls
+(profiles/r02_pods_vs_throughput_hwqueues.json).  The pod server removes that
+bound the way MPS does on NVIDIA.  One server process per GPU owns the only
+HIP context.  Fractional pods are CPU-only clients (``client.py``) on a Unix
+socket, and their inferences run as HIP-graph replays in the server.
+
+Design (MI355X-first):
+
+* **Lanes.**  ``lanes`` HIP streams are created first, so that with
+  ``GPU_MAX_HW_QUEUES=lanes`` each one owns a hardware queue.  Every tenant's
+  graph is replayed on whichever lane is free.  A CUDA/HIP graph may be
+  launched on any stream, so tenants do not need their own queue; 28 tenants
+  on 28 queues oversubscribe the command processor's queue slots and lose
+  throughput (tools/mps_probe.py: 323-421 inf/s at 28 tenants with 8-32
+  queues, against 476 at 8 and 16 tenants on their own queues).
+* **Fairness.**  Requests enter one FIFO and each client has at most one
+  request in flight, so the lanes serve the tenants round-robin and every
+  tenant sees the same latency.  Queues shared through HIP's round-robin
+  stream mapping instead gave a 20-50 ms spread at 20 tenants.
+* **Memory slices.**  A tenant registers with its slice's memory
+  (``NOS_AMD_MEMORY_LIMIT_GB`` from the device plugin).  The server measures
+  the peak device memory of the tenant's build and graph capture, and refuses
+  the tenant when that peak exceeds the slice.  The check runs at admission
+  and is hard: nothing is allocated at replay time.  Process pods only get a
+  cooperative caching-allocator cap.
+* **CU slices.**  A tenant whose allocation carries a CU mask gets its own
+  CU-masked stream (``hipExtStreamCreateWithCUMask``), the per-queue form of
+  ``ROC_GLOBAL_CU_MASK``.  Unmasked tenants share every CU, which is MPS's
+  default.
+* **Kernel configs.**  All tenants use the fractional-pod kernel configs of
+  :func:`nos_amd.models.pod.kernel_config`: co-tenants fill the CU slots, so
+  there are no key splits and the x6 GEMMs use 128x128 tiles.
+
+``device="cpu"`` runs the tiny test model without streams or graphs (protocol
+tests on machines without a GPU).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import queue
+import socket
+import threading
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import numpy as np
+
+from . import protocol as P
+
+log = logging.getLogger("nos_amd.podserver")
+
+DEFAULT_LANES = 8
+DEFAULT_MAX_TENANTS = 48  # MPS's client limit per server (Volta+)
+
+
+@dataclass
+class Tenant:
+    id: int
+    pod: str
+    memory_limit_gb: float
+    dtype: str
+    model: object
+    x: object                      # static input tensor (graph input)
+    stream: object = None          # own CU-masked stream (masked tenants), else None
+    graph: object = None
+    outputs: tuple = ()
+    footprint_gb: float = 0.0
+    cu_mask: str | None = None
+    completed: int = 0
+    gpu_s: float = 0.0
+    registered_at: float = field(default_factory=time.monotonic)
+
+
+@dataclass
+class _Job:
+    tenant: Tenant
+    payload: bytes
+    want_outputs: bool
+    done: threading.Event = field(default_factory=threading.Event)
+    t_enq: float = field(default_factory=time.monotonic)
+    t_start: float = 0.0
+    t_end: float = 0.0
+    outputs: list = field(default_factory=list)
+    error: str | None = None
+
+
+class AdmissionError(RuntimeError):
+    pass
+
+
+class PodServer:
+    def __init__(self, socket_path: str | os.PathLike, device: str = "cuda", lanes: int = DEFAULT_LANES,
+                 max_tenants: int = DEFAULT_MAX_TENANTS, memory_gb: float | None = None, graphs: bool = True,
+                 kernel_config: dict | None = None):
+        if lanes < 1:
+            raise ValueError("lanes must be >= 1")
+        self.path = Path(socket_path)
+        self.device = device
+        self.gpu = device == "cuda"
+        self.lanes_n = lanes
+        self.max_tenants = max_tenants
+        self.graphs = graphs and self.gpu
+        self.tenants: dict[int, Tenant] = {}
+        self._next_id = 1
+        self._lock = threading.Lock()          # tenant table
+        self._build_lock = threading.Lock()    # one registration (build + capture + accounting) at a time
+        self._q: queue.Queue[_Job | None] = queue.Queue()
+        self._stop = threading.Event()
+        self._threads: list[threading.Thread] = []
+        self._lanes: list = []
+        self._sock: socket.socket | None = None
+        self.kernel_config = kernel_config
+        self.memory_gb = memory_gb
+        self.info: dict = {}
+
+    # ------------------------------------------------------------ lifecycle
+    def _init_device(self) -> None:
+        import torch
+
+        if not self.gpu:
+            torch.set_num_threads(1)
+            self.info = {"device": "cpu", "lanes": self.lanes_n}
+            return
+        from ..models.pod import kernel_config
+        from ..ops import (_lib, set_attention_f32_variant, set_f32_math, set_gemm_f32_policy, set_gemm_f32x6_tile,
+                           set_gemm_policy)
+
+        _lib.require_native_on_gpu()
+        torch.cuda.set_device(0)
+        torch.backends.cuda.matmul.allow_tf32 = False
+        # fractional-pod configs: the co-tenants fill the CU slots (pod.kernel_config)
+        cfg = self.kernel_config or kernel_config(0.5, os.environ, 0)
+        set_gemm_policy(cfg["gemm_bf16"])
+        set_gemm_f32_policy(cfg["gemm_f32"])
+        set_attention_f32_variant(cfg["attention_f32"])
+        set_f32_math(cfg["f32_math"])
+        set_gemm_f32x6_tile(cfg["gemm_f32x6_tile"])
+        self.kernel_config = cfg
+        props = torch.cuda.get_device_properties(0)
+        total_gb = props.total_memory / 2 ** 30
+        self.memory_gb = min(self.memory_gb or total_gb, total_gb)
+        # lanes first: with GPU_MAX_HW_QUEUES >= lanes each gets its own HW queue
+        self._lanes = [torch.cuda.Stream() for _ in range(self.lanes_n)]
+        self._setup_stream = torch.cuda.Stream()
+        self.info = {"device": props.name, "multiprocessor_count": props.multi_processor_count,
+                     "lanes": self.lanes_n, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                     "memory_gb": round(self.memory_gb, 1), "kernel_config": cfg,
+                     "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES")}
+
+    def start(self) -> "PodServer":
+        self._init_device()
+        self.path.parent.mkdir(parents=True, exist_ok=True)
+        if self.path.exists():
+            self.path.unlink()
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        tmp = self.path.with_name(self.path.name + ".tmp")
+        if tmp.exists():
+            tmp.unlink()
+        s.bind(str(tmp))
+        s.listen(256)
+        os.replace(tmp, self.path)  # the socket appears only once the server accepts
+        self._sock = s
+        for i in range(self.lanes_n):
+            t = threading.Thread(target=self._lane, args=(i,), name=f"lane-{i}", daemon=True)
+            t.start()
+            self._threads.append(t)
+        t = threading.Thread(target=self._accept, name="accept", daemon=True)
+        t.start()
+        self._threads.append(t)
+        log.info("pod server on %s: %s", self.path, self.info)
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._sock is not None:
+            try:
+                self._sock.shutdown(socket.SHUT_RDWR)
+            except OSError:
+                pass
+            self._sock.close()
+        for _ in range(self.lanes_n):
+            self._q.put(None)
+        for t in self._threads:
+            t.join(timeout=10)
+        try:
+            self.path.unlink()
+        except FileNotFoundError:
+            pass
+        if self.gpu:
+            import torch
+
+            torch.cuda.synchronize()
+
+    def serve_forever(self) -> None:
+        while not self._stop.is_set():
+            self._stop.wait(1.0)
+
+    # ------------------------------------------------------------ connections
+    def _accept(self) -> None:
+        while not self._stop.is_set():
+            try:
+                conn, _ = self._sock.accept()
+            except OSError:
+                return
+            threading.Thread(target=self._serve, args=(conn,), daemon=True).start()
+
+    def _serve(self, conn: socket.socket) -> None:
+        tenant: Tenant | None = None
+        try:
+            while not self._stop.is_set():
+                try:
+                    req, payload = P.recv_msg(conn)
+                except (ConnectionError, OSError):
+                    return
+                op = req.get("op")
+                try:
+                    if op == "register":
+                        if tenant is not None:
+                            raise AdmissionError("connection already holds a tenant")
+                        tenant = self._register(req)
+                        P.send_msg(conn, {"ok": True, "tenant": tenant.id, "footprint_gb": tenant.footprint_gb,
+                                          "input_shape": list(tenant.x.shape), "server": self.info,
+                                          "tenants": len(self.tenants)})
+                    elif op == "infer":
+                        if tenant is None:
+                            raise AdmissionError("register first")
+                        job = _Job(tenant, payload, bool(req.get("outputs")))
+                        self._q.put(job)
+                        job.done.wait()
+                        if job.error:
+                            raise RuntimeError(job.error)
+                        descs, out = P.pack_arrays(job.outputs) if job.outputs else ([], b"")
+                        P.send_msg(conn, {"ok": True, "queue_us": round(1e6 * (job.t_start - job.t_enq), 1),
+                                          "gpu_us": round(1e6 * (job.t_end - job.t_start), 1), "outputs": descs},
+                                   out)
+                    elif op == "stats":
+                        P.send_msg(conn, {"ok": True, **self.stats()})
+                    elif op == "close":
+                        P.send_msg(conn, {"ok": True})
+                        return
+                    else:
+                        raise P.ProtocolError(f"unknown op {op!r}")
+                except (AdmissionError, P.ProtocolError, RuntimeError, ValueError, KeyError) as e:
+                    P.send_msg(conn, {"ok": False, "error": f"{type(e).__name__}: {e}"})
+        finally:
+            if tenant is not None:
+                self._unregister(tenant)
+            conn.close()
+
+    # ------------------------------------------------------------ tenants
+    def _register(self, req: dict) -> Tenant:
+        limit = float(req.get("memory_limit_gb") or 0)
+        dtype = req.get("dtype", "fp32")
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError(f"dtype {dtype!r}")
+        with self._lock:
+            if len(self.tenants) >= self.max_tenants:
+                raise AdmissionError(f"server full ({self.max_tenants} tenants)")
+            if self.memory_gb and limit:
+                held = sum(t.memory_limit_gb for t in self.tenants.values())
+                if held + limit > self.memory_gb + 1e-6:
+                    raise AdmissionError(f"slice of {limit} GB does not fit: {held} of {self.memory_gb} GB held")
+            tid = self._next_id
+            self._next_id += 1
+        with self._build_lock:
+            t = self._build(tid, req, dtype, limit)
+        with self._lock:
+            self.tenants[tid] = t
+        log.info("tenant %d (%s) registered: %.3f GB of a %s GB slice", tid, t.pod, t.footprint_gb, limit or "-")
+        return t
+
+    def _build(self, tid: int, req: dict, dtype: str, limit: float) -> Tenant:
+        import torch
+
+        from ..models.pod import _build
+        from ..models.yolos import GraphedTenant, demo_input_hw
+
+        seed = int(req.get("seed", 0))
+        mask = req.get("cu_mask") or None
+        if not self.gpu:
+            m, x = _build(dtype, seed, demo_input_hw(), "cpu")
+            return Tenant(tid, str(req.get("pod", tid)), limit, dtype, m, x)
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        stream = None
+        try:
+            m, x = _build(dtype, seed, demo_input_hw(), "cuda")
+            if mask:
+                from ..bench_support import cus_from_hex
+                from ..ops.streams import CUMaskedStream
+
+                stream = CUMaskedStream(cus_from_hex(mask), self.info["multiprocessor_count"])
+            gt = GraphedTenant(m, stream.torch if stream else self._setup_stream, x)
+            with torch.no_grad():
+                if self.graphs:  # the lanes keep replaying other tenants meanwhile
+                    gt.capture(capture_error_mode="thread_local")
+                else:
+                    gt.launch()
+                    gt.stream.synchronize()
+            peak = (torch.cuda.max_memory_allocated() - base) / 2 ** 30
+        except Exception:
+            if stream is not None:
+                stream.close()
+            raise
+        t = Tenant(tid, str(req.get("pod", tid)), limit, dtype, m, x, stream=stream, graph=gt.graph,
+                   outputs=gt.outputs, footprint_gb=round(peak, 3), cu_mask=mask)
+        if limit and peak > limit:
+            self._free(t)
+            raise AdmissionError(f"tenant needs {peak:.2f} GB, its slice has {limit} GB")
+        return t
+
+    def _free(self, t: Tenant) -> None:
+        t.graph = t.model = t.x = None
+        t.outputs = ()
+        if t.stream is not None:
+            t.stream.close()
+            t.stream = None
+        if self.gpu:
+            import torch
+
+            torch.cuda.empty_cache()
+
+    def _unregister(self, t: Tenant) -> None:
+        with self._lock:
+            self.tenants.pop(t.id, None)
+        with self._build_lock:
+            self._free(t)
+        log.info("tenant %d (%s) left after %d inferences", t.id, t.pod, t.completed)
+
+    def stats(self) -> dict:
+        with self._lock:
+            ts = [{"tenant": t.id, "pod": t.pod, "completed": t.completed, "gpu_s": round(t.gpu_s, 4),
+                   "footprint_gb": t.footprint_gb, "memory_limit_gb": t.memory_limit_gb, "cu_mask": t.cu_mask}
+                  for t in self.tenants.values()]
+        return {"tenants": ts, "server": self.info, "queued": self._q.qsize(), "pid": os.getpid()}
+
+    # ------------------------------------------------------------ lanes
+    def _lane(self, i: int) -> None:
+        import torch
+
+        lane = self._lanes[i] if self.gpu else None
+        while True:
+            job = self._q.get()
+            if job is None:
+                return
+            job.t_start = time.monotonic()
+            try:
+                self._run(job, lane)
+            except Exception as e:  # reported to that tenant only
+                job.error = f"{type(e).__name__}: {e}"
+            job.t_end = time.monotonic()
+            t = job.tenant
+            t.completed += 1
+            t.gpu_s += job.t_end - job.t_start
+            job.done.set()
+
+    def _run(self, job: _Job, lane) -> None:
+        import torch
+
+        t = job.tenant
+        x_in = None
+        if job.payload:
+            x_in = np.frombuffer(job.payload, dtype=np.float32)
+            if x_in.size != t.x.numel():
+                raise ValueError(f"input has {x_in.size} values, the tenant's model takes {t.x.numel()}")
+        with torch.no_grad():
+            if not self.gpu:
+                if x_in is not None:
+                    t.x.copy_(torch.from_numpy(x_in.copy()).view(t.x.shape))
+                t.outputs = t.model(t.x)
+            else:
+                s = t.stream.torch if t.stream is not None else lane
+                with torch.cuda.stream(s):
+                    if x_in is not None:
+                        t.x.copy_(torch.from_numpy(x_in.copy()).view(t.x.shape).to(t.x.dtype))
+                    if t.graph is not None:
+                        t.graph.replay()
+                    else:
+                        t.outputs = t.model(t.x)
+                s.synchronize()
+            if job.want_outputs:
+                job.outputs = [o.detach().float().cpu().numpy() for o in t.outputs]
+
+
+__all__ = ["PodServer", "Tenant", "AdmissionError", "DEFAULT_LANES", "DEFAULT_MAX_TENANTS"]

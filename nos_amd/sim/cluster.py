@@ -104,18 +104,23 @@ class SimCluster:
     # ------------------------------------------------------------ topology
     def add_node(self, name: str, kind: str | None = C.PARTITIONING_CUMASK, gpus: int = 8, compute: str = "SPX",
                  memory: str = "NPS1", smi=None, runtime=None, on_stop=None, probe=None,
-                 node_resources: dict | None = None) -> SimNode:
+                 node_resources: dict | None = None, pod_server_tenants: int = 0,
+                 pod_server_dir: str = C.DEFAULT_POD_SERVER_SOCKET_DIR) -> SimNode:
+        """``pod_server_tenants`` > 0: the node's cumask slices are served by a
+        pod server per GPU (labeler + device plugin as a DaemonSet with
+        ``podServerTenants`` / ``podServerSocketDir`` would run them)."""
         smi = smi or FakeSmi(gpus=gpus, compute=compute, memory=memory, node=name)
         labels = {"kubernetes.io/hostname": name}
         if kind:
             labels[C.LABEL_GPU_PARTITIONING] = kind
         self.api.create(kf.build_node(name).with_labels(labels).get())
-        plugin = NosAmdDevicePlugin(name, smi, mode=kind, cu_policy=self.cu_policy)
+        plugin = NosAmdDevicePlugin(name, smi, mode=kind, cu_policy=self.cu_policy,
+                                    pod_server_dir=pod_server_dir if pod_server_tenants > 0 else "")
         kubelet = Kubelet(self.api, name, [plugin], node_resources=node_resources, runtime=runtime, on_stop=on_stop)
         kubelet.sync_node_status()
         mgr = Manager(self.api, f"node-{name}", self.clock, resync_s=self.resync_s)
         mgr.add(kubelet.controller())
-        labeler = NodeLabeler(self.api, name, smi)
+        labeler = NodeLabeler(self.api, name, smi, pod_server_tenants)
         mgr.add(labeler.controller())
         agents: dict = {"labeler": labeler}
         if kind == C.PARTITIONING_AMDPART:

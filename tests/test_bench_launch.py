@@ -64,7 +64,9 @@ def test_latency_table_rows_are_self_consistent():
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     rows = d["latency_table"]
-    assert [(t["mode"], t["pods"]) for t in rows] == [("shared", 1), ("shared", 3), ("cumask", 1), ("cumask", 3)]
+    # server mode (the default) adds pod-server rows in front of the process-pod rows
+    assert [(t["mode"], t["pods"]) for t in rows] == [("server", 1), ("server", 3), ("shared", 1), ("shared", 3),
+                                                      ("cumask", 1), ("cumask", 3)]
     for t in rows:
         assert t["concurrent"] == t["pods"]
         assert t["pods_over_latency"] == pytest.approx(t["inf_per_s"], rel=1e-3)
