@@ -77,7 +77,7 @@ def parse_args(argv=None):
                          "pods are CPU-only client processes, their inferences run in one HIP context); "
                          "shared: each pod its own GPU process, memory-capped, kernels on all CUs; "
                          "cumask: each pod its own GPU process with exclusive XCD-symmetric CUs")
-    ap.add_argument("--server-lanes", type=int, default=8,
+    ap.add_argument("--server-lanes", type=int, default=12,
                     help="pod server lanes (streams, one hardware queue each) the tenants' graphs run on")
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-graphs", action="store_true")

@@ -146,7 +146,7 @@ def test_client_side_never_imports_torch():
     import subprocess
     import sys
 
-    code = ("import sys; import nos_amd.podserver.client, nos_amd.podserver.protocol; "
+    code = ("import sys; import nos_amd.podserver.client, nos_amd.podserver.protocol, nos_amd.models.pod; "
             "print('torch' in sys.modules)")
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True)
     assert out.stdout.strip() == "False"
