@@ -69,6 +69,12 @@ DEFAULT_VALUES: dict = {
                            "defaultComputeMode": "SPX", "defaultMemoryMode": "NPS1"},
         "gpuAgent": {"enabled": True, "reportConfigIntervalSeconds": 10, "probeEnabled": True},
         "devicePlugin": {"enabled": True},
+        # pod server on cumask nodes (nos_amd/podserver, the MPS analogue): one
+        # server process per GPU hosts every slice pod's inferences, so slices
+        # per GPU are bounded by memory and tenantsPerGpu, not by the 8 HWS
+        # process slots
+        "podServer": {"enabled": False, "tenantsPerGpu": 48, "lanes": 12,
+                      "socketDir": C.DEFAULT_POD_SERVER_SOCKET_DIR},
     },
 }
 
@@ -118,6 +124,9 @@ def validate_values(v: dict) -> None:
         raise ValueError("gpuPartitioner.slicePlacement must be pack|spread|measured")
     if gp["cuPolicy"] not in ("even", "proportional", "shared"):
         raise ValueError("gpuPartitioner.cuPolicy must be even|proportional|shared")
+    ps = gp["podServer"]
+    if ps["enabled"] and not (1 <= int(ps["lanes"]) <= 32 and int(ps["tenantsPerGpu"]) >= 1):
+        raise ValueError("gpuPartitioner.podServer: lanes must be 1..32 (one HW queue each), tenantsPerGpu >= 1")
     if int(v["amdGpuResourceMemoryGB"]) <= 0:
         raise ValueError("amdGpuResourceMemoryGB must be > 0")
     if v["metrics"]["serviceMonitor"] and not v["metrics"]["authProxy"]:
@@ -440,7 +449,7 @@ def gpupartitioner() -> dict[str, list[dict]]:
 def node_agents() -> dict[str, list[dict]]:
     out: dict[str, list[dict]] = {}
     gp = _V["gpuPartitioner"]
-    pa, ga = gp["partitionAgent"], gp["gpuAgent"]
+    pa, ga, ps = gp["partitionAgent"], gp["gpuAgent"], gp["podServer"]
     node_rules = [_rule([""], ["nodes"], RO + ["patch", "update"]), _rule([""], ["pods"], RO + ["delete"]),
                   _rule([""], ["configmaps"], RO), EVENTS]
     # partition agent (migagent analogue)
@@ -466,7 +475,8 @@ def node_agents() -> dict[str, list[dict]]:
     vol, mnt = _cfg_mount(name + "-config")
     cfg = {"apiVersion": C.CONFIG_API_VERSION, "kind": "GpuAgentConfig", "health": {"healthProbeBindAddress": ":8081"},
            "metrics": {"bindAddress": "127.0.0.1:8080"},
-           "reportConfigIntervalSeconds": ga["reportConfigIntervalSeconds"], "probeEnabled": ga["probeEnabled"]}
+           "reportConfigIntervalSeconds": ga["reportConfigIntervalSeconds"], "probeEnabled": ga["probeEnabled"],
+           "podServerTenants": ps["tenantsPerGpu"] if ps["enabled"] else 0}
     c = _container("gpuagent", "nos_amd.cmd.gpuagent", ["--config", "/etc/nos-amd/gpu_agent_config.yaml"],
                    image=IMAGE_ROCM, env=NODE_ENV, mounts=HOST_MOUNTS + [mnt], privileged=True)
     if ga["enabled"]:
@@ -483,7 +493,7 @@ def node_agents() -> dict[str, list[dict]]:
            "health": {"healthProbeBindAddress": ":8081"},
            "configMap": {"name": C.DEFAULT_DEVICE_PLUGIN_CM_NAME, "namespace": _ns()},
            "socketDir": C.DEVICE_PLUGIN_DIR, "cuPolicy": gp["cuPolicy"], "deviceEnv": "container",
-           "rescanSeconds": 5}
+           "rescanSeconds": 5, "podServerSocketDir": ps["socketDir"] if ps["enabled"] else ""}
     c = _container("device-plugin", "nos_amd.cmd.deviceplugin", ["--config", "/etc/nos-amd/device_plugin_config.yaml"],
                    image=IMAGE_ROCM, env=NODE_ENV,
                    mounts=HOST_MOUNTS + [{"name": "device-plugins", "mountPath": C.DEVICE_PLUGIN_DIR}, mnt],
@@ -500,6 +510,20 @@ def node_agents() -> dict[str, list[dict]]:
         out["deviceplugin/daemonset.yaml"] = [_sa(name), _config_map(name + "-config", {
             "device_plugin_config.yaml": yaml.safe_dump(cfg)})] + dss
         out["deviceplugin/rbac.yaml"] = _cluster_role(name, node_rules)
+    # pod server (MPS-daemon analogue): one process per GPU, sockets in a host
+    # directory the device plugin mounts into every pod-server slice pod
+    if ps["enabled"]:
+        name = "nos-amd-podserver"
+        c = _container("podserver", "nos_amd.cmd.podserver",
+                       ["--gpus", "all", "--socket-dir", ps["socketDir"], "--lanes", str(ps["lanes"]),
+                        "--max-tenants", str(ps["tenantsPerGpu"])],
+                       image=IMAGE_ROCM, env=NODE_ENV,
+                       mounts=HOST_MOUNTS[:2] + [{"name": "podserver-sockets", "mountPath": ps["socketDir"]}],
+                       privileged=True, probes=False)
+        c["resources"] = {"requests": {"cpu": "2", "memory": "4Gi"}, "limits": {"memory": "64Gi"}}
+        ds = _daemonset(name, c, C.PARTITIONING_CUMASK, HOST_VOLUMES[:2] + [
+            {"name": "podserver-sockets", "hostPath": {"path": ps["socketDir"], "type": "DirectoryOrCreate"}}])
+        out["podserver/daemonset.yaml"] = [_sa(name), ds]
     return out
 
 

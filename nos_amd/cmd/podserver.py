@@ -22,9 +22,50 @@ def socket_path(socket_dir: str | os.PathLike, gpu: int) -> Path:
     return Path(socket_dir) / f"gpu-{gpu}.sock"
 
 
+def _gpu_indices(spec: str) -> list[int]:
+    """``all`` (amd-smi's GPUs, read without initialising HIP) or a comma list."""
+    if spec != "all":
+        return [int(v) for v in spec.split(",") if v.strip()]
+    from ..gpu.amdsmi import AmdSmi
+
+    return [g.index for g in AmdSmi.real().gpus()]
+
+
+def supervise(gpus: list[int], argv: list[str], restart_s: float = 2.0) -> int:
+    """One server process per GPU, restarted when it dies (the DaemonSet pod's
+    entry point).  This process never touches the GPU, so starting the
+    servers from it is safe."""
+    import subprocess
+    import time
+
+    def start(g):
+        return subprocess.Popen([sys.executable, "-m", "nos_amd.cmd.podserver", "--gpu", str(g)] + argv)
+
+    procs = {g: start(g) for g in gpus}
+    stop = threading.Event()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, lambda *_: stop.set())
+    while not stop.wait(1.0):
+        for g, p in list(procs.items()):
+            if p.poll() is not None:
+                logging.getLogger("nos_amd.podserver").warning("server of GPU %d exited (%s): restarting", g, p.returncode)
+                time.sleep(restart_s)
+                procs[g] = start(g)
+    for p in procs.values():
+        p.terminate()
+    for p in procs.values():
+        try:
+            p.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    return 0
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpu", type=int, default=0, help="host GPU index (HIP_VISIBLE_DEVICES unless already set)")
+    ap.add_argument("--gpus", default="", help="'all' or a comma list: supervise one server per GPU")
+    ap.add_argument("--log-level", default="info")
     ap.add_argument("--socket-dir", default="")
     ap.add_argument("--socket", default="", help="explicit socket path (default <socket-dir>/gpu-<gpu>.sock)")
     ap.add_argument("--lanes", type=int, default=8, help="streams = hardware queues the tenants are served on")
@@ -33,7 +74,14 @@ def main(argv=None) -> int:
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
     ap.add_argument("--no-graphs", action="store_true")
     args = ap.parse_args(argv)
-    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    if args.gpus:
+        rest = ["--socket-dir", args.socket_dir, "--lanes", str(args.lanes), "--max-tenants", str(args.max_tenants),
+                "--memory-gb", str(args.memory_gb), "--device", args.device, "--log-level", args.log_level]
+        if args.no_graphs:
+            rest.append("--no-graphs")
+        return supervise(_gpu_indices(args.gpus), rest)
     # before anything initialises HIP: the GPU, and one hardware queue per lane
     if args.device == "cuda":
         os.environ.setdefault("HIP_VISIBLE_DEVICES", str(args.gpu))

@@ -188,3 +188,53 @@ def test_pod_server_node_schedules_slices_by_memory_not_hws_slots():
     assert len(info["envs"]) == 28
     assert all(e[C.ENV_POD_SERVER] == "/tmp/psx/gpu-1.sock" and C.ENV_VISIBLE_DEVICES not in e
                for e in info["envs"])
+
+
+def test_podserver_binary_supervises_one_server_per_gpu(tmp_path):
+    """``nos_amd.cmd.podserver --gpus 0,1`` (the DaemonSet entry point): one
+    server per GPU at <socket-dir>/gpu-<i>.sock, stopped by SIGTERM."""
+    import os
+    import signal
+    import subprocess
+    import sys
+
+    from nos_amd.cmd.podserver import socket_path
+
+    env = {**os.environ, "OMP_NUM_THREADS": "1"}
+    p = subprocess.Popen([sys.executable, "-m", "nos_amd.cmd.podserver", "--gpus", "0,1", "--device", "cpu",
+                          "--socket-dir", str(tmp_path), "--lanes", "1"], env=env,
+                         stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        for g in (0, 1):
+            c = PodClient(socket_path(tmp_path, g), connect_timeout_s=60)
+            c.register(f"p{g}")
+            c.infer()
+            assert c.stats()["server"]["device"] == "cpu"
+            c.close()
+    finally:
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) == 0
+
+
+def test_manifests_render_the_pod_server_and_its_configs():
+    import yaml
+
+    from nos_amd.api import config as cfgmod
+    from nos_amd.cmd import manifests as m
+
+    out = m.render(m.apply_set(m.merge_values(m.DEFAULT_VALUES, {}), "gpuPartitioner.podServer.enabled=true"))
+    ds = [o for o in yaml.safe_load_all(out["podserver/daemonset.yaml"]) if o and o["kind"] == "DaemonSet"][0]
+    spec = ds["spec"]["template"]["spec"]
+    assert spec["nodeSelector"] == {C.LABEL_GPU_PARTITIONING: C.PARTITIONING_CUMASK}
+    assert spec["containers"][0]["args"][:2] == ["--gpus", "all"]
+
+    def embedded(key, fname):
+        cm = [o for o in yaml.safe_load_all(out[key]) if o and o["kind"] == "ConfigMap"][0]
+        return cfgmod.parse(yaml.safe_load(cm["data"][fname]))
+
+    assert embedded("gpuagent/daemonset.yaml", "gpu_agent_config.yaml").pod_server_tenants == 48
+    assert embedded("deviceplugin/daemonset.yaml", "device_plugin_config.yaml").pod_server_socket_dir == \
+        C.DEFAULT_POD_SERVER_SOCKET_DIR
+    with pytest.raises(ValueError, match="lanes"):
+        m.render(m.apply_set(m.merge_values(m.DEFAULT_VALUES, {"gpuPartitioner": {"podServer": {
+            "enabled": True, "lanes": 64}}}), "namespace=nos-system"))
