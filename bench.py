@@ -12,12 +12,15 @@ What one run does, per GPU (one rank per GPU, RCCL for the rank barrier):
 1. control plane (untimed, CPU): the nos-amd scheduler, cumask partitioner
    and device plugin (in-process simulated cluster) place ``--pods-per-gpu``
    pods requesting ``amd.com/gpu-<slice>gb`` on an N-GPU node.  Each pod
-   gets the device plugin's allocation env (``HIP_VISIBLE_DEVICES``,
-   ``NOS_AMD_MEMORY_LIMIT_GB``, and ``ROC_GLOBAL_CU_MASK`` for ``--mode
-   cumask``).  The node's schedulable capacity for the slice size is also
-   counted by the simulator (``schedulable_fractional_pods_per_node_sim``);
-2. data plane: each pod is started as its own process with that env
-   (:mod:`nos_amd.models.pod`), YOLOS-small fp32 (the reference's
+   gets the device plugin's allocation env: ``NOS_AMD_POD_SERVER`` (the
+   GPU's server socket) + ``NOS_AMD_MEMORY_LIMIT_GB`` in server mode,
+   otherwise ``HIP_VISIBLE_DEVICES``, ``NOS_AMD_MEMORY_LIMIT_GB`` and, for
+   ``--mode cumask``, ``ROC_GLOBAL_CU_MASK``.  The node's schedulable capacity
+   for the slice size is also counted by the simulator
+   (``schedulable_fractional_pods_per_node_sim``);
+2. data plane: in server mode one pod server per rank (its GPU,
+   ``--server-lanes`` streams); each pod is started as its own process with
+   its env (:mod:`nos_amd.models.pod`), YOLOS-small fp32 (the reference's
    precision), random-init weights, a synthetic 800x1066 image;
 3. once every pod is warm, ``--warmup`` then ``--steps`` slices of
    ``--step-s`` wall seconds are timed (barrier + synchronize on both
@@ -26,13 +29,18 @@ What one run does, per GPU (one rank per GPU, RCCL for the rank barrier):
    through the window (no gap > 25 % of it).
 
 value = fractional pods observed running concurrently on the node (all GPUs).
-On MI355X the bound is not memory but the amdgpu hardware scheduler: it runs
-at most 8 GPU processes per logical GPU at once (hws_max_conc_proc; more are
-time-sliced at a ~50 ms quantum, aggregate throughput falls:
-profiles/r02_pods_vs_throughput_hwqueues.json), so the control plane
-schedules at most 8 slices per SPX GPU (node label
-amd.com/gpu.max-concurrent-processes, nos_amd/gpu/kfd.py) and the default
-slice is 288 GB / 8 = 36 GB: schedulable == observed.  vs_baseline =
+Default ``--mode server``: the pods' slices are served by the GPU's pod server
+(nos_amd/podserver, the MPS analogue).  Every pod is its own CPU-only client
+process, and its inferences run as HIP-graph replays in one server process per
+GPU.  Separate GPU processes are bounded by the amdgpu hardware scheduler,
+which runs at most 8 GPU processes per logical GPU at once
+(hws_max_conc_proc; more are time-sliced at a ~50 ms quantum and aggregate
+throughput falls: profiles/r02_pods_vs_throughput_hwqueues.json).  The server
+is ONE such process, so as with the reference's MPS only memory bounds the
+slices: 28 x 10 GB pods per 288 GB MI355X, the reference's 10 GB slice size.
+``--mode shared|cumask`` runs each pod as its own GPU process (8 x 36 GB
+slices, the HWS bound; node label amd.com/gpu.max-concurrent-processes,
+nos_amd/gpu/kfd.py).  vs_baseline =
 value / (8 x GPUs): 8 is the reference's schedulable 10 GB fractional pods per
 A100-80GB (MPS).  gpu_util_pct is the mean amd-smi gfx activity over the window.
 aggregate_inf_per_s (fp32) is compared with 21.89 inf/s per GPU (the
@@ -40,7 +48,7 @@ reference's best aggregate, 7 MPS pods on one A100).
 
 Also in the JSON: one whole-GPU pod's rate (``--ref-pod-s``), a bf16 fleet on
 the gfx950 kernels (``--extra-bf16-s``), the reference demo's latency table
-(1/3/5/7 pods, shared and CU-mask slices; default on single-GPU runs,
+(1/3/5/7 pods: pod-server, shared and CU-mask slices; default on single-GPU runs,
 ``--table``), and with WORLD_SIZE > 1 a data-parallel trainer pod per GPU
 (slot 0: its own pod process with its device-plugin env, CU mask included,
 nos_amd/models/trainer_pod.py -- bf16 MLP forward + backward with bucketed
