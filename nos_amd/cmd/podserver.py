@@ -31,7 +31,7 @@ def _gpu_indices(spec: str) -> list[int]:
     return [g.index for g in AmdSmi.real().gpus()]
 
 
-def supervise(gpus: list[int], argv: list[str], restart_s: float = 2.0) -> int:
+def supervise(gpus: list[int], argv: list[str], metrics_port: int = 0, restart_s: float = 2.0) -> int:
     """One server process per GPU, restarted when it dies (the DaemonSet pod's
     entry point).  This process never touches the GPU, so starting the
     servers from it is safe."""
@@ -39,7 +39,8 @@ def supervise(gpus: list[int], argv: list[str], restart_s: float = 2.0) -> int:
     import time
 
     def start(g):
-        return subprocess.Popen([sys.executable, "-m", "nos_amd.cmd.podserver", "--gpu", str(g)] + argv)
+        port = ["--metrics-port", str(metrics_port + g)] if metrics_port else []
+        return subprocess.Popen([sys.executable, "-m", "nos_amd.cmd.podserver", "--gpu", str(g)] + argv + port)
 
     procs = {g: start(g) for g in gpus}
     stop = threading.Event()
@@ -73,6 +74,8 @@ def main(argv=None) -> int:
     ap.add_argument("--memory-gb", type=float, default=0.0, help="slice memory the server admits (0 = the GPU's)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--metrics-port", type=int, default=0,
+                    help="Prometheus /metrics of this server (supervisor: port + GPU index; 0 = off)")
     args = ap.parse_args(argv)
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
@@ -81,7 +84,7 @@ def main(argv=None) -> int:
                 "--memory-gb", str(args.memory_gb), "--device", args.device, "--log-level", args.log_level]
         if args.no_graphs:
             rest.append("--no-graphs")
-        return supervise(_gpu_indices(args.gpus), rest)
+        return supervise(_gpu_indices(args.gpus), rest, args.metrics_port)
     # before anything initialises HIP: the GPU, and one hardware queue per lane
     if args.device == "cuda":
         os.environ.setdefault("HIP_VISIBLE_DEVICES", str(args.gpu))
@@ -92,6 +95,10 @@ def main(argv=None) -> int:
     path = args.socket or socket_path(args.socket_dir or C.DEFAULT_POD_SERVER_SOCKET_DIR, args.gpu)
     srv = PodServer(path, device=args.device, lanes=args.lanes, max_tenants=args.max_tenants,
                     memory_gb=args.memory_gb or None, graphs=not args.no_graphs).start()
+    if args.metrics_port:
+        from ..observability import metrics
+
+        metrics.serve(args.metrics_port)
     stop = threading.Event()
     for sig in (signal.SIGTERM, signal.SIGINT):
         signal.signal(sig, lambda *_: stop.set())

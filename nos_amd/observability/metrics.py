@@ -33,6 +33,16 @@ ALLREDUCE_BUSBW = Gauge("nos_allreduce_busbw_gbps", "tenant all-reduce bus bandw
 RECONCILES = Counter("nos_reconciles_total", "reconcile calls", ["controller", "result"], registry=REGISTRY)
 INFERENCE_TIME = Histogram("inference_time_seconds", "Time required for running a single inference",
                            registry=REGISTRY)  # same name as the reference demo client
+# pod server (nos_amd/podserver): tenants hosted, requests waiting for a lane,
+# completed inferences per pod, request latency (queue + replay)
+PODSERVER_TENANTS = Gauge("nos_podserver_tenants", "pods hosted by the GPU's pod server", ["gpu"],
+                          registry=REGISTRY)
+PODSERVER_QUEUED = Gauge("nos_podserver_queued_requests", "requests waiting for a lane", ["gpu"], registry=REGISTRY)
+PODSERVER_INFERENCES = Counter("nos_podserver_inferences_total", "inferences run for a pod", ["gpu", "pod"],
+                               registry=REGISTRY)
+PODSERVER_REQUEST_TIME = Histogram("nos_podserver_request_seconds", "pod-server request time (queue + replay)",
+                                   ["gpu"], registry=REGISTRY,
+                                   buckets=(0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1))
 
 
 def exposition() -> bytes:

@@ -54,6 +54,7 @@ from pathlib import Path
 
 import numpy as np
 
+from ..observability import metrics as M
 from . import protocol as P
 
 log = logging.getLogger("nos_amd.podserver")
@@ -121,6 +122,7 @@ class PodServer:
         self.kernel_config = kernel_config
         self.memory_gb = memory_gb
         self.info: dict = {}
+        self.gpu_label = os.environ.get("HIP_VISIBLE_DEVICES", "0") if self.gpu else "cpu"  # metrics label
 
     # ------------------------------------------------------------ lifecycle
     def _init_device(self) -> None:
@@ -275,6 +277,7 @@ class PodServer:
             t = self._build(tid, req, dtype, limit)
         with self._lock:
             self.tenants[tid] = t
+            M.PODSERVER_TENANTS.labels(self.gpu_label).set(len(self.tenants))
         log.info("tenant %d (%s) registered: %.3f GB of a %s GB slice", tid, t.pod, t.footprint_gb, limit or "-")
         return t
 
@@ -332,6 +335,11 @@ class PodServer:
     def _unregister(self, t: Tenant) -> None:
         with self._lock:
             self.tenants.pop(t.id, None)
+            M.PODSERVER_TENANTS.labels(self.gpu_label).set(len(self.tenants))
+        try:
+            M.PODSERVER_INFERENCES.remove(self.gpu_label, t.pod)
+        except KeyError:
+            pass
         with self._build_lock:
             self._free(t)
         log.info("tenant %d (%s) left after %d inferences", t.id, t.pod, t.completed)
@@ -361,6 +369,9 @@ class PodServer:
             t = job.tenant
             t.completed += 1
             t.gpu_s += job.t_end - job.t_start
+            M.PODSERVER_INFERENCES.labels(self.gpu_label, t.pod).inc()
+            M.PODSERVER_REQUEST_TIME.labels(self.gpu_label).observe(job.t_end - job.t_enq)
+            M.PODSERVER_QUEUED.labels(self.gpu_label).set(self._q.qsize())
             job.done.set()
 
     def _run(self, job: _Job, lane) -> None:

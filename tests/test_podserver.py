@@ -238,3 +238,22 @@ def test_manifests_render_the_pod_server_and_its_configs():
     with pytest.raises(ValueError, match="lanes"):
         m.render(m.apply_set(m.merge_values(m.DEFAULT_VALUES, {"gpuPartitioner": {"podServer": {
             "enabled": True, "lanes": 64}}}), "namespace=nos-system"))
+
+
+def test_server_exports_prometheus_metrics(server):
+    from nos_amd.observability import metrics as M
+
+    c = PodClient(server.path, connect_timeout_s=5)
+    c.register("metered")
+    for _ in range(3):
+        c.infer()
+    text = M.exposition().decode()
+    assert 'nos_podserver_tenants{gpu="cpu"} 1.0' in text
+    assert 'nos_podserver_inferences_total{gpu="cpu",pod="metered"} 3.0' in text
+    assert "nos_podserver_request_seconds_count" in text
+    c.close()
+    deadline = time.monotonic() + 5
+    while server.tenants and time.monotonic() < deadline:
+        time.sleep(0.01)
+    text = M.exposition().decode()
+    assert 'pod="metered"' not in text and 'nos_podserver_tenants{gpu="cpu"} 0.0' in text
