@@ -74,6 +74,8 @@ def main(argv=None) -> int:
     ap.add_argument("--memory-gb", type=float, default=0.0, help="slice memory the server admits (0 = the GPU's)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-solo-graphs", action="store_true",
+                    help="no second graph per tenant under the whole-GPU kernel configs (replayed when it runs alone)")
     ap.add_argument("--metrics-port", type=int, default=0,
                     help="Prometheus /metrics of this server (supervisor: port + GPU index; 0 = off)")
     args = ap.parse_args(argv)
@@ -84,6 +86,8 @@ def main(argv=None) -> int:
                 "--memory-gb", str(args.memory_gb), "--device", args.device, "--log-level", args.log_level]
         if args.no_graphs:
             rest.append("--no-graphs")
+        if args.no_solo_graphs:
+            rest.append("--no-solo-graphs")
         return supervise(_gpu_indices(args.gpus), rest, args.metrics_port)
     # before anything initialises HIP: the GPU, and one hardware queue per lane
     if args.device == "cuda":
@@ -94,7 +98,8 @@ def main(argv=None) -> int:
 
     path = args.socket or socket_path(args.socket_dir or C.DEFAULT_POD_SERVER_SOCKET_DIR, args.gpu)
     srv = PodServer(path, device=args.device, lanes=args.lanes, max_tenants=args.max_tenants,
-                    memory_gb=args.memory_gb or None, graphs=not args.no_graphs).start()
+                    memory_gb=args.memory_gb or None, graphs=not args.no_graphs,
+                    solo_graphs=not args.no_solo_graphs).start()
     if args.metrics_port:
         from ..observability import metrics
 

@@ -332,15 +332,16 @@ class GraphedTenant:
     graph: torch.cuda.CUDAGraph | None = None
     outputs: tuple = field(default_factory=tuple)
 
-    def capture(self, warmup: int = 2, capture_error_mode: str = "global") -> None:
+    def capture(self, warmup: int = 2, capture_error_mode: str = "global", pool=None) -> None:
         """``capture_error_mode="thread_local"`` when other threads keep
-        launching while this one captures (the pod server's lanes)."""
+        launching while this one captures (the pod server's lanes); ``pool``
+        shares another graph's memory pool (graphs never replayed at once)."""
         with torch.cuda.stream(self.stream):
             for _ in range(warmup):
                 self.outputs = self.model(self.pixel_values)
         self.stream.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=self.stream, capture_error_mode=capture_error_mode):
+        with torch.cuda.graph(self.graph, pool=pool, stream=self.stream, capture_error_mode=capture_error_mode):
             self.outputs = self.model(self.pixel_values)
         self.stream.synchronize()
 

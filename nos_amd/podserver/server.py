@@ -34,9 +34,14 @@ Design (MI355X-first):
   CU-masked stream (``hipExtStreamCreateWithCUMask``), the per-queue form of
   ``ROC_GLOBAL_CU_MASK``.  Unmasked tenants share every CU, which is MPS's
   default.
-* **Kernel configs.**  All tenants use the fractional-pod kernel configs of
-  :func:`nos_amd.models.pod.kernel_config`: co-tenants fill the CU slots, so
-  there are no key splits and the x6 GEMMs use 128x128 tiles.
+* **Kernel configs.**  Tenants run the fractional-pod kernel configs of
+  :func:`nos_amd.models.pod.kernel_config` while co-tenants fill the CU slots
+  (no key splits, x6 GEMMs on 128x128 tiles).  A tenant alone on the GPU
+  needs the whole-GPU configs instead (fewest rounds of tiles, attention key
+  splits): configs are baked into a graph at capture, so an unmasked tenant
+  gets a second, *solo* graph captured under the whole-GPU configs in the
+  same memory pool (a tenant never replays two graphs at once), and a lane
+  replays it when no other job is running or queued (``solo_graphs``).
 
 ``device="cpu"`` runs the tiny test model without streams or graphs (protocol
 tests on machines without a GPU).
@@ -76,7 +81,10 @@ class Tenant:
     outputs: tuple = ()
     footprint_gb: float = 0.0
     cu_mask: str | None = None
+    solo_graph: object = None      # whole-GPU configs, replayed when the tenant runs alone
+    solo_outputs: tuple = ()
     completed: int = 0
+    solo_completed: int = 0
     gpu_s: float = 0.0
     registered_at: float = field(default_factory=time.monotonic)
 
@@ -101,7 +109,7 @@ class AdmissionError(RuntimeError):
 class PodServer:
     def __init__(self, socket_path: str | os.PathLike, device: str = "cuda", lanes: int = DEFAULT_LANES,
                  max_tenants: int = DEFAULT_MAX_TENANTS, memory_gb: float | None = None, graphs: bool = True,
-                 kernel_config: dict | None = None):
+                 kernel_config: dict | None = None, solo_graphs: bool = True):
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.path = Path(socket_path)
@@ -117,9 +125,13 @@ class PodServer:
         self._q: queue.Queue[_Job | None] = queue.Queue()
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
+        self._conns: dict[socket.socket, threading.Thread] = {}  # open client connections
         self._lanes: list = []
         self._sock: socket.socket | None = None
         self.kernel_config = kernel_config
+        self.solo_graphs = solo_graphs and self.graphs
+        self.solo_config: dict | None = None
+        self._busy = 0                          # lanes running a job
         self.memory_gb = memory_gb
         self.info: dict = {}
         self.gpu_label = os.environ.get("HIP_VISIBLE_DEVICES", "0") if self.gpu else "cpu"  # metrics label
@@ -133,20 +145,18 @@ class PodServer:
             self.info = {"device": "cpu", "lanes": self.lanes_n}
             return
         from ..models.pod import kernel_config
-        from ..ops import (_lib, set_attention_f32_variant, set_f32_math, set_gemm_f32_policy, set_gemm_f32x6_tile,
-                           set_gemm_policy)
+        from ..ops import _lib
 
         _lib.require_native_on_gpu()
         torch.cuda.set_device(0)
         torch.backends.cuda.matmul.allow_tf32 = False
         # fractional-pod configs: the co-tenants fill the CU slots (pod.kernel_config)
         cfg = self.kernel_config or kernel_config(0.5, os.environ, 0)
-        set_gemm_policy(cfg["gemm_bf16"])
-        set_gemm_f32_policy(cfg["gemm_f32"])
-        set_attention_f32_variant(cfg["attention_f32"])
-        set_f32_math(cfg["f32_math"])
-        set_gemm_f32x6_tile(cfg["gemm_f32x6_tile"])
         self.kernel_config = cfg
+        if self.solo_graphs:
+            solo = kernel_config(1.0, os.environ, 0)
+            self.solo_config = solo if solo != cfg else None
+        self._apply_config(cfg)
         props = torch.cuda.get_device_properties(0)
         total_gb = props.total_memory / 2 ** 30
         self.memory_gb = min(self.memory_gb or total_gb, total_gb)
@@ -156,7 +166,20 @@ class PodServer:
         self.info = {"device": props.name, "multiprocessor_count": props.multi_processor_count,
                      "lanes": self.lanes_n, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                      "memory_gb": round(self.memory_gb, 1), "kernel_config": cfg,
+                     "solo_kernel_config": self.solo_config,
                      "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES")}
+
+    @staticmethod
+    def _apply_config(cfg: dict) -> None:
+        """Process-wide kernel configs; a graph keeps the ones it was captured under."""
+        from ..ops import set_attention_f32_variant, set_f32_math, set_gemm_f32_policy, set_gemm_f32x6_tile, \
+            set_gemm_policy
+
+        set_gemm_policy(cfg["gemm_bf16"])
+        set_gemm_f32_policy(cfg["gemm_f32"])
+        set_attention_f32_variant(cfg["attention_f32"])
+        set_f32_math(cfg["f32_math"])
+        set_gemm_f32x6_tile(cfg["gemm_f32x6_tile"])
 
     def start(self) -> "PodServer":
         self._init_device()
@@ -189,10 +212,28 @@ class PodServer:
             except OSError:
                 pass
             self._sock.close()
+        # close every client connection and wait for its thread: each one
+        # unregisters (frees) its tenant, so no thread touches the GPU once stop()
+        # returns -- a daemon thread still freeing a HIP graph while the
+        # interpreter exits aborts the process
+        with self._lock:
+            conns = list(self._conns.items())
+        for c, _ in conns:
+            try:
+                c.shutdown(socket.SHUT_RDWR)
+            except OSError:
+                pass
+        for _, t in conns:
+            t.join(timeout=30)
         for _ in range(self.lanes_n):
             self._q.put(None)
         for t in self._threads:
             t.join(timeout=10)
+        with self._lock:
+            left = list(self.tenants.values())
+            self.tenants.clear()
+        for t in left:
+            self._free(t)
         try:
             self.path.unlink()
         except FileNotFoundError:
@@ -213,7 +254,10 @@ class PodServer:
                 conn, _ = self._sock.accept()
             except OSError:
                 return
-            threading.Thread(target=self._serve, args=(conn,), daemon=True).start()
+            t = threading.Thread(target=self._serve, args=(conn,), daemon=True)
+            with self._lock:
+                self._conns[conn] = t
+            t.start()
 
     def _serve(self, conn: socket.socket) -> None:
         tenant: Tenant | None = None
@@ -247,6 +291,9 @@ class PodServer:
                     elif op == "stats":
                         P.send_msg(conn, {"ok": True, **self.stats()})
                     elif op == "close":
+                        if tenant is not None:  # freed before the ack: close() returns with the slice released
+                            self._unregister(tenant)
+                            tenant = None
                         P.send_msg(conn, {"ok": True})
                         return
                     else:
@@ -256,6 +303,8 @@ class PodServer:
         finally:
             if tenant is not None:
                 self._unregister(tenant)
+            with self._lock:
+                self._conns.pop(conn, None)
             conn.close()
 
     # ------------------------------------------------------------ tenants
@@ -309,21 +358,32 @@ class PodServer:
                 else:
                     gt.launch()
                     gt.stream.synchronize()
+                solo = None
+                if self.solo_config is not None and not mask:
+                    # the lanes only replay graphs, so switching the process-wide
+                    # configs for this capture changes no other tenant's kernels
+                    solo = GraphedTenant(m, self._setup_stream, x)
+                    try:
+                        self._apply_config(self.solo_config)
+                        solo.capture(capture_error_mode="thread_local", pool=gt.graph.pool())
+                    finally:
+                        self._apply_config(self.kernel_config)
             peak = (torch.cuda.max_memory_allocated() - base) / 2 ** 30
         except Exception:
             if stream is not None:
                 stream.close()
             raise
         t = Tenant(tid, str(req.get("pod", tid)), limit, dtype, m, x, stream=stream, graph=gt.graph,
-                   outputs=gt.outputs, footprint_gb=round(peak, 3), cu_mask=mask)
+                   outputs=gt.outputs, footprint_gb=round(peak, 3), cu_mask=mask,
+                   solo_graph=solo.graph if solo else None, solo_outputs=solo.outputs if solo else ())
         if limit and peak > limit:
             self._free(t)
             raise AdmissionError(f"tenant needs {peak:.2f} GB, its slice has {limit} GB")
         return t
 
     def _free(self, t: Tenant) -> None:
-        t.graph = t.model = t.x = None
-        t.outputs = ()
+        t.graph = t.solo_graph = t.model = t.x = None
+        t.outputs = t.solo_outputs = ()
         if t.stream is not None:
             t.stream.close()
             t.stream = None
@@ -346,7 +406,8 @@ class PodServer:
 
     def stats(self) -> dict:
         with self._lock:
-            ts = [{"tenant": t.id, "pod": t.pod, "completed": t.completed, "gpu_s": round(t.gpu_s, 4),
+            ts = [{"tenant": t.id, "pod": t.pod, "completed": t.completed, "solo_completed": t.solo_completed,
+                   "gpu_s": round(t.gpu_s, 4),
                    "footprint_gb": t.footprint_gb, "memory_limit_gb": t.memory_limit_gb, "cu_mask": t.cu_mask}
                   for t in self.tenants.values()]
         return {"tenants": ts, "server": self.info, "queued": self._q.qsize(), "pid": os.getpid()}
@@ -361,10 +422,16 @@ class PodServer:
             if job is None:
                 return
             job.t_start = time.monotonic()
+            with self._lock:
+                self._busy += 1
+                alone = self._busy == 1 and self._q.qsize() == 0  # no other tenant running or waiting
             try:
-                self._run(job, lane)
+                self._run(job, lane, alone)
             except Exception as e:  # reported to that tenant only
                 job.error = f"{type(e).__name__}: {e}"
+            finally:
+                with self._lock:
+                    self._busy -= 1
             job.t_end = time.monotonic()
             t = job.tenant
             t.completed += 1
@@ -374,7 +441,7 @@ class PodServer:
             M.PODSERVER_QUEUED.labels(self.gpu_label).set(self._q.qsize())
             job.done.set()
 
-    def _run(self, job: _Job, lane) -> None:
+    def _run(self, job: _Job, lane, alone: bool = False) -> None:
         import torch
 
         t = job.tenant
@@ -387,19 +454,24 @@ class PodServer:
             if not self.gpu:
                 if x_in is not None:
                     t.x.copy_(torch.from_numpy(x_in.copy()).view(t.x.shape))
-                t.outputs = t.model(t.x)
+                t.outputs = outs = t.model(t.x)
             else:
                 s = t.stream.torch if t.stream is not None else lane
                 with torch.cuda.stream(s):
                     if x_in is not None:
                         t.x.copy_(torch.from_numpy(x_in.copy()).view(t.x.shape).to(t.x.dtype))
-                    if t.graph is not None:
+                    outs = t.outputs
+                    if alone and t.solo_graph is not None:
+                        t.solo_graph.replay()
+                        outs = t.solo_outputs
+                        t.solo_completed += 1
+                    elif t.graph is not None:
                         t.graph.replay()
                     else:
-                        t.outputs = t.model(t.x)
+                        t.outputs = outs = t.model(t.x)
                 s.synchronize()
             if job.want_outputs:
-                job.outputs = [o.detach().float().cpu().numpy() for o in t.outputs]
+                job.outputs = [o.detach().float().cpu().numpy() for o in outs]
 
 
 __all__ = ["PodServer", "Tenant", "AdmissionError", "DEFAULT_LANES", "DEFAULT_MAX_TENANTS"]

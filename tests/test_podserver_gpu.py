@@ -47,10 +47,17 @@ def test_server_replays_match_the_eager_model_bit_for_bit(server):
     x = np.random.default_rng(1).standard_normal(rep["input_shape"]).astype(np.float32)
     outs, meta = c.infer(x, outputs=True)
     assert meta["gpu_us"] > 0
-    m, _ = _build("fp32", 3, demo_input_hw(), "cuda")  # same kernels: the server's configs are process-wide
-    with torch.no_grad():
-        ref = m(torch.from_numpy(x).cuda())
-    torch.cuda.synchronize()
+    # a lone tenant replays its solo graph: the eager reference runs under the
+    # same (whole-GPU) configs, which are process-wide
+    assert next(iter(server.tenants.values())).solo_completed == 1
+    m, _ = _build("fp32", 3, demo_input_hw(), "cuda")
+    server._apply_config(server.solo_config)
+    try:
+        with torch.no_grad():
+            ref = m(torch.from_numpy(x).cuda())
+        torch.cuda.synchronize()
+    finally:
+        server._apply_config(server.kernel_config)
     for o, r in zip(outs, ref):
         assert np.array_equal(o, r.float().cpu().numpy())
     c.close()
@@ -93,3 +100,26 @@ def test_more_clients_than_lanes_all_progress(server):
     assert max(counts) <= 1.5 * min(counts) + 2, counts  # FIFO service: equal shares
     for c in clients:
         c.close()
+
+
+def test_a_lone_tenant_replays_its_solo_graph_with_the_same_results(server):
+    """A tenant alone on the GPU replays the graph captured under the whole-GPU
+    configs (key splits, latency tiles); its outputs stay within fp32
+    accuracy of the co-tenancy graph's (a key split only reorders the sums)."""
+    from nos_amd.podserver.client import PodClient
+
+    assert server.solo_config is not None and server.solo_config != server.kernel_config
+    c = PodClient(server.path, connect_timeout_s=10)
+    rep = c.register("solo", seed=5, memory_limit_gb=10)
+    x = np.random.default_rng(2).standard_normal(rep["input_shape"]).astype(np.float32)
+    outs, _ = c.infer(x, outputs=True)
+    t = next(iter(server.tenants.values()))
+    assert t.solo_graph is not None and t.solo_completed == 1
+    # the co-tenancy graph on the same input, replayed directly
+    with torch.no_grad(), torch.cuda.stream(server._setup_stream):
+        t.graph.replay()
+    server._setup_stream.synchronize()
+    for o, r in zip(outs, t.outputs):
+        r = r.float().cpu().numpy()
+        assert np.abs(o - r).max() <= 1e-4 * (np.abs(r).max() + 1e-6)
+    c.close()
