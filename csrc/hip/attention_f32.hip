@@ -49,8 +49,18 @@ __device__ __forceinline__ float xor32_sum(float v) {
 __device__ __forceinline__ int kswz(int row) { return row & 15; }
 __device__ __forceinline__ int vswz(int row) { return ((row >> 2) & 1) << 3; }
 
+// LDS-DMA as inline asm + explicit vmcnt(0) before the publishing barrier:
+// with the builtin, hipcc drained the next stage's DMA before this stage's
+// LDS reads (attention.hip: glds16)
 __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+}
+
+__device__ __forceinline__ void dma_wait_publish() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 }
 
 // G = 2: two groups of W waves walk interleaved key tiles of the same
@@ -114,6 +124,9 @@ __global__ __launch_bounds__(64 * W * G, OCC) void attn_fwd_f32_d64_kernel(
       qf[4 * u + 2] = x.z * c;
       qf[4 * u + 3] = x.w * c;
     }
+    // Q in registers before the first (asm) DMA: see attention_f32x.hip
+#pragma unroll
+    for (int u = 0; u < 32; ++u) asm volatile("" : "+v"(qf[u]));
   }
 
   // piece p: tensor p / (PIECES/2) (K, V), 4 rows from (p % (PIECES/2)) * 4;
@@ -154,7 +167,7 @@ __global__ __launch_bounds__(64 * W * G, OCC) void attn_fwd_f32_d64_kernel(
   }
   float m = 0.f, l = 0.f;  // reference max (log2 units), this lane-half's partial row sum
 
-  __syncthreads();  // stage 0 landed (vmcnt(0)) and is visible
+  dma_wait_publish();  // stage 0 landed and is visible
 
   for (int it = 0; it < niters; ++it) {
     const int buf = it & 1;
@@ -223,7 +236,7 @@ __global__ __launch_bounds__(64 * W * G, OCC) void attn_fwd_f32_d64_kernel(
           oacc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1, s[t][r], oacc[1], 0, 0, 0);
         }
     }
-    __syncthreads();  // next stage landed; every wave is done with this buffer
+    dma_wait_publish();  // next stage landed; every wave is done with this buffer
   }
 
   float a0 = 1.f;

@@ -58,8 +58,22 @@ __device__ __forceinline__ float xor32_sum(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// LDS-DMA of 16 bytes per lane issued as inline asm: with the builtin, hipcc
+// assumes every ds_read may alias an in-flight LDS-DMA and inserts
+// s_waitcnt vmcnt(0) before the first LDS read after the issue -- draining
+// the NEXT tile's loads before the CURRENT tile's math (seen in the ISA: one
+// L2/HBM round trip per tile).  The ring is ordered by the explicit
+// vmcnt(0) + barrier that ends each tile (dma_wait_publish).
 __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+}
+
+// every DMA this wave issued has landed, then the workgroup barrier publishes them
+__device__ __forceinline__ void dma_wait_publish() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 }
 
 template <bool PERSIST>
@@ -137,6 +151,13 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
         const float x[8] = {x0.x * c, x0.y * c, x0.z * c, x0.w * c, x1.x * c, x1.y * c, x1.z * c, x1.w * c};
         nos::split8(x, qf[ks][0], qf[ks][1], qf[ks][2]);
       }
+      // Q in registers before the first DMA (see glds16: the compiler cannot
+      // count the asm DMA, so a Q load sunk into the key loop would make it
+      // wait with vmcnt(n) counts that drain the in-flight tiles)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(qf[ks][p]));
     }
 
     // ---- LDS-DMA staging: per tile 6 planes x 32 rows x 128 B = 24 wave
@@ -160,14 +181,13 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
     }
     float m = 0.f, l = 0.f;  // reference max (log2 units), this lane-half's partial row sum
 
-    __syncthreads();  // tile 0 landed and is visible
+    dma_wait_publish();  // tile 0 landed and is visible
 
     for (int t = t0; t < t1; ++t) {
       const int buf = (t - t0) & 1;
       const bool more = t + 1 < t1;
       // the next tile's 6 DMA pieces, into the buffer released by the barrier
-      // ending t-1 (issuing them between the QK^T or the PV MFMA groups
-      // instead measured the same or slower: profiles/r03_f32x6_fleet_ab.json)
+      // ending t-1; they stay in flight through this tile's math
       if (more) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) stage_piece(t + 1, buf ^ 1, i);
@@ -239,7 +259,7 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
           }
           oacc[db] = nos::mma6(a, pf[s2], oacc[db]);
         }
-      __syncthreads();  // next tile landed (vmcnt(0)); every wave is done with `buf`
+      dma_wait_publish();  // next tile landed; every wave is done with `buf`
     }
 
     const float lt = xor32_sum(l);

@@ -30,6 +30,9 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("NOS_AMD_ARCH", "gfx950")
 
 HIP_SOURCES = ["attention.hip", "attention_f32.hip", "attention_f32x.hip", "gemm_f32.hip", "gemm_f32x.hip", "gemm.hip", "layernorm.hip", "probes.hip", "runtime.hip"]
+# per-source compiler flags, {file: [flags]} (CMakeLists.txt sets the same:
+# tests/test_build_config.py); tools/build_variant.py adds to it for A/B builds
+HIP_EXTRA_FLAGS: dict[str, list[str]] = {}
 HIP_LIB = HERE / "libnos_hip.so"
 SMI_LIB = HERE / "libnos_amdsmi.so"
 
@@ -94,7 +97,8 @@ def build_hip(force: bool = False, jobs: int = 8, verbose: bool = False, src_dir
     def compile_one(pair: tuple[Path, Path]) -> None:
         src, obj = pair
         _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
-              "-Wno-unused-result", "-I", str(src_dir), "-c", str(src), "-o", str(obj)], verbose)
+              "-Wno-unused-result", "-Wno-inline-asm", *HIP_EXTRA_FLAGS.get(src.name, []), "-I", str(src_dir), "-c",
+              str(src), "-o", str(obj)], verbose)
 
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:

@@ -17,3 +17,9 @@ def test_cmake_and_python_build_list_the_same_hip_sources():
     assert in_cmake == sorted(build.HIP_SOURCES)
     on_disk = sorted(p.name for p in (REPO / "csrc" / "hip").glob("*.hip"))
     assert on_disk == sorted(build.HIP_SOURCES)
+
+
+def test_cmake_sets_the_same_per_source_flags():
+    cmake = (REPO / "CMakeLists.txt").read_text()
+    props = dict(re.findall(r'set_source_files_properties\(csrc/hip/(\S+) PROPERTIES COMPILE_OPTIONS "([^"]*)"\)', cmake))
+    assert {k: v.split(";") for k, v in props.items()} == build.HIP_EXTRA_FLAGS

@@ -1,0 +1,74 @@
+"""One pod server with N YOLOS-small fp32 tenants in this process, driven by
+client threads over its Unix socket for a fixed window: the pod-server fleet
+in a single process, for ``rocprofv3 --kernel-trace --stats`` (the bench runs
+the server as its own process, under the clean pod launcher).
+
+  python tools/podserver_once.py --tenants 28 --lanes 12 --window 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import threading
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tenants", type=int, default=28)
+    ap.add_argument("--lanes", type=int, default=12)
+    ap.add_argument("--window", type=float, default=8.0)
+    ap.add_argument("--warmup", type=float, default=2.0)
+    ap.add_argument("--slice-gb", type=float, default=10.0)
+    a = ap.parse_args()
+    # one hardware queue per lane: before anything initialises HIP (cmd/podserver.py)
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(a.lanes, 32))
+    from nos_amd.podserver.client import PodClient
+    from nos_amd.podserver.server import PodServer
+
+    path = Path(tempfile.mkdtemp(prefix="nos_ps_", dir="/tmp")) / "gpu-0.sock"
+    srv = PodServer(path, device="cuda", lanes=a.lanes, max_tenants=max(48, a.tenants)).start()
+    try:
+        t0 = time.monotonic()
+        clients = [PodClient(path, connect_timeout_s=30) for _ in range(a.tenants)]
+        for i, c in enumerate(clients):
+            c.register(f"pod-{i}", seed=i, memory_limit_gb=a.slice_gb)
+        build_s = time.monotonic() - t0
+        stop = threading.Event()
+        marks: list[list[float]] = [[] for _ in clients]
+
+        def loop(i: int) -> None:
+            while not stop.is_set():
+                clients[i].infer()
+                marks[i].append(time.monotonic())
+
+        th = [threading.Thread(target=loop, args=(i,), daemon=True) for i in range(a.tenants)]
+        for t in th:
+            t.start()
+        time.sleep(a.warmup)
+        w0 = time.monotonic()
+        time.sleep(a.window)
+        w1 = time.monotonic()
+        stop.set()
+        for t in th:
+            t.join(timeout=30)
+        done = [sum(1 for m in mk if w0 <= m < w1) for mk in marks]
+        solo = sum(t.solo_completed for t in srv.tenants.values())
+        for c in clients:
+            c.close()
+        print(json.dumps({"tenants": a.tenants, "lanes": a.lanes, "window_s": round(w1 - w0, 3),
+                          "build_s": round(build_s, 1), "inf_per_s": round(sum(done) / (w1 - w0), 2),
+                          "min_done": min(done), "max_done": max(done), "solo_replays": solo,
+                          "kernel_config": srv.kernel_config}), flush=True)
+    finally:
+        srv.stop()
+
+
+if __name__ == "__main__":
+    main()
