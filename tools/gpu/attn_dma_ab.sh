@@ -7,8 +7,11 @@ O=$GRAFT_REPO_ROOT/gpurun_out/$1; shift
 TAGS="$* new"
 mkdir -p $O
 lib() { [ "$1" = new ] || echo build/variants/$1/libnos_hip.so; }
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > $O/kernels.log 2>&1 || exit 1
-tail -1 $O/kernels.log
+for tag in $TAGS; do
+  NOS_AMD_HIP_LIB=$(lib $tag) timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 \
+    --timeout-method thread > $O/kernels_$tag.log 2>&1 || exit 1
+  echo "$tag: $(tail -1 $O/kernels_$tag.log)"
+done
 for R in 1 2; do for tag in $TAGS; do
   for v in "--dtype fp32 --variant x6" "--dtype fp32 --variant x6n" "--dtype fp32 --variant auto" "--dtype bf16"; do
     NOS_AMD_HIP_LIB=$(lib $tag) timeout -k 10 120 python tools/attn_bench.py $v --batches 1,8 | sed "s/^{/{\"lib\": \"$tag\", /" >> $O/attn.jsonl 2>>$O/err.log || exit 1
