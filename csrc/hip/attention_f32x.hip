@@ -228,14 +228,14 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
       // P = exp2(S - m), split into three pieces: pf[s2][piece] covers the
       // 16 keys of registers 8*s2 .. 8*s2+7
       bf16x8_t pf[2][3];
-      f32x2_t ps2 = {0.f, 0.f};
-      const f32x2_t nm2 = {-m, -m};
+      float ls[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j2 = 0; j2 < 8; ++j2) {
-        f32x2_t x = f32x2_t{s[2 * j2], s[2 * j2 + 1]} + nm2;
-        x.x = __builtin_amdgcn_exp2f(x.x);
-        x.y = __builtin_amdgcn_exp2f(x.y);
-        ps2 += x;
+        const float x0 = __builtin_amdgcn_exp2f(s[2 * j2] - m);
+        const float x1 = __builtin_amdgcn_exp2f(s[2 * j2 + 1] - m);
+        ls[(2 * j2) & 3] += x0;
+        ls[(2 * j2 + 1) & 3] += x1;
+        const f32x2_t x = {x0, x1};
         bf16x2_t a, bb, cc;
         nos::split2(x, a, bb, cc);
         const int s2 = j2 >> 2, e = 2 * (j2 & 3);
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
         pf[s2][1][e] = bb.x; pf[s2][1][e + 1] = bb.y;
         pf[s2][2][e] = cc.x; pf[s2][2][e + 1] = cc.y;
       }
-      l += ps2.x + ps2.y;
+      l += (ls[0] + ls[1]) + (ls[2] + ls[3]);
 #pragma unroll
       for (int db = 0; db < 2; ++db)
 #pragma unroll

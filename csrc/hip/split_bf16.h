@@ -14,13 +14,16 @@ namespace nos {
 
 // x (2 lanes of a pair) -> three bf16 pieces, exactly: each residual of an
 // fp32 minus its bf16 rounding has <= 16 significant bits, so the
-// subtractions are exact
+// subtractions are exact.  The subtractions are scalar v_sub_f32 (the files
+// are built with -fno-slp-vectorize): a v_pk_add_f32 beside the MFMAs costs
+// more issue cycles than its two halves (x6 attention 3-5 % faster,
+// profiles/r03_x6_scalar_split_ab.json)
 __device__ __forceinline__ void split2(f32x2_t x, bf16x2_t& p0, bf16x2_t& p1, bf16x2_t& p2) {
   p0 = __builtin_convertvector(x, bf16x2_t);
-  const f32x2_t r1 = x - __builtin_convertvector(p0, f32x2_t);
-  p1 = __builtin_convertvector(r1, bf16x2_t);
-  const f32x2_t r2 = r1 - __builtin_convertvector(p1, f32x2_t);
-  p2 = __builtin_convertvector(r2, bf16x2_t);
+  const float r1x = x.x - (float)p0.x, r1y = x.y - (float)p0.y;
+  p1 = __builtin_convertvector(f32x2_t{r1x, r1y}, bf16x2_t);
+  const float r2x = r1x - (float)p1.x, r2y = r1y - (float)p1.y;
+  p2 = __builtin_convertvector(f32x2_t{r2x, r2y}, bf16x2_t);
 }
 
 __device__ __forceinline__ void split8(const float* x, bf16x8_t& p0, bf16x8_t& p1, bf16x8_t& p2) {

@@ -31,8 +31,13 @@ ARCH = os.environ.get("NOS_AMD_ARCH", "gfx950")
 
 HIP_SOURCES = ["attention.hip", "attention_f32.hip", "attention_f32x.hip", "gemm_f32.hip", "gemm_f32x.hip", "gemm.hip", "layernorm.hip", "probes.hip", "runtime.hip"]
 # per-source compiler flags, {file: [flags]} (CMakeLists.txt sets the same:
-# tests/test_build_config.py); tools/build_variant.py adds to it for A/B builds
-HIP_EXTRA_FLAGS: dict[str, list[str]] = {}
+# tests/test_build_config.py); tools/build_variant.py adds to it for A/B builds.
+# The bf16x6 kernels split fp32 into bf16 pieces and run the softmax with
+# scalar f32 ops: without SLP re-packing them into v_pk_*_f32 next to the
+# MFMAs, x6 attention is 3-5 % faster and the 28-pod fleet +2 %
+# (profiles/r03_x6_scalar_split_ab.json)
+HIP_EXTRA_FLAGS: dict[str, list[str]] = {"attention_f32x.hip": ["-fno-slp-vectorize"],
+                                         "gemm_f32x.hip": ["-fno-slp-vectorize"]}
 HIP_LIB = HERE / "libnos_hip.so"
 SMI_LIB = HERE / "libnos_amdsmi.so"
 
