@@ -257,3 +257,44 @@ def test_server_exports_prometheus_metrics(server):
         time.sleep(0.01)
     text = M.exposition().decode()
     assert 'pod="metered"' not in text and 'nos_podserver_tenants{gpu="cpu"} 0.0' in text
+
+
+def test_lanes_know_when_a_tenant_runs_alone(server, monkeypatch):
+    """The lane passes ``alone`` (no other job running or queued) to the run:
+    a lone client always runs alone (its solo graph on a GPU); clients that
+    keep the lanes busy mostly do not.  stop() leaves no tenant behind."""
+    seen: list[bool] = []
+    orig = server._run
+
+    def spy(job, lane, alone=False):
+        seen.append(alone)
+        time.sleep(0.01)  # long enough for co-tenants' jobs to overlap
+        return orig(job, lane, alone)
+
+    monkeypatch.setattr(server, "_run", spy)
+    c = PodClient(server.path, connect_timeout_s=5)
+    c.register("solo")
+    for _ in range(5):
+        c.infer()
+    assert seen == [True] * 5
+    seen.clear()
+    others = [PodClient(server.path, connect_timeout_s=5) for _ in range(2)]
+    for i, o in enumerate(others):
+        o.register(f"co{i}")
+    stop = threading.Event()
+
+    def loop(cl):
+        while not stop.is_set():
+            cl.infer()
+
+    th = [threading.Thread(target=loop, args=(cl,)) for cl in [c, *others]]
+    for t in th:
+        t.start()
+    time.sleep(1.0)
+    stop.set()
+    for t in th:
+        t.join()
+    assert seen.count(False) > len(seen) // 2, seen.count(False)
+    assert server._busy == 0
+    server.stop()
+    assert server.tenants == {}
