@@ -469,3 +469,31 @@ def test_qkv_projection_writing_the_attention_planes_is_bit_identical(B, S, H, v
         ops.set_f32_math("exact")
         ops.set_attention_f32_variant("auto")
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("variant", ["x6n", "x6"])
+def test_attention_planes_padding_rows_are_never_read(variant):
+    """The attention from the projection's planes never reads the padding rows
+    past S of each batch (the tail tile re-reads row S - 1 under P = 0): NaN
+    poured into them leaves the result bit-identical to the unfused path."""
+    torch.manual_seed(7)
+    B, S, H, K = 2, 77, 3, 384
+    x = torch.randn(B, S, K, device=DEV)
+    w = torch.randn(3 * H * 64, K, device=DEV) * 0.05
+    wg, c1, c2 = ops.fold_layernorm(w, torch.randn(3 * H * 64, device=DEV), torch.randn(K, device=DEV),
+                                    torch.randn(K, device=DEV))
+    ops.set_f32_math("x6")
+    ops.set_attention_f32_variant(variant)
+    try:
+        ref = ops.attention_qkv(ops.linear_ln(x, wg, c1, c2), H)
+        qkv, ws = ops.linear_ln_qkv_x6(x, wg, c1, c2, H)
+        skvp = (S + 31) // 32 * 32
+        row = 6 * H * 64  # int16 elements per token row of the six planes
+        planes = ws[:B * skvp * row].view(B, skvp, row)
+        planes[:, S:, :] = 0x7FC0  # bf16 NaN in every padding row
+        got = ops.attention_presplit(qkv, ws, H)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_f32_math("exact")
+        ops.set_attention_f32_variant("auto")
+    assert torch.isfinite(got).all() and torch.equal(got, ref)
