@@ -472,10 +472,11 @@ def test_qkv_projection_writing_the_attention_planes_is_bit_identical(B, S, H, v
 
 
 @pytest.mark.parametrize("variant", ["x6n", "x6"])
-def test_attention_planes_padding_rows_are_never_read(variant):
-    """The attention from the projection's planes never reads the padding rows
-    past S of each batch (the tail tile re-reads row S - 1 under P = 0): NaN
-    poured into them leaves the result bit-identical to the unfused path."""
+def test_attention_planes_padding_rows_never_reach_the_output(variant):
+    """Garbage in the planes' padding rows past S of each batch (NaN here)
+    never reaches the output: the presplit entry zeroes those rows before the
+    attention reads the tail tile, so the result stays bit-identical to the
+    unfused path."""
     torch.manual_seed(7)
     B, S, H, K = 2, 77, 3, 384
     x = torch.randn(B, S, K, device=DEV)
