@@ -31,8 +31,6 @@
 //    head share an XCD's L2 (K/V of one head = 870 KB at S = 3401).
 #include "common.h"
 
-#include <type_traits>
-
 namespace {
 
 constexpr int D = 64;
@@ -271,254 +269,6 @@ __global__ __launch_bounds__(NT, 4) void attn_fwd_d64_kernel(
   }
 }
 
-
-// ---------------------------------------------------------------------------
-// Ping-pong variant (nos_attn_set_bf16_variant(1)): the same tiles, fragments
-// and LDS images, but the two wave groups run OUT of phase.  A tile's work is
-// X(t) = PV of the group's previous tile + QK^T of tile t (16 MFMAs) and
-// Y(t) = its softmax (VALU + v_exp); each iteration has two phases split by
-// an s_barrier, group 0 runs X then Y and group 1 runs Y then X, so on every
-// SIMD (group-0 wave w and group-1 wave w share SIMD w % 4) one wave issues
-// MFMAs while its partner runs the softmax (MI355X_MICROARCH.md, "Two waves
-// per SIMD").  PV lags QK^T by one tile, so a stage carries the K tiles of
-// its iteration and the V tiles of the previous one (same 2-deep ring).
-__device__ __forceinline__ void glds16_asm(const void* g, unsigned char* lds_wave_base) {
-  const unsigned lds = __builtin_amdgcn_readfirstlane(
-      (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds_wave_base);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
-}
-
-__global__ __launch_bounds__(NT, 4) void attn_fwd_d64_pp_kernel(
-    const unsigned short* __restrict__ q, const unsigned short* __restrict__ k,
-    const unsigned short* __restrict__ v, unsigned short* __restrict__ o, int B, int H, int Sq, int Skv,
-    int ld_in, long long bs_in, int ld_out, long long bs_out, float c /* scale * log2(e) */, int nqb) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-
-  const int nwg = B * H * nqb;
-  const int w = nos::xcd_remap(blockIdx.x, nwg);
-  const int b = w / (H * nqb);
-  const int rem = w - b * (H * nqb);
-  const int h = rem / nqb;
-  const int qb = rem - h * nqb;
-
-  const int tid = threadIdx.x;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wid >> 2;
-  const int wq = wid & 3;
-  const int lane = tid & 63;
-  const int r = lane & 31;
-  const int hh = lane >> 5;
-
-  const unsigned short* qb_ptr = q + b * bs_in + h * D;
-  const unsigned short* kb_ptr = k + b * bs_in + h * D;
-  const unsigned short* vb_ptr = v + b * bs_in + h * D;
-
-  const int qrow = qb * QBLK + wq * 32 + r;
-  const int qrow_c = qrow < Sq ? qrow : Sq - 1;
-  bf16x8_t qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks)
-    qf[ks] = *reinterpret_cast<const bf16x8_t*>(qb_ptr + (long long)qrow_c * ld_in + ks * 16 + hh * 8);
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(qf[ks]));  // Q landed before the (asm) DMA
-
-  // stage `it`: K rows of tiles 2it, 2it+1 and V rows of tiles 2it-2, 2it-1
-  // (clamped into [0, Skv): the unused ones are never read)
-  auto stage = [&](int it, int buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = wid * 4 + i;
-      const int is_v = p >> 4;
-      const int R = (p & 15) * 8;
-      const int row = R + (lane >> 3);
-      const int g = row >> 6, lr = row & 63;
-      const int pc = lane & 7;
-      const int lc = pc ^ (is_v ? vswz(lr) : kswz(lr));
-      int kv = (it - is_v) * 2 * KVBLK + row;
-      kv = kv < 0 ? 0 : (kv < Skv ? kv : Skv - 1);
-      const unsigned short* src = (is_v ? vb_ptr : kb_ptr) + (long long)kv * ld_in + lc * 8;
-      unsigned char* dst = smem + buf * PAIR_BYTES + g * 2 * TILE_BYTES + is_v * TILE_BYTES + (R & 63) * 128;
-      glds16_asm(src, dst);
-    }
-  };
-
-  const int ntiles = (Skv + KVBLK - 1) / KVBLK;
-  const int niters = (ntiles + 1) / 2;
-
-  int koff[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) koff[ks] = r * 128 + (((2 * ks + hh) ^ kswz(r)) << 4);
-  const int g16 = (lane >> 4) & 1;
-  const int tq = (lane & 15) >> 2;
-  const int tp = lane & 3;
-  const int vlb = (tq >> 1) & 1;
-  int voff[2];
-#pragma unroll
-  for (int db = 0; db < 2; ++db)
-    voff[db] = (4 * hh + tq) * 128 + (((4 * (db ^ vlb)) + 2 * g16 + (tp >> 1)) << 4) + 8 * (tp & 1);
-
-  f32x16_t oacc[2];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { oacc[0][i] = 0.f; oacc[1][i] = 0.f; }
-  float m = 0.f, l = 0.f;
-  f32x16_t sacc[2];
-  bf16x8_t pf[2][2];
-  bool haves = false, havep = false;  // S of tile ts awaits its softmax / P awaits its PV
-  int ts = 0;
-
-  auto do_qk = [&](const unsigned char* kl) __attribute__((always_inline)) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sacc[kb][i] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(kl + koff[ks] + kb * 32 * 128);
-        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], sacc[kb], 0, 0, 0);
-      }
-    }
-  };
-  auto do_pv = [&](const unsigned char* vl) __attribute__((always_inline)) {
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const unsigned char* base = vl + voff[db] + (kb * 32 + s2 * 16) * 128;
-          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base));
-          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + 8 * 128));
-          const s16x8_t a16 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a16), pf[kb][s2],
-                                                             oacc[db], 0, 0, 0);
-        }
-    }
-  };
-  auto do_softmax = [&](int t) __attribute__((always_inline)) {
-    if ((t + 1) * KVBLK > Skv) {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int kv = t * KVBLK + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          if (kv >= Skv) sacc[kb][i] = -INFINITY;
-        }
-    }
-    float mt = sacc[0][0];
-#pragma unroll
-    for (int i = 1; i < 16; ++i) mt = fmaxf(mt, sacc[0][i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[1][i]);
-    const float mrel = fmaf(xor32_max(mt), c, -m);
-    const bool first = t == grp;
-    if (first || !__all(mrel <= RESCALE_THR)) {
-      const float delta = first ? mrel : fmaxf(mrel, 0.f);
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-      m += delta;
-      l *= alpha;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        oacc[0][i] *= alpha;
-        oacc[1][i] *= alpha;
-      }
-    }
-    const f32x2_t c2 = {c, c}, nm2 = {-m, -m};
-    f32x2_t ps2 = {0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int j2 = 0; j2 < 8; ++j2) {
-        const f32x2_t sv = {sacc[kb][2 * j2], sacc[kb][2 * j2 + 1]};
-        f32x2_t x = sv * c2 + nm2;
-        x.x = __builtin_amdgcn_exp2f(x.x);
-        x.y = __builtin_amdgcn_exp2f(x.y);
-        ps2 += x;
-        const bf16x2_t pb = __builtin_convertvector(x, bf16x2_t);
-        pf[kb][j2 >> 2][2 * (j2 & 3)] = pb.x;
-        pf[kb][j2 >> 2][2 * (j2 & 3) + 1] = pb.y;
-      }
-    l += ps2.x + ps2.y;
-  };
-
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // one loop per group (compile-time G): the register allocator then sizes
-  // each loop on its own instead of keeping both groups' live state at once
-  auto run = [&](auto gc) __attribute__((always_inline)) {
-    constexpr int G = decltype(gc)::value;
-    for (int it = 0; it <= niters; ++it) {  // iteration niters: the last PVs only
-      const int buf = it & 1;
-      if (it < niters) stage(it + 1, buf ^ 1);  // into the buffer freed by the barrier ending it-1
-      const unsigned char* kl = smem + buf * PAIR_BYTES + G * 2 * TILE_BYTES;
-      const unsigned char* vl = kl + TILE_BYTES;  // V of this group's previous tile (2it - 2 + G)
-      const int t = 2 * it + G;
-      const bool qk = it < niters && t < ntiles;
-      if constexpr (G == 0) {  // phase A: X
-        if (havep) { do_pv(vl); havep = false; }
-        if (qk) { do_qk(kl); haves = true; ts = t; }
-      } else {                 // phase A: Y of the previous tile
-        if (haves) { do_softmax(ts); haves = false; havep = true; }
-      }
-      __builtin_amdgcn_s_barrier();
-      if constexpr (G == 0) {  // phase B: Y
-        if (haves) { do_softmax(ts); haves = false; havep = true; }
-      } else {                 // phase B: X
-        if (havep) { do_pv(vl); havep = false; }
-        if (qk) { do_qk(kl); haves = true; ts = t; }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // next stage landed; everyone done with `buf`
-    }
-  };
-  if (grp == 0)
-    run(std::integral_constant<int, 0>{});
-  else
-    run(std::integral_constant<int, 1>{});
-
-  float* xch = reinterpret_cast<float*>(smem) + wq * (34 * 64);
-  if (grp == 1) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      xch[i * 64 + lane] = oacc[0][i];
-      xch[(16 + i) * 64 + lane] = oacc[1][i];
-    }
-    xch[32 * 64 + lane] = m;
-    xch[33 * 64 + lane] = l;
-  }
-  __syncthreads();
-  if (grp == 0) {
-    const float m1 = xch[32 * 64 + lane];
-    const float l1 = xch[33 * 64 + lane];
-    const bool g1 = ntiles > 1;
-    const float mf = g1 ? fmaxf(m, m1) : m;
-    const float a0 = __builtin_amdgcn_exp2f(m - mf);
-    const float a1 = g1 ? __builtin_amdgcn_exp2f(m1 - mf) : 0.f;
-    float lt = l * a0 + l1 * a1;
-    lt += __shfl_xor(lt, 32, 64);
-    const float inv = 1.f / lt;
-    if (qrow < Sq) {
-      unsigned short* op = o + b * bs_out + (long long)qrow * ld_out + h * D;
-#pragma unroll
-      for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d = 32 * db + 8 * g + 4 * hh;
-          bf16x4_t ov;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int ri = 4 * g + e;
-            const float o1 = xch[(16 * db + ri) * 64 + lane];
-            ov[e] = (__bf16)((oacc[db][ri] * a0 + o1 * a1) * inv);
-          }
-          *reinterpret_cast<bf16x4_t*>(op + d) = ov;
-        }
-    }
-  }
-}
-
-int g_bf16_variant = 0;  // 0 = lockstep groups (attn_fwd_d64_kernel), 1 = ping-pong
 }  // namespace
 
 // q/k/v: bf16 [B, S, *] rows with row stride ld_in (elements) and batch stride
@@ -532,15 +282,8 @@ NOS_API int nos_attn_fwd_d64(const void* q, const void* k, const void* v, void* 
   const int nqb = (Sq + QBLK - 1) / QBLK;
   const int nwg = B * H * nqb;
   const float c = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(g_bf16_variant == 1 ? attn_fwd_d64_pp_kernel : attn_fwd_d64_kernel, dim3(nwg), dim3(NT),
-                     LDS_BYTES, stream, (const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v,
-                     (unsigned short*)o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, nqb);
+  hipLaunchKernelGGL(attn_fwd_d64_kernel, dim3(nwg), dim3(NT), LDS_BYTES, stream, (const unsigned short*)q,
+                     (const unsigned short*)k, (const unsigned short*)v, (unsigned short*)o, B, H, Sq, Skv, ld_in,
+                     bs_in, ld_out, bs_out, c, nqb);
   return (int)hipGetLastError();
-}
-
-// bf16 attention schedule: 0 = both wave groups in lockstep (default), 1 = ping-pong
-NOS_API int nos_attn_set_bf16_variant(int v) {
-  if (v < 0 || v > 1) return (int)hipErrorInvalidValue;
-  g_bf16_variant = v;
-  return 0;
 }

@@ -277,15 +277,6 @@ def set_attention_f32_variant(variant: str) -> None:
 _ATTN_F32_VARIANT = "auto"
 
 
-def set_attention_bf16_variant(variant: str) -> None:
-    """bf16 attention schedule (csrc/hip/attention.hip): ``"lockstep"``
-    (default: both wave groups run QK^T, softmax and PV in the same phase) or
-    ``"pingpong"`` (the groups run out of phase, one group's MFMAs beside the
-    other's softmax on every SIMD)."""
-    code = {"lockstep": 0, "pingpong": 1}[variant]
-    _lib.check(_lib.lib().nos_attn_set_bf16_variant(code), "nos_attn_set_bf16_variant")
-
-
 def attention_f32_variant() -> str:
     return _ATTN_F32_VARIANT
 

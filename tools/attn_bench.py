@@ -20,7 +20,6 @@ def main() -> None:
     ap.add_argument("--H", type=int, default=6)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--variant", default="auto")
-    ap.add_argument("--bf16-variant", default="lockstep", help="bf16 schedule: lockstep | pingpong")
     a = ap.parse_args()
     import torch
 
@@ -28,7 +27,6 @@ def main() -> None:
 
     dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[a.dtype]
     ops.set_attention_f32_variant(a.variant)
-    ops.set_attention_bf16_variant(a.bf16_variant)
     for B in map(int, a.batches.split(",")):
         qkv = torch.randn(B, a.S, 3 * a.H * 64, device="cuda", dtype=dt)
         out = torch.empty(B, a.S, a.H * 64, device="cuda", dtype=dt)
@@ -49,7 +47,7 @@ def main() -> None:
             s.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / (a.iters // 10 * 10)
         fl = 4.0 * B * a.H * a.S * a.S * 64
-        print(json.dumps({"dtype": a.dtype, "variant": a.variant if a.dtype == "fp32" else a.bf16_variant, "B": B, "S": a.S, "H": a.H, "us": round(us, 2),
+        print(json.dumps({"dtype": a.dtype, "variant": a.variant, "B": B, "S": a.S, "H": a.H, "us": round(us, 2),
                           "tflops": round(fl / us / 1e6, 1)}), flush=True)
 
 
