@@ -367,14 +367,18 @@ class PodServerProc:
 
         from nos_amd.podbench import REPO
 
-        self.path = os.path.join(args.pod_server_dir, f"gpu-{args.local_gpu}.sock")
+        from nos_amd.podserver.allocations import socket_path
+
+        self.path = str(socket_path(args.pod_server_dir, args.local_gpu))
         env = {k: v for k, v in os.environ.items()
                if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
                             "ROC_GLOBAL_CU_MASK", "CUDA_VISIBLE_DEVICES") and not k.startswith("TORCHELASTIC_")}
         env.update({"HIP_VISIBLE_DEVICES": gpu_env, "PYTHONPATH": str(REPO) + os.pathsep + env.get("PYTHONPATH", "")})
-        cmd = [sys.executable, "-u", "-m", "nos_amd.cmd.podserver", "--gpu", str(args.local_gpu), "--socket",
-               self.path, "--lanes", str(args.server_lanes), "--max-tenants", str(POD_SERVER_TENANTS),
-               "--device", args.device]
+        # the server reads the slices from the records the (simulated) device
+        # plugin wrote when it allocated them (tokens; podserver/allocations.py)
+        cmd = [sys.executable, "-u", "-m", "nos_amd.cmd.podserver", "--gpu", str(args.local_gpu), "--hip-id",
+               gpu_env, "--socket-dir", args.pod_server_dir, "--lanes", str(args.server_lanes),
+               "--max-tenants", str(POD_SERVER_TENANTS), "--device", args.device]
         self.log = os.path.join(workdir, "podserver.log")
         self.proc = launcher.spawn(cmd, env, self.log, str(REPO))
         self._timeout = subprocess.TimeoutExpired

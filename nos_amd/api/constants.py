@@ -84,6 +84,7 @@ ENV_VISIBLE_DEVICES = "HIP_VISIBLE_DEVICES"
 ENV_MEMORY_LIMIT_GB = "NOS_AMD_MEMORY_LIMIT_GB"
 ENV_POD_SERVER = "NOS_AMD_POD_SERVER"        # pod-server socket of the slice's GPU
 ENV_POD_CU_MASK = "NOS_AMD_POD_CU_MASK"      # CU mask the pod server applies to the tenant's stream
+ENV_POD_TOKEN = "NOS_AMD_POD_TOKEN"          # per-allocation token: the pod server's key to the slice record
 DEFAULT_POD_SERVER_SOCKET_DIR = "/run/nos-amd/podserver"
 
 # --------------------------------------------------------------- defaults

@@ -56,7 +56,12 @@ def schedulable_pods(n_gpus: int, slice_gb: int, num_cus: int = 256, placement: 
     8 HWS process slots, or ``pod_server_tenants`` when the pod server hosts
     the slices; hybrid: the partitioner also picks each GPU's compute/memory
     mode, 8 slots per partition)."""
-    cl = _cluster(n_gpus, num_cus, placement, "even", kind, pod_server_tenants)
+    import tempfile
+
+    # allocation records of the probe's pod-server slices go to a scratch dir
+    scratch = tempfile.TemporaryDirectory(prefix="nos_cap_") if pod_server_tenants else None
+    cl = _cluster(n_gpus, num_cus, placement, "even", kind, pod_server_tenants,
+                  scratch.name if scratch else C.DEFAULT_POD_SERVER_SOCKET_DIR)
     total = n_gpus * per_gpu_attempt
     for i in range(total):
         cl.submit_pod(f"cap-{i}", {f"{C.AMD_SLICE_RESOURCE_PREFIX}{slice_gb}gb": 1})
@@ -74,6 +79,8 @@ def schedulable_pods(n_gpus: int, slice_gb: int, num_cus: int = 256, placement: 
     if kind == C.PARTITIONING_HYBRID:
         node = cl.nodes["mi355x-0"]
         out["modes"] = [f"{c}/{m}" for c, m in zip(node.smi.compute, node.smi.memory)]
+    if scratch is not None:
+        scratch.cleanup()
     return out
 
 
@@ -82,7 +89,7 @@ def _gpu_of(env: dict) -> str:
     if env.get(C.ENV_VISIBLE_DEVICES):
         return env[C.ENV_VISIBLE_DEVICES]
     sock = env.get(C.ENV_POD_SERVER, "")
-    m = re.search(r"gpu-(\d+)\.sock$", sock.split(",")[0])
+    m = re.search(r"gpu-(\d+)/server\.sock$", sock.split(",")[0])
     return m.group(1) if m else ""
 
 

@@ -85,6 +85,11 @@ class NosAmdDevicePlugin:
         # cumask slices served by the node's pod server (nos_amd/podserver): the
         # pod gets the socket of its GPU's server, never a device node
         self.pod_server_dir = pod_server_dir
+        self.pod_server_allocations = None
+        if pod_server_dir:
+            from ..podserver.allocations import AllocationStore
+
+            self.pod_server_allocations = AllocationStore(pod_server_dir)
         # "container": the runtime mounts only the allocated render nodes, so
         # HIP inside the container numbers them 0..k-1 in host order;
         # "host": tenants run on the host and see every GPU (simulator, bare metal)
@@ -394,38 +399,56 @@ class NosAmdDevicePlugin:
             return alloc
 
     def _allocate_pod_server(self, resource: str, device_ids: list[str], owner: str) -> ContainerAllocation:
-        """A slice served by the GPU's pod server (the MPS-client analogue): the
-        server socket, the slice's memory and, unless the CU policy is
-        "shared", its CU mask for the server to apply to the tenant's stream.
-        No ``/dev/kfd`` and no render node: the pod must not open the GPU
-        (that would take an HWS process slot, which is what the server saves)."""
-        from ..cmd.podserver import socket_path
+        """A slice served by the GPU's pod server (the MPS-client analogue).
+
+        The pod gets its GPU's server socket (only that GPU's socket
+        directory is mounted), a fresh allocation token, and no ``/dev/kfd``
+        or render node: it must not open the GPU (that would take an HWS
+        process slot, which is what the server saves).  The slice -- memory
+        and, unless the CU policy is "shared", the CU mask -- goes into an
+        allocation record keyed by the token's hash that only the server
+        reads (podserver/allocations.py): the server takes the slice from
+        the record, never from the pod, and evicts the tenant when
+        :meth:`release` deletes the record (reference: the MPS replica's
+        memory fixed by the plugin, ``internal/partitioning/mps/partitioner.go:123-157``)."""
+        from ..podserver.allocations import new_token, socket_dir, socket_path
 
         with self._lock:
-            alloc = ContainerAllocation(device_ids=list(device_ids), mounts=[self.pod_server_dir])
+            alloc = ContainerAllocation(device_ids=list(device_ids))
             gpus = {g.index: g for g in self._gpus()}
-            socks: list[str] = []
-            mask_cus: set[int] = set()
-            n_cus = mem = 0
+            per_gpu: dict[int, dict] = {}
             for did in device_ids:
                 d = self.devices.get(did)
                 if d is None or d.resource != resource:
                     raise KeyError(f"unknown device {did} for {resource}")
                 if not d.healthy:
                     raise RuntimeError(f"device {did} is unhealthy")
-                sp = str(socket_path(self.pod_server_dir, d.gpu_index))
-                if sp not in socks:
-                    socks.append(sp)
+                g = per_gpu.setdefault(d.gpu_index, {"memory_gb": 0, "cus": set(), "device_ids": [], "n_cus": 0})
                 s = self.cu_slots.get(did)
                 if s is not None:
-                    mask_cus.update(s.cus())
+                    g["cus"].update(s.cus())
                 xcds, per_xcd = _cu_geometry(gpus.get(d.gpu_index))
-                n_cus = max(n_cus, xcds * per_xcd)
-                mem += d.memory_gb
+                g["n_cus"] = xcds * per_xcd
+                g["memory_gb"] += d.memory_gb
+                g["device_ids"].append(did)
+            token = new_token()
+            socks, masks = [], []
+            for gi, g in sorted(per_gpu.items()):
+                mask = mask_hex(sorted(g["cus"]), g["n_cus"]) if g["cus"] and len(g["cus"]) < g["n_cus"] else None
+                self.pod_server_allocations.write(gi, token, {
+                    "memory_gb": g["memory_gb"], "cu_mask": mask, "device_ids": g["device_ids"],
+                    "owner": owner or "unknown", "resource": resource})
+                socks.append(str(socket_path(self.pod_server_dir, gi)))
+                alloc.mounts.append(str(socket_dir(self.pod_server_dir, gi)))
+                if mask:
+                    masks.append(mask)
+            for did in device_ids:
                 self.allocated[did] = owner or "unknown"
+            mem = sum(g["memory_gb"] for g in per_gpu.values())
             alloc.envs[C.ENV_POD_SERVER] = ",".join(socks)
-            if mask_cus and len(mask_cus) < n_cus:
-                alloc.envs[C.ENV_POD_CU_MASK] = mask_hex(sorted(mask_cus), n_cus)
+            alloc.envs[C.ENV_POD_TOKEN] = token
+            if masks:
+                alloc.envs[C.ENV_POD_CU_MASK] = ",".join(masks)
             if mem:
                 alloc.envs[C.ENV_MEMORY_LIMIT_GB] = str(mem)
             return alloc
@@ -438,6 +461,9 @@ class NosAmdDevicePlugin:
             stale = [did for did in device_ids if did in self.devices and not self.devices[did].healthy]
             for did in stale:
                 self.devices.pop(did, None)
+            if released and self.pod_server_allocations is not None:
+                # the pod server evicts the tenants of these records
+                self.pod_server_allocations.remove_devices(released)
         if released and self.mode in SLICE_MODES:
             self.refresh()
 

@@ -214,11 +214,15 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
         from ..api import constants as C
 
         if os.environ.get(C.ENV_POD_SERVER):
-            # pod-server slice: register the model in the server, infer through it
+            # pod-server slice: ship the model to the server as a program (op
+            # graph + weights, built with numpy: this process never imports
+            # torch or opens the GPU), then infer through it
             from ..podserver.client import PodClient
+            from .yolos_program import demo_tenant
 
-            client = PodClient.from_env()
-            rep = client.register(f"pod-{slot}", dtype=dtype, seed=seed)
+            program, weights = demo_tenant(dtype, seed, small=device == "cuda")
+            client = PodClient.from_env(reconnect_s=float(os.environ.get("NOS_AMD_POD_RECONNECT_S", "0")))
+            rep = client.register(f"pod-{slot}", program, weights)
             s = t = _ServerTenant(client)
             for _ in range(warmup):
                 t.launch()

@@ -1,12 +1,20 @@
 """Fractional pod side of the pod server (server.py): stdlib + numpy only.
 
 A pod scheduled onto a pod-server slice gets, from the device plugin,
-``NOS_AMD_POD_SERVER`` (the GPU's server socket, under a host directory the
-container mounts) and ``NOS_AMD_MEMORY_LIMIT_GB`` (its slice), optionally
-``NOS_AMD_POD_CU_MASK``, and no ``/dev/kfd`` or render node.  The container
-never opens the GPU.  It registers its model once, then sends inference
-requests.  This is the role MPS clients play in the reference: their CUDA
-calls go to the MPS server, which runs them in the server's context.
+``NOS_AMD_POD_SERVER`` (its GPU's server socket, in the one per-GPU directory
+the container mounts), ``NOS_AMD_POD_TOKEN`` (the allocation's token: the
+server reads the slice's memory and CU mask from the plugin's record of it),
+``NOS_AMD_MEMORY_LIMIT_GB`` (informational) and no ``/dev/kfd`` or render
+node.  The container never opens the GPU.  It registers its model once -- a
+program (op graph + weights, program.py) -- then sends inference requests.
+This is the role MPS clients play in the reference: their CUDA calls go to
+the MPS server, which runs them in the server's context.
+
+Server loss.  A request whose connection breaks raises
+:class:`PodServerGone` (the pod exits non-zero and the kubelet restarts it),
+unless the client was made with ``reconnect_s`` > 0: it then waits up to that
+long for the server (the supervisor restarts a dead one), registers the same
+program again with the same token, and retries the request once.
 """
 from __future__ import annotations
 
@@ -16,7 +24,7 @@ import time
 
 import numpy as np
 
-from ..api.constants import ENV_POD_CU_MASK, ENV_POD_SERVER
+from ..api.constants import ENV_MEMORY_LIMIT_GB, ENV_POD_CU_MASK, ENV_POD_SERVER, ENV_POD_TOKEN
 from . import protocol as P
 
 
@@ -24,23 +32,33 @@ class PodServerError(RuntimeError):
     pass
 
 
+class PodServerGone(PodServerError):
+    """The connection to the pod server broke (server died or evicted us)."""
+
+
+def _connect(path: str, timeout_s: float) -> socket.socket:
+    deadline = time.monotonic() + timeout_s
+    while True:  # the server's socket appears once it accepts (server.start)
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        try:
+            s.connect(path)
+            return s
+        except (FileNotFoundError, ConnectionRefusedError):
+            s.close()
+            if time.monotonic() > deadline:
+                raise PodServerError(f"no pod server at {path} after {timeout_s} s")
+            time.sleep(0.1)
+
+
 class PodClient:
-    def __init__(self, path: str | os.PathLike, connect_timeout_s: float = 60.0):
-        deadline = time.monotonic() + connect_timeout_s
-        while True:  # the server's socket appears once it accepts (server.start)
-            s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
-            try:
-                s.connect(str(path))
-                break
-            except (FileNotFoundError, ConnectionRefusedError):
-                s.close()
-                if time.monotonic() > deadline:
-                    raise PodServerError(f"no pod server at {path} after {connect_timeout_s} s")
-                time.sleep(0.1)
-        self.sock = s
+    def __init__(self, path: str | os.PathLike, connect_timeout_s: float = 60.0, reconnect_s: float = 0.0):
         self.path = str(path)
+        self.sock = _connect(self.path, connect_timeout_s)
+        self.reconnect_s = reconnect_s
         self.tenant: int | None = None
         self.info: dict = {}
+        self._reg: tuple[dict, bytes] | None = None
+        self.reconnects = 0
 
     @classmethod
     def from_env(cls, env: dict | None = None, **kw) -> "PodClient":
@@ -51,30 +69,64 @@ class PodClient:
         return cls(path, **kw)
 
     def _call(self, req: dict, payload: bytes = b"") -> tuple[dict, bytes]:
-        P.send_msg(self.sock, req, payload)
-        rep, data = P.recv_msg(self.sock)
+        if self.sock is None:
+            raise PodServerGone("client is closed")
+        try:
+            P.send_msg(self.sock, req, payload)
+            rep, data = P.recv_msg(self.sock)
+        except (ConnectionError, OSError) as e:
+            raise PodServerGone(f"pod server connection lost: {e}") from e
         if not rep.get("ok"):
             raise PodServerError(rep.get("error", "pod server error"))
         return rep, data
 
-    def register(self, pod: str, dtype: str = "fp32", seed: int = 0, memory_limit_gb: float | None = None,
-                 cu_mask: str | None = None, env: dict | None = None) -> dict:
-        """Build the pod's model in the server; the slice comes from the device
-        plugin's env unless given."""
+    def register(self, pod: str, program: dict, weights: bytes = b"", token: str | None = None,
+                 memory_limit_gb: float | None = None, cu_mask: str | None = None, env: dict | None = None) -> dict:
+        """Ship the pod's program (op graph + weight bytes, program.py) to the
+        server.  The allocation token comes from the device plugin's env; the
+        slice itself is the plugin's record.  ``memory_limit_gb`` /
+        ``cu_mask`` matter only to a server without allocation records."""
         env = os.environ if env is None else env
-        if memory_limit_gb is None and env.get("NOS_AMD_MEMORY_LIMIT_GB"):
-            memory_limit_gb = float(env["NOS_AMD_MEMORY_LIMIT_GB"])
-        rep, _ = self._call({"op": "register", "pod": pod, "dtype": dtype, "seed": seed,
-                             "memory_limit_gb": memory_limit_gb, "cu_mask": cu_mask or env.get(ENV_POD_CU_MASK)})
+        if memory_limit_gb is None and env.get(ENV_MEMORY_LIMIT_GB):
+            memory_limit_gb = float(env[ENV_MEMORY_LIMIT_GB])
+        req = {"op": "register", "pod": pod, "program": program, "token": token or env.get(ENV_POD_TOKEN),
+               "memory_limit_gb": memory_limit_gb, "cu_mask": cu_mask or env.get(ENV_POD_CU_MASK)}
+        rep, _ = self._call(req, weights)
+        self._reg = (req, weights)
         self.tenant = rep["tenant"]
         self.info = rep
         return rep
+
+    def _reregister(self) -> None:
+        deadline = time.monotonic() + self.reconnect_s
+        last = None
+        while time.monotonic() < deadline:
+            try:
+                self.sock.close()
+            except OSError:
+                pass
+            try:
+                self.sock = _connect(self.path, max(0.1, deadline - time.monotonic()))
+                rep, _ = self._call(*self._reg)
+                self.tenant, self.info = rep["tenant"], rep
+                self.reconnects += 1
+                return
+            except PodServerError as e:  # not up yet / still holding our old tenant: retry
+                last = e
+                time.sleep(0.2)
+        raise PodServerGone(f"pod server did not come back within {self.reconnect_s} s: {last}")
 
     def infer(self, x: np.ndarray | None = None, outputs: bool = False) -> tuple[list[np.ndarray], dict]:
         """One inference on the pod's model; ``x`` replaces the resident input
         (float32, the model's input shape)."""
         payload = b"" if x is None else np.ascontiguousarray(x, dtype=np.float32).tobytes()
-        rep, data = self._call({"op": "infer", "outputs": outputs}, payload)
+        try:
+            rep, data = self._call({"op": "infer", "outputs": outputs}, payload)
+        except PodServerGone:
+            if self.reconnect_s <= 0 or self._reg is None:
+                raise
+            self._reregister()
+            rep, data = self._call({"op": "infer", "outputs": outputs}, payload)
         return (P.unpack_arrays(rep["outputs"], data) if outputs else []), rep
 
     def stats(self) -> dict:
@@ -91,4 +143,4 @@ class PodClient:
         self.sock = None
 
 
-__all__ = ["PodClient", "PodServerError", "ENV_POD_SERVER", "ENV_POD_CU_MASK"]
+__all__ = ["PodClient", "PodServerError", "PodServerGone", "ENV_POD_SERVER", "ENV_POD_CU_MASK", "ENV_POD_TOKEN"]

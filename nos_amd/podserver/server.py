@@ -24,12 +24,23 @@ Design (MI355X-first):
   request in flight, so the lanes serve the tenants round-robin and every
   tenant sees the same latency.  Queues shared through HIP's round-robin
   stream mapping instead gave a 20-50 ms spread at 20 tenants.
-* **Memory slices.**  A tenant registers with its slice's memory
-  (``NOS_AMD_MEMORY_LIMIT_GB`` from the device plugin).  The server measures
-  the peak device memory of the tenant's build and graph capture, and refuses
-  the tenant when that peak exceeds the slice.  The check runs at admission
-  and is hard: nothing is allocated at replay time.  Process pods only get a
-  cooperative caching-allocator cap.
+* **Programs.**  A tenant ships its model as a program -- a static op graph
+  over the whitelisted nos-amd ops plus raw weight bytes (program.py) -- not
+  code.  The server validates it (shapes, dtypes, kernel constraints), lowers
+  it with its small graph compiler (constant folding, LayerNorm folding,
+  epilogue and QKV-attention fusion) onto the gfx950 kernels, and captures it
+  into HIP graphs like any model.
+* **Admission.**  With an allocations directory (the deployed default), a
+  tenant registers with the per-allocation token the device plugin minted
+  (``NOS_AMD_POD_TOKEN``); its slice memory and CU mask come from the
+  plugin's record, never from the client, one tenant per token, and a
+  tenant whose record disappears (its pod's devices were released) is
+  evicted (allocations.py).  Memory is checked twice, both hard: the
+  program's static estimate before anything is allocated, then the measured
+  peak device memory of the build and graph capture.  Slots and memory are
+  reserved under the lock before the (slow) build, so concurrent
+  registrations cannot over-commit.  Nothing is allocated at replay time.
+  Process pods only get a cooperative caching-allocator cap.
 * **CU slices.**  A tenant whose allocation carries a CU mask gets its own
   CU-masked stream (``hipExtStreamCreateWithCUMask``), the per-queue form of
   ``ROC_GLOBAL_CU_MASK``.  Unmasked tenants share every CU, which is MPS's
@@ -43,8 +54,8 @@ Design (MI355X-first):
   same memory pool (a tenant never replays two graphs at once), and a lane
   replays it when no other job is running or queued (``solo_graphs``).
 
-``device="cpu"`` runs the tiny test model without streams or graphs (protocol
-tests on machines without a GPU).
+``device="cpu"`` runs programs eagerly on the CPU, without streams or graphs
+(protocol tests on machines without a GPU).
 """
 from __future__ import annotations
 
@@ -74,7 +85,7 @@ class Tenant:
     pod: str
     memory_limit_gb: float
     dtype: str
-    model: object
+    model: object                  # the compiled program (program.CompiledProgram)
     x: object                      # static input tensor (graph input)
     stream: object = None          # own CU-masked stream (masked tenants), else None
     graph: object = None
@@ -87,6 +98,13 @@ class Tenant:
     solo_completed: int = 0
     gpu_s: float = 0.0
     registered_at: float = field(default_factory=time.monotonic)
+    token: str | None = None       # allocation token (None: open admission)
+    record_path: object = None     # the device plugin's allocation record
+    device_ids: tuple = ()
+    conn: object = None            # the client connection (closed on eviction)
+    program: str = ""
+    compile_stats: dict = field(default_factory=dict)
+    evicted: str | None = None
 
 
 @dataclass
@@ -109,7 +127,15 @@ class AdmissionError(RuntimeError):
 class PodServer:
     def __init__(self, socket_path: str | os.PathLike, device: str = "cuda", lanes: int = DEFAULT_LANES,
                  max_tenants: int = DEFAULT_MAX_TENANTS, memory_gb: float | None = None, graphs: bool = True,
-                 kernel_config: dict | None = None, solo_graphs: bool = True):
+                 kernel_config: dict | None = None, solo_graphs: bool = True,
+                 allocations_dir: str | os.PathLike | None = None, pod_resources=None,
+                 reap_interval_s: float = 1.0):
+        """``allocations_dir``: this GPU's allocation records (tokens
+        required; allocations.py).  Without it admission is open: the client
+        declares its slice, which must be > 0 when the server accounts
+        memory (tests, bare metal).  ``pod_resources``: a PodResources lister
+        (resource/client.py) -- tenants whose devices no pod holds any more
+        are evicted."""
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.path = Path(socket_path)
@@ -135,6 +161,12 @@ class PodServer:
         self.memory_gb = memory_gb
         self.info: dict = {}
         self.gpu_label = os.environ.get("HIP_VISIBLE_DEVICES", "0") if self.gpu else "cpu"  # metrics label
+        self.allocations_dir = Path(allocations_dir) if allocations_dir else None
+        self.pod_resources = pod_resources
+        self.reap_interval_s = reap_interval_s
+        self._pending: dict[int, float] = {}    # tenant id -> slice GB reserved while its build runs
+        self._tokens: set[str] = set()           # tokens holding a tenant (or a pending build)
+        self.evictions = 0
 
     # ------------------------------------------------------------ lifecycle
     def _init_device(self) -> None:
@@ -201,6 +233,10 @@ class PodServer:
         t = threading.Thread(target=self._accept, name="accept", daemon=True)
         t.start()
         self._threads.append(t)
+        if self.allocations_dir is not None or self.pod_resources is not None:
+            t = threading.Thread(target=self._reap, name="reaper", daemon=True)
+            t.start()
+            self._threads.append(t)
         log.info("pod server on %s: %s", self.path, self.info)
         return self
 
@@ -272,9 +308,11 @@ class PodServer:
                     if op == "register":
                         if tenant is not None:
                             raise AdmissionError("connection already holds a tenant")
-                        tenant = self._register(req)
+                        tenant = self._register(req, payload, conn)
                         P.send_msg(conn, {"ok": True, "tenant": tenant.id, "footprint_gb": tenant.footprint_gb,
+                                          "memory_limit_gb": tenant.memory_limit_gb, "cu_mask": tenant.cu_mask,
                                           "input_shape": list(tenant.x.shape), "server": self.info,
+                                          "program": tenant.program, "compile": tenant.compile_stats,
                                           "tenants": len(self.tenants)})
                     elif op == "infer":
                         if tenant is None:
@@ -308,44 +346,92 @@ class PodServer:
             conn.close()
 
     # ------------------------------------------------------------ tenants
-    def _register(self, req: dict) -> Tenant:
+    def _admission(self, req: dict) -> tuple[float, str | None, str | None, object, tuple]:
+        """(slice GB, CU mask, token, record path, device ids) of a register
+        request: from the device plugin's record when the server has an
+        allocations directory, else as the client declares them."""
+        if self.allocations_dir is not None:
+            from .allocations import lookup
+
+            token = req.get("token")
+            if not token:
+                raise AdmissionError("no allocation token: this pod was not allocated a pod-server slice "
+                                     "(NOS_AMD_POD_TOKEN)")
+            hit = lookup(self.allocations_dir, str(token))
+            if hit is None:
+                raise AdmissionError("unknown allocation token (not allocated on this GPU, or released)")
+            rec, path = hit
+            limit = float(rec.get("memory_gb") or 0)
+            if limit <= 0:
+                raise AdmissionError("the allocation carries no memory slice")
+            return limit, rec.get("cu_mask") or None, str(token), path, tuple(rec.get("device_ids", ()))
         limit = float(req.get("memory_limit_gb") or 0)
-        dtype = req.get("dtype", "fp32")
-        if dtype not in ("fp32", "bf16"):
-            raise ValueError(f"dtype {dtype!r}")
+        if self.memory_gb and limit <= 0:
+            raise AdmissionError("a memory slice (memory_limit_gb > 0) is required: the server accounts memory")
+        return limit, req.get("cu_mask") or None, None, None, ()
+
+    def _register(self, req: dict, payload: bytes = b"", conn=None) -> Tenant:
+        from . import program as PG
+
+        limit, mask, token, record, dev_ids = self._admission(req)
+        if "program" not in req:
+            raise AdmissionError("register carries no program (nos-amd.program/v1 op graph + weights)")
+        prog = PG.parse(req["program"], payload, gpu=self.gpu)
+        need = prog.bytes_estimate / 2 ** 30
+        if limit and need > limit:
+            raise AdmissionError(f"tenant needs {need:.2f} GB (static estimate), its slice has {limit} GB")
         with self._lock:
-            if len(self.tenants) >= self.max_tenants:
+            if token is not None and token in self._tokens:
+                raise AdmissionError("the allocation already holds a tenant")
+            if len(self.tenants) + len(self._pending) >= self.max_tenants:
                 raise AdmissionError(f"server full ({self.max_tenants} tenants)")
             if self.memory_gb and limit:
-                held = sum(t.memory_limit_gb for t in self.tenants.values())
+                held = sum(t.memory_limit_gb for t in self.tenants.values()) + sum(self._pending.values())
                 if held + limit > self.memory_gb + 1e-6:
                     raise AdmissionError(f"slice of {limit} GB does not fit: {held} of {self.memory_gb} GB held")
             tid = self._next_id
             self._next_id += 1
-        with self._build_lock:
-            t = self._build(tid, req, dtype, limit)
+            self._pending[tid] = limit           # reserved before the slow build
+            if token is not None:
+                self._tokens.add(token)
+        try:
+            with self._build_lock:
+                t = self._build(tid, req, prog, limit, mask)
+        except BaseException:
+            with self._lock:
+                self._pending.pop(tid, None)
+                if token is not None:
+                    self._tokens.discard(token)
+            raise
+        t.token, t.record_path, t.device_ids, t.conn = token, record, dev_ids, conn
         with self._lock:
+            self._pending.pop(tid, None)
             self.tenants[tid] = t
             M.PODSERVER_TENANTS.labels(self.gpu_label).set(len(self.tenants))
-        log.info("tenant %d (%s) registered: %.3f GB of a %s GB slice", tid, t.pod, t.footprint_gb, limit or "-")
+        log.info("tenant %d (%s, %s) registered: %.3f GB of a %s GB slice", tid, t.pod, t.program, t.footprint_gb,
+                 limit or "-")
         return t
 
-    def _build(self, tid: int, req: dict, dtype: str, limit: float) -> Tenant:
+    def _build(self, tid: int, req: dict, prog, limit: float, mask: str | None) -> Tenant:
         import torch
 
-        from ..models.pod import _build
-        from ..models.yolos import GraphedTenant, demo_input_hw
+        from ..models.yolos import GraphedTenant
 
-        seed = int(req.get("seed", 0))
-        mask = req.get("cu_mask") or None
+        pod = str(req.get("pod", tid))[:253]
+        dtype = prog.inputs[0].dtype
         if not self.gpu:
-            m, x = _build(dtype, seed, demo_input_hw(), "cpu")
-            return Tenant(tid, str(req.get("pod", tid)), limit, dtype, m, x)
+            with torch.no_grad():
+                m = prog.compile("cpu")
+            x = prog.input_tensor("cpu")
+            return Tenant(tid, pod, limit, dtype, m, x, program=prog.name, compile_stats=dict(m.stats), cu_mask=mask)
         base = torch.cuda.memory_allocated()
         torch.cuda.reset_peak_memory_stats()
         stream = None
         try:
-            m, x = _build(dtype, seed, demo_input_hw(), "cuda")
+            with torch.no_grad(), torch.cuda.stream(self._setup_stream):
+                m = prog.compile("cuda")
+                x = prog.input_tensor("cuda")
+            self._setup_stream.synchronize()
             if mask:
                 from ..bench_support import cus_from_hex
                 from ..ops.streams import CUMaskedStream
@@ -372,14 +458,61 @@ class PodServer:
         except Exception:
             if stream is not None:
                 stream.close()
+            torch.cuda.empty_cache()
             raise
-        t = Tenant(tid, str(req.get("pod", tid)), limit, dtype, m, x, stream=stream, graph=gt.graph,
+        t = Tenant(tid, pod, limit, dtype, m, x, stream=stream, graph=gt.graph,
                    outputs=gt.outputs, footprint_gb=round(peak, 3), cu_mask=mask,
-                   solo_graph=solo.graph if solo else None, solo_outputs=solo.outputs if solo else ())
+                   solo_graph=solo.graph if solo else None, solo_outputs=solo.outputs if solo else (),
+                   program=prog.name, compile_stats=dict(m.stats))
         if limit and peak > limit:
             self._free(t)
             raise AdmissionError(f"tenant needs {peak:.2f} GB, its slice has {limit} GB")
         return t
+
+    # ------------------------------------------------------------ eviction
+    def evict(self, t: Tenant, reason: str) -> None:
+        """Drop a tenant whose allocation is gone: close its connection (its
+        thread unregisters and frees it once an in-flight replay finished)."""
+        if t.evicted:
+            return
+        t.evicted = reason
+        self.evictions += 1
+        log.warning("evicting tenant %d (%s): %s", t.id, t.pod, reason)
+        c = t.conn
+        if c is not None:
+            try:
+                c.shutdown(socket.SHUT_RDWR)
+            except OSError:
+                pass
+
+    def reap_once(self) -> int:
+        """Evict tenants whose allocation record vanished or whose devices no
+        pod holds (PodResources).  Returns the number evicted."""
+        with self._lock:
+            ts = [t for t in self.tenants.values() if not t.evicted]
+        used = None
+        if self.pod_resources is not None:
+            try:
+                used = {d for pr in self.pod_resources.list() for c in pr.containers for cd in c.devices
+                        for d in cd.device_ids}
+            except Exception as e:  # kubelet unreachable: decide on the records alone
+                log.info("PodResources unavailable: %s", e)
+        n = 0
+        for t in ts:
+            if t.record_path is not None and not Path(t.record_path).exists():
+                self.evict(t, "allocation released (record removed by the device plugin)")
+                n += 1
+            elif used is not None and t.device_ids and not any(d in used for d in t.device_ids):
+                self.evict(t, "allocation released (no pod holds its devices in PodResources)")
+                n += 1
+        return n
+
+    def _reap(self) -> None:
+        while not self._stop.wait(self.reap_interval_s):
+            try:
+                self.reap_once()
+            except Exception:
+                log.exception("reaper pass failed")
 
     def _free(self, t: Tenant) -> None:
         t.graph = t.solo_graph = t.model = t.x = None
@@ -395,6 +528,8 @@ class PodServer:
     def _unregister(self, t: Tenant) -> None:
         with self._lock:
             self.tenants.pop(t.id, None)
+            if t.token is not None:
+                self._tokens.discard(t.token)
             M.PODSERVER_TENANTS.labels(self.gpu_label).set(len(self.tenants))
         try:
             M.PODSERVER_INFERENCES.remove(self.gpu_label, t.pod)
@@ -406,11 +541,13 @@ class PodServer:
 
     def stats(self) -> dict:
         with self._lock:
-            ts = [{"tenant": t.id, "pod": t.pod, "completed": t.completed, "solo_completed": t.solo_completed,
-                   "gpu_s": round(t.gpu_s, 4),
+            ts = [{"tenant": t.id, "pod": t.pod, "program": t.program, "completed": t.completed,
+                   "solo_completed": t.solo_completed, "gpu_s": round(t.gpu_s, 4),
                    "footprint_gb": t.footprint_gb, "memory_limit_gb": t.memory_limit_gb, "cu_mask": t.cu_mask}
                   for t in self.tenants.values()]
-        return {"tenants": ts, "server": self.info, "queued": self._q.qsize(), "pid": os.getpid()}
+            pending = len(self._pending)
+        return {"tenants": ts, "pending": pending, "server": self.info, "queued": self._q.qsize(), "pid": os.getpid(),
+                "evictions": self.evictions}
 
     # ------------------------------------------------------------ lanes
     def _lane(self, i: int) -> None:

@@ -1,0 +1,309 @@
+"""Pod-server admission and failure handling (CPU):
+
+* allocation tokens (podserver/allocations.py): a tenant registers only with
+  the token the device plugin minted, gets the slice of the plugin's record
+  whatever it claims, one tenant per token, and loses its tenant when its pod
+  is deleted from the kubelet (record removed) or when PodResources no longer
+  lists its devices -- reference: the MPS replica's slice fixed by the device
+  plugin, ``internal/partitioning/mps/partitioner.go:123-157``, device usage
+  from PodResources, ``pkg/resource/client.go:39-87``;
+* slot and memory reservation before the (slow) build: concurrent
+  registrations never over-commit;
+* program validation: whatever a client sends is refused before anything is
+  allocated unless it is a well-formed program over the whitelisted ops;
+* server crashes: the supervisor restarts a killed server, a client with
+  ``reconnect_s`` re-registers and carries on, and a pod without it exits
+  non-zero (so the kubelet restarts it).
+"""
+from __future__ import annotations
+
+import os
+import signal
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from nos_amd.api import constants as C
+from nos_amd.models.yolos_program import demo_tenant
+from nos_amd.podserver import program as PG
+from nos_amd.podserver.allocations import AllocationStore, records_dir, socket_path
+from nos_amd.podserver.client import PodClient, PodServerError, PodServerGone
+from nos_amd.podserver.server import PodServer
+
+YOLOS = demo_tenant("fp32", 0, small=False)
+
+
+def _wait(cond, timeout=10.0):
+    deadline = time.monotonic() + timeout
+    while not cond():
+        if time.monotonic() > deadline:
+            return False
+        time.sleep(0.02)
+    return True
+
+
+@pytest.fixture
+def tokened(tmp_path):
+    """A GPU-1 server reading the records an AllocationStore writes."""
+    store = AllocationStore(tmp_path)
+    srv = PodServer(socket_path(tmp_path, 1), device="cpu", lanes=1, max_tenants=4, memory_gb=40,
+                    allocations_dir=records_dir(tmp_path, 1), reap_interval_s=0.05).start()
+    yield store, srv
+    srv.stop()
+
+
+def test_tokens_bind_tenants_to_their_allocation(tokened):
+    store, srv = tokened
+    store.write(1, "tok-a", {"memory_gb": 10, "cu_mask": None, "device_ids": ["g1::10gb::0"]})
+    store.write(1, "tok-zero", {"memory_gb": 0, "device_ids": ["g1::0gb::0"]})
+    store.write(0, "tok-gpu0", {"memory_gb": 10, "device_ids": ["g0::10gb::0"]})
+    c = PodClient(srv.path, connect_timeout_s=5)
+    with pytest.raises(PodServerError, match="no allocation token"):
+        c.register("p", *YOLOS, env={})
+    with pytest.raises(PodServerError, match="unknown allocation token"):
+        c.register("p", *YOLOS, token="forged")
+    with pytest.raises(PodServerError, match="unknown allocation token"):  # another GPU's allocation
+        c.register("p", *YOLOS, token="tok-gpu0")
+    with pytest.raises(PodServerError, match="no memory slice"):
+        c.register("p", *YOLOS, token="tok-zero")
+    # the slice is the record's, whatever the client claims
+    rep = c.register("p", *YOLOS, token="tok-a", memory_limit_gb=100, cu_mask="ffff")
+    assert rep["memory_limit_gb"] == 10 and rep["cu_mask"] is None
+    c.infer()
+    d = PodClient(srv.path, connect_timeout_s=5)
+    with pytest.raises(PodServerError, match="already holds a tenant"):
+        d.register("p-again", *YOLOS, token="tok-a")
+    c.close()  # the token is free again once its tenant left
+    assert _wait(lambda: not srv.tenants)
+    d.register("p-again", *YOLOS, token="tok-a")
+    d.close()
+
+
+def test_a_released_allocation_evicts_its_tenant(tokened):
+    store, srv = tokened
+    store.write(1, "tok-b", {"memory_gb": 10, "device_ids": ["g1::10gb::1"]})
+    store.write(1, "tok-c", {"memory_gb": 10, "device_ids": ["g1::10gb::2"]})
+    b, c = PodClient(srv.path, connect_timeout_s=5), PodClient(srv.path, connect_timeout_s=5)
+    b.register("b", *YOLOS, token="tok-b")
+    c.register("c", *YOLOS, token="tok-c")
+    b.infer()
+    assert store.remove_devices(["g1::10gb::1"]) == 1
+    assert _wait(lambda: len(srv.tenants) == 1)
+    with pytest.raises(PodServerGone):
+        b.infer()
+    c.infer()  # the other tenant is untouched
+    assert srv.stats()["evictions"] == 1
+    c.close()
+
+
+def test_pod_resources_eviction_without_records(tmp_path):
+    from nos_amd.resource.client import ContainerDevices, ContainerResources, PodResources
+
+    class Lister:
+        pods = [PodResources("p", "ns", [ContainerResources("c", [ContainerDevices("amd.com/gpu-10gb", ["d1"])])])]
+
+        def list(self):
+            return list(self.pods)
+
+    store = AllocationStore(tmp_path)
+    path = store.write(0, "tok", {"memory_gb": 10, "device_ids": ["d1"]})
+    lister = Lister()
+    srv = PodServer(socket_path(tmp_path, 0), device="cpu", lanes=1, memory_gb=40,
+                    allocations_dir=records_dir(tmp_path, 0), pod_resources=lister, reap_interval_s=3600).start()
+    try:
+        c = PodClient(srv.path, connect_timeout_s=5)
+        c.register("p", *YOLOS, token="tok")
+        assert srv.reap_once() == 0
+        lister.pods = []  # the kubelet no longer runs a pod with d1 (the plugin has not synced yet)
+        assert path.exists() and srv.reap_once() == 1
+        assert _wait(lambda: not srv.tenants)
+    finally:
+        srv.stop()
+
+
+def test_a_pod_deleted_from_the_kubelet_simulator_loses_its_tenant(tmp_path):
+    """End to end through the control plane: scheduler -> device plugin
+    Allocate (token + record) -> pod registers with its env -> the pod is
+    deleted -> kubelet teardown releases the devices -> the record goes ->
+    the server evicts the tenant."""
+    from nos_amd.api.config import GpuPartitionerConfig
+    from nos_amd.gpu.fakesmi import FakeSmi
+    from nos_amd.sim.cluster import SimCluster
+
+    cl = SimCluster(partitioner_config=GpuPartitionerConfig(cuPolicy="shared"))
+    cl.add_node("n0", C.PARTITIONING_CUMASK, smi=FakeSmi(gpus=1, node="n0"), pod_server_tenants=48,
+                pod_server_dir=str(tmp_path))
+    cl.settle(30)
+    for i in range(2):
+        cl.submit_pod(f"tenant-{i}", {f"{C.AMD_SLICE_RESOURCE_PREFIX}10gb": 1})
+    cl.settle(600, until=lambda: not cl.pending_pods())
+    envs = {k: rc.envs for k, conts in cl.nodes["n0"].kubelet.running_containers().items() for rc in conts}
+    assert len(envs) == 2
+    srv = PodServer(socket_path(tmp_path, 0), device="cpu", lanes=1, memory_gb=288,
+                    allocations_dir=records_dir(tmp_path, 0), reap_interval_s=0.05).start()
+    try:
+        clients = {}
+        for key, env in envs.items():
+            assert env[C.ENV_POD_SERVER] == str(srv.path)
+            c = clients[key] = PodClient.from_env(env, connect_timeout_s=5)
+            rep = c.register(key, *YOLOS, env=env)
+            assert rep["memory_limit_gb"] == 10
+            c.infer()
+        gone, stays = sorted(envs)
+        cl.api.delete("Pod", gone.split("/", 1)[1], gone.split("/", 1)[0])
+        cl.settle(60)
+        assert _wait(lambda: len(srv.tenants) == 1)
+        assert next(iter(srv.tenants.values())).pod == stays
+        with pytest.raises(PodServerGone):
+            clients[gone].infer()
+        clients[stays].infer()
+        clients[stays].close()
+    finally:
+        srv.stop()
+
+
+def test_concurrent_registrations_cannot_overcommit(tmp_path, monkeypatch):
+    """Slots and slice memory are reserved before the build: 6 clients racing
+    for a 3-tenant, 30 GB server while each build takes a while."""
+    srv = PodServer(tmp_path / "s.sock", device="cpu", lanes=1, max_tenants=3, memory_gb=30).start()
+    orig = srv._build
+
+    def slow_build(*a, **kw):
+        time.sleep(0.3)
+        return orig(*a, **kw)
+
+    monkeypatch.setattr(srv, "_build", slow_build)
+    try:
+        results: list[str] = []
+        clients = [PodClient(srv.path, connect_timeout_s=5) for _ in range(6)]
+
+        def go(i):
+            try:
+                clients[i].register(f"p{i}", *YOLOS, memory_limit_gb=8 if i % 2 else 12)
+                results.append("ok")
+            except PodServerError as e:
+                results.append(str(e))
+
+        th = [threading.Thread(target=go, args=(i,)) for i in range(6)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        ok = results.count("ok")
+        assert 1 <= ok <= 3 and len(srv.tenants) == ok
+        assert sum(t.memory_limit_gb for t in srv.tenants.values()) <= 30
+        assert all(r == "ok" or "server full" in r or "does not fit" in r for r in results), results
+        assert srv.stats()["pending"] == 0
+        for c in clients:
+            c.close()
+    finally:
+        srv.stop()
+
+
+@pytest.mark.parametrize("mutate,match", [
+    (lambda p, w: p["nodes"].append({"op": "exec", "inputs": ["pixel_values"], "output": "z"}), "not one the pod"),
+    (lambda p, w: p["nodes"].insert(0, {"op": "relu", "inputs": ["later"], "output": "y"}), "not defined before"),
+    (lambda p, w: p["params"][0].update(offset=len(w)), "outside the"),
+    (lambda p, w: p["params"][1].update(offset=p["params"][0]["offset"]), "overlap"),
+    (lambda p, w: p["params"][0].update(shape=[3, 3]), "nbytes"),
+    (lambda p, w: p["nodes"][-1]["attrs"].update(evil=1), "unknown attributes"),
+    (lambda p, w: p.update(outputs=["nope"]), "outputs must name"),
+    (lambda p, w: p.update(format="pickle"), "format"),
+    (lambda p, w: p["nodes"].append({"op": "reshape", "inputs": ["pixel_values"], "output": "r",
+                                     "attrs": {"shape": [7, 7]}}), "cannot reshape"),
+    (lambda p, w: p["nodes"].append({"op": "linear", "inputs": ["pixel_values", "patch_w"], "output": "l"}),
+     "weight"),
+])
+def test_malformed_programs_are_refused_before_anything_is_built(mutate, match):
+    import copy
+
+    p, w = copy.deepcopy(YOLOS[0]), YOLOS[1]
+    mutate(p, w)
+    with pytest.raises(PG.ProgramError, match=match):
+        PG.parse(p, w)
+
+
+def test_gpu_kernel_constraints_are_checked_at_parse_time():
+    p, w = PG.mlp_program(dim=96, layers=1, batch=8, dtype="bf16")  # K = 96: not a multiple of 64
+    PG.parse(p, w)  # fine for the CPU reference path
+    with pytest.raises(PG.ProgramError, match="K % 64"):
+        PG.parse(p, w, gpu=True)
+    b = PG.Builder("attn")
+    x = b.input("x", [1, 16, 3 * 2 * 32])
+    b.op("attention", x, heads=2, out="a")
+    with pytest.raises(PG.ProgramError, match="head_dim 64"):
+        PG.parse(*b.build(["a"]), gpu=True)
+
+
+def test_static_estimate_refuses_a_program_larger_than_its_slice(tmp_path):
+    srv = PodServer(tmp_path / "s.sock", device="cpu", lanes=1, memory_gb=40).start()
+    try:
+        c = PodClient(srv.path, connect_timeout_s=5)
+        big = PG.mlp_program(dim=512, layers=2, batch=4096, dtype="fp32")
+        est = PG.parse(*big).bytes_estimate / 2 ** 30
+        with pytest.raises(PodServerError, match="static estimate"):
+            c.register("big", *big, memory_limit_gb=round(est / 2, 3))
+        assert not srv.tenants and srv.stats()["pending"] == 0
+        c.register("big", *big, memory_limit_gb=round(est * 2, 3))
+        c.close()
+    finally:
+        srv.stop()
+
+
+# ----------------------------------------------------------------- crashes
+def _supervised(tmp_path):
+    env = {**os.environ, "OMP_NUM_THREADS": "1"}
+    return subprocess.Popen([sys.executable, "-m", "nos_amd.cmd.podserver", "--gpus", "0", "--device", "cpu",
+                             "--socket-dir", str(tmp_path), "--lanes", "1", "--open-admission"], env=env,
+                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+
+
+def test_supervisor_restarts_a_killed_server_and_clients_reregister(tmp_path):
+    sup = _supervised(tmp_path)
+    try:
+        path = socket_path(tmp_path, 0)
+        keep = PodClient(path, connect_timeout_s=60, reconnect_s=60)
+        keep.register("keep", *YOLOS, memory_limit_gb=10)
+        plain = PodClient(path, connect_timeout_s=5)
+        plain.register("plain", *YOLOS, memory_limit_gb=10)
+        x = np.random.default_rng(0).standard_normal(keep.info["input_shape"]).astype(np.float32)
+        before, _ = keep.infer(x, outputs=True)
+        pid = keep.stats()["pid"]
+        os.kill(pid, signal.SIGKILL)  # the server dies mid-run
+        with pytest.raises(PodServerGone):
+            plain.infer()
+        after, _ = keep.infer(x, outputs=True)  # waits for the restart, registers again, retries
+        assert keep.reconnects == 1 and keep.stats()["pid"] != pid
+        np.testing.assert_array_equal(before[0], after[0])
+        keep.close()
+    finally:
+        sup.send_signal(signal.SIGTERM)
+        assert sup.wait(timeout=60) == 0
+
+
+def test_a_pod_exits_nonzero_when_its_server_dies(tmp_path):
+    from nos_amd.models.pod import STATE_READY, StatusBoard
+
+    srv = subprocess.Popen([sys.executable, "-m", "nos_amd.cmd.podserver", "--gpu", "0", "--device", "cpu",
+                            "--socket-dir", str(tmp_path), "--lanes", "1", "--open-admission"],
+                           env={**os.environ, "OMP_NUM_THREADS": "1"}, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL)
+    board = StatusBoard(tmp_path / "board", pods=1)
+    env = {**os.environ, C.ENV_POD_SERVER: str(socket_path(tmp_path, 0)), C.ENV_MEMORY_LIMIT_GB: "10",
+           "OMP_NUM_THREADS": "1"}
+    pod = subprocess.Popen([sys.executable, "-m", "nos_amd.models.pod", "--status", str(tmp_path / "board"),
+                            "--slot", "0", "--out", str(tmp_path), "--device", "cpu"], env=env,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    try:
+        assert _wait(lambda: board.states()[0] == STATE_READY and board.counts()[0] > 2, timeout=120)
+        srv.kill()
+        assert pod.wait(timeout=60) == 1
+        assert b"connection lost" in pod.stderr.read()
+    finally:
+        for p in (pod, srv):
+            if p.poll() is None:
+                p.kill()

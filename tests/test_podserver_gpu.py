@@ -1,6 +1,8 @@
-"""The pod server on the MI355X: tenants' YOLOS-small fp32 inferences run as
-HIP-graph replays on the server's lanes.  Checks that the server's results are
-bit-identical to the same model run eagerly with the same kernels, that its
+"""The pod server on the MI355X: tenants ship programs (op graph + weights)
+whose inferences run as HIP-graph replays on the server's lanes.  Checks that
+a YOLOS-small fp32 program's results are bit-identical to YolosDetector run
+eagerly with the same weights and kernels, that two architectures (YOLOS +
+the bf16 GEMM-MLP probe) co-hosted each match their own eager output, that
 memory admission refuses a tenant that exceeds its slice, and that more
 clients than lanes all make progress.  The server runs inside the test
 process; its clients are threads with sockets and never touch the GPU."""
@@ -18,13 +20,19 @@ from nos_amd import ops
 pytestmark = pytest.mark.gpu
 
 
+def _yolos(seed: int, dtype: str = "fp32"):
+    from nos_amd.models.yolos_program import demo_tenant
+
+    return demo_tenant(dtype, seed, small=True)
+
+
 @pytest.fixture
 def server(tmp_path):
     from nos_amd.ops import _lib
     from nos_amd.podserver.server import PodServer
 
     _lib.require_native_on_gpu()
-    srv = PodServer(tmp_path / "gpu-0.sock", device="cuda", lanes=2, max_tenants=8).start()
+    srv = PodServer(tmp_path / "gpu-0" / "server.sock", device="cuda", lanes=2, max_tenants=8).start()
     yield srv
     srv.stop()
     # the server set process-wide kernel configs: back to the library defaults
@@ -36,13 +44,14 @@ def server(tmp_path):
 
 
 def test_server_replays_match_the_eager_model_bit_for_bit(server):
-    from nos_amd.models.pod import _build
-    from nos_amd.models.yolos import demo_input_hw
+    from nos_amd.models.yolos import YolosConfig, YolosDetector
+    from nos_amd.models.yolos_program import yolos_weights
     from nos_amd.podserver.client import PodClient
 
     c = PodClient(server.path, connect_timeout_s=10)
-    rep = c.register("pod-a", seed=3, memory_limit_gb=10)
+    rep = c.register("pod-a", *_yolos(3), memory_limit_gb=10)
     assert rep["server"]["kernel_config"]["f32_math"] == "x6"
+    assert rep["compile"]["qkv_attention_fused"] == 12 and rep["compile"]["layernorm_folded"] == 24
     assert 0.05 < rep["footprint_gb"] < 10
     x = np.random.default_rng(1).standard_normal(rep["input_shape"]).astype(np.float32)
     outs, meta = c.infer(x, outputs=True)
@@ -50,7 +59,10 @@ def test_server_replays_match_the_eager_model_bit_for_bit(server):
     # a lone tenant replays its solo graph: the eager reference runs under the
     # same (whole-GPU) configs, which are process-wide
     assert next(iter(server.tenants.values())).solo_completed == 1
-    m, _ = _build("fp32", 3, demo_input_hw(), "cuda")
+    cfg = YolosConfig.small()
+    m = YolosDetector(cfg)
+    m.load_numpy(yolos_weights(cfg, 3))
+    m = m.cuda().eval()
     server._apply_config(server.solo_config)
     try:
         with torch.no_grad():
@@ -63,14 +75,80 @@ def test_server_replays_match_the_eager_model_bit_for_bit(server):
     c.close()
 
 
+def test_two_architectures_cohosted_each_match_their_eager_output(server):
+    """YOLOS-small fp32 and the bf16 GEMM-MLP probe tenant in one server:
+    each tenant's replayed outputs equal its own program run eagerly (same
+    kernels, same configs) bit for bit."""
+    from nos_amd.podserver import program as PG
+    from nos_amd.podserver.client import PodClient
+
+    yolos, mlp = _yolos(4), PG.mlp_program(dim=1024, layers=4, batch=256, dtype="bf16", seed=5)
+    a, b = PodClient(server.path, connect_timeout_s=10), PodClient(server.path, connect_timeout_s=10)
+    ra = a.register("yolos", *yolos, memory_limit_gb=10)
+    rb = b.register("mlp", *mlp, memory_limit_gb=2)
+    assert rb["compile"]["layernorm_folded"] == 4 and rb["compile"]["residual_fused"] == 4
+    rng = np.random.default_rng(6)
+    xa = rng.standard_normal(ra["input_shape"]).astype(np.float32)
+    xb = rng.standard_normal(rb["input_shape"]).astype(np.float32)
+    oa, _ = a.infer(xa, outputs=True)  # one at a time: each replays its solo graph
+    ob, _ = b.infer(xb, outputs=True)
+    server._apply_config(server.solo_config)
+    try:
+        with torch.no_grad():
+            for (prog, w), x, o in ((yolos, xa, oa), (mlp, xb, ob)):
+                P = PG.parse(prog, w, gpu=True)
+                ref = P.compile("cuda")(P.input_tensor("cuda", x))
+                torch.cuda.synchronize()
+                for oo, r in zip(o, ref):
+                    assert np.array_equal(oo, r.float().cpu().numpy())
+                # and near the unfused fp32 reference (bf16: per-op rounding)
+                eag = P.reference(torch.from_numpy(x))
+                err = np.abs(o[0] - eag[0].numpy()).max() / np.abs(eag[0].numpy()).max()
+                assert err < (3e-2 if "mlp" in P.name else 1e-4), (P.name, err)
+    finally:
+        server._apply_config(server.kernel_config)
+    # concurrent load: a request may replay the co-tenancy graph (other kernel
+    # configs: sums in another order), so within fp32 accuracy of the solo run
+    res, stop = [], threading.Event()
+
+    def hammer():
+        while not stop.is_set():
+            b.infer()
+
+    th = threading.Thread(target=hammer)
+    th.start()
+    try:
+        for _ in range(4):
+            res.append(a.infer(xa, outputs=True)[0][0])
+    finally:
+        stop.set()
+        th.join(timeout=30)
+    for r in res:
+        assert np.abs(r - oa[0]).max() <= 1e-4 * (np.abs(oa[0]).max() + 1e-6)
+    a.close()
+    b.close()
+
+
 def test_a_tenant_larger_than_its_slice_is_refused(server):
     from nos_amd.podserver.client import PodClient, PodServerError
 
     c = PodClient(server.path, connect_timeout_s=10)
-    with pytest.raises(PodServerError, match="slice has 0.05 GB"):
-        c.register("tiny-slice", memory_limit_gb=0.05)
-    assert not server.tenants
-    c.register("ok", memory_limit_gb=10)  # the refused build left nothing behind
+    prog = _yolos(0)
+    with pytest.raises(PodServerError, match="slice has 0.05 GB"):  # the static estimate
+        c.register("tiny-slice", *prog, memory_limit_gb=0.05)
+    # past the estimate, the measured peak of the build decides: an estimate
+    # of 0 lets the build run, and the real footprint refuses it
+    import nos_amd.podserver.program as PG
+
+    orig = PG.Program.bytes_estimate
+    try:
+        PG.Program.bytes_estimate = property(lambda self: 0)
+        with pytest.raises(PodServerError, match="slice has 0.05 GB"):
+            c.register("tiny-slice", *prog, memory_limit_gb=0.05)
+    finally:
+        PG.Program.bytes_estimate = orig
+    assert not server.tenants and server.stats()["pending"] == 0
+    c.register("ok", *prog, memory_limit_gb=10)  # the refused build left nothing behind
     c.infer()
     c.close()
 
@@ -81,7 +159,7 @@ def test_more_clients_than_lanes_all_progress(server):
     n = 5
     clients = [PodClient(server.path, connect_timeout_s=10) for _ in range(n)]
     for i, c in enumerate(clients):
-        c.register(f"p{i}", seed=i, memory_limit_gb=10)
+        c.register(f"p{i}", *_yolos(i), memory_limit_gb=10)
     counts, stop = [0] * n, threading.Event()
 
     def loop(i):
@@ -110,7 +188,7 @@ def test_a_lone_tenant_replays_its_solo_graph_with_the_same_results(server):
 
     assert server.solo_config is not None and server.solo_config != server.kernel_config
     c = PodClient(server.path, connect_timeout_s=10)
-    rep = c.register("solo", seed=5, memory_limit_gb=10)
+    rep = c.register("solo", *_yolos(5), memory_limit_gb=10)
     x = np.random.default_rng(2).standard_normal(rep["input_shape"]).astype(np.float32)
     outs, _ = c.infer(x, outputs=True)
     t = next(iter(server.tenants.values()))
