@@ -111,6 +111,10 @@ def parse_args(argv=None):
     ap.add_argument("--table-modes", default="shared,cumask")
     ap.add_argument("--table-window-s", type=float, default=5.0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--quota", action="store_true",
+                    help="BASELINE config 5 instead of the headline: two namespaces' ElasticQuotas on the GPU's "
+                         "pod-server slices, borrowing then fair-share preemption acting on running tenants "
+                         "(nos_amd/quotabench.py); prints its own JSON line")
     return ap.parse_args(argv)
 
 
@@ -414,8 +418,62 @@ def _hws_limit() -> int:
     return hws_max_concurrent_processes()
 
 
+def run_quota(args) -> int:
+    """``--quota``: config 5 on this GPU -- the real control plane with
+    ElasticQuotas, the kubelet starting every admitted pod as a pod process
+    against this GPU's pod server, borrowing, then CapacityScheduling
+    preemption stopping the borrowers' tenants."""
+    import shutil
+    import tempfile
+
+    from nos_amd.podbench import PodLauncher
+    from nos_amd.quotabench import ProcessRuntime, scenario_for
+
+    launcher = PodLauncher()  # before anything here touches the GPU
+    args.pod_server_dir = tempfile.mkdtemp(prefix="nos_q_", dir="/tmp")
+    work = tempfile.mkdtemp(prefix="nos_q_pods_")
+    args.local_gpu = 0
+    slices = args.pods_per_gpu or 28
+    sc = scenario_for(slices, args.slice_gb or 10, pod_server_dir=args.pod_server_dir, live=True)
+    server = PodServerProc(launcher, args, "0", work)
+    sampler = None
+    try:
+        log(0, f"pod server ready in {server.wait_ready():.1f} s")
+        if args.device == "cuda":
+            import torch
+
+            torch.cuda.set_device(0)
+            sampler = UtilSampler(0)
+        rt = ProcessRuntime(launcher, work, dtype=args.dtype, device=args.device)
+        try:
+            res = sc.run(rt, phase_timeout_s=900, sampler=sampler)
+        finally:
+            rt.close()
+        try:
+            res["pod_server"] = server.info()
+        except Exception as e:
+            res["pod_server"] = {"error": repr(e)}
+    finally:
+        if sampler:
+            sampler.close()
+        server.close()
+        launcher.close()
+        shutil.rmtree(work, ignore_errors=True)
+        shutil.rmtree(args.pod_server_dir, ignore_errors=True)
+    line = json.dumps({"metric": "config5: ElasticQuota borrowing + CapacityScheduling preemption on running "
+                                 "pod-server tenants (1 node)", "dtype": args.dtype, "device": args.device,
+                       "data": "synthetic (random-init YOLOS-small programs)", **res})
+    print(line, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            f.write(line + "\n")
+    return 0
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
+    if args.quota:
+        return run_quota(args)
     server_mode = args.mode == "server"
     args.pods_per_gpu = args.pods_per_gpu or (28 if server_mode else 8)
     args.slice_gb = args.slice_gb or (10 if server_mode else 36)

@@ -67,7 +67,10 @@ __device__ __forceinline__ float xor32_sum(float v) {
 __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
   const unsigned lds = __builtin_amdgcn_readfirstlane(
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds_wave_base);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+  // m0 is an operand ("{m0}"), so the compiler writes it and knows it is live
+  // (a clobbered m0 is undefined behaviour: m0 is a reserved register); the
+  // s_nop is the SALU-write-m0 -> LDS-DMA wait state the compiler cannot see
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(lds) : "memory");
 }
 
 // every DMA this wave issued has landed, then the workgroup barrier publishes them

@@ -78,7 +78,11 @@ class NodeLabeler:
             return Result()
         want = node_labels(self.smi, self.pod_server_tenants)
         have = ko.labels(node)
-        diff = {k: v for k, v in want.items() if have.get(k) != v}
+        diff: dict = {k: v for k, v in want.items() if have.get(k) != v}
+        if self.pod_server_tenants <= 0 and C.LABEL_POD_SERVER_TENANTS in have:
+            # the pod server was disabled: without the label the slice model
+            # caps slices per GPU at the HWS process slots again (gpu/cumask.py)
+            diff[C.LABEL_POD_SERVER_TENANTS] = None
         if diff:
             self.api.patch("Node", self.node_name, {"metadata": {"labels": diff}})
         return Result(requeue_after=self.REFRESH_S)

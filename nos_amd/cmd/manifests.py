@@ -61,7 +61,9 @@ DEFAULT_VALUES: dict = {
         "devicePluginDelaySeconds": 5,
         "planReportTimeoutSeconds": 300,
         "slicePlacement": "pack",
-        "cuPolicy": "proportional",
+        # auto: "shared" with the pod server (its tenants share every CU, MPS's
+        # default), "proportional" CU masks for process pods otherwise
+        "cuPolicy": "auto",
         "reserveWholeGpus": 0,
         "preferredMemoryMode": "NPS1",
         "knownPartitionGeometries": None,  # list override; default: derived from each node's amd-smi memory/XCDs
@@ -114,6 +116,18 @@ def apply_set(values: dict, expr: str) -> dict:
     return merge_values(values, node)
 
 
+def resolve_values(v: dict) -> dict:
+    """Defaults that depend on other values: ``cuPolicy: auto`` is ``shared``
+    when the pod server is enabled -- its tenants then share every CU and the
+    lanes' HIP graphs (an explicit even/proportional policy gives pod-server
+    tenants CU-masked streams, captured under slice-budgeted kernel configs)
+    -- and ``proportional`` otherwise."""
+    gp = v["gpuPartitioner"]
+    if gp.get("cuPolicy") == "auto":
+        gp["cuPolicy"] = "shared" if gp["podServer"]["enabled"] else "proportional"
+    return v
+
+
 def validate_values(v: dict) -> None:
     if v["namespace"] in ("", "default"):
         raise ValueError("nos-amd must not be installed in the 'default' namespace")
@@ -122,8 +136,8 @@ def validate_values(v: dict) -> None:
         raise ValueError("gpuPartitioner batch windows must be > 0")
     if gp["slicePlacement"] not in ("pack", "spread", "measured"):
         raise ValueError("gpuPartitioner.slicePlacement must be pack|spread|measured")
-    if gp["cuPolicy"] not in ("even", "proportional", "shared"):
-        raise ValueError("gpuPartitioner.cuPolicy must be even|proportional|shared")
+    if gp["cuPolicy"] not in ("auto", "even", "proportional", "shared"):
+        raise ValueError("gpuPartitioner.cuPolicy must be auto|even|proportional|shared")
     ps = gp["podServer"]
     if ps["enabled"] and not (1 <= int(ps["lanes"]) <= 32 and int(ps["tenantsPerGpu"]) >= 1):
         raise ValueError("gpuPartitioner.podServer: lanes must be 1..32 (one HW queue each), tenantsPerGpu >= 1")
@@ -552,7 +566,7 @@ def telemetry() -> dict[str, list[dict]]:
 def render(values: dict | None = None) -> dict[str, str]:
     """Render every manifest file for ``values`` (merged over DEFAULT_VALUES)."""
     global _V
-    v = merge_values(DEFAULT_VALUES, values or {})
+    v = resolve_values(merge_values(DEFAULT_VALUES, values or {}))
     validate_values(v)
     prev, _V = _V, v
     try:

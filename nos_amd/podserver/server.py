@@ -43,8 +43,10 @@ Design (MI355X-first):
   Process pods only get a cooperative caching-allocator cap.
 * **CU slices.**  A tenant whose allocation carries a CU mask gets its own
   CU-masked stream (``hipExtStreamCreateWithCUMask``), the per-queue form of
-  ``ROC_GLOBAL_CU_MASK``.  Unmasked tenants share every CU, which is MPS's
-  default.
+  ``ROC_GLOBAL_CU_MASK``, and its graph is captured under the slice-budgeted
+  kernel configs a masked process pod uses (``ops.set_cu_budget``: grids
+  sized to its CUs).  Unmasked tenants share every CU, which is MPS's
+  default and the chart's default for pod-server nodes (cuPolicy auto).
 * **Kernel configs.**  Tenants run the fractional-pod kernel configs of
   :func:`nos_amd.models.pod.kernel_config` while co-tenants fill the CU slots
   (no key splits, x6 GEMMs on 128x128 tiles).  A tenant alone on the GPU
@@ -432,18 +434,35 @@ class PodServer:
                 m = prog.compile("cuda")
                 x = prog.input_tensor("cuda")
             self._setup_stream.synchronize()
+            budget_cfg = None
             if mask:
                 from ..bench_support import cus_from_hex
+                from ..models.pod import kernel_config
                 from ..ops.streams import CUMaskedStream
 
-                stream = CUMaskedStream(cus_from_hex(mask), self.info["multiprocessor_count"])
+                cus = cus_from_hex(mask)
+                stream = CUMaskedStream(cus, self.info["multiprocessor_count"])
+                # a CU-mask slice plans for its own CUs: slice-sized persistent
+                # grids and the budget-aware configs a masked process pod uses
+                frac = limit / self.memory_gb if limit and self.memory_gb else 0.5
+                budget_cfg = (kernel_config(frac, os.environ, len(cus)), len(cus))
             gt = GraphedTenant(m, stream.torch if stream else self._setup_stream, x)
             with torch.no_grad():
-                if self.graphs:  # the lanes keep replaying other tenants meanwhile
-                    gt.capture(capture_error_mode="thread_local")
-                else:
-                    gt.launch()
-                    gt.stream.synchronize()
+                try:
+                    if budget_cfg is not None:
+                        from ..ops import set_cu_budget
+
+                        self._apply_config(budget_cfg[0])
+                        set_cu_budget(budget_cfg[1])
+                    if self.graphs:  # the lanes keep replaying other tenants meanwhile
+                        gt.capture(capture_error_mode="thread_local")
+                    else:
+                        gt.launch()
+                        gt.stream.synchronize()
+                finally:
+                    if budget_cfg is not None:
+                        set_cu_budget(0)
+                        self._apply_config(self.kernel_config)
                 solo = None
                 if self.solo_config is not None and not mask:
                     # the lanes only replay graphs, so switching the process-wide

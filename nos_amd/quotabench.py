@@ -1,0 +1,337 @@
+"""BASELINE config 5: elastic quotas and GPU partitioning acting on running tenants.
+
+The reference's elastic quota (``pkg/scheduler/plugins/capacityscheduling/
+capacity_scheduling.go:468-675`` for victim selection,
+``internal/controllers/elasticquota/elasticquota.go:38-72`` for
+``status.used`` and the ``in-quota`` / ``over-quota`` pod labels) lets a
+namespace borrow other namespaces' unused ``min`` and takes it back by
+preempting the borrower's over-quota pods when the lender needs it.  This
+harness runs that flow end to end on one node with the real control plane
+(scheduler + CapacityScheduling, operator, cumask partitioner, device plugin,
+kubelet) and REAL tenants behind the kubelet:
+
+1. two namespaces with ElasticQuotas on ``nos.nebuly.com/gpu-memory``, each
+   ``min`` = half the node's slice memory, ``max`` = all of it;
+2. team-a submits more 10 GB slice pods than its ``min``: they all run, the
+   ones past ``min`` borrowing team-b's unused quota (``over-quota``);
+3. team-b submits its ``min`` worth of pods: the node is full, so
+   CapacityScheduling's PostFilter preempts team-a's over-quota pods; the
+   kubelet stops each victim's tenant (its process ends, the device plugin
+   releases the slice and deletes the allocation record, the pod server
+   evicts the tenant if it is still registered) and the preemptor's pod
+   starts on the freed slice.
+
+The kubelet's ``runtime`` / ``on_stop`` hooks are the data plane: a
+:class:`RecordingRuntime` for the CPU rehearsal (tests) or a
+:class:`ProcessRuntime` that starts every admitted pod as a real pod process
+with its device-plugin env (``models/pod.py`` against the GPU's pod server).
+The simulated cluster's clock follows the wall clock while tenants run.
+
+Reported: preemptions, the time from a victim's stop to the preemptor's
+first inference, concurrently running tenants, EQ ``status.used`` and pod
+labels checked against the tenants actually running, and (GPU) amd-smi
+utilisation per phase.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import sys
+import tempfile
+import threading
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+from .api import constants as C
+from .api import v1alpha1
+from .api.config import GpuPartitionerConfig
+from .kube import objects as ko
+
+GPU_MEM = C.RESOURCE_GPU_MEMORY
+
+
+@dataclass
+class Tenant:
+    key: str
+    env: dict
+    t_start: float
+    t_ready: float | None = None
+    t_stop: float | None = None
+    handle: object = None
+
+
+class RecordingRuntime:
+    """CPU rehearsal: a tenant is 'running' from its container start to its
+    stop, 'ready' (first inference) at once."""
+
+    def __init__(self):
+        self.tenants: dict[str, Tenant] = {}
+        self.lock = threading.Lock()
+
+    def start(self, key: str, env: dict) -> None:
+        now = time.monotonic()
+        with self.lock:
+            self.tenants[key] = Tenant(key, env, now, now)
+
+    def stop(self, key: str) -> None:
+        with self.lock:
+            t = self.tenants.get(key)
+            if t is not None and t.t_stop is None:
+                t.t_stop = time.monotonic()
+
+    def poll(self) -> None:
+        pass
+
+    def running(self) -> set[str]:
+        with self.lock:
+            return {k for k, t in self.tenants.items() if t.t_stop is None}
+
+    def ready(self) -> set[str]:
+        with self.lock:
+            return {k for k, t in self.tenants.items() if t.t_stop is None and t.t_ready is not None}
+
+    def close(self) -> None:
+        pass
+
+
+class ProcessRuntime(RecordingRuntime):
+    """Every admitted pod is a real pod process (``models/pod.py``) with its
+    device-plugin env; 'ready' = its first inference completed (status
+    board).  Stopping a tenant sets its board's stop flag (graceful: the pod
+    closes its pod-server connection) and kills it after ``grace_s``."""
+
+    def __init__(self, launcher, workdir: str, dtype: str = "fp32", device: str = "cuda", grace_s: float = 10.0):
+        super().__init__()
+        self.launcher, self.dir, self.dtype, self.device, self.grace = launcher, Path(workdir), dtype, device, grace_s
+        self._n = 0
+
+    def start(self, key: str, env: dict) -> None:
+        from .models.pod import StatusBoard
+        from .podbench import REPO
+
+        self._n += 1
+        d = self.dir / f"t{self._n:03d}"
+        d.mkdir(parents=True, exist_ok=True)
+        board = StatusBoard(d / "status.bin", pods=1)
+        penv = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE",
+                                                                 "HIP_VISIBLE_DEVICES", "ROC_GLOBAL_CU_MASK")}
+        penv.update({k: str(v) for k, v in env.items()})
+        penv["PYTHONPATH"] = str(REPO) + os.pathsep + penv.get("PYTHONPATH", "")
+        cmd = [sys.executable, "-u", "-m", "nos_amd.models.pod", "--status", str(board.path), "--slot", "0",
+               "--out", str(d), "--dtype", self.dtype, "--seed", str(self._n), "--device", self.device]
+        proc = self.launcher.spawn(cmd, penv, str(d / "pod.err"), str(REPO))
+        with self.lock:
+            self.tenants[key] = Tenant(key, env, time.monotonic(), handle=(proc, board, d))
+
+    def stop(self, key: str) -> None:
+        with self.lock:
+            t = self.tenants.get(key)
+            if t is None or t.t_stop is not None:
+                return
+            t.t_stop = time.monotonic()
+        proc, board, _ = t.handle
+        board.stop()
+
+        def reap():
+            try:
+                proc.wait(timeout=self.grace)
+            except Exception:
+                proc.kill()
+
+        threading.Thread(target=reap, daemon=True).start()
+
+    def poll(self) -> None:
+        from .models.pod import STATE_FAILED
+
+        with self.lock:
+            ts = [t for t in self.tenants.values() if t.t_ready is None and t.t_stop is None]
+        for t in ts:
+            proc, board, d = t.handle
+            if board.counts()[0] >= 1:
+                t.t_ready = float(board.row(0)[2])  # CLOCK_MONOTONIC of its first completion
+            elif board.states()[0] == STATE_FAILED or proc.poll() is not None:
+                err = (d / "pod.err").read_text()[-1500:] if (d / "pod.err").exists() else ""
+                raise RuntimeError(f"tenant {t.key} failed:\n{err}")
+
+    def close(self) -> None:
+        with self.lock:
+            keys = [k for k, t in self.tenants.items() if t.t_stop is None]
+        for k in keys:
+            self.stop(k)
+        deadline = time.monotonic() + self.grace + 5
+        for t in list(self.tenants.values()):
+            proc = t.handle[0]
+            try:
+                proc.wait(timeout=max(0.5, deadline - time.monotonic()))
+            except Exception:
+                proc.kill()
+
+
+@dataclass
+class QuotaScenario:
+    gpus: int = 1
+    slice_gb: int = 10
+    team_a_pods: int = 20
+    team_b_pods: int = 14
+    min_gb: int = 140                 # per team
+    max_gb: int = 280
+    pod_server_dir: str = ""
+    tenants_per_gpu: int = 48         # the pod server's tenant cap (memory bounds 10 GB slices at 28 first)
+    live: bool = False                # sim clock follows the wall clock (real tenants)
+    batch_window_s: float = 2.0
+    events: list = field(default_factory=list)
+
+    def build(self, runtime):
+        from .gpu.fakesmi import FakeSmi
+        from .sim.cluster import SimCluster
+
+        self.runtime = runtime
+        cfg = GpuPartitionerConfig(cuPolicy="shared", batchWindowTimeoutSeconds=int(max(1, self.batch_window_s * 2)),
+                                   batchWindowIdleSeconds=int(max(1, self.batch_window_s)))
+        cl = self.cl = SimCluster(partitioner_config=cfg)
+        cl.add_node("mi355x-0", C.PARTITIONING_CUMASK, smi=FakeSmi(gpus=self.gpus, node="mi355x-0"),
+                    pod_server_tenants=self.tenants_per_gpu, pod_server_dir=self.pod_server_dir,
+                    runtime=lambda pod, conts: self._start(pod, conts), on_stop=lambda pod, conts: self._stop(pod))
+        for ns in ("team-a", "team-b"):
+            cl.api.create({"kind": "Namespace", "metadata": {"name": ns}})
+            # CapacityScheduling always compares cpu and memory (the reference's
+            # usedOverWith); the pods' 100m / 0 stay far inside these
+            cl.api.create(v1alpha1.build_eq(ns, "quota").with_min({GPU_MEM: self.min_gb, "cpu": "32", "memory": "256Gi"})
+                          .with_max({GPU_MEM: self.max_gb, "cpu": "64", "memory": "1Ti"}).get())
+        self._settle(30)
+        return cl
+
+    # ------------------------------------------------------------ kubelet hooks
+    def _start(self, pod: dict, conts) -> None:
+        env = {}
+        for rc in conts:
+            env.update(rc.envs)
+        key = ko.key(pod)
+        self.runtime.start(key, env)
+        self.events.append(("start", key, time.monotonic()))
+
+    def _stop(self, pod: dict) -> None:
+        key = ko.key(pod)
+        self.runtime.stop(key)
+        self.events.append(("stop", key, time.monotonic()))
+
+    # ------------------------------------------------------------ driving
+    def _settle(self, sim_s: float, until=None) -> None:
+        self.cl.settle(sim_s, until=until)
+
+    def drive(self, until, timeout_s: float, tick_s: float = 0.05) -> bool:
+        """Run the control plane until ``until()``: in live mode the sim
+        clock follows the wall clock and the runtime is polled."""
+        if not self.live:
+            self.cl.settle(timeout_s, until=until)
+            return until()
+        w0, s0 = time.monotonic(), self.cl.clock.now()
+        while True:
+            self.cl.settle(tick_s, until=until)
+            target = s0 + (time.monotonic() - w0)
+            if self.cl.clock.now() < target:
+                self.cl.clock.advance(target - self.cl.clock.now())
+            self.runtime.poll()
+            if until():
+                return True
+            if time.monotonic() - w0 > timeout_s:
+                return False
+            time.sleep(tick_s)
+
+    def submit(self, ns: str, n: int, prefix: str) -> list[str]:
+        keys = []
+        for i in range(n):
+            self.cl.submit_pod(f"{prefix}-{i}", {f"{C.AMD_SLICE_RESOURCE_PREFIX}{self.slice_gb}gb": 1}, namespace=ns)
+            keys.append(f"{ns}/{prefix}-{i}")
+            if not self.live:
+                self.cl.clock.advance(1)
+        return keys
+
+    # ------------------------------------------------------------ observations
+    def labels(self, ns: str) -> dict[str, str | None]:
+        return {ko.key(p): ko.labels(p).get(C.LABEL_CAPACITY_INFO) for p in self.cl.pods(ns)
+                if ko.pod_phase(p) == ko.RUNNING}
+
+    def used_gb(self, ns: str) -> float:
+        eq = self.cl.api.get(v1alpha1.KIND_EQ, "quota", ns)
+        return float(((eq.get("status") or {}).get("used") or {}).get(GPU_MEM, 0))
+
+    def snapshot(self) -> dict:
+        run = self.runtime.running()
+        out = {}
+        for ns in ("team-a", "team-b"):
+            lab = self.labels(ns)
+            mine = {k for k in run if k.startswith(ns + "/")}
+            out[ns] = {"running_pods": len(lab), "tenants_running": len(mine),
+                       "in_quota": sum(1 for v in lab.values() if v == "in-quota"),
+                       "over_quota": sum(1 for v in lab.values() if v == "over-quota"),
+                       "status_used_gb": self.used_gb(ns), "tenant_gb": len(mine) * self.slice_gb,
+                       "pods_match_tenants": set(lab) == mine}
+        return out
+
+    def run(self, runtime, phase_timeout_s: float = 600.0, sampler=None) -> dict:
+        """Both phases; returns the measurements."""
+        self.build(runtime)
+        res: dict = {"config": {"gpus": self.gpus, "slice_gb": self.slice_gb, "team_a_pods": self.team_a_pods,
+                                "team_b_pods": self.team_b_pods, "min_gb": self.min_gb, "max_gb": self.max_gb}}
+        t0 = time.monotonic()
+        a = self.submit("team-a", self.team_a_pods, "a")
+        ok = self.drive(lambda: set(a) <= self.runtime.ready() and self._labels_settled(), phase_timeout_s)
+        res["phase_a"] = {"ok": ok, "seconds": round(time.monotonic() - t0, 2), **self.snapshot()}
+        if sampler is not None:
+            res["phase_a"]["gpu_util_pct"] = sampler.mean(t0, time.monotonic())[0]
+        t1 = time.monotonic()
+        over_a = {k for k, v in self.labels("team-a").items() if v == "over-quota"}
+        p0 = self.cl.scheduler.stats.get("preemptions", 0)
+        b = self.submit("team-b", self.team_b_pods, "b")
+        ok = self.drive(lambda: set(b) <= self.runtime.ready() and self._labels_settled(), phase_timeout_s)
+        t2 = time.monotonic()
+        stops = sorted(t for kind, k, t in self.events if kind == "stop" and t >= t1)
+        b_ready = sorted(self.runtime.tenants[k].t_ready for k in b if k in self.runtime.tenants
+                         and self.runtime.tenants[k].t_ready is not None)
+        # the k-th victim's stop frees the slice the k-th preempting pod runs on
+        lat = [r - s for s, r in zip(stops, b_ready[len(b_ready) - len(stops):])] if stops else []
+        res["phase_b"] = {"ok": ok, "seconds": round(t2 - t1, 2), "preemptions":
+                          self.cl.scheduler.stats.get("preemptions", 0) - p0, "victims": len(stops),
+                          # CapacityScheduling may only take back borrowed quota
+                          "victims_over_quota_only": {k for kind, k, t in self.events
+                                                      if kind == "stop" and t >= t1} <= over_a,
+                          "preemption_to_running_s": {"n": len(lat),
+                                                      "p50": round(sorted(lat)[len(lat) // 2], 3) if lat else None,
+                                                      "max": round(max(lat), 3) if lat else None},
+                          "submit_to_all_running_s": round((b_ready[-1] - t1) if b_ready else -1, 3),
+                          **self.snapshot()}
+        if sampler is not None:
+            res["phase_b"]["gpu_util_pct"] = sampler.mean(t1, t2)[0]
+        res["concurrent_tenants"] = len(self.runtime.running())
+        return res
+
+    def _labels_settled(self) -> bool:
+        for ns in ("team-a", "team-b"):
+            if any(v is None for v in self.labels(ns).values()):
+                return False
+        return True
+
+
+def scenario_for(slices_per_gpu: int, slice_gb: int = 10, **kw) -> QuotaScenario:
+    """The default split of a node with ``slices_per_gpu`` slice slots: each
+    team's min is half of them, team-a runs 5/7 of them (borrowing), then
+    team-b claims its min (preempting team-a's borrowed slices)."""
+    half = slices_per_gpu // 2
+    return QuotaScenario(slice_gb=slice_gb, team_a_pods=max(half + 1, round(slices_per_gpu * 5 / 7)),
+                         team_b_pods=half, min_gb=half * slice_gb, max_gb=slices_per_gpu * slice_gb,
+                         tenants_per_gpu=slices_per_gpu, **kw)
+
+
+def run_cpu_rehearsal(tmp: str | None = None, **kw) -> dict:
+    d = tmp or tempfile.mkdtemp(prefix="nos_quota_")
+    try:
+        sc = QuotaScenario(pod_server_dir=d, **kw)
+        return sc.run(RecordingRuntime())
+    finally:
+        if tmp is None:
+            shutil.rmtree(d, ignore_errors=True)
+
+
+__all__ = ["QuotaScenario", "RecordingRuntime", "ProcessRuntime", "run_cpu_rehearsal"]

@@ -365,3 +365,38 @@ def test_lanes_know_when_a_tenant_runs_alone(server, monkeypatch):
     assert server._busy == 0
     server.stop()
     assert server.tenants == {}
+
+
+def test_chart_defaults_pod_server_nodes_to_shared_cus():
+    """cuPolicy "auto": shared CUs when the pod server is enabled (its tenants
+    share the lanes' graphs, MPS's default), proportional masks otherwise; an
+    explicit policy wins."""
+    import yaml
+
+    from nos_amd.cmd import manifests as m
+
+    def policy(values):
+        out = m.render(values)
+        cm = [o for o in yaml.safe_load_all(out["deviceplugin/daemonset.yaml"]) if o and o["kind"] == "ConfigMap"][0]
+        return yaml.safe_load(cm["data"]["device_plugin_config.yaml"])["cuPolicy"]
+
+    assert policy({}) == "proportional"
+    assert policy({"gpuPartitioner": {"podServer": {"enabled": True}}}) == "shared"
+    assert policy({"gpuPartitioner": {"cuPolicy": "even", "podServer": {"enabled": True}}}) == "even"
+
+
+def test_node_labeler_removes_the_pod_server_label_when_disabled():
+    from nos_amd.agents.devices import NodeLabeler
+    from nos_amd.gpu.fakesmi import FakeSmi
+    from nos_amd.kube import objects as ko
+    from nos_amd.runtime.manager import Request
+    from nos_amd.sim.apiserver import ApiServer
+
+    api = ApiServer()
+    api.create({"apiVersion": "v1", "kind": "Node", "metadata": {"name": "n1", "labels": {}}})
+    smi = FakeSmi(gpus=1, node="n1")
+    NodeLabeler(api, "n1", smi, pod_server_tenants=48).reconcile(Request("n1"))
+    assert ko.labels(api.get("Node", "n1"))[C.LABEL_POD_SERVER_TENANTS] == "48"
+    NodeLabeler(api, "n1", smi, pod_server_tenants=0).reconcile(Request("n1"))
+    labels = ko.labels(api.get("Node", "n1"))
+    assert C.LABEL_POD_SERVER_TENANTS not in labels and labels[C.LABEL_AMD_COUNT] == "1"

@@ -1,0 +1,65 @@
+"""BASELINE config 5 harness (nos_amd/quotabench.py, ``bench.py --quota``):
+ElasticQuota borrowing and CapacityScheduling fair-share preemption acting on
+running tenants, rehearsed on the CPU.
+
+Reference: victim selection ``pkg/scheduler/plugins/capacityscheduling/
+capacity_scheduling.go:468-675``; ``status.used`` and the in-quota /
+over-quota labels ``internal/controllers/elasticquota/elasticquota.go:38-72``.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+from nos_amd.quotabench import RecordingRuntime, scenario_for
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def test_borrow_then_preempt_then_replace_on_a_full_node(tmp_path):
+    """28 slice slots: team-a borrows 6 slices past its min, team-b claims its
+    min, exactly the 6 borrowed slices are taken back, and at every step the
+    EQ status.used and the pod labels describe the tenants actually running."""
+    sc = scenario_for(28, pod_server_dir=str(tmp_path))
+    rt = RecordingRuntime()
+    res = sc.run(rt)
+    a = res["phase_a"]
+    assert a["ok"] and a["team-a"]["running_pods"] == 20
+    assert (a["team-a"]["in_quota"], a["team-a"]["over_quota"]) == (14, 6)
+    assert a["team-a"]["status_used_gb"] == a["team-a"]["tenant_gb"] == 200
+    assert a["team-a"]["pods_match_tenants"]
+    b = res["phase_b"]
+    assert b["ok"] and b["preemptions"] == 6 and b["victims"] == 6 and b["victims_over_quota_only"]
+    for team in ("team-a", "team-b"):
+        t = b[team]
+        assert t["running_pods"] == t["tenants_running"] == 14 and t["in_quota"] == 14 and t["over_quota"] == 0
+        assert t["status_used_gb"] == t["tenant_gb"] == 140 and t["pods_match_tenants"]
+    assert res["concurrent_tenants"] == 28
+    # the victims' allocation records are gone (their pod-server tenants get evicted),
+    # the 28 running tenants' records remain
+    assert len(list((tmp_path / ".allocations" / "gpu-0").glob("*.json"))) == 28
+    assert b["preemption_to_running_s"]["n"] == 6
+
+
+@pytest.mark.timeout(600)
+def test_bench_quota_runs_real_pod_processes_against_a_pod_server():
+    """``bench.py --quota --device cpu``: the kubelet starts every admitted pod
+    as a pod process (numpy-only client) against a CPU pod server; the
+    borrowers' processes are stopped by preemption and the lender's pods run."""
+    cmd = [sys.executable, "bench.py", "--quota", "--device", "cpu", "--pods-per-gpu", "6"]
+    r = subprocess.run(cmd, cwd=REPO, env={**os.environ, "OMP_NUM_THREADS": "1"}, capture_output=True, text=True,
+                       timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["metric"].startswith("config5")
+    assert d["phase_a"]["ok"] and d["phase_a"]["team-a"]["over_quota"] == 1
+    b = d["phase_b"]
+    assert b["ok"] and b["preemptions"] >= 1 and b["victims"] == 1 and b["victims_over_quota_only"]
+    assert b["team-a"]["tenants_running"] == b["team-b"]["tenants_running"] == 3
+    assert b["team-b"]["pods_match_tenants"] and b["team-a"]["pods_match_tenants"]
+    assert d["concurrent_tenants"] == 6 and d["pod_server"]["device"] == "cpu"
