@@ -198,6 +198,14 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
         return t.tolist()
 
+    def gather(self, obj) -> list:
+        """Every rank's ``obj`` (picklable), in rank order."""
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
     def close(self) -> None:
         if self.dist:
             self.dist.destroy_process_group()
@@ -207,16 +215,20 @@ class UtilSampler:
     """amd-smi gfx activity of this rank's GPU at a fixed period; windows are
     cut out of the sample stream by timestamp."""
 
-    def __init__(self, hip_id: int, period_s: float = 0.02):
+    def __init__(self, hip_id: int, period_s: float = 0.02, smi=None):
+        """``hip_id``: this rank's GPU as HIP numbers it; amd-smi is asked by
+        ITS index (the two orders can differ on a node)."""
         self.samples: list[tuple[float, int]] = []
         self.clocks: list[tuple[float, int]] = []
         self.err = None
         self._stop = threading.Event()
         self.period = period_s
         try:
-            from nos_amd.gpu.amdsmi import AmdSmi
+            if smi is None:
+                from nos_amd.gpu.amdsmi import AmdSmi
 
-            self.smi = AmdSmi.real()
+                smi = AmdSmi.real()
+            self.smi = smi
             ids = {g.hip_id: g.index for g in self.smi.gpus()}
             self.index = ids.get(hip_id, hip_id)
         except Exception as e:  # amd-smi unusable here: util unreported
@@ -335,8 +347,25 @@ class FleetStartError(RuntimeError):
     """Pods of some rank failed to start; raised on EVERY rank (the flag is reduced)."""
 
 
-def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, step_s, sampler, device="cuda"):
+GPU_PROCS = {"max": 0, "runs": []}  # GPU processes per GPU in every fleet run (HWS bound: hws_max_conc_proc)
+
+
+def gpu_processes(envs: list[dict], server_alive: bool) -> int:
+    """GPU processes on this rank's GPU while ``envs`` run: this rank, the pod
+    server, and every pod that is not a pod-server client (process pods, the
+    DP trainer)."""
+    from nos_amd.api import constants as C
+
+    return 1 + int(server_alive) + sum(1 for e in envs if not e.get(C.ENV_POD_SERVER))
+
+
+def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, step_s, sampler, device="cuda",
+              server_alive: bool = False):
     from nos_amd.podbench import PodFleet
+
+    n = gpu_processes(envs, server_alive)
+    GPU_PROCS["max"] = max(GPU_PROCS["max"], n)
+    GPU_PROCS["runs"].append(n)
 
     fleet = PodFleet(envs, dtype=dtype, graphs=graphs, extra_env=extra_env, launcher=launcher, device=device)
     try:
@@ -410,6 +439,15 @@ class PodServerProc:
     def close(self) -> None:
         if self.proc.poll() is None:
             self.proc.kill()
+
+
+def _close_server(server: "PodServerProc") -> dict:
+    try:
+        info = server.info()
+    except Exception as e:  # reported, not fatal: the pods' own records are the measurement
+        info = {"error": repr(e)}
+    server.close()
+    return info
 
 
 def _hws_limit() -> int:
@@ -532,14 +570,17 @@ def main(argv=None) -> int:
         ref = {"inf_per_s": round(w1.throughput, 3), "latency_s": w1.mean_latency_s, "gpu_util_pct": u1}
 
     server = None
+    server_socket = None
     if server_mode or any(m == "server" for m, _, _ in table_plans):
         server = PodServerProc(launcher, args, args.gpu_env, args.pod_server_dir)
+        server_socket = server.path
         log(rank, f"pod server ready in {server.wait_ready():.1f} s on {server.path}")
     trainer_error = None
+    srv = server is not None
     try:
         w, util, n_util, ready_s, tr = run_fleet(d, launcher, fleet_envs(pod_envs), args.dtype, not args.no_graphs,
                                                  fleet_env, args.warmup, args.steps, args.step_s, sampler,
-                                                 device=args.device)
+                                                 device=args.device, server_alive=srv)
     except FleetStartError as e:
         if not use_coll:
             raise
@@ -551,35 +592,38 @@ def main(argv=None) -> int:
         use_coll, fleet_envs = False, (lambda e: e)
         w, util, n_util, ready_s, tr = run_fleet(d, launcher, pod_envs, args.dtype, not args.no_graphs,
                                                  fleet_env, args.warmup, args.steps, args.step_s, sampler,
-                                                 device=args.device)
+                                                 device=args.device, server_alive=srv)
     bf = None
     if args.extra_bf16_s > 0 and args.dtype != "bf16" and d.cuda:
         wb, ub, _, _, _ = run_fleet(d, launcher, fleet_envs(pod_envs), "bf16", not args.no_graphs, extra_env, 2, 1,
-                                    args.extra_bf16_s, sampler)
+                                    args.extra_bf16_s, sampler, server_alive=srv)
         bf = {"inf_per_s": round(wb.throughput, 2), "mean_latency_s": wb.mean_latency_s,
               "concurrent_pods": wb.concurrent, "gpu_util_pct": ub}
     table = []
+    server_info = None
     for mode, n, tenvs in table_plans:  # the reference demo's latency-vs-pods rows (README.md:63-71)
+        if mode != "server" and server is not None:
+            # process-pod rows: the server's GPU process would be one HWS slot
+            # more than the pods and this rank (7 + 2 > 8: time-sliced)
+            server_info = _close_server(server)
+            server = None
         wt, ut, _, _, _ = run_fleet(d, launcher, tenvs, args.dtype, not args.no_graphs, extra_env, 1, 1,
-                                    args.table_window_s, sampler, device=args.device)
+                                    args.table_window_s, sampler, device=args.device,
+                                    server_alive=server is not None)
         table.append({"mode": mode, "pods": n, "concurrent": wt.concurrent, "inf_per_s": round(wt.throughput, 2),
                       "mean_latency_s": wt.mean_latency_s, "gpu_util_pct": ut,
                       "pods_over_latency": round(n / wt.mean_latency_s, 2) if wt.mean_latency_s else None,
                       "cu_mask": (wt.pods[0].info.get("cu_mask") if wt.pods else None)})
         log(rank, f"table {table[-1]}")
-    server_info = None
     if server is not None:
-        try:
-            server_info = server.info()
-        except Exception as e:  # reported, not fatal: the pods' own records are the measurement
-            server_info = {"error": repr(e)}
-        server.close()
+        server_info = _close_server(server)
     if sampler:
         sampler.close()
     launcher.close()
 
     # whole-job aggregates (window = slowest rank's)
-    elapsed, = d.reduce([w.window_s], "max")
+    elapsed, gp_max = d.reduce([w.window_s, float(GPU_PROCS["max"])], "max")
+    sockets = d.gather(server_socket) if server_mode else None
     running = w.concurrent  # inference pods and the trainer pod alike
     sums = d.reduce([w.completed, float(running), util if util is not None else -1e9, float(len(w.inference_pods)),
                      ref["inf_per_s"] if ref else 0.0, bf["inf_per_s"] if bf else 0.0,
@@ -629,6 +673,10 @@ def main(argv=None) -> int:
         # what bounds it on this node: the amdgpu hardware scheduler's concurrent
         # processes per logical GPU (VMIDs), read from the driver
         "hws_max_concurrent_processes_per_gpu": _hws_limit(),
+        # the most GPU processes any GPU held in any window (rank + pod server +
+        # process pods / trainer): must stay within the HWS limit above
+        "max_gpu_processes_per_gpu": int(gp_max),
+        "pod_server_sockets": sockets,
         # server mode: the GPU processes are the pod server (+ the trainer pod),
         # so the HWS bound does not apply to the pods; memory does (28 x 10 GB)
         "pod_server": None if not server_mode else {**(server_info or {}), "tenants_per_gpu_max": POD_SERVER_TENANTS},

@@ -32,8 +32,11 @@ class FakeSmi:
 
     def __init__(self, gpus: int = 8, compute: str = "SPX", memory: str = "NPS1", cus: int = 256, xcds: int = 8,
                  vram_mb: int = 294912, model: str = "AMD Instinct MI355X", node: str = "node",
-                 max_procs: int = 8):
+                 max_procs: int = 8, hip_order: list[int] | None = None):
+        """``hip_order``: HIP id of each GPU (SPX), a permutation -- HIP's
+        enumeration need not follow amd-smi's index order."""
         self._lock = threading.RLock()
+        self.hip_order = list(hip_order) if hip_order is not None else None
         self.max_concurrent_processes = max_procs  # KFD HWS concurrent processes per logical GPU
         self.node = node
         self.model = model
@@ -66,6 +69,8 @@ class FakeSmi:
         with self._lock:
             self._check(i, "gpu")
             base = sum(PARTITIONS_PER_MODE[self.compute[j]] for j in range(i) if j not in self.lost)
+            if self.hip_order is not None:
+                base = self.hip_order[i]
             g = GpuInfo(index=i, num_cus=self.cus, num_xcds=self.xcds, compute_mode=self.compute[i],
                         memory_mode=self.memory[i], num_partitions=PARTITIONS_PER_MODE[self.compute[i]],
                         hip_id=base, drm_render=128 + base, vram_mb=self.vram_mb, bdf=f"0000:{0x11 + i:02x}:00.0",
