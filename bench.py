@@ -441,6 +441,21 @@ class PodServerProc:
             self.proc.kill()
 
 
+def _normalise_table(table: list[dict]) -> None:
+    """Per row: latency over the same mode's 1-pod row, raw and at the 1-pod
+    row's GFX clock (latency scales as 1/clock): under load the MI355X clock
+    drops (DVFS), which the raw ratio mixes with contention between pods."""
+    solo = {r["mode"]: r for r in table if r["pods"] == 1 and r.get("mean_latency_s")}
+    for r in table:
+        s1 = solo.get(r["mode"])
+        if not s1 or not r.get("mean_latency_s"):
+            continue
+        r["latency_vs_solo"] = round(r["mean_latency_s"] / s1["mean_latency_s"], 3)
+        if r.get("sclk_mhz") and s1.get("sclk_mhz"):
+            r["latency_vs_solo_at_solo_clock"] = round(r["mean_latency_s"] * r["sclk_mhz"] / s1["sclk_mhz"]
+                                                       / s1["mean_latency_s"], 3)
+
+
 def _close_server(server: "PodServerProc") -> dict:
     try:
         info = server.info()
@@ -611,12 +626,13 @@ def main(argv=None) -> int:
                                     args.table_window_s, sampler, device=args.device,
                                     server_alive=server is not None)
         table.append({"mode": mode, "pods": n, "concurrent": wt.concurrent, "inf_per_s": round(wt.throughput, 2),
-                      "mean_latency_s": wt.mean_latency_s, "gpu_util_pct": ut,
+                      "mean_latency_s": wt.mean_latency_s, "gpu_util_pct": ut, "sclk_mhz": wt.sclk_mhz,
                       "pods_over_latency": round(n / wt.mean_latency_s, 2) if wt.mean_latency_s else None,
                       "cu_mask": (wt.pods[0].info.get("cu_mask") if wt.pods else None)})
         log(rank, f"table {table[-1]}")
     if server is not None:
         server_info = _close_server(server)
+    _normalise_table(table)
     if sampler:
         sampler.close()
     launcher.close()

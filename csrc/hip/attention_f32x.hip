@@ -168,10 +168,18 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
     // + lane / 8, physical chunk lane % 8 = logical chunk ^ swizzle.
     // The planes are padded to whole tiles with zeros: a tile's address is a
     // wave-uniform base plus the hoisted per-lane offsets.
+    // The tail tile's rows past Skv re-read the last key's planes (finite
+    // values; the -inf mask makes their P exactly 0), so the padding rows of
+    // the planes are never read and need no zeroing (no memset per call).
     const unsigned short* pb = kvs + (long long)b * skvp * (6 * ldh) + hd * D;
     auto stage_piece = [&](int t, int buf, int i) {
       const int p = wid * 6 + i;
-      glds16(pb + (long long)t * (KVB * 6) * ldh + soff[i], smem + buf * STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
+      long long off = (long long)t * (KVB * 6) * ldh + soff[i];
+      if ((t + 1) * KVB > Skv) {
+        const int over = t * KVB + (p & 3) * 8 + (lane >> 3) - (Skv - 1);
+        if (over > 0) off -= (long long)over * 6 * ldh;
+      }
+      glds16(pb + off, smem + buf * STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
     };
 #pragma unroll
     for (int i = 0; i < 6; ++i) stage_piece(t0, 0, i);
@@ -304,7 +312,8 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
 
 // K and V rows of the fused projection -> six bf16 planes per token:
 // kvs[b][s][plane][H*64], plane = 3 * (0 K, 1 V) + piece, s < Skvp (rows
-// past Skv are zeros).  One thread: 8 dims of one (token, tensor, head).
+// past Skv are written as zeros, though the attention never reads them).
+// One thread: 8 dims of one (token, tensor, head).
 __global__ __launch_bounds__(256) void split_kv_kernel(const float* __restrict__ k, const float* __restrict__ v,
                                                        unsigned short* __restrict__ kvs, int S, int Sp, int H,
                                                        int ld_in, long long bs_in, int n8) {
@@ -469,20 +478,12 @@ NOS_API int nos_attn_fwd_f32x6_d64(const float* q, const float* k, const float* 
 }
 
 // The same attention when the K/V planes are already at the start of ws
-// (written by the QKV projection's epilogue, nos_gemm_ln_f32x6_qkv): only the
-// padding rows of every batch are zeroed here.
+// (written by the QKV projection's epilogue, nos_gemm_ln_f32x6_qkv).  The
+// padding rows of the planes are never read (the kernel's tail tile re-reads
+// the last key), so nothing is zeroed: no memset node per call.
 NOS_API int nos_attn_fwd_f32x6_presplit_d64(const float* q, float* o, int B, int H, int Sq, int Skv, int ld_in,
                                             long long bs_in, int ld_out, long long bs_out, float scale, void* ws,
                                             long long ws_bytes, hipStream_t stream) {
   if (int rc = check_args(q, o, ws, ws_bytes, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out)) return rc;
-  const int skvp = (Skv + KVB - 1) / KVB * KVB;
-  if (skvp > Skv) {
-    const size_t row_bytes = (size_t)6 * H * D * 2;
-    for (int b = 0; b < B; ++b) {
-      unsigned char* pad = static_cast<unsigned char*>(ws) + ((size_t)b * skvp + Skv) * row_bytes;
-      const hipError_t e = hipMemsetAsync(pad, 0, (size_t)(skvp - Skv) * row_bytes, stream);
-      if (e != hipSuccess) return (int)e;
-    }
-  }
   return run_from_planes(q, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, scale, ws, stream);
 }

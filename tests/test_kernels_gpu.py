@@ -474,9 +474,9 @@ def test_qkv_projection_writing_the_attention_planes_is_bit_identical(B, S, H, v
 @pytest.mark.parametrize("variant", ["x6n", "x6"])
 def test_attention_planes_padding_rows_never_reach_the_output(variant):
     """Garbage in the planes' padding rows past S of each batch (NaN here)
-    never reaches the output: the presplit entry zeroes those rows before the
-    attention reads the tail tile, so the result stays bit-identical to the
-    unfused path."""
+    never reaches the output: the kernel's tail tile re-reads the last key
+    instead of the padding rows (no memset per call), so the result stays
+    bit-identical to the unfused path."""
     torch.manual_seed(7)
     B, S, H, K = 2, 77, 3, 384
     x = torch.randn(B, S, K, device=DEV)

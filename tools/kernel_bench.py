@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--x6-tile", type=int, default=-1, help="x6 GEMM tile override (3: 128x64 4x1 waves)")
     ap.add_argument("--stage", type=int, default=0, help="x6 GEMM K-stage config (1: BK32 3-deep, 2: BK64)")
     ap.add_argument("--f32-math", default="exact", choices=["exact", "x6"], help="fp32 GEMM math (ops.set_f32_math)")
+    ap.add_argument("--attn-f32", default="x6n,x6", help="fp32 attention variants to time (--dtype fp32)")
     a = ap.parse_args()
     ops.set_f32_math(a.f32_math)
     if a.x6_tile >= 0:
@@ -67,12 +68,19 @@ def main():
     B = a.batch
     res = {}
     if "attn" in a.only:
-        qkv = torch.randn(B, S, 3 * hid, device="cuda", dtype=torch.bfloat16)
-        out = torch.empty(B, S, hid, device="cuda", dtype=torch.bfloat16)
-        us = timeit(lambda: ops.attention_qkv(qkv, H, out=out), a.iters)
+        adt = torch.float32 if a.dtype == "fp32" else torch.bfloat16
+        qkv = torch.randn(B, S, 3 * hid, device="cuda", dtype=adt)
+        out = torch.empty(B, S, hid, device="cuda", dtype=adt)
         fl = B * 4 * S * S * hid
-        res["attn_us"] = us
-        res["attn_tflops"] = fl / us / 1e6
+        variants = a.attn_f32.split(",") if a.dtype == "fp32" else [""]
+        for v in variants:
+            if v:
+                ops.set_attention_f32_variant(v)
+            us = timeit(lambda: ops.attention_qkv(qkv, H, out=out), a.iters)
+            sfx = f"_{v}" if v else ""
+            res[f"attn{sfx}_us"] = us
+            res[f"attn{sfx}_tflops"] = fl / us / 1e6
+        ops.set_attention_f32_variant("auto")
     if "torch" in a.only:
         qkv = torch.randn(B, S, 3, H, 64, device="cuda", dtype=torch.bfloat16)
         q, k, v = (t.transpose(1, 2).contiguous() for t in qkv.unbind(2))
