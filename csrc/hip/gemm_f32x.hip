@@ -94,8 +94,9 @@ __device__ __forceinline__ unsigned short bf16_bits(float x) {
   return __builtin_bit_cast(unsigned short, (__bf16)x);
 }
 
-// WGM x WGN waves per workgroup (4 or 8); NT threads
-template <bool LN, int BM, int BN, bool PERSIST, int RS, int BK, int WGM = 2, int WGN = 2>
+// WGM x WGN waves per workgroup (4 or 8); NT threads.  PIPE: software-
+// pipelined K loop (2-deep ring only, see below)
+template <bool LN, int BM, int BN, bool PERSIST, int RS, int BK, int WGM = 2, int WGN = 2, bool PIPE = false>
 __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_f32x6_kernel(
     const float* __restrict__ A, int lda, const unsigned short* __restrict__ Wp, int ldw, long long wplane,
     const float* __restrict__ bias, const float* __restrict__ c1, const float* __restrict__ c2,
@@ -178,6 +179,144 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_f3
   for (int q = 0; q < S; ++q)
     if (q < nk) stage(q * BK, smem + q * STAGE);
 
+  // LayerNorm statistics of this thread's share of one stage's A rows
+  auto ln_stats = [&](const unsigned char* ta, int kt) {
+    if constexpr (LN) {
+#pragma unroll
+      for (int q = 0; q < FPT / 4; ++q) {
+        const int lc = spart * (FPT / 4) + q;
+        const float4 v = *reinterpret_cast<const float4*>(ta + srow * AROW + ((lc ^ L::aswz(srow)) << 4));
+        if (kt == 0 && q == 0) sshift = v.x;
+        const float d0 = v.x - sshift, d1 = v.y - sshift, d2 = v.z - sshift, d3 = v.w - sshift;
+        ssum += (d0 + d1) + (d2 + d3);
+        ssq = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, ssq))));
+      }
+    }
+  };
+
+  if constexpr (PIPE) {
+    // Software-pipelined K loop.  The fragments of MFMA step s+1 (the fp32 A
+    // rows and the three W planes) are read from LDS, and A is split into
+    // its three bf16 pieces, WHILE the 6*MI*NI MFMAs of step s run: the
+    // reads and the ~46 VALU ops of a split fill the MFMAs' issue gaps
+    // (an MFMA holds the wave's vector issue for 8 of its 32 cycles) instead
+    // of a split phase with no MFMA and LDS waits right before each MFMA.
+    // The stage boundary sits before the LAST step's MFMAs: every wave has
+    // read that step (lgkmcnt(0)), so the barrier frees the buffer for the
+    // DMA of stage kt+2 and publishes stage kt+1, whose first step is then
+    // read and split under the last step's MFMAs.  The accumulation order is
+    // the unpipelined loop's: results are bit-identical.
+    static_assert(RS == 2 && BK == 32, "the pipelined K loop runs a 2-deep ring of 2-step stages");
+    struct Raw {
+      float4 x0[MI], x1[MI];
+      bf16x8_t w[NI][3];
+    };
+    auto load_raw = [&](const unsigned char* base, int s, Raw& r) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wm * (BM / WGM) + i * 32 + c;
+        r.x0[i] = *reinterpret_cast<const float4*>(base + row * AROW + (((4 * s + 2 * h) ^ L::aswz(row)) << 4));
+        r.x1[i] = *reinterpret_cast<const float4*>(base + row * AROW + (((4 * s + 2 * h + 1) ^ L::aswz(row)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int row = wn * (BN / WGN) + j * 32 + c;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          r.w[j][p] = *reinterpret_cast<const bf16x8_t*>(base + TA + p * TWP + row * WROW +
+                                                          (((2 * s + h) ^ L::wswz(row)) << 4));
+      }
+    };
+    auto split_raw = [&](const Raw& r, bf16x8_t (&af)[MI][3]) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const float x[8] = {r.x0[i].x, r.x0[i].y, r.x0[i].z, r.x0[i].w, r.x1[i].x, r.x1[i].y, r.x1[i].z, r.x1[i].w};
+        nos::split8(x, af[i][0], af[i][1], af[i][2]);
+      }
+    };
+    // one quarter of a split8: elements 2k, 2k+1 of row block i
+    auto split_unit = [&](const Raw& r, bf16x8_t (&af)[MI][3], int i, int k) {
+      const float4 v = k < 2 ? r.x0[i] : r.x1[i];
+      const f32x2_t x = (k & 1) ? f32x2_t{v.z, v.w} : f32x2_t{v.x, v.y};
+      bf16x2_t a, b, cc;
+      nos::split2(x, a, b, cc);
+      af[i][0][2 * k] = a.x; af[i][0][2 * k + 1] = a.y;
+      af[i][1][2 * k] = b.x; af[i][1][2 * k + 1] = b.y;
+      af[i][2][2 * k] = cc.x; af[i][2][2 * k + 1] = cc.y;
+      // pin the pieces here: without it LLVM sinks the split into the next
+      // block (past the stage barrier), where its only users are
+      asm volatile("" : "+v"(af[i][0]), "+v"(af[i][1]), "+v"(af[i][2]));
+    };
+    // One MFMA step (6*MI*NI MFMAs on af/r) with the NEXT step's fragments
+    // read from `nb` (step ns) and split underneath, in MI*NI chunks fenced by
+    // sched_barrier: chunk q = the six MFMAs of block q, plus (chunk 0) the A
+    // reads, (every MI-th chunk) one W block's three plane reads, and from
+    // chunk 1 on a quarter of a row block's split -- the split's A reads
+    // land during chunk 0's MFMAs, the W reads are used one step later.
+    auto step = [&](const bf16x8_t (&af)[MI][3], const Raw& r, const unsigned char* nb, int ns, Raw& rn,
+                    bf16x8_t (&afn)[MI][3], bool stats, int skt) {
+      constexpr int NB = MI * NI, NSP = 4 * MI;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int bi = q / NI, bj = q % NI;
+        acc[bi][bj] = nos::mma6(af[bi], r.w[bj], acc[bi][bj]);
+        if (q == 0) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const int row = wm * (BM / WGM) + i * 32 + c;
+            rn.x0[i] = *reinterpret_cast<const float4*>(nb + row * AROW + (((4 * ns + 2 * h) ^ L::aswz(row)) << 4));
+            rn.x1[i] =
+                *reinterpret_cast<const float4*>(nb + row * AROW + (((4 * ns + 2 * h + 1) ^ L::aswz(row)) << 4));
+          }
+        }
+        if (q % MI == 0) {
+          const int j = q / MI;
+          const int row = wn * (BN / WGN) + j * 32 + c;
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            rn.w[j][p] = *reinterpret_cast<const bf16x8_t*>(nb + TA + p * TWP + row * WROW +
+                                                             (((2 * ns + h) ^ L::wswz(row)) << 4));
+        }
+#pragma unroll
+        for (int u = 0; u < NSP; ++u)
+          if (NB > 1 && 1 + u * (NB - 1) / NSP == q) split_unit(rn, afn, u / 4, u % 4);
+        if (stats && q == NB - 1) ln_stats(nb, skt);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (NB == 1) {
+#pragma unroll
+        for (int u = 0; u < NSP; ++u) split_unit(rn, afn, u / 4, u % 4);
+      }
+    };
+
+    wait_stages<LPS>(nk > 1 ? 1 : 0);  // stage 0 landed (stage 1 may stay in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // two fragment sets in ping-pong (A: step 0 of a stage, B: step 1), so
+    // nothing is copied between registers across the loop
+    Raw ra, rb;
+    bf16x8_t afa[MI][3], afb[MI][3];
+    load_raw(smem, 0, ra);
+    ln_stats(smem, 0);
+    split_raw(ra, afa);
+    for (int kt = 0; kt + 1 < nk; ++kt) {
+      const unsigned char* base = smem + (kt & 1) * STAGE;
+      step(afa, ra, base, 1, rb, afb, false, 0);  // step 1 of stage kt read under step 0's MFMAs
+      // stage boundary: stage kt+1 landed (the only DMA in flight), every
+      // wave has read all of stage kt (step 1 is in rb)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < nk) stage((kt + 2) * BK, smem + (kt & 1) * STAGE);
+      // step 0 of stage kt+1 (and its LayerNorm statistics) under step 1's MFMAs
+      step(afb, rb, smem + ((kt + 1) & 1) * STAGE, 0, ra, afa, true, kt + 1);
+    }
+    step(afa, ra, smem + ((nk - 1) & 1) * STAGE, 1, rb, afb, false, 0);  // the last stage
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] = nos::mma6(afb[i], rb.w[j], acc[i][j]);
+  } else {
   for (int kt = 0; kt < nk; ++kt) {
     // slice kt landed (the newer slices issued so far stay in flight: S-1 of
     // them after the prologue, S-2 later) and every wave is done with slice
@@ -190,17 +329,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_f3
     const unsigned char* cur = smem + slot * STAGE;
     const unsigned char* ta = cur;
     const unsigned char* tw = cur + TA;
-    if constexpr (LN) {
-#pragma unroll
-      for (int q = 0; q < FPT / 4; ++q) {
-        const int lc = spart * (FPT / 4) + q;
-        const float4 v = *reinterpret_cast<const float4*>(ta + srow * AROW + ((lc ^ L::aswz(srow)) << 4));
-        if (kt == 0 && q == 0) sshift = v.x;
-        const float d0 = v.x - sshift, d1 = v.y - sshift, d2 = v.z - sshift, d3 = v.w - sshift;
-        ssum += (d0 + d1) + (d2 + d3);
-        ssq = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, ssq))));
-      }
-    }
+    ln_stats(ta, kt);
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {  // 16-deep MFMA steps: lane holds k = 16s + 8h .. +7
       bf16x8_t af[MI][3], wf[NI][3];
@@ -227,6 +356,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_f3
         for (int j = 0; j < NI; ++j) acc[i][j] = nos::mma6(af[i], wf[j], acc[i][j]);
     }
   }
+  }  // !PIPE
   __syncthreads();  // every wave is done with the ring (the next tile's prologue, the LN statistics)
 
   if constexpr (LN) {
@@ -289,8 +419,27 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_f3
   }  // tiles
 }
 
+int g_pipe = 1;  // software-pipelined K loop on 2-deep rings (nos_gemm_f32x6_set_pipeline)
+
+template <bool LN, int BM, int BN, int RS, int BK, int WGM, int WGN, bool PIPE>
+int launch_p(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
+             const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K,
+             int epi, float eps, hipStream_t st, KvOut kv);
+
 template <bool LN, int BM, int BN, int RS, int BK, int WGM = 2, int WGN = 2>
 int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
+             const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K,
+             int epi, float eps, hipStream_t st, KvOut kv) {
+  if constexpr (RS == 2 && BK == 32) {
+    if (g_pipe) return launch_p<LN, BM, BN, RS, BK, WGM, WGN, true>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr,
+                                                                    C, ldc, M, N, K, epi, eps, st, kv);
+  }
+  return launch_p<LN, BM, BN, RS, BK, WGM, WGN, false>(A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N,
+                                                       K, epi, eps, st, kv);
+}
+
+template <bool LN, int BM, int BN, int RS, int BK, int WGM, int WGN, bool PIPE>
+int launch_p(const float* A, int lda, const unsigned short* Wp, int ldw, long long wplane, const float* bias,
              const float* c1, const float* c2, const float* R, int ldr, float* C, int ldc, int M, int N, int K,
              int epi, float eps, hipStream_t st, KvOut kv) {
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
@@ -299,13 +448,16 @@ int launch_t(const float* A, int lda, const unsigned short* Wp, int ldw, long lo
   const size_t ring = RS * (size_t)(BM * Lay<BK>::AROW + 3 * BN * Lay<BK>::WROW);
   const size_t lds = ring > 2 * BM * sizeof(float) ? ring : 2 * BM * sizeof(float);
   constexpr int NT = 64 * WGM * WGN;
-  const int grid = nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM, WGN>, NT, lds, ntiles);
+  const int grid =
+      nos_grid_for((const void*)gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM, WGN, PIPE>, NT, lds, ntiles);
   if (grid < ntiles)
-    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM, WGN>), dim3((unsigned)grid), dim3(NT), lds, st, A,
-                       lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n, kv);
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, true, RS, BK, WGM, WGN, PIPE>), dim3((unsigned)grid), dim3(NT),
+                       lds, st, A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m,
+                       tiles_n, kv);
   else
-    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false, RS, BK, WGM, WGN>), dim3((unsigned)ntiles), dim3(NT), lds, st, A,
-                       lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps, tiles_m, tiles_n, kv);
+    hipLaunchKernelGGL((gemm_f32x6_kernel<LN, BM, BN, false, RS, BK, WGM, WGN, PIPE>), dim3((unsigned)ntiles),
+                       dim3(NT), lds, st, A, lda, Wp, ldw, wplane, bias, c1, c2, R, ldr, C, ldc, M, N, K, epi, eps,
+                       tiles_m, tiles_n, kv);
   return (int)hipGetLastError();
 }
 
@@ -373,6 +525,14 @@ int launch(const float* A, int lda, const unsigned short* Wp, int ldw, long long
 NOS_API int nos_gemm_f32x6_set_tile(int tile) {
   if (tile < -1 || tile > 7) return (int)hipErrorInvalidValue;
   g_tile = tile;
+  return 0;
+}
+
+// 1 (default): software-pipelined K loop on the 2-deep-ring configs; 0: the
+// unpipelined loop (A/B; the results are bit-identical)
+NOS_API int nos_gemm_f32x6_set_pipeline(int on) {
+  if (on < 0 || on > 1) return (int)hipErrorInvalidValue;
+  g_pipe = on;
   return 0;
 }
 

@@ -181,6 +181,13 @@ def set_gemm_f32x6_tile(tile: str) -> None:
     _lib.check(_lib.lib().nos_gemm_f32x6_set_tile(code), "nos_gemm_f32x6_set_tile")
 
 
+def set_gemm_f32x6_pipeline(on: bool) -> None:
+    """x6 GEMM K loop: software-pipelined (default: the next MFMA step's
+    fragments are read and split under the current step's MFMAs) or the
+    plain loop (A/B; bit-identical results)."""
+    _lib.check(_lib.lib().nos_gemm_f32x6_set_pipeline(int(bool(on))), "nos_gemm_f32x6_set_pipeline")
+
+
 def split_bf16x3(t: torch.Tensor) -> torch.Tensor:
     """fp32 tensor -> [3, *t.shape] bf16 pieces with t == p0 + p1 + p2 exactly."""
     t = t.float()
@@ -497,5 +504,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_f32_math", "f32_math", "set_gemm_f32x6_tile", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_f32_math", "f32_math", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

@@ -49,6 +49,7 @@ _SIGS = {
     "nos_gemm_f32_pick_tile": [c_int, c_int],
     "nos_gemm_f32x6_set_stage": [c_int],
     "nos_gemm_f32x6_set_tile": [c_int],
+    "nos_gemm_f32x6_set_pipeline": [c_int],
     "nos_gemm_set_policy": [c_int],
     "nos_gemm_set_persistent": [c_int],
     "nos_gemm_f32_set_policy": [c_int],

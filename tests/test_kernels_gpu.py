@@ -198,6 +198,52 @@ def test_linear_fp32_split_is_as_accurate_as_exact_f32(M, N, K):
     assert errs["x6"][0] <= 1.5 * errs["exact"][0] and errs["x6"][1] <= 1.5 * errs["exact"][1], errs
 
 
+@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3, 5, 7])
+@pytest.mark.parametrize("M,N,K,kind", [(3401, 1152, 384, "ln"), (3401, 384, 1536, "resid"), (257, 200, 96, "gelu"),
+                                        (100, 92, 64, "ln"), (3401, 1152, 384, "qkv"), (64, 64, 32, "plain")])
+def test_linear_fp32_x6_pipelined_loop_is_bit_identical(tile, M, N, K, kind):
+    """The software-pipelined x6 K loop (next step's LDS reads and A split
+    under the current step's MFMAs) accumulates in the plain loop's order:
+    every tile config, epilogue and K (one stage, two, many) bit for bit."""
+    from nos_amd.ops import _lib
+
+    torch.manual_seed(M + N + K)
+    x = torch.randn(1, M, K, device=DEV) * 2 + 0.5
+    w = torch.randn(N, K, device=DEV) * 0.05
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(1, M, N, device=DEV)
+    g, be = torch.randn(K, device=DEV), torch.randn(K, device=DEV)
+    wg, c1, c2 = ops.fold_layernorm(w, b, g, be)
+
+    def run():
+        if kind == "ln":
+            return (ops.linear_ln(x, wg, c1, c2, act="gelu"),)
+        if kind == "qkv":
+            H = N // 192
+            qkv, ws = ops.linear_ln_qkv_x6(x, wg, c1, c2, H)
+            return (qkv[..., :N // 3].clone(), ws[:M * 6 * (N // 3)].clone())  # the planes' S rows (no padding)
+        if kind == "resid":
+            return (ops.linear(x, w, b, residual=r),)
+        return (ops.linear(x, w, b, act="gelu" if kind == "gelu" else None),)
+
+    ops.set_f32_math("x6")
+    ops.set_attention_f32_variant("x6n")
+    _lib.check(_lib.lib().nos_gemm_f32x6_set_tile(tile), "set_tile")
+    try:
+        ops.set_gemm_f32x6_pipeline(False)
+        ref = run()
+        ops.set_gemm_f32x6_pipeline(True)
+        got = run()
+        torch.cuda.synchronize()
+    finally:
+        ops.set_gemm_f32x6_pipeline(True)
+        _lib.check(_lib.lib().nos_gemm_f32x6_set_tile(-1), "set_tile")
+        ops.set_f32_math("exact")
+        ops.set_attention_f32_variant("auto")
+    for a, c in zip(ref, got):
+        assert torch.equal(a, c)
+
+
 @pytest.mark.parametrize("stage,tile", [(1, -1), (2, -1), (0, 3), (0, 5), (0, 7)])
 @pytest.mark.parametrize("M,N,K,ln", [(3401, 1152, 384, True), (3401, 384, 1536, False), (257, 200, 96, False),
                                       (100, 92, 384, True)])

@@ -57,8 +57,10 @@ def main():
     ap.add_argument("--stage", type=int, default=0, help="x6 GEMM K-stage config (1: BK32 3-deep, 2: BK64)")
     ap.add_argument("--f32-math", default="exact", choices=["exact", "x6"], help="fp32 GEMM math (ops.set_f32_math)")
     ap.add_argument("--attn-f32", default="x6n,x6", help="fp32 attention variants to time (--dtype fp32)")
+    ap.add_argument("--pipeline", type=int, default=1, help="x6 GEMM software-pipelined K loop (1) or plain (0)")
     a = ap.parse_args()
     ops.set_f32_math(a.f32_math)
+    ops.set_gemm_f32x6_pipeline(bool(a.pipeline))
     if a.x6_tile >= 0:
         ops._lib.check(ops._lib.lib().nos_gemm_f32x6_set_tile(a.x6_tile), "nos_gemm_f32x6_set_tile")
     if a.stage:
