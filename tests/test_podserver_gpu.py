@@ -201,3 +201,37 @@ def test_a_lone_tenant_replays_its_solo_graph_with_the_same_results(server):
         r = r.float().cpu().numpy()
         assert np.abs(o - r).max() <= 1e-4 * (np.abs(r).max() + 1e-6)
     c.close()
+
+
+def test_both_graphs_follow_every_new_input(server):
+    """Each replay of a tenant's co-tenancy and solo graphs computes on the
+    input just written, bit-identical to the eager program under the same
+    configs, input after input (regression: a memset node in the captured
+    graph made replays return an earlier input's outputs,
+    profiles/r04_graph_memset_staleness.json)."""
+    from nos_amd.podserver import program as PG
+
+    prog = _yolos(6)
+    t = server._build(99, {"pod": "g"}, PG.parse(*prog, gpu=True), 10.0, None)
+    try:
+        rng = np.random.default_rng(9)
+        s = server._lanes[0]
+        for _ in range(3):
+            x = torch.from_numpy(rng.standard_normal(tuple(t.x.shape)).astype(np.float32))
+            for graph, outs, cfg in ((t.graph, t.outputs, server.kernel_config),
+                                     (t.solo_graph, t.solo_outputs, server.solo_config)):
+                with torch.no_grad(), torch.cuda.stream(s):
+                    t.x.copy_(x.view(t.x.shape).to(t.x.dtype))  # the server's _run: copy, then replay
+                    graph.replay()
+                s.synchronize()
+                server._apply_config(cfg)
+                try:
+                    with torch.no_grad():
+                        ref = t.model(t.x)
+                    torch.cuda.synchronize()
+                finally:
+                    server._apply_config(server.kernel_config)
+                for o, r in zip(outs, ref):
+                    assert torch.equal(o, r)
+    finally:
+        server._free(t)
