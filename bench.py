@@ -676,8 +676,10 @@ def main(argv=None) -> int:
                                   f"{world} GPU(s)",
                    "pods_per_gpu": args.pods_per_gpu, "slice_gb": args.slice_gb, "mode": args.mode,
                    "pod_execution": ("one CPU-only client process per pod with its device-plugin env (pod-server "
-                                     "socket + slice), its inferences run as HIP-graph replays in the GPU's pod "
-                                     f"server process ({args.server_lanes} lanes; the MPS architecture)")
+                                     "socket + allocation token); the pod ships its model as a program (op graph + "
+                                     "weights, nos_amd/podserver/program.py) and its inferences run as HIP-graph "
+                                     f"replays in the GPU's pod server process ({args.server_lanes} lanes; the MPS "
+                                     "architecture)")
                    if server_mode else "one GPU process per pod with its device-plugin env",
                    "graphs": not args.no_graphs,
                    "collective_tenant": use_coll, "step_s": args.step_s, "bursty": args.bursty or None,
