@@ -26,19 +26,21 @@ def main() -> None:
     ap.add_argument("--window", type=float, default=8.0)
     ap.add_argument("--warmup", type=float, default=2.0)
     ap.add_argument("--slice-gb", type=float, default=10.0)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args()
     # one hardware queue per lane: before anything initialises HIP (cmd/podserver.py)
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(a.lanes, 32))
+    from nos_amd.models.yolos_program import demo_tenant
     from nos_amd.podserver.client import PodClient
     from nos_amd.podserver.server import PodServer
 
-    path = Path(tempfile.mkdtemp(prefix="nos_ps_", dir="/tmp")) / "gpu-0.sock"
+    path = Path(tempfile.mkdtemp(prefix="nos_ps_", dir="/tmp")) / "gpu-0" / "server.sock"
     srv = PodServer(path, device="cuda", lanes=a.lanes, max_tenants=max(48, a.tenants)).start()
     try:
         t0 = time.monotonic()
         clients = [PodClient(path, connect_timeout_s=30) for _ in range(a.tenants)]
         for i, c in enumerate(clients):
-            c.register(f"pod-{i}", seed=i, memory_limit_gb=a.slice_gb)
+            c.register(f"pod-{i}", *demo_tenant(a.dtype, i), memory_limit_gb=a.slice_gb)
         build_s = time.monotonic() - t0
         stop = threading.Event()
         marks: list[list[float]] = [[] for _ in clients]
