@@ -227,7 +227,13 @@ class QuotaScenario:
             self.cl.settle(timeout_s, until=until)
             return until()
         w0, s0 = time.monotonic(), self.cl.clock.now()
+        last = w0
         while True:
+            if time.monotonic() - last > 10:  # progress for long live phases
+                last = time.monotonic()
+                print(f"[quota] {last - w0:.0f} s: {len(self.runtime.ready())} tenants ready, "
+                      f"{len(self.runtime.running())} running, {len(self.cl.pending_pods())} pods pending",
+                      file=sys.stderr, flush=True)
             self.cl.settle(tick_s, until=until)
             target = s0 + (time.monotonic() - w0)
             if self.cl.clock.now() < target:

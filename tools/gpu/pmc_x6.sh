@@ -7,12 +7,12 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 i=0
 for CNT in "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" \
-           "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE" \
-           "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
+           "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_WAVES" \
+           "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $CNT --kernel-trace --output-format csv -d $OUT/pass$i -o run -- python3 $R/tools/x6_pmc_once.py > $OUT/pass$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/pass$i.log; exit 1; }
 done
-python3 $R/tools/pmc_summary.py $OUT --out $OUT/summary.json && python3 - $OUT/summary.json <<'PY'
+python3 $R/tools/pmc_summary.py $OUT --out $OUT/summary.json && rm -rf $OUT/pass1 $OUT/pass2 $OUT/pass3 && python3 - $OUT/summary.json <<'PY'
 import json,sys
 d=json.load(open(sys.argv[1]))
 for k,v in d.items():

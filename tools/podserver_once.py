@@ -27,6 +27,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=float, default=2.0)
     ap.add_argument("--slice-gb", type=float, default=10.0)
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--pipeline", type=int, default=1, help="x6 GEMM software-pipelined K loop (1) or plain (0)")
     a = ap.parse_args()
     # one hardware queue per lane: before anything initialises HIP (cmd/podserver.py)
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(a.lanes, 32))
@@ -36,6 +37,9 @@ def main() -> None:
 
     path = Path(tempfile.mkdtemp(prefix="nos_ps_", dir="/tmp")) / "gpu-0" / "server.sock"
     srv = PodServer(path, device="cuda", lanes=a.lanes, max_tenants=max(48, a.tenants)).start()
+    from nos_amd import ops
+
+    ops.set_gemm_f32x6_pipeline(bool(a.pipeline))  # process-wide: every capture below
     try:
         t0 = time.monotonic()
         clients = [PodClient(path, connect_timeout_s=30) for _ in range(a.tenants)]
@@ -55,8 +59,18 @@ def main() -> None:
             t.start()
         time.sleep(a.warmup)
         w0 = time.monotonic()
-        time.sleep(a.window)
+        clocks = []
+        try:
+            from nos_amd.gpu.amdsmi import AmdSmi
+
+            smi = AmdSmi.real()
+            while time.monotonic() - w0 < a.window:
+                clocks.append(smi.clock(0)["sclk_mhz"])
+                time.sleep(0.1)
+        except Exception:  # no amd-smi: just wait
+            time.sleep(max(0.0, a.window - (time.monotonic() - w0)))
         w1 = time.monotonic()
+        sclk = round(sum(clocks) / len(clocks)) if clocks else None
         stop.set()
         for t in th:
             t.join(timeout=30)
@@ -67,7 +81,8 @@ def main() -> None:
         print(json.dumps({"tenants": a.tenants, "lanes": a.lanes, "window_s": round(w1 - w0, 3),
                           "build_s": round(build_s, 1), "inf_per_s": round(sum(done) / (w1 - w0), 2),
                           "min_done": min(done), "max_done": max(done), "solo_replays": solo,
-                          "kernel_config": srv.kernel_config}), flush=True)
+                          "kernel_config": srv.kernel_config, "pipeline": a.pipeline,
+                          "sclk_mhz": sclk}), flush=True)
     finally:
         srv.stop()
 
