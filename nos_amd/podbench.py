@@ -138,15 +138,19 @@ class PodLauncher:
     never touches the GPU).  Line-delimited JSON over pipes."""
 
     def __init__(self):
+        import threading
+
+        self._lock = threading.Lock()  # one request/reply in flight: callers may be several threads
         self.p = subprocess.Popen([sys.executable, "-u", "-m", "nos_amd.podbench", "--launcher"],
                                   stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, cwd=str(REPO),
                                   env={**os.environ, "PYTHONPATH": str(REPO) + os.pathsep +
                                        os.environ.get("PYTHONPATH", "")})
 
     def _call(self, msg: dict) -> dict:
-        self.p.stdin.write(json.dumps(msg) + "\n")
-        self.p.stdin.flush()
-        line = self.p.stdout.readline()
+        with self._lock:
+            self.p.stdin.write(json.dumps(msg) + "\n")
+            self.p.stdin.flush()
+            line = self.p.stdout.readline()
         if not line:
             raise RuntimeError("pod launcher died")
         r = json.loads(line)

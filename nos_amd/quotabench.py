@@ -298,6 +298,14 @@ class QuotaScenario:
                          and self.runtime.tenants[k].t_ready is not None)
         # the k-th victim's stop frees the slice the k-th preempting pod runs on
         lat = [r - s for s, r in zip(stops, b_ready[len(b_ready) - len(stops):])] if stops else []
+        # split: victim stop -> preemptor's container start (control plane:
+        # scheduling retry, bind, device release and allocation), then
+        # container start -> first inference (pod start-up, program
+        # registration, first replay)
+        pre = sorted((self.runtime.tenants[k] for k in b if k in self.runtime.tenants), key=lambda t: t.t_start)
+        late = pre[len(pre) - len(stops):] if stops else []
+        cp = [t.t_start - s for s, t in zip(stops, late)]
+        up = [t.t_ready - t.t_start for t in late if t.t_ready is not None]
         res["phase_b"] = {"ok": ok, "seconds": round(t2 - t1, 2), "preemptions":
                           self.cl.scheduler.stats.get("preemptions", 0) - p0, "victims": len(stops),
                           # CapacityScheduling may only take back borrowed quota
@@ -306,6 +314,8 @@ class QuotaScenario:
                           "preemption_to_running_s": {"n": len(lat),
                                                       "p50": round(sorted(lat)[len(lat) // 2], 3) if lat else None,
                                                       "max": round(max(lat), 3) if lat else None},
+                          "victim_stop_to_preemptor_start_s": _stats(cp),
+                          "preemptor_start_to_first_inference_s": _stats(up),
                           "submit_to_all_running_s": round((b_ready[-1] - t1) if b_ready else -1, 3),
                           **self.snapshot()}
         if sampler is not None:
@@ -318,6 +328,11 @@ class QuotaScenario:
             if any(v is None for v in self.labels(ns).values()):
                 return False
         return True
+
+
+def _stats(v: list[float]) -> dict:
+    v = sorted(v)
+    return {"n": len(v), "p50": round(v[len(v) // 2], 3) if v else None, "max": round(v[-1], 3) if v else None}
 
 
 def scenario_for(slices_per_gpu: int, slice_gb: int = 10, **kw) -> QuotaScenario:
