@@ -241,7 +241,8 @@ def test_both_graphs_follow_every_new_input(server):
 def test_a_torch_transformer_encoder_tenant(server, dtype):
     """A third architecture: a tenant's own ``nn.TransformerEncoder``
     (pre-LN, GELU) shipped as a program, against the same module run by
-    PyTorch on the GPU in fp32."""
+    PyTorch in fp32 on the CPU (on the GPU, PyTorch's fused encoder fast path
+    is itself only ~1e-4 accurate)."""
     from nos_amd.models.encoder_program import encoder_program, random_encoder_weights
     from nos_amd.podserver.client import PodClient
 
@@ -251,15 +252,14 @@ def test_a_torch_transformer_encoder_tenant(server, dtype):
                                              norm_first=True)
     enc = torch.nn.TransformerEncoder(layer, L, norm=torch.nn.LayerNorm(hid), enable_nested_tensor=False)
     enc.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()})
-    enc = enc.cuda().eval()
+    enc = enc.eval()
     c = PodClient(server.path, connect_timeout_s=10)
     rep = c.register("enc", *encoder_program(w, L, heads, (2, S, hid), dtype), memory_limit_gb=2)
     assert rep["compile"]["qkv_attention_fused"] == L
     x = np.random.default_rng(5).standard_normal(rep["input_shape"]).astype(np.float32)
     out, _ = c.infer(x, outputs=True)
-    torch.backends.cuda.matmul.allow_tf32 = False
     with torch.no_grad():
-        ref = enc(torch.from_numpy(x).cuda()).cpu().numpy()
+        ref = enc(torch.from_numpy(x)).numpy()
     err = np.abs(out[0] - ref).max() / np.abs(ref).max()
     assert err < (1e-4 if dtype == "fp32" else 3e-2), err
     c.close()
