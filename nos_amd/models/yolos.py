@@ -284,17 +284,33 @@ class GraphedTenant:
     graph: torch.cuda.CUDAGraph | None = None
     outputs: tuple = field(default_factory=tuple)
 
-    def capture(self, warmup: int = 2, capture_error_mode: str = "global", pool=None) -> None:
+    def capture(self, warmup: int = 2, capture_error_mode: str = "global", pool=None, light: bool = False) -> None:
         """``capture_error_mode="thread_local"`` when other threads keep
         launching while this one captures (the pod server's lanes); ``pool``
-        shares another graph's memory pool (graphs never replayed at once)."""
+        shares another graph's memory pool (graphs never replayed at once).
+        ``light``: capture on this stream only, without the device-wide
+        synchronize, ``gc.collect()`` and ``empty_cache()`` that
+        ``torch.cuda.graph`` runs first -- in the pod server those waited for
+        every lane's in-flight replays and walked the whole Python heap per
+        capture (the warm-ups are synchronised on this stream instead)."""
         with torch.cuda.stream(self.stream):
             for _ in range(warmup):
                 self.outputs = self.model(self.pixel_values)
         self.stream.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=pool, stream=self.stream, capture_error_mode=capture_error_mode):
-            self.outputs = self.model(self.pixel_values)
+        if light:
+            with torch.cuda.stream(self.stream):
+                if pool is None:
+                    self.graph.capture_begin(capture_error_mode=capture_error_mode)
+                else:
+                    self.graph.capture_begin(pool, capture_error_mode=capture_error_mode)
+                try:
+                    self.outputs = self.model(self.pixel_values)
+                finally:
+                    self.graph.capture_end()
+        else:
+            with torch.cuda.graph(self.graph, pool=pool, stream=self.stream, capture_error_mode=capture_error_mode):
+                self.outputs = self.model(self.pixel_values)
         self.stream.synchronize()
 
     def launch(self) -> None:

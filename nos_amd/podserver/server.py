@@ -429,11 +429,14 @@ class PodServer:
         base = torch.cuda.memory_allocated()
         torch.cuda.reset_peak_memory_stats()
         stream = None
+        t0 = time.monotonic()
+        times = {}
         try:
             with torch.no_grad(), torch.cuda.stream(self._setup_stream):
                 m = prog.compile("cuda")
                 x = prog.input_tensor("cuda")
             self._setup_stream.synchronize()
+            times["compile_ms"] = round(1e3 * (time.monotonic() - t0), 1)
             budget_cfg = None
             if mask:
                 from ..bench_support import cus_from_hex
@@ -455,7 +458,7 @@ class PodServer:
                         self._apply_config(budget_cfg[0])
                         set_cu_budget(budget_cfg[1])
                     if self.graphs:  # the lanes keep replaying other tenants meanwhile
-                        gt.capture(capture_error_mode="thread_local")
+                        gt.capture(warmup=1, capture_error_mode="thread_local", light=True)
                     else:
                         gt.launch()
                         gt.stream.synchronize()
@@ -470,10 +473,12 @@ class PodServer:
                     solo = GraphedTenant(m, self._setup_stream, x)
                     try:
                         self._apply_config(self.solo_config)
-                        solo.capture(capture_error_mode="thread_local", pool=gt.graph.pool())
+                        # one warm-up: the first capture's already ran every kernel
+                        solo.capture(warmup=1, capture_error_mode="thread_local", pool=gt.graph.pool(), light=True)
                     finally:
                         self._apply_config(self.kernel_config)
             peak = (torch.cuda.max_memory_allocated() - base) / 2 ** 30
+            times["build_ms"] = round(1e3 * (time.monotonic() - t0), 1)
         except Exception:
             if stream is not None:
                 stream.close()
@@ -482,7 +487,7 @@ class PodServer:
         t = Tenant(tid, pod, limit, dtype, m, x, stream=stream, graph=gt.graph,
                    outputs=gt.outputs, footprint_gb=round(peak, 3), cu_mask=mask,
                    solo_graph=solo.graph if solo else None, solo_outputs=solo.outputs if solo else (),
-                   program=prog.name, compile_stats=dict(m.stats))
+                   program=prog.name, compile_stats={**m.stats, **times})
         if limit and peak > limit:
             self._free(t)
             raise AdmissionError(f"tenant needs {peak:.2f} GB, its slice has {limit} GB")

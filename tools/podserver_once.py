@@ -43,9 +43,11 @@ def main() -> None:
     try:
         t0 = time.monotonic()
         clients = [PodClient(path, connect_timeout_s=30) for _ in range(a.tenants)]
-        for i, c in enumerate(clients):
-            c.register(f"pod-{i}", *demo_tenant(a.dtype, i), memory_limit_gb=a.slice_gb)
-        build_s = time.monotonic() - t0
+        progs = [demo_tenant(a.dtype, i) for i in range(a.tenants)]
+        t_built = time.monotonic()
+        reps = [c.register(f"pod-{i}", *progs[i], memory_limit_gb=a.slice_gb) for i, c in enumerate(clients)]
+        build_s = time.monotonic() - t_built
+        srv_build_ms = sorted(r["compile"].get("build_ms", 0) for r in reps)
         stop = threading.Event()
         marks: list[list[float]] = [[] for _ in clients]
 
@@ -79,7 +81,10 @@ def main() -> None:
         for c in clients:
             c.close()
         print(json.dumps({"tenants": a.tenants, "lanes": a.lanes, "window_s": round(w1 - w0, 3),
-                          "build_s": round(build_s, 1), "inf_per_s": round(sum(done) / (w1 - w0), 2),
+                          "build_s": round(build_s, 1), "programs_s": round(t_built - t0, 1),
+                          "server_build_ms_p50": srv_build_ms[len(srv_build_ms) // 2],
+                          "server_compile_ms_p50": sorted(r["compile"].get("compile_ms", 0) for r in reps)[len(reps) // 2],
+                          "inf_per_s": round(sum(done) / (w1 - w0), 2),
                           "min_done": min(done), "max_done": max(done), "solo_replays": solo,
                           "kernel_config": srv.kernel_config, "pipeline": a.pipeline,
                           "sclk_mhz": sclk}), flush=True)
