@@ -296,26 +296,35 @@ class QuotaScenario:
         stops = sorted(t for kind, k, t in self.events if kind == "stop" and t >= t1)
         b_ready = sorted(self.runtime.tenants[k].t_ready for k in b if k in self.runtime.tenants
                          and self.runtime.tenants[k].t_ready is not None)
-        # the k-th victim's stop frees the slice the k-th preempting pod runs on
-        lat = [r - s for s, r in zip(stops, b_ready[len(b_ready) - len(stops):])] if stops else []
-        # split: victim stop -> preemptor's container start (control plane:
-        # scheduling retry, bind, device release and allocation), then
-        # container start -> first inference (pod start-up, program
-        # registration, first replay)
-        pre = sorted((self.runtime.tenants[k] for k in b if k in self.runtime.tenants), key=lambda t: t.t_start)
-        late = pre[len(pre) - len(stops):] if stops else []
-        cp = [t.t_start - s for s, t in zip(stops, late)]
-        up = [t.t_ready - t.t_start for t in late if t.t_ready is not None]
+        # each victim's stop frees one slice: its preemptor is the earliest
+        # team-b container started at or after that stop (the pods that did
+        # not need a victim wait for the partitioner to add slices instead)
+        b_ts = sorted((self.runtime.tenants[k] for k in b if k in self.runtime.tenants), key=lambda t: t.t_start)
+        used: set[int] = set()
+        pairs = []
+        for st in stops:
+            j = next((i for i, t in enumerate(b_ts) if i not in used and t.t_start >= st - 1e-3), None)
+            if j is not None:
+                used.add(j)
+                pairs.append((st, b_ts[j]))
+        cp = [t.t_start - st for st, t in pairs]
+        up = [t.t_ready - t.t_start for _, t in pairs if t.t_ready is not None]
+        lat = [t.t_ready - st for st, t in pairs if t.t_ready is not None]
+        others = [t for i, t in enumerate(b_ts) if i not in used]
         res["phase_b"] = {"ok": ok, "seconds": round(t2 - t1, 2), "preemptions":
                           self.cl.scheduler.stats.get("preemptions", 0) - p0, "victims": len(stops),
                           # CapacityScheduling may only take back borrowed quota
                           "victims_over_quota_only": {k for kind, k, t in self.events
                                                       if kind == "stop" and t >= t1} <= over_a,
-                          "preemption_to_running_s": {"n": len(lat),
-                                                      "p50": round(sorted(lat)[len(lat) // 2], 3) if lat else None,
-                                                      "max": round(max(lat), 3) if lat else None},
+                          "preemption_to_running_s": _stats(lat),
                           "victim_stop_to_preemptor_start_s": _stats(cp),
                           "preemptor_start_to_first_inference_s": _stats(up),
+                          # pods placed on slices the partitioner added (batch window + device-plugin delay)
+                          "submit_to_start_without_preemption_s": _stats([t.t_start - t1 for t in others]),
+                          "timeline_s": {"victim_stops": [round(x - t1, 3) for x in stops],
+                                         "team_b_starts": [round(t.t_start - t1, 3) for t in b_ts],
+                                         "team_b_first_inference": [round(t.t_ready - t1, 3) for t in b_ts
+                                                                    if t.t_ready is not None]},
                           "submit_to_all_running_s": round((b_ready[-1] - t1) if b_ready else -1, 3),
                           **self.snapshot()}
         if sampler is not None:
