@@ -1,8 +1,13 @@
 """Wire format between fractional pods and the node's pod server.
 
-One message = an 8-byte header (two big-endian uint32: JSON length, payload
-length), a UTF-8 JSON object, then an opaque payload (raw little-endian
-tensor bytes: an input image, returned detections).  Requests carry ``op``;
+One message = a 12-byte header (big-endian uint32 JSON length, uint64
+payload length), a UTF-8 JSON object, then an opaque payload (raw
+little-endian tensor bytes: a tenant's weights, an input image, returned
+detections).  A receiver bounds the payload per message (``payload_limit``):
+the pod server allows a register request as many weight bytes as the
+tenant's memory slice holds -- tens of GB on a 288 GB GPU -- and other
+requests ``MAX_PAYLOAD``; an oversized payload is read and dropped so the
+connection stays in step and the sender gets an error reply, not a reset.  Requests carry ``op``;
 replies carry ``ok`` and, on failure, ``error``.  Pure stdlib + numpy: a
 client pod never imports torch or opens the GPU -- its kernels run in the
 server's HIP context, which is the point of the server (see server.py).
@@ -15,17 +20,23 @@ import struct
 
 import numpy as np
 
-_HDR = struct.Struct(">II")
+_HDR = struct.Struct(">IQ")
 MAX_JSON = 1 << 20
 MAX_PAYLOAD = 1 << 30
+_DRAIN = 1 << 24
 
 
 class ProtocolError(RuntimeError):
     pass
 
 
-def _recv_exact(sock: socket.socket, n: int) -> bytes:
-    buf = bytearray(n)
+class PayloadTooLarge(ProtocolError):
+    """The payload was over the receiver's limit; it has been read and
+    dropped, so the connection can carry the error reply."""
+
+
+def _recv_exact(sock: socket.socket, n: int) -> bytearray:
+    buf = bytearray(n)  # returned as is: no second copy of a multi-GB payload
     view = memoryview(buf)
     got = 0
     while got < n:
@@ -33,7 +44,17 @@ def _recv_exact(sock: socket.socket, n: int) -> bytes:
         if k == 0:
             raise ConnectionError("peer closed the connection")
         got += k
-    return bytes(buf)
+    return buf
+
+
+def _drain(sock: socket.socket, n: int) -> None:
+    buf = bytearray(min(n, _DRAIN))
+    view = memoryview(buf)
+    while n:
+        k = sock.recv_into(view[:min(n, len(buf))])
+        if k == 0:
+            raise ConnectionError("peer closed the connection")
+        n -= k
 
 
 def send_msg(sock: socket.socket, obj: dict, payload: bytes | memoryview = b"") -> None:
@@ -43,12 +64,20 @@ def send_msg(sock: socket.socket, obj: dict, payload: bytes | memoryview = b"") 
         sock.sendall(payload)
 
 
-def recv_msg(sock: socket.socket) -> tuple[dict, bytes]:
+def recv_msg(sock: socket.socket, payload_limit=None) -> tuple[dict, bytes | bytearray]:
+    """(JSON object, payload).  ``payload_limit(obj) -> int`` bounds the
+    payload of this message (default ``MAX_PAYLOAD``).  An oversized JSON
+    header desynchronises nothing that can be trusted: ConnectionError."""
     nj, npay = _HDR.unpack(_recv_exact(sock, _HDR.size))
-    if nj > MAX_JSON or npay > MAX_PAYLOAD:
-        raise ProtocolError(f"message too large ({nj} B header, {npay} B payload)")
+    if nj > MAX_JSON:
+        raise ConnectionError(f"message header too large ({nj} B)")
     obj = json.loads(_recv_exact(sock, nj))
+    limit = MAX_PAYLOAD if payload_limit is None or not isinstance(obj, dict) else int(payload_limit(obj))
+    if npay > limit:
+        _drain(sock, npay)
+        raise PayloadTooLarge(f"payload of {npay} B is over this request's limit of {limit} B")
     if not isinstance(obj, dict):
+        _drain(sock, npay)
         raise ProtocolError("message is not a JSON object")
     return obj, _recv_exact(sock, npay) if npay else b""
 
@@ -74,4 +103,4 @@ def unpack_arrays(descs: list[dict], payload: bytes) -> list[np.ndarray]:
     return out
 
 
-__all__ = ["send_msg", "recv_msg", "pack_arrays", "unpack_arrays", "ProtocolError"]
+__all__ = ["send_msg", "recv_msg", "pack_arrays", "unpack_arrays", "ProtocolError", "PayloadTooLarge", "MAX_PAYLOAD"]

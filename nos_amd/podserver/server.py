@@ -302,8 +302,11 @@ class PodServer:
         try:
             while not self._stop.is_set():
                 try:
-                    req, payload = P.recv_msg(conn)
-                except (ConnectionError, OSError):
+                    req, payload = P.recv_msg(conn, self._payload_limit)
+                except P.ProtocolError as e:  # payload drained: the connection is still in step
+                    P.send_msg(conn, {"ok": False, "error": f"{type(e).__name__}: {e}"})
+                    continue
+                except (ConnectionError, OSError, ValueError):
                     return
                 op = req.get("op")
                 try:
@@ -346,6 +349,18 @@ class PodServer:
             with self._lock:
                 self._conns.pop(conn, None)
             conn.close()
+
+    def _payload_limit(self, req: dict) -> int:
+        """Bytes a request may carry: a register request's weights may fill
+        its memory slice (the static estimate then checks weights +
+        activations against it); everything else is an input image."""
+        if req.get("op") != "register":
+            return P.MAX_PAYLOAD
+        try:
+            limit = self._admission(req)[0]
+        except AdmissionError:
+            return P.MAX_PAYLOAD  # _register reports the admission error itself
+        return int(limit * 2 ** 30) if limit else int((self.memory_gb or 64) * 2 ** 30)
 
     # ------------------------------------------------------------ tenants
     def _admission(self, req: dict) -> tuple[float, str | None, str | None, object, tuple]:

@@ -254,6 +254,31 @@ def test_static_estimate_refuses_a_program_larger_than_its_slice(tmp_path):
         srv.stop()
 
 
+def test_weights_may_fill_the_slice_but_not_exceed_it(tmp_path, monkeypatch):
+    """A register request's payload is bounded by the tenant's slice, not by
+    the 1 GiB cap on input images (multi-GB models on big slices); past the
+    slice the server drains the payload and replies with an error on the
+    same connection, which then registers a smaller program."""
+    from nos_amd.podserver import protocol as P
+
+    monkeypatch.setattr(P, "MAX_PAYLOAD", 1 << 16)  # weights well past it, inputs too
+    srv = PodServer(tmp_path / "s.sock", device="cpu", lanes=1, memory_gb=40).start()
+    try:
+        c = PodClient(srv.path, connect_timeout_s=5)
+        prog, w = PG.mlp_program(dim=256, layers=2, batch=8, dtype="fp32")
+        assert len(w) > 1 << 16
+        with pytest.raises(PodServerError, match="PayloadTooLarge"):
+            c.register("big", prog, w, memory_limit_gb=len(w) / 2 / 2 ** 30)
+        rep = c.register("ok", prog, w, memory_limit_gb=1)  # same connection, still in step
+        assert rep["tenants"] == 1
+        with pytest.raises(PodServerError, match="PayloadTooLarge"):  # an input over MAX_PAYLOAD
+            c.infer(np.zeros((1 << 15,), np.float32))
+        c.infer()
+        c.close()
+    finally:
+        srv.stop()
+
+
 # ----------------------------------------------------------------- crashes
 def _supervised(tmp_path):
     env = {**os.environ, "OMP_NUM_THREADS": "1"}

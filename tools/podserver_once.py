@@ -19,6 +19,23 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
 
+def make(kind: str, dtype: str, seed: int):
+    """(program, weights) of one tenant kind."""
+    from nos_amd.models.yolos_program import demo_tenant
+
+    if kind == "yolos":
+        return demo_tenant(dtype, seed)
+    if kind == "bert":  # BERT-base trunk: 12 x (768 hidden, 12 heads, 3072 MLP) at seq 512
+        from nos_amd.models.encoder_program import encoder_program, random_encoder_weights
+
+        return encoder_program(random_encoder_weights(12, 768, 3072, seed), 12, 12, (1, 512, 768), "fp32")
+    if kind == "mlp":
+        from nos_amd.podserver.program import mlp_program
+
+        return mlp_program(dim=4096, layers=4, batch=256, dtype="bf16", seed=seed)
+    raise SystemExit(f"unknown tenant kind {kind!r}")
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--tenants", type=int, default=28)
@@ -28,7 +45,13 @@ def main() -> None:
     ap.add_argument("--slice-gb", type=float, default=10.0)
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--pipeline", type=int, default=1, help="x6 GEMM software-pipelined K loop (1) or plain (0)")
+    ap.add_argument("--mix", default="", help="heterogeneous tenants instead of --tenants YOLOS pods, e.g. "
+                    "yolos:20,bert:4,mlp:4 (bert = BERT-base-shaped fp32 encoder at seq 512, mlp = bf16 GEMM-MLP "
+                    "probe); per-kind rates in the output")
     a = ap.parse_args()
+    kinds = ([k for spec in a.mix.split(",") for k in [spec.split(":")[0]] * int(spec.split(":")[1])]
+             if a.mix else ["yolos"] * a.tenants)
+    a.tenants = len(kinds)
     # one hardware queue per lane: before anything initialises HIP (cmd/podserver.py)
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(a.lanes, 32))
     from nos_amd.models.yolos_program import demo_tenant
@@ -43,7 +66,7 @@ def main() -> None:
     try:
         t0 = time.monotonic()
         clients = [PodClient(path, connect_timeout_s=30) for _ in range(a.tenants)]
-        progs = [demo_tenant(a.dtype, i) for i in range(a.tenants)]
+        progs = [make(k, a.dtype, i) for i, k in enumerate(kinds)]
         t_built = time.monotonic()
         reps = [c.register(f"pod-{i}", *progs[i], memory_limit_gb=a.slice_gb) for i, c in enumerate(clients)]
         build_s = time.monotonic() - t_built
@@ -82,6 +105,13 @@ def main() -> None:
             c.close()
         print(json.dumps({"tenants": a.tenants, "lanes": a.lanes, "window_s": round(w1 - w0, 3),
                           "build_s": round(build_s, 1), "programs_s": round(t_built - t0, 1),
+                          "per_kind": {k: {"tenants": kinds.count(k),
+                                           "inf_per_s": round(sum(d for d, kk in zip(done, kinds) if kk == k)
+                                                              / (w1 - w0), 2),
+                                           "program": next(r["program"] for r, kk in zip(reps, kinds) if kk == k),
+                                           "footprint_gb": max(r["footprint_gb"] for r, kk in zip(reps, kinds)
+                                                               if kk == k)}
+                                       for k in sorted(set(kinds))},
                           "server_build_ms_p50": srv_build_ms[len(srv_build_ms) // 2],
                           "server_compile_ms_p50": sorted(r["compile"].get("compile_ms", 0) for r in reps)[len(reps) // 2],
                           "inf_per_s": round(sum(done) / (w1 - w0), 2),
