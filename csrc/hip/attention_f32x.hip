@@ -32,6 +32,7 @@
 //    as in attention_f32.hip; PERSIST: slice-sized grid (nos::xcd_chunk).
 #include "common.h"
 #include "split_bf16.h"
+#include "split_f16.h"
 
 namespace {
 
@@ -310,6 +311,252 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
   }  // items
 }
 
+// ---------------------------------------------------------------- fp16x3
+// The same attention on two fp16 pieces per operand (split_f16.h: three
+// fp16 MFMAs per product instead of six bf16 ones, same per-product error
+// bound).  K and V arrive as four fp16 planes per token (K hi, K lo, V hi,
+// V lo), written by the fused-LN QKV projection's epilogue on per-head
+// power-of-two scales kvsc[0][h] / kvsc[1][h] that the host derives from the
+// weights (LN output has L2 norm <= sqrt(K), so |k_j| <= sqrt(K)|W_j| + |b_j|
+// bounds every key and value of a head before anything runs).  Q is split
+// here on a per-query-row scale (the row is lane-local: lane r and r + 32
+// hold its two halves), and that scale and the head's key scale fold into
+// the one FMA that already turns a score into exp2 units; P <= 2^8 (deferred
+// rescale) needs no scale; the value scale is divided out with 1/l.
+constexpr int H3_STAGE = 4 * IMG;            // K hi, K lo, V hi, V lo
+constexpr int H3_LDS_BYTES = 2 * H3_STAGE;   // 32 KiB ring
+constexpr int H3_WG_PER_CU = 4;
+
+template <bool PERSIST>
+__global__ __launch_bounds__(NT, H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
+    const float* __restrict__ q, const _Float16* __restrict__ kvs, float* __restrict__ o, int B, int H, int Sq,
+    int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, const float* __restrict__ kvsc,
+    int nqb, int nsplit, float* __restrict__ part) {
+  const int ldh = H * D;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int nwg = B * H * nqb * nsplit;
+  nos::XcdChunk chunk;
+  if constexpr (PERSIST) {
+    chunk = nos::xcd_chunk(blockIdx.x, gridDim.x, nwg);
+  } else {
+    chunk.first = nos::xcd_remap(blockIdx.x, nwg);
+    chunk.end = chunk.first + 1;
+    chunk.step = 1;
+  }
+
+  const int tid = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int r = lane & 31;
+  const int hh = lane >> 5;
+
+  int koff[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) koff[ks] = r * 128 + (((2 * ks + hh) ^ kswz(r)) << 4);
+  const int g16 = (lane >> 4) & 1;
+  const int tq = (lane & 15) >> 2;
+  const int tp = lane & 3;
+  const int vlb = (tq >> 1) & 1;
+  int voff[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+    voff[db] = (4 * hh + tq) * 128 + (((4 * (db ^ vlb)) + 2 * g16 + (tp >> 1)) << 4) + 8 * (tp & 1);
+
+  const int ntiles = (Skv + KVB - 1) / KVB;
+  const int skvp = ntiles * KVB;
+  int soff[4];  // staging: per-lane element offset of instruction i within a tile
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = wid * 4 + i;
+    const int plane = p >> 2;
+    const int row = (p & 3) * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ (plane < 2 ? kswz(row) : vswz(row));
+    soff[i] = (row * 4 + plane) * ldh + lc * 8;
+  }
+
+  for (int w = chunk.first; w < chunk.end; w += chunk.step) {
+    if (PERSIST && w != chunk.first) __syncthreads();
+    const int sp = w % nsplit;
+    const int wq = w / nsplit;
+    const int b = wq / (H * nqb);
+    const int rem = wq - b * (H * nqb);
+    const int hd = rem / nqb;
+    const int qb = rem - hd * nqb;
+    const long long boff = (long long)b * bs_in + hd * D;
+    const int tps = (ntiles + nsplit - 1) / nsplit;
+    const int t0 = sp * tps, t1 = min(ntiles, t0 + tps);
+    const float ksc = kvsc[hd], vinv = 1.f / kvsc[H + hd];  // powers of two
+
+    // ---- Q pieces (B operand) on this query row's scale: lane holds
+    // Q[row r][d = 16ks + 8hh .. +7] * c * 2^e
+    const int qrow = qb * QBLK + wid * 32 + r;
+    f16x8_t qf[4][2];
+    float fs;  // s' -> exp2 units: 2^-e / ksc
+    {
+      const float* qp = q + boff + (long long)min(qrow, Sq - 1) * ld_in + 8 * hh;
+      float x[4][8];
+      float mx = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const float4 x0 = *reinterpret_cast<const float4*>(qp + 16 * ks);
+        const float4 x1 = *reinterpret_cast<const float4*>(qp + 16 * ks + 4);
+        x[ks][0] = x0.x; x[ks][1] = x0.y; x[ks][2] = x0.z; x[ks][3] = x0.w;
+        x[ks][4] = x1.x; x[ks][5] = x1.y; x[ks][6] = x1.z; x[ks][7] = x1.w;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(x[ks][j]));
+      }
+      const int e = nos::h3_scale_exp(xor32_max(mx) * c);
+      const float qm = c * nos::pow2i(e);
+      fs = nos::pow2i(-e) / ksc;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          f16x2_t hi, lo;
+          nos::split2h(f32x2_t{x[ks][j] * qm, x[ks][j + 1] * qm}, hi, lo);
+          qf[ks][0][j] = hi.x; qf[ks][0][j + 1] = hi.y;
+          qf[ks][1][j] = lo.x; qf[ks][1][j + 1] = lo.y;
+        }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) asm volatile("" : "+v"(qf[ks][p]));
+    }
+
+    const _Float16* pb = kvs + (long long)b * skvp * (4 * ldh) + hd * D;
+    auto stage_piece = [&](int t, int buf, int i) {
+      const int p = wid * 4 + i;
+      long long off = (long long)t * (KVB * 4) * ldh + soff[i];
+      if ((t + 1) * KVB > Skv) {  // tail tile: rows past Skv re-read the last key
+        const int over = t * KVB + (p & 3) * 8 + (lane >> 3) - (Skv - 1);
+        if (over > 0) off -= (long long)over * 4 * ldh;
+      }
+      glds16(pb + off, smem + buf * H3_STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
+    };
+#pragma unroll
+    for (int i = 0; i < 4; ++i) stage_piece(t0, 0, i);
+
+    f32x16_t oacc[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      oacc[0][i] = 0.f;
+      oacc[1][i] = 0.f;
+    }
+    float m = 0.f, l = 0.f;
+
+    dma_wait_publish();
+
+    for (int t = t0; t < t1; ++t) {
+      const int buf = (t - t0) & 1;
+      if (t + 1 < t1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) stage_piece(t + 1, buf ^ 1, i);
+      }
+      const unsigned char* kl = smem + buf * H3_STAGE;
+      const unsigned char* vl = kl + 2 * IMG;
+
+      f32x16_t s;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        f16x8_t a[2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) a[p] = *reinterpret_cast<const f16x8_t*>(kl + p * IMG + koff[ks]);
+        s = nos::mma3h(a, qf[ks], s);
+      }
+      if ((t + 1) * KVB > Skv) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (t * KVB + (i & 3) + 8 * (i >> 2) + 4 * hh >= Skv) s[i] = -INFINITY;
+      }
+      float mt = s[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mt = fmaxf(mt, s[i]);
+      const float mrel = xor32_max(mt) * fs - m;
+      if (t == t0 || !__all(mrel <= RESCALE_THR)) {
+        const float delta = t == t0 ? mrel : fmaxf(mrel, 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        m += delta;
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          oacc[0][i] *= alpha;
+          oacc[1][i] *= alpha;
+        }
+      }
+      f16x8_t pf[2][2];
+      float ls[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j2 = 0; j2 < 8; ++j2) {
+        const float x0 = __builtin_amdgcn_exp2f(fmaf(s[2 * j2], fs, -m));
+        const float x1 = __builtin_amdgcn_exp2f(fmaf(s[2 * j2 + 1], fs, -m));
+        ls[(2 * j2) & 3] += x0;
+        ls[(2 * j2 + 1) & 3] += x1;
+        f16x2_t hi, lo;
+        nos::split2h(f32x2_t{x0, x1}, hi, lo);
+        const int s2 = j2 >> 2, e = 2 * (j2 & 3);
+        pf[s2][0][e] = hi.x; pf[s2][0][e + 1] = hi.y;
+        pf[s2][1][e] = lo.x; pf[s2][1][e + 1] = lo.y;
+      }
+      l += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          f16x8_t a[2];
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const unsigned char* base = vl + p * IMG + voff[db] + s2 * 16 * 128;
+            const s16x4_t lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base));
+            const s16x4_t hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + 8 * 128));
+            const s16x8_t a16 = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+            a[p] = __builtin_bit_cast(f16x8_t, a16);
+          }
+          oacc[db] = nos::mma3h(a, pf[s2], oacc[db]);
+        }
+      dma_wait_publish();
+    }
+
+    const float lt = xor32_sum(l);
+    if (nsplit > 1) {  // unnormalised partial (O, m, l), O on the unit scale
+      if (qrow < Sq) {
+        const long long row = ((long long)sp * B + b) * Sq + qrow;
+        float* op = part + row * ldh + hd * D;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(op + 32 * db + 8 * g + 4 * hh) =
+                float4{oacc[db][4 * g + 0] * vinv, oacc[db][4 * g + 1] * vinv, oacc[db][4 * g + 2] * vinv,
+                       oacc[db][4 * g + 3] * vinv};
+        if (hh == 0) {
+          float* ml = part + (long long)nsplit * B * Sq * ldh + (row * H + hd) * 2;
+          ml[0] = m;
+          ml[1] = lt;
+        }
+      }
+      continue;
+    }
+    const float inv = vinv / lt;
+    if (qrow < Sq) {
+      float* op = o + (long long)b * bs_out + (long long)qrow * ld_out + hd * D;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float4 y;
+          y.x = oacc[db][4 * g + 0] * inv;
+          y.y = oacc[db][4 * g + 1] * inv;
+          y.z = oacc[db][4 * g + 2] * inv;
+          y.w = oacc[db][4 * g + 3] * inv;
+          *reinterpret_cast<float4*>(op + 32 * db + 8 * g + 4 * hh) = y;
+        }
+    }
+  }  // items
+}
+
 // K and V rows of the fused projection -> six bf16 planes per token:
 // kvs[b][s][plane][H*64], plane = 3 * (0 K, 1 V) + piece, s < Skvp (rows
 // past Skv are written as zeros, though the attention never reads them).
@@ -363,10 +610,10 @@ constexpr int WG_PER_CU = 3;  // the kernel's launch bound
 // the (budgeted) CUs empty -- one YOLOS image is 162 q-blocks for 768 slots --
 // split the keys so the grid fills them, at most MAX_SPLIT ways and never so
 // finely that a split has no tile.
-int pick_split(long long nwg1, int ntiles) {
+int pick_split(long long nwg1, int ntiles, int wg_per_cu = WG_PER_CU) {
   int n = g_kvsplit;
   if (n == 0) {
-    const long long slots = (long long)WG_PER_CU * nos_effective_cus();
+    const long long slots = (long long)wg_per_cu * nos_effective_cus();
     n = nwg1 >= slots ? 1 : (int)(slots / nwg1);
   }
   n = n < 1 ? 1 : (n > MAX_SPLIT ? MAX_SPLIT : n);
@@ -486,4 +733,48 @@ NOS_API int nos_attn_fwd_f32x6_presplit_d64(const float* q, float* o, int B, int
                                             long long ws_bytes, hipStream_t stream) {
   if (int rc = check_args(q, o, ws, ws_bytes, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out)) return rc;
   return run_from_planes(q, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, scale, ws, stream);
+}
+
+namespace {
+
+int launch_h3(const float* q, const _Float16* kvs, float* o, int B, int H, int Sq, int Skv, int ld_in,
+              long long bs_in, int ld_out, long long bs_out, float c, const float* kvsc, int nqb, int nsplit,
+              float* part, hipStream_t stream) {
+  const long long nwg = (long long)B * H * nqb * nsplit;
+  const int grid = nos_grid_for((const void*)attn_fwd_f32h3_d64_kernel<true>, NT, H3_LDS_BYTES, nwg);
+  if (grid < nwg)
+    hipLaunchKernelGGL((attn_fwd_f32h3_d64_kernel<true>), dim3((unsigned)grid), dim3(NT), H3_LDS_BYTES, stream, q,
+                       kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit, part);
+  else
+    hipLaunchKernelGGL((attn_fwd_f32h3_d64_kernel<false>), dim3((unsigned)nwg), dim3(NT), H3_LDS_BYTES, stream, q,
+                       kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit, part);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// fp16x3 attention from the four fp16 planes per token that the QKV
+// projection's epilogue wrote at the start of ws (nos_gemm_ln_f32x6_qkv_h3)
+// on the per-head scales kvsc [2][H] (K, then V; powers of two).  Same
+// contract and workspace as nos_attn_fwd_f32x6_presplit_d64.
+NOS_API int nos_attn_fwd_f32h3_presplit_d64(const float* q, float* o, int B, int H, int Sq, int Skv, int ld_in,
+                                            long long bs_in, int ld_out, long long bs_out, float scale,
+                                            const float* kvsc, void* ws, long long ws_bytes, hipStream_t stream) {
+  if (int rc = check_args(q, o, ws, ws_bytes, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out)) return rc;
+  if (kvsc == nullptr) return (int)hipErrorInvalidValue;
+  const float c = scale * 1.4426950408889634f;
+  const int nqb = (Sq + QBLK - 1) / QBLK;
+  const long long nwg = (long long)B * H * nqb;
+  const int skvp = (Skv + KVB - 1) / KVB * KVB;
+  const int nsplit = pick_split(nwg, skvp / KVB, H3_WG_PER_CU);
+  auto* kvs = static_cast<const _Float16*>(ws);
+  float* part = reinterpret_cast<float*>(static_cast<unsigned char*>(ws) +
+                                         ((long long)B * skvp * 6 * H * D * 2 + 15) / 16 * 16);
+  const int rc = launch_h3(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit, part,
+                           stream);
+  if (rc != 0 || nsplit == 1) return rc;
+  const long long n4 = (long long)B * Sq * H * (D / 4);
+  hipLaunchKernelGGL(merge_splits_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, part, o, B, H, Sq,
+                     nsplit, ld_out, bs_out, n4);
+  return (int)hipGetLastError();
 }

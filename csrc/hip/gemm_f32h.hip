@@ -1,0 +1,366 @@
+// fp32 GEMM on the fp16x3 split (split_f16.h): both operands arrive as two
+// fp16 planes on power-of-two scales, and each 16-deep step of a 32x32 block
+// is three v_mfma_f32_32x32x16_f16 (hi.hi + hi.lo + lo.hi) -- half the
+// matrix-pipe work of the bf16x6 GEMM (gemm_f32x.hip) and no split in the K
+// loop at all:
+//
+//   C[M,N] = act(rinv[m] * csc[n] * (A'[m,:] . W'[n,:]) + bias[n]) (+ R)
+//
+//  * A' = the rows of A split by nos_split_rows_h3 (below): per row, a scale
+//    2^e_m that puts max|a| just under 2^14 (or, LayerNorm mode, the rows
+//    normalised first and scaled by the sqrt(K) bound of a normalised row),
+//    written as hi / lo planes [2][M][K]; rinv[m] = 2^-e_m;
+//  * W' = the weight's rows on their own scales 2^f_n, split once per
+//    weight by the host (ops.split_f32_weight_h3); csc[n] = 2^-f_n;
+//  * 4 waves per workgroup (4 x 1: 32-row strips, or 2 x 2), 128 x 128
+//    tiles, BK = 32 per stage in a 2-deep LDS ring filled by LDS-DMA
+//    (global_load_lds_dwordx4; every plane as rows of 64 B, 16-byte chunks
+//    XOR-swizzled by (row >> 2) & 3 -- conflict-free fragment reads);
+//  * the fragments of step s+1 are read from LDS while step s's MFMAs run
+//    (two register sets in ping-pong, one stage boundary per two steps);
+//  * epilogue: scales, bias, GELU / ReLU, residual, and optionally the K / V
+//    columns of a fused QKV projection as the attention's fp16 planes
+//    (KvOut: attention_f32x.hip's h3 kernel reads them).
+#include "common.h"
+#include "split_f16.h"
+
+namespace {
+
+enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
+
+constexpr int BK = 32, ROWB = BK * 2;  // one plane row of a stage: 64 B = 4 chunks
+
+__device__ __forceinline__ int swz(int row) { return (row >> 2) & 3; }
+
+__device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds_wave_base);
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(lds) : "memory");
+}
+
+__device__ __forceinline__ float erf_fast(float x) {  // Abramowitz-Stegun 7.1.26, |err| <= 1.5e-7
+  const float ax = fabsf(x);
+  const float t = 1.f / fmaf(0.3275911f, ax, 1.f);
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float r = fmaf(-p * t, expf(-ax * ax), 1.f);
+  return copysignf(r, x);
+}
+
+// the K / V columns (>= qcols) of a fused QKV projection as the h3
+// attention's planes kvs[b][s][K hi, K lo, V hi, V lo][hd], each head on
+// kvsc[0 / 1][head]; rows per batch S, padded to skvp
+struct KvOut {
+  unsigned short* kvs = nullptr;
+  const float* kvsc = nullptr;
+  int qcols = 0, hd = 0, S = 0, skvp = 0;
+};
+
+template <int BM, int BN, int WGM, int WGN, bool PERSIST>
+__global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_h3_kernel(
+    const _Float16* __restrict__ Ap, int lda, long long aplane, const float* __restrict__ rinv,
+    const _Float16* __restrict__ Wp, int ldw, long long wplane, const float* __restrict__ csc,
+    const float* __restrict__ bias, const float* __restrict__ R, int ldr, float* __restrict__ C, int ldc, int M,
+    int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv) {
+  constexpr int NW = WGM * WGN, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
+  static_assert(NW == 4 && MI >= 1 && NI >= 1, "4 waves");
+  constexpr int TA = 2 * BM * ROWB, STAGE = TA + 2 * BN * ROWB;
+  constexpr int APW = TA / 1024 / NW, WPW = 2 * BN * ROWB / 1024 / NW;  // 1 KiB DMA pieces per wave
+  static_assert(APW * NW * 1024 == TA && WPW * NW * 1024 == 2 * BN * ROWB, "equal DMA count per wave");
+  constexpr int LPS = APW + WPW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int c = lane & 31, h = lane >> 5;
+  const int wm = wid / WGN, wn = wid % WGN;
+  const int ntiles = tiles_m * tiles_n;
+  const int nk = K / BK;
+  nos::XcdChunk chunk;
+  if constexpr (PERSIST) {
+    chunk = nos::xcd_chunk(blockIdx.x, gridDim.x, ntiles);
+  } else {
+    chunk.first = nos::xcd_remap(blockIdx.x, ntiles);
+    chunk.end = chunk.first + 1;
+    chunk.step = 1;
+  }
+  for (int tt = chunk.first; tt < chunk.end; tt += chunk.step) {
+    if (PERSIST && tt != chunk.first) __syncthreads();
+    const int tm = tt / tiles_n, tn = tt - tm * tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    // a 1 KiB piece = 16 rows x 64 B of one plane; lane L: row L / 4, chunk L % 4
+    auto stage = [&](int k0, unsigned char* dst) {
+#pragma unroll
+      for (int i = 0; i < APW; ++i) {
+        const int p = wid * APW + i;
+        const int plane = p / (BM / 16), rb = (p % (BM / 16)) * 16;
+        const int row = rb + (lane >> 2);
+        int g = m0 + row;
+        g = g < M ? g : M - 1;
+        glds16(Ap + plane * aplane + (long long)g * lda + k0 + (((lane & 3) ^ swz(row)) << 3),
+               dst + plane * BM * ROWB + rb * ROWB);
+      }
+#pragma unroll
+      for (int i = 0; i < WPW; ++i) {
+        const int p = wid * WPW + i;
+        const int plane = p / (BN / 16), rb = (p % (BN / 16)) * 16;
+        const int row = rb + (lane >> 2);
+        int g = n0 + row;
+        g = g < N ? g : N - 1;
+        glds16(Wp + plane * wplane + (long long)g * ldw + k0 + (((lane & 3) ^ swz(row)) << 3),
+               dst + TA + plane * BN * ROWB + rb * ROWB);
+      }
+    };
+
+    f32x16_t acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    struct Frag {
+      f16x8_t a[MI][2], w[NI][2];
+    };
+    // fragments of 16-deep step s (0 / 1) of the stage at base
+    auto load = [&](const unsigned char* base, int s, Frag& f) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wm * (BM / WGM) + i * 32 + c;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          f.a[i][p] = *reinterpret_cast<const f16x8_t*>(base + p * BM * ROWB + row * ROWB +
+                                                        (((2 * s + h) ^ swz(row)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int row = wn * (BN / WGN) + j * 32 + c;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          f.w[j][p] = *reinterpret_cast<const f16x8_t*>(base + TA + p * BN * ROWB + row * ROWB +
+                                                        (((2 * s + h) ^ swz(row)) << 4));
+      }
+    };
+    auto mma = [&](const Frag& f) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = nos::mma3h(f.a[i], f.w[j], acc[i][j]);
+    };
+
+    stage(0, smem);
+    if (nk > 1) stage(BK, smem + STAGE);
+    if (nk > 1) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");  // stage 0 landed, stage 1 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    Frag fa, fb;
+    load(smem, 0, fa);
+    for (int kt = 0; kt < nk; ++kt) {
+      const unsigned char* cur = smem + (kt & 1) * STAGE;
+      load(cur, 1, fb);  // step 1 read under step 0's MFMAs
+      mma(fa);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nk) {
+        // stage kt+1 landed (the only DMA in flight); every wave has read stage kt
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + 2 < nk) stage((kt + 2) * BK, smem + (kt & 1) * STAGE);
+        load(smem + ((kt + 1) & 1) * STAGE, 0, fa);  // next stage's step 0 under step 1's MFMAs
+      }
+      mma(fb);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // every wave is done with the ring (the next tile's prologue)
+
+    // epilogue: register r of lane (c, h) = row (r&3) + 8(r>>2) + 4h of the block, column c
+    float rsv[MI][16];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        rsv[i][r] = rinv[m < M ? m : M - 1];
+      }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int n = n0 + wn * (BN / WGN) + j * 32 + c;
+      const int nc = n < N ? n : N - 1;
+      const float cs = csc[nc];
+      const float p2 = (epi & EPI_BIAS) ? bias[nc] : 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2);
+          if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+          if (epi & EPI_RELU) v = fmaxf(v, 0.f);
+          if (m < M && n < N) {
+            if (epi & EPI_RESID) v += R[(long long)m * ldr + n];
+            if (kv.kvs != nullptr && n >= kv.qcols) {
+              const int t = (n - kv.qcols) >= kv.hd;  // 0: K, 1: V
+              const int col = n - kv.qcols - t * kv.hd;
+              const int b = kv.S == M ? 0 : m / kv.S;
+              const long long row = (long long)b * kv.skvp + (m - b * kv.S);
+              const float x = v * kv.kvsc[t * (kv.hd >> 6) + (col >> 6)];
+              const _Float16 h0 = (_Float16)x;
+              const _Float16 h1 = (_Float16)(x - (float)h0);
+              unsigned short* dst = kv.kvs + (row * 4 + 2 * t) * kv.hd + col;
+              dst[0] = __builtin_bit_cast(unsigned short, h0);
+              dst[kv.hd] = __builtin_bit_cast(unsigned short, h1);
+            } else {
+              C[(long long)m * ldc + n] = v;
+            }
+          }
+        }
+      }
+    }
+  }  // tiles
+}
+
+template <int BM, int BN, int WGM, int WGN>
+int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, const _Float16* Wp, int ldw,
+             long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C, int ldc, int M,
+             int N, int K, int epi, KvOut kv, hipStream_t st) {
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const long long ntiles = (long long)tiles_m * tiles_n;
+  if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
+  const size_t lds = 2 * (size_t)(2 * BM * ROWB + 2 * BN * ROWB);
+  const int grid = nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true>, 256, lds, ntiles);
+  if (grid < ntiles)
+    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true>), dim3((unsigned)grid), dim3(256), lds, st, Ap, lda,
+                       aplane, rinv, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m, tiles_n, kv);
+  else
+    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false>), dim3((unsigned)ntiles), dim3(256), lds, st, Ap,
+                       lda, aplane, rinv, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m, tiles_n,
+                       kv);
+  return (int)hipGetLastError();
+}
+
+int g_layout = 0;  // 0: 4 x 1 waves, 1: 2 x 2 waves (nos_gemm_f32h3_set_layout)
+
+// ------------------------------------------------------------ row split
+// One wave per row: the row's scale (max |a|, or in LayerNorm mode the
+// sqrt(K) bound of a normalised row), then its hi / lo planes.  K % 8 == 0.
+__global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restrict__ A, int lda,
+                                                            _Float16* __restrict__ P, int ldp, long long pplane,
+                                                            float* __restrict__ rinv, int M, int K, int ln,
+                                                            float eps, int eln) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* a = A + (long long)row * lda;
+  float mu = 0.f, rs = 1.f;
+  int e;
+  if (ln) {
+    float s = 0.f;
+    for (int k = lane * 4; k < K; k += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(a + k);
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    mu = s / (float)K;
+    float q = 0.f;
+    for (int k = lane * 4; k < K; k += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(a + k);
+      const float d0 = v.x - mu, d1 = v.y - mu, d2 = v.z - mu, d3 = v.w - mu;
+      q = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, q))));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    rs = rsqrtf(q / (float)K + eps);
+    e = eln;  // |x^| <= sqrt(K): the host's exponent for it
+  } else {
+    float mx = 0.f;
+    for (int k = lane * 4; k < K; k += 256) {
+      const float4 v = *reinterpret_cast<const float4*>(a + k);
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    e = nos::h3_scale_exp(mx);
+  }
+  const float sc = nos::pow2i(e);
+  const float mul = rs * sc, add = -mu * mul;
+  _Float16* ph = P + (long long)row * ldp;
+  _Float16* pl = ph + pplane;
+  for (int k = lane * 4; k < K; k += 256) {
+    const float4 v = *reinterpret_cast<const float4*>(a + k);
+    f16x2_t h01, l01, h23, l23;
+    nos::split2h(f32x2_t{fmaf(v.x, mul, add), fmaf(v.y, mul, add)}, h01, l01);
+    nos::split2h(f32x2_t{fmaf(v.z, mul, add), fmaf(v.w, mul, add)}, h23, l23);
+    typedef __attribute__((ext_vector_type(4))) _Float16 f16x4_t;
+    *reinterpret_cast<f16x4_t*>(ph + k) = f16x4_t{h01.x, h01.y, h23.x, h23.y};
+    *reinterpret_cast<f16x4_t*>(pl + k) = f16x4_t{l01.x, l01.y, l23.x, l23.y};
+  }
+  if (lane == 0) rinv[row] = nos::pow2i(-e);
+}
+
+}  // namespace
+
+NOS_API int nos_gemm_f32h3_set_layout(int layout) {
+  if (layout < 0 || layout > 1) return (int)hipErrorInvalidValue;
+  g_layout = layout;
+  return 0;
+}
+
+// Split the rows of fp32 A [M, K] (lda) into hi / lo fp16 planes P (row
+// stride ldp, plane stride pplane elements) on per-row power-of-two scales,
+// rinv[m] = 1 / scale.  ln != 0: the rows are LayerNorm-normalised first
+// (no gamma / beta: those are folded into the weight and bias) and scaled by
+// 2^eln (the host's bound for |x^| <= sqrt(K)).  K % 4 == 0, rows 16-byte aligned.
+NOS_API int nos_split_rows_h3(const float* A, int lda, void* P, int ldp, long long pplane, float* rinv, int M, int K,
+                              int ln, float eps, int eln, hipStream_t stream) {
+  if (M <= 0 || K <= 0 || (K % 4) || (lda % 4) || (ldp % 4) || ldp < K || pplane < (long long)M * ldp)
+    return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)A) | ((uintptr_t)P)) & 15) return (int)hipErrorInvalidValue;
+  if (eln < -126 || eln > 126) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(split_rows_h3_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, stream, A, lda,
+                     static_cast<_Float16*>(P), ldp, pplane, rinv, M, K, ln, eps, eln);
+  return (int)hipGetLastError();
+}
+
+// C = act(rinv[m] csc[n] (A' . W'^T) + bias) (+ R) on the fp16 planes of A
+// (nos_split_rows_h3) and W ([2][N][K], ldw, plane stride wplane; row scales
+// csc).  kvs != nullptr: a fused QKV projection (N = 3 hd) whose K / V
+// columns go to the h3 attention's planes (S rows per batch padded to skvp,
+// per-head scales kvsc [2][hd / 64]); Q to C.  K % 32 == 0.
+NOS_API int nos_gemm_f32h3(const void* Ap, int lda, long long aplane, const float* rinv, const void* Wp, int ldw,
+                           long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C,
+                           int ldc, int M, int N, int K, int epi, void* kvs, int S, int skvp, const float* kvsc,
+                           hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0) return (int)hipErrorInvalidValue;
+  if ((lda % 8) || (ldw % 8) || lda < K || ldw < K || aplane < (long long)M * lda || wplane < (long long)N * ldw)
+    return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)Ap) | ((uintptr_t)Wp)) & 15) return (int)hipErrorInvalidValue;
+  if (!rinv || !csc || ((epi & EPI_BIAS) && !bias) || ((epi & EPI_RESID) && (!R || ldr < N)))
+    return (int)hipErrorInvalidValue;
+  KvOut kv;
+  if (kvs != nullptr) {
+    if (!kvsc || N % 3 || (N / 3) % 64 || S <= 0 || M % S || skvp < S || (((uintptr_t)kvs) & 15))
+      return (int)hipErrorInvalidValue;
+    kv.kvs = static_cast<unsigned short*>(kvs);
+    kv.kvsc = kvsc;
+    kv.hd = N / 3;
+    kv.qcols = kv.hd;
+    kv.S = S;
+    kv.skvp = skvp;
+  } else if (ldc < N) {
+    return (int)hipErrorInvalidValue;
+  }
+  const auto* a = static_cast<const _Float16*>(Ap);
+  const auto* w = static_cast<const _Float16*>(Wp);
+  if (g_layout == 1)
+    return launch_t<128, 128, 2, 2>(a, lda, aplane, rinv, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, kv,
+                                    stream);
+  return launch_t<128, 128, 4, 1>(a, lda, aplane, rinv, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, kv,
+                                  stream);
+}

@@ -85,9 +85,13 @@ __device__ __forceinline__ void wait_stages(int n) {
 // attention reads (attention_f32x.hip: kvs[b][s][plane][hd], rows padded to
 // skvp per batch), exactly the split its streaming kernel would make, so the
 // fp32 K/V never go to memory; the Q columns go to C as usual.
+// With kvsc (the fp16x3 attention, attention_f32x.hip): four fp16 planes per
+// token instead (K hi, K lo, V hi, V lo: kvs[b][s][plane][hd], split_f16.h),
+// each head's K / V on the power-of-two scale kvsc[0 / 1][head].
 struct KvOut {
   unsigned short* kvs = nullptr;
   int qcols = 0, hd = 0, S = 0, skvp = 0;
+  const float* kvsc = nullptr;
 };
 
 __device__ __forceinline__ unsigned short bf16_bits(float x) {
@@ -402,6 +406,15 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_f3
             const int col = n - kv.qcols - t * kv.hd;
             const int b = kv.S == M ? 0 : m / kv.S;
             const long long row = (long long)b * kv.skvp + (m - b * kv.S);
+            if (kv.kvsc != nullptr) {
+              const float x = v * kv.kvsc[t * (kv.hd >> 6) + (col >> 6)];
+              const _Float16 h0 = (_Float16)x;
+              const _Float16 h1 = (_Float16)(x - (float)h0);
+              unsigned short* dst = kv.kvs + (row * 4 + 2 * t) * kv.hd + col;
+              dst[0] = __builtin_bit_cast(unsigned short, h0);
+              dst[kv.hd] = __builtin_bit_cast(unsigned short, h1);
+              continue;
+            }
             unsigned short* dst = kv.kvs + (row * 6 + 3 * t) * kv.hd + col;
             const __bf16 p0 = (__bf16)v;
             const float r1 = v - (float)p0;
@@ -565,12 +578,16 @@ NOS_API int nos_gemm_ln_f32x6(const float* A, int lda, const void* Wp, int ldw, 
 // S rows per batch padded to skvp); Q goes to C[:, :hd].  The attention then
 // runs from the planes (nos_attn_fwd_f32x6_presplit_d64): no fp32 K/V store,
 // no streaming split.
-NOS_API int nos_gemm_ln_f32x6_qkv(const float* A, int lda, const void* Wp, int ldw, long long wplane,
-                                  const float* c1, const float* c2, float* C, int ldc, int M, int N, int K, int epi,
-                                  float eps, void* kvs, int S, int skvp, hipStream_t stream) {
+namespace {
+
+int qkv_planes(const float* A, int lda, const void* Wp, int ldw, long long wplane, const float* c1, const float* c2,
+               float* C, int ldc, int M, int N, int K, int epi, float eps, void* kvs, int S, int skvp,
+               const float* kvsc, hipStream_t stream) {
   if (kvs == nullptr || N % 3 != 0 || S <= 0 || M % S != 0 || skvp < S || (((uintptr_t)kvs) & 15))
     return (int)hipErrorInvalidValue;
+  if (kvsc != nullptr && (N / 3) % 64 != 0) return (int)hipErrorInvalidValue;
   KvOut kv;
+  kv.kvsc = kvsc;
   kv.kvs = static_cast<unsigned short*>(kvs);
   kv.hd = N / 3;
   kv.qcols = kv.hd;
@@ -578,4 +595,23 @@ NOS_API int nos_gemm_ln_f32x6_qkv(const float* A, int lda, const void* Wp, int l
   kv.skvp = skvp;
   return launch(A, lda, static_cast<const unsigned short*>(Wp), ldw, wplane, nullptr, c1, c2, nullptr, 0, C, ldc, M,
                 N, K, epi & ~(EPI_BIAS | EPI_RESID), eps, true, stream, kv);
+}
+
+}  // namespace
+
+NOS_API int nos_gemm_ln_f32x6_qkv(const float* A, int lda, const void* Wp, int ldw, long long wplane,
+                                  const float* c1, const float* c2, float* C, int ldc, int M, int N, int K, int epi,
+                                  float eps, void* kvs, int S, int skvp, hipStream_t stream) {
+  return qkv_planes(A, lda, Wp, ldw, wplane, c1, c2, C, ldc, M, N, K, epi, eps, kvs, S, skvp, nullptr, stream);
+}
+
+// The same projection writing the fp16x3 attention's four planes per token,
+// each head's K / V on the power-of-two scale kvsc[0 / 1][head]
+// (nos_attn_fwd_f32h3_presplit_d64).
+NOS_API int nos_gemm_ln_f32x6_qkv_h3(const float* A, int lda, const void* Wp, int ldw, long long wplane,
+                                     const float* c1, const float* c2, float* C, int ldc, int M, int N, int K,
+                                     int epi, float eps, void* kvs, int S, int skvp, const float* kvsc,
+                                     hipStream_t stream) {
+  if (kvsc == nullptr) return (int)hipErrorInvalidValue;
+  return qkv_planes(A, lda, Wp, ldw, wplane, c1, c2, C, ldc, M, N, K, epi, eps, kvs, S, skvp, kvsc, stream);
 }

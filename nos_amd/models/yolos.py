@@ -176,13 +176,11 @@ class YolosDetector(nn.Module):
         folded = self.folded_weights()
         h = self._embed(pixel_values, lin)
         # fp32 under x6 math: the QKV projection writes K / V as the attention's
-        # bf16 planes directly (no fp32 K/V round trip, no split kernel)
-        presplit = (h.is_cuda and h.dtype == torch.float32 and ops.f32_math() == "x6"
-                    and ops.attention_f32_variant().startswith("x6"))
+        # bf16x6 / fp16x3 planes directly (no fp32 K/V round trip, no split kernel)
+        presplit = ops.ln_qkv_fusable(h)
         for L, fw in zip(self.layers, folded):
             if presplit:
-                qkv, ws = ops.linear_ln_qkv_x6(h, fw["qkv_w"], fw["qkv_c1"], fw["qkv_c2"], nh, eps=eps)
-                a = ops.attention_presplit(qkv, ws, nh)
+                a = ops.ln_qkv_attention(h, fw["qkv_w"], fw["qkv_c1"], fw["qkv_c2"], nh, eps=eps)
             else:
                 qkv = ops.linear_ln(h, fw["qkv_w"], fw["qkv_c1"], fw["qkv_c2"], eps=eps)
                 a = ops.attention_qkv(qkv, nh)

@@ -134,7 +134,10 @@ def _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K):
     o2, r2 = _gemm_io(x, weight, out, residual, M, N, K)
     _check_f32(residual=r2)
     ldr = r2.stride(0) if r2 is not None else 0
-    if _F32_MATH == "x6":
+    if _F32_MATH == "h3":
+        ap, rinv = _split_rows_h3(x2, ln=False)
+        _gemm_h3(ap, rinv, weight, bias, r2, o2, _epi(bias, act, residual))
+    elif _F32_MATH == "x6":
         wp = split_f32_weight(weight)
         rc = _lib.lib().nos_gemm_f32x6(x2.data_ptr(), x2.stride(0), wp.data_ptr(), wp.stride(1), wp.stride(0),
                                        _ptr(bias), _ptr(r2), ldr, o2.data_ptr(), o2.stride(0), M, N, K,
@@ -150,6 +153,64 @@ def _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K):
 
 _F32_MATH = "exact"
 _SPLIT_CACHE: dict[int, tuple] = {}
+_SPLIT_H3_CACHE: dict[int, tuple] = {}
+
+
+def _pow2_exp(mx: torch.Tensor) -> torch.Tensor:
+    """Exponents e with mx * 2^e < 2^14 (0 where mx == 0), clamped to +-126."""
+    e = 14 - torch.frexp(mx).exponent.to(torch.int64)
+    return torch.where(mx > 0, e, torch.zeros_like(e)).clamp(-126, 126)
+
+
+@torch.no_grad()
+def split_f32_weight_h3(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """The fp16x3 form of an fp32 weight [N, K]: every row on its own
+    power-of-two scale (max |w| just under 2^14) as hi / lo fp16 planes
+    [2, N, K], and the inverse scales [N] -- cached per tensor and version
+    like :func:`split_f32_weight`."""
+    key = id(w)
+    hit = _SPLIT_H3_CACHE.get(key)
+    if hit is not None:
+        ref, ver, ptr, out = hit
+        if ref() is w and ver == w._version and ptr == w.data_ptr():
+            return out
+    import weakref
+
+    wf = w.float()
+    e = _pow2_exp(wf.abs().amax(dim=1))
+    ws = torch.ldexp(wf, e[:, None].to(wf.device))
+    hi = ws.half()
+    lo = (ws - hi.float()).half()
+    out = (torch.stack([hi, lo]).contiguous(),
+           torch.ldexp(torch.ones_like(e, dtype=torch.float32), -e).to(w.device).contiguous())
+    _SPLIT_H3_CACHE[key] = (weakref.ref(w, lambda _r, k=key: _SPLIT_H3_CACHE.pop(k, None)), w._version,
+                            w.data_ptr(), out)
+    return out
+
+
+def _split_rows_h3(x2: torch.Tensor, ln: bool, eps: float = 0.0) -> tuple[torch.Tensor, torch.Tensor]:
+    """Rows of fp32 x2 [M, K] -> (hi / lo fp16 planes [2, M, K], 1 / row
+    scale [M]) by ``nos_split_rows_h3``; ``ln``: the rows LayerNorm-normalised
+    first, on the sqrt(K) bound's scale."""
+    M, K = x2.shape
+    planes = torch.empty((2, M, K), dtype=torch.float16, device=x2.device)
+    rinv = torch.empty((M,), dtype=torch.float32, device=x2.device)
+    eln = 14 - math.frexp(math.sqrt(K))[1]
+    rc = _lib.lib().nos_split_rows_h3(x2.data_ptr(), x2.stride(0), planes.data_ptr(), K, M * K, rinv.data_ptr(), M,
+                                      K, int(ln), float(eps), eln, _stream())
+    _lib.check(rc, "nos_split_rows_h3")
+    return planes, rinv
+
+
+def _gemm_h3(ap, rinv, weight, bias, r2, o2, epi, kv=None) -> None:
+    M, K = ap.shape[1], ap.shape[2]
+    N = weight.shape[0]
+    wp, csc = split_f32_weight_h3(weight)
+    kvs, S, skvp, kvsc = kv if kv is not None else (None, 0, 0, None)
+    rc = _lib.lib().nos_gemm_f32h3(ap.data_ptr(), K, M * K, rinv.data_ptr(), wp.data_ptr(), K, N * K, csc.data_ptr(),
+                                   _ptr(bias), _ptr(r2), r2.stride(0) if r2 is not None else 0, o2.data_ptr(),
+                                   o2.stride(0), M, N, K, epi, _ptr(kvs), S, skvp, _ptr(kvsc), _stream())
+    _lib.check(rc, "nos_gemm_f32h3")
 
 
 def set_f32_math(mode: str) -> None:
@@ -158,11 +219,16 @@ def set_f32_math(mode: str) -> None:
     ``"x6"`` -- every operand split into three bf16 pieces (exact: 3 x 8
     mantissa bits) and the six piece products of order >= 2^-16 summed by
     bf16 MFMAs in fp32 (csrc/hip/split_bf16.h): the same accuracy against fp64
-    (tests/test_kernels_gpu.py) at 6/16 of the matrix-pipe time.  The fp32
+    (tests/test_kernels_gpu.py) at 6/16 of the matrix-pipe time -- or
+    ``"h3"`` -- every operand as two fp16 pieces on a power-of-two scale
+    per row (csrc/hip/split_f16.h, gemm_f32h.hip: the activation rows split
+    by a pre-pass, LayerNorm applied in it, the weight once), three fp16
+    MFMAs per product: half of x6's matrix-pipe work, within the exact
+    kernel's error against fp64 (tests/test_gemm_h3_gpu.py).  The fp32
     attention has its own switch (``set_attention_f32_variant("x6")``)."""
     global _F32_MATH
-    if mode not in ("exact", "x6"):
-        raise ValueError(f"f32 math must be 'exact' or 'x6', got {mode!r}")
+    if mode not in ("exact", "x6", "h3"):
+        raise ValueError(f"f32 math must be 'exact', 'x6' or 'h3', got {mode!r}")
     _F32_MATH = mode
 
 
@@ -179,6 +245,12 @@ def set_gemm_f32x6_tile(tile: str) -> None:
     names = {"policy": -1, "128x64": 3, "128x128": 5, "wide": 6, "256x128": 7}  # wide: 128x128 if N >= 1024, else 128x64
     code = names[tile] if tile in names else int(tile)  # numeric codes: gemm_f32x.hip g_tile (A/B)
     _lib.check(_lib.lib().nos_gemm_f32x6_set_tile(code), "nos_gemm_f32x6_set_tile")
+
+
+def set_gemm_f32h3_layout(layout: str) -> None:
+    """h3 GEMM waves: ``"4x1"`` (default: 32-row strips, each wave reads the
+    whole W tile) or ``"2x2"`` (A/B)."""
+    _lib.check(_lib.lib().nos_gemm_f32h3_set_layout({"4x1": 0, "2x2": 1}[layout]), "nos_gemm_f32h3_set_layout")
 
 
 def set_gemm_f32x6_pipeline(on: bool) -> None:
@@ -268,9 +340,16 @@ def set_attention_f32_variant(variant: str) -> None:
     kernel (attention_f32x.hip: fp32 operands as three bf16 pieces, six
     exact piece products per product on the bf16 matrix pipes; the keys are
     split 1-4 ways when the grid would leave CU slots empty), ``"x6k<n>"``
-    with n key splits forced, ``"x6n"`` = ``"x6k1"`` (never split)."""
+    with n key splits forced, ``"x6n"`` = ``"x6k1"`` (never split);
+    ``"h3"`` / ``"h3n"`` / ``"h3k<n>"``: the fp16x3 kernel (two fp16 pieces
+    per operand on power-of-two scales, three MFMAs per product: the x6
+    kernel's per-product error bound at half its matrix-pipe work) wherever
+    the attention follows a fused-LN QKV projection
+    (:func:`ln_qkv_attention`), whose weights bound every key and value; a
+    bare :func:`attention_qkv` runs the x6 kernel."""
     global _ATTN_F32_VARIANT
-    x6 = {"x6": 0, "x6n": 1, "x6k1": 1, "x6k2": 2, "x6k3": 3, "x6k4": 4}
+    x6 = {"x6": 0, "x6n": 1, "x6k1": 1, "x6k2": 2, "x6k3": 3, "x6k4": 4,
+          "h3": 0, "h3n": 1, "h3k1": 1, "h3k2": 2, "h3k3": 3, "h3k4": 4}
     code = {"auto": 0, "w4k64": 1, "w4k64g2": 2, "w4k32": 3, "w2k64": 4, "w8k64": 5, "w4k32o4": 6,
             "w4k32g2": 7}.get(variant, 0)
     if variant not in x6 and code == 0 and variant != "auto":
@@ -331,7 +410,10 @@ def linear_ln(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Ten
         if K % 32:
             raise ValueError("native fp32 linear_ln needs K % 32 == 0")
         o2, _ = _gemm_io(x, wg, out, None, M, N, K)
-        if _F32_MATH == "x6":
+        if _F32_MATH == "h3":
+            ap, rinv = _split_rows_h3(x2, ln=True, eps=eps)
+            _gemm_h3(ap, rinv, wg, c2, None, o2, EPI_BIAS | _epi(None, act, None))
+        elif _F32_MATH == "x6":
             wp = split_f32_weight(wg)
             rc = _lib.lib().nos_gemm_ln_f32x6(x2.data_ptr(), x2.stride(0), wp.data_ptr(), wp.stride(1), wp.stride(0),
                                               c1.data_ptr(), c2.data_ptr(), o2.data_ptr(), o2.stride(0), M, N, K,
@@ -418,7 +500,7 @@ def attention_qkv(qkv: torch.Tensor, num_heads: int, out: torch.Tensor | None = 
     L = _lib.lib()
     args = (base, base + hd * es, base + 2 * hd * es, out.data_ptr(), B, num_heads, S, S, qkv.stride(1),
             qkv.stride(0), out.stride(1), out.stride(0), float(scale))
-    if qkv.dtype == torch.float32 and _ATTN_F32_VARIANT.startswith("x6"):
+    if qkv.dtype == torch.float32 and _ATTN_F32_VARIANT[:2] in ("x6", "h3"):
         # the split K/V planes: a stream-ordered allocation (graph-capture safe)
         nbytes = int(L.nos_attn_f32x6_workspace(B, num_heads, S, S))
         ws = torch.empty(nbytes // 2, dtype=torch.int16, device=qkv.device)
@@ -480,6 +562,111 @@ def attention_presplit(qkv: torch.Tensor, ws: torch.Tensor, num_heads: int, scal
     return out
 
 
+_H3_SCALES: dict[int, tuple] = {}
+
+
+@torch.no_grad()
+def h3_head_scales(wg: torch.Tensor, c2: torch.Tensor, num_heads: int) -> torch.Tensor:
+    """Per-head power-of-two scales [2, H] (K, V) for the fp16x3 attention's
+    planes, from the folded LN-QKV weights alone: the LayerNorm output x^ of
+    a row has ||x^||_2 <= sqrt(K), so every output column j obeys
+    |y_j| <= sqrt(K) ||wg_j||_2 + |c2_j|; each head's K and V get the scale
+    that puts that bound just under 2^14 (fp16 holds 65504).  Cached per
+    weight tensor and version, like :func:`split_f32_weight`."""
+    key = id(wg)
+    hit = _H3_SCALES.get(key)
+    if hit is not None:
+        ref, ver, ptr, sc = hit
+        if ref() is wg and ver == wg._version and ptr == wg.data_ptr():
+            return sc
+    import weakref
+
+    K = wg.shape[1]
+    hd = num_heads * 64
+    bound = math.sqrt(K) * wg.double().norm(dim=1) + c2.double().abs()
+    b = bound[hd:].view(2, num_heads, 64).amax(dim=2)                 # [K|V, head]
+    e = 14 - torch.frexp(b).exponent.to(torch.int64)                  # b < 2^exponent
+    e = torch.where(b > 0, e, torch.zeros_like(e)).clamp(-126, 126)
+    sc = torch.ldexp(torch.ones_like(b), e).float().contiguous().to(wg.device)
+    _H3_SCALES[key] = (weakref.ref(wg, lambda _r, k=key: _H3_SCALES.pop(k, None)), wg._version, wg.data_ptr(), sc)
+    return sc
+
+
+def linear_ln_qkv_h3(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, num_heads: int,
+                     eps: float = 1e-12) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """:func:`linear_ln_qkv_x6` writing the fp16x3 attention's planes (K and V
+    as fp16 hi / lo pieces on the per-head scales of :func:`h3_head_scales`):
+    returns (qkv with valid Q columns, workspace, scales) for
+    :func:`attention_presplit_h3`."""
+    B, S, K = x.shape
+    N = wg.shape[0]
+    if N != 3 * num_heads * 64 or x.dtype != torch.float32 or not x.is_cuda:
+        raise ValueError("linear_ln_qkv_h3: fp32 CUDA input and a [3*H*64, K] projection")
+    _check_f32(x=x, weight=wg, c1=c1, c2=c2)
+    if K % 32:
+        raise ValueError("linear_ln_qkv_h3 needs K % 32 == 0")
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    out = torch.empty((B, S, N), dtype=torch.float32, device=x.device)
+    L = _lib.lib()
+    nbytes = int(L.nos_attn_f32x6_workspace(B, num_heads, S, S))
+    ws = torch.empty(nbytes // 2, dtype=torch.int16, device=x.device)
+    skvp = (S + 31) // 32 * 32
+    sc = h3_head_scales(wg, c2, num_heads)
+    if _F32_MATH == "h3":
+        ap, rinv = _split_rows_h3(x2, ln=True, eps=eps)
+        _gemm_h3(ap, rinv, wg, c2, None, out.view(M, N), EPI_BIAS, kv=(ws, S, skvp, sc))
+        return out, ws, sc
+    wp = split_f32_weight(wg)
+    rc = L.nos_gemm_ln_f32x6_qkv_h3(x2.data_ptr(), x2.stride(0), wp.data_ptr(), wp.stride(1), wp.stride(0),
+                                    c1.data_ptr(), c2.data_ptr(), out.data_ptr(), N, M, N, K, 0, float(eps),
+                                    ws.data_ptr(), S, skvp, sc.data_ptr(), _stream())
+    _lib.check(rc, "nos_gemm_ln_f32x6_qkv_h3")
+    return out, ws, sc
+
+
+def attention_presplit_h3(qkv: torch.Tensor, ws: torch.Tensor, scales: torch.Tensor, num_heads: int,
+                          scale: float | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """fp16x3 attention from the planes :func:`linear_ln_qkv_h3` wrote."""
+    B, S, three_hd = qkv.shape
+    hd = three_hd // 3
+    if out is None:
+        out = torch.empty((B, S, hd), dtype=torch.float32, device=qkv.device)
+    if out.dtype != torch.float32 or out.stride(-1) != 1 or out.shape != (B, S, hd):
+        raise ValueError("out must be [B, S, H*64] fp32 with unit inner stride")
+    if scales.shape != (2, num_heads) or scales.dtype != torch.float32 or not scales.is_contiguous():
+        raise ValueError("scales must be the [2, H] fp32 tensor of linear_ln_qkv_h3")
+    scale = scale if scale is not None else 1.0 / math.sqrt(64)
+    rc = _lib.lib().nos_attn_fwd_f32h3_presplit_d64(qkv.data_ptr(), out.data_ptr(), B, num_heads, S, S,
+                                                    qkv.stride(1), qkv.stride(0), out.stride(1), out.stride(0),
+                                                    float(scale), scales.data_ptr(), ws.data_ptr(),
+                                                    ws.numel() * ws.element_size(), _stream())
+    _lib.check(rc, "nos_attn_fwd_f32h3_presplit_d64")
+    return out
+
+
+def ln_qkv_fusable(x: torch.Tensor) -> bool:
+    """Whether :func:`ln_qkv_attention` runs fused for this input: an fp32 pod
+    on the GPU under x6 math and an x6 / h3 attention variant."""
+    return (x.is_cuda and x.dtype == torch.float32 and _F32_MATH in ("x6", "h3")
+            and _ATTN_F32_VARIANT[:2] in ("x6", "h3"))
+
+
+def ln_qkv_attention(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, num_heads: int,
+                     eps: float = 1e-12) -> torch.Tensor:
+    """attention(LayerNorm(x) @ W_qkv^T + b) for an fp32 pod (see
+    :func:`ln_qkv_fusable`): the QKV projection writes the attention's K / V
+    planes straight from its epilogue -- fp16x3 planes under an ``h3``
+    variant, bf16x6 planes otherwise."""
+    if _ATTN_F32_VARIANT.startswith("h3"):
+        qkv, ws, sc = linear_ln_qkv_h3(x, wg, c1, c2, num_heads, eps=eps)
+        return attention_presplit_h3(qkv, ws, sc, num_heads)
+    if _F32_MATH == "h3":  # x6 attention after an h3 projection: the unfused pair
+        return attention_qkv(linear_ln(x, wg, c1, c2, eps=eps), num_heads)
+    qkv, ws = linear_ln_qkv_x6(x, wg, c1, c2, num_heads, eps=eps)
+    return attention_presplit(qkv, ws, num_heads)
+
+
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None,
               out: torch.Tensor | None = None) -> torch.Tensor:
     """q,k,v [B, S, H, 64] (rows contiguous per token) -> [B, Sq, H, 64]."""
@@ -504,5 +691,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_f32_math", "f32_math", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

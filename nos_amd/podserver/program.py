@@ -685,10 +685,8 @@ class CompiledProgram:
                 y = ops.linear_ln(a[0].contiguous(), a[1], a[2], a[3], act=s.attrs.get("act"), eps=s.attrs["eps"])
             elif k == "ln_qkv_attention":
                 h = a[0].contiguous()
-                if (h.is_cuda and h.dtype.itemsize == 4 and ops.f32_math() == "x6"
-                        and ops.attention_f32_variant().startswith("x6")):
-                    qkv, ws = ops.linear_ln_qkv_x6(h, a[1], a[2], a[3], s.attrs["heads"], eps=s.attrs["eps"])
-                    y = ops.attention_presplit(qkv, ws, s.attrs["heads"])
+                if ops.ln_qkv_fusable(h):
+                    y = ops.ln_qkv_attention(h, a[1], a[2], a[3], s.attrs["heads"], eps=s.attrs["eps"])
                 else:
                     qkv = ops.linear_ln(h, a[1], a[2], a[3], eps=s.attrs["eps"])
                     y = ops.attention_qkv(qkv, s.attrs["heads"])

@@ -55,7 +55,7 @@ def main():
                     "(throughput, latency)")
     ap.add_argument("--x6-tile", type=int, default=-1, help="x6 GEMM tile override (3: 128x64 4x1 waves)")
     ap.add_argument("--stage", type=int, default=0, help="x6 GEMM K-stage config (1: BK32 3-deep, 2: BK64)")
-    ap.add_argument("--f32-math", default="exact", choices=["exact", "x6"], help="fp32 GEMM math (ops.set_f32_math)")
+    ap.add_argument("--f32-math", default="exact", choices=["exact", "x6", "h3"], help="fp32 GEMM math (ops.set_f32_math)")
     ap.add_argument("--attn-f32", default="x6n,x6", help="fp32 attention variants to time (--dtype fp32)")
     ap.add_argument("--pipeline", type=int, default=1, help="x6 GEMM software-pipelined K loop (1) or plain (0)")
     a = ap.parse_args()
