@@ -656,7 +656,8 @@ def main(argv=None) -> int:
     kc = next((p.info.get("kernel_config") for p in w.inference_pods if p.info.get("kernel_config")), None) or {}
     f32_math = kc.get("f32_math") if args.dtype == "fp32" else None
     # matrix-pipe FLOPs per model FLOP and the pipe's FLOP per clock per SIMD
-    pipe_flops_per_flop, pipe_rate = (6, 1024) if f32_math == "x6" else (1, 64 if args.dtype == "fp32" else 1024)
+    pipe_flops_per_flop, pipe_rate = ({"x6": 6, "h3": 3}[f32_math], 1024) if f32_math in ("x6", "h3") else \
+        (1, 64 if args.dtype == "fp32" else 1024)
     result = {
         "metric": METRIC,
         "value": value,
@@ -711,14 +712,17 @@ def main(argv=None) -> int:
         "mean_latency_s": None if lat is None else round(lat, 5),
         "window_s": round(elapsed, 3),
         "achieved_tflops": round(agg * flops_per_image(cfg, hw) / 1e12, 2),
-        # how the fp32 pods multiply: "x6" = bf16x6 split (fp32 operands as three
-        # exact bf16 pieces, six piece products per product on the bf16 MFMA,
-        # error vs fp64 <= the exact-f32 MFMA's: tests/test_kernels_gpu.py),
+        # how the fp32 pods multiply: "h3" = fp16x3 split (two fp16 pieces per
+        # operand on power-of-two scales, three products per product on the
+        # fp16 MFMA), "x6" = bf16x6 split (three exact bf16 pieces, six
+        # products on the bf16 MFMA) -- both with errors vs fp64 <= the
+        # exact-f32 MFMA's (tests/test_gemm_h3_gpu.py, test_kernels_gpu.py) --
         # "exact" = v_mfma_f32_32x32x2_f32
         "f32_math": f32_math,
         # the share of the matrix pipes' peak at the measured clock that the
         # executed MFMAs use (256 CUs x 4 SIMDs x 64 fp32 / 1024 bf16 FLOP per
-        # clock; an x6 fp32 FLOP costs six bf16 FLOPs): amd-smi's gfx activity
+        # clock; an x6 fp32 FLOP costs six bf16 FLOPs, an h3 one three fp16
+        # FLOPs at the same rate): amd-smi's gfx activity
         # reads 100 % whenever any kernel runs, this does not
         "matrix_pipe_util_pct": (round(100.0 * agg * flops_per_image(cfg, hw) * pipe_flops_per_flop /
                                        (world * 256 * 4 * pipe_rate * w.sclk_mhz * 1e6), 1)

@@ -146,8 +146,14 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
     when its grid leaves CU slots empty (``x6``: batch-1 attention 164 -> 133
     us); fractional pods never split (``x6n``: the co-tenants fill the slots,
     8 pods 410 vs 399 inf/s with the split) and run the x6 GEMMs on 128x128
-    tiles with 4 x 1 waves (466 vs 448 for 128x64 and 425 for 64x64 tiles).  ``NOS_AMD_F32_MATH=exact`` /
-    ``NOS_AMD_ATTN_F32_VARIANT=<tiling>`` select the exact-f32 MFMA kernels."""
+    tiles with 4 x 1 waves (466 vs 448 for 128x64 and 425 for 64x64 tiles).  Since then the
+    default is the fp16x3 split (``h3``: two fp16 pieces per operand on
+    power-of-two scales, three fp16 MFMAs per product, errors vs fp64 at or
+    below the exact-f32 kernels'): 28-tenant fleet 482 (x6) -> 640 inf/s
+    (profiles/r04_h3_fleet_ab.json); ``h3`` splits keys for a whole-GPU pod,
+    ``h3n`` never.  ``NOS_AMD_F32_MATH=x6|exact`` /
+    ``NOS_AMD_ATTN_F32_VARIANT=x6|<tiling>`` select the bf16x6 or exact-f32
+    MFMA kernels."""
     env = os.environ if env is None else env
     whole = memory_fraction is None or memory_fraction >= 0.99
     if cu_budget and not whole:
@@ -156,8 +162,8 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
         gf = "latency" if whole else "small"
     return {"gemm_bf16": env.get("NOS_AMD_GEMM_POLICY") or ("latency" if whole else "throughput"),
             "gemm_f32": env.get("NOS_AMD_GEMM_F32_POLICY") or gf,
-            "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or ("x6" if whole else "x6n"),
-            "f32_math": env.get("NOS_AMD_F32_MATH") or "x6",
+            "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or ("h3" if whole else "h3n"),
+            "f32_math": env.get("NOS_AMD_F32_MATH") or "h3",
             "gemm_f32x6_tile": env.get("NOS_AMD_X6_TILE") or ("policy" if whole else "128x128")}
 
 

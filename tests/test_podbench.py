@@ -137,15 +137,15 @@ def test_pod_kernel_config_follows_the_slice():
     from nos_amd.models.pod import kernel_config
 
     whole = kernel_config(None, {})
-    assert whole == {"gemm_bf16": "latency", "gemm_f32": "latency", "attention_f32": "x6", "f32_math": "x6",
+    assert whole == {"gemm_bf16": "latency", "gemm_f32": "latency", "attention_f32": "h3", "f32_math": "h3",
                      "gemm_f32x6_tile": "policy"}
     assert kernel_config(1.0, {}) == whole
     frac = kernel_config(36 / 288, {})
-    assert frac == {"gemm_bf16": "throughput", "gemm_f32": "small", "attention_f32": "x6n", "f32_math": "x6",
+    assert frac == {"gemm_bf16": "throughput", "gemm_f32": "small", "attention_f32": "h3n", "f32_math": "h3",
                     "gemm_f32x6_tile": "128x128"}
     # an exclusive CU-mask slice plans for its own CUs (budget-aware tiles)
     assert kernel_config(36 / 288, {}, cu_budget=32) == {"gemm_bf16": "throughput", "gemm_f32": "latency",
-                                                         "attention_f32": "x6n", "f32_math": "x6",
+                                                         "attention_f32": "h3n", "f32_math": "h3",
                                                          "gemm_f32x6_tile": "128x128"}
     assert kernel_config(None, {}, cu_budget=32) == whole
     # A/B overrides win over the slice rule: the exact-f32 MFMA kernels stay selectable
