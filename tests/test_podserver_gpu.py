@@ -134,17 +134,20 @@ def test_a_tenant_larger_than_its_slice_is_refused(server):
 
     c = PodClient(server.path, connect_timeout_s=10)
     prog = _yolos(0)
-    with pytest.raises(PodServerError, match="slice has 0.05 GB"):  # the static estimate
+    # weights (~0.09 GB) larger than the slice: refused before they are read
+    with pytest.raises(PodServerError, match="PayloadTooLarge"):
         c.register("tiny-slice", *prog, memory_limit_gb=0.05)
+    with pytest.raises(PodServerError, match="slice has 0.2 GB"):  # the static estimate
+        c.register("tiny-slice", *prog, memory_limit_gb=0.2)
     # past the estimate, the measured peak of the build decides: an estimate
-    # of 0 lets the build run, and the real footprint refuses it
+    # of 0 lets the build run, and the real footprint (~0.47 GB) refuses it
     import nos_amd.podserver.program as PG
 
     orig = PG.Program.bytes_estimate
     try:
         PG.Program.bytes_estimate = property(lambda self: 0)
-        with pytest.raises(PodServerError, match="slice has 0.05 GB"):
-            c.register("tiny-slice", *prog, memory_limit_gb=0.05)
+        with pytest.raises(PodServerError, match="slice has 0.2 GB"):
+            c.register("tiny-slice", *prog, memory_limit_gb=0.2)
     finally:
         PG.Program.bytes_estimate = orig
     assert not server.tenants and server.stats()["pending"] == 0
