@@ -331,7 +331,7 @@ template <bool PERSIST>
 __global__ __launch_bounds__(NT, H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
     const float* __restrict__ q, const _Float16* __restrict__ kvs, float* __restrict__ o, int B, int H, int Sq,
     int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, const float* __restrict__ kvsc,
-    int nqb, int nsplit, float* __restrict__ part) {
+    int nqb, int nsplit, float* __restrict__ part, _Float16* __restrict__ op, long long opl, float osc) {
   const int ldh = H * D;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(NT, H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
     }
     const float inv = vinv / lt;
     if (qrow < Sq) {
-      float* op = o + (long long)b * bs_out + (long long)qrow * ld_out + hd * D;
+      const long long ob = (long long)b * bs_out + (long long)qrow * ld_out + hd * D;
 #pragma unroll
       for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -551,7 +551,17 @@ __global__ __launch_bounds__(NT, H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
           y.y = oacc[db][4 * g + 1] * inv;
           y.z = oacc[db][4 * g + 2] * inv;
           y.w = oacc[db][4 * g + 3] * inv;
-          *reinterpret_cast<float4*>(op + 32 * db + 8 * g + 4 * hh) = y;
+          const int d = 32 * db + 8 * g + 4 * hh;
+          if (op != nullptr) {  // the proj GEMM's A planes on the static scale osc
+            f16x2_t h01, l01, h23, l23;
+            nos::split2h(f32x2_t{y.x * osc, y.y * osc}, h01, l01);
+            nos::split2h(f32x2_t{y.z * osc, y.w * osc}, h23, l23);
+            typedef __attribute__((ext_vector_type(4))) _Float16 f16x4_t;
+            *reinterpret_cast<f16x4_t*>(op + ob + d) = f16x4_t{h01.x, h01.y, h23.x, h23.y};
+            *reinterpret_cast<f16x4_t*>(op + opl + ob + d) = f16x4_t{l01.x, l01.y, l23.x, l23.y};
+          } else {
+            *reinterpret_cast<float4*>(o + ob + d) = y;
+          }
         }
     }
   }  // items
@@ -625,7 +635,9 @@ int pick_split(long long nwg1, int ntiles, int wg_per_cu = WG_PER_CU) {
 // sum_i l_i 2^(m_i - M), M = max_i m_i (m in log2 units, O_i unnormalised)
 __global__ __launch_bounds__(256) void merge_splits_kernel(const float* __restrict__ part, float* __restrict__ o,
                                                            int B, int H, int Sq, int nsplit, int ld_out,
-                                                           long long bs_out, long long n4) {
+                                                           long long bs_out, long long n4,
+                                                           _Float16* __restrict__ op = nullptr, long long opl = 0,
+                                                           float osc = 1.f) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n4) return;
   const int ldh = H * D;
@@ -650,8 +662,17 @@ __global__ __launch_bounds__(256) void merge_splits_kernel(const float* __restri
   }
   const float inv = 1.f / L;
   const long long b = row / Sq, s = row - b * Sq;
-  *reinterpret_cast<float4*>(o + b * bs_out + s * ld_out + col) = float4{acc.x * inv, acc.y * inv, acc.z * inv,
-                                                                          acc.w * inv};
+  const float4 y = float4{acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv};
+  if (op != nullptr) {
+    f16x2_t h01, l01, h23, l23;
+    nos::split2h(f32x2_t{y.x * osc, y.y * osc}, h01, l01);
+    nos::split2h(f32x2_t{y.z * osc, y.w * osc}, h23, l23);
+    typedef __attribute__((ext_vector_type(4))) _Float16 f16x4_t;
+    *reinterpret_cast<f16x4_t*>(op + b * bs_out + s * ld_out + col) = f16x4_t{h01.x, h01.y, h23.x, h23.y};
+    *reinterpret_cast<f16x4_t*>(op + opl + b * bs_out + s * ld_out + col) = f16x4_t{l01.x, l01.y, l23.x, l23.y};
+    return;
+  }
+  *reinterpret_cast<float4*>(o + b * bs_out + s * ld_out + col) = y;
 }
 
 }  // namespace
@@ -739,15 +760,15 @@ namespace {
 
 int launch_h3(const float* q, const _Float16* kvs, float* o, int B, int H, int Sq, int Skv, int ld_in,
               long long bs_in, int ld_out, long long bs_out, float c, const float* kvsc, int nqb, int nsplit,
-              float* part, hipStream_t stream) {
+              float* part, _Float16* op, long long opl, float osc, hipStream_t stream) {
   const long long nwg = (long long)B * H * nqb * nsplit;
   const int grid = nos_grid_for((const void*)attn_fwd_f32h3_d64_kernel<true>, NT, H3_LDS_BYTES, nwg);
   if (grid < nwg)
     hipLaunchKernelGGL((attn_fwd_f32h3_d64_kernel<true>), dim3((unsigned)grid), dim3(NT), H3_LDS_BYTES, stream, q,
-                       kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit, part);
+                       kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit, part, op, opl, osc);
   else
     hipLaunchKernelGGL((attn_fwd_f32h3_d64_kernel<false>), dim3((unsigned)nwg), dim3(NT), H3_LDS_BYTES, stream, q,
-                       kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit, part);
+                       kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit, part, op, opl, osc);
   return (int)hipGetLastError();
 }
 
@@ -757,11 +778,20 @@ int launch_h3(const float* q, const _Float16* kvs, float* o, int B, int H, int S
 // projection's epilogue wrote at the start of ws (nos_gemm_ln_f32x6_qkv_h3)
 // on the per-head scales kvsc [2][H] (K, then V; powers of two).  Same
 // contract and workspace as nos_attn_fwd_f32x6_presplit_d64.
+//
+// oplanes != nullptr: the output goes, instead of o, to the next h3 GEMM's A
+// planes (hi at oplanes, lo at oplanes + opl elements, same row / batch
+// strides as o) on the static scale osc (the host's bound of |O|: every O
+// row is a convex combination of V rows); o is then only checked for shape.
 NOS_API int nos_attn_fwd_f32h3_presplit_d64(const float* q, float* o, int B, int H, int Sq, int Skv, int ld_in,
                                             long long bs_in, int ld_out, long long bs_out, float scale,
-                                            const float* kvsc, void* ws, long long ws_bytes, hipStream_t stream) {
+                                            const float* kvsc, void* ws, long long ws_bytes, void* oplanes,
+                                            long long opl, float osc, hipStream_t stream) {
   if (int rc = check_args(q, o, ws, ws_bytes, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out)) return rc;
   if (kvsc == nullptr) return (int)hipErrorInvalidValue;
+  auto* op = static_cast<_Float16*>(oplanes);
+  if (op != nullptr && ((((uintptr_t)op) & 7) || opl < (long long)B * bs_out || !(osc > 0.f)))
+    return (int)hipErrorInvalidValue;
   const float c = scale * 1.4426950408889634f;
   const int nqb = (Sq + QBLK - 1) / QBLK;
   const long long nwg = (long long)B * H * nqb;
@@ -771,10 +801,10 @@ NOS_API int nos_attn_fwd_f32h3_presplit_d64(const float* q, float* o, int B, int
   float* part = reinterpret_cast<float*>(static_cast<unsigned char*>(ws) +
                                          ((long long)B * skvp * 6 * H * D * 2 + 15) / 16 * 16);
   const int rc = launch_h3(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit, part,
-                           stream);
+                           op, opl, osc, stream);
   if (rc != 0 || nsplit == 1) return rc;
   const long long n4 = (long long)B * Sq * H * (D / 4);
   hipLaunchKernelGGL(merge_splits_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, part, o, B, H, Sq,
-                     nsplit, ld_out, bs_out, n4);
+                     nsplit, ld_out, bs_out, n4, op, opl, osc);
   return (int)hipGetLastError();
 }

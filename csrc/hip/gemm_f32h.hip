@@ -58,12 +58,22 @@ struct KvOut {
   int qcols = 0, hd = 0, S = 0, skvp = 0;
 };
 
+// the output as the NEXT h3 GEMM's A planes ([2][M][ldp], plane stride
+// pplane) on the static scale sc (the host's bound of this output: fc1's
+// GELU rows feeding fc2), instead of fp32 C
+struct PlaneOut {
+  unsigned short* p = nullptr;
+  long long pplane = 0;
+  int ldp = 0;
+  float sc = 1.f;
+};
+
 template <int BM, int BN, int WGM, int WGN, bool PERSIST>
 __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_h3_kernel(
-    const _Float16* __restrict__ Ap, int lda, long long aplane, const float* __restrict__ rinv,
+    const _Float16* __restrict__ Ap, int lda, long long aplane, const float* __restrict__ rinv, float rconst,
     const _Float16* __restrict__ Wp, int ldw, long long wplane, const float* __restrict__ csc,
     const float* __restrict__ bias, const float* __restrict__ R, int ldr, float* __restrict__ C, int ldc, int M,
-    int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv) {
+    int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv, PlaneOut po) {
   constexpr int NW = WGM * WGN, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
   static_assert(NW == 4 && MI >= 1 && NI >= 1, "4 waves");
   constexpr int TA = 2 * BM * ROWB, STAGE = TA + 2 * BN * ROWB;
@@ -186,7 +196,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_h3_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        rsv[i][r] = rinv[m < M ? m : M - 1];
+        rsv[i][r] = rinv != nullptr ? rinv[m < M ? m : M - 1] : rconst;
       }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -215,6 +225,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_h3_kernel(
               unsigned short* dst = kv.kvs + (row * 4 + 2 * t) * kv.hd + col;
               dst[0] = __builtin_bit_cast(unsigned short, h0);
               dst[kv.hd] = __builtin_bit_cast(unsigned short, h1);
+            } else if (po.p != nullptr) {
+              const float x = v * po.sc;
+              const _Float16 h0 = (_Float16)x;
+              const _Float16 h1 = (_Float16)(x - (float)h0);
+              po.p[(long long)m * po.ldp + n] = __builtin_bit_cast(unsigned short, h0);
+              po.p[po.pplane + (long long)m * po.ldp + n] = __builtin_bit_cast(unsigned short, h1);
             } else {
               C[(long long)m * ldc + n] = v;
             }
@@ -226,9 +242,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_h3_kernel(
 }
 
 template <int BM, int BN, int WGM, int WGN>
-int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, const _Float16* Wp, int ldw,
-             long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C, int ldc, int M,
-             int N, int K, int epi, KvOut kv, hipStream_t st) {
+int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, float rconst, const _Float16* Wp,
+             int ldw, long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C, int ldc,
+             int M, int N, int K, int epi, KvOut kv, PlaneOut po, hipStream_t st) {
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const long long ntiles = (long long)tiles_m * tiles_n;
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
@@ -236,43 +252,70 @@ int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, c
   const int grid = nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true>, 256, lds, ntiles);
   if (grid < ntiles)
     hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true>), dim3((unsigned)grid), dim3(256), lds, st, Ap, lda,
-                       aplane, rinv, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m, tiles_n, kv);
+                       aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
+                       tiles_n, kv, po);
   else
     hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false>), dim3((unsigned)ntiles), dim3(256), lds, st, Ap,
-                       lda, aplane, rinv, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m, tiles_n,
-                       kv);
+                       lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
+                       tiles_n, kv, po);
   return (int)hipGetLastError();
 }
 
 int g_layout = 0;  // 0: 4 x 1 waves, 1: 2 x 2 waves (nos_gemm_f32h3_set_layout)
 
 // ------------------------------------------------------------ row split
-// One wave per row: the row's scale (max |a|, or in LayerNorm mode the
-// sqrt(K) bound of a normalised row), then its hi / lo planes.  K % 8 == 0.
+// One wave per row, the whole row in registers (F4 float4s per lane: K <=
+// 256 F4): one read of the row, its scale (max |a|, or in LayerNorm mode
+// the mean / variance and the host's sqrt(K) bound of a normalised row),
+// then its hi / lo planes.  F4 = 0: rows longer than 4096, re-read per pass.
+template <int F4>
 __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restrict__ A, int lda,
                                                             _Float16* __restrict__ P, int ldp, long long pplane,
                                                             float* __restrict__ rinv, int M, int K, int ln,
                                                             float eps, int eln) {
+  typedef __attribute__((ext_vector_type(4))) _Float16 f16x4_t;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= M) return;
   const float* a = A + (long long)row * lda;
+  constexpr int NR = F4 > 0 ? F4 : 1;
+  float4 v[NR];
+  auto get = [&](int i, int k) -> float4 {  // chunk i of this lane (k = its first column)
+    if constexpr (F4 > 0) return v[i];
+    return *reinterpret_cast<const float4*>(a + k);
+  };
+  const int nchunk = F4 > 0 ? F4 : (K + 255) / 256;
+  if constexpr (F4 > 0) {
+#pragma unroll
+    for (int i = 0; i < F4; ++i) {
+      const int k = (lane + 64 * i) * 4;
+      v[i] = k < K ? *reinterpret_cast<const float4*>(a + k) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
   float mu = 0.f, rs = 1.f;
   int e;
   if (ln) {
     float s = 0.f;
-    for (int k = lane * 4; k < K; k += 256) {
-      const float4 v = *reinterpret_cast<const float4*>(a + k);
-      s += (v.x + v.y) + (v.z + v.w);
+#pragma unroll
+    for (int i = 0; i < nchunk; ++i) {
+      const int k = (lane + 64 * i) * 4;
+      if (k < K) {
+        const float4 x = get(i, k);
+        s += (x.x + x.y) + (x.z + x.w);
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     mu = s / (float)K;
     float q = 0.f;
-    for (int k = lane * 4; k < K; k += 256) {
-      const float4 v = *reinterpret_cast<const float4*>(a + k);
-      const float d0 = v.x - mu, d1 = v.y - mu, d2 = v.z - mu, d3 = v.w - mu;
-      q = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, q))));
+#pragma unroll
+    for (int i = 0; i < nchunk; ++i) {
+      const int k = (lane + 64 * i) * 4;
+      if (k < K) {
+        const float4 x = get(i, k);
+        const float d0 = x.x - mu, d1 = x.y - mu, d2 = x.z - mu, d3 = x.w - mu;
+        q = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, q))));
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
@@ -280,9 +323,13 @@ __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restr
     e = eln;  // |x^| <= sqrt(K): the host's exponent for it
   } else {
     float mx = 0.f;
-    for (int k = lane * 4; k < K; k += 256) {
-      const float4 v = *reinterpret_cast<const float4*>(a + k);
-      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+#pragma unroll
+    for (int i = 0; i < nchunk; ++i) {
+      const int k = (lane + 64 * i) * 4;
+      if (k < K) {
+        const float4 x = get(i, k);
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
@@ -292,14 +339,17 @@ __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restr
   const float mul = rs * sc, add = -mu * mul;
   _Float16* ph = P + (long long)row * ldp;
   _Float16* pl = ph + pplane;
-  for (int k = lane * 4; k < K; k += 256) {
-    const float4 v = *reinterpret_cast<const float4*>(a + k);
-    f16x2_t h01, l01, h23, l23;
-    nos::split2h(f32x2_t{fmaf(v.x, mul, add), fmaf(v.y, mul, add)}, h01, l01);
-    nos::split2h(f32x2_t{fmaf(v.z, mul, add), fmaf(v.w, mul, add)}, h23, l23);
-    typedef __attribute__((ext_vector_type(4))) _Float16 f16x4_t;
-    *reinterpret_cast<f16x4_t*>(ph + k) = f16x4_t{h01.x, h01.y, h23.x, h23.y};
-    *reinterpret_cast<f16x4_t*>(pl + k) = f16x4_t{l01.x, l01.y, l23.x, l23.y};
+#pragma unroll
+  for (int i = 0; i < nchunk; ++i) {
+    const int k = (lane + 64 * i) * 4;
+    if (k < K) {
+      const float4 x = get(i, k);
+      f16x2_t h01, l01, h23, l23;
+      nos::split2h(f32x2_t{fmaf(x.x, mul, add), fmaf(x.y, mul, add)}, h01, l01);
+      nos::split2h(f32x2_t{fmaf(x.z, mul, add), fmaf(x.w, mul, add)}, h23, l23);
+      *reinterpret_cast<f16x4_t*>(ph + k) = f16x4_t{h01.x, h01.y, h23.x, h23.y};
+      *reinterpret_cast<f16x4_t*>(pl + k) = f16x4_t{l01.x, l01.y, l23.x, l23.y};
+    }
   }
   if (lane == 0) rinv[row] = nos::pow2i(-e);
 }
@@ -323,29 +373,45 @@ NOS_API int nos_split_rows_h3(const float* A, int lda, void* P, int ldp, long lo
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)A) | ((uintptr_t)P)) & 15) return (int)hipErrorInvalidValue;
   if (eln < -126 || eln > 126) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(split_rows_h3_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, stream, A, lda,
-                     static_cast<_Float16*>(P), ldp, pplane, rinv, M, K, ln, eps, eln);
+  auto* p = static_cast<_Float16*>(P);
+  const dim3 grid((unsigned)((M + 3) / 4)), blk(256);
+  if (K <= 512)
+    hipLaunchKernelGGL(split_rows_h3_kernel<2>, grid, blk, 0, stream, A, lda, p, ldp, pplane, rinv, M, K, ln, eps, eln);
+  else if (K <= 1024)
+    hipLaunchKernelGGL(split_rows_h3_kernel<4>, grid, blk, 0, stream, A, lda, p, ldp, pplane, rinv, M, K, ln, eps, eln);
+  else if (K <= 2048)
+    hipLaunchKernelGGL(split_rows_h3_kernel<8>, grid, blk, 0, stream, A, lda, p, ldp, pplane, rinv, M, K, ln, eps, eln);
+  else if (K <= 4096)
+    hipLaunchKernelGGL(split_rows_h3_kernel<16>, grid, blk, 0, stream, A, lda, p, ldp, pplane, rinv, M, K, ln, eps,
+                       eln);
+  else
+    hipLaunchKernelGGL(split_rows_h3_kernel<0>, grid, blk, 0, stream, A, lda, p, ldp, pplane, rinv, M, K, ln, eps, eln);
   return (int)hipGetLastError();
 }
 
 // C = act(rinv[m] csc[n] (A' . W'^T) + bias) (+ R) on the fp16 planes of A
-// (nos_split_rows_h3) and W ([2][N][K], ldw, plane stride wplane; row scales
-// csc).  kvs != nullptr: a fused QKV projection (N = 3 hd) whose K / V
-// columns go to the h3 attention's planes (S rows per batch padded to skvp,
-// per-head scales kvsc [2][hd / 64]); Q to C.  K % 32 == 0.
-NOS_API int nos_gemm_f32h3(const void* Ap, int lda, long long aplane, const float* rinv, const void* Wp, int ldw,
-                           long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C,
-                           int ldc, int M, int N, int K, int epi, void* kvs, int S, int skvp, const float* kvsc,
+// (nos_split_rows_h3, or a producer's plane output; rinv == nullptr: every
+// row's inverse scale is rconst) and W ([2][N][K], ldw, plane stride wplane;
+// row scales csc).  kvs != nullptr: a fused QKV projection (N = 3 hd) whose
+// K / V columns go to the h3 attention's planes (S rows per batch padded to
+// skvp, per-head scales kvsc [2][hd / 64]); Q to C.  P != nullptr: the
+// output as the next h3 GEMM's A planes ([2][M][ldp], plane stride pplane)
+// on the scale psc, instead of C.  K % 32 == 0.
+NOS_API int nos_gemm_f32h3(const void* Ap, int lda, long long aplane, const float* rinv, float rconst,
+                           const void* Wp, int ldw, long long wplane, const float* csc, const float* bias,
+                           const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi, void* kvs, int S,
+                           int skvp, const float* kvsc, void* P, int ldp, long long pplane, float psc,
                            hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0) return (int)hipErrorInvalidValue;
   if ((lda % 8) || (ldw % 8) || lda < K || ldw < K || aplane < (long long)M * lda || wplane < (long long)N * ldw)
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)Ap) | ((uintptr_t)Wp)) & 15) return (int)hipErrorInvalidValue;
-  if (!rinv || !csc || ((epi & EPI_BIAS) && !bias) || ((epi & EPI_RESID) && (!R || ldr < N)))
+  if ((!rinv && !(rconst > 0.f)) || !csc || ((epi & EPI_BIAS) && !bias) || ((epi & EPI_RESID) && (!R || ldr < N)))
     return (int)hipErrorInvalidValue;
   KvOut kv;
+  PlaneOut po;
   if (kvs != nullptr) {
-    if (!kvsc || N % 3 || (N / 3) % 64 || S <= 0 || M % S || skvp < S || (((uintptr_t)kvs) & 15))
+    if (!kvsc || N % 3 || (N / 3) % 64 || S <= 0 || M % S || skvp < S || (((uintptr_t)kvs) & 15) || P)
       return (int)hipErrorInvalidValue;
     kv.kvs = static_cast<unsigned short*>(kvs);
     kv.kvsc = kvsc;
@@ -353,14 +419,21 @@ NOS_API int nos_gemm_f32h3(const void* Ap, int lda, long long aplane, const floa
     kv.qcols = kv.hd;
     kv.S = S;
     kv.skvp = skvp;
-  } else if (ldc < N) {
+  }
+  if (P != nullptr) {
+    if (ldp < N || pplane < (long long)M * ldp || !(psc > 0.f)) return (int)hipErrorInvalidValue;
+    po.p = static_cast<unsigned short*>(P);
+    po.ldp = ldp;
+    po.pplane = pplane;
+    po.sc = psc;
+  } else if (ldc < (kvs != nullptr ? N / 3 : N)) {
     return (int)hipErrorInvalidValue;
   }
   const auto* a = static_cast<const _Float16*>(Ap);
   const auto* w = static_cast<const _Float16*>(Wp);
   if (g_layout == 1)
-    return launch_t<128, 128, 2, 2>(a, lda, aplane, rinv, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, kv,
-                                    stream);
-  return launch_t<128, 128, 4, 1>(a, lda, aplane, rinv, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, kv,
-                                  stream);
+    return launch_t<128, 128, 2, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
+                                    epi, kv, po, stream);
+  return launch_t<128, 128, 4, 1>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
+                                  epi, kv, po, stream);
 }

@@ -178,15 +178,24 @@ class YolosDetector(nn.Module):
         # fp32 under x6 math: the QKV projection writes K / V as the attention's
         # bf16x6 / fp16x3 planes directly (no fp32 K/V round trip, no split kernel)
         presplit = ops.ln_qkv_fusable(h)
+        # h3 math: attention -> proj and fc1 -> fc2 hand their activations
+        # over as the consumer GEMM's fp16 planes (no fp32 round trip, no split pass)
+        handoff = presplit and ops.h3_planes_active(attention=True)
+        mlp_handoff = h.is_cuda and h.dtype == torch.float32 and ops.h3_planes_active()
         for L, fw in zip(self.layers, folded):
             if presplit:
-                a = ops.ln_qkv_attention(h, fw["qkv_w"], fw["qkv_c1"], fw["qkv_c2"], nh, eps=eps)
+                a = ops.ln_qkv_attention(h, fw["qkv_w"], fw["qkv_c1"], fw["qkv_c2"], nh, eps=eps, planes_out=handoff)
             else:
                 qkv = ops.linear_ln(h, fw["qkv_w"], fw["qkv_c1"], fw["qkv_c2"], eps=eps)
                 a = ops.attention_qkv(qkv, nh)
-            h = ops.linear(a, L.proj_w, L.proj_b, residual=h)
-            m = ops.linear_ln(h, fw["fc1_w"], fw["fc1_c1"], fw["fc1_c2"], act="gelu", eps=eps)
-            h = ops.linear(m, L.fc2_w, L.fc2_b, residual=h)
+            h = (ops.linear_planes(a, L.proj_w, L.proj_b, residual=h) if handoff
+                 else ops.linear(a, L.proj_w, L.proj_b, residual=h))
+            if mlp_handoff:
+                m = ops.linear_ln_to_planes(h, fw["fc1_w"], fw["fc1_c1"], fw["fc1_c2"], act="gelu", eps=eps)
+                h = ops.linear_planes(m, L.fc2_w, L.fc2_b, residual=h)
+            else:
+                m = ops.linear_ln(h, fw["fc1_w"], fw["fc1_c1"], fw["fc1_c2"], act="gelu", eps=eps)
+                h = ops.linear(m, L.fc2_w, L.fc2_b, residual=h)
         det = h[:, -cfg.num_detection_tokens:, :].contiguous()
         if det.dtype == torch.float32:  # 100 rows: not worth a kernel of its own in fp32
             y = F.layer_norm(det, (cfg.hidden_size,), self.ln_f_w, self.ln_f_b, eps)

@@ -10,6 +10,7 @@ Every op has two implementations:
 from __future__ import annotations
 
 import math
+from typing import NamedTuple
 
 import torch
 import torch.nn.functional as F
@@ -202,15 +203,106 @@ def _split_rows_h3(x2: torch.Tensor, ln: bool, eps: float = 0.0) -> tuple[torch.
     return planes, rinv
 
 
-def _gemm_h3(ap, rinv, weight, bias, r2, o2, epi, kv=None) -> None:
+def _gemm_h3(ap, rinv, weight, bias, r2, o2, epi, kv=None, rconst: float = 0.0, planes_out=None) -> None:
+    """One h3 GEMM on A planes ap [2, M, K] (row scales rinv, or rconst for
+    every row) into o2 [M, N] -- or, with ``planes_out`` = (planes [2, M, N],
+    scale), into the next GEMM's A planes."""
     M, K = ap.shape[1], ap.shape[2]
     N = weight.shape[0]
     wp, csc = split_f32_weight_h3(weight)
     kvs, S, skvp, kvsc = kv if kv is not None else (None, 0, 0, None)
-    rc = _lib.lib().nos_gemm_f32h3(ap.data_ptr(), K, M * K, rinv.data_ptr(), wp.data_ptr(), K, N * K, csc.data_ptr(),
-                                   _ptr(bias), _ptr(r2), r2.stride(0) if r2 is not None else 0, o2.data_ptr(),
-                                   o2.stride(0), M, N, K, epi, _ptr(kvs), S, skvp, _ptr(kvsc), _stream())
+    pp, psc = planes_out if planes_out is not None else (None, 1.0)
+    rc = _lib.lib().nos_gemm_f32h3(ap.data_ptr(), K, M * K, _ptr(rinv), float(rconst), wp.data_ptr(), K, N * K,
+                                   csc.data_ptr(), _ptr(bias), _ptr(r2), r2.stride(0) if r2 is not None else 0,
+                                   _ptr(o2), o2.stride(0) if o2 is not None else N, M, N, K, epi, _ptr(kvs), S, skvp,
+                                   _ptr(kvsc), _ptr(pp), N, M * N, float(psc), _stream())
     _lib.check(rc, "nos_gemm_f32h3")
+
+
+class H3Planes(NamedTuple):
+    """An activation handed between two h3 kernels as the consumer GEMM's A
+    operand: hi / lo fp16 planes [2, M, K] on per-row scales (``rinv``) or one
+    static scale (``rconst`` = its inverse), with the logical shape [..., K]."""
+    planes: torch.Tensor
+    rinv: torch.Tensor | None
+    rconst: float
+    shape: tuple
+
+
+def _pow2_scale_under(bound: float) -> float:
+    """The power of two s with bound * s < 2^14 (fp16's headroom for h3)."""
+    if not bound > 0:
+        return 1.0
+    e = max(-126, min(126, 14 - math.frexp(bound)[1]))
+    return math.ldexp(1.0, e)
+
+
+_H3_OUT_SCALE: dict[tuple, tuple] = {}
+
+
+@torch.no_grad()
+def _h3_out_scale(wg: torch.Tensor, c2: torch.Tensor, act: str | None) -> float:
+    """Static scale for the output of the LN-folded GEMM (wg, c2) as planes:
+    |y_j| <= sqrt(K) ||wg_j||_2 + |c2_j| for every LayerNorm-normalised row,
+    and GELU / ReLU never exceed that (or 0.17 below zero)."""
+    key = (id(wg), act)
+    hit = _H3_OUT_SCALE.get(key)
+    if hit is not None and hit[0]() is wg and hit[1] == wg._version:
+        return hit[2]
+    import weakref
+
+    b = float((math.sqrt(wg.shape[1]) * wg.double().norm(dim=1) + c2.double().abs()).max())
+    if act in ("gelu", "relu"):
+        b = max(b, 0.2)
+    sc = _pow2_scale_under(b)
+    _H3_OUT_SCALE[key] = (weakref.ref(wg, lambda _r, k=key: _H3_OUT_SCALE.pop(k, None)), wg._version, sc)
+    return sc
+
+
+def linear_planes(a: H3Planes, weight: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
+                  residual: torch.Tensor | None = None) -> torch.Tensor:
+    """act(A @ weight^T + bias) + residual for an A handed over as h3 planes
+    (see :class:`H3Planes`): no split pre-pass, no fp32 round trip of A."""
+    M, K = a.planes.shape[1], a.planes.shape[2]
+    N = weight.shape[0]
+    if weight.dim() != 2 or weight.shape[1] != K or weight.dtype != torch.float32 or weight.stride(-1) != 1:
+        raise ValueError(f"weight must be fp32 [N, {K}] with unit inner stride")
+    _check_f32(bias=bias)
+    out = torch.empty((M, N), dtype=torch.float32, device=a.planes.device)
+    r2 = None
+    if residual is not None:
+        if residual.numel() != M * N or residual.dtype != torch.float32:
+            raise ValueError(f"residual must be fp32 [{M}, {N}]")
+        r2 = residual.reshape(M, N)
+        _check_f32(residual=r2)
+    _gemm_h3(a.planes, a.rinv, weight, bias, r2, out, _epi(bias, act, residual), rconst=a.rconst)
+    return out.view(*a.shape[:-1], N)
+
+
+def linear_ln_to_planes(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor,
+                        act: str | None = None, eps: float = 1e-12) -> H3Planes:
+    """:func:`linear_ln` under h3 math whose output goes straight to the next
+    GEMM's A planes on the static scale of :func:`_h3_out_scale` (fc1 -> fc2)."""
+    if _F32_MATH != "h3" or not x.is_cuda or x.dtype != torch.float32:
+        raise ValueError("linear_ln_to_planes needs h3 math and an fp32 CUDA input")
+    K = x.shape[-1]
+    N = wg.shape[0]
+    x2 = x.reshape(-1, K)
+    _check_f32(x=x2, weight=wg, c1=c1, c2=c2)
+    if K % 32:
+        raise ValueError("linear_ln_to_planes needs K % 32 == 0")
+    M = x2.shape[0]
+    ap, rinv = _split_rows_h3(x2, ln=True, eps=eps)
+    sc = _h3_out_scale(wg, c2, act)
+    planes = torch.empty((2, M, N), dtype=torch.float16, device=x.device)
+    _gemm_h3(ap, rinv, wg, c2, None, None, EPI_BIAS | _epi(None, act, None), planes_out=(planes, sc))
+    return H3Planes(planes, None, 1.0 / sc, (*x.shape[:-1], N))
+
+
+def h3_planes_active(attention: bool = False) -> bool:
+    """Whether producers hand activations over as h3 planes (h3 math, and for
+    the attention an h3 variant)."""
+    return _F32_MATH == "h3" and (not attention or _ATTN_F32_VARIANT.startswith("h3"))
 
 
 def set_f32_math(mode: str) -> None:
@@ -584,12 +676,17 @@ def h3_head_scales(wg: torch.Tensor, c2: torch.Tensor, num_heads: int) -> torch.
     K = wg.shape[1]
     hd = num_heads * 64
     bound = math.sqrt(K) * wg.double().norm(dim=1) + c2.double().abs()
-    b = bound[hd:].view(2, num_heads, 64).amax(dim=2)                 # [K|V, head]
+    b = bound[hd:].view(2, num_heads, 64).amax(dim=2).cpu()           # [K|V, head]
     e = 14 - torch.frexp(b).exponent.to(torch.int64)                  # b < 2^exponent
     e = torch.where(b > 0, e, torch.zeros_like(e)).clamp(-126, 126)
-    sc = torch.ldexp(torch.ones_like(b), e).float().contiguous().to(wg.device)
+    sc_host = torch.ldexp(torch.ones_like(b), e).float().contiguous()
+    sc = sc_host.to(wg.device)
     _H3_SCALES[key] = (weakref.ref(wg, lambda _r, k=key: _H3_SCALES.pop(k, None)), wg._version, wg.data_ptr(), sc)
+    _H3_SCALES_HOST[key] = sc_host
     return sc
+
+
+_H3_SCALES_HOST: dict[int, torch.Tensor] = {}
 
 
 def linear_ln_qkv_h3(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, num_heads: int,
@@ -626,22 +723,35 @@ def linear_ln_qkv_h3(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: to
 
 
 def attention_presplit_h3(qkv: torch.Tensor, ws: torch.Tensor, scales: torch.Tensor, num_heads: int,
-                          scale: float | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """fp16x3 attention from the planes :func:`linear_ln_qkv_h3` wrote."""
+                          scale: float | None = None, out: torch.Tensor | None = None,
+                          planes_out: float | None = None):
+    """fp16x3 attention from the planes :func:`linear_ln_qkv_h3` wrote.
+    ``planes_out`` = a static scale s with |O| * s < 2^14 (every O row is a
+    convex combination of V rows: the smallest V head scale works): the
+    output goes to the proj GEMM's A planes instead, as :class:`H3Planes`."""
     B, S, three_hd = qkv.shape
     hd = three_hd // 3
-    if out is None:
-        out = torch.empty((B, S, hd), dtype=torch.float32, device=qkv.device)
-    if out.dtype != torch.float32 or out.stride(-1) != 1 or out.shape != (B, S, hd):
-        raise ValueError("out must be [B, S, H*64] fp32 with unit inner stride")
+    planes = None
+    if planes_out is not None:  # planes [2, B*S, hd] with o's strides; o itself is never written
+        planes = torch.empty((2, B * S, hd), dtype=torch.float16, device=qkv.device)
+        o_ptr, ld_out, bs_out = planes.data_ptr(), hd, S * hd
+    else:
+        if out is None:
+            out = torch.empty((B, S, hd), dtype=torch.float32, device=qkv.device)
+        if out.dtype != torch.float32 or out.stride(-1) != 1 or out.shape != (B, S, hd):
+            raise ValueError("out must be [B, S, H*64] fp32 with unit inner stride")
+        o_ptr, ld_out, bs_out = out.data_ptr(), out.stride(1), out.stride(0)
     if scales.shape != (2, num_heads) or scales.dtype != torch.float32 or not scales.is_contiguous():
         raise ValueError("scales must be the [2, H] fp32 tensor of linear_ln_qkv_h3")
     scale = scale if scale is not None else 1.0 / math.sqrt(64)
-    rc = _lib.lib().nos_attn_fwd_f32h3_presplit_d64(qkv.data_ptr(), out.data_ptr(), B, num_heads, S, S,
-                                                    qkv.stride(1), qkv.stride(0), out.stride(1), out.stride(0),
+    rc = _lib.lib().nos_attn_fwd_f32h3_presplit_d64(qkv.data_ptr(), o_ptr, B, num_heads, S, S,
+                                                    qkv.stride(1), qkv.stride(0), ld_out, bs_out,
                                                     float(scale), scales.data_ptr(), ws.data_ptr(),
-                                                    ws.numel() * ws.element_size(), _stream())
+                                                    ws.numel() * ws.element_size(), _ptr(planes), B * S * hd,
+                                                    float(planes_out or 1.0), _stream())
     _lib.check(rc, "nos_attn_fwd_f32h3_presplit_d64")
+    if planes is not None:
+        return H3Planes(planes, None, 1.0 / planes_out, (B, S, hd))
     return out
 
 
@@ -653,14 +763,16 @@ def ln_qkv_fusable(x: torch.Tensor) -> bool:
 
 
 def ln_qkv_attention(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, num_heads: int,
-                     eps: float = 1e-12) -> torch.Tensor:
+                     eps: float = 1e-12, planes_out: bool = False):
     """attention(LayerNorm(x) @ W_qkv^T + b) for an fp32 pod (see
     :func:`ln_qkv_fusable`): the QKV projection writes the attention's K / V
     planes straight from its epilogue -- fp16x3 planes under an ``h3``
-    variant, bf16x6 planes otherwise."""
+    variant, bf16x6 planes otherwise.  ``planes_out`` (h3 variant only):
+    the output as the proj GEMM's :class:`H3Planes`."""
     if _ATTN_F32_VARIANT.startswith("h3"):
         qkv, ws, sc = linear_ln_qkv_h3(x, wg, c1, c2, num_heads, eps=eps)
-        return attention_presplit_h3(qkv, ws, sc, num_heads)
+        osc = float(_H3_SCALES_HOST[id(wg)][1].min()) if planes_out else None
+        return attention_presplit_h3(qkv, ws, sc, num_heads, planes_out=osc)
     if _F32_MATH == "h3":  # x6 attention after an h3 projection: the unfused pair
         return attention_qkv(linear_ln(x, wg, c1, c2, eps=eps), num_heads)
     qkv, ws = linear_ln_qkv_x6(x, wg, c1, c2, num_heads, eps=eps)
@@ -691,5 +803,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "H3Planes", "linear_planes", "linear_ln_to_planes", "h3_planes_active", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

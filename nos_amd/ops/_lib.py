@@ -38,12 +38,13 @@ _SIGS = {
     "nos_gemm_ln_f32x6_qkv_h3": [c_void_p, c_int, c_void_p, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_int,
                                  c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "nos_attn_fwd_f32h3_presplit_d64": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_ll, c_int, c_ll,
-                                        c_float, c_void_p, c_void_p, c_ll, c_void_p],
+                                        c_float, c_void_p, c_void_p, c_ll, c_void_p, c_ll, c_float, c_void_p],
     "nos_attn_f32x6_set_kvsplit": [c_int],
     "nos_split_rows_h3": [c_void_p, c_int, c_void_p, c_int, c_ll, c_void_p, c_int, c_int, c_int, c_float, c_int,
                           c_void_p],
-    "nos_gemm_f32h3": [c_void_p, c_int, c_ll, c_void_p, c_void_p, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_int,
-                       c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "nos_gemm_f32h3": [c_void_p, c_int, c_ll, c_void_p, c_float, c_void_p, c_int, c_ll, c_void_p, c_void_p,
+                       c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                       c_void_p, c_int, c_ll, c_float, c_void_p],
     "nos_gemm_f32h3_set_layout": [c_int],
     "nos_gemm_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],

@@ -516,6 +516,7 @@ class CompiledProgram:
             steps = self._fold_layernorm(steps)
             steps = self._fuse_epilogues(steps)
             steps = self._fuse_qkv_attention(steps)
+            steps = self._mark_plane_handoffs(steps)
             self.steps = self._plan_releases(steps)
             used = {i for s in self.steps for i in s.inputs} | set(self.outputs)
             for k in [k for k in self.consts if k not in used]:  # e.g. weights replaced by their LN-folded form
@@ -649,6 +650,23 @@ class CompiledProgram:
         self.stats["qkv_attention_fused"] = n
         return [s for s in steps if s.output not in drop]
 
+    def _mark_plane_handoffs(self, steps: list[_Step]) -> list[_Step]:
+        """A fused LN-QKV attention or LN-GEMM whose only consumer is a
+        linear's A operand may, under h3 math, hand its output over as that
+        GEMM's fp16 planes (ops.H3Planes): marked here, decided per run."""
+        uses = self._consumers(steps, self.outputs)
+        by_out = {s.output: s for s in steps}
+        n = 0
+        for s in steps:
+            if s.kind != "linear" or s.inputs[0] in s.inputs[1:]:
+                continue
+            p = by_out.get(s.inputs[0])
+            if p is not None and p.kind in ("ln_qkv_attention", "linear_ln") and uses.get(p.output) == 1:
+                p.attrs["planes_out"] = True
+                n += 1
+        self.stats["plane_handoffs"] = n
+        return steps
+
     def _plan_releases(self, steps: list[_Step]) -> list[_Step]:
         last: dict[str, int] = {}
         for k, s in enumerate(steps):
@@ -679,14 +697,25 @@ class CompiledProgram:
             k = s.kind
             if k == "linear":
                 res = a.pop() if s.attrs.get("residual") else None
-                y = ops.linear(a[0].contiguous(), a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
-                               residual=res)
+                if isinstance(a[0], ops.H3Planes):
+                    y = ops.linear_planes(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
+                                          residual=res)
+                else:
+                    y = ops.linear(a[0].contiguous(), a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
+                                   residual=res)
             elif k == "linear_ln":
-                y = ops.linear_ln(a[0].contiguous(), a[1], a[2], a[3], act=s.attrs.get("act"), eps=s.attrs["eps"])
+                xx = a[0].contiguous()
+                if (s.attrs.get("planes_out") and xx.is_cuda and xx.dtype.itemsize == 4
+                        and ops.h3_planes_active()):
+                    y = ops.linear_ln_to_planes(xx, a[1], a[2], a[3], act=s.attrs.get("act"), eps=s.attrs["eps"])
+                else:
+                    y = ops.linear_ln(xx, a[1], a[2], a[3], act=s.attrs.get("act"), eps=s.attrs["eps"])
             elif k == "ln_qkv_attention":
                 h = a[0].contiguous()
                 if ops.ln_qkv_fusable(h):
-                    y = ops.ln_qkv_attention(h, a[1], a[2], a[3], s.attrs["heads"], eps=s.attrs["eps"])
+                    y = ops.ln_qkv_attention(h, a[1], a[2], a[3], s.attrs["heads"], eps=s.attrs["eps"],
+                                             planes_out=bool(s.attrs.get("planes_out"))
+                                             and ops.h3_planes_active(attention=True))
                 else:
                     qkv = ops.linear_ln(h, a[1], a[2], a[3], eps=s.attrs["eps"])
                     y = ops.attention_qkv(qkv, s.attrs["heads"])

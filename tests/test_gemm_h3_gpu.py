@@ -149,3 +149,66 @@ def test_h3_qkv_projection_with_h3_attention(B, S, H):
         errs[name] = (e.max().item(), e.mean().item())
     print("h3 path error vs fp64 (max, mean):", errs)
     assert errs["h3"][0] <= 1.5 * errs["exact"][0] + 1e-7 and errs["h3"][1] <= 1.5 * errs["exact"][1], errs
+
+
+def test_h3_mlp_plane_handoff_matches_fp64():
+    """fc1 (LN-folded, GELU) writing fc2's A planes on the static scale from
+    its weights, fc2 reading them: the fc1 -> fc2 chain against fp64, within
+    the exact-f32 chain's error."""
+    torch.manual_seed(4)
+    M, K, F = 3401, 384, 1536
+    x = torch.randn(M, K, device=DEV) * 2 + 0.3
+    w1 = torch.randn(F, K, device=DEV) * 0.05
+    b1 = torch.randn(F, device=DEV) * 0.1
+    w2 = torch.randn(K, F, device=DEV) * 0.03
+    b2 = torch.randn(K, device=DEV) * 0.1
+    g, be = 1 + 0.2 * torch.randn(K, device=DEV), 0.2 * torch.randn(K, device=DEV)
+    wg, c1, c2 = ops.fold_layernorm(w1, b1, g, be)
+    xd = torch.nn.functional.layer_norm(x.cpu().double(), (K,), g.cpu().double(), be.cpu().double(), 1e-12)
+    hid = torch.nn.functional.gelu(xd @ w1.cpu().double().t() + b1.cpu().double())
+    ref = hid @ w2.cpu().double().t() + b2.cpu().double() + x.cpu().double()
+
+    def exact():
+        m = ops.linear_ln(x, wg, c1, c2, act="gelu")
+        return ops.linear(m, w2, b2, residual=x)
+
+    def handoff():
+        m = ops.linear_ln_to_planes(x, wg, c1, c2, act="gelu")
+        assert isinstance(m, ops.H3Planes) and m.rinv is None and m.shape == (M, F)
+        return ops.linear_planes(m, w2, b2, residual=x)
+
+    errs = {}
+    for name, m, fn in (("exact", "exact", exact), ("h3", "h3", handoff)):
+        e = (_with_math(m, fn).cpu().double() - ref).abs()
+        errs[name] = (e.max().item(), e.mean().item())
+    print("fc1 -> fc2 error vs fp64 (max, mean):", errs)
+    assert errs["h3"][0] <= 1.5 * errs["exact"][0] and errs["h3"][1] <= 1.5 * errs["exact"][1], errs
+
+
+@pytest.mark.parametrize("variant", ["h3n", "h3"])
+def test_h3_yolos_with_plane_handoffs_matches_the_fp32_reference(variant):
+    """YOLOS-small under the default h3 kernels, attention -> proj and fc1 ->
+    fc2 handing their activations over as planes: logits and boxes within
+    the exact-fp32 tolerance of the PyTorch fp32 model, and the compiled
+    program of the same weights marks 24 hand-offs and agrees."""
+    from nos_amd.models.yolos import YolosConfig, YolosDetector, make_demo_input
+
+    cfg = YolosConfig.small()
+    m = YolosDetector(cfg, backend="torch")
+    m.reset_parameters(0)
+    m = m.to(DEV).eval()
+    x = make_demo_input(cfg, device=DEV, dtype=torch.float32, seed=0)
+    with torch.no_grad():
+        ref = m(x)
+        m.backend = "native"
+        ops.set_f32_math("h3")
+        ops.set_attention_f32_variant(variant)
+        try:
+            got = m(x)
+            torch.cuda.synchronize()
+        finally:
+            ops.set_f32_math("exact")
+            ops.set_attention_f32_variant("auto")
+    rng = (ref[0].max() - ref[0].min()).item()
+    assert (got[0] - ref[0]).abs().max().item() <= 1e-4 * rng
+    assert (got[1] - ref[1]).abs().max().item() <= 1e-4
