@@ -45,6 +45,7 @@ def main() -> None:
     ap.add_argument("--slice-gb", type=float, default=10.0)
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--pipeline", type=int, default=1, help="x6 GEMM software-pipelined K loop (1) or plain (0)")
+    ap.add_argument("--h3-layout", default="4x1", choices=["4x1", "2x2"], help="h3 GEMM wave layout")
     ap.add_argument("--mix", default="", help="heterogeneous tenants instead of --tenants YOLOS pods, e.g. "
                     "yolos:20,bert:4,mlp:4 (bert = BERT-base-shaped fp32 encoder at seq 512, mlp = bf16 GEMM-MLP "
                     "probe); per-kind rates in the output")
@@ -63,6 +64,7 @@ def main() -> None:
     from nos_amd import ops
 
     ops.set_gemm_f32x6_pipeline(bool(a.pipeline))  # process-wide: every capture below
+    ops.set_gemm_f32h3_layout(a.h3_layout)
     try:
         t0 = time.monotonic()
         clients = [PodClient(path, connect_timeout_s=30) for _ in range(a.tenants)]
@@ -116,7 +118,7 @@ def main() -> None:
                           "server_compile_ms_p50": sorted(r["compile"].get("compile_ms", 0) for r in reps)[len(reps) // 2],
                           "inf_per_s": round(sum(done) / (w1 - w0), 2),
                           "min_done": min(done), "max_done": max(done), "solo_replays": solo,
-                          "kernel_config": srv.kernel_config, "pipeline": a.pipeline,
+                          "kernel_config": srv.kernel_config, "pipeline": a.pipeline, "h3_layout": a.h3_layout,
                           "sclk_mhz": sclk}), flush=True)
     finally:
         srv.stop()
