@@ -69,13 +69,13 @@ struct PlaneOut {
 };
 
 template <int BM, int BN, int WGM, int WGN, bool PERSIST>
-__global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_h3_kernel(
+__global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3_kernel(
     const _Float16* __restrict__ Ap, int lda, long long aplane, const float* __restrict__ rinv, float rconst,
     const _Float16* __restrict__ Wp, int ldw, long long wplane, const float* __restrict__ csc,
     const float* __restrict__ bias, const float* __restrict__ R, int ldr, float* __restrict__ C, int ldc, int M,
     int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv, PlaneOut po) {
   constexpr int NW = WGM * WGN, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
-  static_assert(NW == 4 && MI >= 1 && NI >= 1, "4 waves");
+  static_assert((NW == 4 || NW == 8) && MI >= 1 && NI >= 1, "4 or 8 waves");
   constexpr int TA = 2 * BM * ROWB, STAGE = TA + 2 * BN * ROWB;
   constexpr int APW = TA / 1024 / NW, WPW = 2 * BN * ROWB / 1024 / NW;  // 1 KiB DMA pieces per wave
   static_assert(APW * NW * 1024 == TA && WPW * NW * 1024 == 2 * BN * ROWB, "equal DMA count per wave");
@@ -249,19 +249,20 @@ int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, f
   const long long ntiles = (long long)tiles_m * tiles_n;
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
   const size_t lds = 2 * (size_t)(2 * BM * ROWB + 2 * BN * ROWB);
-  const int grid = nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true>, 256, lds, ntiles);
+  constexpr int NT = 64 * WGM * WGN;
+  const int grid = nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true>, NT, lds, ntiles);
   if (grid < ntiles)
-    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true>), dim3((unsigned)grid), dim3(256), lds, st, Ap, lda,
+    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true>), dim3((unsigned)grid), dim3(NT), lds, st, Ap, lda,
                        aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
                        tiles_n, kv, po);
   else
-    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false>), dim3((unsigned)ntiles), dim3(256), lds, st, Ap,
+    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false>), dim3((unsigned)ntiles), dim3(NT), lds, st, Ap,
                        lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
                        tiles_n, kv, po);
   return (int)hipGetLastError();
 }
 
-int g_layout = 0;  // 0: 4 x 1 waves, 1: 2 x 2 waves (nos_gemm_f32h3_set_layout)
+int g_layout = 0;  // 0: 128x128, 4 x 1 waves; 1: 128x128, 2 x 2; 2: 256x128, 4 x 2 (nos_gemm_f32h3_set_layout)
 
 // ------------------------------------------------------------ row split
 // One wave per row, the whole row in registers (F4 float4s per lane: K <=
@@ -357,7 +358,7 @@ __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restr
 }  // namespace
 
 NOS_API int nos_gemm_f32h3_set_layout(int layout) {
-  if (layout < 0 || layout > 1) return (int)hipErrorInvalidValue;
+  if (layout < 0 || layout > 2) return (int)hipErrorInvalidValue;
   g_layout = layout;
   return 0;
 }
@@ -431,6 +432,9 @@ NOS_API int nos_gemm_f32h3(const void* Ap, int lda, long long aplane, const floa
   }
   const auto* a = static_cast<const _Float16*>(Ap);
   const auto* w = static_cast<const _Float16*>(Wp);
+  if (g_layout == 2)
+    return launch_t<256, 128, 4, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
+                                    epi, kv, po, stream);
   if (g_layout == 1)
     return launch_t<128, 128, 2, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
                                     epi, kv, po, stream);

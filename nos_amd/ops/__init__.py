@@ -340,9 +340,12 @@ def set_gemm_f32x6_tile(tile: str) -> None:
 
 
 def set_gemm_f32h3_layout(layout: str) -> None:
-    """h3 GEMM waves: ``"4x1"`` (default: 32-row strips, each wave reads the
-    whole W tile) or ``"2x2"`` (A/B)."""
-    _lib.check(_lib.lib().nos_gemm_f32h3_set_layout({"4x1": 0, "2x2": 1}[layout]), "nos_gemm_f32h3_set_layout")
+    """h3 GEMM tiles / waves: ``"4x1"`` (default: 128x128, 32-row strips,
+    each wave reads the whole W tile), ``"2x2"`` (128x128, 64x64 per wave) or
+    ``"256x128"`` (8 waves of 64x64, one workgroup per CU) -- A/B; the
+    results are bit-identical."""
+    _lib.check(_lib.lib().nos_gemm_f32h3_set_layout({"4x1": 0, "2x2": 1, "256x128": 2}[layout]),
+               "nos_gemm_f32h3_set_layout")
 
 
 def set_gemm_f32x6_pipeline(on: bool) -> None:

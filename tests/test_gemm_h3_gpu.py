@@ -107,13 +107,13 @@ def test_h3_wave_layouts_are_bit_identical():
     w = torch.randn(384, 384, device=DEV) * 0.05
     b = torch.randn(384, device=DEV)
     outs = []
-    for lay in ("4x1", "2x2"):
+    for lay in ("4x1", "2x2", "256x128"):
         ops.set_gemm_f32h3_layout(lay)
         try:
             outs.append(_with_math("h3", lambda: ops.linear(x, w, b, act="gelu", residual=x)))
         finally:
             ops.set_gemm_f32h3_layout("4x1")
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
 @pytest.mark.parametrize("B,S,H", [(1, 3401, 6), (2, 77, 3)])

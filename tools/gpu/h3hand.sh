@@ -9,6 +9,8 @@ grep -E "handoff|fc1 -> fc2|passed|failed" $O/tests.log | tail -5
 for r in 1 2; do
   timeout -k 10 240 python -u tools/podserver_once.py --tenants 28 --window 8 > $O/fleet_r$r.json 2> $O/fleet_r$r.err || { echo "fleet failed"; tail -20 $O/fleet_r$r.err; exit 1; }
   timeout -k 10 240 python -u tools/podserver_once.py --tenants 28 --window 8 --h3-layout 2x2 > $O/fleet22_r$r.json 2> $O/fleet22_r$r.err || { echo "fleet 2x2 failed"; tail -20 $O/fleet22_r$r.err; exit 1; }
+  timeout -k 10 240 python -u tools/podserver_once.py --tenants 28 --window 8 --h3-layout 256x128 > $O/fleet256_r$r.json 2> $O/fleet256_r$r.err || { echo "fleet 256 failed"; tail -20 $O/fleet256_r$r.err; exit 1; }
+  echo "r$r 256x128 $(python -c 'import json,sys; d=json.load(open(sys.argv[1])); print(d["inf_per_s"], d["sclk_mhz"])' $O/fleet256_r$r.json)"
   echo "r$r 2x2 $(python -c 'import json,sys; d=json.load(open(sys.argv[1])); print(d["inf_per_s"], d["sclk_mhz"])' $O/fleet22_r$r.json)"
   echo "r$r $(python -c 'import json,sys; d=json.load(open(sys.argv[1])); print(d["inf_per_s"], d["sclk_mhz"], d["server_build_ms_p50"])' $O/fleet_r$r.json)"
 done
