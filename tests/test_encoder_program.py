@@ -27,6 +27,7 @@ def test_encoder_program_matches_torch_transformer_encoder(dtype):
     prog = PG.parse(*encoder_program(w, L, heads, (2, S, hid), dtype))
     m = prog.compile("cpu")
     assert m.stats["layernorm_folded"] == 2 * L and m.stats["qkv_attention_fused"] == L
+    assert m.stats["plane_handoffs"] == 2 * L  # attention -> out_proj, linear1 -> linear2 (used under h3)
     assert m.stats["residual_fused"] == 2 * L and m.stats["activation_fused"] == L
     x = torch.randn(2, S, hid, generator=torch.Generator().manual_seed(2))
     with torch.no_grad():

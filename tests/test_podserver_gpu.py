@@ -52,6 +52,7 @@ def test_server_replays_match_the_eager_model_bit_for_bit(server):
     rep = c.register("pod-a", *_yolos(3), memory_limit_gb=10)
     assert rep["server"]["kernel_config"]["f32_math"] == "h3"
     assert rep["compile"]["qkv_attention_fused"] == 12 and rep["compile"]["layernorm_folded"] == 24
+    assert rep["compile"]["plane_handoffs"] == 24
     assert 0.05 < rep["footprint_gb"] < 10
     x = np.random.default_rng(1).standard_normal(rep["input_shape"]).astype(np.float32)
     outs, meta = c.infer(x, outputs=True)
