@@ -684,7 +684,11 @@ def h3_head_scales(wg: torch.Tensor, c2: torch.Tensor, num_heads: int) -> torch.
     e = torch.where(b > 0, e, torch.zeros_like(e)).clamp(-126, 126)
     sc_host = torch.ldexp(torch.ones_like(b), e).float().contiguous()
     sc = sc_host.to(wg.device)
-    _H3_SCALES[key] = (weakref.ref(wg, lambda _r, k=key: _H3_SCALES.pop(k, None)), wg._version, wg.data_ptr(), sc)
+    def drop(_r, k=key):
+        _H3_SCALES.pop(k, None)
+        _H3_SCALES_HOST.pop(k, None)
+
+    _H3_SCALES[key] = (weakref.ref(wg, drop), wg._version, wg.data_ptr(), sc)
     _H3_SCALES_HOST[key] = sc_host
     return sc
 
