@@ -28,9 +28,26 @@ namespace {
 
 enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
 
-constexpr int BK = 32, ROWB = BK * 2;  // one plane row of a stage: 64 B = 4 chunks
+constexpr int BK = 32;  // K granule of the API (K % 32 == 0); stages are BKT = 32 or 16 deep
 
-__device__ __forceinline__ int swz(int row) { return (row >> 2) & 3; }
+// 16-byte chunk swizzle of a plane row of CH chunks (BKT 32: 64 B rows, 4
+// chunks; BKT 16: 32 B rows, 2 chunks): 16 consecutive lanes reading the same
+// logical chunk of 16 consecutive rows hit 16 distinct 16-byte slots
+template <int CH>
+__device__ __forceinline__ int swz(int row) { return CH == 4 ? ((row >> 2) & 3) : ((row >> 3) & 1); }
+
+// s_waitcnt vmcnt(n * LPS) for a runtime n in [0, 3]
+template <int LPS>
+__device__ __forceinline__ void wait_stages(int n) {
+  if (n <= 0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (n == 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+  else if (n == 2)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPS) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LPS) : "memory");
+}
 
 __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_base) {
   const unsigned lds = __builtin_amdgcn_readfirstlane(
@@ -68,7 +85,9 @@ struct PlaneOut {
   float sc = 1.f;
 };
 
-template <int BM, int BN, int WGM, int WGN, bool PERSIST>
+// BKT: K depth of an LDS stage (32: two 16-deep MFMA steps, or 16: one);
+// RS: stages in the ring (RS - 1 of them in flight ahead of the one computed)
+template <int BM, int BN, int WGM, int WGN, bool PERSIST, int BKT = 32, int RS = 2>
 __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3_kernel(
     const _Float16* __restrict__ Ap, int lda, long long aplane, const float* __restrict__ rinv, float rconst,
     const _Float16* __restrict__ Wp, int ldw, long long wplane, const float* __restrict__ csc,
@@ -76,17 +95,20 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv, PlaneOut po) {
   constexpr int NW = WGM * WGN, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
   static_assert((NW == 4 || NW == 8) && MI >= 1 && NI >= 1, "4 or 8 waves");
+  constexpr int ROWB = BKT * 2, CH = ROWB / 16, RPP = 1024 / ROWB, NSTEP = BKT / 16;
+  static_assert((BKT == 32 || BKT == 16) && RS >= 2 && RS <= 4, "stage shape");
   constexpr int TA = 2 * BM * ROWB, STAGE = TA + 2 * BN * ROWB;
   constexpr int APW = TA / 1024 / NW, WPW = 2 * BN * ROWB / 1024 / NW;  // 1 KiB DMA pieces per wave
   static_assert(APW * NW * 1024 == TA && WPW * NW * 1024 == 2 * BN * ROWB, "equal DMA count per wave");
   constexpr int LPS = APW + WPW;
+  static_assert((RS - 2) * LPS < 64, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int c = lane & 31, h = lane >> 5;
   const int wm = wid / WGN, wn = wid % WGN;
   const int ntiles = tiles_m * tiles_n;
-  const int nk = K / BK;
+  const int nk = K / BKT;
   nos::XcdChunk chunk;
   if constexpr (PERSIST) {
     chunk = nos::xcd_chunk(blockIdx.x, gridDim.x, ntiles);
@@ -100,26 +122,26 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     const int tm = tt / tiles_n, tn = tt - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
 
-    // a 1 KiB piece = 16 rows x 64 B of one plane; lane L: row L / 4, chunk L % 4
+    // a 1 KiB piece = RPP rows x ROWB bytes of one plane; lane L: row L / CH, chunk L % CH
     auto stage = [&](int k0, unsigned char* dst) {
 #pragma unroll
       for (int i = 0; i < APW; ++i) {
         const int p = wid * APW + i;
-        const int plane = p / (BM / 16), rb = (p % (BM / 16)) * 16;
-        const int row = rb + (lane >> 2);
+        const int plane = p / (BM / RPP), rb = (p % (BM / RPP)) * RPP;
+        const int row = rb + lane / CH;
         int g = m0 + row;
         g = g < M ? g : M - 1;
-        glds16(Ap + plane * aplane + (long long)g * lda + k0 + (((lane & 3) ^ swz(row)) << 3),
+        glds16(Ap + plane * aplane + (long long)g * lda + k0 + (((lane % CH) ^ swz<CH>(row)) << 3),
                dst + plane * BM * ROWB + rb * ROWB);
       }
 #pragma unroll
       for (int i = 0; i < WPW; ++i) {
         const int p = wid * WPW + i;
-        const int plane = p / (BN / 16), rb = (p % (BN / 16)) * 16;
-        const int row = rb + (lane >> 2);
+        const int plane = p / (BN / RPP), rb = (p % (BN / RPP)) * RPP;
+        const int row = rb + lane / CH;
         int g = n0 + row;
         g = g < N ? g : N - 1;
-        glds16(Wp + plane * wplane + (long long)g * ldw + k0 + (((lane & 3) ^ swz(row)) << 3),
+        glds16(Wp + plane * wplane + (long long)g * ldw + k0 + (((lane % CH) ^ swz<CH>(row)) << 3),
                dst + TA + plane * BN * ROWB + rb * ROWB);
       }
     };
@@ -143,7 +165,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
 #pragma unroll
         for (int p = 0; p < 2; ++p)
           f.a[i][p] = *reinterpret_cast<const f16x8_t*>(base + p * BM * ROWB + row * ROWB +
-                                                        (((2 * s + h) ^ swz(row)) << 4));
+                                                        (((NSTEP * s + h) ^ swz<CH>(row)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
@@ -151,7 +173,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
 #pragma unroll
         for (int p = 0; p < 2; ++p)
           f.w[j][p] = *reinterpret_cast<const f16x8_t*>(base + TA + p * BN * ROWB + row * ROWB +
-                                                        (((2 * s + h) ^ swz(row)) << 4));
+                                                        (((NSTEP * s + h) ^ swz<CH>(row)) << 4));
       }
     };
     auto mma = [&](const Frag& f) {
@@ -161,8 +183,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         for (int j = 0; j < NI; ++j) acc[i][j] = nos::mma3h(f.a[i], f.w[j], acc[i][j]);
     };
 
+    if constexpr (BKT == 32 && RS == 2) {
     stage(0, smem);
-    if (nk > 1) stage(BK, smem + STAGE);
+    if (nk > 1) stage(BKT, smem + STAGE);
     if (nk > 1) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");  // stage 0 landed, stage 1 in flight
     } else {
@@ -181,11 +204,36 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (kt + 2 < nk) stage((kt + 2) * BK, smem + (kt & 1) * STAGE);
+        if (kt + 2 < nk) stage((kt + 2) * BKT, smem + (kt & 1) * STAGE);
         load(smem + ((kt + 1) & 1) * STAGE, 0, fa);  // next stage's step 0 under step 1's MFMAs
       }
       mma(fb);
       __builtin_amdgcn_sched_barrier(0);
+    }
+    } else {
+    // deep ring: RS - 1 stages in flight ahead of the one computed
+#pragma unroll
+    for (int q = 0; q < RS - 1; ++q)
+      if (q < nk) stage(q * BKT, smem + q * STAGE);
+    for (int kt = 0; kt < nk; ++kt) {
+      // stage kt landed (later ones may stay in flight); every wave is done
+      // with stage kt - 1, whose buffer stage kt + RS - 1 reuses
+      wait_stages<LPS>(min(RS - 2, nk - 1 - kt));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + RS - 1 < nk) stage((kt + RS - 1) * BKT, smem + ((kt + RS - 1) % RS) * STAGE);
+      const unsigned char* cur = smem + (kt % RS) * STAGE;
+      Frag f0;
+      load(cur, 0, f0);
+      if constexpr (NSTEP == 2) {
+        Frag f1;
+        load(cur, 1, f1);
+        mma(f0);
+        mma(f1);
+      } else {
+        mma(f0);
+      }
+    }
     }
     __syncthreads();  // every wave is done with the ring (the next tile's prologue)
 
@@ -241,28 +289,31 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   }  // tiles
 }
 
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, int BKT = 32, int RS = 2>
 int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, float rconst, const _Float16* Wp,
              int ldw, long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C, int ldc,
              int M, int N, int K, int epi, KvOut kv, PlaneOut po, hipStream_t st) {
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const long long ntiles = (long long)tiles_m * tiles_n;
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
-  const size_t lds = 2 * (size_t)(2 * BM * ROWB + 2 * BN * ROWB);
+  const size_t lds = RS * (size_t)(2 * BM * BKT * 2 + 2 * BN * BKT * 2);
   constexpr int NT = 64 * WGM * WGN;
-  const int grid = nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true>, NT, lds, ntiles);
+  const int grid = nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS>, NT, lds, ntiles);
   if (grid < ntiles)
-    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true>), dim3((unsigned)grid), dim3(NT), lds, st, Ap, lda,
+    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS>), dim3((unsigned)grid), dim3(NT), lds, st, Ap, lda,
                        aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
                        tiles_n, kv, po);
   else
-    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false>), dim3((unsigned)ntiles), dim3(NT), lds, st, Ap,
+    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false, BKT, RS>), dim3((unsigned)ntiles), dim3(NT), lds, st, Ap,
                        lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
                        tiles_n, kv, po);
   return (int)hipGetLastError();
 }
 
-int g_layout = 0;  // 0: 128x128, 4 x 1 waves; 1: 128x128, 2 x 2; 2: 256x128, 4 x 2 (nos_gemm_f32h3_set_layout)
+// nos_gemm_f32h3_set_layout: 0: 128x128, 4 x 1 waves; 1: 128x128, 2 x 2;
+// 2: 256x128, 4 x 2 (8 waves); 3: 128x128 4 x 1, 3-deep ring of BK-32
+// stages (96 KiB); 4 / 5: 128x128 4 x 1 / 2 x 2, 4-deep ring of BK-16 stages
+int g_layout = 0;
 
 // ------------------------------------------------------------ row split
 // One wave per row, the whole row in registers (F4 float4s per lane: K <=
@@ -358,7 +409,7 @@ __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restr
 }  // namespace
 
 NOS_API int nos_gemm_f32h3_set_layout(int layout) {
-  if (layout < 0 || layout > 2) return (int)hipErrorInvalidValue;
+  if (layout < 0 || layout > 5) return (int)hipErrorInvalidValue;
   g_layout = layout;
   return 0;
 }
@@ -432,6 +483,15 @@ NOS_API int nos_gemm_f32h3(const void* Ap, int lda, long long aplane, const floa
   }
   const auto* a = static_cast<const _Float16*>(Ap);
   const auto* w = static_cast<const _Float16*>(Wp);
+  if (g_layout == 3)
+    return launch_t<128, 128, 4, 1, 32, 3>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
+                                           N, K, epi, kv, po, stream);
+  if (g_layout == 4)
+    return launch_t<128, 128, 4, 1, 16, 4>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
+                                           N, K, epi, kv, po, stream);
+  if (g_layout == 5)
+    return launch_t<128, 128, 2, 2, 16, 4>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
+                                           N, K, epi, kv, po, stream);
   if (g_layout == 2)
     return launch_t<256, 128, 4, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
                                     epi, kv, po, stream);

@@ -342,9 +342,11 @@ def set_gemm_f32x6_tile(tile: str) -> None:
 def set_gemm_f32h3_layout(layout: str) -> None:
     """h3 GEMM tiles / waves: ``"4x1"`` (default: 128x128, 32-row strips,
     each wave reads the whole W tile), ``"2x2"`` (128x128, 64x64 per wave) or
-    ``"256x128"`` (8 waves of 64x64, one workgroup per CU) -- A/B; the
-    results are bit-identical."""
-    _lib.check(_lib.lib().nos_gemm_f32h3_set_layout({"4x1": 0, "2x2": 1, "256x128": 2}[layout]),
+    ``"256x128"`` (8 waves of 64x64, one workgroup per CU), ``"4x1r3"``
+    (3-deep ring of BK-32 stages), ``"4x1k16"`` / ``"2x2k16"`` (4-deep ring
+    of BK-16 stages) -- A/B; the results are bit-identical."""
+    _lib.check(_lib.lib().nos_gemm_f32h3_set_layout({"4x1": 0, "2x2": 1, "256x128": 2, "4x1r3": 3, "4x1k16": 4,
+                                                     "2x2k16": 5}[layout]),
                "nos_gemm_f32h3_set_layout")
 
 

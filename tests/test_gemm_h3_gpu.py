@@ -107,13 +107,15 @@ def test_h3_wave_layouts_are_bit_identical():
     w = torch.randn(384, 384, device=DEV) * 0.05
     b = torch.randn(384, device=DEV)
     outs = []
-    for lay in ("4x1", "2x2", "256x128"):
+    lays = ("4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16")
+    for lay in lays:
         ops.set_gemm_f32h3_layout(lay)
         try:
             outs.append(_with_math("h3", lambda: ops.linear(x, w, b, act="gelu", residual=x)))
         finally:
             ops.set_gemm_f32h3_layout("4x1")
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    for lay, o in zip(lays[1:], outs[1:]):
+        assert torch.equal(outs[0], o), lay
 
 
 @pytest.mark.parametrize("B,S,H", [(1, 3401, 6), (2, 77, 3)])
