@@ -12,7 +12,7 @@
 //    written as hi / lo planes [2][M][K]; rinv[m] = 2^-e_m;
 //  * W' = the weight's rows on their own scales 2^f_n, split once per
 //    weight by the host (ops.split_f32_weight_h3); csc[n] = 2^-f_n;
-//  * 4 waves per workgroup (4 x 1: 32-row strips, or 2 x 2), 128 x 128
+//  * 4 waves per workgroup (2 x 2, or 4 x 1: 32-row strips), 128 x 128
 //    tiles, BK = 32 per stage in a 2-deep LDS ring filled by LDS-DMA
 //    (global_load_lds_dwordx4; every plane as rows of 64 B, 16-byte chunks
 //    XOR-swizzled by (row >> 2) & 3 -- conflict-free fragment reads);
@@ -312,8 +312,11 @@ int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, f
 
 // nos_gemm_f32h3_set_layout: 0: 128x128, 4 x 1 waves; 1: 128x128, 2 x 2;
 // 2: 256x128, 4 x 2 (8 waves); 3: 128x128 4 x 1, 3-deep ring of BK-32
-// stages (96 KiB); 4 / 5: 128x128 4 x 1 / 2 x 2, 4-deep ring of BK-16 stages
-int g_layout = 0;
+// stages (96 KiB); 4 / 5: 128x128 4 x 1 / 2 x 2, 4-deep ring of BK-16 stages.
+// Default 2 x 2: 64 x 64 per wave reads 8 KiB of fragments per 12 MFMAs
+// (4 x 1: 10 KiB); 28-tenant fleet 679.9 / 679.8 vs 679.0 / 676.2 inf/s,
+// the deeper rings 605-635 (profiles/r04_h3_layout_ab.json)
+int g_layout = 1;
 
 // ------------------------------------------------------------ row split
 // One wave per row, the whole row in registers (F4 float4s per lane: K <=

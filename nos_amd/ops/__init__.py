@@ -340,8 +340,8 @@ def set_gemm_f32x6_tile(tile: str) -> None:
 
 
 def set_gemm_f32h3_layout(layout: str) -> None:
-    """h3 GEMM tiles / waves: ``"4x1"`` (default: 128x128, 32-row strips,
-    each wave reads the whole W tile), ``"2x2"`` (128x128, 64x64 per wave) or
+    """h3 GEMM tiles / waves: ``"2x2"`` (default: 128x128, 64x64 per wave),
+    ``"4x1"`` (128x128, 32-row strips, each wave reads the whole W tile),
     ``"256x128"`` (8 waves of 64x64, one workgroup per CU), ``"4x1r3"``
     (3-deep ring of BK-32 stages), ``"4x1k16"`` / ``"2x2k16"`` (4-deep ring
     of BK-16 stages) -- A/B; the results are bit-identical."""

@@ -113,7 +113,7 @@ def test_h3_wave_layouts_are_bit_identical():
         try:
             outs.append(_with_math("h3", lambda: ops.linear(x, w, b, act="gelu", residual=x)))
         finally:
-            ops.set_gemm_f32h3_layout("4x1")
+            ops.set_gemm_f32h3_layout("2x2")
     for lay, o in zip(lays[1:], outs[1:]):
         assert torch.equal(outs[0], o), lay
 
