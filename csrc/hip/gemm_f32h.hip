@@ -246,6 +246,33 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         rsv[i][r] = rinv != nullptr ? rinv[m < M ? m : M - 1] : rconst;
       }
+    // interior tile stored as fp32 C (the common case): tile-local 32-bit
+    // offsets from wave-uniform base pointers (saddr stores, no 64-bit
+    // address math per element) and no bounds tests
+    const bool interior = m0 + BM <= M && n0 + BN <= N && kv.kvs == nullptr && po.p == nullptr;
+    if (interior) {
+      float* Ct = C + (long long)m0 * ldc + n0;
+      const float* Rt = (epi & EPI_RESID) ? R + (long long)m0 * ldr + n0 : nullptr;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int cl = wn * (BN / WGN) + j * 32 + c;
+        const float cs = csc[n0 + cl];
+        const float p2 = (epi & EPI_BIAS) ? bias[n0 + cl] : 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2);
+            if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+            if (epi & EPI_RELU) v = fmaxf(v, 0.f);
+            if (epi & EPI_RESID) v += Rt[(unsigned)(rl * ldr + cl)];
+            Ct[(unsigned)(rl * ldc + cl)] = v;
+          }
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int n = n0 + wn * (BN / WGN) + j * 32 + c;
