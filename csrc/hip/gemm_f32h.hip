@@ -346,19 +346,21 @@ int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, f
 int g_layout = 1;
 
 // ------------------------------------------------------------ row split
-// One wave per row, the whole row in registers (F4 float4s per lane: K <=
-// 256 F4): one read of the row, its scale (max |a|, or in LayerNorm mode
-// the mean / variance and the host's sqrt(K) bound of a normalised row),
-// then its hi / lo planes.  F4 = 0: rows longer than 4096, re-read per pass.
-template <int F4>
+// LPR lanes per row (64: a wave; 32: a half-wave, two rows per wave), the
+// whole row in registers (F4 float4s per lane: K <= 4 LPR F4): one read of
+// the row, its scale (max |a|, or in LayerNorm mode the mean / variance and
+// the host's sqrt(K) bound of a normalised row), then its hi / lo planes.
+// F4 = 0: rows longer than 4096, re-read per pass.
+template <int F4, int LPR = 64>
 __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restrict__ A, int lda,
                                                             _Float16* __restrict__ P, int ldp, long long pplane,
                                                             float* __restrict__ rinv, int M, int K, int ln,
                                                             float eps, int eln) {
   typedef __attribute__((ext_vector_type(4))) _Float16 f16x4_t;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (row >= M) return;
+  constexpr int RPB = 256 / LPR;  // rows per block
+  const int row = blockIdx.x * RPB + (int)(threadIdx.x / LPR);
+  const int lane = threadIdx.x % LPR;
+  if (row >= M) return;  // whole half-waves: LPR-lane reductions never mix a live and a retired row
   const float* a = A + (long long)row * lda;
   constexpr int NR = F4 > 0 ? F4 : 1;
   float4 v[NR];
@@ -366,11 +368,11 @@ __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restr
     if constexpr (F4 > 0) return v[i];
     return *reinterpret_cast<const float4*>(a + k);
   };
-  const int nchunk = F4 > 0 ? F4 : (K + 255) / 256;
+  const int nchunk = F4 > 0 ? F4 : (K + 4 * LPR - 1) / (4 * LPR);
   if constexpr (F4 > 0) {
 #pragma unroll
     for (int i = 0; i < F4; ++i) {
-      const int k = (lane + 64 * i) * 4;
+      const int k = (lane + LPR * i) * 4;
       v[i] = k < K ? *reinterpret_cast<const float4*>(a + k) : float4{0.f, 0.f, 0.f, 0.f};
     }
   }
@@ -380,19 +382,19 @@ __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restr
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < nchunk; ++i) {
-      const int k = (lane + 64 * i) * 4;
+      const int k = (lane + LPR * i) * 4;
       if (k < K) {
         const float4 x = get(i, k);
         s += (x.x + x.y) + (x.z + x.w);
       }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     mu = s / (float)K;
     float q = 0.f;
 #pragma unroll
     for (int i = 0; i < nchunk; ++i) {
-      const int k = (lane + 64 * i) * 4;
+      const int k = (lane + LPR * i) * 4;
       if (k < K) {
         const float4 x = get(i, k);
         const float d0 = x.x - mu, d1 = x.y - mu, d2 = x.z - mu, d3 = x.w - mu;
@@ -400,21 +402,21 @@ __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restr
       }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    for (int o = LPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
     rs = rsqrtf(q / (float)K + eps);
     e = eln;  // |x^| <= sqrt(K): the host's exponent for it
   } else {
     float mx = 0.f;
 #pragma unroll
     for (int i = 0; i < nchunk; ++i) {
-      const int k = (lane + 64 * i) * 4;
+      const int k = (lane + LPR * i) * 4;
       if (k < K) {
         const float4 x = get(i, k);
         mx = fmaxf(mx, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
       }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    for (int o = LPR / 2; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     e = nos::h3_scale_exp(mx);
   }
   const float sc = nos::pow2i(e);
@@ -423,7 +425,7 @@ __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restr
   _Float16* pl = ph + pplane;
 #pragma unroll
   for (int i = 0; i < nchunk; ++i) {
-    const int k = (lane + 64 * i) * 4;
+    const int k = (lane + LPR * i) * 4;
     if (k < K) {
       const float4 x = get(i, k);
       f16x2_t h01, l01, h23, l23;
@@ -457,9 +459,11 @@ NOS_API int nos_split_rows_h3(const float* A, int lda, void* P, int ldp, long lo
   if (eln < -126 || eln > 126) return (int)hipErrorInvalidValue;
   auto* p = static_cast<_Float16*>(P);
   const dim3 grid((unsigned)((M + 3) / 4)), blk(256);
-  if (K <= 512)
-    hipLaunchKernelGGL(split_rows_h3_kernel<2>, grid, blk, 0, stream, A, lda, p, ldp, pplane, rinv, M, K, ln, eps, eln);
-  else if (K <= 1024)
+  if (K <= 512) {  // a half-wave per row: every lane busy at K = 384, one fewer reduction step
+    const dim3 g2((unsigned)((M + 7) / 8));
+    hipLaunchKernelGGL((split_rows_h3_kernel<4, 32>), g2, blk, 0, stream, A, lda, p, ldp, pplane, rinv, M, K, ln, eps,
+                       eln);
+  } else if (K <= 1024)
     hipLaunchKernelGGL(split_rows_h3_kernel<4>, grid, blk, 0, stream, A, lda, p, ldp, pplane, rinv, M, K, ln, eps, eln);
   else if (K <= 2048)
     hipLaunchKernelGGL(split_rows_h3_kernel<8>, grid, blk, 0, stream, A, lda, p, ldp, pplane, rinv, M, K, ln, eps, eln);
