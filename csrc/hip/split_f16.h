@@ -24,11 +24,20 @@ typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
 
 namespace nos {
 
-// x (2 lanes of a pair, already scaled) -> hi / lo fp16 pieces
+// x (2 lanes of a pair, already scaled) -> hi / lo fp16 pieces.  The lo
+// pair is two mixed-precision FMAs, f16(x - 1.0 * hi) with hi read as fp16
+// (v_fma_mixlo_f16 / v_fma_mixhi_f16: one rounding of the exact difference,
+// the same value as converting x - (float)hi), instead of two fp16 -> fp32
+// conversions, two subtractions and a pack.
 __device__ __forceinline__ void split2h(f32x2_t x, f16x2_t& hi, f16x2_t& lo) {
   hi = __builtin_convertvector(x, f16x2_t);
-  const float rx = x.x - (float)hi.x, ry = x.y - (float)hi.y;
-  lo = __builtin_convertvector(f32x2_t{rx, ry}, f16x2_t);
+  const unsigned hb = __builtin_bit_cast(unsigned, hi);
+  unsigned lb;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(lb)
+      : "v"(x.x), "v"(hb), "v"(x.y));
+  lo = __builtin_bit_cast(f16x2_t, lb);
 }
 
 // acc += a.b as the three piece products, smallest first (a: A operand)
