@@ -55,14 +55,19 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_ba
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(lds) : "memory");
 }
 
-__device__ __forceinline__ float erf_fast(float x) {  // Abramowitz-Stegun 7.1.26, |err| <= 1.5e-7
+// Abramowitz-Stegun 7.1.26, |err| <= 1.5e-7, on the hardware reciprocal and
+// exp2 (v_rcp_f32 / v_exp_f32, ~1 ulp each): an IEEE division and expf's
+// range reduction cost ~15 more VALU per element, and fc1's GELU epilogue is
+// the largest VALU block of the h3 GEMMs
+__device__ __forceinline__ float erf_fast(float x) {
   const float ax = fabsf(x);
-  const float t = 1.f / fmaf(0.3275911f, ax, 1.f);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.f));
   float p = fmaf(1.061405429f, t, -1.453152027f);
   p = fmaf(p, t, 1.421413741f);
   p = fmaf(p, t, -0.284496736f);
   p = fmaf(p, t, 0.254829592f);
-  const float r = fmaf(-p * t, expf(-ax * ax), 1.f);
+  const float e = __builtin_amdgcn_exp2f(-ax * ax * 1.4426950408889634f);  // exp(-x^2); 0 past |x| ~ 10
+  const float r = fmaf(-p * t, e, 1.f);
   return copysignf(r, x);
 }
 
