@@ -85,8 +85,10 @@ def parse_args(argv=None):
                          "pods are CPU-only client processes, their inferences run in one HIP context); "
                          "shared: each pod its own GPU process, memory-capped, kernels on all CUs; "
                          "cumask: each pod its own GPU process with exclusive XCD-symmetric CUs")
-    ap.add_argument("--server-lanes", type=int, default=12,
-                    help="pod server lanes (streams, one hardware queue each) the tenants' graphs run on")
+    ap.add_argument("--server-lanes", type=int, default=16,
+                    help="pod server lanes (streams, one hardware queue each) the tenants' graphs run on; 16 with "
+                         "the h3 kernels: 712.7 vs 702.3 (12) / 673.5 (8) / 628.4 (20) inf/s at 28 tenants "
+                         "(profiles/r04_h3_lanes_ab.json)")
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--ref-pod-s", type=float, default=4.0,
@@ -337,7 +339,7 @@ def trainer_stats(w) -> dict | None:
     return {"iterations": round(n_it, 2), "running": p.running, "max_gap_s": round(p.max_gap_s, 3),
             "gemm_tflops": round(n_it * (i.get("flops_per_step") or 0) / w.window_s / 1e12, 2),
             "buckets": i.get("buckets"), "buckets_launched_in_backward": i.get("launched_in_backward"),
-            "allreduce_gb_per_s": round(n_it * (i.get("bucket_bytes") or 0) / w.window_s / 1e9, 2)
+            "allreduce_gb_per_s": round(n_it * (i.get("bucket_bytes") or 0) / w.window_s / 1e9, 4)
             if (i.get("world_size") or 1) > 1 else 0.0,
             "bucket_busbw_gbps": i.get("bucket_busbw_gbps"), "backend": i.get("backend"),
             "cu_mask": i.get("cu_mask"), "pid": i.get("pid")}
@@ -410,7 +412,9 @@ class PodServerProc:
         # the server reads the slices from the records the (simulated) device
         # plugin wrote when it allocated them (tokens; podserver/allocations.py)
         cmd = [sys.executable, "-u", "-m", "nos_amd.cmd.podserver", "--gpu", str(args.local_gpu), "--hip-id",
-               gpu_env, "--socket-dir", args.pod_server_dir, "--lanes", str(args.server_lanes),
+               gpu_env, "--socket-dir", args.pod_server_dir,
+               # a CPU rehearsal's lanes are threads on the host's cores: a few serve every tenant
+               "--lanes", str(args.server_lanes if args.device == "cuda" else min(args.server_lanes, 4)),
                "--max-tenants", str(POD_SERVER_TENANTS), "--device", args.device]
         self.log = os.path.join(workdir, "podserver.log")
         self.proc = launcher.spawn(cmd, env, self.log, str(REPO))
@@ -734,7 +738,7 @@ def main(argv=None) -> int:
         "bf16_gfx950_kernels": None if bf is None else {**bf, "inf_per_s_node": round(bf_sum, 2)},
         "trainer_error": trainer_error,
         "trainer_pods": None if tr is None else {"per_node_gemm_tflops": round(tr_tf, 2),
-                                                 "per_node_allreduce_gb_per_s": round(tr_gbs, 2),
+                                                 "per_node_allreduce_gb_per_s": round(tr_gbs, 4),
                                                  "rank0": tr, "bucket_mb": args.coll_bucket_mb,
                                                  "gemm_dim": args.coll_dim,
                                                  "step": "bf16 MLP (4 x dim^2 layers, batch dim) forward + backward, "

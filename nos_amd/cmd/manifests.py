@@ -75,7 +75,7 @@ DEFAULT_VALUES: dict = {
         # server process per GPU hosts every slice pod's inferences, so slices
         # per GPU are bounded by memory and tenantsPerGpu, not by the 8 HWS
         # process slots
-        "podServer": {"enabled": False, "tenantsPerGpu": 48, "lanes": 12,
+        "podServer": {"enabled": False, "tenantsPerGpu": 48, "lanes": 16,
                       "socketDir": C.DEFAULT_POD_SERVER_SOCKET_DIR},
     },
 }

@@ -92,7 +92,7 @@ def main(argv=None) -> int:
     ap.add_argument("--log-level", default="info")
     ap.add_argument("--socket-dir", default="")
     ap.add_argument("--socket", default="", help="explicit socket path (default <socket-dir>/gpu-<gpu>/server.sock)")
-    ap.add_argument("--lanes", type=int, default=8, help="streams = hardware queues the tenants are served on")
+    ap.add_argument("--lanes", type=int, default=16, help="streams = hardware queues the tenants are served on")
     ap.add_argument("--max-tenants", type=int, default=48)
     ap.add_argument("--memory-gb", type=float, default=0.0, help="slice memory the server admits (0 = the GPU's)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")

@@ -77,7 +77,7 @@ from . import protocol as P
 
 log = logging.getLogger("nos_amd.podserver")
 
-DEFAULT_LANES = 8
+DEFAULT_LANES = 16  # 28-tenant fleet with the h3 kernels: 16 > 12 > 8 > 20 (profiles/r04_h3_lanes_ab.json)
 DEFAULT_MAX_TENANTS = 48  # MPS's client limit per server (Volta+)
 
 

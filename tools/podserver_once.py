@@ -3,7 +3,7 @@ client threads over its Unix socket for a fixed window: the pod-server fleet
 in a single process, for ``rocprofv3 --kernel-trace --stats`` (the bench runs
 the server as its own process, under the clean pod launcher).
 
-  python tools/podserver_once.py --tenants 28 --lanes 12 --window 8
+  python tools/podserver_once.py --tenants 28 --lanes 16 --window 8
 """
 from __future__ import annotations
 
@@ -39,7 +39,7 @@ def make(kind: str, dtype: str, seed: int):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--tenants", type=int, default=28)
-    ap.add_argument("--lanes", type=int, default=12)
+    ap.add_argument("--lanes", type=int, default=16)
     ap.add_argument("--window", type=float, default=8.0)
     ap.add_argument("--warmup", type=float, default=2.0)
     ap.add_argument("--slice-gb", type=float, default=10.0)
