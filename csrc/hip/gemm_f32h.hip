@@ -254,7 +254,53 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     // interior tile stored as fp32 C (the common case): tile-local 32-bit
     // offsets from wave-uniform base pointers (saddr stores, no 64-bit
     // address math per element) and no bounds tests
-    const bool interior = m0 + BM <= M && n0 + BN <= N && kv.kvs == nullptr && po.p == nullptr;
+    const bool full = m0 + BM <= M && n0 + BN <= N;
+    // interior tile of the next GEMM's A planes (fc1 -> fc2) or of the K / V
+    // planes of a one-sequence QKV projection (a 128-column tile never
+    // straddles Q / K / V: hd % 128 == 0 is checked by the host): the same
+    // tile-relative 32-bit offsets, two fp16 stores per element
+    if (full && !(epi & EPI_RESID) &&
+        (po.p != nullptr || (kv.kvs != nullptr && kv.S == M && n0 >= kv.qcols && kv.hd % BN == 0))) {
+      unsigned short* hi;
+      long long lo_off;
+      int ld;
+      int t = 0;
+      if (po.p != nullptr) {
+        hi = po.p + (long long)m0 * po.ldp + n0;
+        lo_off = po.pplane;
+        ld = po.ldp;
+      } else {
+        t = (n0 - kv.qcols) >= kv.hd;
+        hi = kv.kvs + ((long long)m0 * 4 + 2 * t) * kv.hd + (n0 - kv.qcols - t * kv.hd);
+        lo_off = kv.hd;
+        ld = 4 * kv.hd;
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int cl = wn * (BN / WGN) + j * 32 + c;
+        const float cs = csc[n0 + cl];
+        const float p2 = (epi & EPI_BIAS) ? bias[n0 + cl] : 0.f;
+        const float osc = po.p != nullptr ? po.sc : kv.kvsc[t * (kv.hd >> 6) + ((n0 - kv.qcols - t * kv.hd + cl) >> 6)];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2);
+            if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+            if (epi & EPI_RELU) v = fmaxf(v, 0.f);
+            const float x = v * osc;
+            const _Float16 h0 = (_Float16)x;
+            const _Float16 h1 = (_Float16)(x - (float)h0);
+            const unsigned off = (unsigned)(rl * ld + cl);
+            hi[off] = __builtin_bit_cast(unsigned short, h0);
+            hi[lo_off + off] = __builtin_bit_cast(unsigned short, h1);
+          }
+        }
+      }
+      continue;
+    }
+    const bool interior = full && kv.kvs == nullptr && po.p == nullptr;
     if (interior) {
       float* Ct = C + (long long)m0 * ldc + n0;
       const float* Rt = (epi & EPI_RESID) ? R + (long long)m0 * ldr + n0 : nullptr;
