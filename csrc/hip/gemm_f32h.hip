@@ -300,7 +300,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
       }
       continue;
     }
-    const bool interior = full && kv.kvs == nullptr && po.p == nullptr;
+    const bool interior = full && po.p == nullptr && (kv.kvs == nullptr || n0 + BN <= kv.qcols);  // Q columns too
     if (interior) {
       float* Ct = C + (long long)m0 * ldc + n0;
       const float* Rt = (epi & EPI_RESID) ? R + (long long)m0 * ldr + n0 : nullptr;
