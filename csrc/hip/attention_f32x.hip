@@ -325,10 +325,12 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
 // rescale) needs no scale; the value scale is divided out with 1/l.
 constexpr int H3_STAGE = 4 * IMG;            // K hi, K lo, V hi, V lo
 constexpr int H3_LDS_BYTES = 2 * H3_STAGE;   // 32 KiB ring
-constexpr int H3_WG_PER_CU = 4;
+constexpr int H3_WG_PER_CU = 4;  // 4-wave workgroups (HW = 4); HW = 8: 2
 
-template <bool PERSIST>
-__global__ __launch_bounds__(NT, H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
+// HW waves per workgroup (4 or 8) x 32 query rows; the 16 DMA pieces of a
+// key tile are spread over the waves (16 / HW each)
+template <bool PERSIST, int HW>
+__global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
     const float* __restrict__ q, const _Float16* __restrict__ kvs, float* __restrict__ o, int B, int H, int Sq,
     int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, const float* __restrict__ kvsc,
     int nqb, int nsplit, float* __restrict__ part, _Float16* __restrict__ op, long long opl, float osc) {
@@ -365,10 +367,11 @@ __global__ __launch_bounds__(NT, H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
 
   const int ntiles = (Skv + KVB - 1) / KVB;
   const int skvp = ntiles * KVB;
-  int soff[4];  // staging: per-lane element offset of instruction i within a tile
+  constexpr int PPW = 16 / HW, HQBLK = 32 * HW;
+  int soff[PPW];  // staging: per-lane element offset of instruction i within a tile
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int p = wid * 4 + i;
+  for (int i = 0; i < PPW; ++i) {
+    const int p = wid * PPW + i;
     const int plane = p >> 2;
     const int row = (p & 3) * 8 + (lane >> 3);
     const int lc = (lane & 7) ^ (plane < 2 ? kswz(row) : vswz(row));
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(NT, H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
 
     // ---- Q pieces (B operand) on this query row's scale: lane holds
     // Q[row r][d = 16ks + 8hh .. +7] * c * 2^e
-    const int qrow = qb * QBLK + wid * 32 + r;
+    const int qrow = qb * HQBLK + wid * 32 + r;
     f16x8_t qf[4][2];
     float fs;  // s' -> exp2 units: 2^-e / ksc
     {
@@ -426,7 +429,7 @@ __global__ __launch_bounds__(NT, H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
 
     const _Float16* pb = kvs + (long long)b * skvp * (4 * ldh) + hd * D;
     auto stage_piece = [&](int t, int buf, int i) {
-      const int p = wid * 4 + i;
+      const int p = wid * PPW + i;
       long long off = (long long)t * (KVB * 4) * ldh + soff[i];
       if ((t + 1) * KVB > Skv) {  // tail tile: rows past Skv re-read the last key
         const int over = t * KVB + (p & 3) * 8 + (lane >> 3) - (Skv - 1);
@@ -435,7 +438,7 @@ __global__ __launch_bounds__(NT, H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
       glds16(pb + off, smem + buf * H3_STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
     };
 #pragma unroll
-    for (int i = 0; i < 4; ++i) stage_piece(t0, 0, i);
+    for (int i = 0; i < PPW; ++i) stage_piece(t0, 0, i);
 
     f32x16_t oacc[2];
 #pragma unroll
@@ -451,7 +454,7 @@ __global__ __launch_bounds__(NT, H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
       const int buf = (t - t0) & 1;
       if (t + 1 < t1) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) stage_piece(t + 1, buf ^ 1, i);
+        for (int i = 0; i < PPW; ++i) stage_piece(t + 1, buf ^ 1, i);
       }
       const unsigned char* kl = smem + buf * H3_STAGE;
       const unsigned char* vl = kl + 2 * IMG;
@@ -758,16 +761,21 @@ NOS_API int nos_attn_fwd_f32x6_presplit_d64(const float* q, float* o, int B, int
 
 namespace {
 
+int g_h3_waves = 4;  // nos_attn_f32h3_set_waves
+
+template <int HW>
 int launch_h3(const float* q, const _Float16* kvs, float* o, int B, int H, int Sq, int Skv, int ld_in,
               long long bs_in, int ld_out, long long bs_out, float c, const float* kvsc, int nqb, int nsplit,
               float* part, _Float16* op, long long opl, float osc, hipStream_t stream) {
   const long long nwg = (long long)B * H * nqb * nsplit;
-  const int grid = nos_grid_for((const void*)attn_fwd_f32h3_d64_kernel<true>, NT, H3_LDS_BYTES, nwg);
+  const int grid = nos_grid_for((const void*)attn_fwd_f32h3_d64_kernel<true, HW>, 64 * HW, H3_LDS_BYTES, nwg);
   if (grid < nwg)
-    hipLaunchKernelGGL((attn_fwd_f32h3_d64_kernel<true>), dim3((unsigned)grid), dim3(NT), H3_LDS_BYTES, stream, q,
+    hipLaunchKernelGGL((attn_fwd_f32h3_d64_kernel<true, HW>), dim3((unsigned)grid), dim3(64 * HW), H3_LDS_BYTES,
+                       stream, q,
                        kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit, part, op, opl, osc);
   else
-    hipLaunchKernelGGL((attn_fwd_f32h3_d64_kernel<false>), dim3((unsigned)nwg), dim3(NT), H3_LDS_BYTES, stream, q,
+    hipLaunchKernelGGL((attn_fwd_f32h3_d64_kernel<false, HW>), dim3((unsigned)nwg), dim3(64 * HW), H3_LDS_BYTES,
+                       stream, q,
                        kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit, part, op, opl, osc);
   return (int)hipGetLastError();
 }
@@ -793,18 +801,30 @@ NOS_API int nos_attn_fwd_f32h3_presplit_d64(const float* q, float* o, int B, int
   if (op != nullptr && ((((uintptr_t)op) & 7) || opl < (long long)B * bs_out || !(osc > 0.f)))
     return (int)hipErrorInvalidValue;
   const float c = scale * 1.4426950408889634f;
-  const int nqb = (Sq + QBLK - 1) / QBLK;
+  const int hw = g_h3_waves;
+  const int nqb = (Sq + 32 * hw - 1) / (32 * hw);
   const long long nwg = (long long)B * H * nqb;
   const int skvp = (Skv + KVB - 1) / KVB * KVB;
-  const int nsplit = pick_split(nwg, skvp / KVB, H3_WG_PER_CU);
+  const int nsplit = pick_split(nwg, skvp / KVB, hw == 8 ? 2 : H3_WG_PER_CU);
   auto* kvs = static_cast<const _Float16*>(ws);
   float* part = reinterpret_cast<float*>(static_cast<unsigned char*>(ws) +
                                          ((long long)B * skvp * 6 * H * D * 2 + 15) / 16 * 16);
-  const int rc = launch_h3(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit, part,
-                           op, opl, osc, stream);
+  const int rc = hw == 8 ? launch_h3<8>(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit,
+                                        part, op, opl, osc, stream)
+                         : launch_h3<4>(q, kvs, o, B, H, Sq, Skv, ld_in, bs_in, ld_out, bs_out, c, kvsc, nqb, nsplit,
+                                        part, op, opl, osc, stream);
   if (rc != 0 || nsplit == 1) return rc;
   const long long n4 = (long long)B * Sq * H * (D / 4);
   hipLaunchKernelGGL(merge_splits_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream, part, o, B, H, Sq,
                      nsplit, ld_out, bs_out, n4, op, opl, osc);
   return (int)hipGetLastError();
+}
+
+// h3 attention workgroup size: 4 waves (default: 128 query rows, 4
+// workgroups per CU) or 8 (256 rows, 2 per CU: each key tile is loaded
+// once for twice the queries).  A/B knob; the results are bit-identical.
+NOS_API int nos_attn_f32h3_set_waves(int waves) {
+  if (waves != 4 && waves != 8) return (int)hipErrorInvalidValue;
+  g_h3_waves = waves;
+  return 0;
 }

@@ -350,6 +350,12 @@ def set_gemm_f32h3_layout(layout: str) -> None:
                "nos_gemm_f32h3_set_layout")
 
 
+def set_attention_f32h3_waves(waves: int) -> None:
+    """h3 attention workgroups of 4 waves (default: 128 query rows, 4 per CU)
+    or 8 (256 rows, 2 per CU; A/B, bit-identical results)."""
+    _lib.check(_lib.lib().nos_attn_f32h3_set_waves(int(waves)), "nos_attn_f32h3_set_waves")
+
+
 def set_gemm_f32x6_pipeline(on: bool) -> None:
     """x6 GEMM K loop: software-pipelined (default: the next MFMA step's
     fragments are read and split under the current step's MFMAs) or the
@@ -812,5 +818,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "H3Planes", "linear_planes", "linear_ln_to_planes", "h3_planes_active", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "H3Planes", "set_attention_f32h3_waves", "linear_planes", "linear_ln_to_planes", "h3_planes_active", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

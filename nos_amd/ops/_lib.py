@@ -46,6 +46,7 @@ _SIGS = {
                        c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                        c_void_p, c_int, c_ll, c_float, c_void_p],
     "nos_gemm_f32h3_set_layout": [c_int],
+    "nos_attn_f32h3_set_waves": [c_int],
     "nos_gemm_bf16": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nos_gemm_f32": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,

@@ -137,3 +137,19 @@ def test_h3_yolos_tenant_matches_the_x6_tenant():
         ops.set_attention_f32_variant("auto")
     for a, c in zip(outs["x6n"], outs["h3n"]):
         assert (a - c).abs().max().item() <= 1e-4 * max(1.0, a.abs().max().item())
+
+
+@pytest.mark.parametrize("variant", ["h3n", "h3k3"])
+def test_h3_eight_wave_workgroups_are_bit_identical(variant):
+    """256-query workgroups (8 waves) compute every query row exactly as the
+    4-wave ones: same key tiles in the same order per row."""
+    B, S, H = 2, 301, 3
+    x, w, b, gam, bet = _problem(B, S, H, seed=21)
+    outs = []
+    for waves in (4, 8):
+        ops.set_attention_f32h3_waves(waves)
+        try:
+            outs.append(_run(x, w, b, gam, bet, H, "x6", variant))
+        finally:
+            ops.set_attention_f32h3_waves(4)
+    assert torch.equal(outs[0], outs[1])
