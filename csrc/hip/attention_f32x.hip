@@ -761,7 +761,9 @@ NOS_API int nos_attn_fwd_f32x6_presplit_d64(const float* q, float* o, int B, int
 
 namespace {
 
-int g_h3_waves = 4;  // nos_attn_f32h3_set_waves
+// nos_attn_f32h3_set_waves; 8: the 28-tenant fleet 756 vs 743 inf/s over
+// 4 rounds (profiles/r04_h3_attn_waves_ab.json)
+int g_h3_waves = 8;
 
 template <int HW>
 int launch_h3(const float* q, const _Float16* kvs, float* o, int B, int H, int Sq, int Skv, int ld_in,
@@ -820,9 +822,9 @@ NOS_API int nos_attn_fwd_f32h3_presplit_d64(const float* q, float* o, int B, int
   return (int)hipGetLastError();
 }
 
-// h3 attention workgroup size: 4 waves (default: 128 query rows, 4
-// workgroups per CU) or 8 (256 rows, 2 per CU: each key tile is loaded
-// once for twice the queries).  A/B knob; the results are bit-identical.
+// h3 attention workgroup size: 8 waves (default: 256 query rows, 2
+// workgroups per CU: each key tile is loaded once for twice the queries) or
+// 4 (128 rows, 4 per CU).  The results are bit-identical.
 NOS_API int nos_attn_f32h3_set_waves(int waves) {
   if (waves != 4 && waves != 8) return (int)hipErrorInvalidValue;
   g_h3_waves = waves;

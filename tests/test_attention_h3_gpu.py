@@ -151,5 +151,5 @@ def test_h3_eight_wave_workgroups_are_bit_identical(variant):
         try:
             outs.append(_run(x, w, b, gam, bet, H, "x6", variant))
         finally:
-            ops.set_attention_f32h3_waves(4)
+            ops.set_attention_f32h3_waves(8)
     assert torch.equal(outs[0], outs[1])

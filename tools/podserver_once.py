@@ -47,7 +47,7 @@ def main() -> None:
     ap.add_argument("--pipeline", type=int, default=1, help="x6 GEMM software-pipelined K loop (1) or plain (0)")
     ap.add_argument("--h3-layout", default="2x2", choices=["4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16"],
                     help="h3 GEMM tile / wave layout / ring")
-    ap.add_argument("--h3-attn-waves", type=int, default=4, choices=[4, 8], help="h3 attention waves per workgroup")
+    ap.add_argument("--h3-attn-waves", type=int, default=8, choices=[4, 8], help="h3 attention waves per workgroup")
     ap.add_argument("--mix", default="", help="heterogeneous tenants instead of --tenants YOLOS pods, e.g. "
                     "yolos:20,bert:4,mlp:4 (bert = BERT-base-shaped fp32 encoder at seq 512, mlp = bf16 GEMM-MLP "
                     "probe); per-kind rates in the output")
