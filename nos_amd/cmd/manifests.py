@@ -530,12 +530,14 @@ def node_agents() -> dict[str, list[dict]]:
         name = "nos-amd-podserver"
         c = _container("podserver", "nos_amd.cmd.podserver",
                        ["--gpus", "all", "--socket-dir", ps["socketDir"], "--lanes", str(ps["lanes"]),
-                        "--max-tenants", str(ps["tenantsPerGpu"])],
+                        "--max-tenants", str(ps["tenantsPerGpu"]),
+                        # evict tenants whose devices no pod holds (kubelet PodResources)
+                        "--pod-resources-socket", C.KUBELET_PODRESOURCES_SOCKET],
                        image=IMAGE_ROCM, env=NODE_ENV,
-                       mounts=HOST_MOUNTS[:2] + [{"name": "podserver-sockets", "mountPath": ps["socketDir"]}],
+                       mounts=HOST_MOUNTS + [{"name": "podserver-sockets", "mountPath": ps["socketDir"]}],
                        privileged=True, probes=False)
         c["resources"] = {"requests": {"cpu": "2", "memory": "4Gi"}, "limits": {"memory": "64Gi"}}
-        ds = _daemonset(name, c, C.PARTITIONING_CUMASK, HOST_VOLUMES[:2] + [
+        ds = _daemonset(name, c, C.PARTITIONING_CUMASK, HOST_VOLUMES[:3] + [
             {"name": "podserver-sockets", "hostPath": {"path": ps["socketDir"], "type": "DirectoryOrCreate"}}])
         out["podserver/daemonset.yaml"] = [_sa(name), ds]
     return out

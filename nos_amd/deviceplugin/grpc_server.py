@@ -73,7 +73,7 @@ class _ResourceServicer:
             out.append(pb.ContainerAllocateResponse(
                 envs=a.envs, devices=[pb.DeviceSpec(container_path=d, host_path=d, permissions="rw")
                                       for d in a.devices],
-                mounts=[pb.Mount(container_path=m, host_path=m, read_only=False) for m in a.mounts]))
+                mounts=[pb.Mount(container_path=m, host_path=m, read_only=True) for m in a.mounts]))
         return pb.AllocateResponse(container_responses=out)
 
     def PreStartContainer(self, request, context):  # noqa: N802

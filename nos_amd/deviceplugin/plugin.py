@@ -73,7 +73,11 @@ class ContainerAllocation:
     envs: dict[str, str] = field(default_factory=dict)
     devices: list[str] = field(default_factory=list)
     device_ids: list[str] = field(default_factory=list)
-    mounts: list[str] = field(default_factory=list)   # host directories mounted at the same path
+    # host directories mounted at the same path, always READ-ONLY: the pod-server
+    # socket directory -- connect() on a unix socket needs no write access to the
+    # mount, and a writable one would let a tenant unlink server.sock (cutting off
+    # every co-tenant) or bind a listener there that collects other pods' tokens
+    mounts: list[str] = field(default_factory=list)
 
 
 class NosAmdDevicePlugin:
@@ -90,6 +94,14 @@ class NosAmdDevicePlugin:
             from ..podserver.allocations import AllocationStore
 
             self.pod_server_allocations = AllocationStore(pod_server_dir)
+        # records a previous plugin process wrote: device id -> (owner, CU slots),
+        # adopted at the first refresh that has the slice table (_restore_records)
+        self._restored: dict[str, tuple[str, frozenset]] = {}
+        if self.pod_server_allocations is not None:
+            for _path, rec in self.pod_server_allocations.load():
+                slots = rec.get("cu_slots") or {}
+                for did in rec.get("device_ids", []):
+                    self._restored[did] = (str(rec.get("owner") or "restored"), frozenset(slots.get(did, ())))
         # "container": the runtime mounts only the allocated render nodes, so
         # HIP inside the container numbers them 0..k-1 in host order;
         # "host": tenants run on the host and see every GPU (simulator, bare metal)
@@ -187,6 +199,7 @@ class NosAmdDevicePlugin:
                                        d.hip_id, d.drm_render)
             before = {k: (d.resource, d.healthy) for k, d in self.devices.items()}
             self.devices = devs
+            self._restore_records()
             self._layout_cu_slots()
             changed = {k: (d.resource, d.healthy) for k, d in self.devices.items()} != before or self.generation == 0
             if not changed:
@@ -245,6 +258,32 @@ class NosAmdDevicePlugin:
                 devs[did] = Device(did, C.AMD_SLICE_RESOURCE_PREFIX + prof, gi.index, healthy=pi is not None,
                                    partition=pi.partition if pi else -1, profile=prof, memory_gb=mem,
                                    hip_id=pi.hip_id if pi else -1, drm_render=pi.drm_render if pi else -1)
+
+    def _restore_records(self) -> None:
+        """After a plugin restart: adopt the pod-server allocations whose
+        records survived -- their devices stay allocated to the same owner and
+        keep their CU slots, so new replicas are laid out around live tenants'
+        masks -- and delete orphan records (devices the current slice table no
+        longer has).  Waits until the slice table is loaded (the devices of a
+        cumask node are unknown before).  A later PodResources sync
+        (:meth:`sync_allocated`) releases the adopted devices no pod holds,
+        which deletes their records and evicts their tenants."""
+        if not self._restored or self.mode != C.PARTITIONING_CUMASK or self.config is None:
+            return
+        info = {g.index: g for g in self._gpus()}
+        orphans = []
+        for did, (owner, slots) in self._restored.items():
+            d = self.devices.get(did)
+            if d is None:
+                orphans.append(did)
+                continue
+            self.allocated.setdefault(did, owner)
+            if slots and did not in self.cu_slots:
+                self.cu_slots[did] = CUSlotSet(slots, _cu_geometry(info.get(d.gpu_index))[0])
+        self._restored.clear()
+        if orphans:
+            n = self.pod_server_allocations.remove_devices(orphans)
+            log.warning("deleted %d orphan pod-server allocation record(s): devices %s are gone", n, orphans)
 
     def _layout_cu_slots(self) -> None:
         """XCD-symmetric CU slots for every slice replica (:func:`layout_slots`):
@@ -437,7 +476,10 @@ class NosAmdDevicePlugin:
                 mask = mask_hex(sorted(g["cus"]), g["n_cus"]) if g["cus"] and len(g["cus"]) < g["n_cus"] else None
                 self.pod_server_allocations.write(gi, token, {
                     "memory_gb": g["memory_gb"], "cu_mask": mask, "device_ids": g["device_ids"],
-                    "owner": owner or "unknown", "resource": resource})
+                    "owner": owner or "unknown", "resource": resource,
+                    # per-device CU slots: a restarted plugin keeps them (_restore_records)
+                    "cu_slots": {did: sorted(self.cu_slots[did].slots) for did in g["device_ids"]
+                                 if did in self.cu_slots}})
                 socks.append(str(socket_path(self.pod_server_dir, gi)))
                 alloc.mounts.append(str(socket_dir(self.pod_server_dir, gi)))
                 if mask:

@@ -52,11 +52,48 @@ def new_token() -> str:
 
 
 class AllocationStore:
-    """The device plugin's side: write and delete records."""
+    """The device plugin's side: write and delete records.
+
+    The device -> record index is rebuilt from the files at construction
+    (:meth:`load`), so a restarted plugin still finds -- and on release
+    deletes -- the records it wrote before the restart; their tenants keep
+    running until then (reference: the MIG agent re-reads the devices it
+    created from the driver and kubelet at start-up,
+    ``/root/reference/internal/controllers/migagent/actuator.go:134-138``,
+    ``pkg/resource/client.go:39-87``)."""
 
     def __init__(self, root: str | os.PathLike):
         self.root = Path(root)
         self._by_device: dict[str, set[Path]] = {}
+        self.load()
+
+    def load(self) -> list[tuple[Path, dict]]:
+        """(path, record) of every record on disk (all GPUs), re-indexed by
+        device id; unreadable or half-written files are deleted."""
+        out = []
+        self._by_device = {}
+        base = self.root / RECORDS
+        if not base.is_dir():
+            return out
+        for path in sorted(base.glob("gpu-*/*")):
+            if path.suffix != ".json":
+                path.unlink(missing_ok=True)  # a .tmp a crash left behind
+                continue
+            try:
+                rec = json.loads(path.read_text())
+                if not isinstance(rec, dict):
+                    raise ValueError("not an object")
+            except (OSError, ValueError):
+                path.unlink(missing_ok=True)
+                continue
+            for did in rec.get("device_ids", []):
+                self._by_device.setdefault(did, set()).add(path)
+            out.append((path, rec))
+        return out
+
+    def devices(self) -> set[str]:
+        """Device ids that hold a record."""
+        return {d for d, ps in self._by_device.items() if ps}
 
     def write(self, gpu: int, token: str, record: dict) -> Path:
         d = records_dir(self.root, gpu)

@@ -81,7 +81,7 @@ class Value:
 
     @property
     def numel(self) -> int:
-        return int(np.prod(self.shape, dtype=np.int64)) if self.shape else 1
+        return math.prod(self.shape)
 
     @property
     def nbytes(self) -> int:
@@ -109,10 +109,18 @@ def _int(v, what: str, lo: int | None = None) -> int:
     return v
 
 
+def _dim(d, what: str) -> int:
+    """One dimension: an int in [1, MAX_NUMEL] (products are then taken on
+    Python ints, which cannot wrap)."""
+    d = _int(d, what, 1)
+    _req(d <= MAX_NUMEL, f"{what} {d} is over {MAX_NUMEL}")
+    return d
+
+
 def _shape(v, what: str) -> tuple[int, ...]:
     _req(isinstance(v, list) and len(v) <= MAX_RANK, f"{what} must be a list of at most {MAX_RANK} dims")
-    s = tuple(_int(d, f"{what} dim", 1) for d in v)
-    _req(int(np.prod(s, dtype=np.int64)) <= MAX_NUMEL if s else True, f"{what} has more than {MAX_NUMEL} elements")
+    s = tuple(_dim(d, f"{what} dim") for d in v)
+    _req(math.prod(s) <= MAX_NUMEL, f"{what} has more than {MAX_NUMEL} elements")
     return s
 
 
@@ -225,18 +233,20 @@ def _infer(node: Node, ins: list[Value], gpu: bool) -> tuple[tuple[int, ...], st
              f"{what}: shape must be a list of integers")
         _req(sum(1 for d in want if d == -1) <= 1 and all(d == -1 or d >= 1 for d in want),
              f"{what}: shape dims must be >= 1, at most one -1")
+        _req(all(d <= MAX_NUMEL for d in want), f"{what}: shape dims must be <= {MAX_NUMEL}")
         n = ins[0].numel
-        known = int(np.prod([d for d in want if d != -1], dtype=np.int64)) if want else 1
+        known = math.prod(d for d in want if d != -1)
         if -1 in want:
             _req(known > 0 and n % known == 0, f"{what}: cannot reshape {ins[0].shape} to {want}")
             want = [n // known if d == -1 else d for d in want]
-        _req(int(np.prod(want, dtype=np.int64)) == n if want else n == 1, f"{what}: cannot reshape {ins[0].shape} to {want}")
+        _req(math.prod(want) == n, f"{what}: cannot reshape {ins[0].shape} to {want}")
         return tuple(want), ins[0].dtype
     if op == "permute":
         only("dims")
         arity(1, 1)
         dims = a.get("dims")
-        _req(isinstance(dims, list) and sorted(dims) == list(range(len(ins[0].shape))),
+        _req(isinstance(dims, list) and all(isinstance(d, int) and not isinstance(d, bool) for d in dims)
+             and sorted(dims) == list(range(len(ins[0].shape))),
              f"{what}: dims must be a permutation of 0..{len(ins[0].shape) - 1}")
         return tuple(ins[0].shape[d] for d in dims), ins[0].dtype
     if op == "expand":
@@ -247,7 +257,7 @@ def _infer(node: Node, ins: list[Value], gpu: bool) -> tuple[tuple[int, ...], st
         _req(isinstance(want, list) and len(want) == len(s), f"{what}: shape must have rank {len(s)}")
         out = []
         for src, d in zip(s, want):
-            _req(isinstance(d, int) and (d == -1 or d == src or (src == 1 and d >= 1)),
+            _req(isinstance(d, int) and (d == -1 or d == src or (src == 1 and 1 <= d <= MAX_NUMEL)),
                  f"{what}: cannot expand {s} to {want}")
             out.append(src if d == -1 else d)
         return tuple(out), ins[0].dtype
@@ -273,6 +283,23 @@ def _infer(node: Node, ins: list[Value], gpu: bool) -> tuple[tuple[int, ...], st
 
 OPS = ("linear", "layernorm", "attention", "add", "mul", *UNARY, "cat", "slice", "reshape", "permute", "expand",
        "cast", "interpolate")
+NEVER_FOLD = ("attention",)
+GEMM_OPS = ("linear",)
+
+
+def _workspace(node: Node, ins: list[Value], out: Value, f32_math: str) -> int:
+    """Transient device bytes one op allocates while it runs, beyond its
+    inputs and output (an upper bound; :meth:`Program.bytes_estimate_for`)."""
+    op = node.op
+    if op == "linear" and ins[0].dtype == "fp32" and f32_math == "h3":
+        m = ins[0].numel // ins[0].shape[-1]
+        return ins[0].nbytes + 4 * m                       # A's fp16 planes + row scales
+    if op == "attention":
+        b, s, three_hd = ins[0].shape
+        hd = three_hd // 3
+        skvp = -(-s // 32) * 32
+        return b * skvp * 6 * hd * 2 + 4 * b * s * (hd + 2 * node.attrs["heads"]) * 4 + ins[0].nbytes
+    return 0
 
 
 @dataclass
@@ -293,13 +320,41 @@ class Program:
 
     @property
     def bytes_estimate(self) -> int:
-        """Device bytes a build needs, estimated before anything is allocated:
-        weights, their fp32 x6 planes (3 bf16 copies = 1.5x an fp32 matrix),
-        the input, and the peak of the unfused graph's live activations when
-        every value is released after its last consumer (what the compiled
-        program does; fusion only removes intermediates), twice over: one
-        graph plus the solo graph's private buffers.  The measured peak of
-        the real build is checked again after it."""
+        return self.bytes_estimate_for(None)
+
+    def foldable(self) -> set[str]:
+        """Node outputs the compiler folds to constants at load time (every
+        input a weight or another folded value; never attention)."""
+        const = set(self.params)
+        out = set()
+        for n in self.nodes:
+            if n.op not in NEVER_FOLD and all(i in const for i in n.inputs):
+                const.add(n.output)
+                out.add(n.output)
+        return out
+
+    def bytes_estimate_for(self, kernel_config: dict | None = None) -> int:
+        """Device bytes a build needs, bounded before anything is allocated:
+
+        * the weights, plus their split planes under the server's fp32 math
+          (``kernel_config["f32_math"]``; h3: two fp16 planes = 1x an fp32
+          matrix + row scales; x6: three bf16 planes = 1.5x; exact: none) and
+          the folded copy LayerNorm / RMSNorm folding makes of a weight
+          (+ its two bias vectors);
+        * constant-folded values, which are weights too: they are counted as
+          persistent (they are materialised at load time and live
+          for the tenant's lifetime), never released;
+        * the input, and the peak of the unfused graph's live activations
+          when every value is released after its last consumer (what the
+          compiled program does; fusion only removes intermediates) plus the
+          largest per-op workspace live at that point (GEMM A planes, the
+          attention's K/V planes, conv im2col planes, ...; :func:`_workspace`),
+          twice over: one graph plus the solo graph's private buffers.
+
+        The measured peak of the real build is checked again after it."""
+        f32_math = (kernel_config or {}).get("f32_math", "h3")
+        folded = self.foldable()
+        persistent = sum(self.values[o].nbytes for o in folded)
         last = {}
         for k, n in enumerate(self.nodes):
             for i in n.inputs:
@@ -307,14 +362,28 @@ class Program:
         keep = set(self.outputs)
         live = peak = 0
         for k, n in enumerate(self.nodes):
+            if n.output in folded:
+                continue
+            ws = _workspace(n, [self.values[i] for i in n.inputs], self.values[n.output], f32_math)
             live += self.values[n.output].nbytes
-            peak = max(peak, live)
+            peak = max(peak, live + ws)
             for i in set(n.inputs):
                 v = self.values[i]
-                if v.kind == "node" and last.get(i) == k and i not in keep:
+                if v.kind == "node" and i not in folded and last.get(i) == k and i not in keep:
                     live -= v.nbytes
-        planes = sum(v.nbytes * 3 // 2 for v in self.params.values() if v.dtype == "fp32" and len(v.shape) == 2)
-        return self.param_bytes + planes + sum(v.nbytes for v in self.inputs) + 2 * peak
+        plane_mult = {"h3": 1.0, "x6": 1.5}.get(f32_math, 0.0)
+        planes = 0
+        by_out = {n.output: n for n in self.nodes}
+        for n in self.nodes:
+            if n.op not in GEMM_OPS or len(n.inputs) < 2 or n.inputs[1] not in self.params:
+                continue
+            w = self.values[n.inputs[1]]
+            if w.dtype == "fp32":
+                planes += int(w.nbytes * plane_mult) + 4 * w.shape[0]
+            src = by_out.get(n.inputs[0])
+            if src is not None and src.op in ("layernorm", "rmsnorm"):  # the folded copy + c1 / c2
+                planes += w.nbytes + 8 * w.shape[0]
+        return self.param_bytes + planes + persistent + sum(v.nbytes for v in self.inputs) + 2 * peak
 
     # ------------------------------------------------------------ tensors
     def tensors(self, device) -> dict:
@@ -428,7 +497,7 @@ def parse(obj: dict, payload: bytes | memoryview = b"", gpu: bool = False) -> Pr
         _req(isinstance(attrs, dict), "attrs must be an object")
         n = Node(op, list(refs), _name(d.get("output"), "node output"), dict(attrs))
         shape, dt = _infer(n, [values[r] for r in refs], gpu)
-        _req(int(np.prod(shape, dtype=np.int64)) <= MAX_NUMEL, f"node {n.output!r}: output too large")
+        _req(math.prod(shape) <= MAX_NUMEL, f"node {n.output!r}: output too large")
         define(Value(n.output, shape, dt, "node"))
         nodes.append(n)
     outs = obj.get("outputs")
@@ -526,12 +595,24 @@ class CompiledProgram:
 
     # ------------------------------------------------------------ passes
     def _fold_constants(self, prog: Program) -> list[_Step]:
+        """Run every all-constant node once at load time.  A constant is freed
+        as soon as no later node (folded or not) and no output uses it, so a
+        chain of large folded values never holds more than its live links
+        (:meth:`Program.bytes_estimate_for` counts them as weights)."""
+        last: dict[str, int] = {}
+        for k, n in enumerate(prog.nodes):
+            for i in n.inputs:
+                last[i] = k
+        keep = set(self.outputs)
         steps = []
         folded = 0
-        for n in prog.nodes:
-            if all(i in self.consts for i in n.inputs) and n.op != "attention":
+        for k, n in enumerate(prog.nodes):
+            if all(i in self.consts for i in n.inputs) and n.op not in NEVER_FOLD:
                 self.consts[n.output] = _eager(n.op, [self.consts[i] for i in n.inputs], n.attrs).contiguous()
                 folded += 1
+                for i in set(n.inputs):
+                    if last.get(i) == k and i not in keep:
+                        self.consts.pop(i, None)
             else:
                 steps.append(_Step(n.op, list(n.inputs), n.output, dict(n.attrs)))
         # weights only feeding folded nodes are dead now

@@ -65,14 +65,16 @@ def send_msg(sock: socket.socket, obj: dict, payload: bytes | memoryview = b"") 
 
 
 def recv_msg(sock: socket.socket, payload_limit=None) -> tuple[dict, bytes | bytearray]:
-    """(JSON object, payload).  ``payload_limit(obj) -> int`` bounds the
-    payload of this message (default ``MAX_PAYLOAD``).  An oversized JSON
+    """(JSON object, payload).  ``payload_limit(obj, npay) -> int`` bounds
+    the payload of this message (default ``MAX_PAYLOAD``); it sees the
+    announced payload size before a byte of it is read, so a receiver can
+    reserve (or refuse) what the payload is for first.  An oversized JSON
     header desynchronises nothing that can be trusted: ConnectionError."""
     nj, npay = _HDR.unpack(_recv_exact(sock, _HDR.size))
     if nj > MAX_JSON:
         raise ConnectionError(f"message header too large ({nj} B)")
     obj = json.loads(_recv_exact(sock, nj))
-    limit = MAX_PAYLOAD if payload_limit is None or not isinstance(obj, dict) else int(payload_limit(obj))
+    limit = MAX_PAYLOAD if payload_limit is None or not isinstance(obj, dict) else int(payload_limit(obj, npay))
     if npay > limit:
         _drain(sock, npay)
         raise PayloadTooLarge(f"payload of {npay} B is over this request's limit of {limit} B")

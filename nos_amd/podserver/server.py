@@ -131,7 +131,7 @@ class PodServer:
                  max_tenants: int = DEFAULT_MAX_TENANTS, memory_gb: float | None = None, graphs: bool = True,
                  kernel_config: dict | None = None, solo_graphs: bool = True,
                  allocations_dir: str | os.PathLike | None = None, pod_resources=None,
-                 reap_interval_s: float = 1.0):
+                 reap_interval_s: float = 1.0, max_inflight_register_gb: float = 16.0):
         """``allocations_dir``: this GPU's allocation records (tokens
         required; allocations.py).  Without it admission is open: the client
         declares its slice, which must be > 0 when the server accounts
@@ -168,6 +168,8 @@ class PodServer:
         self.reap_interval_s = reap_interval_s
         self._pending: dict[int, float] = {}    # tenant id -> slice GB reserved while its build runs
         self._tokens: set[str] = set()           # tokens holding a tenant (or a pending build)
+        self._inflight_bytes = 0                 # register payload bytes claimed and not yet built
+        self.max_inflight_register_bytes = int(max_inflight_register_gb * 2 ** 30)
         self.evictions = 0
 
     # ------------------------------------------------------------ lifecycle
@@ -299,21 +301,40 @@ class PodServer:
 
     def _serve(self, conn: socket.socket) -> None:
         tenant: Tenant | None = None
+        claim: dict = {}   # this connection's register reservation (_claim), made before its payload is read
+
+        def limit(req: dict, npay: int) -> int:
+            if req.get("op") != "register":
+                return P.MAX_PAYLOAD
+            claim.clear()
+            if tenant is not None:
+                claim["error"] = "AdmissionError: connection already holds a tenant"
+                return 0
+            try:
+                return self._claim(req, npay, claim)
+            except AdmissionError as e:
+                claim.clear()
+                claim["error"] = f"AdmissionError: {e}"
+                return 0
+
         try:
             while not self._stop.is_set():
                 try:
-                    req, payload = P.recv_msg(conn, self._payload_limit)
+                    req, payload = P.recv_msg(conn, limit)
                 except P.ProtocolError as e:  # payload drained: the connection is still in step
-                    P.send_msg(conn, {"ok": False, "error": f"{type(e).__name__}: {e}"})
+                    err = claim.pop("error", None) or f"{type(e).__name__}: {e}"
+                    self._release_claim(claim)
+                    P.send_msg(conn, {"ok": False, "error": err})
                     continue
                 except (ConnectionError, OSError, ValueError):
+                    self._release_claim(claim)
                     return
                 op = req.get("op")
                 try:
                     if op == "register":
-                        if tenant is not None:
-                            raise AdmissionError("connection already holds a tenant")
-                        tenant = self._register(req, payload, conn)
+                        if "error" in claim:
+                            raise AdmissionError(claim.pop("error").split(": ", 1)[-1])
+                        tenant = self._register(req, payload, conn, claim)
                         P.send_msg(conn, {"ok": True, "tenant": tenant.id, "footprint_gb": tenant.footprint_gb,
                                           "memory_limit_gb": tenant.memory_limit_gb, "cu_mask": tenant.cu_mask,
                                           "input_shape": list(tenant.x.shape), "server": self.info,
@@ -341,26 +362,64 @@ class PodServer:
                         return
                     else:
                         raise P.ProtocolError(f"unknown op {op!r}")
-                except (AdmissionError, P.ProtocolError, RuntimeError, ValueError, KeyError) as e:
+                except Exception as e:  # noqa: BLE001 -- reported to this client; the server keeps serving
+                    if op == "register":
+                        self._release_claim(claim)
                     P.send_msg(conn, {"ok": False, "error": f"{type(e).__name__}: {e}"})
         finally:
+            self._release_claim(claim)
             if tenant is not None:
                 self._unregister(tenant)
             with self._lock:
                 self._conns.pop(conn, None)
             conn.close()
 
-    def _payload_limit(self, req: dict) -> int:
-        """Bytes a request may carry: a register request's weights may fill
-        its memory slice (the static estimate then checks weights +
-        activations against it); everything else is an input image."""
-        if req.get("op") != "register":
-            return P.MAX_PAYLOAD
-        try:
-            limit = self._admission(req)[0]
-        except AdmissionError:
-            return P.MAX_PAYLOAD  # _register reports the admission error itself
-        return int(limit * 2 ** 30) if limit else int((self.memory_gb or 64) * 2 ** 30)
+    def _claim(self, req: dict, npay: int, claim: dict) -> int:
+        """Admit a register request BEFORE its payload is read: check the
+        token, claim it (one tenant per token), reserve a tenant slot, the
+        slice's memory and ``npay`` bytes of the server's in-flight register
+        budget, all under the lock.  Returns the payload limit (the slice:
+        weights may fill it, the static estimate then checks weights +
+        activations).  A second register with the same token, or many
+        connections sending slice-sized weights at once, are refused before
+        any of their bytes are buffered in host memory."""
+        limit, mask, token, record, dev_ids = self._admission(req)
+        cap = int(limit * 2 ** 30) if limit else int((self.memory_gb or 64) * 2 ** 30)
+        with self._lock:
+            if token is not None and token in self._tokens:
+                raise AdmissionError("the allocation already holds a tenant (or a registration in flight)")
+            if len(self.tenants) + len(self._pending) >= self.max_tenants:
+                raise AdmissionError(f"server full ({self.max_tenants} tenants)")
+            if self.memory_gb and limit:
+                held = sum(t.memory_limit_gb for t in self.tenants.values()) + sum(self._pending.values())
+                if held + limit > self.memory_gb + 1e-6:
+                    raise AdmissionError(f"slice of {limit} GB does not fit: {held} of {self.memory_gb} GB held")
+            # host memory: registrations buffer their weights here; one may always
+            # proceed (a big tenant is never starved), more only within the budget
+            if self._inflight_bytes and self._inflight_bytes + min(npay, cap) > self.max_inflight_register_bytes:
+                raise AdmissionError(f"{self._inflight_bytes / 2 ** 30:.1f} GB of registrations in flight; retry")
+            tid = self._next_id
+            self._next_id += 1
+            self._pending[tid] = limit
+            if token is not None:
+                self._tokens.add(token)
+            nb = min(npay, cap)
+            self._inflight_bytes += nb
+        claim.update(tid=tid, limit=limit, mask=mask, token=token, record=record, dev_ids=dev_ids, nbytes=nb,
+                     pending=True)
+        return cap
+
+    def _release_claim(self, claim: dict, keep_token: bool = False) -> None:
+        """Undo :meth:`_claim` (idempotent): the pending slot and memory, the
+        in-flight bytes and, unless the tenant now holds it, the token."""
+        if not claim.get("pending"):
+            return
+        with self._lock:
+            self._pending.pop(claim["tid"], None)
+            self._inflight_bytes -= claim["nbytes"]
+            if claim["token"] is not None and not keep_token:
+                self._tokens.discard(claim["token"])
+        claim.clear()
 
     # ------------------------------------------------------------ tenants
     def _admission(self, req: dict) -> tuple[float, str | None, str | None, object, tuple]:
@@ -387,44 +446,33 @@ class PodServer:
             raise AdmissionError("a memory slice (memory_limit_gb > 0) is required: the server accounts memory")
         return limit, req.get("cu_mask") or None, None, None, ()
 
-    def _register(self, req: dict, payload: bytes = b"", conn=None) -> Tenant:
+    def _register(self, req: dict, payload: bytes = b"", conn=None, claim: dict | None = None) -> Tenant:
+        """Build a tenant for a register request whose slot, memory and token
+        :meth:`_claim` reserved before its payload was read (direct callers
+        without a claim get one here); the claim is released on failure."""
         from . import program as PG
 
-        limit, mask, token, record, dev_ids = self._admission(req)
-        if "program" not in req:
-            raise AdmissionError("register carries no program (nos-amd.program/v1 op graph + weights)")
-        prog = PG.parse(req["program"], payload, gpu=self.gpu)
-        need = prog.bytes_estimate / 2 ** 30
-        if limit and need > limit:
-            raise AdmissionError(f"tenant needs {need:.2f} GB (static estimate), its slice has {limit} GB")
-        with self._lock:
-            if token is not None and token in self._tokens:
-                raise AdmissionError("the allocation already holds a tenant")
-            if len(self.tenants) + len(self._pending) >= self.max_tenants:
-                raise AdmissionError(f"server full ({self.max_tenants} tenants)")
-            if self.memory_gb and limit:
-                held = sum(t.memory_limit_gb for t in self.tenants.values()) + sum(self._pending.values())
-                if held + limit > self.memory_gb + 1e-6:
-                    raise AdmissionError(f"slice of {limit} GB does not fit: {held} of {self.memory_gb} GB held")
-            tid = self._next_id
-            self._next_id += 1
-            self._pending[tid] = limit           # reserved before the slow build
-            if token is not None:
-                self._tokens.add(token)
+        if claim is None or not claim.get("pending"):
+            claim = {}
+            self._claim(req, len(payload), claim)
         try:
+            if "program" not in req:
+                raise AdmissionError("register carries no program (nos-amd.program/v1 op graph + weights)")
+            prog = PG.parse(req["program"], payload, gpu=self.gpu)
+            limit, mask, tid = claim["limit"], claim["mask"], claim["tid"]
+            need = prog.bytes_estimate_for(self.kernel_config) / 2 ** 30
+            if limit and need > limit:
+                raise AdmissionError(f"tenant needs {need:.2f} GB (static estimate), its slice has {limit} GB")
             with self._build_lock:
                 t = self._build(tid, req, prog, limit, mask)
         except BaseException:
-            with self._lock:
-                self._pending.pop(tid, None)
-                if token is not None:
-                    self._tokens.discard(token)
+            self._release_claim(claim)
             raise
-        t.token, t.record_path, t.device_ids, t.conn = token, record, dev_ids, conn
+        t.token, t.record_path, t.device_ids, t.conn = claim["token"], claim["record"], claim["dev_ids"], conn
         with self._lock:
-            self._pending.pop(tid, None)
             self.tenants[tid] = t
             M.PODSERVER_TENANTS.labels(self.gpu_label).set(len(self.tenants))
+        self._release_claim(claim, keep_token=True)
         log.info("tenant %d (%s, %s) registered: %.3f GB of a %s GB slice", tid, t.pod, t.program, t.footprint_gb,
                  limit or "-")
         return t

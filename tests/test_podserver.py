@@ -294,7 +294,13 @@ def test_manifests_render_the_pod_server_and_its_configs():
     ds = [o for o in yaml.safe_load_all(out["podserver/daemonset.yaml"]) if o and o["kind"] == "DaemonSet"][0]
     spec = ds["spec"]["template"]["spec"]
     assert spec["nodeSelector"] == {C.LABEL_GPU_PARTITIONING: C.PARTITIONING_CUMASK}
-    assert spec["containers"][0]["args"][:2] == ["--gpus", "all"]
+    args = spec["containers"][0]["args"]
+    assert args[:2] == ["--gpus", "all"]
+    # the PodResources reaper is on in deployment: flag + the kubelet socket's directory
+    assert args[args.index("--pod-resources-socket") + 1] == C.KUBELET_PODRESOURCES_SOCKET
+    mounts = {v["mountPath"] for v in spec["containers"][0]["volumeMounts"]}
+    assert "/var/lib/kubelet/pod-resources" in mounts
+    assert any(v.get("hostPath", {}).get("path") == "/var/lib/kubelet/pod-resources" for v in spec["volumes"])
 
     def embedded(key, fname):
         cm = [o for o in yaml.safe_load_all(out[key]) if o and o["kind"] == "ConfigMap"][0]

@@ -332,3 +332,180 @@ def test_a_pod_exits_nonzero_when_its_server_dies(tmp_path):
         for p in (pod, srv):
             if p.poll() is None:
                 p.kill()
+
+
+# ----------------------------------------------------------------- claims before payloads
+def _raw_register(path, token, npay, send=None):
+    """A register request announcing ``npay`` payload bytes, of which only
+    ``send`` are sent (default all): the server's claim happens on the header."""
+    import json
+    import socket
+    import struct
+
+    s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    s.connect(str(path))
+    prog, w = PG.mlp_program(dim=64, layers=1, batch=8, dtype="fp32")
+    w = w + bytes(npay - len(w)) if npay > len(w) else w[:npay]
+    js = json.dumps({"op": "register", "pod": "raw", "token": token, "program": prog, "memory_limit_gb": 1}).encode()
+    s.sendall(struct.pack(">IQ", len(js), len(w)) + js)
+    s.sendall(w[:len(w) if send is None else send])
+    return s, w
+
+
+def test_a_token_is_claimed_before_its_payload_is_read(tokened):
+    """one valid token on many connections, each sending slice-sized
+    weights, must not make the server buffer N x slice bytes.  The first
+    connection's header claims the token; a second register with it is refused
+    while the first payload is still in flight."""
+    from nos_amd.podserver import protocol as P
+
+    store, srv = tokened
+    store.write(1, "tok-x", {"memory_gb": 10, "device_ids": ["g1::10gb::7"]})
+    a, w = _raw_register(srv.path, "tok-x", 1 << 20, send=1 << 10)   # stalls mid-payload
+    assert _wait(lambda: "tok-x" in srv._tokens and srv.stats()["pending"] == 1)
+    c = PodClient(srv.path, connect_timeout_s=5)
+    with pytest.raises(PodServerError, match="registration in flight"):
+        c.register("again", *YOLOS, token="tok-x")
+    a.sendall(w[1 << 10:])                                            # the first one completes
+    rep, _ = P.recv_msg(a)
+    assert rep["ok"], rep
+    assert len(srv.tenants) == 1 and srv._inflight_bytes == 0
+    a.close()
+    c.close()
+
+
+def test_register_bytes_in_flight_are_capped(tmp_path):
+    from nos_amd.podserver import protocol as P
+
+    srv = PodServer(tmp_path / "s.sock", device="cpu", lanes=1, memory_gb=40,
+                    max_inflight_register_gb=1.5 / 1024).start()   # 1.5 MiB
+    try:
+        a, w = _raw_register(srv.path, None, 1 << 20, send=10)       # 1 MiB claimed, stalled
+        assert _wait(lambda: srv._inflight_bytes == 1 << 20)
+        b, _ = _raw_register(srv.path, None, 1 << 20)                # would make 2 MiB: refused, drained
+        rep, _ = P.recv_msg(b)
+        assert not rep["ok"] and "in flight" in rep["error"]
+        assert srv.stats()["pending"] == 1
+        a.sendall(w[10:])
+        assert P.recv_msg(a)[0]["ok"]
+        assert srv._inflight_bytes == 0 and srv.stats()["pending"] == 0
+        b2, _ = _raw_register(srv.path, None, 1 << 20)               # room again
+        assert P.recv_msg(b2)[0]["ok"]
+        for s in (a, b, b2):
+            s.close()
+    finally:
+        srv.stop()
+
+
+def test_a_dropped_connection_releases_its_claim(tokened):
+    store, srv = tokened
+    store.write(1, "tok-d", {"memory_gb": 10, "device_ids": ["g1::10gb::8"]})
+    a, _ = _raw_register(srv.path, "tok-d", 1 << 20, send=100)
+    assert _wait(lambda: srv.stats()["pending"] == 1)
+    a.close()                                                        # mid-payload
+    assert _wait(lambda: srv.stats()["pending"] == 0 and not srv._tokens and srv._inflight_bytes == 0)
+    c = PodClient(srv.path, connect_timeout_s=5)
+    c.register("p", *YOLOS, token="tok-d")                           # the token is usable again
+    c.close()
+
+
+# ----------------------------------------------------------------- device plugin restart
+def _pod_server_plugin(root, smi):
+    from nos_amd.deviceplugin.plugin import NosAmdDevicePlugin
+
+    p = NosAmdDevicePlugin("n1", smi, mode=C.PARTITIONING_CUMASK, cu_policy="even", pod_server_dir=str(root))
+    p.set_config("n1-1", {"gpus": [{"index": 0, "slices": [{"profile": "10gb", "replicas": 4}]}]})
+    return p
+
+
+def test_plugin_restart_keeps_live_records_and_their_cu_slots(tmp_path):
+    """records survive a device-plugin restart -- the new
+    process adopts them (devices stay allocated, CU slots stay put), a new pod
+    gets a non-overlapping mask, orphan records are deleted, and records of
+    pods PodResources no longer lists are released."""
+    from nos_amd.gpu.fakesmi import FakeSmi
+    from nos_amd.podserver.allocations import lookup
+
+    smi = FakeSmi(gpus=1, node="n1")
+    root = tmp_path / "ps"
+    p1 = _pod_server_plugin(root, smi)
+    ids = sorted(d.id for d in p1.list_devices("amd.com/gpu-10gb"))
+    toks, masks = {}, {}
+    for did in ids[:3]:
+        a = p1.allocate("amd.com/gpu-10gb", [did], owner=f"ns/{did}")
+        toks[did], masks[did] = a.envs[C.ENV_POD_TOKEN], a.envs[C.ENV_POD_CU_MASK]
+    slots1 = {did: p1.cu_slots[did].slots for did in ids[:3]}
+    # an orphan: a record for a device no slice table has any more
+    AllocationStore(root).write(0, "tok-orphan", {"memory_gb": 10, "device_ids": ["gone::10gb::0"]})
+    del p1                                                           # the plugin process restarts
+
+    p2 = _pod_server_plugin(root, smi)
+    assert {did: p2.allocated[did] for did in ids[:3]} == {did: f"ns/{did}" for did in ids[:3]}
+    assert {did: p2.cu_slots[did].slots for did in ids[:3]} == slots1
+    for did in ids[:3]:
+        assert lookup(records_dir(root, 0), toks[did]) is not None   # records kept, tenants keep running
+    assert lookup(records_dir(root, 0), "tok-orphan") is None        # orphan deleted
+    new = p2.allocate("amd.com/gpu-10gb", [ids[3]], owner="ns/new")
+    new_cus = set(p2.cus_of(ids[3]))
+    assert new_cus and all(not (new_cus & set(p2.cus_of(did))) for did in ids[:3])
+    assert int(new.envs[C.ENV_POD_CU_MASK], 16) & int(masks[ids[0]], 16) == 0
+    # PodResources: the pod of ids[0] is gone -> its record goes (its tenant is evicted)
+    p2.sync_allocated(set(ids[1:]))
+    assert lookup(records_dir(root, 0), toks[ids[0]]) is None
+    assert lookup(records_dir(root, 0), toks[ids[1]]) is not None
+
+
+def test_pod_server_allocations_are_mounted_read_only(tmp_path):
+    from nos_amd.deviceplugin.grpc_server import _ResourceServicer
+    from nos_amd.gpu.fakesmi import FakeSmi
+    from nos_amd.grpcapi.protos import deviceplugin as pb
+
+    p = _pod_server_plugin(tmp_path / "ps", FakeSmi(gpus=1, node="n1"))
+
+    class Owner:
+        plugin = p
+
+    ids = [d.id for d in p.list_devices("amd.com/gpu-10gb")]
+    req = pb.AllocateRequest(container_requests=[pb.ContainerAllocateRequest(devices_ids=[i]) for i in ids[:2]])
+    rep = _ResourceServicer(Owner(), "amd.com/gpu-10gb").Allocate(req, None)
+    mounts = [m for cr in rep.container_responses for m in cr.mounts]
+    assert len(mounts) == 2 and all(m.read_only for m in mounts)
+    assert all(m.host_path == str(tmp_path / "ps" / "gpu-0") for m in mounts)
+
+
+# ----------------------------------------------------------------- ADVICE r4: estimate + overflow
+@pytest.mark.parametrize("shape", [[2 ** 62, 4], [2 ** 63, 1], [2 ** 40, 2 ** 40]])
+def test_huge_shapes_are_refused_not_wrapped(shape):
+    b = PG.Builder("huge")
+    b.input("x", shape)
+    b.op("relu", "x", out="y")
+    with pytest.raises(PG.ProgramError, match="over|more than"):
+        PG.parse(*b.build(["y"]))
+
+
+def test_mixed_permute_dims_are_a_program_error():
+    b = PG.Builder("perm")
+    b.input("x", [2, 3])
+    b.op("permute", "x", dims=[1, "0"], out="y")
+    with pytest.raises(PG.ProgramError, match="permutation"):
+        PG.parse(*b.build(["y"]))
+
+
+def test_constant_folded_chains_count_as_persistent_weights():
+    """A chain of all-constant nodes is materialised at load time: the static
+    estimate must count every folded value, not release it like an activation."""
+    b = PG.Builder("fold")
+    x = b.input("x", [4, 64])
+    w = b.param("w", np.ones((1, 64), np.float32))
+    big = [b.op("expand", w, shape=[4096, 64])]
+    for _ in range(4):
+        big.append(b.op("mul", big[-1], big[-1]))
+    y = b.op("add", x, b.op("slice", big[-1], dim=0, start=0, end=4))
+    p = PG.parse(*b.build([y]))
+    assert p.foldable() >= set(big)
+    assert p.bytes_estimate >= sum(p.values[v].nbytes for v in big)
+    import torch
+
+    m = p.compile("cpu")
+    assert set(big).isdisjoint(m.consts)           # dead folded values were freed
+    assert torch.allclose(m(torch.zeros(4, 64))[0], torch.ones(4, 64))
