@@ -26,7 +26,15 @@
 
 namespace {
 
-enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8 };
+enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8, EPI_BIAS_ROW = 16 };
+
+// batched GEMMs (nos_gemm_f32h3_batched): per-batch element strides of every
+// operand (0 = shared by the whole batch, e.g. a conv weight); the tile index
+// runs over nb x tiles_m x tiles_n, one batch's tiles adjacent (one XCD's L2)
+struct Batch {
+  int nb = 1;
+  long long a = 0, rinv = 0, w = 0, csc = 0, c = 0, r = 0;
+};
 
 constexpr int BK = 32;  // K granule of the API (K % 32 == 0); stages are BKT = 32 or 16 deep
 
@@ -97,7 +105,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     const _Float16* __restrict__ Ap, int lda, long long aplane, const float* __restrict__ rinv, float rconst,
     const _Float16* __restrict__ Wp, int ldw, long long wplane, const float* __restrict__ csc,
     const float* __restrict__ bias, const float* __restrict__ R, int ldr, float* __restrict__ C, int ldc, int M,
-    int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv, PlaneOut po) {
+    int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv, PlaneOut po, Batch bt) {
   constexpr int NW = WGM * WGN, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
   static_assert((NW == 4 || NW == 8) && MI >= 1 && NI >= 1, "4 or 8 waves");
   constexpr int ROWB = BKT * 2, CH = ROWB / 16, RPP = 1024 / ROWB, NSTEP = BKT / 16;
@@ -112,7 +120,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int c = lane & 31, h = lane >> 5;
   const int wm = wid / WGN, wn = wid % WGN;
-  const int ntiles = tiles_m * tiles_n;
+  const int ntiles1 = tiles_m * tiles_n, ntiles = ntiles1 * bt.nb;
   const int nk = K / BKT;
   nos::XcdChunk chunk;
   if constexpr (PERSIST) {
@@ -124,8 +132,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   }
   for (int tt = chunk.first; tt < chunk.end; tt += chunk.step) {
     if (PERSIST && tt != chunk.first) __syncthreads();
-    const int tm = tt / tiles_n, tn = tt - tm * tiles_n;
+    const int bb = tt / ntiles1, t1 = tt - bb * ntiles1;
+    const int tm = t1 / tiles_n, tn = t1 - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
+    // this tile's batch element (wave-uniform scalar offsets)
+    const _Float16* __restrict__ Ab = Ap + bb * bt.a;
+    const _Float16* __restrict__ Wb = Wp + bb * bt.w;
+    const float* __restrict__ rinvb = rinv != nullptr ? rinv + bb * bt.rinv : nullptr;
+    const float* __restrict__ cscb = csc + bb * bt.csc;
+    float* __restrict__ Cb = C != nullptr ? C + bb * bt.c : nullptr;
+    const float* __restrict__ Rb = R != nullptr ? R + bb * bt.r : nullptr;
 
     // a 1 KiB piece = RPP rows x ROWB bytes of one plane; lane L: row L / CH, chunk L % CH
     auto stage = [&](int k0, unsigned char* dst) {
@@ -136,7 +152,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         const int row = rb + lane / CH;
         int g = m0 + row;
         g = g < M ? g : M - 1;
-        glds16(Ap + plane * aplane + (long long)g * lda + k0 + (((lane % CH) ^ swz<CH>(row)) << 3),
+        glds16(Ab + plane * aplane + (long long)g * lda + k0 + (((lane % CH) ^ swz<CH>(row)) << 3),
                dst + plane * BM * ROWB + rb * ROWB);
       }
 #pragma unroll
@@ -146,7 +162,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         const int row = rb + lane / CH;
         int g = n0 + row;
         g = g < N ? g : N - 1;
-        glds16(Wp + plane * wplane + (long long)g * ldw + k0 + (((lane % CH) ^ swz<CH>(row)) << 3),
+        glds16(Wb + plane * wplane + (long long)g * ldw + k0 + (((lane % CH) ^ swz<CH>(row)) << 3),
                dst + TA + plane * BN * ROWB + rb * ROWB);
       }
     };
@@ -243,13 +259,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     __syncthreads();  // every wave is done with the ring (the next tile's prologue)
 
     // epilogue: register r of lane (c, h) = row (r&3) + 8(r>>2) + 4h of the block, column c
-    float rsv[MI][16];
+    float rsv[MI][16], rbv[MI][16];  // row scales; row bias (conv: per output channel)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        rsv[i][r] = rinv != nullptr ? rinv[m < M ? m : M - 1] : rconst;
+        rsv[i][r] = rinvb != nullptr ? rinvb[m < M ? m : M - 1] : rconst;
+        rbv[i][r] = (epi & EPI_BIAS_ROW) ? bias[m < M ? m : M - 1] : 0.f;
       }
     // interior tile stored as fp32 C (the common case): tile-local 32-bit
     // offsets from wave-uniform base pointers (saddr stores, no 64-bit
@@ -278,7 +295,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int cl = wn * (BN / WGN) + j * 32 + c;
-        const float cs = csc[n0 + cl];
+        const float cs = cscb[n0 + cl];
         const float p2 = (epi & EPI_BIAS) ? bias[n0 + cl] : 0.f;
         const float osc = po.p != nullptr ? po.sc : kv.kvsc[t * (kv.hd >> 6) + ((n0 - kv.qcols - t * kv.hd + cl) >> 6)];
 #pragma unroll
@@ -286,7 +303,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2);
+            float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
             if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
             if (epi & EPI_RELU) v = fmaxf(v, 0.f);
             const float x = v * osc;
@@ -302,19 +319,19 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     }
     const bool interior = full && po.p == nullptr && (kv.kvs == nullptr || n0 + BN <= kv.qcols);  // Q columns too
     if (interior) {
-      float* Ct = C + (long long)m0 * ldc + n0;
-      const float* Rt = (epi & EPI_RESID) ? R + (long long)m0 * ldr + n0 : nullptr;
+      float* Ct = Cb + (long long)m0 * ldc + n0;
+      const float* Rt = (epi & EPI_RESID) ? Rb + (long long)m0 * ldr + n0 : nullptr;
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int cl = wn * (BN / WGN) + j * 32 + c;
-        const float cs = csc[n0 + cl];
+        const float cs = cscb[n0 + cl];
         const float p2 = (epi & EPI_BIAS) ? bias[n0 + cl] : 0.f;
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2);
+            float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
             if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
             if (epi & EPI_RELU) v = fmaxf(v, 0.f);
             if (epi & EPI_RESID) v += Rt[(unsigned)(rl * ldr + cl)];
@@ -328,18 +345,18 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     for (int j = 0; j < NI; ++j) {
       const int n = n0 + wn * (BN / WGN) + j * 32 + c;
       const int nc = n < N ? n : N - 1;
-      const float cs = csc[nc];
+      const float cs = cscb[nc];
       const float p2 = (epi & EPI_BIAS) ? bias[nc] : 0.f;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2);
+          float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
           if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
           if (epi & EPI_RELU) v = fmaxf(v, 0.f);
           if (m < M && n < N) {
-            if (epi & EPI_RESID) v += R[(long long)m * ldr + n];
+            if (epi & EPI_RESID) v += Rb[(long long)m * ldr + n];
             if (kv.kvs != nullptr && n >= kv.qcols) {
               const int t = (n - kv.qcols) >= kv.hd;  // 0: K, 1: V
               const int col = n - kv.qcols - t * kv.hd;
@@ -358,7 +375,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
               po.p[(long long)m * po.ldp + n] = __builtin_bit_cast(unsigned short, h0);
               po.p[po.pplane + (long long)m * po.ldp + n] = __builtin_bit_cast(unsigned short, h1);
             } else {
-              C[(long long)m * ldc + n] = v;
+              Cb[(long long)m * ldc + n] = v;
             }
           }
         }
@@ -370,9 +387,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
 template <int BM, int BN, int WGM, int WGN, int BKT = 32, int RS = 2>
 int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, float rconst, const _Float16* Wp,
              int ldw, long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C, int ldc,
-             int M, int N, int K, int epi, KvOut kv, PlaneOut po, hipStream_t st) {
+             int M, int N, int K, int epi, KvOut kv, PlaneOut po, Batch bt, hipStream_t st) {
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
-  const long long ntiles = (long long)tiles_m * tiles_n;
+  const long long ntiles = (long long)tiles_m * tiles_n * bt.nb;
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
   const size_t lds = RS * (size_t)(2 * BM * BKT * 2 + 2 * BN * BKT * 2);
   constexpr int NT = 64 * WGM * WGN;
@@ -380,11 +397,11 @@ int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, f
   if (grid < ntiles)
     hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS>), dim3((unsigned)grid), dim3(NT), lds, st, Ap, lda,
                        aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
-                       tiles_n, kv, po);
+                       tiles_n, kv, po, bt);
   else
     hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false, BKT, RS>), dim3((unsigned)ntiles), dim3(NT), lds, st, Ap,
                        lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
-                       tiles_n, kv, po);
+                       tiles_n, kv, po, bt);
   return (int)hipGetLastError();
 }
 
@@ -429,7 +446,21 @@ __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restr
   }
   float mu = 0.f, rs = 1.f;
   int e;
-  if (ln) {
+  if (ln == 2) {  // RMSNorm: x / sqrt(mean(x^2) + eps) (gamma folded into the weight)
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < nchunk; ++i) {
+      const int k = (lane + LPR * i) * 4;
+      if (k < K) {
+        const float4 x = get(i, k);
+        q = fmaf(x.x, x.x, fmaf(x.y, x.y, fmaf(x.z, x.z, fmaf(x.w, x.w, q))));
+      }
+    }
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    rs = rsqrtf(q / (float)K + eps);
+    e = eln;  // |x^| <= sqrt(K) for an RMS-normalised row too
+  } else if (ln) {
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < nchunk; ++i) {
@@ -501,13 +532,14 @@ NOS_API int nos_gemm_f32h3_set_layout(int layout) {
 // stride ldp, plane stride pplane elements) on per-row power-of-two scales,
 // rinv[m] = 1 / scale.  ln != 0: the rows are LayerNorm-normalised first
 // (no gamma / beta: those are folded into the weight and bias) and scaled by
-// 2^eln (the host's bound for |x^| <= sqrt(K)).  K % 4 == 0, rows 16-byte aligned.
+// 2^eln (the host's bound for |x^| <= sqrt(K)); ln == 2: RMSNorm-normalised
+// (x / sqrt(mean(x^2) + eps), same bound).  K % 4 == 0, rows 16-byte aligned.
 NOS_API int nos_split_rows_h3(const float* A, int lda, void* P, int ldp, long long pplane, float* rinv, int M, int K,
                               int ln, float eps, int eln, hipStream_t stream) {
   if (M <= 0 || K <= 0 || (K % 4) || (lda % 4) || (ldp % 4) || ldp < K || pplane < (long long)M * ldp)
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)A) | ((uintptr_t)P)) & 15) return (int)hipErrorInvalidValue;
-  if (eln < -126 || eln > 126) return (int)hipErrorInvalidValue;
+  if (eln < -126 || eln > 126 || ln < 0 || ln > 2) return (int)hipErrorInvalidValue;
   auto* p = static_cast<_Float16*>(P);
   const dim3 grid((unsigned)((M + 3) / 4)), blk(256);
   if (K <= 512) {  // a half-wave per row: every lane busy at K = 384, one fewer reduction step
@@ -525,6 +557,34 @@ NOS_API int nos_split_rows_h3(const float* A, int lda, void* P, int ldp, long lo
     hipLaunchKernelGGL(split_rows_h3_kernel<0>, grid, blk, 0, stream, A, lda, p, ldp, pplane, rinv, M, K, ln, eps, eln);
   return (int)hipGetLastError();
 }
+
+namespace {
+
+int run_h3(const void* Ap, int lda, long long aplane, const float* rinv, float rconst, const void* Wp, int ldw,
+           long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C, int ldc, int M,
+           int N, int K, int epi, KvOut kv, PlaneOut po, Batch bt, hipStream_t stream) {
+  const auto* a = static_cast<const _Float16*>(Ap);
+  const auto* w = static_cast<const _Float16*>(Wp);
+  if (g_layout == 3)
+    return launch_t<128, 128, 4, 1, 32, 3>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
+                                           N, K, epi, kv, po, bt, stream);
+  if (g_layout == 4)
+    return launch_t<128, 128, 4, 1, 16, 4>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
+                                           N, K, epi, kv, po, bt, stream);
+  if (g_layout == 5)
+    return launch_t<128, 128, 2, 2, 16, 4>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
+                                           N, K, epi, kv, po, bt, stream);
+  if (g_layout == 2)
+    return launch_t<256, 128, 4, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
+                                    epi, kv, po, bt, stream);
+  if (g_layout == 1)
+    return launch_t<128, 128, 2, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
+                                    epi, kv, po, bt, stream);
+  return launch_t<128, 128, 4, 1>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
+                                  epi, kv, po, bt, stream);
+}
+
+}  // namespace
 
 // C = act(rinv[m] csc[n] (A' . W'^T) + bias) (+ R) on the fp16 planes of A
 // (nos_split_rows_h3, or a producer's plane output; rinv == nullptr: every
@@ -545,6 +605,7 @@ NOS_API int nos_gemm_f32h3(const void* Ap, int lda, long long aplane, const floa
   if ((((uintptr_t)Ap) | ((uintptr_t)Wp)) & 15) return (int)hipErrorInvalidValue;
   if ((!rinv && !(rconst > 0.f)) || !csc || ((epi & EPI_BIAS) && !bias) || ((epi & EPI_RESID) && (!R || ldr < N)))
     return (int)hipErrorInvalidValue;
+  if ((epi & EPI_BIAS_ROW) && ((epi & EPI_BIAS) || !bias)) return (int)hipErrorInvalidValue;
   KvOut kv;
   PlaneOut po;
   if (kvs != nullptr) {
@@ -566,23 +627,41 @@ NOS_API int nos_gemm_f32h3(const void* Ap, int lda, long long aplane, const floa
   } else if (ldc < (kvs != nullptr ? N / 3 : N)) {
     return (int)hipErrorInvalidValue;
   }
-  const auto* a = static_cast<const _Float16*>(Ap);
-  const auto* w = static_cast<const _Float16*>(Wp);
-  if (g_layout == 3)
-    return launch_t<128, 128, 4, 1, 32, 3>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
-                                           N, K, epi, kv, po, stream);
-  if (g_layout == 4)
-    return launch_t<128, 128, 4, 1, 16, 4>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
-                                           N, K, epi, kv, po, stream);
-  if (g_layout == 5)
-    return launch_t<128, 128, 2, 2, 16, 4>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
-                                           N, K, epi, kv, po, stream);
-  if (g_layout == 2)
-    return launch_t<256, 128, 4, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
-                                    epi, kv, po, stream);
-  if (g_layout == 1)
-    return launch_t<128, 128, 2, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
-                                    epi, kv, po, stream);
-  return launch_t<128, 128, 4, 1>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
-                                  epi, kv, po, stream);
+  return run_h3(Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, kv, po,
+                Batch{}, stream);
+}
+
+// nb independent GEMMs C_b = act(rinv_b[m] csc_b[n] (A'_b . W'_b^T) + bias) (+ R_b),
+// operand b at base + b * stride (elements; a stride of 0 shares the operand
+// across the batch: a conv's weight, a broadcast matmul side).  The planes of
+// A_b are [2][M][lda] with plane stride aplane (likewise W_b); C_b / R_b are
+// [M][ldc] / [M][ldr].  EPI_BIAS: bias per column n; EPI_BIAS_ROW: per row m
+// (a conv computed as W . patches^T, NCHW out).  One launch, the tiles of all
+// batch elements in one grid.  K % 32 == 0.
+NOS_API int nos_gemm_f32h3_batched(const void* Ap, int lda, long long aplane, long long sa, const float* rinv,
+                                   long long srinv, float rconst, const void* Wp, int ldw, long long wplane,
+                                   long long sw, const float* csc, long long scsc, const float* bias, const float* R,
+                                   int ldr, long long sr, float* C, int ldc, long long sc, int M, int N, int K, int nb,
+                                   int epi, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || nb <= 0 || (K % BK) != 0) return (int)hipErrorInvalidValue;
+  if ((lda % 8) || (ldw % 8) || lda < K || ldw < K || aplane < (long long)M * lda || wplane < (long long)N * ldw)
+    return (int)hipErrorInvalidValue;
+  if (sa < 0 || sw < 0 || srinv < 0 || scsc < 0 || sr < 0 || sc < 0 || (sa % 8) || (sw % 8))
+    return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)Ap) | ((uintptr_t)Wp)) & 15) return (int)hipErrorInvalidValue;
+  if ((!rinv && !(rconst > 0.f)) || !csc || !C || ldc < N) return (int)hipErrorInvalidValue;
+  if ((epi & (EPI_BIAS | EPI_BIAS_ROW)) == (EPI_BIAS | EPI_BIAS_ROW) || ((epi & (EPI_BIAS | EPI_BIAS_ROW)) && !bias) ||
+      ((epi & EPI_RESID) && (!R || ldr < N)))
+    return (int)hipErrorInvalidValue;
+  if (nb > 1 && sc < (long long)(M - 1) * ldc + N) return (int)hipErrorInvalidValue;  // outputs never overlap
+  Batch bt;
+  bt.nb = nb;
+  bt.a = sa;
+  bt.rinv = srinv;
+  bt.w = sw;
+  bt.csc = scsc;
+  bt.c = sc;
+  bt.r = sr;
+  return run_h3(Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, KvOut{},
+                PlaneOut{}, bt, stream);
 }

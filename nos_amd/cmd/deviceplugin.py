@@ -45,7 +45,7 @@ def main(argv=None) -> int:
     mode = partitioning_kind(api.get("Node", node))
     plugin = NosAmdDevicePlugin(node, smi, mode=mode, expose_partitions_as_gpu=args.expose_partitions_as_gpu,
                                 cu_policy=cfg.cu_policy, device_env=args.device_env or cfg.device_env,
-                                pod_server_dir=cfg.pod_server_socket_dir)
+                                pod_server_dir=cfg.pod_server_socket_dir, adopt_records=True)
     mgr = common.manager_for(api, f"nos-deviceplugin-{node}", cfg)
     ref = DevicePluginConfigRef(cfg.config_map.name, cfg.config_map.namespace)
     watcher = ConfigWatcher(api, node, plugin, ref)  # loads the slice table whenever the node is a cumask node

@@ -82,7 +82,12 @@ class ContainerAllocation:
 
 class NosAmdDevicePlugin:
     def __init__(self, node_name: str, smi: AmdSmi, mode: str | None = None, expose_partitions_as_gpu: bool = False,
-                 cu_policy: str = "proportional", device_env: str = "host", pod_server_dir: str = ""):
+                 cu_policy: str = "proportional", device_env: str = "host", pod_server_dir: str = "",
+                 adopt_records: bool = False):
+        """``adopt_records``: the node's only plugin process (the deployed
+        binary) adopts the pod-server allocation records a previous process
+        wrote and deletes orphans (:meth:`_restore_records`); simulations that
+        run several plugins over one records directory leave them alone."""
         if device_env not in ("host", "container"):
             raise ValueError(f"device_env must be 'host' or 'container', not {device_env!r}")
         self.node_name = node_name
@@ -97,7 +102,7 @@ class NosAmdDevicePlugin:
         # records a previous plugin process wrote: device id -> (owner, CU slots),
         # adopted at the first refresh that has the slice table (_restore_records)
         self._restored: dict[str, tuple[str, frozenset]] = {}
-        if self.pod_server_allocations is not None:
+        if self.pod_server_allocations is not None and adopt_records:
             for _path, rec in self.pod_server_allocations.load():
                 slots = rec.get("cu_slots") or {}
                 for did in rec.get("device_ids", []):

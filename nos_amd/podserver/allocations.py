@@ -69,7 +69,7 @@ class AllocationStore:
 
     def load(self) -> list[tuple[Path, dict]]:
         """(path, record) of every record on disk (all GPUs), re-indexed by
-        device id; unreadable or half-written files are deleted."""
+        device id; half-written (``.tmp``) or unreadable files are skipped."""
         out = []
         self._by_device = {}
         base = self.root / RECORDS
@@ -77,14 +77,12 @@ class AllocationStore:
             return out
         for path in sorted(base.glob("gpu-*/*")):
             if path.suffix != ".json":
-                path.unlink(missing_ok=True)  # a .tmp a crash left behind
                 continue
             try:
                 rec = json.loads(path.read_text())
                 if not isinstance(rec, dict):
                     raise ValueError("not an object")
             except (OSError, ValueError):
-                path.unlink(missing_ok=True)
                 continue
             for did in rec.get("device_ids", []):
                 self._by_device.setdefault(did, set()).add(path)

@@ -413,7 +413,8 @@ def test_a_dropped_connection_releases_its_claim(tokened):
 def _pod_server_plugin(root, smi):
     from nos_amd.deviceplugin.plugin import NosAmdDevicePlugin
 
-    p = NosAmdDevicePlugin("n1", smi, mode=C.PARTITIONING_CUMASK, cu_policy="even", pod_server_dir=str(root))
+    p = NosAmdDevicePlugin("n1", smi, mode=C.PARTITIONING_CUMASK, cu_policy="even", pod_server_dir=str(root),
+                           adopt_records=True)
     p.set_config("n1-1", {"gpus": [{"index": 0, "slices": [{"profile": "10gb", "replicas": 4}]}]})
     return p
 
@@ -509,3 +510,22 @@ def test_constant_folded_chains_count_as_persistent_weights():
     m = p.compile("cpu")
     assert set(big).isdisjoint(m.consts)           # dead folded values were freed
     assert torch.allclose(m(torch.zeros(4, 64))[0], torch.ones(4, 64))
+
+
+def test_simulated_plugins_sharing_a_records_dir_keep_each_others_records(tmp_path):
+    """bench.py plans several placements over one pod-server directory (the
+    main fleet + the latency-table rows, one server): without adopt_records a
+    later plugin must not delete an earlier plugin's records as orphans."""
+    from nos_amd.deviceplugin.plugin import NosAmdDevicePlugin
+    from nos_amd.gpu.fakesmi import FakeSmi
+    from nos_amd.podserver.allocations import lookup
+
+    root = tmp_path / "ps"
+    toks = []
+    for reps in (4, 1):
+        p = NosAmdDevicePlugin("n1", FakeSmi(gpus=1, node="n1"), mode=C.PARTITIONING_CUMASK, cu_policy="shared",
+                               pod_server_dir=str(root))
+        p.set_config("n1-1", {"gpus": [{"index": 0, "slices": [{"profile": "10gb", "replicas": reps}]}]})
+        for d in p.list_devices("amd.com/gpu-10gb"):
+            toks.append(p.allocate("amd.com/gpu-10gb", [d.id]).envs[C.ENV_POD_TOKEN])
+    assert all(lookup(records_dir(root, 0), t) is not None for t in toks)
