@@ -26,7 +26,9 @@
 
 namespace {
 
-enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8, EPI_BIAS_ROW = 16 };
+enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8, EPI_BIAS_ROW = 16, EPI_RESID_PRE = 32 };
+// EPI_RESID adds R after the activation (transformer residuals); EPI_RESID_PRE
+// before it (ResNet: relu(conv + bn + identity))
 
 // batched GEMMs (nos_gemm_f32h3_batched): per-batch element strides of every
 // operand (0 = shared by the whole batch, e.g. a conv weight); the tile index
@@ -276,7 +278,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     // planes of a one-sequence QKV projection (a 128-column tile never
     // straddles Q / K / V: hd % 128 == 0 is checked by the host): the same
     // tile-relative 32-bit offsets, two fp16 stores per element
-    if (full && !(epi & EPI_RESID) &&
+    if (full && !(epi & (EPI_RESID | EPI_RESID_PRE)) &&
         (po.p != nullptr || (kv.kvs != nullptr && kv.S == M && n0 >= kv.qcols && kv.hd % BN == 0))) {
       unsigned short* hi;
       long long lo_off;
@@ -320,7 +322,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     const bool interior = full && po.p == nullptr && (kv.kvs == nullptr || n0 + BN <= kv.qcols);  // Q columns too
     if (interior) {
       float* Ct = Cb + (long long)m0 * ldc + n0;
-      const float* Rt = (epi & EPI_RESID) ? Rb + (long long)m0 * ldr + n0 : nullptr;
+      const float* Rt = (epi & (EPI_RESID | EPI_RESID_PRE)) ? Rb + (long long)m0 * ldr + n0 : nullptr;
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int cl = wn * (BN / WGN) + j * 32 + c;
@@ -332,6 +334,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
           for (int r = 0; r < 16; ++r) {
             const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
             float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
+            if (epi & EPI_RESID_PRE) v += Rt[(unsigned)(rl * ldr + cl)];
             if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
             if (epi & EPI_RELU) v = fmaxf(v, 0.f);
             if (epi & EPI_RESID) v += Rt[(unsigned)(rl * ldr + cl)];
@@ -353,6 +356,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
+          if ((epi & EPI_RESID_PRE) && m < M && n < N) v += Rb[(long long)m * ldr + n];
           if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
           if (epi & EPI_RELU) v = fmaxf(v, 0.f);
           if (m < M && n < N) {
@@ -605,7 +609,7 @@ NOS_API int nos_gemm_f32h3(const void* Ap, int lda, long long aplane, const floa
   if ((((uintptr_t)Ap) | ((uintptr_t)Wp)) & 15) return (int)hipErrorInvalidValue;
   if ((!rinv && !(rconst > 0.f)) || !csc || ((epi & EPI_BIAS) && !bias) || ((epi & EPI_RESID) && (!R || ldr < N)))
     return (int)hipErrorInvalidValue;
-  if ((epi & EPI_BIAS_ROW) && ((epi & EPI_BIAS) || !bias)) return (int)hipErrorInvalidValue;
+  if (((epi & EPI_BIAS_ROW) && ((epi & EPI_BIAS) || !bias)) || (epi & EPI_RESID_PRE)) return (int)hipErrorInvalidValue;
   KvOut kv;
   PlaneOut po;
   if (kvs != nullptr) {
@@ -651,7 +655,7 @@ NOS_API int nos_gemm_f32h3_batched(const void* Ap, int lda, long long aplane, lo
   if ((((uintptr_t)Ap) | ((uintptr_t)Wp)) & 15) return (int)hipErrorInvalidValue;
   if ((!rinv && !(rconst > 0.f)) || !csc || !C || ldc < N) return (int)hipErrorInvalidValue;
   if ((epi & (EPI_BIAS | EPI_BIAS_ROW)) == (EPI_BIAS | EPI_BIAS_ROW) || ((epi & (EPI_BIAS | EPI_BIAS_ROW)) && !bias) ||
-      ((epi & EPI_RESID) && (!R || ldr < N)))
+      ((epi & (EPI_RESID | EPI_RESID_PRE)) && (!R || ldr < N)) || (epi & EPI_RESID && epi & EPI_RESID_PRE))
     return (int)hipErrorInvalidValue;
   if (nb > 1 && sc < (long long)(M - 1) * ldc + N) return (int)hipErrorInvalidValue;  // outputs never overlap
   Batch bt;

@@ -85,10 +85,25 @@ _SIGS = {
     "nos_runtime_version": [ctypes.POINTER(c_int)],
     "nos_set_cu_budget": [c_int],
     "nos_get_cu_budget": [],
+    # general tenant programs (tenant_ops.hip, attention_h3g.hip, gemm_f32h.hip)
+    "nos_gemm_f32h3_batched": [c_void_p, c_int, c_ll, c_ll, c_void_p, c_ll, c_float, c_void_p, c_int, c_ll, c_ll,
+                               c_void_p, c_ll, c_void_p, c_void_p, c_int, c_ll, c_void_p, c_int, c_ll, c_int, c_int,
+                               c_int, c_int, c_int, c_void_p],
+    "nos_embedding": [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_int, c_void_p],
+    "nos_rmsnorm": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p],
+    "nos_softmax": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nos_rotary": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_ll, c_int, c_void_p],
+    "nos_im2col_h3": [c_void_p, c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                      c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nos_attn_h3g_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
+    "nos_attn_h3g_set_kvsplit": [c_int],
+    "nos_attn_h3g": [c_void_p, c_int, c_ll, c_void_p, c_int, c_ll, c_void_p, c_int, c_ll, c_void_p, c_int, c_ll,
+                     c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_float, c_void_p,
+                     c_ll, c_void_p],
 }
 
 
-_RESTYPES = {"nos_attn_f32x6_workspace": c_ll}
+_RESTYPES = {"nos_attn_f32x6_workspace": c_ll, "nos_attn_h3g_workspace": c_ll}
 
 
 class NativeUnavailable(RuntimeError):

@@ -1,0 +1,377 @@
+"""Ops of general pod-server tenant programs (decoder LLMs, conv nets).
+
+The YOLOS-class encoder ops live in :mod:`nos_amd.ops`; this module adds
+what conv nets and decoder LLMs need, each lowered onto gfx950 kernels of
+``libnos_hip.so`` for CUDA tensors and onto a plain PyTorch fp32 reference
+for CPU tensors (the numerics tests compare the two):
+
+* :func:`conv2d` -- implicit-GEMM convolution on the fp16x3 (h3) matrix
+  pipes: ``nos_im2col_h3`` writes an image's patches straight as the GEMM's
+  split planes (per-patch power-of-two scales), and ONE batched
+  ``nos_gemm_f32h3_batched`` launch computes ``W . patches^T`` for every
+  image, NCHW out, bias per output channel, ReLU / GELU and a residual in
+  the epilogue (BatchNorm is folded into the weights by the compiler);
+* :func:`matmul` -- batched activation x activation GEMM on the same kernel
+  (both sides split at run time, a broadcast side has stride 0);
+* :func:`sdpa` -- attention with causal masking, head_dim 64 / 128,
+  grouped-query K/V heads and fused rotary embeddings (``nos_attn_h3g``);
+* :func:`linear_rms` -- RMSNorm folded into the following GEMM (the row
+  statistics in the split pre-pass, gamma in the weight);
+* :func:`embedding`, :func:`rmsnorm`, :func:`softmax`, :func:`rotary` --
+  row / gather kernels (``tenant_ops.hip``), fp32 and bf16.
+
+bf16 tensors run the fp32-only GEMM / attention kernels on an fp32 copy
+(more precision than the tenant asked for, never less).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import EPI_BIAS, EPI_GELU, EPI_RELU, EPI_RESID, _lib, _split_rows_h3, _stream, split_f32_weight_h3
+
+EPI_BIAS_ROW, EPI_RESID_PRE = 16, 32  # gemm_f32h.hip: bias per row; residual added before the activation
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _act_epi(act: str | None) -> int:
+    return EPI_GELU if act == "gelu" else (EPI_RELU if act == "relu" else 0)
+
+
+def _act(y: torch.Tensor, act: str | None) -> torch.Tensor:
+    return F.gelu(y) if act == "gelu" else (F.relu(y) if act == "relu" else y)
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    return t if t.dtype == torch.float32 else t.float()
+
+
+def _pad_k(t: torch.Tensor, mult: int = 32) -> torch.Tensor:
+    k = t.shape[-1]
+    kp = -(-k // mult) * mult
+    return t if kp == k else F.pad(t, (0, kp - k))
+
+
+def _bf(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return 1
+    if t.dtype == torch.float32:
+        return 0
+    raise ValueError(f"tenant ops take fp32 or bf16 tensors, got {t.dtype}")
+
+
+# ------------------------------------------------------------------ references
+def conv2d_ref(x, w, bias=None, stride=(1, 1), padding=(0, 0), dilation=(1, 1), act=None, residual=None,
+               residual_first: bool = False):
+    y = F.conv2d(x.float(), w.float(), None if bias is None else bias.float(), stride, padding, dilation)
+    if residual is not None and residual_first:
+        y = y + residual.float()
+    y = _act(y, act)
+    if residual is not None and not residual_first:
+        y = y + residual.float()
+    return y.to(x.dtype)
+
+
+def rope_ref(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos0: int = 0) -> torch.Tensor:
+    """rotate_half rotary on x [B, S, H, D] with tables [>= pos0 + S, D]."""
+    S, D = x.shape[1], x.shape[-1]
+    c = cos[pos0:pos0 + S].float()[None, :, None, :]
+    s = sin[pos0:pos0 + S].float()[None, :, None, :]
+    xf = x.float()
+    rot = torch.cat([-xf[..., D // 2:], xf[..., :D // 2]], dim=-1)
+    return (xf * c + rot * s).to(x.dtype)
+
+
+def sdpa_ref(q, k, v, causal: bool = False, scale: float | None = None, rope=None) -> torch.Tensor:
+    """q [B, Sq, H, D], k / v [B, Skv, Hkv, D] -> [B, Sq, H, D] in fp32 math."""
+    B, Sq, H, D = q.shape
+    Skv, Hkv = k.shape[1], k.shape[2]
+    qf, kf, vf = q.float(), k.float(), v.float()
+    if rope is not None:
+        cos, sin = rope[0], rope[1]
+        qf = rope_ref(qf, cos, sin, Skv - Sq)
+        kf = rope_ref(kf, cos, sin, 0)
+    if Hkv != H:
+        kf = kf.repeat_interleave(H // Hkv, dim=2)
+        vf = vf.repeat_interleave(H // Hkv, dim=2)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    s = torch.einsum("bqhd,bkhd->bhqk", qf, kf) * scale
+    if causal:
+        i = torch.arange(Sq, device=q.device)[:, None] + (Skv - Sq)
+        j = torch.arange(Skv, device=q.device)[None, :]
+        s = s.masked_fill(j > i, float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    return torch.einsum("bhqk,bkhd->bqhd", p, vf).to(q.dtype)
+
+
+def rmsnorm_ref(x, weight, eps=1e-6):
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (weight.float() * y.to(x.dtype).float()).to(x.dtype)
+
+
+def linear_rms_ref(x, wg, bias=None, act=None, eps=1e-6):
+    xf = x.float()
+    y = (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)) @ wg.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    return _act(y, act).to(x.dtype)
+
+
+# ------------------------------------------------------------------ gather / row kernels
+def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    """table[ids] for int ids of any shape; out [*ids.shape, D]."""
+    if not table.is_cuda:
+        return F.embedding(ids.long(), table)
+    V, D = table.shape
+    ids32 = ids.to(torch.int32).contiguous()
+    out = torch.empty((*ids.shape, D), dtype=table.dtype, device=table.device)
+    row_bytes = D * table.element_size()
+    if row_bytes % 16 or not table.is_contiguous():
+        raise ValueError("native embedding needs a contiguous table with 16-byte rows")
+    _lib.check(_lib.lib().nos_embedding(ids32.data_ptr(), table.data_ptr(), out.data_ptr(), ids32.numel(), V,
+                                        row_bytes, _stream()), "nos_embedding")
+    return out
+
+
+def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6) -> torch.Tensor:
+    if not x.is_cuda:
+        return rmsnorm_ref(x, weight, eps)
+    D = x.shape[-1]
+    x2 = x.reshape(-1, D)
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    w = weight.to(x.dtype).contiguous()
+    out = torch.empty(x2.shape, dtype=x.dtype, device=x.device)
+    _lib.check(_lib.lib().nos_rmsnorm(x2.data_ptr(), w.data_ptr(), out.data_ptr(), x2.shape[0], D, x2.stride(0), D,
+                                      float(eps), _bf(x), _stream()), "nos_rmsnorm")
+    return out.view(x.shape)
+
+
+def softmax(x: torch.Tensor) -> torch.Tensor:
+    """softmax over the last dim."""
+    if not x.is_cuda:
+        return torch.softmax(x.float(), dim=-1).to(x.dtype)
+    L = x.shape[-1]
+    x2 = x.reshape(-1, L)
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    out = torch.empty(x2.shape, dtype=x.dtype, device=x.device)
+    _lib.check(_lib.lib().nos_softmax(x2.data_ptr(), out.data_ptr(), x2.shape[0], L, x2.stride(0), L, _bf(x),
+                                      _stream()), "nos_softmax")
+    return out.view(x.shape)
+
+
+def _rows_view(x: torch.Tensor) -> tuple[int, int]:
+    """(token row stride, batch stride) of x [B, S, H, D] whose heads are
+    contiguous per token (e.g. a slice of a fused projection)."""
+    B, S, H, D = x.shape
+    if x.stride(-1) != 1 or x.stride(-2) != D:
+        raise ValueError("x needs contiguous heads per token")
+    return x.stride(1), x.stride(0)
+
+
+def rotary(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """rotate_half rotary embedding of x [B, S, H, D] with fp32 tables [S, D]."""
+    if not x.is_cuda:
+        return rope_ref(x, cos, sin)
+    B, S, H, D = x.shape
+    if x.stride(-1) != 1 or x.stride(-2) != D:
+        x = x.contiguous()
+    ld, bs = _rows_view(x)
+    c, s = cos.float().contiguous(), sin.float().contiguous()
+    if c.shape[0] < S or c.shape[1] != D:
+        raise ValueError(f"rotary tables must be [>= {S}, {D}]")
+    out = torch.empty((B, S, H, D), dtype=x.dtype, device=x.device)
+    _lib.check(_lib.lib().nos_rotary(x.data_ptr(), c.data_ptr(), s.data_ptr(), out.data_ptr(), B, S, H, D, ld, bs,
+                                     _bf(x), _stream()), "nos_rotary")
+    return out
+
+
+# ------------------------------------------------------------------ GEMM-class ops (h3)
+def _gemm_batched(ap, rinv, sa, srinv, wp, csc, sw, scsc, out, M, N, K, nb, epi, bias=None, residual=None,
+                  ldc=None, sc=None, ldr=None, sr=None) -> None:
+    L = _lib.lib()
+    ldc = N if ldc is None else ldc
+    rc = L.nos_gemm_f32h3_batched(ap.data_ptr(), K, ap[0].numel(), sa,
+                                  rinv.data_ptr(), srinv, 0.0, wp.data_ptr(), K, wp[0].numel(), sw, csc.data_ptr(),
+                                  scsc, _ptr(bias), _ptr(residual), ldr or ldc, sr or 0, out.data_ptr(), ldc,
+                                  M * ldc if sc is None else sc, M, N, K, nb, epi, _stream())
+    _lib.check(rc, "nos_gemm_f32h3_batched")
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, stride=(1, 1), padding=(0, 0),
+           dilation=(1, 1), act: str | None = None, residual: torch.Tensor | None = None,
+           w2: torch.Tensor | None = None, residual_first: bool = False) -> torch.Tensor:
+    """act(conv2d(x, w) + bias) + residual, groups = 1, NCHW
+    (``residual_first``: act(conv2d(x, w) + bias + residual), a ResNet block's
+    tail).  ``w2``: the weight as a [OC, Kp] fp32 matrix (K = C*KH*KW
+    zero-padded to 32), which the compiler keeps as a constant so its split
+    planes are cached."""
+    if not x.is_cuda:
+        return conv2d_ref(x, w, bias, stride, padding, dilation, act, residual, residual_first)
+    dt = x.dtype
+    xf = _f32(x).contiguous()
+    N, C, H, W = xf.shape
+    OC, _, KH, KW = w.shape
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    OH = (H + 2 * ph - dh * (KH - 1) - 1) // sh + 1
+    OW = (W + 2 * pw - dw * (KW - 1) - 1) // sw + 1
+    K = C * KH * KW
+    Kp = -(-K // 32) * 32
+    if w2 is None:
+        w2 = _pad_k(_f32(w).reshape(OC, K)).contiguous()
+    if w2.shape != (OC, Kp) or w2.dtype != torch.float32:
+        raise ValueError(f"conv weight matrix must be fp32 [{OC}, {Kp}]")
+    P = OH * OW
+    planes = torch.empty((2, N * P, Kp), dtype=torch.float16, device=x.device)
+    prinv = torch.empty((N * P,), dtype=torch.float32, device=x.device)
+    L = _lib.lib()
+    _lib.check(L.nos_im2col_h3(xf.data_ptr(), planes.data_ptr(), N * P * Kp, prinv.data_ptr(), N, C, H, W, KH, KW,
+                               sh, sw, ph, pw, dh, dw, Kp, _stream()), "nos_im2col_h3")
+    wp, wsc = split_f32_weight_h3(w2)
+    out = torch.empty((N, OC, OH, OW), dtype=torch.float32, device=x.device)
+    epi = _act_epi(act) | (EPI_BIAS_ROW if bias is not None else 0)
+    if residual is not None:
+        epi |= EPI_RESID_PRE if residual_first else EPI_RESID
+    b = _f32(bias).contiguous() if bias is not None else None
+    r = _f32(residual).contiguous() if residual is not None else None
+    if r is not None and r.shape != out.shape:
+        raise ValueError(f"residual must be {tuple(out.shape)}")
+    # out[n] = W [OC, Kp] . patches[n]^T: A = the weight (shared, stride 0), W-operand = image n's patches
+    _gemm_batched(wp, wsc, 0, 0, planes, prinv, P * Kp, P, out, OC, P, Kp, N, epi, bias=b, residual=r,
+                  ldc=P, sc=OC * P, ldr=P, sr=OC * P)
+    return out if dt == torch.float32 else out.to(dt)
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a [..., M, K] @ b [..., K, N]; batch dims equal, or one side 2-D."""
+    if not a.is_cuda:
+        return (a.float() @ b.float()).to(a.dtype)
+    dt = a.dtype
+    M, K = a.shape[-2:]
+    N = b.shape[-1]
+    ba, bb = a.shape[:-2], b.shape[:-2]
+    if ba and bb and ba != bb:
+        raise ValueError(f"matmul batch dims must match (or one side 2-D): {tuple(a.shape)} @ {tuple(b.shape)}")
+    bshape = ba or bb
+    nb = math.prod(bshape) if bshape else 1
+    a2 = _pad_k(_f32(a).reshape(-1, M, K)).reshape(-1, _pad_k_len(K)).contiguous()
+    bt = _pad_k(_f32(b).reshape(-1, K, N).transpose(1, 2)).reshape(-1, _pad_k_len(K)).contiguous()
+    Kp = a2.shape[1]
+    ap, arinv = _split_rows_h3(a2, ln=False)
+    bp, brinv = _split_rows_h3(bt, ln=False)
+    out = torch.empty((nb, M, N), dtype=torch.float32, device=a.device)
+    _gemm_batched(ap, arinv, M * Kp if ba else 0, M if ba else 0, bp, brinv, N * Kp if bb else 0, N if bb else 0,
+                  out, M, N, Kp, nb, 0)
+    out = out.view(*bshape, M, N)
+    return out if dt == torch.float32 else out.to(dt)
+
+
+def _pad_k_len(k: int) -> int:
+    return -(-k // 32) * 32
+
+
+def linear_rms(x: torch.Tensor, wg: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
+               eps: float = 1e-6) -> torch.Tensor:
+    """act(RMSNorm(x) @ (W * gamma)^T + b): the row statistics in the h3 split
+    pre-pass (``nos_split_rows_h3`` mode 2), gamma folded into ``wg``."""
+    if not x.is_cuda:
+        return linear_rms_ref(x, wg, bias, act, eps)
+    dt = x.dtype
+    K = x.shape[-1]
+    N = wg.shape[0]
+    if K % 32:
+        raise ValueError("native linear_rms needs K % 32 == 0")
+    x2 = _f32(x).reshape(-1, K)
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    M = x2.shape[0]
+    planes = torch.empty((2, M, K), dtype=torch.float16, device=x.device)
+    rinv = torch.empty((M,), dtype=torch.float32, device=x.device)
+    eln = 14 - math.frexp(math.sqrt(K))[1]
+    _lib.check(_lib.lib().nos_split_rows_h3(x2.data_ptr(), x2.stride(0), planes.data_ptr(), K, M * K, rinv.data_ptr(),
+                                            M, K, 2, float(eps), eln, _stream()), "nos_split_rows_h3")
+    wp, csc = split_f32_weight_h3(wg)
+    out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    b = _f32(bias).contiguous() if bias is not None else None
+    epi = _act_epi(act) | (EPI_BIAS if b is not None else 0)
+    _gemm_batched(planes, rinv, 0, 0, wp, csc, 0, 0, out, M, N, K, 1, epi, bias=b)
+    out = out.view(*x.shape[:-1], N)
+    return out if dt == torch.float32 else out.to(dt)
+
+
+_ROPE_BOUND: dict[int, tuple] = {}
+
+
+def _rope_bound(cos: torch.Tensor, sin: torch.Tensor) -> float:
+    key = id(cos)
+    hit = _ROPE_BOUND.get(key)
+    if hit is not None and hit[0] is sin and hit[1] == cos._version:
+        return hit[2]
+    b = float(cos.abs().max() + sin.abs().max())
+    _ROPE_BOUND[key] = (sin, cos._version, b)
+    return b
+
+
+def sdpa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False, scale: float | None = None,
+         rope: tuple | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """softmax(scale q k^T [causal]) v: q [B, Sq, H, D], k / v [B, Skv, Hkv, D]
+    (heads contiguous per token; any token / batch strides, e.g. slices of a
+    fused QKV projection), D = 64 or 128, H % Hkv == 0.  ``rope`` = (cos, sin)
+    fp32 tables [Skv, D]: q and k are rotated first (inside the kernels)."""
+    if not q.is_cuda:
+        return sdpa_ref(q, k, v, causal, scale, rope)
+    dt = q.dtype
+    B, Sq, H, D = q.shape
+    Skv, Hkv = k.shape[1], k.shape[2]
+    if D not in (64, 128) or H % Hkv or v.shape != k.shape or k.shape[0] != B or k.shape[3] != D:
+        raise ValueError(f"native sdpa: head_dim 64/128, H % Hkv == 0; got q {tuple(q.shape)}, k {tuple(k.shape)}")
+    qf, kf, vf = (_f32(t) for t in (q, k, v))
+    try:
+        (ldq, bsq), (ldk, bsk), (ldv, bsv) = _rows_view(qf), _rows_view(kf), _rows_view(vf)
+    except ValueError:
+        qf, kf, vf = qf.contiguous(), kf.contiguous(), vf.contiguous()
+        (ldq, bsq), (ldk, bsk), (ldv, bsv) = _rows_view(qf), _rows_view(kf), _rows_view(vf)
+    if any(s % 4 for s in (ldq, bsq, ldk, bsk, ldv, bsv)) or any(t.data_ptr() % 16 for t in (qf, kf, vf)):
+        qf, kf, vf = qf.contiguous(), kf.contiguous(), vf.contiguous()
+        (ldq, bsq), (ldk, bsk), (ldv, bsv) = _rows_view(qf), _rows_view(kf), _rows_view(vf)
+    if out is None or out.dtype != torch.float32:
+        o = torch.empty((B, Sq, H, D), dtype=torch.float32, device=q.device)
+    else:
+        o = out
+    L = _lib.lib()
+    nbytes = int(L.nos_attn_h3g_workspace(B, H, Hkv, Sq, Skv, D))
+    ws = torch.empty((nbytes + 256,), dtype=torch.uint8, device=q.device)
+    wptr = (ws.data_ptr() + 255) // 256 * 256
+    rc_, rs_, rb = None, None, 0.0
+    if rope is not None:
+        rc_, rs_ = rope[0], rope[1]
+        if rc_.dtype != torch.float32 or not rc_.is_contiguous() or rc_.shape != (Skv, D) or rs_.shape != (Skv, D):
+            raise ValueError(f"rope tables must be contiguous fp32 [{Skv}, {D}]")
+        rb = _rope_bound(rc_, rs_)
+    sc = scale if scale is not None else 1.0 / math.sqrt(D)
+    rc = L.nos_attn_h3g(qf.data_ptr(), ldq, bsq, kf.data_ptr(), ldk, bsk, vf.data_ptr(), ldv, bsv, o.data_ptr(),
+                        o.stride(1), o.stride(0), B, H, Hkv, Sq, Skv, D, int(bool(causal)), float(sc), _ptr(rc_),
+                        _ptr(rs_), float(rb), wptr, nbytes, _stream())
+    _lib.check(rc, "nos_attn_h3g")
+    if out is not None and out is not o:
+        out.copy_(o)
+        return out
+    return o if dt == torch.float32 else o.to(dt)
+
+
+def set_attention_h3g_kvsplit(n: int) -> None:
+    """Key splits of :func:`sdpa` (0 = auto: fill the CU slots)."""
+    _lib.check(_lib.lib().nos_attn_h3g_set_kvsplit(int(n)), "nos_attn_h3g_set_kvsplit")
+
+
+__all__ = ["conv2d", "matmul", "sdpa", "linear_rms", "embedding", "rmsnorm", "softmax", "rotary", "conv2d_ref",
+           "sdpa_ref", "rope_ref", "rmsnorm_ref", "linear_rms_ref", "set_attention_h3g_kvsplit", "EPI_BIAS_ROW"]

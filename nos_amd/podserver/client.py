@@ -119,7 +119,12 @@ class PodClient:
     def infer(self, x: np.ndarray | None = None, outputs: bool = False) -> tuple[list[np.ndarray], dict]:
         """One inference on the pod's model; ``x`` replaces the resident input
         (float32, the model's input shape)."""
-        payload = b"" if x is None else np.ascontiguousarray(x, dtype=np.float32).tobytes()
+        if x is None:
+            payload = b""
+        elif np.issubdtype(np.asarray(x).dtype, np.integer):  # token ids of an i32 input
+            payload = np.ascontiguousarray(x, dtype=np.int32).tobytes()
+        else:
+            payload = np.ascontiguousarray(x, dtype=np.float32).tobytes()
         try:
             rep, data = self._call({"op": "infer", "outputs": outputs}, payload)
         except PodServerGone:

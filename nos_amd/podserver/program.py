@@ -58,12 +58,14 @@ from dataclasses import dataclass, field
 import numpy as np
 
 FORMAT = "nos-amd.program/v1"
-WIRE_DTYPES = {"fp32": 4, "bf16": 2}
+WIRE_DTYPES = {"fp32": 4, "bf16": 2, "i32": 4}   # i32: token ids (an input only; consumed by embedding)
+FLOAT_DTYPES = ("fp32", "bf16")
 MAX_NODES = 8192
 MAX_PARAMS = 8192
 MAX_NUMEL = 1 << 31          # elements of one value
 MAX_RANK = 8
-UNARY = ("gelu", "relu", "sigmoid", "silu")
+UNARY = ("gelu", "relu", "sigmoid", "silu", "tanh", "exp", "neg", "rsqrt")
+BINARY = ("add", "mul", "sub", "div")
 ACTS = (None, "gelu", "relu")
 INTERP_MODES = ("bicubic", "bilinear", "nearest")
 
@@ -161,8 +163,8 @@ def _infer(node: Node, ins: list[Value], gpu: bool) -> tuple[tuple[int, ...], st
         arity(2, 3)
         dt = same_dtype()
         x, w = ins[0], ins[1]
-        _req(len(w.shape) == 2 and len(x.shape) >= 1 and x.shape[-1] == w.shape[1],
-             f"{what}: x [..., K] and weight [N, K] required, got {x.shape} and {w.shape}")
+        _req(len(w.shape) == 2 and len(x.shape) >= 1 and x.shape[-1] == w.shape[1] and dt in FLOAT_DTYPES,
+             f"{what}: float x [..., K] and weight [N, K] required, got {x.shape} and {w.shape}")
         if len(ins) == 3:
             _req(ins[2].shape == (w.shape[0],), f"{what}: bias must be [{w.shape[0]}], got {ins[2].shape}")
         _req(a.get("act") in ACTS, f"{what}: act must be one of {ACTS}")
@@ -175,30 +177,34 @@ def _infer(node: Node, ins: list[Value], gpu: bool) -> tuple[tuple[int, ...], st
         arity(3, 3)
         dt = same_dtype()
         d = ins[0].shape[-1] if ins[0].shape else 0
-        _req(ins[1].shape == (d,) and ins[2].shape == (d,), f"{what}: gamma/beta must be [{d}]")
+        _req(ins[1].shape == (d,) and ins[2].shape == (d,) and dt in FLOAT_DTYPES, f"{what}: gamma/beta must be [{d}]")
         eps = a.get("eps", 1e-5)
         _req(isinstance(eps, (int, float)) and 0 < eps < 1, f"{what}: eps must be in (0, 1)")
         return ins[0].shape, dt
     if op == "attention":
-        only("heads", "scale")
+        only("heads", "scale", "causal")
         arity(1, 1)
         x = ins[0]
         h = _int(a.get("heads"), f"{what}: heads", 1)
-        _req(len(x.shape) == 3 and x.shape[2] % (3 * h) == 0,
-             f"{what}: qkv must be [B, S, 3*heads*D], got {x.shape} with {h} heads")
+        _req(len(x.shape) == 3 and x.shape[2] % (3 * h) == 0 and x.dtype in FLOAT_DTYPES,
+             f"{what}: qkv must be a float [B, S, 3*heads*D], got {x.shape} with {h} heads")
         d = x.shape[2] // (3 * h)
         if "scale" in a:
             _req(isinstance(a["scale"], (int, float)) and a["scale"] > 0, f"{what}: scale must be > 0")
+        _req(isinstance(a.get("causal", False), bool), f"{what}: causal must be a bool")
         if gpu:
-            _req(d == 64, f"{what}: the attention kernels are built for head_dim 64, got {d}")
+            _req(d in (64, 128), f"{what}: the attention kernels take head_dim 64 or 128, got {d}")
         return (x.shape[0], x.shape[1], h * d), x.dtype
-    if op in ("add", "mul"):
+    if op in BINARY:
         only()
         arity(2, 2)
-        return _broadcast(ins[0].shape, ins[1].shape, what), same_dtype()
+        dt = same_dtype()
+        _req(dt in FLOAT_DTYPES, f"{what}: takes float tensors")
+        return _broadcast(ins[0].shape, ins[1].shape, what), dt
     if op in UNARY:
         only()
         arity(1, 1)
+        _req(ins[0].dtype in FLOAT_DTYPES, f"{what}: takes a float tensor")
         return ins[0].shape, ins[0].dtype
     if op == "cat":
         only("dim")
@@ -264,7 +270,8 @@ def _infer(node: Node, ins: list[Value], gpu: bool) -> tuple[tuple[int, ...], st
     if op == "cast":
         only("dtype")
         arity(1, 1)
-        _req(a.get("dtype") in WIRE_DTYPES, f"{what}: dtype must be one of {sorted(WIRE_DTYPES)}")
+        _req(a.get("dtype") in FLOAT_DTYPES and ins[0].dtype in FLOAT_DTYPES,
+             f"{what}: casts between {FLOAT_DTYPES} only")
         return ins[0].shape, a["dtype"]
     if op == "interpolate":
         only("size", "mode")
@@ -276,15 +283,139 @@ def _infer(node: Node, ins: list[Value], gpu: bool) -> tuple[tuple[int, ...], st
              f"{what}: size must be [H, W]")
         _req(a.get("mode", "bicubic") in INTERP_MODES, f"{what}: mode must be one of {INTERP_MODES}")
         return (x.shape[0], x.shape[1], size[0], size[1]), x.dtype
-    raise ProgramError(f"{what}: op {op!r} is not one the pod server runs "
-                       f"(whitelist: linear layernorm attention add mul {' '.join(UNARY)} cat slice reshape permute "
-                       f"expand cast interpolate)")
+    if op == "conv2d":
+        only("stride", "padding", "dilation", "groups")
+        arity(2, 3)
+        dt = same_dtype()
+        x, w = ins[0], ins[1]
+        _req(len(x.shape) == 4 and len(w.shape) == 4 and x.shape[1] == w.shape[1],
+             f"{what}: x [N, C, H, W] and weight [OC, C, KH, KW] required, got {x.shape} and {w.shape}")
+        _req(a.get("groups", 1) == 1, f"{what}: only groups = 1 convolutions run on the pod server")
+        if len(ins) == 3:
+            _req(ins[2].shape == (w.shape[0],), f"{what}: bias must be [{w.shape[0]}]")
+        st = _pair(a.get("stride", [1, 1]), f"{what}: stride", 1)
+        pd = _pair(a.get("padding", [0, 0]), f"{what}: padding", 0)
+        dl = _pair(a.get("dilation", [1, 1]), f"{what}: dilation", 1)
+        oh = (x.shape[2] + 2 * pd[0] - dl[0] * (w.shape[2] - 1) - 1) // st[0] + 1
+        ow = (x.shape[3] + 2 * pd[1] - dl[1] * (w.shape[3] - 1) - 1) // st[1] + 1
+        _req(oh >= 1 and ow >= 1, f"{what}: empty output for input {x.shape}")
+        return (x.shape[0], w.shape[0], oh, ow), dt
+    if op == "batchnorm":
+        only("eps")
+        arity(5, 5)
+        dt = same_dtype()
+        x = ins[0]
+        _req(len(x.shape) >= 2 and all(v.shape == (x.shape[1],) for v in ins[1:]),
+             f"{what}: x [N, C, ...] and gamma / beta / mean / var [C] required")
+        _eps(a, what)
+        return x.shape, dt
+    if op in ("max_pool2d", "avg_pool2d"):
+        only("kernel", "stride", "padding")
+        arity(1, 1)
+        x = ins[0]
+        _req(len(x.shape) == 4 and x.dtype in FLOAT_DTYPES, f"{what}: takes a float [N, C, H, W] tensor")
+        k = _pair(a.get("kernel"), f"{what}: kernel", 1)
+        st = _pair(a.get("stride", list(k)), f"{what}: stride", 1)
+        pd = _pair(a.get("padding", [0, 0]), f"{what}: padding", 0)
+        _req(pd[0] <= k[0] // 2 and pd[1] <= k[1] // 2, f"{what}: padding must be <= kernel / 2")
+        oh, ow = (x.shape[2] + 2 * pd[0] - k[0]) // st[0] + 1, (x.shape[3] + 2 * pd[1] - k[1]) // st[1] + 1
+        _req(oh >= 1 and ow >= 1, f"{what}: empty output")
+        return (x.shape[0], x.shape[1], oh, ow), x.dtype
+    if op in ("mean", "sum"):
+        only("dims", "keepdim")
+        arity(1, 1)
+        x = ins[0]
+        r = len(x.shape)
+        dims = a.get("dims")
+        _req(isinstance(dims, list) and dims and all(isinstance(d, int) and not isinstance(d, bool) and -r <= d < r
+                                                      for d in dims), f"{what}: dims must be a list of axes")
+        dd = sorted({d % r for d in dims})
+        keep = a.get("keepdim", False)
+        _req(isinstance(keep, bool), f"{what}: keepdim must be a bool")
+        _req(x.dtype in FLOAT_DTYPES, f"{what}: takes a float tensor")
+        return tuple((1 if i in dd else n) for i, n in enumerate(x.shape) if keep or i not in dd), x.dtype
+    if op == "matmul":
+        only()
+        arity(2, 2)
+        dt = same_dtype()
+        x, y = ins
+        _req(len(x.shape) >= 2 and len(y.shape) >= 2 and x.shape[-1] == y.shape[-2],
+             f"{what}: [..., M, K] @ [..., K, N] required, got {x.shape} and {y.shape}")
+        bx, by = x.shape[:-2], y.shape[:-2]
+        _req(not bx or not by or bx == by, f"{what}: batch dims must match or one side be 2-D")
+        return (bx or by) + (x.shape[-2], y.shape[-1]), dt
+    if op == "softmax":
+        only("dim")
+        arity(1, 1)
+        _req(a.get("dim", -1) in (-1, len(ins[0].shape) - 1), f"{what}: softmax runs over the last dim")
+        _req(ins[0].dtype in FLOAT_DTYPES, f"{what}: takes a float tensor")
+        return ins[0].shape, ins[0].dtype
+    if op == "embedding":
+        only()
+        arity(2, 2)
+        ids, table = ins
+        _req(ids.dtype == "i32", f"{what}: ids must be i32, got {ids.dtype}")
+        _req(len(table.shape) == 2 and table.dtype in FLOAT_DTYPES, f"{what}: table must be a float [V, D]")
+        if gpu:
+            _req(table.shape[1] * WIRE_DTYPES[table.dtype] % 16 == 0, f"{what}: table rows must be 16-byte multiples")
+        return ids.shape + (table.shape[1],), table.dtype
+    if op == "rmsnorm":
+        only("eps")
+        arity(2, 2)
+        dt = same_dtype()
+        _req(len(ins[0].shape) >= 1 and ins[1].shape == (ins[0].shape[-1],), f"{what}: weight must be [D]")
+        _eps(a, what)
+        return ins[0].shape, dt
+    if op == "rotary":
+        only()
+        arity(3, 3)
+        x, c, sn = ins
+        _req(len(x.shape) == 4 and x.shape[3] % 2 == 0 and x.dtype in FLOAT_DTYPES,
+             f"{what}: x must be [B, S, H, D] with D even")
+        _req(c.shape == sn.shape == (x.shape[1], x.shape[3]) and c.dtype == sn.dtype == "fp32",
+             f"{what}: cos / sin must be fp32 [S, D] = [{x.shape[1]}, {x.shape[3]}]")
+        return x.shape, x.dtype
+    if op == "sdpa":
+        only("causal", "scale")
+        arity(3, 3)
+        dt = same_dtype()
+        q, k, v = ins
+        _req(len(q.shape) == 4 and len(k.shape) == 4 and k.shape == v.shape and q.shape[0] == k.shape[0]
+             and q.shape[3] == k.shape[3] and q.shape[2] % k.shape[2] == 0,
+             f"{what}: q [B, Sq, H, D], k / v [B, Skv, Hkv, D] with H % Hkv == 0 required, got {q.shape}, {k.shape}")
+        _req(isinstance(a.get("causal", False), bool), f"{what}: causal must be a bool")
+        if a.get("causal"):
+            _req(q.shape[1] <= k.shape[1], f"{what}: causal attention needs Sq <= Skv")
+        if "scale" in a:
+            _req(isinstance(a["scale"], (int, float)) and a["scale"] > 0, f"{what}: scale must be > 0")
+        if gpu:
+            _req(q.shape[3] in (64, 128), f"{what}: the attention kernels take head_dim 64 or 128, got {q.shape[3]}")
+        return q.shape, dt
+    raise ProgramError(f"{what}: op {op!r} is not one the pod server runs (whitelist: {' '.join(OPS)})")
 
 
-OPS = ("linear", "layernorm", "attention", "add", "mul", *UNARY, "cat", "slice", "reshape", "permute", "expand",
-       "cast", "interpolate")
-NEVER_FOLD = ("attention",)
-GEMM_OPS = ("linear",)
+def _pair(v, what: str, lo: int) -> tuple[int, int]:
+    if isinstance(v, int) and not isinstance(v, bool):
+        v = [v, v]
+    _req(isinstance(v, list) and len(v) == 2, f"{what} must be an int or [h, w]")
+    return (_int(v[0], what, lo), _int(v[1], what, lo))
+
+
+def _eps(a: dict, what: str) -> None:
+    eps = a.get("eps", 1e-5)
+    _req(isinstance(eps, (int, float)) and not isinstance(eps, bool) and 0 < eps < 1, f"{what}: eps must be in (0, 1)")
+
+
+OPS = ("linear", "layernorm", "attention", *BINARY, *UNARY, "cat", "slice", "reshape", "permute", "expand",
+       "cast", "interpolate",
+       # general tenants: conv nets and decoder LLMs (nos_amd/ops/tenant.py)
+       "conv2d", "batchnorm", "max_pool2d", "avg_pool2d", "mean", "sum", "matmul", "softmax", "embedding",
+       "rmsnorm", "rotary", "sdpa")
+NEVER_FOLD = ("attention", "sdpa")
+# step kinds that run a gfx950 kernel of libnos_hip.so (CompiledProgram.stats["kernels"])
+NATIVE_KINDS = ("linear", "linear_ln", "linear_rms", "ln_qkv_attention", "attention", "layernorm", "conv2d", "matmul",
+                "softmax", "embedding", "rmsnorm", "rotary", "sdpa")
+GEMM_OPS = ("linear", "conv2d")
 
 
 def _workspace(node: Node, ins: list[Value], out: Value, f32_math: str) -> int:
@@ -294,12 +425,36 @@ def _workspace(node: Node, ins: list[Value], out: Value, f32_math: str) -> int:
     if op == "linear" and ins[0].dtype == "fp32" and f32_math == "h3":
         m = ins[0].numel // ins[0].shape[-1]
         return ins[0].nbytes + 4 * m                       # A's fp16 planes + row scales
+    if op == "linear_rms" or (op == "linear" and ins[0].dtype == "bf16" and f32_math == "h3"):
+        m = ins[0].numel // ins[0].shape[-1]
+        return 2 * m * ins[0].shape[-1] * 4 + 4 * m + out.numel * 4
     if op == "attention":
         b, s, three_hd = ins[0].shape
-        hd = three_hd // 3
-        skvp = -(-s // 32) * 32
-        return b * skvp * 6 * hd * 2 + 4 * b * s * (hd + 2 * node.attrs["heads"]) * 4 + ins[0].nbytes
+        h = node.attrs["heads"]
+        return _attn_ws(b, s, s, h, h, three_hd // (3 * h)) + ins[0].nbytes + out.numel * 4
+    if op == "sdpa":
+        (b, sq, h, d), (_, skv, hkv, _) = ins[0].shape, ins[1].shape
+        copies = sum(v.numel * 4 for v in ins[:3]) if ins[0].dtype != "fp32" else 0
+        return _attn_ws(b, sq, skv, h, hkv, d) + copies + out.numel * 4
+    if op == "conv2d":
+        n, c, _, _ = ins[0].shape
+        oc, _, kh, kw = ins[1].shape
+        p = out.numel // (n * oc)
+        kp = -(-(c * kh * kw) // 32) * 32
+        return n * p * (kp * 4 + 4) + ins[0].numel * 4 + out.numel * 4
+    if op == "matmul":
+        k = ins[0].shape[-1]
+        kp = -(-k // 32) * 32
+        rows = ins[0].numel // k + ins[1].numel // k
+        return rows * kp * 12 + out.numel * 4          # padded fp32 copies + planes + the fp32 result
     return 0
+
+
+def _attn_ws(b: int, sq: int, skv: int, h: int, hkv: int, d: int) -> int:
+    """Upper bound of both attention kernels' workspaces (attention_f32x.hip
+    nos_attn_f32x6_workspace, attention_h3g.hip nos_attn_h3g_workspace)."""
+    skvp = -(-skv // 32) * 32
+    return b * max(h, hkv) * skvp * 6 * d * 2 + 4 * b * sq * h * (d + 2) * 4 + b * hkv * (skv // 256 + 2) * 8 + 4096
 
 
 @dataclass
@@ -405,9 +560,21 @@ class Program:
         import torch
 
         v = self.inputs[0]
-        x = torch.zeros(v.shape, dtype=torch_dtype(v.dtype)) if data is None else \
-            torch.from_numpy(np.ascontiguousarray(data, dtype=np.float32)).view(v.shape).to(torch_dtype(v.dtype))
+        if data is None:
+            x = torch.zeros(v.shape, dtype=torch_dtype(v.dtype))
+        elif v.dtype == "i32":
+            x = torch.from_numpy(np.ascontiguousarray(data, dtype=np.int32)).view(v.shape)
+        else:
+            x = torch.from_numpy(np.ascontiguousarray(data, dtype=np.float32)).view(v.shape).to(torch_dtype(v.dtype))
         return x.to(device)
+
+    def id_bound(self) -> int | None:
+        """For an i32 (token id) input: the smallest embedding table it
+        indexes -- ids must lie in [0, bound) (checked per request)."""
+        if self.inputs[0].dtype != "i32":
+            return None
+        vs = [self.values[n.inputs[1]].shape[0] for n in self.nodes if n.op == "embedding"]
+        return min(vs) if vs else None
 
     # ------------------------------------------------------------ execution
     def compile(self, device, params: dict | None = None) -> "CompiledProgram":
@@ -420,7 +587,7 @@ class Program:
 
         ps = params if params is not None else self.tensors("cpu")
         env = {k: t.float().cpu() for k, t in ps.items()}
-        env[self.inputs[0].name] = x.float().cpu()
+        env[self.inputs[0].name] = x.cpu() if self.inputs[0].dtype == "i32" else x.float().cpu()
         with torch.no_grad():
             for n in self.nodes:
                 args = [env[i] for i in n.inputs]
@@ -434,7 +601,7 @@ class Program:
 def torch_dtype(dt: str):
     import torch
 
-    return {"fp32": torch.float32, "bf16": torch.bfloat16}[dt]
+    return {"fp32": torch.float32, "bf16": torch.bfloat16, "i32": torch.int32}[dt]
 
 
 def parse(obj: dict, payload: bytes | memoryview = b"", gpu: bool = False) -> Program:
@@ -469,7 +636,7 @@ def parse(obj: dict, payload: bytes | memoryview = b"", gpu: bool = False) -> Pr
     for d in ps:
         _req(isinstance(d, dict), "params must be objects")
         dt = d.get("dtype", "fp32")
-        _req(dt in WIRE_DTYPES, f"param dtype must be one of {sorted(WIRE_DTYPES)}")
+        _req(dt in FLOAT_DTYPES, f"param dtype must be one of {FLOAT_DTYPES}")
         v = Value(_name(d.get("name"), "param name"), _shape(d.get("shape"), "param shape"), dt, "param")
         off, nb = _int(d.get("offset"), "param offset", 0), _int(d.get("nbytes"), "param nbytes", 0)
         _req(nb == v.nbytes, f"param {v.name!r}: nbytes {nb} != {v.nbytes} for {v.shape} {dt}")
@@ -522,6 +689,11 @@ def _eager(op: str, args: list, attrs: dict, ref: bool = False):
         x = args[0]
         return F.layer_norm(x, (x.shape[-1],), args[1], args[2], attrs.get("eps", 1e-5))
     if op == "attention":
+        if attrs.get("causal") or args[0].shape[-1] // (3 * attrs["heads"]) != 64 or not args[0].is_cuda:
+            from ..ops import tenant as T
+
+            q, k, v = _qkv_views(args[0], attrs["heads"])
+            return T.sdpa(q, k, v, causal=attrs.get("causal", False), scale=attrs.get("scale")).flatten(2)
         return ops.attention_qkv(args[0].contiguous(), attrs["heads"], scale=attrs.get("scale"))
     if op == "add":
         return args[0] + args[1]
@@ -552,7 +724,61 @@ def _eager(op: str, args: list, attrs: dict, ref: bool = False):
         mode = attrs.get("mode", "bicubic")
         return F.interpolate(args[0], size=tuple(attrs["size"]), mode=mode,
                              align_corners=None if mode == "nearest" else False)
+    if op == "sub":
+        return args[0] - args[1]
+    if op == "div":
+        return args[0] / args[1]
+    if op == "tanh":
+        return torch.tanh(args[0])
+    if op == "exp":
+        return torch.exp(args[0])
+    if op == "neg":
+        return -args[0]
+    if op == "rsqrt":
+        return torch.rsqrt(args[0])
+    if op == "conv2d":
+        return F.conv2d(args[0], args[1], args[2] if len(args) > 2 else None, _pair2(attrs, "stride", 1),
+                        _pair2(attrs, "padding", 0), _pair2(attrs, "dilation", 1))
+    if op == "batchnorm":
+        return F.batch_norm(args[0], args[3], args[4], args[1], args[2], False, 0.0, attrs.get("eps", 1e-5))
+    if op == "max_pool2d":
+        k = _pair2(attrs, "kernel", 1)
+        return F.max_pool2d(args[0], k, attrs.get("stride") and _pair2(attrs, "stride", 1) or k,
+                            _pair2(attrs, "padding", 0))
+    if op == "avg_pool2d":
+        k = _pair2(attrs, "kernel", 1)
+        return F.avg_pool2d(args[0], k, attrs.get("stride") and _pair2(attrs, "stride", 1) or k,
+                            _pair2(attrs, "padding", 0))
+    if op == "mean":
+        return args[0].mean(dim=attrs["dims"], keepdim=attrs.get("keepdim", False))
+    if op == "sum":
+        return args[0].sum(dim=attrs["dims"], keepdim=attrs.get("keepdim", False))
+    if op == "matmul":
+        return args[0] @ args[1]
+    if op == "softmax":
+        return torch.softmax(args[0].float(), dim=-1).to(args[0].dtype)
+    if op == "embedding":
+        return F.embedding(args[0].long(), args[1])
+    from ..ops import tenant as T
+
+    if op == "rmsnorm":
+        return T.rmsnorm_ref(args[0], args[1], attrs.get("eps", 1e-5))
+    if op == "rotary":
+        return T.rope_ref(args[0], args[1], args[2])
+    if op == "sdpa":
+        return T.sdpa_ref(args[0], args[1], args[2], attrs.get("causal", False), attrs.get("scale"))
     raise ProgramError(f"op {op!r}")
+
+
+def _pair2(attrs: dict, key: str, default: int) -> tuple[int, int]:
+    v = attrs.get(key, default)
+    return (v, v) if isinstance(v, int) else (v[0], v[1])
+
+
+def _qkv_views(qkv, heads: int):
+    """q, k, v [B, S, H, D] views of a fused projection [B, S, 3*H*D]."""
+    B, S, n = qkv.shape
+    return qkv.view(B, S, 3, heads, n // (3 * heads)).unbind(2)
 
 
 @dataclass
@@ -580,18 +806,23 @@ class CompiledProgram:
         self.input_name = prog.inputs[0].name
         self.outputs = list(prog.outputs)
         self.stats: dict[str, int] = {}
+        self.aux: dict[str, object] = {}   # derived weights a kernel reads (e.g. conv weights as padded matrices)
         with torch.no_grad():
             steps = self._fold_constants(prog)
+            steps = self._fold_batchnorm(steps)
+            steps = self._merge_parallel_linears(steps)
             steps = self._fold_layernorm(steps)
+            steps = self._fold_rmsnorm(steps)
             steps = self._fuse_epilogues(steps)
             steps = self._fuse_qkv_attention(steps)
+            steps = self._fuse_rotary_sdpa(steps)
             steps = self._mark_plane_handoffs(steps)
+            self._prep_conv_weights(steps)
             self.steps = self._plan_releases(steps)
             used = {i for s in self.steps for i in s.inputs} | set(self.outputs)
             for k in [k for k in self.consts if k not in used]:  # e.g. weights replaced by their LN-folded form
                 del self.consts[k]
-        self.stats["kernels"] = sum(1 for s in self.steps if s.kind in ("linear", "linear_ln", "ln_qkv_attention",
-                                                                           "attention", "layernorm"))
+        self.stats["kernels"] = sum(1 for s in self.steps if s.kind in NATIVE_KINDS)
 
     # ------------------------------------------------------------ passes
     def _fold_constants(self, prog: Program) -> list[_Step]:
@@ -621,6 +852,79 @@ class CompiledProgram:
             del self.consts[k]
         self.stats["constant_folded"] = folded
         return steps
+
+    def _fold_batchnorm(self, steps: list[_Step]) -> list[_Step]:
+        """conv2d -> batchnorm (inference statistics, all weights constant)
+        becomes one conv2d with W' = W gamma / sqrt(var + eps) and
+        b' = (b - mean) gamma / sqrt(var + eps) + beta."""
+        import torch
+
+        uses = self._consumers(steps, self.outputs)
+        by_out = {s.output: s for s in steps}
+        drop, n = set(), 0
+        for s in steps:
+            if s.kind != "batchnorm":
+                continue
+            c = by_out.get(s.inputs[0])
+            if (c is None or c.kind != "conv2d" or uses.get(c.output) != 1
+                    or not all(i in self.consts for i in c.inputs[1:] + s.inputs[1:])):
+                continue
+            w = self.consts[c.inputs[1]]
+            b = self.consts[c.inputs[2]].float() if len(c.inputs) > 2 else 0.0
+            g, be, mu, var = (self.consts[i].float() for i in s.inputs[1:])
+            inv = g * torch.rsqrt(var + s.attrs.get("eps", 1e-5))
+            base = f"{s.output}::bn"
+            self.consts[base + ".w"] = (w.float() * inv[:, None, None, None]).to(w.dtype).contiguous()
+            self.consts[base + ".b"] = ((b - mu) * inv + be).to(w.dtype).contiguous()
+            c.inputs = [c.inputs[0], base + ".w", base + ".b"]
+            drop.add(c.output)
+            c.output = s.output
+            by_out[s.output] = c
+            s.kind = "__dropped__"
+            n += 1
+        self.stats["batchnorm_folded"] = n
+        return [s for s in steps if s.kind != "__dropped__"]
+
+    def _merge_parallel_linears(self, steps: list[_Step]) -> list[_Step]:
+        """Linears that read the same activation with constant weights (Q / K /
+        V projections, an MLP's gate / up) become ONE GEMM over the
+        concatenated weights, each original output a column slice (a view) of
+        it: fewer, wider launches, and the norm before them gets a single
+        consumer, which lets it fold into the GEMM."""
+        import torch
+
+        groups: dict[str, list[_Step]] = {}
+        for s in steps:
+            if (s.kind == "linear" and s.inputs[0] not in self.consts and not s.attrs
+                    and all(i in self.consts for i in s.inputs[1:])):
+                groups.setdefault(s.inputs[0], []).append(s)
+        first: dict[int, _Step] = {}
+        n = 0
+        for x, g in groups.items():
+            if len(g) < 2 or len({self.consts[m.inputs[1]].dtype for m in g}) != 1:
+                continue
+            ws = [self.consts[m.inputs[1]] for m in g]
+            name = f"{g[0].output}::merged"
+            self.consts[name + ".w"] = torch.cat(ws, dim=0).contiguous()
+            ins = [x, name + ".w"]
+            if any(len(m.inputs) > 2 for m in g):
+                self.consts[name + ".b"] = torch.cat([self.consts[m.inputs[2]] if len(m.inputs) > 2 else
+                                                      torch.zeros(w.shape[0], dtype=w.dtype, device=w.device)
+                                                      for m, w in zip(g, ws)]).contiguous()
+                ins.append(name + ".b")
+            first[id(g[0])] = _Step("linear", ins, name, {})
+            off = 0
+            for m, w in zip(g, ws):
+                m.kind, m.inputs, m.attrs = "slice", [name], {"dim": -1, "start": off, "end": off + w.shape[0]}
+                off += w.shape[0]
+            n += len(g)
+        out = []
+        for s in steps:
+            if id(s) in first:
+                out.append(first[id(s)])
+            out.append(s)
+        self.stats["linears_merged"] = n
+        return out
 
     @staticmethod
     def _consumers(steps: list[_Step], outputs: list[str]) -> dict[str, int]:
@@ -658,6 +962,31 @@ class CompiledProgram:
         self.stats["layernorm_folded"] = n
         return [s for s in steps if s.output not in drop]
 
+    def _fold_rmsnorm(self, steps: list[_Step]) -> list[_Step]:
+        """rmsnorm -> linear (its only consumer, constant weights) becomes one
+        ``linear_rms``: gamma folded into the weight, the row statistics in
+        the h3 split pre-pass (ops.tenant.linear_rms)."""
+        uses = self._consumers(steps, self.outputs)
+        by_out = {s.output: s for s in steps}
+        drop, n = set(), 0
+        for s in steps:
+            if s.kind != "linear" or s.inputs[0] not in by_out:
+                continue
+            rn = by_out[s.inputs[0]]
+            if rn.kind != "rmsnorm" or uses.get(rn.output) != 1 or not all(i in self.consts for i in
+                                                                              s.inputs[1:] + rn.inputs[1:]):
+                continue
+            w, g = self.consts[s.inputs[1]], self.consts[rn.inputs[1]]
+            base = f"{s.output}::rms"
+            self.consts[base + ".w"] = (w.float() * g.float()[None, :]).to(w.dtype).contiguous()
+            s.kind = "linear_rms"
+            s.inputs = [rn.inputs[0], base + ".w"] + s.inputs[2:]
+            s.attrs = {"act": s.attrs.get("act"), "eps": rn.attrs.get("eps", 1e-5)}
+            drop.add(rn.output)
+            n += 1
+        self.stats["rmsnorm_folded"] = n
+        return [s for s in steps if s.output not in drop]
+
     def _fuse_epilogues(self, steps: list[_Step]) -> list[_Step]:
         uses = self._consumers(steps, self.outputs)
         by_out = {s.output: s for s in steps}
@@ -665,11 +994,22 @@ class CompiledProgram:
         keep = []
         n_act = n_res = 0
         for s in steps:
+            orig = list(s.inputs)
             s.inputs = [rename.get(i, i) for i in s.inputs]
             src = by_out.get(s.inputs[0]) if s.inputs else None
-            if (s.kind in ("gelu", "relu") and src is not None and src.kind in ("linear", "linear_ln")
+            if (s.kind in ("gelu", "relu") and src is not None and src.kind in ("linear", "linear_ln", "linear_rms")
                     and uses.get(src.output) == 1 and not src.attrs.get("act") and "residual" not in src.attrs):
                 src.attrs["act"] = s.kind
+                rename[s.output] = src.output
+                n_act += 1
+                continue
+            if (s.kind in ("gelu", "relu") and src is not None and src.kind == "conv2d" and uses.get(orig[0]) == 1
+                    and not src.attrs.get("act")):
+                # conv -> act, or conv + residual -> act (a ResNet block's tail: the
+                # residual goes in before the activation)
+                src.attrs["act"] = s.kind
+                if src.attrs.get("residual"):
+                    src.attrs["residual_first"] = True
                 rename[s.output] = src.output
                 n_act += 1
                 continue
@@ -677,7 +1017,8 @@ class CompiledProgram:
                 a, b = s.inputs
                 for prod, other in ((a, b), (b, a)):
                     p = by_out.get(prod)
-                    if (p is not None and p.kind == "linear" and uses.get(prod) == 1 and "residual" not in p.attrs
+                    if (p is not None and p.kind in ("linear", "conv2d") and uses.get(prod) == 1
+                            and "residual" not in p.attrs
                             and self._shape(prod) == self._shape(s.output) == self._shape(other)
                             and self._dtype(prod) == self._dtype(other) and other != prod):
                         p.attrs["residual"] = True
@@ -723,6 +1064,8 @@ class CompiledProgram:
             d = self._shape(s.output)[-1] // s.attrs["heads"]
             if "scale" in s.attrs and s.attrs["scale"] != 1.0 / math.sqrt(d):
                 continue  # the fused kernels use the default 1/sqrt(head_dim)
+            if s.attrs.get("causal") or d != 64:
+                continue  # the general attention (ops.tenant.sdpa) runs it
             s.kind = "ln_qkv_attention"
             s.attrs = {"heads": s.attrs["heads"], "eps": p.attrs["eps"]}
             s.inputs = list(p.inputs)
@@ -730,6 +1073,47 @@ class CompiledProgram:
             n += 1
         self.stats["qkv_attention_fused"] = n
         return [s for s in steps if s.output not in drop]
+
+    def _fuse_rotary_sdpa(self, steps: list[_Step]) -> list[_Step]:
+        """rotary(q), rotary(k) -> sdpa with the same constant tables: the
+        rotation moves into the attention (Q on load, K in its split pass)."""
+        uses = self._consumers(steps, self.outputs)
+        by_out = {s.output: s for s in steps}
+        drop, n = set(), 0
+        for s in steps:
+            if s.kind != "sdpa":
+                continue
+            pq, pk = by_out.get(s.inputs[0]), by_out.get(s.inputs[1])
+            if (pq is None or pk is None or pq is pk or pq.kind != "rotary" or pk.kind != "rotary"
+                    or uses.get(pq.output) != 1 or uses.get(pk.output) != 1 or pq.inputs[1:] != pk.inputs[1:]
+                    or not all(i in self.consts for i in pq.inputs[1:])
+                    or self._shape(pq.inputs[1])[0] != self._shape(s.inputs[1])[1]):
+                continue
+            s.inputs = [pq.inputs[0], pk.inputs[0], s.inputs[2]] + pq.inputs[1:]
+            s.attrs = {**s.attrs, "rope": True}
+            drop |= {pq.output, pk.output}
+            n += 1
+        self.stats["rotary_fused"] = n
+        return [s for s in steps if s.output not in drop]
+
+    def _prep_conv_weights(self, steps: list[_Step]) -> None:
+        """GPU: every conv weight [OC, C, KH, KW] also as the fp32 [OC, Kp]
+        matrix the h3 GEMM reads (K = C KH KW zero-padded to 32), kept so its
+        split planes are cached across replays."""
+        import torch.nn.functional as F
+
+        if not self.gpu:
+            return
+        for s in steps:
+            if s.kind != "conv2d" or s.inputs[1] not in self.consts:
+                continue
+            w = self.consts[s.inputs[1]]
+            k = w[0].numel()
+            w2 = w.float().reshape(w.shape[0], k)
+            kp = -(-k // 32) * 32
+            name = s.inputs[1] + "::mat"
+            self.aux[name] = (F.pad(w2, (0, kp - k)) if kp != k else w2).contiguous()
+            s.attrs["w2"] = name
 
     def _mark_plane_handoffs(self, steps: list[_Step]) -> list[_Step]:
         """A fused LN-QKV attention or LN-GEMM whose only consumer is a
@@ -770,6 +1154,7 @@ class CompiledProgram:
     # ------------------------------------------------------------ run
     def __call__(self, x) -> tuple:
         from .. import ops
+        from ..ops import tenant as T
 
         env = dict(self.consts)
         env[self.input_name] = x
@@ -801,7 +1186,28 @@ class CompiledProgram:
                     qkv = ops.linear_ln(h, a[1], a[2], a[3], eps=s.attrs["eps"])
                     y = ops.attention_qkv(qkv, s.attrs["heads"])
             elif k == "attention":
-                y = ops.attention_qkv(a[0].contiguous(), s.attrs["heads"], scale=s.attrs.get("scale"))
+                y = _eager("attention", [a[0].contiguous()], s.attrs)
+            elif k == "conv2d":
+                res = a.pop() if s.attrs.get("residual") else None
+                y = T.conv2d(a[0], a[1], a[2] if len(a) > 2 else None, _pair2(s.attrs, "stride", 1),
+                             _pair2(s.attrs, "padding", 0), _pair2(s.attrs, "dilation", 1), act=s.attrs.get("act"),
+                             residual=res, w2=self.aux.get(s.attrs.get("w2")),
+                             residual_first=bool(s.attrs.get("residual_first")))
+            elif k == "linear_rms":
+                y = T.linear_rms(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"), eps=s.attrs["eps"])
+            elif k == "matmul":
+                y = T.matmul(a[0], a[1])
+            elif k == "softmax":
+                y = T.softmax(a[0])
+            elif k == "embedding":
+                y = T.embedding(a[0], a[1])
+            elif k == "rmsnorm":
+                y = T.rmsnorm(a[0], a[1], s.attrs.get("eps", 1e-5))
+            elif k == "rotary":
+                y = T.rotary(a[0], a[1], a[2])
+            elif k == "sdpa":
+                y = T.sdpa(a[0], a[1], a[2], causal=s.attrs.get("causal", False), scale=s.attrs.get("scale"),
+                           rope=(a[3], a[4]) if s.attrs.get("rope") else None)
             elif k == "layernorm":
                 xx = a[0].contiguous()
                 if xx.is_cuda and str(xx.dtype) == "torch.bfloat16":

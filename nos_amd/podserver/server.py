@@ -107,6 +107,7 @@ class Tenant:
     program: str = ""
     compile_stats: dict = field(default_factory=dict)
     evicted: str | None = None
+    id_bound: int | None = None    # token-id input: ids must lie in [0, id_bound)
 
 
 @dataclass
@@ -488,7 +489,8 @@ class PodServer:
             with torch.no_grad():
                 m = prog.compile("cpu")
             x = prog.input_tensor("cpu")
-            return Tenant(tid, pod, limit, dtype, m, x, program=prog.name, compile_stats=dict(m.stats), cu_mask=mask)
+            return Tenant(tid, pod, limit, dtype, m, x, program=prog.name, compile_stats=dict(m.stats), cu_mask=mask,
+                          id_bound=prog.id_bound())
         base = torch.cuda.memory_allocated()
         torch.cuda.reset_peak_memory_stats()
         stream = None
@@ -550,7 +552,7 @@ class PodServer:
         t = Tenant(tid, pod, limit, dtype, m, x, stream=stream, graph=gt.graph,
                    outputs=gt.outputs, footprint_gb=round(peak, 3), cu_mask=mask,
                    solo_graph=solo.graph if solo else None, solo_outputs=solo.outputs if solo else (),
-                   program=prog.name, compile_stats={**m.stats, **times})
+                   program=prog.name, compile_stats={**m.stats, **times}, id_bound=prog.id_bound())
         if limit and peak > limit:
             self._free(t)
             raise AdmissionError(f"tenant needs {peak:.2f} GB, its slice has {limit} GB")
@@ -671,9 +673,12 @@ class PodServer:
         t = job.tenant
         x_in = None
         if job.payload:
-            x_in = np.frombuffer(job.payload, dtype=np.float32)
+            ids = str(t.x.dtype) == "torch.int32"
+            x_in = np.frombuffer(job.payload, dtype=np.int32 if ids else np.float32)
             if x_in.size != t.x.numel():
                 raise ValueError(f"input has {x_in.size} values, the tenant's model takes {t.x.numel()}")
+            if ids and t.id_bound is not None and x_in.size and (x_in.min() < 0 or x_in.max() >= t.id_bound):
+                raise ValueError(f"token ids must lie in [0, {t.id_bound})")
         with torch.no_grad():
             if not self.gpu:
                 if x_in is not None:
@@ -683,7 +688,7 @@ class PodServer:
                 s = t.stream.torch if t.stream is not None else lane
                 with torch.cuda.stream(s):
                     if x_in is not None:
-                        t.x.copy_(torch.from_numpy(x_in.copy()).view(t.x.shape).to(t.x.dtype))
+                        t.x.copy_(torch.from_numpy(x_in.copy()).view(t.x.shape).to(t.x.dtype), non_blocking=False)
                     outs = t.outputs
                     if alone and t.solo_graph is not None:
                         t.solo_graph.replay()
