@@ -113,6 +113,9 @@ def parse_args(argv=None):
     ap.add_argument("--table-modes", default="shared,cumask")
     ap.add_argument("--table-window-s", type=float, default=5.0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--tenant-mix", default="", metavar="FAMILY:N,...",
+                    help="server mode: a mixed fleet of model families, e.g. yolos:16,resnet:6,llama:6 "
+                         "(pods of the other families ship prebuilt programs; per-family throughput in 'mix')")
     ap.add_argument("--quota", action="store_true",
                     help="BASELINE config 5 instead of the headline: two namespaces' ElasticQuotas on the GPU's "
                          "pod-server slices, borrowing then fair-share preemption acting on running tenants "
@@ -305,6 +308,67 @@ def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+TENANT_FAMILIES = ("yolos", "resnet", "llama")
+
+
+def assign_tenant_mix(args, envs: list[dict]) -> list[str]:
+    """``--tenant-mix yolos:16,resnet:6,llama:6``: build the non-YOLOS
+    programs once (ResNet-18 at 224x224 via torch.fx, a random-init Llama
+    decoder at seq 512), write them under the pod-server directory, and point
+    pod slots at them (NOS_AMD_POD_PROGRAM), interleaved so each family is
+    spread over the fleet.  Returns the family of every pod slot."""
+    from nos_amd.podserver.program import save_program
+
+    want = []
+    for part in args.tenant_mix.split(","):
+        fam, n = part.split(":")
+        if fam not in TENANT_FAMILIES:
+            raise SystemExit(f"--tenant-mix: family must be one of {TENANT_FAMILIES}, got {fam!r}")
+        want += [fam] * int(n)
+    if len(want) != len(envs):
+        raise SystemExit(f"--tenant-mix names {len(want)} pods, the fleet has {len(envs)}")
+    # interleave: slot i takes the family furthest behind its share
+    order, cnt = [], {f: 0 for f in TENANT_FAMILIES}
+    tot = {f: want.count(f) for f in TENANT_FAMILIES}
+    for i in range(len(want)):
+        f = min((f for f in TENANT_FAMILIES if cnt[f] < tot[f]), key=lambda f: (cnt[f] + 1) / tot[f])
+        cnt[f] += 1
+        order.append(f)
+    small = args.device == "cuda"
+    built = {}
+    for fam in set(order) - {"yolos"}:
+        prefix = os.path.join(args.pod_server_dir, f"program-{fam}")
+        if fam == "resnet":
+            from nos_amd.models.resnet import resnet_tenant
+
+            save_program(prefix, *resnet_tenant(args.dtype, 0, small=small))
+        else:
+            from nos_amd.models.llama_program import llama_tenant
+
+            save_program(prefix, *llama_tenant(args.dtype, 0, small=small))
+        built[fam] = prefix
+    for e, fam in zip(envs, order):
+        if fam in built:
+            e["NOS_AMD_POD_PROGRAM"] = built[fam]
+    args.extra_bf16_s, args.table, args.ref_pod_s = 0.0, "", 0.0
+    return order
+
+
+def mix_stats(w, families: list[str]) -> dict:
+    """Per-family inferences/s and mean latency of a mixed fleet window."""
+    out = {}
+    for p in w.inference_pods:
+        fam = families[p.slot] if p.slot < len(families) else "?"
+        f = out.setdefault(fam, {"pods": 0, "completed": 0.0, "running": 0, "program": p.info.get("program")})
+        f["pods"] += 1
+        f["completed"] += p.completed
+        f["running"] += int(p.running)
+    for f in out.values():
+        f["inf_per_s"] = round(f.pop("completed") / w.window_s, 2) if w.window_s else 0.0
+        f["mean_latency_s"] = round(f["pods"] / f["inf_per_s"], 5) if f["inf_per_s"] else None
+    return out
 
 
 def with_trainer(d: Dist, envs: list[dict], args) -> list[dict]:
@@ -573,6 +637,7 @@ def main(argv=None) -> int:
                    for mode in args.table_modes.split(",") if args.table
                    for n in map(int, args.table.split(","))]
     args.gpu_env = envs[0].get("HIP_VISIBLE_DEVICES", str(local))  # this rank's GPU (folded runs: shared)
+    families = assign_tenant_mix(args, envs) if args.tenant_mix else None
 
     d.init_gpu()
     sampler = UtilSampler(d.device) if d.cuda else None
@@ -612,8 +677,9 @@ def main(argv=None) -> int:
         w, util, n_util, ready_s, tr = run_fleet(d, launcher, pod_envs, args.dtype, not args.no_graphs,
                                                  fleet_env, args.warmup, args.steps, args.step_s, sampler,
                                                  device=args.device, server_alive=srv)
+    mix = mix_stats(w, families) if families else None
     bf = None
-    if args.extra_bf16_s > 0 and args.dtype != "bf16" and d.cuda:
+    if args.extra_bf16_s > 0 and args.dtype != "bf16" and d.cuda and not families:
         wb, ub, _, _, _ = run_fleet(d, launcher, fleet_envs(pod_envs), "bf16", not args.no_graphs, extra_env, 2, 1,
                                     args.extra_bf16_s, sampler, server_alive=srv)
         bf = {"inf_per_s": round(wb.throughput, 2), "mean_latency_s": wb.mean_latency_s,
@@ -751,6 +817,7 @@ def main(argv=None) -> int:
                                                                        "bucket's all-reduce, NCCL-tests busbw"},
         "rank0_window": w.as_dict(),
         "latency_table": table or None,
+        "tenant_mix": mix,
         "rank0_ref_pod": ref,
         "pods_ready_s": round(ready_s, 1),
         "control_plane": cp,

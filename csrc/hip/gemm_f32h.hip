@@ -100,14 +100,64 @@ struct PlaneOut {
   float sc = 1.f;
 };
 
+// ROWSPLIT (LnOut): a workgroup owns a whole row block -- it runs the
+// tiles_n tiles of its BM rows one after the other -- and, once its fp32 C
+// rows are stored, splits them LayerNorm-normalised into the NEXT GEMM's h3
+// A planes (what nos_split_rows_h3 in LN mode would do in a separate launch):
+// the pre-LN residual GEMMs (attention proj, fc2) hand the following LN-GEMM
+// (QKV, fc1) its operand, the rows read back from this CU's L1/L2
+struct LnOut {
+  _Float16* p = nullptr;
+  long long pplane = 0;
+  int ldp = 0;
+  float* rinv = nullptr;
+  float eps = 0.f;
+  int eln = 0;
+};
+
+// one LayerNorm-normalised row (N % 4 == 0) by a 32-lane half-wave: mean,
+// variance (two passes over the row, re-read from cache), then hi / lo
+// pieces of (x - mu) rstd 2^eln; rinv = 2^-eln (the consumer's row scale)
+__device__ __forceinline__ void ln_split_row(const float* __restrict__ x, int N, _Float16* __restrict__ ph,
+                                             _Float16* __restrict__ pl, float* __restrict__ rinv, float eps,
+                                             int eln, int lane) {
+  typedef __attribute__((ext_vector_type(4))) _Float16 f16x4_t;
+  float s = 0.f;
+  for (int k = lane * 4; k < N; k += 128) {
+    const float4 v = *reinterpret_cast<const float4*>(x + k);
+    s += (v.x + v.y) + (v.z + v.w);
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mu = s / (float)N;
+  float q = 0.f;
+  for (int k = lane * 4; k < N; k += 128) {
+    const float4 v = *reinterpret_cast<const float4*>(x + k);
+    const float d0 = v.x - mu, d1 = v.y - mu, d2 = v.z - mu, d3 = v.w - mu;
+    q = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, q))));
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float mul = rsqrtf(q / (float)N + eps) * nos::pow2i(eln), add = -mu * mul;
+  for (int k = lane * 4; k < N; k += 128) {
+    const float4 v = *reinterpret_cast<const float4*>(x + k);
+    f16x2_t h01, l01, h23, l23;
+    nos::split2h(f32x2_t{fmaf(v.x, mul, add), fmaf(v.y, mul, add)}, h01, l01);
+    nos::split2h(f32x2_t{fmaf(v.z, mul, add), fmaf(v.w, mul, add)}, h23, l23);
+    *reinterpret_cast<f16x4_t*>(ph + k) = f16x4_t{h01.x, h01.y, h23.x, h23.y};
+    *reinterpret_cast<f16x4_t*>(pl + k) = f16x4_t{l01.x, l01.y, l23.x, l23.y};
+  }
+  if (lane == 0) *rinv = nos::pow2i(-eln);
+}
+
 // BKT: K depth of an LDS stage (32: two 16-deep MFMA steps, or 16: one);
 // RS: stages in the ring (RS - 1 of them in flight ahead of the one computed)
-template <int BM, int BN, int WGM, int WGN, bool PERSIST, int BKT = 32, int RS = 2>
+template <int BM, int BN, int WGM, int WGN, bool PERSIST, int BKT = 32, int RS = 2, bool ROWSPLIT = false>
 __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3_kernel(
     const _Float16* __restrict__ Ap, int lda, long long aplane, const float* __restrict__ rinv, float rconst,
     const _Float16* __restrict__ Wp, int ldw, long long wplane, const float* __restrict__ csc,
     const float* __restrict__ bias, const float* __restrict__ R, int ldr, float* __restrict__ C, int ldc, int M,
-    int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv, PlaneOut po, Batch bt) {
+    int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv, PlaneOut po, Batch bt, LnOut lo) {
   constexpr int NW = WGM * WGN, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
   static_assert((NW == 4 || NW == 8) && MI >= 1 && NI >= 1, "4 or 8 waves");
   constexpr int ROWB = BKT * 2, CH = ROWB / 16, RPP = 1024 / ROWB, NSTEP = BKT / 16;
@@ -125,7 +175,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   const int ntiles1 = tiles_m * tiles_n, ntiles = ntiles1 * bt.nb;
   const int nk = K / BKT;
   nos::XcdChunk chunk;
-  if constexpr (PERSIST) {
+  if constexpr (ROWSPLIT) {  // this workgroup's row block: its tiles_n tiles in order
+    chunk.first = nos::xcd_remap(blockIdx.x, tiles_m) * tiles_n;
+    chunk.end = chunk.first + tiles_n;
+    chunk.step = 1;
+  } else if constexpr (PERSIST) {
     chunk = nos::xcd_chunk(blockIdx.x, gridDim.x, ntiles);
   } else {
     chunk.first = nos::xcd_remap(blockIdx.x, ntiles);
@@ -133,7 +187,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     chunk.step = 1;
   }
   for (int tt = chunk.first; tt < chunk.end; tt += chunk.step) {
-    if (PERSIST && tt != chunk.first) __syncthreads();
+    if ((PERSIST || ROWSPLIT) && tt != chunk.first) __syncthreads();
     const int bb = tt / ntiles1, t1 = tt - bb * ntiles1;
     const int tm = t1 / tiles_n, tn = t1 - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
@@ -386,6 +440,18 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
       }
     }
   }  // tiles
+  if constexpr (ROWSPLIT) {
+    // every wave's C stores of the row block are done and visible to the workgroup
+    __syncthreads();
+    const int m0 = (chunk.first / tiles_n) * BM;
+    const int hw = tid >> 5, l32 = tid & 31;
+    for (int r = hw; r < BM; r += NW * 2) {
+      const int m = m0 + r;
+      if (m < M)
+        ln_split_row(C + (long long)m * ldc, N, lo.p + (long long)m * lo.ldp, lo.p + lo.pplane + (long long)m * lo.ldp,
+                     lo.rinv + m, lo.eps, lo.eln, l32);
+    }
+  }
 }
 
 template <int BM, int BN, int WGM, int WGN, int BKT = 32, int RS = 2>
@@ -401,11 +467,11 @@ int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, f
   if (grid < ntiles)
     hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS>), dim3((unsigned)grid), dim3(NT), lds, st, Ap, lda,
                        aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
-                       tiles_n, kv, po, bt);
+                       tiles_n, kv, po, bt, LnOut{});
   else
     hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false, BKT, RS>), dim3((unsigned)ntiles), dim3(NT), lds, st, Ap,
                        lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
-                       tiles_n, kv, po, bt);
+                       tiles_n, kv, po, bt, LnOut{});
   return (int)hipGetLastError();
 }
 
@@ -668,4 +734,42 @@ NOS_API int nos_gemm_f32h3_batched(const void* Ap, int lda, long long aplane, lo
   bt.r = sr;
   return run_h3(Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, KvOut{},
                 PlaneOut{}, bt, stream);
+}
+
+// C = act(rinv[m] csc[n] (A' . W'^T) + bias) + R (a pre-LN residual GEMM,
+// nos_gemm_f32h3's contract without the KV / plane outputs), and the rows of
+// C LayerNorm-normalised (eps; no gamma / beta: those are folded into the
+// next GEMM) as that GEMM's h3 A planes P ([2][M][ldp], plane stride pplane)
+// on the scale 2^eln, rinv_out[m] = 2^-eln -- nos_split_rows_h3's LN mode
+// fused: one workgroup per 128-row block runs the block's tiles, then splits
+// its rows.  N % 4 == 0, K % 32 == 0.
+NOS_API int nos_gemm_f32h3_ln_out(const void* Ap, int lda, long long aplane, const float* rinv, float rconst,
+                                  const void* Wp, int ldw, long long wplane, const float* csc, const float* bias,
+                                  const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi, void* P,
+                                  int ldp, long long pplane, float* rinv_out, float eps, int eln, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0 || (N % 4) || !C || ldc < N || (ldc % 4)) return (int)hipErrorInvalidValue;
+  if ((lda % 8) || (ldw % 8) || lda < K || ldw < K || aplane < (long long)M * lda || wplane < (long long)N * ldw)
+    return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)Ap) | ((uintptr_t)Wp) | ((uintptr_t)C)) & 15) return (int)hipErrorInvalidValue;
+  if ((!rinv && !(rconst > 0.f)) || !csc || ((epi & EPI_BIAS) && !bias) || ((epi & EPI_RESID) && (!R || ldr < N)) ||
+      (epi & (EPI_BIAS_ROW | EPI_RESID_PRE)))
+    return (int)hipErrorInvalidValue;
+  if (!P || !rinv_out || ldp < N || (ldp % 4) || pplane < (long long)M * ldp || (((uintptr_t)P) & 7) || !(eps >= 0.f) ||
+      eln < -126 || eln > 126)
+    return (int)hipErrorInvalidValue;
+  LnOut lo;
+  lo.p = static_cast<_Float16*>(P);
+  lo.pplane = pplane;
+  lo.ldp = ldp;
+  lo.rinv = rinv_out;
+  lo.eps = eps;
+  lo.eln = eln;
+  constexpr int BM = 128, BN = 128;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  constexpr size_t lds = 2 * (size_t)(2 * BM * 32 * 2 + 2 * BN * 32 * 2);
+  hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, 2, 2, false, 32, 2, true>), dim3((unsigned)tiles_m), dim3(256), lds,
+                     stream, static_cast<const _Float16*>(Ap), lda, aplane, rinv, rconst,
+                     static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
+                     tiles_n, KvOut{}, PlaneOut{}, Batch{}, lo);
+  return (int)hipGetLastError();
 }

@@ -164,7 +164,9 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
             "gemm_f32": env.get("NOS_AMD_GEMM_F32_POLICY") or gf,
             "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or ("h3" if whole else "h3n"),
             "f32_math": env.get("NOS_AMD_F32_MATH") or "h3",
-            "gemm_f32x6_tile": env.get("NOS_AMD_X6_TILE") or ("policy" if whole else "128x128")}
+            "gemm_f32x6_tile": env.get("NOS_AMD_X6_TILE") or ("policy" if whole else "128x128"),
+            # pre-LN residual GEMMs hand the next LN-GEMM its planes (ops.set_ln_handoff)
+            "ln_handoff": env.get("NOS_AMD_LN_HANDOFF") or ("off" if whole else "on")}
 
 
 def slice_cu_budget(env: dict | None = None) -> int:
@@ -224,9 +226,16 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             # graph + weights, built with numpy: this process never imports
             # torch or opens the GPU), then infer through it
             from ..podserver.client import PodClient
-            from .yolos_program import demo_tenant
 
-            program, weights = demo_tenant(dtype, seed, small=device == "cuda")
+            prefix = os.environ.get("NOS_AMD_POD_PROGRAM")
+            if prefix:  # a prebuilt program (a conv net, a decoder LLM, ...): save_program's files
+                from ..podserver.program import load_program
+
+                program, weights = load_program(prefix)
+            else:
+                from .yolos_program import demo_tenant
+
+                program, weights = demo_tenant(dtype, seed, small=device == "cuda")
             client = PodClient.from_env(reconnect_s=float(os.environ.get("NOS_AMD_POD_RECONNECT_S", "0")))
             rep = client.register(f"pod-{slot}", program, weights)
             s = t = _ServerTenant(client)
@@ -234,6 +243,7 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
                 t.launch()
             srv = rep.get("server") or {}
             info = {"slot": slot, "pid": os.getpid(), "dtype": dtype, "graphs": graphs, "memory_fraction": None,
+                    "program": rep.get("program"),
                     "device": srv.get("device"), "multiprocessor_count": srv.get("multiprocessor_count"),
                     "cu_mask": os.environ.get(C.ENV_POD_CU_MASK), "cu_budget": 0,
                     "kernel_config": srv.get("kernel_config"), "hip_visible_devices": None,

@@ -62,8 +62,19 @@ def attention_ref(q, k, v, scale=None):
 # ---------------------------------------------------------------- dispatchers
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            act: str | None = None, residual: torch.Tensor | None = None,
-           out: torch.Tensor | None = None, max_wg: int = 0) -> torch.Tensor:
-    """y = act(x @ weight^T + bias) + residual; x [..., K], weight [N, K]."""
+           out: torch.Tensor | None = None, max_wg: int = 0, ln_eps: float | None = None):
+    """y = act(x @ weight^T + bias) + residual; x [..., K], weight [N, K].
+    ``ln_eps`` (fp32 under h3 math): also return y's LayerNorm-normalised
+    planes for the next LN-GEMM, ``(y, H3Planes)`` (:func:`linear_planes`)."""
+    if ln_eps is not None:
+        if not (x.is_cuda and x.dtype == torch.float32 and _F32_MATH == "h3"):
+            raise ValueError("ln_eps needs an fp32 CUDA input under h3 math")
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if x2.stride(-1) != 1 or K % 32:
+            raise ValueError("ln_eps needs unit inner stride and K % 32 == 0")
+        ap, rinv = _split_rows_h3(x2, ln=False)
+        return linear_planes(H3Planes(ap, rinv, 0.0, tuple(x.shape)), weight, bias, act, residual, ln_eps=ln_eps)
     if not x.is_cuda:
         return linear_ref(x, weight, bias, act, residual)
     K = x.shape[-1]
@@ -260,9 +271,11 @@ def _h3_out_scale(wg: torch.Tensor, c2: torch.Tensor, act: str | None) -> float:
 
 
 def linear_planes(a: H3Planes, weight: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
-                  residual: torch.Tensor | None = None) -> torch.Tensor:
+                  residual: torch.Tensor | None = None, ln_eps: float | None = None):
     """act(A @ weight^T + bias) + residual for an A handed over as h3 planes
-    (see :class:`H3Planes`): no split pre-pass, no fp32 round trip of A."""
+    (see :class:`H3Planes`): no split pre-pass, no fp32 round trip of A.
+    ``ln_eps``: also return the output LayerNorm-normalised as the next
+    LN-GEMM's planes (:func:`_gemm_h3_ln_out`) -- ``(out, H3Planes)``."""
     M, K = a.planes.shape[1], a.planes.shape[2]
     N = weight.shape[0]
     if weight.dim() != 2 or weight.shape[1] != K or weight.dtype != torch.float32 or weight.stride(-1) != 1:
@@ -275,12 +288,49 @@ def linear_planes(a: H3Planes, weight: torch.Tensor, bias: torch.Tensor | None =
             raise ValueError(f"residual must be fp32 [{M}, {N}]")
         r2 = residual.reshape(M, N)
         _check_f32(residual=r2)
+    if ln_eps is not None:
+        lnp = _gemm_h3_ln_out(a.planes, a.rinv, a.rconst, weight, bias, r2, out, _epi(bias, act, residual), ln_eps)
+        return out.view(*a.shape[:-1], N), H3Planes(lnp[0], lnp[1], 0.0, (*a.shape[:-1], N))
     _gemm_h3(a.planes, a.rinv, weight, bias, r2, out, _epi(bias, act, residual), rconst=a.rconst)
     return out.view(*a.shape[:-1], N)
 
 
+def _gemm_h3_ln_out(ap, rinv, rconst: float, weight, bias, r2, o2, epi: int, eps: float):
+    """:func:`_gemm_h3` whose workgroups also split their finished rows of
+    ``o2`` LayerNorm-normalised into the next GEMM's A planes
+    (``nos_gemm_f32h3_ln_out``): returns (planes [2, M, N], rinv [M])."""
+    M, K = ap.shape[1], ap.shape[2]
+    N = weight.shape[0]
+    wp, csc = split_f32_weight_h3(weight)
+    planes = torch.empty((2, M, N), dtype=torch.float16, device=o2.device)
+    rin = torch.empty((M,), dtype=torch.float32, device=o2.device)
+    eln = 14 - math.frexp(math.sqrt(N))[1]
+    rc = _lib.lib().nos_gemm_f32h3_ln_out(ap.data_ptr(), K, M * K, _ptr(rinv), float(rconst), wp.data_ptr(), K, N * K,
+                                          csc.data_ptr(), _ptr(bias), _ptr(r2), r2.stride(0) if r2 is not None else 0,
+                                          o2.data_ptr(), o2.stride(0), M, N, K, epi, planes.data_ptr(), N, M * N,
+                                          rin.data_ptr(), float(eps), eln, _stream())
+    _lib.check(rc, "nos_gemm_f32h3_ln_out")
+    return planes, rin
+
+
+_LN_HANDOFF = False
+
+
+def set_ln_handoff(on: bool) -> None:
+    """Pre-LN residual GEMMs hand the next LN-GEMM its LayerNorm-normalised
+    A planes from their own workgroups (``nos_gemm_f32h3_ln_out``: no
+    ``nos_split_rows_h3`` launch) -- the fractional-pod config; a whole-GPU
+    tenant keeps the separate pass (the row-owning grid is 3x smaller)."""
+    global _LN_HANDOFF
+    _LN_HANDOFF = bool(on)
+
+
+def ln_handoff_active() -> bool:
+    return _LN_HANDOFF and _F32_MATH == "h3"
+
+
 def linear_ln_to_planes(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor,
-                        act: str | None = None, eps: float = 1e-12) -> H3Planes:
+                        act: str | None = None, eps: float = 1e-12, pre: H3Planes | None = None) -> H3Planes:
     """:func:`linear_ln` under h3 math whose output goes straight to the next
     GEMM's A planes on the static scale of :func:`_h3_out_scale` (fc1 -> fc2)."""
     if _F32_MATH != "h3" or not x.is_cuda or x.dtype != torch.float32:
@@ -292,7 +342,7 @@ def linear_ln_to_planes(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2:
     if K % 32:
         raise ValueError("linear_ln_to_planes needs K % 32 == 0")
     M = x2.shape[0]
-    ap, rinv = _split_rows_h3(x2, ln=True, eps=eps)
+    ap, rinv = (pre.planes, pre.rinv) if pre is not None else _split_rows_h3(x2, ln=True, eps=eps)
     sc = _h3_out_scale(wg, c2, act)
     planes = torch.empty((2, M, N), dtype=torch.float16, device=x.device)
     _gemm_h3(ap, rinv, wg, c2, None, None, EPI_BIAS | _epi(None, act, None), planes_out=(planes, sc))
@@ -501,8 +551,10 @@ def linear_ln_ref(x, wg, c1, c2, act=None, eps=1e-12):
 
 
 def linear_ln(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, act: str | None = None,
-              eps: float = 1e-12, out: torch.Tensor | None = None, max_wg: int = 0) -> torch.Tensor:
-    """act(LayerNorm(x) @ W^T + b) with LN folded by :func:`fold_layernorm`."""
+              eps: float = 1e-12, out: torch.Tensor | None = None, max_wg: int = 0,
+              pre: H3Planes | None = None) -> torch.Tensor:
+    """act(LayerNorm(x) @ W^T + b) with LN folded by :func:`fold_layernorm`
+    (``pre``: x's LN-normalised planes, already made by its producer)."""
     if not x.is_cuda:
         return linear_ln_ref(x, wg, c1, c2, act, eps)
     K = x.shape[-1]
@@ -515,7 +567,7 @@ def linear_ln(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Ten
             raise ValueError("native fp32 linear_ln needs K % 32 == 0")
         o2, _ = _gemm_io(x, wg, out, None, M, N, K)
         if _F32_MATH == "h3":
-            ap, rinv = _split_rows_h3(x2, ln=True, eps=eps)
+            ap, rinv = (pre.planes, pre.rinv) if pre is not None else _split_rows_h3(x2, ln=True, eps=eps)
             _gemm_h3(ap, rinv, wg, c2, None, o2, EPI_BIAS | _epi(None, act, None))
         elif _F32_MATH == "x6":
             wp = split_f32_weight(wg)
@@ -706,7 +758,7 @@ _H3_SCALES_HOST: dict[int, torch.Tensor] = {}
 
 
 def linear_ln_qkv_h3(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, num_heads: int,
-                     eps: float = 1e-12) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+                     eps: float = 1e-12, pre: H3Planes | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """:func:`linear_ln_qkv_x6` writing the fp16x3 attention's planes (K and V
     as fp16 hi / lo pieces on the per-head scales of :func:`h3_head_scales`):
     returns (qkv with valid Q columns, workspace, scales) for
@@ -727,7 +779,7 @@ def linear_ln_qkv_h3(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: to
     skvp = (S + 31) // 32 * 32
     sc = h3_head_scales(wg, c2, num_heads)
     if _F32_MATH == "h3":
-        ap, rinv = _split_rows_h3(x2, ln=True, eps=eps)
+        ap, rinv = (pre.planes, pre.rinv) if pre is not None else _split_rows_h3(x2, ln=True, eps=eps)
         _gemm_h3(ap, rinv, wg, c2, None, out.view(M, N), EPI_BIAS, kv=(ws, S, skvp, sc))
         return out, ws, sc
     wp = split_f32_weight(wg)
@@ -779,14 +831,14 @@ def ln_qkv_fusable(x: torch.Tensor) -> bool:
 
 
 def ln_qkv_attention(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, num_heads: int,
-                     eps: float = 1e-12, planes_out: bool = False):
+                     eps: float = 1e-12, planes_out: bool = False, pre: H3Planes | None = None):
     """attention(LayerNorm(x) @ W_qkv^T + b) for an fp32 pod (see
     :func:`ln_qkv_fusable`): the QKV projection writes the attention's K / V
     planes straight from its epilogue -- fp16x3 planes under an ``h3``
     variant, bf16x6 planes otherwise.  ``planes_out`` (h3 variant only):
     the output as the proj GEMM's :class:`H3Planes`."""
     if _ATTN_F32_VARIANT.startswith("h3"):
-        qkv, ws, sc = linear_ln_qkv_h3(x, wg, c1, c2, num_heads, eps=eps)
+        qkv, ws, sc = linear_ln_qkv_h3(x, wg, c1, c2, num_heads, eps=eps, pre=pre)
         osc = float(_H3_SCALES_HOST[id(wg)][1].min()) if planes_out else None
         return attention_presplit_h3(qkv, ws, sc, num_heads, planes_out=osc)
     if _F32_MATH == "h3":  # x6 attention after an h3 projection: the unfused pair
@@ -819,5 +871,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "H3Planes", "set_attention_f32h3_waves", "linear_planes", "linear_ln_to_planes", "h3_planes_active", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_ln_handoff", "ln_handoff_active", "set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "H3Planes", "set_attention_f32h3_waves", "linear_planes", "linear_ln_to_planes", "h3_planes_active", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

@@ -96,6 +96,9 @@ _SIGS = {
     "nos_im2col_h3": [c_void_p, c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nos_attn_h3g_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
+    "nos_gemm_f32h3_ln_out": [c_void_p, c_int, c_ll, c_void_p, c_float, c_void_p, c_int, c_ll, c_void_p, c_void_p,
+                              c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_ll,
+                              c_void_p, c_float, c_int, c_void_p],
     "nos_attn_h3g_set_kvsplit": [c_int],
     "nos_attn_h3g": [c_void_p, c_int, c_ll, c_void_p, c_int, c_ll, c_void_p, c_int, c_ll, c_void_p, c_int, c_ll,
                      c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_float, c_void_p,

@@ -331,7 +331,8 @@ class PodFleet:
             info = {k: r.get(k) for k in ("pid", "multiprocessor_count", "cu_mask", "hip_visible_devices",
                                            "memory_limit_gb", "memory_fraction", "max_allocated_gb", "cu_budget",
                                            "kind", "world_size", "backend", "flops_per_step", "bucket_bytes",
-                                           "buckets", "bucket_busbw_gbps", "launched_in_backward", "kernel_config")}
+                                           "buckets", "bucket_busbw_gbps", "launched_in_backward", "kernel_config",
+                                           "program")}
             info["kind"] = kind
             out.append(PodResult(i, c, (w / c) if c > 0 else None, gap, running, info))
         return WindowStats(w, out)

@@ -817,6 +817,7 @@ class CompiledProgram:
             steps = self._fuse_qkv_attention(steps)
             steps = self._fuse_rotary_sdpa(steps)
             steps = self._mark_plane_handoffs(steps)
+            steps = self._mark_ln_handoffs(steps)
             self._prep_conv_weights(steps)
             self.steps = self._plan_releases(steps)
             used = {i for s in self.steps for i in s.inputs} | set(self.outputs)
@@ -1132,6 +1133,29 @@ class CompiledProgram:
         self.stats["plane_handoffs"] = n
         return steps
 
+    def _mark_ln_handoffs(self, steps: list[_Step]) -> list[_Step]:
+        """A pre-LN residual GEMM (fp32 linear + residual) whose output the next
+        LN-GEMM (``linear_ln`` / ``ln_qkv_attention``) normalises may, under h3
+        math with ``ops.set_ln_handoff``, hand over that LN's A planes from its
+        own workgroups (``nos_gemm_f32h3_ln_out``): marked here with the
+        consumer's eps, decided per run."""
+        by_out = {s.output: s for s in steps}
+        eps_of: dict[str, set] = {}
+        for s in steps:
+            if s.kind in ("linear_ln", "ln_qkv_attention") and s.inputs[0] in by_out:
+                eps_of.setdefault(s.inputs[0], set()).add(s.attrs.get("eps", 1e-12))
+        n = 0
+        for name, eps in eps_of.items():
+            p = by_out[name]
+            if (p.kind == "linear" and p.attrs.get("residual") and len(eps) == 1 and self._dtype(name) == "fp32"
+                    and self._shape(name)[-1] % 4 == 0 and sum(1 for s in steps if s.kind in
+                                                              ("linear_ln", "ln_qkv_attention")
+                                                              and s.inputs[0] == name) == 1):
+                p.attrs["ln_out"] = next(iter(eps))
+                n += 1
+        self.stats["ln_handoffs"] = n
+        return steps
+
     def _plan_releases(self, steps: list[_Step]) -> list[_Step]:
         last: dict[str, int] = {}
         for k, s in enumerate(steps):
@@ -1163,25 +1187,34 @@ class CompiledProgram:
             k = s.kind
             if k == "linear":
                 res = a.pop() if s.attrs.get("residual") else None
+                ln_eps = s.attrs.get("ln_out")
+                if ln_eps is not None and not (ops.ln_handoff_active() and (isinstance(a[0], ops.H3Planes) or (
+                        a[0].is_cuda and a[0].dtype.itemsize == 4))):
+                    ln_eps = None
                 if isinstance(a[0], ops.H3Planes):
                     y = ops.linear_planes(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
-                                          residual=res)
+                                          residual=res, ln_eps=ln_eps)
                 else:
                     y = ops.linear(a[0].contiguous(), a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
-                                   residual=res)
+                                   residual=res, ln_eps=ln_eps)
+                if ln_eps is not None:
+                    y, env[s.output + "::lnp"] = y
             elif k == "linear_ln":
                 xx = a[0].contiguous()
+                pre = env.pop(s.inputs[0] + "::lnp", None)  # its producer's LN planes (_mark_ln_handoffs)
                 if (s.attrs.get("planes_out") and xx.is_cuda and xx.dtype.itemsize == 4
                         and ops.h3_planes_active()):
-                    y = ops.linear_ln_to_planes(xx, a[1], a[2], a[3], act=s.attrs.get("act"), eps=s.attrs["eps"])
+                    y = ops.linear_ln_to_planes(xx, a[1], a[2], a[3], act=s.attrs.get("act"), eps=s.attrs["eps"],
+                                                pre=pre)
                 else:
-                    y = ops.linear_ln(xx, a[1], a[2], a[3], act=s.attrs.get("act"), eps=s.attrs["eps"])
+                    y = ops.linear_ln(xx, a[1], a[2], a[3], act=s.attrs.get("act"), eps=s.attrs["eps"], pre=pre)
             elif k == "ln_qkv_attention":
                 h = a[0].contiguous()
+                pre = env.pop(s.inputs[0] + "::lnp", None)
                 if ops.ln_qkv_fusable(h):
                     y = ops.ln_qkv_attention(h, a[1], a[2], a[3], s.attrs["heads"], eps=s.attrs["eps"],
                                              planes_out=bool(s.attrs.get("planes_out"))
-                                             and ops.h3_planes_active(attention=True))
+                                             and ops.h3_planes_active(attention=True), pre=pre)
                 else:
                     qkv = ops.linear_ln(h, a[1], a[2], a[3], eps=s.attrs["eps"])
                     y = ops.attention_qkv(qkv, s.attrs["heads"])
@@ -1275,6 +1308,27 @@ class Builder:
                  "nodes": self.nodes, "outputs": list(outputs)}, b"".join(self.chunks))
 
 
+def save_program(prefix: str, program: dict, weights: bytes) -> None:
+    """A built program as ``<prefix>.json`` + ``<prefix>.bin`` (a tenant
+    builds once -- e.g. with torch.fx -- and its pods ship the files)."""
+    import json
+
+    with open(prefix + ".json", "w") as f:
+        json.dump(program, f)
+    with open(prefix + ".bin", "wb") as f:
+        f.write(weights)
+
+
+def load_program(prefix: str) -> tuple[dict, bytes]:
+    """:func:`save_program`'s files back (JSON + raw bytes: nothing executable)."""
+    import json
+
+    with open(prefix + ".json") as f:
+        program = json.load(f)
+    with open(prefix + ".bin", "rb") as f:
+        return program, f.read()
+
+
 def mlp_program(dim: int = 1024, layers: int = 4, batch: int = 256, dtype: str = "bf16", seed: int = 0,
                 hidden: int | None = None) -> tuple[dict, bytes]:
     """The GEMM-MLP probe tenant (BASELINE config 4's workload): ``layers``
@@ -1300,4 +1354,5 @@ def mlp_program(dim: int = 1024, layers: int = 4, batch: int = 256, dtype: str =
 
 
 __all__ = ["FORMAT", "Program", "CompiledProgram", "ProgramError", "Builder", "parse", "mlp_program", "bf16_bits",
+           "save_program", "load_program",
            "bf16_to_f32", "OPS", "torch_dtype"]

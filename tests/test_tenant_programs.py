@@ -1,0 +1,156 @@
+"""General pod-server tenants on the CPU: a torch.nn conv net (exported with
+torch.fx) and a ``transformers`` Llama decoder as programs, compiled by the
+server's graph compiler and co-hosted with YOLOS in one pod server.  Each is
+compared with its own torch fp32 module.  GPU runs (gfx950 kernels, fp64
+references): tests/test_tenant_programs_gpu.py."""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from nos_amd.models.llama_program import llama_config, llama_model, llama_program
+from nos_amd.models.resnet import resnet_tenant, resnet_tiny
+from nos_amd.models.yolos_program import demo_tenant
+from nos_amd.podserver import program as PG
+from nos_amd.podserver.client import PodClient, PodServerError
+from nos_amd.podserver.export import ExportError, export
+from nos_amd.podserver.server import PodServer
+
+
+@pytest.fixture(scope="module")
+def llama():
+    m = llama_model(llama_config(False), 0)
+    return m, llama_program(m, 64)
+
+
+def test_resnet_program_matches_the_module():
+    prog, w = resnet_tenant("fp32", 0, small=False)
+    p = PG.parse(prog, w, gpu=True)
+    cm = p.compile("cpu")
+    # every conv + BN (+ residual) (+ ReLU) is one kernel step
+    assert cm.stats["batchnorm_folded"] == 6 and cm.stats["residual_fused"] == 2 and cm.stats["activation_fused"] == 5
+    assert sum(1 for s in cm.steps if s.kind == "conv2d") == 6
+    x = torch.randn(1, 3, 32, 32)
+    with torch.no_grad():
+        ref = resnet_tiny(0)(x)
+    assert torch.allclose(cm(x)[0], ref, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(p.reference(x)[0], ref, atol=1e-5, rtol=1e-5)
+
+
+def test_llama_program_matches_hf(llama):
+    m, (prog, w) = llama
+    p = PG.parse(prog, w, gpu=True)
+    cm = p.compile("cpu")
+    L = m.config.num_hidden_layers
+    assert cm.stats["linears_merged"] == 5 * L            # q / k / v and gate / up
+    assert cm.stats["rmsnorm_folded"] == 2 * L + 1 and cm.stats["rotary_fused"] == L
+    assert cm.stats["residual_fused"] == 2 * L
+    ids = torch.randint(0, m.config.vocab_size, (1, 64))
+    with torch.no_grad():
+        ref = m(ids).logits
+    assert torch.allclose(cm(ids.int())[0], ref, atol=2e-5, rtol=1e-5)
+    assert torch.allclose(p.reference(ids.int())[0], ref, atol=2e-5, rtol=1e-5)
+    assert p.id_bound() == m.config.vocab_size
+
+
+def test_llama_bf16_program_tracks_the_fp32_module(llama):
+    m, _ = llama
+    prog, w = llama_program(m, 64, dtype="bf16")
+    cm = PG.parse(prog, w, gpu=True).compile("cpu")
+    ids = torch.randint(0, m.config.vocab_size, (1, 64))
+    with torch.no_grad():
+        ref = m(ids).logits
+    out = cm(ids.int())[0].float()
+    assert (out - ref).abs().max() < 0.05 * ref.abs().max()
+
+
+def test_export_refuses_what_a_program_cannot_express():
+    class Grouped(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.c = nn.Conv2d(8, 8, 3, groups=8)
+
+        def forward(self, x):
+            return self.c(x)
+
+    with pytest.raises(ExportError, match="groups"):
+        export(Grouped(), torch.zeros(1, 8, 8, 8))
+
+    class Odd(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.e = nn.Embedding(10, 4)
+
+        def forward(self, x):
+            return self.e(x)
+
+    with pytest.raises(ExportError, match="Embedding"):
+        export(Odd(), torch.zeros(1, 3, dtype=torch.long))
+
+
+@pytest.mark.parametrize("node,match", [
+    ({"op": "conv2d", "inputs": ["x", "w4"], "output": "y", "attrs": {"groups": 2}}, "groups = 1"),
+    ({"op": "softmax", "inputs": ["x"], "output": "y", "attrs": {"dim": 0}}, "last dim"),
+    ({"op": "sdpa", "inputs": ["q32", "q32", "q32"], "output": "y"}, "head_dim 64 or 128"),
+    ({"op": "embedding", "inputs": ["x", "w2"], "output": "y"}, "ids must be i32"),
+    ({"op": "rotary", "inputs": ["q32", "w2", "w2"], "output": "y"}, "cos / sin"),
+    ({"op": "matmul", "inputs": ["x", "w4"], "output": "y"}, r"\[\.\.\., M, K\]"),
+])
+def test_new_ops_are_validated_at_parse_time(node, match):
+    b = PG.Builder("bad")
+    b.input("x", [1, 4, 6, 6])
+    b.param("w4", np.zeros((4, 4, 3, 3), np.float32))
+    b.param("w2", np.zeros((4, 4), np.float32))
+    b.param("q32", np.zeros((1, 8, 2, 32), np.float32))
+    prog, w = b.build(["x"])
+    prog["nodes"].append(node)
+    prog["outputs"] = [node["output"]]
+    with pytest.raises(PG.ProgramError, match=match):
+        PG.parse(prog, w, gpu=True)
+
+
+def test_one_pod_server_cohosts_yolos_a_conv_net_and_a_decoder(tmp_path, llama):
+    """The MPS-client analogue beyond ViT encoders: three model families in
+    one server process, each replying with its own module's outputs."""
+    m, lprog = llama
+    srv = PodServer(tmp_path / "s.sock", device="cpu", lanes=2, memory_gb=40).start()
+    try:
+        clients = {}
+        for name, prog in (("yolos", demo_tenant("fp32", 0, small=False)),
+                           ("resnet", resnet_tenant("fp32", 0, small=False)), ("llama", lprog)):
+            c = clients[name] = PodClient(srv.path, connect_timeout_s=5)
+            rep = c.register(name, *prog, memory_limit_gb=2)
+            assert rep["compile"]["kernels"] > 0
+        assert len(srv.tenants) == 3
+        x = np.random.default_rng(0).standard_normal((1, 3, 32, 32)).astype(np.float32)
+        out, _ = clients["resnet"].infer(x, outputs=True)
+        with torch.no_grad():
+            ref = resnet_tiny(0)(torch.from_numpy(x)).numpy()
+        np.testing.assert_allclose(out[0], ref, atol=1e-5, rtol=1e-5)
+        ids = np.random.default_rng(1).integers(0, m.config.vocab_size, (1, 64)).astype(np.int32)
+        out, _ = clients["llama"].infer(ids, outputs=True)
+        with torch.no_grad():
+            ref = m(torch.from_numpy(ids).long()).logits.numpy()
+        np.testing.assert_allclose(out[0], ref, atol=2e-5, rtol=1e-5)
+        with pytest.raises(PodServerError, match="token ids must lie"):
+            clients["llama"].infer(np.full((1, 64), m.config.vocab_size, np.int32))
+        clients["yolos"].infer()
+        for c in clients.values():
+            c.close()
+    finally:
+        srv.stop()
+
+
+def test_estimate_counts_the_new_ops_workspaces(llama):
+    _, (prog, w) = llama
+    p = PG.parse(prog, w, gpu=True)
+    q = copy.deepcopy(prog)
+    for n in q["nodes"]:
+        if n["op"] == "sdpa":
+            n["op"], n["inputs"], n["attrs"] = "add", n["inputs"][:2], {}
+    # same graph with the attention replaced by an elementwise op: the attention workspace is gone
+    assert p.bytes_estimate > PG.parse(q, w).bytes_estimate
