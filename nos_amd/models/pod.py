@@ -237,7 +237,7 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
 
                 program, weights = demo_tenant(dtype, seed, small=device == "cuda")
             client = PodClient.from_env(reconnect_s=float(os.environ.get("NOS_AMD_POD_RECONNECT_S", "0")))
-            rep = client.register(f"pod-{slot}", program, weights)
+            rep = client.register(os.environ.get("NOS_AMD_POD_NAME") or f"pod-{slot}", program, weights)
             s = t = _ServerTenant(client)
             for _ in range(warmup):
                 t.launch()

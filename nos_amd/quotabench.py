@@ -101,9 +101,11 @@ class ProcessRuntime(RecordingRuntime):
     board).  Stopping a tenant sets its board's stop flag (graceful: the pod
     closes its pod-server connection) and kills it after ``grace_s``."""
 
-    def __init__(self, launcher, workdir: str, dtype: str = "fp32", device: str = "cuda", grace_s: float = 10.0):
+    def __init__(self, launcher, workdir: str, dtype: str = "fp32", device: str = "cuda", grace_s: float = 10.0,
+                 extra_env: dict | None = None):
         super().__init__()
         self.launcher, self.dir, self.dtype, self.device, self.grace = launcher, Path(workdir), dtype, device, grace_s
+        self.extra_env = dict(extra_env or {})   # e.g. NOS_AMD_POD_DUTY for bursty tenants
         self._n = 0
 
     def start(self, key: str, env: dict) -> None:
@@ -116,10 +118,18 @@ class ProcessRuntime(RecordingRuntime):
         board = StatusBoard(d / "status.bin", pods=1)
         penv = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE",
                                                                  "HIP_VISIBLE_DEVICES", "ROC_GLOBAL_CU_MASK")}
+        trainer = env.get("NOS_AMD_POD_KIND") == "trainer"
+        if not trainer:
+            penv.update(self.extra_env)
         penv.update({k: str(v) for k, v in env.items()})
         penv["PYTHONPATH"] = str(REPO) + os.pathsep + penv.get("PYTHONPATH", "")
-        cmd = [sys.executable, "-u", "-m", "nos_amd.models.pod", "--status", str(board.path), "--slot", "0",
-               "--out", str(d), "--dtype", self.dtype, "--seed", str(self._n), "--device", self.device]
+        penv["NOS_AMD_POD_NAME"] = key  # the server's tenant name: footprints map back to pods
+        if trainer:  # the DP trainer tenant: its own GPU process (models/trainer_pod.py)
+            cmd = [sys.executable, "-u", "-m", "nos_amd.models.trainer_pod", "--status", str(board.path), "--slot",
+                   "0", "--out", str(d), "--device", self.device]
+        else:
+            cmd = [sys.executable, "-u", "-m", "nos_amd.models.pod", "--status", str(board.path), "--slot", "0",
+                   "--out", str(d), "--dtype", self.dtype, "--seed", str(self._n), "--device", self.device]
         proc = self.launcher.spawn(cmd, penv, str(d / "pod.err"), str(REPO))
         with self.lock:
             self.tenants[key] = Tenant(key, env, time.monotonic(), handle=(proc, board, d))
@@ -339,6 +349,175 @@ class QuotaScenario:
         return True
 
 
+@dataclass
+class ComposedScenario(QuotaScenario):
+    """BASELINE config 5 as ONE scenario: "ElasticQuota +
+    dynamic partition + CU-mask under bursty synthetic PyTorch-ROCm/RCCL
+    tenants".  Two nodes under one control plane:
+
+    * ``mi355x-0`` (cumask, pod server per GPU): per GPU one DP trainer pod
+      (``training`` namespace, a 36 GB slice; its own GPU process running
+      forward / backward / RCCL all-reduce, models/trainer_pod.py), then
+      team-a's inference tenants arriving in ``waves`` bursts (each tenant
+      with a duty cycle, ``NOS_AMD_POD_DUTY``), borrowing team-b's quota;
+    * ``mi355x-part`` (amdpart, FakeSmi: the mode switch is SIMULATED -- the
+      pool has no root to switch an MI355X's compute mode): ``batch`` pods
+      requesting CPX partitions it does not have, so the partitioner plans a
+      repartition SPX -> CPX and the agent applies it;
+    * then team-b claims its min and CapacityScheduling preempts team-a's
+      over-quota tenants (the reference flows:
+      ``capacity_scheduling.go:468-675``, ``partitioner_controller.go:81-200``).
+
+    Reported per phase: GPU util, running tenants, quota ``status.used``
+    against the pod server's measured footprints (``footprint_gb`` sum of the
+    namespace's tenants), preemptions, and the repartition count and latency."""
+
+    trainers: bool = True
+    trainer_slice_gb: int = 36
+    waves: int = 3
+    wave_gap_s: float = 4.0
+    duty: str = "1.5:0.5"
+    part_gpus: int = 1
+    part_pods: int = 8
+    part_resource: str = "amd.com/partition-1xcd.36gb"
+    server_stats: object = None     # () -> pod-server stats (live runs), for the footprint comparison
+
+    def build(self, runtime):
+        from .gpu.fakesmi import FakeSmi
+
+        cl = super().build(runtime)
+        self.sim_runtime = RecordingRuntime()
+        self.part = cl.add_node("mi355x-part", C.PARTITIONING_AMDPART, gpus=self.part_gpus,
+                                smi=FakeSmi(gpus=self.part_gpus, node="mi355x-part"),
+                                runtime=lambda pod, conts: self.sim_runtime.start(ko.key(pod), {}),
+                                on_stop=lambda pod, conts: self.sim_runtime.stop(ko.key(pod)))
+        for ns in ("training", "batch"):
+            cl.api.create({"kind": "Namespace", "metadata": {"name": ns}})
+        self._settle(30)
+        return cl
+
+    def _start(self, pod: dict, conts) -> None:
+        env = {}
+        for rc in conts:
+            env.update(rc.envs)
+        if ko.labels(pod).get("nos.nebuly.com/tenant-kind") == "trainer":
+            # a GPU process of its own: the slice's GPU instead of the pod-server socket
+            sock = env.pop(C.ENV_POD_SERVER, "")
+            env.pop(C.ENV_POD_TOKEN, None)
+            gpu = sock.rsplit("gpu-", 1)[-1].split("/", 1)[0] if "gpu-" in sock else "0"
+            env.update({"HIP_VISIBLE_DEVICES": gpu, "NOS_AMD_POD_KIND": "trainer", "RANK": "0", "WORLD_SIZE": "1",
+                        "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(29600 + int(gpu)),
+                        "NOS_AMD_COLL_DIM": "2048", "NOS_AMD_COLL_BUCKET_MB": "32"})
+        key = ko.key(pod)
+        self.runtime.start(key, env)
+        self.events.append(("start", key, time.monotonic()))
+
+    def _phase_util(self, sampler, t0: float) -> float | None:
+        return sampler.mean(t0, time.monotonic())[0] if sampler is not None else None
+
+    def footprints(self) -> dict:
+        """Per namespace: the pod server's measured build footprints of its
+        tenants (GB), from the server's stats (live runs only)."""
+        if self.server_stats is None:
+            return {}
+        out: dict[str, float] = {}
+        try:
+            st = self.server_stats()
+        except Exception as e:  # reported, not fatal
+            return {"error": repr(e)}
+        for t in st.get("tenants", []):
+            ns = str(t.get("pod", "")).split("/", 1)[0]
+            out[ns] = round(out.get(ns, 0.0) + float(t.get("footprint_gb") or 0.0), 3)
+        return out
+
+    def quota_vs_footprint(self) -> dict:
+        fp = self.footprints()
+        snap = self.snapshot()
+        return {ns: {"status_used_gb": snap[ns]["status_used_gb"], "slice_gb_running": snap[ns]["tenant_gb"],
+                     "server_footprint_gb": fp.get(ns)} for ns in ("team-a", "team-b")}
+
+    def run(self, runtime, phase_timeout_s: float = 600.0, sampler=None) -> dict:
+        self.build(runtime)
+        res: dict = {"config": {"gpus": self.gpus, "slice_gb": self.slice_gb, "team_a_pods": self.team_a_pods,
+                                "team_b_pods": self.team_b_pods, "min_gb": self.min_gb, "max_gb": self.max_gb,
+                                "trainers": self.gpus if self.trainers else 0, "waves": self.waves,
+                                "duty": self.duty, "part_gpus": self.part_gpus, "part_pods": self.part_pods,
+                                "part_resource": self.part_resource,
+                                "part_switch": "simulated (FakeSmi; the pool cannot switch MI355X modes)"}}
+        # phase 0: one DP trainer pod per GPU of the pod-server node
+        t0 = time.monotonic()
+        tr = []
+        if self.trainers:
+            for g in range(self.gpus):
+                self.cl.submit_pod(f"trainer-{g}", {f"{C.AMD_SLICE_RESOURCE_PREFIX}{self.trainer_slice_gb}gb": 1},
+                                   namespace="training", labels={"nos.nebuly.com/tenant-kind": "trainer"})
+                tr.append(f"training/trainer-{g}")
+            ok = self.drive(lambda: set(tr) <= self.runtime.ready(), phase_timeout_s)
+            res["phase_trainers"] = {"ok": ok, "seconds": round(time.monotonic() - t0, 2), "trainers": len(tr),
+                                     "gpu_util_pct": self._phase_util(sampler, t0)}
+        # phase A: team-a in bursts, borrowing
+        t1 = time.monotonic()
+        a, per = [], -(-self.team_a_pods // self.waves)
+        for w in range(self.waves):
+            n = min(per, self.team_a_pods - len(a))
+            a += self.submit_range("team-a", len(a), n, "a")
+            if w + 1 < self.waves:
+                self.drive(lambda: False, self.wave_gap_s)   # the next burst arrives later
+        ok = self.drive(lambda: set(a) <= self.runtime.ready() and self._labels_settled(), phase_timeout_s)
+        res["phase_a"] = {"ok": ok, "seconds": round(time.monotonic() - t1, 2), **self.snapshot(),
+                          "gpu_util_pct": self._phase_util(sampler, t1), "quota_vs_footprint": self.quota_vs_footprint()}
+        # phase P: pending partition pods force a repartition of the amdpart node
+        tp = time.monotonic()
+        sw0, plans0 = self.part.smi.switches, self.cl.clock.now()
+        modes0 = list(self.part.smi.compute)
+        keys = []
+        for i in range(self.part_pods):
+            self.cl.submit_pod(f"p-{i}", {self.part_resource: 1}, namespace="batch")
+            keys.append(f"batch/p-{i}")
+        ok = self.drive(lambda: set(keys) <= self.sim_runtime.running(), phase_timeout_s)
+        res["phase_repartition"] = {"ok": ok, "submit_to_all_running_s": round(time.monotonic() - tp, 2),
+                                    "submit_to_all_running_sim_s": round(self.cl.clock.now() - plans0, 2),
+                                    "mode_switches": self.part.smi.switches - sw0, "modes_before": modes0,
+                                    "modes_after": list(self.part.smi.compute), "pods_running": len(
+                                        set(keys) & self.sim_runtime.running()),
+                                    "gpu_util_pct": self._phase_util(sampler, tp)}
+        # phase B: team-b claims its min, preempting team-a's borrowed tenants
+        b_res = self._phase_b(phase_timeout_s, sampler)
+        res["phase_b"] = {**b_res, "quota_vs_footprint": self.quota_vs_footprint()}
+        res["concurrent_tenants"] = len(self.runtime.running())
+        return res
+
+    def submit_range(self, ns: str, start: int, n: int, prefix: str) -> list[str]:
+        keys = []
+        for i in range(start, start + n):
+            self.cl.submit_pod(f"{prefix}-{i}", {f"{C.AMD_SLICE_RESOURCE_PREFIX}{self.slice_gb}gb": 1}, namespace=ns)
+            keys.append(f"{ns}/{prefix}-{i}")
+        return keys
+
+    def _phase_b(self, phase_timeout_s: float, sampler) -> dict:
+        t1 = time.monotonic()
+        over_a = {k for k, v in self.labels("team-a").items() if v == "over-quota"}
+        p0 = self.cl.scheduler.stats.get("preemptions", 0)
+        b = self.submit_range("team-b", 0, self.team_b_pods, "b")
+        ok = self.drive(lambda: set(b) <= self.runtime.ready() and self._labels_settled(), phase_timeout_s)
+        stops = [k for kind, k, t in self.events if kind == "stop" and t >= t1]
+        return {"ok": ok, "seconds": round(time.monotonic() - t1, 2),
+                "preemptions": self.cl.scheduler.stats.get("preemptions", 0) - p0, "victims": len(stops),
+                "victims_over_quota_only": set(stops) <= over_a, **self.snapshot(),
+                "gpu_util_pct": self._phase_util(sampler, t1)}
+
+
+def composed_for(gpus: int, tenant_slots_per_gpu: int = 25, slice_gb: int = 10, **kw) -> ComposedScenario:
+    """A node of ``gpus`` GPUs, each holding one 36 GB trainer slice and
+    ``tenant_slots_per_gpu`` 10 GB tenant slices: team-a borrows to 5/7 of
+    the tenant slots, team-b then claims its half."""
+    slots = gpus * tenant_slots_per_gpu
+    half = slots // 2
+    return ComposedScenario(gpus=gpus, slice_gb=slice_gb, team_a_pods=max(half + 1, round(slots * 5 / 7)),
+                            team_b_pods=half, min_gb=half * slice_gb, max_gb=slots * slice_gb,
+                            tenants_per_gpu=tenant_slots_per_gpu + 1, **kw)
+
+
 def _stats(v: list[float]) -> dict:
     v = sorted(v)
     return {"n": len(v), "p50": round(v[len(v) // 2], 3) if v else None, "max": round(v[-1], 3) if v else None}
@@ -364,4 +543,5 @@ def run_cpu_rehearsal(tmp: str | None = None, **kw) -> dict:
             shutil.rmtree(d, ignore_errors=True)
 
 
-__all__ = ["QuotaScenario", "RecordingRuntime", "ProcessRuntime", "run_cpu_rehearsal"]
+__all__ = ["QuotaScenario", "ComposedScenario", "composed_for", "RecordingRuntime", "ProcessRuntime",
+           "run_cpu_rehearsal"]

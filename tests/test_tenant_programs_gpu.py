@@ -76,7 +76,8 @@ def test_gpu_pod_server_cohosts_three_model_families(tmp_path):
             c = clients[name] = PodClient(srv.path, connect_timeout_s=30)
             rep = c.register(name, prog, w, memory_limit_gb=4)
             est = PG.parse(prog, w, gpu=True).bytes_estimate_for(srv.kernel_config) / 2 ** 30
-            assert rep["footprint_gb"] <= est, (name, rep["footprint_gb"], est)
+            # (+16 MB: the caching allocator's per-allocation rounding of ~100 small tensors)
+            assert rep["footprint_gb"] <= est + 0.016, (name, rep["footprint_gb"], est)
         x = np.random.default_rng(0).standard_normal((1, 3, 224, 224)).astype(np.float32)
         ids = np.random.default_rng(1).integers(0, lm.config.vocab_size, (1, 64)).astype(np.int32)
         for _ in range(3):  # replays

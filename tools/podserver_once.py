@@ -19,6 +19,9 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
 
+_CACHE: dict = {}
+
+
 def make(kind: str, dtype: str, seed: int):
     """(program, weights) of one tenant kind."""
     from nos_amd.models.yolos_program import demo_tenant
@@ -33,6 +36,18 @@ def make(kind: str, dtype: str, seed: int):
         from nos_amd.podserver.program import mlp_program
 
         return mlp_program(dim=4096, layers=4, batch=256, dtype="bf16", seed=seed)
+    if kind == "resnet":  # ResNet-18 at 224x224 (torch.fx export), one program shared by the pods
+        if "resnet" not in _CACHE:
+            from nos_amd.models.resnet import resnet_tenant
+
+            _CACHE["resnet"] = resnet_tenant(dtype, 0)
+        return _CACHE["resnet"]
+    if kind == "llama":  # a random-init Llama decoder (1024 hidden, 8 layers, head_dim 128, GQA) at seq 512
+        if "llama" not in _CACHE:
+            from nos_amd.models.llama_program import llama_tenant
+
+            _CACHE["llama"] = llama_tenant(dtype, 0)
+        return _CACHE["llama"]
     raise SystemExit(f"unknown tenant kind {kind!r}")
 
 
@@ -50,7 +65,8 @@ def main() -> None:
     ap.add_argument("--h3-attn-waves", type=int, default=8, choices=[4, 8], help="h3 attention waves per workgroup")
     ap.add_argument("--mix", default="", help="heterogeneous tenants instead of --tenants YOLOS pods, e.g. "
                     "yolos:20,bert:4,mlp:4 (bert = BERT-base-shaped fp32 encoder at seq 512, mlp = bf16 GEMM-MLP "
-                    "probe); per-kind rates in the output")
+                    "probe, resnet = ResNet-18 at 224x224, llama = Llama decoder at seq 512); per-kind rates in "
+                    "the output")
     a = ap.parse_args()
     kinds = ([k for spec in a.mix.split(",") for k in [spec.split(":")[0]] * int(spec.split(":")[1])]
              if a.mix else ["yolos"] * a.tenants)
