@@ -152,11 +152,14 @@ __device__ __forceinline__ void ln_split_row(const float* __restrict__ x, int N,
 
 // BKT: K depth of an LDS stage (32: two 16-deep MFMA steps, or 16: one);
 // RS: stages in the ring (RS - 1 of them in flight ahead of the one computed)
-template <int BM, int BN, int WGM, int WGN, bool PERSIST, int BKT = 32, int RS = 2, bool ROWSPLIT = false>
+// BATCHED: the tile index spans nb batch elements (Batch strides); false: one
+// GEMM, no per-tile batch offsets (fewer live SGPRs in the hot path)
+template <int BM, int BN, int WGM, int WGN, bool PERSIST, int BKT = 32, int RS = 2, bool ROWSPLIT = false,
+          bool BATCHED = false>
 __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3_kernel(
     const _Float16* __restrict__ Ap, int lda, long long aplane, const float* __restrict__ rinv, float rconst,
     const _Float16* __restrict__ Wp, int ldw, long long wplane, const float* __restrict__ csc,
-    const float* __restrict__ bias, const float* __restrict__ R, int ldr, float* __restrict__ C, int ldc, int M,
+    const float* __restrict__ bias, const float* __restrict__ R, int ldr0, float* __restrict__ C, int ldc0, int M,
     int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv, PlaneOut po, Batch bt, LnOut lo) {
   constexpr int NW = WGM * WGN, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
   static_assert((NW == 4 || NW == 8) && MI >= 1 && NI >= 1, "4 or 8 waves");
@@ -170,9 +173,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int c = lane & 31, h = lane >> 5;
+  const int c0 = lane & 31, h0 = lane >> 5;
   const int wm = wid / WGN, wn = wid % WGN;
-  const int ntiles1 = tiles_m * tiles_n, ntiles = ntiles1 * bt.nb;
+  const int ntiles1 = tiles_m * tiles_n, ntiles = BATCHED ? ntiles1 * bt.nb : ntiles1;
   const int nk = K / BKT;
   nos::XcdChunk chunk;
   if constexpr (ROWSPLIT) {  // this workgroup's row block: its tiles_n tiles in order
@@ -188,16 +191,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   }
   for (int tt = chunk.first; tt < chunk.end; tt += chunk.step) {
     if ((PERSIST || ROWSPLIT) && tt != chunk.first) __syncthreads();
-    const int bb = tt / ntiles1, t1 = tt - bb * ntiles1;
+    const int bb = BATCHED ? tt / ntiles1 : 0, t1 = BATCHED ? tt - bb * ntiles1 : tt;
     const int tm = t1 / tiles_n, tn = t1 - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
     // this tile's batch element (wave-uniform scalar offsets)
-    const _Float16* __restrict__ Ab = Ap + bb * bt.a;
-    const _Float16* __restrict__ Wb = Wp + bb * bt.w;
-    const float* __restrict__ rinvb = rinv != nullptr ? rinv + bb * bt.rinv : nullptr;
-    const float* __restrict__ cscb = csc + bb * bt.csc;
-    float* __restrict__ Cb = C != nullptr ? C + bb * bt.c : nullptr;
-    const float* __restrict__ Rb = R != nullptr ? R + bb * bt.r : nullptr;
+    const _Float16* __restrict__ Ab = BATCHED ? Ap + bb * bt.a : Ap;
+    const _Float16* __restrict__ Wb = BATCHED ? Wp + bb * bt.w : Wp;
+    const float* __restrict__ rinvb = BATCHED && rinv != nullptr ? rinv + bb * bt.rinv : rinv;
+    const float* __restrict__ cscb = BATCHED ? csc + bb * bt.csc : csc;
+    float* __restrict__ Cb = BATCHED && C != nullptr ? C + bb * bt.c : C;
+    const float* __restrict__ Rb = BATCHED && R != nullptr ? R + bb * bt.r : R;
 
     // a 1 KiB piece = RPP rows x ROWB bytes of one plane; lane L: row L / CH, chunk L % CH
     auto stage = [&](int k0, unsigned char* dst) {
@@ -238,19 +241,19 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     auto load = [&](const unsigned char* base, int s, Frag& f) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const int row = wm * (BM / WGM) + i * 32 + c;
+        const int row = wm * (BM / WGM) + i * 32 + c0;
 #pragma unroll
         for (int p = 0; p < 2; ++p)
           f.a[i][p] = *reinterpret_cast<const f16x8_t*>(base + p * BM * ROWB + row * ROWB +
-                                                        (((NSTEP * s + h) ^ swz<CH>(row)) << 4));
+                                                        (((NSTEP * s + h0) ^ swz<CH>(row)) << 4));
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int row = wn * (BN / WGN) + j * 32 + c;
+        const int row = wn * (BN / WGN) + j * 32 + c0;
 #pragma unroll
         for (int p = 0; p < 2; ++p)
           f.w[j][p] = *reinterpret_cast<const f16x8_t*>(base + TA + p * BN * ROWB + row * ROWB +
-                                                        (((NSTEP * s + h) ^ swz<CH>(row)) << 4));
+                                                        (((NSTEP * s + h0) ^ swz<CH>(row)) << 4));
       }
     };
     auto mma = [&](const Frag& f) {
@@ -314,7 +317,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     }
     __syncthreads();  // every wave is done with the ring (the next tile's prologue)
 
-    // epilogue: register r of lane (c, h) = row (r&3) + 8(r>>2) + 4h of the block, column c
+    // epilogue: register r of lane (c, h) = row (r&3) + 8(r>>2) + 4h of the block, column c.
+    // Persistent loops: the lane coordinates are re-materialised per tile (opaque
+    // copies), so the compiler cannot hoist the epilogue's 16 MI NI per-lane
+    // offsets out of the tile loop and keep them live across the K loop (that
+    // hoisting spilled the PERSIST variants: 200+ VGPRs to scratch)
+    int c = c0, h = h0, ldc = ldc0, ldr = ldr0;
+    if constexpr (PERSIST || ROWSPLIT) {
+      asm volatile("" : "+v"(c), "+v"(h));
+      asm volatile("" : "+s"(ldc), "+s"(ldr));
+    }
     float rsv[MI][16], rbv[MI][16];  // row scales; row bias (conv: per output channel)
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -322,7 +334,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         rsv[i][r] = rinvb != nullptr ? rinvb[m < M ? m : M - 1] : rconst;
-        rbv[i][r] = (epi & EPI_BIAS_ROW) ? bias[m < M ? m : M - 1] : 0.f;
+        rbv[i][r] = (BATCHED && (epi & EPI_BIAS_ROW)) ? bias[m < M ? m : M - 1] : 0.f;
       }
     // interior tile stored as fp32 C (the common case): tile-local 32-bit
     // offsets from wave-uniform base pointers (saddr stores, no 64-bit
@@ -376,7 +388,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     const bool interior = full && po.p == nullptr && (kv.kvs == nullptr || n0 + BN <= kv.qcols);  // Q columns too
     if (interior) {
       float* Ct = Cb + (long long)m0 * ldc + n0;
-      const float* Rt = (epi & (EPI_RESID | EPI_RESID_PRE)) ? Rb + (long long)m0 * ldr + n0 : nullptr;
+      const float* Rt = (epi & EPI_RESID) || (BATCHED && (epi & EPI_RESID_PRE)) ? Rb + (long long)m0 * ldr + n0 : nullptr;
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int cl = wn * (BN / WGN) + j * 32 + c;
@@ -388,7 +400,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
           for (int r = 0; r < 16; ++r) {
             const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
             float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
-            if (epi & EPI_RESID_PRE) v += Rt[(unsigned)(rl * ldr + cl)];
+            if (BATCHED && (epi & EPI_RESID_PRE)) v += Rt[(unsigned)(rl * ldr + cl)];
             if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
             if (epi & EPI_RELU) v = fmaxf(v, 0.f);
             if (epi & EPI_RESID) v += Rt[(unsigned)(rl * ldr + cl)];
@@ -410,7 +422,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
-          if ((epi & EPI_RESID_PRE) && m < M && n < N) v += Rb[(long long)m * ldr + n];
+          if (BATCHED && (epi & EPI_RESID_PRE) && m < M && n < N) v += Rb[(long long)m * ldr + n];
           if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
           if (epi & EPI_RELU) v = fmaxf(v, 0.f);
           if (m < M && n < N) {
@@ -448,13 +460,13 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     for (int r = hw; r < BM; r += NW * 2) {
       const int m = m0 + r;
       if (m < M)
-        ln_split_row(C + (long long)m * ldc, N, lo.p + (long long)m * lo.ldp, lo.p + lo.pplane + (long long)m * lo.ldp,
+        ln_split_row(C + (long long)m * ldc0, N, lo.p + (long long)m * lo.ldp, lo.p + lo.pplane + (long long)m * lo.ldp,
                      lo.rinv + m, lo.eps, lo.eln, l32);
     }
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int BKT = 32, int RS = 2>
+template <int BM, int BN, int WGM, int WGN, int BKT = 32, int RS = 2, bool BATCHED = false>
 int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, float rconst, const _Float16* Wp,
              int ldw, long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C, int ldc,
              int M, int N, int K, int epi, KvOut kv, PlaneOut po, Batch bt, hipStream_t st) {
@@ -463,15 +475,16 @@ int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, f
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
   const size_t lds = RS * (size_t)(2 * BM * BKT * 2 + 2 * BN * BKT * 2);
   constexpr int NT = 64 * WGM * WGN;
-  const int grid = nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS>, NT, lds, ntiles);
+  const int grid =
+      nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS, false, BATCHED>, NT, lds, ntiles);
   if (grid < ntiles)
-    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS>), dim3((unsigned)grid), dim3(NT), lds, st, Ap, lda,
-                       aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
-                       tiles_n, kv, po, bt, LnOut{});
+    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS, false, BATCHED>), dim3((unsigned)grid),
+                       dim3(NT), lds, st, Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
+                       N, K, epi, tiles_m, tiles_n, kv, po, bt, LnOut{});
   else
-    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false, BKT, RS>), dim3((unsigned)ntiles), dim3(NT), lds, st, Ap,
-                       lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
-                       tiles_n, kv, po, bt, LnOut{});
+    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false, BKT, RS, false, BATCHED>), dim3((unsigned)ntiles),
+                       dim3(NT), lds, st, Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
+                       N, K, epi, tiles_m, tiles_n, kv, po, bt, LnOut{});
   return (int)hipGetLastError();
 }
 
@@ -630,11 +643,16 @@ NOS_API int nos_split_rows_h3(const float* A, int lda, void* P, int ldp, long lo
 
 namespace {
 
+// batched: the BATCHED instantiation (batch strides, per-row bias, residual
+// before the activation -- kept out of the one-GEMM kernels' registers)
 int run_h3(const void* Ap, int lda, long long aplane, const float* rinv, float rconst, const void* Wp, int ldw,
            long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C, int ldc, int M,
-           int N, int K, int epi, KvOut kv, PlaneOut po, Batch bt, hipStream_t stream) {
+           int N, int K, int epi, KvOut kv, PlaneOut po, Batch bt, hipStream_t stream, bool batched = false) {
   const auto* a = static_cast<const _Float16*>(Ap);
   const auto* w = static_cast<const _Float16*>(Wp);
+  if (batched)  // batched GEMMs (convs, matmuls) on the default 128x128, 2 x 2 layout
+    return launch_t<128, 128, 2, 2, 32, 2, true>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C,
+                                                 ldc, M, N, K, epi, kv, po, bt, stream);
   if (g_layout == 3)
     return launch_t<128, 128, 4, 1, 32, 3>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
                                            N, K, epi, kv, po, bt, stream);
@@ -733,7 +751,7 @@ NOS_API int nos_gemm_f32h3_batched(const void* Ap, int lda, long long aplane, lo
   bt.c = sc;
   bt.r = sr;
   return run_h3(Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, KvOut{},
-                PlaneOut{}, bt, stream);
+                PlaneOut{}, bt, stream, true);
 }
 
 // C = act(rinv[m] csc[n] (A' . W'^T) + bias) + R (a pre-LN residual GEMM,

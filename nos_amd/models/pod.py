@@ -165,8 +165,10 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
             "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or ("h3" if whole else "h3n"),
             "f32_math": env.get("NOS_AMD_F32_MATH") or "h3",
             "gemm_f32x6_tile": env.get("NOS_AMD_X6_TILE") or ("policy" if whole else "128x128"),
-            # pre-LN residual GEMMs hand the next LN-GEMM its planes (ops.set_ln_handoff)
-            "ln_handoff": env.get("NOS_AMD_LN_HANDOFF") or ("off" if whole else "on")}
+            # pre-LN residual GEMMs handing the next LN-GEMM its planes (ops.set_ln_handoff):
+            # off -- the row-owning grid is 3x smaller; 28-tenant fleet 611 (on) vs
+            # 725 (off) inf/s (profiles/r05_ln_handoff_ab.json)
+            "ln_handoff": env.get("NOS_AMD_LN_HANDOFF") or "off"}
 
 
 def slice_cu_budget(env: dict | None = None) -> int:

@@ -894,9 +894,13 @@ class CompiledProgram:
         consumer, which lets it fold into the GEMM."""
         import torch
 
+        # a linear whose output feeds a GELU / ReLU keeps its own GEMM: the
+        # activation fuses into that GEMM's epilogue, which a column slice of a
+        # merged GEMM would lose (YOLOS's two detection heads)
+        act_fed = {s.inputs[0] for s in steps if s.kind in ("gelu", "relu")}
         groups: dict[str, list[_Step]] = {}
         for s in steps:
-            if (s.kind == "linear" and s.inputs[0] not in self.consts and not s.attrs
+            if (s.kind == "linear" and s.inputs[0] not in self.consts and not s.attrs and s.output not in act_fed
                     and all(i in self.consts for i in s.inputs[1:])):
                 groups.setdefault(s.inputs[0], []).append(s)
         first: dict[int, _Step] = {}
