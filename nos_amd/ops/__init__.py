@@ -794,13 +794,18 @@ def linear_ln_qkv_h3(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: to
 
 def attention_presplit_h3(qkv: torch.Tensor, ws: torch.Tensor, scales: torch.Tensor, num_heads: int,
                           scale: float | None = None, out: torch.Tensor | None = None,
-                          planes_out: float | None = None):
+                          planes_out: float | None = None, q_range: tuple[int, int] | None = None):
     """fp16x3 attention from the planes :func:`linear_ln_qkv_h3` wrote.
     ``planes_out`` = a static scale s with |O| * s < 2^14 (every O row is a
     convex combination of V rows: the smallest V head scale works): the
-    output goes to the proj GEMM's A planes instead, as :class:`H3Planes`."""
-    B, S, three_hd = qkv.shape
+    output goes to the proj GEMM's A planes instead, as :class:`H3Planes`.
+    ``q_range`` = (q0, q1): only those query rows (every key): O [B, q1 - q0, hd]."""
+    B, Skv, three_hd = qkv.shape
     hd = three_hd // 3
+    q0, q1 = q_range if q_range is not None else (0, Skv)
+    if not 0 <= q0 < q1 <= Skv:
+        raise ValueError(f"q_range {q_range} outside 0..{Skv}")
+    S = q1 - q0
     planes = None
     if planes_out is not None:  # planes [2, B*S, hd] with o's strides; o itself is never written
         planes = torch.empty((2, B * S, hd), dtype=torch.float16, device=qkv.device)
@@ -814,7 +819,8 @@ def attention_presplit_h3(qkv: torch.Tensor, ws: torch.Tensor, scales: torch.Ten
     if scales.shape != (2, num_heads) or scales.dtype != torch.float32 or not scales.is_contiguous():
         raise ValueError("scales must be the [2, H] fp32 tensor of linear_ln_qkv_h3")
     scale = scale if scale is not None else 1.0 / math.sqrt(64)
-    rc = _lib.lib().nos_attn_fwd_f32h3_presplit_d64(qkv.data_ptr(), o_ptr, B, num_heads, S, S,
+    q_ptr = qkv.data_ptr() + q0 * qkv.stride(1) * qkv.element_size()
+    rc = _lib.lib().nos_attn_fwd_f32h3_presplit_d64(q_ptr, o_ptr, B, num_heads, S, Skv,
                                                     qkv.stride(1), qkv.stride(0), ld_out, bs_out,
                                                     float(scale), scales.data_ptr(), ws.data_ptr(),
                                                     ws.numel() * ws.element_size(), _ptr(planes), B * S * hd,
@@ -833,7 +839,8 @@ def ln_qkv_fusable(x: torch.Tensor) -> bool:
 
 
 def ln_qkv_attention(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, num_heads: int,
-                     eps: float = 1e-12, planes_out: bool = False, pre: H3Planes | None = None):
+                     eps: float = 1e-12, planes_out: bool = False, pre: H3Planes | None = None,
+                     q_range: tuple[int, int] | None = None):
     """attention(LayerNorm(x) @ W_qkv^T + b) for an fp32 pod (see
     :func:`ln_qkv_fusable`): the QKV projection writes the attention's K / V
     planes straight from its epilogue -- fp16x3 planes under an ``h3``
@@ -842,11 +849,13 @@ def ln_qkv_attention(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: to
     if _ATTN_F32_VARIANT.startswith("h3"):
         qkv, ws, sc = linear_ln_qkv_h3(x, wg, c1, c2, num_heads, eps=eps, pre=pre)
         osc = float(_H3_SCALES_HOST[id(wg)][1].min()) if planes_out else None
-        return attention_presplit_h3(qkv, ws, sc, num_heads, planes_out=osc)
+        return attention_presplit_h3(qkv, ws, sc, num_heads, planes_out=osc, q_range=q_range)
     if _F32_MATH == "h3":  # x6 attention after an h3 projection: the unfused pair
-        return attention_qkv(linear_ln(x, wg, c1, c2, eps=eps), num_heads)
-    qkv, ws = linear_ln_qkv_x6(x, wg, c1, c2, num_heads, eps=eps)
-    return attention_presplit(qkv, ws, num_heads)
+        y = attention_qkv(linear_ln(x, wg, c1, c2, eps=eps), num_heads)
+    else:
+        qkv, ws = linear_ln_qkv_x6(x, wg, c1, c2, num_heads, eps=eps)
+        y = attention_presplit(qkv, ws, num_heads)
+    return y[:, q_range[0]:q_range[1]] if q_range is not None else y
 
 
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | None = None,

@@ -693,8 +693,11 @@ def _eager(op: str, args: list, attrs: dict, ref: bool = False):
             from ..ops import tenant as T
 
             q, k, v = _qkv_views(args[0], attrs["heads"])
+            if "q_start" in attrs:
+                q = q[:, attrs["q_start"]:attrs["q_end"]]
             return T.sdpa(q, k, v, causal=attrs.get("causal", False), scale=attrs.get("scale")).flatten(2)
-        return ops.attention_qkv(args[0].contiguous(), attrs["heads"], scale=attrs.get("scale"))
+        y = ops.attention_qkv(args[0].contiguous(), attrs["heads"], scale=attrs.get("scale"))
+        return y[:, attrs["q_start"]:attrs["q_end"]] if "q_start" in attrs else y
     if op == "add":
         return args[0] + args[1]
     if op == "mul":
@@ -807,8 +810,11 @@ class CompiledProgram:
         self.outputs = list(prog.outputs)
         self.stats: dict[str, int] = {}
         self.aux: dict[str, object] = {}   # derived weights a kernel reads (e.g. conv weights as padded matrices)
+        self._new_shapes: dict[str, tuple] = {}   # values the passes create or re-shape
+        self._new_dtypes: dict[str, str] = {}
         with torch.no_grad():
             steps = self._fold_constants(prog)
+            steps = self._pushdown_row_slices(steps)
             steps = self._fold_batchnorm(steps)
             steps = self._merge_parallel_linears(steps)
             steps = self._fold_layernorm(steps)
@@ -853,6 +859,100 @@ class CompiledProgram:
             del self.consts[k]
         self.stats["constant_folded"] = folded
         return steps
+
+    def _pushdown_row_slices(self, steps: list[_Step]) -> list[_Step]:
+        """Dead-row elimination: a slice along a row (non-feature) dim of a value
+        only it consumes moves above the row-wise op that made it -- elementwise
+        ops, linears, norms -- and into an attention as a query range (its keys
+        and values still cover every row).  YOLOS keeps only its 100 detection
+        tokens after the last layer: that layer's attention, projection and MLP
+        then run on those 100 rows instead of 3401."""
+        n = 0
+        while True:
+            steps = self._dedupe_slices(steps)
+            uses = self._consumers(steps, self.outputs)
+            by_out = {s.output: s for s in steps}
+            hit = None
+            for s in steps:
+                if s.kind != "slice":
+                    continue
+                src = s.inputs[0]
+                p = by_out.get(src)
+                if p is None or uses.get(src) != 1:
+                    continue
+                shp = self._shape(src)
+                r = len(shp)
+                d = s.attrs["dim"] % r
+                if d == r - 1:
+                    continue  # a feature-column slice: not row-wise
+                plan = self._slice_plan(p, d, r, shp)
+                if plan is not None:
+                    hit = (s, p, d, plan)
+                    break
+            if hit is None:
+                break
+            s, p, d, plan = hit
+            st, en = s.attrs["start"], s.attrs["end"]
+            new_steps = []
+            for idx, dim in plan:  # slice these inputs of p
+                name = p.inputs[idx]
+                nn_ = f"{name}::rows{st}_{en}_{n}"
+                sh = list(self._shape(name))
+                sh[dim] = en - st
+                self._new_shapes[nn_] = tuple(sh)
+                self._new_dtypes[nn_] = self._dtype(name)
+                new_steps.append(_Step("slice", [name], nn_, {"dim": dim, "start": st, "end": en}))
+                p.inputs[idx] = nn_
+            if p.kind in ("attention",):  # a query range on top of any earlier one
+                q0 = p.attrs.get("q_start", 0)
+                p.attrs["q_start"], p.attrs["q_end"] = q0 + st, q0 + en
+            p.output = s.output
+            self._new_shapes[s.output] = self._shape(s.output)
+            i = steps.index(p)
+            steps = [x for x in steps if x is not s]
+            steps[i:i] = new_steps
+            n += 1
+        self.stats["row_slices_pushed"] = n
+        return steps
+
+    def _dedupe_slices(self, steps: list[_Step]) -> list[_Step]:
+        """Identical slices of one value (the same rows pushed up two paths,
+        e.g. a residual and the norm after it) become one."""
+        seen: dict[tuple, str] = {}
+        rename: dict[str, str] = {}
+        out = []
+        for s in steps:
+            s.inputs = [rename.get(i, i) for i in s.inputs]
+            if s.kind == "slice" and s.output not in self.outputs:
+                key = (s.inputs[0], s.attrs["dim"] % len(self._shape(s.inputs[0])), s.attrs["start"], s.attrs["end"])
+                if key in seen:
+                    rename[s.output] = seen[key]
+                    continue
+                seen[key] = s.output
+            out.append(s)
+        return out
+
+    def _slice_plan(self, p: _Step, d: int, r: int, out_shape) -> list[tuple[int, int]] | None:
+        """Which inputs of row-wise step ``p`` (output rank ``r``) to slice along
+        output dim ``d``, as (input index, input dim); None: not row-wise in d."""
+        if p.kind in UNARY or p.kind == "cast":
+            return [(0, d)]
+        if p.kind in ("linear", "layernorm", "rmsnorm"):
+            return [(0, d)] if len(self._shape(p.inputs[0])) == r else None
+        if p.kind in BINARY:
+            plan = []
+            for i, name in enumerate(p.inputs):
+                sh = self._shape(name)
+                di = d - (r - len(sh))
+                if di < 0 or sh[di] == 1:
+                    continue  # broadcast along d: every row uses the same values
+                if sh[di] != out_shape[d]:
+                    return None
+                plan.append((i, di))
+            return plan
+        if p.kind == "attention" and d == 1 and not p.attrs.get("causal"):
+            return []  # the query range; keys / values still read every row
+        return None
 
     def _fold_batchnorm(self, steps: list[_Step]) -> list[_Step]:
         """conv2d -> batchnorm (inference statistics, all weights constant)
@@ -1072,7 +1172,8 @@ class CompiledProgram:
             if s.attrs.get("causal") or d != 64:
                 continue  # the general attention (ops.tenant.sdpa) runs it
             s.kind = "ln_qkv_attention"
-            s.attrs = {"heads": s.attrs["heads"], "eps": p.attrs["eps"]}
+            s.attrs = {"heads": s.attrs["heads"], "eps": p.attrs["eps"],
+                       **{k: s.attrs[k] for k in ("q_start", "q_end") if k in s.attrs}}
             s.inputs = list(p.inputs)
             drop.add(p.output)
             n += 1
@@ -1172,11 +1273,15 @@ class CompiledProgram:
         return steps
 
     def _shape(self, name: str):
+        if name in self._new_shapes:
+            return self._new_shapes[name]
         v = self.program.values.get(name)
         return v.shape if v is not None else tuple(self.consts[name].shape)
 
     def _dtype(self, name: str):
         v = self.program.values.get(name)
+        if v is None and name in self._new_dtypes:
+            return self._new_dtypes[name]
         return v.dtype if v is not None else str(self.consts[name].dtype)
 
     # ------------------------------------------------------------ run
@@ -1215,13 +1320,16 @@ class CompiledProgram:
             elif k == "ln_qkv_attention":
                 h = a[0].contiguous()
                 pre = env.pop(s.inputs[0] + "::lnp", None)
+                qr = (s.attrs["q_start"], s.attrs["q_end"]) if "q_start" in s.attrs else None
                 if ops.ln_qkv_fusable(h):
                     y = ops.ln_qkv_attention(h, a[1], a[2], a[3], s.attrs["heads"], eps=s.attrs["eps"],
                                              planes_out=bool(s.attrs.get("planes_out"))
-                                             and ops.h3_planes_active(attention=True), pre=pre)
+                                             and ops.h3_planes_active(attention=True), pre=pre, q_range=qr)
                 else:
                     qkv = ops.linear_ln(h, a[1], a[2], a[3], eps=s.attrs["eps"])
                     y = ops.attention_qkv(qkv, s.attrs["heads"])
+                    if qr is not None:
+                        y = y[:, qr[0]:qr[1]]
             elif k == "attention":
                 y = _eager("attention", [a[0].contiguous()], s.attrs)
             elif k == "conv2d":

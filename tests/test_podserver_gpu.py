@@ -43,7 +43,7 @@ def server(tmp_path):
     ops.set_gemm_f32x6_tile("policy")
 
 
-def test_server_replays_match_the_eager_model_bit_for_bit(server):
+def test_server_replays_match_the_eager_model(server):
     from nos_amd.models.yolos import YolosConfig, YolosDetector
     from nos_amd.models.yolos_program import yolos_weights
     from nos_amd.podserver.client import PodClient
@@ -73,8 +73,13 @@ def test_server_replays_match_the_eager_model_bit_for_bit(server):
         torch.cuda.synchronize()
     finally:
         server._apply_config(server.kernel_config)
+    # the encoder runs the same kernels in the same order; the last layer only on
+    # the 100 detection tokens (row-slice pushdown: its attention may then split
+    # the keys differently), so fp32-class agreement rather than bit equality
+    assert rep["compile"]["row_slices_pushed"] >= 8
     for o, r in zip(outs, ref):
-        assert np.array_equal(o, r.float().cpu().numpy())
+        r = r.float().cpu().numpy()
+        assert np.abs(o - r).max() <= 1e-5 * (np.abs(r).max() + 1)
     c.close()
 
 
