@@ -116,6 +116,9 @@ def parse_args(argv=None):
     ap.add_argument("--tenant-mix", default="", metavar="FAMILY:N,...",
                     help="server mode: a mixed fleet of model families, e.g. yolos:16,resnet:6,llama:6 "
                          "(pods of the other families ship prebuilt programs; per-family throughput in 'mix')")
+    ap.add_argument("--composed", action="store_true",
+                    help="with --quota: BASELINE config 5 composed -- DP trainer pods, bursty team-a waves, a "
+                         "simulated amdpart repartition, then preemption (quotabench.ComposedScenario)")
     ap.add_argument("--quota", action="store_true",
                     help="BASELINE config 5 instead of the headline: two namespaces' ElasticQuotas on the GPU's "
                          "pod-server slices, borrowing then fair-share preemption acting on running tenants "
@@ -555,8 +558,24 @@ def run_quota(args) -> int:
     work = tempfile.mkdtemp(prefix="nos_q_pods_")
     args.local_gpu = 0
     slices = args.pods_per_gpu or 28
-    sc = scenario_for(slices, args.slice_gb or 10, pod_server_dir=args.pod_server_dir, live=True)
     server = PodServerProc(launcher, args, "0", work)
+    if args.composed:
+        from nos_amd.quotabench import composed_for
+
+        def server_stats():
+            from nos_amd.podserver.client import PodClient
+
+            c = PodClient(server.path, connect_timeout_s=5)
+            try:
+                return c.stats()
+            finally:
+                c.close()
+
+        # 36 GB of the GPU for the trainer pod, the rest in 10 GB tenant slices
+        sc = composed_for(1, args.pods_per_gpu or 25, args.slice_gb or 10, pod_server_dir=args.pod_server_dir,
+                          live=True, server_stats=server_stats)
+    else:
+        sc = scenario_for(slices, args.slice_gb or 10, pod_server_dir=args.pod_server_dir, live=True)
     sampler = None
     try:
         log(0, f"pod server ready in {server.wait_ready():.1f} s")
@@ -565,7 +584,8 @@ def run_quota(args) -> int:
 
             torch.cuda.set_device(0)
             sampler = UtilSampler(0)
-        rt = ProcessRuntime(launcher, work, dtype=args.dtype, device=args.device)
+        rt = ProcessRuntime(launcher, work, dtype=args.dtype, device=args.device,
+                            extra_env={"NOS_AMD_POD_DUTY": sc.duty} if args.composed else None)
         try:
             res = sc.run(rt, phase_timeout_s=900, sampler=sampler)
         finally:
@@ -581,8 +601,10 @@ def run_quota(args) -> int:
         launcher.close()
         shutil.rmtree(work, ignore_errors=True)
         shutil.rmtree(args.pod_server_dir, ignore_errors=True)
-    line = json.dumps({"metric": "config5: ElasticQuota borrowing + CapacityScheduling preemption on running "
-                                 "pod-server tenants (1 node)", "dtype": args.dtype, "device": args.device,
+    metric = ("config5 composed: DP trainer pods + bursty ElasticQuota tenants on a pod-server node, a simulated "
+              "amdpart repartition, CapacityScheduling preemption" if args.composed else
+              "config5: ElasticQuota borrowing + CapacityScheduling preemption on running pod-server tenants (1 node)")
+    line = json.dumps({"metric": metric, "dtype": args.dtype, "device": args.device,
                        "data": "synthetic (random-init YOLOS-small programs)", **res})
     print(line, flush=True)
     if args.json_out:

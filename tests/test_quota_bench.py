@@ -63,3 +63,40 @@ def test_bench_quota_runs_real_pod_processes_against_a_pod_server():
     assert b["team-a"]["tenants_running"] == b["team-b"]["tenants_running"] == 3
     assert b["team-b"]["pods_match_tenants"] and b["team-a"]["pods_match_tenants"]
     assert d["concurrent_tenants"] == 6 and d["pod_server"]["device"] == "cpu"
+
+
+def test_composed_config5_rehearsal_on_an_8gpu_node(tmp_path):
+    """config 5 as ONE scenario on an 8-GPU pod-server node
+    -- one DP trainer pod per GPU, team-a's tenants in three bursts borrowing
+    team-b's quota, pending CPX pods forcing a (simulated) repartition of an
+    amdpart node, then team-b claiming its min by preemption."""
+    from nos_amd.quotabench import RecordingRuntime, composed_for
+
+    sc = composed_for(8, pod_server_dir=str(tmp_path), part_gpus=2, part_pods=12)
+    res = sc.run(RecordingRuntime())
+    assert res["phase_trainers"]["ok"] and res["phase_trainers"]["trainers"] == 8
+    a = res["phase_a"]
+    assert a["ok"] and a["team-a"]["tenants_running"] == sc.team_a_pods and a["team-a"]["over_quota"] > 0
+    assert a["team-a"]["status_used_gb"] == a["team-a"]["tenant_gb"] == sc.team_a_pods * 10
+    p = res["phase_repartition"]
+    assert p["ok"] and p["pods_running"] == 12 and p["mode_switches"] >= 2 and set(p["modes_after"]) == {"CPX"}
+    b = res["phase_b"]
+    assert b["ok"] and b["victims"] == b["preemptions"] == a["team-a"]["over_quota"] and b["victims_over_quota_only"]
+    assert b["team-b"]["tenants_running"] == sc.team_b_pods and b["team-a"]["over_quota"] == 0
+    for ns in ("team-a", "team-b"):
+        assert b[ns]["status_used_gb"] == b[ns]["tenant_gb"] and b[ns]["pods_match_tenants"]
+    assert res["concurrent_tenants"] == 8 + 2 * sc.team_b_pods  # trainers + both teams at their min
+
+
+@pytest.mark.timeout(600)
+def test_bench_quota_composed_runs_trainer_and_tenant_processes():
+    cmd = [sys.executable, "bench.py", "--quota", "--composed", "--device", "cpu", "--pods-per-gpu", "6"]
+    r = subprocess.run(cmd, cwd=REPO, env={**os.environ, "OMP_NUM_THREADS": "1"}, capture_output=True, text=True,
+                       timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["metric"].startswith("config5 composed")
+    assert d["phase_trainers"]["ok"] and d["phase_a"]["ok"] and d["phase_repartition"]["ok"] and d["phase_b"]["ok"]
+    assert d["phase_repartition"]["mode_switches"] == 1 and d["phase_b"]["preemptions"] >= 1
+    assert d["concurrent_tenants"] == 7  # the trainer + 3 + 3
+    assert "server_footprint_gb" in d["phase_b"]["quota_vs_footprint"]["team-b"]
