@@ -30,6 +30,8 @@
 //    LDS read ds_read_b64_tr_b16 (no LDS round trip for P);
 //  * deferred rescale (P <= 2^8) and XCD-aware (batch, head, q-block) order
 //    as in attention_f32.hip; PERSIST: slice-sized grid (nos::xcd_chunk).
+#include <type_traits>
+
 #include "common.h"
 #include "split_bf16.h"
 #include "split_f16.h"
@@ -72,6 +74,14 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_ba
   // (a clobbered m0 is undefined behaviour: m0 is a reserved register); the
   // s_nop is the SALU-write-m0 -> LDS-DMA wait state the compiler cannot see
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(lds) : "memory");
+}
+
+// LDS-DMA from a wave-uniform tile base (SGPR pair) plus a per-lane 32-bit byte
+// offset: the steady-state tiles need no 64-bit VALU address arithmetic
+__device__ __forceinline__ void glds16_s(const void* sbase, unsigned voff, unsigned char* lds_wave_base) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds_wave_base);
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(lds) : "memory");
 }
 
 // every DMA this wave issued has landed, then the workgroup barrier publishes them
@@ -437,6 +447,12 @@ __global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_
       }
       glds16(pb + off, smem + buf * H3_STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
     };
+    // full tiles: uniform base + the per-lane byte offsets (2 * soff)
+    auto stage_full = [&](int t, int buf, int i) {
+      const int p = wid * PPW + i;
+      glds16_s(pb + (long long)t * (KVB * 4) * ldh, (unsigned)soff[i] * 2u,
+               smem + buf * H3_STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
+    };
 #pragma unroll
     for (int i = 0; i < PPW; ++i) stage_piece(t0, 0, i);
 
@@ -450,11 +466,19 @@ __global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_
 
     dma_wait_publish();
 
-    for (int t = t0; t < t1; ++t) {
+    // the tile body; MASKED: the tail tile (keys past Skv masked).  Peeled out of
+    // the main loop -- if-converted into it, the mask cost 48 VALU per tile
+    auto tile = [&](int t, auto masked) {
+      constexpr bool MASKED = decltype(masked)::value;
       const int buf = (t - t0) & 1;
       if (t + 1 < t1) {
+        if ((t + 2) * KVB <= Skv) {
 #pragma unroll
-        for (int i = 0; i < PPW; ++i) stage_piece(t + 1, buf ^ 1, i);
+          for (int i = 0; i < PPW; ++i) stage_full(t + 1, buf ^ 1, i);
+        } else {
+#pragma unroll
+          for (int i = 0; i < PPW; ++i) stage_piece(t + 1, buf ^ 1, i);
+        }
       }
       const unsigned char* kl = smem + buf * H3_STAGE;
       const unsigned char* vl = kl + 2 * IMG;
@@ -469,7 +493,7 @@ __global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_
         for (int p = 0; p < 2; ++p) a[p] = *reinterpret_cast<const f16x8_t*>(kl + p * IMG + koff[ks]);
         s = nos::mma3h(a, qf[ks], s);
       }
-      if ((t + 1) * KVB > Skv) {
+      if constexpr (MASKED) {
 #pragma unroll
         for (int i = 0; i < 16; ++i)
           if (t * KVB + (i & 3) + 8 * (i >> 2) + 4 * hh >= Skv) s[i] = -INFINITY;
@@ -489,21 +513,24 @@ __global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_
           oacc[1][i] *= alpha;
         }
       }
+      // packed: score -> exp2 units as v_pk_fma_f32 on key pairs, the row sum as
+      // v_pk_add_f32 into two pair accumulators -- the same four partial sums in
+      // the same order as four scalar ones (bit-identical), half the instructions
       f16x8_t pf[2][2];
-      float ls[4] = {0.f, 0.f, 0.f, 0.f};
+      f32x2_t ls2[2] = {f32x2_t{0.f, 0.f}, f32x2_t{0.f, 0.f}};
+      const f32x2_t fs2 = {fs, fs}, nm2 = {-m, -m};
 #pragma unroll
       for (int j2 = 0; j2 < 8; ++j2) {
-        const float x0 = __builtin_amdgcn_exp2f(fmaf(s[2 * j2], fs, -m));
-        const float x1 = __builtin_amdgcn_exp2f(fmaf(s[2 * j2 + 1], fs, -m));
-        ls[(2 * j2) & 3] += x0;
-        ls[(2 * j2 + 1) & 3] += x1;
+        const f32x2_t e2 = __builtin_elementwise_fma(f32x2_t{s[2 * j2], s[2 * j2 + 1]}, fs2, nm2);
+        const f32x2_t x = {__builtin_amdgcn_exp2f(e2.x), __builtin_amdgcn_exp2f(e2.y)};
+        ls2[j2 & 1] += x;
         f16x2_t hi, lo;
-        nos::split2h(f32x2_t{x0, x1}, hi, lo);
+        nos::split2h(x, hi, lo);
         const int s2 = j2 >> 2, e = 2 * (j2 & 3);
         pf[s2][0][e] = hi.x; pf[s2][0][e + 1] = hi.y;
         pf[s2][1][e] = lo.x; pf[s2][1][e + 1] = lo.y;
       }
-      l += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+      l += (ls2[0].x + ls2[0].y) + (ls2[1].x + ls2[1].y);
 #pragma unroll
       for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -520,7 +547,10 @@ __global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_
           oacc[db] = nos::mma3h(a, pf[s2], oacc[db]);
         }
       dma_wait_publish();
-    }
+    };
+    const int tm = (Skv % KVB) ? max(t0, min(t1, ntiles - 1)) : t1;  // the tail tile, if any, is the last
+    for (int t = t0; t < tm; ++t) tile(t, std::false_type{});
+    for (int t = tm; t < t1; ++t) tile(t, std::true_type{});
 
     const float lt = xor32_sum(l);
     if (nsplit > 1) {  // unnormalised partial (O, m, l), O on the unit scale

@@ -69,6 +69,14 @@ __device__ __forceinline__ void glds16(const void* g, unsigned char* lds_wave_ba
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(lds) : "memory");
 }
 
+// LDS-DMA from a wave-uniform tile base (SGPR pair) plus a per-lane 32-bit byte
+// offset: the steady-state tiles need no 64-bit VALU address arithmetic
+__device__ __forceinline__ void glds16_s(const void* sbase, unsigned voff, unsigned char* lds_wave_base) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds_wave_base);
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(lds) : "memory");
+}
+
 __device__ __forceinline__ void dma_wait_publish() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -304,6 +312,11 @@ __global__ __launch_bounds__(64 * HW, D == 64 ? 2 : 1) void attn_h3g_kernel(
       }
       glds16(pb + o2, smem + buf * STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
     };
+    auto stage_full = [&](int t, int buf, int i) {  // full tiles: uniform base + per-lane byte offset
+      const int p = wid * PPW + i;
+      glds16_s(pb + (long long)t * (KVB * 4) * D, (unsigned)soff[i] * 2u,
+               smem + buf * STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
+    };
 
     f32x16_t oacc[2 * NH];
 #pragma unroll
@@ -321,8 +334,13 @@ __global__ __launch_bounds__(64 * HW, D == 64 ? 2 : 1) void attn_h3g_kernel(
     for (int t = t0; t < t1; ++t) {
       const int buf = (t - t0) & 1;
       if (t + 1 < t1) {
+        if ((t + 2) * KVB <= Skv) {
 #pragma unroll
-        for (int i = 0; i < PPW; ++i) stage_piece(t + 1, buf ^ 1, i);
+          for (int i = 0; i < PPW; ++i) stage_full(t + 1, buf ^ 1, i);
+        } else {
+#pragma unroll
+          for (int i = 0; i < PPW; ++i) stage_piece(t + 1, buf ^ 1, i);
+        }
       }
       const unsigned char* st = smem + buf * STAGE;
 
@@ -368,21 +386,24 @@ __global__ __launch_bounds__(64 * HW, D == 64 ? 2 : 1) void attn_h3g_kernel(
 #pragma unroll
           for (int i = 0; i < 16; ++i) oacc[db][i] *= alpha;
       }
+      // packed: score -> exp2 units as v_pk_fma_f32 on key pairs, the row sum as
+      // v_pk_add_f32 into two pair accumulators -- the same four partial sums in
+      // the same order as four scalar ones (bit-identical), half the instructions
       f16x8_t pf[2][2];
-      float ls[4] = {0.f, 0.f, 0.f, 0.f};
+      f32x2_t ls2[2] = {f32x2_t{0.f, 0.f}, f32x2_t{0.f, 0.f}};
+      const f32x2_t fs2 = {fs, fs}, nm2 = {-m, -m};
 #pragma unroll
       for (int j2 = 0; j2 < 8; ++j2) {
-        const float x0 = __builtin_amdgcn_exp2f(fmaf(s[2 * j2], fs, -m));
-        const float x1 = __builtin_amdgcn_exp2f(fmaf(s[2 * j2 + 1], fs, -m));
-        ls[(2 * j2) & 3] += x0;
-        ls[(2 * j2 + 1) & 3] += x1;
+        const f32x2_t e2 = __builtin_elementwise_fma(f32x2_t{s[2 * j2], s[2 * j2 + 1]}, fs2, nm2);
+        const f32x2_t x = {__builtin_amdgcn_exp2f(e2.x), __builtin_amdgcn_exp2f(e2.y)};
+        ls2[j2 & 1] += x;
         f16x2_t hi, lo;
-        nos::split2h(f32x2_t{x0, x1}, hi, lo);
+        nos::split2h(x, hi, lo);
         const int s2 = j2 >> 2, e = 2 * (j2 & 3);
         pf[s2][0][e] = hi.x; pf[s2][0][e + 1] = hi.y;
         pf[s2][1][e] = lo.x; pf[s2][1][e + 1] = lo.y;
       }
-      l += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+      l += (ls2[0].x + ls2[0].y) + (ls2[1].x + ls2[1].y);
 #pragma unroll
       for (int db = 0; db < 2 * NH; ++db)
 #pragma unroll
