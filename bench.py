@@ -227,6 +227,7 @@ class UtilSampler:
         """``hip_id``: this rank's GPU as HIP numbers it; amd-smi is asked by
         ITS index (the two orders can differ on a node)."""
         self.samples: list[tuple[float, int]] = []
+        self.umc: list[tuple[float, int]] = []      # memory-controller (HBM) activity %, same stream
         self.clocks: list[tuple[float, int]] = []
         self.err = None
         self._stop = threading.Event()
@@ -250,7 +251,10 @@ class UtilSampler:
         k = 0
         while not self._stop.is_set():
             try:
-                self.samples.append((time.monotonic(), self.smi.activity(self.index)["gfx"]))
+                a = self.smi.activity(self.index)
+                now = time.monotonic()
+                self.samples.append((now, a["gfx"]))
+                self.umc.append((now, a["umc"]))
                 if k % 5 == 0:  # GFX clock at 10 Hz: tells DVFS apart from contention
                     self.clocks.append((time.monotonic(), self.smi.clock(self.index)["sclk_mhz"]))
             except Exception as e:
@@ -262,6 +266,10 @@ class UtilSampler:
     def mean(self, t0: float, t1: float) -> tuple[float | None, int]:
         v = [u for t, u in self.samples if t0 <= t <= t1]
         return (sum(v) / len(v) if v else None), len(v)
+
+    def mean_umc(self, t0: float, t1: float) -> float | None:
+        v = [u for t, u in self.umc if t0 <= t <= t1]
+        return round(sum(v) / len(v), 1) if v else None
 
     def mean_sclk(self, t0: float, t1: float) -> float | None:
         v = [u for t, u in self.clocks if t0 <= t <= t1]
@@ -302,6 +310,7 @@ def fleet_window(d: Dist, fleet, warmup: int, steps: int, step_s: float, sampler
     util = sampler.mean(t0, t1) if sampler else (None, 0)
     if sampler:
         fleet.sclk_mhz = sampler.mean_sclk(t0, t1)
+        fleet.umc_pct = sampler.mean_umc(t0, t1)
     return t0, t1, util
 
 
@@ -455,6 +464,7 @@ def run_fleet(d: Dist, launcher, envs, dtype, graphs, extra_env, warmup, steps, 
         fleet.stop()
         w = fleet.window(t0, t1)
         w.sclk_mhz = getattr(fleet, "sclk_mhz", None)
+        w.umc_pct = getattr(fleet, "umc_pct", None)
     finally:
         fleet.close()
     return w, util, n_util, ready_s, trainer_stats(w)
@@ -719,6 +729,7 @@ def main(argv=None) -> int:
                                     server_alive=server is not None)
         table.append({"mode": mode, "pods": n, "concurrent": wt.concurrent, "inf_per_s": round(wt.throughput, 2),
                       "mean_latency_s": wt.mean_latency_s, "gpu_util_pct": ut, "sclk_mhz": wt.sclk_mhz,
+                      "umc_util_pct": getattr(wt, "umc_pct", None),
                       "pods_over_latency": round(n / wt.mean_latency_s, 2) if wt.mean_latency_s else None,
                       "cu_mask": (wt.pods[0].info.get("cu_mask") if wt.pods else None)})
         log(rank, f"table {table[-1]}")
@@ -780,6 +791,7 @@ def main(argv=None) -> int:
         "gpu_util_pct": None if util_mean is None else round(util_mean, 1),
         "gpu_util_samples": n_util,
         "rank0_sclk_mhz": w.sclk_mhz,
+        "rank0_umc_util_pct": getattr(w, "umc_pct", None),
         "schedulable_fractional_pods_per_node": value,
         # what bounds it on this node: the amdgpu hardware scheduler's concurrent
         # processes per logical GPU (VMIDs), read from the driver

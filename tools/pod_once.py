@@ -19,7 +19,13 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--memory-fraction", type=float, default=None, help="as a fractional pod (kernel_config)")
+    ap.add_argument("--cu-mask", default="", help="a CU-mask slice (hex, ROC_GLOBAL_CU_MASK) with its CU budget: "
+                    "the cumask process pod of the latency table, e.g. 0xffffffff for 32 CUs")
     a = ap.parse_args()
+    import os
+
+    if a.cu_mask:  # before HIP initialises: the runtime reads it at queue creation
+        os.environ["ROC_GLOBAL_CU_MASK"] = a.cu_mask
     import torch
 
     from nos_amd.models.pod import _build
@@ -31,7 +37,12 @@ def main() -> None:
     from nos_amd import ops
     from nos_amd.models.pod import kernel_config
 
-    cfg = kernel_config(a.memory_fraction, os.environ)  # the pod's kernel choices (NOS_AMD_* overrides apply)
+    from nos_amd.models.pod import slice_cu_budget
+
+    budget = slice_cu_budget(os.environ)
+    cfg = kernel_config(a.memory_fraction, os.environ, budget)  # the pod's kernel choices (NOS_AMD_* overrides apply)
+    if budget:
+        ops.set_cu_budget(budget)
     ops.set_gemm_policy(cfg["gemm_bf16"])
     ops.set_gemm_f32_policy(cfg["gemm_f32"])
     ops.set_attention_f32_variant(cfg["attention_f32"])
@@ -51,7 +62,7 @@ def main() -> None:
             t.launch()
         s.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
-    print(f"{a.dtype}: {dt * 1e3:.3f} ms/inference ({1 / dt:.1f} inf/s)")
+    print(f"{a.dtype}: {dt * 1e3:.3f} ms/inference ({1 / dt:.1f} inf/s), cu budget {budget}", flush=True)
 
 
 if __name__ == "__main__":
