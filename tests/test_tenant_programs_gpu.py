@@ -93,3 +93,29 @@ def test_gpu_pod_server_cohosts_three_model_families(tmp_path):
             c.close()
     finally:
         srv.stop()
+
+
+@pytest.mark.parametrize("family", ["resnet", "llama"])
+def test_bf16_tenant_programs_run_on_gpu(family):
+    """bf16 programs of the new families: bf16 weights / activations, the
+    GEMM-class ops on the fp32 kernels over an fp32 copy (never less precise
+    than asked); close to the fp32 module at bf16 tolerance."""
+    if family == "resnet":
+        m = resnet18(seed=0)
+        prog, w = resnet_tenant("bf16", 0)
+        x = torch.randn(1, 3, 224, 224)
+        with torch.no_grad():
+            ref = m(x)
+        inp = x.cuda()
+    else:
+        lm = llama_model(llama_config(False), 0)
+        prog, w = llama_program(lm, 64, dtype="bf16")
+        ids = torch.randint(0, lm.config.vocab_size, (1, 64))
+        with torch.no_grad():
+            ref = lm(ids).logits
+        inp = ids.int().cuda()
+    cm = PG.parse(prog, w, gpu=True).compile("cuda")
+    with torch.no_grad():
+        got = cm(inp)[0].float().cpu()
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max() <= 0.05 * ref.abs().max(), float((got - ref).abs().max() / ref.abs().max())
