@@ -100,67 +100,47 @@ struct PlaneOut {
   float sc = 1.f;
 };
 
-// ROWSPLIT (LnOut): a workgroup owns a whole row block -- it runs the
-// tiles_n tiles of its BM rows one after the other -- and, once its fp32 C
-// rows are stored, splits them LayerNorm-normalised into the NEXT GEMM's h3
-// A planes (what nos_split_rows_h3 in LN mode would do in a separate launch):
-// the pre-LN residual GEMMs (attention proj, fc2) hand the following LN-GEMM
-// (QKV, fc1) its operand, the rows read back from this CU's L1/L2
-struct LnOut {
-  _Float16* p = nullptr;
-  long long pplane = 0;
-  int ldp = 0;
-  float* rinv = nullptr;
-  float eps = 0.f;
-  int eln = 0;
+// LayerNorm hand-off between a pre-LN residual GEMM and the LN-GEMM after it
+// (no nos_split_rows_h3 pass, no fp16 planes of the activation):
+//  * MODE 2 (producer): the epilogue also writes each row's statistics over
+//    the tile's columns, (mean, M2 = sum (x - mean)^2), to sout[m][tn]
+//    (spart = tiles_n parts of BN columns): the fp32 tile goes through LDS,
+//    two threads per row, two-pass in registers, Chan's merge of the halves;
+//  * MODE 1 (consumer): A is the fp32 rows X themselves; a workgroup merges
+//    each of its rows' part statistics (Chan), and every stage's A tile is
+//    loaded into registers, normalised ((x - mean) rstd 2^eln, the sqrt(K)
+//    bound's scale) and split into the h3 planes in LDS -- what the split
+//    pass did, one K-slice at a time, under the previous stage's MFMAs.
+struct LnIo {
+  const float* x = nullptr;     // MODE 1: A rows (fp32, row stride ldx)
+  const float2* sin = nullptr;  // MODE 1: part statistics [M][nparts], parts of pw columns
+  float2* sout = nullptr;       // MODE 2: [M][spart]
+  int ldx = 0, nparts = 0, pw = 0, spart = 0;
+  float eps = 0.f, sc = 1.f;    // MODE 1: LayerNorm eps, 2^eln
 };
 
-// one LayerNorm-normalised row (N % 4 == 0) by a 32-lane half-wave: mean,
-// variance (two passes over the row, re-read from cache), then hi / lo
-// pieces of (x - mu) rstd 2^eln; rinv = 2^-eln (the consumer's row scale)
-__device__ __forceinline__ void ln_split_row(const float* __restrict__ x, int N, _Float16* __restrict__ ph,
-                                             _Float16* __restrict__ pl, float* __restrict__ rinv, float eps,
-                                             int eln, int lane) {
-  typedef __attribute__((ext_vector_type(4))) _Float16 f16x4_t;
-  float s = 0.f;
-  for (int k = lane * 4; k < N; k += 128) {
-    const float4 v = *reinterpret_cast<const float4*>(x + k);
-    s += (v.x + v.y) + (v.z + v.w);
-  }
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  const float mu = s / (float)N;
-  float q = 0.f;
-  for (int k = lane * 4; k < N; k += 128) {
-    const float4 v = *reinterpret_cast<const float4*>(x + k);
-    const float d0 = v.x - mu, d1 = v.y - mu, d2 = v.z - mu, d3 = v.w - mu;
-    q = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, q))));
-  }
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
-  const float mul = rsqrtf(q / (float)N + eps) * nos::pow2i(eln), add = -mu * mul;
-  for (int k = lane * 4; k < N; k += 128) {
-    const float4 v = *reinterpret_cast<const float4*>(x + k);
-    f16x2_t h01, l01, h23, l23;
-    nos::split2h(f32x2_t{fmaf(v.x, mul, add), fmaf(v.y, mul, add)}, h01, l01);
-    nos::split2h(f32x2_t{fmaf(v.z, mul, add), fmaf(v.w, mul, add)}, h23, l23);
-    *reinterpret_cast<f16x4_t*>(ph + k) = f16x4_t{h01.x, h01.y, h23.x, h23.y};
-    *reinterpret_cast<f16x4_t*>(pl + k) = f16x4_t{l01.x, l01.y, l23.x, l23.y};
-  }
-  if (lane == 0) *rinv = nos::pow2i(-eln);
+// Chan et al.'s pairwise update of (count, mean, M2) with a part (nb, mb, m2b)
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float mb, float m2b) {
+  const float tot = n + nb;
+  if (!(nb > 0.f)) return;
+  const float d = mb - mean, f = nb / tot;
+  mean = fmaf(d, f, mean);
+  m2 += m2b + d * d * n * f;
+  n = tot;
 }
 
 // BKT: K depth of an LDS stage (32: two 16-deep MFMA steps, or 16: one);
 // RS: stages in the ring (RS - 1 of them in flight ahead of the one computed)
 // BATCHED: the tile index spans nb batch elements (Batch strides); false: one
 // GEMM, no per-tile batch offsets (fewer live SGPRs in the hot path)
-template <int BM, int BN, int WGM, int WGN, bool PERSIST, int BKT = 32, int RS = 2, bool ROWSPLIT = false,
+// MODE: 0 A as planes (LDS-DMA); 1 A = LayerNorm(X) (LnIo); 2 row statistics out
+template <int BM, int BN, int WGM, int WGN, bool PERSIST, int BKT = 32, int RS = 2, int MODE = 0,
           bool BATCHED = false>
 __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3_kernel(
     const _Float16* __restrict__ Ap, int lda, long long aplane, const float* __restrict__ rinv, float rconst,
     const _Float16* __restrict__ Wp, int ldw, long long wplane, const float* __restrict__ csc,
     const float* __restrict__ bias, const float* __restrict__ R, int ldr0, float* __restrict__ C, int ldc0, int M,
-    int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv, PlaneOut po, Batch bt, LnOut lo) {
+    int N, int K, int epi, int tiles_m, int tiles_n, KvOut kv, PlaneOut po, Batch bt, LnIo ln) {
   constexpr int NW = WGM * WGN, MI = BM / (32 * WGM), NI = BN / (32 * WGN);
   static_assert((NW == 4 || NW == 8) && MI >= 1 && NI >= 1, "4 or 8 waves");
   constexpr int ROWB = BKT * 2, CH = ROWB / 16, RPP = 1024 / ROWB, NSTEP = BKT / 16;
@@ -170,6 +150,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   static_assert(APW * NW * 1024 == TA && WPW * NW * 1024 == 2 * BN * ROWB, "equal DMA count per wave");
   constexpr int LPS = APW + WPW;
   static_assert((RS - 2) * LPS < 64, "vmcnt range");
+  static_assert(MODE == 0 || (BM == 128 && BN == 128 && NW == 4 && BKT == 32 && RS == 2 && !BATCHED),
+                "the LayerNorm hand-off runs the 128 x 128, 2 x 2 tile");
+  static_assert(MODE != 2 || BM * BN * 4 <= RS * STAGE, "the statistics tile fits the ring");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -178,11 +161,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   const int ntiles1 = tiles_m * tiles_n, ntiles = BATCHED ? ntiles1 * bt.nb : ntiles1;
   const int nk = K / BKT;
   nos::XcdChunk chunk;
-  if constexpr (ROWSPLIT) {  // this workgroup's row block: its tiles_n tiles in order
-    chunk.first = nos::xcd_remap(blockIdx.x, tiles_m) * tiles_n;
-    chunk.end = chunk.first + tiles_n;
-    chunk.step = 1;
-  } else if constexpr (PERSIST) {
+  if constexpr (PERSIST) {
     chunk = nos::xcd_chunk(blockIdx.x, gridDim.x, ntiles);
   } else {
     chunk.first = nos::xcd_remap(blockIdx.x, ntiles);
@@ -190,7 +169,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     chunk.step = 1;
   }
   for (int tt = chunk.first; tt < chunk.end; tt += chunk.step) {
-    if ((PERSIST || ROWSPLIT) && tt != chunk.first) __syncthreads();
+    if (PERSIST && tt != chunk.first) __syncthreads();
     const int bb = BATCHED ? tt / ntiles1 : 0, t1 = BATCHED ? tt - bb * ntiles1 : tt;
     const int tm = t1 / tiles_n, tn = t1 - tm * tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
@@ -203,7 +182,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     const float* __restrict__ Rb = BATCHED && R != nullptr ? R + bb * bt.r : R;
 
     // a 1 KiB piece = RPP rows x ROWB bytes of one plane; lane L: row L / CH, chunk L % CH
-    auto stage = [&](int k0, unsigned char* dst) {
+    auto stage_a = [&](int k0, unsigned char* dst) {
 #pragma unroll
       for (int i = 0; i < APW; ++i) {
         const int p = wid * APW + i;
@@ -214,6 +193,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         glds16(Ab + plane * aplane + (long long)g * lda + k0 + (((lane % CH) ^ swz<CH>(row)) << 3),
                dst + plane * BM * ROWB + rb * ROWB);
       }
+    };
+    auto stage_w = [&](int k0, unsigned char* dst) {
 #pragma unroll
       for (int i = 0; i < WPW; ++i) {
         const int p = wid * WPW + i;
@@ -224,6 +205,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         glds16(Wb + plane * wplane + (long long)g * ldw + k0 + (((lane % CH) ^ swz<CH>(row)) << 3),
                dst + TA + plane * BN * ROWB + rb * ROWB);
       }
+    };
+    auto stage = [&](int k0, unsigned char* dst) {
+      stage_a(k0, dst);
+      stage_w(k0, dst);
     };
 
     f32x16_t acc[MI][NI];
@@ -263,7 +248,90 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         for (int j = 0; j < NI; ++j) acc[i][j] = nos::mma3h(f.a[i], f.w[j], acc[i][j]);
     };
 
-    if constexpr (BKT == 32 && RS == 2) {
+    if constexpr (MODE == 1) {
+    // A = LayerNorm(X): thread t owns rows t/4 and 64 + t/4 of the tile and the
+    // 8-deep k chunk t%4 of each stage (one 16-byte piece per plane and row)
+    constexpr int AR = 2;
+    const int q = tid & 3;
+    float mul[AR], add[AR];
+    const float* xr[AR];
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      int g = m0 + (tid >> 2) + 64 * i;
+      g = g < M ? g : M - 1;
+      xr[i] = ln.x + (long long)g * ln.ldx + q * 8;
+      const float2* st = ln.sin + (long long)g * ln.nparts;
+      float n = 0.f, mean = 0.f, m2 = 0.f;
+      for (int p = 0; p < ln.nparts; ++p) {
+        const float2 v = st[p];
+        const int nb = min(ln.pw, K - p * ln.pw);
+        chan_merge(n, mean, m2, (float)nb, v.x, v.y);
+      }
+      mul[i] = rsqrtf(m2 / (float)K + ln.eps) * ln.sc;
+      add[i] = -mean * mul[i];
+    }
+    float4 xa[AR][2];
+    auto aload = [&](int k0) {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        xa[i][0] = *reinterpret_cast<const float4*>(xr[i] + k0);
+        xa[i][1] = *reinterpret_cast<const float4*>(xr[i] + k0 + 4);
+      }
+    };
+    auto awrite = [&](unsigned char* dst) {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const int row = (tid >> 2) + 64 * i;
+        const float4 u = xa[i][0], w = xa[i][1];
+        f16x2_t h0, l0, h1, l1, h2, l2, h3, l3;
+        nos::split2h(f32x2_t{fmaf(u.x, mul[i], add[i]), fmaf(u.y, mul[i], add[i])}, h0, l0);
+        nos::split2h(f32x2_t{fmaf(u.z, mul[i], add[i]), fmaf(u.w, mul[i], add[i])}, h1, l1);
+        nos::split2h(f32x2_t{fmaf(w.x, mul[i], add[i]), fmaf(w.y, mul[i], add[i])}, h2, l2);
+        nos::split2h(f32x2_t{fmaf(w.z, mul[i], add[i]), fmaf(w.w, mul[i], add[i])}, h3, l3);
+        const int off = row * ROWB + ((q ^ swz<CH>(row)) << 4);
+        *reinterpret_cast<f16x8_t*>(dst + off) = f16x8_t{h0.x, h0.y, h1.x, h1.y, h2.x, h2.y, h3.x, h3.y};
+        *reinterpret_cast<f16x8_t*>(dst + BM * ROWB + off) = f16x8_t{l0.x, l0.y, l1.x, l1.y, l2.x, l2.y, l3.x, l3.y};
+      }
+    };
+    aload(0);
+    stage_w(0, smem);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    awrite(smem);
+    if (nk > 1) {
+      aload(BKT);
+      stage_w(BKT, smem + STAGE);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    Frag fa, fb;
+    load(smem, 0, fa);
+    for (int kt = 0; kt < nk; ++kt) {
+      const unsigned char* cur = smem + (kt & 1) * STAGE;
+      load(cur, 1, fb);
+      mma(fa);
+      __builtin_amdgcn_sched_barrier(0);
+      // stage kt+1's A rows (registers) landed: normalised and split into the
+      // buffer every wave finished reading last iteration, under fa's MFMAs
+      if (kt + 1 < nk) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        awrite(smem + ((kt + 1) & 1) * STAGE);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mma(fb);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nk) {
+        // the barrier (stage kt+1 complete, stage kt read by every wave) waits under fb's MFMAs
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + 2 < nk) {
+          aload((kt + 2) * BKT);
+          stage_w((kt + 2) * BKT, smem + (kt & 1) * STAGE);
+        }
+        load(smem + ((kt + 1) & 1) * STAGE, 0, fa);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    } else if constexpr (BKT == 32 && RS == 2) {
     stage(0, smem);
     if (nk > 1) stage(BKT, smem + STAGE);
     if (nk > 1) {
@@ -323,7 +391,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     // offsets out of the tile loop and keep them live across the K loop (that
     // hoisting spilled the PERSIST variants: 200+ VGPRs to scratch)
     int c = c0, h = h0, ldc = ldc0, ldr = ldr0;
-    if constexpr (PERSIST || ROWSPLIT) {
+    if constexpr (PERSIST || MODE != 0) {
       asm volatile("" : "+v"(c), "+v"(h));
       asm volatile("" : "+s"(ldc), "+s"(ldr));
     }
@@ -336,6 +404,73 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         rsv[i][r] = rinvb != nullptr ? rinvb[m < M ? m : M - 1] : rconst;
         rbv[i][r] = (BATCHED && (epi & EPI_BIAS_ROW)) ? bias[m < M ? m : M - 1] : 0.f;
       }
+    if constexpr (MODE == 2) {
+      // (without sout: only the epilogue, plain fp32 C through LDS)
+      // the tile goes to C through LDS: act(acc scale + bias) in the MFMA
+      // layout into T (row stride BN), then threads 2r, 2r+1 take the two
+      // 64-column halves of row r (16-byte chunks in a per-lane rotation:
+      // conflict-free), add the residual, store C as float4 and reduce the
+      // row's (mean, M2) over the valid columns; Chan's merge of the halves
+      float* const T = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int cl = wn * (BN / WGN) + j * 32 + c;
+        const int nc = n0 + cl < N ? n0 + cl : N - 1;
+        const float cs = cscb[nc];
+        const float p2 = (epi & EPI_BIAS) ? bias[nc] : 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2);
+            if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+            if (epi & EPI_RELU) v = fmaxf(v, 0.f);
+            T[rl * BN + cl] = v;
+          }
+        }
+      }
+      __syncthreads();
+      const int rr = tid >> 1, hf = tid & 1, m = m0 + rr;
+      const int nv = m < M ? max(0, min(BN / 2, N - n0 - hf * (BN / 2))) : 0;
+      const float* tr = T + rr * BN + hf * (BN / 2);
+      const long long col0 = n0 + hf * (BN / 2);
+      float4 v[16];
+      float sum = 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int k = ((u + tid) & 15) * 4;
+        v[u] = *reinterpret_cast<const float4*>(tr + k);
+        if (k < nv) {
+          if (epi & EPI_RESID) {
+            const float4 q = *reinterpret_cast<const float4*>(Rb + (long long)m * ldr + col0 + k);
+            v[u].x += q.x;
+            v[u].y += q.y;
+            v[u].z += q.z;
+            v[u].w += q.w;
+          }
+          *reinterpret_cast<float4*>(Cb + (long long)m * ldc + col0 + k) = v[u];
+          sum += (v[u].x + v[u].y) + (v[u].z + v[u].w);
+        }
+      }
+      const float mean = nv > 0 ? sum / (float)nv : 0.f;
+      float m2 = 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int k = ((u + tid) & 15) * 4;
+        if (k < nv) {
+          const float d0 = v[u].x - mean, d1 = v[u].y - mean, d2 = v[u].z - mean, d3 = v[u].w - mean;
+          m2 = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, m2))));
+        }
+      }
+      float n = (float)nv, mu = mean;
+      const float on = __shfl_xor(n, 1, 64), omu = __shfl_xor(mu, 1, 64), om2 = __shfl_xor(m2, 1, 64);
+      if (ln.sout != nullptr && hf == 0 && n + on > 0.f) {
+        chan_merge(n, mu, m2, on, omu, om2);
+        ln.sout[(long long)m * ln.spart + tn] = float2{mu, m2};
+      }
+      continue;
+    }
     // interior tile stored as fp32 C (the common case): tile-local 32-bit
     // offsets from wave-uniform base pointers (saddr stores, no 64-bit
     // address math per element) and no bounds tests
@@ -452,39 +587,27 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
       }
     }
   }  // tiles
-  if constexpr (ROWSPLIT) {
-    // every wave's C stores of the row block are done and visible to the workgroup
-    __syncthreads();
-    const int m0 = (chunk.first / tiles_n) * BM;
-    const int hw = tid >> 5, l32 = tid & 31;
-    for (int r = hw; r < BM; r += NW * 2) {
-      const int m = m0 + r;
-      if (m < M)
-        ln_split_row(C + (long long)m * ldc0, N, lo.p + (long long)m * lo.ldp, lo.p + lo.pplane + (long long)m * lo.ldp,
-                     lo.rinv + m, lo.eps, lo.eln, l32);
-    }
-  }
 }
 
-template <int BM, int BN, int WGM, int WGN, int BKT = 32, int RS = 2, bool BATCHED = false>
+template <int BM, int BN, int WGM, int WGN, int BKT = 32, int RS = 2, bool BATCHED = false, int MODE = 0>
 int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, float rconst, const _Float16* Wp,
              int ldw, long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C, int ldc,
-             int M, int N, int K, int epi, KvOut kv, PlaneOut po, Batch bt, hipStream_t st) {
+             int M, int N, int K, int epi, KvOut kv, PlaneOut po, Batch bt, hipStream_t st, LnIo ln = LnIo{}) {
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
   const long long ntiles = (long long)tiles_m * tiles_n * bt.nb;
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
   const size_t lds = RS * (size_t)(2 * BM * BKT * 2 + 2 * BN * BKT * 2);
   constexpr int NT = 64 * WGM * WGN;
   const int grid =
-      nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS, false, BATCHED>, NT, lds, ntiles);
+      nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS, MODE, BATCHED>, NT, lds, ntiles);
   if (grid < ntiles)
-    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS, false, BATCHED>), dim3((unsigned)grid),
+    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS, MODE, BATCHED>), dim3((unsigned)grid),
                        dim3(NT), lds, st, Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
-                       N, K, epi, tiles_m, tiles_n, kv, po, bt, LnOut{});
+                       N, K, epi, tiles_m, tiles_n, kv, po, bt, ln);
   else
-    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false, BKT, RS, false, BATCHED>), dim3((unsigned)ntiles),
+    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false, BKT, RS, MODE, BATCHED>), dim3((unsigned)ntiles),
                        dim3(NT), lds, st, Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
-                       N, K, epi, tiles_m, tiles_n, kv, po, bt, LnOut{});
+                       N, K, epi, tiles_m, tiles_n, kv, po, bt, ln);
   return (int)hipGetLastError();
 }
 
@@ -495,6 +618,9 @@ int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, f
 // (4 x 1: 10 KiB); 28-tenant fleet 679.9 / 679.8 vs 679.0 / 676.2 inf/s,
 // the deeper rings 605-635 (profiles/r04_h3_layout_ab.json)
 int g_layout = 1;
+// plain fp32-C GEMMs (no KV / plane output, N % 4 == 0, aligned C / R) through
+// the LDS epilogue of MODE 2 (float4 stores and residual loads along rows)
+bool g_lds_epi = false;
 
 // ------------------------------------------------------------ row split
 // LPR lanes per row (64: a wave; 32: a half-wave, two rows per wave), the
@@ -603,7 +729,50 @@ __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restr
   if (lane == 0) rinv[row] = nos::pow2i(-e);
 }
 
+// per-row (mean, M2) of fp32 rows over all K columns (one statistics part): a
+// half-wave per row, the row read twice (the second pass from cache)
+__global__ __launch_bounds__(256) void row_stats_kernel(const float* __restrict__ X, int ldx, float2* __restrict__ out,
+                                                        int M, int K) {
+  const int row = blockIdx.x * 8 + (int)(threadIdx.x >> 5), lane = threadIdx.x & 31;
+  if (row >= M) return;  // whole half-waves
+  const float* x = X + (long long)row * ldx;
+  float s = 0.f;
+  for (int k = lane * 4; k < K; k += 128) {
+    const float4 v = *reinterpret_cast<const float4*>(x + k);
+    s += (v.x + v.y) + (v.z + v.w);
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mu = s / (float)K;
+  float q = 0.f;
+  for (int k = lane * 4; k < K; k += 128) {
+    const float4 v = *reinterpret_cast<const float4*>(x + k);
+    const float d0 = v.x - mu, d1 = v.y - mu, d2 = v.z - mu, d3 = v.w - mu;
+    q = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, q))));
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  if (lane == 0) out[row] = float2{mu, q};
+}
+
 }  // namespace
+
+// (mean, M2) of every fp32 row of X [M, K] (row stride ldx) into stats [M]
+// (float2): the statistics input of nos_gemm_f32h3_lna (nparts 1, pw K) when
+// the producer of X is not an h3 GEMM.  K % 4 == 0, rows 16-byte aligned.
+NOS_API int nos_row_stats(const float* X, int ldx, void* stats, int M, int K, hipStream_t stream) {
+  if (M <= 0 || K <= 0 || (K % 4) || (ldx % 4) || ldx < K || !X || !stats || (((uintptr_t)X) & 15) ||
+      (((uintptr_t)stats) & 7))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_stats_kernel, dim3((unsigned)((M + 7) / 8)), dim3(256), 0, stream, X, ldx,
+                     static_cast<float2*>(stats), M, K);
+  return (int)hipGetLastError();
+}
+
+NOS_API int nos_gemm_f32h3_set_lds_epilogue(int on) {
+  g_lds_epi = on != 0;
+  return 0;
+}
 
 NOS_API int nos_gemm_f32h3_set_layout(int layout) {
   if (layout < 0 || layout > 5) return (int)hipErrorInvalidValue;
@@ -665,9 +834,14 @@ int run_h3(const void* Ap, int lda, long long aplane, const float* rinv, float r
   if (g_layout == 2)
     return launch_t<256, 128, 4, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
                                     epi, kv, po, bt, stream);
-  if (g_layout == 1)
+  if (g_layout == 1) {
+    if (g_lds_epi && kv.kvs == nullptr && po.p == nullptr && C != nullptr && !(N % 4) && !(ldc % 4) &&
+        !(((uintptr_t)C) & 15) && (!(epi & EPI_RESID) || (!(ldr % 4) && !(((uintptr_t)R) & 15))))
+      return launch_t<128, 128, 2, 2, 32, 2, false, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr,
+                                                       C, ldc, M, N, K, epi, kv, po, bt, stream);
     return launch_t<128, 128, 2, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
                                     epi, kv, po, bt, stream);
+  }
   return launch_t<128, 128, 4, 1>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
                                   epi, kv, po, bt, stream);
 }
@@ -754,40 +928,84 @@ NOS_API int nos_gemm_f32h3_batched(const void* Ap, int lda, long long aplane, lo
                 PlaneOut{}, bt, stream, true);
 }
 
-// C = act(rinv[m] csc[n] (A' . W'^T) + bias) + R (a pre-LN residual GEMM,
-// nos_gemm_f32h3's contract without the KV / plane outputs), and the rows of
-// C LayerNorm-normalised (eps; no gamma / beta: those are folded into the
-// next GEMM) as that GEMM's h3 A planes P ([2][M][ldp], plane stride pplane)
-// on the scale 2^eln, rinv_out[m] = 2^-eln -- nos_split_rows_h3's LN mode
-// fused: one workgroup per 128-row block runs the block's tiles, then splits
-// its rows.  N % 4 == 0, K % 32 == 0.
-NOS_API int nos_gemm_f32h3_ln_out(const void* Ap, int lda, long long aplane, const float* rinv, float rconst,
-                                  const void* Wp, int ldw, long long wplane, const float* csc, const float* bias,
-                                  const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi, void* P,
-                                  int ldp, long long pplane, float* rinv_out, float eps, int eln, hipStream_t stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0 || (N % 4) || !C || ldc < N || (ldc % 4)) return (int)hipErrorInvalidValue;
+// nos_gemm_f32h3's plain contract (fp32 C, no KV / plane outputs; N % 4 == 0,
+// C / R rows 16-byte aligned) plus the row statistics of the finished C for
+// the LayerNorm of the next GEMM:
+// stats[m][tn] = (mean, sum of squared deviations) of C[m, 128 tn .. 128 tn + 127]
+// (the valid columns), ceil(N / 128) parts per row -- nos_gemm_f32h3_lna's input.
+NOS_API int nos_gemm_f32h3_stats(const void* Ap, int lda, long long aplane, const float* rinv, float rconst,
+                                 const void* Wp, int ldw, long long wplane, const float* csc, const float* bias,
+                                 const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi, void* stats,
+                                 hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0 || !C || ldc < N || !stats || (N % 4) || (ldc % 4) ||
+      (((uintptr_t)C) & 15))
+    return (int)hipErrorInvalidValue;
+  if ((epi & EPI_RESID) && ((ldr % 4) || (((uintptr_t)R) & 15))) return (int)hipErrorInvalidValue;
   if ((lda % 8) || (ldw % 8) || lda < K || ldw < K || aplane < (long long)M * lda || wplane < (long long)N * ldw)
     return (int)hipErrorInvalidValue;
-  if ((((uintptr_t)Ap) | ((uintptr_t)Wp) | ((uintptr_t)C)) & 15) return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)Ap) | ((uintptr_t)Wp)) & 15 || (((uintptr_t)stats) & 7)) return (int)hipErrorInvalidValue;
   if ((!rinv && !(rconst > 0.f)) || !csc || ((epi & EPI_BIAS) && !bias) || ((epi & EPI_RESID) && (!R || ldr < N)) ||
       (epi & (EPI_BIAS_ROW | EPI_RESID_PRE)))
     return (int)hipErrorInvalidValue;
-  if (!P || !rinv_out || ldp < N || (ldp % 4) || pplane < (long long)M * ldp || (((uintptr_t)P) & 7) || !(eps >= 0.f) ||
-      eln < -126 || eln > 126)
+  LnIo ln;
+  ln.sout = static_cast<float2*>(stats);
+  ln.spart = (N + 127) / 128;
+  return launch_t<128, 128, 2, 2, 32, 2, false, 2>(static_cast<const _Float16*>(Ap), lda, aplane, rinv, rconst,
+                                                   static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
+                                                   C, ldc, M, N, K, epi, KvOut{}, PlaneOut{}, Batch{}, stream, ln);
+}
+
+// C = act(2^-eln csc[n] (LN(X)' . W'^T) + bias) with LN(X)' = (X - mean) rstd
+// 2^eln split into h3 planes inside the GEMM (no nos_split_rows_h3 pass): X
+// fp32 [M, K] (row stride ldx, 16-byte aligned rows), its row statistics
+// stats [M][nparts] = (mean, M2) over parts of pw columns (nos_gemm_f32h3_stats:
+// pw 128; nos_row_stats: one part of K), rstd = 1 / sqrt(M2 / K + eps);
+// LayerNorm's gamma / beta folded into W and bias.  The KV / plane outputs of
+// nos_gemm_f32h3.  K % 32 == 0.
+NOS_API int nos_gemm_f32h3_lna(const float* X, int ldx, const void* stats, int nparts, int pw, float eps, int eln,
+                               const void* Wp, int ldw, long long wplane, const float* csc, const float* bias,
+                               const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi, void* kvs,
+                               int S, int skvp, const float* kvsc, void* P, int ldp, long long pplane, float psc,
+                               hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || (K % BK) != 0 || !X || (ldx % 4) || ldx < K || !stats || nparts <= 0 || pw <= 0 ||
+      (long long)nparts * pw < K || (long long)(nparts - 1) * pw >= K)
     return (int)hipErrorInvalidValue;
-  LnOut lo;
-  lo.p = static_cast<_Float16*>(P);
-  lo.pplane = pplane;
-  lo.ldp = ldp;
-  lo.rinv = rinv_out;
-  lo.eps = eps;
-  lo.eln = eln;
-  constexpr int BM = 128, BN = 128;
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
-  constexpr size_t lds = 2 * (size_t)(2 * BM * 32 * 2 + 2 * BN * 32 * 2);
-  hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, 2, 2, false, 32, 2, true>), dim3((unsigned)tiles_m), dim3(256), lds,
-                     stream, static_cast<const _Float16*>(Ap), lda, aplane, rinv, rconst,
-                     static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, tiles_m,
-                     tiles_n, KvOut{}, PlaneOut{}, Batch{}, lo);
-  return (int)hipGetLastError();
+  if ((ldw % 8) || ldw < K || wplane < (long long)N * ldw || (((uintptr_t)Wp) & 15) || (((uintptr_t)X) & 15) ||
+      (((uintptr_t)stats) & 7))
+    return (int)hipErrorInvalidValue;
+  if (!csc || ((epi & EPI_BIAS) && !bias) || ((epi & EPI_RESID) && (!R || ldr < N)) ||
+      (epi & (EPI_BIAS_ROW | EPI_RESID_PRE)) || !(eps >= 0.f) || eln < -126 || eln > 126)
+    return (int)hipErrorInvalidValue;
+  KvOut kv;
+  PlaneOut po;
+  if (kvs != nullptr) {
+    if (!kvsc || N % 3 || (N / 3) % 64 || S <= 0 || M % S || skvp < S || (((uintptr_t)kvs) & 15) || P)
+      return (int)hipErrorInvalidValue;
+    kv.kvs = static_cast<unsigned short*>(kvs);
+    kv.kvsc = kvsc;
+    kv.hd = N / 3;
+    kv.qcols = kv.hd;
+    kv.S = S;
+    kv.skvp = skvp;
+  }
+  if (P != nullptr) {
+    if (ldp < N || pplane < (long long)M * ldp || !(psc > 0.f)) return (int)hipErrorInvalidValue;
+    po.p = static_cast<unsigned short*>(P);
+    po.ldp = ldp;
+    po.pplane = pplane;
+    po.sc = psc;
+  } else if (!C || ldc < (kvs != nullptr ? N / 3 : N)) {
+    return (int)hipErrorInvalidValue;
+  }
+  LnIo ln;
+  ln.x = X;
+  ln.ldx = ldx;
+  ln.sin = static_cast<const float2*>(stats);
+  ln.nparts = nparts;
+  ln.pw = pw;
+  ln.eps = eps;
+  ln.sc = ldexpf(1.f, eln);
+  return launch_t<128, 128, 2, 2, 32, 2, false, 1>(nullptr, K, (long long)M * K, nullptr, ldexpf(1.f, -eln),
+                                                   static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
+                                                   C, ldc, M, N, K, epi, kv, po, Batch{}, stream, ln);
 }

@@ -62,19 +62,19 @@ def attention_ref(q, k, v, scale=None):
 # ---------------------------------------------------------------- dispatchers
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
            act: str | None = None, residual: torch.Tensor | None = None,
-           out: torch.Tensor | None = None, max_wg: int = 0, ln_eps: float | None = None):
+           out: torch.Tensor | None = None, max_wg: int = 0, row_stats: bool = False):
     """y = act(x @ weight^T + bias) + residual; x [..., K], weight [N, K].
-    ``ln_eps`` (fp32 under h3 math): also return y's LayerNorm-normalised
-    planes for the next LN-GEMM, ``(y, H3Planes)`` (:func:`linear_planes`)."""
-    if ln_eps is not None:
+    ``row_stats`` (fp32 under h3 math): also return y's row statistics for
+    the next LN-GEMM, ``(y, RowStats)`` (:func:`linear_planes`)."""
+    if row_stats:
         if not (x.is_cuda and x.dtype == torch.float32 and _F32_MATH == "h3"):
-            raise ValueError("ln_eps needs an fp32 CUDA input under h3 math")
+            raise ValueError("row_stats needs an fp32 CUDA input under h3 math")
         K = x.shape[-1]
         x2 = x.reshape(-1, K)
         if x2.stride(-1) != 1 or K % 32:
-            raise ValueError("ln_eps needs unit inner stride and K % 32 == 0")
+            raise ValueError("row_stats needs unit inner stride and K % 32 == 0")
         ap, rinv = _split_rows_h3(x2, ln=False)
-        return linear_planes(H3Planes(ap, rinv, 0.0, tuple(x.shape)), weight, bias, act, residual, ln_eps=ln_eps)
+        return linear_planes(H3Planes(ap, rinv, 0.0, tuple(x.shape)), weight, bias, act, residual, row_stats=True)
     if not x.is_cuda:
         return linear_ref(x, weight, bias, act, residual)
     K = x.shape[-1]
@@ -270,12 +270,20 @@ def _h3_out_scale(wg: torch.Tensor, c2: torch.Tensor, act: str | None) -> float:
     return sc
 
 
+class RowStats(NamedTuple):
+    """LayerNorm statistics of an fp32 activation [M, K] handed from its
+    producer GEMM to the LN-GEMM after it: ``stats`` [M, nparts, 2] = (mean,
+    sum of squared deviations) over parts of ``pw`` columns."""
+    stats: torch.Tensor
+    pw: int
+
+
 def linear_planes(a: H3Planes, weight: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
-                  residual: torch.Tensor | None = None, ln_eps: float | None = None):
+                  residual: torch.Tensor | None = None, row_stats: bool = False):
     """act(A @ weight^T + bias) + residual for an A handed over as h3 planes
     (see :class:`H3Planes`): no split pre-pass, no fp32 round trip of A.
-    ``ln_eps``: also return the output LayerNorm-normalised as the next
-    LN-GEMM's planes (:func:`_gemm_h3_ln_out`) -- ``(out, H3Planes)``."""
+    ``row_stats``: also return the output's row statistics for the next
+    LN-GEMM (``nos_gemm_f32h3_stats``) -- ``(out, RowStats)``."""
     M, K = a.planes.shape[1], a.planes.shape[2]
     N = weight.shape[0]
     if weight.dim() != 2 or weight.shape[1] != K or weight.dtype != torch.float32 or weight.stride(-1) != 1:
@@ -288,39 +296,65 @@ def linear_planes(a: H3Planes, weight: torch.Tensor, bias: torch.Tensor | None =
             raise ValueError(f"residual must be fp32 [{M}, {N}]")
         r2 = residual.reshape(M, N)
         _check_f32(residual=r2)
-    if ln_eps is not None:
-        lnp = _gemm_h3_ln_out(a.planes, a.rinv, a.rconst, weight, bias, r2, out, _epi(bias, act, residual), ln_eps)
-        return out.view(*a.shape[:-1], N), H3Planes(lnp[0], lnp[1], 0.0, (*a.shape[:-1], N))
+    if row_stats:
+        wp, csc = split_f32_weight_h3(weight)
+        st = torch.empty((M, (N + 127) // 128, 2), dtype=torch.float32, device=out.device)
+        rc = _lib.lib().nos_gemm_f32h3_stats(a.planes.data_ptr(), K, M * K, _ptr(a.rinv), float(a.rconst),
+                                             wp.data_ptr(), K, N * K, csc.data_ptr(), _ptr(bias), _ptr(r2),
+                                             r2.stride(0) if r2 is not None else 0, out.data_ptr(), N, M, N, K,
+                                             _epi(bias, act, residual), st.data_ptr(), _stream())
+        _lib.check(rc, "nos_gemm_f32h3_stats")
+        return out.view(*a.shape[:-1], N), RowStats(st, 128)
     _gemm_h3(a.planes, a.rinv, weight, bias, r2, out, _epi(bias, act, residual), rconst=a.rconst)
     return out.view(*a.shape[:-1], N)
 
 
-def _gemm_h3_ln_out(ap, rinv, rconst: float, weight, bias, r2, o2, epi: int, eps: float):
-    """:func:`_gemm_h3` whose workgroups also split their finished rows of
-    ``o2`` LayerNorm-normalised into the next GEMM's A planes
-    (``nos_gemm_f32h3_ln_out``): returns (planes [2, M, N], rinv [M])."""
-    M, K = ap.shape[1], ap.shape[2]
-    N = weight.shape[0]
-    wp, csc = split_f32_weight_h3(weight)
-    planes = torch.empty((2, M, N), dtype=torch.float16, device=o2.device)
-    rin = torch.empty((M,), dtype=torch.float32, device=o2.device)
-    eln = 14 - math.frexp(math.sqrt(N))[1]
-    rc = _lib.lib().nos_gemm_f32h3_ln_out(ap.data_ptr(), K, M * K, _ptr(rinv), float(rconst), wp.data_ptr(), K, N * K,
-                                          csc.data_ptr(), _ptr(bias), _ptr(r2), r2.stride(0) if r2 is not None else 0,
-                                          o2.data_ptr(), o2.stride(0), M, N, K, epi, planes.data_ptr(), N, M * N,
-                                          rin.data_ptr(), float(eps), eln, _stream())
-    _lib.check(rc, "nos_gemm_f32h3_ln_out")
-    return planes, rin
+def _row_stats(x2: torch.Tensor) -> RowStats:
+    """(mean, M2) of every row of fp32 x2 [M, K] in one part (``nos_row_stats``):
+    the LN-GEMM's statistics when no h3 GEMM produced x2."""
+    M, K = x2.shape
+    st = torch.empty((M, 1, 2), dtype=torch.float32, device=x2.device)
+    _lib.check(_lib.lib().nos_row_stats(x2.data_ptr(), x2.stride(0), st.data_ptr(), M, K, _stream()), "nos_row_stats")
+    return RowStats(st, K)
+
+
+def _lna_ok(x2: torch.Tensor) -> bool:
+    return x2.stride(1) == 1 and x2.stride(0) % 4 == 0 and x2.data_ptr() % 16 == 0
+
+
+def _gemm_ln_h3(x2: torch.Tensor, pre, eps: float, wg: torch.Tensor, c2: torch.Tensor, o2, epi: int, kv=None,
+                planes_out=None) -> None:
+    """act(LayerNorm(x2) @ wg^T + c2) under h3 math (LN's gamma / beta folded
+    into wg / c2).  With the LN hand-off on (:func:`set_ln_handoff`) the GEMM
+    normalises and splits x2 itself, K-slice by K-slice
+    (``nos_gemm_f32h3_lna``), from the row statistics its producer wrote
+    (``pre``: :class:`RowStats`) or ``nos_row_stats``; otherwise the split
+    pre-pass writes x2's normalised planes first (``nos_split_rows_h3``)."""
+    M, K = x2.shape
+    N = wg.shape[0]
+    if _LN_HANDOFF and _lna_ok(x2):
+        st = pre if isinstance(pre, RowStats) else _row_stats(x2)
+        wp, csc = split_f32_weight_h3(wg)
+        kvs, S, skvp, kvsc = kv if kv is not None else (None, 0, 0, None)
+        pp, psc = planes_out if planes_out is not None else (None, 1.0)
+        eln = 14 - math.frexp(math.sqrt(K))[1]
+        rc = _lib.lib().nos_gemm_f32h3_lna(x2.data_ptr(), x2.stride(0), st.stats.data_ptr(), st.stats.shape[1], st.pw,
+                                           float(eps), eln, wp.data_ptr(), K, N * K, csc.data_ptr(), c2.data_ptr(),
+                                           None, 0, _ptr(o2), o2.stride(0) if o2 is not None else N, M, N, K, epi,
+                                           _ptr(kvs), S, skvp, _ptr(kvsc), _ptr(pp), N, M * N, float(psc), _stream())
+        _lib.check(rc, "nos_gemm_f32h3_lna")
+        return
+    ap, rinv = (pre.planes, pre.rinv) if isinstance(pre, H3Planes) else _split_rows_h3(x2, ln=True, eps=eps)
+    _gemm_h3(ap, rinv, wg, c2, None, o2, epi, kv=kv, planes_out=planes_out)
 
 
 _LN_HANDOFF = False
 
 
 def set_ln_handoff(on: bool) -> None:
-    """Pre-LN residual GEMMs hand the next LN-GEMM its LayerNorm-normalised
-    A planes from their own workgroups (``nos_gemm_f32h3_ln_out``: no
-    ``nos_split_rows_h3`` launch) -- the fractional-pod config; a whole-GPU
-    tenant keeps the separate pass (the row-owning grid is 3x smaller)."""
+    """LayerNorm hand-off under h3 math: the LN-GEMMs normalise and split
+    their fp32 input inside the GEMM (no ``nos_split_rows_h3`` pass), from
+    row statistics the pre-LN residual GEMM wrote in its epilogue."""
     global _LN_HANDOFF
     _LN_HANDOFF = bool(on)
 
@@ -330,7 +364,7 @@ def ln_handoff_active() -> bool:
 
 
 def linear_ln_to_planes(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor,
-                        act: str | None = None, eps: float = 1e-12, pre: H3Planes | None = None) -> H3Planes:
+                        act: str | None = None, eps: float = 1e-12, pre=None) -> H3Planes:
     """:func:`linear_ln` under h3 math whose output goes straight to the next
     GEMM's A planes on the static scale of :func:`_h3_out_scale` (fc1 -> fc2)."""
     if _F32_MATH != "h3" or not x.is_cuda or x.dtype != torch.float32:
@@ -342,10 +376,9 @@ def linear_ln_to_planes(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2:
     if K % 32:
         raise ValueError("linear_ln_to_planes needs K % 32 == 0")
     M = x2.shape[0]
-    ap, rinv = (pre.planes, pre.rinv) if pre is not None else _split_rows_h3(x2, ln=True, eps=eps)
     sc = _h3_out_scale(wg, c2, act)
     planes = torch.empty((2, M, N), dtype=torch.float16, device=x.device)
-    _gemm_h3(ap, rinv, wg, c2, None, None, EPI_BIAS | _epi(None, act, None), planes_out=(planes, sc))
+    _gemm_ln_h3(x2, pre, eps, wg, c2, None, EPI_BIAS | _epi(None, act, None), planes_out=(planes, sc))
     return H3Planes(planes, None, 1.0 / sc, (*x.shape[:-1], N))
 
 
@@ -387,6 +420,13 @@ def set_gemm_f32x6_tile(tile: str) -> None:
     names = {"policy": -1, "128x64": 3, "128x128": 5, "wide": 6, "256x128": 7}  # wide: 128x128 if N >= 1024, else 128x64
     code = names[tile] if tile in names else int(tile)  # numeric codes: gemm_f32x.hip g_tile (A/B)
     _lib.check(_lib.lib().nos_gemm_f32x6_set_tile(code), "nos_gemm_f32x6_set_tile")
+
+
+def set_gemm_f32h3_lds_epilogue(on: bool) -> None:
+    """Plain fp32-C h3 GEMMs store C through LDS (float4 row stores and
+    residual loads, the LN hand-off producer's epilogue) instead of one dword
+    per element in the MFMA layout."""
+    _lib.check(_lib.lib().nos_gemm_f32h3_set_lds_epilogue(int(bool(on))), "nos_gemm_f32h3_set_lds_epilogue")
 
 
 def set_gemm_f32h3_layout(layout: str) -> None:
@@ -554,9 +594,9 @@ def linear_ln_ref(x, wg, c1, c2, act=None, eps=1e-12):
 
 def linear_ln(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, act: str | None = None,
               eps: float = 1e-12, out: torch.Tensor | None = None, max_wg: int = 0,
-              pre: H3Planes | None = None) -> torch.Tensor:
+              pre=None) -> torch.Tensor:
     """act(LayerNorm(x) @ W^T + b) with LN folded by :func:`fold_layernorm`
-    (``pre``: x's LN-normalised planes, already made by its producer)."""
+    (``pre``: x's row statistics, :class:`RowStats`, from its producer)."""
     if not x.is_cuda:
         return linear_ln_ref(x, wg, c1, c2, act, eps)
     K = x.shape[-1]
@@ -569,8 +609,7 @@ def linear_ln(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Ten
             raise ValueError("native fp32 linear_ln needs K % 32 == 0")
         o2, _ = _gemm_io(x, wg, out, None, M, N, K)
         if _F32_MATH == "h3":
-            ap, rinv = (pre.planes, pre.rinv) if pre is not None else _split_rows_h3(x2, ln=True, eps=eps)
-            _gemm_h3(ap, rinv, wg, c2, None, o2, EPI_BIAS | _epi(None, act, None))
+            _gemm_ln_h3(x2, pre, eps, wg, c2, o2, EPI_BIAS | _epi(None, act, None))
         elif _F32_MATH == "x6":
             wp = split_f32_weight(wg)
             rc = _lib.lib().nos_gemm_ln_f32x6(x2.data_ptr(), x2.stride(0), wp.data_ptr(), wp.stride(1), wp.stride(0),
@@ -760,7 +799,7 @@ _H3_SCALES_HOST: dict[int, torch.Tensor] = {}
 
 
 def linear_ln_qkv_h3(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, num_heads: int,
-                     eps: float = 1e-12, pre: H3Planes | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+                     eps: float = 1e-12, pre=None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """:func:`linear_ln_qkv_x6` writing the fp16x3 attention's planes (K and V
     as fp16 hi / lo pieces on the per-head scales of :func:`h3_head_scales`):
     returns (qkv with valid Q columns, workspace, scales) for
@@ -781,8 +820,7 @@ def linear_ln_qkv_h3(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: to
     skvp = (S + 31) // 32 * 32
     sc = h3_head_scales(wg, c2, num_heads)
     if _F32_MATH == "h3":
-        ap, rinv = (pre.planes, pre.rinv) if pre is not None else _split_rows_h3(x2, ln=True, eps=eps)
-        _gemm_h3(ap, rinv, wg, c2, None, out.view(M, N), EPI_BIAS, kv=(ws, S, skvp, sc))
+        _gemm_ln_h3(x2, pre, eps, wg, c2, out.view(M, N), EPI_BIAS, kv=(ws, S, skvp, sc))
         return out, ws, sc
     wp = split_f32_weight(wg)
     rc = L.nos_gemm_ln_f32x6_qkv_h3(x2.data_ptr(), x2.stride(0), wp.data_ptr(), wp.stride(1), wp.stride(0),
@@ -839,7 +877,7 @@ def ln_qkv_fusable(x: torch.Tensor) -> bool:
 
 
 def ln_qkv_attention(x: torch.Tensor, wg: torch.Tensor, c1: torch.Tensor, c2: torch.Tensor, num_heads: int,
-                     eps: float = 1e-12, planes_out: bool = False, pre: H3Planes | None = None,
+                     eps: float = 1e-12, planes_out: bool = False, pre=None,
                      q_range: tuple[int, int] | None = None):
     """attention(LayerNorm(x) @ W_qkv^T + b) for an fp32 pod (see
     :func:`ln_qkv_fusable`): the QKV projection writes the attention's K / V

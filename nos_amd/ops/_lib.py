@@ -96,9 +96,14 @@ _SIGS = {
     "nos_im2col_h3": [c_void_p, c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nos_attn_h3g_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
-    "nos_gemm_f32h3_ln_out": [c_void_p, c_int, c_ll, c_void_p, c_float, c_void_p, c_int, c_ll, c_void_p, c_void_p,
-                              c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_ll,
-                              c_void_p, c_float, c_int, c_void_p],
+    # LayerNorm hand-off (gemm_f32h.hip): producer row statistics, LN in the consumer's A load
+    "nos_gemm_f32h3_stats": [c_void_p, c_int, c_ll, c_void_p, c_float, c_void_p, c_int, c_ll, c_void_p, c_void_p,
+                             c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "nos_gemm_f32h3_lna": [c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_int, c_void_p, c_int, c_ll, c_void_p,
+                           c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                           c_int, c_void_p, c_void_p, c_int, c_ll, c_float, c_void_p],
+    "nos_row_stats": [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p],
+    "nos_gemm_f32h3_set_lds_epilogue": [c_int],
     "nos_attn_h3g_set_kvsplit": [c_int],
     "nos_attn_h3g": [c_void_p, c_int, c_ll, c_void_p, c_int, c_ll, c_void_p, c_int, c_ll, c_void_p, c_int, c_ll,
                      c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_float, c_void_p,

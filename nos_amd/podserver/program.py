@@ -1239,24 +1239,23 @@ class CompiledProgram:
         return steps
 
     def _mark_ln_handoffs(self, steps: list[_Step]) -> list[_Step]:
-        """A pre-LN residual GEMM (fp32 linear + residual) whose output the next
-        LN-GEMM (``linear_ln`` / ``ln_qkv_attention``) normalises may, under h3
-        math with ``ops.set_ln_handoff``, hand over that LN's A planes from its
-        own workgroups (``nos_gemm_f32h3_ln_out``): marked here with the
-        consumer's eps, decided per run."""
+        """A pre-LN residual GEMM (fp32 linear + residual) whose output exactly
+        one LN-GEMM (``linear_ln`` / ``ln_qkv_attention``) normalises writes,
+        under h3 math with ``ops.set_ln_handoff``, that output's row statistics
+        in its epilogue (``nos_gemm_f32h3_stats``); the LN-GEMM then applies
+        the LayerNorm in its own A load (``nos_gemm_f32h3_lna``) -- no split
+        pass.  Marked here, decided per run."""
         by_out = {s.output: s for s in steps}
-        eps_of: dict[str, set] = {}
+        consumers: dict[str, int] = {}
         for s in steps:
             if s.kind in ("linear_ln", "ln_qkv_attention") and s.inputs[0] in by_out:
-                eps_of.setdefault(s.inputs[0], set()).add(s.attrs.get("eps", 1e-12))
+                consumers[s.inputs[0]] = consumers.get(s.inputs[0], 0) + 1
         n = 0
-        for name, eps in eps_of.items():
+        for name, k in consumers.items():
             p = by_out[name]
-            if (p.kind == "linear" and p.attrs.get("residual") and len(eps) == 1 and self._dtype(name) == "fp32"
-                    and self._shape(name)[-1] % 4 == 0 and sum(1 for s in steps if s.kind in
-                                                              ("linear_ln", "ln_qkv_attention")
-                                                              and s.inputs[0] == name) == 1):
-                p.attrs["ln_out"] = next(iter(eps))
+            if (p.kind == "linear" and p.attrs.get("residual") and k == 1 and self._dtype(name) == "fp32"
+                    and self._shape(name)[-1] % 32 == 0):
+                p.attrs["row_stats"] = True
                 n += 1
         self.stats["ln_handoffs"] = n
         return steps
@@ -1296,21 +1295,19 @@ class CompiledProgram:
             k = s.kind
             if k == "linear":
                 res = a.pop() if s.attrs.get("residual") else None
-                ln_eps = s.attrs.get("ln_out")
-                if ln_eps is not None and not (ops.ln_handoff_active() and (isinstance(a[0], ops.H3Planes) or (
-                        a[0].is_cuda and a[0].dtype.itemsize == 4))):
-                    ln_eps = None
+                rs = bool(s.attrs.get("row_stats")) and ops.ln_handoff_active() and (
+                    isinstance(a[0], ops.H3Planes) or (a[0].is_cuda and a[0].dtype.itemsize == 4))
                 if isinstance(a[0], ops.H3Planes):
                     y = ops.linear_planes(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
-                                          residual=res, ln_eps=ln_eps)
+                                          residual=res, row_stats=rs)
                 else:
                     y = ops.linear(a[0].contiguous(), a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
-                                   residual=res, ln_eps=ln_eps)
-                if ln_eps is not None:
+                                   residual=res, row_stats=rs)
+                if rs:
                     y, env[s.output + "::lnp"] = y
             elif k == "linear_ln":
                 xx = a[0].contiguous()
-                pre = env.pop(s.inputs[0] + "::lnp", None)  # its producer's LN planes (_mark_ln_handoffs)
+                pre = env.pop(s.inputs[0] + "::lnp", None)  # its producer's row statistics (_mark_ln_handoffs)
                 if (s.attrs.get("planes_out") and xx.is_cuda and xx.dtype.itemsize == 4
                         and ops.h3_planes_active()):
                     y = ops.linear_ln_to_planes(xx, a[1], a[2], a[3], act=s.attrs.get("act"), eps=s.attrs["eps"],

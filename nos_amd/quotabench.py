@@ -91,6 +91,11 @@ class RecordingRuntime:
         with self.lock:
             return {k for k, t in self.tenants.items() if t.t_stop is None and t.t_ready is not None}
 
+    def progress(self, key: str) -> int | None:
+        """Completions (inferences / training steps) of a live tenant; None:
+        not measured (the CPU rehearsal)."""
+        return None
+
     def close(self) -> None:
         pass
 
@@ -163,6 +168,11 @@ class ProcessRuntime(RecordingRuntime):
             elif board.states()[0] == STATE_FAILED or proc.poll() is not None:
                 err = (d / "pod.err").read_text()[-1500:] if (d / "pod.err").exists() else ""
                 raise RuntimeError(f"tenant {t.key} failed:\n{err}")
+
+    def progress(self, key: str) -> int | None:
+        with self.lock:
+            t = self.tenants.get(key)
+        return None if t is None else int(t.handle[1].counts()[0])
 
     def close(self) -> None:
         with self.lock:
@@ -412,6 +422,20 @@ class ComposedScenario(QuotaScenario):
         self.runtime.start(key, env)
         self.events.append(("start", key, time.monotonic()))
 
+    def _trainer_progress(self, mark: dict) -> dict | None:
+        """Training steps the trainer pods completed since ``mark`` (updated
+        in place) and their rate: the DP job keeps stepping (forward,
+        backward, bucketed all-reduce) while the inference tenants come and go."""
+        now = time.monotonic()
+        steps = {k: self.runtime.progress(k) for k in self.trainer_keys}
+        if not steps or any(v is None for v in steps.values()):
+            return None
+        done = sum(v - mark.get(k, 0) for k, v in steps.items())
+        dt = now - mark.get("_t", now)
+        mark.update(steps)
+        mark["_t"] = now
+        return {"steps": done, "steps_per_s": round(done / dt, 2) if dt > 0 else None}
+
     def _phase_util(self, sampler, t0: float) -> float | None:
         return sampler.mean(t0, time.monotonic())[0] if sampler is not None else None
 
@@ -455,6 +479,9 @@ class ComposedScenario(QuotaScenario):
             ok = self.drive(lambda: set(tr) <= self.runtime.ready(), phase_timeout_s)
             res["phase_trainers"] = {"ok": ok, "seconds": round(time.monotonic() - t0, 2), "trainers": len(tr),
                                      "gpu_util_pct": self._phase_util(sampler, t0)}
+        self.trainer_keys = tr
+        mark: dict = {}
+        self._trainer_progress(mark)
         # phase A: team-a in bursts, borrowing
         t1 = time.monotonic()
         a, per = [], -(-self.team_a_pods // self.waves)
@@ -465,7 +492,8 @@ class ComposedScenario(QuotaScenario):
                 self.drive(lambda: False, self.wave_gap_s)   # the next burst arrives later
         ok = self.drive(lambda: set(a) <= self.runtime.ready() and self._labels_settled(), phase_timeout_s)
         res["phase_a"] = {"ok": ok, "seconds": round(time.monotonic() - t1, 2), **self.snapshot(),
-                          "gpu_util_pct": self._phase_util(sampler, t1), "quota_vs_footprint": self.quota_vs_footprint()}
+                          "gpu_util_pct": self._phase_util(sampler, t1), "quota_vs_footprint": self.quota_vs_footprint(),
+                          "trainer": self._trainer_progress(mark)}
         # phase P: pending partition pods force a repartition of the amdpart node
         tp = time.monotonic()
         sw0, plans0 = self.part.smi.switches, self.cl.clock.now()
@@ -480,10 +508,10 @@ class ComposedScenario(QuotaScenario):
                                     "mode_switches": self.part.smi.switches - sw0, "modes_before": modes0,
                                     "modes_after": list(self.part.smi.compute), "pods_running": len(
                                         set(keys) & self.sim_runtime.running()),
-                                    "gpu_util_pct": self._phase_util(sampler, tp)}
+                                    "gpu_util_pct": self._phase_util(sampler, tp), "trainer": self._trainer_progress(mark)}
         # phase B: team-b claims its min, preempting team-a's borrowed tenants
         b_res = self._phase_b(phase_timeout_s, sampler)
-        res["phase_b"] = {**b_res, "quota_vs_footprint": self.quota_vs_footprint()}
+        res["phase_b"] = {**b_res, "quota_vs_footprint": self.quota_vs_footprint(), "trainer": self._trainer_progress(mark)}
         res["concurrent_tenants"] = len(self.runtime.running())
         return res
 

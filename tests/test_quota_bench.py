@@ -100,3 +100,5 @@ def test_bench_quota_composed_runs_trainer_and_tenant_processes():
     assert d["phase_repartition"]["mode_switches"] == 1 and d["phase_b"]["preemptions"] >= 1
     assert d["concurrent_tenants"] == 7  # the trainer + 3 + 3
     assert "server_footprint_gb" in d["phase_b"]["quota_vs_footprint"]["team-b"]
+    # the DP trainer keeps stepping through every phase
+    assert all(d[p]["trainer"]["steps"] >= 1 for p in ("phase_a", "phase_b"))

@@ -63,6 +63,7 @@ def main() -> None:
     ap.add_argument("--h3-layout", default="2x2", choices=["4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16"],
                     help="h3 GEMM tile / wave layout / ring")
     ap.add_argument("--h3-attn-waves", type=int, default=8, choices=[4, 8], help="h3 attention waves per workgroup")
+    ap.add_argument("--lds-epi", type=int, default=0, help="plain fp32-C h3 GEMMs store C through LDS (1)")
     ap.add_argument("--mix", default="", help="heterogeneous tenants instead of --tenants YOLOS pods, e.g. "
                     "yolos:20,bert:4,mlp:4 (bert = BERT-base-shaped fp32 encoder at seq 512, mlp = bf16 GEMM-MLP "
                     "probe, resnet = ResNet-18 at 224x224, llama = Llama decoder at seq 512); per-kind rates in "
@@ -84,6 +85,7 @@ def main() -> None:
     ops.set_gemm_f32x6_pipeline(bool(a.pipeline))  # process-wide: every capture below
     ops.set_gemm_f32h3_layout(a.h3_layout)
     ops.set_attention_f32h3_waves(a.h3_attn_waves)
+    ops.set_gemm_f32h3_lds_epilogue(bool(a.lds_epi))
     try:
         t0 = time.monotonic()
         clients = [PodClient(path, connect_timeout_s=30) for _ in range(a.tenants)]
@@ -137,7 +139,7 @@ def main() -> None:
                           "server_compile_ms_p50": sorted(r["compile"].get("compile_ms", 0) for r in reps)[len(reps) // 2],
                           "inf_per_s": round(sum(done) / (w1 - w0), 2),
                           "min_done": min(done), "max_done": max(done), "solo_replays": solo,
-                          "kernel_config": srv.kernel_config, "pipeline": a.pipeline, "h3_layout": a.h3_layout,
+                          "kernel_config": srv.kernel_config, "pipeline": a.pipeline, "h3_layout": a.h3_layout, "lds_epi": a.lds_epi,
                           "sclk_mhz": sclk}), flush=True)
     finally:
         srv.stop()
