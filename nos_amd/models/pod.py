@@ -165,10 +165,12 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
             "attention_f32": env.get("NOS_AMD_ATTN_F32_VARIANT") or ("h3" if whole else "h3n"),
             "f32_math": env.get("NOS_AMD_F32_MATH") or "h3",
             "gemm_f32x6_tile": env.get("NOS_AMD_X6_TILE") or ("policy" if whole else "128x128"),
-            # pre-LN residual GEMMs handing the next LN-GEMM its planes (ops.set_ln_handoff):
-            # off -- the row-owning grid is 3x smaller; 28-tenant fleet 611 (on) vs
-            # 725 (off) inf/s (profiles/r05_ln_handoff_ab.json)
-            "ln_handoff": env.get("NOS_AMD_LN_HANDOFF") or "off"}
+            # LayerNorm hand-off (ops.set_ln_handoff): residual GEMMs write row
+            # statistics, LN-GEMMs normalise in their A load -- no split pass;
+            # 28-tenant fleet 799 (on) vs 784 (off) inf/s (profiles/r05_lna_fleet_ab.json)
+            "ln_handoff": env.get("NOS_AMD_LN_HANDOFF") or "on",
+            # plain fp32-C h3 GEMMs store C through LDS (float4 rows): 801 vs 799 inf/s
+            "h3_epilogue": env.get("NOS_AMD_H3_EPILOGUE") or "lds"}
 
 
 def slice_cu_budget(env: dict | None = None) -> int:

@@ -63,7 +63,8 @@ def main() -> None:
     ap.add_argument("--h3-layout", default="2x2", choices=["4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16"],
                     help="h3 GEMM tile / wave layout / ring")
     ap.add_argument("--h3-attn-waves", type=int, default=8, choices=[4, 8], help="h3 attention waves per workgroup")
-    ap.add_argument("--lds-epi", type=int, default=0, help="plain fp32-C h3 GEMMs store C through LDS (1)")
+    ap.add_argument("--lds-epi", type=int, default=1, help="plain fp32-C h3 GEMMs store C through LDS (1) or "
+                    "from the MFMA registers (0)")
     ap.add_argument("--mix", default="", help="heterogeneous tenants instead of --tenants YOLOS pods, e.g. "
                     "yolos:20,bert:4,mlp:4 (bert = BERT-base-shaped fp32 encoder at seq 512, mlp = bf16 GEMM-MLP "
                     "probe, resnet = ResNet-18 at 224x224, llama = Llama decoder at seq 512); per-kind rates in "
