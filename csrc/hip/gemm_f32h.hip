@@ -21,12 +21,16 @@
 //  * epilogue: scales, bias, GELU / ReLU, residual, and optionally the K / V
 //    columns of a fused QKV projection as the attention's fp16 planes
 //    (KvOut: attention_f32x.hip's h3 kernel reads them).
+#include <type_traits>
+
 #include "common.h"
 #include "split_f16.h"
 
 namespace {
 
 enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8, EPI_BIAS_ROW = 16, EPI_RESID_PRE = 32 };
+template <int E>
+using EpiC = std::integral_constant<int, E>;
 // EPI_RESID adds R after the activation (transformer residuals); EPI_RESID_PRE
 // before it (ResNet: relu(conv + bn + identity))
 
@@ -391,160 +395,203 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     // offsets out of the tile loop and keep them live across the K loop (that
     // hoisting spilled the PERSIST variants: 200+ VGPRs to scratch)
     int c = c0, h = h0, ldc = ldc0, ldr = ldr0;
-    if constexpr (PERSIST || MODE != 0) {
-      asm volatile("" : "+v"(c), "+v"(h));
-      asm volatile("" : "+s"(ldc), "+s"(ldr));
-    }
+    asm volatile("" : "+v"(c), "+v"(h));
+    asm volatile("" : "+s"(ldc), "+s"(ldr));
     float rsv[MI][16], rbv[MI][16];  // row scales; row bias (conv: per output channel)
+    if (rinvb != nullptr) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          rsv[i][r] = rinvb[m < M ? m : M - 1];
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rsv[i][r] = rconst;
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        rsv[i][r] = rinvb != nullptr ? rinvb[m < M ? m : M - 1] : rconst;
         rbv[i][r] = (BATCHED && (epi & EPI_BIAS_ROW)) ? bias[m < M ? m : M - 1] : 0.f;
       }
-    if constexpr (MODE == 2) {
-      // (without sout: only the epilogue, plain fp32 C through LDS)
-      // the tile goes to C through LDS: act(acc scale + bias) in the MFMA
-      // layout into T (row stride BN), then threads 2r, 2r+1 take the two
-      // 64-column halves of row r (16-byte chunks in a per-lane rotation:
-      // conflict-free), add the residual, store C as float4 and reduce the
-      // row's (mean, M2) over the valid columns; Chan's merge of the halves
-      float* const T = reinterpret_cast<float*>(smem);
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int cl = wn * (BN / WGN) + j * 32 + c;
-        const int nc = n0 + cl < N ? n0 + cl : N - 1;
-        const float cs = cscb[nc];
-        const float p2 = (epi & EPI_BIAS) ? bias[nc] : 0.f;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2);
-            if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
-            if (epi & EPI_RELU) v = fmaxf(v, 0.f);
-            T[rl * BN + cl] = v;
+    // the interior epilogues, instantiated per flag combination (EpiC<E>): with
+    // runtime flags the compiler kept a branch per element and flag (hundreds
+    // of basic blocks); E < 0 is the generic runtime-flag form.  true: done
+    auto epilogue = [&](auto ec) -> bool {
+      constexpr int E = decltype(ec)::value;
+      auto has = [&](int f) -> bool {
+        if constexpr (E < 0) return (epi & f) != 0;
+        else return (E & f) != 0;
+      };
+      if constexpr (MODE == 2) {
+        // (without sout: only the epilogue, plain fp32 C through LDS)
+        // the tile goes to C through LDS: act(acc scale + bias) in the MFMA
+        // layout into T (row stride BN), then threads 2r, 2r+1 take the two
+        // 64-column halves of row r (16-byte chunks in a per-lane rotation:
+        // conflict-free), add the residual, store C as float4 and reduce the
+        // row's (mean, M2) over the valid columns; Chan's merge of the halves
+        float* const T = reinterpret_cast<float*>(smem);
+  #pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int cl = wn * (BN / WGN) + j * 32 + c;
+          const int nc = n0 + cl < N ? n0 + cl : N - 1;
+          const float cs = cscb[nc];
+          const float p2 = has(EPI_BIAS) ? bias[nc] : 0.f;
+  #pragma unroll
+          for (int i = 0; i < MI; ++i) {
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2);
+              if (has(EPI_GELU)) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+              if (has(EPI_RELU)) v = fmaxf(v, 0.f);
+              T[rl * BN + cl] = v;
+            }
           }
         }
-      }
-      __syncthreads();
-      const int rr = tid >> 1, hf = tid & 1, m = m0 + rr;
-      const int nv = m < M ? max(0, min(BN / 2, N - n0 - hf * (BN / 2))) : 0;
-      const float* tr = T + rr * BN + hf * (BN / 2);
-      const long long col0 = n0 + hf * (BN / 2);
-      float4 v[16];
-      float sum = 0.f;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int k = ((u + tid) & 15) * 4;
-        v[u] = *reinterpret_cast<const float4*>(tr + k);
-        if (k < nv) {
-          if (epi & EPI_RESID) {
-            const float4 q = *reinterpret_cast<const float4*>(Rb + (long long)m * ldr + col0 + k);
-            v[u].x += q.x;
-            v[u].y += q.y;
-            v[u].z += q.z;
-            v[u].w += q.w;
+        __syncthreads();
+        const int rr = tid >> 1, hf = tid & 1, m = m0 + rr;
+        const int nv = m < M ? max(0, min(BN / 2, N - n0 - hf * (BN / 2))) : 0;
+        const float* tr = T + rr * BN + hf * (BN / 2);
+        const long long col0 = n0 + hf * (BN / 2);
+        float4 v[16];
+        float sum = 0.f;
+  #pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int k = ((u + tid) & 15) * 4;
+          v[u] = *reinterpret_cast<const float4*>(tr + k);
+          if (k < nv) {
+            if (has(EPI_RESID)) {
+              const float4 q = *reinterpret_cast<const float4*>(Rb + (long long)m * ldr + col0 + k);
+              v[u].x += q.x;
+              v[u].y += q.y;
+              v[u].z += q.z;
+              v[u].w += q.w;
+            }
+            *reinterpret_cast<float4*>(Cb + (long long)m * ldc + col0 + k) = v[u];
+            sum += (v[u].x + v[u].y) + (v[u].z + v[u].w);
           }
-          *reinterpret_cast<float4*>(Cb + (long long)m * ldc + col0 + k) = v[u];
-          sum += (v[u].x + v[u].y) + (v[u].z + v[u].w);
         }
-      }
-      const float mean = nv > 0 ? sum / (float)nv : 0.f;
-      float m2 = 0.f;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int k = ((u + tid) & 15) * 4;
-        if (k < nv) {
-          const float d0 = v[u].x - mean, d1 = v[u].y - mean, d2 = v[u].z - mean, d3 = v[u].w - mean;
-          m2 = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, m2))));
+        const float mean = nv > 0 ? sum / (float)nv : 0.f;
+        float m2 = 0.f;
+  #pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int k = ((u + tid) & 15) * 4;
+          if (k < nv) {
+            const float d0 = v[u].x - mean, d1 = v[u].y - mean, d2 = v[u].z - mean, d3 = v[u].w - mean;
+            m2 = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, m2))));
+          }
         }
+        float n = (float)nv, mu = mean;
+        const float on = __shfl_xor(n, 1, 64), omu = __shfl_xor(mu, 1, 64), om2 = __shfl_xor(m2, 1, 64);
+        if (ln.sout != nullptr && hf == 0 && n + on > 0.f) {
+          chan_merge(n, mu, m2, on, omu, om2);
+          ln.sout[(long long)m * ln.spart + tn] = float2{mu, m2};
+        }
+        return true;
       }
-      float n = (float)nv, mu = mean;
-      const float on = __shfl_xor(n, 1, 64), omu = __shfl_xor(mu, 1, 64), om2 = __shfl_xor(m2, 1, 64);
-      if (ln.sout != nullptr && hf == 0 && n + on > 0.f) {
-        chan_merge(n, mu, m2, on, omu, om2);
-        ln.sout[(long long)m * ln.spart + tn] = float2{mu, m2};
+      // interior tile stored as fp32 C (the common case): tile-local 32-bit
+      // offsets from wave-uniform base pointers (saddr stores, no 64-bit
+      // address math per element) and no bounds tests
+      const bool full = m0 + BM <= M && n0 + BN <= N;
+      // interior tile of the next GEMM's A planes (fc1 -> fc2) or of the K / V
+      // planes of a one-sequence QKV projection (a 128-column tile never
+      // straddles Q / K / V: hd % 128 == 0 is checked by the host): the same
+      // tile-relative 32-bit offsets, two fp16 stores per element
+      if (full && !(has(EPI_RESID) || has(EPI_RESID_PRE)) &&
+          (po.p != nullptr || (kv.kvs != nullptr && kv.S == M && n0 >= kv.qcols && kv.hd % BN == 0))) {
+        unsigned short* hi;
+        long long lo_off;
+        int ld;
+        int t = 0;
+        if (po.p != nullptr) {
+          hi = po.p + (long long)m0 * po.ldp + n0;
+          lo_off = po.pplane;
+          ld = po.ldp;
+        } else {
+          t = (n0 - kv.qcols) >= kv.hd;
+          hi = kv.kvs + ((long long)m0 * 4 + 2 * t) * kv.hd + (n0 - kv.qcols - t * kv.hd);
+          lo_off = kv.hd;
+          ld = 4 * kv.hd;
+        }
+  #pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int cl = wn * (BN / WGN) + j * 32 + c;
+          const float cs = cscb[n0 + cl];
+          const float p2 = has(EPI_BIAS) ? bias[n0 + cl] : 0.f;
+          const float osc = po.p != nullptr ? po.sc : kv.kvsc[t * (kv.hd >> 6) + ((n0 - kv.qcols - t * kv.hd + cl) >> 6)];
+  #pragma unroll
+          for (int i = 0; i < MI; ++i) {
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
+              if (has(EPI_GELU)) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+              if (has(EPI_RELU)) v = fmaxf(v, 0.f);
+              const float x = v * osc;
+              const _Float16 h0 = (_Float16)x;
+              const _Float16 h1 = (_Float16)(x - (float)h0);
+              const unsigned off = (unsigned)(rl * ld + cl);
+              hi[off] = __builtin_bit_cast(unsigned short, h0);
+              hi[lo_off + off] = __builtin_bit_cast(unsigned short, h1);
+            }
+          }
+        }
+        return true;
       }
-      continue;
+      const bool interior = full && po.p == nullptr && (kv.kvs == nullptr || n0 + BN <= kv.qcols);  // Q columns too
+      if (interior) {
+        float* Ct = Cb + (long long)m0 * ldc + n0;
+        const float* Rt = has(EPI_RESID) || (BATCHED && has(EPI_RESID_PRE)) ? Rb + (long long)m0 * ldr + n0 : nullptr;
+  #pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int cl = wn * (BN / WGN) + j * 32 + c;
+          const float cs = cscb[n0 + cl];
+          const float p2 = has(EPI_BIAS) ? bias[n0 + cl] : 0.f;
+  #pragma unroll
+          for (int i = 0; i < MI; ++i) {
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
+              if (BATCHED && has(EPI_RESID_PRE)) v += Rt[(unsigned)(rl * ldr + cl)];
+              if (has(EPI_GELU)) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+              if (has(EPI_RELU)) v = fmaxf(v, 0.f);
+              if (has(EPI_RESID)) v += Rt[(unsigned)(rl * ldr + cl)];
+              Ct[(unsigned)(rl * ldc + cl)] = v;
+            }
+          }
+        }
+        return true;
+      }
+      return false;
+    };
+    // interior tiles specialised for the flag sets each mode meets; boundary
+    // tiles (and any other flag set) take the runtime-flag path below
+    bool done = false;
+    if constexpr (MODE == 1) {
+      if (epi == EPI_BIAS) done = epilogue(EpiC<EPI_BIAS>{});
+      else if (epi == (EPI_BIAS | EPI_GELU)) done = epilogue(EpiC<EPI_BIAS | EPI_GELU>{});
+      else done = epilogue(EpiC<-1>{});
+    } else if constexpr (MODE == 2) {
+      if (epi == (EPI_BIAS | EPI_RESID)) done = epilogue(EpiC<EPI_BIAS | EPI_RESID>{});
+      else done = epilogue(EpiC<-1>{});
+    } else if constexpr (BATCHED) {
+      done = epilogue(EpiC<-1>{});
+    } else {
+      switch (epi) {
+        case EPI_BIAS: done = epilogue(EpiC<EPI_BIAS>{}); break;
+        case EPI_BIAS | EPI_GELU: done = epilogue(EpiC<EPI_BIAS | EPI_GELU>{}); break;
+        case EPI_BIAS | EPI_RESID: done = epilogue(EpiC<EPI_BIAS | EPI_RESID>{}); break;
+        default: done = epilogue(EpiC<-1>{}); break;
+      }
     }
-    // interior tile stored as fp32 C (the common case): tile-local 32-bit
-    // offsets from wave-uniform base pointers (saddr stores, no 64-bit
-    // address math per element) and no bounds tests
-    const bool full = m0 + BM <= M && n0 + BN <= N;
-    // interior tile of the next GEMM's A planes (fc1 -> fc2) or of the K / V
-    // planes of a one-sequence QKV projection (a 128-column tile never
-    // straddles Q / K / V: hd % 128 == 0 is checked by the host): the same
-    // tile-relative 32-bit offsets, two fp16 stores per element
-    if (full && !(epi & (EPI_RESID | EPI_RESID_PRE)) &&
-        (po.p != nullptr || (kv.kvs != nullptr && kv.S == M && n0 >= kv.qcols && kv.hd % BN == 0))) {
-      unsigned short* hi;
-      long long lo_off;
-      int ld;
-      int t = 0;
-      if (po.p != nullptr) {
-        hi = po.p + (long long)m0 * po.ldp + n0;
-        lo_off = po.pplane;
-        ld = po.ldp;
-      } else {
-        t = (n0 - kv.qcols) >= kv.hd;
-        hi = kv.kvs + ((long long)m0 * 4 + 2 * t) * kv.hd + (n0 - kv.qcols - t * kv.hd);
-        lo_off = kv.hd;
-        ld = 4 * kv.hd;
-      }
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int cl = wn * (BN / WGN) + j * 32 + c;
-        const float cs = cscb[n0 + cl];
-        const float p2 = (epi & EPI_BIAS) ? bias[n0 + cl] : 0.f;
-        const float osc = po.p != nullptr ? po.sc : kv.kvsc[t * (kv.hd >> 6) + ((n0 - kv.qcols - t * kv.hd + cl) >> 6)];
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
-            if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
-            if (epi & EPI_RELU) v = fmaxf(v, 0.f);
-            const float x = v * osc;
-            const _Float16 h0 = (_Float16)x;
-            const _Float16 h1 = (_Float16)(x - (float)h0);
-            const unsigned off = (unsigned)(rl * ld + cl);
-            hi[off] = __builtin_bit_cast(unsigned short, h0);
-            hi[lo_off + off] = __builtin_bit_cast(unsigned short, h1);
-          }
-        }
-      }
-      continue;
-    }
-    const bool interior = full && po.p == nullptr && (kv.kvs == nullptr || n0 + BN <= kv.qcols);  // Q columns too
-    if (interior) {
-      float* Ct = Cb + (long long)m0 * ldc + n0;
-      const float* Rt = (epi & EPI_RESID) || (BATCHED && (epi & EPI_RESID_PRE)) ? Rb + (long long)m0 * ldr + n0 : nullptr;
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int cl = wn * (BN / WGN) + j * 32 + c;
-        const float cs = cscb[n0 + cl];
-        const float p2 = (epi & EPI_BIAS) ? bias[n0 + cl] : 0.f;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
-            if (BATCHED && (epi & EPI_RESID_PRE)) v += Rt[(unsigned)(rl * ldr + cl)];
-            if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
-            if (epi & EPI_RELU) v = fmaxf(v, 0.f);
-            if (epi & EPI_RESID) v += Rt[(unsigned)(rl * ldr + cl)];
-            Ct[(unsigned)(rl * ldc + cl)] = v;
-          }
-        }
-      }
-      continue;
-    }
+    if (done) continue;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int n = n0 + wn * (BN / WGN) + j * 32 + c;
@@ -558,10 +605,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
           const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
           if (BATCHED && (epi & EPI_RESID_PRE) && m < M && n < N) v += Rb[(long long)m * ldr + n];
-          if (epi & EPI_GELU) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
-          if (epi & EPI_RELU) v = fmaxf(v, 0.f);
+          if ((epi & EPI_GELU)) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+          if ((epi & EPI_RELU)) v = fmaxf(v, 0.f);
           if (m < M && n < N) {
-            if (epi & EPI_RESID) v += Rb[(long long)m * ldr + n];
+            if ((epi & EPI_RESID)) v += Rb[(long long)m * ldr + n];
             if (kv.kvs != nullptr && n >= kv.qcols) {
               const int t = (n - kv.qcols) >= kv.hd;  // 0: K, 1: V
               const int col = n - kv.qcols - t * kv.hd;

@@ -28,7 +28,7 @@ def main() -> None:
     torch.manual_seed(0)
     S, D, H = 3401, 384, 6
 
-    def timed(fn) -> float:
+    def timed1(fn) -> float:
         for _ in range(3):
             fn()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
@@ -38,7 +38,17 @@ def main() -> None:
             e1.record()
         torch.cuda.synchronize()
         t = sorted(e0.elapsed_time(e1) * 1e3 for e0, e1 in ev)
-        return round(t[len(t) // 2], 1)
+        return t[len(t) // 2]
+
+    def timed(fn, setup=None) -> float:
+        """min over 5 rounds of the median of ``iters`` (rounds interleave with
+        the other configurations' through the caller's order)"""
+        best = []
+        for _ in range(5):
+            if setup:
+                setup()
+            best.append(timed1(fn))
+        return round(min(best), 1)
 
     res = {}
     for B in (int(b) for b in a.batches.split(",")):
@@ -51,11 +61,12 @@ def main() -> None:
             r = torch.randn(M, N, device="cuda")
             p, ri = ops._split_rows_h3(x, ln=False)
             A = ops.H3Planes(p, ri, 0.0, (M, K))
-            row[name] = {"plain_us": timed(lambda: ops.linear_planes(A, w, b, residual=r)),
-                         "stats_us": timed(lambda: ops.linear_planes(A, w, b, residual=r, row_stats=True))}
-            ops.set_gemm_f32h3_lds_epilogue(True)
-            row[name]["plain_lds_epi_us"] = timed(lambda: ops.linear_planes(A, w, b, residual=r))
-            ops.set_gemm_f32h3_lds_epilogue(False)
+            row[name] = {
+                "plain_reg_epi_us": timed(lambda: ops.linear_planes(A, w, b, residual=r),
+                                          lambda: ops.set_gemm_f32h3_lds_epilogue(False)),
+                "plain_lds_epi_us": timed(lambda: ops.linear_planes(A, w, b, residual=r),
+                                          lambda: ops.set_gemm_f32h3_lds_epilogue(True)),
+                "stats_us": timed(lambda: ops.linear_planes(A, w, b, residual=r, row_stats=True))}
         x = torch.randn(B, S, D, device="cuda") * 2 + 1
         wq = torch.randn(3 * D, D, device="cuda") / D ** 0.5
         cq = torch.randn(3 * D, device="cuda") * 0.1
