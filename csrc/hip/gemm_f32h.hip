@@ -460,38 +460,48 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         const float* tr = T + rr * BN + hf * (BN / 2);
         const long long col0 = n0 + hf * (BN / 2);
         float4 v[16];
+        // sout == nullptr: the plain LDS epilogue (no statistics); a whole row
+        // half (every tile of N % 128 == 0) without per-chunk tests
+        const bool want = ln.sout != nullptr;
         float sum = 0.f;
+        auto pass1 = [&](auto wholec) {
+          constexpr bool W = decltype(wholec)::value;
   #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int k = ((u + tid) & 15) * 4;
-          v[u] = *reinterpret_cast<const float4*>(tr + k);
-          if (k < nv) {
-            if (has(EPI_RESID)) {
-              const float4 q = *reinterpret_cast<const float4*>(Rb + (long long)m * ldr + col0 + k);
-              v[u].x += q.x;
-              v[u].y += q.y;
-              v[u].z += q.z;
-              v[u].w += q.w;
+          for (int u = 0; u < 16; ++u) {
+            const int k = ((u + tid) & 15) * 4;
+            v[u] = *reinterpret_cast<const float4*>(tr + k);
+            if (W || k < nv) {
+              if (has(EPI_RESID)) {
+                const float4 q = *reinterpret_cast<const float4*>(Rb + (long long)m * ldr + col0 + k);
+                v[u].x += q.x;
+                v[u].y += q.y;
+                v[u].z += q.z;
+                v[u].w += q.w;
+              }
+              *reinterpret_cast<float4*>(Cb + (long long)m * ldc + col0 + k) = v[u];
+              if (want) sum += (v[u].x + v[u].y) + (v[u].z + v[u].w);
             }
-            *reinterpret_cast<float4*>(Cb + (long long)m * ldc + col0 + k) = v[u];
-            sum += (v[u].x + v[u].y) + (v[u].z + v[u].w);
           }
-        }
-        const float mean = nv > 0 ? sum / (float)nv : 0.f;
-        float m2 = 0.f;
+        };
+        if (nv == BN / 2) pass1(std::true_type{});
+        else pass1(std::false_type{});
+        if (want) {
+          const float mean = nv > 0 ? sum / (float)nv : 0.f;
+          float m2 = 0.f;
   #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int k = ((u + tid) & 15) * 4;
-          if (k < nv) {
-            const float d0 = v[u].x - mean, d1 = v[u].y - mean, d2 = v[u].z - mean, d3 = v[u].w - mean;
-            m2 = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, m2))));
+          for (int u = 0; u < 16; ++u) {
+            const int k = ((u + tid) & 15) * 4;
+            if (k < nv) {
+              const float d0 = v[u].x - mean, d1 = v[u].y - mean, d2 = v[u].z - mean, d3 = v[u].w - mean;
+              m2 = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, m2))));
+            }
           }
-        }
-        float n = (float)nv, mu = mean;
-        const float on = __shfl_xor(n, 1, 64), omu = __shfl_xor(mu, 1, 64), om2 = __shfl_xor(m2, 1, 64);
-        if (ln.sout != nullptr && hf == 0 && n + on > 0.f) {
-          chan_merge(n, mu, m2, on, omu, om2);
-          ln.sout[(long long)m * ln.spart + tn] = float2{mu, m2};
+          float n = (float)nv, mu = mean;
+          const float on = __shfl_xor(n, 1, 64), omu = __shfl_xor(mu, 1, 64), om2 = __shfl_xor(m2, 1, 64);
+          if (hf == 0 && n + on > 0.f) {
+            chan_merge(n, mu, m2, on, omu, om2);
+            ln.sout[(long long)m * ln.spart + tn] = float2{mu, m2};
+          }
         }
         return true;
       }
@@ -580,6 +590,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
       else done = epilogue(EpiC<-1>{});
     } else if constexpr (MODE == 2) {
       if (epi == (EPI_BIAS | EPI_RESID)) done = epilogue(EpiC<EPI_BIAS | EPI_RESID>{});
+      else if (epi == EPI_BIAS) done = epilogue(EpiC<EPI_BIAS>{});
       else done = epilogue(EpiC<-1>{});
     } else if constexpr (BATCHED) {
       done = epilogue(EpiC<-1>{});

@@ -36,7 +36,10 @@ HIP_SOURCES = ["attention.hip", "attention_f32.hip", "attention_f32x.hip", "gemm
 # scalar f32 ops: without SLP re-packing them into v_pk_*_f32 next to the
 # MFMAs, x6 attention is 3-5 % faster and the 28-pod fleet +2 %
 # (profiles/r03_x6_scalar_split_ab.json)
-HIP_EXTRA_FLAGS: dict[str, list[str]] = {"attention_f32x.hip": ["-fno-slp-vectorize"],
+# attention_f32x: -fno-honor-nans drops the canonicalising v_max_f32 the score
+# row maximum got around every fmaxf (21 -> 17 VALU per QK tile); scores are
+# never NaN for finite inputs
+HIP_EXTRA_FLAGS: dict[str, list[str]] = {"attention_f32x.hip": ["-fno-slp-vectorize", "-fno-honor-nans"],
                                          "gemm_f32x.hip": ["-fno-slp-vectorize"]}
 HIP_LIB = HERE / "libnos_hip.so"
 SMI_LIB = HERE / "libnos_amdsmi.so"
