@@ -40,7 +40,8 @@ HIP_SOURCES = ["attention.hip", "attention_f32.hip", "attention_f32x.hip", "gemm
 # row maximum got around every fmaxf (21 -> 17 VALU per QK tile); scores are
 # never NaN for finite inputs
 HIP_EXTRA_FLAGS: dict[str, list[str]] = {"attention_f32x.hip": ["-fno-slp-vectorize", "-fno-honor-nans"],
-                                         "gemm_f32x.hip": ["-fno-slp-vectorize"]}
+                                         "gemm_f32x.hip": ["-fno-slp-vectorize"],
+                                         "attention.hip": ["-fno-slp-vectorize", "-fno-honor-nans"]}
 HIP_LIB = HERE / "libnos_hip.so"
 SMI_LIB = HERE / "libnos_amdsmi.so"
 
