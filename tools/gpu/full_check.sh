@@ -1,9 +1,9 @@
-# Full GPU check of the committed tree: pytest -m gpu, smoke(), the default
+# Full GPU check of the committed tree (the driver's round-end steps): pytest -m gpu, smoke(), the default
 # bench.py (the driver's command), then fleet kernel stats.
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${1:-r5_full}
+O=$R/gpurun_out/${1:-full_check}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputests.log 2>&1 || { echo gpu tests failed; grep -E "FAILED|Error|assert" $O/gputests.log | head -30; tail -5 $O/gputests.log; exit 1; }
 tail -2 $O/gputests.log
