@@ -814,6 +814,8 @@ class CompiledProgram:
         self._new_dtypes: dict[str, str] = {}
         with torch.no_grad():
             steps = self._fold_constants(prog)
+            steps = self._distribute_add_over_cat(steps)
+            steps = self._fuse_cast_relayout(steps)
             steps = self._pushdown_row_slices(steps)
             steps = self._fold_batchnorm(steps)
             steps = self._merge_parallel_linears(steps)
@@ -822,6 +824,7 @@ class CompiledProgram:
             steps = self._fuse_epilogues(steps)
             steps = self._fuse_qkv_attention(steps)
             steps = self._fuse_rotary_sdpa(steps)
+            steps = self._cat_into_buffer(steps)
             steps = self._mark_plane_handoffs(steps)
             steps = self._mark_ln_handoffs(steps)
             self._prep_conv_weights(steps)
@@ -859,6 +862,140 @@ class CompiledProgram:
             del self.consts[k]
         self.stats["constant_folded"] = folded
         return steps
+
+    def _cat_into_buffer(self, steps: list[_Step]) -> list[_Step]:
+        """A cat whose parts are constants plus one GEMM output (YOLOS's [cls,
+        patches, detection tokens]) needs no copy kernel: the constant parts go
+        into a persistent buffer once, at build, and the GEMM writes its rows
+        straight into the buffer's slab (``out=``).  Only where the slab is
+        contiguous (every dim before the cat dim of size 1)."""
+        import torch
+
+        uses = self._consumers(steps, self.outputs)
+        by_out = {s.output: s for s in steps}
+        n = 0
+        for c in steps:
+            if c.kind != "cat" or c.output in self.outputs:
+                continue
+            dyn = [i for i in c.inputs if i not in self.consts]
+            if len(dyn) != 1 or c.inputs.count(dyn[0]) != 1:
+                continue
+            p = by_out.get(dyn[0])
+            shape = tuple(self._shape(c.output))
+            d = c.attrs.get("dim", 0) % len(shape)
+            if (p is None or p.kind != "linear" or uses.get(p.output) != 1 or p.attrs.get("row_stats")
+                    or math.prod(shape[:d]) != 1 or self._dtype(p.output) not in ("fp32", "bf16")):
+                continue
+            buf = torch.empty(shape, dtype=torch_dtype(self._dtype(c.output)), device=self.device)
+            off = 0
+            for i in c.inputs:
+                ln = self._shape(i)[d]
+                if i != p.output:
+                    buf.narrow(d, off, ln).copy_(self.consts[i])
+                else:
+                    p.attrs["out_into"] = (c.output + "::buf", d, off)
+                off += ln
+            self.aux[c.output + "::buf"] = buf
+            c.kind, c.inputs, c.attrs = "cat_buffer", [p.output], {"buf": c.output + "::buf"}
+            n += 1
+        self.stats["cats_in_place"] = n
+        return steps
+
+    def _fuse_cast_relayout(self, steps: list[_Step]) -> list[_Step]:
+        """cast -> reshape / permute chain (each value read once) -> ONE
+        relayout step: the chain's views, and the one copy a non-viewable
+        reshape needs done as the cast (strided read, converted contiguous
+        write) -- a bf16 tenant's image cast and its patch extraction are one
+        launch instead of two."""
+        uses = self._consumers(steps, self.outputs)
+        by_in: dict[str, list[_Step]] = {}
+        for s in steps:
+            for i in s.inputs:
+                by_in.setdefault(i, []).append(s)
+        drop: set[int] = set()
+        n = 0
+        for s in steps:
+            if s.kind != "cast" or uses.get(s.output) != 1 or s.output in self.outputs:
+                continue
+            chain, cur = [], s.output
+            while uses.get(cur) == 1 and cur not in self.outputs:
+                nxt = by_in[cur][0]
+                if nxt.kind not in ("reshape", "permute"):
+                    break
+                chain.append(nxt)
+                cur = nxt.output
+            if not chain:
+                continue
+            ops_ = [("reshape", list(c.attrs["shape"])) if c.kind == "reshape" else ("permute", list(c.attrs["dims"]))
+                    for c in chain]
+            last = chain[-1]
+            for c in chain[:-1]:
+                drop.add(id(c))
+            drop.add(id(s))
+            last.kind, last.inputs, last.attrs = "relayout", [s.inputs[0]], {"chain": ops_, "dtype": s.attrs["dtype"]}
+            n += 1
+        self.stats["cast_relayouts_fused"] = n
+        return [s for s in steps if id(s) not in drop]
+
+    def _distribute_add_over_cat(self, steps: list[_Step]) -> list[_Step]:
+        """add(cat(parts), c) with c a constant -> cat(add(part_i, c_i)): the
+        constant parts fold here and the add on a GEMM's part becomes that
+        GEMM's residual (YOLOS: the position embeddings added to [cls, patches,
+        detection tokens] -- the patch-embedding GEMM absorbs its slice, the
+        cls / detection slices fold; one elementwise launch fewer)."""
+        uses = self._consumers(steps, self.outputs)
+        by_out = {s.output: s for s in steps}
+        drop: set[int] = set()
+        before: dict[int, list[_Step]] = {}
+        n = 0
+        for s in steps:
+            if s.kind != "add":
+                continue
+            for catn, cn in ((s.inputs[0], s.inputs[1]), (s.inputs[1], s.inputs[0])):
+                c = by_out.get(catn)
+                if c is None or c.kind != "cat" or uses.get(catn) != 1 or cn not in self.consts or catn == cn:
+                    continue
+                cst = self.consts[cn]
+                cshape = tuple(self._shape(catn))
+                if tuple(self._shape(s.output)) != cshape or cst.dim() > len(cshape):
+                    continue  # the constant must not broadcast the cat's output up
+                r = len(cshape)
+                d = c.attrs.get("dim", 0) % r
+                dc = d - (r - cst.dim())  # the constant's dim aligned with d (< 0: broadcast)
+                full = dc >= 0 and cst.shape[dc] == cshape[d]
+                if dc >= 0 and not full and cst.shape[dc] != 1:
+                    continue
+                parts, new, off = [], [], 0
+                for k, pi in enumerate(c.inputs):
+                    ln = self._shape(pi)[d]
+                    ci = cst.narrow(dc, off, ln).contiguous() if full else cst
+                    off += ln
+                    name = f"{s.output}::cat{k}"
+                    if pi in self.consts:
+                        self.consts[name] = (self.consts[pi] + ci).contiguous()
+                    else:
+                        cname = f"{s.output}::c{k}"
+                        self.consts[cname] = ci
+                        new.append(_Step("add", [pi, cname], name, {}))
+                        self._new_shapes[name] = tuple(self._shape(pi))
+                        self._new_dtypes[name] = self._dtype(pi)
+                    parts.append(name)
+                c.inputs, c.output = parts, s.output
+                before[id(c)] = new
+                drop.add(id(s))
+                n += 1
+                break
+        out = []
+        for s in steps:
+            out.extend(before.get(id(s), []))
+            if id(s) not in drop:
+                out.append(s)
+        # constants only the distributed adds read are dead now
+        live = {i for s in out for i in s.inputs} | set(self.outputs)
+        for k in [k for k in self.consts if k not in live]:
+            del self.consts[k]
+        self.stats["adds_distributed"] = n
+        return out
 
     def _pushdown_row_slices(self, steps: list[_Step]) -> list[_Step]:
         """Dead-row elimination: a slice along a row (non-feature) dim of a value
@@ -994,18 +1131,32 @@ class CompiledProgram:
         consumer, which lets it fold into the GEMM."""
         import torch
 
-        # a linear whose output feeds a GELU / ReLU keeps its own GEMM: the
-        # activation fuses into that GEMM's epilogue, which a column slice of a
-        # merged GEMM would lose (YOLOS's two detection heads)
-        act_fed = {s.inputs[0] for s in steps if s.kind in ("gelu", "relu")}
-        groups: dict[str, list[_Step]] = {}
+        # a linear whose output feeds a GELU / ReLU merges only with linears
+        # whose outputs feed the same activation (and nothing else): the merged
+        # GEMM gets that activation (fused into its epilogue) and each original
+        # activation becomes a column slice of it -- YOLOS's two detection
+        # heads; mixed groups would lose the fusion
+        uses = self._consumers(steps, self.outputs)
+        act_of: dict[str, _Step] = {}
         for s in steps:
-            if (s.kind == "linear" and s.inputs[0] not in self.consts and not s.attrs and s.output not in act_fed
+            if s.kind in ("gelu", "relu") and uses.get(s.inputs[0]) == 1:
+                act_of[s.inputs[0]] = s
+        act_fed = {s.inputs[0] for s in steps if s.kind in ("gelu", "relu")}
+        groups: dict[tuple, list[_Step]] = {}
+        for s in steps:
+            if (s.kind == "linear" and s.inputs[0] not in self.consts and not s.attrs
                     and all(i in self.consts for i in s.inputs[1:])):
-                groups.setdefault(s.inputs[0], []).append(s)
-        first: dict[int, _Step] = {}
+                if s.output in act_of:
+                    key = (s.inputs[0], act_of[s.output].kind)
+                elif s.output not in act_fed:
+                    key = (s.inputs[0], None)
+                else:
+                    continue
+                groups.setdefault(key, []).append(s)
+        first: dict[int, list[_Step]] = {}
+        dead: set[int] = set()
         n = 0
-        for x, g in groups.items():
+        for (x, act), g in groups.items():
             if len(g) < 2 or len({self.consts[m.inputs[1]].dtype for m in g}) != 1:
                 continue
             ws = [self.consts[m.inputs[1]] for m in g]
@@ -1017,17 +1168,26 @@ class CompiledProgram:
                                                       torch.zeros(w.shape[0], dtype=w.dtype, device=w.device)
                                                       for m, w in zip(g, ws)]).contiguous()
                 ins.append(name + ".b")
-            first[id(g[0])] = _Step("linear", ins, name, {})
+            new_steps = [_Step("linear", ins, name, {})]
+            src = name
+            if act is not None:
+                src = name + "::" + act
+                new_steps.append(_Step(act, [name], src, {}))
+            first[id(g[0])] = new_steps
             off = 0
             for m, w in zip(g, ws):
-                m.kind, m.inputs, m.attrs = "slice", [name], {"dim": -1, "start": off, "end": off + w.shape[0]}
+                tgt = act_of[m.output] if act is not None else m
+                tgt.kind, tgt.inputs, tgt.attrs = "slice", [src], {"dim": -1, "start": off, "end": off + w.shape[0]}
+                if act is not None:
+                    dead.add(id(m))
                 off += w.shape[0]
             n += len(g)
         out = []
         for s in steps:
             if id(s) in first:
-                out.append(first[id(s)])
-            out.append(s)
+                out.extend(first[id(s)])
+            if id(s) not in dead:
+                out.append(s)
         self.stats["linears_merged"] = n
         return out
 
@@ -1281,7 +1441,10 @@ class CompiledProgram:
         v = self.program.values.get(name)
         if v is None and name in self._new_dtypes:
             return self._new_dtypes[name]
-        return v.dtype if v is not None else str(self.consts[name].dtype)
+        if v is not None:
+            return v.dtype
+        t = str(self.consts[name].dtype)  # a constant: its wire name, as program values carry
+        return {"torch.float32": "fp32", "torch.bfloat16": "bf16", "torch.int32": "i32"}.get(t, t)
 
     # ------------------------------------------------------------ run
     def __call__(self, x) -> tuple:
@@ -1297,9 +1460,17 @@ class CompiledProgram:
                 res = a.pop() if s.attrs.get("residual") else None
                 rs = bool(s.attrs.get("row_stats")) and ops.ln_handoff_active() and (
                     isinstance(a[0], ops.H3Planes) or (a[0].is_cuda and a[0].dtype.itemsize == 4))
+                into = s.attrs.get("out_into")  # (buffer, dim, offset): a slab of a cat's buffer
                 if isinstance(a[0], ops.H3Planes):
                     y = ops.linear_planes(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
                                           residual=res, row_stats=rs)
+                elif into is not None:
+                    dst = self.aux[into[0]].narrow(into[1], into[2], self._shape(s.output)[into[1]])
+                    y = ops.linear(a[0].contiguous(), a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
+                                   residual=res, out=dst if dst.is_cuda else None)
+                    if y.data_ptr() != dst.data_ptr():
+                        dst.copy_(y)
+                    y = dst
                 else:
                     y = ops.linear(a[0].contiguous(), a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
                                    residual=res, row_stats=rs)
@@ -1358,12 +1529,36 @@ class CompiledProgram:
                     import torch.nn.functional as F
 
                     y = F.layer_norm(xx, (xx.shape[-1],), a[1], a[2], s.attrs.get("eps", 1e-5))
+            elif k == "relayout":
+                y = _relayout(a[0], s.attrs["chain"], s.attrs["dtype"])
+            elif k == "cat_buffer":  # its GEMM part was written in place; the constant parts at build
+                y = self.aux[s.attrs["buf"]]
             else:
                 y = _eager(k, a, s.attrs)
             env[s.output] = y
             for r in s.release:
                 env.pop(r, None)
         return tuple(env[o] for o in self.outputs)
+
+
+def _relayout(x, chain, dtype: str):
+    """Apply the reshape / permute chain as views; the first reshape that
+    cannot be a view is the one copy, written straight in ``dtype``."""
+    import torch
+
+    td = torch_dtype(dtype)
+    v, done = x, x.dtype == td
+    for op, arg in chain:
+        if op == "permute":
+            v = v.permute(*arg)
+            continue
+        try:
+            v = v.view(*arg)
+        except RuntimeError:
+            out = torch.empty(arg, dtype=td, device=v.device)
+            out.view(v.shape).copy_(v)
+            v, done = out, True
+    return v if done else v.to(td)
 
 
 # ---------------------------------------------------------------- building (numpy only)

@@ -63,10 +63,13 @@ def test_outputs_match_the_tenants_own_eager_model(server):
     prog = demo_tenant("fp32", 7, small=False)
     rep = reg(c, "pod-a", prog=prog)
     assert rep["tenant"] >= 1 and rep["server"]["lanes"] == 2 and rep["program"].startswith("yolos")
-    # the graph compiler folded the LNs into the GEMMs and fused QKV + attention
-    assert rep["compile"]["layernorm_folded"] == 4 and rep["compile"]["qkv_attention_fused"] == 2
-    assert rep["compile"]["plane_handoffs"] == 4
-    assert rep["compile"]["residual_fused"] == 4 and rep["compile"]["activation_fused"] == 6
+    # the graph compiler folded the LNs into the GEMMs (the final one into the
+    # two detection heads' merged first GEMM) and fused QKV + attention
+    assert rep["compile"]["layernorm_folded"] == 5 and rep["compile"]["qkv_attention_fused"] == 2
+    assert rep["compile"]["plane_handoffs"] == 4 and rep["compile"]["linears_merged"] == 2
+    # (+1 residual: the position embeddings, distributed over the token cat, into the patch GEMM)
+    assert rep["compile"]["residual_fused"] == 5 and rep["compile"]["activation_fused"] == 5
+    assert rep["compile"]["adds_distributed"] == 1
     x = np.random.default_rng(0).standard_normal(rep["input_shape"]).astype(np.float32)
     outs, meta = c.infer(x, outputs=True)
     m = YolosDetector(YolosConfig.test(), backend="torch")

@@ -51,9 +51,9 @@ def test_server_replays_match_the_eager_model(server):
     c = PodClient(server.path, connect_timeout_s=10)
     rep = c.register("pod-a", *_yolos(3), memory_limit_gb=10)
     assert rep["server"]["kernel_config"]["f32_math"] == "h3"
-    assert rep["compile"]["qkv_attention_fused"] == 12 and rep["compile"]["layernorm_folded"] == 24
-    # the heads' first GEMMs keep their fused ReLU: not merged
-    assert rep["compile"]["linears_merged"] == 0
+    assert rep["compile"]["qkv_attention_fused"] == 12 and rep["compile"]["layernorm_folded"] == 25
+    # the heads' first GEMMs (both ReLU) merge into one, ReLU fused, the final LN folded into it
+    assert rep["compile"]["linears_merged"] == 2
     assert rep["compile"]["plane_handoffs"] == 24
     assert 0.05 < rep["footprint_gb"] < 10
     x = np.random.default_rng(1).standard_normal(rep["input_shape"]).astype(np.float32)
