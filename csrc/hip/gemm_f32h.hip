@@ -39,7 +39,7 @@ using EpiC = std::integral_constant<int, E>;
 // runs over nb x tiles_m x tiles_n, one batch's tiles adjacent (one XCD's L2)
 struct Batch {
   int nb = 1;
-  long long a = 0, rinv = 0, w = 0, csc = 0, c = 0, r = 0;
+  long long a = 0, rinv = 0, w = 0, csc = 0, c = 0, r = 0, bias = 0;  // bias: grouped convs' per-group rows
 };
 
 constexpr int BK = 32;  // K granule of the API (K % 32 == 0); stages are BKT = 32 or 16 deep
@@ -184,6 +184,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     const float* __restrict__ cscb = BATCHED ? csc + bb * bt.csc : csc;
     float* __restrict__ Cb = BATCHED && C != nullptr ? C + bb * bt.c : C;
     const float* __restrict__ Rb = BATCHED && R != nullptr ? R + bb * bt.r : R;
+    const float* __restrict__ biasb = BATCHED && bias != nullptr ? bias + bb * bt.bias : bias;
 
     // a 1 KiB piece = RPP rows x ROWB bytes of one plane; lane L: row L / CH, chunk L % CH
     auto stage_a = [&](int k0, unsigned char* dst) {
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        rbv[i][r] = (BATCHED && (epi & EPI_BIAS_ROW)) ? bias[m < M ? m : M - 1] : 0.f;
+        rbv[i][r] = (BATCHED && (epi & EPI_BIAS_ROW)) ? biasb[m < M ? m : M - 1] : 0.f;
       }
     // the interior epilogues, instantiated per flag combination (EpiC<E>): with
     // runtime flags the compiler kept a branch per element and flag (hundreds
@@ -441,7 +442,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
           const int cl = wn * (BN / WGN) + j * 32 + c;
           const int nc = n0 + cl < N ? n0 + cl : N - 1;
           const float cs = cscb[nc];
-          const float p2 = has(EPI_BIAS) ? bias[nc] : 0.f;
+          const float p2 = has(EPI_BIAS) ? biasb[nc] : 0.f;
   #pragma unroll
           for (int i = 0; i < MI; ++i) {
   #pragma unroll
@@ -533,7 +534,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         for (int j = 0; j < NI; ++j) {
           const int cl = wn * (BN / WGN) + j * 32 + c;
           const float cs = cscb[n0 + cl];
-          const float p2 = has(EPI_BIAS) ? bias[n0 + cl] : 0.f;
+          const float p2 = has(EPI_BIAS) ? biasb[n0 + cl] : 0.f;
           const float osc = po.p != nullptr ? po.sc : kv.kvsc[t * (kv.hd >> 6) + ((n0 - kv.qcols - t * kv.hd + cl) >> 6)];
   #pragma unroll
           for (int i = 0; i < MI; ++i) {
@@ -562,7 +563,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         for (int j = 0; j < NI; ++j) {
           const int cl = wn * (BN / WGN) + j * 32 + c;
           const float cs = cscb[n0 + cl];
-          const float p2 = has(EPI_BIAS) ? bias[n0 + cl] : 0.f;
+          const float p2 = has(EPI_BIAS) ? biasb[n0 + cl] : 0.f;
   #pragma unroll
           for (int i = 0; i < MI; ++i) {
   #pragma unroll
@@ -608,7 +609,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
       const int n = n0 + wn * (BN / WGN) + j * 32 + c;
       const int nc = n < N ? n : N - 1;
       const float cs = cscb[nc];
-      const float p2 = (epi & EPI_BIAS) ? bias[nc] : 0.f;
+      const float p2 = (epi & EPI_BIAS) ? biasb[nc] : 0.f;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
 #pragma unroll
@@ -956,17 +957,18 @@ NOS_API int nos_gemm_f32h3(const void* Ap, int lda, long long aplane, const floa
 // across the batch: a conv's weight, a broadcast matmul side).  The planes of
 // A_b are [2][M][lda] with plane stride aplane (likewise W_b); C_b / R_b are
 // [M][ldc] / [M][ldr].  EPI_BIAS: bias per column n; EPI_BIAS_ROW: per row m
-// (a conv computed as W . patches^T, NCHW out).  One launch, the tiles of all
+// (a conv computed as W . patches^T, NCHW out), batch element b's bias at
+// bias + b * sbias (a grouped conv's groups).  One launch, the tiles of all
 // batch elements in one grid.  K % 32 == 0.
 NOS_API int nos_gemm_f32h3_batched(const void* Ap, int lda, long long aplane, long long sa, const float* rinv,
                                    long long srinv, float rconst, const void* Wp, int ldw, long long wplane,
-                                   long long sw, const float* csc, long long scsc, const float* bias, const float* R,
-                                   int ldr, long long sr, float* C, int ldc, long long sc, int M, int N, int K, int nb,
-                                   int epi, hipStream_t stream) {
+                                   long long sw, const float* csc, long long scsc, const float* bias, long long sbias,
+                                   const float* R, int ldr, long long sr, float* C, int ldc, long long sc, int M, int N,
+                                   int K, int nb, int epi, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || nb <= 0 || (K % BK) != 0) return (int)hipErrorInvalidValue;
   if ((lda % 8) || (ldw % 8) || lda < K || ldw < K || aplane < (long long)M * lda || wplane < (long long)N * ldw)
     return (int)hipErrorInvalidValue;
-  if (sa < 0 || sw < 0 || srinv < 0 || scsc < 0 || sr < 0 || sc < 0 || (sa % 8) || (sw % 8))
+  if (sa < 0 || sw < 0 || srinv < 0 || scsc < 0 || sr < 0 || sc < 0 || sbias < 0 || (sa % 8) || (sw % 8))
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)Ap) | ((uintptr_t)Wp)) & 15) return (int)hipErrorInvalidValue;
   if ((!rinv && !(rconst > 0.f)) || !csc || !C || ldc < N) return (int)hipErrorInvalidValue;
@@ -982,6 +984,7 @@ NOS_API int nos_gemm_f32h3_batched(const void* Ap, int lda, long long aplane, lo
   bt.csc = scsc;
   bt.c = sc;
   bt.r = sr;
+  bt.bias = sbias;
   return run_h3(Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K, epi, KvOut{},
                 PlaneOut{}, bt, stream, true);
 }

@@ -87,8 +87,8 @@ _SIGS = {
     "nos_get_cu_budget": [],
     # general tenant programs (tenant_ops.hip, attention_h3g.hip, gemm_f32h.hip)
     "nos_gemm_f32h3_batched": [c_void_p, c_int, c_ll, c_ll, c_void_p, c_ll, c_float, c_void_p, c_int, c_ll, c_ll,
-                               c_void_p, c_ll, c_void_p, c_void_p, c_int, c_ll, c_void_p, c_int, c_ll, c_int, c_int,
-                               c_int, c_int, c_int, c_void_p],
+                               c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_int, c_ll, c_void_p, c_int, c_ll, c_int,
+                               c_int, c_int, c_int, c_int, c_void_p],
     "nos_embedding": [c_void_p, c_void_p, c_void_p, c_ll, c_int, c_int, c_void_p],
     "nos_rmsnorm": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p],
     "nos_softmax": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],

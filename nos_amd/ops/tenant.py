@@ -67,8 +67,8 @@ def _bf(t: torch.Tensor) -> int:
 
 # ------------------------------------------------------------------ references
 def conv2d_ref(x, w, bias=None, stride=(1, 1), padding=(0, 0), dilation=(1, 1), act=None, residual=None,
-               residual_first: bool = False):
-    y = F.conv2d(x.float(), w.float(), None if bias is None else bias.float(), stride, padding, dilation)
+               residual_first: bool = False, groups: int = 1):
+    y = F.conv2d(x.float(), w.float(), None if bias is None else bias.float(), stride, padding, dilation, groups)
     if residual is not None and residual_first:
         y = y + residual.float()
     y = _act(y, act)
@@ -195,46 +195,57 @@ def rotary(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tenso
 
 # ------------------------------------------------------------------ GEMM-class ops (h3)
 def _gemm_batched(ap, rinv, sa, srinv, wp, csc, sw, scsc, out, M, N, K, nb, epi, bias=None, residual=None,
-                  ldc=None, sc=None, ldr=None, sr=None) -> None:
+                  ldc=None, sc=None, ldr=None, sr=None, sbias=0, c_off=0, w_off=0, wr_off=0) -> None:
+    """``c_off`` / ``w_off`` / ``wr_off``: element offsets of batch element
+    0's C, W-operand planes and W-operand row scales (a grouped conv's image
+    n; the planes keep the whole tensor's plane stride)."""
     L = _lib.lib()
     ldc = N if ldc is None else ldc
     rc = L.nos_gemm_f32h3_batched(ap.data_ptr(), K, ap[0].numel(), sa,
-                                  rinv.data_ptr(), srinv, 0.0, wp.data_ptr(), K, wp[0].numel(), sw, csc.data_ptr(),
-                                  scsc, _ptr(bias), _ptr(residual), ldr or ldc, sr or 0, out.data_ptr(), ldc,
-                                  M * ldc if sc is None else sc, M, N, K, nb, epi, _stream())
+                                  rinv.data_ptr(), srinv, 0.0, wp.data_ptr() + 2 * w_off, K, wp[0].numel(), sw,
+                                  csc.data_ptr() + 4 * wr_off, scsc, _ptr(bias), sbias, _ptr(residual), ldr or ldc,
+                                  sr or 0, out.data_ptr() + 4 * c_off, ldc, M * ldc if sc is None else sc, M, N, K, nb,
+                                  epi, _stream())
     _lib.check(rc, "nos_gemm_f32h3_batched")
 
 
 def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, stride=(1, 1), padding=(0, 0),
            dilation=(1, 1), act: str | None = None, residual: torch.Tensor | None = None,
-           w2: torch.Tensor | None = None, residual_first: bool = False) -> torch.Tensor:
-    """act(conv2d(x, w) + bias) + residual, groups = 1, NCHW
+           w2: torch.Tensor | None = None, residual_first: bool = False, groups: int = 1) -> torch.Tensor:
+    """act(conv2d(x, w) + bias) + residual, NCHW
     (``residual_first``: act(conv2d(x, w) + bias + residual), a ResNet block's
-    tail).  ``w2``: the weight as a [OC, Kp] fp32 matrix (K = C*KH*KW
+    tail).  ``w2``: the weight as a [OC, Kp] fp32 matrix (K = C/groups*KH*KW
     zero-padded to 32), which the compiler keeps as a constant so its split
-    planes are cached."""
+    planes are cached.  ``groups``: the image seen as N*groups images of
+    C/groups channels (each group's channels are contiguous in NCHW), one
+    batched GEMM per image over the groups (depthwise: groups = C)."""
     if not x.is_cuda:
-        return conv2d_ref(x, w, bias, stride, padding, dilation, act, residual, residual_first)
+        return conv2d_ref(x, w, bias, stride, padding, dilation, act, residual, residual_first, groups)
     dt = x.dtype
     xf = _f32(x).contiguous()
     N, C, H, W = xf.shape
-    OC, _, KH, KW = w.shape
+    OC, Cg, KH, KW = w.shape
+    G = groups
+    if C != Cg * G or OC % G:
+        raise ValueError(f"conv2d groups={G}: input channels {C} / weight {tuple(w.shape)} do not match")
+    OCg = OC // G
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
     OH = (H + 2 * ph - dh * (KH - 1) - 1) // sh + 1
     OW = (W + 2 * pw - dw * (KW - 1) - 1) // sw + 1
-    K = C * KH * KW
+    K = Cg * KH * KW
     Kp = -(-K // 32) * 32
     if w2 is None:
         w2 = _pad_k(_f32(w).reshape(OC, K)).contiguous()
     if w2.shape != (OC, Kp) or w2.dtype != torch.float32:
         raise ValueError(f"conv weight matrix must be fp32 [{OC}, {Kp}]")
     P = OH * OW
-    planes = torch.empty((2, N * P, Kp), dtype=torch.float16, device=x.device)
-    prinv = torch.empty((N * P,), dtype=torch.float32, device=x.device)
+    NG = N * G
+    planes = torch.empty((2, NG * P, Kp), dtype=torch.float16, device=x.device)
+    prinv = torch.empty((NG * P,), dtype=torch.float32, device=x.device)
     L = _lib.lib()
-    _lib.check(L.nos_im2col_h3(xf.data_ptr(), planes.data_ptr(), N * P * Kp, prinv.data_ptr(), N, C, H, W, KH, KW,
+    _lib.check(L.nos_im2col_h3(xf.data_ptr(), planes.data_ptr(), NG * P * Kp, prinv.data_ptr(), NG, Cg, H, W, KH, KW,
                                sh, sw, ph, pw, dh, dw, Kp, _stream()), "nos_im2col_h3")
     wp, wsc = split_f32_weight_h3(w2)
     out = torch.empty((N, OC, OH, OW), dtype=torch.float32, device=x.device)
@@ -245,9 +256,17 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, s
     r = _f32(residual).contiguous() if residual is not None else None
     if r is not None and r.shape != out.shape:
         raise ValueError(f"residual must be {tuple(out.shape)}")
-    # out[n] = W [OC, Kp] . patches[n]^T: A = the weight (shared, stride 0), W-operand = image n's patches
-    _gemm_batched(wp, wsc, 0, 0, planes, prinv, P * Kp, P, out, OC, P, Kp, N, epi, bias=b, residual=r,
-                  ldc=P, sc=OC * P, ldr=P, sr=OC * P)
+    if G == 1:
+        # out[n] = W [OC, Kp] . patches[n]^T: A = the weight (shared, stride 0), W-operand = image n's patches
+        _gemm_batched(wp, wsc, 0, 0, planes, prinv, P * Kp, P, out, OC, P, Kp, N, epi, bias=b, residual=r,
+                      ldc=P, sc=OC * P, ldr=P, sr=OC * P)
+    else:
+        # per image: batch = the groups -- A = group g's weight rows, W-operand
+        # = group g's patches (image n*G + g of the im2col), C = its OCg channels
+        for n in range(N):
+            _gemm_batched(wp, wsc, OCg * Kp, OCg, planes, prinv, P * Kp, P, out, OCg, P, Kp, G, epi,
+                          bias=b, residual=r[n:] if r is not None else None, ldc=P, sc=OCg * P, ldr=P,
+                          sr=OCg * P, sbias=OCg, c_off=n * OC * P, w_off=n * G * P * Kp, wr_off=n * G * P)
     return out if dt == torch.float32 else out.to(dt)
 
 

@@ -93,12 +93,14 @@ def export(module, example, name: str = "module", dtype: str = "fp32") -> tuple[
             m = mods[n.target]
             x = ref(n.args[0])
             if isinstance(m, nn.Conv2d):
-                if m.groups != 1 or isinstance(m.padding, str) or m.padding_mode != "zeros":
-                    raise ExportError(f"{n.target}: only groups = 1, zero-padded convolutions")
+                if isinstance(m.padding, str) or m.padding_mode != "zeros":
+                    raise ExportError(f"{n.target}: only zero-padded convolutions with explicit padding")
                 ins = [x, param(m.weight, n.target + ".weight")]
                 if m.bias is not None:
                     ins.append(param(m.bias, n.target + ".bias"))
-                emit(n, "conv2d", *ins, stride=_pair(m.stride), padding=_pair(m.padding), dilation=_pair(m.dilation))
+                g = {"groups": int(m.groups)} if m.groups != 1 else {}
+                emit(n, "conv2d", *ins, stride=_pair(m.stride), padding=_pair(m.padding), dilation=_pair(m.dilation),
+                     **g)
             elif isinstance(m, nn.BatchNorm2d):
                 if m.running_mean is None:
                     raise ExportError(f"{n.target}: BatchNorm without running statistics")

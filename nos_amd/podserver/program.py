@@ -288,9 +288,11 @@ def _infer(node: Node, ins: list[Value], gpu: bool) -> tuple[tuple[int, ...], st
         arity(2, 3)
         dt = same_dtype()
         x, w = ins[0], ins[1]
-        _req(len(x.shape) == 4 and len(w.shape) == 4 and x.shape[1] == w.shape[1],
-             f"{what}: x [N, C, H, W] and weight [OC, C, KH, KW] required, got {x.shape} and {w.shape}")
-        _req(a.get("groups", 1) == 1, f"{what}: only groups = 1 convolutions run on the pod server")
+        g = a.get("groups", 1)
+        _req(isinstance(g, int) and not isinstance(g, bool) and 1 <= g <= 65536, f"{what}: groups must be an int >= 1")
+        _req(len(x.shape) == 4 and len(w.shape) == 4 and x.shape[1] == w.shape[1] * g and w.shape[0] % g == 0,
+             f"{what}: x [N, C, H, W] and weight [OC, C / groups, KH, KW] (OC % groups == 0) required, got "
+             f"{x.shape} and {w.shape} for groups = {g}")
         if len(ins) == 3:
             _req(ins[2].shape == (w.shape[0],), f"{what}: bias must be [{w.shape[0]}]")
         st = _pair(a.get("stride", [1, 1]), f"{what}: stride", 1)
@@ -438,10 +440,10 @@ def _workspace(node: Node, ins: list[Value], out: Value, f32_math: str) -> int:
         return _attn_ws(b, sq, skv, h, hkv, d) + copies + out.numel * 4
     if op == "conv2d":
         n, c, _, _ = ins[0].shape
-        oc, _, kh, kw = ins[1].shape
+        oc, cg, kh, kw = ins[1].shape
         p = out.numel // (n * oc)
-        kp = -(-(c * kh * kw) // 32) * 32
-        return n * p * (kp * 4 + 4) + ins[0].numel * 4 + out.numel * 4
+        kp = -(-(cg * kh * kw) // 32) * 32
+        return n * (c // cg) * p * (kp * 4 + 4) + ins[0].numel * 4 + out.numel * 4
     if op == "matmul":
         k = ins[0].shape[-1]
         kp = -(-k // 32) * 32
@@ -741,7 +743,7 @@ def _eager(op: str, args: list, attrs: dict, ref: bool = False):
         return torch.rsqrt(args[0])
     if op == "conv2d":
         return F.conv2d(args[0], args[1], args[2] if len(args) > 2 else None, _pair2(attrs, "stride", 1),
-                        _pair2(attrs, "padding", 0), _pair2(attrs, "dilation", 1))
+                        _pair2(attrs, "padding", 0), _pair2(attrs, "dilation", 1), attrs.get("groups", 1))
     if op == "batchnorm":
         return F.batch_norm(args[0], args[3], args[4], args[1], args[2], False, 0.0, attrs.get("eps", 1e-5))
     if op == "max_pool2d":
@@ -1505,7 +1507,7 @@ class CompiledProgram:
                 y = T.conv2d(a[0], a[1], a[2] if len(a) > 2 else None, _pair2(s.attrs, "stride", 1),
                              _pair2(s.attrs, "padding", 0), _pair2(s.attrs, "dilation", 1), act=s.attrs.get("act"),
                              residual=res, w2=self.aux.get(s.attrs.get("w2")),
-                             residual_first=bool(s.attrs.get("residual_first")))
+                             residual_first=bool(s.attrs.get("residual_first")), groups=s.attrs.get("groups", 1))
             elif k == "linear_rms":
                 y = T.linear_rms(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"), eps=s.attrs["eps"])
             elif k == "matmul":

@@ -68,6 +68,25 @@ def test_conv2d_h3_matches_fp64(cfg, epi):
     _close_to_fp64(got, ref64, f32)
 
 
+@pytest.mark.parametrize("n,c,oc,k,s,groups", [(1, 32, 32, 3, 1, 32), (2, 24, 48, 3, 2, 4), (2, 64, 64, 5, 1, 64),
+                                              (1, 12, 36, 1, 1, 3)])
+def test_grouped_conv2d_h3_matches_fp64(n, c, oc, k, s, groups):
+    """Grouped / depthwise convolutions: one batched h3 GEMM per image over
+    the groups, bias per group, residual before the ReLU."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(n, c, 19, 23, device="cuda", generator=g)
+    w = torch.randn(oc, c // groups, k, k, device="cuda", generator=g) / math.sqrt(c // groups * k * k)
+    b = torch.randn(oc, device="cuda", generator=g)
+    pd = (k // 2, k // 2)
+    ref = F.conv2d(x.double(), w.double(), b.double(), (s, s), pd, 1, groups)
+    r = torch.randn(ref.shape, device="cuda", generator=g)
+    ref64 = F.relu(ref + r.double())
+    got = T.conv2d(x, w, b, (s, s), pd, (1, 1), act="relu", residual=r, residual_first=True, groups=groups)
+    f32 = F.relu(F.conv2d(x, w, b, (s, s), pd, 1, groups) + r)
+    assert got.shape == ref64.shape
+    _close_to_fp64(got, ref64, f32)
+
+
 @pytest.mark.parametrize("shapes", [((4, 100, 96), (4, 96, 70)), ((2, 3, 33, 64), (2, 3, 64, 40)),
                                     ((5, 64, 128), (128, 256)), ((300, 50), (3, 50, 64))])
 def test_matmul_h3_matches_fp64(shapes):

@@ -41,6 +41,45 @@ def test_resnet_program_matches_the_module():
     assert torch.allclose(p.reference(x)[0], ref, atol=1e-5, rtol=1e-5)
 
 
+class MobileBlock(nn.Module):
+    """Depthwise-separable and grouped convolutions (MobileNet / ResNeXt
+    style): depthwise 3x3 + BN + ReLU, pointwise 1x1, grouped 3x3 stride 2."""
+
+    def __init__(self, c=16):
+        super().__init__()
+        self.dw = nn.Conv2d(c, c, 3, padding=1, groups=c, bias=False)
+        self.bn = nn.BatchNorm2d(c)
+        self.pw = nn.Conv2d(c, 2 * c, 1)
+        self.gc = nn.Conv2d(2 * c, 2 * c, 3, stride=2, padding=1, groups=4)
+        self.pool = nn.AdaptiveAvgPool2d(1)
+        self.fc = nn.Linear(2 * c, 10)
+        g = torch.Generator().manual_seed(0)
+        with torch.no_grad():
+            for p in self.parameters():
+                p.copy_(torch.randn(p.shape, generator=g) * 0.2)
+            self.bn.running_mean.copy_(torch.randn(c, generator=g) * 0.1)
+            self.bn.running_var.copy_(torch.rand(c, generator=g) + 0.5)
+
+    def forward(self, x):
+        x = torch.relu(self.bn(self.dw(x)))
+        x = torch.relu(self.pw(x))
+        x = self.gc(x)
+        return self.fc(torch.flatten(self.pool(x), 1))
+
+
+def test_grouped_and_depthwise_convs_export_and_match():
+    m = MobileBlock().eval()
+    x = torch.randn(2, 16, 20, 20)
+    prog, w = export(m, x, name="mobile")
+    p = PG.parse(prog, w, gpu=True)
+    cm = p.compile("cpu")
+    assert cm.stats["batchnorm_folded"] == 1
+    assert [n.attrs.get("groups", 1) for n in p.nodes if n.op == "conv2d"] == [16, 1, 4]
+    with torch.no_grad():
+        ref = m(x)
+    assert torch.allclose(cm(x)[0], ref, atol=1e-5, rtol=1e-5)
+
+
 def test_llama_program_matches_hf(llama):
     m, (prog, w) = llama
     p = PG.parse(prog, w, gpu=True)
@@ -69,16 +108,16 @@ def test_llama_bf16_program_tracks_the_fp32_module(llama):
 
 
 def test_export_refuses_what_a_program_cannot_express():
-    class Grouped(nn.Module):
+    class Same(nn.Module):
         def __init__(self):
             super().__init__()
-            self.c = nn.Conv2d(8, 8, 3, groups=8)
+            self.c = nn.Conv2d(8, 8, 3, padding="same")
 
         def forward(self, x):
             return self.c(x)
 
-    with pytest.raises(ExportError, match="groups"):
-        export(Grouped(), torch.zeros(1, 8, 8, 8))
+    with pytest.raises(ExportError, match="explicit padding"):
+        export(Same(), torch.zeros(1, 8, 8, 8))
 
     class Odd(nn.Module):
         def __init__(self):
@@ -93,7 +132,7 @@ def test_export_refuses_what_a_program_cannot_express():
 
 
 @pytest.mark.parametrize("node,match", [
-    ({"op": "conv2d", "inputs": ["x", "w4"], "output": "y", "attrs": {"groups": 2}}, "groups = 1"),
+    ({"op": "conv2d", "inputs": ["x", "w4"], "output": "y", "attrs": {"groups": 2}}, "OC % groups"),
     ({"op": "softmax", "inputs": ["x"], "output": "y", "attrs": {"dim": 0}}, "last dim"),
     ({"op": "sdpa", "inputs": ["q32", "q32", "q32"], "output": "y"}, "head_dim 64 or 128"),
     ({"op": "embedding", "inputs": ["x", "w2"], "output": "y"}, "ids must be i32"),

@@ -119,3 +119,24 @@ def test_bf16_tenant_programs_run_on_gpu(family):
         got = cm(inp)[0].float().cpu()
     assert torch.isfinite(got).all()
     assert (got - ref).abs().max() <= 0.05 * ref.abs().max(), float((got - ref).abs().max() / ref.abs().max())
+
+
+def test_grouped_conv_program_on_gpu_matches_fp64():
+    """Depthwise + grouped convolutions exported from torch.nn run on the h3
+    kernels within 4x torch-fp32's error against fp64."""
+    from test_tenant_programs import MobileBlock
+
+    from nos_amd.podserver.export import export
+
+    m = MobileBlock().eval()
+    x = torch.randn(2, 16, 20, 20)
+    prog, w = export(m, x, name="mobile")
+    cm = PG.parse(prog, w, gpu=True).compile("cuda")
+    xc = x.cuda()
+    with torch.no_grad():
+        got = cm(xc)[0]
+        mc = m.cuda()
+        f32 = mc(xc)
+        ref64 = mc.double()(xc.double())
+    e, e32 = _err(got, ref64), _err(f32, ref64)
+    assert e <= max(4 * e32, 1e-5), (e, e32)
