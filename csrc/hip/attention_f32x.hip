@@ -404,6 +404,7 @@ __global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_
     // ---- Q pieces (B operand) on this query row's scale: lane holds
     // Q[row r][d = 16ks + 8hh .. +7] * c * 2^e
     const int qrow = qb * HQBLK + wid * 32 + r;
+    const bool live = qb * HQBLK + wid * 32 < Sq;  // wave-uniform
     f16x8_t qf[4][2];
     float fs;  // s' -> exp2 units: 2^-e / ksc
     {
@@ -479,6 +480,12 @@ __global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_
 #pragma unroll
           for (int i = 0; i < PPW; ++i) stage_piece(t + 1, buf ^ 1, i);
         }
+      }
+      // a wave whose 32 query rows all lie past Sq (the last query block of a
+      // head, a query range) only stages and keeps the barriers
+      if (!live) {
+        dma_wait_publish();
+        return;
       }
       const unsigned char* kl = smem + buf * H3_STAGE;
       const unsigned char* vl = kl + 2 * IMG;
