@@ -90,6 +90,18 @@ __device__ __forceinline__ void dma_wait_publish() {
   __syncthreads();
 }
 
+// the same with the newest N DMAs left in flight (a deeper ring): a counted
+// vmcnt and a raw barrier -- __syncthreads() would drain them (vmcnt(0))
+template <int N>
+__device__ __forceinline__ void dma_wait_publish_keep(bool keep) {
+  if (keep)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
 template <bool PERSIST>
 __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
     const float* __restrict__ q, const unsigned short* __restrict__ kvs, float* __restrict__ o, int B, int H, int Sq,
@@ -334,7 +346,8 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
 // the one FMA that already turns a score into exp2 units; P <= 2^8 (deferred
 // rescale) needs no scale; the value scale is divided out with 1/l.
 constexpr int H3_STAGE = 4 * IMG;            // K hi, K lo, V hi, V lo
-constexpr int H3_LDS_BYTES = 2 * H3_STAGE;   // 32 KiB ring
+constexpr int H3_RING = 2;  // stages; 3 (two tiles in flight) measured slower: 138 VGPRs, 802 vs 818 inf/s
+constexpr int H3_LDS_BYTES = H3_RING * H3_STAGE;  // 48 KiB
 constexpr int H3_WG_PER_CU = 4;  // 4-wave workgroups (HW = 4); HW = 8: 2
 
 // HW waves per workgroup (4 or 8) x 32 query rows; the 16 DMA pieces of a
@@ -454,8 +467,22 @@ __global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_
       glds16_s(pb + (long long)t * (KVB * 4) * ldh, (unsigned)soff[i] * 2u,
                smem + buf * H3_STAGE + (p >> 2) * IMG + (p & 3) * 8 * 128);
     };
+    // tile u into ring slot `slot` (full tiles from a uniform base)
+    auto stage_tile = [&](int u, int slot) {
+      if ((u + 1) * KVB <= Skv) {
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) stage_full(u, slot, i);
+      } else {
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) stage_piece(u, slot, i);
+      }
+    };
+    // the first H3_RING - 1 tiles in flight; tile t0 landed and published
 #pragma unroll
     for (int i = 0; i < PPW; ++i) stage_piece(t0, 0, i);
+#pragma unroll
+    for (int q = 1; q < H3_RING - 1; ++q)
+      if (t0 + q < t1) stage_tile(t0 + q, q);
 
     f32x16_t oacc[2];
 #pragma unroll
@@ -465,26 +492,23 @@ __global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_
     }
     float m = 0.f, l = 0.f;
 
-    dma_wait_publish();
+    static_assert(H3_RING == 2 || H3_RING == 3, "ring depth");
+    dma_wait_publish_keep<PPW>(H3_RING == 3 && t0 + 1 < t1);
 
     // the tile body; MASKED: the tail tile (keys past Skv masked).  Peeled out of
     // the main loop -- if-converted into it, the mask cost 48 VALU per tile
     auto tile = [&](int t, auto masked) {
       constexpr bool MASKED = decltype(masked)::value;
-      const int buf = (t - t0) & 1;
-      if (t + 1 < t1) {
-        if ((t + 2) * KVB <= Skv) {
-#pragma unroll
-          for (int i = 0; i < PPW; ++i) stage_full(t + 1, buf ^ 1, i);
-        } else {
-#pragma unroll
-          for (int i = 0; i < PPW; ++i) stage_piece(t + 1, buf ^ 1, i);
-        }
-      }
+      const int buf = (t - t0) % H3_RING;
+      // tile t + H3_RING - 1 into the slot tile t - 1 left (every wave passed
+      // the barrier that ended tile t - 1)
+      if (t + H3_RING - 1 < t1) stage_tile(t + H3_RING - 1, (t - t0 + H3_RING - 1) % H3_RING);
+      // at the end: tile t + 1 landed (the ring's newer tile may stay in flight)
+      const bool keep = H3_RING == 3 && t + 2 < t1;
       // a wave whose 32 query rows all lie past Sq (the last query block of a
       // head, a query range) only stages and keeps the barriers
       if (!live) {
-        dma_wait_publish();
+        dma_wait_publish_keep<PPW>(keep);
         return;
       }
       const unsigned char* kl = smem + buf * H3_STAGE;
@@ -553,7 +577,7 @@ __global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_
           }
           oacc[db] = nos::mma3h(a, pf[s2], oacc[db]);
         }
-      dma_wait_publish();
+      dma_wait_publish_keep<PPW>(keep);
     };
     const int tm = (Skv % KVB) ? max(t0, min(t1, ntiles - 1)) : t1;  // the tail tile, if any, is the last
     for (int t = t0; t < tm; ++t) tile(t, std::false_type{});
