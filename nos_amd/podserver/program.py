@@ -1463,18 +1463,21 @@ class CompiledProgram:
                 rs = bool(s.attrs.get("row_stats")) and ops.ln_handoff_active() and (
                     isinstance(a[0], ops.H3Planes) or (a[0].is_cuda and a[0].dtype.itemsize == 4))
                 into = s.attrs.get("out_into")  # (buffer, dim, offset): a slab of a cat's buffer
+                # rows with unit inner stride go in as they are (a merged GEMM's
+                # column slice: the kernels take the row stride); others are copied
+                xa = a[0] if isinstance(a[0], ops.H3Planes) else _rows(a[0])
                 if isinstance(a[0], ops.H3Planes):
                     y = ops.linear_planes(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
                                           residual=res, row_stats=rs)
                 elif into is not None:
                     dst = self.aux[into[0]].narrow(into[1], into[2], self._shape(s.output)[into[1]])
-                    y = ops.linear(a[0].contiguous(), a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
+                    y = ops.linear(xa, a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
                                    residual=res, out=dst if dst.is_cuda else None)
                     if y.data_ptr() != dst.data_ptr():
                         dst.copy_(y)
                     y = dst
                 else:
-                    y = ops.linear(a[0].contiguous(), a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
+                    y = ops.linear(xa, a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
                                    residual=res, row_stats=rs)
                 if rs:
                     y, env[s.output + "::lnp"] = y
@@ -1541,6 +1544,18 @@ class CompiledProgram:
             for r in s.release:
                 env.pop(r, None)
         return tuple(env[o] for o in self.outputs)
+
+
+def _rows(x):
+    """x as-is when its rows [..., K] view as a 2-D [M, K] with unit inner
+    stride and 16-byte-aligned rows (what the GEMMs take), else contiguous."""
+    if x.stride(-1) == 1 and x.element_size() * x.stride(-2 if x.dim() > 1 else -1) % 16 == 0 and x.data_ptr() % 16 == 0:
+        try:
+            x.view(-1, x.shape[-1])
+            return x
+        except RuntimeError:
+            pass
+    return x.contiguous()
 
 
 def _relayout(x, chain, dtype: str):
