@@ -146,7 +146,7 @@ def _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K):
     o2, r2 = _gemm_io(x, weight, out, residual, M, N, K)
     _check_f32(residual=r2)
     ldr = r2.stride(0) if r2 is not None else 0
-    if _F32_MATH == "h3":
+    if _F32_MATH == "h3" and M > H3_MIN_ROWS:
         ap, rinv = _split_rows_h3(x2, ln=False)
         _gemm_h3(ap, rinv, weight, bias, r2, o2, _epi(bias, act, residual))
     elif _F32_MATH == "x6":
@@ -164,6 +164,10 @@ def _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K):
 
 
 _F32_MATH = "exact"
+# h3 math: a GEMM of at most this many rows (YOLOS's detection-head layers on
+# their 100 tokens) runs on the exact-f32 MFMA kernel -- one launch, no split
+# pass, the f32 pipe's rate is ample for ~30 MFLOP -- instead of split + h3 GEMM
+H3_MIN_ROWS = int(__import__("os").environ.get("NOS_AMD_H3_MIN_ROWS", "128"))
 _SPLIT_CACHE: dict[int, tuple] = {}
 _SPLIT_H3_CACHE: dict[int, tuple] = {}
 
@@ -279,17 +283,23 @@ class RowStats(NamedTuple):
 
 
 def linear_planes(a: H3Planes, weight: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
-                  residual: torch.Tensor | None = None, row_stats: bool = False):
+                  residual: torch.Tensor | None = None, row_stats: bool = False, out: torch.Tensor | None = None):
     """act(A @ weight^T + bias) + residual for an A handed over as h3 planes
     (see :class:`H3Planes`): no split pre-pass, no fp32 round trip of A.
     ``row_stats``: also return the output's row statistics for the next
-    LN-GEMM (``nos_gemm_f32h3_stats``) -- ``(out, RowStats)``."""
+    LN-GEMM (``nos_gemm_f32h3_stats``) -- ``(out, RowStats)``.  ``out``: an
+    [M, N]-viewable fp32 destination (e.g. a slab of a cat's buffer)."""
     M, K = a.planes.shape[1], a.planes.shape[2]
     N = weight.shape[0]
     if weight.dim() != 2 or weight.shape[1] != K or weight.dtype != torch.float32 or weight.stride(-1) != 1:
         raise ValueError(f"weight must be fp32 [N, {K}] with unit inner stride")
     _check_f32(bias=bias)
-    out = torch.empty((M, N), dtype=torch.float32, device=a.planes.device)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.planes.device)
+    else:
+        if out.dtype != torch.float32 or out.numel() != M * N:
+            raise ValueError(f"out must hold fp32 [{M}, {N}]")
+        out = out.view(M, N)
     r2 = None
     if residual is not None:
         if residual.numel() != M * N or residual.dtype != torch.float32:

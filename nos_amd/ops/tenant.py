@@ -270,6 +270,27 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, s
     return out if dt == torch.float32 else out.to(dt)
 
 
+def patches(x: torch.Tensor, ph: int, pw: int):
+    """A ViT's patch rows of an fp32 NCHW image: [N, (H/ph)(W/pw), C ph pw]
+    with columns (c, dy, dx).  On the GPU under h3 math, the GEMM's A planes
+    straight from the image (im2col with stride = kernel, no padding) as
+    :class:`ops.H3Planes`; otherwise the PyTorch views + copy."""
+    from .. import ops
+
+    N, C, H, W = x.shape
+    hp, wp = H // ph, W // pw
+    K = C * ph * pw
+    if not (x.is_cuda and x.dtype == torch.float32 and ops.h3_planes_active() and K % 32 == 0):
+        return x.reshape(N, C, hp, ph, wp, pw).permute(0, 2, 4, 1, 3, 5).reshape(N, hp * wp, K)
+    xf = x.contiguous()
+    P = hp * wp
+    planes = torch.empty((2, N * P, K), dtype=torch.float16, device=x.device)
+    prinv = torch.empty((N * P,), dtype=torch.float32, device=x.device)
+    _lib.check(_lib.lib().nos_im2col_h3(xf.data_ptr(), planes.data_ptr(), N * P * K, prinv.data_ptr(), N, C, H, W, ph,
+                                        pw, ph, pw, 0, 0, 1, 1, K, _stream()), "nos_im2col_h3")
+    return ops.H3Planes(planes, prinv, 0.0, (N, P, K))
+
+
 def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """a [..., M, K] @ b [..., K, N]; batch dims equal, or one side 2-D."""
     if not a.is_cuda:

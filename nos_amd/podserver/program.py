@@ -53,6 +53,7 @@ runs the unfused graph eagerly in fp32 (the numerics reference of tests).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -815,9 +816,15 @@ class CompiledProgram:
         self._new_shapes: dict[str, tuple] = {}   # values the passes create or re-shape
         self._new_dtypes: dict[str, str] = {}
         with torch.no_grad():
+            # NOS_AMD_SKIP_PASSES=name,...: leave launch-trimming passes out (A/B runs)
+            skip = set(os.environ.get("NOS_AMD_SKIP_PASSES", "").split(","))
             steps = self._fold_constants(prog)
-            steps = self._distribute_add_over_cat(steps)
-            steps = self._fuse_cast_relayout(steps)
+            if "add_over_cat" not in skip:
+                steps = self._distribute_add_over_cat(steps)
+            if "cast_relayout" not in skip:
+                steps = self._fuse_cast_relayout(steps)
+            if "patchify" not in skip:
+                steps = self._fuse_patchify(steps)
             steps = self._pushdown_row_slices(steps)
             steps = self._fold_batchnorm(steps)
             steps = self._merge_parallel_linears(steps)
@@ -826,7 +833,8 @@ class CompiledProgram:
             steps = self._fuse_epilogues(steps)
             steps = self._fuse_qkv_attention(steps)
             steps = self._fuse_rotary_sdpa(steps)
-            steps = self._cat_into_buffer(steps)
+            if "cat_buffer" not in skip:
+                steps = self._cat_into_buffer(steps)
             steps = self._mark_plane_handoffs(steps)
             steps = self._mark_ln_handoffs(steps)
             self._prep_conv_weights(steps)
@@ -902,6 +910,44 @@ class CompiledProgram:
             n += 1
         self.stats["cats_in_place"] = n
         return steps
+
+    def _fuse_patchify(self, steps: list[_Step]) -> list[_Step]:
+        """reshape [N, C, H/ph, ph, W/pw, pw] -> permute (0, 2, 4, 1, 3, 5) ->
+        reshape [N, P, C ph pw] of an fp32 image, read only by linears: a
+        ViT's patch extraction.  One ``patches`` step: under h3 math the
+        im2col kernel writes the patch rows straight as the GEMM's h3 planes
+        (``nos_im2col_h3``: stride = kernel, no padding) -- no copy, no split
+        pass; elsewhere the same views in PyTorch."""
+        uses = self._consumers(steps, self.outputs)
+        by_in: dict[str, list[_Step]] = {}
+        for s in steps:
+            for i in s.inputs:
+                by_in.setdefault(i, []).append(s)
+        drop: set[int] = set()
+        n = 0
+        for r1 in steps:
+            if r1.kind != "reshape" or uses.get(r1.output) != 1 or self._dtype(r1.inputs[0]) != "fp32":
+                continue
+            xs = tuple(self._shape(r1.inputs[0]))
+            sh = tuple(r1.attrs["shape"])
+            if len(xs) != 4 or len(sh) != 6 or sh[0] != xs[0] or sh[1] != xs[1] or sh[2] * sh[3] != xs[2] \
+                    or sh[4] * sh[5] != xs[3]:
+                continue
+            pm = by_in[r1.output][0]
+            if pm.kind != "permute" or list(pm.attrs["dims"]) != [0, 2, 4, 1, 3, 5] or uses.get(pm.output) != 1:
+                continue
+            r2 = by_in[pm.output][0]
+            N, C, hp, ph, wp, pw = sh
+            if (r2.kind != "reshape" or list(r2.attrs["shape"]) != [N, hp * wp, C * ph * pw] or (C * ph * pw) % 32
+                    or r2.output in self.outputs
+                    or not all(c.kind == "linear" and c.inputs[0] == r2.output for c in by_in.get(r2.output, []))):
+                continue
+            drop.add(id(r1))
+            drop.add(id(pm))
+            r2.kind, r2.inputs, r2.attrs = "patches", [r1.inputs[0]], {"ph": ph, "pw": pw}
+            n += 1
+        self.stats["patchify_fused"] = n
+        return [s for s in steps if id(s) not in drop]
 
     def _fuse_cast_relayout(self, steps: list[_Step]) -> list[_Step]:
         """cast -> reshape / permute chain (each value read once) -> ONE
@@ -1467,8 +1513,11 @@ class CompiledProgram:
                 # column slice: the kernels take the row stride); others are copied
                 xa = a[0] if isinstance(a[0], ops.H3Planes) else _rows(a[0])
                 if isinstance(a[0], ops.H3Planes):
+                    dst = self.aux[into[0]].narrow(into[1], into[2], self._shape(s.output)[into[1]]) if into else None
                     y = ops.linear_planes(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
-                                          residual=res, row_stats=rs)
+                                          residual=res, row_stats=rs, out=dst)
+                    if dst is not None:
+                        y = (dst, y[1]) if rs else dst
                 elif into is not None:
                     dst = self.aux[into[0]].narrow(into[1], into[2], self._shape(s.output)[into[1]])
                     y = ops.linear(xa, a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
@@ -1536,6 +1585,8 @@ class CompiledProgram:
                     y = F.layer_norm(xx, (xx.shape[-1],), a[1], a[2], s.attrs.get("eps", 1e-5))
             elif k == "relayout":
                 y = _relayout(a[0], s.attrs["chain"], s.attrs["dtype"])
+            elif k == "patches":
+                y = T.patches(a[0], s.attrs["ph"], s.attrs["pw"])
             elif k == "cat_buffer":  # its GEMM part was written in place; the constant parts at build
                 y = self.aux[s.attrs["buf"]]
             else:
