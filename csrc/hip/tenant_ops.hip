@@ -122,6 +122,30 @@ __global__ __launch_bounds__(256) void rotary_kernel(const void* __restrict__ x,
   st_from_f32(y, yo + d + hd, fmaf(x1, c[d + hd], x0 * sv[d + hd]), bf16);
 }
 
+// ------------------------------------------------------------------ cast + unary
+// y = f(x) with the input and output dtypes independent (fp32 / bf16): a
+// cast next to an activation (a bf16 head's fp32 sigmoid output) is one pass,
+// f evaluated in fp32 and rounded once.  op: 0 identity, 1 relu, 2 sigmoid,
+// 3 silu, 4 gelu (erf), 5 tanh, 6 exp, 7 neg.
+__global__ __launch_bounds__(256) void unary_kernel(const void* __restrict__ x, int xbf, void* __restrict__ y, int ybf,
+                                                    long long n, int op) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float v = ld_as_f32(x, i, xbf);
+  float r;
+  switch (op) {
+    case 1: r = fmaxf(v, 0.f); break;
+    case 2: r = 1.f / (1.f + expf(-v)); break;
+    case 3: r = v / (1.f + expf(-v)); break;
+    case 4: r = 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); break;
+    case 5: r = tanhf(v); break;
+    case 6: r = expf(v); break;
+    case 7: r = -v; break;
+    default: r = v;
+  }
+  st_from_f32(y, i, r, ybf);
+}
+
 // ------------------------------------------------------------------ conv2d im2col -> h3 planes
 // The patches of one NCHW image as the B operand of the h3 GEMM
 // out[n][oc][p] = sum_k W[oc][k] patch[n][p][k] (k = (c, kh, kw), torch's
@@ -131,11 +155,16 @@ __global__ __launch_bounds__(256) void rotary_kernel(const void* __restrict__ x,
 // A half-wave per patch row: pass 1 gathers the row's max, pass 2 gathers
 // again (L1/L2 hits: neighbouring rows of the block overlap) and writes the
 // pieces -- 32 lanes write 64 contiguous bytes of a plane row per step.
-template <int KH, int KW>
-__global__ __launch_bounds__(256) void im2col_h3_kernel(const float* __restrict__ x, _Float16* __restrict__ P,
+// The image is read through strides (unit stride along W): a cropped view
+// (a ViT's input sliced to whole patches) needs no contiguous copy.  BF:
+// plain bf16 rows instead (a bf16 tenant's patch GEMM operand; no scale,
+// no max pass, rinv unused) -- the image's cast and patch relayout in one pass.
+template <int KH, int KW, bool BF>
+__global__ __launch_bounds__(256) void im2col_h3_kernel(const float* __restrict__ x, void* __restrict__ Pv,
                                                         long long pplane, float* __restrict__ rinv, int Nimg, int C,
-                                                        int H, int W, int OH, int OW, int kh_rt, int kw_rt, int sh,
-                                                        int sw, int ph, int pw, int dh, int dw, int K, int Kp) {
+                                                        int H, int W, long long sN, long long sC, long long sH, int OH,
+                                                        int OW, int kh_rt, int kw_rt, int sh, int sw, int ph, int pw,
+                                                        int dh, int dw, int K, int Kp) {
   const int kh_n = KH > 0 ? KH : kh_rt, kw_n = KW > 0 ? KW : kw_rt;
   const int khw = kh_n * kw_n;
   const long long P1 = (long long)OH * OW;
@@ -146,22 +175,27 @@ __global__ __launch_bounds__(256) void im2col_h3_kernel(const float* __restrict_
   const int p = (int)(row - n * P1);
   const int oh = p / OW, ow = p - oh * OW;
   const int ih0 = oh * sh - ph, iw0 = ow * sw - pw;
-  const float* xn = x + (long long)n * C * H * W;
+  const float* xn = x + (long long)n * sN;
   auto gather = [&](int k) -> float {
     if (k >= K) return 0.f;
     const int c = k / khw;
     const int r = k - c * khw;
     const int i = r / kw_n, j = r - i * kw_n;
     const int ih = ih0 + i * dh, iw = iw0 + j * dw;
-    return (ih >= 0 && ih < H && iw >= 0 && iw < W) ? xn[((long long)c * H + ih) * W + iw] : 0.f;
+    return (ih >= 0 && ih < H && iw >= 0 && iw < W) ? xn[c * sC + ih * sH + iw] : 0.f;
   };
+  if constexpr (BF) {
+    unsigned short* pb = static_cast<unsigned short*>(Pv) + row * Kp;
+    for (int k = lane; k < Kp; k += 32) pb[k] = nos::f32_to_bf16(gather(k));
+    return;
+  }
   float mx = 0.f;
   for (int k = lane; k < K; k += 32) mx = fmaxf(mx, fabsf(gather(k)));
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
   const int e = nos::h3_scale_exp(mx);
   const float sc = nos::pow2i(e);
-  _Float16* ph_ = P + row * Kp;
+  _Float16* ph_ = static_cast<_Float16*>(Pv) + row * Kp;
   _Float16* pl_ = ph_ + pplane;
   for (int k = lane; k < Kp; k += 32) {
     const float v = gather(k) * sc;
@@ -212,32 +246,52 @@ NOS_API int nos_rotary(const void* x, const float* cos_t, const float* sin_t, vo
   return (int)hipGetLastError();
 }
 
-// Patches of x [N, C, H, W] (fp32, contiguous) for a KHxKW conv (stride,
-// padding, dilation) as h3 planes: hi at P, lo at P + pplane elements, rows
-// [N * OH * OW][Kp], Kp % 32 == 0, Kp >= C * KH * KW; rinv [N * OH * OW].
-NOS_API int nos_im2col_h3(const float* x, void* P, long long pplane, float* rinv, int N, int C, int H, int W, int KH,
-                          int KW, int sh, int sw, int ph, int pw, int dh, int dw, int Kp, hipStream_t stream) {
+// Patches of x [N, C, H, W] (fp32; element strides sN / sC / sH, unit
+// stride along W) for a KHxKW conv (stride, padding, dilation): rows
+// [N * OH * OW][Kp], Kp >= C * KH * KW, columns past K zero.  bf16 == 0: h3
+// planes, hi at P, lo at P + pplane elements, Kp % 32 == 0, rinv [N * OH *
+// OW]; bf16 == 1: one bf16 matrix at P (pplane, rinv unused).
+NOS_API int nos_im2col(const float* x, long long sN, long long sC, long long sH, void* P, long long pplane,
+                       float* rinv, int N, int C, int H, int W, int KH, int KW, int sh, int sw, int ph, int pw, int dh,
+                       int dw, int Kp, int bf16, hipStream_t stream) {
   if (N <= 0 || C <= 0 || H <= 0 || W <= 0 || KH <= 0 || KW <= 0 || sh <= 0 || sw <= 0 || ph < 0 || pw < 0 ||
-      dh <= 0 || dw <= 0)
+      dh <= 0 || dw <= 0 || (bf16 != 0 && bf16 != 1) || sH < W || sC < (long long)(H - 1) * sH + W ||
+      (N > 1 && sN < (long long)(C - 1) * sC + (long long)(H - 1) * sH + W))
     return (int)hipErrorInvalidValue;
   const int OH = (H + 2 * ph - dh * (KH - 1) - 1) / sh + 1, OW = (W + 2 * pw - dw * (KW - 1) - 1) / sw + 1;
   const long long K = (long long)C * KH * KW;
   const long long rows = (long long)N * OH * OW;
-  if (OH <= 0 || OW <= 0 || K > INT_MAX || Kp < K || (Kp % 32) || pplane < rows * Kp || rows > (1LL << 31))
+  if (OH <= 0 || OW <= 0 || K > INT_MAX || Kp < K || rows > (1LL << 31) ||
+      (!bf16 && ((Kp % 32) || pplane < rows * Kp)))
     return (int)hipErrorInvalidValue;
-  auto* p = static_cast<_Float16*>(P);
   const dim3 grid((unsigned)((rows + 7) / 8)), blk(256);
-#define NOS_IM2COL(kh, kw)                                                                                       \
-  hipLaunchKernelGGL((im2col_h3_kernel<kh, kw>), grid, blk, 0, stream, x, p, pplane, rinv, N, C, H, W, OH, OW, KH, \
-                     KW, sh, sw, ph, pw, dh, dw, (int)K, Kp)
-  if (KH == 1 && KW == 1)
-    NOS_IM2COL(1, 1);
+#define NOS_IM2COL(kh, kw, bf)                                                                                        \
+  hipLaunchKernelGGL((im2col_h3_kernel<kh, kw, bf>), grid, blk, 0, stream, x, P, pplane, rinv, N, C, H, W, sN, sC, sH, \
+                     OH, OW, KH, KW, sh, sw, ph, pw, dh, dw, (int)K, Kp)
+  if (bf16)
+    NOS_IM2COL(0, 0, true);
+  else if (KH == 1 && KW == 1)
+    NOS_IM2COL(1, 1, false);
   else if (KH == 3 && KW == 3)
-    NOS_IM2COL(3, 3);
+    NOS_IM2COL(3, 3, false);
   else if (KH == 7 && KW == 7)
-    NOS_IM2COL(7, 7);
+    NOS_IM2COL(7, 7, false);
   else
-    NOS_IM2COL(0, 0);
+    NOS_IM2COL(0, 0, false);
 #undef NOS_IM2COL
+  return (int)hipGetLastError();
+}
+
+// the contiguous-image form (conv2d's im2col)
+NOS_API int nos_im2col_h3(const float* x, void* P, long long pplane, float* rinv, int N, int C, int H, int W, int KH,
+                          int KW, int sh, int sw, int ph, int pw, int dh, int dw, int Kp, hipStream_t stream) {
+  return nos_im2col(x, (long long)C * H * W, (long long)H * W, W, P, pplane, rinv, N, C, H, W, KH, KW, sh, sw, ph, pw,
+                    dh, dw, Kp, 0, stream);
+}
+
+NOS_API int nos_unary(const void* x, int xbf16, void* y, int ybf16, long long n, int op, hipStream_t stream) {
+  if (n <= 0 || op < 0 || op > 7 || (xbf16 != 0 && xbf16 != 1) || (ybf16 != 0 && ybf16 != 1))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(unary_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, xbf16, y, ybf16, n, op);
   return (int)hipGetLastError();
 }

@@ -95,6 +95,9 @@ _SIGS = {
     "nos_rotary": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_ll, c_int, c_void_p],
     "nos_im2col_h3": [c_void_p, c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nos_im2col": [c_void_p, c_ll, c_ll, c_ll, c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                   c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "nos_unary": [c_void_p, c_int, c_void_p, c_int, c_ll, c_int, c_void_p],
     "nos_attn_h3g_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
     # LayerNorm hand-off (gemm_f32h.hip): producer row statistics, LN in the consumer's A load
     "nos_gemm_f32h3_stats": [c_void_p, c_int, c_ll, c_void_p, c_float, c_void_p, c_int, c_ll, c_void_p, c_void_p,

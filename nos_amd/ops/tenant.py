@@ -153,6 +153,26 @@ def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float = 1e-6) -> torch.T
     return out.view(x.shape)
 
 
+UNARY_CODES = {"relu": 1, "sigmoid": 2, "silu": 3, "gelu": 4, "tanh": 5, "exp": 6, "neg": 7}
+
+
+def unary(x: torch.Tensor, op: str, dtype: torch.dtype) -> torch.Tensor:
+    """``op`` (a :data:`UNARY_CODES` activation) of fp32 / bf16 x into a
+    ``dtype`` tensor: evaluated in fp32 and rounded once, in one pass on the
+    GPU (a cast beside an activation costs no launch of its own)."""
+    if not x.is_cuda:
+        xf = x.float()
+        y = {"relu": F.relu, "sigmoid": torch.sigmoid, "silu": F.silu, "gelu": F.gelu, "tanh": torch.tanh,
+             "exp": torch.exp, "neg": torch.neg}[op](xf)
+        return y.to(dtype)
+    xc = x.contiguous()
+    out = torch.empty(x.shape, dtype=dtype, device=x.device)
+    if out.numel():
+        _lib.check(_lib.lib().nos_unary(xc.data_ptr(), _bf(xc), out.data_ptr(), int(dtype == torch.bfloat16),
+                                        xc.numel(), UNARY_CODES[op], _stream()), "nos_unary")
+    return out
+
+
 def softmax(x: torch.Tensor) -> torch.Tensor:
     """softmax over the last dim."""
     if not x.is_cuda:
@@ -270,24 +290,43 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, s
     return out if dt == torch.float32 else out.to(dt)
 
 
-def patches(x: torch.Tensor, ph: int, pw: int):
+def patches(x: torch.Tensor, ph: int, pw: int, dtype: torch.dtype = torch.float32, hp: int | None = None,
+            wp: int | None = None):
     """A ViT's patch rows of an fp32 NCHW image: [N, (H/ph)(W/pw), C ph pw]
-    with columns (c, dy, dx).  On the GPU under h3 math, the GEMM's A planes
-    straight from the image (im2col with stride = kernel, no padding) as
-    :class:`ops.H3Planes`; otherwise the PyTorch views + copy."""
+    with columns (c, dy, dx), in ``dtype``.  On the GPU one im2col pass over
+    the image (stride = kernel, no padding; a cropped view is read through
+    its strides, no contiguous copy): fp32 under h3 math as the GEMM's A
+    planes (:class:`ops.H3Planes`), bf16 as the GEMM's bf16 operand (the cast
+    folded in); otherwise the PyTorch views + copy.  ``hp`` x ``wp`` patches
+    from the image's top-left corner (default: as many as fit)."""
     from .. import ops
 
     N, C, H, W = x.shape
-    hp, wp = H // ph, W // pw
+    hp = H // ph if hp is None else hp
+    wp = W // pw if wp is None else wp
+    if not (0 < hp * ph <= H and 0 < wp * pw <= W):
+        raise ValueError(f"patches: {hp}x{wp} patches of {ph}x{pw} exceed the {H}x{W} image")
     K = C * ph * pw
-    if not (x.is_cuda and x.dtype == torch.float32 and ops.h3_planes_active() and K % 32 == 0):
-        return x.reshape(N, C, hp, ph, wp, pw).permute(0, 2, 4, 1, 3, 5).reshape(N, hp * wp, K)
-    xf = x.contiguous()
     P = hp * wp
+    bf = dtype == torch.bfloat16
+    gpu = x.is_cuda and x.dtype == torch.float32 and (bf or (dtype == torch.float32 and ops.h3_planes_active()
+                                                                and K % 32 == 0))
+    if not gpu:
+        x = x[:, :, :hp * ph, :wp * pw]
+        y = x.reshape(N, C, hp, ph, wp, pw).permute(0, 2, 4, 1, 3, 5).reshape(N, P, K)
+        return y.to(dtype)
+    if x.stride(3) != 1:
+        x = x.contiguous()
+    sN, sC, sH = x.stride(0), x.stride(1), x.stride(2)
+    if bf:
+        out = torch.empty((N, P, K), dtype=torch.bfloat16, device=x.device)
+        _lib.check(_lib.lib().nos_im2col(x.data_ptr(), sN, sC, sH, out.data_ptr(), 0, None, N, C, hp * ph, wp * pw, ph,
+                                         pw, ph, pw, 0, 0, 1, 1, K, 1, _stream()), "nos_im2col")
+        return out
     planes = torch.empty((2, N * P, K), dtype=torch.float16, device=x.device)
     prinv = torch.empty((N * P,), dtype=torch.float32, device=x.device)
-    _lib.check(_lib.lib().nos_im2col_h3(xf.data_ptr(), planes.data_ptr(), N * P * K, prinv.data_ptr(), N, C, H, W, ph,
-                                        pw, ph, pw, 0, 0, 1, 1, K, _stream()), "nos_im2col_h3")
+    _lib.check(_lib.lib().nos_im2col(x.data_ptr(), sN, sC, sH, planes.data_ptr(), N * P * K, prinv.data_ptr(), N, C,
+                                     hp * ph, wp * pw, ph, pw, ph, pw, 0, 0, 1, 1, K, 0, _stream()), "nos_im2col")
     return ops.H3Planes(planes, prinv, 0.0, (N, P, K))
 
 

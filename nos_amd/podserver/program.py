@@ -417,7 +417,7 @@ OPS = ("linear", "layernorm", "attention", *BINARY, *UNARY, "cat", "slice", "res
 NEVER_FOLD = ("attention", "sdpa")
 # step kinds that run a gfx950 kernel of libnos_hip.so (CompiledProgram.stats["kernels"])
 NATIVE_KINDS = ("linear", "linear_ln", "linear_rms", "ln_qkv_attention", "attention", "layernorm", "conv2d", "matmul",
-                "softmax", "embedding", "rmsnorm", "rotary", "sdpa")
+                "softmax", "embedding", "rmsnorm", "rotary", "sdpa", "patches", "unary")
 GEMM_OPS = ("linear", "conv2d")
 
 
@@ -821,16 +821,18 @@ class CompiledProgram:
             steps = self._fold_constants(prog)
             if "add_over_cat" not in skip:
                 steps = self._distribute_add_over_cat(steps)
-            if "cast_relayout" not in skip:
-                steps = self._fuse_cast_relayout(steps)
             if "patchify" not in skip:
                 steps = self._fuse_patchify(steps)
+            if "cast_relayout" not in skip:
+                steps = self._fuse_cast_relayout(steps)
             steps = self._pushdown_row_slices(steps)
             steps = self._fold_batchnorm(steps)
             steps = self._merge_parallel_linears(steps)
             steps = self._fold_layernorm(steps)
             steps = self._fold_rmsnorm(steps)
             steps = self._fuse_epilogues(steps)
+            if "cast_unary" not in skip:
+                steps = self._fuse_cast_unary(steps)
             steps = self._fuse_qkv_attention(steps)
             steps = self._fuse_rotary_sdpa(steps)
             if "cat_buffer" not in skip:
@@ -912,22 +914,40 @@ class CompiledProgram:
         return steps
 
     def _fuse_patchify(self, steps: list[_Step]) -> list[_Step]:
-        """reshape [N, C, H/ph, ph, W/pw, pw] -> permute (0, 2, 4, 1, 3, 5) ->
-        reshape [N, P, C ph pw] of an fp32 image, read only by linears: a
-        ViT's patch extraction.  One ``patches`` step: under h3 math the
-        im2col kernel writes the patch rows straight as the GEMM's h3 planes
-        (``nos_im2col_h3``: stride = kernel, no padding) -- no copy, no split
-        pass; elsewhere the same views in PyTorch."""
+        """[cast fp32 -> bf16] -> [crop slices] -> reshape [N, C, H/ph, ph,
+        W/pw, pw] -> permute (0, 2, 4, 1, 3, 5) -> reshape [N, P, C ph pw] of
+        an fp32 image, read only by linears: a ViT's patch extraction.  One
+        ``patches`` step on the image itself: the im2col kernel reads the
+        top-left (H/ph)ph x (W/pw)pw window through the image's strides (the
+        crop is free) and writes the patch rows straight as the GEMM's h3
+        planes (fp32 under h3 math: no copy, no split pass) or as bf16 rows
+        (the cast folded in); elsewhere the same views in PyTorch."""
         uses = self._consumers(steps, self.outputs)
         by_in: dict[str, list[_Step]] = {}
+        by_out = {s.output: s for s in steps}
         for s in steps:
             for i in s.inputs:
                 by_in.setdefault(i, []).append(s)
         drop: set[int] = set()
         n = 0
         for r1 in steps:
-            if r1.kind != "reshape" or uses.get(r1.output) != 1 or self._dtype(r1.inputs[0]) != "fp32":
+            if r1.kind != "reshape" or uses.get(r1.output) != 1:
                 continue
+            dt = self._dtype(r1.inputs[0])
+            if dt not in ("fp32", "bf16"):
+                continue
+            # the image behind the crops (and the cast of a bf16 tenant)
+            src, pre = r1.inputs[0], []
+            while (src in by_out and by_out[src].kind == "slice" and uses.get(src) == 1
+                   and by_out[src].attrs["dim"] % 4 in (2, 3) and by_out[src].attrs["start"] == 0):
+                pre.append(by_out[src])
+                src = by_out[src].inputs[0]
+            if dt == "bf16":
+                c = by_out.get(src)
+                if c is None or c.kind != "cast" or uses.get(src) != 1 or self._dtype(c.inputs[0]) != "fp32":
+                    continue
+                pre.append(c)
+                src = c.inputs[0]
             xs = tuple(self._shape(r1.inputs[0]))
             sh = tuple(r1.attrs["shape"])
             if len(xs) != 4 or len(sh) != 6 or sh[0] != xs[0] or sh[1] != xs[1] or sh[2] * sh[3] != xs[2] \
@@ -938,15 +958,52 @@ class CompiledProgram:
                 continue
             r2 = by_in[pm.output][0]
             N, C, hp, ph, wp, pw = sh
-            if (r2.kind != "reshape" or list(r2.attrs["shape"]) != [N, hp * wp, C * ph * pw] or (C * ph * pw) % 32
-                    or r2.output in self.outputs
+            if (r2.kind != "reshape" or list(r2.attrs["shape"]) != [N, hp * wp, C * ph * pw]
+                    or (dt == "fp32" and (C * ph * pw) % 32) or r2.output in self.outputs
                     or not all(c.kind == "linear" and c.inputs[0] == r2.output for c in by_in.get(r2.output, []))):
                 continue
-            drop.add(id(r1))
-            drop.add(id(pm))
-            r2.kind, r2.inputs, r2.attrs = "patches", [r1.inputs[0]], {"ph": ph, "pw": pw}
+            drop.update(id(x) for x in (r1, pm, *pre))
+            r2.kind, r2.inputs = "patches", [src]
+            r2.attrs = {"ph": ph, "pw": pw, "hp": hp, "wp": wp, "dtype": dt}
             n += 1
         self.stats["patchify_fused"] = n
+        return [s for s in steps if id(s) not in drop]
+
+    def _fuse_cast_unary(self, steps: list[_Step]) -> list[_Step]:
+        """cast -> activation, or activation -> cast (each value read once):
+        one ``unary`` step that evaluates the activation in fp32 and writes
+        the cast's dtype (a bf16 head's fp32 sigmoid boxes: one launch, not
+        two).  Runs after the epilogue fusion, so only activations no GEMM
+        absorbed are left."""
+        from ..ops.tenant import UNARY_CODES
+
+        uses = self._consumers(steps, self.outputs)
+        by_out = {s.output: s for s in steps}
+        drop: set[int] = set()
+        n = 0
+        for s in steps:
+            if id(s) in drop:
+                continue
+            if s.kind in UNARY_CODES:
+                p = by_out.get(s.inputs[0])
+                if (p is None or p.kind != "cast" or id(p) in drop or uses.get(p.output) != 1
+                        or p.output in self.outputs):
+                    continue
+                src, act, dt = p.inputs[0], s.kind, self._dtype(s.output)
+            elif s.kind == "cast":
+                p = by_out.get(s.inputs[0])
+                if (p is None or p.kind not in UNARY_CODES or id(p) in drop or uses.get(p.output) != 1
+                        or p.output in self.outputs):
+                    continue
+                src, act, dt = p.inputs[0], p.kind, s.attrs["dtype"]
+            else:
+                continue
+            if self._dtype(src) not in ("fp32", "bf16") or dt not in ("fp32", "bf16"):
+                continue
+            drop.add(id(p))
+            s.kind, s.inputs, s.attrs = "unary", [src], {"op": act, "dtype": dt}
+            n += 1
+        self.stats["cast_unary_fused"] = n
         return [s for s in steps if id(s) not in drop]
 
     def _fuse_cast_relayout(self, steps: list[_Step]) -> list[_Step]:
@@ -1585,8 +1642,11 @@ class CompiledProgram:
                     y = F.layer_norm(xx, (xx.shape[-1],), a[1], a[2], s.attrs.get("eps", 1e-5))
             elif k == "relayout":
                 y = _relayout(a[0], s.attrs["chain"], s.attrs["dtype"])
+            elif k == "unary":
+                y = T.unary(a[0], s.attrs["op"], torch_dtype(s.attrs["dtype"]))
             elif k == "patches":
-                y = T.patches(a[0], s.attrs["ph"], s.attrs["pw"])
+                at = s.attrs
+                y = T.patches(a[0], at["ph"], at["pw"], torch_dtype(at.get("dtype", "fp32")), at.get("hp"), at.get("wp"))
             elif k == "cat_buffer":  # its GEMM part was written in place; the constant parts at build
                 y = self.aux[s.attrs["buf"]]
             else:

@@ -176,3 +176,48 @@ def test_row_kernels(dt):
     e = T.embedding(ids, table)
     assert torch.equal(e[0], table[[0, 5, 999, 5]]) and torch.equal(e[1, :3], table[[1, 2, 3]])
     assert not e[1, 3].any()
+
+
+@pytest.mark.parametrize("n,hw", [(1, (80, 107)), (2, (64, 96))])
+def test_patches_read_a_cropped_image_in_place(n, hw):
+    """ViT patch rows straight from a non-contiguous crop of an fp32 image:
+    the bf16 rows are bit-identical to torch's cast of the same views, the h3
+    planes reconstruct the fp32 rows exactly (hi + lo carry 22 bits, the
+    inputs are fp16-representable up to the row scale)."""
+    from nos_amd import ops
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    img = torch.randn((n, 3, *hw), device="cuda", generator=g)
+    p = 16
+    hp, wp = hw[0] // p, hw[1] // p
+    want = img[:, :, :hp * p, :wp * p].reshape(n, 3, hp, p, wp, p).permute(0, 2, 4, 1, 3, 5).reshape(n, hp * wp, -1)
+    got = T.patches(img, p, p, torch.bfloat16)
+    assert got.dtype == torch.bfloat16 and got.shape == want.shape
+    assert torch.equal(got, want.to(torch.bfloat16))
+    prev = ops.f32_math()
+    ops.set_f32_math("h3")
+    try:
+        pl = T.patches(img, p, p)
+    finally:
+        ops.set_f32_math(prev)
+    assert isinstance(pl, ops.H3Planes)
+    rows = (pl.planes[0].float() + pl.planes[1].float()) * pl.rinv[:, None]
+    err = (rows.view_as(want) - want).abs().max() / want.abs().max()
+    assert float(err) < 1e-6
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("op", ["relu", "sigmoid", "silu", "gelu", "tanh", "exp", "neg"])
+@pytest.mark.parametrize("dts", [(torch.bfloat16, torch.float32), (torch.float32, torch.bfloat16),
+                                 (torch.float32, torch.float32)])
+def test_cast_unary_matches_fp32_math(op, dts):
+    """One-pass activation with independent input / output dtypes against
+    torch's fp32 evaluation of the same input, rounded once."""
+    src, dst = dts
+    x = (torch.randn(3, 1001, device="cuda", generator=torch.Generator(device="cuda").manual_seed(2)) * 3).to(src)
+    got = T.unary(x, op, dst)
+    ref = T.unary(x.cpu(), op, torch.float32).to(torch.float64)
+    assert got.dtype == dst and got.shape == x.shape
+    tol = 2 ** -7 if dst == torch.bfloat16 else 2e-6
+    err = (got.double().cpu() - ref).abs() / ref.abs().clamp_min(1.0)
+    assert float(err.max()) <= tol

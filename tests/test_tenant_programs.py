@@ -193,3 +193,44 @@ def test_estimate_counts_the_new_ops_workspaces(llama):
             n["op"], n["inputs"], n["attrs"] = "add", n["inputs"][:2], {}
     # same graph with the attention replaced by an elementwise op: the attention workspace is gone
     assert p.bytes_estimate > PG.parse(q, w).bytes_estimate
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_vit_patch_extraction_is_one_step_on_the_uncropped_image(dtype):
+    """YOLOS at an input that is not a whole number of patches: the crop
+    slice, the bf16 cast and the reshape / permute / reshape chain become one
+    ``patches`` step that reads the original fp32 image (the kernel crops via
+    strides and casts as it writes); outputs match the unfused reference."""
+    from nos_amd.models.yolos import YolosConfig
+    from nos_amd.models.yolos_program import yolos_program, yolos_weights
+
+    cfg = YolosConfig.test()
+    p = cfg.patch_size
+    hw = (cfg.image_size[0] + p // 2, cfg.image_size[1] + 3)
+    prog = PG.parse(*yolos_program(cfg, yolos_weights(cfg, 3), hw, dtype))
+    m = prog.compile("cpu")
+    assert m.stats["patchify_fused"] == 1
+    first = [s for s in m.steps if s.kind == "patches"]
+    assert len(first) == 1 and first[0].inputs == [m.input_name]
+    assert first[0].attrs["hp"] == hw[0] // p and first[0].attrs["wp"] == hw[1] // p
+    assert not any(s.kind in ("cast", "relayout") and s.inputs == [m.input_name] for s in m.steps)
+    x = torch.from_numpy(np.random.default_rng(1).standard_normal((1, 3, *hw)).astype(np.float32))
+    tol = dict(rtol=1e-4, atol=1e-5) if dtype == "fp32" else dict(rtol=0.1, atol=0.1)
+    for o, r in zip(m(x), prog.reference(x)):
+        np.testing.assert_allclose(o.float().numpy(), r.float().numpy(), **tol)
+
+
+def test_bf16_heads_cast_and_sigmoid_are_one_step():
+    """The bf16 YOLOS box head's cast to fp32 and sigmoid compile to one
+    ``unary`` step (fp32 math, one rounding) matching the reference."""
+    prog = PG.parse(*demo_tenant("bf16", 2, small=False))
+    m = prog.compile("cpu")
+    assert m.stats["cast_unary_fused"] == 1
+    u = [s for s in m.steps if s.kind == "unary"]
+    assert len(u) == 1 and u[0].attrs == {"op": "sigmoid", "dtype": "fp32"} and u[0].output == "pred_boxes"
+    assert not any(s.kind in ("cast", "sigmoid") for s in m.steps)
+    x = torch.from_numpy(np.random.default_rng(4).standard_normal(prog.inputs[0].shape).astype(np.float32))
+    outs = m(x)
+    assert outs[1].dtype == torch.float32
+    for o, r in zip(outs, prog.reference(x)):
+        np.testing.assert_allclose(o.float().numpy(), r.float().numpy(), rtol=0.1, atol=0.1)
