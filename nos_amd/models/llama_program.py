@@ -64,9 +64,16 @@ def rope_tables(seq: int, head_dim: int, theta: float) -> tuple[np.ndarray, np.n
     return np.cos(emb).astype(np.float32), np.sin(emb).astype(np.float32)
 
 
-def llama_program(model, seq: int, batch: int = 1, dtype: str = "fp32") -> tuple[dict, bytes]:
+def llama_program(model, seq: int, batch: int = 1, dtype: str = "fp32",
+                  rope_len: int | None = None) -> tuple[dict, bytes]:
     """(program, weights) of causal-LM logits [batch, seq, vocab] for token
-    ids [batch, seq] (i32)."""
+    ids [batch, seq] (i32).  ``rope_len`` (>= seq): the rotary tables' rows
+    in the weights, sliced to ``seq`` in the graph (folded at load) -- the
+    programs of several sequence lengths then share one weight payload (the
+    pod server's shape variants)."""
+    rope_len = seq if rope_len is None else rope_len
+    if rope_len < seq:
+        raise ValueError(f"rope_len {rope_len} < seq {seq}")
     cfg = model.config
     sd = {k: v.detach().float().cpu().numpy() for k, v in model.state_dict().items()}
     d, nh = cfg.hidden_size, cfg.num_attention_heads
@@ -76,8 +83,10 @@ def llama_program(model, seq: int, batch: int = 1, dtype: str = "fp32") -> tuple
     b = Builder(f"llama-h{d}-l{cfg.num_hidden_layers}-{dtype}")
     ids = b.input("input_ids", [batch, seq], "i32")
     P = lambda k: b.param(k, sd[k], dtype)  # noqa: E731
-    cos, sin = rope_tables(seq, hd, float(getattr(cfg, "rope_theta", 10000.0)))
+    cos, sin = rope_tables(rope_len, hd, float(getattr(cfg, "rope_theta", 10000.0)))
     rc, rs = b.param("rope.cos", cos, "fp32"), b.param("rope.sin", sin, "fp32")
+    if rope_len > seq:
+        rc, rs = (b.op("slice", t, dim=0, start=0, end=seq) for t in (rc, rs))
     h = b.op("embedding", ids, P("model.embed_tokens.weight"))
     for i in range(cfg.num_hidden_layers):
         p = f"model.layers.{i}."

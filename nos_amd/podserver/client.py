@@ -81,16 +81,21 @@ class PodClient:
         return rep, data
 
     def register(self, pod: str, program: dict, weights: bytes = b"", token: str | None = None,
-                 memory_limit_gb: float | None = None, cu_mask: str | None = None, env: dict | None = None) -> dict:
+                 memory_limit_gb: float | None = None, cu_mask: str | None = None, env: dict | None = None,
+                 variants: list[dict] | None = None) -> dict:
         """Ship the pod's program (op graph + weight bytes, program.py) to the
         server.  The allocation token comes from the device plugin's env; the
         slice itself is the plugin's record.  ``memory_limit_gb`` /
-        ``cu_mask`` matter only to a server without allocation records."""
+        ``cu_mask`` matter only to a server without allocation records.
+        ``variants``: the same model's programs for other input shapes (over
+        the same ``weights``); :meth:`infer` routes by the input's shape."""
         env = os.environ if env is None else env
         if memory_limit_gb is None and env.get(ENV_MEMORY_LIMIT_GB):
             memory_limit_gb = float(env[ENV_MEMORY_LIMIT_GB])
         req = {"op": "register", "pod": pod, "program": program, "token": token or env.get(ENV_POD_TOKEN),
                "memory_limit_gb": memory_limit_gb, "cu_mask": cu_mask or env.get(ENV_POD_CU_MASK)}
+        if variants:
+            req["variants"] = list(variants)
         rep, _ = self._call(req, weights)
         self._reg = (req, weights)
         self.tenant = rep["tenant"]
@@ -118,20 +123,24 @@ class PodClient:
 
     def infer(self, x: np.ndarray | None = None, outputs: bool = False) -> tuple[list[np.ndarray], dict]:
         """One inference on the pod's model; ``x`` replaces the resident input
-        (float32, the model's input shape)."""
+        (float32, one of the registered input shapes; without ``x`` the
+        primary shape's resident input runs)."""
+        req = {"op": "infer", "outputs": outputs}
         if x is None:
             payload = b""
         elif np.issubdtype(np.asarray(x).dtype, np.integer):  # token ids of an i32 input
             payload = np.ascontiguousarray(x, dtype=np.int32).tobytes()
         else:
             payload = np.ascontiguousarray(x, dtype=np.float32).tobytes()
+        if x is not None:
+            req["shape"] = [int(d) for d in np.shape(x)]
         try:
-            rep, data = self._call({"op": "infer", "outputs": outputs}, payload)
+            rep, data = self._call(req, payload)
         except PodServerGone:
             if self.reconnect_s <= 0 or self._reg is None:
                 raise
             self._reregister()
-            rep, data = self._call({"op": "infer", "outputs": outputs}, payload)
+            rep, data = self._call(req, payload)
         return (P.unpack_arrays(rep["outputs"], data) if outputs else []), rep
 
     def stats(self) -> dict:

@@ -65,6 +65,7 @@ MAX_NODES = 8192
 MAX_PARAMS = 8192
 MAX_NUMEL = 1 << 31          # elements of one value
 MAX_RANK = 8
+MAX_VARIANTS = 8             # input shapes one tenant may register (parse_variants)
 UNARY = ("gelu", "relu", "sigmoid", "silu", "tanh", "exp", "neg", "rsqrt")
 BINARY = ("add", "mul", "sub", "div")
 ACTS = (None, "gelu", "relu")
@@ -605,6 +606,28 @@ def torch_dtype(dt: str):
     import torch
 
     return {"fp32": torch.float32, "bf16": torch.bfloat16, "i32": torch.int32}[dt]
+
+
+def parse_variants(objs: list, payload: bytes | memoryview = b"", gpu: bool = False) -> list[Program]:
+    """A tenant's programs for several input shapes (sequence-length or image
+    size buckets) over ONE weight payload: each is parsed like :func:`parse`;
+    all must declare the same weights (names, shapes, dtypes, payload spans)
+    and input dtype, and their input shapes must differ.  The server builds
+    one graph per shape on shared weight tensors and routes each request by
+    its input shape."""
+    _req(isinstance(objs, list) and 1 <= len(objs) <= MAX_VARIANTS,
+         f"a tenant registers 1 to {MAX_VARIANTS} program variants")
+    progs = [parse(o, payload, gpu=gpu) for o in objs]
+    p0 = progs[0]
+    seen = set()
+    for p in progs:
+        sig = {k: (v.shape, v.dtype) for k, v in p.params.items()}
+        _req(sig == {k: (v.shape, v.dtype) for k, v in p0.params.items()} and p.param_layout == p0.param_layout,
+             f"variant {p.name!r} declares other weights than {p0.name!r}: variants share one weight payload")
+        _req(p.inputs[0].dtype == p0.inputs[0].dtype, "variants take the same input dtype")
+        _req(p.inputs[0].shape not in seen, f"two variants take the input shape {list(p.inputs[0].shape)}")
+        seen.add(p.inputs[0].shape)
+    return progs
 
 
 def parse(obj: dict, payload: bytes | memoryview = b"", gpu: bool = False) -> Program:

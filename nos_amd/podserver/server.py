@@ -108,6 +108,19 @@ class Tenant:
     compile_stats: dict = field(default_factory=dict)
     evicted: str | None = None
     id_bound: int | None = None    # token-id input: ids must lie in [0, id_bound)
+    alts: dict = field(default_factory=dict)   # other input shapes -> _Variant (same weights)
+
+
+@dataclass
+class _Variant:
+    """One more input shape of a tenant (program.parse_variants): its own
+    compiled program, static input and graphs over the tenant's weights."""
+    model: object
+    x: object
+    graph: object = None
+    outputs: tuple = ()
+    solo_graph: object = None
+    solo_outputs: tuple = ()
 
 
 @dataclass
@@ -115,6 +128,7 @@ class _Job:
     tenant: Tenant
     payload: bytes
     want_outputs: bool
+    shape: tuple | None = None
     done: threading.Event = field(default_factory=threading.Event)
     t_enq: float = field(default_factory=time.monotonic)
     t_start: float = 0.0
@@ -340,13 +354,17 @@ class PodServer:
                         tenant = self._register(req, payload, conn, claim)
                         P.send_msg(conn, {"ok": True, "tenant": tenant.id, "footprint_gb": tenant.footprint_gb,
                                           "memory_limit_gb": tenant.memory_limit_gb, "cu_mask": tenant.cu_mask,
-                                          "input_shape": list(tenant.x.shape), "server": self.info,
+                                          "input_shape": list(tenant.x.shape),
+                                          "input_shapes": [list(tenant.x.shape)] + [list(k) for k in tenant.alts],
+                                          "server": self.info,
                                           "program": tenant.program, "compile": tenant.compile_stats,
                                           "tenants": len(self.tenants)})
                     elif op == "infer":
                         if tenant is None:
                             raise AdmissionError("register first")
-                        job = _Job(tenant, payload, bool(req.get("outputs")))
+                        shp = req.get("shape")
+                        shp = tuple(int(d) for d in shp) if isinstance(shp, list) and len(shp) <= 8 else None
+                        job = _Job(tenant, payload, bool(req.get("outputs")), shp)
                         self._q.put(job)
                         job.done.wait()
                         if job.error:
@@ -461,13 +479,18 @@ class PodServer:
         try:
             if "program" not in req:
                 raise AdmissionError("register carries no program (nos-amd.program/v1 op graph + weights)")
-            prog = PG.parse(req["program"], payload, gpu=self.gpu)
+            extra = req.get("variants") or []
+            if not isinstance(extra, list):
+                raise AdmissionError("variants must be a list of programs")
+            progs = PG.parse_variants([req["program"], *extra], payload, gpu=self.gpu)
             limit, mask, tid = claim["limit"], claim["mask"], claim["tid"]
-            need = prog.bytes_estimate_for(self.kernel_config) / 2 ** 30
+            # the weights once, every variant's activations, planes and folded copies
+            need = sum(p.bytes_estimate_for(self.kernel_config) for p in progs) / 2 ** 30
+            need -= (len(progs) - 1) * progs[0].param_bytes / 2 ** 30
             if limit and need > limit:
                 raise AdmissionError(f"tenant needs {need:.2f} GB (static estimate), its slice has {limit} GB")
             with self._build_lock:
-                t = self._build(tid, req, prog, limit, mask)
+                t = self._build(tid, req, progs, limit, mask)
         except BaseException:
             self._release_claim(claim)
             raise
@@ -480,19 +503,25 @@ class PodServer:
                  limit or "-")
         return t
 
-    def _build(self, tid: int, req: dict, prog, limit: float, mask: str | None) -> Tenant:
+    def _build(self, tid: int, req: dict, progs, limit: float, mask: str | None) -> Tenant:
+        """Compile and capture a tenant: one program per input shape
+        (``progs[0]`` the primary; or one Program), all over one set of
+        weight tensors."""
         import torch
 
         from ..models.yolos import GraphedTenant
 
+        progs = progs if isinstance(progs, list) else [progs]
         pod = str(req.get("pod", tid))[:253]
+        prog = progs[0]
         dtype = prog.inputs[0].dtype
         if not self.gpu:
             with torch.no_grad():
-                m = prog.compile("cpu")
-            x = prog.input_tensor("cpu")
+                params = prog.tensors("cpu")
+                built = [(p.compile("cpu", params=params), p.input_tensor("cpu")) for p in progs]
+            m, x = built[0]
             return Tenant(tid, pod, limit, dtype, m, x, program=prog.name, compile_stats=dict(m.stats), cu_mask=mask,
-                          id_bound=prog.id_bound())
+                          id_bound=prog.id_bound(), alts={tuple(xv.shape): _Variant(mv, xv) for mv, xv in built[1:]})
         base = torch.cuda.memory_allocated()
         torch.cuda.reset_peak_memory_stats()
         stream = None
@@ -500,8 +529,9 @@ class PodServer:
         times = {}
         try:
             with torch.no_grad(), torch.cuda.stream(self._setup_stream):
-                m = prog.compile("cuda")
-                x = prog.input_tensor("cuda")
+                params = prog.tensors("cuda")
+                built = [(p.compile("cuda", params=params), p.input_tensor("cuda")) for p in progs]
+                del params   # each compiled program holds the weights it reads
             self._setup_stream.synchronize()
             times["compile_ms"] = round(1e3 * (time.monotonic() - t0), 1)
             budget_cfg = None
@@ -516,34 +546,7 @@ class PodServer:
                 # grids and the budget-aware configs a masked process pod uses
                 frac = limit / self.memory_gb if limit and self.memory_gb else 0.5
                 budget_cfg = (kernel_config(frac, os.environ, len(cus)), len(cus))
-            gt = GraphedTenant(m, stream.torch if stream else self._setup_stream, x)
-            with torch.no_grad():
-                try:
-                    if budget_cfg is not None:
-                        from ..ops import set_cu_budget
-
-                        self._apply_config(budget_cfg[0])
-                        set_cu_budget(budget_cfg[1])
-                    if self.graphs:  # the lanes keep replaying other tenants meanwhile
-                        gt.capture(warmup=1, capture_error_mode="thread_local", light=True)
-                    else:
-                        gt.launch()
-                        gt.stream.synchronize()
-                finally:
-                    if budget_cfg is not None:
-                        set_cu_budget(0)
-                        self._apply_config(self.kernel_config)
-                solo = None
-                if self.solo_config is not None and not mask:
-                    # the lanes only replay graphs, so switching the process-wide
-                    # configs for this capture changes no other tenant's kernels
-                    solo = GraphedTenant(m, self._setup_stream, x)
-                    try:
-                        self._apply_config(self.solo_config)
-                        # one warm-up: the first capture's already ran every kernel
-                        solo.capture(warmup=1, capture_error_mode="thread_local", pool=gt.graph.pool(), light=True)
-                    finally:
-                        self._apply_config(self.kernel_config)
+            variants = [self._capture(m, x, stream, budget_cfg, mask, GraphedTenant) for m, x in built]
             peak = (torch.cuda.max_memory_allocated() - base) / 2 ** 30
             times["build_ms"] = round(1e3 * (time.monotonic() - t0), 1)
         except Exception:
@@ -551,14 +554,52 @@ class PodServer:
                 stream.close()
             torch.cuda.empty_cache()
             raise
-        t = Tenant(tid, pod, limit, dtype, m, x, stream=stream, graph=gt.graph,
-                   outputs=gt.outputs, footprint_gb=round(peak, 3), cu_mask=mask,
-                   solo_graph=solo.graph if solo else None, solo_outputs=solo.outputs if solo else (),
-                   program=prog.name, compile_stats={**m.stats, **times}, id_bound=prog.id_bound())
+        v0 = variants[0]
+        t = Tenant(tid, pod, limit, dtype, v0.model, v0.x, stream=stream, graph=v0.graph,
+                   outputs=v0.outputs, footprint_gb=round(peak, 3), cu_mask=mask,
+                   solo_graph=v0.solo_graph, solo_outputs=v0.solo_outputs,
+                   program=prog.name, compile_stats={**v0.model.stats, **times}, id_bound=prog.id_bound(),
+                   alts={tuple(v.x.shape): v for v in variants[1:]})
         if limit and peak > limit:
             self._free(t)
             raise AdmissionError(f"tenant needs {peak:.2f} GB, its slice has {limit} GB")
         return t
+
+    def _capture(self, m, x, stream, budget_cfg, mask, GraphedTenant) -> _Variant:
+        """The graphs of one compiled program: under the slice's configs on
+        its CU-masked stream, plus (unmasked) the whole-GPU solo graph in the
+        same memory pool."""
+        import torch
+
+        gt = GraphedTenant(m, stream.torch if stream else self._setup_stream, x)
+        with torch.no_grad():
+            try:
+                if budget_cfg is not None:
+                    from ..ops import set_cu_budget
+
+                    self._apply_config(budget_cfg[0])
+                    set_cu_budget(budget_cfg[1])
+                if self.graphs:  # the lanes keep replaying other tenants meanwhile
+                    gt.capture(warmup=1, capture_error_mode="thread_local", light=True)
+                else:
+                    gt.launch()
+                    gt.stream.synchronize()
+            finally:
+                if budget_cfg is not None:
+                    set_cu_budget(0)
+                    self._apply_config(self.kernel_config)
+            solo = None
+            if self.solo_config is not None and not mask and self.graphs:
+                # the lanes only replay graphs, so switching the process-wide
+                # configs for this capture changes no other tenant's kernels
+                solo = GraphedTenant(m, self._setup_stream, x)
+                try:
+                    self._apply_config(self.solo_config)
+                    # one warm-up: the first capture's already ran every kernel
+                    solo.capture(warmup=1, capture_error_mode="thread_local", pool=gt.graph.pool(), light=True)
+                finally:
+                    self._apply_config(self.kernel_config)
+        return _Variant(m, x, gt.graph, gt.outputs, solo.graph if solo else None, solo.outputs if solo else ())
 
     # ------------------------------------------------------------ eviction
     def evict(self, t: Tenant, reason: str) -> None:
@@ -608,6 +649,7 @@ class PodServer:
     def _free(self, t: Tenant) -> None:
         t.graph = t.solo_graph = t.model = t.x = None
         t.outputs = t.solo_outputs = ()
+        t.alts = {}
         if t.stream is not None:
             t.stream.close()
             t.stream = None
@@ -673,33 +715,46 @@ class PodServer:
         import torch
 
         t = job.tenant
+        # the primary shape, or the variant the request's input shape names
+        # (an input of another shape but exactly one variant's size -- a
+        # flattened array -- goes to that variant)
+        v = t
+        if t.alts and job.shape is not None and job.shape != tuple(t.x.shape):
+            v = t.alts.get(job.shape)
+            if v is None:
+                n = len(job.payload) // 4
+                fit = [w for w in (t, *t.alts.values()) if w.x.numel() == n]
+                if len(fit) != 1:
+                    raise ValueError(f"no program variant takes the input shape {list(job.shape)} "
+                                     f"(registered: {[list(t.x.shape)] + [list(k) for k in t.alts]})")
+                v = fit[0]
         x_in = None
         if job.payload:
-            ids = str(t.x.dtype) == "torch.int32"
+            ids = str(v.x.dtype) == "torch.int32"
             x_in = np.frombuffer(job.payload, dtype=np.int32 if ids else np.float32)
-            if x_in.size != t.x.numel():
-                raise ValueError(f"input has {x_in.size} values, the tenant's model takes {t.x.numel()}")
+            if x_in.size != v.x.numel():
+                raise ValueError(f"input has {x_in.size} values, the tenant's model takes {v.x.numel()}")
             if ids and t.id_bound is not None and x_in.size and (x_in.min() < 0 or x_in.max() >= t.id_bound):
                 raise ValueError(f"token ids must lie in [0, {t.id_bound})")
         with torch.no_grad():
             if not self.gpu:
                 if x_in is not None:
-                    t.x.copy_(torch.from_numpy(x_in.copy()).view(t.x.shape))
-                t.outputs = outs = t.model(t.x)
+                    v.x.copy_(torch.from_numpy(x_in.copy()).view(v.x.shape))
+                v.outputs = outs = v.model(v.x)
             else:
                 s = t.stream.torch if t.stream is not None else lane
                 with torch.cuda.stream(s):
                     if x_in is not None:
-                        t.x.copy_(torch.from_numpy(x_in.copy()).view(t.x.shape).to(t.x.dtype), non_blocking=False)
-                    outs = t.outputs
-                    if alone and t.solo_graph is not None:
-                        t.solo_graph.replay()
-                        outs = t.solo_outputs
+                        v.x.copy_(torch.from_numpy(x_in.copy()).view(v.x.shape).to(v.x.dtype), non_blocking=False)
+                    outs = v.outputs
+                    if alone and v.solo_graph is not None:
+                        v.solo_graph.replay()
+                        outs = v.solo_outputs
                         t.solo_completed += 1
-                    elif t.graph is not None:
-                        t.graph.replay()
+                    elif v.graph is not None:
+                        v.graph.replay()
                     else:
-                        t.outputs = outs = t.model(t.x)
+                        v.outputs = outs = v.model(v.x)
                 s.synchronize()
             if job.want_outputs:
                 job.outputs = [o.detach().float().cpu().numpy() for o in outs]

@@ -234,3 +234,67 @@ def test_bf16_heads_cast_and_sigmoid_are_one_step():
     assert outs[1].dtype == torch.float32
     for o, r in zip(outs, prog.reference(x)):
         np.testing.assert_allclose(o.float().numpy(), r.float().numpy(), rtol=0.1, atol=0.1)
+
+
+def test_a_tenant_serves_several_input_shapes_over_one_weight_payload(tmp_path, llama):
+    """Shape buckets: a decoder at sequence lengths 64 / 32 / 16 and a ViT at
+    two image sizes register once each (one weight payload, one graph per
+    shape); every request runs the variant its input shape names and matches
+    the module at that shape; unknown shapes fail that request only."""
+    from nos_amd.models.yolos import YolosConfig
+    from nos_amd.models.yolos_program import yolos_program, yolos_weights
+
+    m, (p64, w) = llama
+    variants = [llama_program(m, s, rope_len=64) for s in (32, 16)]
+    assert all(vw == w for _, vw in variants)
+    cfg = YolosConfig.test()
+    yw = yolos_weights(cfg, 5)
+    y0, yp = yolos_program(cfg, yw, cfg.image_size)
+    hw1 = (cfg.image_size[0] + 32, cfg.image_size[1] - 16)
+    y1, yp1 = yolos_program(cfg, yw, hw1)
+    assert yp1 == yp
+    srv = PodServer(tmp_path / "s.sock", device="cpu", lanes=2, memory_gb=40).start()
+    try:
+        lc = PodClient(srv.path, connect_timeout_s=5)
+        rep = lc.register("llm", p64, w, memory_limit_gb=4, variants=[p for p, _ in variants])
+        assert rep["input_shapes"] == [[1, 64], [1, 32], [1, 16]]
+        for s in (16, 64, 32):
+            ids = np.random.default_rng(s).integers(0, m.config.vocab_size, (1, s)).astype(np.int32)
+            out, _ = lc.infer(ids, outputs=True)
+            with torch.no_grad():
+                ref = m(torch.from_numpy(ids).long()).logits.numpy()
+            assert out[0].shape == ref.shape
+            np.testing.assert_allclose(out[0], ref, atol=2e-5, rtol=1e-5)
+        with pytest.raises(PodServerError, match="no program variant takes the input shape"):
+            lc.infer(np.zeros((1, 48), np.int32))
+        yc = PodClient(srv.path, connect_timeout_s=5)
+        rep = yc.register("vit", y0, yp, memory_limit_gb=2, variants=[y1])
+        assert rep["input_shapes"] == [[1, 3, *cfg.image_size], [1, 3, *hw1]]
+        for shape, prog in (((1, 3, *hw1), y1), ((1, 3, *cfg.image_size), y0)):
+            x = np.random.default_rng(7).standard_normal(shape).astype(np.float32)
+            outs, _ = yc.infer(x, outputs=True)
+            ref = PG.parse(prog, yp).reference(torch.from_numpy(x))
+            for o, r in zip(outs, ref):
+                np.testing.assert_allclose(o, r.numpy(), rtol=1e-4, atol=1e-5)
+        lc.infer()   # no input: the primary shape's resident input
+        lc.close()
+        yc.close()
+    finally:
+        srv.stop()
+
+
+def test_variants_must_share_their_weights():
+    from nos_amd.models.yolos import YolosConfig
+    from nos_amd.models.yolos_program import yolos_program, yolos_weights
+
+    cfg = YolosConfig.test()
+    y0, yp = yolos_program(cfg, yolos_weights(cfg, 5), cfg.image_size)
+    with pytest.raises(PG.ProgramError, match="two variants take the input shape"):
+        PG.parse_variants([y0, y0], yp)
+    other = copy.deepcopy(y0)
+    other["inputs"][0]["shape"] = [1, 3, 64, 64]
+    other["params"][0]["shape"] = [1] + other["params"][0]["shape"][1:]
+    with pytest.raises(PG.ProgramError):
+        PG.parse_variants([y0, other], yp)
+    with pytest.raises(PG.ProgramError, match="1 to 8 program variants"):
+        PG.parse_variants([y0] * 9, yp)

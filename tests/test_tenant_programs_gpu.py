@@ -140,3 +140,37 @@ def test_grouped_conv_program_on_gpu_matches_fp64():
         ref64 = mc.double()(xc.double())
     e, e32 = _err(got, ref64), _err(f32, ref64)
     assert e <= max(4 * e32, 1e-5), (e, e32)
+
+
+def test_gpu_tenant_shape_variants_share_weights(tmp_path):
+    """A decoder registered at sequence lengths 64 / 32 / 16 over one weight
+    payload on the GPU server: one captured graph per shape, each request
+    replays the graph of its input's shape and matches the module; the build
+    footprint stays inside the variants' combined static estimate and well
+    below three separate tenants' weights."""
+    from nos_amd.podserver.client import PodClient
+    from nos_amd.podserver.server import PodServer
+
+    lm = llama_model(llama_config(False), 0)
+    progs = [llama_program(lm, s, rope_len=64) for s in (64, 32, 16)]
+    w = progs[0][1]
+    srv = PodServer(tmp_path / "s.sock", device="cuda", lanes=4, memory_gb=64).start()
+    try:
+        c = PodClient(srv.path, connect_timeout_s=30)
+        rep = c.register("llm", progs[0][0], w, memory_limit_gb=4, variants=[p for p, _ in progs[1:]])
+        assert rep["input_shapes"] == [[1, 64], [1, 32], [1, 16]]
+        parsed = PG.parse_variants([p for p, _ in progs], w, gpu=True)
+        est = (sum(p.bytes_estimate_for(srv.kernel_config) for p in parsed) - 2 * parsed[0].param_bytes) / 2 ** 30
+        assert rep["footprint_gb"] <= est + 0.016, (rep["footprint_gb"], est)
+        t = next(iter(srv.tenants.values()))
+        assert all(v.graph is not None for v in t.alts.values()) and t.graph is not None
+        for s in (16, 64, 32, 16):
+            ids = np.random.default_rng(s).integers(0, lm.config.vocab_size, (1, s)).astype(np.int32)
+            out, _ = c.infer(ids, outputs=True)
+            with torch.no_grad():
+                ref = lm(torch.from_numpy(ids).long()).logits.numpy()
+            assert out[0].shape == ref.shape
+            assert np.abs(out[0] - ref).max() <= 1e-4 * np.abs(ref).max()
+        c.close()
+    finally:
+        srv.stop()
