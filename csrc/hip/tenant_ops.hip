@@ -268,8 +268,14 @@ NOS_API int nos_im2col(const float* x, long long sN, long long sC, long long sH,
 #define NOS_IM2COL(kh, kw, bf)                                                                                        \
   hipLaunchKernelGGL((im2col_h3_kernel<kh, kw, bf>), grid, blk, 0, stream, x, P, pplane, rinv, N, C, H, W, sN, sC, sH, \
                      OH, OW, KH, KW, sh, sw, ph, pw, dh, dw, (int)K, Kp)
-  if (bf16)
+  // ViT patch embeddings (16x16, stride 16) and the common conv kernels get
+  // compile-time sizes: the per-element (c, i, j) split is then multiplies
+  if (bf16 && KH == 16 && KW == 16)
+    NOS_IM2COL(16, 16, true);
+  else if (bf16)
     NOS_IM2COL(0, 0, true);
+  else if (KH == 16 && KW == 16)
+    NOS_IM2COL(16, 16, false);
   else if (KH == 1 && KW == 1)
     NOS_IM2COL(1, 1, false);
   else if (KH == 3 && KW == 3)

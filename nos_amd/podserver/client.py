@@ -82,13 +82,15 @@ class PodClient:
 
     def register(self, pod: str, program: dict, weights: bytes = b"", token: str | None = None,
                  memory_limit_gb: float | None = None, cu_mask: str | None = None, env: dict | None = None,
-                 variants: list[dict] | None = None) -> dict:
+                 variants: list[dict] | None = None, train: dict | None = None) -> dict:
         """Ship the pod's program (op graph + weight bytes, program.py) to the
         server.  The allocation token comes from the device plugin's env; the
         slice itself is the plugin's record.  ``memory_limit_gb`` /
         ``cu_mask`` matter only to a server without allocation records.
         ``variants``: the same model's programs for other input shapes (over
-        the same ``weights``); :meth:`infer` routes by the input's shape."""
+        the same ``weights``); :meth:`infer` routes by the input's shape.
+        ``train``: register a training tenant (podserver/training.py: loss,
+        optimizer, lr, ...) driven by :meth:`train_step`."""
         env = os.environ if env is None else env
         if memory_limit_gb is None and env.get(ENV_MEMORY_LIMIT_GB):
             memory_limit_gb = float(env[ENV_MEMORY_LIMIT_GB])
@@ -96,6 +98,8 @@ class PodClient:
                "memory_limit_gb": memory_limit_gb, "cu_mask": cu_mask or env.get(ENV_POD_CU_MASK)}
         if variants:
             req["variants"] = list(variants)
+        if train is not None:
+            req["train"] = dict(train)
         rep, _ = self._call(req, weights)
         self._reg = (req, weights)
         self.tenant = rep["tenant"]
@@ -142,6 +146,22 @@ class PodClient:
             self._reregister()
             rep, data = self._call(req, payload)
         return (P.unpack_arrays(rep["outputs"], data) if outputs else []), rep
+
+    def train_step(self, x: np.ndarray, target: np.ndarray) -> dict:
+        """One optimisation step of a training tenant on (x, target): the
+        target has the trained output's shape (mse, float) or its shape
+        without the class dim (cross_entropy, int class ids).  Returns the
+        reply: ``loss`` (before the step's update), ``step``, timings."""
+        xa = np.ascontiguousarray(x, dtype=np.int32 if np.issubdtype(np.asarray(x).dtype, np.integer) else np.float32)
+        ta = np.asarray(target)
+        ta = np.ascontiguousarray(ta, dtype=np.int32 if np.issubdtype(ta.dtype, np.integer) else np.float32)
+        xb = xa.tobytes()
+        return self._call({"op": "train", "x_bytes": len(xb)}, xb + ta.tobytes())[0]
+
+    def weights(self) -> bytes:
+        """A training tenant's current weights in its program's payload
+        layout: ``register(program, weights=...)`` resumes from them."""
+        return self._call({"op": "weights"})[1]
 
     def stats(self) -> dict:
         return self._call({"op": "stats"})[0]

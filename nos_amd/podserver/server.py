@@ -61,6 +61,7 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 import queue
@@ -109,6 +110,7 @@ class Tenant:
     evicted: str | None = None
     id_bound: int | None = None    # token-id input: ids must lie in [0, id_bound)
     alts: dict = field(default_factory=dict)   # other input shapes -> _Variant (same weights)
+    trainer: object = None         # a training tenant (training.Trainer): steps instead of inferences
 
 
 @dataclass
@@ -129,6 +131,9 @@ class _Job:
     payload: bytes
     want_outputs: bool
     shape: tuple | None = None
+    kind: str = "infer"            # or "train": one optimisation step, payload = input + target
+    x_bytes: int = 0
+    loss: float | None = None
     done: threading.Event = field(default_factory=threading.Event)
     t_enq: float = field(default_factory=time.monotonic)
     t_start: float = 0.0
@@ -373,6 +378,24 @@ class PodServer:
                         P.send_msg(conn, {"ok": True, "queue_us": round(1e6 * (job.t_start - job.t_enq), 1),
                                           "gpu_us": round(1e6 * (job.t_end - job.t_start), 1), "outputs": descs},
                                    out)
+                    elif op == "train":
+                        if tenant is None or tenant.trainer is None:
+                            raise AdmissionError("train needs a training tenant (register with a train spec)")
+                        xb = req.get("x_bytes")
+                        if not isinstance(xb, int) or not 0 <= xb <= len(payload):
+                            raise ValueError("train: x_bytes must split the payload into input + target")
+                        job = _Job(tenant, payload, False, kind="train", x_bytes=xb)
+                        self._q.put(job)
+                        job.done.wait()
+                        if job.error:
+                            raise RuntimeError(job.error)
+                        P.send_msg(conn, {"ok": True, "loss": job.loss, "step": tenant.trainer.steps,
+                                          "queue_us": round(1e6 * (job.t_start - job.t_enq), 1),
+                                          "gpu_us": round(1e6 * (job.t_end - job.t_start), 1)})
+                    elif op == "weights":
+                        if tenant is None or tenant.trainer is None:
+                            raise AdmissionError("weights: only a training tenant's weights change")
+                        P.send_msg(conn, {"ok": True, "step": tenant.trainer.steps}, tenant.trainer.weights_bytes())
                     elif op == "stats":
                         P.send_msg(conn, {"ok": True, **self.stats()})
                     elif op == "close":
@@ -482,15 +505,31 @@ class PodServer:
             extra = req.get("variants") or []
             if not isinstance(extra, list):
                 raise AdmissionError("variants must be a list of programs")
-            progs = PG.parse_variants([req["program"], *extra], payload, gpu=self.gpu)
             limit, mask, tid = claim["limit"], claim["mask"], claim["tid"]
-            # the weights once, every variant's activations, planes and folded copies
-            need = sum(p.bytes_estimate_for(self.kernel_config) for p in progs) / 2 ** 30
-            need -= (len(progs) - 1) * progs[0].param_bytes / 2 ** 30
-            if limit and need > limit:
-                raise AdmissionError(f"tenant needs {need:.2f} GB (static estimate), its slice has {limit} GB")
-            with self._build_lock:
-                t = self._build(tid, req, progs, limit, mask)
+            if req.get("train") is not None:
+                from .training import parse_train_spec, train_bytes_estimate
+
+                if extra:
+                    raise AdmissionError("a training tenant takes one input shape (no variants)")
+                prog = PG.parse(req["program"], payload)
+                spec = parse_train_spec(req["train"], prog)
+                need = train_bytes_estimate(prog, spec) / 2 ** 30
+                if limit and need > limit:
+                    raise AdmissionError(f"training tenant needs {need:.2f} GB (static estimate), "
+                                         f"its slice has {limit} GB")
+                with self._build_lock:
+                    t = self._build_trainer(tid, req, prog, spec, limit, mask)
+                progs = None
+            else:
+                progs = PG.parse_variants([req["program"], *extra], payload, gpu=self.gpu)
+            if progs is not None:
+                # the weights once, every variant's activations, planes and folded copies
+                need = sum(p.bytes_estimate_for(self.kernel_config) for p in progs) / 2 ** 30
+                need -= (len(progs) - 1) * progs[0].param_bytes / 2 ** 30
+                if limit and need > limit:
+                    raise AdmissionError(f"tenant needs {need:.2f} GB (static estimate), its slice has {limit} GB")
+                with self._build_lock:
+                    t = self._build(tid, req, progs, limit, mask)
         except BaseException:
             self._release_claim(claim)
             raise
@@ -563,6 +602,51 @@ class PodServer:
         if limit and peak > limit:
             self._free(t)
             raise AdmissionError(f"tenant needs {peak:.2f} GB, its slice has {limit} GB")
+        return t
+
+    def _build_trainer(self, tid: int, req: dict, prog, spec: dict, limit: float, mask: str | None) -> Tenant:
+        """A training tenant (training.py): fp32 master weights, optimizer
+        state and, on the GPU, forward + backward + step captured into one
+        graph on the tenant's (CU-masked) stream."""
+        import torch
+
+        from .training import Trainer
+
+        pod = str(req.get("pod", tid))[:253]
+        if not self.gpu:
+            tr = Trainer(prog, spec, "cpu")
+            return Tenant(tid, pod, limit, "fp32", tr.module, tr.x, program=prog.name, cu_mask=mask, trainer=tr,
+                          compile_stats={"train": spec["optimizer"], "loss": spec["loss"]},
+                          id_bound=prog.id_bound())
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        stream = None
+        t0 = time.monotonic()
+        try:
+            if mask:
+                from ..bench_support import cus_from_hex
+                from ..ops.streams import CUMaskedStream
+
+                stream = CUMaskedStream(cus_from_hex(mask), self.info["multiprocessor_count"])
+            cap = stream.torch if stream else self._setup_stream
+            with torch.cuda.stream(cap):
+                tr = Trainer(prog, spec, "cuda")
+            cap.synchronize()
+            if self.graphs:
+                tr.capture(cap)
+            peak = (torch.cuda.max_memory_allocated() - base) / 2 ** 30
+        except Exception:
+            if stream is not None:
+                stream.close()
+            torch.cuda.empty_cache()
+            raise
+        t = Tenant(tid, pod, limit, "fp32", tr.module, tr.x, stream=stream, footprint_gb=round(peak, 3),
+                   cu_mask=mask, program=prog.name, trainer=tr, id_bound=prog.id_bound(),
+                   compile_stats={"train": spec["optimizer"], "loss": spec["loss"], "graph": tr.graph is not None,
+                                  "build_ms": round(1e3 * (time.monotonic() - t0), 1)})
+        if limit and peak > limit:
+            self._free(t)
+            raise AdmissionError(f"training tenant needs {peak:.2f} GB, its slice has {limit} GB")
         return t
 
     def _capture(self, m, x, stream, budget_cfg, mask, GraphedTenant) -> _Variant:
@@ -650,6 +734,7 @@ class PodServer:
         t.graph = t.solo_graph = t.model = t.x = None
         t.outputs = t.solo_outputs = ()
         t.alts = {}
+        t.trainer = None
         if t.stream is not None:
             t.stream.close()
             t.stream = None
@@ -676,7 +761,9 @@ class PodServer:
         with self._lock:
             ts = [{"tenant": t.id, "pod": t.pod, "program": t.program, "completed": t.completed,
                    "solo_completed": t.solo_completed, "gpu_s": round(t.gpu_s, 4),
-                   "footprint_gb": t.footprint_gb, "memory_limit_gb": t.memory_limit_gb, "cu_mask": t.cu_mask}
+                   "footprint_gb": t.footprint_gb, "memory_limit_gb": t.memory_limit_gb, "cu_mask": t.cu_mask,
+                   "kind": "train" if t.trainer is not None else "infer",
+                   "train_steps": t.trainer.steps if t.trainer is not None else 0}
                   for t in self.tenants.values()]
             pending = len(self._pending)
         return {"tenants": ts, "pending": pending, "server": self.info, "queued": self._q.qsize(), "pid": os.getpid(),
@@ -715,6 +802,8 @@ class PodServer:
         import torch
 
         t = job.tenant
+        if t.trainer is not None:
+            return self._run_trainer(job, lane)
         # the primary shape, or the variant the request's input shape names
         # (an input of another shape but exactly one variant's size -- a
         # flattened array -- goes to that variant)
@@ -758,6 +847,48 @@ class PodServer:
                 s.synchronize()
             if job.want_outputs:
                 job.outputs = [o.detach().float().cpu().numpy() for o in outs]
+
+
+    def _run_trainer(self, job: _Job, lane) -> None:
+        """A training tenant's request: one optimisation step (payload =
+        input + target) or a forward pass with the current weights."""
+        import torch
+
+        tr = job.tenant.trainer
+        ids = str(tr.x.dtype) == "torch.int32"
+        nb = job.x_bytes if job.kind == "train" else len(job.payload)
+        x = None
+        if nb:
+            x = np.frombuffer(job.payload[:nb], dtype=np.int32 if ids else np.float32)
+            if x.size != tr.x.numel():
+                raise ValueError(f"input has {x.size} values, the tenant's model takes {tr.x.numel()}")
+            t = job.tenant
+            if ids and t.id_bound is not None and x.size and (x.min() < 0 or x.max() >= t.id_bound):
+                raise ValueError(f"token ids must lie in [0, {t.id_bound})")
+            x = torch.from_numpy(x.copy())
+        y = None
+        if job.kind == "train":
+            ci = tr.spec["target_dtype"] == "i32"
+            y = np.frombuffer(job.payload[nb:], dtype=np.int32 if ci else np.float32)
+            if y.size != tr.y.numel():
+                raise ValueError(f"target has {y.size} values, the trained output takes {tr.y.numel()}")
+            if ci and y.size and (y.min() < 0 or y.max() >= tr.prog.values[tr.prog.outputs[tr.spec["output"]]].shape[-1]):
+                raise ValueError("class ids must index the logits")
+            y = torch.from_numpy(y.copy())
+        s = job.tenant.stream.torch if (self.gpu and job.tenant.stream is not None) else lane
+        ctx = torch.cuda.stream(s) if self.gpu else contextlib.nullcontext()
+        with ctx:
+            if job.kind == "train":
+                loss = tr.step(x, y)
+                if self.gpu:
+                    s.synchronize()
+                job.loss = float(loss.detach())
+            else:
+                outs = tr.forward(x)
+                if self.gpu:
+                    s.synchronize()
+                if job.want_outputs:
+                    job.outputs = [o.detach().float().cpu().numpy() for o in outs]
 
 
 __all__ = ["PodServer", "Tenant", "AdmissionError", "DEFAULT_LANES", "DEFAULT_MAX_TENANTS"]

@@ -42,6 +42,8 @@ def make(kind: str, dtype: str, seed: int):
 
             _CACHE["resnet"] = resnet_tenant(dtype, 0)
         return _CACHE["resnet"]
+    if kind == "llama-ft":  # the same decoder as a TRAINING tenant (next-token cross entropy, AdamW)
+        return make("llama", "fp32", seed)
     if kind == "llama":  # a random-init Llama decoder (1024 hidden, 8 layers, head_dim 128, GQA) at seq 512
         if "llama" not in _CACHE:
             from nos_amd.models.llama_program import llama_tenant
@@ -67,8 +69,9 @@ def main() -> None:
                     "from the MFMA registers (0)")
     ap.add_argument("--mix", default="", help="heterogeneous tenants instead of --tenants YOLOS pods, e.g. "
                     "yolos:20,bert:4,mlp:4 (bert = BERT-base-shaped fp32 encoder at seq 512, mlp = bf16 GEMM-MLP "
-                    "probe, resnet = ResNet-18 at 224x224, llama = Llama decoder at seq 512); per-kind rates in "
-                    "the output")
+                    "probe, resnet = ResNet-18 at 224x224, llama = Llama decoder at seq 512, llama-ft = that decoder "
+                    "fine-tuned in the server: a training tenant, its rate in optimisation steps/s); per-kind rates "
+                    "in the output")
     a = ap.parse_args()
     kinds = ([k for spec in a.mix.split(",") for k in [spec.split(":")[0]] * int(spec.split(":")[1])]
              if a.mix else ["yolos"] * a.tenants)
@@ -92,7 +95,17 @@ def main() -> None:
         clients = [PodClient(path, connect_timeout_s=30) for _ in range(a.tenants)]
         progs = [make(k, a.dtype, i) for i, k in enumerate(kinds)]
         t_built = time.monotonic()
-        reps = [c.register(f"pod-{i}", *progs[i], memory_limit_gb=a.slice_gb) for i, c in enumerate(clients)]
+        train = {"loss": "cross_entropy", "optimizer": "adamw", "lr": 1e-4}
+        reps = [c.register(f"pod-{i}", *progs[i], memory_limit_gb=a.slice_gb,
+                           train=train if kinds[i].endswith("-ft") else None) for i, c in enumerate(clients)]
+        batches = {}
+        for i, k in enumerate(kinds):
+            if k.endswith("-ft"):
+                import numpy as np
+
+                shp = reps[i]["input_shape"]
+                ids = np.random.default_rng(i).integers(0, 32000, (shp[0], shp[1] + 1)).astype(np.int32)
+                batches[i] = (ids[:, :-1], ids[:, 1:])
         build_s = time.monotonic() - t_built
         srv_build_ms = sorted(r["compile"].get("build_ms", 0) for r in reps)
         stop = threading.Event()
@@ -100,7 +113,10 @@ def main() -> None:
 
         def loop(i: int) -> None:
             while not stop.is_set():
-                clients[i].infer()
+                if i in batches:
+                    clients[i].train_step(*batches[i])
+                else:
+                    clients[i].infer()
                 marks[i].append(time.monotonic())
 
         th = [threading.Thread(target=loop, args=(i,), daemon=True) for i in range(a.tenants)]
