@@ -851,6 +851,8 @@ class CompiledProgram:
             steps = self._pushdown_row_slices(steps)
             steps = self._fold_batchnorm(steps)
             steps = self._merge_parallel_linears(steps)
+            if "blockdiag" not in skip:
+                steps = self._merge_blockdiag_linears(steps)
             steps = self._fold_layernorm(steps)
             steps = self._fold_rmsnorm(steps)
             steps = self._fuse_epilogues(steps)
@@ -1297,10 +1299,13 @@ class CompiledProgram:
                                                       for m, w in zip(g, ws)]).contiguous()
                 ins.append(name + ".b")
             new_steps = [_Step("linear", ins, name, {})]
+            self._new_shapes[name] = tuple(self._shape(x)[:-1]) + (sum(w.shape[0] for w in ws),)
+            self._new_dtypes[name] = self._dtype(g[0].output)
             src = name
             if act is not None:
                 src = name + "::" + act
                 new_steps.append(_Step(act, [name], src, {}))
+                self._new_shapes[src], self._new_dtypes[src] = self._new_shapes[name], self._new_dtypes[name]
             first[id(g[0])] = new_steps
             off = 0
             for m, w in zip(g, ws):
@@ -1318,6 +1323,113 @@ class CompiledProgram:
                 out.append(s)
         self.stats["linears_merged"] = n
         return out
+
+    def _merge_blockdiag_linears(self, steps: list[_Step], max_rows: int = 1024) -> list[_Step]:
+        """Small linears over ADJACENT column slices of one activation, with
+        the same activation after them (YOLOS's two detection heads after
+        their merged first layer: 384 -> 384 -> 92 classes and 384 -> 384 ->
+        4 boxes) become ONE GEMM over the block-diagonal weight
+        [[W1, 0], [0, W2]] on the joined slice, each original output a column
+        slice of it -- a chain of such layers collapses level by level.  Only
+        for at most ``max_rows`` rows: the zero blocks double the GEMM's
+        FLOPs, which only a launch-bound GEMM does not notice."""
+        import torch
+
+        total = 0
+        while True:
+            uses = self._consumers(steps, self.outputs)
+            by_out = {s.output: s for s in steps}
+            act_of = {s.inputs[0]: s for s in steps if s.kind in ("gelu", "relu") and uses.get(s.inputs[0]) == 1}
+            act_fed = {s.inputs[0] for s in steps if s.kind in ("gelu", "relu")}
+            groups: dict[tuple, list[tuple[int, int, _Step]]] = {}
+            for s in steps:
+                sl = by_out.get(s.inputs[0]) if s.kind == "linear" else None
+                if (sl is None or sl.kind != "slice" or s.attrs or not all(i in self.consts for i in s.inputs[1:])
+                        or uses.get(sl.output) != 1):
+                    continue
+                shape = tuple(self._shape(sl.inputs[0]))
+                if sl.attrs["dim"] % len(shape) != len(shape) - 1 or math.prod(shape[:-1]) > max_rows:
+                    continue
+                if s.output in act_of:
+                    act = act_of[s.output].kind
+                elif s.output not in act_fed:
+                    act = None
+                else:
+                    continue
+                key = (sl.inputs[0], act, str(self.consts[s.inputs[1]].dtype))
+                groups.setdefault(key, []).append((sl.attrs["start"], sl.attrs["end"], s))
+            first: dict[int, list[_Step]] = {}
+            dead: set[int] = set()
+            n = 0
+            for (x, act, _), g in groups.items():
+                g.sort(key=lambda t: t[0])
+                runs, cur = [], [g[0]]
+                for t in g[1:]:
+                    if t[0] == cur[-1][1]:
+                        cur.append(t)
+                    else:
+                        runs.append(cur)
+                        cur = [t]
+                runs.append(cur)
+                for run in runs:
+                    if len(run) < 2:
+                        continue
+                    ws = [self.consts[m.inputs[1]] for _, _, m in run]
+                    nrow, ncol = sum(w.shape[0] for w in ws), sum(w.shape[1] for w in ws)
+                    wbd = torch.zeros((nrow, ncol), dtype=ws[0].dtype, device=ws[0].device)
+                    r = c = 0
+                    for w in ws:
+                        wbd[r:r + w.shape[0], c:c + w.shape[1]] = w
+                        r, c = r + w.shape[0], c + w.shape[1]
+                    m0 = run[0][2]
+                    name = f"{m0.output}::blockdiag"
+                    self.consts[name + ".w"] = wbd
+                    lo, hi = run[0][0], run[-1][1]
+                    new_steps = []
+                    src = x
+                    if lo != 0 or hi != self._shape(x)[-1]:
+                        src = name + "::in"
+                        new_steps.append(_Step("slice", [x], src, {"dim": -1, "start": lo, "end": hi}))
+                        self._new_shapes[src] = tuple(self._shape(x)[:-1]) + (hi - lo,)
+                        self._new_dtypes[src] = self._dtype(x)
+                    ins = [src, name + ".w"]
+                    if any(len(m.inputs) > 2 for _, _, m in run):
+                        self.consts[name + ".b"] = torch.cat(
+                            [self.consts[m.inputs[2]] if len(m.inputs) > 2 else
+                             torch.zeros(w.shape[0], dtype=w.dtype, device=w.device)
+                             for (_, _, m), w in zip(run, ws)]).contiguous()
+                        ins.append(name + ".b")
+                    new_steps.append(_Step("linear", ins, name, {}))
+                    self._new_shapes[name] = tuple(self._shape(x)[:-1]) + (nrow,)
+                    self._new_dtypes[name] = self._dtype(m0.output)
+                    out = name
+                    if act is not None:
+                        out = name + "::" + act
+                        new_steps.append(_Step(act, [name], out, {}))
+                        self._new_shapes[out], self._new_dtypes[out] = self._new_shapes[name], self._new_dtypes[name]
+                    first[id(m0)] = new_steps
+                    off = 0
+                    for (_, _, m), w in zip(run, ws):
+                        dead.add(id(by_out[m.inputs[0]]))   # the input slice
+                        tgt = act_of[m.output] if act is not None else m
+                        tgt.kind, tgt.inputs, tgt.attrs = "slice", [out], {"dim": -1, "start": off,
+                                                                           "end": off + w.shape[0]}
+                        if act is not None:
+                            dead.add(id(m))
+                        off += w.shape[0]
+                    n += len(run)
+            if not n:
+                break
+            total += n
+            merged = []
+            for s in steps:
+                if id(s) in first:
+                    merged.extend(first[id(s)])
+                if id(s) not in dead:
+                    merged.append(s)
+            steps = merged
+        self.stats["linears_blockdiag_merged"] = total
+        return steps
 
     @staticmethod
     def _consumers(steps: list[_Step], outputs: list[str]) -> dict[str, int]:

@@ -66,9 +66,11 @@ def test_outputs_match_the_tenants_own_eager_model(server):
     # the graph compiler folded the LNs into the GEMMs (the final one into the
     # two detection heads' merged first GEMM) and fused QKV + attention
     assert rep["compile"]["layernorm_folded"] == 5 and rep["compile"]["qkv_attention_fused"] == 2
-    assert rep["compile"]["plane_handoffs"] == 4 and rep["compile"]["linears_merged"] == 2
+    assert rep["compile"]["plane_handoffs"] == 5 and rep["compile"]["linears_merged"] == 2
+    # the heads' second and third layers: one block-diagonal GEMM per level
+    assert rep["compile"]["linears_blockdiag_merged"] == 4
     # (+1 residual: the position embeddings, distributed over the token cat, into the patch GEMM)
-    assert rep["compile"]["residual_fused"] == 5 and rep["compile"]["activation_fused"] == 5
+    assert rep["compile"]["residual_fused"] == 5 and rep["compile"]["activation_fused"] == 4
     assert rep["compile"]["adds_distributed"] == 1
     x = np.random.default_rng(0).standard_normal(rep["input_shape"]).astype(np.float32)
     outs, meta = c.infer(x, outputs=True)

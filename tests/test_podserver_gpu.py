@@ -54,7 +54,9 @@ def test_server_replays_match_the_eager_model(server):
     assert rep["compile"]["qkv_attention_fused"] == 12 and rep["compile"]["layernorm_folded"] == 25
     # the heads' first GEMMs (both ReLU) merge into one, ReLU fused, the final LN folded into it
     assert rep["compile"]["linears_merged"] == 2
-    assert rep["compile"]["plane_handoffs"] == 24
+    # ... and their second / third layers into block-diagonal GEMMs (2 + 2)
+    assert rep["compile"]["linears_blockdiag_merged"] == 4
+    assert rep["compile"]["plane_handoffs"] == 25
     assert 0.05 < rep["footprint_gb"] < 10
     x = np.random.default_rng(1).standard_normal(rep["input_shape"]).astype(np.float32)
     outs, meta = c.infer(x, outputs=True)
