@@ -12,7 +12,7 @@ tail -2 $O/smoke.log
 timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || { echo bench failed; tail -30 $O/bench.log; exit 1; }
 grep '^{' $O/bench.log | tail -1 > $O/bench.json
 python3 -c "import json;d=json.load(open('$O/bench.json'));print({k:d.get(k) for k in ('value','aggregate_inf_per_s','matrix_pipe_util_pct','aggregate_vs_single_pod','bf16_fleet_inf_per_s','rank0_sclk_mhz')})"
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/tools/podserver_once.py --tenants 28 --lanes 12 --window 4 > $O/prof.log 2>&1 || { echo prof failed; tail -10 $O/prof.log; exit 1; }
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/tools/podserver_once.py --tenants 28 --window 4 > $O/prof.log 2>&1 || { echo prof failed; tail -10 $O/prof.log; exit 1; }
 cd $R
 f=$(find $O/prof -name "*kernel_stats.csv" | head -1); cp $f $O/kernel_stats.csv; rm -rf $O/prof
 python3 - $O/kernel_stats.csv <<'PY'
