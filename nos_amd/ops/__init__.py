@@ -283,12 +283,15 @@ class RowStats(NamedTuple):
 
 
 def linear_planes(a: H3Planes, weight: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
-                  residual: torch.Tensor | None = None, row_stats: bool = False, out: torch.Tensor | None = None):
+                  residual: torch.Tensor | None = None, row_stats: bool = False, out: torch.Tensor | None = None,
+                  stats_out: torch.Tensor | None = None):
     """act(A @ weight^T + bias) + residual for an A handed over as h3 planes
     (see :class:`H3Planes`): no split pre-pass, no fp32 round trip of A.
     ``row_stats``: also return the output's row statistics for the next
-    LN-GEMM (``nos_gemm_f32h3_stats``) -- ``(out, RowStats)``.  ``out``: an
-    [M, N]-viewable fp32 destination (e.g. a slab of a cat's buffer)."""
+    LN-GEMM (``nos_gemm_f32h3_stats``) -- ``(out, RowStats)``, written into
+    ``stats_out`` (fp32 [M, ceil(N / 128), 2], contiguous) when given.
+    ``out``: an [M, N]-viewable fp32 destination (e.g. a slab of a cat's
+    buffer)."""
     M, K = a.planes.shape[1], a.planes.shape[2]
     N = weight.shape[0]
     if weight.dim() != 2 or weight.shape[1] != K or weight.dtype != torch.float32 or weight.stride(-1) != 1:
@@ -308,7 +311,13 @@ def linear_planes(a: H3Planes, weight: torch.Tensor, bias: torch.Tensor | None =
         _check_f32(residual=r2)
     if row_stats:
         wp, csc = split_f32_weight_h3(weight)
-        st = torch.empty((M, (N + 127) // 128, 2), dtype=torch.float32, device=out.device)
+        shape = (M, (N + 127) // 128, 2)
+        if stats_out is None:
+            st = torch.empty(shape, dtype=torch.float32, device=out.device)
+        else:
+            if tuple(stats_out.shape) != shape or stats_out.dtype != torch.float32 or not stats_out.is_contiguous():
+                raise ValueError(f"stats_out must be a contiguous fp32 {list(shape)}")
+            st = stats_out
         rc = _lib.lib().nos_gemm_f32h3_stats(a.planes.data_ptr(), K, M * K, _ptr(a.rinv), float(a.rconst),
                                              wp.data_ptr(), K, N * K, csc.data_ptr(), _ptr(bias), _ptr(r2),
                                              r2.stride(0) if r2 is not None else 0, out.data_ptr(), N, M, N, K,

@@ -840,7 +840,7 @@ class CompiledProgram:
         self._new_dtypes: dict[str, str] = {}
         with torch.no_grad():
             # NOS_AMD_SKIP_PASSES=name,...: leave launch-trimming passes out (A/B runs)
-            skip = set(os.environ.get("NOS_AMD_SKIP_PASSES", "").split(","))
+            skip = self._skip = set(os.environ.get("NOS_AMD_SKIP_PASSES", "").split(","))
             steps = self._fold_constants(prog)
             if "add_over_cat" not in skip:
                 steps = self._distribute_add_over_cat(steps)
@@ -1657,8 +1657,35 @@ class CompiledProgram:
                     and self._shape(name)[-1] % 32 == 0):
                 p.attrs["row_stats"] = True
                 n += 1
+            elif p.kind == "cat_buffer" and k == 1 and "cat_stats" not in self._skip and self._mark_cat_stats(p, by_out):
+                n += 1
         self.stats["ln_handoffs"] = n
         return steps
+
+    def _mark_cat_stats(self, c: _Step, by_out: dict) -> bool:
+        """An LN-GEMM reading a cat written in place by its GEMM part (YOLOS's
+        [cls, patches, detection tokens] before layer 0): the GEMM writes its
+        rows' statistics into a stats buffer whose constant rows are computed
+        here, once -- the LN-GEMM then needs no statistics pass.  Row-wise
+        cats of fp32 rows whose width is whole 128-column parts only."""
+        import torch
+
+        p = by_out.get(c.inputs[0])
+        buf = self.aux[c.attrs["buf"]]
+        shape = tuple(buf.shape)
+        into = p.attrs.get("out_into") if p is not None else None
+        if (p is None or p.kind != "linear" or into is None or buf.dtype != torch.float32 or len(shape) < 2
+                or into[1] % len(shape) != len(shape) - 2 or shape[-1] % 128 or math.prod(shape[:-2]) != 1):
+            return False
+        rows = buf.reshape(-1, shape[-1]).double().view(shape[-2], shape[-1] // 128, 128)
+        mean = rows.mean(-1)
+        st = torch.stack([mean, ((rows - mean[..., None]) ** 2).sum(-1)], dim=-1).float().contiguous()
+        name = c.attrs["buf"] + "::stats"
+        self.aux[name] = st
+        c.attrs["stats"] = name
+        p.attrs["row_stats"] = True
+        p.attrs["stats_into"] = name
+        return True
 
     def _plan_releases(self, steps: list[_Step]) -> list[_Step]:
         last: dict[str, int] = {}
@@ -1706,8 +1733,11 @@ class CompiledProgram:
                 xa = a[0] if isinstance(a[0], ops.H3Planes) else _rows(a[0])
                 if isinstance(a[0], ops.H3Planes):
                     dst = self.aux[into[0]].narrow(into[1], into[2], self._shape(s.output)[into[1]]) if into else None
+                    sto = None
+                    if rs and into and s.attrs.get("stats_into"):   # the cat buffer's row statistics (slab rows)
+                        sto = self.aux[s.attrs["stats_into"]].narrow(0, into[2], a[0].planes.shape[1])
                     y = ops.linear_planes(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
-                                          residual=res, row_stats=rs, out=dst)
+                                          residual=res, row_stats=rs, out=dst, stats_out=sto)
                     if dst is not None:
                         y = (dst, y[1]) if rs else dst
                 elif into is not None:
@@ -1784,6 +1814,10 @@ class CompiledProgram:
                 y = T.patches(a[0], at["ph"], at["pw"], torch_dtype(at.get("dtype", "fp32")), at.get("hp"), at.get("wp"))
             elif k == "cat_buffer":  # its GEMM part was written in place; the constant parts at build
                 y = self.aux[s.attrs["buf"]]
+                if env.pop(s.inputs[0] + "::lnp", None) is not None:
+                    # the GEMM wrote its rows' statistics into the buffer's stats, whose
+                    # constant rows were filled at build: the whole buffer's, for its LN-GEMM
+                    env[s.output + "::lnp"] = ops.RowStats(self.aux[s.attrs["stats"]], 128)
             else:
                 y = _eager(k, a, s.attrs)
             env[s.output] = y
