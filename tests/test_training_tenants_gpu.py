@@ -90,3 +90,52 @@ def test_graphed_decoder_fine_tuning(tmp_path):
         c.close()
     finally:
         srv.stop()
+
+
+def test_trainer_captures_while_other_tenants_replay_and_on_a_cu_slice(tmp_path):
+    """A training tenant registers (warm-up + graph capture) while an
+    inference tenant replays continuously on the lanes, on its own CU-masked
+    stream; both keep answering correctly."""
+    import threading
+
+    torch.manual_seed(1)
+    m = Mlp()
+    prog, w = export(copy.deepcopy(m), torch.zeros(4, 8, 32), name="mlp")
+    srv = PodServer(tmp_path / "s.sock", device="cuda", lanes=4, memory_gb=64).start()
+    stop = threading.Event()
+    errors = []
+    try:
+        y = PodClient(srv.path, connect_timeout_s=30)
+        y.register("yolos", *demo_tenant("fp32", 0, small=False), memory_limit_gb=2)
+        y.infer()
+
+        def spin():
+            try:
+                while not stop.is_set():
+                    y.infer()
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errors.append(e)
+
+        th = threading.Thread(target=spin, daemon=True)
+        th.start()
+        c = PodClient(srv.path, connect_timeout_s=30)
+        rep = c.register("trainer", prog, w, memory_limit_gb=1, cu_mask="0xffffffff",
+                         train={"loss": "mse", "optimizer": "sgd", "lr": 0.05, "momentum": 0.9})
+        assert rep["compile"]["graph"] is True and rep["cu_mask"] == "0xffffffff"
+        ref = copy.deepcopy(m).cuda().train()
+        ro = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9)
+        for x, t in _data(2, 4):
+            r = c.train_step(x, t)
+            ro.zero_grad()
+            loss = torch.nn.functional.mse_loss(ref(torch.from_numpy(x).cuda()), torch.from_numpy(t).cuda())
+            loss.backward()
+            ro.step()
+            np.testing.assert_allclose(r["loss"], float(loss.detach()), rtol=1e-4)
+        stop.set()
+        th.join(timeout=60)
+        assert not errors, errors
+        c.close()
+        y.close()
+    finally:
+        stop.set()
+        srv.stop()
