@@ -130,3 +130,20 @@ def test_train_specs_are_validated_before_allocation(server):
     with pytest.raises(PodServerError, match="no variants"):
         c.register("v", prog, w, memory_limit_gb=1, train={}, variants=[prog])
     c.close()
+
+
+def test_bf16_program_trains_in_fp32_and_checkpoints_in_its_wire_dtype(server):
+    torch.manual_seed(2)
+    prog, w = export(Mlp(), torch.zeros(4, 8, 32), name="mlp16", dtype="bf16")
+    c = PodClient(server.path, connect_timeout_s=5)
+    c.register("t16", prog, w, memory_limit_gb=1, train={"optimizer": "adamw", "lr": 1e-2})
+    losses = [c.train_step(x, y)["loss"] for x, y in _data(4, 1) * 6]   # one batch, six times
+    assert losses[-1] < losses[0]
+    wb = c.weights()
+    assert len(wb) == len(w) and wb != w
+    c2 = PodClient(server.path, connect_timeout_s=5)
+    c2.register("s16", prog, wb, memory_limit_gb=1)
+    out, _ = c2.infer(_data(4, 1)[0][0], outputs=True)
+    assert np.isfinite(out[0]).all()
+    c.close()
+    c2.close()
