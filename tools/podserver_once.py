@@ -42,6 +42,14 @@ def make(kind: str, dtype: str, seed: int):
 
             _CACHE["resnet"] = resnet_tenant(dtype, 0)
         return _CACHE["resnet"]
+    if kind == "llama-var":  # the decoder registered at seq 512 / 256 / 128 (shape variants, one weight payload)
+        if "llama-var" not in _CACHE:
+            from nos_amd.models.llama_program import llama_config, llama_model, llama_program
+
+            m = llama_model(llama_config(True), 0)
+            progs = [llama_program(m, s_, rope_len=512, dtype=dtype) for s_ in (512, 256, 128)]
+            _CACHE["llama-var"] = (progs[0][0], progs[0][1], [p for p, _ in progs[1:]])
+        return _CACHE["llama-var"]
     if kind == "llama-ft":  # the same decoder as a TRAINING tenant (next-token cross entropy, AdamW)
         return make("llama", "fp32", seed)
     if kind == "llama":  # a random-init Llama decoder (1024 hidden, 8 layers, head_dim 128, GQA) at seq 512
@@ -70,8 +78,9 @@ def main() -> None:
     ap.add_argument("--mix", default="", help="heterogeneous tenants instead of --tenants YOLOS pods, e.g. "
                     "yolos:20,bert:4,mlp:4 (bert = BERT-base-shaped fp32 encoder at seq 512, mlp = bf16 GEMM-MLP "
                     "probe, resnet = ResNet-18 at 224x224, llama = Llama decoder at seq 512, llama-ft = that decoder "
-                    "fine-tuned in the server: a training tenant, its rate in optimisation steps/s); per-kind rates "
-                    "in the output")
+                    "fine-tuned in the server: a training tenant, its rate in optimisation steps/s; llama-var = that "
+                    "decoder registered at seq 512 / 256 / 128, requests cycling through the three shapes); per-kind "
+                    "rates in the output")
     a = ap.parse_args()
     kinds = ([k for spec in a.mix.split(",") for k in [spec.split(":")[0]] * int(spec.split(":")[1])]
              if a.mix else ["yolos"] * a.tenants)
@@ -96,8 +105,9 @@ def main() -> None:
         progs = [make(k, a.dtype, i) for i, k in enumerate(kinds)]
         t_built = time.monotonic()
         train = {"loss": "cross_entropy", "optimizer": "adamw", "lr": 1e-4}
-        reps = [c.register(f"pod-{i}", *progs[i], memory_limit_gb=a.slice_gb,
-                           train=train if kinds[i].endswith("-ft") else None) for i, c in enumerate(clients)]
+        reps = [c.register(f"pod-{i}", *progs[i][:2], memory_limit_gb=a.slice_gb,
+                           train=train if kinds[i].endswith("-ft") else None,
+                           variants=progs[i][2] if len(progs[i]) > 2 else None) for i, c in enumerate(clients)]
         batches = {}
         for i, k in enumerate(kinds):
             if k.endswith("-ft"):
@@ -106,15 +116,26 @@ def main() -> None:
                 shp = reps[i]["input_shape"]
                 ids = np.random.default_rng(i).integers(0, 32000, (shp[0], shp[1] + 1)).astype(np.int32)
                 batches[i] = (ids[:, :-1], ids[:, 1:])
+        shapes = {}
+        for i, r in enumerate(reps):
+            if len(r.get("input_shapes", [])) > 1:
+                import numpy as np
+
+                g = np.random.default_rng(i)
+                shapes[i] = [g.integers(0, 32000, tuple(sh)).astype(np.int32) for sh in r["input_shapes"]]
         build_s = time.monotonic() - t_built
         srv_build_ms = sorted(r["compile"].get("build_ms", 0) for r in reps)
         stop = threading.Event()
         marks: list[list[float]] = [[] for _ in clients]
 
         def loop(i: int) -> None:
+            k = 0
             while not stop.is_set():
                 if i in batches:
                     clients[i].train_step(*batches[i])
+                elif i in shapes:
+                    clients[i].infer(shapes[i][k % len(shapes[i])])
+                    k += 1
                 else:
                     clients[i].infer()
                 marks[i].append(time.monotonic())
