@@ -657,16 +657,22 @@ int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, f
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
   const size_t lds = RS * (size_t)(2 * BM * BKT * 2 + 2 * BN * BKT * 2);
   constexpr int NT = 64 * WGM * WGN;
-  const int grid =
-      nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS, MODE, BATCHED>, NT, lds, ntiles);
-  if (grid < ntiles)
-    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS, MODE, BATCHED>), dim3((unsigned)grid),
-                       dim3(NT), lds, st, Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
-                       N, K, epi, tiles_m, tiles_n, kv, po, bt, ln);
-  else
-    hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false, BKT, RS, MODE, BATCHED>), dim3((unsigned)ntiles),
-                       dim3(NT), lds, st, Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
-                       N, K, epi, tiles_m, tiles_n, kv, po, bt, ln);
+  // batched GEMMs always launch one workgroup per tile: their persistent
+  // form (a CU slice's capped grid) needs 21 more VGPRs than 256 and spilled
+  // to scratch; the CU mask bounds where the tiles run either way
+  if constexpr (!BATCHED) {
+    const int grid =
+        nos_grid_for((const void*)gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS, MODE, BATCHED>, NT, lds, ntiles);
+    if (grid < ntiles) {
+      hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, true, BKT, RS, MODE, BATCHED>), dim3((unsigned)grid),
+                         dim3(NT), lds, st, Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc,
+                         M, N, K, epi, tiles_m, tiles_n, kv, po, bt, ln);
+      return (int)hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((gemm_h3_kernel<BM, BN, WGM, WGN, false, BKT, RS, MODE, BATCHED>), dim3((unsigned)ntiles),
+                     dim3(NT), lds, st, Ap, lda, aplane, rinv, rconst, Wp, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N,
+                     K, epi, tiles_m, tiles_n, kv, po, bt, ln);
   return (int)hipGetLastError();
 }
 

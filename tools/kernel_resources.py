@@ -29,9 +29,14 @@ def demangle(names: list[str]) -> list[str]:
 
 
 def analyse(src: Path, arch: str = "gfx950") -> list[dict]:
+    # the per-source options of the real build (no-NaN / no-SLP attention and
+    # GEMM sources), so the report describes the kernels that actually ship
+    sys.path.insert(0, str(REPO))
+    from nos_amd._native.build import HIP_EXTRA_FLAGS
+
     r = subprocess.run(["/opt/rocm/bin/hipcc", f"--offload-arch={arch}", "-O3", "-std=c++17", "--cuda-device-only",
-                        "-I", str(REPO / "csrc" / "hip"), "-c", str(src), "-o", "/dev/null",
-                        "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
+                        *HIP_EXTRA_FLAGS.get(src.name, []), "-I", str(REPO / "csrc" / "hip"), "-c", str(src), "-o",
+                        "/dev/null", "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
     rows: list[dict] = []
     for line in r.stderr.splitlines():
         m = re.search(r"remark: (?:\S+ )?Function Name: (\S+)", line)
