@@ -715,7 +715,13 @@ def _eager(op: str, args: list, attrs: dict, ref: bool = False):
         x = args[0]
         return F.layer_norm(x, (x.shape[-1],), args[1], args[2], attrs.get("eps", 1e-5))
     if op == "attention":
-        if attrs.get("causal") or args[0].shape[-1] // (3 * attrs["heads"]) != 64 or not args[0].is_cuda:
+        # fp32 under h3 math: the h3 flash kernel with per-row scales (a bare
+        # attention has no LN-folded weights to bound K / V; the x6 kernel it
+        # replaces spends six MFMAs per product instead of three)
+        h3 = (args[0].is_cuda and args[0].dtype == torch.float32 and ops.f32_math() == "h3" and not ref
+              and os.environ.get("NOS_AMD_BARE_ATTN_X6") != "1")   # (=1: the x6 kernel, for A/B)
+        if (attrs.get("causal") or args[0].shape[-1] // (3 * attrs["heads"]) != 64 or not args[0].is_cuda
+                or h3):
             from ..ops import tenant as T
 
             q, k, v = _qkv_views(args[0], attrs["heads"])

@@ -174,3 +174,36 @@ def test_gpu_tenant_shape_variants_share_weights(tmp_path):
         c.close()
     finally:
         srv.stop()
+
+
+def test_bare_fp32_attention_runs_the_h3_flash_kernel():
+    """A post-LN block's attention (its QKV projection reads the residual
+    stream, so no LayerNorm folds into it) under h3 math: the per-row-scale
+    h3 flash kernel, within 4x torch fp32's error against fp64."""
+    from nos_amd.podserver.program import Builder
+
+    g = np.random.default_rng(3)
+    S, D, H = 333, 384, 6
+    b = Builder("bare-attn")
+    x = b.input("x", [1, S, D])
+    wq = b.param("wqkv", (g.standard_normal((3 * D, D)) / D ** 0.5).astype(np.float32))
+    bq = b.param("bqkv", (g.standard_normal(3 * D) * 0.1).astype(np.float32))
+    wo = b.param("wo", (g.standard_normal((D, D)) / D ** 0.5).astype(np.float32))
+    a = b.op("attention", b.op("linear", x, wq, bq), heads=H)
+    y = b.op("add", b.op("linear", a, wo), x, out="y")
+    prog, w = b.build([y])
+    p = PG.parse(prog, w, gpu=True)
+    cm = p.compile("cuda")
+    assert any(s.kind == "attention" for s in cm.steps)
+    xt = torch.from_numpy(g.standard_normal((1, S, D)).astype(np.float32))
+    with torch.no_grad():
+        got = cm(xt.cuda())[0]
+        ps = {k: v.double() for k, v in p.tensors("cpu").items()}
+        qkv = xt.double() @ ps["wqkv"].t() + ps["bqkv"]
+        q, k, v = qkv.view(1, S, 3, H, D // H).unbind(2)
+        att = torch.softmax(torch.einsum("bqhd,bkhd->bhqk", q, k) / (D // H) ** 0.5, -1)
+        o = torch.einsum("bhqk,bkhd->bqhd", att, v).reshape(1, S, D)
+        ref64 = o @ ps["wo"].t() + xt.double()
+        f32 = p.reference(xt)[0]
+    e, e32 = _err(got.cpu(), ref64), _err(f32, ref64)
+    assert e <= max(4 * e32, 1e-5), (e, e32)
