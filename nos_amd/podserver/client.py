@@ -68,12 +68,12 @@ class PodClient:
             raise PodServerError(f"{ENV_POD_SERVER} is not set: this pod was not allocated a pod-server slice")
         return cls(path, **kw)
 
-    def _call(self, req: dict, payload: bytes = b"") -> tuple[dict, bytes]:
+    def _call(self, req: dict, payload: bytes = b"", reply_limit: int | None = None) -> tuple[dict, bytes]:
         if self.sock is None:
             raise PodServerGone("client is closed")
         try:
             P.send_msg(self.sock, req, payload)
-            rep, data = P.recv_msg(self.sock)
+            rep, data = P.recv_msg(self.sock, None if reply_limit is None else (lambda obj, n: reply_limit))
         except (ConnectionError, OSError) as e:
             raise PodServerGone(f"pod server connection lost: {e}") from e
         if not rep.get("ok"):
@@ -161,7 +161,9 @@ class PodClient:
     def weights(self) -> bytes:
         """A training tenant's current weights in its program's payload
         layout: ``register(program, weights=...)`` resumes from them."""
-        return self._call({"op": "weights"})[1]
+        # a weight payload may exceed the protocol's default 1 GiB reply bound
+        # (the server's slice bounds it); the caller asked for all of it
+        return self._call({"op": "weights"}, reply_limit=1 << 42)[1]
 
     def stats(self) -> dict:
         return self._call({"op": "stats"})[0]
