@@ -46,6 +46,21 @@ that the server checks against the tenant's slice before building.
    dropped after their last consumer, so a HIP graph captured from the
    compiled program reuses their memory.
 
+Later passes (round 4-5), each trimming launches or memory round trips (the
+full order is in :class:`CompiledProgram`; ``NOS_AMD_SKIP_PASSES=name,...``
+leaves the switchable ones out for A/B runs): ``add`` over ``cat``
+distribution (position embeddings become the patch GEMM's residual), ViT
+patch extraction as one strided im2col (``patchify``; bf16: the cast folded
+in), cast + reshape / permute chains as one ``relayout``, row-slice
+pushdown (YOLOS's last layer on its detection tokens only), BatchNorm
+folding, parallel linears merged (Q / K / V, gate / up, the detection heads'
+first layers), small linears over adjacent column slices merged into
+block-diagonal GEMMs (``blockdiag``), RMSNorm folding, cast + activation as
+one ``unary`` pass (``cast_unary``), rotary fused into ``sdpa``, a cat
+written in place by its GEMM (``cat_buffer``), fp16-plane and LayerNorm
+hand-offs between h3 kernels (``cat_stats``: layer 0's statistics from the
+patch GEMM plus build-time constant rows), conv weight preparation.
+
 The compiled program is a callable ``(x) -> tuple(outputs)``, captured into a
 HIP graph by the server exactly like a built-in model.  :meth:`Program.reference`
 runs the unfused graph eagerly in fp32 (the numerics reference of tests).
