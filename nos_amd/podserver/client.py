@@ -165,6 +165,12 @@ class PodClient:
         # (the server's slice bounds it); the caller asked for all of it
         return self._call({"op": "weights"}, reply_limit=1 << 42)[1]
 
+    def checkpoint(self) -> bytes:
+        """A training tenant's weights followed by its optimizer state:
+        ``register(program, weights=<this>, train={..., "resume": True})``
+        continues the run where it stopped."""
+        return self._call({"op": "checkpoint"}, reply_limit=1 << 42)[1]
+
     def stats(self) -> dict:
         return self._call({"op": "stats"})[0]
 

@@ -396,6 +396,11 @@ class PodServer:
                         if tenant is None or tenant.trainer is None:
                             raise AdmissionError("weights: only a training tenant's weights change")
                         P.send_msg(conn, {"ok": True, "step": tenant.trainer.steps}, tenant.trainer.weights_bytes())
+                    elif op == "checkpoint":
+                        if tenant is None or tenant.trainer is None:
+                            raise AdmissionError("checkpoint: only a training tenant has optimizer state")
+                        P.send_msg(conn, {"ok": True, "step": tenant.trainer.steps},
+                                   tenant.trainer.checkpoint_bytes())
                     elif op == "stats":
                         P.send_msg(conn, {"ok": True, **self.stats()})
                     elif op == "close":
@@ -517,8 +522,17 @@ class PodServer:
                 if limit and need > limit:
                     raise AdmissionError(f"training tenant needs {need:.2f} GB (static estimate), "
                                          f"its slice has {limit} GB")
+                state = None
+                if spec["resume"]:   # payload = weights + optimizer state (Trainer.checkpoint_bytes)
+                    from .training import state_nbytes
+
+                    wlen = max((o + n for o, n in prog.param_layout.values()), default=0)
+                    if len(payload) != wlen + state_nbytes(prog, spec):
+                        raise AdmissionError(f"resume payload of {len(payload)} bytes: the weights take {wlen}, "
+                                             f"the optimizer state {state_nbytes(prog, spec)}")
+                    state = bytes(payload[wlen:])
                 with self._build_lock:
-                    t = self._build_trainer(tid, req, prog, spec, limit, mask)
+                    t = self._build_trainer(tid, req, prog, spec, limit, mask, state)
                 progs = None
             else:
                 progs = PG.parse_variants([req["program"], *extra], payload, gpu=self.gpu)
@@ -604,7 +618,8 @@ class PodServer:
             raise AdmissionError(f"tenant needs {peak:.2f} GB, its slice has {limit} GB")
         return t
 
-    def _build_trainer(self, tid: int, req: dict, prog, spec: dict, limit: float, mask: str | None) -> Tenant:
+    def _build_trainer(self, tid: int, req: dict, prog, spec: dict, limit: float, mask: str | None,
+                       state: bytes | None = None) -> Tenant:
         """A training tenant (training.py): fp32 master weights, optimizer
         state and, on the GPU, forward + backward + step captured into one
         graph on the tenant's (CU-masked) stream."""
@@ -614,7 +629,7 @@ class PodServer:
 
         pod = str(req.get("pod", tid))[:253]
         if not self.gpu:
-            tr = Trainer(prog, spec, "cpu")
+            tr = Trainer(prog, spec, "cpu", state)
             return Tenant(tid, pod, limit, "fp32", tr.module, tr.x, program=prog.name, cu_mask=mask, trainer=tr,
                           compile_stats={"train": spec["optimizer"], "loss": spec["loss"]},
                           id_bound=prog.id_bound())
@@ -630,7 +645,7 @@ class PodServer:
                 stream = CUMaskedStream(cus_from_hex(mask), self.info["multiprocessor_count"])
             cap = stream.torch if stream else self._setup_stream
             with torch.cuda.stream(cap):
-                tr = Trainer(prog, spec, "cuda")
+                tr = Trainer(prog, spec, "cuda", state)
             cap.synchronize()
             if self.graphs:
                 tr.capture(cap)

@@ -23,8 +23,10 @@ shared context:
   warm-up steps are undone (weights restored, optimizer state zeroed in
   place), so the first replayed step is the first real step.
 * **State.**  :meth:`Trainer.weights_bytes` returns the current weights in
-  the program's payload layout: re-registering with them resumes training
-  (weights-only checkpoint; optimizer state restarts).
+  the program's payload layout; :meth:`Trainer.checkpoint_bytes` appends the
+  optimizer state (:func:`state_keys`), and a ``resume`` spec over that
+  payload continues the run step for step (the capture restores the loaded
+  state in place after its warm-up).
 
 Memory is bounded like an inference tenant's: a static estimate before
 anything is allocated (:func:`train_bytes_estimate`), then the measured peak
@@ -38,7 +40,7 @@ from .program import Program, ProgramError, _eager, _qkv_views, _req
 
 LOSSES = ("mse", "cross_entropy")
 OPTIMIZERS = ("sgd", "adamw")
-SPEC_KEYS = {"loss", "optimizer", "lr", "momentum", "weight_decay", "betas", "eps", "output", "frozen"}
+SPEC_KEYS = {"loss", "optimizer", "lr", "momentum", "weight_decay", "betas", "eps", "output", "frozen", "resume"}
 
 
 def parse_train_spec(spec, prog: Program) -> dict:
@@ -78,6 +80,7 @@ def parse_train_spec(spec, prog: Program) -> dict:
     return {"loss": loss, "optimizer": opt, "lr": lr, "momentum": num("momentum", 0.0, 0.0, 0.999),
             "weight_decay": num("weight_decay", 0.0, 0.0, 1.0), "betas": [float(b) for b in betas],
             "eps": num("eps", 1e-8, 1e-12, 1.0), "output": out, "frozen": sorted(set(frozen) | constant_weights(prog)),
+            "resume": bool(spec.get("resume", False)),
             "target_shape": tshape, "target_dtype": tdt}
 
 
@@ -160,10 +163,27 @@ def _module_cls():
     return ProgramModule
 
 
+def state_keys(spec: dict) -> list[str]:
+    """The optimizer state a checkpoint carries per trainable weight, in
+    order: SGD's momentum buffer (with momentum), AdamW's two moments + step."""
+    if spec["optimizer"] == "sgd":
+        return ["momentum_buffer"] if spec["momentum"] > 0 else []
+    return ["exp_avg", "exp_avg_sq", "step"]
+
+
+def state_nbytes(prog: Program, spec: dict) -> int:
+    """Bytes of the optimizer-state block that follows the weights in a
+    resume payload (fp32, weight by weight in program order)."""
+    keys = state_keys(spec)
+    per = sum(v.numel for k, v in prog.params.items() if k not in spec["frozen"])
+    n = sum(1 for k in prog.params if k not in spec["frozen"])
+    return 4 * (per * sum(1 for k in keys if k != "step") + n * ("step" in keys))
+
+
 class Trainer:
     """Optimisation steps of one training tenant (see the module docstring)."""
 
-    def __init__(self, prog: Program, spec: dict, device):
+    def __init__(self, prog: Program, spec: dict, device, state: bytes | None = None):
         import torch
 
         self.prog, self.spec = prog, spec
@@ -183,6 +203,54 @@ class Trainer:
         self.graph = None
         self.loss = None
         self.steps = 0
+        self._resume = None
+        if state is not None:
+            self._load_state(state)
+
+    def _load_state(self, raw: bytes) -> None:
+        """Optimizer state from a checkpoint (:meth:`checkpoint_bytes`), set
+        before the first step -- the optimizers then continue from it."""
+        import numpy as np
+        import torch
+
+        if len(raw) != state_nbytes(self.prog, self.spec):
+            raise ProgramError(f"optimizer state of {len(raw)} bytes, the spec needs "
+                               f"{state_nbytes(self.prog, self.spec)}")
+        a = np.frombuffer(raw, dtype=np.float32)
+        off = 0
+        cap = self.device.type == "cuda"
+        saved = {}
+        for p in self.module.weights:
+            st = {}
+            for k in state_keys(self.spec):
+                if k == "step":
+                    v = torch.tensor(float(a[off]), dtype=torch.float32)
+                    st[k] = v.to(self.device) if cap else v
+                    off += 1
+                else:
+                    st[k] = torch.from_numpy(a[off:off + p.numel()].copy()).view(p.shape).to(self.device)
+                    off += p.numel()
+            if st:
+                self.opt.state[p] = st
+                saved[p] = {k: v.clone() for k, v in st.items()}
+        self._resume = saved
+
+    def checkpoint_bytes(self) -> bytes:
+        """Weights (payload layout) followed by the optimizer state: a
+        register payload for ``train={..., "resume": True}``."""
+        import numpy as np
+
+        parts = [self.weights_bytes()]
+        for p in self.module.weights:
+            st = self.opt.state.get(p, {})
+            for k in state_keys(self.spec):
+                v = st.get(k)
+                if k == "step":
+                    parts.append(np.asarray([float(v) if v is not None else 0.0], np.float32).tobytes())
+                else:
+                    t = v.detach().float().cpu().numpy() if v is not None else np.zeros(p.shape, np.float32)
+                    parts.append(np.ascontiguousarray(t, dtype=np.float32).tobytes())
+        return b"".join(parts)
 
     def _loss(self):
         import torch.nn.functional as F
@@ -212,10 +280,13 @@ class Trainer:
             with torch.no_grad():
                 for p, s in zip(self.module.weights, saved):
                     p.copy_(s)
-                for st in self.opt.state.values():   # a fresh optimizer, in place (the graph keeps the addresses)
-                    for v in st.values():
+                for p, st in self.opt.state.items():   # in place: the graph keeps the addresses
+                    for k, v in st.items():
                         if torch.is_tensor(v):
-                            v.zero_()
+                            if self._resume is not None and p in self._resume:
+                                v.copy_(self._resume[p][k])   # the checkpoint's state
+                            else:
+                                v.zero_()                      # a fresh optimizer
             self.opt.zero_grad(set_to_none=True)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):

@@ -147,3 +147,31 @@ def test_bf16_program_trains_in_fp32_and_checkpoints_in_its_wire_dtype(server):
     assert np.isfinite(out[0]).all()
     c.close()
     c2.close()
+
+
+@pytest.mark.parametrize("opt", [dict(optimizer="sgd", lr=0.05, momentum=0.9), dict(optimizer="adamw", lr=1e-2)])
+def test_checkpoint_resumes_weights_and_optimizer_state(server, opt):
+    """Train 3 steps, checkpoint, resume in a new tenant for 3 more: the
+    losses equal 6 uninterrupted steps (momentum / Adam moments carried)."""
+    torch.manual_seed(3)
+    prog, w = export(Mlp(), torch.zeros(4, 8, 32), name="mlp")
+    data = _data(5, 6)
+    spec = dict(loss="mse", **opt)
+    a = PodClient(server.path, connect_timeout_s=5)
+    a.register("a", prog, w, memory_limit_gb=1, train=spec)
+    straight = [a.train_step(x, y)["loss"] for x, y in data]
+    a.close()
+    b = PodClient(server.path, connect_timeout_s=5)
+    b.register("b", prog, w, memory_limit_gb=1, train=spec)
+    first = [b.train_step(x, y)["loss"] for x, y in data[:3]]
+    ck = b.checkpoint()
+    b.close()
+    c = PodClient(server.path, connect_timeout_s=5)
+    c.register("c", prog, ck, memory_limit_gb=1, train={**spec, "resume": True})
+    rest = [c.train_step(x, y)["loss"] for x, y in data[3:]]
+    np.testing.assert_allclose(first + rest, straight, rtol=1e-6)
+    c.close()
+    d = PodClient(server.path, connect_timeout_s=5)
+    with pytest.raises(PodServerError, match="resume payload"):
+        d.register("d", prog, w, memory_limit_gb=1, train={**spec, "resume": True})
+    d.close()

@@ -139,3 +139,31 @@ def test_trainer_captures_while_other_tenants_replay_and_on_a_cu_slice(tmp_path)
     finally:
         stop.set()
         srv.stop()
+
+
+def test_graphed_checkpoint_resume_continues_the_run(tmp_path):
+    """GPU: a resumed training tenant's captured graph starts from the
+    checkpoint's weights and AdamW moments (the capture's warm-up restores
+    them in place), so 3 + 3 steps equal 6 uninterrupted ones."""
+    torch.manual_seed(4)
+    prog, w = export(Mlp(), torch.zeros(4, 8, 32), name="mlp")
+    data = _data(6, 6)
+    spec = {"loss": "mse", "optimizer": "adamw", "lr": 1e-2}
+    srv = PodServer(tmp_path / "s.sock", device="cuda", lanes=2, memory_gb=64).start()
+    try:
+        a = PodClient(srv.path, connect_timeout_s=30)
+        a.register("a", prog, w, memory_limit_gb=1, train=spec)
+        straight = [a.train_step(x, y)["loss"] for x, y in data]
+        a.close()
+        b = PodClient(srv.path, connect_timeout_s=30)
+        b.register("b", prog, w, memory_limit_gb=1, train=spec)
+        first = [b.train_step(x, y)["loss"] for x, y in data[:3]]
+        ck = b.checkpoint()
+        b.close()
+        c = PodClient(srv.path, connect_timeout_s=30)
+        c.register("c", prog, ck, memory_limit_gb=1, train={**spec, "resume": True})
+        rest = [c.train_step(x, y)["loss"] for x, y in data[3:]]
+        np.testing.assert_allclose(first + rest, straight, rtol=1e-5)
+        c.close()
+    finally:
+        srv.stop()
