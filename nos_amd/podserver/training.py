@@ -17,8 +17,8 @@ shared context:
   spec's ``frozen`` names.
 * **Step.**  forward -> loss (``mse`` against a float target of the
   output's shape, or ``cross_entropy`` of logits [..., C] against int class
-  ids [...]) -> backward -> optimizer step (SGD with momentum / AdamW,
-  torch.optim, capturable) -- on the GPU captured ONCE into a HIP graph, so
+  ids [...]) -> backward -> optimizer step (SGD with (Nesterov) momentum /
+  Adam / AdamW, torch.optim, capturable) -- on the GPU captured ONCE into a HIP graph, so
   a step is one graph replay on any lane, like an inference.  The capture's
   warm-up steps are undone (weights restored, optimizer state zeroed in
   place), so the first replayed step is the first real step.
@@ -39,8 +39,9 @@ import math
 from .program import Program, ProgramError, _eager, _qkv_views, _req
 
 LOSSES = ("mse", "cross_entropy")
-OPTIMIZERS = ("sgd", "adamw")
-SPEC_KEYS = {"loss", "optimizer", "lr", "momentum", "weight_decay", "betas", "eps", "output", "frozen", "resume"}
+OPTIMIZERS = ("sgd", "adam", "adamw")
+SPEC_KEYS = {"loss", "optimizer", "lr", "momentum", "nesterov", "weight_decay", "betas", "eps", "output", "frozen",
+             "resume"}
 
 
 def parse_train_spec(spec, prog: Program) -> dict:
@@ -61,6 +62,8 @@ def parse_train_spec(spec, prog: Program) -> dict:
         return float(v)
 
     lr = num("lr", 1e-3, 0.0, 10.0)
+    _req(not spec.get("nesterov") or (opt == "sgd" and num("momentum", 0.0, 0.0, 0.999) > 0),
+         "train.nesterov needs sgd with momentum > 0")
     _req(lr > 0, "train.lr must be > 0")
     out = spec.get("output", 0)
     _req(isinstance(out, int) and 0 <= out < len(prog.outputs), "train.output must index a program output")
@@ -80,7 +83,7 @@ def parse_train_spec(spec, prog: Program) -> dict:
     return {"loss": loss, "optimizer": opt, "lr": lr, "momentum": num("momentum", 0.0, 0.0, 0.999),
             "weight_decay": num("weight_decay", 0.0, 0.0, 1.0), "betas": [float(b) for b in betas],
             "eps": num("eps", 1e-8, 1e-12, 1.0), "output": out, "frozen": sorted(set(frozen) | constant_weights(prog)),
-            "resume": bool(spec.get("resume", False)),
+            "resume": bool(spec.get("resume", False)), "nesterov": bool(spec.get("nesterov", False)),
             "target_shape": tshape, "target_dtype": tdt}
 
 
@@ -104,7 +107,7 @@ def train_bytes_estimate(prog: Program, spec: dict) -> int:
     plus the capture's private pool)."""
     w = sum(v.numel * 4 for v in prog.params.values())
     trainable = sum(v.numel * 4 for k, v in prog.params.items() if k not in spec["frozen"])
-    states = {"sgd": 1 if spec["momentum"] > 0 else 0, "adamw": 2}[spec["optimizer"]]
+    states = {"sgd": 1 if spec["momentum"] > 0 else 0, "adam": 2, "adamw": 2}[spec["optimizer"]]
     acts = sum(prog.values[n.output].numel * 4 for n in prog.nodes)
     tgt = math.prod(spec["target_shape"]) * 4
     return w + trainable * (1 + states) + sum(v.numel * 4 for v in prog.inputs) + tgt + 2 * acts
@@ -192,11 +195,12 @@ class Trainer:
         ps = list(self.module.weights)
         cap = self.device.type == "cuda"
         if spec["optimizer"] == "sgd":
-            self.opt = torch.optim.SGD(ps, lr=spec["lr"], momentum=spec["momentum"],
+            self.opt = torch.optim.SGD(ps, lr=spec["lr"], momentum=spec["momentum"], nesterov=spec["nesterov"],
                                        weight_decay=spec["weight_decay"], foreach=True)
         else:
-            self.opt = torch.optim.AdamW(ps, lr=spec["lr"], betas=tuple(spec["betas"]), eps=spec["eps"],
-                                         weight_decay=spec["weight_decay"], capturable=cap, foreach=True)
+            cls = torch.optim.AdamW if spec["optimizer"] == "adamw" else torch.optim.Adam
+            self.opt = cls(ps, lr=spec["lr"], betas=tuple(spec["betas"]), eps=spec["eps"],
+                           weight_decay=spec["weight_decay"], capturable=cap, foreach=True)
         self.x = prog.input_tensor(self.device)
         tdt = torch.int64 if spec["target_dtype"] == "i32" else torch.float32
         self.y = torch.zeros(spec["target_shape"], dtype=tdt, device=self.device)

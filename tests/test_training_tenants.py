@@ -43,6 +43,8 @@ def _data(seed, n=5):
 
 
 @pytest.mark.parametrize("opt", [dict(optimizer="sgd", lr=0.05, momentum=0.9),
+                                 dict(optimizer="sgd", lr=0.05, momentum=0.9, nesterov=True),
+                                 dict(optimizer="adam", lr=1e-2, weight_decay=0.01),
                                  dict(optimizer="adamw", lr=1e-2, weight_decay=0.01)])
 def test_training_tenant_matches_torch_optim(server, opt):
     torch.manual_seed(0)
@@ -52,8 +54,12 @@ def test_training_tenant_matches_torch_optim(server, opt):
     rep = c.register("trainer", prog, w, memory_limit_gb=1, train=dict(loss="mse", **opt))
     assert rep["compile"]["train"] == opt["optimizer"]
     ref = copy.deepcopy(m).train()
-    ro = (torch.optim.SGD(ref.parameters(), lr=opt["lr"], momentum=opt["momentum"]) if opt["optimizer"] == "sgd"
-          else torch.optim.AdamW(ref.parameters(), lr=opt["lr"], weight_decay=opt["weight_decay"]))
+    if opt["optimizer"] == "sgd":
+        ro = torch.optim.SGD(ref.parameters(), lr=opt["lr"], momentum=opt["momentum"],
+                             nesterov=opt.get("nesterov", False))
+    else:
+        cls = torch.optim.AdamW if opt["optimizer"] == "adamw" else torch.optim.Adam
+        ro = cls(ref.parameters(), lr=opt["lr"], weight_decay=opt["weight_decay"])
     for k, (x, y) in enumerate(_data(1)):
         r = c.train_step(x, y)
         ro.zero_grad()
@@ -118,7 +124,8 @@ def test_train_specs_are_validated_before_allocation(server):
     p = PG.parse(prog, w)
     for bad, match in (({"loss": "hinge"}, "train.loss"), ({"lr": 0}, "train.lr"), ({"lr": float("nan")}, "train.lr"),
                        ({"frozen": ["nope"]}, "train.frozen"), ({"schedule": 1}, "unknown train keys"),
-                       ({"loss": "cross_entropy", "output": 3}, "train.output")):
+                       ({"loss": "cross_entropy", "output": 3}, "train.output"),
+                       ({"nesterov": True}, "train.nesterov")):
         with pytest.raises(PG.ProgramError, match=match):
             parse_train_spec(bad, p)
     spec = parse_train_spec({"optimizer": "adamw"}, p)

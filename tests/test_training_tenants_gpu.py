@@ -27,6 +27,8 @@ def _no_tf32():
 
 
 @pytest.mark.parametrize("opt", [dict(optimizer="sgd", lr=0.05, momentum=0.9),
+                                 dict(optimizer="sgd", lr=0.05, momentum=0.9, nesterov=True),
+                                 dict(optimizer="adam", lr=1e-2, weight_decay=0.01),
                                  dict(optimizer="adamw", lr=1e-2, weight_decay=0.01)])
 def test_graphed_training_tenant_beside_an_inference_tenant(tmp_path, opt):
     torch.manual_seed(0)
@@ -40,9 +42,12 @@ def test_graphed_training_tenant_beside_an_inference_tenant(tmp_path, opt):
         y = PodClient(srv.path, connect_timeout_s=30)
         y.register("yolos", *demo_tenant("fp32", 0, small=False), memory_limit_gb=2)
         ref = copy.deepcopy(m).cuda().train()
-        ro = (torch.optim.SGD(ref.parameters(), lr=opt["lr"], momentum=opt["momentum"])
-              if opt["optimizer"] == "sgd"
-              else torch.optim.AdamW(ref.parameters(), lr=opt["lr"], weight_decay=opt["weight_decay"]))
+        if opt["optimizer"] == "sgd":
+            ro = torch.optim.SGD(ref.parameters(), lr=opt["lr"], momentum=opt["momentum"],
+                                 nesterov=opt.get("nesterov", False))
+        else:
+            cls = torch.optim.AdamW if opt["optimizer"] == "adamw" else torch.optim.Adam
+            ro = cls(ref.parameters(), lr=opt["lr"], weight_decay=opt["weight_decay"])
         for k, (x, t) in enumerate(_data(1, 6)):
             r = c.train_step(x, t)
             y.infer()
