@@ -50,6 +50,23 @@ def _connect(path: str, timeout_s: float) -> socket.socket:
             time.sleep(0.1)
 
 
+def _wire(a, want: str | None, what: str) -> np.ndarray:
+    """``a`` as the bytes the tenant reads: the registered program's type
+    (``want``, from the register reply) decides, not the array's -- a uint8
+    image or an int arange for an fp32 model goes as float32 values.  Float
+    data for an id input is refused rather than truncated.  Without ``want``
+    (no register reply seen) integer arrays go as int32, others as float32."""
+    a = np.asarray(a)
+    is_int = np.issubdtype(a.dtype, np.integer) or a.dtype == np.bool_
+    if want == "i32":
+        if not is_int:
+            raise PodServerError(f"{what}: the tenant's model takes integer ids, got {a.dtype}")
+        return np.ascontiguousarray(a, dtype=np.int32)
+    if want == "f32" or not is_int:
+        return np.ascontiguousarray(a, dtype=np.float32)
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
 class PodClient:
     def __init__(self, path: str | os.PathLike, connect_timeout_s: float = 60.0, reconnect_s: float = 0.0):
         self.path = str(path)
@@ -58,6 +75,8 @@ class PodClient:
         self.tenant: int | None = None
         self.info: dict = {}
         self._reg: tuple[dict, bytes] | None = None
+        self.input_dtype: str | None = None    # "f32" / "i32": the registered program's input (register reply)
+        self.target_dtype: str | None = None   # a training tenant's target
         self.reconnects = 0
 
     @classmethod
@@ -102,6 +121,8 @@ class PodClient:
             req["train"] = dict(train)
         rep, _ = self._call(req, weights)
         self._reg = (req, weights)
+        self.input_dtype = rep.get("input_dtype")
+        self.target_dtype = rep.get("target_dtype")
         self.tenant = rep["tenant"]
         self.info = rep
         return rep
@@ -132,12 +153,11 @@ class PodClient:
         req = {"op": "infer", "outputs": outputs}
         if x is None:
             payload = b""
-        elif np.issubdtype(np.asarray(x).dtype, np.integer):  # token ids of an i32 input
-            payload = np.ascontiguousarray(x, dtype=np.int32).tobytes()
         else:
-            payload = np.ascontiguousarray(x, dtype=np.float32).tobytes()
-        if x is not None:
+            wire = _wire(x, self.input_dtype, "input")
+            payload = wire.tobytes()
             req["shape"] = [int(d) for d in np.shape(x)]
+            req["dtype"] = "i32" if wire.dtype == np.int32 else "f32"
         try:
             rep, data = self._call(req, payload)
         except PodServerGone:
@@ -152,11 +172,11 @@ class PodClient:
         target has the trained output's shape (mse, float) or its shape
         without the class dim (cross_entropy, int class ids).  Returns the
         reply: ``loss`` (before the step's update), ``step``, timings."""
-        xa = np.ascontiguousarray(x, dtype=np.int32 if np.issubdtype(np.asarray(x).dtype, np.integer) else np.float32)
-        ta = np.asarray(target)
-        ta = np.ascontiguousarray(ta, dtype=np.int32 if np.issubdtype(ta.dtype, np.integer) else np.float32)
+        xa = _wire(x, self.input_dtype, "input")
+        ta = _wire(target, self.target_dtype, "target")
         xb = xa.tobytes()
-        return self._call({"op": "train", "x_bytes": len(xb)}, xb + ta.tobytes())[0]
+        return self._call({"op": "train", "x_bytes": len(xb), "dtype": "i32" if xa.dtype == np.int32 else "f32",
+                           "target_dtype": "i32" if ta.dtype == np.int32 else "f32"}, xb + ta.tobytes())[0]
 
     def weights(self) -> bytes:
         """A training tenant's current weights in its program's payload

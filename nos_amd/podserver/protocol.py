@@ -17,6 +17,7 @@ from __future__ import annotations
 import json
 import socket
 import struct
+import time
 
 import numpy as np
 
@@ -35,15 +36,28 @@ class PayloadTooLarge(ProtocolError):
     dropped, so the connection can carry the error reply."""
 
 
-def _recv_exact(sock: socket.socket, n: int) -> bytearray:
+def _recv_exact(sock: socket.socket, n: int, deadline: float | None = None) -> bytearray:
+    """``n`` bytes; with a ``deadline`` (time.monotonic()) the whole read must
+    end by then -- a trickle of bytes does not reset it -- else TimeoutError
+    (an OSError), the socket's own timeout restored either way."""
     buf = bytearray(n)  # returned as is: no second copy of a multi-GB payload
     view = memoryview(buf)
     got = 0
-    while got < n:
-        k = sock.recv_into(view[got:], n - got)
-        if k == 0:
-            raise ConnectionError("peer closed the connection")
-        got += k
+    old = sock.gettimeout() if deadline is not None else None
+    try:
+        while got < n:
+            if deadline is not None:
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    raise TimeoutError(f"payload not received in time ({got} of {n} B)")
+                sock.settimeout(left)
+            k = sock.recv_into(view[got:], n - got)
+            if k == 0:
+                raise ConnectionError("peer closed the connection")
+            got += k
+    finally:
+        if deadline is not None:
+            sock.settimeout(old)
     return buf
 
 
@@ -64,12 +78,16 @@ def send_msg(sock: socket.socket, obj: dict, payload: bytes | memoryview = b"") 
         sock.sendall(payload)
 
 
-def recv_msg(sock: socket.socket, payload_limit=None) -> tuple[dict, bytes | bytearray]:
+def recv_msg(sock: socket.socket, payload_limit=None, payload_timeout=None) -> tuple[dict, bytes | bytearray]:
     """(JSON object, payload).  ``payload_limit(obj, npay) -> int`` bounds
     the payload of this message (default ``MAX_PAYLOAD``); it sees the
     announced payload size before a byte of it is read, so a receiver can
     reserve (or refuse) what the payload is for first.  An oversized JSON
-    header desynchronises nothing that can be trusted: ConnectionError."""
+    header desynchronises nothing that can be trusted: ConnectionError.
+    ``payload_timeout(obj, npay) -> seconds | None``: a deadline for the
+    payload once its header has arrived (TimeoutError, an OSError, past it):
+    a sender that announces a payload and stalls cannot hold what the
+    receiver reserved for it."""
     nj, npay = _HDR.unpack(_recv_exact(sock, _HDR.size))
     if nj > MAX_JSON:
         raise ConnectionError(f"message header too large ({nj} B)")
@@ -81,7 +99,10 @@ def recv_msg(sock: socket.socket, payload_limit=None) -> tuple[dict, bytes | byt
     if not isinstance(obj, dict):
         _drain(sock, npay)
         raise ProtocolError("message is not a JSON object")
-    return obj, _recv_exact(sock, npay) if npay else b""
+    if not npay:
+        return obj, b""
+    t = payload_timeout(obj, npay) if payload_timeout is not None else None
+    return obj, _recv_exact(sock, npay, None if t is None else time.monotonic() + float(t))
 
 
 def pack_arrays(arrays: list[np.ndarray]) -> tuple[list[dict], bytes]:

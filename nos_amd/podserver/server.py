@@ -146,18 +146,40 @@ class AdmissionError(RuntimeError):
     pass
 
 
+def _wire_dtype(x) -> str:
+    """The element type a tenant's input travels as: "i32" (token ids) or "f32"."""
+    return "i32" if str(getattr(x, "dtype", "")) == "torch.int32" else "f32"
+
+
+def _target_wire(trainer) -> str:
+    """A training tenant's target on the wire: class ids (i32) or values (f32)."""
+    return "i32" if trainer.spec["target_dtype"] == "i32" else "f32"
+
+
+def _check_wire_dtype(sent, want: str, what: str) -> None:
+    """The payload carries no dtype of its own: a request that names one must
+    name the tenant's (an int array read as float32 bit patterns, or floats
+    read as ids, would run without error and answer garbage).  Requests of
+    older clients name none and are taken as the tenant's type."""
+    if sent is not None and sent != want:
+        raise ValueError(f"{what} sent as {sent!r}, the tenant's model takes {want!r}")
+
+
 class PodServer:
     def __init__(self, socket_path: str | os.PathLike, device: str = "cuda", lanes: int = DEFAULT_LANES,
                  max_tenants: int = DEFAULT_MAX_TENANTS, memory_gb: float | None = None, graphs: bool = True,
                  kernel_config: dict | None = None, solo_graphs: bool = True,
                  allocations_dir: str | os.PathLike | None = None, pod_resources=None,
-                 reap_interval_s: float = 1.0, max_inflight_register_gb: float = 16.0):
+                 reap_interval_s: float = 1.0, max_inflight_register_gb: float = 16.0,
+                 register_timeout_s: float = 30.0, register_min_mb_s: float = 50.0):
         """``allocations_dir``: this GPU's allocation records (tokens
         required; allocations.py).  Without it admission is open: the client
         declares its slice, which must be > 0 when the server accounts
         memory (tests, bare metal).  ``pod_resources``: a PodResources lister
         (resource/client.py) -- tenants whose devices no pod holds any more
-        are evicted."""
+        are evicted.  ``register_timeout_s`` + payload / ``register_min_mb_s``:
+        the deadline of a register payload once its header arrived (a stalled
+        sender's claim is released and its connection closed)."""
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.path = Path(socket_path)
@@ -190,6 +212,8 @@ class PodServer:
         self._tokens: set[str] = set()           # tokens holding a tenant (or a pending build)
         self._inflight_bytes = 0                 # register payload bytes claimed and not yet built
         self.max_inflight_register_bytes = int(max_inflight_register_gb * 2 ** 30)
+        self.register_timeout_s = float(register_timeout_s)
+        self.register_min_mb_s = float(register_min_mb_s)
         self.evictions = 0
 
     # ------------------------------------------------------------ lifecycle
@@ -334,15 +358,21 @@ class PodServer:
                 return 0
             try:
                 return self._claim(req, npay, claim)
-            except AdmissionError as e:
+            except (AdmissionError, TypeError, ValueError) as e:  # bad field types are a refusal, not a crash
                 claim.clear()
                 claim["error"] = f"AdmissionError: {e}"
                 return 0
 
+        def deadline(req: dict, npay: int) -> float | None:
+            # only a claimed register payload holds a reservation worth bounding
+            if req.get("op") != "register" or not claim.get("pending"):
+                return None
+            return self.register_timeout_s + npay / (self.register_min_mb_s * 1e6)
+
         try:
             while not self._stop.is_set():
                 try:
-                    req, payload = P.recv_msg(conn, limit)
+                    req, payload = P.recv_msg(conn, limit, deadline)
                 except P.ProtocolError as e:  # payload drained: the connection is still in step
                     err = claim.pop("error", None) or f"{type(e).__name__}: {e}"
                     self._release_claim(claim)
@@ -360,6 +390,9 @@ class PodServer:
                         P.send_msg(conn, {"ok": True, "tenant": tenant.id, "footprint_gb": tenant.footprint_gb,
                                           "memory_limit_gb": tenant.memory_limit_gb, "cu_mask": tenant.cu_mask,
                                           "input_shape": list(tenant.x.shape),
+                                          "input_dtype": _wire_dtype(tenant.x),
+                                          "target_dtype": (_target_wire(tenant.trainer)
+                                                           if tenant.trainer is not None else None),
                                           "input_shapes": [list(tenant.x.shape)] + [list(k) for k in tenant.alts],
                                           "server": self.info,
                                           "program": tenant.program, "compile": tenant.compile_stats,
@@ -369,6 +402,7 @@ class PodServer:
                             raise AdmissionError("register first")
                         shp = req.get("shape")
                         shp = tuple(int(d) for d in shp) if isinstance(shp, list) and len(shp) <= 8 else None
+                        _check_wire_dtype(req.get("dtype"), _wire_dtype(tenant.x), "input")
                         job = _Job(tenant, payload, bool(req.get("outputs")), shp)
                         self._q.put(job)
                         job.done.wait()
@@ -384,6 +418,8 @@ class PodServer:
                         xb = req.get("x_bytes")
                         if not isinstance(xb, int) or not 0 <= xb <= len(payload):
                             raise ValueError("train: x_bytes must split the payload into input + target")
+                        _check_wire_dtype(req.get("dtype"), _wire_dtype(tenant.trainer.x), "input")
+                        _check_wire_dtype(req.get("target_dtype"), _target_wire(tenant.trainer), "target")
                         job = _Job(tenant, payload, False, kind="train", x_bytes=xb)
                         self._q.put(job)
                         job.done.wait()

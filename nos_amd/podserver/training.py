@@ -39,6 +39,7 @@ import math
 from .program import Program, ProgramError, _eager, _qkv_views, _req
 
 LOSSES = ("mse", "cross_entropy")
+_STEP_SPLIT = 1 << 24   # a checkpointed step count = hi * 2^24 + lo, both exact in float32
 OPTIMIZERS = ("sgd", "adam", "adamw")
 SPEC_KEYS = {"loss", "optimizer", "lr", "momentum", "nesterov", "weight_decay", "betas", "eps", "output", "frozen",
              "resume"}
@@ -61,6 +62,8 @@ def parse_train_spec(spec, prog: Program) -> dict:
              f"train.{key} must be a number in [{lo}, {hi}]")
         return float(v)
 
+    for key in ("resume", "nesterov"):   # strict: bool("false") is True
+        _req(isinstance(spec.get(key, False), bool), f"train.{key} must be true or false")
     lr = num("lr", 1e-3, 0.0, 10.0)
     _req(not spec.get("nesterov") or (opt == "sgd" and num("momentum", 0.0, 0.0, 0.999) > 0),
          "train.nesterov needs sgd with momentum > 0")
@@ -180,7 +183,8 @@ def state_nbytes(prog: Program, spec: dict) -> int:
     keys = state_keys(spec)
     per = sum(v.numel for k, v in prog.params.items() if k not in spec["frozen"])
     n = sum(1 for k in prog.params if k not in spec["frozen"])
-    return 4 * (per * sum(1 for k in keys if k != "step") + n * ("step" in keys))
+    # Adam's step: two float32 slots, hi * 2^24 + lo, exact past 2^24 steps
+    return 4 * (per * sum(1 for k in keys if k != "step") + 2 * n * ("step" in keys))
 
 
 class Trainer:
@@ -228,9 +232,9 @@ class Trainer:
             st = {}
             for k in state_keys(self.spec):
                 if k == "step":
-                    v = torch.tensor(float(a[off]), dtype=torch.float32)
+                    v = torch.tensor(float(int(a[off]) * _STEP_SPLIT + int(a[off + 1])), dtype=torch.float32)
                     st[k] = v.to(self.device) if cap else v
-                    off += 1
+                    off += 2
                 else:
                     st[k] = torch.from_numpy(a[off:off + p.numel()].copy()).view(p.shape).to(self.device)
                     off += p.numel()
@@ -250,7 +254,8 @@ class Trainer:
             for k in state_keys(self.spec):
                 v = st.get(k)
                 if k == "step":
-                    parts.append(np.asarray([float(v) if v is not None else 0.0], np.float32).tobytes())
+                    n = int(round(float(v))) if v is not None else 0
+                    parts.append(np.asarray(divmod(n, _STEP_SPLIT), np.float32).tobytes())
                 else:
                     t = v.detach().float().cpu().numpy() if v is not None else np.zeros(p.shape, np.float32)
                     parts.append(np.ascontiguousarray(t, dtype=np.float32).tobytes())

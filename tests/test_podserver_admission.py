@@ -409,6 +409,80 @@ def test_a_dropped_connection_releases_its_claim(tokened):
     c.close()
 
 
+def test_a_stalled_register_payload_times_out_and_frees_its_claim(tmp_path):
+    """a client that sends only a register header (or
+    part of its payload) and stalls must not hold its slot, slice and
+    in-flight bytes forever: the payload has a deadline, then the claim is
+    released and the connection closed."""
+    srv = PodServer(tmp_path / "s.sock", device="cpu", lanes=1, memory_gb=40, max_inflight_register_gb=1.5 / 1024,
+                    register_timeout_s=0.5, register_min_mb_s=1e6).start()
+    try:
+        a, _ = _raw_register(srv.path, None, 1 << 20, send=0)         # header only
+        assert _wait(lambda: srv._inflight_bytes == 1 << 20)
+        assert _wait(lambda: srv._inflight_bytes == 0 and srv.stats()["pending"] == 0, timeout=10)
+        a.settimeout(5)
+        assert a.recv(1) == b""                                      # the server closed it
+        a.close()
+        c = PodClient(srv.path, connect_timeout_s=5)                   # the budget is free again
+        c.register("p", *YOLOS, memory_limit_gb=10)
+        c.close()
+    finally:
+        srv.stop()
+
+
+def test_a_bad_memory_limit_type_is_an_error_reply_not_a_dropped_connection(tmp_path):
+    """a list for memory_limit_gb under open admission."""
+    from nos_amd.podserver import protocol as P
+    import socket
+
+    srv = PodServer(tmp_path / "s.sock", device="cpu", lanes=1, memory_gb=40).start()
+    try:
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.connect(str(srv.path))
+        prog, w = YOLOS
+        P.send_msg(s, {"op": "register", "pod": "x", "program": prog, "memory_limit_gb": [1, 2]}, w)
+        rep, _ = P.recv_msg(s)
+        assert not rep["ok"] and "AdmissionError" in rep["error"]
+        P.send_msg(s, {"op": "stats"})                                # the connection is still in step
+        assert P.recv_msg(s)[0]["ok"]
+        s.close()
+    finally:
+        srv.stop()
+
+
+def test_integer_data_for_an_fp32_tenant_goes_as_values(tmp_path):
+    """the wire carries no dtype of its own, so the
+    client converts by the registered program's input type (a uint8 image
+    for an fp32 model arrives as float32 values, not reinterpreted bits) and
+    the server refuses a request that names another type."""
+    from nos_amd.podserver import protocol as P
+    import socket
+
+    prog, w = PG.mlp_program(dim=32, layers=1, batch=2, dtype="fp32", seed=0)
+    srv = PodServer(tmp_path / "s.sock", device="cpu", lanes=1, memory_gb=40).start()
+    try:
+        c = PodClient(srv.path, connect_timeout_s=5)
+        rep = c.register("p", prog, w, memory_limit_gb=1)
+        assert rep["input_dtype"] == "f32" and c.input_dtype == "f32"
+        shape = rep["input_shape"]
+        xi = (np.arange(int(np.prod(shape))) % 7).reshape(shape).astype(np.uint8)
+        oi, _ = c.infer(xi, outputs=True)
+        of, _ = c.infer(xi.astype(np.float32), outputs=True)
+        assert np.array_equal(oi[0], of[0])
+        # a raw request naming the wrong type is refused
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.connect(str(srv.path))
+        P.send_msg(s, {"op": "register", "pod": "q", "program": prog, "memory_limit_gb": 1}, w)
+        assert P.recv_msg(s)[0]["ok"]
+        P.send_msg(s, {"op": "infer", "shape": shape, "dtype": "i32"}, xi.astype(np.int32).tobytes())
+        rep2, _ = P.recv_msg(s)
+        assert not rep2["ok"] and "takes 'f32'" in rep2["error"]
+        s.close()
+        c.close()
+    finally:
+        srv.stop()
+
+
 # ----------------------------------------------------------------- device plugin restart
 def _pod_server_plugin(root, smi):
     from nos_amd.deviceplugin.plugin import NosAmdDevicePlugin

@@ -125,7 +125,8 @@ def test_train_specs_are_validated_before_allocation(server):
     for bad, match in (({"loss": "hinge"}, "train.loss"), ({"lr": 0}, "train.lr"), ({"lr": float("nan")}, "train.lr"),
                        ({"frozen": ["nope"]}, "train.frozen"), ({"schedule": 1}, "unknown train keys"),
                        ({"loss": "cross_entropy", "output": 3}, "train.output"),
-                       ({"nesterov": True}, "train.nesterov")):
+                       ({"nesterov": True}, "train.nesterov"), ({"resume": "false"}, "train.resume"),
+                       ({"optimizer": "sgd", "momentum": 0.9, "nesterov": "false"}, "train.nesterov")):
         with pytest.raises(PG.ProgramError, match=match):
             parse_train_spec(bad, p)
     spec = parse_train_spec({"optimizer": "adamw"}, p)
@@ -182,3 +183,25 @@ def test_checkpoint_resumes_weights_and_optimizer_state(server, opt):
     with pytest.raises(PodServerError, match="resume payload"):
         d.register("d", prog, w, memory_limit_gb=1, train={**spec, "resume": True})
     d.close()
+
+
+def test_adam_step_count_checkpoints_exactly_past_float32_range(server):
+    """Adam's step is stored as two exact float32 slots, so
+    a count above 2^24 survives checkpoint -> resume."""
+    from nos_amd.podserver.training import Trainer
+
+    prog, w = export(Mlp(), torch.zeros(4, 8, 32), name="mlp")
+    p = PG.parse(prog, w)
+    spec = parse_train_spec({"optimizer": "adamw"}, p)
+    tr = Trainer(p, spec, "cpu")
+    x, y = _data(4, 1)[0]
+    tr.step(torch.from_numpy(x), torch.from_numpy(y))
+    big = (1 << 24) + 3
+    for st in tr.opt.state.values():   # float32 cannot hold 2^24 + 3: an exact count to checkpoint
+        st["step"] = torch.tensor(float(big), dtype=torch.float64)
+    ck = tr.checkpoint_bytes()
+    tr2 = Trainer(p, {**spec, "resume": True}, "cpu", ck[len(w):])
+    steps = {float(st["step"]) for st in tr2.opt.state.values()}
+    assert steps == {float(np.float32(big))}   # restored into torch's float32 step tensor from the exact count
+    raw = np.frombuffer(ck[len(w):], np.float32)
+    assert (1.0 in raw) and (3.0 in raw)         # hi = 1, lo = 3: the exact split
