@@ -1,7 +1,7 @@
 """YOLOS as a pod-server program (numpy only: the client pod never imports torch).
 
 A pod on a pod-server slice ships its model to the GPU's server as a program
-(nos_amd/podserver/program.py): this module writes the YOLOS detector of the
+(nos_amd/podserver/program/): this module writes the YOLOS detector of the
 reference demo (``demos/gpu-sharing-comparison/client/main.py:14-25``) as that
 op graph, with random-init weights drawn by numpy (no network, no
 checkpoints).  The graph spells the model out op by op -- patchify,

@@ -31,8 +31,14 @@ def load(root: Path) -> dict[str, dict[str, float]]:
 def derive(c: dict[str, float], cus: int = 256) -> dict[str, float]:
     out = {}
     if c.get("GRBM_GUI_ACTIVE") and c.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None:
-        # MFMA busy cycles are summed over CUs (SIMD-cycles / 4 per CU on gfx9 counters)
+        # the rounds-1..5 figure, kept for comparison: busy / (GRBM_GUI_ACTIVE x CUs)
         out["mfma_busy_pct_of_cu_cycles"] = 100.0 * c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] * cus)
+        # the matrix-pipe utilisation itself: SQ_VALU_MFMA_BUSY_CYCLES counts SIMD
+        # cycles (32 per 32x32x16 MFMA) summed over the chip's 4 x CUs SIMDs, and
+        # rocprofv3's GRBM_GUI_ACTIVE is the sum over the 8 XCDs (MI355X_MICROARCH.md,
+        # DVFS note), so the elapsed cycles are GUI / 8 and the pipe-cycles available
+        # GUI / 8 x 4 x CUs.  (The old figure is half of this: it divided by GUI x CUs.)
+        out["mfma_util_pct"] = 100.0 * c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * 4 * cus)
     if c.get("SQ_INSTS_MFMA"):
         out["valu_per_mfma"] = c.get("SQ_INSTS_VALU", 0.0) / c["SQ_INSTS_MFMA"]
     h, m = c.get("TCC_HIT_sum"), c.get("TCC_MISS_sum")
