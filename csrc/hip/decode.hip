@@ -1,0 +1,479 @@
+// Stateful decoding on the pod server (nos_amd/podserver/program/, ops
+// kv_write / rotary_at / sdpa_cache / pos_add / pos_set / argmax) and the
+// skinny GEMMs a decode step is made of.  A tenant's K / V cache and its
+// position counter live in device memory across requests; every kernel here
+// reads the positions ON THE DEVICE, so one captured HIP graph serves every
+// step of a generation, and every index a position produces is bounds-checked
+// against the buffers (a replay never faults on a bad counter: rows past the
+// cache are dropped, table rows clamp).
+//
+//  * nos_kv_write -- cache[b, pos[b] + s] = x[b, s] (optionally rotated at
+//    that position first: the K projection's rotary fused into the write);
+//  * nos_rotary_pos -- rotate_half rotary at positions pos[b] + s;
+//  * nos_attn_decode -- flash-decoding: query rows at positions pos[b] + i
+//    attend the cached keys 0 .. pos[b] + i.  The cache is HBM-bound (per key
+//    2 x D loads for G x Sq x 2 D FLOPs, ~2 FLOP/B at Sq = 1): the kernel runs
+//    at the cache's own precision with fp32 FMAs on the VALU -- exact for an
+//    fp32 cache, more precise than the h3 pipes -- and spends its effort on
+//    bandwidth: one workgroup per (sequence, K/V head, 128-key split), every
+//    query head of the group (grouped-query) served from one read of the
+//    split's keys and values, staged through LDS with 16-byte loads;
+//    nos_attn_decode_combine merges the splits (log-sum-exp);
+//  * nos_pos_update -- pos += n / pos = n;
+//  * nos_argmax -- greedy next tokens, one wave per row;
+//  * nos_gemv -- y = act(r x W^T + b) + R for M <= 8 rows (a decode step's
+//    every GEMM): weight-streaming, each wave two output columns, lanes over
+//    K with 16-byte weight loads, x rows in LDS (optionally RMS-normalised in
+//    the prologue: RMSNorm folded into the GEMM, gamma in W), exact fp32 math.
+#include <float.h>
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8, EPI_SILU = 64 };
+
+__device__ __forceinline__ float ldf(const void* p, long long i, int bf) {
+  return bf ? nos::bf16_to_f32(static_cast<const unsigned short*>(p)[i]) : static_cast<const float*>(p)[i];
+}
+
+__device__ __forceinline__ void stf(void* p, long long i, float v, int bf) {
+  if (bf)
+    static_cast<unsigned short*>(p)[i] = nos::f32_to_bf16(v);
+  else
+    static_cast<float*>(p)[i] = v;
+}
+
+// 4 consecutive elements (16-byte fp32 or 8-byte bf16 load) as floats
+__device__ __forceinline__ float4 ld4(const void* p, long long i, int bf) {
+  if (bf) {
+    const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const unsigned short*>(p) + i);
+    return float4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                  __uint_as_float(u.y & 0xffff0000u)};
+  }
+  return *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+}
+
+// ------------------------------------------------------------------ kv_write / rotary at device positions
+// one thread per (b, s, h, d < D/2) pair (d, d + D/2): the rotate_half pair
+// a fused rotary needs; without tables it just copies both elements
+__global__ __launch_bounds__(256) void kv_write_kernel(const void* __restrict__ x, int xbf, int ldx, long long bsx,
+                                                       void* __restrict__ cache, int cbf, const int* __restrict__ pos,
+                                                       const float* __restrict__ cs, const float* __restrict__ sn,
+                                                       int R, int B, int S, int H, int D, int L) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int hd = D / 2;
+  if (i >= (long long)B * S * H * hd) return;
+  const int d = (int)(i % hd);
+  long long r = i / hd;
+  const int h = (int)(r % H);
+  r /= H;
+  const int s = (int)(r % S), b = (int)(r / S);
+  const int p = pos[b] + s;
+  if (p < 0 || p >= L) return;  // past the cache: dropped (the server reports the overflow)
+  const long long xo = b * bsx + (long long)s * ldx + (long long)h * D;
+  float x0 = ldf(x, xo + d, xbf), x1 = ldf(x, xo + d + hd, xbf);
+  if (cs != nullptr) {
+    const long long t = (long long)min(p, R - 1) * D;
+    const float y0 = fmaf(x0, cs[t + d], -x1 * sn[t + d]);
+    const float y1 = fmaf(x1, cs[t + d + hd], x0 * sn[t + d + hd]);
+    x0 = y0;
+    x1 = y1;
+  }
+  const long long co = (((long long)b * L + p) * H + h) * D;
+  stf(cache, co + d, x0, cbf);
+  stf(cache, co + d + hd, x1, cbf);
+}
+
+__global__ __launch_bounds__(256) void rotary_pos_kernel(const void* __restrict__ x, int ldx, long long bsx,
+                                                         void* __restrict__ y, const int* __restrict__ pos,
+                                                         const float* __restrict__ cs, const float* __restrict__ sn,
+                                                         int R, int B, int S, int H, int D, int bf) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int hd = D / 2;
+  if (i >= (long long)B * S * H * hd) return;
+  const int d = (int)(i % hd);
+  long long r = i / hd;
+  const int h = (int)(r % H);
+  r /= H;
+  const int s = (int)(r % S), b = (int)(r / S);
+  const int p = min(max(pos[b] + s, 0), R - 1);
+  const long long xo = b * bsx + (long long)s * ldx + (long long)h * D;
+  const float x0 = ldf(x, xo + d, bf), x1 = ldf(x, xo + d + hd, bf);
+  const long long t = (long long)p * D;
+  const long long yo = (((long long)b * S + s) * H + h) * D;
+  stf(y, yo + d, fmaf(x0, cs[t + d], -x1 * sn[t + d]), bf);
+  stf(y, yo + d + hd, fmaf(x1, cs[t + d + hd], x0 * sn[t + d + hd]), bf);
+}
+
+// ------------------------------------------------------------------ decode attention
+constexpr int KC = 128;      // keys per split (one workgroup)
+constexpr int MAXR = 32;     // query rows (G x Sq) per launch
+
+// workgroup (b, kvh, split): rows r = qi * G + g (query token qi of Sq, query
+// head kvh * G + g); q rows scaled (and rotated) into LDS, the split's keys
+// into LDS, scores -> per-row max / sum -> probabilities in LDS, the split's
+// values into LDS, P V; the partial (acc[D], m, l) of every row to ws
+template <int D>
+__global__ __launch_bounds__(256) void attn_decode_kernel(
+    const void* __restrict__ q, int qbf, int ldq, long long bsq, const void* __restrict__ kc,
+    const void* __restrict__ vc, int cbf, const int* __restrict__ pos, const float* __restrict__ cs,
+    const float* __restrict__ sn, int Rtab, float* __restrict__ ws, int B, int H, int Hkv, int Sq, int q0, int L,
+    int NS, float scale) {
+  constexpr int DP = D + 4;  // padded LDS row (16-byte reads of consecutive rows hit distinct banks)
+  __shared__ __attribute__((aligned(16))) float qs[MAXR * D];
+  __shared__ __attribute__((aligned(16))) float kv[KC * DP];
+  __shared__ float sc[MAXR * KC];
+  __shared__ float mrow[MAXR], lrow[MAXR];
+  const int G = H / Hkv, R = G * Sq;
+  const int split = blockIdx.x % NS, bk = blockIdx.x / NS;
+  const int kvh = bk % Hkv, b = bk / Hkv;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int p0 = pos[b] + q0;                              // position of query row qi = 0 of this launch
+  const int kend = min(p0 + Sq, L);                        // keys 0 .. kend - 1 are visible to some row
+  const int k0 = split * KC, nk = min(KC, kend - k0);
+  float* const out = ws + (long long)blockIdx.x * R * (D + 2);
+  if (nk <= 0 || p0 < 0) {  // an empty split (or a bad counter): l = 0, skipped by the combine
+    for (int r = tid; r < R; r += 256) {
+      out[r * (D + 2) + D] = -INFINITY;
+      out[r * (D + 2) + D + 1] = 0.f;
+    }
+    return;
+  }
+  // q rows -> LDS, times the softmax scale (rotated at their positions first)
+  for (int e = tid; e < R * (D / 2); e += 256) {
+    const int r = e / (D / 2), d = e % (D / 2);
+    const int qi = r / G, g = r % G, h = kvh * G + g;
+    const long long qo = b * bsq + (long long)(q0 + qi) * ldq + (long long)h * D;
+    float x0 = ldf(q, qo + d, qbf), x1 = ldf(q, qo + d + D / 2, qbf);
+    if (cs != nullptr) {
+      const long long t = (long long)min(max(p0 + qi, 0), Rtab - 1) * D;
+      const float y0 = fmaf(x0, cs[t + d], -x1 * sn[t + d]);
+      const float y1 = fmaf(x1, cs[t + d + D / 2], x0 * sn[t + d + D / 2]);
+      x0 = y0;
+      x1 = y1;
+    }
+    qs[r * D + d] = x0 * scale;
+    qs[r * D + d + D / 2] = x1 * scale;
+  }
+  // the split's keys -> LDS (rows past nk zero)
+  const long long cstride = (long long)Hkv * D;  // cache row (token) stride
+  const long long cbase = ((long long)b * L + k0) * cstride + (long long)kvh * D;
+  auto stage = [&](const void* c) {
+    for (int e = tid; e < KC * (D / 4); e += 256) {
+      const int j = e / (D / 4), d4 = (e % (D / 4)) * 4;
+      const float4 v = j < nk ? ld4(c, cbase + j * cstride + d4, cbf) : float4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<float4*>(&kv[j * DP + d4]) = v;
+    }
+  };
+  stage(kc);
+  __syncthreads();
+  // scores: thread -> key j, rows of one parity
+  {
+    const int j = tid & (KC - 1), rh = tid >> 7;
+    const int jabs = k0 + j;
+    float acc[MAXR / 2];
+#pragma unroll
+    for (int i = 0; i < MAXR / 2; ++i) acc[i] = 0.f;
+    for (int d4 = 0; d4 < D; d4 += 4) {
+      const float4 kk = *reinterpret_cast<const float4*>(&kv[j * DP + d4]);
+#pragma unroll
+      for (int i = 0; i < MAXR / 2; ++i) {
+        const int r = rh + 2 * i;
+        if (r < R) {
+          const float4 qq = *reinterpret_cast<const float4*>(&qs[r * D + d4]);
+          acc[i] = fmaf(qq.x, kk.x, fmaf(qq.y, kk.y, fmaf(qq.z, kk.z, fmaf(qq.w, kk.w, acc[i]))));
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MAXR / 2; ++i) {
+      const int r = rh + 2 * i;
+      if (r < R) {
+        const int qpos = p0 + r / G;  // causal: this row sees keys <= its position
+        sc[r * KC + j] = (j < nk && jabs <= qpos) ? acc[i] : -INFINITY;
+      }
+    }
+  }
+  __syncthreads();
+  // per-row max / sum over the split; probabilities back into sc
+  for (int r = wid; r < R; r += 4) {
+    const float s0 = sc[r * KC + lane], s1 = sc[r * KC + lane + 64];
+    const float m = nos::wave_max(fmaxf(s0, s1));
+    const float e0 = m == -INFINITY ? 0.f : __expf(s0 - m), e1 = m == -INFINITY ? 0.f : __expf(s1 - m);
+    sc[r * KC + lane] = e0;
+    sc[r * KC + lane + 64] = e1;
+    const float l = nos::wave_sum(e0 + e1);
+    if (lane == 0) {
+      mrow[r] = m;
+      lrow[r] = l;
+    }
+  }
+  __syncthreads();  // every wave is done with the keys
+  stage(vc);
+  __syncthreads();
+  // P V: thread -> column d, rows of one residue
+  {
+    constexpr int RS = 256 / D;  // rows in parallel
+    const int d = tid % D, r0 = tid / D;
+    for (int r = r0; r < R; r += RS) {
+      float a = 0.f;
+      for (int j = 0; j < nk; ++j) a = fmaf(sc[r * KC + j], kv[j * DP + d], a);
+      out[r * (D + 2) + d] = a;
+    }
+    for (int r = tid; r < R; r += 256) {
+      out[r * (D + 2) + D] = mrow[r];
+      out[r * (D + 2) + D + 1] = lrow[r];
+    }
+  }
+}
+
+// out[b, q0 + qi, h, :] = sum_s e^(m_s - M) acc_s / sum_s e^(m_s - M) l_s over the splits
+template <int D>
+__global__ __launch_bounds__(D) void attn_decode_combine_kernel(const float* __restrict__ ws, void* __restrict__ o,
+                                                                int obf, int B, int H, int Hkv, int Sq, int q0,
+                                                                int Sq_total, int NS) {
+  const int G = H / Hkv, R = G * Sq;
+  const int row = blockIdx.x;  // (b, kvh, r)
+  const int r = row % R, bk = row / R;
+  const int kvh = bk % Hkv, b = bk / Hkv;
+  const int qi = r / G, g = r % G, h = kvh * G + g;
+  const int d = threadIdx.x;
+  float M = -INFINITY;
+  for (int s = 0; s < NS; ++s) {
+    const float* p = ws + ((long long)(bk * NS + s) * R + r) * (D + 2);
+    if (p[D + 1] > 0.f) M = fmaxf(M, p[D]);
+  }
+  float num = 0.f, den = 0.f;
+  for (int s = 0; s < NS; ++s) {
+    const float* p = ws + ((long long)(bk * NS + s) * R + r) * (D + 2);
+    if (p[D + 1] > 0.f) {
+      const float w = __expf(p[D] - M);
+      num = fmaf(w, p[d], num);
+      den = fmaf(w, p[D + 1], den);
+    }
+  }
+  const long long oo = (((long long)b * Sq_total + q0 + qi) * H + h) * D + d;
+  stf(o, oo, den > 0.f ? num / den : 0.f, obf);
+}
+
+// ------------------------------------------------------------------ positions, argmax
+__global__ void pos_update_kernel(int* __restrict__ pos, int B, int add, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) pos[i] = add ? pos[i] + n : n;
+}
+
+// first index of the row maximum (torch.argmax's tie rule); NaN rows give the NaN's index
+__global__ __launch_bounds__(256) void argmax_kernel(const void* __restrict__ x, int bf, int rows, int L, int ldx,
+                                                     int* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float best = -INFINITY;
+  int bi = INT_MAX;
+  for (int j = lane; j < L; j += 64) {
+    const float v = ldf(x, (long long)row * ldx + j, bf);
+    if (v > best || (v != v && best == best)) {
+      best = v;
+      bi = j;
+    }
+  }
+  if (bi == INT_MAX) bi = L;  // an all -inf row: resolved to index 0 below
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    const bool onan = ob != ob, mnan = best != best;
+    if ((onan && !mnan) || (onan == mnan && (ob > best || (ob == best && oi < bi)))) {
+      best = ob;
+      bi = oi;
+    }
+  }
+  if (lane == 0) out[row] = bi >= L ? 0 : bi;
+}
+
+// ------------------------------------------------------------------ GEMV (M <= 8)
+template <int M>
+__global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, int xbf, int ldx,
+                                                   const void* __restrict__ w, int wbf, int ldw,
+                                                   const void* __restrict__ bias, const void* __restrict__ res,
+                                                   int ldr, void* __restrict__ y, int ldy, int N, int K, int epi,
+                                                   float rms_eps) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];  // [M][K] fp32
+  __shared__ float rsc[M];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int e = tid * 4; e < M * K; e += 1024) {
+    const int m = e / K, k = e % K;
+    *reinterpret_cast<float4*>(&xs[e]) = ld4(x, (long long)m * ldx + k, xbf);
+  }
+  __syncthreads();
+  if (rms_eps > 0.f) {  // RMSNorm of each row, gamma folded into W
+    for (int m = wid; m < M; m += 4) {
+      float q = 0.f;
+      for (int k = lane; k < K; k += 64) q = fmaf(xs[m * K + k], xs[m * K + k], q);
+      q = nos::wave_sum(q);
+      if (lane == 0) rsc[m] = rsqrtf(q / (float)K + rms_eps);
+    }
+  } else if (tid < M) {
+    rsc[tid] = 1.f;
+  }
+  __syncthreads();
+  const int ngrp = (N + 7) / 8;  // 8 columns per workgroup pass: 4 waves x 2
+  for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
+    const int n0 = grp * 8 + wid * 2;
+    float acc[2][M];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int m = 0; m < M; ++m) acc[c][m] = 0.f;
+    const int nc0 = min(n0, N - 1), nc1 = min(n0 + 1, N - 1);
+    const long long w0 = (long long)nc0 * ldw, w1 = (long long)nc1 * ldw;
+    for (int k = lane * 4; k < K; k += 256) {
+      const float4 a = ld4(w, w0 + k, wbf), c4 = ld4(w, w1 + k, wbf);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const float4 xv = *reinterpret_cast<const float4*>(&xs[m * K + k]);
+        acc[0][m] = fmaf(a.x, xv.x, fmaf(a.y, xv.y, fmaf(a.z, xv.z, fmaf(a.w, xv.w, acc[0][m]))));
+        acc[1][m] = fmaf(c4.x, xv.x, fmaf(c4.y, xv.y, fmaf(c4.z, xv.z, fmaf(c4.w, xv.w, acc[1][m]))));
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int m = 0; m < M; ++m) acc[c][m] = nos::wave_sum(acc[c][m]);
+    // lane (c * M + m) finishes output (m, n0 + c)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int n = n0 + c;
+        if (lane == c * M + m && n < N) {
+          float v = acc[c][m] * rsc[m];
+          if (epi & EPI_BIAS) v += ldf(bias, n, wbf);
+          if (epi & EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+          if (epi & EPI_RELU) v = fmaxf(v, 0.f);
+          if (epi & EPI_SILU) v = v / (1.f + __expf(-v));
+          if (epi & EPI_RESID) v += ldf(res, (long long)m * ldr + n, xbf);
+          stf(y, (long long)m * ldy + n, v, xbf);
+        }
+      }
+  }
+}
+
+}  // namespace
+
+NOS_API int nos_kv_write(const void* x, int xbf, int ldx, long long bsx, void* cache, int cbf, const int* pos,
+                         const float* cos_t, const float* sin_t, int R, int B, int S, int H, int D, int L,
+                         hipStream_t stream) {
+  if (B <= 0 || S <= 0 || H <= 0 || D <= 0 || (D % 2) || L <= 0 || S > L || ldx < H * D || !x || !cache || !pos ||
+      (B > 1 && bsx < (long long)(S - 1) * ldx + H * D) || (xbf != 0 && xbf != 1) || (cbf != 0 && cbf != 1) ||
+      ((cos_t == nullptr) != (sin_t == nullptr)) || (cos_t && R <= 0))
+    return (int)hipErrorInvalidValue;
+  const long long n = (long long)B * S * H * (D / 2);
+  hipLaunchKernelGGL(kv_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, xbf, ldx, bsx, cache,
+                     cbf, pos, cos_t, sin_t, R, B, S, H, D, L);
+  return (int)hipGetLastError();
+}
+
+NOS_API int nos_rotary_pos(const void* x, int ldx, long long bsx, void* y, const int* pos, const float* cos_t,
+                           const float* sin_t, int R, int B, int S, int H, int D, int bf16, hipStream_t stream) {
+  if (B <= 0 || S <= 0 || H <= 0 || D <= 0 || (D % 2) || R <= 0 || ldx < H * D || !cos_t || !sin_t || !pos ||
+      (B > 1 && bsx < (long long)(S - 1) * ldx + H * D) || (bf16 != 0 && bf16 != 1))
+    return (int)hipErrorInvalidValue;
+  const long long n = (long long)B * S * H * (D / 2);
+  hipLaunchKernelGGL(rotary_pos_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, ldx, bsx, y, pos,
+                     cos_t, sin_t, R, B, S, H, D, bf16);
+  return (int)hipGetLastError();
+}
+
+// bytes of nos_attn_decode's workspace
+NOS_API long long nos_attn_decode_workspace(int B, int H, int Hkv, int Sq, int L, int D) {
+  if (B <= 0 || H <= 0 || Hkv <= 0 || Sq <= 0 || L <= 0 || H % Hkv) return -1;
+  const int G = H / Hkv, rows = G * (Sq < MAXR / G ? Sq : (MAXR / G > 0 ? MAXR / G : 1));
+  const long long NS = (L + KC - 1) / KC;
+  return (long long)B * Hkv * NS * rows * (D + 2) * 4;
+}
+
+// q [B, Sq, H, D] (heads contiguous per token; token stride ldq, batch stride
+// bsq; fp32 / bf16), caches [B, L, Hkv, D] contiguous (fp32 / bf16), pos [B]
+// i32: query i at position pos[b] + i sees keys 0 .. min(pos[b] + i, L - 1).
+// cos / sin [R, D] fp32 (or null): q rotated at its positions.  out [B, Sq, H,
+// D] contiguous (obf: bf16).  Query tokens are processed in launches of at
+// most 32 / G (the rows a workgroup holds), each a decode pass + combine.
+NOS_API int nos_attn_decode(const void* q, int qbf, int ldq, long long bsq, const void* kc, const void* vc, int cbf,
+                            const int* pos, const float* cos_t, const float* sin_t, int R, void* out, int obf, int B,
+                            int H, int Hkv, int Sq, int L, int D, float scale, void* ws, long long ws_bytes,
+                            hipStream_t stream) {
+  if (B <= 0 || H <= 0 || Hkv <= 0 || H % Hkv || H / Hkv > MAXR || Sq <= 0 || L <= 0 || (D != 64 && D != 128) ||
+      ldq < H * D || (B > 1 && bsq < (long long)(Sq - 1) * ldq + H * D) || !q || !kc || !vc || !pos || !out ||
+      !ws || ((cos_t == nullptr) != (sin_t == nullptr)) || (cos_t && R <= 0) || (qbf != 0 && qbf != 1) ||
+      (cbf != 0 && cbf != 1) || (obf != 0 && obf != 1) || !(scale > 0.f))
+    return (int)hipErrorInvalidValue;
+  if (ws_bytes < nos_attn_decode_workspace(B, H, Hkv, Sq, L, D)) return (int)hipErrorInvalidValue;
+  const int G = H / Hkv, chunk = MAXR / G;
+  const int NS = (L + KC - 1) / KC;
+  for (int q0 = 0; q0 < Sq; q0 += chunk) {
+    const int sq = Sq - q0 < chunk ? Sq - q0 : chunk;
+    const unsigned grid = (unsigned)(B * Hkv * NS);
+    const unsigned rows = (unsigned)(B * Hkv * G * sq);
+    if (D == 64) {
+      hipLaunchKernelGGL(attn_decode_kernel<64>, dim3(grid), dim3(256), 0, stream, q, qbf, ldq, bsq, kc, vc, cbf, pos,
+                         cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale);
+      hipLaunchKernelGGL(attn_decode_combine_kernel<64>, dim3(rows), dim3(64), 0, stream,
+                         static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
+    } else {
+      hipLaunchKernelGGL(attn_decode_kernel<128>, dim3(grid), dim3(256), 0, stream, q, qbf, ldq, bsq, kc, vc, cbf,
+                         pos, cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale);
+      hipLaunchKernelGGL(attn_decode_combine_kernel<128>, dim3(rows), dim3(128), 0, stream,
+                         static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
+    }
+  }
+  return (int)hipGetLastError();
+}
+
+NOS_API int nos_pos_update(int* pos, int B, int add, int n, hipStream_t stream) {
+  if (!pos || B <= 0 || n < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pos_update_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, stream, pos, B, add, n);
+  return (int)hipGetLastError();
+}
+
+NOS_API int nos_argmax(const void* x, int bf16, int rows, int L, int ldx, int* out, hipStream_t stream) {
+  if (!x || !out || rows <= 0 || L <= 0 || ldx < L || (bf16 != 0 && bf16 != 1)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, x, bf16, rows, L, ldx,
+                     out);
+  return (int)hipGetLastError();
+}
+
+// y [M, N] = act(rms(x) x [M, K] . W [N, K]^T + bias) + res, M <= 8; x, y, res
+// share x's dtype (xbf), W and bias W's (wbf); K % 4 == 0, rows 16-byte
+// (fp32) / 8-byte (bf16) aligned, M x K x 4 <= 64 KiB (the x rows in LDS).
+// rms_eps > 0: each x row RMS-normalised first.  grid: the CUs' worth of
+// workgroups walk the N / 8 column groups.
+NOS_API int nos_gemv(const void* x, int xbf, int ldx, const void* w, int wbf, int ldw, const void* bias,
+                     const void* res, int ldr, void* y, int ldy, int M, int N, int K, int epi, float rms_eps,
+                     hipStream_t stream) {
+  if (!x || !w || !y || M <= 0 || M > 8 || N <= 0 || K <= 0 || (K % 4) || ldx < K || ldw < K || ldy < N ||
+      (long long)M * K * 4 > 65536 || (xbf != 0 && xbf != 1) || (wbf != 0 && wbf != 1) ||
+      ((epi & EPI_BIAS) && !bias) || ((epi & EPI_RESID) && (!res || ldr < N)) || (ldx % 4) || (ldw % 4) ||
+      ((uintptr_t)x & (xbf ? 7 : 15)) || ((uintptr_t)w & (wbf ? 7 : 15)))
+    return (int)hipErrorInvalidValue;
+  const int ngrp = (N + 7) / 8;
+  const int cap = 4 * nos_effective_cus();
+  const unsigned grid = (unsigned)(ngrp < cap ? ngrp : cap);
+  const size_t lds = (size_t)M * K * 4;
+#define NOS_GEMV(m)                                                                                                 \
+  hipLaunchKernelGGL(gemv_kernel<m>, dim3(grid), dim3(256), lds, stream, x, xbf, ldx, w, wbf, ldw, bias, res, ldr, y, \
+                     ldy, N, K, epi, rms_eps)
+  switch (M) {
+    case 1: NOS_GEMV(1); break;
+    case 2: NOS_GEMV(2); break;
+    case 3: NOS_GEMV(3); break;
+    case 4: NOS_GEMV(4); break;
+    case 5: NOS_GEMV(5); break;
+    case 6: NOS_GEMV(6); break;
+    case 7: NOS_GEMV(7); break;
+    default: NOS_GEMV(8); break;
+  }
+#undef NOS_GEMV
+  return (int)hipGetLastError();
+}

@@ -29,7 +29,7 @@ BUILD = REPO / "build" / "native"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("NOS_AMD_ARCH", "gfx950")
 
-HIP_SOURCES = ["attention.hip", "attention_f32.hip", "attention_f32x.hip", "gemm_f32.hip", "gemm_f32x.hip", "gemm_f32h.hip", "gemm.hip", "layernorm.hip", "probes.hip", "runtime.hip", "tenant_ops.hip", "attention_h3g.hip"]
+HIP_SOURCES = ["attention.hip", "attention_f32.hip", "attention_f32x.hip", "gemm_f32.hip", "gemm_f32x.hip", "gemm_f32h.hip", "gemm.hip", "layernorm.hip", "probes.hip", "runtime.hip", "tenant_ops.hip", "attention_h3g.hip", "decode.hip"]
 # per-source compiler flags, {file: [flags]} (CMakeLists.txt sets the same:
 # tests/test_build_config.py); tools/build_variant.py adds to it for A/B builds.
 # The bf16x6 kernels split fp32 into bf16 pieces and run the softmax with

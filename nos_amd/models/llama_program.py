@@ -107,6 +107,79 @@ def llama_program(model, seq: int, batch: int = 1, dtype: str = "fp32",
     return b.build([logits])
 
 
+def llama_decode_programs(model, prompt_len: int, max_len: int, batch: int = 1, dtype: str = "fp32",
+                          extend: tuple[int, ...] = ()) -> tuple[list[dict], bytes]:
+    """A STATEFUL generation tenant: ``[prefill, decode, *extends]`` programs
+    over one weight payload and one state -- per layer a K and a V cache
+    ``[batch, max_len, kv_heads, head_dim]`` plus the position counter
+    ``pos`` [batch] (i32) -- registered as shape variants (the server routes
+    by the input's shape):
+
+    * prefill, input ids ``[batch, prompt_len]``: starts a sequence
+      (``pos_set`` 0), writes the prompt's K / V into the caches, attends
+      causally (the compiler sees position 0 and runs the flash kernel on the
+      fresh keys), advances ``pos`` by ``prompt_len``;
+    * decode, input ids ``[batch, 1]``: one token at the device-side position
+      -- rotary at ``pos``, ``kv_write`` of its K / V, ``sdpa_cache`` over the
+      cache (decode.hip), ``pos`` += 1;
+    * ``extend`` lengths: like decode for chunks of that many tokens (a longer
+      prompt = prefill + extends + decode steps).
+
+    Every program outputs the last token's logits ``[batch, 1, vocab]`` and
+    the greedy next ids ``[batch, 1]`` (i32, ``argmax``), so a client's
+    generation loop sends back one id per step.  The caches' bytes count
+    against the slice at registration; a replay never allocates state."""
+    if not 0 < prompt_len <= max_len:
+        raise ValueError(f"prompt_len must be in [1, {max_len}]")
+    cfg = model.config
+    sd = {k: v.detach().float().cpu().numpy() for k, v in model.state_dict().items()}
+    d, nh = cfg.hidden_size, cfg.num_attention_heads
+    nkv = cfg.num_key_value_heads
+    hd = getattr(cfg, "head_dim", None) or d // nh
+    eps = float(cfg.rms_norm_eps)
+    cos, sin = rope_tables(max_len, hd, float(getattr(cfg, "rope_theta", 10000.0)))
+    head = "lm_head.weight" if "lm_head.weight" in sd else "model.embed_tokens.weight"
+    cache_dt = "bf16" if dtype == "bf16" else "fp32"
+    progs = []
+    chunks = [(prompt_len, True), (1, False)] + [(n, False) for n in extend]
+    weights = b""
+    for seq, reset in chunks:
+        b = Builder(f"llama-h{d}-l{cfg.num_hidden_layers}-{dtype}-{'prefill' if reset else 'step'}{seq}")
+        ids = b.input("input_ids", [batch, seq], "i32")
+        P = lambda k: b.param(k, sd[k], dtype)  # noqa: E731
+        rc, rs = b.param("rope.cos", cos, "fp32"), b.param("rope.sin", sin, "fp32")
+        b.state("pos", [batch], "i32")
+        caches = [(b.state(f"kc{i}", [batch, max_len, nkv, hd], cache_dt),
+                   b.state(f"vc{i}", [batch, max_len, nkv, hd], cache_dt)) for i in range(cfg.num_hidden_layers)]
+        p = b.op("pos_set", "pos", value=0) if reset else "pos"
+        h = b.op("embedding", ids, P("model.embed_tokens.weight"))
+        for i in range(cfg.num_hidden_layers):
+            pf = f"model.layers.{i}."
+            y = b.op("rmsnorm", h, P(pf + "input_layernorm.weight"), eps=eps)
+            q = b.op("reshape", b.op("linear", y, P(pf + "self_attn.q_proj.weight")), shape=[batch, seq, nh, hd])
+            k = b.op("reshape", b.op("linear", y, P(pf + "self_attn.k_proj.weight")), shape=[batch, seq, nkv, hd])
+            v = b.op("reshape", b.op("linear", y, P(pf + "self_attn.v_proj.weight")), shape=[batch, seq, nkv, hd])
+            q, k = b.op("rotary_at", q, rc, rs, p), b.op("rotary_at", k, rc, rs, p)
+            kc = b.op("kv_write", caches[i][0], k, p)
+            vc = b.op("kv_write", caches[i][1], v, p)
+            o = b.op("reshape", b.op("sdpa_cache", q, kc, vc, p), shape=[batch, seq, nh * hd])
+            h = b.op("add", b.op("linear", o, P(pf + "self_attn.o_proj.weight")), h)
+            y = b.op("rmsnorm", h, P(pf + "post_attention_layernorm.weight"), eps=eps)
+            g = b.op("linear", y, P(pf + "mlp.gate_proj.weight"))
+            u = b.op("linear", y, P(pf + "mlp.up_proj.weight"))
+            h = b.op("add", b.op("linear", b.op("mul", b.op("silu", g), u), P(pf + "mlp.down_proj.weight")), h)
+        if seq > 1:   # only the last token's logits: the LM head runs on one row
+            h = b.op("slice", h, dim=1, start=seq - 1, end=seq)
+        h = b.op("rmsnorm", h, P("model.norm.weight"), eps=eps)
+        logits = b.op("linear", h, P(head), out="logits")
+        nxt = b.op("argmax", logits, out="next_ids")
+        b.op("pos_add", p, n=seq)
+        prog, w = b.build([logits, nxt])
+        progs.append(prog)
+        weights = w
+    return progs, weights
+
+
 def llama_tenant(dtype: str = "fp32", seed: int = 0, small: bool = True, seq: int = 512,
                  batch: int = 1) -> tuple[dict, bytes]:
     """(program, weights) of the decoder-LLM tenant (``small=False``: the
@@ -115,4 +188,4 @@ def llama_tenant(dtype: str = "fp32", seed: int = 0, small: bool = True, seq: in
     return llama_program(m, seq if small else 64, batch, dtype)
 
 
-__all__ = ["llama_config", "llama_model", "llama_program", "llama_tenant", "rope_tables"]
+__all__ = ["llama_config", "llama_model", "llama_program", "llama_decode_programs", "llama_tenant", "rope_tables"]

@@ -81,6 +81,14 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     N = weight.shape[0]
     x2 = x.reshape(-1, K)
     M = x2.shape[0]
+    if M <= _GEMV_ROWS and weight.dim() == 2 and weight.shape[1] == K:
+        from . import tenant as T
+
+        if T.gemv_ok(x2, weight) and (bias is None or bias.is_contiguous()):
+            # a decode step's skinny GEMM: weight-streaming, exact fp32 math
+            o2, r2 = _gemm_io(x, weight, out, residual, M, N, K)
+            T.gemv(x2, weight, bias, act, r2, out=o2)
+            return o2.view(*x.shape[:-1], N)
     if x.dtype == torch.float32:
         return _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K)
     if x2.stride(-1) != 1 or weight.stride(-1) != 1 or K % 64 or x.dtype != torch.bfloat16:
@@ -164,6 +172,7 @@ def _linear_f32(x, x2, weight, bias, act, residual, out, M, N, K):
 
 
 _F32_MATH = "exact"
+_GEMV_ROWS = 8   # tenant.GEMV_MAX_ROWS: GEMMs of at most this many rows run on the GEMV kernel
 # h3 math: a GEMM of at most this many rows (YOLOS's detection-head layers on
 # their 100 tokens) runs on the exact-f32 MFMA kernel -- one launch, no split
 # pass, the f32 pipe's rate is ample for ~30 MFLOP -- instead of split + h3 GEMM

@@ -98,6 +98,18 @@ _SIGS = {
     "nos_im2col": [c_void_p, c_ll, c_ll, c_ll, c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nos_unary": [c_void_p, c_int, c_void_p, c_int, c_ll, c_int, c_void_p],
+    # decode.hip: stateful decoding (K / V caches and positions on the device) and skinny GEMMs
+    "nos_kv_write": [c_void_p, c_int, c_int, c_ll, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                     c_int, c_int, c_int, c_void_p],
+    "nos_rotary_pos": [c_void_p, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                       c_int, c_int, c_void_p],
+    "nos_attn_decode_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
+    "nos_attn_decode": [c_void_p, c_int, c_int, c_ll, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                        c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_ll, c_void_p],
+    "nos_pos_update": [c_void_p, c_int, c_int, c_int, c_void_p],
+    "nos_argmax": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "nos_gemv": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int,
+                 c_int, c_int, c_int, c_float, c_void_p],
     "nos_attn_h3g_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
     # LayerNorm hand-off (gemm_f32h.hip): producer row statistics, LN in the consumer's A load
     "nos_gemm_f32h3_stats": [c_void_p, c_int, c_ll, c_void_p, c_float, c_void_p, c_int, c_ll, c_void_p, c_void_p,
@@ -114,7 +126,7 @@ _SIGS = {
 }
 
 
-_RESTYPES = {"nos_attn_f32x6_workspace": c_ll, "nos_attn_h3g_workspace": c_ll}
+_RESTYPES = {"nos_attn_f32x6_workspace": c_ll, "nos_attn_h3g_workspace": c_ll, "nos_attn_decode_workspace": c_ll}
 
 
 class NativeUnavailable(RuntimeError):

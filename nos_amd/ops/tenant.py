@@ -373,6 +373,10 @@ def linear_rms(x: torch.Tensor, wg: torch.Tensor, bias: torch.Tensor | None = No
     if x2.stride(-1) != 1:
         x2 = x2.contiguous()
     M = x2.shape[0]
+    if M <= GEMV_MAX_ROWS and gemv_ok(x2, wg):   # a decode step: the RMS statistics in the GEMV's prologue
+        out = gemv(x2, wg, bias, act, rms_eps=float(eps) or 1e-30)
+        out = out.view(*x.shape[:-1], N)
+        return out if dt == torch.float32 else out.to(dt)
     planes = torch.empty((2, M, K), dtype=torch.float16, device=x.device)
     rinv = torch.empty((M,), dtype=torch.float32, device=x.device)
     eln = 14 - math.frexp(math.sqrt(K))[1]
@@ -447,10 +451,163 @@ def sdpa(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: bool = False
     return o if dt == torch.float32 else o.to(dt)
 
 
+# ------------------------------------------------------------------ stateful decoding (decode.hip)
+def _i32_pos(pos: torch.Tensor, B: int) -> torch.Tensor:
+    if pos.dtype != torch.int32 or pos.shape != (B,) or not pos.is_contiguous():
+        raise ValueError(f"positions must be a contiguous i32 [{B}] tensor, got {pos.dtype} {tuple(pos.shape)}")
+    return pos
+
+
+def kv_write(cache: torch.Tensor, x: torch.Tensor, pos: torch.Tensor, rope: tuple | None = None) -> torch.Tensor:
+    """cache[b, pos[b] + s] = x[b, s] in place (rows past the cache dropped);
+    ``rope`` = (cos, sin) fp32 tables: x rotated at those positions first.
+    Returns ``cache``."""
+    from ..podserver.program.reference import kv_write_ref, rotary_at_ref
+
+    if not cache.is_cuda:
+        return kv_write_ref(cache, rotary_at_ref(x, rope[0], rope[1], pos) if rope else x, pos)
+    B, L, H, D = cache.shape
+    S = x.shape[1]
+    if x.shape[0] != B or x.shape[2:] != cache.shape[2:] or not cache.is_contiguous():
+        raise ValueError(f"kv_write: x {tuple(x.shape)} does not fit the cache {tuple(cache.shape)}")
+    try:
+        ldx, bsx = _rows_view(x)
+    except ValueError:
+        x = x.contiguous()
+        ldx, bsx = _rows_view(x)
+    c = s_ = None
+    R = 0
+    if rope is not None:
+        c, s_ = rope[0].float().contiguous(), rope[1].float().contiguous()
+        R = c.shape[0]
+    _lib.check(_lib.lib().nos_kv_write(x.data_ptr(), _bf(x), ldx, bsx, cache.data_ptr(), _bf(cache),
+                                       _i32_pos(pos, B).data_ptr(), _ptr(c), _ptr(s_), R, B, S, H, D, L, _stream()),
+               "nos_kv_write")
+    return cache
+
+
+def rotary_at(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
+    """rotate_half rotary of x [B, S, H, D] at positions pos[b] + s (table rows clamped)."""
+    from ..podserver.program.reference import rotary_at_ref
+
+    if not x.is_cuda:
+        return rotary_at_ref(x, cos, sin, pos)
+    B, S, H, D = x.shape
+    try:
+        ldx, bsx = _rows_view(x)
+    except ValueError:
+        x = x.contiguous()
+        ldx, bsx = _rows_view(x)
+    c, s_ = cos.float().contiguous(), sin.float().contiguous()
+    if c.shape[1] != D or s_.shape != c.shape:
+        raise ValueError(f"rotary tables must be [positions, {D}]")
+    out = torch.empty((B, S, H, D), dtype=x.dtype, device=x.device)
+    _lib.check(_lib.lib().nos_rotary_pos(x.data_ptr(), ldx, bsx, out.data_ptr(), _i32_pos(pos, B).data_ptr(),
+                                         c.data_ptr(), s_.data_ptr(), c.shape[0], B, S, H, D, _bf(x), _stream()),
+               "nos_rotary_pos")
+    return out
+
+
+def sdpa_cache(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos: torch.Tensor, scale: float | None = None,
+               rope: tuple | None = None) -> torch.Tensor:
+    """Query i of sequence b, at position pos[b] + i, attends the cached keys
+    0 .. pos[b] + i: q [B, Sq, H, D], caches [B, L, Hkv, D] (fp32 / bf16).
+    ``rope`` = (cos, sin): q rotated at its positions inside the kernel.  The
+    flash-decoding kernel (decode.hip) for CUDA tensors, fp32 math."""
+    from ..podserver.program.reference import rotary_at_ref, sdpa_cache_ref
+
+    if not q.is_cuda:
+        return sdpa_cache_ref(rotary_at_ref(q, rope[0], rope[1], pos) if rope else q, kc, vc, pos, scale)
+    B, Sq, H, D = q.shape
+    L, Hkv = kc.shape[1], kc.shape[2]
+    if (kc.shape != vc.shape or kc.dtype != vc.dtype or kc.shape[0] != B or kc.shape[3] != D or H % Hkv
+            or D not in (64, 128) or not kc.is_contiguous() or not vc.is_contiguous()):
+        raise ValueError(f"sdpa_cache: q {tuple(q.shape)} vs caches {tuple(kc.shape)}")
+    try:
+        ldq, bsq = _rows_view(q)
+    except ValueError:
+        q = q.contiguous()
+        ldq, bsq = _rows_view(q)
+    c = s_ = None
+    R = 0
+    if rope is not None:
+        c, s_ = rope[0].float().contiguous(), rope[1].float().contiguous()
+        R = c.shape[0]
+    L_ = _lib.lib()
+    nb = int(L_.nos_attn_decode_workspace(B, H, Hkv, Sq, L, D))
+    ws = torch.empty((max(nb, 4) // 4,), dtype=torch.float32, device=q.device)
+    out = torch.empty((B, Sq, H, D), dtype=q.dtype, device=q.device)
+    sc = scale if scale is not None else 1.0 / math.sqrt(D)
+    _lib.check(L_.nos_attn_decode(q.data_ptr(), _bf(q), ldq, bsq, kc.data_ptr(), vc.data_ptr(), _bf(kc),
+                                  _i32_pos(pos, B).data_ptr(), _ptr(c), _ptr(s_), R, out.data_ptr(), _bf(out), B, H,
+                                  Hkv, Sq, L, D, float(sc), ws.data_ptr(), ws.numel() * 4, _stream()),
+               "nos_attn_decode")
+    return out
+
+
+def pos_update(pos: torch.Tensor, add: bool, n: int) -> torch.Tensor:
+    """pos += n (``add``) or pos = n, in place; returns ``pos``."""
+    if not pos.is_cuda:
+        return pos.add_(n) if add else pos.fill_(n)
+    _lib.check(_lib.lib().nos_pos_update(_i32_pos(pos, pos.shape[0]).data_ptr(), pos.shape[0], int(bool(add)), int(n),
+                                         _stream()), "nos_pos_update")
+    return pos
+
+
+def argmax(x: torch.Tensor) -> torch.Tensor:
+    """Index of the maximum over the last dim (first on ties), i32."""
+    if not x.is_cuda:
+        return x.float().argmax(dim=-1).to(torch.int32)
+    L = x.shape[-1]
+    x2 = x.reshape(-1, L)
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    out = torch.empty(x.shape[:-1], dtype=torch.int32, device=x.device)
+    _lib.check(_lib.lib().nos_argmax(x2.data_ptr(), _bf(x2), x2.shape[0], L, x2.stride(0), out.data_ptr(), _stream()),
+               "nos_argmax")
+    return out
+
+
+GEMV_MAX_ROWS = 8
+EPI_SILU = 64  # decode.hip's GEMV: SiLU epilogue
+
+
+def gemv_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
+    """Whether the skinny-GEMM kernel takes this [M, K] x [N, K] product."""
+    M, K = x2.shape
+    return (x2.is_cuda and 0 < M <= GEMV_MAX_ROWS and K % 4 == 0 and M * K * 4 <= 65536 and x2.stride(-1) == 1
+            and w.stride(-1) == 1 and x2.stride(0) % 4 == 0 and w.stride(0) % 4 == 0
+            and x2.dtype in (torch.float32, torch.bfloat16) and w.dtype in (torch.float32, torch.bfloat16)
+            and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+
+
+def gemv(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
+         residual: torch.Tensor | None = None, out: torch.Tensor | None = None, rms_eps: float = 0.0) -> torch.Tensor:
+    """y [M, N] = act(rms(x) [M, K] W^T + b) + R for M <= 8 (:func:`gemv_ok`):
+    the weight-streaming kernel of a decode step, exact fp32 math; y, R in
+    x's dtype, bias in W's.  ``rms_eps`` > 0: x rows RMS-normalised first
+    (RMSNorm folded into the GEMM, gamma in W)."""
+    M, K = x2.shape
+    N = w.shape[0]
+    y = out if out is not None else torch.empty((M, N), dtype=x2.dtype, device=x2.device)
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESID if residual is not None else 0)
+    epi |= {"gelu": EPI_GELU, "relu": EPI_RELU, "silu": EPI_SILU}.get(act or "", 0)
+    b = None if bias is None else bias.to(w.dtype).contiguous()
+    r = None if residual is None else residual.reshape(M, N).to(x2.dtype)
+    if r is not None and r.stride(-1) != 1:
+        r = r.contiguous()
+    if y.dtype != x2.dtype or y.stride(-1) != 1:
+        raise ValueError("gemv: out must be x's dtype with unit inner stride")
+    _lib.check(_lib.lib().nos_gemv(x2.data_ptr(), _bf(x2), x2.stride(0), w.data_ptr(), _bf(w), w.stride(0), _ptr(b),
+                                   _ptr(r), r.stride(0) if r is not None else 0, y.data_ptr(), y.stride(0), M, N, K,
+                                   epi, float(rms_eps), _stream()), "nos_gemv")
+    return y
+
+
 def set_attention_h3g_kvsplit(n: int) -> None:
     """Key splits of :func:`sdpa` (0 = auto: fill the CU slots)."""
     _lib.check(_lib.lib().nos_attn_h3g_set_kvsplit(int(n)), "nos_attn_h3g_set_kvsplit")
 
 
-__all__ = ["conv2d", "matmul", "sdpa", "linear_rms", "embedding", "rmsnorm", "softmax", "rotary", "conv2d_ref",
+__all__ = ["kv_write", "rotary_at", "sdpa_cache", "pos_update", "argmax", "gemv", "gemv_ok", "conv2d", "matmul", "sdpa", "linear_rms", "embedding", "rmsnorm", "softmax", "rotary", "conv2d_ref",
            "sdpa_ref", "rope_ref", "rmsnorm_ref", "linear_rms_ref", "set_attention_h3g_kvsplit", "EPI_BIAS_ROW"]

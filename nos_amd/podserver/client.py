@@ -146,10 +146,12 @@ class PodClient:
                 time.sleep(0.2)
         raise PodServerGone(f"pod server did not come back within {self.reconnect_s} s: {last}")
 
-    def infer(self, x: np.ndarray | None = None, outputs: bool = False) -> tuple[list[np.ndarray], dict]:
+    def infer(self, x: np.ndarray | None = None, outputs: bool | list = False) -> tuple[list[np.ndarray], dict]:
         """One inference on the pod's model; ``x`` replaces the resident input
-        (float32, one of the registered input shapes; without ``x`` the
-        primary shape's resident input runs)."""
+        (one of the registered input shapes; without ``x`` the primary
+        shape's resident input runs).  ``outputs``: return every output
+        (True), none, or those of the listed indices.  A stateful tenant's
+        reply carries its counters (``rep["state"]``, e.g. the position)."""
         req = {"op": "infer", "outputs": outputs}
         if x is None:
             payload = b""
@@ -166,6 +168,34 @@ class PodClient:
             self._reregister()
             rep, data = self._call(req, payload)
         return (P.unpack_arrays(rep["outputs"], data) if outputs else []), rep
+
+    def reset(self) -> dict:
+        """Zero a stateful tenant's state (K / V caches, positions): a new
+        sequence.  Returns the reply (``state``: the counters, now 0)."""
+        return self._call({"op": "reset"})[0]
+
+    def generate(self, prompt: np.ndarray, max_new_tokens: int, next_output: int = -1) -> tuple[np.ndarray, dict]:
+        """Greedy generation on a stateful decoder tenant
+        (models/llama_program.llama_decode_programs): the prompt ids [B, P]
+        go to the prefill variant, then one [B, 1] decode request per new
+        token, each returning only the program's next-ids output
+        (``next_output``).  Returns (ids [B, max_new_tokens], timings: the
+        prefill's and every decode step's round trip in seconds, the server's
+        final counters)."""
+        prompt = np.asarray(prompt)
+        B = prompt.shape[0]
+        t0 = time.monotonic()
+        outs, rep = self.infer(prompt, outputs=[next_output])
+        t1 = time.monotonic()
+        tok = outs[0].reshape(B, -1)[:, -1].astype(np.int32)
+        toks, steps = [tok], []
+        for _ in range(max_new_tokens - 1):
+            s0 = time.monotonic()
+            outs, rep = self.infer(tok.reshape(B, 1), outputs=[next_output])
+            steps.append(time.monotonic() - s0)
+            tok = outs[0].reshape(B, -1)[:, -1].astype(np.int32)
+            toks.append(tok)
+        return np.stack(toks, axis=1), {"prefill_s": t1 - t0, "step_s": steps, "state": rep.get("state")}
 
     def train_step(self, x: np.ndarray, target: np.ndarray) -> dict:
         """One optimisation step of a training tenant on (x, target): the

@@ -30,6 +30,7 @@ class Builder:
         self.inputs: list[dict] = []
         self.params: list[dict] = []
         self.nodes: list[dict] = []
+        self.states: list[dict] = []
         self.chunks: list[bytes] = []
         self.offset = 0
         self._n = 0
@@ -47,6 +48,11 @@ class Builder:
         self.offset += len(raw)
         return name
 
+    def state(self, name: str, shape, dtype: str = "fp32") -> str:
+        """A state buffer (zero at registration, kept across requests)."""
+        self.states.append({"name": name, "shape": list(shape), "dtype": dtype})
+        return name
+
     def op(self, op: str, *inputs: str, out: str | None = None, **attrs) -> str:
         self._n += 1
         out = out or f"%{self._n}"
@@ -55,8 +61,11 @@ class Builder:
         return out
 
     def build(self, outputs: list[str]) -> tuple[dict, bytes]:
-        return ({"format": FORMAT, "name": self.name, "inputs": self.inputs, "params": self.params,
-                 "nodes": self.nodes, "outputs": list(outputs)}, b"".join(self.chunks))
+        prog = {"format": FORMAT, "name": self.name, "inputs": self.inputs, "params": self.params,
+                "nodes": self.nodes, "outputs": list(outputs)}
+        if self.states:
+            prog["state"] = self.states
+        return prog, b"".join(self.chunks)
 
 
 def save_program(prefix: str, program: dict, weights: bytes) -> None:

@@ -9,7 +9,7 @@ import os
 from dataclasses import dataclass, field
 
 from .graph import Program
-from .ir import BINARY, NATIVE_KINDS, NEVER_FOLD, UNARY, ProgramError, torch_dtype
+from .ir import BINARY, NATIVE_KINDS, NEVER_FOLD, STATE_WRITERS, UNARY, ProgramError, torch_dtype
 from .reference import _eager
 
 
@@ -27,13 +27,15 @@ class Lowered:
     passes below turn its nodes into ``self.steps`` (the package docstring
     lists them); :class:`execute.CompiledProgram` adds the executor."""
 
-    def __init__(self, prog: Program, device, params: dict | None = None):
+    def __init__(self, prog: Program, device, params: dict | None = None, state: dict | None = None):
         import torch
 
         self.program = prog
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
         self.consts: dict[str, object] = dict(params) if params is not None else prog.tensors(self.device)
+        # the tenant's state buffers (shared by its variants; updated in place by every run)
+        self.state: dict[str, object] = state if state is not None else prog.state_tensors(self.device)
         self.input_name = prog.inputs[0].name
         self.outputs = list(prog.outputs)
         self.stats: dict[str, int] = {}
@@ -44,6 +46,7 @@ class Lowered:
             # NOS_AMD_SKIP_PASSES=name,...: leave launch-trimming passes out (A/B runs)
             skip = self._skip = set(os.environ.get("NOS_AMD_SKIP_PASSES", "").split(","))
             steps = self._fold_constants(prog)
+            steps = self._lower_static_positions(steps)
             if "add_over_cat" not in skip:
                 steps = self._distribute_add_over_cat(steps)
             if "patchify" not in skip:
@@ -62,6 +65,7 @@ class Lowered:
                 steps = self._fuse_cast_unary(steps)
             steps = self._fuse_qkv_attention(steps)
             steps = self._fuse_rotary_sdpa(steps)
+            steps = self._fuse_rotary_at(steps)
             if "cat_buffer" not in skip:
                 steps = self._cat_into_buffer(steps)
             steps = self._mark_plane_handoffs(steps)
@@ -100,6 +104,48 @@ class Lowered:
         for k in [k for k in self.consts if k not in live]:
             del self.consts[k]
         self.stats["constant_folded"] = folded
+        return steps
+
+    def _lower_static_positions(self, steps: list[_Step]) -> list[_Step]:
+        """Positions the program fixes itself (``pos_set`` and then ``pos_add``
+        by constants) are known at build: a prefill program that starts a
+        sequence (position 0) then needs no cache reads --
+        ``rotary_at`` becomes ``rotary`` on constant table rows, and an
+        ``sdpa_cache`` whose caches were just written from the same keys /
+        values at position 0 (Sq = their S) is causal ``sdpa`` on those keys
+        and values (the flash kernel; the writes stay, for the decode steps
+        after it).  Dynamic positions keep the cache kernels."""
+        by_out = {s.output: s for s in steps}
+        known: dict[str, int] = {}
+        n = 0
+        for s in steps:
+            if s.kind == "pos_set":
+                known[s.output] = int(s.attrs["value"])
+            elif s.kind == "pos_add" and s.inputs[0] in known:
+                known[s.output] = known[s.inputs[0]] + int(s.attrs["n"])
+            elif s.kind == "rotary_at" and s.inputs[3] in known and all(i in self.consts for i in s.inputs[1:3]):
+                p0, S = known[s.inputs[3]], self._shape(s.inputs[0])[1]
+                if p0 + S > self._shape(s.inputs[1])[0]:
+                    continue
+                tabs = []
+                for t in s.inputs[1:3]:
+                    name = f"{t}::rows{p0}:{p0 + S}"
+                    if name not in self.consts:
+                        self.consts[name] = self.consts[t][p0:p0 + S].contiguous()
+                    tabs.append(name)
+                s.kind, s.inputs = "rotary", [s.inputs[0], *tabs]
+                n += 1
+            elif s.kind == "sdpa_cache" and known.get(s.inputs[3]) == 0:
+                wk, wv = by_out.get(s.inputs[1]), by_out.get(s.inputs[2])
+                sq = self._shape(s.inputs[0])[1]
+                if (wk is None or wv is None or wk.kind != "kv_write" or wv.kind != "kv_write"
+                        or wk.inputs[2] != s.inputs[3] or wv.inputs[2] != s.inputs[3]
+                        or self._shape(wk.inputs[1])[1] != sq or self._shape(wv.inputs[1])[1] != sq):
+                    continue
+                s.kind, s.inputs = "sdpa", [s.inputs[0], wk.inputs[1], wv.inputs[1]]
+                s.attrs = {"causal": True, **({"scale": s.attrs["scale"]} if "scale" in s.attrs else {})}
+                n += 1
+        self.stats["static_positions"] = n
         return steps
 
     def _cat_into_buffer(self, steps: list[_Step]) -> list[_Step]:
@@ -745,13 +791,20 @@ class Lowered:
     def _reorder(self, steps: list[_Step]) -> list[_Step]:
         """A fused residual may come from a value defined after the producer:
         re-sort topologically (stable)."""
-        defined = set(self.consts) | {self.input_name}
+        defined = set(self.consts) | {self.input_name} | set(self.state)
+        # an in-place state update waits for every earlier reader of the version it overwrites
+        readers_before = {}
+        for k, s in enumerate(steps):
+            if s.kind in STATE_WRITERS:
+                readers_before[id(s)] = {id(r) for r in steps[:k] if s.inputs[0] in r.inputs}
+        placed: set[int] = set()
         out, pending = [], list(steps)
         while pending:
             for i, s in enumerate(pending):
-                if all(x in defined for x in s.inputs):
+                if all(x in defined for x in s.inputs) and readers_before.get(id(s), set()) <= placed:
                     out.append(s)
                     defined.add(s.output)
+                    placed.add(id(s))
                     pending.pop(i)
                     break
             else:
@@ -802,6 +855,28 @@ class Lowered:
             drop |= {pq.output, pk.output}
             n += 1
         self.stats["rotary_fused"] = n
+        return [s for s in steps if s.output not in drop]
+
+    def _fuse_rotary_at(self, steps: list[_Step]) -> list[_Step]:
+        """A decode step's rotary at the device-side position: the K rotation
+        into its ``kv_write`` (rotated as it is written to the cache) and the Q
+        rotation into ``sdpa_cache`` (rotated as the kernel loads it)."""
+        uses = self._consumers(steps, self.outputs)
+        by_out = {s.output: s for s in steps}
+        drop, n = set(), 0
+        for s in steps:
+            if s.kind not in ("kv_write", "sdpa_cache") or s.attrs.get("rope"):
+                continue
+            slot, pos = (1, s.inputs[2]) if s.kind == "kv_write" else (0, s.inputs[3])
+            r = by_out.get(s.inputs[slot])
+            if (r is None or r.kind != "rotary_at" or uses.get(r.output) != 1 or r.inputs[3] != pos
+                    or not all(i in self.consts for i in r.inputs[1:3])):
+                continue
+            s.inputs = s.inputs[:slot] + [r.inputs[0]] + s.inputs[slot + 1:] + r.inputs[1:3]
+            s.attrs = {**s.attrs, "rope": True}
+            drop.add(r.output)
+            n += 1
+        self.stats["rotary_at_fused"] = n
         return [s for s in steps if s.output not in drop]
 
     def _prep_conv_weights(self, steps: list[_Step]) -> None:
@@ -894,7 +969,7 @@ class Lowered:
         for k, s in enumerate(steps):
             for i in s.inputs:
                 last[i] = k
-        keep = set(self.outputs) | set(self.consts) | {self.input_name}
+        keep = set(self.outputs) | set(self.consts) | {self.input_name} | set(self.state)
         for name, k in last.items():
             if name not in keep:
                 steps[k].release.append(name)

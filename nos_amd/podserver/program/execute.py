@@ -20,6 +20,7 @@ class CompiledProgram(Lowered):
         from ...ops import tenant as T
 
         env = dict(self.consts)
+        env.update(self.state)
         env[self.input_name] = x
         for s in self.steps:
             a = [env[i] for i in s.inputs]
@@ -113,6 +114,17 @@ class CompiledProgram(Lowered):
             elif k == "patches":
                 at = s.attrs
                 y = T.patches(a[0], at["ph"], at["pw"], torch_dtype(at.get("dtype", "fp32")), at.get("hp"), at.get("wp"))
+            elif k == "kv_write":
+                y = T.kv_write(a[0], a[1], a[2], rope=(a[3], a[4]) if s.attrs.get("rope") else None)
+            elif k == "sdpa_cache":
+                y = T.sdpa_cache(a[0], a[1], a[2], a[3], scale=s.attrs.get("scale"),
+                                 rope=(a[4], a[5]) if s.attrs.get("rope") else None)
+            elif k == "rotary_at":
+                y = T.rotary_at(a[0], a[1], a[2], a[3])
+            elif k in ("pos_add", "pos_set"):
+                y = T.pos_update(a[0], add=k == "pos_add", n=int(s.attrs["n" if k == "pos_add" else "value"]))
+            elif k == "argmax":
+                y = T.argmax(a[0])
             elif k == "cat_buffer":  # its GEMM part was written in place; the constant parts at build
                 y = self.aux[s.attrs["buf"]]
                 if env.pop(s.inputs[0] + "::lnp", None) is not None:

@@ -4,7 +4,7 @@ its weights as tensors, and the entry points to the compiler and the eager
 reference."""
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 
@@ -61,11 +61,21 @@ class Program:
     outputs: list[str]
     values: dict[str, Value]
     payload: bytes | memoryview = b""
+    state: dict[str, Value] = field(default_factory=dict)        # persistent buffers (K / V caches, positions)
+    state_root: dict[str, str] = field(default_factory=dict)     # a state's in-place versions -> the state
 
     # ------------------------------------------------------------ accounting
     @property
     def param_bytes(self) -> int:
         return sum(v.nbytes for v in self.params.values())
+
+    @property
+    def state_bytes(self) -> int:
+        return sum(v.nbytes for v in self.state.values())
+
+    def is_state(self, name: str) -> bool:
+        """A state buffer or one of its in-place versions (the same memory)."""
+        return name in self.state or name in self.state_root
 
     @property
     def bytes_estimate(self) -> int:
@@ -114,11 +124,13 @@ class Program:
             if n.output in folded:
                 continue
             ws = _workspace(n, [self.values[i] for i in n.inputs], self.values[n.output], f32_math)
-            live += self.values[n.output].nbytes
+            if not self.is_state(n.output):   # an in-place state update allocates nothing
+                live += self.values[n.output].nbytes
             peak = max(peak, live + ws)
             for i in set(n.inputs):
                 v = self.values[i]
-                if v.kind == "node" and i not in folded and last.get(i) == k and i not in keep:
+                if (v.kind == "node" and i not in folded and last.get(i) == k and i not in keep
+                        and not self.is_state(i)):
                     live -= v.nbytes
         plane_mult = {"h3": 1.0, "x6": 1.5}.get(f32_math, 0.0)
         planes = 0
@@ -132,7 +144,10 @@ class Program:
             src = by_out.get(n.inputs[0])
             if src is not None and src.op in ("layernorm", "rmsnorm"):  # the folded copy + c1 / c2
                 planes += w.nbytes + 8 * w.shape[0]
-        return self.param_bytes + planes + persistent + sum(v.nbytes for v in self.inputs) + 2 * peak
+        # the state (K / V caches, positions) is allocated once, at registration,
+        # and never grows at replay: it counts in full against the slice
+        return (self.param_bytes + planes + persistent + self.state_bytes + sum(v.nbytes for v in self.inputs)
+                + 2 * peak)
 
     # ------------------------------------------------------------ tensors
     def tensors(self, device) -> dict:
@@ -149,6 +164,12 @@ class Program:
                 t = t.view(torch.bfloat16)
             out[name] = t.to(device)
         return out
+
+    def state_tensors(self, device) -> dict:
+        """The state buffers, zero-initialised (a fresh sequence at position 0)."""
+        import torch
+
+        return {k: torch.zeros(v.shape, dtype=torch_dtype(v.dtype), device=device) for k, v in self.state.items()}
 
     def input_tensor(self, device, data: np.ndarray | None = None):
         import torch
@@ -171,18 +192,26 @@ class Program:
         return min(vs) if vs else None
 
     # ------------------------------------------------------------ execution
-    def compile(self, device, params: dict | None = None) -> "CompiledProgram":  # noqa: F821
+    def compile(self, device, params: dict | None = None, state: dict | None = None) -> "CompiledProgram":  # noqa: F821
+        """``state``: the tenant's state tensors (:meth:`state_tensors`), shared
+        by every variant compiled over them; None: fresh zero buffers."""
         from .execute import CompiledProgram
 
-        return CompiledProgram(self, device, params)
+        return CompiledProgram(self, device, params, state)
 
-    def reference(self, x, params: dict | None = None) -> tuple:
+    def reference(self, x, params: dict | None = None, state: dict | None = None) -> tuple:
         """Eager, unfused, fp32 evaluation of the graph on the CPU (the
-        numerics reference: every op in plain PyTorch)."""
+        numerics reference: every op in plain PyTorch).  ``state``: the
+        tenant's state tensors (fp32 / i32 on the CPU), updated in place --
+        pass the same dict to consecutive calls (prefill, then decode steps);
+        None: a fresh zero state, dropped after the call."""
         import torch
 
         ps = params if params is not None else self.tensors("cpu")
         env = {k: t.float().cpu() for k, t in ps.items()}
+        if state is None:
+            state = {k: (t if t.dtype == torch.int32 else t.float()) for k, t in self.state_tensors("cpu").items()}
+        env.update(state)
         env[self.inputs[0].name] = x.cpu() if self.inputs[0].dtype == "i32" else x.float().cpu()
         with torch.no_grad():
             for n in self.nodes:

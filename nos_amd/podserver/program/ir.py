@@ -28,7 +28,7 @@ class Value:
     name: str
     shape: tuple[int, ...]
     dtype: str
-    kind: str                 # "input" | "param" | "node"
+    kind: str                 # "input" | "param" | "state" | "node"
 
     @property
     def numel(self) -> int:
@@ -111,10 +111,20 @@ OPS = ("linear", "layernorm", "attention", *BINARY, *UNARY, "cat", "slice", "res
        # general tenants: conv nets and decoder LLMs (nos_amd/ops/tenant.py)
        "conv2d", "batchnorm", "max_pool2d", "avg_pool2d", "mean", "sum", "matmul", "softmax", "embedding",
        "rmsnorm", "rotary", "sdpa")
-NEVER_FOLD = ("attention", "sdpa")
+# stateful decoding (round 6): ops over state buffers that persist across a
+# tenant's requests (a K / V cache, a position counter).  STATE_WRITERS update
+# their first input IN PLACE and return its new version (the validator makes
+# the old version dead from then on, so in-place equals SSA semantics)
+STATE_OPS = ("kv_write", "sdpa_cache", "rotary_at", "pos_add", "pos_set", "argmax")
+STATE_WRITERS = ("kv_write", "pos_add", "pos_set")
+STATE_DTYPES = ("fp32", "bf16", "i32")
+MAX_STATE = 1024
+OPS = OPS + STATE_OPS
+NEVER_FOLD = ("attention", "sdpa", *STATE_OPS)
 # step kinds that run a gfx950 kernel of libnos_hip.so (CompiledProgram.stats["kernels"])
 NATIVE_KINDS = ("linear", "linear_ln", "linear_rms", "ln_qkv_attention", "attention", "layernorm", "conv2d", "matmul",
-                "softmax", "embedding", "rmsnorm", "rotary", "sdpa", "patches", "unary")
+                "softmax", "embedding", "rmsnorm", "rotary", "sdpa", "patches", "unary", "kv_write", "sdpa_cache",
+                "rotary_at", "pos_add", "pos_set", "argmax")
 GEMM_OPS = ("linear", "conv2d")
 
 

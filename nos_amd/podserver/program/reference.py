@@ -109,7 +109,64 @@ def _eager(op: str, args: list, attrs: dict, ref: bool = False):
         return T.rope_ref(args[0], args[1], args[2])
     if op == "sdpa":
         return T.sdpa_ref(args[0], args[1], args[2], attrs.get("causal", False), attrs.get("scale"))
+    if op == "kv_write":
+        return kv_write_ref(args[0], args[1], args[2])
+    if op == "sdpa_cache":
+        return sdpa_cache_ref(args[0], args[1], args[2], args[3], attrs.get("scale"))
+    if op == "rotary_at":
+        return rotary_at_ref(args[0], args[1], args[2], args[3])
+    if op == "pos_add":
+        return args[0].add_(int(attrs["n"]))
+    if op == "pos_set":
+        return args[0].fill_(int(attrs["value"]))
+    if op == "argmax":
+        return args[0].float().argmax(dim=-1).to(torch.int32)
     raise ProgramError(f"op {op!r}")
+
+
+def kv_write_ref(cache, x, pos):
+    """cache[b, pos[b] + i] = x[b, i] for the rows that fit (in place)."""
+    L, S = cache.shape[1], x.shape[1]
+    for b in range(cache.shape[0]):
+        p0 = int(pos[b])
+        n = max(0, min(S, L - p0))
+        if p0 >= 0 and n:
+            cache[b, p0:p0 + n] = x[b, :n].to(cache.dtype)
+    return cache
+
+
+def sdpa_cache_ref(q, kc, vc, pos, scale=None):
+    """Query i of sequence b at position pos[b] + i attends the cached keys
+    0 .. min(pos[b] + i, L - 1) (fp32 math; grouped-query K / V heads)."""
+    import math
+
+    import torch
+
+    B, Sq, H, D = q.shape
+    L, Hkv = kc.shape[1], kc.shape[2]
+    kf = kc.float().repeat_interleave(H // Hkv, dim=2)
+    vf = vc.float().repeat_interleave(H // Hkv, dim=2)
+    sc = scale if scale is not None else 1.0 / math.sqrt(D)
+    s = torch.einsum("bqhd,bkhd->bhqk", q.float(), kf) * sc
+    qpos = pos.to(torch.long).view(B, 1) + torch.arange(Sq).view(1, Sq)            # [B, Sq]
+    keep = torch.arange(L).view(1, 1, L) <= qpos.clamp(max=L - 1).view(B, Sq, 1)    # [B, Sq, L]
+    s = s.masked_fill(~keep[:, None], float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    return torch.einsum("bhqk,bkhd->bqhd", p, vf).to(q.dtype)
+
+
+def rotary_at_ref(x, cos, sin, pos):
+    """rotate_half rotary of x [B, S, H, D] at positions pos[b] + i (table
+    rows clamped to the table)."""
+    import torch
+
+    B, S, H, D = x.shape
+    idx = (pos.to(torch.long).view(B, 1) + torch.arange(S).view(1, S)).clamp(0, cos.shape[0] - 1)   # [B, S]
+    c = cos.float()[idx][:, :, None, :]
+    sn = sin.float()[idx][:, :, None, :]
+    xf = x.float()
+    rot = torch.cat([-xf[..., D // 2:], xf[..., :D // 2]], dim=-1)
+    return (xf * c + rot * sn).to(x.dtype)
 
 
 def _pair2(attrs: dict, key: str, default: int) -> tuple[int, int]:

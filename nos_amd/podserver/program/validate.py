@@ -6,7 +6,8 @@ from __future__ import annotations
 import math
 
 from .graph import Program
-from .ir import (FLOAT_DTYPES, FORMAT, MAX_NUMEL, MAX_PARAMS, MAX_NODES, MAX_RANK, MAX_VARIANTS, OPS, ACTS, BINARY,
+from .ir import (FLOAT_DTYPES, FORMAT, MAX_NUMEL, MAX_PARAMS, MAX_NODES, MAX_RANK, MAX_STATE, MAX_VARIANTS, OPS,
+                 STATE_DTYPES, STATE_WRITERS, ACTS, BINARY,
                  INTERP_MODES, UNARY, WIRE_DTYPES, Node, ProgramError, Value, _broadcast, _eps, _int, _name,
                  _pair, _req, _shape)
 
@@ -263,7 +264,65 @@ def _infer(node: Node, ins: list[Value], gpu: bool) -> tuple[tuple[int, ...], st
         if gpu:
             _req(q.shape[3] in (64, 128), f"{what}: the attention kernels take head_dim 64 or 128, got {q.shape[3]}")
         return q.shape, dt
+    if op == "kv_write":
+        # cache [B, L, Hkv, D] <- x [B, S, Hkv, D] at rows pos[b] .. pos[b] + S - 1 (rows past L are dropped)
+        only()
+        arity(3, 3)
+        c, x, p = ins
+        _req(len(c.shape) == 4 and c.dtype in FLOAT_DTYPES, f"{what}: the cache must be a float [B, L, Hkv, D] state")
+        _req(len(x.shape) == 4 and x.shape[0] == c.shape[0] and x.shape[2:] == c.shape[2:] and x.dtype == c.dtype
+             and x.shape[1] <= c.shape[1], f"{what}: x must be [{c.shape[0]}, S <= {c.shape[1]}, {c.shape[2]}, "
+             f"{c.shape[3]}] {c.dtype}, got {x.shape} {x.dtype}")
+        _pos_vector(p, c.shape[0], what)
+        return c.shape, c.dtype
+    if op == "sdpa_cache":
+        # q [B, Sq, H, D] at positions pos[b] + i over the cached keys 0 .. pos[b] + i (causal)
+        only("scale")
+        arity(4, 4)
+        q, kc, vc, p = ins
+        _req(len(q.shape) == 4 and len(kc.shape) == 4 and kc.shape == vc.shape and kc.dtype == vc.dtype
+             and q.shape[0] == kc.shape[0] and q.shape[3] == kc.shape[3] and q.shape[2] % kc.shape[2] == 0
+             and q.shape[1] <= kc.shape[1] and q.dtype in FLOAT_DTYPES and kc.dtype in FLOAT_DTYPES,
+             f"{what}: q [B, Sq, H, D], caches [B, L >= Sq, Hkv, D] with H % Hkv == 0 required, got {q.shape}, "
+             f"{kc.shape}")
+        _pos_vector(p, q.shape[0], what)
+        if "scale" in a:
+            _req(isinstance(a["scale"], (int, float)) and not isinstance(a["scale"], bool) and a["scale"] > 0,
+                 f"{what}: scale must be > 0")
+        if gpu:
+            _req(q.shape[3] in (64, 128), f"{what}: the decode attention kernel takes head_dim 64 or 128")
+            _req(q.shape[2] // kc.shape[2] <= 16, f"{what}: at most 16 query heads per K / V head")
+        return q.shape, q.dtype
+    if op == "rotary_at":
+        only()
+        arity(4, 4)
+        x, c, sn, p = ins
+        _req(len(x.shape) == 4 and x.shape[3] % 2 == 0 and x.dtype in FLOAT_DTYPES,
+             f"{what}: x must be [B, S, H, D] with D even")
+        _req(len(c.shape) == 2 and c.shape == sn.shape and c.shape[1] == x.shape[3] and c.dtype == sn.dtype == "fp32",
+             f"{what}: cos / sin must be fp32 [positions, {x.shape[3]}]")
+        _pos_vector(p, x.shape[0], what)
+        return x.shape, x.dtype
+    if op in ("pos_add", "pos_set"):
+        only("n" if op == "pos_add" else "value")
+        arity(1, 1)
+        _req(ins[0].dtype == "i32" and len(ins[0].shape) == 1, f"{what}: takes an i32 [B] position state")
+        v = a.get("n" if op == "pos_add" else "value")
+        _req(isinstance(v, int) and not isinstance(v, bool) and 0 <= v <= 1 << 24,
+             f"{what}: {'n' if op == 'pos_add' else 'value'} must be an int in [0, 2^24]")
+        return ins[0].shape, "i32"
+    if op == "argmax":
+        only("dim")
+        arity(1, 1)
+        _req(a.get("dim", -1) in (-1, len(ins[0].shape) - 1) and len(ins[0].shape) >= 1,
+             f"{what}: argmax runs over the last dim")
+        _req(ins[0].dtype in FLOAT_DTYPES, f"{what}: takes a float tensor")
+        return ins[0].shape[:-1], "i32"
     raise ProgramError(f"{what}: op {op!r} is not one the pod server runs (whitelist: {' '.join(OPS)})")
+
+
+def _pos_vector(p: Value, b: int, what: str) -> None:
+    _req(p.dtype == "i32" and p.shape == (b,), f"{what}: pos must be an i32 [{b}] (a position state), got {p.shape}")
 
 
 
@@ -284,6 +343,8 @@ def parse_variants(objs: list, payload: bytes | memoryview = b"", gpu: bool = Fa
         _req(sig == {k: (v.shape, v.dtype) for k, v in p0.params.items()} and p.param_layout == p0.param_layout,
              f"variant {p.name!r} declares other weights than {p0.name!r}: variants share one weight payload")
         _req(p.inputs[0].dtype == p0.inputs[0].dtype, "variants take the same input dtype")
+        _req({k: (v.shape, v.dtype) for k, v in p.state.items()} == {k: (v.shape, v.dtype) for k, v in p0.state.items()},
+             f"variant {p.name!r} declares other state than {p0.name!r}: variants share one state")
         _req(p.inputs[0].shape not in seen, f"two variants take the input shape {list(p.inputs[0].shape)}")
         seen.add(p.inputs[0].shape)
     return progs
@@ -294,7 +355,7 @@ def parse(obj: dict, payload: bytes | memoryview = b"", gpu: bool = False) -> Pr
     ``gpu``: also check the native kernels' shape constraints."""
     _req(isinstance(obj, dict), "program must be a JSON object")
     _req(obj.get("format") == FORMAT, f"program format must be {FORMAT!r}")
-    extra = set(obj) - {"format", "name", "inputs", "params", "nodes", "outputs", "meta"}
+    extra = set(obj) - {"format", "name", "inputs", "params", "state", "nodes", "outputs", "meta"}
     _req(not extra, f"unknown program keys {sorted(extra)}")
     name = str(obj.get("name", "program"))[:128]
     values: dict[str, Value] = {}
@@ -334,6 +395,21 @@ def parse(obj: dict, payload: bytes | memoryview = b"", gpu: bool = False) -> Pr
     spans.sort()
     for (a0, a1, an), (b0, _b1, bn) in zip(spans, spans[1:]):
         _req(b0 >= a1, f"params {an!r} and {bn!r} overlap in the payload")
+    st = obj.get("state", [])
+    _req(isinstance(st, list) and len(st) <= MAX_STATE, f"state must be a list of at most {MAX_STATE}")
+    state: dict[str, Value] = {}
+    for d in st:
+        _req(isinstance(d, dict) and set(d) <= {"name", "shape", "dtype"}, "a state is {name, shape, dtype}")
+        dt = d.get("dtype", "fp32")
+        _req(dt in STATE_DTYPES, f"state dtype must be one of {STATE_DTYPES}")
+        v = Value(_name(d.get("name"), "state name"), _shape(d.get("shape"), "state shape"), dt, "state")
+        define(v)
+        state[v.name] = v
+    # state versions: root name -> its current version; an in-place writer's
+    # output becomes the current version and the one it consumed is dead
+    current = {k: k for k in state}
+    root_of = {k: k for k in state}
+    dead: set[str] = set()
     ns = obj.get("nodes")
     _req(isinstance(ns, list) and 0 < len(ns) <= MAX_NODES, f"nodes must be a list of 1..{MAX_NODES}")
     nodes = []
@@ -345,15 +421,26 @@ def parse(obj: dict, payload: bytes | memoryview = b"", gpu: bool = False) -> Pr
         _req(isinstance(refs, list) and refs, f"node of op {op}: inputs must be a non-empty list")
         for r in refs:
             _req(isinstance(r, str) and r in values, f"node of op {op}: input {r!r} is not defined before it")
+            _req(r not in dead, f"node of op {op}: state version {r!r} was updated in place before this node "
+                 f"(use {current.get(root_of.get(r, r), r)!r})")
         attrs = d.get("attrs") or {}
         _req(isinstance(attrs, dict), "attrs must be an object")
         n = Node(op, list(refs), _name(d.get("output"), "node output"), dict(attrs))
         shape, dt = _infer(n, [values[r] for r in refs], gpu)
         _req(math.prod(shape) <= MAX_NUMEL, f"node {n.output!r}: output too large")
+        if op in STATE_WRITERS:
+            tgt = refs[0]
+            _req(tgt in root_of, f"node {n.output!r} ({op}): updates a state in place; {tgt!r} is not one")
+            _req(refs.count(tgt) == 1, f"node {n.output!r} ({op}): the updated state cannot also be an operand")
+            dead.add(tgt)
+            root_of[n.output] = root_of[tgt]
+            current[root_of[tgt]] = n.output
         define(Value(n.output, shape, dt, "node"))
         nodes.append(n)
     outs = obj.get("outputs")
     _req(isinstance(outs, list) and outs and all(isinstance(o, str) and o in values for o in outs),
          "outputs must name defined values")
-    return Program(name, inputs, params, layout, nodes, list(outs), values, payload)
+    _req(not any(o in root_of for o in outs), "a state (or a version of one) cannot be an output: it is mutable")
+    return Program(name, inputs, params, layout, nodes, list(outs), values, payload, state=state,
+                   state_root={k: v for k, v in root_of.items() if k != v})
 

@@ -111,6 +111,8 @@ class Tenant:
     id_bound: int | None = None    # token-id input: ids must lie in [0, id_bound)
     alts: dict = field(default_factory=dict)   # other input shapes -> _Variant (same weights)
     trainer: object = None         # a training tenant (training.Trainer): steps instead of inferences
+    state: dict = field(default_factory=dict)       # persistent buffers (K / V caches, positions), every variant's
+    pos_limits: dict = field(default_factory=dict)  # position state -> rows of the caches written at it
 
 
 @dataclass
@@ -129,7 +131,7 @@ class _Variant:
 class _Job:
     tenant: Tenant
     payload: bytes
-    want_outputs: bool
+    want_outputs: bool | list     # True: every output; a list: those output indices
     shape: tuple | None = None
     kind: str = "infer"            # or "train": one optimisation step, payload = input + target
     x_bytes: int = 0
@@ -140,6 +142,7 @@ class _Job:
     t_end: float = 0.0
     outputs: list = field(default_factory=list)
     error: str | None = None
+    state: dict | None = None      # the tenant's counters after the run (stateful tenants)
 
 
 class AdmissionError(RuntimeError):
@@ -149,6 +152,19 @@ class AdmissionError(RuntimeError):
 def _wire_dtype(x) -> str:
     """The element type a tenant's input travels as: "i32" (token ids) or "f32"."""
     return "i32" if str(getattr(x, "dtype", "")) == "torch.int32" else "f32"
+
+
+def _pos_limits(progs) -> dict:
+    """Position state -> the fewest cache rows any ``kv_write`` at it writes
+    (past that the writes are dropped: the server reports the overflow)."""
+    lim: dict[str, int] = {}
+    for p in progs:
+        for n in p.nodes:
+            if n.op == "kv_write":
+                root = p.state_root.get(n.inputs[2], n.inputs[2])
+                rows = p.values[n.inputs[0]].shape[1]
+                lim[root] = min(lim.get(root, rows), rows)
+    return lim
 
 
 def _target_wire(trainer) -> str:
@@ -403,15 +419,28 @@ class PodServer:
                         shp = req.get("shape")
                         shp = tuple(int(d) for d in shp) if isinstance(shp, list) and len(shp) <= 8 else None
                         _check_wire_dtype(req.get("dtype"), _wire_dtype(tenant.x), "input")
-                        job = _Job(tenant, payload, bool(req.get("outputs")), shp)
+                        want = req.get("outputs")
+                        if isinstance(want, list):   # a selection of the program's outputs, by index
+                            if not all(isinstance(i, int) and not isinstance(i, bool) for i in want) or len(want) > 64:
+                                raise ValueError("outputs must be true / false or a list of output indices")
+                        else:
+                            want = bool(want)
+                        job = _Job(tenant, payload, want, shp)
                         self._q.put(job)
                         job.done.wait()
                         if job.error:
                             raise RuntimeError(job.error)
                         descs, out = P.pack_arrays(job.outputs) if job.outputs else ([], b"")
-                        P.send_msg(conn, {"ok": True, "queue_us": round(1e6 * (job.t_start - job.t_enq), 1),
-                                          "gpu_us": round(1e6 * (job.t_end - job.t_start), 1), "outputs": descs},
-                                   out)
+                        rep = {"ok": True, "queue_us": round(1e6 * (job.t_start - job.t_enq), 1),
+                               "gpu_us": round(1e6 * (job.t_end - job.t_start), 1), "outputs": descs}
+                        if job.state is not None:
+                            rep["state"] = job.state
+                        P.send_msg(conn, rep, out)
+                    elif op == "reset":
+                        if tenant is None:
+                            raise AdmissionError("register first")
+                        self._reset_state(tenant)
+                        P.send_msg(conn, {"ok": True, "state": self._counters(tenant)})
                     elif op == "train":
                         if tenant is None or tenant.trainer is None:
                             raise AdmissionError("train needs a training tenant (register with a train spec)")
@@ -553,6 +582,8 @@ class PodServer:
                 if extra:
                     raise AdmissionError("a training tenant takes one input shape (no variants)")
                 prog = PG.parse(req["program"], payload)
+                if prog.state:
+                    raise AdmissionError("a stateful program (K / V caches) cannot be a training tenant")
                 spec = parse_train_spec(req["train"], prog)
                 need = train_bytes_estimate(prog, spec) / 2 ** 30
                 if limit and need > limit:
@@ -575,7 +606,7 @@ class PodServer:
             if progs is not None:
                 # the weights once, every variant's activations, planes and folded copies
                 need = sum(p.bytes_estimate_for(self.kernel_config) for p in progs) / 2 ** 30
-                need -= (len(progs) - 1) * progs[0].param_bytes / 2 ** 30
+                need -= (len(progs) - 1) * (progs[0].param_bytes + progs[0].state_bytes) / 2 ** 30
                 if limit and need > limit:
                     raise AdmissionError(f"tenant needs {need:.2f} GB (static estimate), its slice has {limit} GB")
                 with self._build_lock:
@@ -607,10 +638,12 @@ class PodServer:
         if not self.gpu:
             with torch.no_grad():
                 params = prog.tensors("cpu")
-                built = [(p.compile("cpu", params=params), p.input_tensor("cpu")) for p in progs]
+                state = prog.state_tensors("cpu")
+                built = [(p.compile("cpu", params=params, state=state), p.input_tensor("cpu")) for p in progs]
             m, x = built[0]
             return Tenant(tid, pod, limit, dtype, m, x, program=prog.name, compile_stats=dict(m.stats), cu_mask=mask,
-                          id_bound=prog.id_bound(), alts={tuple(xv.shape): _Variant(mv, xv) for mv, xv in built[1:]})
+                          id_bound=prog.id_bound(), alts={tuple(xv.shape): _Variant(mv, xv) for mv, xv in built[1:]},
+                          state=state, pos_limits=_pos_limits(progs))
         base = torch.cuda.memory_allocated()
         torch.cuda.reset_peak_memory_stats()
         stream = None
@@ -619,7 +652,8 @@ class PodServer:
         try:
             with torch.no_grad(), torch.cuda.stream(self._setup_stream):
                 params = prog.tensors("cuda")
-                built = [(p.compile("cuda", params=params), p.input_tensor("cuda")) for p in progs]
+                state = prog.state_tensors("cuda")   # allocated once: a replay never grows it
+                built = [(p.compile("cuda", params=params, state=state), p.input_tensor("cuda")) for p in progs]
                 del params   # each compiled program holds the weights it reads
             self._setup_stream.synchronize()
             times["compile_ms"] = round(1e3 * (time.monotonic() - t0), 1)
@@ -636,6 +670,11 @@ class PodServer:
                 frac = limit / self.memory_gb if limit and self.memory_gb else 0.5
                 budget_cfg = (kernel_config(frac, os.environ, len(cus)), len(cus))
             variants = [self._capture(m, x, stream, budget_cfg, mask, GraphedTenant) for m, x in built]
+            if state:   # the capture's warm-up runs advanced the state: a fresh sequence at position 0
+                with torch.cuda.stream(self._setup_stream):
+                    for st in state.values():
+                        st.zero_()
+                self._setup_stream.synchronize()
             peak = (torch.cuda.max_memory_allocated() - base) / 2 ** 30
             times["build_ms"] = round(1e3 * (time.monotonic() - t0), 1)
         except Exception:
@@ -648,7 +687,7 @@ class PodServer:
                    outputs=v0.outputs, footprint_gb=round(peak, 3), cu_mask=mask,
                    solo_graph=v0.solo_graph, solo_outputs=v0.solo_outputs,
                    program=prog.name, compile_stats={**v0.model.stats, **times}, id_bound=prog.id_bound(),
-                   alts={tuple(v.x.shape): v for v in variants[1:]})
+                   alts={tuple(v.x.shape): v for v in variants[1:]}, state=state, pos_limits=_pos_limits(progs))
         if limit and peak > limit:
             self._free(t)
             raise AdmissionError(f"tenant needs {peak:.2f} GB, its slice has {limit} GB")
@@ -786,6 +825,7 @@ class PodServer:
         t.outputs = t.solo_outputs = ()
         t.alts = {}
         t.trainer = None
+        t.state = {}
         if t.stream is not None:
             t.stream.close()
             t.stream = None
@@ -897,8 +937,39 @@ class PodServer:
                         v.outputs = outs = v.model(v.x)
                 s.synchronize()
             if job.want_outputs:
-                job.outputs = [o.detach().float().cpu().numpy() for o in outs]
+                sel = outs if job.want_outputs is True else [outs[i] for i in job.want_outputs if -len(outs) <= i < len(outs)]
+                job.outputs = [o.detach().float().cpu().numpy() for o in sel]
+            if t.state:
+                job.state = self._counters(t)
+                for name, rows in t.pos_limits.items():
+                    over = [p for p in job.state.get(name, ()) if p > rows]
+                    if over:
+                        raise RuntimeError(f"context full: position {max(over)} is past the {rows} cache rows "
+                                           f"(state {name!r}); reset the tenant or start a new sequence")
 
+    def _counters(self, t: Tenant) -> dict:
+        """A stateful tenant's small i32 states (its positions), read back
+        after the run the lane has synchronised."""
+        import torch
+
+        return {k: [int(v) for v in st.cpu().tolist()] for k, st in t.state.items()
+                if st.dtype == torch.int32 and st.numel() <= 64}
+
+    def _reset_state(self, t: Tenant) -> None:
+        """Zero a tenant's state (a new sequence at position 0).  Its requests
+        arrive on its one connection, one at a time, so no run of it is in
+        flight; the zeroing runs on its own stream and is waited for."""
+        import torch
+
+        if not self.gpu:
+            for st in t.state.values():
+                st.zero_()
+            return
+        s = t.stream.torch if t.stream is not None else self._setup_stream
+        with torch.cuda.stream(s):
+            for st in t.state.values():
+                st.zero_()
+        s.synchronize()
 
     def _run_trainer(self, job: _Job, lane) -> None:
         """A training tenant's request: one optimisation step (payload =
