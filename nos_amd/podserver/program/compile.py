@@ -27,7 +27,8 @@ class Lowered:
     passes below turn its nodes into ``self.steps`` (the package docstring
     lists them); :class:`execute.CompiledProgram` adds the executor."""
 
-    def __init__(self, prog: Program, device, params: dict | None = None, state: dict | None = None):
+    def __init__(self, prog: Program, device, params: dict | None = None, state: dict | None = None,
+                 derived: dict | None = None):
         import torch
 
         self.program = prog
@@ -36,6 +37,9 @@ class Lowered:
         self.consts: dict[str, object] = dict(params) if params is not None else prog.tensors(self.device)
         # the tenant's state buffers (shared by its variants; updated in place by every run)
         self.state: dict[str, object] = state if state is not None else prog.state_tensors(self.device)
+        # derived constants (folded / merged weights) by recipe and source tensors, shared by
+        # the variants compiled over the same params: one copy per tenant, not per shape
+        self._derived: dict = derived if derived is not None else {}
         self.input_name = prog.inputs[0].name
         self.outputs = list(prog.outputs)
         self.stats: dict[str, int] = {}
@@ -77,6 +81,19 @@ class Lowered:
                 del self.consts[k]
         self.stats["kernels"] = sum(1 for s in self.steps if s.kind in NATIVE_KINDS)
 
+    def _memo(self, tag: str, sources: list, extra, make):
+        """``make()`` once per recipe: ``tag`` + the identities of the source
+        tensors + ``extra`` (hashable).  The sources are held by the cache, so
+        an id is never reused by another tensor while it lives."""
+        import torch
+
+        key = (tag, tuple(id(t) if torch.is_tensor(t) else t for t in sources), extra)
+        hit = self._derived.get(key)
+        if hit is None:
+            hit = (make(), list(sources))
+            self._derived[key] = hit
+        return hit[0]
+
     # ------------------------------------------------------------ passes
     def _fold_constants(self, prog: Program) -> list[_Step]:
         """Run every all-constant node once at load time.  A constant is freed
@@ -92,7 +109,10 @@ class Lowered:
         folded = 0
         for k, n in enumerate(prog.nodes):
             if all(i in self.consts for i in n.inputs) and n.op not in NEVER_FOLD:
-                self.consts[n.output] = _eager(n.op, [self.consts[i] for i in n.inputs], n.attrs).contiguous()
+                srcs = [self.consts[i] for i in n.inputs]
+                self.consts[n.output] = self._memo(
+                    "fold:" + n.op, srcs, repr(sorted(n.attrs.items())),
+                    lambda n=n, srcs=srcs: _eager(n.op, srcs, n.attrs).contiguous())
                 folded += 1
                 for i in set(n.inputs):
                     if last.get(i) == k and i not in keep:
@@ -131,7 +151,8 @@ class Lowered:
                 for t in s.inputs[1:3]:
                     name = f"{t}::rows{p0}:{p0 + S}"
                     if name not in self.consts:
-                        self.consts[name] = self.consts[t][p0:p0 + S].contiguous()
+                        self.consts[name] = self._memo("rows", [self.consts[t]], (p0, S),
+                                                       lambda t=t: self.consts[t][p0:p0 + S].contiguous())
                     tabs.append(name)
                 s.kind, s.inputs = "rotary", [s.inputs[0], *tabs]
                 n += 1
@@ -490,8 +511,12 @@ class Lowered:
             g, be, mu, var = (self.consts[i].float() for i in s.inputs[1:])
             inv = g * torch.rsqrt(var + s.attrs.get("eps", 1e-5))
             base = f"{s.output}::bn"
-            self.consts[base + ".w"] = (w.float() * inv[:, None, None, None]).to(w.dtype).contiguous()
-            self.consts[base + ".b"] = ((b - mu) * inv + be).to(w.dtype).contiguous()
+            eps = s.attrs.get("eps", 1e-5)
+            srcs = [self.consts[i] for i in c.inputs[1:] + s.inputs[1:]]
+            self.consts[base + ".w"], self.consts[base + ".b"] = self._memo(
+                "bn", srcs, eps, lambda w=w, b=b, inv=inv, mu=mu, be=be: (
+                    (w.float() * inv[:, None, None, None]).to(w.dtype).contiguous(),
+                    ((b - mu) * inv + be).to(w.dtype).contiguous()))
             c.inputs = [c.inputs[0], base + ".w", base + ".b"]
             drop.add(c.output)
             c.output = s.output
@@ -539,12 +564,14 @@ class Lowered:
                 continue
             ws = [self.consts[m.inputs[1]] for m in g]
             name = f"{g[0].output}::merged"
-            self.consts[name + ".w"] = torch.cat(ws, dim=0).contiguous()
+            self.consts[name + ".w"] = self._memo("merge.w", ws, None, lambda ws=ws: torch.cat(ws, dim=0).contiguous())
             ins = [x, name + ".w"]
             if any(len(m.inputs) > 2 for m in g):
-                self.consts[name + ".b"] = torch.cat([self.consts[m.inputs[2]] if len(m.inputs) > 2 else
-                                                      torch.zeros(w.shape[0], dtype=w.dtype, device=w.device)
-                                                      for m, w in zip(g, ws)]).contiguous()
+                bs = [self.consts[m.inputs[2]] if len(m.inputs) > 2 else None for m in g]
+                self.consts[name + ".b"] = self._memo(
+                    "merge.b", [*ws, *bs], None, lambda ws=ws, bs=bs: torch.cat(
+                        [bb if bb is not None else torch.zeros(w.shape[0], dtype=w.dtype, device=w.device)
+                         for bb, w in zip(bs, ws)]).contiguous())
                 ins.append(name + ".b")
             new_steps = [_Step("linear", ins, name, {})]
             self._new_shapes[name] = tuple(self._shape(x)[:-1]) + (sum(w.shape[0] for w in ws),)
@@ -623,15 +650,19 @@ class Lowered:
                     if len(run) < 2:
                         continue
                     ws = [self.consts[m.inputs[1]] for _, _, m in run]
-                    nrow, ncol = sum(w.shape[0] for w in ws), sum(w.shape[1] for w in ws)
-                    wbd = torch.zeros((nrow, ncol), dtype=ws[0].dtype, device=ws[0].device)
-                    r = c = 0
-                    for w in ws:
-                        wbd[r:r + w.shape[0], c:c + w.shape[1]] = w
-                        r, c = r + w.shape[0], c + w.shape[1]
+
+                    def blockdiag(ws=ws):
+                        nrow, ncol = sum(w.shape[0] for w in ws), sum(w.shape[1] for w in ws)
+                        wbd = torch.zeros((nrow, ncol), dtype=ws[0].dtype, device=ws[0].device)
+                        r = c = 0
+                        for w in ws:
+                            wbd[r:r + w.shape[0], c:c + w.shape[1]] = w
+                            r, c = r + w.shape[0], c + w.shape[1]
+                        return wbd
+
                     m0 = run[0][2]
                     name = f"{m0.output}::blockdiag"
-                    self.consts[name + ".w"] = wbd
+                    self.consts[name + ".w"] = self._memo("blockdiag.w", ws, None, blockdiag)
                     lo, hi = run[0][0], run[-1][1]
                     new_steps = []
                     src = x
@@ -642,13 +673,14 @@ class Lowered:
                         self._new_dtypes[src] = self._dtype(x)
                     ins = [src, name + ".w"]
                     if any(len(m.inputs) > 2 for _, _, m in run):
-                        self.consts[name + ".b"] = torch.cat(
-                            [self.consts[m.inputs[2]] if len(m.inputs) > 2 else
-                             torch.zeros(w.shape[0], dtype=w.dtype, device=w.device)
-                             for (_, _, m), w in zip(run, ws)]).contiguous()
+                        bs = [self.consts[m.inputs[2]] if len(m.inputs) > 2 else None for _, _, m in run]
+                        self.consts[name + ".b"] = self._memo(
+                            "blockdiag.b", [*ws, *bs], None, lambda ws=ws, bs=bs: torch.cat(
+                                [bb if bb is not None else torch.zeros(w.shape[0], dtype=w.dtype, device=w.device)
+                                 for bb, w in zip(bs, ws)]).contiguous())
                         ins.append(name + ".b")
                     new_steps.append(_Step("linear", ins, name, {}))
-                    self._new_shapes[name] = tuple(self._shape(x)[:-1]) + (nrow,)
+                    self._new_shapes[name] = tuple(self._shape(x)[:-1]) + (sum(w.shape[0] for w in ws),)
                     self._new_dtypes[name] = self._dtype(m0.output)
                     out = name
                     if act is not None:
@@ -704,7 +736,7 @@ class Lowered:
                 continue
             w, b = self.consts[s.inputs[1]], (self.consts[s.inputs[2]] if len(s.inputs) > 2 else None)
             g, be = self.consts[ln.inputs[1]], self.consts[ln.inputs[2]]
-            wg, c1, c2 = ops.fold_layernorm(w, b, g, be)
+            wg, c1, c2 = self._memo("ln", [w, b, g, be], None, lambda w=w, b=b, g=g, be=be: ops.fold_layernorm(w, b, g, be))
             base = f"{s.output}::ln"
             self.consts[base + ".w"], self.consts[base + ".c1"], self.consts[base + ".c2"] = wg, c1, c2
             s.kind = "linear_ln"
@@ -731,7 +763,8 @@ class Lowered:
                 continue
             w, g = self.consts[s.inputs[1]], self.consts[rn.inputs[1]]
             base = f"{s.output}::rms"
-            self.consts[base + ".w"] = (w.float() * g.float()[None, :]).to(w.dtype).contiguous()
+            self.consts[base + ".w"] = self._memo(
+                "rms", [w, g], None, lambda w=w, g=g: (w.float() * g.float()[None, :]).to(w.dtype).contiguous())
             s.kind = "linear_rms"
             s.inputs = [rn.inputs[0], base + ".w"] + s.inputs[2:]
             s.attrs = {"act": s.attrs.get("act"), "eps": rn.attrs.get("eps", 1e-5)}
@@ -892,10 +925,14 @@ class Lowered:
                 continue
             w = self.consts[s.inputs[1]]
             k = w[0].numel()
-            w2 = w.float().reshape(w.shape[0], k)
             kp = -(-k // 32) * 32
             name = s.inputs[1] + "::mat"
-            self.aux[name] = (F.pad(w2, (0, kp - k)) if kp != k else w2).contiguous()
+
+            def mat(w=w, k=k, kp=kp):
+                w2 = w.float().reshape(w.shape[0], k)
+                return (F.pad(w2, (0, kp - k)) if kp != k else w2).contiguous()
+
+            self.aux[name] = self._memo("conv.mat", [w], None, mat)
             s.attrs["w2"] = name
 
     def _mark_plane_handoffs(self, steps: list[_Step]) -> list[_Step]:

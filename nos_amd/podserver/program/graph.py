@@ -144,6 +144,15 @@ class Program:
             src = by_out.get(n.inputs[0])
             if src is not None and src.op in ("layernorm", "rmsnorm"):  # the folded copy + c1 / c2
                 planes += w.nbytes + 8 * w.shape[0]
+        # parallel linears over one activation (Q / K / V, gate / up, heads) are merged into one
+        # weight copy by the compiler (not only the norm-fed ones)
+        readers: dict[str, list] = {}
+        for n in self.nodes:
+            if n.op == "linear" and len(n.inputs) >= 2 and n.inputs[1] in self.params:
+                readers.setdefault(n.inputs[0], []).append(self.values[n.inputs[1]])
+        for ws in readers.values():
+            if len(ws) > 1:
+                planes += sum(w.nbytes + 4 * w.shape[0] for w in ws)
         # the state (K / V caches, positions) is allocated once, at registration,
         # and never grows at replay: it counts in full against the slice
         return (self.param_bytes + planes + persistent + self.state_bytes + sum(v.nbytes for v in self.inputs)
@@ -192,12 +201,15 @@ class Program:
         return min(vs) if vs else None
 
     # ------------------------------------------------------------ execution
-    def compile(self, device, params: dict | None = None, state: dict | None = None) -> "CompiledProgram":  # noqa: F821
+    def compile(self, device, params: dict | None = None, state: dict | None = None,
+                derived: dict | None = None) -> "CompiledProgram":  # noqa: F821
         """``state``: the tenant's state tensors (:meth:`state_tensors`), shared
-        by every variant compiled over them; None: fresh zero buffers."""
+        by every variant compiled over them; None: fresh zero buffers.
+        ``derived``: a dict shared by the variants compiled over the same
+        ``params`` -- their folded / merged weights are then made once."""
         from .execute import CompiledProgram
 
-        return CompiledProgram(self, device, params, state)
+        return CompiledProgram(self, device, params, state, derived)
 
     def reference(self, x, params: dict | None = None, state: dict | None = None) -> tuple:
         """Eager, unfused, fp32 evaluation of the graph on the CPU (the

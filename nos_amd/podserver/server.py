@@ -639,7 +639,10 @@ class PodServer:
             with torch.no_grad():
                 params = prog.tensors("cpu")
                 state = prog.state_tensors("cpu")
-                built = [(p.compile("cpu", params=params, state=state), p.input_tensor("cpu")) for p in progs]
+                derived: dict = {}
+                built = [(p.compile("cpu", params=params, state=state, derived=derived), p.input_tensor("cpu"))
+                         for p in progs]
+                del derived
             m, x = built[0]
             return Tenant(tid, pod, limit, dtype, m, x, program=prog.name, compile_stats=dict(m.stats), cu_mask=mask,
                           id_bound=prog.id_bound(), alts={tuple(xv.shape): _Variant(mv, xv) for mv, xv in built[1:]},
@@ -653,8 +656,10 @@ class PodServer:
             with torch.no_grad(), torch.cuda.stream(self._setup_stream):
                 params = prog.tensors("cuda")
                 state = prog.state_tensors("cuda")   # allocated once: a replay never grows it
-                built = [(p.compile("cuda", params=params, state=state), p.input_tensor("cuda")) for p in progs]
-                del params   # each compiled program holds the weights it reads
+                derived: dict = {}   # folded / merged weights: one copy for all the variants
+                built = [(p.compile("cuda", params=params, state=state, derived=derived), p.input_tensor("cuda"))
+                         for p in progs]
+                del params, derived   # each compiled program holds the weights it reads
             self._setup_stream.synchronize()
             times["compile_ms"] = round(1e3 * (time.monotonic() - t0), 1)
             budget_cfg = None

@@ -233,3 +233,19 @@ def test_reference_equals_hf_forward_logits(model, tenant):
         hf = model(torch.from_numpy(prompt.astype(np.int64))).logits[:, -1:]
     torch.testing.assert_close(logits, hf, rtol=1e-4, atol=1e-4)
     assert int(state["pos"][0]) == 8 and int(nxt.reshape(-1)[0]) == int(hf.argmax(-1).reshape(-1)[0])
+
+
+def test_variants_share_their_folded_and_merged_weights(tenant):
+    """shape variants over one weight payload make ONE copy of
+    each derived constant (RMSNorm-folded, Q / K / V and gate / up merged
+    weights), not one per variant."""
+    progs, w = tenant
+    ps = PG.parse_variants(progs, w)
+    params, state, derived = ps[0].tensors("cpu"), ps[0].state_tensors("cpu"), {}
+    cps = [p.compile("cpu", params=params, state=state, derived=derived) for p in ps]
+
+    def derived_ids(c):
+        return {id(v) for k, v in c.consts.items() if "::" in k and ("merged" in k or "rms" in k)}
+
+    a, b, e = (derived_ids(c) for c in cps)
+    assert a and b == e and b <= a     # the decode / extend variants reuse the prefill's tensors

@@ -50,6 +50,13 @@ def make(kind: str, dtype: str, seed: int):
             progs = [llama_program(m, s_, rope_len=512, dtype=dtype) for s_ in (512, 256, 128)]
             _CACHE["llama-var"] = (progs[0][0], progs[0][1], [p for p, _ in progs[1:]])
         return _CACHE["llama-var"]
+    if kind == "llama-dec":  # that decoder as a STATEFUL generation tenant: 128-token prompts, 1024-row K / V caches
+        if "llama-dec" not in _CACHE:
+            from nos_amd.models.llama_program import llama_config, llama_decode_programs, llama_model
+
+            progs, w = llama_decode_programs(llama_model(llama_config(True), 0), 128, 1024, dtype=dtype)
+            _CACHE["llama-dec"] = (progs[0], w, progs[1:])
+        return _CACHE["llama-dec"]
     if kind == "llama-ft":  # the same decoder as a TRAINING tenant (next-token cross entropy, AdamW)
         return make("llama", "fp32", seed)
     if kind == "llama":  # a random-init Llama decoder (1024 hidden, 8 layers, head_dim 128, GQA) at seq 512
@@ -59,6 +66,15 @@ def make(kind: str, dtype: str, seed: int):
             _CACHE["llama"] = llama_tenant(dtype, 0)
         return _CACHE["llama"]
     raise SystemExit(f"unknown tenant kind {kind!r}")
+
+
+def _lat_summary(lat, kinds, w0: float, w1: float) -> dict | None:
+    """Per-token round trips of the decode tenants inside the window."""
+    xs = sorted(d for i, ls in enumerate(lat) if kinds[i] == "llama-dec" for t, d in ls if w0 <= t < w1)
+    if not xs:
+        return None
+    q = lambda f: round(1e3 * xs[min(len(xs) - 1, int(f * len(xs)))], 3)  # noqa: E731
+    return {"tokens": len(xs), "mean": round(1e3 * sum(xs) / len(xs), 3), "p50": q(0.5), "p90": q(0.9), "p99": q(0.99)}
 
 
 def main() -> None:
@@ -79,7 +95,8 @@ def main() -> None:
                     "yolos:20,bert:4,mlp:4 (bert = BERT-base-shaped fp32 encoder at seq 512, mlp = bf16 GEMM-MLP "
                     "probe, resnet = ResNet-18 at 224x224, llama = Llama decoder at seq 512, llama-ft = that decoder "
                     "fine-tuned in the server: a training tenant, its rate in optimisation steps/s; llama-var = that "
-                    "decoder registered at seq 512 / 256 / 128, requests cycling through the three shapes); per-kind "
+                    "decoder registered at seq 512 / 256 / 128, requests cycling through the three shapes; llama-dec = "
+                    "that decoder generating token by token over its K / V cache: prefill 128, decode to 1024); per-kind "
                     "rates in the output")
     a = ap.parse_args()
     kinds = ([k for spec in a.mix.split(",") for k in [spec.split(":")[0]] * int(spec.split(":")[1])]
@@ -128,8 +145,28 @@ def main() -> None:
         stop = threading.Event()
         marks: list[list[float]] = [[] for _ in clients]
 
+        lat: list[list[float]] = [[] for _ in clients]   # decode tenants: per-token round trips
+
         def loop(i: int) -> None:
             k = 0
+            if kinds[i] == "llama-dec":   # generation: a prompt, then one token per request until the cache fills
+                import numpy as np
+
+                g = np.random.default_rng(i)
+                while not stop.is_set():
+                    outs, _ = clients[i].infer(g.integers(0, 32000, (1, 128)).astype(np.int32), outputs=[1])
+                    tok = outs[0].reshape(1, 1).astype(np.int32)
+                    marks[i].append(time.monotonic())
+                    for _ in range(1024 - 128 - 1):
+                        if stop.is_set():
+                            break
+                        t0 = time.monotonic()
+                        outs, _ = clients[i].infer(tok, outputs=[1])
+                        t1 = time.monotonic()
+                        tok = outs[0].reshape(1, 1).astype(np.int32)
+                        marks[i].append(t1)
+                        lat[i].append((t0, t1 - t0))
+                return
             while not stop.is_set():
                 if i in batches:
                     clients[i].train_step(*batches[i])
@@ -166,6 +203,7 @@ def main() -> None:
             c.close()
         print(json.dumps({"tenants": a.tenants, "lanes": a.lanes, "window_s": round(w1 - w0, 3),
                           "build_s": round(build_s, 1), "programs_s": round(t_built - t0, 1),
+                          "decode_token_latency_ms": _lat_summary(lat, kinds, w0, w1),
                           "per_kind": {k: {"tenants": kinds.count(k),
                                            "inf_per_s": round(sum(d for d, kk in zip(done, kinds) if kk == k)
                                                               / (w1 - w0), 2),
