@@ -21,6 +21,8 @@
 //  * epilogue: scales, bias, GELU / ReLU, residual, and optionally the K / V
 //    columns of a fused QKV projection as the attention's fp16 planes
 //    (KvOut: attention_f32x.hip's h3 kernel reads them).
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "common.h"
@@ -28,7 +30,11 @@
 
 namespace {
 
-enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8, EPI_BIAS_ROW = 16, EPI_RESID_PRE = 32 };
+enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8, EPI_BIAS_ROW = 16, EPI_RESID_PRE = 32,
+             EPI_WIDE = 128 };
+// EPI_WIDE (set by the host, stripped on entry): interior tiles written as
+// fp16 planes go through LDS and leave as 16-byte row stores (8 per plane
+// row chunk) instead of one 2-byte store per element and plane
 template <int E>
 using EpiC = std::integral_constant<int, E>;
 // EPI_RESID adds R after the activation (transformer residuals); EPI_RESID_PRE
@@ -162,6 +168,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int c0 = lane & 31, h0 = lane >> 5;
   const int wm = wid / WGN, wn = wid % WGN;
+  const bool wide = (epi & EPI_WIDE) != 0;
+  epi &= ~EPI_WIDE;
   const int ntiles1 = tiles_m * tiles_n, ntiles = BATCHED ? ntiles1 * bt.nb : ntiles1;
   const int nk = K / BKT;
   nos::XcdChunk chunk;
@@ -530,6 +538,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
           lo_off = kv.hd;
           ld = 4 * kv.hd;
         }
+        // wide: the tile's two planes in LDS (the ring is free: every wave passed the
+        // K loop's last barrier), 16-byte chunks XOR-swizzled by row, then each
+        // thread stores whole 16-byte row chunks of both planes
+        constexpr bool WIDE_FITS = 4 * BM * BN <= RS * STAGE && !BATCHED && BN == 128;
+        unsigned short* const T = reinterpret_cast<unsigned short*>(smem);
   #pragma unroll
         for (int j = 0; j < NI; ++j) {
           const int cl = wn * (BN / WGN) + j * 32 + c;
@@ -547,10 +560,29 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
               const float x = v * osc;
               const _Float16 h0 = (_Float16)x;
               const _Float16 h1 = (_Float16)(x - (float)h0);
-              const unsigned off = (unsigned)(rl * ld + cl);
-              hi[off] = __builtin_bit_cast(unsigned short, h0);
-              hi[lo_off + off] = __builtin_bit_cast(unsigned short, h1);
+              if (WIDE_FITS && wide) {
+                const int sl = rl * BN + ((((cl >> 3) ^ (rl & 15)) << 3) | (cl & 7));
+                T[sl] = __builtin_bit_cast(unsigned short, h0);
+                T[BM * BN + sl] = __builtin_bit_cast(unsigned short, h1);
+              } else {
+                const unsigned off = (unsigned)(rl * ld + cl);
+                hi[off] = __builtin_bit_cast(unsigned short, h0);
+                hi[lo_off + off] = __builtin_bit_cast(unsigned short, h1);
+              }
             }
+          }
+        }
+        if (WIDE_FITS && wide) {
+          __syncthreads();
+          constexpr int CPR = BN / 8;                     // 16-byte chunks per tile row
+          constexpr int NCH = 2 * BM * CPR;               // both planes
+  #pragma unroll
+          for (int q = 0; q < NCH / (64 * NW); ++q) {
+            const int id = tid + q * 64 * NW;
+            const int pl = id / (BM * CPR), rem = id - pl * (BM * CPR);
+            const int row = rem / CPR, ch = rem - row * CPR;
+            const uint4 v = *reinterpret_cast<const uint4*>(T + pl * BM * BN + row * BN + ((ch ^ (row & 15)) << 3));
+            *reinterpret_cast<uint4*>(hi + pl * lo_off + (long long)row * ld + ch * 8) = v;
           }
         }
         return true;
@@ -648,6 +680,23 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   }  // tiles
 }
 
+// LDS-staged 16-byte plane stores (EPI_WIDE) for the interior tiles of GEMMs
+// that write fp16 planes (fc1 -> fc2, the QKV projection's K / V);
+// NOS_AMD_H3_WIDE_PLANES=0 keeps the 2-byte stores (A/B runs)
+bool g_wide_planes = [] {
+  const char* e = getenv("NOS_AMD_H3_WIDE_PLANES");
+  return e == nullptr || atoi(e) != 0;
+}();
+
+// the plane destinations of EPI_WIDE take 16-byte stores at every tile's rows
+bool wide_planes_ok(const KvOut& kv, const PlaneOut& po) {
+  if (!g_wide_planes) return false;
+  if (po.p != nullptr)
+    return !(((uintptr_t)po.p) & 15) && !(po.ldp % 8) && !(po.pplane % 8);
+  if (kv.kvs != nullptr) return !(((uintptr_t)kv.kvs) & 15) && !(kv.hd % 8) && !(kv.qcols % 8);
+  return false;
+}
+
 template <int BM, int BN, int WGM, int WGN, int BKT = 32, int RS = 2, bool BATCHED = false, int MODE = 0>
 int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, float rconst, const _Float16* Wp,
              int ldw, long long wplane, const float* csc, const float* bias, const float* R, int ldr, float* C, int ldc,
@@ -657,6 +706,7 @@ int launch_t(const _Float16* Ap, int lda, long long aplane, const float* rinv, f
   if (ntiles > (1LL << 30)) return (int)hipErrorInvalidValue;
   const size_t lds = RS * (size_t)(2 * BM * BKT * 2 + 2 * BN * BKT * 2);
   constexpr int NT = 64 * WGM * WGN;
+  if (!BATCHED && wide_planes_ok(kv, po)) epi |= EPI_WIDE;
   // batched GEMMs always launch one workgroup per tile: their persistent
   // form (a CU slice's capped grid) needs 21 more VGPRs than 256 and spilled
   // to scratch; the CU mask bounds where the tiles run either way

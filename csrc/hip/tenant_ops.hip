@@ -146,6 +146,28 @@ __global__ __launch_bounds__(256) void unary_kernel(const void* __restrict__ x, 
   st_from_f32(y, i, r, ybf);
 }
 
+// ------------------------------------------------------------------ gated unit
+// y[m, n] = f(a[m, n]) * b[m, n] (SwiGLU's silu(gate) * up; the op codes of
+// unary_kernel): a / b rows at their own strides (the two column halves of a
+// merged gate-up GEMM), y [M, N] contiguous; one pass, f in fp32
+__global__ __launch_bounds__(256) void glu_kernel(const void* __restrict__ a, int lda, const void* __restrict__ b,
+                                                  int ldb, void* __restrict__ y, long long M, int N, int op, int bf) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= M * N) return;
+  const long long m = i / N;
+  const int n = (int)(i - m * N);
+  const float v = ld_as_f32(a, m * lda + n, bf), u = ld_as_f32(b, m * ldb + n, bf);
+  float r;
+  switch (op) {
+    case 1: r = fmaxf(v, 0.f); break;
+    case 2: r = 1.f / (1.f + expf(-v)); break;
+    case 3: r = v / (1.f + expf(-v)); break;
+    case 4: r = 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); break;
+    default: r = v;
+  }
+  st_from_f32(y, i, r * u, bf);
+}
+
 // ------------------------------------------------------------------ conv2d im2col -> h3 planes
 // The patches of one NCHW image as the B operand of the h3 GEMM
 // out[n][oc][p] = sum_k W[oc][k] patch[n][p][k] (k = (c, kh, kw), torch's
@@ -299,5 +321,15 @@ NOS_API int nos_unary(const void* x, int xbf16, void* y, int ybf16, long long n,
   if (n <= 0 || op < 0 || op > 7 || (xbf16 != 0 && xbf16 != 1) || (ybf16 != 0 && ybf16 != 1))
     return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(unary_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, xbf16, y, ybf16, n, op);
+  return (int)hipGetLastError();
+}
+
+NOS_API int nos_glu(const void* a, int lda, const void* b, int ldb, void* y, long long M, int N, int op, int bf16,
+                    hipStream_t stream) {
+  if (!a || !b || !y || M <= 0 || N <= 0 || lda < N || ldb < N || op < 0 || op > 4 || (bf16 != 0 && bf16 != 1))
+    return (int)hipErrorInvalidValue;
+  const long long n = M * N;
+  hipLaunchKernelGGL(glu_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a, lda, b, ldb, y, M, N, op,
+                     bf16);
   return (int)hipGetLastError();
 }

@@ -173,6 +173,31 @@ def unary(x: torch.Tensor, op: str, dtype: torch.dtype) -> torch.Tensor:
     return out
 
 
+def glu(a: torch.Tensor, b: torch.Tensor, op: str = "silu") -> torch.Tensor:
+    """f(a) * b in one pass (SwiGLU: silu(gate) * up), a and b of one shape
+    and dtype; rows of a and b may be strided (column slices of one GEMM)."""
+    f = {"relu": F.relu, "sigmoid": torch.sigmoid, "silu": F.silu, "gelu": F.gelu}[op]
+    if not a.is_cuda or a.shape != b.shape or a.dtype != b.dtype or a.dtype not in (torch.float32, torch.bfloat16):
+        return (f(a.float()) * b.float()).to(a.dtype)
+    N = a.shape[-1]
+
+    def rows(t):
+        t2 = t.reshape(-1, N) if t.is_contiguous() else None
+        if t2 is None:
+            try:
+                t2 = t.view(-1, N)
+            except RuntimeError:
+                t2 = t.contiguous().view(-1, N)
+        return t2 if t2.stride(-1) == 1 else t2.contiguous()
+
+    a2, b2 = rows(a), rows(b)
+    out = torch.empty(a.shape, dtype=a.dtype, device=a.device)
+    if out.numel():
+        _lib.check(_lib.lib().nos_glu(a2.data_ptr(), a2.stride(0), b2.data_ptr(), b2.stride(0), out.data_ptr(),
+                                      a2.shape[0], N, UNARY_CODES[op], _bf(a), _stream()), "nos_glu")
+    return out
+
+
 def softmax(x: torch.Tensor) -> torch.Tensor:
     """softmax over the last dim."""
     if not x.is_cuda:
@@ -609,5 +634,5 @@ def set_attention_h3g_kvsplit(n: int) -> None:
     _lib.check(_lib.lib().nos_attn_h3g_set_kvsplit(int(n)), "nos_attn_h3g_set_kvsplit")
 
 
-__all__ = ["kv_write", "rotary_at", "sdpa_cache", "pos_update", "argmax", "gemv", "gemv_ok", "conv2d", "matmul", "sdpa", "linear_rms", "embedding", "rmsnorm", "softmax", "rotary", "conv2d_ref",
+__all__ = ["glu", "kv_write", "rotary_at", "sdpa_cache", "pos_update", "argmax", "gemv", "gemv_ok", "conv2d", "matmul", "sdpa", "linear_rms", "embedding", "rmsnorm", "softmax", "rotary", "conv2d_ref",
            "sdpa_ref", "rope_ref", "rmsnorm_ref", "linear_rms_ref", "set_attention_h3g_kvsplit", "EPI_BIAS_ROW"]

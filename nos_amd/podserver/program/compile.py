@@ -298,7 +298,35 @@ class Lowered:
             s.kind, s.inputs, s.attrs = "unary", [src], {"op": act, "dtype": dt}
             n += 1
         self.stats["cast_unary_fused"] = n
-        return [s for s in steps if id(s) not in drop]
+        steps = [s for s in steps if id(s) not in drop]
+        # gated units: mul(act(a), b) (SwiGLU's silu(gate) * up) -> ONE glu pass
+        uses = self._consumers(steps, self.outputs)
+        by_out = {s.output: s for s in steps}
+        drop, g = set(), 0
+        for s in steps:
+            if s.kind != "mul":
+                continue
+            for ia, ib in ((0, 1), (1, 0)):
+                p = by_out.get(s.inputs[ia])
+                if (p is not None and p.kind in ("silu", "gelu", "relu", "sigmoid") and uses.get(p.output) == 1
+                        and p.output not in self.outputs and id(p) not in drop
+                        and tuple(self._shape(p.inputs[0])) == tuple(self._shape(s.inputs[ib])) == tuple(self._shape(s.output))
+                        and self._dtype(p.inputs[0]) == self._dtype(s.inputs[ib]) in ("fp32", "bf16")):
+                    drop.add(id(p))
+                    s.kind, s.inputs, s.attrs = "glu", [p.inputs[0], s.inputs[ib]], {"op": p.kind}
+                    g += 1
+                    break
+        self.stats["glu_fused"] = g
+        steps = [s for s in steps if id(s) not in drop]
+        # every other standalone activation on its native pass (no at::native kernel per replay)
+        u = 0
+        for s in steps:
+            if s.kind in UNARY_CODES and self._dtype(s.inputs[0]) in ("fp32", "bf16"):
+                s.attrs = {"op": s.kind, "dtype": self._dtype(s.output)}
+                s.kind = "unary"
+                u += 1
+        self.stats["unary_native"] = u
+        return steps
 
     def _fuse_cast_relayout(self, steps: list[_Step]) -> list[_Step]:
         """cast -> reshape / permute chain (each value read once) -> ONE

@@ -114,6 +114,8 @@ class CompiledProgram(Lowered):
             elif k == "patches":
                 at = s.attrs
                 y = T.patches(a[0], at["ph"], at["pw"], torch_dtype(at.get("dtype", "fp32")), at.get("hp"), at.get("wp"))
+            elif k == "glu":
+                y = T.glu(a[0], a[1], s.attrs["op"])
             elif k == "kv_write":
                 y = T.kv_write(a[0], a[1], a[2], rope=(a[3], a[4]) if s.attrs.get("rope") else None)
             elif k == "sdpa_cache":

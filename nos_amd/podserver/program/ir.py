@@ -124,7 +124,7 @@ NEVER_FOLD = ("attention", "sdpa", *STATE_OPS)
 # step kinds that run a gfx950 kernel of libnos_hip.so (CompiledProgram.stats["kernels"])
 NATIVE_KINDS = ("linear", "linear_ln", "linear_rms", "ln_qkv_attention", "attention", "layernorm", "conv2d", "matmul",
                 "softmax", "embedding", "rmsnorm", "rotary", "sdpa", "patches", "unary", "kv_write", "sdpa_cache",
-                "rotary_at", "pos_add", "pos_set", "argmax")
+                "rotary_at", "pos_add", "pos_set", "argmax", "glu")
 GEMM_OPS = ("linear", "conv2d")
 
 
