@@ -116,6 +116,9 @@ def parse_args(argv=None):
     ap.add_argument("--tenant-mix", default="", metavar="FAMILY:N,...",
                     help="server mode: a mixed fleet of model families, e.g. yolos:16,resnet:6,llama:6 "
                          "(pods of the other families ship prebuilt programs; per-family throughput in 'mix')")
+    ap.add_argument("--isolate-team-b", action="store_true",
+                    help="with --quota --composed: team-b's tenants on an isolated CU pool (cuPolicy split), "
+                         "measured alone and while team-a bursts on the shared pool")
     ap.add_argument("--composed", action="store_true",
                     help="with --quota: BASELINE config 5 composed -- DP trainer pods, bursty team-a waves, a "
                          "simulated amdpart repartition, then preemption (quotabench.ComposedScenario)")
@@ -581,9 +584,24 @@ def run_quota(args) -> int:
             finally:
                 c.close()
 
+        def part_env(key: str) -> dict:
+            """A pod of the (simulated) repartitioned node as a real tenant of
+            this GPU's pod server: an allocation record of a 2 GB slice on the
+            shared CUs, as the device plugin writes one, and its pod env."""
+            from nos_amd.api import constants as C
+            from nos_amd.podserver.allocations import AllocationStore, new_token, socket_path
+
+            tok = new_token()
+            AllocationStore(args.pod_server_dir).write(0, tok, {"memory_gb": 2, "cu_mask": None,
+                                                                "device_ids": [f"part::{key}"], "owner": key,
+                                                                "resource": "partition"})
+            return {C.ENV_POD_SERVER: str(socket_path(args.pod_server_dir, 0)), C.ENV_POD_TOKEN: tok,
+                    C.ENV_MEMORY_LIMIT_GB: "2"}
+
         # 36 GB of the GPU for the trainer pod, the rest in 10 GB tenant slices
         sc = composed_for(1, args.pods_per_gpu or 25, args.slice_gb or 10, pod_server_dir=args.pod_server_dir,
-                          live=True, server_stats=server_stats)
+                          live=True, server_stats=server_stats, isolate_team_b=args.isolate_team_b,
+                          part_tenants=None if args.isolate_team_b else part_env)
     else:
         sc = scenario_for(slices, args.slice_gb or 10, pod_server_dir=args.pod_server_dir, live=True)
     sampler = None

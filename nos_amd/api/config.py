@@ -95,8 +95,13 @@ class GpuPartitionerConfig(ControllerManagerSpec):
     amd_gpu_resource_memory_gb: int = Field(C.DEFAULT_AMD_GPU_RESOURCE_MEMORY_GB, alias="amdGpuResourceMemoryGB")
     # new: CU-mask slice placement over a node's GPUs ("pack" = reference first-fit, "spread")
     slice_placement: str = Field("pack", alias="slicePlacement")
-    # new: CU-mask layout of a GPU's slices in the device plugin ("even" | "proportional" | "shared")
+    # new: CU-mask layout of a GPU's slices in the device plugin ("even" | "proportional" | "shared" |
+    # "split": slices of ``isolatedProfiles`` get proportional masks inside ``isolatedCuSlots`` CU slots
+    # per XCD reserved for them, every other slice shares the remaining slots -- an isolated pool and a
+    # shared pool on one GPU)
     cu_policy: str = Field("proportional", alias="cuPolicy")
+    isolated_profiles: list[str] = Field(default_factory=list, alias="isolatedProfiles")
+    isolated_cu_slots: int = Field(0, alias="isolatedCuSlots")
     # amdpart anti-starvation: whole (SPX) GPUs per node never split for fractional pods
     reserve_whole_gpus: int = Field(0, alias="reserveWholeGpus")
     # NPS mode the planner asks for when a geometry exists in several memory modes
@@ -118,8 +123,10 @@ class GpuPartitionerConfig(ControllerManagerSpec):
             raise ValueError("devicePluginDelaySeconds must be greater than 0")
         if self.slice_placement not in ("pack", "spread", "measured"):
             raise ValueError("slicePlacement must be 'pack', 'spread' or 'measured'")
-        if self.cu_policy not in ("even", "proportional", "shared"):
-            raise ValueError("cuPolicy must be 'even', 'proportional' or 'shared'")
+        if self.cu_policy not in ("even", "proportional", "shared", "split"):
+            raise ValueError("cuPolicy must be 'even', 'proportional', 'shared' or 'split'")
+        if self.cu_policy == "split" and not (self.isolated_profiles and 0 < self.isolated_cu_slots < 32):
+            raise ValueError("cuPolicy split needs isolatedProfiles and 0 < isolatedCuSlots < 32")
 
     def with_defaults(self) -> "GpuPartitionerConfig":
         """Default the device-plugin ConfigMap name/namespace when missing

@@ -32,7 +32,8 @@ def build(api, cfg):
     cs = ClusterState()
     ref = DevicePluginConfigRef(cfg.device_plugin_config_map.name, cfg.device_plugin_config_map.namespace)
     amd = amdpart_strategy(api, None, cfg.reserve_whole_gpus, cfg.preferred_memory_mode)
-    cum = cumask_strategy(api, ref, cfg.device_plugin_delay_seconds, None, cfg.cu_policy, cfg.slice_placement)
+    cum = cumask_strategy(api, ref, cfg.device_plugin_delay_seconds, None, cfg.cu_policy, cfg.slice_placement,
+                          {"isolatedProfiles": cfg.isolated_profiles, "isolatedCuSlots": cfg.isolated_cu_slots})
     hyb = hybrid_strategy(api, ref, cfg.device_plugin_delay_seconds, None)
     mgr = common.manager_for(api, "nos-gpupartitioner", cfg)
     mgr.add(NodeController(api, cs, amd.initializer).controller())

@@ -48,7 +48,7 @@ from ..api import constants as C
 from ..gpu.amdpart import partition_profile
 from ..gpu.amdsmi import AmdSmi, GpuInfo
 from ..gpu.kfd import max_concurrent_processes
-from ..gpu.topology import MI355X_CUS_PER_XCD, MI355X_MEMORY_GB, MI355X_XCDS, CUSlotSet, layout_slots, logical_cu
+from ..gpu.topology import MI355X_CUS_PER_XCD, MI355X_MEMORY_GB, MI355X_XCDS, CUSlotSet, layout_slots, layout_split, logical_cu
 from ..ops.streams import mask_hex
 from ..partitioning import scoring
 
@@ -309,8 +309,15 @@ class NosAmdDevicePlugin:
             xcds, per_xcd = _cu_geometry(g)
             keep = {d.id: self.cu_slots[d.id].slots for d in devs if d.id in self.allocated and d.id in self.cu_slots}
             live = [d for d in devs if d.healthy or d.id in keep]
-            got, bad = layout_slots([(d.id, d.memory_gb) for d in live], keep, self.cu_policy,
-                                    g.memory_gb if g else MI355X_MEMORY_GB, per_xcd)
+            cfg = self.config or {}
+            if self.cu_policy == "split":   # an isolated pool for some profiles, a shared pool for the rest
+                iso = {int(str(p).rstrip("gb")) for p in cfg.get("isolatedProfiles", []) if str(p).rstrip("gb").isdigit()}
+                got, bad = layout_split([(d.id, d.memory_gb) for d in live], keep, iso,
+                                        int(cfg.get("isolatedCuSlots", 0)) * per_xcd // 32,
+                                        g.memory_gb if g else MI355X_MEMORY_GB, per_xcd)
+            else:
+                got, bad = layout_slots([(d.id, d.memory_gb) for d in live], keep, self.cu_policy,
+                                        g.memory_gb if g else MI355X_MEMORY_GB, per_xcd)
             for did, sl in got.items():
                 slots[did] = CUSlotSet(sl, xcds)
             for did in bad:

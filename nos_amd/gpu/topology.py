@@ -129,6 +129,41 @@ def slot_wants(replicas: list[tuple[str, int]], policy: str, gpu_memory_gb: int,
     raise ValueError(f"unknown CU slot policy {policy!r} (one of {SLOT_POLICIES})")
 
 
+def layout_split(replicas: list[tuple[str, int]], keep: dict[str, frozenset], isolated_gb: set[int],
+                 reserved: int, gpu_memory_gb: int, cus_per_xcd: int = MI355X_CUS_PER_XCD
+                 ) -> tuple[dict[str, frozenset], set[str]]:
+    """The ``split`` policy: the top ``reserved`` slots of every XCD form an
+    isolated pool in which each replica of an isolated profile (memory GB in
+    ``isolated_gb``) gets its proportional share, disjoint from every other
+    mask; all other replicas share the remaining slots (one mask, the MPS-like
+    pool), so the isolated tenants' CUs never run a shared tenant's waves.
+    Allocated replicas keep their slots; an isolated replica the pool cannot
+    hold is unhealthy."""
+    shared = frozenset(range(cus_per_xcd - reserved))
+    pool = list(range(cus_per_xcd - reserved, cus_per_xcd))
+    out: dict[str, frozenset] = {}
+    iso = [(rid, mem) for rid, mem in replicas if mem in isolated_gb]
+    for rid, mem in replicas:
+        if mem not in isolated_gb:
+            out[rid] = keep.get(rid, shared)
+        elif rid in keep:
+            out[rid] = frozenset(keep[rid])
+    taken = {s for rid, _ in iso if rid in out for s in out[rid]}
+    free = [s for s in pool if s not in taken]
+    wants = slot_wants(iso, "proportional", gpu_memory_gb, cus_per_xcd)
+    bad: set[str] = set()
+    for rid, _ in sorted(iso):
+        if rid in out:
+            continue
+        w = wants[rid]
+        if w > len(free):
+            bad.add(rid)
+            continue
+        out[rid] = frozenset(free[:w])
+        free = free[w:]
+    return out, bad
+
+
 def layout_slots(replicas: list[tuple[str, int]], keep: dict[str, frozenset], policy: str, gpu_memory_gb: int,
                  cus_per_xcd: int = MI355X_CUS_PER_XCD) -> tuple[dict[str, frozenset], set[str]]:
     """Lay out the CU slots of one GPU's slice replicas.

@@ -154,7 +154,8 @@ class DevicePluginConfigRef:
 
 
 def plugin_config(node_name: str, plan_id: str, partitioning: NodePartitioning, cu_policy: str = "proportional",
-                  allocation: str = "pack", gpu_weights: dict[int, float] | None = None) -> dict:
+                  allocation: str = "pack", gpu_weights: dict[int, float] | None = None,
+                  split: dict | None = None) -> dict:
     """Device-plugin configuration for one node (the ``ToPluginConfig`` of
     ``mps/partitioner.go:123-157``, AMD shape).  With ``allocation:
     measured`` it also carries the probe-measured TFLOP/s per GPU
@@ -172,13 +173,17 @@ def plugin_config(node_name: str, plan_id: str, partitioning: NodePartitioning, 
            "gpus": gpus}
     if gpu_weights:
         out["gpuWeights"] = {int(k): round(float(v), 3) for k, v in sorted(gpu_weights.items())}
+    if cu_policy == "split" and split:   # the isolated pool: its profiles and reserved CU slots per XCD
+        out["isolatedProfiles"] = list(split.get("isolatedProfiles", []))
+        out["isolatedCuSlots"] = int(split.get("isolatedCuSlots", 0))
     return out
 
 
 class CuMaskPartitioner:
     def __init__(self, api, cm_ref: DevicePluginConfigRef | None = None, delay_s: float = 5.0, clock=None,
-                 cu_policy: str = "proportional", allocation: str = "pack"):
+                 cu_policy: str = "proportional", allocation: str = "pack", split: dict | None = None):
         self.api = api
+        self.split = split
         self.cm_ref = cm_ref or DevicePluginConfigRef()
         self.delay_s = delay_s
         self.clock = clock or api.clock
@@ -204,7 +209,7 @@ class CuMaskPartitioner:
                       for g in partitioning.gpus}
             weights = scoring.gpu_capacities(scoring.probe_table(ko.annotations(node)), counts) or None
         data[key] = yaml.safe_dump(plugin_config(name, plan_id, partitioning, self.cu_policy, self.allocation,
-                                                 weights), sort_keys=False)
+                                                 weights, self.split), sort_keys=False)
         self.api.patch("ConfigMap", ref.name, {"data": data}, ref.namespace)
         if self.delay_s > 0:
             self.clock.sleep(self.delay_s)  # ConfigMap propagation (kept for fidelity)
@@ -283,10 +288,10 @@ def amdpart_strategy(api, clock=None, reserve_whole_gpus: int = 0, memory_mode: 
 
 
 def cumask_strategy(api, cm_ref: DevicePluginConfigRef | None = None, delay_s: float = 5.0, clock=None,
-                    cu_policy: str = "proportional", placement: str = "pack") -> Strategy:
+                    cu_policy: str = "proportional", placement: str = "pack", split: dict | None = None) -> Strategy:
     pc = CuMaskPartitionCalculator()
     return Strategy(C.PARTITIONING_CUMASK, CuMaskSnapshotTaker(pc, placement), pc,
-                    CuMaskPartitioner(api, cm_ref, delay_s, clock, cu_policy, placement), cm.SliceCalculator(),
+                    CuMaskPartitioner(api, cm_ref, delay_s, clock, cu_policy, placement, split), cm.SliceCalculator(),
                     cm.SliceFilter())
 
 

@@ -112,8 +112,20 @@ def train_bytes_estimate(prog: Program, spec: dict) -> int:
     trainable = sum(v.numel * 4 for k, v in prog.params.items() if k not in spec["frozen"])
     states = {"sgd": 1 if spec["momentum"] > 0 else 0, "adam": 2, "adamw": 2}[spec["optimizer"]]
     acts = sum(prog.values[n.output].numel * 4 for n in prog.nodes)
+    # the differentiable attention materialises its B x H x Sq x Skv scores: the
+    # scores, the masked copy and the probabilities are kept for backward --
+    # a long-sequence spec is refused here, not at capture
+    scores = 0
+    for n in prog.nodes:
+        if n.op == "sdpa":
+            (b, sq, h, _), skv = prog.values[n.inputs[0]].shape, prog.values[n.inputs[1]].shape[1]
+            scores += 3 * b * h * sq * skv * 4
+        elif n.op == "attention":
+            b, sq, _ = prog.values[n.inputs[0]].shape
+            scores += 3 * b * n.attrs["heads"] * sq * sq * 4
     tgt = math.prod(spec["target_shape"]) * 4
-    return w + trainable * (1 + states) + sum(v.numel * 4 for v in prog.inputs) + tgt + 2 * acts
+    return (w + trainable * (1 + states) + sum(v.numel * 4 for v in prog.inputs) + tgt + 2 * acts
+            + 2 * scores)
 
 
 def _train_op(op: str, args: list, attrs: dict):

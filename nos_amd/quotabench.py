@@ -207,9 +207,7 @@ class QuotaScenario:
         from .sim.cluster import SimCluster
 
         self.runtime = runtime
-        cfg = GpuPartitionerConfig(cuPolicy="shared", batchWindowTimeoutSeconds=int(max(1, self.batch_window_s * 2)),
-                                   batchWindowIdleSeconds=int(max(1, self.batch_window_s)))
-        cl = self.cl = SimCluster(partitioner_config=cfg)
+        cl = self.cl = SimCluster(partitioner_config=self._partitioner_config())
         cl.add_node("mi355x-0", C.PARTITIONING_CUMASK, smi=FakeSmi(gpus=self.gpus, node="mi355x-0"),
                     pod_server_tenants=self.tenants_per_gpu, pod_server_dir=self.pod_server_dir,
                     runtime=lambda pod, conts: self._start(pod, conts), on_stop=lambda pod, conts: self._stop(pod))
@@ -221,6 +219,10 @@ class QuotaScenario:
                           .with_max({GPU_MEM: self.max_gb, "cpu": "64", "memory": "1Ti"}).get())
         self._settle(30)
         return cl
+
+    def _partitioner_config(self) -> GpuPartitionerConfig:
+        return GpuPartitionerConfig(cuPolicy="shared", batchWindowTimeoutSeconds=int(max(1, self.batch_window_s * 2)),
+                                    batchWindowIdleSeconds=int(max(1, self.batch_window_s)))
 
     # ------------------------------------------------------------ kubelet hooks
     def _start(self, pod: dict, conts) -> None:
@@ -283,6 +285,10 @@ class QuotaScenario:
         eq = self.cl.api.get(v1alpha1.KIND_EQ, "quota", ns)
         return float(((eq.get("status") or {}).get("used") or {}).get(GPU_MEM, 0))
 
+    def _gb(self, ns: str) -> int:
+        """The slice profile (GB) of a namespace's tenants."""
+        return getattr(self, "team_b_gb", 0) or self.slice_gb if ns == "team-b" else self.slice_gb
+
     def snapshot(self) -> dict:
         run = self.runtime.running()
         out = {}
@@ -292,7 +298,7 @@ class QuotaScenario:
             out[ns] = {"running_pods": len(lab), "tenants_running": len(mine),
                        "in_quota": sum(1 for v in lab.values() if v == "in-quota"),
                        "over_quota": sum(1 for v in lab.values() if v == "over-quota"),
-                       "status_used_gb": self.used_gb(ns), "tenant_gb": len(mine) * self.slice_gb,
+                       "status_used_gb": self.used_gb(ns), "tenant_gb": len(mine) * self._gb(ns),
                        "pods_match_tenants": set(lab) == mine}
         return out
 
@@ -384,6 +390,7 @@ class ComposedScenario(QuotaScenario):
 
     trainers: bool = True
     trainer_slice_gb: int = 36
+    trainer_dim: int = 2048         # NOS_AMD_COLL_DIM of the trainer pods
     waves: int = 3
     wave_gap_s: float = 4.0
     duty: str = "1.5:0.5"
@@ -391,6 +398,68 @@ class ComposedScenario(QuotaScenario):
     part_pods: int = 8
     part_resource: str = "amd.com/partition-1xcd.36gb"
     server_stats: object = None     # () -> pod-server stats (live runs), for the footprint comparison
+    # team-b on an isolated CU pool (cuPolicy split): its slice profile gets proportional CU masks
+    # inside ``isolated_cu_slots`` slots per XCD, team-a's tenants and the trainer share the rest
+    isolate_team_b: bool = False
+    team_b_gb: int = 0              # team-b's slice profile (0: slice_gb; isolated: a profile of its own)
+    isolated_cu_slots: int = 12
+    solo_s: float = 8.0             # phase C: team-b alone (team-a deleted), its solo latency
+    part_tenants: object = None     # (key) -> env: the repartitioned node's pods as real pod-server tenants
+
+    def _partitioner_config(self) -> GpuPartitionerConfig:
+        if not self.isolate_team_b:
+            return super()._partitioner_config()
+        # spread: every GPU's isolated pool holds its share of team-b's slices (a slot each)
+        return GpuPartitionerConfig(cuPolicy="split", isolatedProfiles=[f"{self.team_b_gb}gb"],
+                                    isolatedCuSlots=self.isolated_cu_slots, slicePlacement="spread",
+                                    batchWindowTimeoutSeconds=int(max(1, self.batch_window_s * 2)),
+                                    batchWindowIdleSeconds=int(max(1, self.batch_window_s)))
+
+    def _part_start(self, key: str) -> None:
+        """A pod of the repartitioned node: recorded (the partition itself is
+        simulated) and, in live runs, also started as a real tenant of the
+        GPU's pod server, so the partition pods load the GPU."""
+        self.sim_runtime.start(key, {})
+        if self.part_tenants is not None:
+            self.runtime.start("part/" + key, self.part_tenants(key))
+
+    def _part_stop(self, key: str) -> None:
+        self.sim_runtime.stop(key)
+        if self.part_tenants is not None:
+            self.runtime.stop("part/" + key)
+
+    def tenant_latency(self, since: dict | None) -> dict:
+        """Per namespace, the pod server's per-tenant inference latency over
+        the interval since ``since`` (a previous :meth:`server_marks`): the
+        replay time per completed request (``gpu_s`` / ``completed`` deltas),
+        mean over the namespace and its slowest tenant."""
+        now = self.server_marks()
+        if not now or since is None:
+            return {}
+        out: dict[str, dict] = {}
+        for pod, (done, gpu_s) in now.items():
+            d0, g0 = since.get(pod, (0, 0.0))
+            if done - d0 <= 0:
+                continue
+            ns = pod.split("/", 1)[0]
+            e = out.setdefault(ns, {"tenants": 0, "requests": 0, "gpu_s": 0.0, "max_ms": 0.0})
+            e["tenants"] += 1
+            e["requests"] += done - d0
+            e["gpu_s"] += gpu_s - g0
+            e["max_ms"] = max(e["max_ms"], 1e3 * (gpu_s - g0) / (done - d0))
+        return {ns: {"tenants": e["tenants"], "requests": e["requests"],
+                     "mean_ms": round(1e3 * e["gpu_s"] / e["requests"], 3), "slowest_tenant_ms": round(e["max_ms"], 3)}
+                for ns, e in out.items()}
+
+    def server_marks(self) -> dict:
+        if self.server_stats is None:
+            return {}
+        try:
+            st = self.server_stats()
+        except Exception:
+            return {}
+        return {str(t.get("pod")): (int(t.get("completed", 0)), float(t.get("gpu_s", 0.0)))
+                for t in st.get("tenants", [])}
 
     def build(self, runtime):
         from .gpu.fakesmi import FakeSmi
@@ -399,8 +468,8 @@ class ComposedScenario(QuotaScenario):
         self.sim_runtime = RecordingRuntime()
         self.part = cl.add_node("mi355x-part", C.PARTITIONING_AMDPART, gpus=self.part_gpus,
                                 smi=FakeSmi(gpus=self.part_gpus, node="mi355x-part"),
-                                runtime=lambda pod, conts: self.sim_runtime.start(ko.key(pod), {}),
-                                on_stop=lambda pod, conts: self.sim_runtime.stop(ko.key(pod)))
+                                runtime=lambda pod, conts: self._part_start(ko.key(pod)),
+                                on_stop=lambda pod, conts: self._part_stop(ko.key(pod)))
         for ns in ("training", "batch"):
             cl.api.create({"kind": "Namespace", "metadata": {"name": ns}})
         self._settle(30)
@@ -414,10 +483,12 @@ class ComposedScenario(QuotaScenario):
             # a GPU process of its own: the slice's GPU instead of the pod-server socket
             sock = env.pop(C.ENV_POD_SERVER, "")
             env.pop(C.ENV_POD_TOKEN, None)
+            if env.get(C.ENV_POD_CU_MASK):   # its slice's CU mask (split: the shared pool) for its own process
+                env["ROC_GLOBAL_CU_MASK"] = env.pop(C.ENV_POD_CU_MASK)
             gpu = sock.rsplit("gpu-", 1)[-1].split("/", 1)[0] if "gpu-" in sock else "0"
             env.update({"HIP_VISIBLE_DEVICES": gpu, "NOS_AMD_POD_KIND": "trainer", "RANK": "0", "WORLD_SIZE": "1",
                         "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(29600 + int(gpu)),
-                        "NOS_AMD_COLL_DIM": "2048", "NOS_AMD_COLL_BUCKET_MB": "32"})
+                        "NOS_AMD_COLL_DIM": str(self.trainer_dim), "NOS_AMD_COLL_BUCKET_MB": "32"})
         key = ko.key(pod)
         self.runtime.start(key, env)
         self.events.append(("start", key, time.monotonic()))
@@ -434,7 +505,9 @@ class ComposedScenario(QuotaScenario):
         dt = now - mark.get("_t", now)
         mark.update(steps)
         mark["_t"] = now
-        return {"steps": done, "steps_per_s": round(done / dt, 2) if dt > 0 else None}
+        flops = 6.0 * self.trainer_dim ** 3 * 4   # CollectiveTenant: batch = dim, 4 layers, forward + backward
+        return {"steps": done, "steps_per_s": round(done / dt, 2) if dt > 0 else None,
+                "tflops": round(done * flops / dt / 1e12, 2) if dt > 0 else None, "flops_per_step": flops}
 
     def _phase_util(self, sampler, t0: float) -> float | None:
         return sampler.mean(t0, time.monotonic())[0] if sampler is not None else None
@@ -467,7 +540,10 @@ class ComposedScenario(QuotaScenario):
                                 "trainers": self.gpus if self.trainers else 0, "waves": self.waves,
                                 "duty": self.duty, "part_gpus": self.part_gpus, "part_pods": self.part_pods,
                                 "part_resource": self.part_resource,
-                                "part_switch": "simulated (FakeSmi; the pool cannot switch MI355X modes)"}}
+                                "part_switch": "simulated (FakeSmi; the pool cannot switch MI355X modes)",
+                                "part_pods_run_as": "pod-server tenants" if self.part_tenants else "recorded only",
+                                "team_b_isolated": self.isolate_team_b, "team_b_gb": self.team_b_gb or self.slice_gb,
+                                "isolated_cu_slots_per_xcd": self.isolated_cu_slots if self.isolate_team_b else 0}}
         # phase 0: one DP trainer pod per GPU of the pod-server node
         t0 = time.monotonic()
         tr = []
@@ -482,8 +558,11 @@ class ComposedScenario(QuotaScenario):
         self.trainer_keys = tr
         mark: dict = {}
         self._trainer_progress(mark)
+        if self.isolate_team_b:
+            return self._run_isolated(res, mark, phase_timeout_s, sampler)
         # phase A: team-a in bursts, borrowing
         t1 = time.monotonic()
+        lat0 = self.server_marks()
         a, per = [], -(-self.team_a_pods // self.waves)
         for w in range(self.waves):
             n = min(per, self.team_a_pods - len(a))
@@ -493,9 +572,10 @@ class ComposedScenario(QuotaScenario):
         ok = self.drive(lambda: set(a) <= self.runtime.ready() and self._labels_settled(), phase_timeout_s)
         res["phase_a"] = {"ok": ok, "seconds": round(time.monotonic() - t1, 2), **self.snapshot(),
                           "gpu_util_pct": self._phase_util(sampler, t1), "quota_vs_footprint": self.quota_vs_footprint(),
-                          "trainer": self._trainer_progress(mark)}
+                          "trainer": self._trainer_progress(mark), "latency": self.tenant_latency(lat0)}
         # phase P: pending partition pods force a repartition of the amdpart node
         tp = time.monotonic()
+        lat0 = self.server_marks()
         sw0, plans0 = self.part.smi.switches, self.cl.clock.now()
         modes0 = list(self.part.smi.compute)
         keys = []
@@ -508,17 +588,81 @@ class ComposedScenario(QuotaScenario):
                                     "mode_switches": self.part.smi.switches - sw0, "modes_before": modes0,
                                     "modes_after": list(self.part.smi.compute), "pods_running": len(
                                         set(keys) & self.sim_runtime.running()),
-                                    "gpu_util_pct": self._phase_util(sampler, tp), "trainer": self._trainer_progress(mark)}
-        # phase B: team-b claims its min, preempting team-a's borrowed tenants
+                                    "gpu_util_pct": self._phase_util(sampler, tp), "trainer": self._trainer_progress(mark),
+                                    "latency": self.tenant_latency(lat0)}
+        if self.part_tenants is not None:   # the partition pods' tenants up (a live run): then measure
+            self.drive(lambda: {"part/" + k for k in keys} <= self.runtime.ready(), phase_timeout_s)
+            lat0 = self.server_marks()
+            self.drive(lambda: False, self.wave_gap_s)
+            res["phase_repartition"]["latency_with_part_tenants"] = self.tenant_latency(lat0)
+        # the batch jobs finish: their pods leave the partitions (and the GPU) before team-b arrives
+        for k in keys:
+            self.cl.api.delete("Pod", k.split("/", 1)[1], "batch")
+        self.drive(lambda: not (set(keys) & self.sim_runtime.running()), phase_timeout_s)
+        # phase B: team-b claims its min, preempting team-a's borrowed tenants (team-a keeps bursting)
         b_res = self._phase_b(phase_timeout_s, sampler)
-        res["phase_b"] = {**b_res, "quota_vs_footprint": self.quota_vs_footprint(), "trainer": self._trainer_progress(mark)}
+        lat0 = self.server_marks()
+        self.drive(lambda: False, self.solo_s)       # a window of team-b beside team-a's in-quota bursts
+        res["phase_b"] = {**b_res, "quota_vs_footprint": self.quota_vs_footprint(), "trainer": self._trainer_progress(mark),
+                          "latency": self.tenant_latency(lat0)}
+        res["concurrent_tenants"] = len(self.runtime.running())
+        # phase C: team-a leaves; team-b's latency alone is its solo reference
+        tc = time.monotonic()
+        for k in list(self.labels("team-a")):
+            self.cl.api.delete("Pod", k.split("/", 1)[1], "team-a")
+        self.drive(lambda: not any(k.startswith("team-a/") for k in self.runtime.running()), phase_timeout_s)
+        lat0 = self.server_marks()
+        self.drive(lambda: False, self.solo_s)
+        lc = self.tenant_latency(lat0)
+        res["phase_c"] = {"seconds": round(time.monotonic() - tc, 2), "latency": lc,
+                          "gpu_util_pct": self._phase_util(sampler, tc), "trainer": self._trainer_progress(mark)}
+        b_ms = (res["phase_b"].get("latency") or {}).get("team-b", {}).get("mean_ms")
+        c_ms = (lc.get("team-b") or {}).get("mean_ms")
+        res["team_b_latency_vs_alone"] = round(b_ms / c_ms, 3) if b_ms and c_ms else None
+        return res
+
+    def _run_isolated(self, res: dict, mark: dict, phase_timeout_s: float, sampler) -> dict:
+        """The isolation variant: team-b's tenants run on
+        their own CU slots (a profile of the isolated pool) before team-a
+        arrives; their latency alone, then while team-a's tenants burst on the
+        shared pool (the trainer there too), then during the repartition.
+        Reclaim by preemption needs both teams on one profile (a freed slice
+        of another profile does not fit the preemptor: the reference's
+        CapacityScheduling semantics) -- the shared variant measures it."""
+        t0 = time.monotonic()
+        b = self.submit_range("team-b", 0, self.team_b_pods, "b", self.team_b_gb)
+        ok = self.drive(lambda: set(b) <= self.runtime.ready() and self._labels_settled(), phase_timeout_s)
+        lat0 = self.server_marks()
+        self.drive(lambda: False, self.solo_s)
+        alone = self.tenant_latency(lat0)
+        res["phase_b_alone"] = {"ok": ok, "seconds": round(time.monotonic() - t0, 2), **self.snapshot(),
+                                "latency": alone, "gpu_util_pct": self._phase_util(sampler, t0),
+                                "trainer": self._trainer_progress(mark)}
+        t1 = time.monotonic()
+        a, per = [], -(-self.team_a_pods // self.waves)
+        lat0 = self.server_marks()
+        for w in range(self.waves):
+            n = min(per, self.team_a_pods - len(a))
+            a += self.submit_range("team-a", len(a), n, "a")
+            if w + 1 < self.waves:
+                self.drive(lambda: False, self.wave_gap_s)
+        ok = self.drive(lambda: set(a) <= self.runtime.ready() and self._labels_settled(), phase_timeout_s)
+        self.drive(lambda: False, self.solo_s)        # every wave running and bursting
+        during = self.tenant_latency(lat0)
+        res["phase_a"] = {"ok": ok, "seconds": round(time.monotonic() - t1, 2), **self.snapshot(),
+                          "latency": during, "gpu_util_pct": self._phase_util(sampler, t1),
+                          "quota_vs_footprint": self.quota_vs_footprint(), "trainer": self._trainer_progress(mark)}
+        b_alone = (alone.get("team-b") or {}).get("mean_ms")
+        b_during = (during.get("team-b") or {}).get("mean_ms")
+        res["team_b_latency_vs_alone"] = round(b_during / b_alone, 3) if b_alone and b_during else None
         res["concurrent_tenants"] = len(self.runtime.running())
         return res
 
-    def submit_range(self, ns: str, start: int, n: int, prefix: str) -> list[str]:
+    def submit_range(self, ns: str, start: int, n: int, prefix: str, gb: int | None = None) -> list[str]:
         keys = []
         for i in range(start, start + n):
-            self.cl.submit_pod(f"{prefix}-{i}", {f"{C.AMD_SLICE_RESOURCE_PREFIX}{self.slice_gb}gb": 1}, namespace=ns)
+            self.cl.submit_pod(f"{prefix}-{i}", {f"{C.AMD_SLICE_RESOURCE_PREFIX}{gb or self.slice_gb}gb": 1},
+                               namespace=ns)
             keys.append(f"{ns}/{prefix}-{i}")
         return keys
 
@@ -526,7 +670,7 @@ class ComposedScenario(QuotaScenario):
         t1 = time.monotonic()
         over_a = {k for k, v in self.labels("team-a").items() if v == "over-quota"}
         p0 = self.cl.scheduler.stats.get("preemptions", 0)
-        b = self.submit_range("team-b", 0, self.team_b_pods, "b")
+        b = self.submit_range("team-b", 0, self.team_b_pods, "b", self.team_b_gb or None)
         ok = self.drive(lambda: set(b) <= self.runtime.ready() and self._labels_settled(), phase_timeout_s)
         stops = [k for kind, k, t in self.events if kind == "stop" and t >= t1]
         return {"ok": ok, "seconds": round(time.monotonic() - t1, 2),
@@ -535,15 +679,26 @@ class ComposedScenario(QuotaScenario):
                 "gpu_util_pct": self._phase_util(sampler, t1)}
 
 
-def composed_for(gpus: int, tenant_slots_per_gpu: int = 25, slice_gb: int = 10, **kw) -> ComposedScenario:
+def composed_for(gpus: int, tenant_slots_per_gpu: int = 25, slice_gb: int = 10, isolate_team_b: bool = False,
+                 **kw) -> ComposedScenario:
     """A node of ``gpus`` GPUs, each holding one 36 GB trainer slice and
     ``tenant_slots_per_gpu`` 10 GB tenant slices: team-a borrows to 5/7 of
-    the tenant slots, team-b then claims its half."""
+    the tenant slots, team-b then claims its half.  ``isolate_team_b``:
+    team-b's pods request a profile of their own (``slice_gb`` + 2 GB) laid
+    out on an isolated CU pool (cuPolicy split), as many as its min holds."""
     slots = gpus * tenant_slots_per_gpu
     half = slots // 2
-    return ComposedScenario(gpus=gpus, slice_gb=slice_gb, team_a_pods=max(half + 1, round(slots * 5 / 7)),
-                            team_b_pods=half, min_gb=half * slice_gb, max_gb=slots * slice_gb,
-                            tenants_per_gpu=tenant_slots_per_gpu + 1, **kw)
+    b_gb = slice_gb + 2 if isolate_team_b else slice_gb
+    # isolated: team-b runs 3/4 of its min first, team-a fills what is left of the slots -- borrowing
+    # the rest of team-b's min
+    b_pods = half * slice_gb // b_gb * 3 // 4 if isolate_team_b else half
+    b_per_gpu = -(-b_pods // gpus)
+    a_pods = (gpus * ((tenant_slots_per_gpu * slice_gb - b_per_gpu * b_gb) // slice_gb) if isolate_team_b
+              else max(half + 1, round(slots * 5 / 7)))
+    return ComposedScenario(gpus=gpus, slice_gb=slice_gb, team_a_pods=a_pods,
+                            team_b_pods=b_pods, min_gb=half * slice_gb, max_gb=slots * slice_gb,
+                            tenants_per_gpu=tenant_slots_per_gpu + 1, isolate_team_b=isolate_team_b,
+                            team_b_gb=b_gb if isolate_team_b else 0, **kw)
 
 
 def _stats(v: list[float]) -> dict:

@@ -83,7 +83,9 @@ class SimCluster:
         fw = build_framework(sched_cfg.profiles[0], api=self.api)
         amd = amdpart_strategy(self.api, self.clock, self.cfg.reserve_whole_gpus, self.cfg.preferred_memory_mode)
         cum = cumask_strategy(self.api, self.cm_ref, self.cfg.device_plugin_delay_seconds, self.clock,
-                              self.cfg.cu_policy, self.cfg.slice_placement)
+                              self.cfg.cu_policy, self.cfg.slice_placement,
+                              {"isolatedProfiles": self.cfg.isolated_profiles,
+                               "isolatedCuSlots": self.cfg.isolated_cu_slots})
         hyb = hybrid_strategy(self.api, self.cm_ref, self.cfg.device_plugin_delay_seconds, self.clock)
         self.partitioner.add(NodeController(self.api, self.cluster_state, amd.initializer).controller())
         self.partitioner.add(PodController(self.api, self.cluster_state).controller())

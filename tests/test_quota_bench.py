@@ -102,3 +102,52 @@ def test_bench_quota_composed_runs_trainer_and_tenant_processes():
     assert "server_footprint_gb" in d["phase_b"]["quota_vs_footprint"]["team-b"]
     # the DP trainer keeps stepping through every phase
     assert all(d[p]["trainer"]["steps"] >= 1 for p in ("phase_a", "phase_b"))
+
+
+def test_composed_config5_with_an_isolated_team_b_on_an_8gpu_node(tmp_path):
+    """team-b on an isolated CU pool (cuPolicy split): its
+    slices' masks are disjoint from each other and from the shared pool that
+    team-a's tenants and the trainers get, on every GPU; team-a bursts in
+    beside it (borrowing the slots team-b leaves)."""
+    from nos_amd.bench_support import cus_from_hex
+    from nos_amd.quotabench import RecordingRuntime, composed_for
+
+    sc = composed_for(8, pod_server_dir=str(tmp_path), isolate_team_b=True)
+    rt = RecordingRuntime()
+    res = sc.run(rt)
+    assert res["config"]["team_b_isolated"] and res["config"]["team_b_gb"] == 12
+    assert res["phase_b_alone"]["ok"] and res["phase_b_alone"]["team-b"]["tenants_running"] == sc.team_b_pods
+    a = res["phase_a"]
+    assert a["ok"] and a["team-a"]["tenants_running"] == sc.team_a_pods and a["team-a"]["over_quota"] > 0
+    started = {k: t.env for k, t in rt.tenants.items()}
+    by_gpu: dict[str, dict[str, set]] = {}
+    for k, env in started.items():
+        if k.startswith(("team-a/", "team-b/")):
+            gpu = env["NOS_AMD_POD_SERVER"].rsplit("gpu-", 1)[-1].split("/", 1)[0]
+            by_gpu.setdefault(gpu, {})[k] = set(cus_from_hex(env["NOS_AMD_POD_CU_MASK"]))
+        elif k.startswith("training/"):
+            assert env.get("ROC_GLOBAL_CU_MASK"), "the trainer runs on the shared pool"
+    assert len(by_gpu) == 8
+    for masks in by_gpu.values():
+        shared = [m for k, m in masks.items() if k.startswith("team-a/")]
+        iso = [m for k, m in masks.items() if k.startswith("team-b/")]
+        assert shared and iso and all(m == shared[0] for m in shared)          # one shared pool
+        for i, m in enumerate(iso):
+            assert not (m & shared[0]) and all(not (m & o) for o in iso[i + 1:])  # isolated, disjoint
+            assert len(m) % 8 == 0                                               # XCD-symmetric
+
+
+def test_partition_pods_start_as_tenants_and_finish(tmp_path):
+    """The repartitioned node's pods also start as (recorded) pod-server
+    tenants, then finish before team-b arrives."""
+    from nos_amd.quotabench import RecordingRuntime, composed_for
+
+    sc = composed_for(2, pod_server_dir=str(tmp_path), part_gpus=1, part_pods=8,
+                      part_tenants=lambda key: {"NOS_AMD_POD_KIND": "partition"})
+    rt = RecordingRuntime()
+    res = sc.run(rt)
+    assert res["phase_repartition"]["ok"] and res["config"]["part_pods_run_as"] == "pod-server tenants"
+    parts = [k for k in rt.tenants if k.startswith("part/")]
+    assert len(parts) == 8 and not (set(parts) & rt.running())
+    assert res["phase_c"]["seconds"] >= 0
+    assert not any(k.startswith("team-a/") for k in rt.running())

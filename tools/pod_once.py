@@ -18,6 +18,8 @@ def main() -> None:
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--seconds", type=float, default=0.0, help="keep inferring for this long instead of --iters "
+                    "(a co-running background pod)")
     ap.add_argument("--memory-fraction", type=float, default=None, help="as a fractional pod (kernel_config)")
     ap.add_argument("--cu-mask", default="", help="a CU-mask slice (hex, ROC_GLOBAL_CU_MASK) with its CU budget: "
                     "the cumask process pod of the latency table, e.g. 0xffffffff for 32 CUs")
@@ -58,10 +60,14 @@ def main() -> None:
             t.launch()
         s.synchronize()
         t0 = time.perf_counter()
-        for _ in range(a.iters):
+        n = 0
+        while n < a.iters if a.seconds <= 0 else time.perf_counter() - t0 < a.seconds:
             t.launch()
+            n += 1
+            if a.seconds > 0 and n % 32 == 0:
+                s.synchronize()
         s.synchronize()
-    dt = (time.perf_counter() - t0) / a.iters
+    dt = (time.perf_counter() - t0) / n
     print(f"{a.dtype}: {dt * 1e3:.3f} ms/inference ({1 / dt:.1f} inf/s), cu budget {budget}", flush=True)
 
 
