@@ -93,6 +93,8 @@ def main(argv=None) -> int:
     ap.add_argument("--socket-dir", default="")
     ap.add_argument("--socket", default="", help="explicit socket path (default <socket-dir>/gpu-<gpu>/server.sock)")
     ap.add_argument("--lanes", type=int, default=16, help="streams = hardware queues the tenants are served on")
+    ap.add_argument("--priority-lanes", type=int, default=2,
+                    help="high-priority streams serving the latency tenants (stateful decoders) from their own queue")
     ap.add_argument("--max-tenants", type=int, default=48)
     ap.add_argument("--memory-gb", type=float, default=0.0, help="slice memory the server admits (0 = the GPU's)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
@@ -109,7 +111,8 @@ def main(argv=None) -> int:
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.INFO),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     if args.gpus:
-        rest = ["--socket-dir", args.socket_dir, "--lanes", str(args.lanes), "--max-tenants", str(args.max_tenants),
+        rest = ["--socket-dir", args.socket_dir, "--lanes", str(args.lanes), "--priority-lanes",
+                str(args.priority_lanes), "--max-tenants", str(args.max_tenants),
                 "--memory-gb", str(args.memory_gb), "--device", args.device, "--log-level", args.log_level]
         if args.no_graphs:
             rest.append("--no-graphs")
@@ -125,7 +128,7 @@ def main(argv=None) -> int:
         if args.hip_id >= 0:
             os.environ["HIP_VISIBLE_DEVICES"] = str(args.hip_id)
         os.environ.setdefault("HIP_VISIBLE_DEVICES", str(args.gpu))
-        os.environ["GPU_MAX_HW_QUEUES"] = str(min(MAX_HW_QUEUES, max(args.lanes, 1)))
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(MAX_HW_QUEUES, max(args.lanes + args.priority_lanes, 1)))
     from ..api import constants as C
     from ..podserver.allocations import records_dir
     from ..podserver.server import PodServer
@@ -138,7 +141,8 @@ def main(argv=None) -> int:
         from ..resource.podresources_grpc import GrpcLister
 
         lister = GrpcLister(args.pod_resources_socket)
-    srv = PodServer(path, device=args.device, lanes=args.lanes, max_tenants=args.max_tenants,
+    srv = PodServer(path, device=args.device, lanes=args.lanes, priority_lanes=args.priority_lanes,
+                    max_tenants=args.max_tenants,
                     memory_gb=args.memory_gb or None, graphs=not args.no_graphs,
                     solo_graphs=not args.no_solo_graphs, allocations_dir=records, pod_resources=lister).start()
     if args.metrics_port:

@@ -101,7 +101,8 @@ class PodClient:
 
     def register(self, pod: str, program: dict, weights: bytes = b"", token: str | None = None,
                  memory_limit_gb: float | None = None, cu_mask: str | None = None, env: dict | None = None,
-                 variants: list[dict] | None = None, train: dict | None = None) -> dict:
+                 variants: list[dict] | None = None, train: dict | None = None,
+                 priority: str | None = None) -> dict:
         """Ship the pod's program (op graph + weight bytes, program.py) to the
         server.  The allocation token comes from the device plugin's env; the
         slice itself is the plugin's record.  ``memory_limit_gb`` /
@@ -119,6 +120,8 @@ class PodClient:
             req["variants"] = list(variants)
         if train is not None:
             req["train"] = dict(train)
+        if priority is not None:   # "latency": the server's priority lanes (default for stateful programs)
+            req["priority"] = priority
         rep, _ = self._call(req, weights)
         self._reg = (req, weights)
         self.input_dtype = rep.get("input_dtype")

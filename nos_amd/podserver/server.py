@@ -111,6 +111,7 @@ class Tenant:
     id_bound: int | None = None    # token-id input: ids must lie in [0, id_bound)
     alts: dict = field(default_factory=dict)   # other input shapes -> _Variant (same weights)
     trainer: object = None         # a training tenant (training.Trainer): steps instead of inferences
+    latency: bool = False          # served by the priority lanes (a generation step per request)
     state: dict = field(default_factory=dict)       # persistent buffers (K / V caches, positions), every variant's
     pos_limits: dict = field(default_factory=dict)  # position state -> rows of the caches written at it
 
@@ -187,7 +188,7 @@ class PodServer:
                  kernel_config: dict | None = None, solo_graphs: bool = True,
                  allocations_dir: str | os.PathLike | None = None, pod_resources=None,
                  reap_interval_s: float = 1.0, max_inflight_register_gb: float = 16.0,
-                 register_timeout_s: float = 30.0, register_min_mb_s: float = 50.0):
+                 register_timeout_s: float = 30.0, register_min_mb_s: float = 50.0, priority_lanes: int = 2):
         """``allocations_dir``: this GPU's allocation records (tokens
         required; allocations.py).  Without it admission is open: the client
         declares its slice, which must be > 0 when the server accounts
@@ -195,7 +196,11 @@ class PodServer:
         (resource/client.py) -- tenants whose devices no pod holds any more
         are evicted.  ``register_timeout_s`` + payload / ``register_min_mb_s``:
         the deadline of a register payload once its header arrived (a stalled
-        sender's claim is released and its connection closed)."""
+        sender's claim is released and its connection closed).
+        ``priority_lanes``: lanes on high-priority streams that serve only
+        latency tenants (stateful decoders by default, or a register request
+        with ``"priority": "latency"``) from their own queue, so a generation
+        step is dispatched ahead of the throughput tenants' kernels."""
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.path = Path(socket_path)
@@ -209,6 +214,9 @@ class PodServer:
         self._lock = threading.Lock()          # tenant table
         self._build_lock = threading.Lock()    # one registration (build + capture + accounting) at a time
         self._q: queue.Queue[_Job | None] = queue.Queue()
+        self._qhi: queue.Queue[_Job | None] = queue.Queue()   # latency tenants' requests
+        self.priority_lanes_n = max(0, int(priority_lanes))
+        self._hi_lanes: list = []
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
         self._conns: dict[socket.socket, threading.Thread] = {}  # open client connections
@@ -258,9 +266,13 @@ class PodServer:
         self.memory_gb = min(self.memory_gb or total_gb, total_gb)
         # lanes first: with GPU_MAX_HW_QUEUES >= lanes each gets its own HW queue
         self._lanes = [torch.cuda.Stream() for _ in range(self.lanes_n)]
+        # latency lanes: the highest stream priority (HSA queue priority), dispatched first
+        hi = torch.cuda.Stream.priority_range()[1] if hasattr(torch.cuda.Stream, "priority_range") else -1
+        self._hi_lanes = [torch.cuda.Stream(priority=hi) for _ in range(self.priority_lanes_n)]
         self._setup_stream = torch.cuda.Stream()
         self.info = {"device": props.name, "multiprocessor_count": props.multi_processor_count,
-                     "lanes": self.lanes_n, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                     "lanes": self.lanes_n, "priority_lanes": self.priority_lanes_n,
+                     "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                      "memory_gb": round(self.memory_gb, 1), "kernel_config": cfg,
                      "solo_kernel_config": self.solo_config,
                      "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES")}
@@ -296,6 +308,10 @@ class PodServer:
             t = threading.Thread(target=self._lane, args=(i,), name=f"lane-{i}", daemon=True)
             t.start()
             self._threads.append(t)
+        for i in range(self.priority_lanes_n):
+            t = threading.Thread(target=self._lane, args=(i, True), name=f"hi-lane-{i}", daemon=True)
+            t.start()
+            self._threads.append(t)
         t = threading.Thread(target=self._accept, name="accept", daemon=True)
         t.start()
         self._threads.append(t)
@@ -329,6 +345,8 @@ class PodServer:
             t.join(timeout=30)
         for _ in range(self.lanes_n):
             self._q.put(None)
+        for _ in range(self.priority_lanes_n):
+            self._qhi.put(None)
         for t in self._threads:
             t.join(timeout=10)
         with self._lock:
@@ -426,7 +444,7 @@ class PodServer:
                         else:
                             want = bool(want)
                         job = _Job(tenant, payload, want, shp)
-                        self._q.put(job)
+                        (self._qhi if tenant.latency and self.priority_lanes_n else self._q).put(job)
                         job.done.wait()
                         if job.error:
                             raise RuntimeError(job.error)
@@ -572,6 +590,8 @@ class PodServer:
         try:
             if "program" not in req:
                 raise AdmissionError("register carries no program (nos-amd.program/v1 op graph + weights)")
+            if req.get("priority") not in (None, "latency", "throughput"):
+                raise AdmissionError("priority must be 'latency' or 'throughput'")
             extra = req.get("variants") or []
             if not isinstance(extra, list):
                 raise AdmissionError("variants must be a list of programs")
@@ -615,6 +635,9 @@ class PodServer:
             self._release_claim(claim)
             raise
         t.token, t.record_path, t.device_ids, t.conn = claim["token"], claim["record"], claim["dev_ids"], conn
+        prio = req.get("priority")
+        # a stateful tenant (a decoder generating token by token) is a latency tenant unless it says otherwise
+        t.latency = prio == "latency" or (prio is None and bool(t.state))
         with self._lock:
             self.tenants[tid] = t
             M.PODSERVER_TENANTS.labels(self.gpu_label).set(len(self.tenants))
@@ -858,7 +881,7 @@ class PodServer:
             ts = [{"tenant": t.id, "pod": t.pod, "program": t.program, "completed": t.completed,
                    "solo_completed": t.solo_completed, "gpu_s": round(t.gpu_s, 4),
                    "footprint_gb": t.footprint_gb, "memory_limit_gb": t.memory_limit_gb, "cu_mask": t.cu_mask,
-                   "kind": "train" if t.trainer is not None else "infer",
+                   "kind": "train" if t.trainer is not None else "infer", "latency": t.latency,
                    "train_steps": t.trainer.steps if t.trainer is not None else 0}
                   for t in self.tenants.values()]
             pending = len(self._pending)
@@ -866,18 +889,20 @@ class PodServer:
                 "evictions": self.evictions}
 
     # ------------------------------------------------------------ lanes
-    def _lane(self, i: int) -> None:
+    def _lane(self, i: int, hi: bool = False) -> None:
         import torch
 
-        lane = self._lanes[i] if self.gpu else None
+        q = self._qhi if hi else self._q
+        lane = (self._hi_lanes if hi else self._lanes)[i] if self.gpu else None
         while True:
-            job = self._q.get()
+            job = q.get()
             if job is None:
                 return
             job.t_start = time.monotonic()
             with self._lock:
                 self._busy += 1
-                alone = self._busy == 1 and self._q.qsize() == 0  # no other tenant running or waiting
+                # no other tenant running or waiting
+                alone = self._busy == 1 and self._q.qsize() == 0 and self._qhi.qsize() == 0
             try:
                 self._run(job, lane, alone)
             except Exception as e:  # reported to that tenant only

@@ -249,3 +249,24 @@ def test_variants_share_their_folded_and_merged_weights(tenant):
 
     a, b, e = (derived_ids(c) for c in cps)
     assert a and b == e and b <= a     # the decode / extend variants reuse the prefill's tensors
+
+
+def test_stateful_tenants_are_latency_tenants_on_the_priority_lanes(tenant, server):
+    """A decoder's generation steps go to the priority lanes' own queue
+    (high-priority streams on a GPU); a tenant may opt out or in."""
+    from nos_amd.models.yolos_program import demo_tenant
+
+    progs, w = tenant
+    a, b, y = (PodClient(server.path, connect_timeout_s=5) for _ in range(3))
+    a.register("dec", progs[0], w, memory_limit_gb=1, variants=progs[1:])
+    b.register("dec-bulk", progs[0], w, memory_limit_gb=1, variants=progs[1:], priority="throughput")
+    y.register("yolos", *demo_tenant("fp32", 0, small=False), memory_limit_gb=1)
+    kinds = {t["pod"]: t["latency"] for t in a.stats()["tenants"]}
+    assert kinds == {"dec": True, "dec-bulk": False, "yolos": False}
+    ids, _ = a.generate(_prompt(6), 4)
+    assert ids.shape == (1, 4)
+    c = PodClient(server.path, connect_timeout_s=5)
+    with pytest.raises(PodServerError, match="priority must be"):
+        c.register("bad", progs[0], w, memory_limit_gb=1, priority="urgent")
+    for x in (a, b, y, c):
+        x.close()

@@ -81,6 +81,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--tenants", type=int, default=28)
     ap.add_argument("--lanes", type=int, default=16)
+    ap.add_argument("--priority-lanes", type=int, default=2, help="high-priority lanes for the decode tenants")
     ap.add_argument("--window", type=float, default=8.0)
     ap.add_argument("--warmup", type=float, default=2.0)
     ap.add_argument("--slice-gb", type=float, default=10.0)
@@ -103,13 +104,14 @@ def main() -> None:
              if a.mix else ["yolos"] * a.tenants)
     a.tenants = len(kinds)
     # one hardware queue per lane: before anything initialises HIP (cmd/podserver.py)
-    os.environ["GPU_MAX_HW_QUEUES"] = str(min(a.lanes, 32))
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(a.lanes + a.priority_lanes, 32))
     from nos_amd.models.yolos_program import demo_tenant
     from nos_amd.podserver.client import PodClient
     from nos_amd.podserver.server import PodServer
 
     path = Path(tempfile.mkdtemp(prefix="nos_ps_", dir="/tmp")) / "gpu-0" / "server.sock"
-    srv = PodServer(path, device="cuda", lanes=a.lanes, max_tenants=max(48, a.tenants)).start()
+    srv = PodServer(path, device="cuda", lanes=a.lanes, priority_lanes=a.priority_lanes,
+                    max_tenants=max(48, a.tenants)).start()
     from nos_amd import ops
 
     ops.set_gemm_f32x6_pipeline(bool(a.pipeline))  # process-wide: every capture below
