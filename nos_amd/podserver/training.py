@@ -115,29 +115,64 @@ def train_bytes_estimate(prog: Program, spec: dict) -> int:
     # the differentiable attention materialises its B x H x Sq x Skv scores: the
     # scores, the masked copy and the probabilities are kept for backward --
     # a long-sequence spec is refused here, not at capture
-    scores = 0
+    # (train_ops.ChunkedAttention: per layer the saved log-sum-exp rows, the live
+    # scores of one query chunk at a time; NOS_AMD_TRAIN_NATIVE=0: the full
+    # B x H x Sq x Skv scores, masked copy and probabilities of every layer)
+    import os
+
+    from .train_ops import scores_bytes
+
+    native = os.environ.get("NOS_AMD_TRAIN_NATIVE", "1") != "0"
+    scores = live = 0
     for n in prog.nodes:
         if n.op == "sdpa":
             (b, sq, h, _), skv = prog.values[n.inputs[0]].shape, prog.values[n.inputs[1]].shape[1]
-            scores += 3 * b * h * sq * skv * 4
         elif n.op == "attention":
             b, sq, _ = prog.values[n.inputs[0]].shape
-            scores += 3 * b * n.attrs["heads"] * sq * sq * 4
+            h, skv = n.attrs["heads"], sq
+        else:
+            continue
+        if native:
+            scores += 4 * b * h * sq
+            live = max(live, scores_bytes(b, h, sq, skv))
+        else:
+            scores += 3 * b * h * sq * skv * 4
+    scores += live
     tgt = math.prod(spec["target_shape"]) * 4
     return (w + trainable * (1 + states) + sum(v.numel * 4 for v in prog.inputs) + tgt + 2 * acts
             + 2 * scores)
 
 
 def _train_op(op: str, args: list, attrs: dict):
-    """One node in differentiable PyTorch (the fused attention kernel has no
-    backward: its softmax form here)."""
+    """One node, differentiable: GEMMs and attention on the gfx950 kernels
+    (train_ops: h3 GEMMs for the forward and both backward products, chunked
+    attention with a log-sum-exp recompute -- no S x S scores kept), the rest
+    in PyTorch.  ``NOS_AMD_TRAIN_NATIVE=0``: PyTorch throughout (A/B)."""
+    import os
+
+    native = os.environ.get("NOS_AMD_TRAIN_NATIVE", "1") != "0"
     if op == "attention":
         from ..ops import tenant as T
+        from . import train_ops
 
         q, k, v = _qkv_views(args[0], attrs["heads"])
         if "q_start" in attrs:
             q = q[:, attrs["q_start"]:attrs["q_end"]]
+        if native:
+            return train_ops.attention(q, k, v, attrs.get("causal", False), attrs.get("scale")).flatten(2)
         return T.sdpa_ref(q, k, v, attrs.get("causal", False), attrs.get("scale")).flatten(2)
+    if op == "sdpa" and native:
+        from . import train_ops
+
+        return train_ops.attention(args[0], args[1], args[2], attrs.get("causal", False), attrs.get("scale"))
+    if op == "linear" and native:
+        import torch.nn.functional as F
+
+        from . import train_ops
+
+        y = train_ops.linear(args[0], args[1], args[2] if len(args) > 2 else None)
+        act = attrs.get("act")
+        return F.gelu(y) if act == "gelu" else (F.relu(y) if act == "relu" else y)
     if op == "cast":
         return args[0]  # fp32 master copy: a bf16 program trains in fp32
     return _eager(op, args, attrs, ref=True)
