@@ -58,10 +58,26 @@ __device__ __forceinline__ float4 ld4(const void* p, long long i, int bf) {
 // ------------------------------------------------------------------ kv_write / rotary at device positions
 // one thread per (b, s, h, d < D/2) pair (d, d + D/2): the rotate_half pair
 // a fused rotary needs; without tables it just copies both elements
+// one K / V pair per launch: blockIdx.y 0 = (x, cache) with the rotary tables
+// (K), 1 = (x2, cache2) plain (V; x2 == nullptr: a single write)
+struct KvPair {
+  const void* x2;
+  int ldx2;
+  long long bsx2;
+  void* cache2;
+};
+
 __global__ __launch_bounds__(256) void kv_write_kernel(const void* __restrict__ x, int xbf, int ldx, long long bsx,
                                                        void* __restrict__ cache, int cbf, const int* __restrict__ pos,
                                                        const float* __restrict__ cs, const float* __restrict__ sn,
-                                                       int R, int B, int S, int H, int D, int L) {
+                                                       int R, int B, int S, int H, int D, int L, KvPair v2) {
+  if (blockIdx.y == 1) {  // the V half: its own rows, no rotation
+    x = v2.x2;
+    ldx = v2.ldx2;
+    bsx = v2.bsx2;
+    cache = v2.cache2;
+    cs = sn = nullptr;
+  }
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   const int hd = D / 2;
   if (i >= (long long)B * S * H * hd) return;
@@ -362,16 +378,19 @@ __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, i
 
 }  // namespace
 
+// x2 / cache2 (optional, same shapes and dtypes): a second write in the same
+// launch without rotation -- a layer's V beside its rotated K
 NOS_API int nos_kv_write(const void* x, int xbf, int ldx, long long bsx, void* cache, int cbf, const int* pos,
                          const float* cos_t, const float* sin_t, int R, int B, int S, int H, int D, int L,
-                         hipStream_t stream) {
+                         const void* x2, int ldx2, long long bsx2, void* cache2, hipStream_t stream) {
   if (B <= 0 || S <= 0 || H <= 0 || D <= 0 || (D % 2) || L <= 0 || S > L || ldx < H * D || !x || !cache || !pos ||
       (B > 1 && bsx < (long long)(S - 1) * ldx + H * D) || (xbf != 0 && xbf != 1) || (cbf != 0 && cbf != 1) ||
-      ((cos_t == nullptr) != (sin_t == nullptr)) || (cos_t && R <= 0))
+      ((cos_t == nullptr) != (sin_t == nullptr)) || (cos_t && R <= 0) || ((x2 == nullptr) != (cache2 == nullptr)) ||
+      (x2 && (ldx2 < H * D || (B > 1 && bsx2 < (long long)(S - 1) * ldx2 + H * D))))
     return (int)hipErrorInvalidValue;
   const long long n = (long long)B * S * H * (D / 2);
-  hipLaunchKernelGGL(kv_write_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, xbf, ldx, bsx, cache,
-                     cbf, pos, cos_t, sin_t, R, B, S, H, D, L);
+  hipLaunchKernelGGL(kv_write_kernel, dim3((unsigned)((n + 255) / 256), x2 ? 2u : 1u), dim3(256), 0, stream, x, xbf,
+                     ldx, bsx, cache, cbf, pos, cos_t, sin_t, R, B, S, H, D, L, KvPair{x2, ldx2, bsx2, cache2});
   return (int)hipGetLastError();
 }
 

@@ -101,7 +101,7 @@ _SIGS = {
     "nos_glu": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_ll, c_int, c_int, c_int, c_void_p],
     # decode.hip: stateful decoding (K / V caches and positions on the device) and skinny GEMMs
     "nos_kv_write": [c_void_p, c_int, c_int, c_ll, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                     c_int, c_int, c_int, c_void_p],
+                     c_int, c_int, c_int, c_void_p, c_int, c_ll, c_void_p, c_void_p],
     "nos_rotary_pos": [c_void_p, c_int, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                        c_int, c_int, c_void_p],
     "nos_attn_decode_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],

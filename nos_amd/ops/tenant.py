@@ -483,13 +483,17 @@ def _i32_pos(pos: torch.Tensor, B: int) -> torch.Tensor:
     return pos
 
 
-def kv_write(cache: torch.Tensor, x: torch.Tensor, pos: torch.Tensor, rope: tuple | None = None) -> torch.Tensor:
+def kv_write(cache: torch.Tensor, x: torch.Tensor, pos: torch.Tensor, rope: tuple | None = None,
+             second: tuple | None = None) -> torch.Tensor:
     """cache[b, pos[b] + s] = x[b, s] in place (rows past the cache dropped);
     ``rope`` = (cos, sin) fp32 tables: x rotated at those positions first.
-    Returns ``cache``."""
+    ``second`` = (cache2, x2): a second, unrotated write of the same shape in
+    the same launch (a layer's V beside its K).  Returns ``cache``."""
     from ..podserver.program.reference import kv_write_ref, rotary_at_ref
 
     if not cache.is_cuda:
+        if second is not None:
+            kv_write_ref(second[0], second[1], pos)
         return kv_write_ref(cache, rotary_at_ref(x, rope[0], rope[1], pos) if rope else x, pos)
     B, L, H, D = cache.shape
     S = x.shape[1]
@@ -505,9 +509,21 @@ def kv_write(cache: torch.Tensor, x: torch.Tensor, pos: torch.Tensor, rope: tupl
     if rope is not None:
         c, s_ = rope[0].float().contiguous(), rope[1].float().contiguous()
         R = c.shape[0]
+    x2p, ld2, bs2, c2p = None, 0, 0, None
+    if second is not None:
+        c2, x2 = second
+        if c2.shape != cache.shape or c2.dtype != cache.dtype or x2.shape != x.shape or x2.dtype != x.dtype \
+                or not c2.is_contiguous():
+            raise ValueError("kv_write: the second write must match the first's shapes and dtypes")
+        try:
+            ld2, bs2 = _rows_view(x2)
+        except ValueError:
+            x2 = x2.contiguous()
+            ld2, bs2 = _rows_view(x2)
+        x2p, c2p = x2.data_ptr(), c2.data_ptr()
     _lib.check(_lib.lib().nos_kv_write(x.data_ptr(), _bf(x), ldx, bsx, cache.data_ptr(), _bf(cache),
-                                       _i32_pos(pos, B).data_ptr(), _ptr(c), _ptr(s_), R, B, S, H, D, L, _stream()),
-               "nos_kv_write")
+                                       _i32_pos(pos, B).data_ptr(), _ptr(c), _ptr(s_), R, B, S, H, D, L, x2p, ld2, bs2,
+                                       c2p, _stream()), "nos_kv_write")
     return cache
 
 

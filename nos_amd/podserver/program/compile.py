@@ -70,6 +70,7 @@ class Lowered:
             steps = self._fuse_qkv_attention(steps)
             steps = self._fuse_rotary_sdpa(steps)
             steps = self._fuse_rotary_at(steps)
+            steps = self._merge_kv_writes(steps)
             if "cat_buffer" not in skip:
                 steps = self._cat_into_buffer(steps)
             steps = self._mark_plane_handoffs(steps)
@@ -939,6 +940,31 @@ class Lowered:
             n += 1
         self.stats["rotary_at_fused"] = n
         return [s for s in steps if s.output not in drop]
+
+    def _merge_kv_writes(self, steps: list[_Step]) -> list[_Step]:
+        """A layer's K and V cache writes at the same position (the K one
+        rotated, the V one plain) in ONE launch: the V write's step becomes
+        the pair (it comes later, so both inputs exist) and names the K
+        cache's new version too."""
+        by_out = {s.output: s for s in steps}
+        drop, n = set(), 0
+        for s in steps:
+            if s.kind != "sdpa_cache":
+                continue
+            wk, wv = by_out.get(s.inputs[1]), by_out.get(s.inputs[2])
+            if (wk is None or wv is None or wk.kind != "kv_write" or wv.kind != "kv_write" or id(wk) in drop
+                    or wv.attrs.get("rope") or wv.attrs.get("pair") or wk.inputs[2] != wv.inputs[2]
+                    or tuple(self._shape(wk.inputs[1])) != tuple(self._shape(wv.inputs[1]))
+                    or tuple(self._shape(wk.inputs[0])) != tuple(self._shape(wv.inputs[0]))
+                    or self._dtype(wk.inputs[0]) != self._dtype(wv.inputs[0])
+                    or steps.index(wk) > steps.index(wv)):
+                continue
+            wv.inputs = wk.inputs + [wv.inputs[0], wv.inputs[1]]   # K cache, K x, pos, [cos, sin], V cache, V x
+            wv.attrs = {"pair": True, "rope": bool(wk.attrs.get("rope")), "k_out": wk.output}
+            drop.add(id(wk))
+            n += 1
+        self.stats["kv_writes_paired"] = n
+        return [s for s in steps if id(s) not in drop]
 
     def _prep_conv_weights(self, steps: list[_Step]) -> None:
         """GPU: every conv weight [OC, C, KH, KW] also as the fp32 [OC, Kp]

@@ -116,6 +116,11 @@ class CompiledProgram(Lowered):
                 y = T.patches(a[0], at["ph"], at["pw"], torch_dtype(at.get("dtype", "fp32")), at.get("hp"), at.get("wp"))
             elif k == "glu":
                 y = T.glu(a[0], a[1], s.attrs["op"])
+            elif k == "kv_write" and s.attrs.get("pair"):   # K (maybe rotated) and V of one layer, one launch
+                r = 5 if s.attrs.get("rope") else 3
+                env[s.attrs["k_out"]] = T.kv_write(a[0], a[1], a[2], rope=(a[3], a[4]) if s.attrs.get("rope") else None,
+                                                   second=(a[r], a[r + 1]))
+                y = a[r]
             elif k == "kv_write":
                 y = T.kv_write(a[0], a[1], a[2], rope=(a[3], a[4]) if s.attrs.get("rope") else None)
             elif k == "sdpa_cache":
