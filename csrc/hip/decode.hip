@@ -32,7 +32,9 @@
 
 namespace {
 
-enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8, EPI_SILU = 64 };
+enum : int { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_RELU = 8, EPI_SILU = 64, EPI_GLU = 256 };
+// EPI_GLU (GEMV): W = [gate; up] (2 Nh rows), y [M, Nh] = silu(x . gate_n) * (x . up_n) -- SwiGLU
+// in the merged gate-up GEMV's epilogue, each wave's two columns being n and n + Nh
 
 __device__ __forceinline__ float ldf(const void* p, long long i, int bf) {
   return bf ? nos::bf16_to_f32(static_cast<const unsigned short*>(p)[i]) : static_cast<const float*>(p)[i];
@@ -334,15 +336,18 @@ __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, i
     rsc[tid] = 1.f;
   }
   __syncthreads();
-  const int ngrp = (N + 7) / 8;  // 8 columns per workgroup pass: 4 waves x 2
+  const bool glu = (epi & EPI_GLU) != 0;
+  const int Nh = N / 2;                                          // GLU: output columns
+  const int ngrp = glu ? (Nh + 3) / 4 : (N + 7) / 8;             // 8 columns per pass: 4 waves x 2
   for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
-    const int n0 = grp * 8 + wid * 2;
+    const int n0 = glu ? grp * 4 + wid : grp * 8 + wid * 2;
     float acc[2][M];
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int m = 0; m < M; ++m) acc[c][m] = 0.f;
-    const int nc0 = min(n0, N - 1), nc1 = min(n0 + 1, N - 1);
+    const int nc0 = glu ? min(n0, Nh - 1) : min(n0, N - 1);
+    const int nc1 = glu ? min(n0, Nh - 1) + Nh : min(n0 + 1, N - 1);
     const long long w0 = (long long)nc0 * ldw, w1 = (long long)nc1 * ldw;
     for (int k = lane * 4; k < K; k += 256) {
       const float4 a = ld4(w, w0 + k, wbf), c4 = ld4(w, w1 + k, wbf);
@@ -357,6 +362,19 @@ __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, i
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int m = 0; m < M; ++m) acc[c][m] = nos::wave_sum(acc[c][m]);
+    if (glu) {  // lane m finishes output (m, n0): silu(gate) * up
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (lane == m && n0 < Nh) {
+          float g = acc[0][m] * rsc[m], u = acc[1][m] * rsc[m];
+          if (epi & EPI_BIAS) {
+            g += ldf(bias, n0, wbf);
+            u += ldf(bias, n0 + Nh, wbf);
+          }
+          stf(y, (long long)m * ldy + n0, g / (1.f + __expf(-g)) * u, xbf);
+        }
+      continue;
+    }
     // lane (c * M + m) finishes output (m, n0 + c)
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -471,12 +489,14 @@ NOS_API int nos_argmax(const void* x, int bf16, int rows, int L, int ldx, int* o
 NOS_API int nos_gemv(const void* x, int xbf, int ldx, const void* w, int wbf, int ldw, const void* bias,
                      const void* res, int ldr, void* y, int ldy, int M, int N, int K, int epi, float rms_eps,
                      hipStream_t stream) {
-  if (!x || !w || !y || M <= 0 || M > 8 || N <= 0 || K <= 0 || (K % 4) || ldx < K || ldw < K || ldy < N ||
+  if (!x || !w || !y || M <= 0 || M > 8 || N <= 0 || K <= 0 || (K % 4) || ldx < K || ldw < K || ldy < ((epi & EPI_GLU) ? N / 2 : N) ||
       (long long)M * K * 4 > 65536 || (xbf != 0 && xbf != 1) || (wbf != 0 && wbf != 1) ||
       ((epi & EPI_BIAS) && !bias) || ((epi & EPI_RESID) && (!res || ldr < N)) || (ldx % 4) || (ldw % 4) ||
       ((uintptr_t)x & (xbf ? 7 : 15)) || ((uintptr_t)w & (wbf ? 7 : 15)))
     return (int)hipErrorInvalidValue;
-  const int ngrp = (N + 7) / 8;
+  if ((epi & EPI_GLU) && ((N % 2) || (epi & (EPI_RESID | EPI_GELU | EPI_RELU | EPI_SILU)) || ldy < N / 2))
+    return (int)hipErrorInvalidValue;
+  const int ngrp = (epi & EPI_GLU) ? (N / 2 + 3) / 4 : (N + 7) / 8;
   const int cap = 4 * nos_effective_cus();
   const unsigned grid = (unsigned)(ngrp < cap ? ngrp : cap);
   const size_t lds = (size_t)M * K * 4;

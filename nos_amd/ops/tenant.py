@@ -384,9 +384,17 @@ def _pad_k_len(k: int) -> int:
 
 
 def linear_rms(x: torch.Tensor, wg: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
-               eps: float = 1e-6) -> torch.Tensor:
+               eps: float = 1e-6, glu: bool = False) -> torch.Tensor:
     """act(RMSNorm(x) @ (W * gamma)^T + b): the row statistics in the h3 split
-    pre-pass (``nos_split_rows_h3`` mode 2), gamma folded into ``wg``."""
+    pre-pass (``nos_split_rows_h3`` mode 2), gamma folded into ``wg``.
+    ``glu``: ``wg`` is a merged [gate; up] weight and the result is
+    silu(gate) * up (the GEMV's epilogue for decode rows)."""
+    if glu:
+        x2g = _f32(x).reshape(-1, x.shape[-1])
+        if not (x.is_cuda and x2g.shape[0] <= GEMV_MAX_ROWS and gemv_ok(x2g.contiguous(), wg)):
+            y = linear_rms(x, wg, bias, act, eps)
+            h = y.shape[-1] // 2
+            return (F.silu(y[..., :h].float()) * y[..., h:].float()).to(y.dtype)
     if not x.is_cuda:
         return linear_rms_ref(x, wg, bias, act, eps)
     dt = x.dtype
@@ -398,9 +406,11 @@ def linear_rms(x: torch.Tensor, wg: torch.Tensor, bias: torch.Tensor | None = No
     if x2.stride(-1) != 1:
         x2 = x2.contiguous()
     M = x2.shape[0]
+    if glu and not gemv_ok(x2, wg):
+        x2 = x2.clone()   # an aligned copy: the GLU form exists only on the GEMV
     if M <= GEMV_MAX_ROWS and gemv_ok(x2, wg):   # a decode step: the RMS statistics in the GEMV's prologue
-        out = gemv(x2, wg, bias, act, rms_eps=float(eps) or 1e-30)
-        out = out.view(*x.shape[:-1], N)
+        out = gemv(x2, wg, bias, act, rms_eps=float(eps) or 1e-30, glu=glu)
+        out = out.view(*x.shape[:-1], N // 2 if glu else N)
         return out if dt == torch.float32 else out.to(dt)
     planes = torch.empty((2, M, K), dtype=torch.float16, device=x.device)
     rinv = torch.empty((M,), dtype=torch.float32, device=x.device)
@@ -611,6 +621,7 @@ def argmax(x: torch.Tensor) -> torch.Tensor:
 
 GEMV_MAX_ROWS = 8
 EPI_SILU = 64  # decode.hip's GEMV: SiLU epilogue
+EPI_GLU = 256  # decode.hip's GEMV: W = [gate; up], y = silu(gate) * up
 
 
 def gemv_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
@@ -623,15 +634,16 @@ def gemv_ok(x2: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 def gemv(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
-         residual: torch.Tensor | None = None, out: torch.Tensor | None = None, rms_eps: float = 0.0) -> torch.Tensor:
+         residual: torch.Tensor | None = None, out: torch.Tensor | None = None, rms_eps: float = 0.0,
+         glu: bool = False) -> torch.Tensor:
     """y [M, N] = act(rms(x) [M, K] W^T + b) + R for M <= 8 (:func:`gemv_ok`):
     the weight-streaming kernel of a decode step, exact fp32 math; y, R in
     x's dtype, bias in W's.  ``rms_eps`` > 0: x rows RMS-normalised first
     (RMSNorm folded into the GEMM, gamma in W)."""
     M, K = x2.shape
     N = w.shape[0]
-    y = out if out is not None else torch.empty((M, N), dtype=x2.dtype, device=x2.device)
-    epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESID if residual is not None else 0)
+    y = out if out is not None else torch.empty((M, N // 2 if glu else N), dtype=x2.dtype, device=x2.device)
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESID if residual is not None else 0) | (EPI_GLU if glu else 0)
     epi |= {"gelu": EPI_GELU, "relu": EPI_RELU, "silu": EPI_SILU}.get(act or "", 0)
     b = None if bias is None else bias.to(w.dtype).contiguous()
     r = None if residual is None else residual.reshape(M, N).to(x2.dtype)

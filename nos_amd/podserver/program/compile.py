@@ -71,6 +71,7 @@ class Lowered:
             steps = self._fuse_rotary_sdpa(steps)
             steps = self._fuse_rotary_at(steps)
             steps = self._merge_kv_writes(steps)
+            steps = self._fuse_gemv_glu(steps)
             if "cat_buffer" not in skip:
                 steps = self._cat_into_buffer(steps)
             steps = self._mark_plane_handoffs(steps)
@@ -940,6 +941,44 @@ class Lowered:
             n += 1
         self.stats["rotary_at_fused"] = n
         return [s for s in steps if s.output not in drop]
+
+    def _fuse_gemv_glu(self, steps: list[_Step]) -> list[_Step]:
+        """Decode rows (at most 8, known statically): ``glu(silu)`` of the two
+        column halves of a merged gate-up ``linear_rms`` becomes that GEMV's
+        epilogue (each wave computes a gate and its up column), one launch
+        instead of two."""
+        from ...ops.tenant import GEMV_MAX_ROWS
+
+        if not self.gpu:
+            return steps
+        uses = self._consumers(steps, self.outputs)
+        by_out = {s.output: s for s in steps}
+        drop, n = set(), 0
+        for s in steps:
+            if s.kind != "glu" or s.attrs.get("op") != "silu":
+                continue
+            a, b = by_out.get(s.inputs[0]), by_out.get(s.inputs[1])
+            if a is None or b is None or a.kind != "slice" or b.kind != "slice" or a.inputs != b.inputs:
+                continue
+            lin = by_out.get(a.inputs[0])
+            shp = tuple(self._shape(lin.output)) if lin is not None else ()
+            if (lin is None or lin.kind != "linear_rms" or lin.attrs.get("act") or len(lin.inputs) > 2
+                    or uses.get(lin.output) != 2 or uses.get(a.output) != 1 or uses.get(b.output) != 1
+                    or math.prod(shp[:-1]) > GEMV_MAX_ROWS or shp[-1] % 2
+                    or any(t.attrs.get("dim") not in (-1, len(shp) - 1) for t in (a, b))
+                    or (a.attrs["start"], a.attrs["end"], b.attrs["start"], b.attrs["end"])
+                    != (0, shp[-1] // 2, shp[-1] // 2, shp[-1])):
+                continue
+            lin.attrs = {**lin.attrs, "glu": True}
+            self._new_shapes[lin.output] = shp[:-1] + (shp[-1] // 2,)
+            drop |= {id(a), id(b), id(s)}
+            rename = {s.output: lin.output}
+            for t in steps:
+                t.inputs = [rename.get(i, i) for i in t.inputs]
+            self.outputs = [rename.get(o, o) for o in self.outputs]
+            n += 1
+        self.stats["gemv_glu_fused"] = n
+        return [s for s in steps if id(s) not in drop]
 
     def _merge_kv_writes(self, steps: list[_Step]) -> list[_Step]:
         """A layer's K and V cache writes at the same position (the K one

@@ -85,7 +85,8 @@ class CompiledProgram(Lowered):
                              residual=res, w2=self.aux.get(s.attrs.get("w2")),
                              residual_first=bool(s.attrs.get("residual_first")), groups=s.attrs.get("groups", 1))
             elif k == "linear_rms":
-                y = T.linear_rms(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"), eps=s.attrs["eps"])
+                y = T.linear_rms(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"), eps=s.attrs["eps"],
+                                 glu=bool(s.attrs.get("glu")))
             elif k == "matmul":
                 y = T.matmul(a[0], a[1])
             elif k == "softmax":

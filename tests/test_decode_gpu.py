@@ -202,3 +202,32 @@ def test_decode_step_logits_match_fp64():
     e32 = float((f32.double() - ref64).abs().max() / ref64.abs().max())
     assert e <= max(4 * e32, 1e-5), (e, e32)
     assert state["pos"].tolist() == [11]
+
+
+@pytest.mark.parametrize("M", [1, 3, 8])
+def test_gemv_glu_epilogue_matches_fp64(M):
+    """SwiGLU in the merged gate-up GEMV's epilogue (RMS prologue too)."""
+    torch.manual_seed(M)
+    K, Nh = 1024, 2816
+    x = torch.randn(M, K, device="cuda")
+    w = torch.randn(2 * Nh, K, device="cuda") / 32
+    got = T.linear_rms(x, w, None, None, eps=1e-5, glu=True)
+    xd = x.double() * torch.rsqrt(x.double().pow(2).mean(-1, keepdim=True) + 1e-5)
+    y = xd @ w.double().t()
+    ref = torch.nn.functional.silu(y[:, :Nh]) * y[:, Nh:]
+    assert float((got.double() - ref).abs().max() / ref.abs().max()) < 2e-6
+
+
+def test_decode_program_uses_the_fused_decode_kernels():
+    """The GPU decode step: rotary fused into the cache write and the decode
+    attention, K and V written in one launch, SwiGLU in the gate-up GEMV."""
+    from nos_amd.models.llama_program import llama_decode_programs
+    from nos_amd.podserver import program as PG
+
+    m = _llama(False)
+    progs, w = llama_decode_programs(m, 8, 64)
+    ps = PG.parse_variants(progs, w, gpu=True)
+    c = ps[1].compile("cuda", params=ps[0].tensors("cuda"))
+    assert c.stats["rotary_at_fused"] == 4 and c.stats["kv_writes_paired"] == 2 and c.stats["gemv_glu_fused"] == 2
+    kinds = [s.kind for s in c.steps if s.kind not in ("slice", "reshape")]
+    assert kinds.count("kv_write") == 2 and "glu" not in kinds and "rotary_at" not in kinds
