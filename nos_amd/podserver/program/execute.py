@@ -102,7 +102,8 @@ class CompiledProgram(Lowered):
                            rope=(a[3], a[4]) if s.attrs.get("rope") else None)
             elif k == "layernorm":
                 xx = a[0].contiguous()
-                if xx.is_cuda and str(xx.dtype) == "torch.bfloat16":
+                D = xx.shape[-1]
+                if xx.is_cuda and str(xx.dtype) == "torch.bfloat16" and D % 8 == 0 and D <= 4096:   # 16-B rows
                     y, _ = ops.layernorm(xx, a[1], a[2], s.attrs.get("eps", 1e-5))
                 else:
                     import torch.nn.functional as F
