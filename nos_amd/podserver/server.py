@@ -61,10 +61,10 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import logging
 import os
-import queue
 import socket
 import threading
 import time
@@ -182,6 +182,43 @@ def _check_wire_dtype(sent, want: str, what: str) -> None:
         raise ValueError(f"{what} sent as {sent!r}, the tenant's model takes {want!r}")
 
 
+class _JobQueue:
+    """The lanes' work queue: two FIFOs, latency requests before throughput
+    ones.  ``get(hi_only=True)`` (a priority lane) waits for a latency
+    request only; ``close()`` makes every ``get`` return None."""
+
+    def __init__(self):
+        self._cv = threading.Condition()
+        self._hi: collections.deque = collections.deque()
+        self._lo: collections.deque = collections.deque()
+        self._closed = False
+
+    def put(self, job, hi: bool = False) -> None:
+        with self._cv:
+            (self._hi if hi else self._lo).append(job)
+            self._cv.notify_all()   # a priority lane may be the one waiting
+
+    def get(self, hi_only: bool = False):
+        with self._cv:
+            while True:   # what was queued before close() still runs
+                if self._hi:
+                    return self._hi.popleft()
+                if self._lo and not hi_only:
+                    return self._lo.popleft()
+                if self._closed:
+                    return None
+                self._cv.wait()
+
+    def qsize(self) -> int:
+        with self._cv:
+            return len(self._hi) + len(self._lo)
+
+    def close(self) -> None:
+        with self._cv:
+            self._closed = True
+            self._cv.notify_all()
+
+
 class PodServer:
     def __init__(self, socket_path: str | os.PathLike, device: str = "cuda", lanes: int = DEFAULT_LANES,
                  max_tenants: int = DEFAULT_MAX_TENANTS, memory_gb: float | None = None, graphs: bool = True,
@@ -197,10 +234,11 @@ class PodServer:
         are evicted.  ``register_timeout_s`` + payload / ``register_min_mb_s``:
         the deadline of a register payload once its header arrived (a stalled
         sender's claim is released and its connection closed).
-        ``priority_lanes``: lanes on high-priority streams that serve only
-        latency tenants (stateful decoders by default, or a register request
-        with ``"priority": "latency"``) from their own queue, so a generation
-        step is dispatched ahead of the throughput tenants' kernels."""
+        ``priority_lanes``: extra lanes on high-priority streams that serve
+        only latency tenants (stateful decoders by default, or a register
+        request with ``"priority": "latency"``); every lane takes a waiting
+        latency request before any throughput request, so a generation step
+        never queues behind throughput tenants' inferences."""
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.path = Path(socket_path)
@@ -213,8 +251,7 @@ class PodServer:
         self._next_id = 1
         self._lock = threading.Lock()          # tenant table
         self._build_lock = threading.Lock()    # one registration (build + capture + accounting) at a time
-        self._q: queue.Queue[_Job | None] = queue.Queue()
-        self._qhi: queue.Queue[_Job | None] = queue.Queue()   # latency tenants' requests
+        self._jobs = _JobQueue()   # latency tenants' requests dequeued first
         self.priority_lanes_n = max(0, int(priority_lanes))
         self._hi_lanes: list = []
         self._stop = threading.Event()
@@ -343,10 +380,7 @@ class PodServer:
                 pass
         for _, t in conns:
             t.join(timeout=30)
-        for _ in range(self.lanes_n):
-            self._q.put(None)
-        for _ in range(self.priority_lanes_n):
-            self._qhi.put(None)
+        self._jobs.close()
         for t in self._threads:
             t.join(timeout=10)
         with self._lock:
@@ -444,7 +478,7 @@ class PodServer:
                         else:
                             want = bool(want)
                         job = _Job(tenant, payload, want, shp)
-                        (self._qhi if tenant.latency and self.priority_lanes_n else self._q).put(job)
+                        self._jobs.put(job, hi=tenant.latency)
                         job.done.wait()
                         if job.error:
                             raise RuntimeError(job.error)
@@ -468,7 +502,7 @@ class PodServer:
                         _check_wire_dtype(req.get("dtype"), _wire_dtype(tenant.trainer.x), "input")
                         _check_wire_dtype(req.get("target_dtype"), _target_wire(tenant.trainer), "target")
                         job = _Job(tenant, payload, False, kind="train", x_bytes=xb)
-                        self._q.put(job)
+                        self._jobs.put(job)
                         job.done.wait()
                         if job.error:
                             raise RuntimeError(job.error)
@@ -885,24 +919,23 @@ class PodServer:
                    "train_steps": t.trainer.steps if t.trainer is not None else 0}
                   for t in self.tenants.values()]
             pending = len(self._pending)
-        return {"tenants": ts, "pending": pending, "server": self.info, "queued": self._q.qsize(), "pid": os.getpid(),
+        return {"tenants": ts, "pending": pending, "server": self.info, "queued": self._jobs.qsize(), "pid": os.getpid(),
                 "evictions": self.evictions}
 
     # ------------------------------------------------------------ lanes
     def _lane(self, i: int, hi: bool = False) -> None:
         import torch
 
-        q = self._qhi if hi else self._q
         lane = (self._hi_lanes if hi else self._lanes)[i] if self.gpu else None
         while True:
-            job = q.get()
+            job = self._jobs.get(hi_only=hi)
             if job is None:
                 return
             job.t_start = time.monotonic()
             with self._lock:
                 self._busy += 1
                 # no other tenant running or waiting
-                alone = self._busy == 1 and self._q.qsize() == 0 and self._qhi.qsize() == 0
+                alone = self._busy == 1 and self._jobs.qsize() == 0
             try:
                 self._run(job, lane, alone)
             except Exception as e:  # reported to that tenant only
@@ -916,7 +949,7 @@ class PodServer:
             t.gpu_s += job.t_end - job.t_start
             M.PODSERVER_INFERENCES.labels(self.gpu_label, t.pod).inc()
             M.PODSERVER_REQUEST_TIME.labels(self.gpu_label).observe(job.t_end - job.t_enq)
-            M.PODSERVER_QUEUED.labels(self.gpu_label).set(self._q.qsize())
+            M.PODSERVER_QUEUED.labels(self.gpu_label).set(self._jobs.qsize())
             job.done.set()
 
     def _run(self, job: _Job, lane, alone: bool = False) -> None:

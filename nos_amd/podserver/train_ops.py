@@ -16,7 +16,9 @@ backward).  Here both run on ``libnos_hip.so``:
   recomputes ``P`` from the saved log-sum-exp (no S x S tensor is ever kept:
   the live scores are ``B x H x C x S``), then ``dV += P^T dO_c``,
   ``dP = dO_c V^T``, ``dS = P (dP - rowsum(dO_c O_c))``, ``dQ_c = dS K``,
-  ``dK += dS^T Q_c`` -- the four products per chunk on the h3 GEMM.
+  ``dK += dS^T Q_c`` -- the four products per chunk on the h3 GEMM;
+* :class:`CrossEntropy` -- the classification loss from the rows'
+  log-sum-exp (no softmax kernel; the round-5 step ran ``F.cross_entropy``).
 
 The math is the textbook flash-attention backward (recompute from the
 log-sum-exp), organised for the h3 GEMM's batched form.  CPU tensors take the
@@ -153,9 +155,39 @@ def attention(q, k, v, causal: bool = False, scale: float | None = None):
     return ChunkedAttention.apply(q, k, v, bool(causal), sc)
 
 
+class CrossEntropy(torch.autograd.Function):
+    """Mean cross-entropy of logits x [N, C] against class ids t [N]
+    (``ignore_index`` -100, as ``F.cross_entropy``): the loss from the rows'
+    log-sum-exp, the gradient ``(exp(x - lse) - onehot(t)) / n_valid`` in one
+    elementwise pass and a scatter -- no softmax kernel, no [N, C]
+    probability tensor kept between forward and backward."""
+
+    @staticmethod
+    def forward(ctx, x, t):
+        valid = t != -100
+        tc = torch.where(valid, t, torch.zeros_like(t)).long()
+        lse = torch.logsumexp(x, -1)
+        nll = (lse - x.gather(1, tc[:, None]).squeeze(1)) * valid
+        n = valid.sum()
+        ctx.save_for_backward(x, tc, lse, valid, n)
+        return nll.sum() / n
+
+    @staticmethod
+    def backward(ctx, g):
+        x, tc, lse, valid, n = ctx.saved_tensors
+        d = torch.exp(x - lse[:, None])
+        d.scatter_add_(1, tc[:, None], -torch.ones_like(lse)[:, None])
+        return d * (valid.to(d.dtype) * (g / n))[:, None], None
+
+
+def cross_entropy(x, t):
+    return CrossEntropy.apply(x, t)
+
+
 def scores_bytes(b: int, h: int, sq: int, skv: int) -> int:
     """Live score bytes of :class:`ChunkedAttention` (a chunk's s, p, dp, ds)."""
     return 4 * b * h * min(sq, CHUNK) * skv * 4
 
 
-__all__ = ["H3Linear", "ChunkedAttention", "linear", "attention", "scores_bytes", "CHUNK"]
+__all__ = ["H3Linear", "ChunkedAttention", "CrossEntropy", "linear", "attention", "cross_entropy", "scores_bytes",
+           "CHUNK"]

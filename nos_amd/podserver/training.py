@@ -35,6 +35,7 @@ of build + capture against the slice.
 from __future__ import annotations
 
 import math
+import os
 
 from .program import Program, ProgramError, _eager, _qkv_views, _req
 
@@ -118,7 +119,6 @@ def train_bytes_estimate(prog: Program, spec: dict) -> int:
     # (train_ops.ChunkedAttention: per layer the saved log-sum-exp rows, the live
     # scores of one query chunk at a time; NOS_AMD_TRAIN_NATIVE=0: the full
     # B x H x Sq x Skv scores, masked copy and probabilities of every layer)
-    import os
 
     from .train_ops import scores_bytes
 
@@ -148,7 +148,6 @@ def _train_op(op: str, args: list, attrs: dict):
     (train_ops: h3 GEMMs for the forward and both backward products, chunked
     attention with a log-sum-exp recompute -- no S x S scores kept), the rest
     in PyTorch.  ``NOS_AMD_TRAIN_NATIVE=0``: PyTorch throughout (A/B)."""
-    import os
 
     native = os.environ.get("NOS_AMD_TRAIN_NATIVE", "1") != "0"
     if op == "attention":
@@ -314,6 +313,10 @@ class Trainer:
         out = self.module(self.x)[self.spec["output"]].float()
         if self.spec["loss"] == "mse":
             return F.mse_loss(out, self.y)
+        if out.is_cuda and os.environ.get("NOS_AMD_TRAIN_NATIVE", "1") != "0":
+            from .train_ops import cross_entropy
+
+            return cross_entropy(out.reshape(-1, out.shape[-1]), self.y.reshape(-1))
         return F.cross_entropy(out.reshape(-1, out.shape[-1]), self.y.reshape(-1))
 
     def _eager_step(self):

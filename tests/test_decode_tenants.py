@@ -270,3 +270,27 @@ def test_stateful_tenants_are_latency_tenants_on_the_priority_lanes(tenant, serv
         c.register("bad", progs[0], w, memory_limit_gb=1, priority="urgent")
     for x in (a, b, y, c):
         x.close()
+
+
+def test_job_queue_serves_latency_requests_first():
+    """Every lane takes a waiting latency request before a throughput one; a
+    priority lane takes latency requests only; close() drains, then stops."""
+    import threading
+
+    from nos_amd.podserver.server import _JobQueue
+
+    q = _JobQueue()
+    q.put("t1")
+    q.put("t2")
+    q.put("d1", hi=True)
+    assert q.get() == "d1" and q.get() == "t1"
+    got = []
+    th = threading.Thread(target=lambda: got.append(q.get(hi_only=True)))
+    th.start()
+    th.join(0.2)
+    assert th.is_alive() and not got          # t2 is not a priority lane's
+    q.put("d2", hi=True)
+    th.join(5)
+    assert got == ["d2"] and q.qsize() == 1
+    q.close()
+    assert q.get() == "t2" and q.get() is None and q.get(hi_only=True) is None

@@ -71,3 +71,20 @@ def test_the_estimate_keeps_no_full_score_tensor():
         p = PG.parse(*llama_program(m, s))
         est[s] = train_bytes_estimate(p, parse_train_spec({"loss": "cross_entropy", "optimizer": "adamw"}, p))
     assert est[4096] < 8 * est[1024]     # the S x S form would be ~16x
+
+
+def test_cross_entropy_matches_torch_with_ignored_rows():
+    import torch.nn.functional as F
+
+    from nos_amd.podserver.train_ops import cross_entropy
+
+    torch.manual_seed(0)
+    x = (torch.randn(37, 101, dtype=torch.float64) * 4).requires_grad_()
+    t = torch.randint(0, 101, (37,))
+    t[[3, 9]] = -100
+    x2 = x.detach().clone().requires_grad_()
+    loss, ref = cross_entropy(x, t), F.cross_entropy(x2, t)
+    loss.backward()
+    ref.backward()
+    torch.testing.assert_close(loss, ref, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(x.grad, x2.grad, rtol=1e-12, atol=1e-12)
