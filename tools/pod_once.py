@@ -49,6 +49,8 @@ def main() -> None:
     ops.set_gemm_f32_policy(cfg["gemm_f32"])
     ops.set_attention_f32_variant(cfg["attention_f32"])
     ops.set_f32_math(cfg["f32_math"])
+    ops.set_ln_handoff(cfg["ln_handoff"] == "on")
+    ops.set_gemm_f32h3_layout(cfg["h3_layout"])
     print("kernel config", cfg, flush=True)
     m, x = _build(a.dtype, 0, demo_input_hw())
     s = torch.cuda.Stream()
