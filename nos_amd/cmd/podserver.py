@@ -94,7 +94,11 @@ def main(argv=None) -> int:
     ap.add_argument("--socket", default="", help="explicit socket path (default <socket-dir>/gpu-<gpu>/server.sock)")
     ap.add_argument("--lanes", type=int, default=16, help="streams = hardware queues the tenants are served on")
     ap.add_argument("--priority-lanes", type=int, default=2,
-                    help="high-priority streams serving the latency tenants (stateful decoders) from their own queue")
+                    help="lanes serving only the latency tenants (stateful decoders); every lane takes latency "
+                         "requests first")
+    ap.add_argument("--latency-cus", type=int, default=0,
+                    help="CUs (multiple of 8, XCD-symmetric) reserved for the priority lanes; the other lanes' streams "
+                         "are CU-masked to the rest")
     ap.add_argument("--max-tenants", type=int, default=48)
     ap.add_argument("--memory-gb", type=float, default=0.0, help="slice memory the server admits (0 = the GPU's)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
@@ -112,7 +116,7 @@ def main(argv=None) -> int:
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     if args.gpus:
         rest = ["--socket-dir", args.socket_dir, "--lanes", str(args.lanes), "--priority-lanes",
-                str(args.priority_lanes), "--max-tenants", str(args.max_tenants),
+                str(args.priority_lanes), "--latency-cus", str(args.latency_cus), "--max-tenants", str(args.max_tenants),
                 "--memory-gb", str(args.memory_gb), "--device", args.device, "--log-level", args.log_level]
         if args.no_graphs:
             rest.append("--no-graphs")
@@ -142,6 +146,7 @@ def main(argv=None) -> int:
 
         lister = GrpcLister(args.pod_resources_socket)
     srv = PodServer(path, device=args.device, lanes=args.lanes, priority_lanes=args.priority_lanes,
+                    latency_cus=args.latency_cus,
                     max_tenants=args.max_tenants,
                     memory_gb=args.memory_gb or None, graphs=not args.no_graphs,
                     solo_graphs=not args.no_solo_graphs, allocations_dir=records, pod_resources=lister).start()

@@ -225,7 +225,8 @@ class PodServer:
                  kernel_config: dict | None = None, solo_graphs: bool = True,
                  allocations_dir: str | os.PathLike | None = None, pod_resources=None,
                  reap_interval_s: float = 1.0, max_inflight_register_gb: float = 16.0,
-                 register_timeout_s: float = 30.0, register_min_mb_s: float = 50.0, priority_lanes: int = 2):
+                 register_timeout_s: float = 30.0, register_min_mb_s: float = 50.0, priority_lanes: int = 2,
+                 latency_cus: int = 0):
         """``allocations_dir``: this GPU's allocation records (tokens
         required; allocations.py).  Without it admission is open: the client
         declares its slice, which must be > 0 when the server accounts
@@ -238,7 +239,11 @@ class PodServer:
         only latency tenants (stateful decoders by default, or a register
         request with ``"priority": "latency"``); every lane takes a waiting
         latency request before any throughput request, so a generation step
-        never queues behind throughput tenants' inferences."""
+        never queues behind throughput tenants' inferences.  ``latency_cus``
+        (a multiple of 8, XCD-symmetric): that many CUs reserved for the
+        priority lanes -- their streams are CU-masked to them and the other
+        lanes' to the rest, so a decode step's chain of small kernels never
+        waits for CUs held by a throughput tenant's long workgroups."""
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.path = Path(socket_path)
@@ -253,6 +258,10 @@ class PodServer:
         self._build_lock = threading.Lock()    # one registration (build + capture + accounting) at a time
         self._jobs = _JobQueue()   # latency tenants' requests dequeued first
         self.priority_lanes_n = max(0, int(priority_lanes))
+        self.latency_cus = int(latency_cus)
+        if self.latency_cus and (self.latency_cus % 8 or self.latency_cus < 0 or not self.priority_lanes_n):
+            raise ValueError("latency_cus must be a positive multiple of 8 (one share per XCD) with priority lanes")
+        self._masked: list = []   # CU-masked lane streams (latency_cus) to close at stop
         self._hi_lanes: list = []
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
@@ -302,13 +311,26 @@ class PodServer:
         total_gb = props.total_memory / 2 ** 30
         self.memory_gb = min(self.memory_gb or total_gb, total_gb)
         # lanes first: with GPU_MAX_HW_QUEUES >= lanes each gets its own HW queue
-        self._lanes = [torch.cuda.Stream() for _ in range(self.lanes_n)]
-        # latency lanes: the highest stream priority (HSA queue priority), dispatched first
-        hi = torch.cuda.Stream.priority_range()[1] if hasattr(torch.cuda.Stream, "priority_range") else -1
-        self._hi_lanes = [torch.cuda.Stream(priority=hi) for _ in range(self.priority_lanes_n)]
+        if self.latency_cus:
+            # CU mask bit i sits on XCD i mod 8: CUs 0 .. n-1 are n / 8 per XCD
+            from ..ops.streams import CUMaskedStream
+
+            ncu = props.multi_processor_count
+            if self.latency_cus >= ncu:
+                raise ValueError(f"latency_cus {self.latency_cus} leaves no CU of {ncu} to the other lanes")
+            rest = range(self.latency_cus, ncu)
+            self._masked = [CUMaskedStream(rest, ncu) for _ in range(self.lanes_n)]
+            self._masked += [CUMaskedStream(range(self.latency_cus), ncu) for _ in range(self.priority_lanes_n)]
+            self._lanes = [m.torch for m in self._masked[:self.lanes_n]]
+            self._hi_lanes = [m.torch for m in self._masked[self.lanes_n:]]
+        else:
+            self._lanes = [torch.cuda.Stream() for _ in range(self.lanes_n)]
+            # latency lanes: the highest stream priority (HSA queue priority), dispatched first
+            hi = torch.cuda.Stream.priority_range()[1] if hasattr(torch.cuda.Stream, "priority_range") else -1
+            self._hi_lanes = [torch.cuda.Stream(priority=hi) for _ in range(self.priority_lanes_n)]
         self._setup_stream = torch.cuda.Stream()
         self.info = {"device": props.name, "multiprocessor_count": props.multi_processor_count,
-                     "lanes": self.lanes_n, "priority_lanes": self.priority_lanes_n,
+                     "lanes": self.lanes_n, "priority_lanes": self.priority_lanes_n, "latency_cus": self.latency_cus,
                      "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                      "memory_gb": round(self.memory_gb, 1), "kernel_config": cfg,
                      "solo_kernel_config": self.solo_config,
@@ -397,6 +419,9 @@ class PodServer:
             import torch
 
             torch.cuda.synchronize()
+            for m in self._masked:
+                m.close()
+            self._masked = []
 
     def serve_forever(self) -> None:
         while not self._stop.is_set():

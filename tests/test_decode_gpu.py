@@ -150,19 +150,21 @@ def _llama(small: bool):
     return llama_model(llama_config(small), 0)
 
 
-@pytest.mark.parametrize("small", [False, True])
-def test_gpu_server_generation_matches_hf_generate(tmp_path, small):
+@pytest.mark.parametrize("small, latency_cus", [(False, 0), (True, 0), (False, 16)])
+def test_gpu_server_generation_matches_hf_generate(tmp_path, small, latency_cus):
     """Greedy generation on the GPU pod server (HIP graphs: prefill on the
     flash kernel, decode steps on decode.hip over device positions) gives
-    transformers' CPU fp32 generate's tokens."""
+    transformers' CPU fp32 generate's tokens -- also with 16 CUs reserved for
+    the latency lanes (their streams and the other lanes' CU-masked)."""
     from nos_amd.models.llama_program import llama_decode_programs
     from nos_amd.podserver.client import PodClient
     from nos_amd.podserver.server import PodServer
 
     m = _llama(small)
     progs, w = llama_decode_programs(m, 16, 256)
-    srv = PodServer(tmp_path / "g.sock", device="cuda", lanes=2, memory_gb=40).start()
+    srv = PodServer(tmp_path / "g.sock", device="cuda", lanes=2, memory_gb=40, latency_cus=latency_cus).start()
     try:
+        assert srv.info["latency_cus"] == latency_cus
         c = PodClient(srv.path, connect_timeout_s=60)
         c.register("llm", progs[0], w, memory_limit_gb=4, variants=progs[1:])
         prompt = np.random.default_rng(0).integers(0, m.config.vocab_size, (1, 16)).astype(np.int32)

@@ -294,3 +294,11 @@ def test_job_queue_serves_latency_requests_first():
     assert got == ["d2"] and q.qsize() == 1
     q.close()
     assert q.get() == "t2" and q.get() is None and q.get(hi_only=True) is None
+
+
+def test_latency_cus_must_be_xcd_symmetric(tmp_path):
+    from nos_amd.podserver.server import PodServer
+
+    for bad, pl in ((12, 2), (-8, 2), (16, 0)):
+        with pytest.raises(ValueError, match="latency_cus"):
+            PodServer(tmp_path / "s.sock", device="cpu", priority_lanes=pl, latency_cus=bad)

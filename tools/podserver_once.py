@@ -82,6 +82,7 @@ def main() -> None:
     ap.add_argument("--tenants", type=int, default=28)
     ap.add_argument("--lanes", type=int, default=16)
     ap.add_argument("--priority-lanes", type=int, default=2, help="high-priority lanes for the decode tenants")
+    ap.add_argument("--latency-cus", type=int, default=0, help="CUs reserved for the priority lanes (multiple of 8)")
     ap.add_argument("--window", type=float, default=8.0)
     ap.add_argument("--warmup", type=float, default=2.0)
     ap.add_argument("--slice-gb", type=float, default=10.0)
@@ -110,7 +111,7 @@ def main() -> None:
     from nos_amd.podserver.server import PodServer
 
     path = Path(tempfile.mkdtemp(prefix="nos_ps_", dir="/tmp")) / "gpu-0" / "server.sock"
-    srv = PodServer(path, device="cuda", lanes=a.lanes, priority_lanes=a.priority_lanes,
+    srv = PodServer(path, device="cuda", lanes=a.lanes, priority_lanes=a.priority_lanes, latency_cus=a.latency_cus,
                     max_tenants=max(48, a.tenants)).start()
     from nos_amd import ops
 
