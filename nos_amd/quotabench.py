@@ -695,6 +695,8 @@ def composed_for(gpus: int, tenant_slots_per_gpu: int = 25, slice_gb: int = 10, 
     b_per_gpu = -(-b_pods // gpus)
     a_pods = (gpus * ((tenant_slots_per_gpu * slice_gb - b_per_gpu * b_gb) // slice_gb) if isolate_team_b
               else max(half + 1, round(slots * 5 / 7)))
+    if isolate_team_b:   # borrowing stops at the quotas' total min (CapacityScheduling's PreFilter)
+        a_pods = min(a_pods, (2 * half * slice_gb - b_pods * b_gb) // slice_gb)
     return ComposedScenario(gpus=gpus, slice_gb=slice_gb, team_a_pods=a_pods,
                             team_b_pods=b_pods, min_gb=half * slice_gb, max_gb=slots * slice_gb,
                             tenants_per_gpu=tenant_slots_per_gpu + 1, isolate_team_b=isolate_team_b,

@@ -151,3 +151,16 @@ def test_partition_pods_start_as_tenants_and_finish(tmp_path):
     assert len(parts) == 8 and not (set(parts) & rt.running())
     assert res["phase_c"]["seconds"] >= 0
     assert not any(k.startswith("team-a/") for k in rt.running())
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_isolated_team_b_fits_small_nodes(tmp_path, gpus):
+    """The isolated variant on the node sizes the GPU bench runs (1 GPU):
+    team-a borrows only up to the quotas' total min, so every tenant it
+    submits is admitted (CapacityScheduling rejects borrowing past it)."""
+    from nos_amd.quotabench import RecordingRuntime, composed_for
+
+    sc = composed_for(gpus, pod_server_dir=str(tmp_path), isolate_team_b=True)
+    res = sc.run(RecordingRuntime())
+    assert res["phase_b_alone"]["ok"] and res["phase_a"]["ok"] and res["phase_a"]["team-a"]["over_quota"] > 0
+    assert res["concurrent_tenants"] == sc.team_a_pods + sc.team_b_pods + gpus
