@@ -93,7 +93,7 @@ def main(argv=None) -> int:
     ap.add_argument("--socket-dir", default="")
     ap.add_argument("--socket", default="", help="explicit socket path (default <socket-dir>/gpu-<gpu>/server.sock)")
     ap.add_argument("--lanes", type=int, default=16, help="streams = hardware queues the tenants are served on")
-    ap.add_argument("--priority-lanes", type=int, default=2,
+    ap.add_argument("--priority-lanes", type=int, default=0,
                     help="lanes serving only the latency tenants (stateful decoders); every lane takes latency "
                          "requests first")
     ap.add_argument("--latency-cus", type=int, default=0,

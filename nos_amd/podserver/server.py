@@ -225,7 +225,7 @@ class PodServer:
                  kernel_config: dict | None = None, solo_graphs: bool = True,
                  allocations_dir: str | os.PathLike | None = None, pod_resources=None,
                  reap_interval_s: float = 1.0, max_inflight_register_gb: float = 16.0,
-                 register_timeout_s: float = 30.0, register_min_mb_s: float = 50.0, priority_lanes: int = 2,
+                 register_timeout_s: float = 30.0, register_min_mb_s: float = 50.0, priority_lanes: int = 0,
                  latency_cus: int = 0):
         """``allocations_dir``: this GPU's allocation records (tokens
         required; allocations.py).  Without it admission is open: the client

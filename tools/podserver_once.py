@@ -81,7 +81,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--tenants", type=int, default=28)
     ap.add_argument("--lanes", type=int, default=16)
-    ap.add_argument("--priority-lanes", type=int, default=2, help="high-priority lanes for the decode tenants")
+    ap.add_argument("--priority-lanes", type=int, default=0, help="high-priority lanes for the decode tenants")
     ap.add_argument("--latency-cus", type=int, default=0, help="CUs reserved for the priority lanes (multiple of 8)")
     ap.add_argument("--window", type=float, default=8.0)
     ap.add_argument("--warmup", type=float, default=2.0)
