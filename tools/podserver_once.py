@@ -88,11 +88,11 @@ def main() -> None:
     ap.add_argument("--slice-gb", type=float, default=10.0)
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--pipeline", type=int, default=1, help="x6 GEMM software-pipelined K loop (1) or plain (0)")
-    ap.add_argument("--h3-layout", default="2x2", choices=["4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16"],
-                    help="h3 GEMM tile / wave layout / ring")
+    ap.add_argument("--h3-layout", default=None, choices=["4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16"],
+                    help="h3 GEMM tile / wave layout / ring (NOS_AMD_H3_LAYOUT: the server's kernel config)")
     ap.add_argument("--h3-attn-waves", type=int, default=8, choices=[4, 8], help="h3 attention waves per workgroup")
-    ap.add_argument("--lds-epi", type=int, default=1, help="plain fp32-C h3 GEMMs store C through LDS (1) or "
-                    "from the MFMA registers (0)")
+    ap.add_argument("--lds-epi", type=int, default=None, help="plain fp32-C h3 GEMMs store C through LDS (1) or "
+                    "from the MFMA registers (0) (NOS_AMD_H3_EPILOGUE: the server's kernel config)")
     ap.add_argument("--mix", default="", help="heterogeneous tenants instead of --tenants YOLOS pods, e.g. "
                     "yolos:20,bert:4,mlp:4 (bert = BERT-base-shaped fp32 encoder at seq 512, mlp = bf16 GEMM-MLP "
                     "probe, resnet = ResNet-18 at 224x224, llama = Llama decoder at seq 512, llama-ft = that decoder "
@@ -106,6 +106,12 @@ def main() -> None:
     a.tenants = len(kinds)
     # one hardware queue per lane: before anything initialises HIP (cmd/podserver.py)
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(a.lanes + a.priority_lanes, 32))
+    # kernel-config A/B knobs go through the server's config (env), which it re-applies around every
+    # capture -- a process-wide setter called after start() would be undone by the first registration
+    if a.h3_layout is not None:
+        os.environ["NOS_AMD_H3_LAYOUT"] = a.h3_layout
+    if a.lds_epi is not None:
+        os.environ["NOS_AMD_H3_EPILOGUE"] = "lds" if a.lds_epi else "reg"
     from nos_amd.models.yolos_program import demo_tenant
     from nos_amd.podserver.client import PodClient
     from nos_amd.podserver.server import PodServer
@@ -116,9 +122,7 @@ def main() -> None:
     from nos_amd import ops
 
     ops.set_gemm_f32x6_pipeline(bool(a.pipeline))  # process-wide: every capture below
-    ops.set_gemm_f32h3_layout(a.h3_layout)
     ops.set_attention_f32h3_waves(a.h3_attn_waves)
-    ops.set_gemm_f32h3_lds_epilogue(bool(a.lds_epi))
     try:
         t0 = time.monotonic()
         clients = [PodClient(path, connect_timeout_s=30) for _ in range(a.tenants)]
