@@ -183,8 +183,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   static_assert(APW * NW * 1024 == TA && WPW * NW * 1024 == 2 * BN * ROWB, "equal DMA count per wave");
   constexpr int LPS = APW + WPW;
   static_assert((RS - 2) * LPS < 64, "vmcnt range");
-  static_assert(MODE == 0 || (BM == 128 && BN == 128 && NW == 4 && BKT == 32 && RS == 2 && !BATCHED),
-                "the LayerNorm hand-off runs the 128 x 128, 2 x 2 tile");
+  static_assert(MODE == 0 || (BM == 128 && BN == 128 && NW == 4 && BKT == 32 && !BATCHED &&
+                              (RS == 2 || (MODE == 2 && RS == 3))),
+                "the LayerNorm hand-off runs the 128 x 128, 2 x 2 tile (the producer also on a 3-deep ring)");
   static_assert(MODE != 2 || BM * BN * 4 <= RS * STAGE, "the statistics tile fits the ring");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -586,11 +587,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
               if (has(EPI_RELU)) v = f32x2_t{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
               f16x2_t h0, h1;
               nos::split2h(v * splat2(osc), h0, h1);
+              // the halves by shifts of the packed words (an element extract h0[1] of the
+              // inline-asm / cvt_pk pair was stored as the LOW half by this compiler)
+              const unsigned hw = __builtin_bit_cast(unsigned, h0), lw = __builtin_bit_cast(unsigned, h1);
   #pragma unroll
               for (int u = 0; u < 2; ++u) {
                 const int rl = rl0 + u;
-                const unsigned short b0 = __builtin_bit_cast(unsigned short, h0[u]);
-                const unsigned short b1 = __builtin_bit_cast(unsigned short, h1[u]);
+                const unsigned short b0 = (unsigned short)(u ? hw >> 16 : hw);
+                const unsigned short b1 = (unsigned short)(u ? lw >> 16 : lw);
                 if (WIDE_FITS && wide) {
                   const int sl = rl * BN + ((((cl >> 3) ^ (rl & 15)) << 3) | (cl & 7));
                   T[sl] = b0;
@@ -771,6 +775,9 @@ int g_layout = 1;
 // plain fp32-C GEMMs (no KV / plane output, N % 4 == 0, aligned C / R) through
 // the LDS epilogue of MODE 2 (float4 stores and residual loads along rows)
 bool g_lds_epi = true;  // 28-tenant fleet 801 vs 799 inf/s, batch-1 residual GEMMs 15-18 % faster
+// LDS ring depth of the LDS-epilogue / row-statistics (MODE 2) GEMMs: 2 (64 KiB, two
+// workgroups per CU) or 3 (96 KiB, one workgroup per CU, stage k+2 in flight under k)
+int g_hot_ring = 2;
 
 // ------------------------------------------------------------ row split
 // LPR lanes per row (64: a wave; 32: a half-wave, two rows per wave), the
@@ -925,8 +932,14 @@ NOS_API int nos_gemm_f32h3_set_lds_epilogue(int on) {
 }
 
 NOS_API int nos_gemm_f32h3_set_layout(int layout) {
-  if (layout < 0 || layout > 5) return (int)hipErrorInvalidValue;
+  if (layout < 0 || layout > 6) return (int)hipErrorInvalidValue;
   g_layout = layout;
+  return 0;
+}
+
+NOS_API int nos_gemm_f32h3_set_hot_ring(int rs) {
+  if (rs != 2 && rs != 3) return (int)hipErrorInvalidValue;
+  g_hot_ring = rs;
   return 0;
 }
 
@@ -981,14 +994,21 @@ int run_h3(const void* Ap, int lda, long long aplane, const float* rinv, float r
   if (g_layout == 5)
     return launch_t<128, 128, 2, 2, 16, 4>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
                                            N, K, epi, kv, po, bt, stream);
+  if (g_layout == 6)
+    return launch_t<128, 128, 2, 2, 32, 3>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
+                                           N, K, epi, kv, po, bt, stream);
   if (g_layout == 2)
     return launch_t<256, 128, 4, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
                                     epi, kv, po, bt, stream);
   if (g_layout == 1) {
     if (g_lds_epi && kv.kvs == nullptr && po.p == nullptr && C != nullptr && !(N % 4) && !(ldc % 4) &&
-        !(((uintptr_t)C) & 15) && (!(epi & EPI_RESID) || (!(ldr % 4) && !(((uintptr_t)R) & 15))))
+        !(((uintptr_t)C) & 15) && (!(epi & EPI_RESID) || (!(ldr % 4) && !(((uintptr_t)R) & 15)))) {
+      if (g_hot_ring == 3)
+        return launch_t<128, 128, 2, 2, 32, 3, false, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R,
+                                                         ldr, C, ldc, M, N, K, epi, kv, po, bt, stream);
       return launch_t<128, 128, 2, 2, 32, 2, false, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr,
                                                        C, ldc, M, N, K, epi, kv, po, bt, stream);
+    }
     return launch_t<128, 128, 2, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
                                     epi, kv, po, bt, stream);
   }
@@ -1102,6 +1122,10 @@ NOS_API int nos_gemm_f32h3_stats(const void* Ap, int lda, long long aplane, cons
   LnIo ln;
   ln.sout = static_cast<float2*>(stats);
   ln.spart = (N + 127) / 128;
+  if (g_hot_ring == 3)
+    return launch_t<128, 128, 2, 2, 32, 3, false, 2>(static_cast<const _Float16*>(Ap), lda, aplane, rinv, rconst,
+                                                     static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
+                                                     C, ldc, M, N, K, epi, KvOut{}, PlaneOut{}, Batch{}, stream, ln);
   return launch_t<128, 128, 2, 2, 32, 2, false, 2>(static_cast<const _Float16*>(Ap), lda, aplane, rinv, rconst,
                                                    static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
                                                    C, ldc, M, N, K, epi, KvOut{}, PlaneOut{}, Batch{}, stream, ln);

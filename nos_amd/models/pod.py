@@ -172,7 +172,9 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
             # plain fp32-C h3 GEMMs store C through LDS (float4 rows): 801 vs 799 inf/s
             "h3_epilogue": env.get("NOS_AMD_H3_EPILOGUE") or "lds",
             # h3 GEMM tile layout (ops.set_gemm_f32h3_layout; the LN hand-off GEMMs keep 2x2)
-            "h3_layout": env.get("NOS_AMD_H3_LAYOUT") or "2x2"}
+            "h3_layout": env.get("NOS_AMD_H3_LAYOUT") or "2x2",
+            # LDS ring of the residual (row-statistics) h3 GEMMs: "2" or "3" stages
+            "h3_hot_ring": env.get("NOS_AMD_H3_HOT_RING") or "2"}
 
 
 def slice_cu_budget(env: dict | None = None) -> int:
@@ -269,7 +271,8 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             frac = apply_memory_limit(0)
             torch.backends.cuda.matmul.allow_tf32 = False  # true fp32 GEMMs (no reduced-precision shortcut)
             from ..ops import (set_attention_f32_variant, set_cu_budget, set_f32_math, set_gemm_f32_policy,
-                               set_gemm_f32h3_layout, set_gemm_f32x6_tile, set_gemm_policy, set_ln_handoff)
+                               set_gemm_f32h3_hot_ring, set_gemm_f32h3_layout, set_gemm_f32x6_tile, set_gemm_policy,
+                               set_ln_handoff)
 
             budget = slice_cu_budget(os.environ)
             cfg = kernel_config(frac, os.environ, budget)
@@ -280,6 +283,7 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             set_gemm_f32x6_tile(cfg["gemm_f32x6_tile"])
             set_ln_handoff(cfg["ln_handoff"] == "on")
             set_gemm_f32h3_layout(cfg["h3_layout"])
+            set_gemm_f32h3_hot_ring(int(cfg["h3_hot_ring"]))
             if budget:  # CU-mask slice: slice-sized persistent grids (ops.set_cu_budget)
                 set_cu_budget(budget)
         m, x = _build(dtype, seed, demo_input_hw(), device)

@@ -457,14 +457,22 @@ def set_gemm_f32h3_lds_epilogue(on: bool) -> None:
     _lib.check(_lib.lib().nos_gemm_f32h3_set_lds_epilogue(int(bool(on))), "nos_gemm_f32h3_set_lds_epilogue")
 
 
+def set_gemm_f32h3_hot_ring(stages: int) -> None:
+    """LDS ring depth of the row-statistics / LDS-epilogue h3 GEMMs (the
+    residual GEMMs of a transformer): 2 (64 KiB, two workgroups per CU) or 3
+    (96 KiB, one workgroup per CU; a stage two ahead in flight)."""
+    _lib.check(_lib.lib().nos_gemm_f32h3_set_hot_ring(int(stages)), "nos_gemm_f32h3_set_hot_ring")
+
+
 def set_gemm_f32h3_layout(layout: str) -> None:
     """h3 GEMM tiles / waves: ``"2x2"`` (default: 128x128, 64x64 per wave),
     ``"4x1"`` (128x128, 32-row strips, each wave reads the whole W tile),
     ``"256x128"`` (8 waves of 64x64, one workgroup per CU), ``"4x1r3"``
     (3-deep ring of BK-32 stages), ``"4x1k16"`` / ``"2x2k16"`` (4-deep ring
-    of BK-16 stages) -- A/B; the results are bit-identical."""
+    of BK-16 stages), ``"2x2r3"`` (2x2, 3-deep BK-32 ring) -- A/B; the
+    results are bit-identical."""
     _lib.check(_lib.lib().nos_gemm_f32h3_set_layout({"4x1": 0, "2x2": 1, "256x128": 2, "4x1r3": 3, "4x1k16": 4,
-                                                     "2x2k16": 5}[layout]),
+                                                     "2x2k16": 5, "2x2r3": 6}[layout]),
                "nos_gemm_f32h3_set_layout")
 
 
@@ -948,5 +956,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_ln_handoff", "ln_handoff_active", "set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "H3Planes", "set_attention_f32h3_waves", "linear_planes", "linear_ln_to_planes", "h3_planes_active", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_ln_handoff", "ln_handoff_active", "set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "set_gemm_f32h3_hot_ring", "H3Planes", "set_attention_f32h3_waves", "linear_planes", "linear_ln_to_planes", "h3_planes_active", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

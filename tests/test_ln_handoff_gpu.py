@@ -38,8 +38,20 @@ def _parts(y64: torch.Tensor, pw: int) -> torch.Tensor:
     return torch.stack(out, 1)
 
 
+@pytest.mark.parametrize("ring", [2, 3])
 @pytest.mark.parametrize("M,N,K", [(3401, 384, 384), (3401, 384, 1536), (100, 768, 384), (257, 132, 64)])
-def test_residual_gemm_writes_its_row_statistics(M, N, K):
+def test_residual_gemm_writes_its_row_statistics(M, N, K, ring):
+    """Also on the 3-deep LDS ring (ops.set_gemm_f32h3_hot_ring): C bit-identical."""
+    ops.set_gemm_f32h3_hot_ring(ring)
+    try:
+        y = _stats_case(M, N, K)
+    finally:
+        ops.set_gemm_f32h3_hot_ring(2)
+    if ring != 2:
+        assert torch.equal(y, _stats_case(M, N, K))
+
+
+def _stats_case(M, N, K):
     g = torch.Generator(device="cuda").manual_seed(M + N)
     x = torch.randn(M, K, device="cuda", generator=g)
     w = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
@@ -57,6 +69,7 @@ def test_residual_gemm_writes_its_row_statistics(M, N, K):
     scale = y.double().abs().amax(1, keepdim=True)
     assert ((got[..., 0] - ref[..., 0]).abs() <= 4e-6 * scale).all()
     assert ((got[..., 1] - ref[..., 1]).abs() <= 1e-5 * ref[..., 1] + 1e-30).all()
+    return y
 
 
 def _ln64(x, wg, c2, eps):

@@ -88,8 +88,10 @@ def main() -> None:
     ap.add_argument("--slice-gb", type=float, default=10.0)
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--pipeline", type=int, default=1, help="x6 GEMM software-pipelined K loop (1) or plain (0)")
-    ap.add_argument("--h3-layout", default=None, choices=["4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16"],
+    ap.add_argument("--h3-layout", default=None, choices=["4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16", "2x2r3"],
                     help="h3 GEMM tile / wave layout / ring (NOS_AMD_H3_LAYOUT: the server's kernel config)")
+    ap.add_argument("--h3-hot-ring", default=None, choices=["2", "3"],
+                    help="LDS ring of the residual / row-statistics h3 GEMMs (NOS_AMD_H3_HOT_RING)")
     ap.add_argument("--h3-attn-waves", type=int, default=8, choices=[4, 8], help="h3 attention waves per workgroup")
     ap.add_argument("--lds-epi", type=int, default=None, help="plain fp32-C h3 GEMMs store C through LDS (1) or "
                     "from the MFMA registers (0) (NOS_AMD_H3_EPILOGUE: the server's kernel config)")
@@ -110,6 +112,8 @@ def main() -> None:
     # capture -- a process-wide setter called after start() would be undone by the first registration
     if a.h3_layout is not None:
         os.environ["NOS_AMD_H3_LAYOUT"] = a.h3_layout
+    if a.h3_hot_ring is not None:
+        os.environ["NOS_AMD_H3_HOT_RING"] = a.h3_hot_ring
     if a.lds_epi is not None:
         os.environ["NOS_AMD_H3_EPILOGUE"] = "lds" if a.lds_epi else "reg"
     from nos_amd.models.yolos_program import demo_tenant
