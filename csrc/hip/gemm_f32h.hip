@@ -91,29 +91,6 @@ __device__ __forceinline__ float erf_fast(float x) {
   return copysignf(r, x);
 }
 
-// packed-fp32 forms for pairs of accumulator registers (v_pk_fma_f32 / v_pk_mul_f32:
-// two lanes' worth of math per VALU issue; the transcendentals stay per element).
-// Bit-identical to the scalar forms: the same IEEE fma / mul sequence.
-__device__ __forceinline__ f32x2_t splat2(float v) { return f32x2_t{v, v}; }
-__device__ __forceinline__ f32x2_t fma2(f32x2_t a, f32x2_t b, f32x2_t c) { return __builtin_elementwise_fma(a, b, c); }
-
-// GELU(v) = 0.5 v (1 + erf(v / sqrt 2)) on a pair, erf as erf_fast
-__device__ __forceinline__ f32x2_t gelu2(f32x2_t v) {
-  const f32x2_t z = v * splat2(0.70710678118654752f);
-  const f32x2_t az = f32x2_t{fabsf(z.x), fabsf(z.y)};
-  const f32x2_t d = fma2(splat2(0.3275911f), az, splat2(1.f));
-  const f32x2_t t = f32x2_t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-  f32x2_t p = fma2(splat2(1.061405429f), t, splat2(-1.453152027f));
-  p = fma2(p, t, splat2(1.421413741f));
-  p = fma2(p, t, splat2(-0.284496736f));
-  p = fma2(p, t, splat2(0.254829592f));
-  const f32x2_t q = (-az * az) * splat2(1.4426950408889634f);
-  const f32x2_t e = f32x2_t{__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
-  f32x2_t r = fma2(-p * t, e, splat2(1.f));
-  r = f32x2_t{copysignf(r.x, z.x), copysignf(r.y, z.y)};
-  return (splat2(0.5f) * v) * (splat2(1.f) + r);
-}
-
 // the K / V columns (>= qcols) of a fused QKV projection as the h3
 // attention's planes kvs[b][s][K hi, K lo, V hi, V lo][hd], each head on
 // kvsc[0 / 1][head]; rows per batch S, padded to skvp
@@ -321,11 +298,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         const int row = (tid >> 2) + 64 * i;
         const float4 u = xa[i][0], w = xa[i][1];
         f16x2_t h0, l0, h1, l1, h2, l2, h3, l3;
-        const f32x2_t m2 = splat2(mul[i]), a2 = splat2(add[i]);
-        nos::split2h(fma2(f32x2_t{u.x, u.y}, m2, a2), h0, l0);
-        nos::split2h(fma2(f32x2_t{u.z, u.w}, m2, a2), h1, l1);
-        nos::split2h(fma2(f32x2_t{w.x, w.y}, m2, a2), h2, l2);
-        nos::split2h(fma2(f32x2_t{w.z, w.w}, m2, a2), h3, l3);
+        nos::split2h(f32x2_t{fmaf(u.x, mul[i], add[i]), fmaf(u.y, mul[i], add[i])}, h0, l0);
+        nos::split2h(f32x2_t{fmaf(u.z, mul[i], add[i]), fmaf(u.w, mul[i], add[i])}, h1, l1);
+        nos::split2h(f32x2_t{fmaf(w.x, mul[i], add[i]), fmaf(w.y, mul[i], add[i])}, h2, l2);
+        nos::split2h(f32x2_t{fmaf(w.z, mul[i], add[i]), fmaf(w.w, mul[i], add[i])}, h3, l3);
         const int off = row * ROWB + ((q ^ swz<CH>(row)) << 4);
         *reinterpret_cast<f16x8_t*>(dst + off) = f16x8_t{h0.x, h0.y, h1.x, h1.y, h2.x, h2.y, h3.x, h3.y};
         *reinterpret_cast<f16x8_t*>(dst + BM * ROWB + off) = f16x8_t{l0.x, l0.y, l1.x, l1.y, l2.x, l2.y, l3.x, l3.y};
@@ -479,14 +455,12 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   #pragma unroll
           for (int i = 0; i < MI; ++i) {
   #pragma unroll
-            for (int r = 0; r < 16; r += 2) {   // register pairs: packed fp32 math
+            for (int r = 0; r < 16; ++r) {
               const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-              f32x2_t v = fma2(f32x2_t{acc[i][j][r], acc[i][j][r + 1]}, f32x2_t{rsv[i][r], rsv[i][r + 1]} * splat2(cs),
-                               splat2(p2));
-              if (has(EPI_GELU)) v = gelu2(v);
-              if (has(EPI_RELU)) v = f32x2_t{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
-              T[rl * BN + cl] = v.x;   // r + 1 is the next row (r even: (r & 3) < 3)
-              T[(rl + 1) * BN + cl] = v.y;
+              float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2);
+              if (has(EPI_GELU)) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+              if (has(EPI_RELU)) v = fmaxf(v, 0.f);
+              T[rl * BN + cl] = v;
             }
           }
         }
@@ -579,31 +553,22 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   #pragma unroll
           for (int i = 0; i < MI; ++i) {
   #pragma unroll
-            for (int r = 0; r < 16; r += 2) {   // register pairs (rows rl, rl + 1): packed fp32 math
-              const int rl0 = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-              f32x2_t v = fma2(f32x2_t{acc[i][j][r], acc[i][j][r + 1]}, f32x2_t{rsv[i][r], rsv[i][r + 1]} * splat2(cs),
-                               splat2(p2) + f32x2_t{rbv[i][r], rbv[i][r + 1]});
-              if (has(EPI_GELU)) v = gelu2(v);
-              if (has(EPI_RELU)) v = f32x2_t{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
-              f16x2_t h0, h1;
-              nos::split2h(v * splat2(osc), h0, h1);
-              // the halves by shifts of the packed words (an element extract h0[1] of the
-              // inline-asm / cvt_pk pair was stored as the LOW half by this compiler)
-              const unsigned hw = __builtin_bit_cast(unsigned, h0), lw = __builtin_bit_cast(unsigned, h1);
-  #pragma unroll
-              for (int u = 0; u < 2; ++u) {
-                const int rl = rl0 + u;
-                const unsigned short b0 = (unsigned short)(u ? hw >> 16 : hw);
-                const unsigned short b1 = (unsigned short)(u ? lw >> 16 : lw);
-                if (WIDE_FITS && wide) {
-                  const int sl = rl * BN + ((((cl >> 3) ^ (rl & 15)) << 3) | (cl & 7));
-                  T[sl] = b0;
-                  T[BM * BN + sl] = b1;
-                } else {
-                  const unsigned off = (unsigned)(rl * ld + cl);
-                  hi[off] = b0;
-                  hi[lo_off + off] = b1;
-                }
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+              float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
+              if (has(EPI_GELU)) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+              if (has(EPI_RELU)) v = fmaxf(v, 0.f);
+              const float x = v * osc;
+              const _Float16 h0 = (_Float16)x;
+              const _Float16 h1 = (_Float16)(x - (float)h0);
+              if (WIDE_FITS && wide) {
+                const int sl = rl * BN + ((((cl >> 3) ^ (rl & 15)) << 3) | (cl & 7));
+                T[sl] = __builtin_bit_cast(unsigned short, h0);
+                T[BM * BN + sl] = __builtin_bit_cast(unsigned short, h1);
+              } else {
+                const unsigned off = (unsigned)(rl * ld + cl);
+                hi[off] = __builtin_bit_cast(unsigned short, h0);
+                hi[lo_off + off] = __builtin_bit_cast(unsigned short, h1);
               }
             }
           }
@@ -635,17 +600,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   #pragma unroll
           for (int i = 0; i < MI; ++i) {
   #pragma unroll
-            for (int r = 0; r < 16; r += 2) {   // register pairs (rows rl, rl + 1): packed fp32 math
+            for (int r = 0; r < 16; ++r) {
               const int rl = wm * (BM / WGM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-              const unsigned o0 = (unsigned)(rl * ldr + cl), o1 = o0 + (unsigned)ldr;
-              f32x2_t v = fma2(f32x2_t{acc[i][j][r], acc[i][j][r + 1]}, f32x2_t{rsv[i][r], rsv[i][r + 1]} * splat2(cs),
-                               splat2(p2) + f32x2_t{rbv[i][r], rbv[i][r + 1]});
-              if (BATCHED && has(EPI_RESID_PRE)) v += f32x2_t{Rt[o0], Rt[o1]};
-              if (has(EPI_GELU)) v = gelu2(v);
-              if (has(EPI_RELU)) v = f32x2_t{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
-              if (has(EPI_RESID)) v += f32x2_t{Rt[o0], Rt[o1]};
-              Ct[(unsigned)(rl * ldc + cl)] = v.x;
-              Ct[(unsigned)((rl + 1) * ldc + cl)] = v.y;
+              float v = fmaf(acc[i][j][r], rsv[i][r] * cs, p2 + rbv[i][r]);
+              if (BATCHED && has(EPI_RESID_PRE)) v += Rt[(unsigned)(rl * ldr + cl)];
+              if (has(EPI_GELU)) v = 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752f));
+              if (has(EPI_RELU)) v = fmaxf(v, 0.f);
+              if (has(EPI_RESID)) v += Rt[(unsigned)(rl * ldr + cl)];
+              Ct[(unsigned)(rl * ldc + cl)] = v;
             }
           }
         }
@@ -776,7 +738,8 @@ int g_layout = 1;
 // the LDS epilogue of MODE 2 (float4 stores and residual loads along rows)
 bool g_lds_epi = true;  // 28-tenant fleet 801 vs 799 inf/s, batch-1 residual GEMMs 15-18 % faster
 // LDS ring depth of the LDS-epilogue / row-statistics (MODE 2) GEMMs: 2 (64 KiB, two
-// workgroups per CU) or 3 (96 KiB, one workgroup per CU, stage k+2 in flight under k)
+// workgroups per CU) or 3 (96 KiB, one workgroup per CU, stage k+2 in flight under k):
+// 28-tenant fleet 792 (3) vs 802 (2) inf/s, profiles/r06_packed_epilogue_rejected.json
 int g_hot_ring = 2;
 
 // ------------------------------------------------------------ row split
