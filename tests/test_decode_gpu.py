@@ -162,7 +162,8 @@ def test_gpu_server_generation_matches_hf_generate(tmp_path, small, latency_cus)
 
     m = _llama(small)
     progs, w = llama_decode_programs(m, 16, 256)
-    srv = PodServer(tmp_path / "g.sock", device="cuda", lanes=2, memory_gb=40, latency_cus=latency_cus).start()
+    srv = PodServer(tmp_path / "g.sock", device="cuda", lanes=2, memory_gb=40, latency_cus=latency_cus,
+                    priority_lanes=2 if latency_cus else 0).start()
     try:
         assert srv.info["latency_cus"] == latency_cus
         c = PodClient(srv.path, connect_timeout_s=60)
