@@ -83,6 +83,7 @@ def main() -> None:
     ap.add_argument("--lanes", type=int, default=16)
     ap.add_argument("--priority-lanes", type=int, default=0, help="high-priority lanes for the decode tenants")
     ap.add_argument("--latency-cus", type=int, default=0, help="CUs reserved for the priority lanes (multiple of 8)")
+    ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES (0: lanes + priority lanes)")
     ap.add_argument("--window", type=float, default=8.0)
     ap.add_argument("--warmup", type=float, default=2.0)
     ap.add_argument("--slice-gb", type=float, default=10.0)
@@ -107,7 +108,7 @@ def main() -> None:
              if a.mix else ["yolos"] * a.tenants)
     a.tenants = len(kinds)
     # one hardware queue per lane: before anything initialises HIP (cmd/podserver.py)
-    os.environ["GPU_MAX_HW_QUEUES"] = str(min(a.lanes + a.priority_lanes, 32))
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(a.hw_queues or (a.lanes + a.priority_lanes), 32))
     # kernel-config A/B knobs go through the server's config (env), which it re-applies around every
     # capture -- a process-wide setter called after start() would be undone by the first registration
     if a.h3_layout is not None:
