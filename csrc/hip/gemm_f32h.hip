@@ -849,6 +849,66 @@ __global__ __launch_bounds__(256) void split_rows_h3_kernel(const float* __restr
   if (lane == 0) rinv[row] = nos::pow2i(-e);
 }
 
+// Column split (the transposed operand of a GEMM, training backward): the
+// COLUMNS of fp32 X [M, K] (row stride ldx, batch stride bsx) become the rows
+// of hi / lo fp16 planes [2][nb * K][ldp] (row b * K + k = column k of batch
+// b, zero-padded from M to Mp = ldp's used length), each on its own
+// power-of-two scale, rinv[b * K + k] = 2^-e: what transposing X into a
+// contiguous copy and splitting its rows gave, without the strided copy.
+// Pass 1: per column and row chunk, max |x| (coalesced along the rows).
+constexpr int COLS_NCH = 32;  // row chunks of the column maxima
+__global__ __launch_bounds__(256) void col_absmax_kernel(const float* __restrict__ X, int ldx, long long bsx, int M,
+                                                         int K, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + tx, c = blockIdx.y, b = blockIdx.z;
+  const int rpc = (M + COLS_NCH - 1) / COLS_NCH, m0 = c * rpc, m1 = min(M, m0 + rpc);
+  const float* x = X + (long long)b * bsx;
+  float mx = 0.f;
+  if (k < K)
+    for (int m = m0 + ty; m < m1; m += 4) mx = fmaxf(mx, fabsf(x[(long long)m * ldx + k]));
+  red[ty][tx] = mx;
+  __syncthreads();
+  if (ty == 0 && k < K)
+    part[((long long)b * COLS_NCH + c) * K + k] = fmaxf(fmaxf(red[0][tx], red[1][tx]), fmaxf(red[2][tx], red[3][tx]));
+}
+
+// Pass 2: a 64 x 64 tile of X through LDS; thread (k, q) writes 16
+// consecutive row-elements of output row k as two 16-byte chunks per plane
+__global__ __launch_bounds__(256) void split_cols_h3_kernel(const float* __restrict__ X, int ldx, long long bsx, int M,
+                                                            int K, int Mp, const float* __restrict__ part,
+                                                            _Float16* __restrict__ P, int ldp, long long pplane,
+                                                            float* __restrict__ rinv) {
+  __shared__ float tile[64][65];
+  const int t = threadIdx.x, k0 = blockIdx.x * 64, m0 = blockIdx.y * 64, b = blockIdx.z;
+  const float* x = X + (long long)b * bsx;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int e = t + 256 * i, r = e >> 6, cc = e & 63;
+    const int m = m0 + r, k = k0 + cc;
+    tile[r][cc] = (m < M && k < K) ? x[(long long)m * ldx + k] : 0.f;
+  }
+  __syncthreads();
+  const int kk = t >> 2, q = t & 3, k = k0 + kk;
+  if (k >= K || m0 + q * 16 >= Mp) return;
+  float mx = 0.f;
+#pragma unroll 8
+  for (int c = 0; c < COLS_NCH; ++c) mx = fmaxf(mx, part[((long long)b * COLS_NCH + c) * K + k]);
+  const int e = nos::h3_scale_exp(mx);
+  const float sc = nos::pow2i(e);
+  f16x2_t h[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    nos::split2h(f32x2_t{tile[q * 16 + 2 * j][kk] * sc, tile[q * 16 + 2 * j + 1][kk] * sc}, h[j], l[j]);
+  _Float16* ph = P + ((long long)b * K + k) * ldp + m0 + q * 16;
+  *reinterpret_cast<f16x8_t*>(ph) = f16x8_t{h[0].x, h[0].y, h[1].x, h[1].y, h[2].x, h[2].y, h[3].x, h[3].y};
+  *reinterpret_cast<f16x8_t*>(ph + 8) = f16x8_t{h[4].x, h[4].y, h[5].x, h[5].y, h[6].x, h[6].y, h[7].x, h[7].y};
+  *reinterpret_cast<f16x8_t*>(ph + pplane) = f16x8_t{l[0].x, l[0].y, l[1].x, l[1].y, l[2].x, l[2].y, l[3].x, l[3].y};
+  *reinterpret_cast<f16x8_t*>(ph + pplane + 8) =
+      f16x8_t{l[4].x, l[4].y, l[5].x, l[5].y, l[6].x, l[6].y, l[7].x, l[7].y};
+  if (blockIdx.y == 0 && q == 0) rinv[(long long)b * K + k] = nos::pow2i(-e);
+}
+
 // per-row (mean, M2) of fp32 rows over all K columns (one statistics part): a
 // half-wave per row, the row read twice (the second pass from cache)
 __global__ __launch_bounds__(256) void row_stats_kernel(const float* __restrict__ X, int ldx, float2* __restrict__ out,
@@ -933,6 +993,26 @@ NOS_API int nos_split_rows_h3(const float* A, int lda, void* P, int ldp, long lo
                        eln);
   else
     hipLaunchKernelGGL(split_rows_h3_kernel<0>, grid, blk, 0, stream, A, lda, p, ldp, pplane, rinv, M, K, ln, eps, eln);
+  return (int)hipGetLastError();
+}
+
+// The columns of fp32 X [nb][M, K] (row stride ldx, batch stride bsx; 16-byte
+// aligned not required) as h3 plane rows: P [2][nb * K][ldp] (plane stride
+// pplane elements), row b * K + k = column k of batch b over Mp = ceil32(M)
+// elements (zeros past M), rinv [nb * K]; work: COLS_NCH * nb * K floats.
+NOS_API int nos_split_cols_h3(const float* X, int ldx, long long bsx, int M, int K, int nb, void* P, int ldp,
+                              long long pplane, float* rinv, float* work, hipStream_t stream) {
+  const int Mp = (M + 31) / 32 * 32;
+  if (M <= 0 || K <= 0 || nb <= 0 || ldx < K || (nb > 1 && bsx < (long long)(M - 1) * ldx + K) || ldp < Mp ||
+      (ldp % 8) || pplane < (long long)nb * K * ldp || !X || !P || !rinv || !work || nb > 65535 ||
+      (long long)(M + 63) / 64 > 65535)
+    return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)P) & 15) || (pplane % 8)) return (int)hipErrorInvalidValue;
+  const unsigned gk = (unsigned)((K + 63) / 64);
+  hipLaunchKernelGGL(col_absmax_kernel, dim3(gk, COLS_NCH, (unsigned)nb), dim3(256), 0, stream, X, ldx, bsx, M, K,
+                     work);
+  hipLaunchKernelGGL(split_cols_h3_kernel, dim3(gk, (unsigned)((Mp + 63) / 64), (unsigned)nb), dim3(256), 0, stream, X,
+                     ldx, bsx, M, K, Mp, work, static_cast<_Float16*>(P), ldp, pplane, rinv);
   return (int)hipGetLastError();
 }
 

@@ -40,6 +40,8 @@ _SIGS = {
     "nos_attn_fwd_f32h3_presplit_d64": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_ll, c_int, c_ll,
                                         c_float, c_void_p, c_void_p, c_ll, c_void_p, c_ll, c_float, c_void_p],
     "nos_attn_f32x6_set_kvsplit": [c_int],
+    "nos_split_cols_h3": [c_void_p, c_int, c_ll, c_int, c_int, c_int, c_void_p, c_int, c_ll, c_void_p, c_void_p,
+                          c_void_p],
     "nos_split_rows_h3": [c_void_p, c_int, c_void_p, c_int, c_ll, c_void_p, c_int, c_int, c_int, c_float, c_int,
                           c_void_p],
     "nos_gemm_f32h3": [c_void_p, c_int, c_ll, c_void_p, c_float, c_void_p, c_int, c_ll, c_void_p, c_void_p,
@@ -152,9 +154,16 @@ def _load() -> ctypes.CDLL:
             fn = getattr(L, name)
         except AttributeError:
             # an older library named by NOS_AMD_HIP_LIB (A/B runs against the previous build):
-            # a config setter it lacks leaves that config at its default
-            if override and "_set_" in name:
-                setattr(L, name, lambda *a: 0)
+            # a config setter it lacks leaves that config at its default, any other entry
+            # point it lacks raises when called
+            if override:
+                if "_set_" in name:
+                    setattr(L, name, lambda *a: 0)
+                else:
+                    def _missing(*a, _n=name):
+                        raise NativeUnavailable(f"{_LIB_PATH} has no {_n}")
+
+                    setattr(L, name, _missing)
                 continue
             raise
         fn.argtypes = argtypes

@@ -355,28 +355,65 @@ def patches(x: torch.Tensor, ph: int, pw: int, dtype: torch.dtype = torch.float3
     return ops.H3Planes(planes, prinv, 0.0, (N, P, K))
 
 
-def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """a [..., M, K] @ b [..., K, N]; batch dims equal, or one side 2-D."""
+COLS_NCH = 32   # gemm_f32h.hip: row chunks of the column maxima (nos_split_cols_h3's work buffer)
+
+
+def _split_cols_h3(x3: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """The columns of fp32 x3 [nb, R, C] as h3 plane rows (``nos_split_cols_h3``):
+    planes [2, nb * C, ceil32(R)] (zero-padded), 1 / row scale [nb * C] -- the
+    split of x3's transpose without a transposed copy."""
+    nb, R, C = x3.shape
+    if x3.stride(-1) != 1 or (nb > 1 and x3.stride(0) < (R - 1) * x3.stride(1) + C):
+        x3 = x3.contiguous()
+    Rp = _pad_k_len(R)
+    planes = torch.empty((2, nb * C, Rp), dtype=torch.float16, device=x3.device)
+    rinv = torch.empty((nb * C,), dtype=torch.float32, device=x3.device)
+    work = torch.empty((COLS_NCH * nb * C,), dtype=torch.float32, device=x3.device)
+    _lib.check(_lib.lib().nos_split_cols_h3(x3.data_ptr(), x3.stride(1), x3.stride(0) if nb > 1 else 0, R, C, nb,
+                                            planes.data_ptr(), Rp, planes[0].numel(), rinv.data_ptr(),
+                                            work.data_ptr(), _stream()), "nos_split_cols_h3")
+    return planes, rinv
+
+
+def _rows_h3(x3: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """The rows of fp32 x3 [nb, R, C] as h3 plane rows [2, nb * R, ceil32(C)]."""
+    R, C = x3.shape[1:]
+    x2 = _pad_k(x3).reshape(-1, _pad_k_len(C))
+    return _split_rows_h3(x2 if x2.stride(-1) == 1 and x2.is_contiguous() else x2.contiguous(), ln=False)
+
+
+def mm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False) -> torch.Tensor:
+    """op(a) @ op(b) on the h3 batched GEMM, op(x) = x^T (last two dims) when
+    the flag is set; batch dims equal, or one side 2-D.  A transposed A or a
+    plain B operand is split by columns (``nos_split_cols_h3``), so no
+    operand is ever copied into its transpose (training's dX = dY W and
+    dW = dY^T X, attention's P V and P^T dO)."""
     if not a.is_cuda:
-        return (a.float() @ b.float()).to(a.dtype)
+        A = a.transpose(-1, -2) if a_t else a
+        B = b.transpose(-1, -2) if b_t else b
+        return (A.float() @ B.float()).to(a.dtype)
     dt = a.dtype
-    M, K = a.shape[-2:]
-    N = b.shape[-1]
+    M, K = (a.shape[-1], a.shape[-2]) if a_t else (a.shape[-2], a.shape[-1])
+    N, Kb = (b.shape[-2], b.shape[-1]) if b_t else (b.shape[-1], b.shape[-2])
     ba, bb = a.shape[:-2], b.shape[:-2]
-    if ba and bb and ba != bb:
-        raise ValueError(f"matmul batch dims must match (or one side 2-D): {tuple(a.shape)} @ {tuple(b.shape)}")
+    if Kb != K or (ba and bb and ba != bb):
+        raise ValueError(f"mm shapes: {tuple(a.shape)}{'^T' if a_t else ''} @ {tuple(b.shape)}{'^T' if b_t else ''}")
     bshape = ba or bb
     nb = math.prod(bshape) if bshape else 1
-    a2 = _pad_k(_f32(a).reshape(-1, M, K)).reshape(-1, _pad_k_len(K)).contiguous()
-    bt = _pad_k(_f32(b).reshape(-1, K, N).transpose(1, 2)).reshape(-1, _pad_k_len(K)).contiguous()
-    Kp = a2.shape[1]
-    ap, arinv = _split_rows_h3(a2, ln=False)
-    bp, brinv = _split_rows_h3(bt, ln=False)
+    a3, b3 = _f32(a).reshape(-1, *a.shape[-2:]), _f32(b).reshape(-1, *b.shape[-2:])
+    ap, arinv = _split_cols_h3(a3) if a_t else _rows_h3(a3)      # A rows: op(a)'s M rows of K
+    bp, brinv = _rows_h3(b3) if b_t else _split_cols_h3(b3)      # W rows: op(b)'s N columns of K
+    Kp = ap.shape[2]
     out = torch.empty((nb, M, N), dtype=torch.float32, device=a.device)
     _gemm_batched(ap, arinv, M * Kp if ba else 0, M if ba else 0, bp, brinv, N * Kp if bb else 0, N if bb else 0,
                   out, M, N, Kp, nb, 0)
     out = out.view(*bshape, M, N)
     return out if dt == torch.float32 else out.to(dt)
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a [..., M, K] @ b [..., K, N]; batch dims equal, or one side 2-D."""
+    return mm(a, b)
 
 
 def _pad_k_len(k: int) -> int:

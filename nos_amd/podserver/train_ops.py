@@ -34,13 +34,15 @@ import torch
 CHUNK = 512   # query rows per attention chunk (live scores: B x H x CHUNK x S fp32)
 
 
-def _mm(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """a @ b on the h3 GEMM for CUDA tensors (batch dims equal or one side 2-D)."""
+def _mm(a: torch.Tensor, b: torch.Tensor, a_t: bool = False, b_t: bool = False) -> torch.Tensor:
+    """op(a) @ op(b) (op = transpose of the last two dims when flagged) on the
+    h3 GEMM for CUDA tensors -- transposed operands split by columns, never
+    copied (``ops.tenant.mm``); batch dims equal or one side 2-D."""
     if a.is_cuda:
         from ..ops import tenant as T
 
-        return T.matmul(a, b)
-    return a @ b
+        return T.mm(a, b, a_t, b_t)
+    return (a.transpose(-1, -2) if a_t else a) @ (b.transpose(-1, -2) if b_t else b)
 
 
 class H3Linear(torch.autograd.Function):
@@ -48,7 +50,7 @@ class H3Linear(torch.autograd.Function):
     def forward(ctx, x, w, b):
         K = x.shape[-1]
         x2 = x.reshape(-1, K)
-        y = _mm(x2, w.t())
+        y = _mm(x2, w, b_t=True)
         if b is not None:
             y = y + b
         ctx.save_for_backward(x2, w)
@@ -61,7 +63,7 @@ class H3Linear(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0]).contiguous()
         dx = _mm(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        dw = _mm(dy2.t(), x2) if ctx.needs_input_grad[1] else None
+        dw = _mm(dy2, x2, a_t=True) if ctx.needs_input_grad[1] else None     # dY^T X, no transposed copies
         db = dy2.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
 
@@ -78,7 +80,10 @@ def _heads(t: torch.Tensor) -> torch.Tensor:
 class ChunkedAttention(torch.autograd.Function):
     """softmax(scale q k^T [causal]) v with q [B, Sq, H, D], k / v [B, Skv,
     Hkv, D] (H % Hkv == 0); the causal mask aligns the last query with the
-    last key (Sq <= Skv), as the inference kernels do."""
+    last key (Sq <= Skv), as the inference kernels do.  Grouped-query heads
+    are GEMM rows: the g query heads of a KV head stack into one [g * C, D]
+    operand per chunk against that head's K / V (no repeated K / V copies;
+    dK / dV sum over the group inside the P^T dO / dS^T Q products)."""
 
     @staticmethod
     def forward(ctx, q, k, v, causal: bool, scale: float):
@@ -86,15 +91,15 @@ class ChunkedAttention(torch.autograd.Function):
         Skv, Hkv = k.shape[1], k.shape[2]
         g = H // Hkv
         ct = torch.float64 if q.dtype == torch.float64 else torch.float32   # fp32 math (fp64 kept for tests)
-        qh = _heads(q.to(ct))
-        kh = _heads(k.to(ct)).repeat_interleave(g, dim=1) if g > 1 else _heads(k.to(ct))
-        vh = _heads(v.to(ct)).repeat_interleave(g, dim=1) if g > 1 else _heads(v.to(ct))
+        qh, kh, vh = _heads(q.to(ct)), _heads(k.to(ct)), _heads(v.to(ct))  # [B, heads, S, D]
         o = torch.empty_like(qh)
         lse = torch.empty(B, H, Sq, device=q.device, dtype=ct)
-        kt = kh.transpose(-1, -2)
+        k3, v3 = kh.reshape(B * Hkv, Skv, D), vh.reshape(B * Hkv, Skv, D)
+        q5, o5 = qh.view(B, Hkv, g, Sq, D), o.view(B, Hkv, g, Sq, D)
         for c0 in range(0, Sq, CHUNK):
             c1 = min(Sq, c0 + CHUNK)
-            s = _mm(qh[:, :, c0:c1].reshape(B * H, c1 - c0, D), kt.reshape(B * H, D, Skv)).view(B, H, c1 - c0, Skv)
+            C = c1 - c0
+            s = _mm(q5[:, :, :, c0:c1].reshape(B * Hkv, g * C, D), k3, b_t=True).view(B, H, C, Skv)
             s = s * scale
             if causal:
                 s = s.masked_fill(_mask(c0, c1, Sq, Skv, q.device), float("-inf"))
@@ -102,8 +107,7 @@ class ChunkedAttention(torch.autograd.Function):
             p = torch.exp(s - m)
             l_ = p.sum(-1, keepdim=True)
             lse[:, :, c0:c1] = (m + torch.log(l_)).squeeze(-1)
-            o[:, :, c0:c1] = _mm((p / l_).reshape(B * H, c1 - c0, Skv), vh.reshape(B * H, Skv, D)).view(
-                B, H, c1 - c0, D)
+            o5[:, :, :, c0:c1] = _mm((p / l_).reshape(B * Hkv, g * C, Skv), v3).view(B, Hkv, g, C, D)
         ctx.save_for_backward(qh, kh, vh, o, lse)
         ctx.causal, ctx.scale, ctx.g, ctx.dt = causal, scale, g, q.dtype
         return o.permute(0, 2, 1, 3).to(q.dtype)
@@ -112,33 +116,31 @@ class ChunkedAttention(torch.autograd.Function):
     def backward(ctx, do):
         qh, kh, vh, o, lse = ctx.saved_tensors
         B, H, Sq, D = qh.shape
-        Skv = kh.shape[2]
+        Hkv, Skv = kh.shape[1], kh.shape[2]
+        g = ctx.g
         doh = _heads(do.to(qh.dtype))
         dq = torch.empty_like(qh)
         dk = torch.zeros_like(kh)
         dv = torch.zeros_like(vh)
-        kt = kh.transpose(-1, -2).reshape(B * H, D, Skv)
-        vt = vh.transpose(-1, -2).reshape(B * H, D, Skv)
+        k3, v3 = kh.reshape(B * Hkv, Skv, D), vh.reshape(B * Hkv, Skv, D)
+        dk3, dv3 = dk.view(B * Hkv, Skv, D), dv.view(B * Hkv, Skv, D)
+        q5, do5, dq5 = qh.view(B, Hkv, g, Sq, D), doh.view(B, Hkv, g, Sq, D), dq.view(B, Hkv, g, Sq, D)
         delta = (doh * o).sum(-1)                                   # rowsum(dO . O)
         for c0 in range(0, Sq, CHUNK):
             c1 = min(Sq, c0 + CHUNK)
             C = c1 - c0
-            qc = qh[:, :, c0:c1].reshape(B * H, C, D)
-            doc = doh[:, :, c0:c1].reshape(B * H, C, D)
-            s = _mm(qc, kt).view(B, H, C, Skv) * ctx.scale
+            qc = q5[:, :, :, c0:c1].reshape(B * Hkv, g * C, D)
+            doc = do5[:, :, :, c0:c1].reshape(B * Hkv, g * C, D)
+            s = _mm(qc, k3, b_t=True).view(B, H, C, Skv) * ctx.scale
             if ctx.causal:
                 s = s.masked_fill(_mask(c0, c1, Sq, Skv, qh.device), float("-inf"))
             p = torch.exp(s - lse[:, :, c0:c1, None])               # recomputed from the log-sum-exp
-            pf = p.reshape(B * H, C, Skv)
-            dv += _mm(pf.transpose(-1, -2), doc).view(B, H, Skv, D)
-            dp = _mm(doc, vt).view(B, H, C, Skv)
-            ds = (p * (dp - delta[:, :, c0:c1, None]) * ctx.scale).reshape(B * H, C, Skv)
-            dq[:, :, c0:c1] = _mm(ds, kh.reshape(B * H, Skv, D)).view(B, H, C, D)
-            dk += _mm(ds.transpose(-1, -2), qc).view(B, H, Skv, D)
-        g = ctx.g
-        if g > 1:   # grouped-query: the K / V gradients of a group's heads add up
-            dk = dk.view(B, H // g, g, Skv, D).sum(2)
-            dv = dv.view(B, H // g, g, Skv, D).sum(2)
+            pf = p.reshape(B * Hkv, g * C, Skv)
+            dv3 += _mm(pf, doc, a_t=True)                                      # P^T dO (the group summed)
+            dp = _mm(doc, v3, b_t=True).view(B, H, C, Skv)                    # dO V^T
+            ds = (p * (dp - delta[:, :, c0:c1, None]) * ctx.scale).reshape(B * Hkv, g * C, Skv)
+            dq5[:, :, :, c0:c1] = _mm(ds, k3).view(B, Hkv, g, C, D)           # dS K
+            dk3 += _mm(ds, qc, a_t=True)                                       # dS^T Q (the group summed)
         back = lambda t: t.permute(0, 2, 1, 3).to(ctx.dt)   # noqa: E731
         return back(dq), back(dk), back(dv), None, None
 

@@ -84,3 +84,25 @@ def test_seq2048_decoder_fine_tune_fits_a_10gb_slice(tmp_path):
         c.close()
     finally:
         srv.stop()
+
+
+@pytest.mark.parametrize("shape", [(1, 37, 45, 29), (6, 128, 100, 64), (3, 513, 64, 200)])
+@pytest.mark.parametrize("a_t, b_t", [(False, False), (True, False), (False, True), (True, True)])
+def test_mm_transposed_operands_match_fp64(shape, a_t, b_t):
+    """ops.tenant.mm: a transposed A or a plain B is split by columns
+    (nos_split_cols_h3, zero-padded reduction dim) -- against fp64, within the
+    h3 GEMM's fp32-class error; 2-D and batched."""
+    from nos_amd.ops import tenant as T
+
+    nb, M, K, N = shape
+    g = torch.Generator(device="cuda").manual_seed(M + K + N)
+    a = torch.randn(nb, K, M, device="cuda", generator=g) if a_t else torch.randn(nb, M, K, device="cuda", generator=g)
+    b = torch.randn(nb, N, K, device="cuda", generator=g) if b_t else torch.randn(nb, K, N, device="cuda", generator=g)
+    a[..., 3] *= 1e3                       # per-row / per-column scales matter
+    for x, y in ((a, b), (a[0], b[0])):
+        got = T.mm(x, y, a_t, b_t)
+        A = x.double().transpose(-1, -2) if a_t else x.double()
+        B = y.double().transpose(-1, -2) if b_t else y.double()
+        ref = A @ B
+        err = (got.double() - ref).abs().max() / ref.abs().max()
+        assert got.shape == ref.shape and float(err) < 2e-6, (shape, a_t, b_t, float(err))

@@ -14,3 +14,4 @@ for r in 1 2; do
   one occ4_r$r $R/nos_amd/_native/libnos_hip.so || exit 1
 done
 bash tools/gpu/r06_decprof.sh
+bash tools/gpu/r06_lat3.sh
