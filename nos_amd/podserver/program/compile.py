@@ -81,6 +81,9 @@ class Lowered:
             used = {i for s in self.steps for i in s.inputs} | set(self.outputs)
             for k in [k for k in self.consts if k not in used]:  # e.g. weights replaced by their LN-folded form
                 del self.consts[k]
+        # the memo holds its recipes' SOURCE tensors (raw weights a fold replaced): only the
+        # build's variants share it -- a compiled program keeping it would keep them alive
+        self._derived = None
         self.stats["kernels"] = sum(1 for s in self.steps if s.kind in NATIVE_KINDS)
 
     def _memo(self, tag: str, sources: list, extra, make):

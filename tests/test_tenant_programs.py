@@ -298,3 +298,34 @@ def test_variants_must_share_their_weights():
         PG.parse_variants([y0, other], yp)
     with pytest.raises(PG.ProgramError, match="1 to 8 program variants"):
         PG.parse_variants([y0] * 9, yp)
+
+
+def test_compiled_program_drops_the_derived_weight_memo():
+    """The memo of derived weights (shared by a tenant's shape variants during
+    the build) holds the source tensors; a compiled program must not keep it,
+    or every raw weight a fold replaced stays allocated (GPU footprint)."""
+    import weakref
+
+    import torch
+
+    from nos_amd.podserver import program as PG
+
+    b = PG.Builder("bnfold")
+    x = b.input("x", [1, 8, 6, 6])
+    w = b.param("w", np.random.default_rng(0).standard_normal((4, 8, 3, 3)) * 0.1)
+    h = b.op("conv2d", x, w, padding=[1, 1])
+    h = b.op("batchnorm", h, b.param("g", np.ones(4)), b.param("be", np.zeros(4)), b.param("mu", np.zeros(4)),
+             b.param("var", np.ones(4)), eps=1e-5)
+    prog, wts = b.build([h])
+    p = PG.parse(prog, wts)
+    params = p.tensors("cpu")
+    raw = weakref.ref(params["w"])
+    derived: dict = {}
+    c = p.compile("cpu", params=params, derived=derived)
+    assert c._derived is None and derived
+    del params, derived
+    import gc
+
+    gc.collect()
+    assert raw() is None, "the raw conv weight outlived the build"
+    assert torch.is_tensor(c(p.input_tensor("cpu"))[0])
