@@ -348,12 +348,13 @@ __global__ __launch_bounds__(NT, 3) void attn_fwd_f32x6_d64_kernel(
 constexpr int H3_STAGE = 4 * IMG;            // K hi, K lo, V hi, V lo
 constexpr int H3_RING = 2;  // stages; 3 (two tiles in flight) measured slower: 138 VGPRs, 802 vs 818 inf/s
 constexpr int H3_LDS_BYTES = H3_RING * H3_STAGE;  // 48 KiB
-constexpr int H3_WG_PER_CU = 4;  // 4-wave workgroups (HW = 4); HW = 8: 2
+constexpr int H3_WG_PER_CU = 4;  // 4-wave workgroups (HW = 4); HW = 8: 2 (134 VGPRs, 3 waves / SIMD; forcing
+                                 // 4 waves / SIMD -- 128 VGPRs, one spill -- fleet 797-799 vs 823-824 inf/s)
 
 // HW waves per workgroup (4 or 8) x 32 query rows; the 16 DMA pieces of a
 // key tile are spread over the waves (16 / HW each)
 template <bool PERSIST, int HW>
-__global__ __launch_bounds__(64 * HW, HW == 8 ? 4 : H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
+__global__ __launch_bounds__(64 * HW, HW == 8 ? 2 : H3_WG_PER_CU) void attn_fwd_f32h3_d64_kernel(
     const float* __restrict__ q, const _Float16* __restrict__ kvs, float* __restrict__ o, int B, int H, int Sq,
     int Skv, int ld_in, long long bs_in, int ld_out, long long bs_out, float c, const float* __restrict__ kvsc,
     int nqb, int nsplit, float* __restrict__ part, _Float16* __restrict__ op, long long opl, float osc) {

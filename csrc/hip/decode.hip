@@ -178,11 +178,21 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   // the split's keys -> LDS (rows past nk zero)
   const long long cstride = (long long)Hkv * D;  // cache row (token) stride
   const long long cbase = ((long long)b * L + k0) * cstride + (long long)kvh * D;
+  // every load of the split issued before the first LDS store (16 float4 per thread at
+  // D = 128): a load-store loop left one cache-row latency exposed per iteration
   auto stage = [&](const void* c) {
-    for (int e = tid; e < KC * (D / 4); e += 256) {
-      const int j = e / (D / 4), d4 = (e % (D / 4)) * 4;
-      const float4 v = j < nk ? ld4(c, cbase + j * cstride + d4, cbf) : float4{0.f, 0.f, 0.f, 0.f};
-      *reinterpret_cast<float4*>(&kv[j * DP + d4]) = v;
+    constexpr int PER = KC * (D / 4) / 256;
+    static_assert(PER * 256 == KC * (D / 4), "whole float4 pieces per thread");
+    float4 v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + 256 * u, j = e / (D / 4), d4 = (e % (D / 4)) * 4;
+      v[u] = j < nk ? ld4(c, cbase + j * cstride + d4, cbf) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + 256 * u, j = e / (D / 4), d4 = (e % (D / 4)) * 4;
+      *reinterpret_cast<float4*>(&kv[j * DP + d4]) = v[u];
     }
   };
   stage(kc);
@@ -283,31 +293,65 @@ __global__ void pos_update_kernel(int* __restrict__ pos, int B, int add, int n) 
 }
 
 // first index of the row maximum (torch.argmax's tie rule); NaN rows give the NaN's index
-__global__ __launch_bounds__(256) void argmax_kernel(const void* __restrict__ x, int bf, int rows, int L, int ldx,
-                                                     int* __restrict__ out) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= rows) return;
+// (value, index) b better than a: NaN beats numbers (torch.argmax), then the
+// larger value, then the smaller index -- the first maximum
+__device__ __forceinline__ bool am_better(float bv, int bi, float av, int ai) {
+  const bool bn = bv != bv, an = av != av;
+  if (bn != an) return bn;
+  if (bn) return bi < ai;
+  return bv > av || (bv == av && bi < ai);
+}
+
+// one workgroup of NT threads per row: 4 independent loads in flight per thread
+// per step (a wave per row left a 32000-wide vocabulary row latency-bound at
+// ~180 us), wave shuffles, then the waves' winners through LDS
+template <int NT>
+__global__ __launch_bounds__(NT) void argmax_kernel(const void* __restrict__ x, int bf, int rows, int L, int ldx,
+                                                    int* __restrict__ out) {
+  __shared__ float sv[NT / 64];
+  __shared__ int si[NT / 64];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const long long base = (long long)row * ldx;
   float best = -INFINITY;
   int bi = INT_MAX;
-  for (int j = lane; j < L; j += 64) {
-    const float v = ldf(x, (long long)row * ldx + j, bf);
-    if (v > best || (v != v && best == best)) {
-      best = v;
-      bi = j;
+  for (int j0 = tid; j0 < L; j0 += 4 * NT) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u * NT;
+      v[u] = j < L ? ldf(x, base + j, bf) : -INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u * NT;
+      if (j < L && am_better(v[u], j, best, bi)) {
+        best = v[u];
+        bi = j;
+      }
     }
   }
-  if (bi == INT_MAX) bi = L;  // an all -inf row: resolved to index 0 below
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float ob = __shfl_xor(best, o, 64);
     const int oi = __shfl_xor(bi, o, 64);
-    const bool onan = ob != ob, mnan = best != best;
-    if ((onan && !mnan) || (onan == mnan && (ob > best || (ob == best && oi < bi)))) {
+    if (am_better(ob, oi, best, bi)) {
       best = ob;
       bi = oi;
     }
   }
-  if (lane == 0) out[row] = bi >= L ? 0 : bi;
+  if (lane == 0) {
+    sv[wid] = best;
+    si[wid] = bi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < NT / 64; ++w)
+      if (am_better(sv[w], si[w], best, bi)) {
+        best = sv[w];
+        bi = si[w];
+      }
+    out[row] = bi >= L ? 0 : bi;  // an all -inf row: index 0
+  }
 }
 
 // ------------------------------------------------------------------ GEMV (M <= 8)
@@ -476,8 +520,10 @@ NOS_API int nos_pos_update(int* pos, int B, int add, int n, hipStream_t stream) 
 
 NOS_API int nos_argmax(const void* x, int bf16, int rows, int L, int ldx, int* out, hipStream_t stream) {
   if (!x || !out || rows <= 0 || L <= 0 || ldx < L || (bf16 != 0 && bf16 != 1)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, x, bf16, rows, L, ldx,
-                     out);
+  if (L >= 4096)
+    hipLaunchKernelGGL(argmax_kernel<1024>, dim3((unsigned)rows), dim3(1024), 0, stream, x, bf16, rows, L, ldx, out);
+  else
+    hipLaunchKernelGGL(argmax_kernel<256>, dim3((unsigned)rows), dim3(256), 0, stream, x, bf16, rows, L, ldx, out);
   return (int)hipGetLastError();
 }
 

@@ -109,6 +109,11 @@ def test_pos_update_and_argmax():
     assert torch.equal(T.argmax(x).long(), x.argmax(-1))
     xb = x.bfloat16()
     assert torch.equal(T.argmax(xb).long(), xb.float().argmax(-1))
+    x[5, 7] = x[5, 30000] = float("nan")      # NaN is the maximum, the first one wins (torch.argmax)
+    x[6] = float("-inf")                      # an all -inf row: index 0
+    assert T.argmax(x).tolist()[5:] == [7, 0]
+    short = torch.randn(3, 1000, device="cuda")  # the 256-thread form
+    assert torch.equal(T.argmax(short).long(), short.argmax(-1))
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 5, 8])
