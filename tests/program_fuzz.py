@@ -4,8 +4,8 @@
 chains (linear / norms / activations / residuals / strided slices /
 softmax), attention blocks (fused-QKV ``attention`` or ``sdpa`` with causal
 masking, grouped-query ratios and rotary), conv nets (grouped, depthwise,
-strided, dilated convs, BatchNorm, pooling) and activation x activation
-``matmul`` -- with dimensions drawn around the kernels' tile edges (1, 31,
+strided, dilated convs, BatchNorm, pooling), activation x activation
+``matmul`` and stateful decoders (K / V caches, device positions) -- with dimensions drawn around the kernels' tile edges (1, 31,
 33, 127, 129, ...), in fp32 or bf16.  Whatever the validator accepts must run
 on the server and agree with the program's eager fp32 reference; whatever it
 refuses must be refused before anything is allocated (``ProgramError``).
@@ -33,7 +33,7 @@ class _Builder(Builder):
 @st.composite
 def programs(draw, gpu: bool = True):
     """(program, weights, input array, description)."""
-    fam = draw(st.sampled_from(["mlp", "mlp", "attn", "sdpa", "conv", "matmul"]))
+    fam = draw(st.sampled_from(["mlp", "mlp", "attn", "sdpa", "conv", "matmul", "decode"]))
     dt = draw(st.sampled_from(["fp32", "fp32", "bf16"]))
     seed = draw(st.integers(0, 2 ** 16))
     rng = np.random.default_rng(seed)
@@ -100,6 +100,27 @@ def programs(draw, gpu: bool = True):
             q, k = b.op("rotary", q, cs, sn), b.op("rotary", k, cs, sn)
         o = b.op("sdpa", q, k, v, causal=draw(st.booleans()))
         h = b.op("linear", b.op("reshape", o, shape=[B, S, nh * hd]), W(D, nh * hd))
+        return (*b.build([h]), data, fam)
+    if fam == "decode":   # stateful: K / V caches + a position counter, written and attended at the positions
+        hd = draw(st.sampled_from((64, 128)))
+        hkv = draw(st.sampled_from((1, 2)))
+        nh = hkv * draw(st.sampled_from((1, 2, 4)))
+        L = max(S, draw(st.sampled_from((16, 100, 300))))
+        cdt = draw(st.sampled_from(("fp32", "bf16")))
+        pos = b.state("pos", [B], "i32")
+        kc, vc = b.state("kc", [B, L, hkv, hd], cdt), b.state("vc", [B, L, hkv, hd], cdt)
+        q = b.op("reshape", b.op("linear", h, W(nh * hd, D)), shape=[B, S, nh, hd])
+        k = b.op("reshape", b.op("linear", h, W(hkv * hd, D)), shape=[B, S, hkv, hd])
+        v = b.op("reshape", b.op("linear", h, W(hkv * hd, D)), shape=[B, S, hkv, hd])
+        if draw(st.booleans()):
+            inv = 1.0 / 10000 ** (np.arange(0, hd, 2) / hd)
+            e = np.concatenate([np.outer(np.arange(L), inv)] * 2, 1)
+            cs, sn = b.param("cos", np.cos(e), "fp32"), b.param("sin", np.sin(e), "fp32")
+            q, k = b.op("rotary_at", q, cs, sn, pos), b.op("rotary_at", k, cs, sn, pos)
+        kc2, vc2 = b.op("kv_write", kc, k, pos), b.op("kv_write", vc, v, pos)
+        o = b.op("sdpa_cache", q, kc2, vc2, pos)
+        h = b.op("linear", b.op("reshape", o, shape=[B, S, nh * hd]), W(D, nh * hd))
+        b.op("pos_add", pos, n=S)
         return (*b.build([h]), data, fam)
     if fam == "matmul":   # activation x activation (scores-like), softmax, back through a linear
         a = b.op("linear", h, W(64, D))

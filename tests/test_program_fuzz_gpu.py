@@ -87,4 +87,4 @@ def test_fuzz_covered_enough(fleet):
     """Runs after the property test (file order): at least 200 accepted
     programs ran, every family among them."""
     assert STATS["ran"] >= 200, dict(STATS)
-    assert all(STATS[f] > 0 for f in ("mlp", "attn", "sdpa", "conv", "matmul")), dict(STATS)
+    assert all(STATS[f] > 0 for f in ("mlp", "attn", "sdpa", "conv", "matmul", "decode")), dict(STATS)
