@@ -45,7 +45,7 @@ def fleet(tmp_path_factory):
     srv.stop()
 
 
-@settings(max_examples=300, deadline=None, derandomize=True, database=None,
+@settings(max_examples=400, deadline=None, derandomize=True, database=None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
                                  HealthCheck.function_scoped_fixture])
 @given(case=programs(gpu=True))
