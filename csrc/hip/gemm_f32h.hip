@@ -955,7 +955,7 @@ NOS_API int nos_gemm_f32h3_set_lds_epilogue(int on) {
 }
 
 NOS_API int nos_gemm_f32h3_set_layout(int layout) {
-  if (layout < 0 || layout > 6) return (int)hipErrorInvalidValue;
+  if (layout < 0 || layout > 7) return (int)hipErrorInvalidValue;
   g_layout = layout;
   return 0;
 }
@@ -1037,6 +1037,9 @@ int run_h3(const void* Ap, int lda, long long aplane, const float* rinv, float r
   if (g_layout == 5)
     return launch_t<128, 128, 2, 2, 16, 4>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
                                            N, K, epi, kv, po, bt, stream);
+  if (g_layout == 7)  // 128 x 64 tiles (48 KiB ring: three workgroups per CU)
+    return launch_t<128, 64, 2, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M, N, K,
+                                   epi, kv, po, bt, stream);
   if (g_layout == 6)
     return launch_t<128, 128, 2, 2, 32, 3>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R, ldr, C, ldc, M,
                                            N, K, epi, kv, po, bt, stream);

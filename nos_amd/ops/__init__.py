@@ -469,10 +469,11 @@ def set_gemm_f32h3_layout(layout: str) -> None:
     ``"4x1"`` (128x128, 32-row strips, each wave reads the whole W tile),
     ``"256x128"`` (8 waves of 64x64, one workgroup per CU), ``"4x1r3"``
     (3-deep ring of BK-32 stages), ``"4x1k16"`` / ``"2x2k16"`` (4-deep ring
-    of BK-16 stages), ``"2x2r3"`` (2x2, 3-deep BK-32 ring) -- A/B; the
+    of BK-16 stages), ``"2x2r3"`` (2x2, 3-deep BK-32 ring), ``"2x2n64"``
+    (128 x 64 tiles, 48 KiB: three workgroups per CU) -- A/B; the
     results are bit-identical."""
     _lib.check(_lib.lib().nos_gemm_f32h3_set_layout({"4x1": 0, "2x2": 1, "256x128": 2, "4x1r3": 3, "4x1k16": 4,
-                                                     "2x2k16": 5, "2x2r3": 6}[layout]),
+                                                     "2x2k16": 5, "2x2r3": 6, "2x2n64": 7}[layout]),
                "nos_gemm_f32h3_set_layout")
 
 

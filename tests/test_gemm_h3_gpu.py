@@ -107,7 +107,7 @@ def test_h3_wave_layouts_are_bit_identical():
     w = torch.randn(384, 384, device=DEV) * 0.05
     b = torch.randn(384, device=DEV)
     outs = []
-    lays = ("4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16")
+    lays = ("4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16", "2x2r3", "2x2n64")
     for lay in lays:
         ops.set_gemm_f32h3_layout(lay)
         try:

@@ -89,7 +89,7 @@ def main() -> None:
     ap.add_argument("--slice-gb", type=float, default=10.0)
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--pipeline", type=int, default=1, help="x6 GEMM software-pipelined K loop (1) or plain (0)")
-    ap.add_argument("--h3-layout", default=None, choices=["4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16", "2x2r3"],
+    ap.add_argument("--h3-layout", default=None, choices=["4x1", "2x2", "256x128", "4x1r3", "4x1k16", "2x2k16", "2x2r3", "2x2n64"],
                     help="h3 GEMM tile / wave layout / ring (NOS_AMD_H3_LAYOUT: the server's kernel config)")
     ap.add_argument("--h3-hot-ring", default=None, choices=["2", "3"],
                     help="LDS ring of the residual / row-statistics h3 GEMMs (NOS_AMD_H3_HOT_RING)")
