@@ -160,9 +160,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   static_assert(APW * NW * 1024 == TA && WPW * NW * 1024 == 2 * BN * ROWB, "equal DMA count per wave");
   constexpr int LPS = APW + WPW;
   static_assert((RS - 2) * LPS < 64, "vmcnt range");
-  static_assert(MODE == 0 || (BM == 128 && BN == 128 && NW == 4 && BKT == 32 && !BATCHED &&
+  static_assert(MODE == 0 || (BM == 128 && (BN == 128 || BN == 64) && NW == 4 && BKT == 32 && !BATCHED &&
                               (RS == 2 || (MODE == 2 && RS == 3))),
-                "the LayerNorm hand-off runs the 128 x 128, 2 x 2 tile (the producer also on a 3-deep ring)");
+                "the LayerNorm hand-off runs 128 x 128 or 128 x 64 2 x 2 tiles (the producer also on a 3-deep ring)");
   static_assert(MODE != 2 || BM * BN * 4 <= RS * STAGE, "the statistics tile fits the ring");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -469,16 +469,17 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         const int nv = m < M ? max(0, min(BN / 2, N - n0 - hf * (BN / 2))) : 0;
         const float* tr = T + rr * BN + hf * (BN / 2);
         const long long col0 = n0 + hf * (BN / 2);
-        float4 v[16];
+        constexpr int HV = BN / 8;  // float4s per row half
+        float4 v[HV];
         // sout == nullptr: the plain LDS epilogue (no statistics); a whole row
-        // half (every tile of N % 128 == 0) without per-chunk tests
+        // half (every tile of N % BN == 0) without per-chunk tests
         const bool want = ln.sout != nullptr;
         float sum = 0.f;
         auto pass1 = [&](auto wholec) {
           constexpr bool W = decltype(wholec)::value;
   #pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const int k = ((u + tid) & 15) * 4;
+          for (int u = 0; u < HV; ++u) {
+            const int k = ((u + tid) & (HV - 1)) * 4;
             v[u] = *reinterpret_cast<const float4*>(tr + k);
             if (W || k < nv) {
               if (has(EPI_RESID)) {
@@ -499,8 +500,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
           const float mean = nv > 0 ? sum / (float)nv : 0.f;
           float m2 = 0.f;
   #pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const int k = ((u + tid) & 15) * 4;
+          for (int u = 0; u < HV; ++u) {
+            const int k = ((u + tid) & (HV - 1)) * 4;
             if (k < nv) {
               const float d0 = v[u].x - mean, d1 = v[u].y - mean, d2 = v[u].z - mean, d3 = v[u].w - mean;
               m2 = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, m2))));
@@ -542,7 +543,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
         // wide: the tile's two planes in LDS (the ring is free: every wave passed the
         // K loop's last barrier), 16-byte chunks XOR-swizzled by row, then each
         // thread stores whole 16-byte row chunks of both planes
-        constexpr bool WIDE_FITS = 4 * BM * BN <= RS * STAGE && !BATCHED && BN == 128;
+        constexpr bool WIDE_FITS = 4 * BM * BN <= RS * STAGE && !BATCHED && (BN == 128 || BN == 64);
+        constexpr int SWM = BN / 8 - 1;  // 16-byte chunk swizzle mask of a tile row
         unsigned short* const T = reinterpret_cast<unsigned short*>(smem);
   #pragma unroll
         for (int j = 0; j < NI; ++j) {
@@ -562,7 +564,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
               const _Float16 h0 = (_Float16)x;
               const _Float16 h1 = (_Float16)(x - (float)h0);
               if (WIDE_FITS && wide) {
-                const int sl = rl * BN + ((((cl >> 3) ^ (rl & 15)) << 3) | (cl & 7));
+                const int sl = rl * BN + ((((cl >> 3) ^ (rl & SWM)) << 3) | (cl & 7));
                 T[sl] = __builtin_bit_cast(unsigned short, h0);
                 T[BM * BN + sl] = __builtin_bit_cast(unsigned short, h1);
               } else {
@@ -582,7 +584,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
             const int id = tid + q * 64 * NW;
             const int pl = id / (BM * CPR), rem = id - pl * (BM * CPR);
             const int row = rem / CPR, ch = rem - row * CPR;
-            const uint4 v = *reinterpret_cast<const uint4*>(T + pl * BM * BN + row * BN + ((ch ^ (row & 15)) << 3));
+            const uint4 v = *reinterpret_cast<const uint4*>(T + pl * BM * BN + row * BN + ((ch ^ (row & SWM)) << 3));
             *reinterpret_cast<uint4*>(hi + pl * lo_off + (long long)row * ld + ch * 8) = v;
           }
         }
@@ -741,6 +743,10 @@ bool g_lds_epi = true;  // 28-tenant fleet 801 vs 799 inf/s, batch-1 residual GE
 // workgroups per CU) or 3 (96 KiB, one workgroup per CU, stage k+2 in flight under k):
 // 28-tenant fleet 792 (3) vs 802 (2) inf/s, profiles/r06_packed_epilogue_rejected.json
 int g_hot_ring = 2;
+// tile width of the LN hand-off GEMMs (row-statistics producers, LN-in-A-load
+// consumers, LDS-epilogue GEMMs): 128, or 64 (48 KiB ring: three workgroups per
+// CU); the statistics parts are this many columns wide
+int g_hot_bn = 128;
 
 // ------------------------------------------------------------ row split
 // LPR lanes per row (64: a wave; 32: a half-wave, two rows per wave), the
@@ -960,6 +966,14 @@ NOS_API int nos_gemm_f32h3_set_layout(int layout) {
   return 0;
 }
 
+NOS_API int nos_gemm_f32h3_set_hot_bn(int bn) {
+  if (bn != 128 && bn != 64) return (int)hipErrorInvalidValue;
+  g_hot_bn = bn;
+  return 0;
+}
+
+NOS_API int nos_gemm_f32h3_hot_bn() { return g_hot_bn; }
+
 NOS_API int nos_gemm_f32h3_set_hot_ring(int rs) {
   if (rs != 2 && rs != 3) return (int)hipErrorInvalidValue;
   g_hot_ring = rs;
@@ -1049,6 +1063,9 @@ int run_h3(const void* Ap, int lda, long long aplane, const float* rinv, float r
   if (g_layout == 1) {
     if (g_lds_epi && kv.kvs == nullptr && po.p == nullptr && C != nullptr && !(N % 4) && !(ldc % 4) &&
         !(((uintptr_t)C) & 15) && (!(epi & EPI_RESID) || (!(ldr % 4) && !(((uintptr_t)R) & 15)))) {
+      if (g_hot_bn == 64)
+        return launch_t<128, 64, 2, 2, 32, 2, false, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R,
+                                                        ldr, C, ldc, M, N, K, epi, kv, po, bt, stream);
       if (g_hot_ring == 3)
         return launch_t<128, 128, 2, 2, 32, 3, false, 2>(a, lda, aplane, rinv, rconst, w, ldw, wplane, csc, bias, R,
                                                          ldr, C, ldc, M, N, K, epi, kv, po, bt, stream);
@@ -1149,8 +1166,8 @@ NOS_API int nos_gemm_f32h3_batched(const void* Ap, int lda, long long aplane, lo
 // nos_gemm_f32h3's plain contract (fp32 C, no KV / plane outputs; N % 4 == 0,
 // C / R rows 16-byte aligned) plus the row statistics of the finished C for
 // the LayerNorm of the next GEMM:
-// stats[m][tn] = (mean, sum of squared deviations) of C[m, 128 tn .. 128 tn + 127]
-// (the valid columns), ceil(N / 128) parts per row -- nos_gemm_f32h3_lna's input.
+// stats[m][tn] = (mean, sum of squared deviations) of C[m, BN tn .. BN tn + BN - 1]
+// (the valid columns), ceil(N / BN) parts per row (BN = nos_gemm_f32h3_hot_bn()) -- nos_gemm_f32h3_lna's input.
 NOS_API int nos_gemm_f32h3_stats(const void* Ap, int lda, long long aplane, const float* rinv, float rconst,
                                  const void* Wp, int ldw, long long wplane, const float* csc, const float* bias,
                                  const float* R, int ldr, float* C, int ldc, int M, int N, int K, int epi, void* stats,
@@ -1167,7 +1184,11 @@ NOS_API int nos_gemm_f32h3_stats(const void* Ap, int lda, long long aplane, cons
     return (int)hipErrorInvalidValue;
   LnIo ln;
   ln.sout = static_cast<float2*>(stats);
-  ln.spart = (N + 127) / 128;
+  ln.spart = (N + g_hot_bn - 1) / g_hot_bn;
+  if (g_hot_bn == 64)
+    return launch_t<128, 64, 2, 2, 32, 2, false, 2>(static_cast<const _Float16*>(Ap), lda, aplane, rinv, rconst,
+                                                    static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
+                                                    C, ldc, M, N, K, epi, KvOut{}, PlaneOut{}, Batch{}, stream, ln);
   if (g_hot_ring == 3)
     return launch_t<128, 128, 2, 2, 32, 3, false, 2>(static_cast<const _Float16*>(Ap), lda, aplane, rinv, rconst,
                                                      static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
@@ -1227,6 +1248,10 @@ NOS_API int nos_gemm_f32h3_lna(const float* X, int ldx, const void* stats, int n
   ln.pw = pw;
   ln.eps = eps;
   ln.sc = ldexpf(1.f, eln);
+  if (g_hot_bn == 64)
+    return launch_t<128, 64, 2, 2, 32, 2, false, 1>(nullptr, K, (long long)M * K, nullptr, ldexpf(1.f, -eln),
+                                                    static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
+                                                    C, ldc, M, N, K, epi, kv, po, Batch{}, stream, ln);
   return launch_t<128, 128, 2, 2, 32, 2, false, 1>(nullptr, K, (long long)M * K, nullptr, ldexpf(1.f, -eln),
                                                    static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
                                                    C, ldc, M, N, K, epi, kv, po, Batch{}, stream, ln);

@@ -174,7 +174,10 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
             # h3 GEMM tile layout (ops.set_gemm_f32h3_layout; the LN hand-off GEMMs keep 2x2)
             "h3_layout": env.get("NOS_AMD_H3_LAYOUT") or "2x2",
             # LDS ring of the residual (row-statistics) h3 GEMMs: "2" or "3" stages
-            "h3_hot_ring": env.get("NOS_AMD_H3_HOT_RING") or "2"}
+            "h3_hot_ring": env.get("NOS_AMD_H3_HOT_RING") or "2",
+            # tile width of the LN hand-off GEMMs: 128 x 64 tiles (48 KiB, three workgroups per CU)
+            # vs 128 x 128 (two): plain GEMMs 799 vs 769 inf/s at a lower clock (profiles/r06_hot_bn_ab.json)
+            "h3_hot_bn": env.get("NOS_AMD_H3_HOT_BN") or "64"}
 
 
 def slice_cu_budget(env: dict | None = None) -> int:
@@ -271,8 +274,8 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             frac = apply_memory_limit(0)
             torch.backends.cuda.matmul.allow_tf32 = False  # true fp32 GEMMs (no reduced-precision shortcut)
             from ..ops import (set_attention_f32_variant, set_cu_budget, set_f32_math, set_gemm_f32_policy,
-                               set_gemm_f32h3_hot_ring, set_gemm_f32h3_layout, set_gemm_f32x6_tile, set_gemm_policy,
-                               set_ln_handoff)
+                               set_gemm_f32h3_hot_bn, set_gemm_f32h3_hot_ring, set_gemm_f32h3_layout,
+                               set_gemm_f32x6_tile, set_gemm_policy, set_ln_handoff)
 
             budget = slice_cu_budget(os.environ)
             cfg = kernel_config(frac, os.environ, budget)
@@ -284,6 +287,7 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             set_ln_handoff(cfg["ln_handoff"] == "on")
             set_gemm_f32h3_layout(cfg["h3_layout"])
             set_gemm_f32h3_hot_ring(int(cfg["h3_hot_ring"]))
+            set_gemm_f32h3_hot_bn(int(cfg["h3_hot_bn"]))
             if budget:  # CU-mask slice: slice-sized persistent grids (ops.set_cu_budget)
                 set_cu_budget(budget)
         m, x = _build(dtype, seed, demo_input_hw(), device)

@@ -298,7 +298,7 @@ def linear_planes(a: H3Planes, weight: torch.Tensor, bias: torch.Tensor | None =
     (see :class:`H3Planes`): no split pre-pass, no fp32 round trip of A.
     ``row_stats``: also return the output's row statistics for the next
     LN-GEMM (``nos_gemm_f32h3_stats``) -- ``(out, RowStats)``, written into
-    ``stats_out`` (fp32 [M, ceil(N / 128), 2], contiguous) when given.
+    ``stats_out`` (fp32 [M, ceil(N / stats_pw()), 2], contiguous) when given.
     ``out``: an [M, N]-viewable fp32 destination (e.g. a slab of a cat's
     buffer)."""
     M, K = a.planes.shape[1], a.planes.shape[2]
@@ -320,7 +320,8 @@ def linear_planes(a: H3Planes, weight: torch.Tensor, bias: torch.Tensor | None =
         _check_f32(residual=r2)
     if row_stats:
         wp, csc = split_f32_weight_h3(weight)
-        shape = (M, (N + 127) // 128, 2)
+        pw = stats_pw()
+        shape = (M, (N + pw - 1) // pw, 2)
         if stats_out is None:
             st = torch.empty(shape, dtype=torch.float32, device=out.device)
         else:
@@ -332,7 +333,7 @@ def linear_planes(a: H3Planes, weight: torch.Tensor, bias: torch.Tensor | None =
                                              r2.stride(0) if r2 is not None else 0, out.data_ptr(), N, M, N, K,
                                              _epi(bias, act, residual), st.data_ptr(), _stream())
         _lib.check(rc, "nos_gemm_f32h3_stats")
-        return out.view(*a.shape[:-1], N), RowStats(st, 128)
+        return out.view(*a.shape[:-1], N), RowStats(st, pw)
     _gemm_h3(a.planes, a.rinv, weight, bias, r2, out, _epi(bias, act, residual), rconst=a.rconst)
     return out.view(*a.shape[:-1], N)
 
@@ -462,6 +463,19 @@ def set_gemm_f32h3_hot_ring(stages: int) -> None:
     residual GEMMs of a transformer): 2 (64 KiB, two workgroups per CU) or 3
     (96 KiB, one workgroup per CU; a stage two ahead in flight)."""
     _lib.check(_lib.lib().nos_gemm_f32h3_set_hot_ring(int(stages)), "nos_gemm_f32h3_set_hot_ring")
+
+
+def set_gemm_f32h3_hot_bn(bn: int) -> None:
+    """Tile width of the LN hand-off GEMMs (row-statistics producers,
+    LN-in-A-load consumers, LDS-epilogue residual GEMMs): 64 (48 KiB ring,
+    three workgroups per CU) or 128.  The row statistics come in parts of
+    this many columns (:func:`stats_pw`)."""
+    _lib.check(_lib.lib().nos_gemm_f32h3_set_hot_bn(int(bn)), "nos_gemm_f32h3_set_hot_bn")
+
+
+def stats_pw() -> int:
+    """Column width of a row-statistics part (the producer GEMM's tile width)."""
+    return int(_lib.lib().nos_gemm_f32h3_hot_bn())
 
 
 def set_gemm_f32h3_layout(layout: str) -> None:
@@ -957,5 +971,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_ln_handoff", "ln_handoff_active", "set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "set_gemm_f32h3_hot_ring", "H3Planes", "set_attention_f32h3_waves", "linear_planes", "linear_ln_to_planes", "h3_planes_active", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_ln_handoff", "ln_handoff_active", "set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "set_gemm_f32h3_hot_ring", "set_gemm_f32h3_hot_bn", "stats_pw", "H3Planes", "set_attention_f32h3_waves", "linear_planes", "linear_ln_to_planes", "h3_planes_active", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

@@ -1077,22 +1077,26 @@ class Lowered:
         [cls, patches, detection tokens] before layer 0): the GEMM writes its
         rows' statistics into a stats buffer whose constant rows are computed
         here, once -- the LN-GEMM then needs no statistics pass.  Row-wise
-        cats of fp32 rows whose width is whole 128-column parts only."""
+        cats of fp32 rows whose width is whole statistics parts (``ops.stats_pw()``) only."""
         import torch
 
         p = by_out.get(c.inputs[0])
         buf = self.aux[c.attrs["buf"]]
         shape = tuple(buf.shape)
         into = p.attrs.get("out_into") if p is not None else None
+        from ... import ops
+
+        pw = ops.stats_pw() if self.gpu else 128   # the producer GEMM's statistics part width (its tile width)
         if (p is None or p.kind != "linear" or into is None or buf.dtype != torch.float32 or len(shape) < 2
-                or into[1] % len(shape) != len(shape) - 2 or shape[-1] % 128 or math.prod(shape[:-2]) != 1):
+                or into[1] % len(shape) != len(shape) - 2 or shape[-1] % pw or math.prod(shape[:-2]) != 1):
             return False
-        rows = buf.reshape(-1, shape[-1]).double().view(shape[-2], shape[-1] // 128, 128)
+        rows = buf.reshape(-1, shape[-1]).double().view(shape[-2], shape[-1] // pw, pw)
         mean = rows.mean(-1)
         st = torch.stack([mean, ((rows - mean[..., None]) ** 2).sum(-1)], dim=-1).float().contiguous()
         name = c.attrs["buf"] + "::stats"
         self.aux[name] = st
         c.attrs["stats"] = name
+        c.attrs["stats_pw"] = pw
         p.attrs["row_stats"] = True
         p.attrs["stats_into"] = name
         return True

@@ -139,7 +139,7 @@ class CompiledProgram(Lowered):
                 if env.pop(s.inputs[0] + "::lnp", None) is not None:
                     # the GEMM wrote its rows' statistics into the buffer's stats, whose
                     # constant rows were filled at build: the whole buffer's, for its LN-GEMM
-                    env[s.output + "::lnp"] = ops.RowStats(self.aux[s.attrs["stats"]], 128)
+                    env[s.output + "::lnp"] = ops.RowStats(self.aux[s.attrs["stats"]], s.attrs.get("stats_pw", 128))
             else:
                 y = _eager(k, a, s.attrs)
             env[s.output] = y

@@ -18,14 +18,17 @@ pytestmark = pytest.mark.gpu
 from nos_amd import ops  # noqa: E402
 
 
-@pytest.fixture(autouse=True)
-def _h3():
+@pytest.fixture(autouse=True, params=[128, 64], ids=["bn128", "bn64"])
+def _h3(request):
+    """Every test on both tile widths of the hand-off GEMMs (ops.set_gemm_f32h3_hot_bn)."""
     torch.backends.cuda.matmul.allow_tf32 = False
-    prev, prev_h = ops.f32_math(), ops.ln_handoff_active()
+    prev, prev_h, prev_bn = ops.f32_math(), ops.ln_handoff_active(), ops.stats_pw()
     ops.set_f32_math("h3")
+    ops.set_gemm_f32h3_hot_bn(request.param)
     yield
     ops.set_f32_math(prev)
     ops.set_ln_handoff(prev_h)
+    ops.set_gemm_f32h3_hot_bn(prev_bn)
 
 
 def _parts(y64: torch.Tensor, pw: int) -> torch.Tensor:
@@ -38,17 +41,23 @@ def _parts(y64: torch.Tensor, pw: int) -> torch.Tensor:
     return torch.stack(out, 1)
 
 
-@pytest.mark.parametrize("ring", [2, 3])
+@pytest.mark.parametrize("ring, bn", [(2, 128), (3, 128), (2, 64)])
 @pytest.mark.parametrize("M,N,K", [(3401, 384, 384), (3401, 384, 1536), (100, 768, 384), (257, 132, 64)])
-def test_residual_gemm_writes_its_row_statistics(M, N, K, ring):
-    """Also on the 3-deep LDS ring (ops.set_gemm_f32h3_hot_ring): C bit-identical."""
+def test_residual_gemm_writes_its_row_statistics(M, N, K, ring, bn):
+    """Also on the 3-deep LDS ring (ops.set_gemm_f32h3_hot_ring) and on 128 x 64
+    tiles (ops.set_gemm_f32h3_hot_bn: statistics parts of 64 columns): C
+    bit-identical to the default."""
+    prev = ops.stats_pw()
     ops.set_gemm_f32h3_hot_ring(ring)
+    ops.set_gemm_f32h3_hot_bn(bn)
     try:
         y = _stats_case(M, N, K)
+        ops.set_gemm_f32h3_hot_ring(2)
+        ops.set_gemm_f32h3_hot_bn(128)
+        assert torch.equal(y, _stats_case(M, N, K))
     finally:
         ops.set_gemm_f32h3_hot_ring(2)
-    if ring != 2:
-        assert torch.equal(y, _stats_case(M, N, K))
+        ops.set_gemm_f32h3_hot_bn(prev)
 
 
 def _stats_case(M, N, K):
@@ -63,8 +72,9 @@ def _stats_case(M, N, K):
     y, st = ops.linear_planes(a, w, b, residual=r, row_stats=True)
     torch.cuda.synchronize()
     assert torch.equal(y, y_ref)  # the statistics epilogue leaves C alone
-    assert st.pw == 128 and st.stats.shape == (M, math.ceil(N / 128), 2)
-    ref = _parts(y.double(), 128)
+    pw = ops.stats_pw()
+    assert st.pw == pw and st.stats.shape == (M, math.ceil(N / pw), 2)
+    ref = _parts(y.double(), pw)
     got = st.stats.double()
     scale = y.double().abs().amax(1, keepdim=True)
     assert ((got[..., 0] - ref[..., 0]).abs() <= 4e-6 * scale).all()

@@ -52,6 +52,7 @@ def main() -> None:
     ops.set_ln_handoff(cfg["ln_handoff"] == "on")
     ops.set_gemm_f32h3_layout(cfg["h3_layout"])
     ops.set_gemm_f32h3_hot_ring(int(cfg["h3_hot_ring"]))
+    ops.set_gemm_f32h3_hot_bn(int(cfg["h3_hot_bn"]))
     print("kernel config", cfg, flush=True)
     m, x = _build(a.dtype, 0, demo_input_hw())
     s = torch.cuda.Stream()
