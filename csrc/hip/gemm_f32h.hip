@@ -743,9 +743,9 @@ bool g_lds_epi = true;  // 28-tenant fleet 801 vs 799 inf/s, batch-1 residual GE
 // workgroups per CU) or 3 (96 KiB, one workgroup per CU, stage k+2 in flight under k):
 // 28-tenant fleet 792 (3) vs 802 (2) inf/s, profiles/r06_packed_epilogue_rejected.json
 int g_hot_ring = 2;
-// tile width of the LN hand-off GEMMs (row-statistics producers, LN-in-A-load
-// consumers, LDS-epilogue GEMMs): 128, or 64 (48 KiB ring: three workgroups per
-// CU); the statistics parts are this many columns wide
+// tile width of the row-statistics producers and LDS-epilogue GEMMs (the
+// residual GEMMs of a transformer): 128, or 64 (48 KiB ring: three workgroups
+// per CU); the statistics parts are this many columns wide
 int g_hot_bn = 128;
 
 // ------------------------------------------------------------ row split
@@ -1248,10 +1248,8 @@ NOS_API int nos_gemm_f32h3_lna(const float* X, int ldx, const void* stats, int n
   ln.pw = pw;
   ln.eps = eps;
   ln.sc = ldexpf(1.f, eln);
-  if (g_hot_bn == 64)
-    return launch_t<128, 64, 2, 2, 32, 2, false, 1>(nullptr, K, (long long)M * K, nullptr, ldexpf(1.f, -eln),
-                                                    static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
-                                                    C, ldc, M, N, K, epi, kv, po, Batch{}, stream, ln);
+  // always 128 x 128: the LN-in-A-load normalises and splits its A tile per workgroup, so
+  // 128 x 64 tiles doubled that VALU work (fleet 760 vs 800 inf/s, profiles/r06_hot_bn_ab.json)
   return launch_t<128, 128, 2, 2, 32, 2, false, 1>(nullptr, K, (long long)M * K, nullptr, ldexpf(1.f, -eln),
                                                    static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
                                                    C, ldc, M, N, K, epi, kv, po, Batch{}, stream, ln);

@@ -466,10 +466,10 @@ def set_gemm_f32h3_hot_ring(stages: int) -> None:
 
 
 def set_gemm_f32h3_hot_bn(bn: int) -> None:
-    """Tile width of the LN hand-off GEMMs (row-statistics producers,
-    LN-in-A-load consumers, LDS-epilogue residual GEMMs): 64 (48 KiB ring,
-    three workgroups per CU) or 128.  The row statistics come in parts of
-    this many columns (:func:`stats_pw`)."""
+    """Tile width of the row-statistics producers and LDS-epilogue GEMMs
+    (a transformer's residual GEMMs): 64 (48 KiB ring, three workgroups per
+    CU) or 128.  The row statistics come in parts of this many columns
+    (:func:`stats_pw`); the LN-in-A-load consumers stay 128 x 128."""
     _lib.check(_lib.lib().nos_gemm_f32h3_set_hot_bn(int(bn)), "nos_gemm_f32h3_set_hot_bn")
 
 
