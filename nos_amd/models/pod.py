@@ -175,9 +175,9 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
             "h3_layout": env.get("NOS_AMD_H3_LAYOUT") or "2x2",
             # LDS ring of the residual (row-statistics) h3 GEMMs: "2" or "3" stages
             "h3_hot_ring": env.get("NOS_AMD_H3_HOT_RING") or "2",
-            # tile width of the residual (row-statistics) h3 GEMMs: 128 x 64 tiles (48 KiB, three
-            # workgroups per CU) vs 128 x 128 (two) -- profiles/r06_hot_bn_ab.json
-            "h3_hot_bn": env.get("NOS_AMD_H3_HOT_BN") or "64"}
+            # tile width of the residual (row-statistics) h3 GEMMs: 128 x 128 (two workgroups per CU);
+            # 128 x 64 (48 KiB, three) measured 2 % slower with the LN hand-off (profiles/r06_hot_bn_ab.json)
+            "h3_hot_bn": env.get("NOS_AMD_H3_HOT_BN") or "128"}
 
 
 def slice_cu_budget(env: dict | None = None) -> int:
