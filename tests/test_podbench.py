@@ -160,4 +160,4 @@ def test_pod_kernel_config_follows_the_slice():
     src = (inspect.getsource(ops.set_attention_f32_variant) + inspect.getsource(ops.set_gemm_f32_policy)
            + inspect.getsource(ops.set_f32_math) + inspect.getsource(ops.set_gemm_f32x6_tile) + inspect.getsource(ops.set_gemm_f32h3_layout))
     for v in (*whole.values(), *frac.values()):
-        assert f'"{v}"' in src or v in ("latency", "throughput", "on", "off", "lds", "reg", "2", "64")
+        assert f'"{v}"' in src or v in ("latency", "throughput", "on", "off", "lds", "reg", "2", "128")
