@@ -201,20 +201,27 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   {
     const int j = tid & (KC - 1), rh = tid >> 7;
     const int jabs = k0 + j;
-    float acc[MAXR / 2];
+    // two partial dot products per row (even / odd float4s of d): at decode's few
+    // rows (G x 1) one chain of D dependent FMAs per row was latency-bound
+    float acc[MAXR / 2], acc2[MAXR / 2];
 #pragma unroll
-    for (int i = 0; i < MAXR / 2; ++i) acc[i] = 0.f;
-    for (int d4 = 0; d4 < D; d4 += 4) {
+    for (int i = 0; i < MAXR / 2; ++i) acc[i] = acc2[i] = 0.f;
+    for (int d4 = 0; d4 < D; d4 += 8) {
       const float4 kk = *reinterpret_cast<const float4*>(&kv[j * DP + d4]);
+      const float4 k2 = *reinterpret_cast<const float4*>(&kv[j * DP + d4 + 4]);
 #pragma unroll
       for (int i = 0; i < MAXR / 2; ++i) {
         const int r = rh + 2 * i;
         if (r < R) {
           const float4 qq = *reinterpret_cast<const float4*>(&qs[r * D + d4]);
+          const float4 q2 = *reinterpret_cast<const float4*>(&qs[r * D + d4 + 4]);
           acc[i] = fmaf(qq.x, kk.x, fmaf(qq.y, kk.y, fmaf(qq.z, kk.z, fmaf(qq.w, kk.w, acc[i]))));
+          acc2[i] = fmaf(q2.x, k2.x, fmaf(q2.y, k2.y, fmaf(q2.z, k2.z, fmaf(q2.w, k2.w, acc2[i]))));
         }
       }
     }
+#pragma unroll
+    for (int i = 0; i < MAXR / 2; ++i) acc[i] += acc2[i];
 #pragma unroll
     for (int i = 0; i < MAXR / 2; ++i) {
       const int r = rh + 2 * i;
@@ -246,9 +253,16 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     constexpr int RS = 256 / D;  // rows in parallel
     const int d = tid % D, r0 = tid / D;
     for (int r = r0; r < R; r += RS) {
-      float a = 0.f;
-      for (int j = 0; j < nk; ++j) a = fmaf(sc[r * KC + j], kv[j * DP + d], a);
-      out[r * (D + 2) + d] = a;
+      // four partial sums: a chain of nk dependent FMAs (each behind two LDS reads) was
+      // latency-bound; keys past nk hold P = 0 and zero V rows, so the unrolled tail adds 0
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      for (int j = 0; j < nk; j += 4) {
+        a0 = fmaf(sc[r * KC + j], kv[j * DP + d], a0);
+        a1 = fmaf(sc[r * KC + j + 1], kv[(j + 1) * DP + d], a1);
+        a2 = fmaf(sc[r * KC + j + 2], kv[(j + 2) * DP + d], a2);
+        a3 = fmaf(sc[r * KC + j + 3], kv[(j + 3) * DP + d], a3);
+      }
+      out[r * (D + 2) + d] = (a0 + a1) + (a2 + a3);
     }
     for (int r = tid; r < R; r += 256) {
       out[r * (D + 2) + D] = mrow[r];
@@ -393,13 +407,27 @@ __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, i
     const int nc0 = glu ? min(n0, Nh - 1) : min(n0, N - 1);
     const int nc1 = glu ? min(n0, Nh - 1) + Nh : min(n0 + 1, N - 1);
     const long long w0 = (long long)nc0 * ldw, w1 = (long long)nc1 * ldw;
-    for (int k = lane * 4; k < K; k += 256) {
-      const float4 a = ld4(w, w0 + k, wbf), c4 = ld4(w, w1 + k, wbf);
+    // four K steps' weight loads issued together (8 float4 in flight per lane): the
+    // one-step loop waited a full memory latency per 256 columns of K
+    for (int k0 = lane * 4; k0 < K; k0 += 1024) {
+      float4 a[4], c4[4];
 #pragma unroll
-      for (int m = 0; m < M; ++m) {
-        const float4 xv = *reinterpret_cast<const float4*>(&xs[m * K + k]);
-        acc[0][m] = fmaf(a.x, xv.x, fmaf(a.y, xv.y, fmaf(a.z, xv.z, fmaf(a.w, xv.w, acc[0][m]))));
-        acc[1][m] = fmaf(c4.x, xv.x, fmaf(c4.y, xv.y, fmaf(c4.z, xv.z, fmaf(c4.w, xv.w, acc[1][m]))));
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + 256 * u;
+        a[u] = k < K ? ld4(w, w0 + k, wbf) : float4{0.f, 0.f, 0.f, 0.f};
+        c4[u] = k < K ? ld4(w, w1 + k, wbf) : float4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + 256 * u;
+        if (k < K) {
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            const float4 xv = *reinterpret_cast<const float4*>(&xs[m * K + k]);
+            acc[0][m] = fmaf(a[u].x, xv.x, fmaf(a[u].y, xv.y, fmaf(a[u].z, xv.z, fmaf(a[u].w, xv.w, acc[0][m]))));
+            acc[1][m] = fmaf(c4[u].x, xv.x, fmaf(c4[u].y, xv.y, fmaf(c4[u].z, xv.z, fmaf(c4[u].w, xv.w, acc[1][m]))));
+          }
+        }
       }
     }
 #pragma unroll
