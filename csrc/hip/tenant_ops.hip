@@ -127,11 +127,12 @@ __global__ __launch_bounds__(256) void rotary_kernel(const void* __restrict__ x,
 // cast next to an activation (a bf16 head's fp32 sigmoid output) is one pass,
 // f evaluated in fp32 and rounded once.  op: 0 identity, 1 relu, 2 sigmoid,
 // 3 silu, 4 gelu (erf), 5 tanh, 6 exp, 7 neg.
+// x rows of N at row stride ldx (ldx == N: flat) -> y [n / N, N] contiguous
 __global__ __launch_bounds__(256) void unary_kernel(const void* __restrict__ x, int xbf, void* __restrict__ y, int ybf,
-                                                    long long n, int op) {
+                                                    long long n, int op, int N, long long ldx) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const float v = ld_as_f32(x, i, xbf);
+  const float v = ld_as_f32(x, ldx == N ? i : (i / N) * ldx + i % N, xbf);
   float r;
   switch (op) {
     case 1: r = fmaxf(v, 0.f); break;
@@ -320,7 +321,21 @@ NOS_API int nos_im2col_h3(const float* x, void* P, long long pplane, float* rinv
 NOS_API int nos_unary(const void* x, int xbf16, void* y, int ybf16, long long n, int op, hipStream_t stream) {
   if (n <= 0 || op < 0 || op > 7 || (xbf16 != 0 && xbf16 != 1) || (ybf16 != 0 && ybf16 != 1))
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(unary_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, xbf16, y, ybf16, n, op);
+  hipLaunchKernelGGL(unary_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, xbf16, y, ybf16, n, op,
+                     1, 1LL);
+  return (int)hipGetLastError();
+}
+
+// the same over a row-strided x [M, N] (ldx >= N; e.g. a column slice of a merged
+// GEMM's output) into a contiguous y [M, N] -- no contiguous copy of x first
+NOS_API int nos_unary_rows(const void* x, long long ldx, int xbf16, void* y, int ybf16, long long M, int N, int op,
+                           hipStream_t stream) {
+  if (M <= 0 || N <= 0 || ldx < N || op < 0 || op > 7 || (xbf16 != 0 && xbf16 != 1) || (ybf16 != 0 && ybf16 != 1) ||
+      !x || !y)
+    return (int)hipErrorInvalidValue;
+  const long long n = M * N;
+  hipLaunchKernelGGL(unary_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, x, xbf16, y, ybf16, n, op,
+                     N, ldx);
   return (int)hipGetLastError();
 }
 

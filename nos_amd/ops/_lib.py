@@ -100,6 +100,7 @@ _SIGS = {
     "nos_im2col": [c_void_p, c_ll, c_ll, c_ll, c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                    c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nos_unary": [c_void_p, c_int, c_void_p, c_int, c_ll, c_int, c_void_p],
+    "nos_unary_rows": [c_void_p, c_ll, c_int, c_void_p, c_int, c_ll, c_int, c_int, c_void_p],
     "nos_glu": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_ll, c_int, c_int, c_int, c_void_p],
     # decode.hip: stateful decoding (K / V caches and positions on the device) and skinny GEMMs
     "nos_kv_write": [c_void_p, c_int, c_int, c_ll, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,

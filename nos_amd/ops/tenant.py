@@ -165,11 +165,22 @@ def unary(x: torch.Tensor, op: str, dtype: torch.dtype) -> torch.Tensor:
         y = {"relu": F.relu, "sigmoid": torch.sigmoid, "silu": F.silu, "gelu": F.gelu, "tanh": torch.tanh,
              "exp": torch.exp, "neg": torch.neg}[op](xf)
         return y.to(dtype)
-    xc = x.contiguous()
     out = torch.empty(x.shape, dtype=dtype, device=x.device)
-    if out.numel():
-        _lib.check(_lib.lib().nos_unary(xc.data_ptr(), _bf(xc), out.data_ptr(), int(dtype == torch.bfloat16),
-                                        xc.numel(), UNARY_CODES[op], _stream()), "nos_unary")
+    if not out.numel():
+        return out
+    N = x.shape[-1] if x.dim() else 1
+    try:   # rows at a uniform stride (e.g. a column slice of a merged GEMM's output): read in place
+        x2 = x.view(-1, N) if x.dim() > 1 else None
+    except RuntimeError:
+        x2 = None
+    if x2 is not None and not x.is_contiguous() and x2.stride(-1) == 1:
+        _lib.check(_lib.lib().nos_unary_rows(x2.data_ptr(), x2.stride(0), _bf(x2), out.data_ptr(),
+                                             int(dtype == torch.bfloat16), x2.shape[0], N, UNARY_CODES[op], _stream()),
+                   "nos_unary_rows")
+        return out
+    xc = x.contiguous()
+    _lib.check(_lib.lib().nos_unary(xc.data_ptr(), _bf(xc), out.data_ptr(), int(dtype == torch.bfloat16),
+                                    xc.numel(), UNARY_CODES[op], _stream()), "nos_unary")
     return out
 
 

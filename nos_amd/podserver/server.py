@@ -182,6 +182,28 @@ def _check_wire_dtype(sent, want: str, what: str) -> None:
         raise ValueError(f"{what} sent as {sent!r}, the tenant's model takes {want!r}")
 
 
+def _host_array(o) -> np.ndarray:
+    """An output on the host as fp32.  A row-strided output (a column slice of
+    a merged GEMM's result, e.g. the class logits beside the box columns)
+    travels as the covering row block and is sliced on the host -- no device
+    copy kernel to make it contiguous first."""
+    import torch
+
+    o = o.detach()
+    if o.is_cuda and not o.is_contiguous() and o.dim() >= 2 and o.stride(-1) == 1 and o.numel():
+        N = o.shape[-1]
+        try:
+            o2 = o.view(-1, N)
+        except RuntimeError:
+            o2 = None
+        if o2 is not None:
+            rows, ld = o2.shape[0], o2.stride(0)
+            if o2.storage_offset() + rows * ld <= o2.untyped_storage().nbytes() // o2.element_size():
+                block = torch.as_strided(o2, (rows, ld), (ld, 1))
+                return block.cpu()[:, :N].float().reshape(o.shape).numpy()
+    return o.float().cpu().numpy()
+
+
 class _JobQueue:
     """The lanes' work queue: two FIFOs, latency requests before throughput
     ones.  ``get(hi_only=True)`` (a priority lane) waits for a latency
@@ -1030,7 +1052,7 @@ class PodServer:
                 s.synchronize()
             if job.want_outputs:
                 sel = outs if job.want_outputs is True else [outs[i] for i in job.want_outputs if -len(outs) <= i < len(outs)]
-                job.outputs = [o.detach().float().cpu().numpy() for o in sel]
+                job.outputs = [_host_array(o) for o in sel]
             if t.state:
                 job.state = self._counters(t)
                 for name, rows in t.pos_limits.items():

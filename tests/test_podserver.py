@@ -412,3 +412,16 @@ def test_node_labeler_removes_the_pod_server_label_when_disabled():
     NodeLabeler(api, "n1", smi, pod_server_tenants=0).reconcile(Request("n1"))
     labels = ko.labels(api.get("Node", "n1"))
     assert C.LABEL_POD_SERVER_TENANTS not in labels and labels[C.LABEL_AMD_COUNT] == "1"
+
+
+def test_host_array_of_row_strided_outputs():
+    """Column slices of a merged result go to the host as their covering row
+    block (no contiguous copy); other layouts as before."""
+    import numpy as np
+    import torch
+
+    from nos_amd.podserver.server import _host_array
+
+    base = torch.arange(100 * 96, dtype=torch.float32).view(100, 96)
+    for t in (base[:, :92], base[:, 92:], base[10:20, 3:7], base.t(), base):
+        assert np.array_equal(_host_array(t), t.contiguous().numpy())

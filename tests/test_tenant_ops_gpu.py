@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -221,3 +222,17 @@ def test_cast_unary_matches_fp32_math(op, dts):
     tol = 2 ** -7 if dst == torch.bfloat16 else 2e-6
     err = (got.double().cpu() - ref).abs() / ref.abs().clamp_min(1.0)
     assert float(err.max()) <= tol
+
+
+def test_unary_reads_row_strided_slices_and_host_copies_them():
+    """A column slice of a merged GEMM's output: ``unary`` reads its rows in
+    place (nos_unary_rows), the server's host copy takes the covering rows."""
+    from nos_amd.podserver.server import _host_array
+
+    base = torch.randn(100, 96, device="cuda")
+    for sl in (base[:, 92:], base[:, :92], base[5:50, 10:20]):
+        for op, f in (("sigmoid", torch.sigmoid), ("relu", torch.relu)):
+            got = T.unary(sl, op, torch.float32)
+            assert got.is_contiguous() and torch.allclose(got, f(sl), rtol=1e-6, atol=1e-7)
+        assert np.array_equal(_host_array(sl), sl.cpu().numpy())
+    assert torch.equal(T.unary(base[:, :92].bfloat16(), "relu", torch.bfloat16), torch.relu(base[:, :92].bfloat16()))
