@@ -201,7 +201,9 @@ def _host_array(o) -> np.ndarray:
             if o2.storage_offset() + rows * ld <= o2.untyped_storage().nbytes() // o2.element_size():
                 block = torch.as_strided(o2, (rows, ld), (ld, 1))
                 return block.cpu()[:, :N].float().reshape(o.shape).numpy()
-    return o.float().cpu().numpy()
+    # to the host first, then fp32: a device-side cast (an int32 next-token id, a bf16
+    # output) would be one more kernel per request on the lane
+    return o.cpu().float().numpy()
 
 
 class _JobQueue:
