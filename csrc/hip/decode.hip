@@ -133,12 +133,24 @@ constexpr int MAXR = 32;     // query rows (G x Sq) per launch
 // head kvh * G + g); q rows scaled (and rotated) into LDS, the split's keys
 // into LDS, scores -> per-row max / sum -> probabilities in LDS, the split's
 // values into LDS, P V; the partial (acc[D], m, l) of every row to ws
+// the step's own K / V rows (written into the caches by this kernel instead of a
+// kv_write launch): token t of batch b at k + b * bsk + t * ldk + h * D (V alike),
+// cache row pos[b] + t; n = 0: none (the caches already hold them)
+struct Fresh {
+  const void* k = nullptr;
+  const void* v = nullptr;
+  void* kc = nullptr;
+  void* vc = nullptr;
+  long long bsk = 0, bsv = 0;
+  int ldk = 0, ldv = 0, bf = 0, n = 0;
+};
+
 template <int D>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const void* __restrict__ q, int qbf, int ldq, long long bsq, const void* __restrict__ kc,
     const void* __restrict__ vc, int cbf, const int* __restrict__ pos, const float* __restrict__ cs,
     const float* __restrict__ sn, int Rtab, float* __restrict__ ws, int B, int H, int Hkv, int Sq, int q0, int L,
-    int NS, float scale) {
+    int NS, float scale, Fresh fr) {
   constexpr int DP = D + 4;  // padded LDS row (16-byte reads of consecutive rows hit distinct banks)
   __shared__ __attribute__((aligned(16))) float qs[MAXR * D];
   __shared__ __attribute__((aligned(16))) float kv[KC * DP];
@@ -152,6 +164,52 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   const int kend = min(p0 + Sq, L);                        // keys 0 .. kend - 1 are visible to some row
   const int k0 = split * KC, nk = min(KC, kend - k0);
   float* const out = ws + (long long)blockIdx.x * R * (D + 2);
+  const long long cstride = (long long)Hkv * D;  // cache row (token) stride
+  // the first launch of a step writes the step's fresh K (rotated) / V rows that fall in
+  // this split's key range into the caches -- every split, empty or not, so a later
+  // launch (query rows q0 > 0) and the next step read them from the cache
+  const bool fresh = fr.n > 0 && q0 == 0 && pos[b] >= 0;
+  auto fresh_row = [&](int t, int d, bool isk, float& x0, float& x1) {
+    const void* src = isk ? fr.k : fr.v;
+    const long long o = (long long)b * (isk ? fr.bsk : fr.bsv) + (long long)t * (isk ? fr.ldk : fr.ldv) +
+                        (long long)kvh * D;
+    x0 = ldf(src, o + d, fr.bf);
+    x1 = ldf(src, o + d + D / 2, fr.bf);
+    if (isk && cs != nullptr) {
+      const long long tt = (long long)min(pos[b] + t, Rtab - 1) * D;
+      const float y0 = fmaf(x0, cs[tt + d], -x1 * sn[tt + d]);
+      const float y1 = fmaf(x1, cs[tt + d + D / 2], x0 * sn[tt + d + D / 2]);
+      x0 = y0;
+      x1 = y1;
+    }
+  };
+  if (fresh) {
+    for (int e = tid; e < 2 * fr.n * (D / 2); e += 256) {
+      const int isv = e >= fr.n * (D / 2), ee = isv ? e - fr.n * (D / 2) : e;
+      const int t = ee / (D / 2), d = ee % (D / 2), jabs = pos[b] + t;
+      if (jabs < k0 || jabs >= k0 + KC || jabs >= L) continue;
+      float x0, x1;
+      fresh_row(t, d, !isv, x0, x1);
+      void* cache = isv ? fr.vc : fr.kc;
+      const long long co = ((long long)b * L + jabs) * cstride + (long long)kvh * D;
+      stf(cache, co + d, x0, cbf);
+      stf(cache, co + d + D / 2, x1, cbf);
+    }
+  }
+  // the fresh rows this split attends come from the registers' source, not the cache
+  // (its stores above may still be in flight): staged over the cache's rows
+  auto overlay = [&](bool isk) {
+    if (!fresh) return;
+    __syncthreads();
+    for (int e = tid; e < fr.n * (D / 2); e += 256) {
+      const int t = e / (D / 2), d = e % (D / 2), j = pos[b] + t - k0;
+      if (j < 0 || j >= nk) continue;
+      float x0, x1;
+      fresh_row(t, d, isk, x0, x1);
+      kv[j * (D + 4) + d] = x0;
+      kv[j * (D + 4) + d + D / 2] = x1;
+    }
+  };
   if (nk <= 0 || p0 < 0) {  // an empty split (or a bad counter): l = 0, skipped by the combine
     for (int r = tid; r < R; r += 256) {
       out[r * (D + 2) + D] = -INFINITY;
@@ -176,7 +234,6 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     qs[r * D + d + D / 2] = x1 * scale;
   }
   // the split's keys -> LDS (rows past nk zero)
-  const long long cstride = (long long)Hkv * D;  // cache row (token) stride
   const long long cbase = ((long long)b * L + k0) * cstride + (long long)kvh * D;
   // every load of the split issued before the first LDS store (16 float4 per thread at
   // D = 128): a load-store loop left one cache-row latency exposed per iteration
@@ -196,6 +253,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     }
   };
   stage(kc);
+  overlay(true);
   __syncthreads();
   // scores: thread -> key j, rows of one parity
   {
@@ -247,6 +305,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
   }
   __syncthreads();  // every wave is done with the keys
   stage(vc);
+  overlay(false);
   __syncthreads();
   // P V: thread -> column d, rows of one residue
   {
@@ -509,16 +568,37 @@ NOS_API long long nos_attn_decode_workspace(int B, int H, int Hkv, int Sq, int L
 // cos / sin [R, D] fp32 (or null): q rotated at its positions.  out [B, Sq, H,
 // D] contiguous (obf: bf16).  Query tokens are processed in launches of at
 // most 32 / G (the rows a workgroup holds), each a decode pass + combine.
+// kn / vn (nfresh > 0): the step's own K / V rows [B, nfresh, Hkv, D] (token stride
+// ldk / ldv, batch stride bsk / bsv; nbf: bf16) -- written into the caches at
+// pos[b] + t (K rotated with cos / sin) by the attention itself, which reads them
+// from there: the kv_write launch of the step folded in (nfresh == Sq).
 NOS_API int nos_attn_decode(const void* q, int qbf, int ldq, long long bsq, const void* kc, const void* vc, int cbf,
                             const int* pos, const float* cos_t, const float* sin_t, int R, void* out, int obf, int B,
                             int H, int Hkv, int Sq, int L, int D, float scale, void* ws, long long ws_bytes,
-                            hipStream_t stream) {
+                            const void* kn, const void* vn, int nbf, int ldk, long long bsk, int ldv, long long bsv,
+                            int nfresh, hipStream_t stream) {
   if (B <= 0 || H <= 0 || Hkv <= 0 || H % Hkv || H / Hkv > MAXR || Sq <= 0 || L <= 0 || (D != 64 && D != 128) ||
       ldq < H * D || (B > 1 && bsq < (long long)(Sq - 1) * ldq + H * D) || !q || !kc || !vc || !pos || !out ||
       !ws || ((cos_t == nullptr) != (sin_t == nullptr)) || (cos_t && R <= 0) || (qbf != 0 && qbf != 1) ||
       (cbf != 0 && cbf != 1) || (obf != 0 && obf != 1) || !(scale > 0.f))
     return (int)hipErrorInvalidValue;
   if (ws_bytes < nos_attn_decode_workspace(B, H, Hkv, Sq, L, D)) return (int)hipErrorInvalidValue;
+  Fresh fr;
+  if (nfresh != 0) {
+    if (nfresh != Sq || !kn || !vn || (nbf != 0 && nbf != 1) || ldk < Hkv * D || ldv < Hkv * D ||
+        (B > 1 && (bsk < (long long)(Sq - 1) * ldk + Hkv * D || bsv < (long long)(Sq - 1) * ldv + Hkv * D)))
+      return (int)hipErrorInvalidValue;
+    fr.k = kn;
+    fr.v = vn;
+    fr.kc = const_cast<void*>(kc);
+    fr.vc = const_cast<void*>(vc);
+    fr.bsk = bsk;
+    fr.bsv = bsv;
+    fr.ldk = ldk;
+    fr.ldv = ldv;
+    fr.bf = nbf;
+    fr.n = nfresh;
+  }
   const int G = H / Hkv, chunk = MAXR / G;
   const int NS = (L + KC - 1) / KC;
   for (int q0 = 0; q0 < Sq; q0 += chunk) {
@@ -527,12 +607,12 @@ NOS_API int nos_attn_decode(const void* q, int qbf, int ldq, long long bsq, cons
     const unsigned rows = (unsigned)(B * Hkv * G * sq);
     if (D == 64) {
       hipLaunchKernelGGL(attn_decode_kernel<64>, dim3(grid), dim3(256), 0, stream, q, qbf, ldq, bsq, kc, vc, cbf, pos,
-                         cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale);
+                         cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale, fr);
       hipLaunchKernelGGL(attn_decode_combine_kernel<64>, dim3(rows), dim3(64), 0, stream,
                          static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
     } else {
       hipLaunchKernelGGL(attn_decode_kernel<128>, dim3(grid), dim3(256), 0, stream, q, qbf, ldq, bsq, kc, vc, cbf,
-                         pos, cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale);
+                         pos, cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale, fr);
       hipLaunchKernelGGL(attn_decode_combine_kernel<128>, dim3(rows), dim3(128), 0, stream,
                          static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
     }

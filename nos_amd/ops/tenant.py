@@ -608,14 +608,20 @@ def rotary_at(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: torch.
 
 
 def sdpa_cache(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos: torch.Tensor, scale: float | None = None,
-               rope: tuple | None = None) -> torch.Tensor:
+               rope: tuple | None = None, fresh: tuple | None = None) -> torch.Tensor:
     """Query i of sequence b, at position pos[b] + i, attends the cached keys
     0 .. pos[b] + i: q [B, Sq, H, D], caches [B, L, Hkv, D] (fp32 / bf16).
-    ``rope`` = (cos, sin): q rotated at its positions inside the kernel.  The
-    flash-decoding kernel (decode.hip) for CUDA tensors, fp32 math."""
-    from ..podserver.program.reference import rotary_at_ref, sdpa_cache_ref
+    ``rope`` = (cos, sin): q rotated at its positions inside the kernel.
+    ``fresh`` = (k, v) [B, Sq, Hkv, D]: the step's own K / V rows, written
+    into the caches at the positions (K rotated by ``rope``) by the same
+    launch -- a ``kv_write`` pair folded in.  The flash-decoding kernel
+    (decode.hip) for CUDA tensors, fp32 math."""
+    from ..podserver.program.reference import kv_write_ref, rotary_at_ref, sdpa_cache_ref
 
     if not q.is_cuda:
+        if fresh is not None:
+            kv_write_ref(kc, rotary_at_ref(fresh[0], rope[0], rope[1], pos) if rope else fresh[0], pos)
+            kv_write_ref(vc, fresh[1], pos)
         return sdpa_cache_ref(rotary_at_ref(q, rope[0], rope[1], pos) if rope else q, kc, vc, pos, scale)
     B, Sq, H, D = q.shape
     L, Hkv = kc.shape[1], kc.shape[2]
@@ -637,9 +643,27 @@ def sdpa_cache(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos: torch.T
     ws = torch.empty((max(nb, 4) // 4,), dtype=torch.float32, device=q.device)
     out = torch.empty((B, Sq, H, D), dtype=q.dtype, device=q.device)
     sc = scale if scale is not None else 1.0 / math.sqrt(D)
+    kn = vn = None
+    ldk = ldv = bsk = bsv = nbf = 0
+    if fresh is not None:
+        kn, vn = fresh
+        if kn.shape != (B, Sq, Hkv, D) or vn.shape != kn.shape or kn.dtype != vn.dtype:
+            raise ValueError(f"sdpa_cache: fresh K / V {tuple(kn.shape)} for q {tuple(q.shape)}")
+        try:
+            ldk, bsk = _rows_view(kn)
+        except ValueError:
+            kn = kn.contiguous()
+            ldk, bsk = _rows_view(kn)
+        try:
+            ldv, bsv = _rows_view(vn)
+        except ValueError:
+            vn = vn.contiguous()
+            ldv, bsv = _rows_view(vn)
+        nbf = _bf(kn)
     _lib.check(L_.nos_attn_decode(q.data_ptr(), _bf(q), ldq, bsq, kc.data_ptr(), vc.data_ptr(), _bf(kc),
                                   _i32_pos(pos, B).data_ptr(), _ptr(c), _ptr(s_), R, out.data_ptr(), _bf(out), B, H,
-                                  Hkv, Sq, L, D, float(sc), ws.data_ptr(), ws.numel() * 4, _stream()),
+                                  Hkv, Sq, L, D, float(sc), ws.data_ptr(), ws.numel() * 4, _ptr(kn), _ptr(vn), nbf,
+                                  ldk, bsk, ldv, bsv, Sq if fresh is not None else 0, _stream()),
                "nos_attn_decode")
     return out
 

@@ -71,6 +71,8 @@ class Lowered:
             steps = self._fuse_rotary_sdpa(steps)
             steps = self._fuse_rotary_at(steps)
             steps = self._merge_kv_writes(steps)
+            if "kv_into_attention" not in skip:
+                steps = self._fuse_kv_write_attention(steps)
             steps = self._fuse_gemv_glu(steps)
             if "cat_buffer" not in skip:
                 steps = self._cat_into_buffer(steps)
@@ -1006,6 +1008,39 @@ class Lowered:
             drop.add(id(wk))
             n += 1
         self.stats["kv_writes_paired"] = n
+        return [s for s in steps if id(s) not in drop]
+
+    def _fuse_kv_write_attention(self, steps: list[_Step]) -> list[_Step]:
+        """GPU: a layer's paired K / V cache write whose new cache versions only
+        its ``sdpa_cache`` reads, at the same positions and (K and q) with the
+        same rotary tables, folds into that attention launch: the decode kernel
+        writes the step's rows into the caches itself and attends them from
+        registers (decode.hip ``Fresh``) -- one launch per layer fewer."""
+        if not self.gpu:
+            return steps
+        uses = self._consumers(steps, self.outputs)
+        by_out = {s.output: s for s in steps}
+        drop, n = set(), 0
+        for s in steps:
+            if s.kind != "sdpa_cache" or s.attrs.get("fresh"):
+                continue
+            w = by_out.get(s.inputs[2])
+            if w is None or w.kind != "kv_write" or not w.attrs.get("pair") or s.inputs[1] != w.attrs.get("k_out"):
+                continue
+            rope = bool(w.attrs.get("rope"))
+            r = 5 if rope else 3                      # w: K cache, K x, pos, [cos, sin], V cache, V x
+            if (rope != bool(s.attrs.get("rope")) or s.inputs[3] != w.inputs[2]
+                    or (rope and list(w.inputs[3:5]) != list(s.inputs[4:6]))
+                    or uses.get(w.output) != 1 or uses.get(w.attrs["k_out"]) != 1
+                    or uses.get(w.inputs[0]) != 1 or uses.get(w.inputs[r]) != 1
+                    or tuple(self._shape(w.inputs[1]))[1] != tuple(self._shape(s.inputs[0]))[1]):
+                continue
+            s.inputs = [s.inputs[0], w.inputs[0], w.inputs[r], s.inputs[3]] + (list(s.inputs[4:6]) if rope else []) \
+                + [w.inputs[1], w.inputs[r + 1]]
+            s.attrs = {**s.attrs, "fresh": True}
+            drop.add(id(w))
+            n += 1
+        self.stats["kv_writes_into_attention"] = n
         return [s for s in steps if id(s) not in drop]
 
     def _prep_conv_weights(self, steps: list[_Step]) -> None:

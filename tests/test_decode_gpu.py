@@ -228,7 +228,8 @@ def test_gemv_glu_epilogue_matches_fp64(M):
 
 def test_decode_program_uses_the_fused_decode_kernels():
     """The GPU decode step: rotary fused into the cache write and the decode
-    attention, K and V written in one launch, SwiGLU in the gate-up GEMV."""
+    attention, K and V written in one launch -- folded into the attention
+    launch itself -- and SwiGLU in the gate-up GEMV."""
     from nos_amd.models.llama_program import llama_decode_programs
     from nos_amd.podserver import program as PG
 
@@ -237,5 +238,32 @@ def test_decode_program_uses_the_fused_decode_kernels():
     ps = PG.parse_variants(progs, w, gpu=True)
     c = ps[1].compile("cuda", params=ps[0].tensors("cuda"))
     assert c.stats["rotary_at_fused"] == 4 and c.stats["kv_writes_paired"] == 2 and c.stats["gemv_glu_fused"] == 2
+    assert c.stats["kv_writes_into_attention"] == 2   # the cache writes inside the decode attention launch
     kinds = [s.kind for s in c.steps if s.kind not in ("slice", "reshape")]
-    assert kinds.count("kv_write") == 2 and "glu" not in kinds and "rotary_at" not in kinds
+    assert "kv_write" not in kinds and "glu" not in kinds and "rotary_at" not in kinds
+
+
+@pytest.mark.parametrize("Sq, G", [(1, 4), (3, 2), (20, 4)])
+@pytest.mark.parametrize("rope", [False, True])
+def test_decode_attention_writes_the_fresh_rows(Sq, G, rope):
+    """sdpa_cache(fresh=(k, v)): the attention launch writes the step's K
+    (rotated) / V rows into the caches and attends them -- the same caches and
+    output as kv_write + sdpa_cache (Sq = 20 at G = 4: three query launches,
+    rows past the first launch's visible keys written too)."""
+    B, L, Hkv, D = 2, 300, 2, 128
+    H = G * Hkv
+    torch.manual_seed(Sq + G)
+    kc = torch.randn(B, L, Hkv, D, device="cuda")
+    vc = torch.randn(B, L, Hkv, D, device="cuda")
+    q = torch.randn(B, Sq, H, D, device="cuda")
+    kx = torch.randn(B, Sq, 3 * Hkv, D, device="cuda")[:, :, :Hkv]     # strided rows, as from a fused projection
+    vx = torch.randn(B, Sq, Hkv, D, device="cuda")
+    pos = torch.tensor([5, 126], dtype=torch.int32, device="cuda")      # the second crosses a 128-key split
+    tabs = _tables(L, D) if rope else None
+    kc2, vc2 = kc.clone(), vc.clone()
+    T.kv_write(kc2, kx, pos, rope=tabs, second=(vc2, vx))
+    ref = T.sdpa_cache(q, kc2, vc2, pos, rope=tabs)
+    got = T.sdpa_cache(q, kc, vc, pos, rope=tabs, fresh=(kx, vx))
+    torch.cuda.synchronize()
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    torch.testing.assert_close(got, ref, rtol=1e-6, atol=1e-6)
