@@ -380,7 +380,7 @@ __device__ __forceinline__ bool am_better(float bv, int bi, float av, int ai) {
 // ~180 us), wave shuffles, then the waves' winners through LDS
 template <int NT>
 __global__ __launch_bounds__(NT) void argmax_kernel(const void* __restrict__ x, int bf, int rows, int L, int ldx,
-                                                    int* __restrict__ out) {
+                                                    int* __restrict__ out, int* __restrict__ pos, int pos_n) {
   __shared__ float sv[NT / 64];
   __shared__ int si[NT / 64];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -424,6 +424,7 @@ __global__ __launch_bounds__(NT) void argmax_kernel(const void* __restrict__ x, 
         bi = si[w];
       }
     out[row] = bi >= L ? 0 : bi;  // an all -inf row: index 0
+    if (pos != nullptr) pos[row] += pos_n;  // the step's position advance folded in (row = sequence)
   }
 }
 
@@ -626,12 +627,18 @@ NOS_API int nos_pos_update(int* pos, int B, int add, int n, hipStream_t stream) 
   return (int)hipGetLastError();
 }
 
-NOS_API int nos_argmax(const void* x, int bf16, int rows, int L, int ldx, int* out, hipStream_t stream) {
-  if (!x || !out || rows <= 0 || L <= 0 || ldx < L || (bf16 != 0 && bf16 != 1)) return (int)hipErrorInvalidValue;
+// pos (or null): pos[row] += pos_n after row's maximum (a decode step's
+// position advance in the same launch; rows = the sequences)
+NOS_API int nos_argmax(const void* x, int bf16, int rows, int L, int ldx, int* out, int* pos, int pos_n,
+                       hipStream_t stream) {
+  if (!x || !out || rows <= 0 || L <= 0 || ldx < L || (bf16 != 0 && bf16 != 1) || pos_n < 0)
+    return (int)hipErrorInvalidValue;
   if (L >= 4096)
-    hipLaunchKernelGGL(argmax_kernel<1024>, dim3((unsigned)rows), dim3(1024), 0, stream, x, bf16, rows, L, ldx, out);
+    hipLaunchKernelGGL(argmax_kernel<1024>, dim3((unsigned)rows), dim3(1024), 0, stream, x, bf16, rows, L, ldx, out,
+                       pos, pos_n);
   else
-    hipLaunchKernelGGL(argmax_kernel<256>, dim3((unsigned)rows), dim3(256), 0, stream, x, bf16, rows, L, ldx, out);
+    hipLaunchKernelGGL(argmax_kernel<256>, dim3((unsigned)rows), dim3(256), 0, stream, x, bf16, rows, L, ldx, out,
+                       pos, pos_n);
   return (int)hipGetLastError();
 }
 

@@ -112,7 +112,7 @@ _SIGS = {
                         c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_ll,
                         c_void_p, c_void_p, c_int, c_int, c_ll, c_int, c_ll, c_int, c_void_p],
     "nos_pos_update": [c_void_p, c_int, c_int, c_int, c_void_p],
-    "nos_argmax": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "nos_argmax": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "nos_gemv": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int,
                  c_int, c_int, c_int, c_float, c_void_p],
     "nos_attn_h3g_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],

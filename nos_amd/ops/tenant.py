@@ -677,17 +677,23 @@ def pos_update(pos: torch.Tensor, add: bool, n: int) -> torch.Tensor:
     return pos
 
 
-def argmax(x: torch.Tensor) -> torch.Tensor:
-    """Index of the maximum over the last dim (first on ties), i32."""
+def argmax(x: torch.Tensor, pos: torch.Tensor | None = None, pos_n: int = 0) -> torch.Tensor:
+    """Index of the maximum over the last dim (first on ties), i32.
+    ``pos`` (i32, one counter per row of x): advanced by ``pos_n`` in the same
+    launch (a decode step's closing ``pos_add`` folded in)."""
     if not x.is_cuda:
+        if pos is not None:
+            pos.add_(pos_n)
         return x.float().argmax(dim=-1).to(torch.int32)
     L = x.shape[-1]
     x2 = x.reshape(-1, L)
     if x2.stride(-1) != 1:
         x2 = x2.contiguous()
+    if pos is not None and (pos.numel() != x2.shape[0] or pos.dtype != torch.int32 or not pos.is_contiguous()):
+        raise ValueError(f"argmax: pos needs one i32 counter per row ({x2.shape[0]})")
     out = torch.empty(x.shape[:-1], dtype=torch.int32, device=x.device)
-    _lib.check(_lib.lib().nos_argmax(x2.data_ptr(), _bf(x2), x2.shape[0], L, x2.stride(0), out.data_ptr(), _stream()),
-               "nos_argmax")
+    _lib.check(_lib.lib().nos_argmax(x2.data_ptr(), _bf(x2), x2.shape[0], L, x2.stride(0), out.data_ptr(), _ptr(pos),
+                                     int(pos_n), _stream()), "nos_argmax")
     return out
 
 

@@ -73,6 +73,7 @@ class Lowered:
             steps = self._merge_kv_writes(steps)
             if "kv_into_attention" not in skip:
                 steps = self._fuse_kv_write_attention(steps)
+            steps = self._fuse_argmax_pos(steps)
             steps = self._fuse_gemv_glu(steps)
             if "cat_buffer" not in skip:
                 steps = self._cat_into_buffer(steps)
@@ -1042,6 +1043,31 @@ class Lowered:
             n += 1
         self.stats["kv_writes_into_attention"] = n
         return [s for s in steps if id(s) not in drop]
+
+    def _fuse_argmax_pos(self, steps: list[_Step]) -> list[_Step]:
+        """GPU: a step's closing ``pos_add`` folds into the ``argmax`` right
+        before it when argmax has one row per counter and nothing between
+        them reads the counter (the decode step's last two launches become
+        one; argmax reads no position)."""
+        if not self.gpu:
+            return steps
+        uses = self._consumers(steps, self.outputs)
+        for k, p in enumerate(steps):
+            if p.kind != "pos_add" or k == 0:
+                continue
+            a = steps[k - 1]
+            shp = tuple(self._shape(a.inputs[0])) if a.kind == "argmax" else ()
+            pshape = tuple(self._shape(p.inputs[0]))
+            if (a.kind != "argmax" or a.attrs.get("pos_out") or len(pshape) != 1 or not shp
+                    or math.prod(shp[:-1]) != pshape[0] or uses.get(p.output, 0) != 0
+                    or self._dtype(p.inputs[0]) != "i32"):
+                continue
+            a.inputs = a.inputs + [p.inputs[0]]
+            a.attrs = {**a.attrs, "pos_out": p.output, "pos_n": int(p.attrs["n"])}
+            self.stats["pos_add_into_argmax"] = 1
+            return steps[:k] + steps[k + 1:]
+        self.stats["pos_add_into_argmax"] = 0
+        return steps
 
     def _prep_conv_weights(self, steps: list[_Step]) -> None:
         """GPU: every conv weight [OC, C, KH, KW] also as the fp32 [OC, Kp]

@@ -133,6 +133,9 @@ class CompiledProgram(Lowered):
                 y = T.rotary_at(a[0], a[1], a[2], a[3])
             elif k in ("pos_add", "pos_set"):
                 y = T.pos_update(a[0], add=k == "pos_add", n=int(s.attrs["n" if k == "pos_add" else "value"]))
+            elif k == "argmax" and s.attrs.get("pos_out"):   # the step's pos_add folded in
+                y = T.argmax(a[0], pos=a[1], pos_n=int(s.attrs["pos_n"]))
+                env[s.attrs["pos_out"]] = a[1]
             elif k == "argmax":
                 y = T.argmax(a[0])
             elif k == "cat_buffer":  # its GEMM part was written in place; the constant parts at build

@@ -114,6 +114,8 @@ def test_pos_update_and_argmax():
     assert T.argmax(x).tolist()[5:] == [7, 0]
     short = torch.randn(3, 1000, device="cuda")  # the 256-thread form
     assert torch.equal(T.argmax(short).long(), short.argmax(-1))
+    p3 = torch.tensor([4, 0, 9], dtype=torch.int32, device="cuda")   # a step's pos_add folded in
+    assert torch.equal(T.argmax(short, pos=p3, pos_n=2).long(), short.argmax(-1)) and p3.tolist() == [6, 2, 11]
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 5, 8])
@@ -239,8 +241,9 @@ def test_decode_program_uses_the_fused_decode_kernels():
     c = ps[1].compile("cuda", params=ps[0].tensors("cuda"))
     assert c.stats["rotary_at_fused"] == 4 and c.stats["kv_writes_paired"] == 2 and c.stats["gemv_glu_fused"] == 2
     assert c.stats["kv_writes_into_attention"] == 2   # the cache writes inside the decode attention launch
+    assert c.stats["pos_add_into_argmax"] == 1         # the position advance inside the argmax launch
     kinds = [s.kind for s in c.steps if s.kind not in ("slice", "reshape")]
-    assert "kv_write" not in kinds and "glu" not in kinds and "rotary_at" not in kinds
+    assert "kv_write" not in kinds and "glu" not in kinds and "rotary_at" not in kinds and "pos_add" not in kinds
 
 
 @pytest.mark.parametrize("Sq, G", [(1, 4), (3, 2), (20, 4)])
