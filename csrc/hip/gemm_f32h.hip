@@ -160,9 +160,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
   static_assert(APW * NW * 1024 == TA && WPW * NW * 1024 == 2 * BN * ROWB, "equal DMA count per wave");
   constexpr int LPS = APW + WPW;
   static_assert((RS - 2) * LPS < 64, "vmcnt range");
-  static_assert(MODE == 0 || (BM == 128 && (BN == 128 || BN == 64) && NW == 4 && BKT == 32 && !BATCHED &&
-                              (RS == 2 || (MODE == 2 && RS == 3))),
-                "the LayerNorm hand-off runs 128 x 128 or 128 x 64 2 x 2 tiles (the producer also on a 3-deep ring)");
+  static_assert(MODE == 0 || (BM == 128 && BKT == 32 && !BATCHED &&
+                              (((BN == 128 || BN == 64) && NW == 4 && (RS == 2 || (MODE == 2 && RS == 3))) ||
+                               (MODE == 1 && BN == 256 && NW == 8 && RS == 2))),
+                "the LayerNorm hand-off runs 128 x 128 or 128 x 64 2 x 2 tiles (the producer also on a 3-deep ring); "
+                "the LN-in-A-load also 128 x 256 with 2 x 4 waves");
   static_assert(MODE != 2 || BM * BN * 4 <= RS * STAGE, "the statistics tile fits the ring");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -265,13 +267,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     if constexpr (MODE == 1) {
     // A = LayerNorm(X): thread t owns rows t/4 and 64 + t/4 of the tile and the
     // 8-deep k chunk t%4 of each stage (one 16-byte piece per plane and row)
-    constexpr int AR = 2;
+    constexpr int AR = BM * 4 / (64 * NW);   // rows per thread: 2 with 4 waves, 1 with 8
+    constexpr int RSTEP = 64 * NW / 4;       // rows between a thread's rows
     const int q = tid & 3;
     float mul[AR], add[AR];
     const float* xr[AR];
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      int g = m0 + (tid >> 2) + 64 * i;
+      int g = m0 + (tid >> 2) + RSTEP * i;
       g = g < M ? g : M - 1;
       xr[i] = ln.x + (long long)g * ln.ldx + q * 8;
       const float2* st = ln.sin + (long long)g * ln.nparts;
@@ -295,7 +298,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN > 4 ? 1 : 2) void gemm_h3
     auto awrite = [&](unsigned char* dst) {
 #pragma unroll
       for (int i = 0; i < AR; ++i) {
-        const int row = (tid >> 2) + 64 * i;
+        const int row = (tid >> 2) + RSTEP * i;
         const float4 u = xa[i][0], w = xa[i][1];
         f16x2_t h0, l0, h1, l1, h2, l2, h3, l3;
         nos::split2h(f32x2_t{fmaf(u.x, mul[i], add[i]), fmaf(u.y, mul[i], add[i])}, h0, l0);
@@ -747,6 +750,9 @@ int g_hot_ring = 2;
 // residual GEMMs of a transformer): 128, or 64 (48 KiB ring: three workgroups
 // per CU); the statistics parts are this many columns wide
 int g_hot_bn = 128;
+// LN-in-A-load GEMMs that write the next GEMM's planes (fc1 -> fc2) on 128 x 256
+// tiles with 8 waves: half the per-workgroup A normalise-and-split work per MFMA
+bool g_lna_wide = false;
 
 // ------------------------------------------------------------ row split
 // LPR lanes per row (64: a wave; 32: a half-wave, two rows per wave), the
@@ -973,6 +979,11 @@ NOS_API int nos_gemm_f32h3_set_hot_bn(int bn) {
 }
 
 NOS_API int nos_gemm_f32h3_hot_bn() { return g_hot_bn; }
+
+NOS_API int nos_gemm_f32h3_set_lna_wide(int on) {
+  g_lna_wide = on != 0;
+  return 0;
+}
 
 NOS_API int nos_gemm_f32h3_set_hot_ring(int rs) {
   if (rs != 2 && rs != 3) return (int)hipErrorInvalidValue;
@@ -1248,8 +1259,13 @@ NOS_API int nos_gemm_f32h3_lna(const float* X, int ldx, const void* stats, int n
   ln.pw = pw;
   ln.eps = eps;
   ln.sc = ldexpf(1.f, eln);
-  // always 128 x 128: the LN-in-A-load normalises and splits its A tile per workgroup, so
-  // 128 x 64 tiles doubled that VALU work (fleet 760 vs 800 inf/s, profiles/r06_hot_bn_ab.json)
+  // 128 x 128 (or 128 x 256 for plane outputs, g_lna_wide): the LN-in-A-load normalises and
+  // splits its A tile per workgroup, so 128 x 64 tiles doubled that VALU work (fleet 760 vs
+  // 800 inf/s, profiles/r06_hot_bn_ab.json)
+  if (g_lna_wide && P != nullptr)
+    return launch_t<128, 256, 2, 4, 32, 2, false, 1>(nullptr, K, (long long)M * K, nullptr, ldexpf(1.f, -eln),
+                                                     static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
+                                                     C, ldc, M, N, K, epi, kv, po, Batch{}, stream, ln);
   return launch_t<128, 128, 2, 2, 32, 2, false, 1>(nullptr, K, (long long)M * K, nullptr, ldexpf(1.f, -eln),
                                                    static_cast<const _Float16*>(Wp), ldw, wplane, csc, bias, R, ldr,
                                                    C, ldc, M, N, K, epi, kv, po, Batch{}, stream, ln);

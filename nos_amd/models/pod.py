@@ -177,7 +177,9 @@ def kernel_config(memory_fraction: float | None, env: dict | None = None, cu_bud
             "h3_hot_ring": env.get("NOS_AMD_H3_HOT_RING") or "2",
             # tile width of the residual (row-statistics) h3 GEMMs: 128 x 128 (two workgroups per CU);
             # 128 x 64 (48 KiB, three) measured 2 % slower with the LN hand-off (profiles/r06_hot_bn_ab.json)
-            "h3_hot_bn": env.get("NOS_AMD_H3_HOT_BN") or "128"}
+            "h3_hot_bn": env.get("NOS_AMD_H3_HOT_BN") or "128",
+            # fc1-class LN-GEMMs (plane outputs) on 128 x 256 tiles, 8 waves
+            "h3_lna_wide": env.get("NOS_AMD_H3_LNA_WIDE") or "off"}
 
 
 def slice_cu_budget(env: dict | None = None) -> int:
@@ -275,7 +277,7 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             torch.backends.cuda.matmul.allow_tf32 = False  # true fp32 GEMMs (no reduced-precision shortcut)
             from ..ops import (set_attention_f32_variant, set_cu_budget, set_f32_math, set_gemm_f32_policy,
                                set_gemm_f32h3_hot_bn, set_gemm_f32h3_hot_ring, set_gemm_f32h3_layout,
-                               set_gemm_f32x6_tile, set_gemm_policy, set_ln_handoff)
+                               set_gemm_f32h3_lna_wide, set_gemm_f32x6_tile, set_gemm_policy, set_ln_handoff)
 
             budget = slice_cu_budget(os.environ)
             cfg = kernel_config(frac, os.environ, budget)
@@ -288,6 +290,7 @@ def run_pod(status: str, slot: int, out: str, dtype: str = "fp32", graphs: bool 
             set_gemm_f32h3_layout(cfg["h3_layout"])
             set_gemm_f32h3_hot_ring(int(cfg["h3_hot_ring"]))
             set_gemm_f32h3_hot_bn(int(cfg["h3_hot_bn"]))
+            set_gemm_f32h3_lna_wide(cfg["h3_lna_wide"] == "on")
             if budget:  # CU-mask slice: slice-sized persistent grids (ops.set_cu_budget)
                 set_cu_budget(budget)
         m, x = _build(dtype, seed, demo_input_hw(), device)

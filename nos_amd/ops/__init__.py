@@ -473,6 +473,13 @@ def set_gemm_f32h3_hot_bn(bn: int) -> None:
     _lib.check(_lib.lib().nos_gemm_f32h3_set_hot_bn(int(bn)), "nos_gemm_f32h3_set_hot_bn")
 
 
+def set_gemm_f32h3_lna_wide(on: bool) -> None:
+    """LN-in-A-load GEMMs writing the next GEMM's planes (fc1 -> fc2) on
+    128 x 256 tiles with 8 waves (half the A normalise-and-split work per
+    MFMA) instead of 128 x 128 -- A/B; the results are bit-identical."""
+    _lib.check(_lib.lib().nos_gemm_f32h3_set_lna_wide(int(bool(on))), "nos_gemm_f32h3_set_lna_wide")
+
+
 def stats_pw() -> int:
     """Column width of a row-statistics part (the producer GEMM's tile width)."""
     return int(_lib.lib().nos_gemm_f32h3_hot_bn())
@@ -971,5 +978,5 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float | 
     return out
 
 
-__all__ = ["set_ln_handoff", "ln_handoff_active", "set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "set_gemm_f32h3_hot_ring", "set_gemm_f32h3_hot_bn", "stats_pw", "H3Planes", "set_attention_f32h3_waves", "linear_planes", "linear_ln_to_planes", "h3_planes_active", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
+__all__ = ["set_ln_handoff", "ln_handoff_active", "set_f32_math", "f32_math", "h3_head_scales", "linear_ln_qkv_h3", "split_f32_weight_h3", "set_gemm_f32h3_layout", "set_gemm_f32h3_hot_ring", "set_gemm_f32h3_hot_bn", "set_gemm_f32h3_lna_wide", "stats_pw", "H3Planes", "set_attention_f32h3_waves", "linear_planes", "linear_ln_to_planes", "h3_planes_active", "attention_presplit_h3", "ln_qkv_fusable", "ln_qkv_attention", "set_gemm_f32x6_tile", "set_gemm_f32x6_pipeline", "linear_ln_qkv_x6", "attention_presplit", "split_f32_weight", "split_bf16x3", "set_cu_budget", "cu_budget", "set_gemm_policy", "set_gemm_persistent", "linear", "linear_ln", "fold_layernorm", "layernorm", "attention", "attention_qkv", "linear_ref",
            "linear_ln_ref", "layernorm_ref", "attention_ref"]

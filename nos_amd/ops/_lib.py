@@ -127,6 +127,7 @@ _SIGS = {
     "nos_gemm_f32h3_set_hot_ring": [c_int],
     "nos_gemm_f32h3_set_hot_bn": [c_int],
     "nos_gemm_f32h3_hot_bn": [],
+    "nos_gemm_f32h3_set_lna_wide": [c_int],
     "nos_attn_h3g_set_kvsplit": [c_int],
     "nos_attn_h3g": [c_void_p, c_int, c_ll, c_void_p, c_int, c_ll, c_void_p, c_int, c_ll, c_void_p, c_int, c_ll,
                      c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_float, c_void_p,

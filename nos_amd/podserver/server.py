@@ -365,7 +365,7 @@ class PodServer:
         """Process-wide kernel configs; a graph keeps the ones it was captured under."""
         from ..ops import set_attention_f32_variant, set_f32_math, set_gemm_f32_policy, set_gemm_f32x6_tile, \
             set_gemm_f32h3_hot_bn, set_gemm_f32h3_hot_ring, set_gemm_f32h3_layout, set_gemm_f32h3_lds_epilogue, \
-            set_gemm_policy, set_ln_handoff
+            set_gemm_f32h3_lna_wide, set_gemm_policy, set_ln_handoff
 
         set_gemm_policy(cfg["gemm_bf16"])
         set_gemm_f32_policy(cfg["gemm_f32"])
@@ -377,6 +377,7 @@ class PodServer:
         set_gemm_f32h3_layout(cfg.get("h3_layout", "2x2"))
         set_gemm_f32h3_hot_ring(int(cfg.get("h3_hot_ring", "2")))
         set_gemm_f32h3_hot_bn(int(cfg.get("h3_hot_bn", "128")))
+        set_gemm_f32h3_lna_wide(cfg.get("h3_lna_wide", "off") == "on")
 
     def start(self) -> "PodServer":
         self._init_device()

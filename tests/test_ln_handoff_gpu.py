@@ -174,3 +174,22 @@ def test_lds_epilogue_equals_the_register_epilogue(M, N, K, act):
             ops.set_gemm_f32h3_lds_epilogue(False)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+def test_wide_lna_tiles_are_bit_identical():
+    """fc1 (LN in the A load, GELU, the next GEMM's planes) on 128 x 256 tiles
+    with 8 waves (ops.set_gemm_f32h3_lna_wide) equals the 128 x 128 form."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(1, 3401, 384, device="cuda", generator=g)
+    w1 = torch.randn(1536, 384, device="cuda", generator=g) / 384 ** 0.5
+    c1 = torch.randn(1536, device="cuda", generator=g) * 0.1
+    ops.set_ln_handoff(True)
+    outs = []
+    for on in (False, True):
+        ops.set_gemm_f32h3_lna_wide(on)
+        try:
+            pl = ops.linear_ln_to_planes(x, w1, w1.sum(1), c1, act="gelu", eps=1e-12)
+            outs.append(pl.planes.clone())
+        finally:
+            ops.set_gemm_f32h3_lna_wide(False)
+    assert torch.equal(outs[0], outs[1])

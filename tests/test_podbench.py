@@ -138,17 +138,17 @@ def test_pod_kernel_config_follows_the_slice():
 
     whole = kernel_config(None, {})
     assert whole == {"gemm_bf16": "latency", "gemm_f32": "latency", "attention_f32": "h3", "f32_math": "h3",
-                     "gemm_f32x6_tile": "policy", "ln_handoff": "on", "h3_epilogue": "lds", "h3_layout": "2x2", "h3_hot_ring": "2", "h3_hot_bn": "128"}
+                     "gemm_f32x6_tile": "policy", "ln_handoff": "on", "h3_epilogue": "lds", "h3_layout": "2x2", "h3_hot_ring": "2", "h3_hot_bn": "128", "h3_lna_wide": "off"}
     assert kernel_config(1.0, {}) == whole
     frac = kernel_config(36 / 288, {})
     assert frac == {"gemm_bf16": "throughput", "gemm_f32": "small", "attention_f32": "h3n", "f32_math": "h3",
                     "gemm_f32x6_tile": "128x128", "ln_handoff": "on",
-                                                         "h3_epilogue": "lds", "h3_layout": "2x2", "h3_hot_ring": "2", "h3_hot_bn": "128"}
+                                                         "h3_epilogue": "lds", "h3_layout": "2x2", "h3_hot_ring": "2", "h3_hot_bn": "128", "h3_lna_wide": "off"}
     # an exclusive CU-mask slice plans for its own CUs (budget-aware tiles)
     assert kernel_config(36 / 288, {}, cu_budget=32) == {"gemm_bf16": "throughput", "gemm_f32": "latency",
                                                          "attention_f32": "h3n", "f32_math": "h3",
                                                          "gemm_f32x6_tile": "128x128", "ln_handoff": "on",
-                                                         "h3_epilogue": "lds", "h3_layout": "2x2", "h3_hot_ring": "2", "h3_hot_bn": "128"}
+                                                         "h3_epilogue": "lds", "h3_layout": "2x2", "h3_hot_ring": "2", "h3_hot_bn": "128", "h3_lna_wide": "off"}
     assert kernel_config(None, {}, cu_budget=32) == whole
     # A/B overrides win over the slice rule: the exact-f32 MFMA kernels stay selectable
     assert kernel_config(0.125, {"NOS_AMD_ATTN_F32_VARIANT": "w4k64"})["attention_f32"] == "w4k64"

@@ -53,6 +53,7 @@ def main() -> None:
     ops.set_gemm_f32h3_layout(cfg["h3_layout"])
     ops.set_gemm_f32h3_hot_ring(int(cfg["h3_hot_ring"]))
     ops.set_gemm_f32h3_hot_bn(int(cfg["h3_hot_bn"]))
+    ops.set_gemm_f32h3_lna_wide(cfg["h3_lna_wide"] == "on")
     print("kernel config", cfg, flush=True)
     m, x = _build(a.dtype, 0, demo_input_hw())
     s = torch.cuda.Stream()

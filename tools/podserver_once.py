@@ -95,6 +95,8 @@ def main() -> None:
                     help="LDS ring of the residual / row-statistics h3 GEMMs (NOS_AMD_H3_HOT_RING)")
     ap.add_argument("--h3-hot-bn", default=None, choices=["64", "128"],
                     help="tile width of the LN hand-off h3 GEMMs (NOS_AMD_H3_HOT_BN)")
+    ap.add_argument("--h3-lna-wide", default=None, choices=["on", "off"],
+                    help="fc1-class LN-GEMMs on 128 x 256 tiles, 8 waves (NOS_AMD_H3_LNA_WIDE)")
     ap.add_argument("--h3-attn-waves", type=int, default=8, choices=[4, 8], help="h3 attention waves per workgroup")
     ap.add_argument("--lds-epi", type=int, default=None, help="plain fp32-C h3 GEMMs store C through LDS (1) or "
                     "from the MFMA registers (0) (NOS_AMD_H3_EPILOGUE: the server's kernel config)")
@@ -117,6 +119,8 @@ def main() -> None:
         os.environ["NOS_AMD_H3_LAYOUT"] = a.h3_layout
     if a.h3_hot_ring is not None:
         os.environ["NOS_AMD_H3_HOT_RING"] = a.h3_hot_ring
+    if a.h3_lna_wide is not None:
+        os.environ["NOS_AMD_H3_LNA_WIDE"] = a.h3_lna_wide
     if a.h3_hot_bn is not None:
         os.environ["NOS_AMD_H3_HOT_BN"] = a.h3_hot_bn
     if a.lds_epi is not None:
