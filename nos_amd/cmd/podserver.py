@@ -99,6 +99,8 @@ def main(argv=None) -> int:
     ap.add_argument("--latency-cus", type=int, default=0,
                     help="CUs (multiple of 8, XCD-symmetric) reserved for the priority lanes; the other lanes' streams "
                          "are CU-masked to the rest")
+    ap.add_argument("--masked-queues", type=int, default=8,
+                    help="with --latency-cus: CU-masked streams (hardware queues) the throughput lanes share")
     ap.add_argument("--max-tenants", type=int, default=48)
     ap.add_argument("--memory-gb", type=float, default=0.0, help="slice memory the server admits (0 = the GPU's)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
@@ -116,7 +118,7 @@ def main(argv=None) -> int:
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
     if args.gpus:
         rest = ["--socket-dir", args.socket_dir, "--lanes", str(args.lanes), "--priority-lanes",
-                str(args.priority_lanes), "--latency-cus", str(args.latency_cus), "--max-tenants", str(args.max_tenants),
+                str(args.priority_lanes), "--latency-cus", str(args.latency_cus), "--masked-queues", str(args.masked_queues), "--max-tenants", str(args.max_tenants),
                 "--memory-gb", str(args.memory_gb), "--device", args.device, "--log-level", args.log_level]
         if args.no_graphs:
             rest.append("--no-graphs")
@@ -146,7 +148,7 @@ def main(argv=None) -> int:
 
         lister = GrpcLister(args.pod_resources_socket)
     srv = PodServer(path, device=args.device, lanes=args.lanes, priority_lanes=args.priority_lanes,
-                    latency_cus=args.latency_cus,
+                    latency_cus=args.latency_cus, masked_queues=args.masked_queues,
                     max_tenants=args.max_tenants,
                     memory_gb=args.memory_gb or None, graphs=not args.no_graphs,
                     solo_graphs=not args.no_solo_graphs, allocations_dir=records, pod_resources=lister).start()

@@ -114,6 +114,7 @@ class Tenant:
     latency: bool = False          # served by the priority lanes (a generation step per request)
     state: dict = field(default_factory=dict)       # persistent buffers (K / V caches, positions), every variant's
     pos_limits: dict = field(default_factory=dict)  # position state -> rows of the caches written at it
+    host: dict = field(default_factory=dict)        # pinned staging buffers (input, outputs, counters)
 
 
 @dataclass
@@ -126,6 +127,7 @@ class _Variant:
     outputs: tuple = ()
     solo_graph: object = None
     solo_outputs: tuple = ()
+    host: dict = field(default_factory=dict)
 
 
 @dataclass
@@ -187,23 +189,70 @@ def _host_array(o) -> np.ndarray:
     a merged GEMM's result, e.g. the class logits beside the box columns)
     travels as the covering row block and is sliced on the host -- no device
     copy kernel to make it contiguous first."""
-    import torch
-
     o = o.detach()
-    if o.is_cuda and not o.is_contiguous() and o.dim() >= 2 and o.stride(-1) == 1 and o.numel():
-        N = o.shape[-1]
-        try:
-            o2 = o.view(-1, N)
-        except RuntimeError:
-            o2 = None
-        if o2 is not None:
-            rows, ld = o2.shape[0], o2.stride(0)
-            if o2.storage_offset() + rows * ld <= o2.untyped_storage().nbytes() // o2.element_size():
-                block = torch.as_strided(o2, (rows, ld), (ld, 1))
-                return block.cpu()[:, :N].float().reshape(o.shape).numpy()
+    block = _covering_block(o) if o.is_cuda else None
+    if block is not None:
+        return block.cpu()[:, :o.shape[-1]].float().reshape(o.shape).numpy()
     # to the host first, then fp32: a device-side cast (an int32 next-token id, a bf16
     # output) would be one more kernel per request on the lane
     return o.cpu().float().numpy()
+
+
+def _covering_block(o):
+    """The contiguous ``(rows, ld)`` block a row-strided output lies in
+    (``o.view(-1, N)`` with unit column stride), or None."""
+    import torch
+
+    if o.is_contiguous() or o.dim() < 2 or o.stride(-1) != 1 or not o.numel():
+        return None
+    N = o.shape[-1]
+    try:
+        o2 = o.view(-1, N)
+    except RuntimeError:
+        return None
+    rows, ld = o2.shape[0], o2.stride(0)
+    if o2.storage_offset() + rows * ld > o2.untyped_storage().nbytes() // o2.element_size():
+        return None
+    return torch.as_strided(o2, (rows, ld), (ld, 1))
+
+
+def _pinned(cache: dict, key, shape, dtype):
+    """A pinned host staging buffer of ``shape`` / ``dtype``, kept in ``cache``
+    (a tenant's or variant's): one per input / output slot, reused by every
+    request (a tenant's requests run one at a time)."""
+    import torch
+
+    b = cache.get(key)
+    if b is None or tuple(b.shape) != tuple(shape) or b.dtype != dtype:
+        b = cache[key] = torch.empty(tuple(shape), dtype=dtype, pin_memory=True)
+    return b
+
+
+def _fetch_start(o, cache: dict, key):
+    """Queue ``o``'s device -> host copy into a pinned buffer on the current
+    stream and return the function that, once the stream is synchronised,
+    gives it as fp32 numpy (what ``_host_array`` gives).  A decode step's
+    outputs and counters then reach the host behind ONE synchronisation
+    instead of a blocking pageable copy each."""
+    import torch
+
+    o = o.detach()
+    if not o.is_cuda:
+        return lambda: _host_array(o)
+    block = _covering_block(o)
+    src = block if block is not None else o
+    if not src.is_contiguous():
+        return lambda: _host_array(o)     # after the synchronisation: a plain blocking copy
+    hb = _pinned(cache, key, src.shape, src.dtype)
+    hb.copy_(src, non_blocking=True)
+
+    def done():
+        h = hb[:, :o.shape[-1]].reshape(o.shape) if block is not None else hb
+        if h.dtype in (torch.bfloat16, torch.float16):
+            h = h.float()
+        return np.array(h.numpy(), dtype=np.float32)   # a copy: the buffer serves the next request
+
+    return done
 
 
 class _JobQueue:
@@ -250,7 +299,7 @@ class PodServer:
                  allocations_dir: str | os.PathLike | None = None, pod_resources=None,
                  reap_interval_s: float = 1.0, max_inflight_register_gb: float = 16.0,
                  register_timeout_s: float = 30.0, register_min_mb_s: float = 50.0, priority_lanes: int = 0,
-                 latency_cus: int = 0):
+                 latency_cus: int = 0, masked_queues: int = 8):
         """``allocations_dir``: this GPU's allocation records (tokens
         required; allocations.py).  Without it admission is open: the client
         declares its slice, which must be > 0 when the server accounts
@@ -267,7 +316,9 @@ class PodServer:
         (a multiple of 8, XCD-symmetric): that many CUs reserved for the
         priority lanes -- their streams are CU-masked to them and the other
         lanes' to the rest, so a decode step's chain of small kernels never
-        waits for CUs held by a throughput tenant's long workgroups."""
+        waits for CUs held by a throughput tenant's long workgroups.
+        ``masked_queues``: with ``latency_cus``, the number of CU-masked
+        streams (each a hardware queue) the throughput lanes share."""
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.path = Path(socket_path)
@@ -285,6 +336,9 @@ class PodServer:
         self.latency_cus = int(latency_cus)
         if self.latency_cus and (self.latency_cus % 8 or self.latency_cus < 0 or not self.priority_lanes_n):
             raise ValueError("latency_cus must be a positive multiple of 8 (one share per XCD) with priority lanes")
+        self.masked_queues = int(masked_queues)
+        if self.masked_queues < 1:
+            raise ValueError("masked_queues must be >= 1")
         self._masked: list = []   # CU-masked lane streams (latency_cus) to close at stop
         self._hi_lanes: list = []
         self._stop = threading.Event()
@@ -343,10 +397,14 @@ class PodServer:
             if self.latency_cus >= ncu:
                 raise ValueError(f"latency_cus {self.latency_cus} leaves no CU of {ncu} to the other lanes")
             rest = range(self.latency_cus, ncu)
-            self._masked = [CUMaskedStream(rest, ncu) for _ in range(self.lanes_n)]
+            # every CU-masked stream is a hardware queue of its own (GPU_MAX_HW_QUEUES does not
+            # pool them): past ~10 of them the decoders starved (16 + 2: 182 ms / token, 8 + 2:
+            # 5 ms), so the throughput lanes share at most masked_queues of them, round robin
+            nq = min(self.lanes_n, self.masked_queues)
+            self._masked = [CUMaskedStream(rest, ncu) for _ in range(nq)]
             self._masked += [CUMaskedStream(range(self.latency_cus), ncu) for _ in range(self.priority_lanes_n)]
-            self._lanes = [m.torch for m in self._masked[:self.lanes_n]]
-            self._hi_lanes = [m.torch for m in self._masked[self.lanes_n:]]
+            self._lanes = [self._masked[i % nq].torch for i in range(self.lanes_n)]
+            self._hi_lanes = [m.torch for m in self._masked[nq:]]
         else:
             self._lanes = [torch.cuda.Stream() for _ in range(self.lanes_n)]
             # latency lanes: the highest stream priority (HSA queue priority), dispatched first
@@ -355,6 +413,7 @@ class PodServer:
         self._setup_stream = torch.cuda.Stream()
         self.info = {"device": props.name, "multiprocessor_count": props.multi_processor_count,
                      "lanes": self.lanes_n, "priority_lanes": self.priority_lanes_n, "latency_cus": self.latency_cus,
+                     "masked_queues": min(self.lanes_n, self.masked_queues) if self.latency_cus else 0,
                      "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                      "memory_gb": round(self.memory_gb, 1), "kernel_config": cfg,
                      "solo_kernel_config": self.solo_config,
@@ -1038,13 +1097,22 @@ class PodServer:
                 if x_in is not None:
                     v.x.copy_(torch.from_numpy(x_in.copy()).view(v.x.shape))
                 v.outputs = outs = v.model(v.x)
+                fetch = [lambda o=o: _host_array(o) for o in self._selected(outs, job.want_outputs)]
+                counters = lambda: self._counters(t)  # noqa: E731
             else:
                 s = t.stream.torch if t.stream is not None else lane
                 with torch.cuda.stream(s):
                     if x_in is not None:
-                        v.x.copy_(torch.from_numpy(x_in.copy()).view(v.x.shape).to(v.x.dtype), non_blocking=False)
+                        if str(v.x.dtype)[6:] == str(x_in.dtype):
+                            # through a pinned buffer: an in-stream copy, no blocking pageable one
+                            hb = _pinned(v.host, "x", v.x.shape, v.x.dtype)
+                            hb.numpy().reshape(-1)[:] = x_in
+                            v.x.copy_(hb, non_blocking=True)
+                        else:
+                            v.x.copy_(torch.from_numpy(x_in.copy()).view(v.x.shape).to(v.x.dtype), non_blocking=False)
                     outs = v.outputs
-                    if alone and v.solo_graph is not None:
+                    solo = alone and v.solo_graph is not None
+                    if solo:
                         v.solo_graph.replay()
                         outs = v.solo_outputs
                         t.solo_completed += 1
@@ -1052,17 +1120,30 @@ class PodServer:
                         v.graph.replay()
                     else:
                         v.outputs = outs = v.model(v.x)
+                    fetch = [_fetch_start(outs[i], v.host, ("out", solo, i))
+                             for i in self._selected(range(len(outs)), job.want_outputs)]
+                    counters = self._counters_start(t) if t.state else None
                 s.synchronize()
             if job.want_outputs:
-                sel = outs if job.want_outputs is True else [outs[i] for i in job.want_outputs if -len(outs) <= i < len(outs)]
-                job.outputs = [_host_array(o) for o in sel]
+                job.outputs = [f() for f in fetch]
             if t.state:
-                job.state = self._counters(t)
+                job.state = counters()
                 for name, rows in t.pos_limits.items():
                     over = [p for p in job.state.get(name, ()) if p > rows]
                     if over:
                         raise RuntimeError(f"context full: position {max(over)} is past the {rows} cache rows "
                                            f"(state {name!r}); reset the tenant or start a new sequence")
+
+    @staticmethod
+    def _selected(items, want) -> list:
+        """The outputs a request asked for: all (``True``), none, or the listed
+        indices (negative ones count from the end; out-of-range ones dropped)."""
+        items = list(items)
+        if not want:
+            return []
+        if want is True:
+            return items
+        return [items[i] for i in want if -len(items) <= i < len(items)]
 
     def _counters(self, t: Tenant) -> dict:
         """A stateful tenant's small i32 states (its positions), read back
@@ -1071,6 +1152,19 @@ class PodServer:
 
         return {k: [int(v) for v in st.cpu().tolist()] for k, st in t.state.items()
                 if st.dtype == torch.int32 and st.numel() <= 64}
+
+    def _counters_start(self, t: Tenant):
+        """``_counters`` behind the lane's one synchronisation: the copies are
+        queued on the current stream into pinned buffers; the returned
+        function reads them once the stream is synchronised."""
+        import torch
+
+        bufs = {}
+        for k, st in t.state.items():
+            if st.dtype == torch.int32 and st.numel() <= 64:
+                hb = bufs[k] = _pinned(t.host, ("state", k), st.shape, st.dtype)
+                hb.copy_(st, non_blocking=True)
+        return lambda: {k: [int(v) for v in hb.tolist()] for k, hb in bufs.items()}
 
     def _reset_state(self, t: Tenant) -> None:
         """Zero a tenant's state (a new sequence at position 0).  Its requests

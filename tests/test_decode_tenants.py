@@ -302,3 +302,13 @@ def test_latency_cus_must_be_xcd_symmetric(tmp_path):
     for bad, pl in ((12, 2), (-8, 2), (16, 0)):
         with pytest.raises(ValueError, match="latency_cus"):
             PodServer(tmp_path / "s.sock", device="cpu", priority_lanes=pl, latency_cus=bad)
+    with pytest.raises(ValueError, match="masked_queues"):
+        PodServer(tmp_path / "s.sock", device="cpu", priority_lanes=2, latency_cus=16, masked_queues=0)
+
+
+def test_selected_outputs():
+    from nos_amd.podserver.server import PodServer
+
+    sel = PodServer._selected
+    assert sel([1, 2, 3], True) == [1, 2, 3] and sel([1, 2, 3], False) == [] and sel([1, 2, 3], None) == []
+    assert sel([1, 2, 3], [0, -1, 5, -4]) == [1, 3]

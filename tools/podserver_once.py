@@ -83,6 +83,8 @@ def main() -> None:
     ap.add_argument("--lanes", type=int, default=16)
     ap.add_argument("--priority-lanes", type=int, default=0, help="high-priority lanes for the decode tenants")
     ap.add_argument("--latency-cus", type=int, default=0, help="CUs reserved for the priority lanes (multiple of 8)")
+    ap.add_argument("--masked-queues", type=int, default=8, help="CU-masked streams the throughput lanes share "
+                    "(with --latency-cus)")
     ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES (0: lanes + priority lanes)")
     ap.add_argument("--window", type=float, default=8.0)
     ap.add_argument("--warmup", type=float, default=2.0)
@@ -131,7 +133,7 @@ def main() -> None:
 
     path = Path(tempfile.mkdtemp(prefix="nos_ps_", dir="/tmp")) / "gpu-0" / "server.sock"
     srv = PodServer(path, device="cuda", lanes=a.lanes, priority_lanes=a.priority_lanes, latency_cus=a.latency_cus,
-                    max_tenants=max(48, a.tenants)).start()
+                    masked_queues=a.masked_queues, max_tenants=max(48, a.tenants)).start()
     from nos_amd import ops
 
     ops.set_gemm_f32x6_pipeline(bool(a.pipeline))  # process-wide: every capture below
