@@ -145,12 +145,59 @@ struct Fresh {
   int ldk = 0, ldv = 0, bf = 0, n = 0;
 };
 
+// row r of group bk = (b, kvh): out[b, q0 + qi, h, d] = sum_s e^(m_s - M) acc_s / sum_s
+// e^(m_s - M) l_s over the NS splits' partials (splits with l = 0 skipped)
+template <int D>
+__device__ __forceinline__ void decode_combine_row(const float* __restrict__ ws, void* __restrict__ o, int obf,
+                                                   int bk, int r, int d, int NS, int G, int R, int H, int Hkv,
+                                                   int Sq_total, int q0) {
+  const int kvh = bk % Hkv, b = bk / Hkv;
+  const int qi = r / G, h = kvh * G + r % G;
+  float M = -INFINITY;
+  for (int s = 0; s < NS; ++s) {
+    const float* p = ws + ((long long)(bk * NS + s) * R + r) * (D + 2);
+    if (p[D + 1] > 0.f) M = fmaxf(M, p[D]);
+  }
+  float num = 0.f, den = 0.f;
+  for (int s = 0; s < NS; ++s) {
+    const float* p = ws + ((long long)(bk * NS + s) * R + r) * (D + 2);
+    if (p[D + 1] > 0.f) {
+      const float w = __expf(p[D] - M);
+      num = fmaf(w, p[d], num);
+      den = fmaf(w, p[D + 1], den);
+    }
+  }
+  const long long oo = (((long long)b * Sq_total + q0 + qi) * H + h) * D + d;
+  stf(o, oo, den > 0.f ? num / den : 0.f, obf);
+}
+
+// the combine launch folded into the decode launch (sync != null): each workgroup
+// publishes its partial (device-scope fence: the splits run on different XCDs, each
+// with its own L2), counts itself in on its group's counter, and the group's last
+// workgroup combines the NS partials and zeroes the counter for the next launch.
+// No workgroup waits on another, so the grid drains whatever the order.
+template <int D>
+__device__ __forceinline__ void decode_combine_last(const float* __restrict__ ws, int* __restrict__ sync,
+                                                    void* __restrict__ o, int obf, int bk, int NS, int G, int R,
+                                                    int H, int Hkv, int Sq_total, int q0, int tid) {
+  if (sync == nullptr) return;
+  __shared__ int last;
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(&sync[bk], 1) == NS - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  for (int e = tid; e < R * D; e += 256) decode_combine_row<D>(ws, o, obf, bk, e / D, e % D, NS, G, R, H, Hkv, Sq_total, q0);
+  if (tid == 0) atomicExch(&sync[bk], 0);
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const void* __restrict__ q, int qbf, int ldq, long long bsq, const void* __restrict__ kc,
     const void* __restrict__ vc, int cbf, const int* __restrict__ pos, const float* __restrict__ cs,
     const float* __restrict__ sn, int Rtab, float* __restrict__ ws, int B, int H, int Hkv, int Sq, int q0, int L,
-    int NS, float scale, Fresh fr) {
+    int NS, float scale, Fresh fr, int* __restrict__ sync, void* __restrict__ o, int obf, int Sq_total) {
   constexpr int DP = D + 4;  // padded LDS row (16-byte reads of consecutive rows hit distinct banks)
   __shared__ __attribute__((aligned(16))) float qs[MAXR * D];
   __shared__ __attribute__((aligned(16))) float kv[KC * DP];
@@ -215,6 +262,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       out[r * (D + 2) + D] = -INFINITY;
       out[r * (D + 2) + D + 1] = 0.f;
     }
+    decode_combine_last<D>(ws, sync, o, obf, bk, NS, G, R, H, Hkv, Sq_total, q0, tid);
     return;
   }
   // q rows -> LDS, times the softmax scale (rotated at their positions first)
@@ -328,6 +376,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       out[r * (D + 2) + D + 1] = lrow[r];
     }
   }
+  decode_combine_last<D>(ws, sync, o, obf, bk, NS, G, R, H, Hkv, Sq_total, q0, tid);
 }
 
 // out[b, q0 + qi, h, :] = sum_s e^(m_s - M) acc_s / sum_s e^(m_s - M) l_s over the splits
@@ -337,26 +386,7 @@ __global__ __launch_bounds__(D) void attn_decode_combine_kernel(const float* __r
                                                                 int Sq_total, int NS) {
   const int G = H / Hkv, R = G * Sq;
   const int row = blockIdx.x;  // (b, kvh, r)
-  const int r = row % R, bk = row / R;
-  const int kvh = bk % Hkv, b = bk / Hkv;
-  const int qi = r / G, g = r % G, h = kvh * G + g;
-  const int d = threadIdx.x;
-  float M = -INFINITY;
-  for (int s = 0; s < NS; ++s) {
-    const float* p = ws + ((long long)(bk * NS + s) * R + r) * (D + 2);
-    if (p[D + 1] > 0.f) M = fmaxf(M, p[D]);
-  }
-  float num = 0.f, den = 0.f;
-  for (int s = 0; s < NS; ++s) {
-    const float* p = ws + ((long long)(bk * NS + s) * R + r) * (D + 2);
-    if (p[D + 1] > 0.f) {
-      const float w = __expf(p[D] - M);
-      num = fmaf(w, p[d], num);
-      den = fmaf(w, p[D + 1], den);
-    }
-  }
-  const long long oo = (((long long)b * Sq_total + q0 + qi) * H + h) * D + d;
-  stf(o, oo, den > 0.f ? num / den : 0.f, obf);
+  decode_combine_row<D>(ws, o, obf, row / R, row % R, threadIdx.x, NS, G, R, H, Hkv, Sq_total, q0);
 }
 
 // ------------------------------------------------------------------ positions, argmax
@@ -572,18 +602,21 @@ NOS_API long long nos_attn_decode_workspace(int B, int H, int Hkv, int Sq, int L
 // kn / vn (nfresh > 0): the step's own K / V rows [B, nfresh, Hkv, D] (token stride
 // ldk / ldv, batch stride bsk / bsv; nbf: bf16) -- written into the caches at
 // pos[b] + t (K rotated with cos / sin) by the attention itself, which reads them
-// from there: the kv_write launch of the step folded in (nfresh == Sq).
+// from there: the kv_write launch of the step folded in (nfresh == Sq).  sync
+// (sync_n >= B x Hkv i32, zero before the first call, left zero by each): the
+// combine folded into the decode launch (its last workgroup per (b, kv head)).
 NOS_API int nos_attn_decode(const void* q, int qbf, int ldq, long long bsq, const void* kc, const void* vc, int cbf,
                             const int* pos, const float* cos_t, const float* sin_t, int R, void* out, int obf, int B,
                             int H, int Hkv, int Sq, int L, int D, float scale, void* ws, long long ws_bytes,
                             const void* kn, const void* vn, int nbf, int ldk, long long bsk, int ldv, long long bsv,
-                            int nfresh, hipStream_t stream) {
+                            int nfresh, int* sync, long long sync_n, hipStream_t stream) {
   if (B <= 0 || H <= 0 || Hkv <= 0 || H % Hkv || H / Hkv > MAXR || Sq <= 0 || L <= 0 || (D != 64 && D != 128) ||
       ldq < H * D || (B > 1 && bsq < (long long)(Sq - 1) * ldq + H * D) || !q || !kc || !vc || !pos || !out ||
       !ws || ((cos_t == nullptr) != (sin_t == nullptr)) || (cos_t && R <= 0) || (qbf != 0 && qbf != 1) ||
       (cbf != 0 && cbf != 1) || (obf != 0 && obf != 1) || !(scale > 0.f))
     return (int)hipErrorInvalidValue;
   if (ws_bytes < nos_attn_decode_workspace(B, H, Hkv, Sq, L, D)) return (int)hipErrorInvalidValue;
+  if (sync != nullptr && sync_n < (long long)B * Hkv) return (int)hipErrorInvalidValue;
   Fresh fr;
   if (nfresh != 0) {
     if (nfresh != Sq || !kn || !vn || (nbf != 0 && nbf != 1) || ldk < Hkv * D || ldv < Hkv * D ||
@@ -608,14 +641,18 @@ NOS_API int nos_attn_decode(const void* q, int qbf, int ldq, long long bsq, cons
     const unsigned rows = (unsigned)(B * Hkv * G * sq);
     if (D == 64) {
       hipLaunchKernelGGL(attn_decode_kernel<64>, dim3(grid), dim3(256), 0, stream, q, qbf, ldq, bsq, kc, vc, cbf, pos,
-                         cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale, fr);
-      hipLaunchKernelGGL(attn_decode_combine_kernel<64>, dim3(rows), dim3(64), 0, stream,
-                         static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
+                         cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale, fr, sync, out,
+                         obf, Sq);
+      if (!sync)
+        hipLaunchKernelGGL(attn_decode_combine_kernel<64>, dim3(rows), dim3(64), 0, stream,
+                           static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
     } else {
       hipLaunchKernelGGL(attn_decode_kernel<128>, dim3(grid), dim3(256), 0, stream, q, qbf, ldq, bsq, kc, vc, cbf,
-                         pos, cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale, fr);
-      hipLaunchKernelGGL(attn_decode_combine_kernel<128>, dim3(rows), dim3(128), 0, stream,
-                         static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
+                         pos, cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale, fr, sync,
+                         out, obf, Sq);
+      if (!sync)
+        hipLaunchKernelGGL(attn_decode_combine_kernel<128>, dim3(rows), dim3(128), 0, stream,
+                           static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
     }
   }
   return (int)hipGetLastError();

@@ -110,7 +110,7 @@ _SIGS = {
     "nos_attn_decode_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
     "nos_attn_decode": [c_void_p, c_int, c_int, c_ll, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                         c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_ll,
-                        c_void_p, c_void_p, c_int, c_int, c_ll, c_int, c_ll, c_int, c_void_p],
+                        c_void_p, c_void_p, c_int, c_int, c_ll, c_int, c_ll, c_int, c_void_p, c_ll, c_void_p],
     "nos_pos_update": [c_void_p, c_int, c_int, c_int, c_void_p],
     "nos_argmax": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "nos_gemv": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int,

@@ -608,14 +608,17 @@ def rotary_at(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: torch.
 
 
 def sdpa_cache(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos: torch.Tensor, scale: float | None = None,
-               rope: tuple | None = None, fresh: tuple | None = None) -> torch.Tensor:
+               rope: tuple | None = None, fresh: tuple | None = None, sync: torch.Tensor | None = None) -> torch.Tensor:
     """Query i of sequence b, at position pos[b] + i, attends the cached keys
     0 .. pos[b] + i: q [B, Sq, H, D], caches [B, L, Hkv, D] (fp32 / bf16).
     ``rope`` = (cos, sin): q rotated at its positions inside the kernel.
     ``fresh`` = (k, v) [B, Sq, Hkv, D]: the step's own K / V rows, written
     into the caches at the positions (K rotated by ``rope``) by the same
-    launch -- a ``kv_write`` pair folded in.  The flash-decoding kernel
-    (decode.hip) for CUDA tensors, fp32 math."""
+    launch -- a ``kv_write`` pair folded in.  ``sync``: a zeroed int32
+    device buffer of >= B x Hkv counters owned by the call site (the kernel
+    leaves it zero): the split combine runs in the decode launch's last
+    workgroup per K / V head instead of a launch of its own.  The
+    flash-decoding kernel (decode.hip) for CUDA tensors, fp32 math."""
     from ..podserver.program.reference import kv_write_ref, rotary_at_ref, sdpa_cache_ref
 
     if not q.is_cuda:
@@ -660,10 +663,14 @@ def sdpa_cache(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos: torch.T
             vn = vn.contiguous()
             ldv, bsv = _rows_view(vn)
         nbf = _bf(kn)
+    if sync is not None and (not sync.is_cuda or sync.dtype != torch.int32 or not sync.is_contiguous()
+                             or sync.numel() < B * Hkv):
+        raise ValueError(f"sdpa_cache: sync needs >= {B * Hkv} contiguous int32 device counters")
     _lib.check(L_.nos_attn_decode(q.data_ptr(), _bf(q), ldq, bsq, kc.data_ptr(), vc.data_ptr(), _bf(kc),
                                   _i32_pos(pos, B).data_ptr(), _ptr(c), _ptr(s_), R, out.data_ptr(), _bf(out), B, H,
                                   Hkv, Sq, L, D, float(sc), ws.data_ptr(), ws.numel() * 4, _ptr(kn), _ptr(vn), nbf,
-                                  ldk, bsk, ldv, bsv, Sq if fresh is not None else 0, _stream()),
+                                  ldk, bsk, ldv, bsv, Sq if fresh is not None else 0, _ptr(sync),
+                                  sync.numel() if sync is not None else 0, _stream()),
                "nos_attn_decode")
     return out
 

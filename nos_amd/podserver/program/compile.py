@@ -73,6 +73,8 @@ class Lowered:
             steps = self._merge_kv_writes(steps)
             if "kv_into_attention" not in skip:
                 steps = self._fuse_kv_write_attention(steps)
+            if os.environ.get("NOS_AMD_FOLD_DECODE_COMBINE", "0") == "1":   # opt-in (A/B: slower alone)
+                self._fold_decode_combines(steps)
             steps = self._fuse_argmax_pos(steps)
             steps = self._fuse_gemv_glu(steps)
             if "cat_buffer" not in skip:
@@ -1043,6 +1045,30 @@ class Lowered:
             n += 1
         self.stats["kv_writes_into_attention"] = n
         return [s for s in steps if id(s) not in drop]
+
+    def _fold_decode_combines(self, steps: list[_Step]) -> None:
+        """GPU: every ``sdpa_cache`` gets its own zeroed counters (B x Hkv
+        int32, kept with the program): the flash-decoding split combine then
+        runs in the decode launch's last workgroup per K / V head
+        (decode.hip ``decode_combine_last``) -- one launch per layer fewer.
+        Opt-in (``NOS_AMD_FOLD_DECODE_COMBINE=1``): one decoder alone ran
+        0.69-0.74 ms / token with it against 0.65 without (every workgroup's
+        device-scope release writes its XCD's L2 back), 8 decoders 2.63 against
+        2.70 ms (``profiles/r06_decode_combine_fold_ab.json``)."""
+        import torch
+
+        if not self.gpu:
+            return
+        n = 0
+        for s in steps:
+            if s.kind != "sdpa_cache":
+                continue
+            B, Hkv = tuple(self._shape(s.inputs[1]))[0], tuple(self._shape(s.inputs[1]))[2]
+            name = s.output + "::sync"
+            self.aux[name] = torch.zeros(B * Hkv, dtype=torch.int32, device=self.device)
+            s.attrs = {**s.attrs, "sync": name}
+            n += 1
+        self.stats["decode_combines_folded"] = n
 
     def _fuse_argmax_pos(self, steps: list[_Step]) -> list[_Step]:
         """GPU: a step's closing ``pos_add`` folds into the ``argmax`` right

@@ -128,7 +128,8 @@ class CompiledProgram(Lowered):
             elif k == "sdpa_cache":
                 y = T.sdpa_cache(a[0], a[1], a[2], a[3], scale=s.attrs.get("scale"),
                                  rope=(a[4], a[5]) if s.attrs.get("rope") else None,
-                                 fresh=(a[-2], a[-1]) if s.attrs.get("fresh") else None)
+                                 fresh=(a[-2], a[-1]) if s.attrs.get("fresh") else None,
+                                 sync=self.aux.get(s.attrs.get("sync")))
             elif k == "rotary_at":
                 y = T.rotary_at(a[0], a[1], a[2], a[3])
             elif k in ("pos_add", "pos_set"):

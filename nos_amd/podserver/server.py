@@ -258,7 +258,9 @@ def _fetch_start(o, cache: dict, key):
 class _JobQueue:
     """The lanes' work queue: two FIFOs, latency requests before throughput
     ones.  ``get(hi_only=True)`` (a priority lane) waits for a latency
-    request only; ``close()`` makes every ``get`` return None."""
+    request only, ``get(lo_only=True)`` (a throughput lane beside CU-reserved
+    priority lanes) for a throughput one; ``close()`` makes every ``get``
+    return None."""
 
     def __init__(self):
         self._cv = threading.Condition()
@@ -271,10 +273,10 @@ class _JobQueue:
             (self._hi if hi else self._lo).append(job)
             self._cv.notify_all()   # a priority lane may be the one waiting
 
-    def get(self, hi_only: bool = False):
+    def get(self, hi_only: bool = False, lo_only: bool = False):
         with self._cv:
             while True:   # what was queued before close() still runs
-                if self._hi:
+                if self._hi and not lo_only:
                     return self._hi.popleft()
                 if self._lo and not hi_only:
                     return self._lo.popleft()
@@ -1041,7 +1043,10 @@ class PodServer:
 
         lane = (self._hi_lanes if hi else self._lanes)[i] if self.gpu else None
         while True:
-            job = self._jobs.get(hi_only=hi)
+            # beside CU-reserved priority lanes the throughput lanes leave latency requests
+            # to them: a decode step queued on a shared masked stream behind an inference
+            # waited for it (16 lanes over 8 masked queues: 12 ms / token)
+            job = self._jobs.get(hi_only=hi, lo_only=not hi and bool(self.latency_cus))
             if job is None:
                 return
             job.t_start = time.monotonic()

@@ -81,6 +81,12 @@ def test_decode_attention_matches_fp64(D, G, Sq, L, cdt):
     e = float((got.double().cpu() - ref64).abs().max())
     e32 = float((ref32.double() - ref64).abs().max())
     assert e <= max(4 * e32, 2e-6), (e, e32)
+    # the combine folded into the decode launch (last workgroup per K / V head): the
+    # same arithmetic, bit for bit, and the counters left zero for the next call
+    sync = torch.zeros(B * Hkv + 3, dtype=torch.int32, device="cuda")
+    for _ in range(2):
+        assert torch.equal(T.sdpa_cache(q, kc, vc, pos, sync=sync), got)
+        assert int(sync.abs().sum()) == 0
 
 
 def test_decode_attention_with_fused_rotary_and_bad_positions():
@@ -98,6 +104,12 @@ def test_decode_attention_with_fused_rotary_and_bad_positions():
     assert torch.isfinite(got).all()
     bad = T.sdpa_cache(q, kc, vc, torch.tensor([-5, 0, 0], dtype=torch.int32, device="cuda"))
     assert torch.isfinite(bad).all() and float(bad[0].abs().max()) == 0.0
+    sync = torch.zeros(B * Hkv, dtype=torch.int32, device="cuda")
+    assert torch.equal(T.sdpa_cache(q, kc, vc, pos, rope=(c, s), sync=sync), got)
+    assert torch.equal(T.sdpa_cache(q, kc, vc, torch.tensor([-5, 0, 0], dtype=torch.int32, device="cuda"),
+                                    sync=sync), bad) and int(sync.abs().sum()) == 0
+    with pytest.raises(ValueError, match="sync"):
+        T.sdpa_cache(q, kc, vc, pos, sync=sync[:2])
 
 
 def test_pos_update_and_argmax():
@@ -228,13 +240,14 @@ def test_gemv_glu_epilogue_matches_fp64(M):
     assert float((got.double() - ref).abs().max() / ref.abs().max()) < 2e-6
 
 
-def test_decode_program_uses_the_fused_decode_kernels():
+def test_decode_program_uses_the_fused_decode_kernels(monkeypatch):
     """The GPU decode step: rotary fused into the cache write and the decode
     attention, K and V written in one launch -- folded into the attention
     launch itself -- and SwiGLU in the gate-up GEMV."""
     from nos_amd.models.llama_program import llama_decode_programs
     from nos_amd.podserver import program as PG
 
+    monkeypatch.setenv("NOS_AMD_FOLD_DECODE_COMBINE", "1")
     m = _llama(False)
     progs, w = llama_decode_programs(m, 8, 64)
     ps = PG.parse_variants(progs, w, gpu=True)
@@ -242,6 +255,7 @@ def test_decode_program_uses_the_fused_decode_kernels():
     assert c.stats["rotary_at_fused"] == 4 and c.stats["kv_writes_paired"] == 2 and c.stats["gemv_glu_fused"] == 2
     assert c.stats["kv_writes_into_attention"] == 2   # the cache writes inside the decode attention launch
     assert c.stats["pos_add_into_argmax"] == 1         # the position advance inside the argmax launch
+    assert c.stats["decode_combines_folded"] == 2      # the split combines inside the decode launches
     kinds = [s.kind for s in c.steps if s.kind not in ("slice", "reshape")]
     assert "kv_write" not in kinds and "glu" not in kinds and "rotary_at" not in kinds and "pos_add" not in kinds
 

@@ -294,6 +294,13 @@ def test_job_queue_serves_latency_requests_first():
     assert got == ["d2"] and q.qsize() == 1
     q.close()
     assert q.get() == "t2" and q.get() is None and q.get(hi_only=True) is None
+    # a throughput lane beside CU-reserved priority lanes leaves latency requests to them
+    q = _JobQueue()
+    q.put("d1", hi=True)
+    q.put("t1")
+    assert q.get(lo_only=True) == "t1" and q.qsize() == 1
+    q.close()
+    assert q.get(lo_only=True) is None and q.get(hi_only=True) == "d1"
 
 
 def test_latency_cus_must_be_xcd_symmetric(tmp_path):
