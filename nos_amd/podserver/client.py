@@ -177,14 +177,19 @@ class PodClient:
         sequence.  Returns the reply (``state``: the counters, now 0)."""
         return self._call({"op": "reset"})[0]
 
-    def generate(self, prompt: np.ndarray, max_new_tokens: int, next_output: int = -1) -> tuple[np.ndarray, dict]:
+    def generate(self, prompt: np.ndarray, max_new_tokens: int, next_output: int = -1,
+                 server_loop: bool = True) -> tuple[np.ndarray, dict]:
         """Greedy generation on a stateful decoder tenant
         (models/llama_program.llama_decode_programs): the prompt ids [B, P]
-        go to the prefill variant, then one [B, 1] decode request per new
-        token, each returning only the program's next-ids output
-        (``next_output``).  Returns (ids [B, max_new_tokens], timings: the
-        prefill's and every decode step's round trip in seconds, the server's
-        final counters)."""
+        go to the prefill variant, then the decode variant runs once per new
+        token, fed the program's next-ids output (``next_output``).
+        ``server_loop``: the decode steps run as ONE ``generate`` request --
+        the server replays the decode graph back to back, feeding the ids on
+        the device, and returns every token at the end (no host round trip
+        per token); otherwise one [B, 1] request per token.  Returns (ids [B,
+        max_new_tokens], timings: the prefill's round trip, every decode
+        step's (server loop: the loop's time / steps), the server's final
+        counters)."""
         prompt = np.asarray(prompt)
         B = prompt.shape[0]
         t0 = time.monotonic()
@@ -192,12 +197,24 @@ class PodClient:
         t1 = time.monotonic()
         tok = outs[0].reshape(B, -1)[:, -1].astype(np.int32)
         toks, steps = [tok], []
-        for _ in range(max_new_tokens - 1):
+        n = max_new_tokens - 1
+        if server_loop and n > 0:
+            wire = _wire(tok.reshape(B, 1), self.input_dtype, "input")
+            req = {"op": "generate", "steps": n, "output": next_output, "shape": [B, 1],
+                   "dtype": "i32" if wire.dtype == np.int32 else "f32"}
             s0 = time.monotonic()
-            outs, rep = self.infer(tok.reshape(B, 1), outputs=[next_output])
-            steps.append(time.monotonic() - s0)
-            tok = outs[0].reshape(B, -1)[:, -1].astype(np.int32)
-            toks.append(tok)
+            rep, data = self._call(req, wire.tobytes())
+            dt = time.monotonic() - s0
+            ids = P.unpack_arrays(rep["outputs"], data)[0].reshape(n, B, -1)[:, :, -1].astype(np.int32)
+            toks += list(ids)
+            steps = [dt / n] * n
+        else:
+            for _ in range(n):
+                s0 = time.monotonic()
+                outs, rep = self.infer(tok.reshape(B, 1), outputs=[next_output])
+                steps.append(time.monotonic() - s0)
+                tok = outs[0].reshape(B, -1)[:, -1].astype(np.int32)
+                toks.append(tok)
         return np.stack(toks, axis=1), {"prefill_s": t1 - t0, "step_s": steps, "state": rep.get("state")}
 
     def train_step(self, x: np.ndarray, target: np.ndarray) -> dict:

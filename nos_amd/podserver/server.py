@@ -138,6 +138,8 @@ class _Job:
     shape: tuple | None = None
     kind: str = "infer"            # or "train": one optimisation step, payload = input + target
     x_bytes: int = 0
+    steps: int = 1                 # "generate": runs, each fed the previous run's output ``feed``
+    feed: int = -1
     loss: float | None = None
     done: threading.Event = field(default_factory=threading.Event)
     t_enq: float = field(default_factory=time.monotonic)
@@ -603,6 +605,27 @@ class PodServer:
                         if job.state is not None:
                             rep["state"] = job.state
                         P.send_msg(conn, rep, out)
+                    elif op == "generate":   # a stateful tenant's decode loop, run in the server
+                        if tenant is None:
+                            raise AdmissionError("register first")
+                        if not tenant.state or tenant.trainer is not None:
+                            raise ValueError("generate needs a stateful (decode) tenant")
+                        n, feed = req.get("steps"), req.get("output", -1)
+                        if (not isinstance(n, int) or isinstance(n, bool) or not 1 <= n <= 4096
+                                or not isinstance(feed, int) or isinstance(feed, bool)):
+                            raise ValueError("generate: steps must be an int in [1, 4096], output an output index")
+                        shp = req.get("shape")
+                        shp = tuple(int(d) for d in shp) if isinstance(shp, list) and len(shp) <= 8 else None
+                        _check_wire_dtype(req.get("dtype"), _wire_dtype(tenant.x), "input")
+                        job = _Job(tenant, payload, [feed], shp, kind="generate", steps=n, feed=feed)
+                        self._jobs.put(job, hi=tenant.latency)
+                        job.done.wait()
+                        if job.error:
+                            raise RuntimeError(job.error)
+                        descs, out = P.pack_arrays(job.outputs)
+                        P.send_msg(conn, {"ok": True, "queue_us": round(1e6 * (job.t_start - job.t_enq), 1),
+                                          "gpu_us": round(1e6 * (job.t_end - job.t_start), 1), "outputs": descs,
+                                          "state": job.state}, out)
                     elif op == "reset":
                         if tenant is None:
                             raise AdmissionError("register first")
@@ -1097,11 +1120,31 @@ class PodServer:
                 raise ValueError(f"input has {x_in.size} values, the tenant's model takes {v.x.numel()}")
             if ids and t.id_bound is not None and x_in.size and (x_in.min() < 0 or x_in.max() >= t.id_bound):
                 raise ValueError(f"token ids must lie in [0, {t.id_bound})")
+        gen = job.kind == "generate"
+
+        def fed(outs) -> object:
+            """generate: the output fed back as the next run's input (ids)."""
+            if not -len(outs) <= job.feed < len(outs):
+                raise ValueError(f"generate: output {job.feed} of {len(outs)}")
+            o = outs[job.feed]
+            if o.numel() != v.x.numel() or o.dtype != v.x.dtype:
+                raise ValueError(f"generate: output {job.feed} {tuple(o.shape)} {o.dtype} does not feed the input "
+                                 f"{tuple(v.x.shape)} {v.x.dtype}")
+            return o
+
         with torch.no_grad():
             if not self.gpu:
                 if x_in is not None:
                     v.x.copy_(torch.from_numpy(x_in.copy()).view(v.x.shape))
                 v.outputs = outs = v.model(v.x)
+                if gen:
+                    toks = [fed(outs).clone()]
+                    for _ in range(job.steps - 1):
+                        v.x.copy_(toks[-1].reshape(v.x.shape))
+                        v.outputs = outs = v.model(v.x)
+                        toks.append(fed(outs).clone())
+                    outs = [torch.stack(toks)]
+                    job.want_outputs = [0]
                 fetch = [lambda o=o: _host_array(o) for o in self._selected(outs, job.want_outputs)]
                 counters = lambda: self._counters(t)  # noqa: E731
             else:
@@ -1115,18 +1158,30 @@ class PodServer:
                             v.x.copy_(hb, non_blocking=True)
                         else:
                             v.x.copy_(torch.from_numpy(x_in.copy()).view(v.x.shape).to(v.x.dtype), non_blocking=False)
-                    outs = v.outputs
                     solo = alone and v.solo_graph is not None
-                    if solo:
-                        v.solo_graph.replay()
-                        outs = v.solo_outputs
-                        t.solo_completed += 1
-                    elif v.graph is not None:
-                        v.graph.replay()
+                    toks = None
+                    for i in range(job.steps if gen else 1):
+                        if i:   # generate: the previous run's ids are this run's input, on the device
+                            v.x.copy_(o.reshape(v.x.shape))
+                        outs = v.outputs
+                        if solo:
+                            v.solo_graph.replay()
+                            outs = v.solo_outputs
+                            t.solo_completed += 1
+                        elif v.graph is not None:
+                            v.graph.replay()
+                        else:
+                            v.outputs = outs = v.model(v.x)
+                        if gen:
+                            o = fed(outs)
+                            if toks is None:
+                                toks = torch.empty((job.steps,) + tuple(o.shape), dtype=o.dtype, device=o.device)
+                            toks[i].copy_(o)
+                    if gen:
+                        fetch = [_fetch_start(toks, v.host, "gen")]
                     else:
-                        v.outputs = outs = v.model(v.x)
-                    fetch = [_fetch_start(outs[i], v.host, ("out", solo, i))
-                             for i in self._selected(range(len(outs)), job.want_outputs)]
+                        fetch = [_fetch_start(outs[i], v.host, ("out", solo, i))
+                                 for i in self._selected(range(len(outs)), job.want_outputs)]
                     counters = self._counters_start(t) if t.state else None
                 s.synchronize()
             if job.want_outputs:

@@ -68,6 +68,32 @@ def test_server_generation_matches_hf_generate_token_for_token(model, tenant, se
     c.close()
 
 
+def test_server_loop_equals_per_token_requests(model, tenant, server):
+    """generate(server_loop=True): ONE request runs the decode steps in the
+    server, ids fed back on the device -- the same tokens and final position
+    as a request per token; bad generate requests are refused."""
+    progs, w = tenant
+    c = PodClient(server.path, connect_timeout_s=5)
+    c.register("llm", progs[0], w, memory_limit_gb=1, variants=progs[1:])
+    p = _prompt(7)
+    a, ta = c.generate(p, 20, server_loop=True)
+    b, tb = c.generate(p, 20, server_loop=False)
+    assert np.array_equal(a, b) and ta["state"] == tb["state"] == {"pos": [8 + 19]}
+    for bad in ({"steps": 0}, {"steps": 5000}, {"steps": True}, {"steps": 2, "output": 9}):
+        with pytest.raises(PodServerError):
+            c._call({"op": "generate", "shape": [1, 1], "dtype": "i32", "output": 1, **bad},
+                    np.array([[1]], np.int32).tobytes())
+    c.close()
+    m = PodClient(server.path, connect_timeout_s=5)     # a stateless tenant has no decode loop
+    from nos_amd.podserver.program import mlp_program
+
+    prog, wb = mlp_program(dim=16, layers=1, batch=4, dtype="fp32")
+    m.register("mlp", prog, wb, memory_limit_gb=1)
+    with pytest.raises(PodServerError, match="stateful"):
+        m._call({"op": "generate", "steps": 2}, b"")
+    m.close()
+
+
 def test_reset_starts_a_new_sequence_and_repeats_it(model, tenant, server):
     progs, w = tenant
     c = PodClient(server.path, connect_timeout_s=5)

@@ -86,6 +86,8 @@ def main() -> None:
     ap.add_argument("--masked-queues", type=int, default=8, help="CU-masked streams the throughput lanes share "
                     "(with --latency-cus)")
     ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES (0: lanes + priority lanes)")
+    ap.add_argument("--gen-chunk", type=int, default=1, help="llama-dec: tokens per request (> 1: the server's "
+                    "generate loop, ids fed back on the device; per-token latency = request time / tokens)")
     ap.add_argument("--window", type=float, default=8.0)
     ap.add_argument("--warmup", type=float, default=2.0)
     ap.add_argument("--slice-gb", type=float, default=10.0)
@@ -179,15 +181,24 @@ def main() -> None:
                     outs, _ = clients[i].infer(g.integers(0, 32000, (1, 128)).astype(np.int32), outputs=[1])
                     tok = outs[0].reshape(1, 1).astype(np.int32)
                     marks[i].append(time.monotonic())
-                    for _ in range(1024 - 128 - 1):
-                        if stop.is_set():
-                            break
+                    left = 1024 - 128 - 1
+                    while left > 0 and not stop.is_set():
+                        n = min(a.gen_chunk, left)
                         t0 = time.monotonic()
-                        outs, _ = clients[i].infer(tok, outputs=[1])
+                        if n > 1:   # the server's decode loop: one request, n tokens
+                            rep, data = clients[i]._call({"op": "generate", "steps": n, "output": 1, "shape": [1, 1],
+                                                          "dtype": "i32"}, tok.tobytes())
+                            from nos_amd.podserver import protocol as P
+
+                            tok = P.unpack_arrays(rep["outputs"], data)[0].reshape(-1)[-1:].reshape(1, 1).astype(np.int32)
+                        else:
+                            outs, _ = clients[i].infer(tok, outputs=[1])
+                            tok = outs[0].reshape(1, 1).astype(np.int32)
                         t1 = time.monotonic()
-                        tok = outs[0].reshape(1, 1).astype(np.int32)
-                        marks[i].append(t1)
-                        lat[i].append((t0, t1 - t0))
+                        left -= n
+                        for _ in range(n):
+                            marks[i].append(t1)
+                            lat[i].append((t0, (t1 - t0) / n))
                 return
             while not stop.is_set():
                 if i in batches:
