@@ -57,6 +57,24 @@ __device__ __forceinline__ float4 ld4(const void* p, long long i, int bf) {
   return *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
 }
 
+// the same 4 elements split into the load and the conversion: a batch of loads stays in
+// flight whatever the dtype (ld4's bf16 path converts inside its branch, so each of its
+// loads waited for its data before the next one issued)
+__device__ __forceinline__ uint4 ld4raw(const void* p, long long i, int bf) {
+  if (bf) {
+    const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const unsigned short*>(p) + i);
+    return uint4{u.x, u.y, 0u, 0u};
+  }
+  return *reinterpret_cast<const uint4*>(static_cast<const float*>(p) + i);
+}
+
+__device__ __forceinline__ float4 cvt4(uint4 r, int bf) {
+  if (bf)
+    return float4{__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u), __uint_as_float(r.y << 16),
+                  __uint_as_float(r.y & 0xffff0000u)};
+  return float4{__uint_as_float(r.x), __uint_as_float(r.y), __uint_as_float(r.z), __uint_as_float(r.w)};
+}
+
 // ------------------------------------------------------------------ kv_write / rotary at device positions
 // one thread per (b, s, h, d < D/2) pair (d, d + D/2): the rotate_half pair
 // a fused rotary needs; without tables it just copies both elements
@@ -192,12 +210,13 @@ __device__ __forceinline__ void decode_combine_last(const float* __restrict__ ws
   if (tid == 0) atomicExch(&sync[bk], 0);
 }
 
-template <int D>
+template <int D, int CBF>
 __global__ __launch_bounds__(256) void attn_decode_kernel(
     const void* __restrict__ q, int qbf, int ldq, long long bsq, const void* __restrict__ kc,
-    const void* __restrict__ vc, int cbf, const int* __restrict__ pos, const float* __restrict__ cs,
+    const void* __restrict__ vc, int /*cbf = CBF*/, const int* __restrict__ pos, const float* __restrict__ cs,
     const float* __restrict__ sn, int Rtab, float* __restrict__ ws, int B, int H, int Hkv, int Sq, int q0, int L,
     int NS, float scale, Fresh fr, int* __restrict__ sync, void* __restrict__ o, int obf, int Sq_total) {
+  constexpr int cbf = CBF;   // the cache dtype fixed at compile time: no per-load dtype branch
   constexpr int DP = D + 4;  // padded LDS row (16-byte reads of consecutive rows hit distinct banks)
   __shared__ __attribute__((aligned(16))) float qs[MAXR * D];
   __shared__ __attribute__((aligned(16))) float kv[KC * DP];
@@ -230,6 +249,26 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       x1 = y1;
     }
   };
+  // the split's K and V rows are loaded into registers first, every load of both in flight
+  // at once; the fresh-row stores, the q staging and the scores overlap their latency (a
+  // fresh row's stale cache value is replaced by the overlay below)
+  const long long cbase = ((long long)b * L + k0) * cstride + (long long)kvh * D;
+  constexpr int PER = KC * (D / 4) / 256;
+  static_assert(PER * 256 == KC * (D / 4), "whole float4 pieces per thread");
+  uint4 kr[PER], vr[PER];
+  const bool live = nk > 0 && p0 >= 0;
+  if (live) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + 256 * u, j = e / (D / 4), d4 = (e % (D / 4)) * 4;
+      kr[u] = j < nk ? ld4raw(kc, cbase + j * cstride + d4, cbf) : uint4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + 256 * u, j = e / (D / 4), d4 = (e % (D / 4)) * 4;
+      vr[u] = j < nk ? ld4raw(vc, cbase + j * cstride + d4, cbf) : uint4{0u, 0u, 0u, 0u};
+    }
+  }
   if (fresh) {
     for (int e = tid; e < 2 * fr.n * (D / 2); e += 256) {
       const int isv = e >= fr.n * (D / 2), ee = isv ? e - fr.n * (D / 2) : e;
@@ -257,7 +296,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
       kv[j * (D + 4) + d + D / 2] = x1;
     }
   };
-  if (nk <= 0 || p0 < 0) {  // an empty split (or a bad counter): l = 0, skipped by the combine
+  if (!live) {  // an empty split (or a bad counter): l = 0, skipped by the combine
     for (int r = tid; r < R; r += 256) {
       out[r * (D + 2) + D] = -INFINITY;
       out[r * (D + 2) + D + 1] = 0.f;
@@ -281,26 +320,15 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     qs[r * D + d] = x0 * scale;
     qs[r * D + d + D / 2] = x1 * scale;
   }
-  // the split's keys -> LDS (rows past nk zero)
-  const long long cbase = ((long long)b * L + k0) * cstride + (long long)kvh * D;
-  // every load of the split issued before the first LDS store (16 float4 per thread at
-  // D = 128): a load-store loop left one cache-row latency exposed per iteration
-  auto stage = [&](const void* c) {
-    constexpr int PER = KC * (D / 4) / 256;
-    static_assert(PER * 256 == KC * (D / 4), "whole float4 pieces per thread");
-    float4 v[PER];
+  // the split's rows -> LDS from the registers loaded at the start (rows past nk zero)
+  auto stage = [&](const uint4 (&v)[PER]) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int e = tid + 256 * u, j = e / (D / 4), d4 = (e % (D / 4)) * 4;
-      v[u] = j < nk ? ld4(c, cbase + j * cstride + d4, cbf) : float4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int e = tid + 256 * u, j = e / (D / 4), d4 = (e % (D / 4)) * 4;
-      *reinterpret_cast<float4*>(&kv[j * DP + d4]) = v[u];
+      *reinterpret_cast<float4*>(&kv[j * DP + d4]) = cvt4(v[u], cbf);
     }
   };
-  stage(kc);
+  stage(kr);
   overlay(true);
   __syncthreads();
   // scores: thread -> key j, rows of one parity
@@ -352,7 +380,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(
     }
   }
   __syncthreads();  // every wave is done with the keys
-  stage(vc);
+  stage(vr);
   overlay(false);
   __syncthreads();
   // P V: thread -> column d, rows of one residue
@@ -459,15 +487,44 @@ __global__ __launch_bounds__(NT) void argmax_kernel(const void* __restrict__ x, 
 }
 
 // ------------------------------------------------------------------ GEMV (M <= 8)
-template <int M>
+template <int M, int WBF>
 __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, int xbf, int ldx,
-                                                   const void* __restrict__ w, int wbf, int ldw,
+                                                   const void* __restrict__ w, int /*wbf = WBF*/, int ldw,
                                                    const void* __restrict__ bias, const void* __restrict__ res,
                                                    int ldr, void* __restrict__ y, int ldy, int N, int K, int epi,
                                                    float rms_eps) {
+  constexpr int wbf = WBF;  // the weight dtype fixed at compile time: no per-load dtype branch
   extern __shared__ __attribute__((aligned(16))) float xs[];  // [M][K] fp32
   __shared__ float rsc[M];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const bool glu = (epi & EPI_GLU) != 0;
+  const int Nh = N / 2;                                          // GLU: output columns
+  const int ngrp = glu ? (Nh + 3) / 4 : (N + 7) / 8;             // 8 columns per pass: 4 waves x 2
+  // the weight rows (two per wave) of column group grp: GLU pairs gate n0 with up n0 + Nh
+  auto rows_of = [&](int grp, int& n0, long long& w0, long long& w1) {
+    n0 = glu ? grp * 4 + wid : grp * 8 + wid * 2;
+    const int nc0 = glu ? min(n0, Nh - 1) : min(n0, N - 1);
+    const int nc1 = glu ? min(n0, Nh - 1) + Nh : min(n0 + 1, N - 1);
+    w0 = (long long)nc0 * ldw;
+    w1 = (long long)nc1 * ldw;
+  };
+  auto load_chunk = [&](long long w0, long long w1, int k0, uint4 (&a)[4], uint4 (&c4)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + 256 * u;
+      a[u] = k < K ? ld4raw(w, w0 + k, wbf) : uint4{0u, 0u, 0u, 0u};
+      c4[u] = k < K ? ld4raw(w, w1 + k, wbf) : uint4{0u, 0u, 0u, 0u};
+    }
+  };
+  // the first group's first K chunk of weights in flight while x is staged and normalised:
+  // the weights do not depend on x, and the two memory latencies were back to back
+  uint4 pa[4], pc[4];
+  if ((int)blockIdx.x < ngrp) {
+    int n0;
+    long long w0, w1;
+    rows_of(blockIdx.x, n0, w0, w1);
+    load_chunk(w0, w1, lane * 4, pa, pc);
+  }
   for (int e = tid * 4; e < M * K; e += 1024) {
     const int m = e / K, k = e % K;
     *reinterpret_cast<float4*>(&xs[e]) = ld4(x, (long long)m * ldx + k, xbf);
@@ -484,38 +541,38 @@ __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, i
     rsc[tid] = 1.f;
   }
   __syncthreads();
-  const bool glu = (epi & EPI_GLU) != 0;
-  const int Nh = N / 2;                                          // GLU: output columns
-  const int ngrp = glu ? (Nh + 3) / 4 : (N + 7) / 8;             // 8 columns per pass: 4 waves x 2
   for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
-    const int n0 = glu ? grp * 4 + wid : grp * 8 + wid * 2;
+    int n0;
+    long long w0, w1;
+    rows_of(grp, n0, w0, w1);
     float acc[2][M];
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int m = 0; m < M; ++m) acc[c][m] = 0.f;
-    const int nc0 = glu ? min(n0, Nh - 1) : min(n0, N - 1);
-    const int nc1 = glu ? min(n0, Nh - 1) + Nh : min(n0 + 1, N - 1);
-    const long long w0 = (long long)nc0 * ldw, w1 = (long long)nc1 * ldw;
     // four K steps' weight loads issued together (8 float4 in flight per lane): the
     // one-step loop waited a full memory latency per 256 columns of K
     for (int k0 = lane * 4; k0 < K; k0 += 1024) {
-      float4 a[4], c4[4];
+      uint4 ra[4], rc[4];
+      if (grp == (int)blockIdx.x && k0 == lane * 4) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + 256 * u;
-        a[u] = k < K ? ld4(w, w0 + k, wbf) : float4{0.f, 0.f, 0.f, 0.f};
-        c4[u] = k < K ? ld4(w, w1 + k, wbf) : float4{0.f, 0.f, 0.f, 0.f};
+        for (int u = 0; u < 4; ++u) {
+          ra[u] = pa[u];
+          rc[u] = pc[u];
+        }
+      } else {
+        load_chunk(w0, w1, k0, ra, rc);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int k = k0 + 256 * u;
         if (k < K) {
+          const float4 a = cvt4(ra[u], wbf), c4 = cvt4(rc[u], wbf);
 #pragma unroll
           for (int m = 0; m < M; ++m) {
             const float4 xv = *reinterpret_cast<const float4*>(&xs[m * K + k]);
-            acc[0][m] = fmaf(a[u].x, xv.x, fmaf(a[u].y, xv.y, fmaf(a[u].z, xv.z, fmaf(a[u].w, xv.w, acc[0][m]))));
-            acc[1][m] = fmaf(c4[u].x, xv.x, fmaf(c4[u].y, xv.y, fmaf(c4[u].z, xv.z, fmaf(c4[u].w, xv.w, acc[1][m]))));
+            acc[0][m] = fmaf(a.x, xv.x, fmaf(a.y, xv.y, fmaf(a.z, xv.z, fmaf(a.w, xv.w, acc[0][m]))));
+            acc[1][m] = fmaf(c4.x, xv.x, fmaf(c4.y, xv.y, fmaf(c4.z, xv.z, fmaf(c4.w, xv.w, acc[1][m]))));
           }
         }
       }
@@ -639,22 +696,28 @@ NOS_API int nos_attn_decode(const void* q, int qbf, int ldq, long long bsq, cons
     const int sq = Sq - q0 < chunk ? Sq - q0 : chunk;
     const unsigned grid = (unsigned)(B * Hkv * NS);
     const unsigned rows = (unsigned)(B * Hkv * G * sq);
+#define NOS_ATTN_DECODE(d, c)                                                                                   \
+  hipLaunchKernelGGL((attn_decode_kernel<d, c>), dim3(grid), dim3(256), 0, stream, q, qbf, ldq, bsq, kc, vc, cbf, pos, \
+                     cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale, fr, sync, out, obf, Sq)
     if (D == 64) {
-      hipLaunchKernelGGL(attn_decode_kernel<64>, dim3(grid), dim3(256), 0, stream, q, qbf, ldq, bsq, kc, vc, cbf, pos,
-                         cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale, fr, sync, out,
-                         obf, Sq);
+      if (cbf)
+        NOS_ATTN_DECODE(64, 1);
+      else
+        NOS_ATTN_DECODE(64, 0);
       if (!sync)
         hipLaunchKernelGGL(attn_decode_combine_kernel<64>, dim3(rows), dim3(64), 0, stream,
                            static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
     } else {
-      hipLaunchKernelGGL(attn_decode_kernel<128>, dim3(grid), dim3(256), 0, stream, q, qbf, ldq, bsq, kc, vc, cbf,
-                         pos, cos_t, sin_t, R, static_cast<float*>(ws), B, H, Hkv, sq, q0, L, NS, scale, fr, sync,
-                         out, obf, Sq);
+      if (cbf)
+        NOS_ATTN_DECODE(128, 1);
+      else
+        NOS_ATTN_DECODE(128, 0);
       if (!sync)
         hipLaunchKernelGGL(attn_decode_combine_kernel<128>, dim3(rows), dim3(128), 0, stream,
                            static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
     }
   }
+  #undef NOS_ATTN_DECODE
   return (int)hipGetLastError();
 }
 
@@ -698,9 +761,13 @@ NOS_API int nos_gemv(const void* x, int xbf, int ldx, const void* w, int wbf, in
   const int cap = 4 * nos_effective_cus();
   const unsigned grid = (unsigned)(ngrp < cap ? ngrp : cap);
   const size_t lds = (size_t)M * K * 4;
-#define NOS_GEMV(m)                                                                                                 \
-  hipLaunchKernelGGL(gemv_kernel<m>, dim3(grid), dim3(256), lds, stream, x, xbf, ldx, w, wbf, ldw, bias, res, ldr, y, \
-                     ldy, N, K, epi, rms_eps)
+#define NOS_GEMV(m)                                                                                                   \
+  if (wbf)                                                                                                            \
+    hipLaunchKernelGGL((gemv_kernel<m, 1>), dim3(grid), dim3(256), lds, stream, x, xbf, ldx, w, wbf, ldw, bias, res,  \
+                       ldr, y, ldy, N, K, epi, rms_eps);                                                              \
+  else                                                                                                                \
+    hipLaunchKernelGGL((gemv_kernel<m, 0>), dim3(grid), dim3(256), lds, stream, x, xbf, ldx, w, wbf, ldw, bias, res,  \
+                       ldr, y, ldy, N, K, epi, rms_eps)
   switch (M) {
     case 1: NOS_GEMV(1); break;
     case 2: NOS_GEMV(2); break;
