@@ -487,12 +487,44 @@ __global__ __launch_bounds__(NT) void argmax_kernel(const void* __restrict__ x, 
 }
 
 // ------------------------------------------------------------------ GEMV (M <= 8)
+// x given as the decode attention's split partials (ws != null): x row m = sequence m's
+// single query token, x[m][h * D + d] combined from the NS splits of (m, h / G) exactly as
+// attn_decode_combine_kernel does -- the combine launch folded into the O-projection
+struct Parts {
+  const float* ws = nullptr;
+  int NS = 0, R = 0, G = 0, Hkv = 0, D = 0;
+};
+
+__device__ __forceinline__ float4 parts_x4(const Parts& pt, int m, int k) {
+  const int h = k / pt.D, d = k % pt.D, kvh = h / pt.G, r = h % pt.G;  // r = g (one query token)
+  const int bk = m * pt.Hkv + kvh;
+  const long long row = (long long)(pt.D + 2);
+  float M = -INFINITY;
+  for (int s = 0; s < pt.NS; ++s) {
+    const float* p = pt.ws + ((long long)(bk * pt.NS + s) * pt.R + r) * row;
+    if (p[pt.D + 1] > 0.f) M = fmaxf(M, p[pt.D]);
+  }
+  float n0 = 0.f, n1 = 0.f, n2 = 0.f, n3 = 0.f, den = 0.f;
+  for (int s = 0; s < pt.NS; ++s) {
+    const float* p = pt.ws + ((long long)(bk * pt.NS + s) * pt.R + r) * row;
+    if (p[pt.D + 1] > 0.f) {
+      const float w = __expf(p[pt.D] - M);
+      n0 = fmaf(w, p[d], n0);
+      n1 = fmaf(w, p[d + 1], n1);
+      n2 = fmaf(w, p[d + 2], n2);
+      n3 = fmaf(w, p[d + 3], n3);
+      den = fmaf(w, p[pt.D + 1], den);
+    }
+  }
+  return den > 0.f ? float4{n0 / den, n1 / den, n2 / den, n3 / den} : float4{0.f, 0.f, 0.f, 0.f};
+}
+
 template <int M, int WBF>
 __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, int xbf, int ldx,
                                                    const void* __restrict__ w, int /*wbf = WBF*/, int ldw,
                                                    const void* __restrict__ bias, const void* __restrict__ res,
                                                    int ldr, void* __restrict__ y, int ldy, int N, int K, int epi,
-                                                   float rms_eps) {
+                                                   float rms_eps, Parts pt) {
   constexpr int wbf = WBF;  // the weight dtype fixed at compile time: no per-load dtype branch
   extern __shared__ __attribute__((aligned(16))) float xs[];  // [M][K] fp32
   __shared__ float rsc[M];
@@ -527,7 +559,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, i
   }
   for (int e = tid * 4; e < M * K; e += 1024) {
     const int m = e / K, k = e % K;
-    *reinterpret_cast<float4*>(&xs[e]) = ld4(x, (long long)m * ldx + k, xbf);
+    *reinterpret_cast<float4*>(&xs[e]) = pt.ws ? parts_x4(pt, m, k) : ld4(x, (long long)m * ldx + k, xbf);
   }
   __syncthreads();
   if (rms_eps > 0.f) {  // RMSNorm of each row, gamma folded into W
@@ -666,7 +698,7 @@ NOS_API int nos_attn_decode(const void* q, int qbf, int ldq, long long bsq, cons
                             const int* pos, const float* cos_t, const float* sin_t, int R, void* out, int obf, int B,
                             int H, int Hkv, int Sq, int L, int D, float scale, void* ws, long long ws_bytes,
                             const void* kn, const void* vn, int nbf, int ldk, long long bsk, int ldv, long long bsv,
-                            int nfresh, int* sync, long long sync_n, hipStream_t stream) {
+                            int nfresh, int* sync, long long sync_n, int partials_only, hipStream_t stream) {
   if (B <= 0 || H <= 0 || Hkv <= 0 || H % Hkv || H / Hkv > MAXR || Sq <= 0 || L <= 0 || (D != 64 && D != 128) ||
       ldq < H * D || (B > 1 && bsq < (long long)(Sq - 1) * ldq + H * D) || !q || !kc || !vc || !pos || !out ||
       !ws || ((cos_t == nullptr) != (sin_t == nullptr)) || (cos_t && R <= 0) || (qbf != 0 && qbf != 1) ||
@@ -674,6 +706,8 @@ NOS_API int nos_attn_decode(const void* q, int qbf, int ldq, long long bsq, cons
     return (int)hipErrorInvalidValue;
   if (ws_bytes < nos_attn_decode_workspace(B, H, Hkv, Sq, L, D)) return (int)hipErrorInvalidValue;
   if (sync != nullptr && sync_n < (long long)B * Hkv) return (int)hipErrorInvalidValue;
+  // partials_only: the splits' partials stay in ws for nos_gemv_partials (one query token)
+  if (partials_only && (sync != nullptr || Sq != 1)) return (int)hipErrorInvalidValue;
   Fresh fr;
   if (nfresh != 0) {
     if (nfresh != Sq || !kn || !vn || (nbf != 0 && nbf != 1) || ldk < Hkv * D || ldv < Hkv * D ||
@@ -704,7 +738,7 @@ NOS_API int nos_attn_decode(const void* q, int qbf, int ldq, long long bsq, cons
         NOS_ATTN_DECODE(64, 1);
       else
         NOS_ATTN_DECODE(64, 0);
-      if (!sync)
+      if (!sync && !partials_only)
         hipLaunchKernelGGL(attn_decode_combine_kernel<64>, dim3(rows), dim3(64), 0, stream,
                            static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
     } else {
@@ -712,7 +746,7 @@ NOS_API int nos_attn_decode(const void* q, int qbf, int ldq, long long bsq, cons
         NOS_ATTN_DECODE(128, 1);
       else
         NOS_ATTN_DECODE(128, 0);
-      if (!sync)
+      if (!sync && !partials_only)
         hipLaunchKernelGGL(attn_decode_combine_kernel<128>, dim3(rows), dim3(128), 0, stream,
                            static_cast<const float*>(ws), out, obf, B, H, Hkv, sq, q0, Sq, NS);
     }
@@ -747,6 +781,10 @@ NOS_API int nos_argmax(const void* x, int bf16, int rows, int L, int ldx, int* o
 // (fp32) / 8-byte (bf16) aligned, M x K x 4 <= 64 KiB (the x rows in LDS).
 // rms_eps > 0: each x row RMS-normalised first.  grid: the CUs' worth of
 // workgroups walk the N / 8 column groups.
+static int gemv_launch(const void* x, int xbf, int ldx, const void* w, int wbf, int ldw, const void* bias,
+                       const void* res, int ldr, void* y, int ldy, int M, int N, int K, int epi, float rms_eps,
+                       Parts pt, hipStream_t stream);
+
 NOS_API int nos_gemv(const void* x, int xbf, int ldx, const void* w, int wbf, int ldw, const void* bias,
                      const void* res, int ldr, void* y, int ldy, int M, int N, int K, int epi, float rms_eps,
                      hipStream_t stream) {
@@ -757,6 +795,35 @@ NOS_API int nos_gemv(const void* x, int xbf, int ldx, const void* w, int wbf, in
     return (int)hipErrorInvalidValue;
   if ((epi & EPI_GLU) && ((N % 2) || (epi & (EPI_RESID | EPI_GELU | EPI_RELU | EPI_SILU)) || ldy < N / 2))
     return (int)hipErrorInvalidValue;
+  return gemv_launch(x, xbf, ldx, w, wbf, ldw, bias, res, ldr, y, ldy, M, N, K, epi, rms_eps, Parts{}, stream);
+}
+
+// y [M, N] = act(x W^T + b) + R with x = the decode attention's split partials
+// (nos_attn_decode with partials_only: ws [M x Hkv, NS, R = G, D + 2] fp32, one
+// query token per sequence), combined in the GEMV's x staging: the combine launch
+// folded into the O-projection.  ybf: y / R dtype; K = Hkv x G x D.
+NOS_API int nos_gemv_partials(const float* ws, long long ws_n, int NS, int R, int G, int Hkv, int D, int ybf,
+                              const void* w, int wbf, int ldw, const void* bias, const void* res, int ldr, void* y,
+                              int ldy, int M, int N, int K, int epi, hipStream_t stream) {
+  if (!ws || NS <= 0 || G <= 0 || Hkv <= 0 || (D != 64 && D != 128) || R != G || K != Hkv * G * D || !w || !y ||
+      M <= 0 || M > 8 || N <= 0 || ws_n < (long long)M * Hkv * NS * R * (D + 2) || (long long)M * K * 4 > 65536 ||
+      (ybf != 0 && ybf != 1) || (wbf != 0 && wbf != 1) || ((epi & EPI_BIAS) && !bias) ||
+      ((epi & EPI_RESID) && (!res || ldr < N)) || ldy < N || (epi & EPI_GLU) || (ldw % 4) || ldw < K ||
+      ((uintptr_t)w & (wbf ? 7 : 15)))
+    return (int)hipErrorInvalidValue;
+  Parts pt;
+  pt.ws = ws;
+  pt.NS = NS;
+  pt.R = R;
+  pt.G = G;
+  pt.Hkv = Hkv;
+  pt.D = D;
+  return gemv_launch(nullptr, ybf, K, w, wbf, ldw, bias, res, ldr, y, ldy, M, N, K, epi, 0.f, pt, stream);
+}
+
+static int gemv_launch(const void* x, int xbf, int ldx, const void* w, int wbf, int ldw, const void* bias,
+                       const void* res, int ldr, void* y, int ldy, int M, int N, int K, int epi, float rms_eps,
+                       Parts pt, hipStream_t stream) {
   const int ngrp = (epi & EPI_GLU) ? (N / 2 + 3) / 4 : (N + 7) / 8;
   const int cap = 4 * nos_effective_cus();
   const unsigned grid = (unsigned)(ngrp < cap ? ngrp : cap);
@@ -764,10 +831,10 @@ NOS_API int nos_gemv(const void* x, int xbf, int ldx, const void* w, int wbf, in
 #define NOS_GEMV(m)                                                                                                   \
   if (wbf)                                                                                                            \
     hipLaunchKernelGGL((gemv_kernel<m, 1>), dim3(grid), dim3(256), lds, stream, x, xbf, ldx, w, wbf, ldw, bias, res,  \
-                       ldr, y, ldy, N, K, epi, rms_eps);                                                              \
+                       ldr, y, ldy, N, K, epi, rms_eps, pt);                                                          \
   else                                                                                                                \
     hipLaunchKernelGGL((gemv_kernel<m, 0>), dim3(grid), dim3(256), lds, stream, x, xbf, ldx, w, wbf, ldw, bias, res,  \
-                       ldr, y, ldy, N, K, epi, rms_eps)
+                       ldr, y, ldy, N, K, epi, rms_eps, pt)
   switch (M) {
     case 1: NOS_GEMV(1); break;
     case 2: NOS_GEMV(2); break;

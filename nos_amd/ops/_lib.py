@@ -110,11 +110,13 @@ _SIGS = {
     "nos_attn_decode_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
     "nos_attn_decode": [c_void_p, c_int, c_int, c_ll, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                         c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_ll,
-                        c_void_p, c_void_p, c_int, c_int, c_ll, c_int, c_ll, c_int, c_void_p, c_ll, c_void_p],
+                        c_void_p, c_void_p, c_int, c_int, c_ll, c_int, c_ll, c_int, c_void_p, c_ll, c_int, c_void_p],
     "nos_pos_update": [c_void_p, c_int, c_int, c_int, c_void_p],
     "nos_argmax": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "nos_gemv": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int,
                  c_int, c_int, c_int, c_float, c_void_p],
+    "nos_gemv_partials": [c_void_p, c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                          c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "nos_attn_h3g_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
     # LayerNorm hand-off (gemm_f32h.hip): producer row statistics, LN in the consumer's A load
     "nos_gemm_f32h3_stats": [c_void_p, c_int, c_ll, c_void_p, c_float, c_void_p, c_int, c_ll, c_void_p, c_void_p,

@@ -607,8 +607,19 @@ def rotary_at(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: torch.
     return out
 
 
+class DecodePartials:
+    """The decode attention's split partials (``sdpa_cache(partials=True)``):
+    ws [B x Hkv, NS, G, D + 2] fp32 -- consumed by :func:`gemv_partials`,
+    which combines them in its x staging (the combine launch folded into the
+    O-projection).  ``shape``: the attention output's [B, 1, H, D]."""
+
+    def __init__(self, ws, NS, G, Hkv, D, shape, dtype):
+        self.ws, self.NS, self.G, self.Hkv, self.D, self.shape, self.dtype = ws, NS, G, Hkv, D, tuple(shape), dtype
+
+
 def sdpa_cache(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos: torch.Tensor, scale: float | None = None,
-               rope: tuple | None = None, fresh: tuple | None = None, sync: torch.Tensor | None = None) -> torch.Tensor:
+               rope: tuple | None = None, fresh: tuple | None = None, sync: torch.Tensor | None = None,
+               partials: bool = False):
     """Query i of sequence b, at position pos[b] + i, attends the cached keys
     0 .. pos[b] + i: q [B, Sq, H, D], caches [B, L, Hkv, D] (fp32 / bf16).
     ``rope`` = (cos, sin): q rotated at its positions inside the kernel.
@@ -617,7 +628,9 @@ def sdpa_cache(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos: torch.T
     launch -- a ``kv_write`` pair folded in.  ``sync``: a zeroed int32
     device buffer of >= B x Hkv counters owned by the call site (the kernel
     leaves it zero): the split combine runs in the decode launch's last
-    workgroup per K / V head instead of a launch of its own.  The
+    workgroup per K / V head instead of a launch of its own.  ``partials``
+    (CUDA, fp32 q, one query token): no combine -- returns the splits'
+    :class:`DecodePartials` for :func:`gemv_partials`.  The
     flash-decoding kernel (decode.hip) for CUDA tensors, fp32 math."""
     from ..podserver.program.reference import kv_write_ref, rotary_at_ref, sdpa_cache_ref
 
@@ -666,12 +679,16 @@ def sdpa_cache(q: torch.Tensor, kc: torch.Tensor, vc: torch.Tensor, pos: torch.T
     if sync is not None and (not sync.is_cuda or sync.dtype != torch.int32 or not sync.is_contiguous()
                              or sync.numel() < B * Hkv):
         raise ValueError(f"sdpa_cache: sync needs >= {B * Hkv} contiguous int32 device counters")
+    if partials and (Sq != 1 or sync is not None or q.dtype != torch.float32):
+        raise ValueError("sdpa_cache: partials need one fp32 query token and no sync")
     _lib.check(L_.nos_attn_decode(q.data_ptr(), _bf(q), ldq, bsq, kc.data_ptr(), vc.data_ptr(), _bf(kc),
                                   _i32_pos(pos, B).data_ptr(), _ptr(c), _ptr(s_), R, out.data_ptr(), _bf(out), B, H,
                                   Hkv, Sq, L, D, float(sc), ws.data_ptr(), ws.numel() * 4, _ptr(kn), _ptr(vn), nbf,
                                   ldk, bsk, ldv, bsv, Sq if fresh is not None else 0, _ptr(sync),
-                                  sync.numel() if sync is not None else 0, _stream()),
+                                  sync.numel() if sync is not None else 0, int(bool(partials)), _stream()),
                "nos_attn_decode")
+    if partials:
+        return DecodePartials(ws, (L + 127) // 128, H // Hkv, Hkv, D, (B, Sq, H, D), q.dtype)
     return out
 
 
@@ -742,10 +759,34 @@ def gemv(x2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, ac
     return y
 
 
+def gemv_partials(p: DecodePartials, w: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None,
+                  residual: torch.Tensor | None = None) -> torch.Tensor:
+    """:func:`gemv` whose x [B, H x D] is the decode attention's output,
+    combined from its split partials in the kernel's x staging
+    (decode.hip ``parts_x4``, the combine kernel's arithmetic): y [B, N] fp32."""
+    B, _, H, D = p.shape
+    K = H * D
+    N = w.shape[0]
+    if w.shape[1] != K or w.stride(-1) != 1 or w.stride(0) % 4 or w.data_ptr() % 16 or B > GEMV_MAX_ROWS:
+        raise ValueError(f"gemv_partials: W {tuple(w.shape)} for x [{B}, {K}]")
+    y = torch.empty((B, N), dtype=torch.float32, device=w.device)
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_RESID if residual is not None else 0)
+    epi |= {"gelu": EPI_GELU, "relu": EPI_RELU, "silu": EPI_SILU}.get(act or "", 0)
+    b = None if bias is None else bias.to(w.dtype).contiguous()
+    r = None if residual is None else residual.reshape(B, N).float()
+    if r is not None and r.stride(-1) != 1:
+        r = r.contiguous()
+    _lib.check(_lib.lib().nos_gemv_partials(p.ws.data_ptr(), p.ws.numel(), p.NS, p.G, p.G, p.Hkv, D, 0, w.data_ptr(),
+                                            _bf(w), w.stride(0), _ptr(b), _ptr(r), r.stride(0) if r is not None else 0,
+                                            y.data_ptr(), y.stride(0), B, N, K, epi, _stream()), "nos_gemv_partials")
+    return y
+
+
 def set_attention_h3g_kvsplit(n: int) -> None:
     """Key splits of :func:`sdpa` (0 = auto: fill the CU slots)."""
     _lib.check(_lib.lib().nos_attn_h3g_set_kvsplit(int(n)), "nos_attn_h3g_set_kvsplit")
 
 
-__all__ = ["glu", "kv_write", "rotary_at", "sdpa_cache", "pos_update", "argmax", "gemv", "gemv_ok", "conv2d", "matmul", "sdpa", "linear_rms", "embedding", "rmsnorm", "softmax", "rotary", "conv2d_ref",
+__all__ = ["glu", "kv_write", "rotary_at", "sdpa_cache", "pos_update", "argmax", "gemv", "gemv_ok", "gemv_partials",
+           "DecodePartials", "conv2d", "matmul", "sdpa", "linear_rms", "embedding", "rmsnorm", "softmax", "rotary", "conv2d_ref",
            "sdpa_ref", "rope_ref", "rmsnorm_ref", "linear_rms_ref", "set_attention_h3g_kvsplit", "EPI_BIAS_ROW"]

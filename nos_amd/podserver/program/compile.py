@@ -77,6 +77,8 @@ class Lowered:
                 self._fold_decode_combines(steps)
             steps = self._fuse_argmax_pos(steps)
             steps = self._fuse_gemv_glu(steps)
+            if "combine_gemv" not in skip:
+                steps = self._fold_combine_into_gemv(steps)
             if "cat_buffer" not in skip:
                 steps = self._cat_into_buffer(steps)
             steps = self._mark_plane_handoffs(steps)
@@ -1069,6 +1071,44 @@ class Lowered:
             s.attrs = {**s.attrs, "sync": name}
             n += 1
         self.stats["decode_combines_folded"] = n
+
+    def _fold_combine_into_gemv(self, steps: list[_Step]) -> list[_Step]:
+        """GPU: a one-token fp32 ``sdpa_cache`` whose output only its layer's
+        O-projection reads (through a reshape to [B, 1, H x D], B <= 8) leaves
+        its split partials to that GEMV, which combines them while it stages
+        x (``ops.tenant.gemv_partials``, decode.hip ``parts_x4``, the combine
+        kernel's arithmetic) -- the combine launch of each layer folded away."""
+        if not self.gpu:
+            return steps
+        uses = self._consumers(steps, self.outputs)
+        by_input: dict[str, list[_Step]] = {}
+        for t in steps:
+            for i in t.inputs:
+                by_input.setdefault(i, []).append(t)
+        drop, n = set(), 0
+        for s in steps:
+            if s.kind != "sdpa_cache" or s.attrs.get("sync") or uses.get(s.output) != 1:
+                continue
+            shp = tuple(self._shape(s.output))
+            if len(shp) != 4 or shp[1] != 1 or shp[0] > 8 or shp[3] not in (64, 128) or self._dtype(s.output) != "fp32":
+                continue
+            r = by_input.get(s.output, [None])[0]
+            if r is None or r.kind != "reshape" or uses.get(r.output) != 1:
+                continue
+            rs = tuple(self._shape(r.output))
+            if rs[0] != shp[0] or math.prod(rs[1:]) != shp[2] * shp[3] or rs[-1] != shp[2] * shp[3]:
+                continue
+            lin = by_input.get(r.output, [None])[0]
+            if (lin is None or lin.kind != "linear" or lin.inputs[0] != r.output or lin.attrs.get("out_into")
+                    or lin.attrs.get("row_stats") or lin.attrs.get("planes_out") or lin.attrs.get("act") == "glu"):
+                continue
+            s.attrs = {**s.attrs, "partials": True}
+            lin.inputs = [s.output] + lin.inputs[1:]
+            lin.attrs = {**lin.attrs, "x_partials": True}
+            drop.add(id(r))
+            n += 1
+        self.stats["decode_combines_into_gemv"] = n
+        return [t for t in steps if id(t) not in drop]
 
     def _fuse_argmax_pos(self, steps: list[_Step]) -> list[_Step]:
         """GPU: a step's closing ``pos_add`` folds into the ``argmax`` right

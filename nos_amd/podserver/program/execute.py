@@ -25,7 +25,11 @@ class CompiledProgram(Lowered):
         for s in self.steps:
             a = [env[i] for i in s.inputs]
             k = s.kind
-            if k == "linear":
+            if k == "linear" and s.attrs.get("x_partials"):   # x = the decode attention's split partials
+                res = a.pop() if s.attrs.get("residual") else None
+                y = T.gemv_partials(a[0], a[1], a[2] if len(a) > 2 else None, act=s.attrs.get("act"),
+                                    residual=res).reshape(self._shape(s.output))
+            elif k == "linear":
                 res = a.pop() if s.attrs.get("residual") else None
                 rs = bool(s.attrs.get("row_stats")) and ops.ln_handoff_active() and (
                     isinstance(a[0], ops.H3Planes) or (a[0].is_cuda and a[0].dtype.itemsize == 4))
@@ -129,7 +133,7 @@ class CompiledProgram(Lowered):
                 y = T.sdpa_cache(a[0], a[1], a[2], a[3], scale=s.attrs.get("scale"),
                                  rope=(a[4], a[5]) if s.attrs.get("rope") else None,
                                  fresh=(a[-2], a[-1]) if s.attrs.get("fresh") else None,
-                                 sync=self.aux.get(s.attrs.get("sync")))
+                                 sync=self.aux.get(s.attrs.get("sync")), partials=bool(s.attrs.get("partials")))
             elif k == "rotary_at":
                 y = T.rotary_at(a[0], a[1], a[2], a[3])
             elif k in ("pos_add", "pos_set"):

@@ -89,6 +89,34 @@ def test_decode_attention_matches_fp64(D, G, Sq, L, cdt):
         assert int(sync.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("B, G, Hkv", [(1, 4, 2), (3, 1, 2), (2, 8, 1)])
+@pytest.mark.parametrize("L", [16, 300, 1100])
+@pytest.mark.parametrize("wdt", [torch.float32, torch.bfloat16])
+def test_gemv_combines_the_decode_partials(D, B, G, Hkv, L, wdt):
+    """The combine launch folded into the O-projection: sdpa_cache(partials)
+    + gemv_partials equals sdpa_cache + gemv bit for bit (bias, residual)."""
+    torch.manual_seed(D + B + G + L)
+    H = G * Hkv
+    kc = torch.randn(B, L, Hkv, D, device="cuda")
+    vc = torch.randn(B, L, Hkv, D, device="cuda")
+    q = torch.randn(B, 1, H, D, device="cuda")
+    pos = torch.randint(0, L, (B,), dtype=torch.int32, device="cuda")
+    pos[0] = L - 1
+    N = 384
+    w = (torch.randn(N, H * D, device="cuda") / 16).to(wdt)
+    bias = torch.randn(N, device="cuda").to(wdt)
+    res = torch.randn(B, N, device="cuda")
+    att = T.sdpa_cache(q, kc, vc, pos)
+    ref = T.gemv(att.reshape(B, H * D), w, bias, None, res)
+    p = T.sdpa_cache(q, kc, vc, pos, partials=True)
+    assert isinstance(p, T.DecodePartials)
+    got = T.gemv_partials(p, w, bias, None, res)
+    assert torch.equal(got, ref)
+    with pytest.raises(ValueError, match="partials"):
+        T.sdpa_cache(q.expand(B, 2, H, D).contiguous(), kc, vc, pos, partials=True)
+
+
 def test_decode_attention_with_fused_rotary_and_bad_positions():
     """q rotated inside the kernel; a negative / huge counter never faults:
     the empty splits are skipped and the rows come out finite."""
@@ -256,6 +284,9 @@ def test_decode_program_uses_the_fused_decode_kernels(monkeypatch):
     assert c.stats["kv_writes_into_attention"] == 2   # the cache writes inside the decode attention launch
     assert c.stats["pos_add_into_argmax"] == 1         # the position advance inside the argmax launch
     assert c.stats["decode_combines_folded"] == 2      # the split combines inside the decode launches
+    monkeypatch.delenv("NOS_AMD_FOLD_DECODE_COMBINE")
+    c2 = ps[1].compile("cuda", params=ps[0].tensors("cuda"))
+    assert c2.stats["decode_combines_into_gemv"] == 2  # by default: the combines inside the O-projection GEMVs
     kinds = [s.kind for s in c.steps if s.kind not in ("slice", "reshape")]
     assert "kv_write" not in kinds and "glu" not in kinds and "rotary_at" not in kinds and "pos_add" not in kinds
 
