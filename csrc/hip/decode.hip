@@ -519,7 +519,7 @@ __device__ __forceinline__ float4 parts_x4(const Parts& pt, int m, int k) {
   return den > 0.f ? float4{n0 / den, n1 / den, n2 / den, n3 / den} : float4{0.f, 0.f, 0.f, 0.f};
 }
 
-template <int M, int WBF>
+template <int M, int WBF, int KU>
 __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, int xbf, int ldx,
                                                    const void* __restrict__ w, int /*wbf = WBF*/, int ldw,
                                                    const void* __restrict__ bias, const void* __restrict__ res,
@@ -540,9 +540,9 @@ __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, i
     w0 = (long long)nc0 * ldw;
     w1 = (long long)nc1 * ldw;
   };
-  auto load_chunk = [&](long long w0, long long w1, int k0, uint4 (&a)[4], uint4 (&c4)[4]) {
+  auto load_chunk = [&](long long w0, long long w1, int k0, uint4 (&a)[KU], uint4 (&c4)[KU]) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < KU; ++u) {
       const int k = k0 + 256 * u;
       a[u] = k < K ? ld4raw(w, w0 + k, wbf) : uint4{0u, 0u, 0u, 0u};
       c4[u] = k < K ? ld4raw(w, w1 + k, wbf) : uint4{0u, 0u, 0u, 0u};
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, i
   };
   // the first group's first K chunk of weights in flight while x is staged and normalised:
   // the weights do not depend on x, and the two memory latencies were back to back
-  uint4 pa[4], pc[4];
+  uint4 pa[KU], pc[KU];
   if ((int)blockIdx.x < ngrp) {
     int n0;
     long long w0, w1;
@@ -582,13 +582,14 @@ __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, i
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int m = 0; m < M; ++m) acc[c][m] = 0.f;
-    // four K steps' weight loads issued together (8 float4 in flight per lane): the
-    // one-step loop waited a full memory latency per 256 columns of K
-    for (int k0 = lane * 4; k0 < K; k0 += 1024) {
-      uint4 ra[4], rc[4];
+    // KU K steps' weight loads issued together (2 KU float4 in flight per lane): the
+    // one-step loop waited a full memory latency per 256 columns of K; KU = 12 takes
+    // K <= 3072 (a down projection) in one batch (the same summation order as KU = 4)
+    for (int k0 = lane * 4; k0 < K; k0 += 256 * KU) {
+      uint4 ra[KU], rc[KU];
       if (grp == (int)blockIdx.x && k0 == lane * 4) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < KU; ++u) {
           ra[u] = pa[u];
           rc[u] = pc[u];
         }
@@ -596,7 +597,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const void* __restrict__ x, i
         load_chunk(w0, w1, k0, ra, rc);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < KU; ++u) {
         const int k = k0 + 256 * u;
         if (k < K) {
           const float4 a = cvt4(ra[u], wbf), c4 = cvt4(rc[u], wbf);
@@ -828,13 +829,20 @@ static int gemv_launch(const void* x, int xbf, int ldx, const void* w, int wbf, 
   const int cap = 4 * nos_effective_cus();
   const unsigned grid = (unsigned)(ngrp < cap ? ngrp : cap);
   const size_t lds = (size_t)M * K * 4;
+#define NOS_GEMV_KU(m, b, ku)                                                                                         \
+  hipLaunchKernelGGL((gemv_kernel<m, b, ku>), dim3(grid), dim3(256), lds, stream, x, xbf, ldx, w, wbf, ldw, bias, res, \
+                     ldr, y, ldy, N, K, epi, rms_eps, pt)
 #define NOS_GEMV(m)                                                                                                   \
-  if (wbf)                                                                                                            \
-    hipLaunchKernelGGL((gemv_kernel<m, 1>), dim3(grid), dim3(256), lds, stream, x, xbf, ldx, w, wbf, ldw, bias, res,  \
-                       ldr, y, ldy, N, K, epi, rms_eps, pt);                                                          \
-  else                                                                                                                \
-    hipLaunchKernelGGL((gemv_kernel<m, 0>), dim3(grid), dim3(256), lds, stream, x, xbf, ldx, w, wbf, ldw, bias, res,  \
-                       ldr, y, ldy, N, K, epi, rms_eps, pt)
+  if (K > 1024) {                                                                                                     \
+    if (wbf)                                                                                                          \
+      NOS_GEMV_KU(m, 1, 12);                                                                                          \
+    else                                                                                                              \
+      NOS_GEMV_KU(m, 0, 12);                                                                                          \
+  } else if (wbf) {                                                                                                   \
+    NOS_GEMV_KU(m, 1, 4);                                                                                             \
+  } else {                                                                                                            \
+    NOS_GEMV_KU(m, 0, 4);                                                                                             \
+  }
   switch (M) {
     case 1: NOS_GEMV(1); break;
     case 2: NOS_GEMV(2); break;
@@ -846,5 +854,6 @@ static int gemv_launch(const void* x, int xbf, int ldx, const void* w, int wbf, 
     default: NOS_GEMV(8); break;
   }
 #undef NOS_GEMV
+#undef NOS_GEMV_KU
   return (int)hipGetLastError();
 }
