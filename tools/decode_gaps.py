@@ -20,7 +20,7 @@ def main() -> None:
     gaps = []
     for i, r in enumerate(rows):
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        k = r["Kernel_Name"][:80]
+        k = r["Kernel_Name"][:70] + (f" grid {r['Grid_Size']}" if "Grid_Size" in r else "")
         busy[k][0] += 1
         busy[k][1] += (e - s) / 1e3
         if i:
