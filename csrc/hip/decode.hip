@@ -780,7 +780,7 @@ NOS_API int nos_argmax(const void* x, int bf16, int rows, int L, int ldx, int* o
 // y [M, N] = act(rms(x) x [M, K] . W [N, K]^T + bias) + res, M <= 8; x, y, res
 // share x's dtype (xbf), W and bias W's (wbf); K % 4 == 0, rows 16-byte
 // (fp32) / 8-byte (bf16) aligned, M x K x 4 <= 64 KiB (the x rows in LDS).
-// rms_eps > 0: each x row RMS-normalised first.  grid: the CUs' worth of
+// rms_eps > 0: each x row RMS-normalised first.  grid: up to 16 workgroups per CU of
 // workgroups walk the N / 8 column groups.
 static int gemv_launch(const void* x, int xbf, int ldx, const void* w, int wbf, int ldw, const void* bias,
                        const void* res, int ldr, void* y, int ldy, int M, int N, int K, int epi, float rms_eps,
@@ -826,7 +826,9 @@ static int gemv_launch(const void* x, int xbf, int ldx, const void* w, int wbf, 
                        const void* res, int ldr, void* y, int ldy, int M, int N, int K, int epi, float rms_eps,
                        Parts pt, hipStream_t stream) {
   const int ngrp = (epi & EPI_GLU) ? (N / 2 + 3) / 4 : (N + 7) / 8;
-  const int cap = 4 * nos_effective_cus();
+  // every column group its own workgroup up to 16 per CU: a vocabulary head (4000 groups) no
+  // longer walks 4 groups per workgroup one memory round trip after another
+  const int cap = 16 * nos_effective_cus();
   const unsigned grid = (unsigned)(ngrp < cap ? ngrp : cap);
   const size_t lds = (size_t)M * K * 4;
 #define NOS_GEMV_KU(m, b, ku)                                                                                         \
