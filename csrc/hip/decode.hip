@@ -780,8 +780,8 @@ NOS_API int nos_argmax(const void* x, int bf16, int rows, int L, int ldx, int* o
 // y [M, N] = act(rms(x) x [M, K] . W [N, K]^T + bias) + res, M <= 8; x, y, res
 // share x's dtype (xbf), W and bias W's (wbf); K % 4 == 0, rows 16-byte
 // (fp32) / 8-byte (bf16) aligned, M x K x 4 <= 64 KiB (the x rows in LDS).
-// rms_eps > 0: each x row RMS-normalised first.  grid: up to 16 workgroups per CU of
-// workgroups walk the N / 8 column groups.
+// rms_eps > 0: each x row RMS-normalised first.  grid: up to 16 workgroups per CU
+// walk the N / 8 column groups.
 static int gemv_launch(const void* x, int xbf, int ldx, const void* w, int wbf, int ldw, const void* bias,
                        const void* res, int ldr, void* y, int ldy, int M, int N, int K, int epi, float rms_eps,
                        Parts pt, hipStream_t stream);
